@@ -1,0 +1,197 @@
+/*
+ * kmerpair.h — C ABI of the MI355X-native k-mer pair engine (libkmerpair.so).
+ *
+ * Drop-in boundary for the hot path of Isabella136/uniprot_kmer_based_clustering:
+ * the Rust module surface that src/main.rs calls in src/protein.rs and src/graph/*.
+ * The reference has no FFI of its own; each entry point below names the
+ * reference interface it replaces (file:line in the reference tree).  INTEGRATION.md
+ * shows the Rust `extern "C"` block a maintainer would add to bind it.
+ *
+ * Conventions
+ *  - Plain C: integer status returns (kmp_status), no exceptions or aborts cross the ABI.
+ *  - Host-buffer API (kmp_load_proteins … kmp_edges_get): caller-owned inputs are copied
+ *    before return; results are library-owned objects the caller frees.
+ *  - Calls are synchronous, like the reference's graph methods (each spawns and joins
+ *    its own pool before returning, mod.rs:81-124).  One host thread per kmp_ctx.
+ *  - Device-stage API (kmp_dev_*): plain device pointers + an optional hipStream_t passed
+ *    as void*; no allocation, no synchronisation inside, so a multi-GPU host (one process
+ *    per GPU, RCCL all-gather between stages) can drive the stages on its own streams.
+ *  - Proteins are indexed 0..N-1 in input (file) order; edges are (p, q, w) with p < q,
+ *    sorted by (p, q) — the reference's post-combine_edges graph with orientation [p, q]
+ *    (single-thread visitor order, vertex.rs:100).
+ */
+#ifndef KMERPAIR_H
+#define KMERPAIR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KMP_ABI_VERSION 1
+
+typedef enum {
+    KMP_OK = 0,
+    KMP_EINVAL = 1,     /* bad argument (reference: panic / expect) */
+    KMP_ENOMEM = 2,     /* host or device allocation failed */
+    KMP_EDEVICE = 3,    /* HIP runtime error or no usable gfx950 device */
+    KMP_ERCCL = 4,      /* reserved: collective failure reported by a multi-GPU host */
+    KMP_EOVERFLOW = 5,  /* caller buffer too small; *n holds the size needed */
+    KMP_ESTATE = 6,     /* call out of order (e.g. kmp_pairs before kmp_load_proteins) */
+    KMP_EIO = 7         /* file could not be read / written */
+} kmp_status;
+
+/* length laws of the synthetic generator */
+enum { KMP_LEN_NORMAL300 = 0, KMP_LEN_LOGUNIFORM = 1 };
+
+/* pair scores (kmp_pair_opts.score) */
+enum { KMP_SCORE_COUNT = 0, KMP_SCORE_JACCARD = 1 };
+
+typedef struct kmp_ctx kmp_ctx;
+typedef struct kmp_edges kmp_edges;
+
+/* The reference's stderr counters (graph/mod.rs:50,51,545,695) plus set statistics. */
+typedef struct {
+    uint64_t n_proteins;
+    uint64_t n_windows;   /* Σ (L-k+1): Protein.five_mers total (protein.rs:114) */
+    uint64_t sum_S;       /* Σ |K(p)|, distinct k-mers per protein */
+    uint64_t distinct;    /* distinct k-mers over all proteins (main.rs:318) */
+    uint64_t repeat;      /* df >= 2 k-mers: "Number of 5mers found in at least two proteins" (mod.rs:50) */
+    uint64_t sum_cdf2;    /* Σ C(df,2): "Number of total edges" (mod.rs:51) */
+    uint64_t sum_w_diff;  /* Σ w over class-differing pairs: edges after AMR filter (mod.rs:695) */
+    uint64_t n_edges;     /* emitted pairs: "Number of edges now" after collapse (mod.rs:545) */
+    uint64_t n_align;     /* emitted pairs with w > align_threshold (mod.rs:242) */
+    uint64_t max_df;
+} kmp_counters;
+
+typedef struct {
+    uint32_t min_shared;         /* emit iff w >= min_shared (reference: 1) */
+    int32_t require_class_diff;  /* 1: drop same-AMR-class pairs (mod.rs:549-697); 0: keep */
+    uint32_t align_threshold;    /* alignment candidates: w > threshold (mod.rs:242: 10) */
+    int32_t score;               /* KMP_SCORE_COUNT | KMP_SCORE_JACCARD (build extension) */
+} kmp_pair_opts;
+
+/* defaults: min_shared 1, require_class_diff 1, align_threshold 10, score COUNT */
+void kmp_pair_opts_default(kmp_pair_opts* opts);
+
+/* ------------------------------------------------------------------ context -------- */
+int kmp_version(void);                         /* KMP_ABI_VERSION */
+const char* kmp_status_string(int status);
+/* device: HIP ordinal; cpu_threads: host threads for ingest / planning (reference: `threads`, main.rs:57-60) */
+int kmp_ctx_create(kmp_ctx** ctx, int device, int cpu_threads);
+void kmp_ctx_destroy(kmp_ctx* ctx);
+const char* kmp_last_error(const kmp_ctx* ctx);
+
+/* ------------------------------------------------------------------ ingest --------- */
+/* Replaces the Protein::new batch (protein.rs:107-132 via main.rs:65-72).  residues: the
+ * packed sequence bytes of all proteins; offsets[N+1]: byte offsets; class_id[N]: AMR
+ * class per protein, equal ids <=> equal get_amr_class() strings (protein.rs:135-138).
+ * class_id may be NULL (all one class).  Copies to the device before return. */
+int kmp_load_proteins(kmp_ctx* ctx, const uint8_t* residues, const uint64_t* offsets, uint32_t n,
+                      const uint16_t* class_id);
+
+/* ------------------------------------------------------------------ k-mers --------- */
+/* Protein.five_mers generalised to k in {1..7} (protein.rs:29-37,107-132): all L-k+1 windows
+ * in position order, duplicates kept; radix-21 big-endian codes.  Replaces get_five_mers
+ * (protein.rs:141-143). */
+int kmp_extract(kmp_ctx* ctx, int k);
+int kmp_get_kmers(kmp_ctx* ctx, uint32_t protein, uint32_t* out, uint64_t cap, uint64_t* n);
+
+/* ------------------------------------------------------------------ sets ----------- */
+/* K(p): sorted distinct codes per protein (main.rs:280-282), plus the global repeat
+ * (df >= 2) filter of remove_unique_five_mers (protein.rs:151-162). */
+int kmp_build_sets(kmp_ctx* ctx, int k);
+int kmp_get_set(kmp_ctx* ctx, uint32_t protein, uint32_t* out, uint64_t cap, uint64_t* n);
+int kmp_counters_get(kmp_ctx* ctx, kmp_counters* out);
+
+/* ------------------------------------------------------------------ pairs ---------- */
+/* Fused Graph::new (mod.rs:39-193) + remove_uninteresting_edges (mod.rs:549-697) +
+ * combine_edges (mod.rs:322-546): every pair p<q with w = |K(p) ∩ K(q)| >= min_shared
+ * (and differing classes when required), w = the collapsed KmerEdge::Group length.
+ * Requires kmp_build_sets for the same k.  Result is library-owned. */
+int kmp_pairs(kmp_ctx* ctx, const kmp_pair_opts* opts, kmp_edges** out);
+int kmp_edges_count(const kmp_edges* e, uint64_t* n);
+/* copies up to cap edges; *n = total; KMP_EOVERFLOW if cap < total.  Any output pointer
+ * may be NULL.  score[] is w for KMP_SCORE_COUNT, Jaccard w/(S_p+S_q-w) otherwise. */
+int kmp_edges_get(const kmp_edges* e, uint32_t* p, uint32_t* q, uint32_t* w, float* score,
+                  uint64_t cap, uint64_t* n);
+void kmp_edges_free(kmp_edges* e);
+
+/* ------------------------------------------------------------------ device stages -- */
+/* Workspace sizes for the device stages; all in bytes. */
+typedef struct {
+    uint64_t tile_slots;      /* LDS hash slots per row tile */
+    uint64_t tile_cap;        /* max set entries per row tile */
+    uint64_t rows_max;        /* max proteins per row tile */
+} kmp_pair_geometry;
+void kmp_dev_pair_geometry(kmp_pair_geometry* g);
+
+/* win_off[p] = Σ_{i<p} max(0, L_i - k + 1) for p in 0..N (exclusive scan on device). */
+int kmp_dev_window_offsets(const uint64_t* d_res_off, uint32_t n, int k, uint64_t* d_win_off,
+                           void* stream);
+/* All windows' codes, position order, at d_codes[win_off[p] ...]. */
+int kmp_dev_extract(const uint8_t* d_res, const uint64_t* d_res_off, const uint64_t* d_win_off,
+                    uint32_t n, int k, uint32_t* d_codes, void* stream);
+/* Fused extract + per-protein sort + dedup: K(p) ascending at d_set[win_off[p] ...],
+ * |K(p)| in d_set_len[p].  d_scratch: >= 4 * win_off[N] bytes (used by proteins whose
+ * window count exceeds the in-LDS sort, may be NULL when none does). */
+int kmp_dev_build_sets(const uint8_t* d_res, const uint64_t* d_res_off, const uint64_t* d_win_off,
+                       uint32_t n, int k, uint32_t* d_set, uint32_t* d_set_len, uint32_t* d_scratch,
+                       void* stream);
+/* Number of 32-bit words of each repeat bitmap for k (21^k bits rounded up). */
+uint64_t kmp_dev_repeat_bitmap_words(int k);
+/* remove_unique_five_mers (protein.rs:151-162): marks df>=1 / df>=2 in two bitmaps, then
+ * compacts each set to its repeat k-mers (d_rep[win_off[p] ...], d_rep_len[p]).  The two
+ * bitmaps (d_bits, 2 * kmp_dev_repeat_bitmap_words(k) words) are zeroed inside. */
+int kmp_dev_filter_repeats(const uint32_t* d_set, const uint32_t* d_set_len, const uint64_t* d_win_off,
+                           uint32_t n, int k, uint32_t* d_bits, uint32_t* d_rep, uint32_t* d_rep_len,
+                           void* stream);
+
+/* A work item of the pair kernel: rows [row_beg,row_end) × columns [col_beg,col_end). */
+typedef struct {
+    uint32_t row_beg, row_end, col_beg, col_end;
+} kmp_work_item;
+
+/* Host-side planner: row tiles packed greedily (Σ len <= tile_cap, count <= rows_max),
+ * each tile's upper-triangle column range cut into chunks of about chunk_cost set entries.
+ * Returns the item count in *n_items (capacity cap; KMP_EOVERFLOW with the needed size). */
+int kmp_plan_pairs(const uint32_t* set_len, uint32_t n, uint64_t chunk_cost, kmp_work_item* items,
+                   uint64_t cap, uint64_t* n_items);
+
+/* The pair kernel over work items [0, n_items): appends (p, q, w) with p < q, w >= min_shared
+ * and (if required) class[p] != class[q] to d_p/d_q/d_w (unordered) at positions
+ * d_count[0]++ (< cap; d_count keeps counting past cap so the caller can resize and rerun).
+ * d_set/d_set_len/d_win_off describe the (possibly repeat-filtered) sets.
+ * d_count must be zeroed by the caller (it is a 64-bit counter). */
+int kmp_dev_pairs(const uint32_t* d_set, const uint32_t* d_set_len, const uint64_t* d_win_off,
+                  const uint16_t* d_class, uint32_t n, const kmp_work_item* d_items, uint64_t n_items,
+                  uint32_t min_shared, int require_class_diff, uint32_t* d_p, uint32_t* d_q,
+                  uint32_t* d_w, uint64_t cap, unsigned long long* d_count, void* stream);
+
+/* Canonical order: sorts n edges by (p, q) in place (keys packed p·N+q).  d_tmp: bytes from
+ * kmp_dev_sort_edges_tmp_bytes(n, n_proteins). */
+uint64_t kmp_dev_sort_edges_tmp_bytes(uint64_t n, uint32_t n_proteins);
+int kmp_dev_sort_edges(uint32_t* d_p, uint32_t* d_q, uint32_t* d_w, uint64_t n, uint32_t n_proteins,
+                       void* d_tmp, uint64_t tmp_bytes, void* stream);
+
+/* ------------------------------------------------------------------ host utilities - */
+/* FASTA ingest with seq_io semantics (main.rs:62-72): id = header up to the first space,
+ * seq = the record's sequence bytes; AMR class = id.split_terminator('|')[3]
+ * (protein.rs:135-138) interned to ids in order of first appearance.  Library-owned
+ * output buffers; free each with kmp_free_host.  ids: NUL-separated id strings. */
+int kmp_read_fasta(const char* path, uint32_t* n, uint8_t** residues, uint64_t** offsets,
+                   uint16_t** class_id, char** ids, uint64_t* ids_bytes, uint32_t* n_classes);
+/* Synthetic sets of SURVEY.md §8d.  residues is malloc'd (free with kmp_free_host);
+ * offsets[N+1], class_id[N], family[N] are caller buffers (class_id/family may be NULL). */
+int kmp_synth_packed(uint32_t n, uint64_t seed, int length_law, uint8_t** residues,
+                     uint64_t* offsets, uint16_t* class_id, uint32_t* family);
+int kmp_synth_write_fasta(const char* path, uint32_t n, uint64_t seed, int length_law);
+void kmp_free_host(void* p);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KMERPAIR_H */

@@ -1,0 +1,452 @@
+/*
+ * kmp_oracle.c — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference's k-mer pair path
+ * (Isabella136/uniprot_kmer_based_clustering, snapshot 2025-05-23).  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library, and
+ * only as the checker / the timed CPU baseline; the product path never calls it.
+ *
+ * PARITY UNPINNED.  The reference is a Rust crate that cannot be built in this image
+ * (no rustc/cargo, crates not vendored, nightly-only) and it ships no
+ * tests, known-answer vectors or golden outputs.  This restatement is therefore pinned
+ * only by (1) hand-derived known-answer tests of the reference semantics
+ * (tests/golden/), (2) an independent NumPy restatement in tests/ (sparse A·Aᵀ), and
+ * (3) the dataset counters SURVEY.md §8c lists for uniprot_arg.fasta.
+ *
+ * Algorithm, phase for phase (file:line into /root/reference):
+ *   windows + radix-21 codes ......... src/protein.rs:9-54 (codec), :107-132 (windows)
+ *   per-protein sort+dedup ........... src/main.rs:280-282
+ *   global df, df>=2 "repeat" split .. src/main.rs:77-122 (merge_sort :23-48), :127-149
+ *   dense repeat ids (boomphf stand-in; ids differ from boomphf, unobservable in the
+ *     edge list) ...................... src/main.rs:139-147, src/protein.rs:151-174
+ *   Σ C(df,2) incidence expansion .... src/graph/mod.rs:39-193, src/graph/vertex.rs:59-140
+ *   AMR-class edge filter ............ src/graph/mod.rs:549-697 (test at :580-587)
+ *   per-pair collapse, w = #kmers .... src/graph/mod.rs:322-546, src/graph/edge.rs:56-85
+ *   alignment candidates w > 10 ...... src/graph/mod.rs:242
+ * The incidence expansion is executed row-wise (Gustavson): protein p walks the posting
+ * list of each of its repeat k-mers and counts the later visitors q; every (k-mer, p, q)
+ * incidence of the reference's multigraph is visited exactly once, the same-class ones
+ * are dropped as mod.rs:584 does, and the per-pair count is the collapsed Group length.
+ * Threading mirrors the reference's model (src/main.rs:84-121): `threads` workers pull
+ * protein indices from one atomic cursor.
+ */
+#include <pthread.h>
+#include <stdatomic.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ORC_OK 0
+#define ORC_EINVAL 1
+#define ORC_ENOMEM 2
+
+/* src/protein.rs:9-13 — code = position in this list, anything else -> 20 (:49-54) */
+static const char AMINO_ACID_LIST[21] = {'C', 'S', 'T', 'A', 'G', 'P', 'D', 'E', 'Q', 'N', 'H',
+                                         'R', 'K', 'M', 'I', 'L', 'V', 'W', 'Y', 'F', '*'};
+
+uint8_t orc_residue_code(uint8_t b) {
+    for (int i = 0; i < 21; ++i)  /* linear search as amino_acid_to_bits does */
+        if ((uint8_t)AMINO_ACID_LIST[i] == b) return (uint8_t)i;
+    return 20;
+}
+
+/* src/protein.rs:114 — windows j in [0, L-k]; L < k yields none (the reference wraps
+ * usize for L < 4 and panics; documented deviation in DESIGN.md). */
+static inline uint64_t n_windows(uint64_t L, int k) { return L >= (uint64_t)k ? L - k + 1 : 0; }
+
+/* src/protein.rs:29-37 generalised to k digits, big-endian base 21 */
+uint32_t orc_pack(const uint8_t* s, int k) {
+    uint32_t v = 0;
+    for (int i = 0; i < k; ++i) v = v * 21u + orc_residue_code(s[i]);
+    return v;
+}
+
+/* codes of every window of every protein; win_off[N+1] gets the CSR offsets */
+int orc_extract(const uint8_t* res, const uint64_t* off, uint32_t n, int k, uint32_t* out,
+                uint64_t* win_off) {
+    if (k < 1 || k > 7) return ORC_EINVAL;
+    uint8_t lut[256];
+    for (int b = 0; b < 256; ++b) lut[b] = orc_residue_code((uint8_t)b);
+    uint64_t w = 0;
+    for (uint32_t p = 0; p < n; ++p) {
+        win_off[p] = w;
+        uint64_t L = off[p + 1] - off[p];
+        const uint8_t* s = res + off[p];
+        uint64_t nw = n_windows(L, k);
+        for (uint64_t j = 0; j < nw; ++j) {
+            uint32_t v = 0;
+            for (int i = 0; i < k; ++i) v = v * 21u + lut[s[j + i]];
+            out[w++] = v;
+        }
+    }
+    win_off[n] = w;
+    return ORC_OK;
+}
+
+/* ---- LSD radix sort of u32 (8-bit digits); tmp has n slots ---- */
+static void radix_u32(uint32_t* a, uint32_t* tmp, uint64_t n) {
+    uint64_t cnt[256];
+    uint32_t *src = a, *dst = tmp;
+    for (int shift = 0; shift < 32; shift += 8) {
+        memset(cnt, 0, sizeof cnt);
+        for (uint64_t i = 0; i < n; ++i) cnt[(src[i] >> shift) & 255]++;
+        if (n == 0 || cnt[(src[0] >> shift) & 255] == n) continue; /* digit constant: skip pass */
+        uint64_t s = 0;
+        for (int d = 0; d < 256; ++d) { uint64_t c = cnt[d]; cnt[d] = s; s += c; }
+        for (uint64_t i = 0; i < n; ++i) dst[cnt[(src[i] >> shift) & 255]++] = src[i];
+        uint32_t* t = src; src = dst; dst = t;
+    }
+    if (src != a) memcpy(a, src, n * sizeof(uint32_t));
+}
+
+static void radix_u64(uint64_t* a, uint64_t* tmp, uint64_t n) {
+    uint64_t cnt[2048];
+    uint64_t *src = a, *dst = tmp;
+    for (int shift = 0; shift < 64; shift += 11) {
+        memset(cnt, 0, sizeof cnt);
+        for (uint64_t i = 0; i < n; ++i) cnt[(src[i] >> shift) & 2047]++;
+        if (n == 0 || cnt[(src[0] >> shift) & 2047] == n) continue;
+        uint64_t s = 0;
+        for (int d = 0; d < 2048; ++d) { uint64_t c = cnt[d]; cnt[d] = s; s += c; }
+        for (uint64_t i = 0; i < n; ++i) dst[cnt[(src[i] >> shift) & 2047]++] = src[i];
+        uint64_t* t = src; src = dst; dst = t;
+    }
+    if (src != a) memcpy(a, src, n * sizeof(uint64_t));
+}
+
+static void insertion_u32(uint32_t* a, uint64_t n) {
+    for (uint64_t i = 1; i < n; ++i) {
+        uint32_t v = a[i];
+        uint64_t j = i;
+        while (j > 0 && a[j - 1] > v) { a[j] = a[j - 1]; --j; }
+        a[j] = v;
+    }
+}
+
+static void sort_u32(uint32_t* a, uint32_t* tmp, uint64_t n) {
+    if (n < 48) insertion_u32(a, n);
+    else radix_u32(a, tmp, n);
+}
+
+static uint64_t dedup_sorted(uint32_t* a, uint64_t n) {
+    if (n == 0) return 0;
+    uint64_t m = 1;
+    for (uint64_t i = 1; i < n; ++i)
+        if (a[i] != a[m - 1]) a[m++] = a[i];
+    return m;
+}
+
+typedef struct {
+    uint64_t n_windows;   /* Σ (L-k+1) */
+    uint64_t sum_S;       /* Σ |K(p)| */
+    uint64_t distinct;    /* D: distinct k-mers over all proteins */
+    uint64_t repeat;      /* R: k-mers with df >= 2 (graph/mod.rs:50) */
+    uint64_t sum_cdf2;    /* Σ C(df,2): "Number of total edges" (graph/mod.rs:51) */
+    uint64_t sum_w_diff;  /* Σ w over class-differing pairs = edges after AMR filter (:695) */
+    uint64_t n_edges;     /* collapsed pairs emitted (:545 when min_shared == 1) */
+    uint64_t n_align;     /* emitted pairs with w > align_threshold (mod.rs:242) */
+    uint64_t pairs_any;   /* pairs with w >= 1 regardless of class */
+    uint64_t max_df;
+} orc_counters;
+
+typedef struct {
+    uint32_t n;
+    int k;
+    uint16_t* cls;
+    uint64_t* win_off;     /* [n+1] */
+    uint32_t* codes;       /* all windows, position order (Protein.five_mers) */
+    uint64_t* set_off;     /* [n+1] CSR of K(p), sorted distinct codes */
+    uint32_t* set_val;
+    uint32_t* distinct;    /* sorted distinct codes [D] */
+    uint32_t* df;          /* df per distinct code [D] */
+    uint64_t n_distinct;
+    uint32_t* rep_codes;   /* sorted repeat codes [R]; dense id = index (boomphf stand-in) */
+    uint64_t n_repeat;
+    uint32_t* rep_df;      /* five_mer_hash_freq (main.rs:154,192) */
+    uint64_t* hid_off;     /* [n+1] CSR of the protein's repeat ids, ascending */
+    uint32_t* hid_val;
+    uint32_t* hid_pos;     /* position of p inside posting(h) for each hid entry */
+    uint64_t* post_off;    /* [R+1] posting lists, protein index order */
+    uint32_t* post_val;
+    orc_counters c;
+    int threads;
+} orc_ctx;
+
+typedef struct {
+    orc_ctx* x;
+    _Atomic uint32_t cursor;
+} set_job;
+
+static void* set_worker(void* arg) {
+    set_job* j = (set_job*)arg;
+    orc_ctx* x = j->x;
+    uint32_t* tmp = NULL;
+    uint64_t tmp_cap = 0;
+    for (;;) {
+        uint32_t p = atomic_fetch_add(&j->cursor, 1);
+        if (p >= x->n) break;
+        uint64_t b = x->win_off[p], e = x->win_off[p + 1], m = e - b;
+        if (m > tmp_cap) {
+            free(tmp);
+            tmp_cap = m;
+            tmp = (uint32_t*)malloc(m * sizeof(uint32_t));
+        }
+        uint32_t* a = x->set_val + b;   /* sets stored at window offsets, compacted below */
+        memcpy(a, x->codes + b, m * sizeof(uint32_t));
+        sort_u32(a, tmp, m);
+        x->set_off[p] = dedup_sorted(a, m); /* temporarily: |K(p)| */
+    }
+    free(tmp);
+    return NULL;
+}
+
+static void run_pool(int threads, void* (*fn)(void*), void* arg) {
+    if (threads <= 1) { fn(arg); return; }
+    pthread_t* t = (pthread_t*)malloc(sizeof(pthread_t) * threads);
+    for (int i = 0; i < threads; ++i) pthread_create(&t[i], NULL, fn, arg);
+    for (int i = 0; i < threads; ++i) pthread_join(t[i], NULL);
+    free(t);
+}
+
+void orc_free_ctx(orc_ctx* x);
+
+/* Builds windows, K(p), df, repeat ids and posting lists. */
+orc_ctx* orc_build(const uint8_t* res, const uint64_t* off, uint32_t n, const uint16_t* cls, int k,
+                   int threads) {
+    if (k < 1 || k > 7) return NULL;
+    orc_ctx* x = (orc_ctx*)calloc(1, sizeof(orc_ctx));
+    x->n = n; x->k = k; x->threads = threads < 1 ? 1 : threads;
+    x->cls = (uint16_t*)malloc(sizeof(uint16_t) * (n ? n : 1));
+    if (cls) memcpy(x->cls, cls, sizeof(uint16_t) * n); else memset(x->cls, 0, sizeof(uint16_t) * n);
+    x->win_off = (uint64_t*)malloc(sizeof(uint64_t) * (n + 1));
+    uint64_t nw = 0;
+    for (uint32_t p = 0; p < n; ++p) nw += n_windows(off[p + 1] - off[p], k);
+    x->codes = (uint32_t*)malloc(sizeof(uint32_t) * (nw ? nw : 1));
+    orc_extract(res, off, n, k, x->codes, x->win_off);
+    x->c.n_windows = nw;
+
+    /* per-protein sort + dedup (main.rs:280-282) */
+    x->set_val = (uint32_t*)malloc(sizeof(uint32_t) * (nw ? nw : 1));
+    x->set_off = (uint64_t*)malloc(sizeof(uint64_t) * (n + 1));
+    set_job sj = {x, 0};
+    run_pool(x->threads, set_worker, &sj);
+    uint64_t s = 0;
+    for (uint32_t p = 0; p < n; ++p) {  /* compact in place (dst <= src always) */
+        uint64_t m = x->set_off[p];
+        memmove(x->set_val + s, x->set_val + x->win_off[p], m * sizeof(uint32_t));
+        x->set_off[p] = s;
+        s += m;
+    }
+    x->set_off[n] = s;
+    x->c.sum_S = s;
+
+    /* global df over distinct per-protein k-mers (main.rs:77-122): one radix sort of
+     * (code << 32 | protein) keys; each run of equal codes is one distinct k-mer, its
+     * length the df, its low halves the posting list in protein-index order (the
+     * visitor order of vertex.rs:100 with threads == 1). */
+    uint64_t* key = (uint64_t*)malloc(sizeof(uint64_t) * (s ? s : 1));
+    uint64_t* ktmp = (uint64_t*)malloc(sizeof(uint64_t) * (s ? s : 1));
+    for (uint32_t p = 0; p < n; ++p)
+        for (uint64_t i = x->set_off[p]; i < x->set_off[p + 1]; ++i)
+            key[i] = ((uint64_t)x->set_val[i] << 32) | p;
+    radix_u64(key, ktmp, s);
+    free(ktmp);
+    uint64_t d = 0, r = 0, cdf2 = 0, maxdf = 0, tot = 0;
+    for (uint64_t i = 0; i < s;) {
+        uint64_t j = i;
+        while (j < s && (key[j] >> 32) == (key[i] >> 32)) ++j;
+        ++d;
+        if (j - i >= 2) { ++r; tot += j - i; }
+        i = j;
+    }
+    x->distinct = (uint32_t*)malloc(sizeof(uint32_t) * (d ? d : 1));
+    x->df = (uint32_t*)malloc(sizeof(uint32_t) * (d ? d : 1));
+    x->rep_codes = (uint32_t*)malloc(sizeof(uint32_t) * (r ? r : 1));
+    x->rep_df = (uint32_t*)malloc(sizeof(uint32_t) * (r ? r : 1));
+    x->post_off = (uint64_t*)malloc(sizeof(uint64_t) * (r + 1));
+    x->post_val = (uint32_t*)malloc(sizeof(uint32_t) * (tot ? tot : 1));
+    d = 0; r = 0; tot = 0;
+    for (uint64_t i = 0; i < s;) {
+        uint64_t j = i;
+        while (j < s && (key[j] >> 32) == (key[i] >> 32)) ++j;
+        uint32_t f = (uint32_t)(j - i);
+        x->distinct[d] = (uint32_t)(key[i] >> 32);
+        x->df[d] = f;
+        ++d;
+        if (f >= 2) {   /* repeat split (main.rs:127-149); dense id = rank among repeats */
+            x->rep_codes[r] = (uint32_t)(key[i] >> 32);
+            x->rep_df[r] = f;
+            x->post_off[r] = tot;
+            for (uint64_t t = i; t < j; ++t) x->post_val[tot++] = (uint32_t)key[t];
+            cdf2 += (uint64_t)f * (f - 1) / 2;
+            if (f > maxdf) maxdf = f;
+            ++r;
+        }
+        i = j;
+    }
+    x->post_off[r] = tot;
+    free(key);
+    x->n_distinct = d;
+    x->n_repeat = r;
+    x->c.distinct = d;
+    x->c.repeat = r;
+    x->c.sum_cdf2 = cdf2;
+    x->c.max_df = maxdf;
+
+    /* remove_unique_five_mers + modify_hash_five_mer (protein.rs:151-174): each protein's
+     * repeat ids, ascending, with its position inside the id's posting list */
+    x->hid_off = (uint64_t*)calloc(n + 1, sizeof(uint64_t));
+    for (uint64_t t = 0; t < tot; ++t) x->hid_off[x->post_val[t] + 1]++;
+    for (uint32_t p = 0; p < n; ++p) x->hid_off[p + 1] += x->hid_off[p];
+    x->hid_val = (uint32_t*)malloc(sizeof(uint32_t) * (tot ? tot : 1));
+    x->hid_pos = (uint32_t*)malloc(sizeof(uint32_t) * (tot ? tot : 1));
+    uint64_t* fill = (uint64_t*)malloc(sizeof(uint64_t) * (n + 1));
+    memcpy(fill, x->hid_off, sizeof(uint64_t) * (n + 1));
+    for (uint64_t h = 0; h < r; ++h)
+        for (uint64_t t = x->post_off[h]; t < x->post_off[h + 1]; ++t) {
+            uint32_t p = x->post_val[t];
+            x->hid_val[fill[p]] = (uint32_t)h;
+            x->hid_pos[fill[p]] = (uint32_t)(t - x->post_off[h]);
+            fill[p]++;
+        }
+    free(fill);
+    return x;
+}
+
+/* ---- pair expansion + class filter + collapse ---- */
+typedef struct {
+    uint32_t* q;
+    uint32_t* w;
+    uint64_t n, cap;
+} edge_buf;
+
+typedef struct {
+    orc_ctx* x;
+    _Atomic uint32_t cursor;
+    uint32_t min_shared;
+    int require_class_diff;
+    uint32_t align_threshold;
+    edge_buf* rows;          /* one per protein p */
+    _Atomic uint64_t pairs_any, sum_w_diff, n_align;
+} pair_job;
+
+static void* pair_worker(void* arg) {
+    pair_job* j = (pair_job*)arg;
+    orc_ctx* x = j->x;
+    uint32_t n = x->n;
+    uint32_t* cnt = (uint32_t*)calloc(n ? n : 1, sizeof(uint32_t));
+    uint32_t* touched = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+    uint32_t* tmp = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+    uint64_t any = 0, wdiff = 0, nal = 0;
+    for (;;) {
+        uint32_t p = atomic_fetch_add(&j->cursor, 1);
+        if (p >= n) break;
+        uint64_t nt = 0;
+        /* every (k-mer h, p, q>p) incidence of the multigraph (vertex.rs:103-137) */
+        for (uint64_t i = x->hid_off[p]; i < x->hid_off[p + 1]; ++i) {
+            uint32_t h = x->hid_val[i];
+            uint64_t b = x->post_off[h] + x->hid_pos[i] + 1, e = x->post_off[h + 1];
+            for (uint64_t t = b; t < e; ++t) {
+                uint32_t q = x->post_val[t];
+                if (cnt[q]++ == 0) touched[nt++] = q;
+            }
+        }
+        sort_u32(touched, tmp, nt);
+        edge_buf* row = &j->rows[p];
+        for (uint64_t t = 0; t < nt; ++t) {
+            uint32_t q = touched[t], w = cnt[q];
+            cnt[q] = 0;
+            ++any;
+            int differ = x->cls[p] != x->cls[q];   /* mod.rs:580-587 */
+            if (differ) wdiff += w;
+            if ((differ || !j->require_class_diff) && w >= j->min_shared) {
+                if (row->n == row->cap) {
+                    row->cap = row->cap ? row->cap * 2 : 16;
+                    row->q = (uint32_t*)realloc(row->q, row->cap * sizeof(uint32_t));
+                    row->w = (uint32_t*)realloc(row->w, row->cap * sizeof(uint32_t));
+                }
+                row->q[row->n] = q;
+                row->w[row->n] = w;
+                row->n++;
+                if (w > j->align_threshold) ++nal;
+            }
+        }
+    }
+    atomic_fetch_add(&j->pairs_any, any);
+    atomic_fetch_add(&j->sum_w_diff, wdiff);
+    atomic_fetch_add(&j->n_align, nal);
+    free(cnt); free(touched); free(tmp);
+    return NULL;
+}
+
+/* Canonical edge list: (p,q,w), p<q, sorted by (p,q).  Arrays malloc'd; free with orc_free. */
+int orc_pairs(orc_ctx* x, uint32_t min_shared, int require_class_diff, uint32_t align_threshold,
+              uint32_t** P, uint32_t** Q, uint32_t** W, uint64_t* n_edges) {
+    if (!x) return ORC_EINVAL;
+    pair_job j;
+    j.x = x;
+    atomic_init(&j.cursor, 0);
+    j.min_shared = min_shared < 1 ? 1 : min_shared;
+    j.require_class_diff = require_class_diff;
+    j.align_threshold = align_threshold;
+    j.rows = (edge_buf*)calloc(x->n ? x->n : 1, sizeof(edge_buf));
+    atomic_init(&j.pairs_any, 0);
+    atomic_init(&j.sum_w_diff, 0);
+    atomic_init(&j.n_align, 0);
+    run_pool(x->threads, pair_worker, &j);
+    uint64_t tot = 0;
+    for (uint32_t p = 0; p < x->n; ++p) tot += j.rows[p].n;
+    uint32_t* pp = (uint32_t*)malloc(sizeof(uint32_t) * (tot ? tot : 1));
+    uint32_t* qq = (uint32_t*)malloc(sizeof(uint32_t) * (tot ? tot : 1));
+    uint32_t* ww = (uint32_t*)malloc(sizeof(uint32_t) * (tot ? tot : 1));
+    uint64_t o = 0;
+    for (uint32_t p = 0; p < x->n; ++p) {
+        edge_buf* r = &j.rows[p];
+        for (uint64_t t = 0; t < r->n; ++t) { pp[o] = p; qq[o] = r->q[t]; ww[o] = r->w[t]; ++o; }
+        free(r->q); free(r->w);
+    }
+    free(j.rows);
+    x->c.pairs_any = atomic_load(&j.pairs_any);
+    x->c.sum_w_diff = atomic_load(&j.sum_w_diff);
+    x->c.n_edges = tot;
+    x->c.n_align = atomic_load(&j.n_align);
+    *P = pp; *Q = qq; *W = ww; *n_edges = tot;
+    return ORC_OK;
+}
+
+void orc_get_counters(const orc_ctx* x, orc_counters* c) { *c = x->c; }
+uint64_t orc_n_windows(const orc_ctx* x) { return x->c.n_windows; }
+const uint32_t* orc_codes(const orc_ctx* x) { return x->codes; }
+const uint64_t* orc_win_off(const orc_ctx* x) { return x->win_off; }
+const uint32_t* orc_set_val(const orc_ctx* x) { return x->set_val; }
+const uint64_t* orc_set_off(const orc_ctx* x) { return x->set_off; }
+const uint32_t* orc_rep_codes(const orc_ctx* x) { return x->rep_codes; }
+const uint32_t* orc_rep_df(const orc_ctx* x) { return x->rep_df; }
+uint64_t orc_n_repeat(const orc_ctx* x) { return x->n_repeat; }
+const uint32_t* orc_distinct(const orc_ctx* x) { return x->distinct; }
+const uint32_t* orc_distinct_df(const orc_ctx* x) { return x->df; }
+uint64_t orc_n_distinct(const orc_ctx* x) { return x->n_distinct; }
+
+/* shared codes of (p,q), ascending (KmerEdgeGroup.kmers by code, edge.rs:56-85) */
+uint64_t orc_shared(const orc_ctx* x, uint32_t p, uint32_t q, uint32_t* out, uint64_t cap) {
+    const uint32_t* a = x->set_val + x->set_off[p];
+    const uint32_t* b = x->set_val + x->set_off[q];
+    uint64_t na = x->set_off[p + 1] - x->set_off[p], nb = x->set_off[q + 1] - x->set_off[q];
+    uint64_t i = 0, k = 0, m = 0;
+    while (i < na && k < nb) {
+        if (a[i] < b[k]) ++i;
+        else if (a[i] > b[k]) ++k;
+        else { if (m < cap) out[m] = a[i]; ++m; ++i; ++k; }
+    }
+    return m;
+}
+
+void orc_free(void* p) { free(p); }
+
+void orc_free_ctx(orc_ctx* x) {
+    if (!x) return;
+    free(x->cls); free(x->win_off); free(x->codes); free(x->set_off); free(x->set_val);
+    free(x->distinct); free(x->df); free(x->rep_codes); free(x->rep_df); free(x->hid_off);
+    free(x->hid_val); free(x->hid_pos); free(x->post_off); free(x->post_val);
+    free(x);
+}

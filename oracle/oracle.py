@@ -1,0 +1,150 @@
+"""ctypes binding of the CPU restatement (oracle/kmp_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, never by the product package.  PARITY UNPINNED — see kmp_oracle.c's
+header and DESIGN.md "Oracle": the Rust reference cannot be built or run here and ships no
+golden outputs, so this restatement is pinned by hand-derived known answers, an
+independent NumPy restatement (tests/numpy_ref.py) and the dataset counters of SURVEY.md §8c.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+
+class Counters(C.Structure):
+    _fields_ = [(name, C.c_uint64) for name in (
+        "n_windows", "sum_S", "distinct", "repeat", "sum_cdf2", "sum_w_diff", "n_edges",
+        "n_align", "pairs_any", "max_df")]
+
+    def as_dict(self):
+        return {name: int(getattr(self, name)) for name, _ in self._fields_}
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = C.CDLL(_LIB_PATH)
+        P = C.c_void_p
+        L.orc_build.restype = P
+        L.orc_build.argtypes = [P, P, C.c_uint32, P, C.c_int, C.c_int]
+        L.orc_pairs.restype = C.c_int
+        L.orc_pairs.argtypes = [P, C.c_uint32, C.c_int, C.c_uint32, C.POINTER(P), C.POINTER(P),
+                                C.POINTER(P), C.POINTER(C.c_uint64)]
+        L.orc_get_counters.argtypes = [P, C.POINTER(Counters)]
+        for name in ("orc_codes", "orc_win_off", "orc_set_val", "orc_set_off", "orc_rep_codes",
+                     "orc_rep_df", "orc_distinct", "orc_distinct_df"):
+            getattr(L, name).restype = P
+            getattr(L, name).argtypes = [P]
+        for name in ("orc_n_windows", "orc_n_repeat", "orc_n_distinct"):
+            getattr(L, name).restype = C.c_uint64
+            getattr(L, name).argtypes = [P]
+        L.orc_shared.restype = C.c_uint64
+        L.orc_shared.argtypes = [P, C.c_uint32, C.c_uint32, P, C.c_uint64]
+        L.orc_free.argtypes = [P]
+        L.orc_free_ctx.argtypes = [P]
+        L.orc_residue_code.restype = C.c_uint8
+        L.orc_residue_code.argtypes = [C.c_uint8]
+        L.orc_pack.restype = C.c_uint32
+        L.orc_pack.argtypes = [C.c_char_p, C.c_int]
+        _lib = L
+    return _lib
+
+
+def _view(ptr, n, dtype):
+    if n == 0:
+        return np.zeros(0, dtype=dtype)
+    ct = {np.uint32: C.c_uint32, np.uint64: C.c_uint64}[dtype]
+    return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ct)), shape=(n,)).copy()
+
+
+class Oracle:
+    """One restated pipeline run over packed proteins (residues u8, offsets u64[N+1])."""
+
+    def __init__(self, residues, offsets, class_id=None, k=5, threads=1):
+        L = lib()
+        self.residues = np.ascontiguousarray(residues, dtype=np.uint8)
+        self.offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        self.n = len(self.offsets) - 1
+        self.cls = None if class_id is None else np.ascontiguousarray(class_id, dtype=np.uint16)
+        self.k = k
+        res_ptr = self.residues.ctypes.data if self.residues.size else None
+        self._ctx = L.orc_build(res_ptr, self.offsets.ctypes.data, self.n,
+                                None if self.cls is None else self.cls.ctypes.data, k, threads)
+        if not self._ctx:
+            raise ValueError("orc_build failed")
+
+    def __del__(self):
+        if getattr(self, "_ctx", None):
+            lib().orc_free_ctx(self._ctx)
+            self._ctx = None
+
+    def counters(self):
+        c = Counters()
+        lib().orc_get_counters(self._ctx, C.byref(c))
+        return c.as_dict()
+
+    def codes(self):
+        L = lib()
+        return _view(L.orc_codes(self._ctx), L.orc_n_windows(self._ctx), np.uint32)
+
+    def win_off(self):
+        return _view(lib().orc_win_off(self._ctx), self.n + 1, np.uint64)
+
+    def sets(self):
+        L = lib()
+        off = _view(L.orc_set_off(self._ctx), self.n + 1, np.uint64)
+        return off, _view(L.orc_set_val(self._ctx), int(off[-1]), np.uint32)
+
+    def repeat(self):
+        L = lib()
+        r = L.orc_n_repeat(self._ctx)
+        return _view(L.orc_rep_codes(self._ctx), r, np.uint32), _view(L.orc_rep_df(self._ctx), r, np.uint32)
+
+    def distinct(self):
+        L = lib()
+        d = L.orc_n_distinct(self._ctx)
+        return _view(L.orc_distinct(self._ctx), d, np.uint32), _view(L.orc_distinct_df(self._ctx), d, np.uint32)
+
+    def pairs(self, min_shared=1, require_class_diff=True, align_threshold=10):
+        L = lib()
+        P, Q, W = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        n = C.c_uint64()
+        st = L.orc_pairs(self._ctx, min_shared, int(require_class_diff), align_threshold,
+                         C.byref(P), C.byref(Q), C.byref(W), C.byref(n))
+        if st != 0:
+            raise RuntimeError(f"orc_pairs status {st}")
+        out = (_view(P.value, n.value, np.uint32), _view(Q.value, n.value, np.uint32),
+               _view(W.value, n.value, np.uint32))
+        for ptr in (P, Q, W):
+            L.orc_free(ptr)
+        return out
+
+    def shared(self, p, q):
+        buf = np.zeros(4096, dtype=np.uint32)
+        m = lib().orc_shared(self._ctx, p, q, buf.ctypes.data, buf.size)
+        if m > buf.size:
+            buf = np.zeros(m, dtype=np.uint32)
+            lib().orc_shared(self._ctx, p, q, buf.ctypes.data, buf.size)
+        return buf[:m].copy()
+
+
+def residue_code(b: int) -> int:
+    return int(lib().orc_residue_code(b))
+
+
+def pack(kmer: bytes) -> int:
+    return int(lib().orc_pack(kmer, len(kmer)))
