@@ -2,7 +2,7 @@
  * kmerpair.h — C ABI of the MI355X-native k-mer pair engine (libkmerpair.so).
  *
  * Drop-in boundary for the hot path of Isabella136/uniprot_kmer_based_clustering:
- * the Rust module surface that src/main.rs calls in src/protein.rs and src/graph/*.
+ * the Rust module surface that src/main.rs calls in src/protein.rs and the src/graph/ modules.
  * The reference has no FFI of its own; each entry point below names the
  * reference interface it replaces (file:line in the reference tree).  INTEGRATION.md
  * shows the Rust `extern "C"` block a maintainer would add to bind it.
@@ -120,58 +120,66 @@ int kmp_edges_get(const kmp_edges* e, uint32_t* p, uint32_t* q, uint32_t* w, flo
 void kmp_edges_free(kmp_edges* e);
 
 /* ------------------------------------------------------------------ device stages -- */
-/* Workspace sizes for the device stages; all in bytes. */
-typedef struct {
-    uint64_t tile_slots;      /* LDS hash slots per row tile */
-    uint64_t tile_cap;        /* max set entries per row tile */
-    uint64_t rows_max;        /* max proteins per row tile */
-} kmp_pair_geometry;
-void kmp_dev_pair_geometry(kmp_pair_geometry* g);
+/* Device layout.  Every per-protein u32 array (window codes, K(p), repeat-filtered K(p))
+ * lives in one buffer of kmp_set_capacity(N, ΣL) elements; protein p owns the 16-B
+ * aligned slot range starting at kmp_set_base(res_off[p], p) = round_up(res_off[p]+4p, 4),
+ * L_p + 4 slots long (>= its window count).  No offset scan is needed on the device. */
+uint64_t kmp_set_capacity(uint32_t n, uint64_t total_residues);
+uint64_t kmp_set_base(uint64_t res_off, uint32_t p);
 
-/* win_off[p] = Σ_{i<p} max(0, L_i - k + 1) for p in 0..N (exclusive scan on device). */
-int kmp_dev_window_offsets(const uint64_t* d_res_off, uint32_t n, int k, uint64_t* d_win_off,
-                           void* stream);
-/* All windows' codes, position order, at d_codes[win_off[p] ...]. */
-int kmp_dev_extract(const uint8_t* d_res, const uint64_t* d_res_off, const uint64_t* d_win_off,
-                    uint32_t n, int k, uint32_t* d_codes, void* stream);
-/* Fused extract + per-protein sort + dedup: K(p) ascending at d_set[win_off[p] ...],
- * |K(p)| in d_set_len[p].  d_scratch: >= 4 * win_off[N] bytes (used by proteins whose
- * window count exceeds the in-LDS sort, may be NULL when none does). */
-int kmp_dev_build_sets(const uint8_t* d_res, const uint64_t* d_res_off, const uint64_t* d_win_off,
-                       uint32_t n, int k, uint32_t* d_set, uint32_t* d_set_len, uint32_t* d_scratch,
+/* All windows' codes in position order (Protein.five_mers, protein.rs:107-132). */
+int kmp_dev_extract(const uint8_t* d_res, const uint64_t* d_res_off, uint32_t n, int k,
+                    uint32_t* d_codes, void* stream);
+/* Fused extract + per-protein sort + dedup: K(p) ascending in p's slot of d_set, |K(p)| in
+ * d_set_len[p].  max_len: longest protein in residues (0 = unknown).  Proteins with more
+ * than KMP_LDS_SORT_MAX windows are sorted in global memory in d_scratch (same capacity as
+ * d_set; may be NULL when max_len shows none is that long). */
+#define KMP_LDS_SORT_MAX 4096
+int kmp_dev_build_sets(const uint8_t* d_res, const uint64_t* d_res_off, uint32_t n, int k,
+                       uint32_t max_len, uint32_t* d_set, uint32_t* d_set_len, uint32_t* d_scratch,
                        void* stream);
-/* Number of 32-bit words of each repeat bitmap for k (21^k bits rounded up). */
+/* 32-bit words of ONE repeat bitmap for k (21^k bits rounded up). */
 uint64_t kmp_dev_repeat_bitmap_words(int k);
-/* remove_unique_five_mers (protein.rs:151-162): marks df>=1 / df>=2 in two bitmaps, then
- * compacts each set to its repeat k-mers (d_rep[win_off[p] ...], d_rep_len[p]).  The two
- * bitmaps (d_bits, 2 * kmp_dev_repeat_bitmap_words(k) words) are zeroed inside. */
-int kmp_dev_filter_repeats(const uint32_t* d_set, const uint32_t* d_set_len, const uint64_t* d_win_off,
+/* remove_unique_five_mers (protein.rs:151-162): zeroes then fills two bitmaps over the
+ * code space (seen once / seen in >= 2 proteins), then compacts every set to its repeat
+ * k-mers (order kept) into d_rep / d_rep_len.  d_bits: 2 * kmp_dev_repeat_bitmap_words(k). */
+int kmp_dev_filter_repeats(const uint32_t* d_set, const uint32_t* d_set_len, const uint64_t* d_res_off,
                            uint32_t n, int k, uint32_t* d_bits, uint32_t* d_rep, uint32_t* d_rep_len,
                            void* stream);
 
-/* A work item of the pair kernel: rows [row_beg,row_end) × columns [col_beg,col_end). */
+/* A work item of the pair kernel: row proteins [row_beg,row_end) (one LDS-resident tile)
+ * against column proteins [col_beg,col_end) (streamed); pairs (p,q) with p < q only. */
 typedef struct {
     uint32_t row_beg, row_end, col_beg, col_end;
 } kmp_work_item;
 
-/* Host-side planner: row tiles packed greedily (Σ len <= tile_cap, count <= rows_max),
- * each tile's upper-triangle column range cut into chunks of about chunk_cost set entries.
- * Returns the item count in *n_items (capacity cap; KMP_EOVERFLOW with the needed size). */
+/* Row-tile geometry of the pair kernel (fixed at build time). */
+typedef struct {
+    uint32_t tile_slots;  /* LDS hash slots per row tile */
+    uint32_t tile_cap;    /* max set entries per row tile */
+    uint32_t rows_max;    /* max proteins per row tile */
+    uint32_t threads;     /* workgroup size */
+} kmp_pair_geometry;
+void kmp_pair_geometry_get(kmp_pair_geometry* g);
+
+/* Host-side planner: row tiles packed greedily in index order (Σ len <= tile_cap, count <=
+ * rows_max; a protein longer than tile_cap is an error), each tile's upper-triangle column
+ * range [tile_beg, N) cut into chunks of about chunk_cost set entries.  Items are emitted
+ * in (tile, chunk) order.  *n_items = items needed; KMP_EOVERFLOW if cap is smaller. */
 int kmp_plan_pairs(const uint32_t* set_len, uint32_t n, uint64_t chunk_cost, kmp_work_item* items,
                    uint64_t cap, uint64_t* n_items);
 
-/* The pair kernel over work items [0, n_items): appends (p, q, w) with p < q, w >= min_shared
- * and (if required) class[p] != class[q] to d_p/d_q/d_w (unordered) at positions
- * d_count[0]++ (< cap; d_count keeps counting past cap so the caller can resize and rerun).
- * d_set/d_set_len/d_win_off describe the (possibly repeat-filtered) sets.
- * d_count must be zeroed by the caller (it is a 64-bit counter). */
-int kmp_dev_pairs(const uint32_t* d_set, const uint32_t* d_set_len, const uint64_t* d_win_off,
+/* The pair kernel over work items [0, n_items): appends (p, q, w) with p < q,
+ * w = |K(p) ∩ K(q)| >= min_shared and (if required) class[p] != class[q] to d_p/d_q/d_w in
+ * arbitrary order at positions d_count[0]++ (< cap; the counter keeps counting past cap so
+ * the caller can resize and rerun).  d_count (one u64) must be zeroed by the caller. */
+int kmp_dev_pairs(const uint32_t* d_set, const uint32_t* d_set_len, const uint64_t* d_res_off,
                   const uint16_t* d_class, uint32_t n, const kmp_work_item* d_items, uint64_t n_items,
                   uint32_t min_shared, int require_class_diff, uint32_t* d_p, uint32_t* d_q,
                   uint32_t* d_w, uint64_t cap, unsigned long long* d_count, void* stream);
 
-/* Canonical order: sorts n edges by (p, q) in place (keys packed p·N+q).  d_tmp: bytes from
- * kmp_dev_sort_edges_tmp_bytes(n, n_proteins). */
+/* Canonical order: sorts n edges by (p, q).  Keys/values are read from d_p/d_q/d_w and the
+ * sorted result is written back to them.  d_tmp: kmp_dev_sort_edges_tmp_bytes(n, N) bytes. */
 uint64_t kmp_dev_sort_edges_tmp_bytes(uint64_t n, uint32_t n_proteins);
 int kmp_dev_sort_edges(uint32_t* d_p, uint32_t* d_q, uint32_t* d_w, uint64_t n, uint32_t n_proteins,
                        void* d_tmp, uint64_t tmp_bytes, void* stream);

@@ -1,0 +1,106 @@
+"""The oracle (CPU restatement, oracle/) against the hand-derived golden vectors, the
+dataset counters of SURVEY.md §8c and an independent NumPy restatement (numpy_ref.py).
+PARITY UNPINNED against the reference binary itself (see DESIGN.md "Oracle")."""
+import numpy as np
+import pytest
+
+from common import (edges_sha256, load_json, make_batch, read_edges_tsv, slice_proteins, tiny,
+                    uniprot)
+import numpy_ref
+
+
+def test_codec_known_answers(oracle_mod):
+    kat = load_json("codec_kat.json")
+    for ch, code in kat["residue_codes"].items():
+        assert oracle_mod.residue_code(ord(ch)) == code, ch
+        assert numpy_ref.LUT[ord(ch)] == code
+    for kmer, code in kat["kmers"]:
+        assert oracle_mod.pack(kmer.encode()) == code, kmer
+        assert int(numpy_ref.window_codes(kmer.encode(), len(kmer))[0]) == code
+
+
+@pytest.mark.parametrize("k", [5, 7])
+def test_tiny_fixture(oracle_mod, k):
+    res, off, cls, _ = tiny()
+    o = oracle_mod.Oracle(res, off, cls, k=k)
+    p, q, w = o.pairs()
+    ep, eq, ew = read_edges_tsv(f"tiny_k{k}_edges.tsv")
+    np.testing.assert_array_equal(p, ep)
+    np.testing.assert_array_equal(q, eq)
+    np.testing.assert_array_equal(w, ew)
+    exp = load_json("tiny_counters.json")[str(k)]
+    c = o.counters()
+    for key, val in exp.items():
+        assert c[key] == val, key
+
+
+def test_windows_and_sets_semantics(oracle_mod):
+    # repeated k-mer inside a protein, L == k, L == k-1, L < k-1, empty protein
+    seqs = [b"AAAAAAA", b"CSTAG", b"CSTA", b"CS", b""]
+    res, off, cls = make_batch(seqs, ["a", "b", "c", "d", "e"])
+    o = oracle_mod.Oracle(res, off, cls, k=5)
+    wo = o.win_off()
+    assert list(np.diff(wo)) == [3, 1, 0, 0, 0]
+    so, sv = o.sets()
+    assert list(np.diff(so)) == [1, 1, 0, 0, 0]
+    assert int(sv[0]) == oracle_mod.pack(b"AAAAA")
+    assert int(sv[1]) == oracle_mod.pack(b"CSTAG")
+
+
+def test_uniprot_counters_and_edges(oracle_mod):
+    res, off, cls, _ = uniprot()
+    gold = load_json("uniprot_counters.json")
+    assert len(off) - 1 == gold["n_proteins"]
+    for k in (5, 7):
+        o = oracle_mod.Oracle(res, off, cls, k=k, threads=4)
+        p, q, w = o.pairs()
+        c = o.counters()
+        g = gold[str(k)]
+        for key in ("distinct", "repeat", "sum_cdf2", "sum_w_diff", "n_edges", "n_align", "pairs_any",
+                    "sum_S", "max_df", "n_windows"):
+            assert c[key] == g[key], (k, key)
+        assert edges_sha256(p, q, w) == g["edges_sha256"]
+        assert np.all(p < q)
+        key = p.astype(np.uint64) * len(off) + q
+        assert np.all(np.diff(key.astype(np.int64)) > 0)
+
+
+@pytest.mark.parametrize("k", [5, 7])
+def test_oracle_vs_numpy_subset(oracle_mod, k):
+    res, off, cls, _ = uniprot()
+    rng = np.random.default_rng(k)
+    idx = np.sort(rng.choice(len(off) - 1, size=2500, replace=False))
+    r2, o2, c2 = slice_proteins(res, off, cls, idx)
+    o = oracle_mod.Oracle(r2, o2, c2, k=k, threads=4)
+    for diff in (True, False):
+        p, q, w = o.pairs(require_class_diff=diff)
+        np_p, np_q, np_w, cnt = numpy_ref.pair_weights(r2, o2, c2, k, require_class_diff=diff)
+        np.testing.assert_array_equal(p, np_p)
+        np.testing.assert_array_equal(q, np_q)
+        np.testing.assert_array_equal(w, np_w)
+    c = o.counters()
+    for key in ("distinct", "repeat", "sum_cdf2", "sum_S"):
+        assert c[key] == cnt[key], key
+
+
+def test_oracle_vs_numpy_synthetic(oracle_mod):
+    import uniprot_kmer_based_clustering_amd as K
+    b = K.synth(1500, 11)
+    o = oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=7, threads=2)
+    p, q, w = o.pairs()
+    np_p, np_q, np_w, _ = numpy_ref.pair_weights(b.residues, b.offsets, b.class_id, 7)
+    np.testing.assert_array_equal(p, np_p)
+    np.testing.assert_array_equal(q, np_q)
+    np.testing.assert_array_equal(w, np_w)
+    assert len(p) > 100  # families make the k=7 edge list non-trivial
+
+
+def test_min_shared_and_threads_invariance(oracle_mod):
+    res, off, cls, _ = uniprot()
+    idx = np.arange(0, len(off) - 1, 7)
+    r2, o2, c2 = slice_proteins(res, off, cls, idx)
+    base = oracle_mod.Oracle(r2, o2, c2, k=5, threads=1).pairs(min_shared=3)
+    multi = oracle_mod.Oracle(r2, o2, c2, k=5, threads=8).pairs(min_shared=3)
+    for a, b in zip(base, multi):
+        np.testing.assert_array_equal(a, b)
+    assert np.all(base[2] >= 3)

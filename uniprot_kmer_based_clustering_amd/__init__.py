@@ -1,0 +1,9 @@
+"""MI355X-native k-mer pair engine for the hot path of Isabella136/uniprot_kmer_based_clustering.
+
+libkmerpair.so (hand-written HIP for gfx950 behind the C ABI of include/kmerpair.h) does
+the work; this package is the Python face used by tests, bench.py and the multi-GPU driver.
+"""
+from . import _lib  # noqa: F401
+from .engine import Edges, KmerPairEngine, Proteins, read_fasta, synth, write_synth_fasta  # noqa: F401
+
+__all__ = ["KmerPairEngine", "Proteins", "Edges", "read_fasta", "synth", "write_synth_fasta"]

@@ -1,0 +1,136 @@
+"""ctypes binding of libkmerpair.so (include/kmerpair.h).
+
+The library is built in-tree (``lib/libkmerpair.so``) by ``__graft_entry__.build()`` /
+``make -C uniprot_kmer_based_clustering_amd/csrc``.  There is no fallback: if the library is
+missing or fails to load, every entry point raises — the product path never substitutes a
+CPU implementation.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libkmerpair.so")
+HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "kmerpair.h")
+
+KMP_OK, KMP_EINVAL, KMP_ENOMEM, KMP_EDEVICE, KMP_ERCCL, KMP_EOVERFLOW, KMP_ESTATE, KMP_EIO = range(8)
+KMP_LEN_NORMAL300, KMP_LEN_LOGUNIFORM = 0, 1
+KMP_SCORE_COUNT, KMP_SCORE_JACCARD = 0, 1
+KMP_LDS_SORT_MAX = 4096
+
+
+class KmpError(RuntimeError):
+    def __init__(self, status: int, where: str, detail: str = ""):
+        self.status = status
+        msg = f"{where}: {status_string(status)} ({status})"
+        if detail:
+            msg += f": {detail}"
+        super().__init__(msg)
+
+
+class Counters(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in (
+        "n_proteins", "n_windows", "sum_S", "distinct", "repeat", "sum_cdf2", "sum_w_diff",
+        "n_edges", "n_align", "max_df")]
+
+    def as_dict(self):
+        return {n: int(getattr(self, n)) for n, _ in self._fields_}
+
+
+class PairOpts(C.Structure):
+    _fields_ = [("min_shared", C.c_uint32), ("require_class_diff", C.c_int32),
+                ("align_threshold", C.c_uint32), ("score", C.c_int32)]
+
+
+class WorkItem(C.Structure):
+    _fields_ = [("row_beg", C.c_uint32), ("row_end", C.c_uint32),
+                ("col_beg", C.c_uint32), ("col_end", C.c_uint32)]
+
+
+class PairGeometry(C.Structure):
+    _fields_ = [("tile_slots", C.c_uint32), ("tile_cap", C.c_uint32),
+                ("rows_max", C.c_uint32), ("threads", C.c_uint32)]
+
+
+P = C.c_void_p
+U8P = C.POINTER(C.c_uint8)
+U64P = C.POINTER(C.c_uint64)
+
+# name -> (restype, argtypes); every function declared in include/kmerpair.h
+SIGNATURES = {
+    "kmp_version": (C.c_int, []),
+    "kmp_status_string": (C.c_char_p, [C.c_int]),
+    "kmp_pair_opts_default": (None, [P]),
+    "kmp_ctx_create": (C.c_int, [C.POINTER(P), C.c_int, C.c_int]),
+    "kmp_ctx_destroy": (None, [P]),
+    "kmp_last_error": (C.c_char_p, [P]),
+    "kmp_load_proteins": (C.c_int, [P, P, P, C.c_uint32, P]),
+    "kmp_extract": (C.c_int, [P, C.c_int]),
+    "kmp_get_kmers": (C.c_int, [P, C.c_uint32, P, C.c_uint64, U64P]),
+    "kmp_build_sets": (C.c_int, [P, C.c_int]),
+    "kmp_get_set": (C.c_int, [P, C.c_uint32, P, C.c_uint64, U64P]),
+    "kmp_counters_get": (C.c_int, [P, P]),
+    "kmp_pairs": (C.c_int, [P, P, C.POINTER(P)]),
+    "kmp_edges_count": (C.c_int, [P, U64P]),
+    "kmp_edges_get": (C.c_int, [P, P, P, P, P, C.c_uint64, U64P]),
+    "kmp_edges_free": (None, [P]),
+    "kmp_set_capacity": (C.c_uint64, [C.c_uint32, C.c_uint64]),
+    "kmp_set_base": (C.c_uint64, [C.c_uint64, C.c_uint32]),
+    "kmp_dev_extract": (C.c_int, [P, P, C.c_uint32, C.c_int, P, P]),
+    "kmp_dev_build_sets": (C.c_int, [P, P, C.c_uint32, C.c_int, C.c_uint32, P, P, P, P]),
+    "kmp_dev_repeat_bitmap_words": (C.c_uint64, [C.c_int]),
+    "kmp_dev_filter_repeats": (C.c_int, [P, P, P, C.c_uint32, C.c_int, P, P, P, P]),
+    "kmp_pair_geometry_get": (None, [P]),
+    "kmp_plan_pairs": (C.c_int, [P, C.c_uint32, C.c_uint64, P, C.c_uint64, U64P]),
+    "kmp_dev_pairs": (C.c_int, [P, P, P, P, C.c_uint32, P, C.c_uint64, C.c_uint32, C.c_int,
+                                P, P, P, C.c_uint64, P, P]),
+    "kmp_dev_sort_edges_tmp_bytes": (C.c_uint64, [C.c_uint64, C.c_uint32]),
+    "kmp_dev_sort_edges": (C.c_int, [P, P, P, C.c_uint64, C.c_uint32, P, C.c_uint64, P]),
+    "kmp_read_fasta": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint32), C.POINTER(P), C.POINTER(P),
+                                 C.POINTER(P), C.POINTER(P), U64P, C.POINTER(C.c_uint32)]),
+    "kmp_synth_packed": (C.c_int, [C.c_uint32, C.c_uint64, C.c_int, C.POINTER(P), P, P, P]),
+    "kmp_synth_write_fasta": (C.c_int, [C.c_char_p, C.c_uint32, C.c_uint64, C.c_int]),
+    "kmp_free_host": (None, [P]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libkmerpair.so (raises if it is missing: no CPU fallback exists)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
+                "(hipcc --offload-arch=gfx950); the k-mer pair path has no CPU fallback")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def status_string(s: int) -> str:
+    try:
+        return lib().kmp_status_string(s).decode()
+    except Exception:  # pragma: no cover - used while formatting another error
+        return "status"
+
+
+def check(status: int, where: str, ctx=None) -> None:
+    if status != KMP_OK:
+        detail = ""
+        if ctx:
+            msg = lib().kmp_last_error(ctx)
+            detail = msg.decode() if msg else ""
+        raise KmpError(status, where, detail)
+
+
+def geometry() -> PairGeometry:
+    g = PairGeometry()
+    lib().kmp_pair_geometry_get(C.byref(g))
+    return g

@@ -1,0 +1,413 @@
+// kmp_api.cpp — host-buffer C ABI (include/kmerpair.h: context … edges).  Each call is
+// synchronous, like the reference's Graph methods; every device step goes through the
+// kmp_dev_* stages of kmp_kernels.hip on the context's own stream.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "kmerpair.h"
+#include "kmp_df.hpp"
+#include "kmp_internal.hpp"
+
+using namespace kmp;
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    hipError_t reserve(size_t b) {
+        if (b <= bytes && p) return hipSuccess;
+        release();
+        hipError_t e = hipMalloc(&p, b ? b : 16);
+        if (e == hipSuccess) bytes = b ? b : 16;
+        return e;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
+}  // namespace
+
+struct kmp_ctx {
+    int device = 0;
+    int threads = 1;
+    std::string err;
+    hipStream_t stream = nullptr;
+
+    uint32_t n = 0;
+    uint64_t total_res = 0;
+    uint32_t max_len = 0;
+    bool loaded = false;
+    std::vector<uint64_t> h_off;
+    std::vector<uint16_t> h_cls;
+    DevBuf res, off, cls;
+
+    int k_codes = 0;
+    DevBuf codes;
+
+    int k_sets = 0;
+    DevBuf set, set_len, rep, rep_len, bits, scratch;
+    std::vector<uint32_t> h_set_len, h_rep_len;
+    kmp_counters counters{};
+
+    DevBuf items, ep, eq, ew, ecount, sort_tmp;
+    uint64_t edge_cap = 0;
+};
+
+struct kmp_edges {
+    std::vector<uint32_t> p, q, w;
+    std::vector<float> score;
+};
+
+namespace {
+
+int fail(kmp_ctx* c, int status, const char* fmt, ...) {
+    if (c) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        std::vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        c->err = buf;
+    }
+    return status;
+}
+
+#define KMP_HIP(ctx, expr)                                                                   \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return fail((ctx), e_ == hipErrorOutOfMemory ? KMP_ENOMEM : KMP_EDEVICE, "%s: %s", \
+                        #expr, hipGetErrorString(e_));                                       \
+    } while (0)
+
+#define KMP_TRY(ctx, expr)                                                                    \
+    do {                                                                                      \
+        int s_ = (expr);                                                                      \
+        if (s_ != KMP_OK) {                                                                   \
+            if ((ctx)->err.empty()) (ctx)->err = std::string(#expr) + ": " + kmp_status_string(s_); \
+            return s_;                                                                        \
+        }                                                                                     \
+    } while (0)
+
+int use_device(kmp_ctx* c) {
+    KMP_HIP(c, hipSetDevice(c->device));
+    return KMP_OK;
+}
+
+uint64_t protein_len(const kmp_ctx* c, uint32_t p) { return c->h_off[p + 1] - c->h_off[p]; }
+
+}  // namespace
+
+extern "C" {
+
+int kmp_version(void) { return KMP_ABI_VERSION; }
+
+const char* kmp_status_string(int s) {
+    switch (s) {
+        case KMP_OK: return "ok";
+        case KMP_EINVAL: return "invalid argument";
+        case KMP_ENOMEM: return "out of memory";
+        case KMP_EDEVICE: return "device error";
+        case KMP_ERCCL: return "collective error";
+        case KMP_EOVERFLOW: return "buffer too small";
+        case KMP_ESTATE: return "call out of order";
+        case KMP_EIO: return "i/o error";
+        default: return "unknown status";
+    }
+}
+
+void kmp_pair_opts_default(kmp_pair_opts* o) {
+    if (!o) return;
+    o->min_shared = 1;
+    o->require_class_diff = 1;
+    o->align_threshold = 10;
+    o->score = KMP_SCORE_COUNT;
+}
+
+int kmp_ctx_create(kmp_ctx** out, int device, int cpu_threads) {
+    if (!out) return KMP_EINVAL;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return KMP_EDEVICE;
+    if (device < 0 || device >= count) return KMP_EINVAL;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return KMP_EDEVICE;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return KMP_EDEVICE;  // kernels are gfx950-only
+    kmp_ctx* c = new (std::nothrow) kmp_ctx;
+    if (!c) return KMP_ENOMEM;
+    c->device = device;
+    c->threads = cpu_threads < 1 ? 1 : cpu_threads;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return KMP_EDEVICE;
+    }
+    *out = c;
+    return KMP_OK;
+}
+
+void kmp_ctx_destroy(kmp_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* kmp_last_error(const kmp_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int kmp_load_proteins(kmp_ctx* c, const uint8_t* residues, const uint64_t* offsets, uint32_t n,
+                      const uint16_t* class_id) {
+    if (!c) return KMP_EINVAL;
+    c->err.clear();
+    if (!offsets) return fail(c, KMP_EINVAL, "offsets is NULL");
+    for (uint32_t p = 0; p < n; ++p)
+        if (offsets[p + 1] < offsets[p]) return fail(c, KMP_EINVAL, "offsets not monotone at %u", p);
+    const uint64_t total = offsets[n] - offsets[0];
+    if (total && !residues) return fail(c, KMP_EINVAL, "residues is NULL");
+    KMP_TRY(c, use_device(c));
+    c->loaded = false;
+    c->k_codes = c->k_sets = 0;
+    c->n = n;
+    c->total_res = total;
+    c->h_off.resize(n + 1);
+    c->max_len = 0;
+    for (uint32_t p = 0; p <= n; ++p) c->h_off[p] = offsets[p] - offsets[0];
+    for (uint32_t p = 0; p < n; ++p) {
+        const uint64_t L = c->h_off[p + 1] - c->h_off[p];
+        if (L > 0xFFFFFFFFull) return fail(c, KMP_EINVAL, "protein %u longer than 2^32 residues", p);
+        c->max_len = std::max<uint32_t>(c->max_len, (uint32_t)L);
+    }
+    c->h_cls.assign(n, 0);
+    if (class_id) std::copy(class_id, class_id + n, c->h_cls.begin());
+    KMP_HIP(c, c->res.reserve(total + 16));
+    KMP_HIP(c, c->off.reserve((n + 1) * sizeof(uint64_t)));
+    KMP_HIP(c, c->cls.reserve((n + 1) * sizeof(uint16_t)));
+    if (total) KMP_HIP(c, hipMemcpyAsync(c->res.p, residues + offsets[0], total, hipMemcpyHostToDevice, c->stream));
+    KMP_HIP(c, hipMemcpyAsync(c->off.p, c->h_off.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+    if (n) KMP_HIP(c, hipMemcpyAsync(c->cls.p, c->h_cls.data(), n * sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
+    KMP_HIP(c, hipStreamSynchronize(c->stream));
+    c->counters = kmp_counters{};
+    c->counters.n_proteins = n;
+    c->loaded = true;
+    return KMP_OK;
+}
+
+int kmp_extract(kmp_ctx* c, int k) {
+    if (!c) return KMP_EINVAL;
+    c->err.clear();
+    if (!c->loaded) return fail(c, KMP_ESTATE, "kmp_load_proteins first");
+    if (k < 1 || k > kMaxK) return fail(c, KMP_EINVAL, "k must be in 1..7, got %d", k);
+    KMP_TRY(c, use_device(c));
+    KMP_HIP(c, c->codes.reserve(kmp_set_capacity(c->n, c->total_res) * sizeof(uint32_t)));
+    KMP_TRY(c, kmp_dev_extract(c->res.as<uint8_t>(), c->off.as<uint64_t>(), c->n, k, c->codes.as<uint32_t>(), c->stream));
+    KMP_HIP(c, hipStreamSynchronize(c->stream));
+    c->k_codes = k;
+    return KMP_OK;
+}
+
+int kmp_get_kmers(kmp_ctx* c, uint32_t p, uint32_t* out, uint64_t cap, uint64_t* n) {
+    if (!c || !n) return KMP_EINVAL;
+    c->err.clear();
+    if (!c->k_codes) return fail(c, KMP_ESTATE, "kmp_extract first");
+    if (p >= c->n) return fail(c, KMP_EINVAL, "protein %u out of range", p);
+    const uint64_t nw = n_windows(protein_len(c, p), c->k_codes);
+    *n = nw;
+    if (cap < nw) return KMP_EOVERFLOW;
+    if (nw == 0) return KMP_OK;
+    if (!out) return fail(c, KMP_EINVAL, "out is NULL");
+    KMP_TRY(c, use_device(c));
+    KMP_HIP(c, hipMemcpyAsync(out, c->codes.as<uint32_t>() + set_base(c->h_off[p], p), nw * sizeof(uint32_t),
+                              hipMemcpyDeviceToHost, c->stream));
+    KMP_HIP(c, hipStreamSynchronize(c->stream));
+    return KMP_OK;
+}
+
+int kmp_build_sets(kmp_ctx* c, int k) {
+    if (!c) return KMP_EINVAL;
+    c->err.clear();
+    if (!c->loaded) return fail(c, KMP_ESTATE, "kmp_load_proteins first");
+    if (k < 1 || k > kMaxK) return fail(c, KMP_EINVAL, "k must be in 1..7, got %d", k);
+    KMP_TRY(c, use_device(c));
+    c->k_sets = 0;
+    const uint64_t capacity = kmp_set_capacity(c->n, c->total_res);
+    const uint64_t words = kmp_dev_repeat_bitmap_words(k);
+    KMP_HIP(c, c->set.reserve(capacity * sizeof(uint32_t)));
+    KMP_HIP(c, c->rep.reserve(capacity * sizeof(uint32_t)));
+    KMP_HIP(c, c->set_len.reserve((c->n + 1) * sizeof(uint32_t)));
+    KMP_HIP(c, c->rep_len.reserve((c->n + 1) * sizeof(uint32_t)));
+    KMP_HIP(c, c->bits.reserve(2 * words * sizeof(uint32_t)));
+    const bool long_path = n_windows(c->max_len, k) > KMP_LDS_SORT_MAX;
+    if (long_path) KMP_HIP(c, c->scratch.reserve(capacity * sizeof(uint32_t)));
+    KMP_TRY(c, kmp_dev_build_sets(c->res.as<uint8_t>(), c->off.as<uint64_t>(), c->n, k, c->max_len,
+                                  c->set.as<uint32_t>(), c->set_len.as<uint32_t>(),
+                                  long_path ? c->scratch.as<uint32_t>() : nullptr, c->stream));
+    KMP_TRY(c, kmp_dev_filter_repeats(c->set.as<uint32_t>(), c->set_len.as<uint32_t>(), c->off.as<uint64_t>(), c->n,
+                                      k, c->bits.as<uint32_t>(), c->rep.as<uint32_t>(), c->rep_len.as<uint32_t>(),
+                                      c->stream));
+    c->h_set_len.resize(c->n);
+    c->h_rep_len.resize(c->n);
+    if (c->n) {
+        KMP_HIP(c, hipMemcpyAsync(c->h_set_len.data(), c->set_len.p, c->n * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                  c->stream));
+        KMP_HIP(c, hipMemcpyAsync(c->h_rep_len.data(), c->rep_len.p, c->n * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                  c->stream));
+    }
+    KMP_HIP(c, hipStreamSynchronize(c->stream));
+    kmp_counters& ct = c->counters;
+    ct = kmp_counters{};
+    ct.n_proteins = c->n;
+    for (uint32_t p = 0; p < c->n; ++p) {
+        ct.n_windows += n_windows(protein_len(c, p), k);
+        ct.sum_S += c->h_set_len[p];
+    }
+    // device df over all sets (main.rs:77-149): distinct / repeat / Σ C(df,2) / max df
+    DfCounters dc{};
+    KMP_TRY(c, device_df_counters(c->set.as<uint32_t>(), c->h_set_len.data(), c->h_off.data(), c->off.as<uint64_t>(), c->n, k, c->stream, &dc,
+                                  c->err));
+    ct.distinct = dc.distinct;
+    ct.repeat = dc.repeat;
+    ct.sum_cdf2 = dc.sum_cdf2;
+    ct.max_df = dc.max_df;
+    c->k_sets = k;
+    return KMP_OK;
+}
+
+int kmp_get_set(kmp_ctx* c, uint32_t p, uint32_t* out, uint64_t cap, uint64_t* n) {
+    if (!c || !n) return KMP_EINVAL;
+    c->err.clear();
+    if (!c->k_sets) return fail(c, KMP_ESTATE, "kmp_build_sets first");
+    if (p >= c->n) return fail(c, KMP_EINVAL, "protein %u out of range", p);
+    const uint64_t m = c->h_set_len[p];
+    *n = m;
+    if (cap < m) return KMP_EOVERFLOW;
+    if (m == 0) return KMP_OK;
+    if (!out) return fail(c, KMP_EINVAL, "out is NULL");
+    KMP_TRY(c, use_device(c));
+    KMP_HIP(c, hipMemcpyAsync(out, c->set.as<uint32_t>() + set_base(c->h_off[p], p), m * sizeof(uint32_t),
+                              hipMemcpyDeviceToHost, c->stream));
+    KMP_HIP(c, hipStreamSynchronize(c->stream));
+    return KMP_OK;
+}
+
+int kmp_counters_get(kmp_ctx* c, kmp_counters* out) {
+    if (!c || !out) return KMP_EINVAL;
+    *out = c->counters;
+    return KMP_OK;
+}
+
+int kmp_pairs(kmp_ctx* c, const kmp_pair_opts* opts, kmp_edges** out) {
+    if (!c || !out) return KMP_EINVAL;
+    *out = nullptr;
+    c->err.clear();
+    if (!c->k_sets) return fail(c, KMP_ESTATE, "kmp_build_sets first");
+    kmp_pair_opts o;
+    kmp_pair_opts_default(&o);
+    if (opts) o = *opts;
+    if (o.score != KMP_SCORE_COUNT && o.score != KMP_SCORE_JACCARD) return fail(c, KMP_EINVAL, "unknown score %d", o.score);
+    KMP_TRY(c, use_device(c));
+
+    // plan (host): row tiles of the repeat-filtered sets, column chunks
+    uint64_t n_items = 0;
+    const uint64_t chunk_cost = 65536;
+    int st = kmp_plan_pairs(c->h_rep_len.data(), c->n, chunk_cost, nullptr, 0, &n_items);
+    if (st != KMP_OK && st != KMP_EOVERFLOW)
+        return fail(c, st, "planner: a repeat-filtered set exceeds the tile capacity (%u k-mers)", kTileCap);
+    std::vector<kmp_work_item> items(n_items);
+    KMP_TRY(c, kmp_plan_pairs(c->h_rep_len.data(), c->n, chunk_cost, items.data(), n_items, &n_items));
+    KMP_HIP(c, c->items.reserve(std::max<uint64_t>(1, n_items) * sizeof(kmp_work_item)));
+    if (n_items)
+        KMP_HIP(c, hipMemcpyAsync(c->items.p, items.data(), n_items * sizeof(kmp_work_item), hipMemcpyHostToDevice,
+                                  c->stream));
+    if (c->edge_cap == 0) c->edge_cap = std::max<uint64_t>(1u << 20, 4ull * c->n);
+    KMP_HIP(c, c->ecount.reserve(sizeof(unsigned long long)));
+    unsigned long long count = 0;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        KMP_HIP(c, c->ep.reserve(c->edge_cap * sizeof(uint32_t)));
+        KMP_HIP(c, c->eq.reserve(c->edge_cap * sizeof(uint32_t)));
+        KMP_HIP(c, c->ew.reserve(c->edge_cap * sizeof(uint32_t)));
+        KMP_HIP(c, hipMemsetAsync(c->ecount.p, 0, sizeof(unsigned long long), c->stream));
+        KMP_TRY(c, kmp_dev_pairs(c->rep.as<uint32_t>(), c->rep_len.as<uint32_t>(), c->off.as<uint64_t>(),
+                                 c->cls.as<uint16_t>(), c->n, c->items.as<kmp_work_item>(), n_items, o.min_shared,
+                                 o.require_class_diff, c->ep.as<uint32_t>(), c->eq.as<uint32_t>(), c->ew.as<uint32_t>(),
+                                 c->edge_cap, c->ecount.as<unsigned long long>(), c->stream));
+        KMP_HIP(c, hipMemcpyAsync(&count, c->ecount.p, sizeof count, hipMemcpyDeviceToHost, c->stream));
+        KMP_HIP(c, hipStreamSynchronize(c->stream));
+        if (count <= c->edge_cap) break;
+        c->edge_cap = count + count / 8 + 1024;
+    }
+    if (count > c->edge_cap) return fail(c, KMP_EDEVICE, "edge count unstable across reruns");
+    const uint64_t tmp = kmp_dev_sort_edges_tmp_bytes(count, c->n);
+    KMP_HIP(c, c->sort_tmp.reserve(tmp));
+    KMP_TRY(c, kmp_dev_sort_edges(c->ep.as<uint32_t>(), c->eq.as<uint32_t>(), c->ew.as<uint32_t>(), count, c->n,
+                                  c->sort_tmp.p, c->sort_tmp.bytes, c->stream));
+    std::unique_ptr<kmp_edges> e(new (std::nothrow) kmp_edges);
+    if (!e) return fail(c, KMP_ENOMEM, "edges");
+    e->p.resize(count);
+    e->q.resize(count);
+    e->w.resize(count);
+    if (count) {
+        KMP_HIP(c, hipMemcpyAsync(e->p.data(), c->ep.p, count * 4, hipMemcpyDeviceToHost, c->stream));
+        KMP_HIP(c, hipMemcpyAsync(e->q.data(), c->eq.p, count * 4, hipMemcpyDeviceToHost, c->stream));
+        KMP_HIP(c, hipMemcpyAsync(e->w.data(), c->ew.p, count * 4, hipMemcpyDeviceToHost, c->stream));
+    }
+    KMP_HIP(c, hipStreamSynchronize(c->stream));
+    e->score.resize(count);
+    uint64_t wdiff = 0, nalign = 0;
+    for (uint64_t i = 0; i < count; ++i) {
+        const uint32_t p = e->p[i], q = e->q[i], w = e->w[i];
+        if (c->h_cls[p] != c->h_cls[q]) wdiff += w;
+        if (w > o.align_threshold) ++nalign;
+        if (o.score == KMP_SCORE_JACCARD) {
+            const uint64_t uni = (uint64_t)c->h_set_len[p] + c->h_set_len[q] - w;
+            e->score[i] = uni ? (float)w / (float)uni : 0.0f;  // exact operands (< 2^24), one rounding
+        } else {
+            e->score[i] = (float)w;
+        }
+    }
+    c->counters.n_edges = count;
+    c->counters.n_align = nalign;
+    c->counters.sum_w_diff = wdiff;
+    *out = e.release();
+    return KMP_OK;
+}
+
+int kmp_edges_count(const kmp_edges* e, uint64_t* n) {
+    if (!e || !n) return KMP_EINVAL;
+    *n = e->p.size();
+    return KMP_OK;
+}
+
+int kmp_edges_get(const kmp_edges* e, uint32_t* p, uint32_t* q, uint32_t* w, float* score, uint64_t cap,
+                  uint64_t* n) {
+    if (!e || !n) return KMP_EINVAL;
+    const uint64_t m = e->p.size();
+    *n = m;
+    if (cap < m) return KMP_EOVERFLOW;
+    if (p) std::copy(e->p.begin(), e->p.end(), p);
+    if (q) std::copy(e->q.begin(), e->q.end(), q);
+    if (w) std::copy(e->w.begin(), e->w.end(), w);
+    if (score) std::copy(e->score.begin(), e->score.end(), score);
+    return KMP_OK;
+}
+
+void kmp_edges_free(kmp_edges* e) { delete e; }
+
+}  // extern "C"

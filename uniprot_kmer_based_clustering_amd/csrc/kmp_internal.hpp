@@ -1,0 +1,45 @@
+// kmp_internal.hpp — shared constants of libkmerpair (host + device).
+#pragma once
+#include <cstdint>
+
+#if defined(__HIPCC__)
+#define KMP_HD __host__ __device__
+#else
+#define KMP_HD
+#endif
+
+namespace kmp {
+
+// Residue alphabet of src/protein.rs:9-13; any other byte encodes as 20 (:49-54).
+constexpr char kAminoAcids[21] = {'C', 'S', 'T', 'A', 'G', 'P', 'D', 'E', 'Q', 'N', 'H',
+                                  'R', 'K', 'M', 'I', 'L', 'V', 'W', 'Y', 'F', '*'};
+constexpr uint32_t kRadix = 21;
+constexpr int kMaxK = 7;  // 21^7 - 1 = 1,801,088,540 < 2^31: every code fits u32, 0xFFFFFFFF is free
+
+inline uint64_t pow21(int k) {
+    uint64_t v = 1;
+    for (int i = 0; i < k; ++i) v *= kRadix;
+    return v;
+}
+
+// windows j in [0, L-k] (protein.rs:114); L < k yields none (documented deviation: the
+// reference wraps usize for L < 4 and panics)
+inline uint64_t n_windows(uint64_t L, int k) { return L >= (uint64_t)k ? L - k + 1 : 0; }
+
+// 16-B aligned per-protein slot of every u32 per-protein array (see kmerpair.h)
+KMP_HD inline uint64_t set_base(uint64_t res_off, uint32_t p) {
+    return (res_off + 4ull * p + 3ull) & ~3ull;
+}
+
+// ---- pair-kernel geometry (LDS budget per workgroup, one workgroup per CU) ----
+constexpr uint32_t kPairThreads = 1024;                 // 16 waves
+constexpr uint32_t kPairWaves = kPairThreads / 64;
+constexpr uint32_t kBucketSlots = 4;                    // one ds_read_b128 per probe step
+constexpr uint32_t kTileBucketsLog2 = 12;
+constexpr uint32_t kTileBuckets = 1u << kTileBucketsLog2;
+constexpr uint32_t kTileSlots = kTileBuckets * kBucketSlots;   // 16384 slots: 64 KiB keys
+constexpr uint32_t kTileCap = 10240;                    // load factor <= 0.625
+constexpr uint32_t kRowsMax = 256;                      // row index fits u8
+constexpr uint32_t kEmptyKey = 0xFFFFFFFFu;
+
+}  // namespace kmp

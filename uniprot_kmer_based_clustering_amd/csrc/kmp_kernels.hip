@@ -1,0 +1,570 @@
+// kmp_kernels.hip — gfx950 (CDNA4) kernels of the k-mer pair path and their C-ABI
+// device-stage entry points (include/kmerpair.h, "device stages").
+//
+// Path (reference file:line it replaces):
+//   build_sets_kernel   Protein::new windows + radix-21 codes (src/protein.rs:29-37,107-132)
+//                       fused with the per-protein sort+dedup of src/main.rs:280-282
+//   mark/compact        remove_unique_five_mers (src/protein.rs:151-162) with the df>=2 test
+//                       of src/main.rs:127-149 as two bitmaps over the 21^k code space
+//   pair_kernel         Graph::new + remove_uninteresting_edges + combine_edges
+//                       (src/graph/mod.rs:39-193, :549-697, :322-546): w(p,q) = |K(p) ∩ K(q)|
+//                       for every p < q of a row tile × column range, class filter, emit
+//   sort edges          the reference's single-thread (p, q) edge order (vertex.rs:100)
+//
+// Wave = 64 lanes everywhere; ballots are 64-bit.
+#include <hip/hip_runtime.h>
+
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include "kmerpair.h"
+#include "kmp_internal.hpp"
+
+using namespace kmp;
+
+namespace {
+
+struct CodeLut {
+    uint8_t v[256];
+};
+constexpr CodeLut make_lut() {
+    CodeLut l{};
+    for (int b = 0; b < 256; ++b) {
+        l.v[b] = 20;  // amino_acid_to_bits: unknown -> 20 (protein.rs:50-51)
+        for (int i = 0; i < 21; ++i)
+            if ((uint8_t)kAminoAcids[i] == (uint8_t)b) { l.v[b] = (uint8_t)i; break; }
+    }
+    return l;
+}
+__constant__ CodeLut c_lut = make_lut();
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+
+// number of set bits of m strictly below this lane
+__device__ __forceinline__ uint32_t mask_rank(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ uint32_t next_pow2(uint32_t n) {
+    return n <= 1 ? 1u : 1u << (32 - __clz(n - 1));
+}
+
+// Block-wide ordered compaction step: every thread offers (keep, value) for position
+// `slot` of the block's 256-element chunk; kept values land at out[carry + rank] in input
+// order.  Returns the number kept by the whole chunk.  Uses wave ballots + 4 LDS words.
+template <int kThreads>
+__device__ __forceinline__ uint32_t block_compact(bool keep, uint32_t value, uint32_t* out, uint32_t carry,
+                                                  uint32_t* wave_tot) {
+    constexpr int kWaves = kThreads / 64;
+    const uint64_t m = __ballot(keep);
+    const uint32_t w = threadIdx.x >> 6;
+    if (lane_id() == 0) wave_tot[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (int i = 0; i < kWaves; ++i) {
+        const uint32_t t = wave_tot[i];
+        before += (i < (int)w) ? t : 0u;
+        total += t;
+    }
+    if (keep) out[carry + before + mask_rank(m)] = value;
+    __syncthreads();  // wave_tot reused by the next chunk
+    return total;
+}
+
+// Ascending bitonic sort of s[0, n) in LDS with the "flip" first stage, so every comparator
+// is ascending and positions >= n behave as +inf without being stored (no padding writes).
+template <int kThreads>
+__device__ void bitonic_sort_lds(uint32_t* s, uint32_t n) {
+    if (n <= 1) return;
+    const uint32_t n2 = next_pow2(n);
+    const uint32_t pairs = n2 >> 1;
+    for (uint32_t m = 2; m <= n2; m <<= 1) {
+        const uint32_t half = m >> 1;
+        const uint32_t hl = __builtin_ctz(half);
+        for (uint32_t t = threadIdx.x; t < pairs; t += kThreads) {
+            const uint32_t blk = t >> hl, o = t & (half - 1);
+            const uint32_t i = blk * m + o, l = blk * m + m - 1 - o;
+            if (l < n) {
+                const uint32_t a = s[i], b = s[l];
+                if (a > b) { s[i] = b; s[l] = a; }
+            }
+        }
+        __syncthreads();
+        for (uint32_t j = half >> 1; j > 0; j >>= 1) {
+            const uint32_t jl = __builtin_ctz(j);
+            for (uint32_t t = threadIdx.x; t < pairs; t += kThreads) {
+                const uint32_t i = ((t >> jl) << (jl + 1)) + (t & (j - 1)), l = i + j;
+                if (l < n) {
+                    const uint32_t a = s[i], b = s[l];
+                    if (a > b) { s[i] = b; s[l] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// The same network over global memory, one workgroup per protein (long proteins only).
+template <int kThreads>
+__device__ void bitonic_sort_global(uint32_t* s, uint32_t n) {
+    if (n <= 1) return;
+    const uint32_t n2 = next_pow2(n);
+    const uint32_t pairs = n2 >> 1;
+    for (uint32_t m = 2; m <= n2; m <<= 1) {
+        const uint32_t half = m >> 1;
+        for (uint32_t j = half; j > 0; j >>= 1) {
+            for (uint32_t t = threadIdx.x; t < pairs; t += kThreads) {
+                uint32_t i, l;
+                if (j == half) {
+                    const uint32_t blk = t / half, o = t % half;
+                    i = blk * m + o;
+                    l = blk * m + m - 1 - o;
+                } else {
+                    i = (t / j) * 2 * j + (t % j);
+                    l = i + j;
+                }
+                if (l < n) {
+                    const uint32_t a = s[i], b = s[l];
+                    if (a > b) { s[i] = b; s[l] = a; }
+                }
+            }
+            __threadfence_block();
+            __syncthreads();
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// Protein::new windows (protein.rs:107-132): every window's code, position order.
+constexpr int kExtractThreads = 256;
+__global__ __launch_bounds__(kExtractThreads) void extract_kernel(const uint8_t* __restrict__ res,
+                                                                  const uint64_t* __restrict__ res_off,
+                                                                  int k, uint32_t* __restrict__ codes) {
+    const uint32_t p = blockIdx.x;
+    const uint64_t off = res_off[p];
+    const uint64_t L = res_off[p + 1] - off;
+    const uint64_t nw = L >= (uint64_t)k ? L - k + 1 : 0;
+    const uint64_t base = set_base(off, p);
+    for (uint64_t j = threadIdx.x; j < nw; j += kExtractThreads) {
+        uint32_t v = 0;
+        for (int i = 0; i < k; ++i) v = v * kRadix + c_lut.v[res[off + j + i]];
+        codes[base + j] = v;
+    }
+}
+
+// Fused windows + per-protein sort + dedup (K(p)), one workgroup per protein, in LDS.
+constexpr int kSetThreads = 256;
+__global__ __launch_bounds__(kSetThreads) void build_sets_kernel(const uint8_t* __restrict__ res,
+                                                                 const uint64_t* __restrict__ res_off,
+                                                                 int k, uint32_t* __restrict__ set,
+                                                                 uint32_t* __restrict__ set_len) {
+    __shared__ uint32_t s[KMP_LDS_SORT_MAX];
+    __shared__ uint8_t rc[KMP_LDS_SORT_MAX + kMaxK];
+    __shared__ uint8_t lut[256];
+    __shared__ uint32_t wave_tot[kSetThreads / 64];
+    const uint32_t p = blockIdx.x;
+    const uint64_t off = res_off[p];
+    const uint64_t L = res_off[p + 1] - off;
+    const uint64_t nw64 = L >= (uint64_t)k ? L - k + 1 : 0;
+    if (nw64 > KMP_LDS_SORT_MAX) return;  // block-uniform: long proteins take the global path
+    const uint32_t nw = (uint32_t)nw64;
+    const uint32_t t = threadIdx.x;
+    lut[t] = c_lut.v[t];
+    __syncthreads();
+    const uint32_t Lr = nw ? nw + k - 1 : 0;  // residues that belong to some window
+    for (uint32_t i = t; i < Lr; i += kSetThreads) rc[i] = lut[res[off + i]];
+    __syncthreads();
+    for (uint32_t j = t; j < nw; j += kSetThreads) {
+        uint32_t v = 0;
+        for (int i = 0; i < k; ++i) v = v * kRadix + rc[j + i];
+        s[j] = v;
+    }
+    __syncthreads();
+    bitonic_sort_lds<kSetThreads>(s, nw);
+    uint32_t* out = set + set_base(off, p);
+    uint32_t carry = 0;
+    for (uint32_t c = 0; c < nw; c += kSetThreads) {
+        const uint32_t i = c + t;
+        const bool keep = i < nw && (i == 0 || s[i] != s[i - 1]);
+        carry += block_compact<kSetThreads>(keep, keep ? s[i] : 0u, out, carry, wave_tot);
+    }
+    if (t == 0) set_len[p] = carry;
+}
+
+constexpr int kLongThreads = 1024;
+__global__ __launch_bounds__(kLongThreads) void build_sets_long_kernel(const uint8_t* __restrict__ res,
+                                                                       const uint64_t* __restrict__ res_off,
+                                                                       int k, uint32_t* __restrict__ set,
+                                                                       uint32_t* __restrict__ set_len,
+                                                                       uint32_t* __restrict__ scratch) {
+    __shared__ uint32_t wave_tot[kLongThreads / 64];
+    const uint32_t p = blockIdx.x;
+    const uint64_t off = res_off[p];
+    const uint64_t L = res_off[p + 1] - off;
+    const uint64_t nw64 = L >= (uint64_t)k ? L - k + 1 : 0;
+    if (nw64 <= KMP_LDS_SORT_MAX) return;
+    const uint32_t nw = (uint32_t)nw64;
+    const uint64_t base = set_base(off, p);
+    uint32_t* s = scratch + base;
+    for (uint32_t j = threadIdx.x; j < nw; j += kLongThreads) {
+        uint32_t v = 0;
+        for (int i = 0; i < k; ++i) v = v * kRadix + c_lut.v[res[off + j + i]];
+        s[j] = v;
+    }
+    __threadfence_block();
+    __syncthreads();
+    bitonic_sort_global<kLongThreads>(s, nw);
+    uint32_t carry = 0;
+    for (uint32_t c = 0; c < nw; c += kLongThreads) {
+        const uint32_t i = c + threadIdx.x;
+        const bool keep = i < nw && (i == 0 || s[i] != s[i - 1]);
+        carry += block_compact<kLongThreads>(keep, keep ? s[i] : 0u, set + base, carry, wave_tot);
+    }
+    if (threadIdx.x == 0) set_len[p] = carry;
+}
+
+// ------------------------------------------------------------------------------------
+// remove_unique_five_mers (protein.rs:151-162).  Pass 1 marks every (protein, distinct
+// k-mer) occurrence in bits1; a second occurrence (bit already set) marks bits2 (df >= 2).
+constexpr int kFilterThreads = 256;
+__global__ __launch_bounds__(kFilterThreads) void mark_kernel(const uint32_t* __restrict__ set,
+                                                              const uint32_t* __restrict__ set_len,
+                                                              const uint64_t* __restrict__ res_off,
+                                                              uint32_t* __restrict__ bits1,
+                                                              uint32_t* __restrict__ bits2) {
+    const uint32_t p = blockIdx.x;
+    const uint32_t len = set_len[p];
+    const uint32_t* s = set + set_base(res_off[p], p);
+    for (uint32_t e = threadIdx.x; e < len; e += kFilterThreads) {
+        const uint32_t x = s[e];
+        const uint32_t bit = 1u << (x & 31u);
+        const uint32_t old = atomicOr(&bits1[x >> 5], bit);
+        if (old & bit) atomicOr(&bits2[x >> 5], bit);
+    }
+}
+
+__global__ __launch_bounds__(kFilterThreads) void compact_repeats_kernel(
+    const uint32_t* __restrict__ set, const uint32_t* __restrict__ set_len,
+    const uint64_t* __restrict__ res_off, const uint32_t* __restrict__ bits2, uint32_t* __restrict__ rep,
+    uint32_t* __restrict__ rep_len) {
+    __shared__ uint32_t wave_tot[kFilterThreads / 64];
+    const uint32_t p = blockIdx.x;
+    const uint32_t len = set_len[p];
+    const uint64_t base = set_base(res_off[p], p);
+    uint32_t carry = 0;
+    for (uint32_t c = 0; c < len; c += kFilterThreads) {
+        const uint32_t e = c + threadIdx.x;
+        uint32_t x = 0;
+        bool keep = false;
+        if (e < len) {
+            x = set[base + e];
+            keep = (bits2[x >> 5] >> (x & 31u)) & 1u;
+        }
+        carry += block_compact<kFilterThreads>(keep, x, rep + base, carry, wave_tot);
+    }
+    if (threadIdx.x == 0) rep_len[p] = carry;
+}
+
+// ------------------------------------------------------------------------------------
+// Pair kernel.  One workgroup per work item (row tile × column range), one per CU.
+//   LDS: the row tile's sets as one multiset hash index: 16,384 u32 keys in 4-slot buckets
+//   (a probe step is one ds_read_b128) + the owning row (u8) per slot; per-wave counters.
+//   Each wave streams one column protein at a time: 64 k-mers per step, one per lane, each
+//   probing the index; a hit on row r adds 1 to the wave's counter for r.  After the column
+//   the touched rows are emitted (p = row, q = column, w = count) if w >= min_shared and the
+//   AMR classes differ (mod.rs:580-587), with one global atomic per wave (ballot + mbcnt).
+__device__ __forceinline__ uint32_t tile_hash(uint32_t x) {
+    return (x * 2654435761u) >> (32 - kTileBucketsLog2);
+}
+
+__global__ __launch_bounds__(kPairThreads) void pair_kernel(
+    const uint32_t* __restrict__ set, const uint32_t* __restrict__ set_len,
+    const uint64_t* __restrict__ res_off, const uint16_t* __restrict__ cls,
+    const kmp_work_item* __restrict__ items, uint32_t min_shared, int require_diff,
+    uint32_t* __restrict__ out_p, uint32_t* __restrict__ out_q, uint32_t* __restrict__ out_w, uint64_t cap,
+    unsigned long long* __restrict__ count) {
+    __shared__ __attribute__((aligned(16))) uint32_t keys[kTileSlots];
+    __shared__ uint8_t rows[kTileSlots];
+    __shared__ uint32_t cnt[kPairWaves][kRowsMax];
+    __shared__ uint8_t touched[kPairWaves][kRowsMax];
+    __shared__ uint32_t ntouched[kPairWaves];
+    __shared__ uint16_t row_cls[kRowsMax];
+
+    const kmp_work_item it = items[blockIdx.x];
+    const uint32_t nrows = it.row_end - it.row_beg;
+    const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+
+    uint4* k4 = reinterpret_cast<uint4*>(keys);
+    for (uint32_t i = tid; i < kTileSlots / 4; i += kPairThreads)
+        k4[i] = make_uint4(kEmptyKey, kEmptyKey, kEmptyKey, kEmptyKey);
+    for (uint32_t i = tid; i < kPairWaves * kRowsMax; i += kPairThreads) (&cnt[0][0])[i] = 0;
+    if (tid < kPairWaves) ntouched[tid] = 0;
+    for (uint32_t r = tid; r < nrows; r += kPairThreads) row_cls[r] = cls[it.row_beg + r];
+    __syncthreads();
+
+    // build: one wave per row protein, one k-mer per lane
+    for (uint32_t r = wave; r < nrows; r += kPairWaves) {
+        const uint32_t p = it.row_beg + r;
+        const uint32_t len = set_len[p];
+        const uint32_t* s = set + set_base(res_off[p], p);
+        for (uint32_t e = lane; e < len; e += 64) {
+            const uint32_t x = s[e];
+            uint32_t b = tile_hash(x);
+            for (uint32_t guard = 0; guard < kTileBuckets; ++guard) {
+                bool done = false;
+#pragma unroll
+                for (uint32_t q = 0; q < kBucketSlots; ++q) {
+                    const uint32_t slot = b * kBucketSlots + q;
+                    if (!done && keys[slot] == kEmptyKey && atomicCAS(&keys[slot], kEmptyKey, x) == kEmptyKey) {
+                        rows[slot] = (uint8_t)r;
+                        done = true;
+                    }
+                }
+                if (done) break;
+                b = (b + 1) & (kTileBuckets - 1);
+            }
+        }
+    }
+    __syncthreads();
+
+    // probe: one wave per column protein
+    for (uint32_t q = it.col_beg + wave; q < it.col_end; q += kPairWaves) {
+        const uint32_t len = set_len[q];
+        if (len == 0 || q <= it.row_beg) continue;
+        const uint32_t lim = min(q - it.row_beg, nrows);  // rows with p < q
+        const uint32_t* s = set + set_base(res_off[q], q);
+        for (uint32_t c = 0; c < len; c += 64) {
+            const uint32_t e = c + lane;
+            bool act = e < len;
+            const uint32_t x = act ? s[e] : 0u;
+            uint32_t b = tile_hash(x);
+            for (uint32_t guard = 0; __ballot(act) != 0 && guard < kTileBuckets; ++guard) {
+                if (act) {
+                    const uint4 kv = k4[b];
+                    uint32_t hm = (uint32_t)(kv.x == x) | ((uint32_t)(kv.y == x) << 1) |
+                                  ((uint32_t)(kv.z == x) << 2) | ((uint32_t)(kv.w == x) << 3);
+                    while (hm) {
+                        const uint32_t sl = __builtin_ctz(hm);
+                        hm &= hm - 1;
+                        const uint32_t r = rows[b * kBucketSlots + sl];
+                        if (r < lim) {
+                            if (atomicAdd(&cnt[wave][r], 1u) == 0u) {
+                                const uint32_t slot = atomicAdd(&ntouched[wave], 1u);
+                                touched[wave][slot] = (uint8_t)r;
+                            }
+                        }
+                    }
+                    act = !((kv.x == kEmptyKey) | (kv.y == kEmptyKey) | (kv.z == kEmptyKey) | (kv.w == kEmptyKey));
+                    b = (b + 1) & (kTileBuckets - 1);
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        const uint32_t nt = ntouched[wave];
+        const uint16_t cq = cls[q];
+        for (uint32_t t0 = 0; t0 < nt; t0 += 64) {
+            const uint32_t t = t0 + lane;
+            bool ok = false;
+            uint32_t r = 0, wv = 0;
+            if (t < nt) {
+                r = touched[wave][t];
+                wv = cnt[wave][r];
+                cnt[wave][r] = 0;
+                ok = wv >= min_shared && (!require_diff || row_cls[r] != cq);
+            }
+            const uint64_t m = __ballot(ok);
+            if (m) {
+                unsigned long long first = 0;
+                if (lane == 0) first = atomicAdd(count, (unsigned long long)__popcll(m));
+                first = __shfl(first, 0);
+                const unsigned long long pos = first + mask_rank(m);
+                if (ok && pos < cap) {
+                    out_p[pos] = it.row_beg + r;
+                    out_q[pos] = q;
+                    out_w[pos] = wv;
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (lane == 0) ntouched[wave] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+}
+
+// ------------------------------------------------------------------------------------
+__global__ void pack_edges_kernel(const uint32_t* __restrict__ p, const uint32_t* __restrict__ q, uint64_t n,
+                                  uint64_t np, unsigned long long* __restrict__ key) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        key[i] = (unsigned long long)p[i] * np + q[i];
+}
+__global__ void unpack_edges_kernel(const unsigned long long* __restrict__ key, uint64_t n, uint64_t np,
+                                    uint32_t* __restrict__ p, uint32_t* __restrict__ q) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        p[i] = (uint32_t)(key[i] / np);
+        q[i] = (uint32_t)(key[i] % np);
+    }
+}
+
+int hip_status(hipError_t e) { return e == hipSuccess ? KMP_OK : KMP_EDEVICE; }
+
+unsigned bits_for(uint64_t v) {  // bits needed to represent values < v
+    unsigned b = 0;
+    while (b < 64 && (v - 1) >> b) ++b;
+    return b ? b : 1;
+}
+
+inline uint64_t align_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
+
+struct SortLayout {
+    uint64_t keys_in, keys_out, vals_out, prim, prim_bytes, total;
+};
+
+SortLayout sort_layout(uint64_t n, uint32_t np) {
+    SortLayout l{};
+    size_t prim = 0;
+    const unsigned end_bit = bits_for((uint64_t)np * np);
+    (void)rocprim::radix_sort_pairs(nullptr, prim, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                    (uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)n, 0u, end_bit);
+    l.keys_in = 0;
+    l.keys_out = align_up(l.keys_in + 8 * n, 256);
+    l.vals_out = align_up(l.keys_out + 8 * n, 256);
+    l.prim = align_up(l.vals_out + 4 * n, 256);
+    l.prim_bytes = prim;
+    l.total = l.prim + prim + 256;
+    return l;
+}
+
+}  // namespace
+
+// ====================================================================================
+extern "C" {
+
+uint64_t kmp_set_capacity(uint32_t n, uint64_t total_residues) { return total_residues + 4ull * n + 8ull; }
+uint64_t kmp_set_base(uint64_t res_off, uint32_t p) { return set_base(res_off, p); }
+
+int kmp_dev_extract(const uint8_t* d_res, const uint64_t* d_res_off, uint32_t n, int k, uint32_t* d_codes,
+                    void* stream) {
+    if (k < 1 || k > kMaxK || (n && (!d_res_off || !d_codes))) return KMP_EINVAL;
+    if (n == 0) return KMP_OK;
+    extract_kernel<<<n, kExtractThreads, 0, as_stream(stream)>>>(d_res, d_res_off, k, d_codes);
+    return hip_status(hipGetLastError());
+}
+
+int kmp_dev_build_sets(const uint8_t* d_res, const uint64_t* d_res_off, uint32_t n, int k, uint32_t max_len,
+                       uint32_t* d_set, uint32_t* d_set_len, uint32_t* d_scratch, void* stream) {
+    if (k < 1 || k > kMaxK || (n && (!d_res_off || !d_set || !d_set_len))) return KMP_EINVAL;
+    if (n == 0) return KMP_OK;
+    hipStream_t st = as_stream(stream);
+    build_sets_kernel<<<n, kSetThreads, 0, st>>>(d_res, d_res_off, k, d_set, d_set_len);
+    const bool maybe_long = max_len == 0 || n_windows(max_len, k) > KMP_LDS_SORT_MAX;
+    if (maybe_long) {
+        if (!d_scratch) return KMP_EINVAL;
+        build_sets_long_kernel<<<n, kLongThreads, 0, st>>>(d_res, d_res_off, k, d_set, d_set_len, d_scratch);
+    }
+    return hip_status(hipGetLastError());
+}
+
+uint64_t kmp_dev_repeat_bitmap_words(int k) {
+    if (k < 1 || k > kMaxK) return 0;
+    return (pow21(k) + 31) / 32;
+}
+
+int kmp_dev_filter_repeats(const uint32_t* d_set, const uint32_t* d_set_len, const uint64_t* d_res_off,
+                           uint32_t n, int k, uint32_t* d_bits, uint32_t* d_rep, uint32_t* d_rep_len,
+                           void* stream) {
+    if (k < 1 || k > kMaxK || (n && (!d_set || !d_set_len || !d_res_off || !d_bits || !d_rep || !d_rep_len)))
+        return KMP_EINVAL;
+    if (n == 0) return KMP_OK;
+    hipStream_t st = as_stream(stream);
+    const uint64_t words = kmp_dev_repeat_bitmap_words(k);
+    hipError_t e = hipMemsetAsync(d_bits, 0, 2 * words * sizeof(uint32_t), st);
+    if (e != hipSuccess) return KMP_EDEVICE;
+    mark_kernel<<<n, kFilterThreads, 0, st>>>(d_set, d_set_len, d_res_off, d_bits, d_bits + words);
+    compact_repeats_kernel<<<n, kFilterThreads, 0, st>>>(d_set, d_set_len, d_res_off, d_bits + words, d_rep,
+                                                         d_rep_len);
+    return hip_status(hipGetLastError());
+}
+
+void kmp_pair_geometry_get(kmp_pair_geometry* g) {
+    if (!g) return;
+    g->tile_slots = kTileSlots;
+    g->tile_cap = kTileCap;
+    g->rows_max = kRowsMax;
+    g->threads = kPairThreads;
+}
+
+int kmp_plan_pairs(const uint32_t* set_len, uint32_t n, uint64_t chunk_cost, kmp_work_item* items, uint64_t cap,
+                   uint64_t* n_items) {
+    if (!n_items || (n && !set_len) || (cap && !items)) return KMP_EINVAL;
+    if (chunk_cost == 0) chunk_cost = 1;
+    uint64_t m = 0;
+    uint32_t r0 = 0;
+    while (r0 < n) {
+        // row tile [r0, r1): greedy in index order
+        uint32_t r1 = r0;
+        uint64_t tot = 0;
+        while (r1 < n && r1 - r0 < kRowsMax && tot + set_len[r1] <= kTileCap) tot += set_len[r1++];
+        if (r1 == r0) return KMP_EINVAL;  // a single set longer than the tile capacity
+        if (tot > 0 && r0 + 1 < n) {
+            // columns [r0+1, n) cut by cost; empty rows-only tiles produce no items
+            uint32_t c0 = r0 + 1;
+            while (c0 < n) {
+                uint32_t c1 = c0;
+                uint64_t cost = 0;
+                while (c1 < n && (cost < chunk_cost || c1 == c0)) cost += set_len[c1++] + 1;
+                if (m < cap) items[m] = kmp_work_item{r0, r1, c0, c1};
+                ++m;
+                c0 = c1;
+            }
+        }
+        r0 = r1;
+    }
+    *n_items = m;
+    return m > cap ? KMP_EOVERFLOW : KMP_OK;
+}
+
+int kmp_dev_pairs(const uint32_t* d_set, const uint32_t* d_set_len, const uint64_t* d_res_off,
+                  const uint16_t* d_class, uint32_t n, const kmp_work_item* d_items, uint64_t n_items,
+                  uint32_t min_shared, int require_class_diff, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w,
+                  uint64_t cap, unsigned long long* d_count, void* stream) {
+    if (n_items == 0) return KMP_OK;
+    if (!d_set || !d_set_len || !d_res_off || !d_class || !d_items || !d_count || (cap && (!d_p || !d_q || !d_w)))
+        return KMP_EINVAL;
+    if (n_items > 0x7FFFFFFFull) return KMP_EINVAL;
+    if (min_shared < 1) min_shared = 1;
+    pair_kernel<<<(uint32_t)n_items, kPairThreads, 0, as_stream(stream)>>>(
+        d_set, d_set_len, d_res_off, d_class, d_items, min_shared, require_class_diff, d_p, d_q, d_w, cap, d_count);
+    return hip_status(hipGetLastError());
+}
+
+uint64_t kmp_dev_sort_edges_tmp_bytes(uint64_t n, uint32_t n_proteins) {
+    return sort_layout(n, n_proteins ? n_proteins : 1).total;
+}
+
+int kmp_dev_sort_edges(uint32_t* d_p, uint32_t* d_q, uint32_t* d_w, uint64_t n, uint32_t n_proteins, void* d_tmp,
+                       uint64_t tmp_bytes, void* stream) {
+    if (n == 0) return KMP_OK;
+    if (!d_p || !d_q || !d_w || !d_tmp || n_proteins == 0) return KMP_EINVAL;
+    const SortLayout l = sort_layout(n, n_proteins);
+    if (tmp_bytes < l.total) return KMP_EINVAL;
+    hipStream_t st = as_stream(stream);
+    char* base = (char*)align_up((uint64_t)(uintptr_t)d_tmp, 256) ;
+    if ((uint64_t)(base - (char*)d_tmp) + l.total - 256 > tmp_bytes) return KMP_EINVAL;
+    auto* kin = reinterpret_cast<unsigned long long*>(base + l.keys_in);
+    auto* kout = reinterpret_cast<unsigned long long*>(base + l.keys_out);
+    auto* vout = reinterpret_cast<uint32_t*>(base + l.vals_out);
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, 8192);
+    pack_edges_kernel<<<blocks, 256, 0, st>>>(d_p, d_q, n, n_proteins, kin);
+    size_t prim = l.prim_bytes;
+    const unsigned end_bit = bits_for((uint64_t)n_proteins * n_proteins);
+    hipError_t e = rocprim::radix_sort_pairs(base + l.prim, prim, kin, kout, d_w, vout, (size_t)n, 0u, end_bit, st);
+    if (e != hipSuccess) return KMP_EDEVICE;
+    unpack_edges_kernel<<<blocks, 256, 0, st>>>(kout, n, n_proteins, d_p, d_q);
+    e = hipMemcpyAsync(d_w, vout, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st);
+    if (e != hipSuccess) return KMP_EDEVICE;
+    return hip_status(hipGetLastError());
+}
+
+}  // extern "C"

@@ -1,0 +1,188 @@
+"""Device-resident pipeline over the kmp_dev_* stages (include/kmerpair.h).
+
+PyTorch is plumbing here: it owns the HBM buffers and the stream; every byte of k-mer work
+runs in libkmerpair's HIP kernels.  One ``DevicePipeline`` holds one protein batch resident
+on one GPU and runs the reference's hot path as stages:
+
+  build_sets   Protein::new + per-protein sort/dedup      (protein.rs:107-132, main.rs:280-282)
+  filter       remove_unique_five_mers (df >= 2)           (protein.rs:151-162, main.rs:127-149)
+  plan         row tiles x column chunks of the N x N upper triangle (host, from set sizes)
+  pairs        Graph::new + remove_uninteresting_edges + combine_edges (graph/mod.rs)
+  sort         canonical (p, q) order
+
+A multi-GPU host (dist.py) runs build_sets on a protein slice, all-gathers the sets over RCCL
+and runs ``pairs`` on its share of the work items.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, lib
+from .engine import Proteins
+
+CHUNK_COST = 65536  # set entries streamed per work item (column side)
+
+
+def _p(t: torch.Tensor | None):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _stream() -> C.c_void_p:
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def plan_pairs(set_len: np.ndarray, chunk_cost: int = CHUNK_COST) -> np.ndarray:
+    """Host planner (kmp_plan_pairs) -> structured array of work items."""
+    L = lib()
+    lens = np.ascontiguousarray(set_len, dtype=np.uint32)
+    n = C.c_uint64()
+    st = L.kmp_plan_pairs(_np(lens), len(lens), chunk_cost, None, 0, C.byref(n))
+    if st not in (_lib.KMP_OK, _lib.KMP_EOVERFLOW):
+        check(st, "kmp_plan_pairs")
+    items = np.zeros((max(1, n.value), 4), dtype=np.uint32)
+    check(L.kmp_plan_pairs(_np(lens), len(lens), chunk_cost, _np(items), n.value, C.byref(n)),
+          "kmp_plan_pairs")
+    return items[:n.value]
+
+
+def _np(a: np.ndarray):
+    return None if a.size == 0 else C.c_void_p(a.ctypes.data)
+
+
+def split_items(items: np.ndarray, set_len: np.ndarray, world: int) -> list:
+    """Cut the (tile, chunk)-ordered item list into `world` contiguous shares of equal
+    estimated cost (column entries probed + row entries inserted per item)."""
+    if world <= 1 or len(items) == 0:
+        return [items] + [items[:0]] * (world - 1)
+    csum = np.concatenate([[0], np.cumsum(set_len.astype(np.int64))])
+    cost = (csum[items[:, 3]] - csum[items[:, 2]]) + (csum[items[:, 1]] - csum[items[:, 0]]) + 1024
+    cum = np.cumsum(cost)
+    cuts = np.searchsorted(cum, cum[-1] * np.arange(1, world) / world)
+    return np.split(items, cuts)
+
+
+class DevicePipeline:
+    def __init__(self, proteins: Proteins, k: int, device: torch.device | str = "cuda",
+                 edge_cap: int | None = None):
+        self.k = k
+        self.dev = torch.device(device)
+        self.n = proteins.n
+        self.offsets_host = np.ascontiguousarray(proteins.offsets, dtype=np.uint64)
+        self.total = int(self.offsets_host[-1])
+        lens = np.diff(self.offsets_host.astype(np.int64))
+        self.max_len = int(lens.max()) if self.n else 0
+        L = lib()
+        dev = self.dev
+        self.res = torch.from_numpy(np.ascontiguousarray(proteins.residues, dtype=np.uint8)).to(dev)
+        self.off = torch.from_numpy(self.offsets_host.view(np.int64)).to(dev)
+        self.cls = torch.from_numpy(np.ascontiguousarray(proteins.class_id, dtype=np.uint16).view(np.int16)).to(dev)
+        cap = int(L.kmp_set_capacity(self.n, self.total))
+        self.set = torch.empty(cap, dtype=torch.int32, device=dev)
+        self.rep = torch.empty(cap, dtype=torch.int32, device=dev)
+        self.set_len = torch.zeros(max(1, self.n), dtype=torch.int32, device=dev)
+        self.rep_len = torch.zeros(max(1, self.n), dtype=torch.int32, device=dev)
+        words = int(L.kmp_dev_repeat_bitmap_words(k))
+        self.bits = torch.empty(2 * words, dtype=torch.int32, device=dev)
+        long_path = self.max_len - k + 1 > _lib.KMP_LDS_SORT_MAX
+        self.scratch = torch.empty(cap, dtype=torch.int32, device=dev) if long_path else None
+        self.edge_cap = edge_cap or max(1 << 20, 4 * self.n)
+        self._alloc_edges(self.edge_cap)
+        self.count = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.items = None
+        self.n_items = 0
+
+    def _alloc_edges(self, cap):
+        self.edge_cap = cap
+        self.ep = torch.empty(cap, dtype=torch.int32, device=self.dev)
+        self.eq = torch.empty(cap, dtype=torch.int32, device=self.dev)
+        self.ew = torch.empty(cap, dtype=torch.int32, device=self.dev)
+
+    # -- stages ---------------------------------------------------------------------
+    def build_sets(self, lo: int = 0, hi: int | None = None) -> None:
+        """K(p) for proteins [lo, hi) (all by default)."""
+        hi = self.n if hi is None else hi
+        if hi <= lo:
+            return
+        check(lib().kmp_dev_build_sets(_p(self.res), C.c_void_p(self.off.data_ptr() + 8 * lo), hi - lo, self.k,
+                                       self.max_len, _sub(self.set, self, lo), _p(self.set_len[lo:]),
+                                       _sub(self.scratch, self, lo) if self.scratch is not None else None,
+                                       _stream()), "kmp_dev_build_sets")
+
+    def filter(self) -> None:
+        check(lib().kmp_dev_filter_repeats(_p(self.set), _p(self.set_len), _p(self.off), self.n, self.k,
+                                           _p(self.bits), _p(self.rep), _p(self.rep_len), _stream()),
+              "kmp_dev_filter_repeats")
+
+    def plan(self, rank: int = 0, world: int = 1, chunk_cost: int = CHUNK_COST) -> np.ndarray:
+        rep_len = self.rep_len[:self.n].cpu().numpy().view(np.uint32)
+        items = plan_pairs(rep_len, chunk_cost)
+        mine = split_items(items, rep_len, world)[rank]
+        self.n_items = len(mine)
+        self.items = torch.from_numpy(np.ascontiguousarray(mine).view(np.int32).reshape(-1)).to(self.dev) \
+            if len(mine) else None
+        self.rep_len_host = rep_len
+        return mine
+
+    def pairs(self, min_shared: int = 1, require_class_diff: bool = True) -> int:
+        """Runs the pair kernel over the planned items; returns the edge count (syncs)."""
+        for _ in range(2):
+            self.count.zero_()
+            check(lib().kmp_dev_pairs(_p(self.rep), _p(self.rep_len), _p(self.off), _p(self.cls), self.n,
+                                      _p(self.items), self.n_items, min_shared, int(require_class_diff),
+                                      _p(self.ep), _p(self.eq), _p(self.ew), self.edge_cap, _p(self.count),
+                                      _stream()), "kmp_dev_pairs")
+            cnt = int(self.count.item())
+            if cnt <= self.edge_cap:
+                self.n_edges = cnt
+                return cnt
+            self._alloc_edges(cnt + cnt // 8 + 1024)
+        raise RuntimeError("edge count unstable across reruns")
+
+    def sort(self, n_edges: int | None = None) -> None:
+        n = self.n_edges if n_edges is None else n_edges
+        if n == 0:
+            return
+        L = lib()
+        nbytes = int(L.kmp_dev_sort_edges_tmp_bytes(n, self.n))
+        if getattr(self, "_sort_tmp", None) is None or self._sort_tmp.numel() < nbytes:
+            self._sort_tmp = torch.empty(nbytes + 256, dtype=torch.uint8, device=self.dev)
+        check(L.kmp_dev_sort_edges(_p(self.ep), _p(self.eq), _p(self.ew), n, self.n, _p(self._sort_tmp),
+                                   self._sort_tmp.numel(), _stream()), "kmp_dev_sort_edges")
+
+    def step(self, min_shared: int = 1, require_class_diff: bool = True) -> int:
+        """The whole single-GPU path: sets -> filter -> plan -> pairs -> canonical sort."""
+        self.build_sets()
+        self.filter()
+        self.plan()
+        n = self.pairs(min_shared, require_class_diff)
+        self.sort(n)
+        return n
+
+    def edges(self):
+        n = self.n_edges
+        return (self.ep[:n].cpu().numpy().view(np.uint32), self.eq[:n].cpu().numpy().view(np.uint32),
+                self.ew[:n].cpu().numpy().view(np.uint32))
+
+    def set_of(self, p: int, repeat_only: bool = False) -> np.ndarray:
+        base = int(lib().kmp_set_base(int(self.offsets_host[p]), p))
+        buf, ln = (self.rep, self.rep_len) if repeat_only else (self.set, self.set_len)
+        m = int(ln[p].item())
+        return buf[base:base + m].cpu().numpy().view(np.uint32)
+
+
+def _sub(t: torch.Tensor | None, pipe: DevicePipeline, lo: int):
+    """Device pointer for a stage launched on proteins [lo, ...): the per-protein slot math
+    uses absolute protein indices, so a slice launch passes the base shifted back by the
+    slot origin of protein lo (kmp_set_base is affine in p: +4 per protein)."""
+    if t is None:
+        return None
+    if lo == 0:
+        return C.c_void_p(t.data_ptr())
+    # slot(p_abs) = base(off[p_abs], p_abs); the slice kernel computes base(off[p_abs], p_rel)
+    # = slot(p_abs) - 4*lo (up to the round-up, which is identical since 4*lo is a multiple
+    # of 4), so shift the pointer forward by 4*lo elements.
+    return C.c_void_p(t.data_ptr() + 4 * 4 * lo)

@@ -1,0 +1,174 @@
+"""Python face of the host-buffer C ABI (include/kmerpair.h), used by tests and tools.
+
+``KmerPairEngine`` follows the reference's call order in src/main.rs: load the proteins
+(``Protein::new`` batch, main.rs:65-72), build the k-mer sets and the repeat filter
+(main.rs:77-199), then the fused graph pass (``Graph::new`` + ``remove_uninteresting_edges``
++ ``combine_edges``, main.rs:217-227) that returns the collapsed edge list.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib
+
+
+def _ptr(a: np.ndarray | None):
+    return None if a is None or a.size == 0 else C.c_void_p(a.ctypes.data)
+
+
+@dataclass
+class Proteins:
+    """Packed protein batch: residues u8[ΣL], offsets u64[N+1], class ids u16[N]."""
+    residues: np.ndarray
+    offsets: np.ndarray
+    class_id: np.ndarray
+    ids: list | None = None
+    n_classes: int = 0
+
+    @property
+    def n(self) -> int:
+        return len(self.offsets) - 1
+
+
+def read_fasta(path: str) -> Proteins:
+    """FASTA ingest with seq_io semantics (libkmerpair kmp_read_fasta)."""
+    L = lib()
+    n = C.c_uint32()
+    res, off, cls, ids = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_void_p()
+    ids_bytes = C.c_uint64()
+    ncls = C.c_uint32()
+    st = L.kmp_read_fasta(path.encode(), C.byref(n), C.byref(res), C.byref(off), C.byref(cls),
+                          C.byref(ids), C.byref(ids_bytes), C.byref(ncls))
+    check(st, f"kmp_read_fasta({path})")
+    try:
+        N = n.value
+        offsets = np.ctypeslib.as_array(C.cast(off, C.POINTER(C.c_uint64)), shape=(N + 1,)).copy()
+        total = int(offsets[-1])
+        residues = (np.ctypeslib.as_array(C.cast(res, C.POINTER(C.c_uint8)), shape=(total,)).copy()
+                    if total else np.zeros(0, np.uint8))
+        class_id = (np.ctypeslib.as_array(C.cast(cls, C.POINTER(C.c_uint16)), shape=(N,)).copy()
+                    if N else np.zeros(0, np.uint16))
+        raw = C.string_at(ids, ids_bytes.value) if ids_bytes.value else b""
+        id_list = [s.decode() for s in raw.split(b"\0")[:N]] if N else []
+    finally:
+        for p in (res, off, cls, ids):
+            L.kmp_free_host(p)
+    return Proteins(residues, offsets, class_id, id_list, ncls.value)
+
+
+def synth(n: int, seed: int, law: int = _lib.KMP_LEN_NORMAL300, with_family=False):
+    """Synthetic protein batch of SURVEY.md §8d (deterministic in (n, seed, law))."""
+    L = lib()
+    offsets = np.zeros(n + 1, dtype=np.uint64)
+    cls = np.zeros(n, dtype=np.uint16)
+    fam = np.zeros(n, dtype=np.uint32)
+    res = C.c_void_p()
+    check(L.kmp_synth_packed(n, seed, law, C.byref(res), _ptr(offsets), _ptr(cls), _ptr(fam)),
+          "kmp_synth_packed")
+    total = int(offsets[-1])
+    try:
+        residues = np.ctypeslib.as_array(C.cast(res, C.POINTER(C.c_uint8)), shape=(total,)).copy()
+    finally:
+        L.kmp_free_host(res)
+    p = Proteins(residues, offsets, cls, None, 15)
+    return (p, fam) if with_family else p
+
+
+def write_synth_fasta(path: str, n: int, seed: int, law: int = _lib.KMP_LEN_NORMAL300) -> None:
+    check(lib().kmp_synth_write_fasta(path.encode(), n, seed, law), "kmp_synth_write_fasta")
+
+
+@dataclass
+class Edges:
+    p: np.ndarray
+    q: np.ndarray
+    w: np.ndarray
+    score: np.ndarray
+
+    def __len__(self):
+        return len(self.p)
+
+
+class KmerPairEngine:
+    """One device context (kmp_ctx) holding a protein batch and its k-mer sets."""
+
+    def __init__(self, device: int = 0, cpu_threads: int = 1):
+        self._ctx = C.c_void_p()
+        check(lib().kmp_ctx_create(C.byref(self._ctx), device, cpu_threads), "kmp_ctx_create")
+
+    def close(self):
+        if self._ctx:
+            lib().kmp_ctx_destroy(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, st, where):
+        check(st, where, self._ctx)
+
+    def load(self, proteins: Proteins) -> None:
+        res = np.ascontiguousarray(proteins.residues, dtype=np.uint8)
+        off = np.ascontiguousarray(proteins.offsets, dtype=np.uint64)
+        cls = np.ascontiguousarray(proteins.class_id, dtype=np.uint16)
+        self._check(lib().kmp_load_proteins(self._ctx, _ptr(res), _ptr(off), len(off) - 1, _ptr(cls)),
+                    "kmp_load_proteins")
+        self.n = len(off) - 1
+
+    def extract(self, k: int) -> None:
+        self._check(lib().kmp_extract(self._ctx, k), "kmp_extract")
+
+    def _get(self, fn, name, p):
+        n = C.c_uint64()
+        st = fn(self._ctx, p, None, 0, C.byref(n))
+        if st not in (_lib.KMP_OK, _lib.KMP_EOVERFLOW):
+            self._check(st, name)
+        out = np.zeros(n.value, dtype=np.uint32)
+        self._check(fn(self._ctx, p, _ptr(out), n.value, C.byref(n)), name)
+        return out
+
+    def get_kmers(self, p: int) -> np.ndarray:
+        return self._get(lib().kmp_get_kmers, "kmp_get_kmers", p)
+
+    def build_sets(self, k: int) -> None:
+        self._check(lib().kmp_build_sets(self._ctx, k), "kmp_build_sets")
+
+    def get_set(self, p: int) -> np.ndarray:
+        return self._get(lib().kmp_get_set, "kmp_get_set", p)
+
+    def counters(self) -> dict:
+        c = _lib.Counters()
+        self._check(lib().kmp_counters_get(self._ctx, C.byref(c)), "kmp_counters_get")
+        return c.as_dict()
+
+    def pairs(self, min_shared=1, require_class_diff=True, align_threshold=10,
+              score=_lib.KMP_SCORE_COUNT) -> Edges:
+        o = _lib.PairOpts(min_shared, int(require_class_diff), align_threshold, score)
+        e = C.c_void_p()
+        self._check(lib().kmp_pairs(self._ctx, C.byref(o), C.byref(e)), "kmp_pairs")
+        try:
+            n = C.c_uint64()
+            check(lib().kmp_edges_count(e, C.byref(n)), "kmp_edges_count")
+            m = n.value
+            p = np.zeros(m, np.uint32)
+            q = np.zeros(m, np.uint32)
+            w = np.zeros(m, np.uint32)
+            s = np.zeros(m, np.float32)
+            check(lib().kmp_edges_get(e, _ptr(p), _ptr(q), _ptr(w), _ptr(s), m, C.byref(n)),
+                  "kmp_edges_get")
+        finally:
+            lib().kmp_edges_free(e)
+        return Edges(p, q, w, s)
