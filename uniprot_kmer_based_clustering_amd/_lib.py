@@ -97,6 +97,17 @@ SIGNATURES = {
 _lib = None
 
 
+def _bind_hip_runtime():
+    """One HIP runtime per process: torch ships its own libamdhip64.so.7 and the soname is
+    shared with /opt/rocm's, so whichever loads first serves both.  Import torch first so
+    its runtime is the one libkmerpair binds to (device pointers and streams from torch are
+    then valid in the library).  Without torch the library binds /opt/rocm's runtime."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # pragma: no cover - torch is part of the image
+        pass
+
+
 def lib():
     """Load libkmerpair.so (raises if it is missing: no CPU fallback exists)."""
     global _lib
@@ -105,6 +116,7 @@ def lib():
             raise RuntimeError(
                 f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
                 "(hipcc --offload-arch=gfx950); the k-mer pair path has no CPU fallback")
+        _bind_hip_runtime()
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)
