@@ -147,36 +147,54 @@ int kmp_dev_filter_repeats(const uint32_t* d_set, const uint32_t* d_set_len, con
                            uint32_t n, int k, uint32_t* d_bits, uint32_t* d_rep, uint32_t* d_rep_len,
                            void* stream);
 
-/* A work item of the pair kernel: row proteins [row_beg,row_end) (one LDS-resident tile)
- * against column proteins [col_beg,col_end) (streamed); pairs (p,q) with p < q only. */
+/* Pair-kernel plan.  The repeat-filtered sets are packed into one dense CSR (dense_off[N+1],
+ * ascending within each set).  Proteins are packed greedily in index order into row tiles
+ * (Σ len <= tile_cap, count <= rows_max); the column axis [0, N) is cut into chunks of about
+ * chunk_cost set entries (chunk_col[c] .. chunk_col[c+1]).  A work item is one row tile
+ * against one chunk, restricted to columns after the tile's first row; items are emitted
+ * chunk-major (all tiles of chunk 0, then chunk 1, ...) and together cover every pair p < q
+ * exactly once. */
 typedef struct {
-    uint32_t row_beg, row_end, col_beg, col_end;
+    uint32_t row_beg, row_end;  /* row proteins [row_beg, row_end): one LDS-resident tile */
+    uint32_t col_beg, col_end;  /* column proteins [col_beg, col_end): streamed */
 } kmp_work_item;
 
 /* Row-tile geometry of the pair kernel (fixed at build time). */
 typedef struct {
-    uint32_t tile_slots;  /* LDS hash slots per row tile */
+    uint32_t tile_slots;  /* exact-table entries per row tile */
     uint32_t tile_cap;    /* max set entries per row tile */
     uint32_t rows_max;    /* max proteins per row tile */
     uint32_t threads;     /* workgroup size */
 } kmp_pair_geometry;
 void kmp_pair_geometry_get(kmp_pair_geometry* g);
 
-/* Host-side planner: row tiles packed greedily in index order (Σ len <= tile_cap, count <=
- * rows_max; a protein longer than tile_cap is an error), each tile's upper-triangle column
- * range [tile_beg, N) cut into chunks of about chunk_cost set entries.  Items are emitted
- * in (tile, chunk) order.  *n_items = items needed; KMP_EOVERFLOW if cap is smaller. */
-int kmp_plan_pairs(const uint32_t* set_len, uint32_t n, uint64_t chunk_cost, kmp_work_item* items,
-                   uint64_t cap, uint64_t* n_items);
+/* Host-side planner.  set_len[N]: repeat-filtered set sizes.  Fills dense_off[N+1] and up to
+ * cap items (*n_items = items needed; KMP_EOVERFLOW if cap is smaller; call with cap 0 to
+ * size).  chunk_cost = 0 picks the default.  A set longer than tile_cap is KMP_EINVAL. */
+int kmp_plan_pairs(const uint32_t* set_len, uint32_t n, uint64_t chunk_cost, uint64_t* dense_off,
+                   kmp_work_item* items, uint64_t cap, uint64_t* n_items);
+
+/* XCD-aware launch order for an 8-XCD device: the n chunk-major items are dealt to 8 lists
+ * (chunk g -> list g % 8) and written as slot 8*s + x = list x's item s, so the workgroups
+ * the dispatcher places on one XCD stream the same column chunk through that XCD's L2.
+ * Short lists are padded with empty items (row_beg == row_end, a no-op in the kernel).
+ * *n_out = slots needed (<= n + 7 * items of one chunk); KMP_EOVERFLOW if cap is smaller.
+ * A speed hint only: any order of the items gives the same edges. */
+int kmp_order_items_xcd(const kmp_work_item* items, uint64_t n, kmp_work_item* out, uint64_t cap,
+                        uint64_t* n_out);
+
+/* Packs the repeat-filtered sets (slot layout) into the dense CSR: d_dense[d_dense_off[p] ...]. */
+int kmp_dev_pack_dense(const uint32_t* d_rep, const uint64_t* d_res_off, const uint64_t* d_dense_off,
+                       uint32_t n, uint32_t* d_dense, void* stream);
 
 /* The pair kernel over work items [0, n_items): appends (p, q, w) with p < q,
  * w = |K(p) ∩ K(q)| >= min_shared and (if required) class[p] != class[q] to d_p/d_q/d_w in
  * arbitrary order at positions d_count[0]++ (< cap; the counter keeps counting past cap so
  * the caller can resize and rerun).  d_count (one u64) must be zeroed by the caller. */
-int kmp_dev_pairs(const uint32_t* d_set, const uint32_t* d_set_len, const uint64_t* d_res_off,
-                  const uint16_t* d_class, uint32_t n, const kmp_work_item* d_items, uint64_t n_items,
-                  uint32_t min_shared, int require_class_diff, uint32_t* d_p, uint32_t* d_q,
-                  uint32_t* d_w, uint64_t cap, unsigned long long* d_count, void* stream);
+int kmp_dev_pairs(const uint32_t* d_dense, const uint64_t* d_dense_off, const uint16_t* d_class, uint32_t n,
+                  const kmp_work_item* d_items, uint64_t n_items, uint32_t min_shared, int require_class_diff,
+                  uint32_t* d_p, uint32_t* d_q, uint32_t* d_w, uint64_t cap, unsigned long long* d_count,
+                  void* stream);
 
 /* Canonical order: sorts n edges by (p, q).  Keys/values are read from d_p/d_q/d_w and the
  * sorted result is written back to them.  d_tmp: kmp_dev_sort_edges_tmp_bytes(n, N) bytes. */

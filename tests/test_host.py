@@ -39,7 +39,7 @@ def test_host_constants():
         b = L.kmp_set_base(off, p)
         assert b % 4 == 0 and off + 4 * p <= b <= off + 4 * p + 3
     g = _lib.geometry()
-    assert g.tile_cap < g.tile_slots and g.rows_max <= 256 and g.threads % 64 == 0
+    assert g.tile_cap <= g.tile_slots and g.rows_max <= 256 and g.threads % 64 == 0
 
 
 def test_fasta_uniprot_matches_independent_parser(tmp_path):
@@ -112,48 +112,60 @@ def test_synthetic_generator_shape():
     assert L2.min() >= 40 and L2.max() <= 2100 and 400 < L2.mean() < 650
 
 
-def plan(lens, chunk):
-    import ctypes as C
-    L = _lib.lib()
-    lens = np.ascontiguousarray(lens, dtype=np.uint32)
-    n = C.c_uint64()
-    st = L.kmp_plan_pairs(lens.ctypes.data, len(lens), chunk, None, 0, C.byref(n))
-    assert st in (_lib.KMP_OK, _lib.KMP_EOVERFLOW)
-    items = (_lib.WorkItem * max(1, n.value))()
-    st = L.kmp_plan_pairs(lens.ctypes.data, len(lens), chunk, items, n.value, C.byref(n))
-    assert st == _lib.KMP_OK
-    return [(it.row_beg, it.row_end, it.col_beg, it.col_end) for it in items[:n.value]], st
+def plan(lens, chunk_cost):
+    from uniprot_kmer_based_clustering_amd.device import Plan
+    return Plan(np.asarray(lens, dtype=np.uint32), chunk_cost)
 
 
-@pytest.mark.parametrize("seed", [0, 1, 2])
-def test_planner_covers_upper_triangle_once(seed):
-    rng = np.random.default_rng(seed)
-    n = 700
-    lens = rng.integers(0, 400, size=n)
-    lens[rng.random(n) < 0.1] = 0
-    g = _lib.geometry()
-    items, _ = plan(lens, 5000)
+def coverage(n, items):
     cover = np.zeros((n, n), dtype=np.int32)
-    for r0, r1, c0, c1 in items:
-        assert r1 - r0 <= g.rows_max and lens[r0:r1].sum() <= g.tile_cap
-        assert c0 > r0
+    for r0, r1, c0, c1 in np.asarray(items, dtype=np.int64):
         for r in range(r0, r1):
             lo = max(c0, r + 1)
             if lo < c1:
                 cover[r, lo:c1] += 1
-    iu = np.triu_indices(n, 1)
-    nonempty_rows = np.array([any(r0 <= i < r1 and lens[r0:r1].sum() > 0 for r0, r1, _, _ in items)
-                              for i in range(n)])
-    for i, j in zip(*iu):
-        if nonempty_rows[i]:
-            assert cover[i, j] == 1
+    return cover
+
+
+@pytest.mark.parametrize("seed,chunk", [(0, 1), (1, 3000), (2, 10 ** 9)])
+def test_planner_covers_upper_triangle_once(seed, chunk):
+    from uniprot_kmer_based_clustering_amd.device import order_xcd
+    rng = np.random.default_rng(seed)
+    n = 900
+    lens = rng.integers(0, 600, size=n)
+    lens[rng.random(n) < 0.1] = 0
+    lens[rng.random(n) < 0.02] = 4000
+    g = _lib.geometry()
+    pl = plan(lens, chunk)
+    np.testing.assert_array_equal(pl.dense_off[1:], np.cumsum(lens))
+    for r0, r1, c0, c1 in pl.items.astype(np.int64):
+        assert r1 - r0 <= g.rows_max and 0 < lens[r0:r1].sum() <= g.tile_cap
+        assert c1 > r0 + 1
+    cover = coverage(n, pl.items)
+    in_item = np.zeros(n, dtype=bool)
+    for r0, r1, _, _ in pl.items.astype(np.int64):
+        in_item[r0:r1] = True
+    for i in range(n - 1):
+        row = cover[i, i + 1:]
+        if in_item[i]:
+            assert np.all(row == 1), i
+        else:
+            assert lens[i] == 0 and np.all(row == 0)
     assert cover[np.tril_indices(n)].sum() == 0
+    # rank shares are contiguous and partition the items; the XCD order is a permutation
+    for world in (2, 3, 8):
+        parts = [pl.share(r, world) for r in range(world)]
+        np.testing.assert_array_equal(np.concatenate(parts), pl.items)
+    ordered = order_xcd(pl.items)
+    real = ordered[ordered[:, 1] > ordered[:, 0]]
+    assert len(real) == len(pl.items)
+    np.testing.assert_array_equal(coverage(n, real), cover)
+    assert len(ordered) % 8 == 0
 
 
 def test_planner_rejects_oversized_set():
-    import ctypes as C
     g = _lib.geometry()
     lens = np.array([10, g.tile_cap + 1, 5], dtype=np.uint32)
-    n = C.c_uint64()
-    st = _lib.lib().kmp_plan_pairs(lens.ctypes.data, 3, 100, None, 0, C.byref(n))
-    assert st == _lib.KMP_EINVAL
+    with pytest.raises(_lib.KmpError) as e:
+        plan(lens, 4)
+    assert e.value.status == _lib.KMP_EINVAL

@@ -82,8 +82,10 @@ SIGNATURES = {
     "kmp_dev_repeat_bitmap_words": (C.c_uint64, [C.c_int]),
     "kmp_dev_filter_repeats": (C.c_int, [P, P, P, C.c_uint32, C.c_int, P, P, P, P]),
     "kmp_pair_geometry_get": (None, [P]),
-    "kmp_plan_pairs": (C.c_int, [P, C.c_uint32, C.c_uint64, P, C.c_uint64, U64P]),
-    "kmp_dev_pairs": (C.c_int, [P, P, P, P, C.c_uint32, P, C.c_uint64, C.c_uint32, C.c_int,
+    "kmp_plan_pairs": (C.c_int, [P, C.c_uint32, C.c_uint64, P, P, C.c_uint64, U64P]),
+    "kmp_order_items_xcd": (C.c_int, [P, C.c_uint64, P, C.c_uint64, U64P]),
+    "kmp_dev_pack_dense": (C.c_int, [P, P, P, C.c_uint32, P, P]),
+    "kmp_dev_pairs": (C.c_int, [P, P, P, C.c_uint32, P, C.c_uint64, C.c_uint32, C.c_int,
                                 P, P, P, C.c_uint64, P, P]),
     "kmp_dev_sort_edges_tmp_bytes": (C.c_uint64, [C.c_uint64, C.c_uint32]),
     "kmp_dev_sort_edges": (C.c_int, [P, P, P, C.c_uint64, C.c_uint32, P, C.c_uint64, P]),

@@ -20,6 +20,7 @@ using namespace kmp;
 
 namespace {
 
+
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
@@ -67,7 +68,7 @@ struct kmp_ctx {
     std::vector<uint32_t> h_set_len, h_rep_len;
     kmp_counters counters{};
 
-    DevBuf items, ep, eq, ew, ecount, sort_tmp;
+    DevBuf items, dense_off, dense, ep, eq, ew, ecount, sort_tmp;
     uint64_t edge_cap = 0;
 };
 
@@ -324,18 +325,27 @@ int kmp_pairs(kmp_ctx* c, const kmp_pair_opts* opts, kmp_edges** out) {
     if (o.score != KMP_SCORE_COUNT && o.score != KMP_SCORE_JACCARD) return fail(c, KMP_EINVAL, "unknown score %d", o.score);
     KMP_TRY(c, use_device(c));
 
-    // plan (host): row tiles of the repeat-filtered sets, column chunks
-    uint64_t n_items = 0;
-    const uint64_t chunk_cost = 65536;
-    int st = kmp_plan_pairs(c->h_rep_len.data(), c->n, chunk_cost, nullptr, 0, &n_items);
+    // plan (host): dense CSR offsets, row tiles x column chunks, XCD-aware launch order
+    std::vector<uint64_t> dense_off(c->n + 1);
+    uint64_t n_plan = 0, n_items = 0;
+    int st = kmp_plan_pairs(c->h_rep_len.data(), c->n, 0, dense_off.data(), nullptr, 0, &n_plan);
     if (st != KMP_OK && st != KMP_EOVERFLOW)
-        return fail(c, st, "planner: a repeat-filtered set exceeds the tile capacity (%u k-mers)", kTileCap);
+        return fail(c, st, "planner: a repeat-filtered set exceeds %u k-mers", kTileCap);
+    std::vector<kmp_work_item> plan(n_plan);
+    KMP_TRY(c, kmp_plan_pairs(c->h_rep_len.data(), c->n, 0, dense_off.data(), plan.data(), n_plan, &n_plan));
+    kmp_order_items_xcd(plan.data(), n_plan, nullptr, 0, &n_items);
     std::vector<kmp_work_item> items(n_items);
-    KMP_TRY(c, kmp_plan_pairs(c->h_rep_len.data(), c->n, chunk_cost, items.data(), n_items, &n_items));
+    KMP_TRY(c, kmp_order_items_xcd(plan.data(), n_plan, items.data(), n_items, &n_items));
     KMP_HIP(c, c->items.reserve(std::max<uint64_t>(1, n_items) * sizeof(kmp_work_item)));
+    KMP_HIP(c, c->dense_off.reserve((c->n + 1) * sizeof(uint64_t)));
+    KMP_HIP(c, c->dense.reserve(std::max<uint64_t>(1, dense_off[c->n]) * sizeof(uint32_t)));
+    KMP_HIP(c, hipMemcpyAsync(c->dense_off.p, dense_off.data(), (c->n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice,
+                              c->stream));
     if (n_items)
         KMP_HIP(c, hipMemcpyAsync(c->items.p, items.data(), n_items * sizeof(kmp_work_item), hipMemcpyHostToDevice,
                                   c->stream));
+    KMP_TRY(c, kmp_dev_pack_dense(c->rep.as<uint32_t>(), c->off.as<uint64_t>(), c->dense_off.as<uint64_t>(), c->n,
+                                  c->dense.as<uint32_t>(), c->stream));
     if (c->edge_cap == 0) c->edge_cap = std::max<uint64_t>(1u << 20, 4ull * c->n);
     KMP_HIP(c, c->ecount.reserve(sizeof(unsigned long long)));
     unsigned long long count = 0;
@@ -344,10 +354,9 @@ int kmp_pairs(kmp_ctx* c, const kmp_pair_opts* opts, kmp_edges** out) {
         KMP_HIP(c, c->eq.reserve(c->edge_cap * sizeof(uint32_t)));
         KMP_HIP(c, c->ew.reserve(c->edge_cap * sizeof(uint32_t)));
         KMP_HIP(c, hipMemsetAsync(c->ecount.p, 0, sizeof(unsigned long long), c->stream));
-        KMP_TRY(c, kmp_dev_pairs(c->rep.as<uint32_t>(), c->rep_len.as<uint32_t>(), c->off.as<uint64_t>(),
-                                 c->cls.as<uint16_t>(), c->n, c->items.as<kmp_work_item>(), n_items, o.min_shared,
-                                 o.require_class_diff, c->ep.as<uint32_t>(), c->eq.as<uint32_t>(), c->ew.as<uint32_t>(),
-                                 c->edge_cap, c->ecount.as<unsigned long long>(), c->stream));
+        KMP_TRY(c, kmp_dev_pairs(c->dense.as<uint32_t>(), c->dense_off.as<uint64_t>(), c->cls.as<uint16_t>(), c->n,
+                                 c->items.as<kmp_work_item>(), n_items, o.min_shared, o.require_class_diff, c->ep.as<uint32_t>(), c->eq.as<uint32_t>(),
+                                 c->ew.as<uint32_t>(), c->edge_cap, c->ecount.as<unsigned long long>(), c->stream));
         KMP_HIP(c, hipMemcpyAsync(&count, c->ecount.p, sizeof count, hipMemcpyDeviceToHost, c->stream));
         KMP_HIP(c, hipStreamSynchronize(c->stream));
         if (count <= c->edge_cap) break;

@@ -34,12 +34,15 @@ KMP_HD inline uint64_t set_base(uint64_t res_off, uint32_t p) {
 // ---- pair-kernel geometry (LDS budget per workgroup, one workgroup per CU) ----
 constexpr uint32_t kPairThreads = 1024;                 // 16 waves
 constexpr uint32_t kPairWaves = kPairThreads / 64;
-constexpr uint32_t kBucketSlots = 4;                    // one ds_read_b128 per probe step
-constexpr uint32_t kTileBucketsLog2 = 12;
-constexpr uint32_t kTileBuckets = 1u << kTileBucketsLog2;
-constexpr uint32_t kTileSlots = kTileBuckets * kBucketSlots;   // 16384 slots: 64 KiB keys
-constexpr uint32_t kTileCap = 10240;                    // load factor <= 0.625
+constexpr uint32_t kTileCap = 16384;                    // row-tile k-mers (exact table: 64 KiB keys + 16 KiB rows)
 constexpr uint32_t kRowsMax = 256;                      // row index fits u8
-constexpr uint32_t kEmptyKey = 0xFFFFFFFFu;
+constexpr uint32_t kBloomLog2 = 12;                     // 4,096 x 64-bit Bloom blocks (32 KiB), 4 bits per key
+constexpr uint32_t kBloomBlocks = 1u << kBloomLog2;
+constexpr uint32_t kBuckets = kBloomBlocks;             // exact-table bucket = Bloom block of the key
+constexpr uint32_t kTileSlots = kTileCap;               // reported by kmp_pair_geometry_get
+constexpr uint32_t kHashMul = 0x9E3779B1u;              // block / bucket hash (top 12 bits)
+constexpr uint32_t kHashMul2 = 0x85EBCA6Bu;             // bit positions inside the block
+constexpr uint32_t kColRegs = 4;                        // column k-mers held per lane (256 per wave pass)
+constexpr uint64_t kChunkCost = 262144;                 // column k-mers per work item (one L2-shared chunk)
 
 }  // namespace kmp

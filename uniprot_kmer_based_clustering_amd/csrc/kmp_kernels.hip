@@ -16,6 +16,9 @@
 
 #include <rocprim/device/device_radix_sort.hpp>
 
+#include <algorithm>
+#include <vector>
+
 #include "kmerpair.h"
 #include "kmp_internal.hpp"
 
@@ -268,128 +271,225 @@ __global__ __launch_bounds__(kFilterThreads) void compact_repeats_kernel(
 }
 
 // ------------------------------------------------------------------------------------
-// Pair kernel.  One workgroup per work item (row tile × column range), one per CU.
-//   LDS: the row tile's sets as one multiset hash index: 16,384 u32 keys in 4-slot buckets
-//   (a probe step is one ds_read_b128) + the owning row (u8) per slot; per-wave counters.
-//   Each wave streams one column protein at a time: 64 k-mers per step, one per lane, each
-//   probing the index; a hit on row r adds 1 to the wave's counter for r.  After the column
-//   the touched rows are emitted (p = row, q = column, w = count) if w >= min_shared and the
-//   AMR classes differ (mod.rs:580-587), with one global atomic per wave (ballot + mbcnt).
-__device__ __forceinline__ uint32_t tile_hash(uint32_t x) {
-    return (x * 2654435761u) >> (32 - kTileBucketsLog2);
+// Dense CSR of the repeat-filtered sets (column stream of the pair kernel).
+__global__ __launch_bounds__(256) void pack_dense_kernel(const uint32_t* __restrict__ rep,
+                                                         const uint64_t* __restrict__ res_off,
+                                                         const uint64_t* __restrict__ dense_off,
+                                                         uint32_t* __restrict__ dense) {
+    const uint32_t p = blockIdx.x;
+    const uint64_t d = dense_off[p], len = dense_off[p + 1] - d;
+    const uint32_t* s = rep + set_base(res_off[p], p);
+    for (uint64_t e = threadIdx.x; e < len; e += 256) dense[d + e] = s[e];
+}
+
+// ------------------------------------------------------------------------------------
+// Pair kernel.  One workgroup (16 waves) per work item = one row tile × one column chunk.
+// LDS holds the row tile as
+//   * a blocked Bloom filter: 4,096 64-bit blocks, 4 bits per key inside the block picked
+//     by the key's top 12 hash bits (≈0.4 % false positives at a full tile; no false
+//     negatives) — the only LDS access of ~all column k-mers (one ds_read_b64);
+//   * an exact multiset table: the tile's k-mers counting-sorted by the same 12-bit block
+//     (keys u32 + owning row u8, bucket b = [F[b], F[b+1])), read only by lanes that pass
+//     the filter;
+//   * per-wave hit counters.
+// Each wave owns the item's columns q ≡ wave (mod 16) and streams them from HBM/L2 straight
+// into registers (kColRegs k-mers per lane, all loads independent, the next column's loads
+// in flight while the current one is probed).  A confirmed hit on row r bumps the wave's
+// counter for r (rows with p = row_beg + r < q only: upper triangle); after the column the
+// touched rows are emitted as (p, q, w) when w >= min_shared and the AMR classes differ
+// (mod.rs:580-587), one global atomic per wave (ballot + mbcnt).
+static_assert(kBuckets == 4 * kPairThreads, "bucket scan assumes 4 buckets per thread");
+static_assert(kTileCap <= 65536, "tile positions fit the exact table");
+
+__device__ __forceinline__ uint64_t bloom_bits(uint32_t x) {
+    const uint32_t g = x * kHashMul2;
+    return (1ull << (g & 63u)) | (1ull << ((g >> 6) & 63u)) | (1ull << ((g >> 12) & 63u)) |
+           (1ull << ((g >> 18) & 63u));
+}
+__device__ __forceinline__ uint32_t bloom_block(uint32_t x) { return (x * kHashMul) >> (32 - kBloomLog2); }
+
+// exclusive scan of one value per thread over the 1024-thread block
+__device__ __forceinline__ uint32_t block_scan_1024(uint32_t v, uint32_t* wave_tot) {
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) wave_tot[w] = x;
+    __syncthreads();
+    uint32_t before = 0;
+    for (uint32_t i = 0; i < w; ++i) before += wave_tot[i];
+    return before + x - v;
+}
+
+struct ColRegs {
+    uint32_t x[kColRegs];
+    uint32_t len;     // wave-uniform
+    uint64_t start;   // wave-uniform
+};
+
+__device__ __forceinline__ void col_load(ColRegs& c, const uint32_t* __restrict__ dense,
+                                         const uint64_t* __restrict__ dense_off, uint32_t q, uint32_t qend,
+                                         uint32_t lane) {
+    if (q >= qend) {
+        c.len = 0;
+        return;
+    }
+    const uint64_t s = dense_off[q];
+    c.start = s;
+    c.len = (uint32_t)(dense_off[q + 1] - s);
+#pragma unroll
+    for (uint32_t i = 0; i < kColRegs; ++i) {
+        const uint32_t e = lane + 64 * i;
+        c.x[i] = e < c.len ? dense[s + e] : 0u;
+    }
 }
 
 __global__ __launch_bounds__(kPairThreads) void pair_kernel(
-    const uint32_t* __restrict__ set, const uint32_t* __restrict__ set_len,
-    const uint64_t* __restrict__ res_off, const uint16_t* __restrict__ cls,
-    const kmp_work_item* __restrict__ items, uint32_t min_shared, int require_diff,
-    uint32_t* __restrict__ out_p, uint32_t* __restrict__ out_q, uint32_t* __restrict__ out_w, uint64_t cap,
-    unsigned long long* __restrict__ count) {
-    __shared__ __attribute__((aligned(16))) uint32_t keys[kTileSlots];
-    __shared__ uint8_t rows[kTileSlots];
+    const uint32_t* __restrict__ dense, const uint64_t* __restrict__ dense_off, const uint16_t* __restrict__ cls,
+    const kmp_work_item* __restrict__ items, uint32_t min_shared, int require_diff, uint32_t* __restrict__ out_p,
+    uint32_t* __restrict__ out_q, uint32_t* __restrict__ out_w, uint64_t cap, unsigned long long* __restrict__ count) {
+    __shared__ uint64_t bloom[kBloomBlocks];
+    __shared__ uint32_t F[kBuckets + 2];
+    __shared__ uint32_t keys[kTileCap];
+    __shared__ uint8_t rows[kTileCap];
     __shared__ uint32_t cnt[kPairWaves][kRowsMax];
     __shared__ uint8_t touched[kPairWaves][kRowsMax];
     __shared__ uint32_t ntouched[kPairWaves];
     __shared__ uint16_t row_cls[kRowsMax];
+    __shared__ uint32_t row_start[kRowsMax + 1];
+    __shared__ uint32_t wave_tot[kPairWaves];
 
     const kmp_work_item it = items[blockIdx.x];
-    const uint32_t nrows = it.row_end - it.row_beg;
+    const uint32_t r0 = it.row_beg, nrows = it.row_end - it.row_beg;
+    if (nrows == 0) return;  // padding item
     const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    const uint32_t qfirst = max(it.col_beg, r0 + 1);
 
-    uint4* k4 = reinterpret_cast<uint4*>(keys);
-    for (uint32_t i = tid; i < kTileSlots / 4; i += kPairThreads)
-        k4[i] = make_uint4(kEmptyKey, kEmptyKey, kEmptyKey, kEmptyKey);
+    // the first column of this wave is loading while the tile is built
+    ColRegs cur;
+    col_load(cur, dense, dense_off, qfirst + wave, it.col_end, lane);
+
+    for (uint32_t i = tid; i < kBloomBlocks; i += kPairThreads) bloom[i] = 0;
+    for (uint32_t i = tid; i < kBuckets + 2; i += kPairThreads) F[i] = 0;
     for (uint32_t i = tid; i < kPairWaves * kRowsMax; i += kPairThreads) (&cnt[0][0])[i] = 0;
     if (tid < kPairWaves) ntouched[tid] = 0;
-    for (uint32_t r = tid; r < nrows; r += kPairThreads) row_cls[r] = cls[it.row_beg + r];
+    const uint64_t d0 = dense_off[r0];
+    for (uint32_t r = tid; r <= nrows; r += kPairThreads) row_start[r] = (uint32_t)(dense_off[r0 + r] - d0);
+    for (uint32_t r = tid; r < nrows; r += kPairThreads) row_cls[r] = cls[r0 + r];
     __syncthreads();
+    const uint32_t ntile = row_start[nrows];
 
-    // build: one wave per row protein, one k-mer per lane
-    for (uint32_t r = wave; r < nrows; r += kPairWaves) {
-        const uint32_t p = it.row_beg + r;
-        const uint32_t len = set_len[p];
-        const uint32_t* s = set + set_base(res_off[p], p);
-        for (uint32_t e = lane; e < len; e += 64) {
-            const uint32_t x = s[e];
-            uint32_t b = tile_hash(x);
-            for (uint32_t guard = 0; guard < kTileBuckets; ++guard) {
-                bool done = false;
-#pragma unroll
-                for (uint32_t q = 0; q < kBucketSlots; ++q) {
-                    const uint32_t slot = b * kBucketSlots + q;
-                    if (!done && keys[slot] == kEmptyKey && atomicCAS(&keys[slot], kEmptyKey, x) == kEmptyKey) {
-                        rows[slot] = (uint8_t)r;
-                        done = true;
-                    }
-                }
-                if (done) break;
-                b = (b + 1) & (kTileBuckets - 1);
-            }
-        }
+    // row tile -> Bloom blocks + bucket counts (pass 1), bucket scan, scatter (pass 2)
+    for (uint32_t e = tid; e < ntile; e += kPairThreads) {
+        const uint32_t x = dense[d0 + e];
+        const uint32_t b = bloom_block(x);
+        atomicOr(&bloom[b], bloom_bits(x));
+        atomicAdd(&F[b + 2], 1u);
     }
     __syncthreads();
+    {
+        const uint32_t c0 = F[4 * tid + 2], c1 = F[4 * tid + 3], c2 = F[4 * tid + 4], c3 = F[4 * tid + 5];
+        const uint32_t ex = block_scan_1024(c0 + c1 + c2 + c3, wave_tot);
+        __syncthreads();
+        F[4 * tid + 1] = ex;  // F[b+1] = start of bucket b (F[0] = 0)
+        F[4 * tid + 2] = ex + c0;
+        F[4 * tid + 3] = ex + c0 + c1;
+        F[4 * tid + 4] = ex + c0 + c1 + c2;
+    }
+    __syncthreads();
+    for (uint32_t r = wave; r < nrows; r += kPairWaves) {
+        const uint32_t rb = row_start[r], re = row_start[r + 1];
+        for (uint32_t e = rb + lane; e < re; e += 64) {
+            const uint32_t x = dense[d0 + e];
+            const uint32_t pos = atomicAdd(&F[bloom_block(x) + 1], 1u);
+            keys[pos] = x;
+            rows[pos] = (uint8_t)r;
+        }
+    }
+    __syncthreads();  // bucket b = [F[b], F[b+1])
 
-    // probe: one wave per column protein
-    for (uint32_t q = it.col_beg + wave; q < it.col_end; q += kPairWaves) {
-        const uint32_t len = set_len[q];
-        if (len == 0 || q <= it.row_beg) continue;
-        const uint32_t lim = min(q - it.row_beg, nrows);  // rows with p < q
-        const uint32_t* s = set + set_base(res_off[q], q);
-        for (uint32_t c = 0; c < len; c += 64) {
-            const uint32_t e = c + lane;
-            bool act = e < len;
-            const uint32_t x = act ? s[e] : 0u;
-            uint32_t b = tile_hash(x);
-            for (uint32_t guard = 0; __ballot(act) != 0 && guard < kTileBuckets; ++guard) {
-                if (act) {
-                    const uint4 kv = k4[b];
-                    uint32_t hm = (uint32_t)(kv.x == x) | ((uint32_t)(kv.y == x) << 1) |
-                                  ((uint32_t)(kv.z == x) << 2) | ((uint32_t)(kv.w == x) << 3);
-                    while (hm) {
-                        const uint32_t sl = __builtin_ctz(hm);
-                        hm &= hm - 1;
-                        const uint32_t r = rows[b * kBucketSlots + sl];
-                        if (r < lim) {
-                            if (atomicAdd(&cnt[wave][r], 1u) == 0u) {
-                                const uint32_t slot = atomicAdd(&ntouched[wave], 1u);
-                                touched[wave][slot] = (uint8_t)r;
-                            }
-                        }
+    for (uint32_t q = qfirst + wave; q < it.col_end; q += kPairWaves) {
+        ColRegs nxt;
+        col_load(nxt, dense, dense_off, q + kPairWaves, it.col_end, lane);
+        const uint32_t len = cur.len;
+        const uint32_t lim = min(q - r0, nrows);  // rows with p < q
+        for (uint32_t base = 0; base < len; base += 64 * kColRegs) {
+            uint32_t x[kColRegs];
+            if (base == 0) {
+#pragma unroll
+                for (uint32_t i = 0; i < kColRegs; ++i) x[i] = cur.x[i];
+            } else {
+#pragma unroll
+                for (uint32_t i = 0; i < kColRegs; ++i) {
+                    const uint32_t e = base + lane + 64 * i;
+                    x[i] = e < len ? dense[cur.start + e] : 0u;
+                }
+            }
+            uint64_t word[kColRegs], want[kColRegs];
+            uint32_t blk[kColRegs];
+#pragma unroll
+            for (uint32_t i = 0; i < kColRegs; ++i) {
+                blk[i] = bloom_block(x[i]);
+                want[i] = bloom_bits(x[i]);
+                word[i] = bloom[blk[i]];
+            }
+            bool any = false;
+            bool pass[kColRegs];
+#pragma unroll
+            for (uint32_t i = 0; i < kColRegs; ++i) {
+                pass[i] = base + lane + 64 * i < len && (word[i] & want[i]) == want[i];
+                any |= pass[i];
+            }
+            if (__ballot(any) == 0) continue;
+#pragma unroll
+            for (uint32_t i = 0; i < kColRegs; ++i) {
+                if (!pass[i]) continue;
+                const uint32_t be = F[blk[i] + 1];
+                for (uint32_t s = F[blk[i]]; s < be; ++s) {
+                    if (keys[s] != x[i]) continue;
+                    const uint32_t r = rows[s];
+                    if (r < lim && atomicAdd(&cnt[wave][r], 1u) == 0u) {
+                        const uint32_t t = atomicAdd(&ntouched[wave], 1u);
+                        touched[wave][t] = (uint8_t)r;
                     }
-                    act = !((kv.x == kEmptyKey) | (kv.y == kEmptyKey) | (kv.z == kEmptyKey) | (kv.w == kEmptyKey));
-                    b = (b + 1) & (kTileBuckets - 1);
                 }
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         const uint32_t nt = ntouched[wave];
-        const uint16_t cq = cls[q];
-        for (uint32_t t0 = 0; t0 < nt; t0 += 64) {
-            const uint32_t t = t0 + lane;
-            bool ok = false;
-            uint32_t r = 0, wv = 0;
-            if (t < nt) {
-                r = touched[wave][t];
-                wv = cnt[wave][r];
-                cnt[wave][r] = 0;
-                ok = wv >= min_shared && (!require_diff || row_cls[r] != cq);
-            }
-            const uint64_t m = __ballot(ok);
-            if (m) {
-                unsigned long long first = 0;
-                if (lane == 0) first = atomicAdd(count, (unsigned long long)__popcll(m));
-                first = __shfl(first, 0);
-                const unsigned long long pos = first + mask_rank(m);
-                if (ok && pos < cap) {
-                    out_p[pos] = it.row_beg + r;
-                    out_q[pos] = q;
-                    out_w[pos] = wv;
+        if (nt != 0) {
+            const uint16_t cq = cls[q];
+            for (uint32_t t0 = 0; t0 < nt; t0 += 64) {
+                const uint32_t t = t0 + lane;
+                bool ok = false;
+                uint32_t r = 0, wv = 0;
+                if (t < nt) {
+                    r = touched[wave][t];
+                    wv = cnt[wave][r];
+                    cnt[wave][r] = 0;
+                    ok = wv >= min_shared && (!require_diff || row_cls[r] != cq);
+                }
+                const uint64_t m = __ballot(ok);
+                if (m) {
+                    unsigned long long first = 0;
+                    if (lane == 0) first = atomicAdd(count, (unsigned long long)__popcll(m));
+                    first = __shfl(first, 0);
+                    const unsigned long long pos = first + mask_rank(m);
+                    if (ok && pos < cap) {
+                        out_p[pos] = r0 + r;
+                        out_q[pos] = q;
+                        out_w[pos] = wv;
+                    }
                 }
             }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            if (lane == 0) ntouched[wave] = 0;
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if (lane == 0) ntouched[wave] = 0;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        cur = nxt;
     }
 }
 
@@ -495,47 +595,85 @@ void kmp_pair_geometry_get(kmp_pair_geometry* g) {
     g->threads = kPairThreads;
 }
 
-int kmp_plan_pairs(const uint32_t* set_len, uint32_t n, uint64_t chunk_cost, kmp_work_item* items, uint64_t cap,
-                   uint64_t* n_items) {
-    if (!n_items || (n && !set_len) || (cap && !items)) return KMP_EINVAL;
-    if (chunk_cost == 0) chunk_cost = 1;
-    uint64_t m = 0;
-    uint32_t r0 = 0;
-    while (r0 < n) {
-        // row tile [r0, r1): greedy in index order
+int kmp_plan_pairs(const uint32_t* set_len, uint32_t n, uint64_t chunk_cost, uint64_t* dense_off,
+                   kmp_work_item* items, uint64_t cap, uint64_t* n_items) {
+    if (!n_items || !dense_off || (n && !set_len) || (cap && !items)) return KMP_EINVAL;
+    if (chunk_cost == 0) chunk_cost = kChunkCost;
+    dense_off[0] = 0;
+    for (uint32_t p = 0; p < n; ++p) {
+        if (set_len[p] > kTileCap) return KMP_EINVAL;
+        dense_off[p + 1] = dense_off[p] + set_len[p];
+    }
+    // row tiles: greedy in index order; tiles whose sets are all empty make no items
+    std::vector<uint32_t> tb, te;
+    for (uint32_t r0 = 0; r0 < n;) {
         uint32_t r1 = r0;
         uint64_t tot = 0;
         while (r1 < n && r1 - r0 < kRowsMax && tot + set_len[r1] <= kTileCap) tot += set_len[r1++];
-        if (r1 == r0) return KMP_EINVAL;  // a single set longer than the tile capacity
         if (tot > 0 && r0 + 1 < n) {
-            // columns [r0+1, n) cut by cost; empty rows-only tiles produce no items
-            uint32_t c0 = r0 + 1;
-            while (c0 < n) {
-                uint32_t c1 = c0;
-                uint64_t cost = 0;
-                while (c1 < n && (cost < chunk_cost || c1 == c0)) cost += set_len[c1++] + 1;
-                if (m < cap) items[m] = kmp_work_item{r0, r1, c0, c1};
-                ++m;
-                c0 = c1;
-            }
+            tb.push_back(r0);
+            te.push_back(r1);
         }
         r0 = r1;
+    }
+    // column chunks (cost counts one per protein so empty runs still split); chunk-major items
+    uint64_t m = 0;
+    for (uint32_t c0 = 0; c0 < n;) {
+        uint32_t c1 = c0;
+        uint64_t cost = 0;
+        while (c1 < n && (cost < chunk_cost || c1 == c0)) cost += set_len[c1++] + 1;
+        for (size_t t = 0; t < tb.size() && tb[t] + 1 < c1; ++t) {
+            if (m < cap) items[m] = kmp_work_item{tb[t], te[t], c0, c1};
+            ++m;
+        }
+        c0 = c1;
     }
     *n_items = m;
     return m > cap ? KMP_EOVERFLOW : KMP_OK;
 }
 
-int kmp_dev_pairs(const uint32_t* d_set, const uint32_t* d_set_len, const uint64_t* d_res_off,
-                  const uint16_t* d_class, uint32_t n, const kmp_work_item* d_items, uint64_t n_items,
-                  uint32_t min_shared, int require_class_diff, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w,
-                  uint64_t cap, unsigned long long* d_count, void* stream) {
+int kmp_order_items_xcd(const kmp_work_item* in, uint64_t n, kmp_work_item* out, uint64_t cap, uint64_t* n_out) {
+    if (!n_out || (n && !in) || (cap && !out)) return KMP_EINVAL;
+    constexpr uint32_t kXcds = 8;
+    // consecutive items of one chunk share col_beg; chunk g -> XCD list g % 8
+    std::vector<std::vector<kmp_work_item>> lists(kXcds);
+    uint64_t g = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (i > 0 && in[i].col_beg != in[i - 1].col_beg) ++g;
+        lists[g % kXcds].push_back(in[i]);
+    }
+    size_t longest = 0;
+    for (auto& l : lists) longest = std::max(longest, l.size());
+    // slot 8*s + x <- lists[x][s]; a short list is padded with empty items (no-ops)
+    const uint64_t m = (uint64_t)longest * kXcds;
+    *n_out = m;
+    if (m > cap) return KMP_EOVERFLOW;
+    for (size_t s = 0; s < longest; ++s)
+        for (uint32_t x = 0; x < kXcds; ++x)
+            out[s * kXcds + x] = s < lists[x].size() ? lists[x][s] : kmp_work_item{0, 0, 0, 0};
+    return KMP_OK;
+}
+
+int kmp_dev_pack_dense(const uint32_t* d_rep, const uint64_t* d_res_off, const uint64_t* d_dense_off, uint32_t n,
+                       uint32_t* d_dense, void* stream) {
+    if (n == 0) return KMP_OK;
+    if (!d_rep || !d_res_off || !d_dense_off || !d_dense) return KMP_EINVAL;
+    pack_dense_kernel<<<n, 256, 0, as_stream(stream)>>>(d_rep, d_res_off, d_dense_off, d_dense);
+    return hip_status(hipGetLastError());
+}
+
+int kmp_dev_pairs(const uint32_t* d_dense, const uint64_t* d_dense_off, const uint16_t* d_class, uint32_t n,
+                  const kmp_work_item* d_items, uint64_t n_items, uint32_t min_shared, int require_class_diff,
+                  uint32_t* d_p, uint32_t* d_q, uint32_t* d_w, uint64_t cap, unsigned long long* d_count,
+                  void* stream) {
+    (void)n;
     if (n_items == 0) return KMP_OK;
-    if (!d_set || !d_set_len || !d_res_off || !d_class || !d_items || !d_count || (cap && (!d_p || !d_q || !d_w)))
+    if (!d_dense || !d_dense_off || !d_class || !d_items || !d_count || (cap && (!d_p || !d_q || !d_w)))
         return KMP_EINVAL;
     if (n_items > 0x7FFFFFFFull) return KMP_EINVAL;
     if (min_shared < 1) min_shared = 1;
     pair_kernel<<<(uint32_t)n_items, kPairThreads, 0, as_stream(stream)>>>(
-        d_set, d_set_len, d_res_off, d_class, d_items, min_shared, require_class_diff, d_p, d_q, d_w, cap, d_count);
+        d_dense, d_dense_off, d_class, d_items, min_shared, require_class_diff, d_p, d_q, d_w, cap, d_count);
     return hip_status(hipGetLastError());
 }
 

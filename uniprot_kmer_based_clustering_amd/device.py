@@ -6,7 +6,7 @@ on one GPU and runs the reference's hot path as stages:
 
   build_sets   Protein::new + per-protein sort/dedup      (protein.rs:107-132, main.rs:280-282)
   filter       remove_unique_five_mers (df >= 2)           (protein.rs:151-162, main.rs:127-149)
-  plan         row tiles x column chunks of the N x N upper triangle (host, from set sizes)
+  plan         dense CSR of the filtered sets, column blocks, row tiles (host, from set sizes)
   pairs        Graph::new + remove_uninteresting_edges + combine_edges (graph/mod.rs)
   sort         canonical (p, q) order
 
@@ -24,7 +24,11 @@ from . import _lib
 from ._lib import check, lib
 from .engine import Proteins
 
-CHUNK_COST = 65536  # set entries streamed per work item (column side)
+CHUNK_COST = 0  # column k-mers per work item (0: the library default, one L2-shared chunk)
+
+
+def _np(a: np.ndarray):
+    return None if a.size == 0 else C.c_void_p(a.ctypes.data)
 
 
 def _p(t: torch.Tensor | None):
@@ -35,34 +39,53 @@ def _stream() -> C.c_void_p:
     return C.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
-def plan_pairs(set_len: np.ndarray, chunk_cost: int = CHUNK_COST) -> np.ndarray:
-    """Host planner (kmp_plan_pairs) -> structured array of work items."""
+class Plan:
+    """Host plan of the pair kernel (kmp_plan_pairs): dense CSR offsets of the filtered sets
+    and the chunk-major work items (row tile x column chunk)."""
+
+    def __init__(self, set_len: np.ndarray, chunk_cost: int = CHUNK_COST):
+        L = lib()
+        lens = np.ascontiguousarray(set_len, dtype=np.uint32)
+        n = len(lens)
+        self.dense_off = np.zeros(n + 1, dtype=np.uint64)
+        ni = C.c_uint64()
+        st = L.kmp_plan_pairs(_np(lens), n, chunk_cost, _np(self.dense_off), None, 0, C.byref(ni))
+        if st not in (_lib.KMP_OK, _lib.KMP_EOVERFLOW):
+            check(st, "kmp_plan_pairs")
+        items = np.zeros((max(1, ni.value), 4), dtype=np.uint32)
+        check(L.kmp_plan_pairs(_np(lens), n, chunk_cost, _np(self.dense_off), _np(items), ni.value,
+                               C.byref(ni)), "kmp_plan_pairs")
+        self.items = items[:ni.value]
+        self.set_len = lens
+
+    def item_costs(self) -> np.ndarray:
+        """Estimated cost per item: column k-mers streamed + row k-mers inserted + a fixed
+        per-item start-up."""
+        if len(self.items) == 0:
+            return np.zeros(0)
+        d = self.dense_off.astype(np.int64)
+        it = self.items.astype(np.int64)
+        return (d[it[:, 3]] - d[np.maximum(it[:, 2], it[:, 0] + 1)]) + (d[it[:, 1]] - d[it[:, 0]]) + 4096
+
+    def share(self, rank: int, world: int) -> np.ndarray:
+        """Contiguous, cost-balanced share of the chunk-major items for `rank` of `world`."""
+        if world <= 1 or len(self.items) == 0:
+            return self.items if rank == 0 else self.items[:0]
+        cum = np.cumsum(self.item_costs())
+        cuts = np.searchsorted(cum, cum[-1] * np.arange(1, world) / world)
+        return np.split(self.items, cuts)[rank]
+
+
+def order_xcd(items: np.ndarray) -> np.ndarray:
+    """XCD-aware launch order (kmp_order_items_xcd); may add empty padding items."""
     L = lib()
-    lens = np.ascontiguousarray(set_len, dtype=np.uint32)
+    items = np.ascontiguousarray(items, dtype=np.uint32).reshape(-1, 4)
     n = C.c_uint64()
-    st = L.kmp_plan_pairs(_np(lens), len(lens), chunk_cost, None, 0, C.byref(n))
-    if st not in (_lib.KMP_OK, _lib.KMP_EOVERFLOW):
-        check(st, "kmp_plan_pairs")
-    items = np.zeros((max(1, n.value), 4), dtype=np.uint32)
-    check(L.kmp_plan_pairs(_np(lens), len(lens), chunk_cost, _np(items), n.value, C.byref(n)),
-          "kmp_plan_pairs")
-    return items[:n.value]
-
-
-def _np(a: np.ndarray):
-    return None if a.size == 0 else C.c_void_p(a.ctypes.data)
-
-
-def split_items(items: np.ndarray, set_len: np.ndarray, world: int) -> list:
-    """Cut the (tile, chunk)-ordered item list into `world` contiguous shares of equal
-    estimated cost (column entries probed + row entries inserted per item)."""
-    if world <= 1 or len(items) == 0:
-        return [items] + [items[:0]] * (world - 1)
-    csum = np.concatenate([[0], np.cumsum(set_len.astype(np.int64))])
-    cost = (csum[items[:, 3]] - csum[items[:, 2]]) + (csum[items[:, 1]] - csum[items[:, 0]]) + 1024
-    cum = np.cumsum(cost)
-    cuts = np.searchsorted(cum, cum[-1] * np.arange(1, world) / world)
-    return np.split(items, cuts)
+    L.kmp_order_items_xcd(_np(items), len(items), None, 0, C.byref(n))
+    out = np.zeros((max(1, n.value), 4), dtype=np.uint32)
+    check(L.kmp_order_items_xcd(_np(items), len(items), _np(out), n.value, C.byref(n)),
+          "kmp_order_items_xcd")
+    return out[:n.value]
 
 
 class DevicePipeline:
@@ -94,6 +117,9 @@ class DevicePipeline:
         self.count = torch.zeros(1, dtype=torch.int64, device=dev)
         self.items = None
         self.n_items = 0
+        self.dense = None
+        self.plan_host = None
+        self._sort_tmp = None
 
     def _alloc_edges(self, cap):
         self.edge_cap = cap
@@ -108,33 +134,40 @@ class DevicePipeline:
         if hi <= lo:
             return
         check(lib().kmp_dev_build_sets(_p(self.res), C.c_void_p(self.off.data_ptr() + 8 * lo), hi - lo, self.k,
-                                       self.max_len, _sub(self.set, self, lo), _p(self.set_len[lo:]),
-                                       _sub(self.scratch, self, lo) if self.scratch is not None else None,
-                                       _stream()), "kmp_dev_build_sets")
+                                       self.max_len, _sub(self.set, lo), _p(self.set_len[lo:]),
+                                       _sub(self.scratch, lo), _stream()), "kmp_dev_build_sets")
 
     def filter(self) -> None:
         check(lib().kmp_dev_filter_repeats(_p(self.set), _p(self.set_len), _p(self.off), self.n, self.k,
                                            _p(self.bits), _p(self.rep), _p(self.rep_len), _stream()),
               "kmp_dev_filter_repeats")
 
-    def plan(self, rank: int = 0, world: int = 1, chunk_cost: int = CHUNK_COST) -> np.ndarray:
+    def plan(self, rank: int = 0, world: int = 1, chunk_cost: int = CHUNK_COST) -> Plan:
+        """Host plan from the filtered set sizes (one D2H of N u32), then the dense CSR pack."""
         rep_len = self.rep_len[:self.n].cpu().numpy().view(np.uint32)
-        items = plan_pairs(rep_len, chunk_cost)
-        mine = split_items(items, rep_len, world)[rank]
+        plan = Plan(rep_len, chunk_cost)
+        mine = order_xcd(plan.share(rank, world))
+        dev = self.dev
+        self.dense_off = torch.from_numpy(plan.dense_off.view(np.int64)).to(dev)
         self.n_items = len(mine)
-        self.items = torch.from_numpy(np.ascontiguousarray(mine).view(np.int32).reshape(-1)).to(self.dev) \
-            if len(mine) else None
+        self.items = (torch.from_numpy(np.ascontiguousarray(mine).view(np.int32).reshape(-1)).to(dev)
+                      if len(mine) else None)
+        total = int(plan.dense_off[-1])
+        if self.dense is None or self.dense.numel() < max(1, total):
+            self.dense = torch.empty(max(1, total), dtype=torch.int32, device=dev)
+        check(lib().kmp_dev_pack_dense(_p(self.rep), _p(self.off), _p(self.dense_off), self.n, _p(self.dense),
+                                       _stream()), "kmp_dev_pack_dense")
+        self.plan_host = plan
         self.rep_len_host = rep_len
-        return mine
+        return plan
 
     def pairs(self, min_shared: int = 1, require_class_diff: bool = True) -> int:
         """Runs the pair kernel over the planned items; returns the edge count (syncs)."""
         for _ in range(2):
             self.count.zero_()
-            check(lib().kmp_dev_pairs(_p(self.rep), _p(self.rep_len), _p(self.off), _p(self.cls), self.n,
-                                      _p(self.items), self.n_items, min_shared, int(require_class_diff),
-                                      _p(self.ep), _p(self.eq), _p(self.ew), self.edge_cap, _p(self.count),
-                                      _stream()), "kmp_dev_pairs")
+            check(lib().kmp_dev_pairs(_p(self.dense), _p(self.dense_off), _p(self.cls), self.n, _p(self.items),
+                                      self.n_items, min_shared, int(require_class_diff), _p(self.ep), _p(self.eq),
+                                      _p(self.ew), self.edge_cap, _p(self.count), _stream()), "kmp_dev_pairs")
             cnt = int(self.count.item())
             if cnt <= self.edge_cap:
                 self.n_edges = cnt
@@ -148,7 +181,7 @@ class DevicePipeline:
             return
         L = lib()
         nbytes = int(L.kmp_dev_sort_edges_tmp_bytes(n, self.n))
-        if getattr(self, "_sort_tmp", None) is None or self._sort_tmp.numel() < nbytes:
+        if self._sort_tmp is None or self._sort_tmp.numel() < nbytes:
             self._sort_tmp = torch.empty(nbytes + 256, dtype=torch.uint8, device=self.dev)
         check(L.kmp_dev_sort_edges(_p(self.ep), _p(self.eq), _p(self.ew), n, self.n, _p(self._sort_tmp),
                                    self._sort_tmp.numel(), _stream()), "kmp_dev_sort_edges")
@@ -174,15 +207,11 @@ class DevicePipeline:
         return buf[base:base + m].cpu().numpy().view(np.uint32)
 
 
-def _sub(t: torch.Tensor | None, pipe: DevicePipeline, lo: int):
-    """Device pointer for a stage launched on proteins [lo, ...): the per-protein slot math
-    uses absolute protein indices, so a slice launch passes the base shifted back by the
-    slot origin of protein lo (kmp_set_base is affine in p: +4 per protein)."""
+def _sub(t: torch.Tensor | None, lo: int):
+    """Device pointer of a per-protein slot buffer for a stage launched on proteins [lo, ...).
+    The kernels compute slot(off[p], p_rel) with p_rel = p - lo; since kmp_set_base is
+    round_up(off + 4p, 4) and 4*lo is a multiple of 4, slot(off, p_rel) = slot(off, p) - 4*lo,
+    so the buffer pointer moves forward by 4*lo elements."""
     if t is None:
         return None
-    if lo == 0:
-        return C.c_void_p(t.data_ptr())
-    # slot(p_abs) = base(off[p_abs], p_abs); the slice kernel computes base(off[p_abs], p_rel)
-    # = slot(p_abs) - 4*lo (up to the round-up, which is identical since 4*lo is a multiple
-    # of 4), so shift the pointer forward by 4*lo elements.
     return C.c_void_p(t.data_ptr() + 4 * 4 * lo)

@@ -90,7 +90,6 @@ def distributed_step(pipe, rank: int, world: int, group=None, min_shared: int = 
                      require_class_diff: bool = True, timers: dict | None = None) -> int:
     """One multi-GPU pass of the path on a DevicePipeline holding the whole batch.
     Returns the canonical edge count (rank 0) or this rank's share (others)."""
-    from .device import plan_pairs  # noqa: F401  (planner shared with the 1-GPU path)
     slices = protein_slices(pipe.offsets_host, world)
     lo, hi = slices[rank]
     pipe.build_sets(lo, hi)
