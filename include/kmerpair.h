@@ -196,6 +196,15 @@ int kmp_dev_pairs(const uint32_t* d_dense, const uint64_t* d_dense_off, const ui
                   uint32_t* d_p, uint32_t* d_q, uint32_t* d_w, uint64_t cap, unsigned long long* d_count,
                   void* stream);
 
+/* Pairs of the proteins whose repeat-filtered set is longer than the tile capacity
+ * (kmp_pair_geometry.tile_cap): those are planned with length 0 (kmp_plan_pairs never sees
+ * them) and counted here against every other protein, from the slot layout of d_rep.  Same
+ * output contract as kmp_dev_pairs (shares d_count).  d_long_ids: the long proteins' indices. */
+int kmp_dev_pairs_long(const uint32_t* d_rep, const uint32_t* d_rep_len, const uint64_t* d_res_off,
+                       const uint16_t* d_class, uint32_t n, const uint32_t* d_long_ids, uint32_t n_long,
+                       uint32_t min_shared, int require_class_diff, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w,
+                       uint64_t cap, unsigned long long* d_count, void* stream);
+
 /* Canonical order: sorts n edges by (p, q).  Keys/values are read from d_p/d_q/d_w and the
  * sorted result is written back to them.  d_tmp: kmp_dev_sort_edges_tmp_bytes(n, N) bytes. */
 uint64_t kmp_dev_sort_edges_tmp_bytes(uint64_t n, uint32_t n_proteins);

@@ -1,0 +1,117 @@
+"""The multi-GPU split (uniprot_kmer_based_clustering_amd/dist.py) on CPU: world_size 2 and 3
+over gloo.  Every rank contributes its protein slice of the set buffer and its share of the
+pair items; the test checks that the all-gathered sets equal the single-process sets and
+that the edges gathered to rank 0 (each rank's edges = the oracle's edges restricted to the
+rank's items) re-sort into exactly the single-process edge list — i.e. the result is
+invariant to the number of ranks.  The pair kernel itself needs a GPU (tests/test_gpu_*)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from common import ROOT, slice_proteins, uniprot
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def build_case():
+    import uniprot_kmer_based_clustering_amd as K
+    from oracle.oracle import Oracle
+    b = K.synth(3000, 21)
+    o = Oracle(b.residues, b.offsets, b.class_id, k=7, threads=2)
+    return b, o
+
+
+def worker(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, ROOT)
+        from uniprot_kmer_based_clustering_amd import _lib
+        from uniprot_kmer_based_clustering_amd.device import Plan
+        from uniprot_kmer_based_clustering_amd.dist import (allgather_sets, gather_edges, protein_slices,
+                                                            slot_range)
+        b, o = build_case()
+        n = b.n
+        L = _lib.lib()
+        so, sv = o.sets()
+        cap = int(L.kmp_set_capacity(n, int(b.offsets[-1])))
+        full = np.full(cap, -1, dtype=np.int32)
+        lens = np.diff(so).astype(np.int32)
+        for p in range(n):
+            base = int(L.kmp_set_base(int(b.offsets[p]), p))
+            full[base:base + lens[p]] = sv[so[p]:so[p + 1]].view(np.int32)
+        slices = protein_slices(b.offsets, world)
+        lo, hi = slices[rank]
+        # this rank only holds its slice (the rest is garbage before the all-gather)
+        buf = torch.full((cap,), -7, dtype=torch.int32)
+        sl_lo, sl_hi = slot_range(b.offsets, lo, hi)
+        buf[sl_lo:sl_hi] = torch.from_numpy(full[sl_lo:sl_hi])
+        ln = torch.full((n,), -3, dtype=torch.int32)
+        ln[lo:hi] = torch.from_numpy(lens[lo:hi])
+        allgather_sets(buf, ln, b.offsets, slices, rank)
+        ok_sets = bool(torch.equal(ln, torch.from_numpy(lens)))
+        for p in range(n):
+            base = int(L.kmp_set_base(int(b.offsets[p]), p))
+            ok_sets &= bool(torch.equal(buf[base:base + lens[p]], torch.from_numpy(full[base:base + lens[p]])))
+
+        # pair share: the oracle's edges restricted to this rank's items (repeat-filtered sizes)
+        rc, _ = o.repeat()
+        rep_len = np.array([np.isin(sv[so[p]:so[p + 1]], rc).sum() for p in range(n)], dtype=np.uint32)
+        mine = Plan(rep_len, 20000).share(rank, world)
+        P, Q, W = o.pairs()
+        keep = np.zeros(len(P), dtype=bool)
+        for r0, r1, c0, c1 in mine.astype(np.int64):
+            keep |= (P >= r0) & (P < r1) & (Q >= c0) & (Q < c1) & (Q > P)
+        ep = torch.from_numpy(P[keep].view(np.int32).copy())
+        eq = torch.from_numpy(Q[keep].view(np.int32).copy())
+        ew = torch.from_numpy(W[keep].view(np.int32).copy())
+        got = gather_edges(ep, eq, ew, int(keep.sum()), rank)
+        if rank == 0:
+            gp, gq, gw = (t.numpy().view(np.uint32) for t in got)
+            order = np.lexsort((gq, gp))
+            ok_edges = (np.array_equal(gp[order], P) and np.array_equal(gq[order], Q)
+                        and np.array_equal(gw[order], W))
+            out_q.put(("edges", ok_edges, len(P), int(keep.sum())))
+        out_q.put(("sets", rank, ok_sets))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_distributed_split_is_invariant(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    msgs = [q.get(timeout=10) for _ in range(world + 1)]
+    sets = [m for m in msgs if m[0] == "sets"]
+    edges = [m for m in msgs if m[0] == "edges"]
+    assert len(sets) == world and all(m[2] for m in sets), sets
+    assert len(edges) == 1 and edges[0][1], edges
+    assert edges[0][2] > 100
+
+
+def test_protein_slices_balance():
+    from uniprot_kmer_based_clustering_amd.dist import protein_slices
+    res, off, cls, _ = uniprot()
+    for world in (1, 2, 4, 8):
+        sl = protein_slices(off, world)
+        assert sl[0][0] == 0 and sl[-1][1] == len(off) - 1
+        assert all(sl[i][1] == sl[i + 1][0] for i in range(world - 1))
+        sizes = [int(off[h]) - int(off[l]) for l, h in sl]
+        assert max(sizes) - min(sizes) <= 2 * int(np.diff(off).max())

@@ -134,19 +134,31 @@ def test_config3_full_size_bit_exact(engine, oracle_mod):
 
 
 def test_long_proteins_global_sort_path(engine, oracle_mod):
+    """Windows > KMP_LDS_SORT_MAX (global-memory sort) and repeat-filtered sets > the tile
+    capacity (long-protein pair kernel), mixed with ordinary proteins."""
     rng = np.random.default_rng(7)
     alpha = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", dtype=np.uint8)
-    base = alpha[rng.integers(0, 20, 9000)].tobytes()
-    seqs = [base, base[1000:6500], base[:3000] + bytes(alpha[rng.integers(0, 20, 5000)]), b"MK" * 2500,
-            base[4000:4300]]
-    res, off, cls = make_batch(seqs, ["a", "b", "c", "d", "a"])
-    o = oracle_mod.Oracle(res, off, cls, k=5)
-    engine.load(batch(res, off, cls))
+    rnd = lambda m: alpha[rng.integers(0, 20, m)].tobytes()  # noqa: E731
+    base = rnd(21000)
+    other = rnd(6000)
+    seqs = [base[:300], base, rnd(500), base[2000:19500], other + base[5000:8000], b"MK" * 2500,
+            base[4000:4300], other[:4000] + rnd(9000), base[:17500], rnd(200) + other[100:400]]
+    cls = ["a", "b", "c", "d", "a", "b", "c", "d", "a", "b"]
+    res, off, cl = make_batch(seqs, cls)
+    o = oracle_mod.Oracle(res, off, cl, k=5)
+    engine.load(batch(res, off, cl))
     engine.build_sets(5)
     so, sv = o.sets()
     for p in range(len(seqs)):
         np.testing.assert_array_equal(engine.get_set(p), sv[so[p]:so[p + 1]])
-    assert_edges(engine.pairs(require_class_diff=False), *o.pairs(require_class_diff=False))
+    rc, _ = o.repeat()
+    rep_len = [int(np.isin(sv[so[p]:so[p + 1]], rc).sum()) for p in range(len(seqs))]
+    assert sum(r > K._lib.geometry().tile_cap for r in rep_len) >= 2  # the long path really runs
+    for diff in (False, True):
+        assert_edges(engine.pairs(require_class_diff=diff), *o.pairs(require_class_diff=diff))
+    for ms in (1, 50, 3000):
+        assert_edges(engine.pairs(min_shared=ms, require_class_diff=False),
+                     *o.pairs(min_shared=ms, require_class_diff=False))
 
 
 def test_edge_cases(engine, oracle_mod):

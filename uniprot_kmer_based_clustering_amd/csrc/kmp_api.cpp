@@ -68,7 +68,7 @@ struct kmp_ctx {
     std::vector<uint32_t> h_set_len, h_rep_len;
     kmp_counters counters{};
 
-    DevBuf items, dense_off, dense, ep, eq, ew, ecount, sort_tmp;
+    DevBuf items, dense_off, dense, long_ids, ep, eq, ew, ecount, sort_tmp;
     uint64_t edge_cap = 0;
 };
 
@@ -326,13 +326,21 @@ int kmp_pairs(kmp_ctx* c, const kmp_pair_opts* opts, kmp_edges** out) {
     KMP_TRY(c, use_device(c));
 
     // plan (host): dense CSR offsets, row tiles x column chunks, XCD-aware launch order
+    // sets longer than a row tile take the long-protein kernel; they are planned with length 0
+    std::vector<uint32_t> plan_len(c->h_rep_len);
+    std::vector<uint32_t> long_ids;
+    for (uint32_t p = 0; p < c->n; ++p)
+        if (plan_len[p] > kTileCap) {
+            long_ids.push_back(p);
+            plan_len[p] = 0;
+        }
     std::vector<uint64_t> dense_off(c->n + 1);
     uint64_t n_plan = 0, n_items = 0;
-    int st = kmp_plan_pairs(c->h_rep_len.data(), c->n, 0, dense_off.data(), nullptr, 0, &n_plan);
+    int st = kmp_plan_pairs(plan_len.data(), c->n, 0, dense_off.data(), nullptr, 0, &n_plan);
     if (st != KMP_OK && st != KMP_EOVERFLOW)
         return fail(c, st, "planner: a repeat-filtered set exceeds %u k-mers", kTileCap);
     std::vector<kmp_work_item> plan(n_plan);
-    KMP_TRY(c, kmp_plan_pairs(c->h_rep_len.data(), c->n, 0, dense_off.data(), plan.data(), n_plan, &n_plan));
+    KMP_TRY(c, kmp_plan_pairs(plan_len.data(), c->n, 0, dense_off.data(), plan.data(), n_plan, &n_plan));
     kmp_order_items_xcd(plan.data(), n_plan, nullptr, 0, &n_items);
     std::vector<kmp_work_item> items(n_items);
     KMP_TRY(c, kmp_order_items_xcd(plan.data(), n_plan, items.data(), n_items, &n_items));
@@ -344,6 +352,10 @@ int kmp_pairs(kmp_ctx* c, const kmp_pair_opts* opts, kmp_edges** out) {
     if (n_items)
         KMP_HIP(c, hipMemcpyAsync(c->items.p, items.data(), n_items * sizeof(kmp_work_item), hipMemcpyHostToDevice,
                                   c->stream));
+    KMP_HIP(c, c->long_ids.reserve(std::max<size_t>(1, long_ids.size()) * sizeof(uint32_t)));
+    if (!long_ids.empty())
+        KMP_HIP(c, hipMemcpyAsync(c->long_ids.p, long_ids.data(), long_ids.size() * sizeof(uint32_t),
+                                  hipMemcpyHostToDevice, c->stream));
     KMP_TRY(c, kmp_dev_pack_dense(c->rep.as<uint32_t>(), c->off.as<uint64_t>(), c->dense_off.as<uint64_t>(), c->n,
                                   c->dense.as<uint32_t>(), c->stream));
     if (c->edge_cap == 0) c->edge_cap = std::max<uint64_t>(1u << 20, 4ull * c->n);
@@ -357,6 +369,11 @@ int kmp_pairs(kmp_ctx* c, const kmp_pair_opts* opts, kmp_edges** out) {
         KMP_TRY(c, kmp_dev_pairs(c->dense.as<uint32_t>(), c->dense_off.as<uint64_t>(), c->cls.as<uint16_t>(), c->n,
                                  c->items.as<kmp_work_item>(), n_items, o.min_shared, o.require_class_diff, c->ep.as<uint32_t>(), c->eq.as<uint32_t>(),
                                  c->ew.as<uint32_t>(), c->edge_cap, c->ecount.as<unsigned long long>(), c->stream));
+        KMP_TRY(c, kmp_dev_pairs_long(c->rep.as<uint32_t>(), c->rep_len.as<uint32_t>(), c->off.as<uint64_t>(),
+                                      c->cls.as<uint16_t>(), c->n, c->long_ids.as<uint32_t>(),
+                                      (uint32_t)long_ids.size(), o.min_shared, o.require_class_diff,
+                                      c->ep.as<uint32_t>(), c->eq.as<uint32_t>(), c->ew.as<uint32_t>(), c->edge_cap,
+                                      c->ecount.as<unsigned long long>(), c->stream));
         KMP_HIP(c, hipMemcpyAsync(&count, c->ecount.p, sizeof count, hipMemcpyDeviceToHost, c->stream));
         KMP_HIP(c, hipStreamSynchronize(c->stream));
         if (count <= c->edge_cap) break;

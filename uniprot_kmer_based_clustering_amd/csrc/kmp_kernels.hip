@@ -494,6 +494,54 @@ __global__ __launch_bounds__(kPairThreads) void pair_kernel(
 }
 
 // ------------------------------------------------------------------------------------
+// Long proteins: a repeat-filtered set longer than the tile capacity never enters a row tile
+// or a column stream (its planned length is 0).  Its pairs are counted here instead: one
+// workgroup per (long protein p, chunk of column proteins), one wave per column q at a time;
+// each lane binary-searches q's k-mers in K(p) (sorted, L2-resident) and the wave reduces the
+// hits.  Pairs of two long proteins are counted once, from the smaller index.
+constexpr uint32_t kLongPairThreads = 256;
+constexpr uint32_t kLongCols = 2048;  // column proteins per workgroup
+
+__global__ __launch_bounds__(kLongPairThreads) void pair_long_kernel(
+    const uint32_t* __restrict__ rep, const uint32_t* __restrict__ rep_len, const uint64_t* __restrict__ res_off,
+    const uint16_t* __restrict__ cls, const uint32_t* __restrict__ long_ids, uint32_t tile_cap, uint32_t n,
+    uint32_t min_shared, int require_diff, uint32_t* __restrict__ out_p, uint32_t* __restrict__ out_q,
+    uint32_t* __restrict__ out_w, uint64_t cap, unsigned long long* __restrict__ count) {
+    const uint32_t p = long_ids[blockIdx.y];
+    const uint32_t lp = rep_len[p];
+    const uint32_t* A = rep + set_base(res_off[p], p);
+    const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+    const uint32_t q0 = blockIdx.x * kLongCols, q1 = min(n, q0 + kLongCols);
+    const uint16_t cp = cls[p];
+    for (uint32_t q = q0 + wave; q < q1; q += kLongPairThreads / 64) {
+        const uint32_t lq = rep_len[q];
+        if (q == p || lq == 0 || (lq > tile_cap && q < p)) continue;
+        const uint32_t* B = rep + set_base(res_off[q], q);
+        uint32_t hits = 0;
+        for (uint32_t e = lane; e < lq; e += 64) {
+            const uint32_t x = B[e];
+            uint32_t lo = 0, hi = lp;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (A[mid] < x) lo = mid + 1; else hi = mid;
+            }
+            hits += (lo < lp && A[lo] == x);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) hits += __shfl_xor(hits, o);
+        const bool ok = hits >= min_shared && (!require_diff || cls[q] != cp);
+        if (ok && lane == 0) {
+            const unsigned long long pos = atomicAdd(count, 1ull);
+            if (pos < cap) {
+                out_p[pos] = min(p, q);
+                out_q[pos] = max(p, q);
+                out_w[pos] = hits;
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
 __global__ void pack_edges_kernel(const uint32_t* __restrict__ p, const uint32_t* __restrict__ q, uint64_t n,
                                   uint64_t np, unsigned long long* __restrict__ key) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
@@ -674,6 +722,22 @@ int kmp_dev_pairs(const uint32_t* d_dense, const uint64_t* d_dense_off, const ui
     if (min_shared < 1) min_shared = 1;
     pair_kernel<<<(uint32_t)n_items, kPairThreads, 0, as_stream(stream)>>>(
         d_dense, d_dense_off, d_class, d_items, min_shared, require_class_diff, d_p, d_q, d_w, cap, d_count);
+    return hip_status(hipGetLastError());
+}
+
+int kmp_dev_pairs_long(const uint32_t* d_rep, const uint32_t* d_rep_len, const uint64_t* d_res_off,
+                       const uint16_t* d_class, uint32_t n, const uint32_t* d_long_ids, uint32_t n_long,
+                       uint32_t min_shared, int require_class_diff, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w,
+                       uint64_t cap, unsigned long long* d_count, void* stream) {
+    if (n_long == 0 || n == 0) return KMP_OK;
+    if (!d_rep || !d_rep_len || !d_res_off || !d_class || !d_long_ids || !d_count || (cap && (!d_p || !d_q || !d_w)))
+        return KMP_EINVAL;
+    if (n_long > 65535) return KMP_EINVAL;
+    if (min_shared < 1) min_shared = 1;
+    const dim3 grid((n + kLongCols - 1) / kLongCols, n_long);
+    pair_long_kernel<<<grid, kLongPairThreads, 0, as_stream(stream)>>>(d_rep, d_rep_len, d_res_off, d_class, d_long_ids,
+                                                                      kTileCap, n, min_shared, require_class_diff,
+                                                                      d_p, d_q, d_w, cap, d_count);
     return hip_status(hipGetLastError());
 }
 

@@ -120,6 +120,9 @@ class DevicePipeline:
         self.dense = None
         self.plan_host = None
         self._sort_tmp = None
+        self.n_long = 0
+        self.long_ids = None
+        self.long_rank = None
 
     def _alloc_edges(self, cap):
         self.edge_cap = cap
@@ -145,8 +148,12 @@ class DevicePipeline:
     def plan(self, rank: int = 0, world: int = 1, chunk_cost: int = CHUNK_COST) -> Plan:
         """Host plan from the filtered set sizes (one D2H of N u32), then the dense CSR pack."""
         rep_len = self.rep_len[:self.n].cpu().numpy().view(np.uint32)
-        plan = Plan(rep_len, chunk_cost)
+        tile_cap = _lib.geometry().tile_cap
+        long_ids = np.flatnonzero(rep_len > tile_cap).astype(np.uint32)
+        plan_len = np.where(rep_len > tile_cap, 0, rep_len).astype(np.uint32)
+        plan = Plan(plan_len, chunk_cost)
         mine = order_xcd(plan.share(rank, world))
+        self.long_rank = rank == world - 1  # the (rare) long-protein pairs run on one rank
         dev = self.dev
         self.dense_off = torch.from_numpy(plan.dense_off.view(np.int64)).to(dev)
         self.n_items = len(mine)
@@ -157,6 +164,8 @@ class DevicePipeline:
             self.dense = torch.empty(max(1, total), dtype=torch.int32, device=dev)
         check(lib().kmp_dev_pack_dense(_p(self.rep), _p(self.off), _p(self.dense_off), self.n, _p(self.dense),
                                        _stream()), "kmp_dev_pack_dense")
+        self.long_ids = torch.from_numpy(long_ids.view(np.int32)).to(dev) if len(long_ids) else None
+        self.n_long = len(long_ids)
         self.plan_host = plan
         self.rep_len_host = rep_len
         return plan
@@ -168,6 +177,11 @@ class DevicePipeline:
             check(lib().kmp_dev_pairs(_p(self.dense), _p(self.dense_off), _p(self.cls), self.n, _p(self.items),
                                       self.n_items, min_shared, int(require_class_diff), _p(self.ep), _p(self.eq),
                                       _p(self.ew), self.edge_cap, _p(self.count), _stream()), "kmp_dev_pairs")
+            if self.n_long and (self.long_rank is None or self.long_rank):
+                check(lib().kmp_dev_pairs_long(_p(self.rep), _p(self.rep_len), _p(self.off), _p(self.cls), self.n,
+                                               _p(self.long_ids), self.n_long, min_shared, int(require_class_diff),
+                                               _p(self.ep), _p(self.eq), _p(self.ew), self.edge_cap, _p(self.count),
+                                               _stream()), "kmp_dev_pairs_long")
             cnt = int(self.count.item())
             if cnt <= self.edge_cap:
                 self.n_edges = cnt
