@@ -190,11 +190,16 @@ int kmp_dev_pack_dense(const uint32_t* d_rep, const uint64_t* d_res_off, const u
 /* The pair kernel over work items [0, n_items): appends (p, q, w) with p < q,
  * w = |K(p) ∩ K(q)| >= min_shared and (if required) class[p] != class[q] to d_p/d_q/d_w in
  * arbitrary order at positions d_count[0]++ (< cap; the counter keeps counting past cap so
- * the caller can resize and rerun).  d_count (one u64) must be zeroed by the caller. */
+ * the caller can resize and rerun).  d_count (one u64) must be zeroed by the caller.
+ * col_window: a column length (set entries) that almost every column fits, e.g. the 99.5th
+ * percentile (kmp_pair_col_window); it sizes the kernel's register window only — longer
+ * columns are handled too, more slowly. */
 int kmp_dev_pairs(const uint32_t* d_dense, const uint64_t* d_dense_off, const uint16_t* d_class, uint32_t n,
-                  const kmp_work_item* d_items, uint64_t n_items, uint32_t min_shared, int require_class_diff,
-                  uint32_t* d_p, uint32_t* d_q, uint32_t* d_w, uint64_t cap, unsigned long long* d_count,
-                  void* stream);
+                  const kmp_work_item* d_items, uint64_t n_items, uint32_t col_window, uint32_t min_shared,
+                  int require_class_diff, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w, uint64_t cap,
+                  unsigned long long* d_count, void* stream);
+/* The column window kmp_dev_pairs should be given for these (planned) set sizes. */
+uint32_t kmp_pair_col_window(const uint32_t* set_len, uint32_t n);
 
 /* Pairs of the proteins whose repeat-filtered set is longer than the tile capacity
  * (kmp_pair_geometry.tile_cap): those are planned with length 0 (kmp_plan_pairs never sees

@@ -85,8 +85,9 @@ SIGNATURES = {
     "kmp_plan_pairs": (C.c_int, [P, C.c_uint32, C.c_uint64, P, P, C.c_uint64, U64P]),
     "kmp_order_items_xcd": (C.c_int, [P, C.c_uint64, P, C.c_uint64, U64P]),
     "kmp_dev_pack_dense": (C.c_int, [P, P, P, C.c_uint32, P, P]),
-    "kmp_dev_pairs": (C.c_int, [P, P, P, C.c_uint32, P, C.c_uint64, C.c_uint32, C.c_int,
+    "kmp_dev_pairs": (C.c_int, [P, P, P, C.c_uint32, P, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int,
                                 P, P, P, C.c_uint64, P, P]),
+    "kmp_pair_col_window": (C.c_uint32, [P, C.c_uint32]),
     "kmp_dev_pairs_long": (C.c_int, [P, P, P, P, C.c_uint32, P, C.c_uint32, C.c_uint32, C.c_int,
                                      P, P, P, C.c_uint64, P, P]),
     "kmp_dev_sort_edges_tmp_bytes": (C.c_uint64, [C.c_uint64, C.c_uint32]),

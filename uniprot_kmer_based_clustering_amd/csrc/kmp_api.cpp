@@ -367,7 +367,8 @@ int kmp_pairs(kmp_ctx* c, const kmp_pair_opts* opts, kmp_edges** out) {
         KMP_HIP(c, c->ew.reserve(c->edge_cap * sizeof(uint32_t)));
         KMP_HIP(c, hipMemsetAsync(c->ecount.p, 0, sizeof(unsigned long long), c->stream));
         KMP_TRY(c, kmp_dev_pairs(c->dense.as<uint32_t>(), c->dense_off.as<uint64_t>(), c->cls.as<uint16_t>(), c->n,
-                                 c->items.as<kmp_work_item>(), n_items, o.min_shared, o.require_class_diff, c->ep.as<uint32_t>(), c->eq.as<uint32_t>(),
+                                 c->items.as<kmp_work_item>(), n_items, kmp_pair_col_window(plan_len.data(), c->n),
+                                 o.min_shared, o.require_class_diff, c->ep.as<uint32_t>(), c->eq.as<uint32_t>(),
                                  c->ew.as<uint32_t>(), c->edge_cap, c->ecount.as<unsigned long long>(), c->stream));
         KMP_TRY(c, kmp_dev_pairs_long(c->rep.as<uint32_t>(), c->rep_len.as<uint32_t>(), c->off.as<uint64_t>(),
                                       c->cls.as<uint16_t>(), c->n, c->long_ids.as<uint32_t>(),

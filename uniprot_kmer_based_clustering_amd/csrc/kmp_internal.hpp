@@ -42,7 +42,8 @@ constexpr uint32_t kBuckets = kBloomBlocks;             // exact-table bucket = 
 constexpr uint32_t kTileSlots = kTileCap;               // reported by kmp_pair_geometry_get
 constexpr uint32_t kHashMul = 0x9E3779B1u;              // block / bucket hash (top 12 bits)
 constexpr uint32_t kHashMul2 = 0x85EBCA6Bu;             // bit positions inside the block
-constexpr uint32_t kColRegs = 4;                        // column k-mers held per lane (256 per wave pass)
+constexpr uint32_t kColRegs = 3;                        // column k-mers per lane held in registers (192 per column)
+constexpr uint32_t kBatch = 8;                          // columns per register batch (two batches in flight)
 constexpr uint64_t kChunkCost = 262144;                 // column k-mers per work item (one L2-shared chunk)
 
 }  // namespace kmp

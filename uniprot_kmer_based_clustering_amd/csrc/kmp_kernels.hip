@@ -17,6 +17,7 @@
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "kmerpair.h"
@@ -293,13 +294,14 @@ __global__ __launch_bounds__(256) void pack_dense_kernel(const uint32_t* __restr
 //     the filter;
 //   * per-wave hit counters.
 // Each wave owns the item's columns q ≡ wave (mod 16) and streams them from HBM/L2 straight
-// into registers (kColRegs k-mers per lane, all loads independent, the next column's loads
-// in flight while the current one is probed).  A confirmed hit on row r bumps the wave's
+// into registers in batches (see "Batched column stream" above).  A confirmed hit on row r bumps the wave's
 // counter for r (rows with p = row_beg + r < q only: upper triangle); after the column the
 // touched rows are emitted as (p, q, w) when w >= min_shared and the AMR classes differ
 // (mod.rs:580-587), one global atomic per wave (ballot + mbcnt).
 static_assert(kBuckets == 4 * kPairThreads, "bucket scan assumes 4 buckets per thread");
 static_assert(kTileCap <= 65536, "tile positions fit the exact table");
+constexpr uint32_t kEdgeBuf = 64;  // per-wave edge buffer (one global atomic per flush)
+constexpr uint32_t kDefer = 48;    // per-wave list of long columns
 
 __device__ __forceinline__ uint64_t bloom_bits(uint32_t x) {
     const uint32_t g = x * kHashMul2;
@@ -324,43 +326,78 @@ __device__ __forceinline__ uint32_t block_scan_1024(uint32_t v, uint32_t* wave_t
     return before + x - v;
 }
 
-struct ColRegs {
-    uint32_t x[kColRegs];
-    uint32_t len;     // wave-uniform
-    uint64_t start;   // wave-uniform
+// Batched column stream.  A wave owns the item's columns q = qw + 16*t.  Their meta (dense
+// range, class) is fetched 2*B columns at a time (lane j = column t0 + j); their k-mers in
+// batches of B columns (C k-mers per lane per column), ping-pong: batch i is probed from
+// registers while batch i+1's loads are in flight.  Every load of the pipelined loop is
+// issued unconditionally (clamped, in-bounds addresses) so the number of younger loads at
+// each use is the same on every path and the compiler's vmcnt waits stay partial; columns
+// longer than 64*C k-mers are deferred to after the loop.
+struct Meta {
+    uint64_t beg, end;  // lane j < 2B: dense range of column t0 + j
+    uint32_t cls;       // lane j < 2B: its class
 };
 
-__device__ __forceinline__ void col_load(ColRegs& c, const uint32_t* __restrict__ dense,
-                                         const uint64_t* __restrict__ dense_off, uint32_t q, uint32_t qend,
-                                         uint32_t lane) {
-    if (q >= qend) {
-        c.len = 0;
-        return;
-    }
-    const uint64_t s = dense_off[q];
-    c.start = s;
-    c.len = (uint32_t)(dense_off[q + 1] - s);
+__device__ __forceinline__ void meta_load(Meta& m, const uint64_t* __restrict__ dense_off,
+                                          const uint16_t* __restrict__ cls, uint32_t qw, uint32_t t0,
+                                          uint32_t ncol, uint32_t lane) {
+    const uint32_t t = t0 + lane;
+    const uint32_t q = qw + kPairWaves * min(t, ncol - 1);  // ncol >= 1 here: always in bounds
+    const uint64_t b = dense_off[q], e = dense_off[q + 1];
+    const uint32_t c = cls[q];
+    const bool v = t < ncol;
+    m.beg = v ? b : 0ull;
+    m.end = v ? e : 0ull;
+    m.cls = v ? c : 0u;
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+template <uint32_t B, uint32_t C>
+struct BatchX {
+    uint32_t x[B][C];
+};
+
+// unconditionally issue the loads of batch columns j0 .. j0+B-1 of meta m
+template <uint32_t B, uint32_t C>
+__device__ __forceinline__ void batch_issue(BatchX<B, C>& b, const uint32_t* __restrict__ dense, const Meta& m,
+                                            uint32_t j0, uint32_t lane) {
 #pragma unroll
-    for (uint32_t i = 0; i < kColRegs; ++i) {
-        const uint32_t e = lane + 64 * i;
-        c.x[i] = e < c.len ? dense[s + e] : 0u;
+    for (uint32_t j = 0; j < B; ++j) {
+        const uint64_t s = readlane64(m.beg, j0 + j);
+        const uint32_t len = (uint32_t)(readlane64(m.end, j0 + j) - s);
+#pragma unroll
+        for (uint32_t i = 0; i < C; ++i) {
+            const uint32_t e = lane + 64 * i;
+            b.x[j][i] = dense[e < len ? s + e : 0ull];  // lanes past len read element 0 (ignored)
+        }
     }
 }
 
+// kAblate (diagnostic builds only, selected by KMP_PAIR_ABLATE): 0 = the kernel; 1 = build the
+// tile + stream the columns, no probing; 2 = build the tile only; 3 = Bloom probes only (no
+// exact table, no counting).  Modes 1-3 produce wrong edges and exist to time the phases.
+template <int kAblate, uint32_t C, uint32_t B>
 __global__ __launch_bounds__(kPairThreads) void pair_kernel(
     const uint32_t* __restrict__ dense, const uint64_t* __restrict__ dense_off, const uint16_t* __restrict__ cls,
     const kmp_work_item* __restrict__ items, uint32_t min_shared, int require_diff, uint32_t* __restrict__ out_p,
     uint32_t* __restrict__ out_q, uint32_t* __restrict__ out_w, uint64_t cap, unsigned long long* __restrict__ count) {
     __shared__ uint64_t bloom[kBloomBlocks];
-    __shared__ uint32_t F[kBuckets + 2];
+    __shared__ uint16_t F[kBuckets + 2];          // bucket starts (u16: the tile has <= 16384 keys)
     __shared__ uint32_t keys[kTileCap];
     __shared__ uint8_t rows[kTileCap];
-    __shared__ uint32_t cnt[kPairWaves][kRowsMax];
-    __shared__ uint8_t touched[kPairWaves][kRowsMax];
-    __shared__ uint32_t ntouched[kPairWaves];
+    __shared__ uint32_t scratch[kPairWaves * kRowsMax + 16];  // build: u32 bucket counts; probe: hit counters
+    __shared__ uint64_t tmask[kPairWaves][kRowsMax / 64];     // rows touched by the wave's current column
+    __shared__ uint32_t ebuf[kPairWaves][3][kEdgeBuf];        // per-wave edge buffer (p, q, w)
     __shared__ uint16_t row_cls[kRowsMax];
     __shared__ uint32_t row_start[kRowsMax + 1];
     __shared__ uint32_t wave_tot[kPairWaves];
+    __shared__ uint32_t defer[kPairWaves][kDefer];            // long columns, probed after the loop
+    static_assert(kPairWaves * kRowsMax + 16 >= kBuckets + 2, "bucket counts fit the counter scratch");
 
     const kmp_work_item it = items[blockIdx.x];
     const uint32_t r0 = it.row_beg, nrows = it.row_end - it.row_beg;
@@ -368,14 +405,21 @@ __global__ __launch_bounds__(kPairThreads) void pair_kernel(
     const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const uint32_t qfirst = max(it.col_beg, r0 + 1);
 
-    // the first column of this wave is loading while the tile is built
-    ColRegs cur;
-    col_load(cur, dense, dense_off, qfirst + wave, it.col_end, lane);
+    // column stream: meta of pairs 0 and 1 and batch 0's k-mers are in flight during the build
+    const uint32_t qw = qfirst + wave;
+    const uint32_t ncol = qw < it.col_end ? (it.col_end - qw + kPairWaves - 1) / kPairWaves : 0u;
+    Meta mcur, mnext;
+    BatchX<B, C> xa, xb;
+    if (ncol > 0) {
+        meta_load(mcur, dense_off, cls, qw, 0, ncol, lane);
+        meta_load(mnext, dense_off, cls, qw, 2 * B, ncol, lane);
+        batch_issue(xa, dense, mcur, 0, lane);
+    }
 
+    uint32_t* Fc = scratch;  // u32 bucket counts during the build
     for (uint32_t i = tid; i < kBloomBlocks; i += kPairThreads) bloom[i] = 0;
-    for (uint32_t i = tid; i < kBuckets + 2; i += kPairThreads) F[i] = 0;
-    for (uint32_t i = tid; i < kPairWaves * kRowsMax; i += kPairThreads) (&cnt[0][0])[i] = 0;
-    if (tid < kPairWaves) ntouched[tid] = 0;
+    for (uint32_t i = tid; i < kBuckets + 2; i += kPairThreads) Fc[i] = 0;
+    if (tid < kPairWaves * (kRowsMax / 64)) (&tmask[0][0])[tid] = 0;
     const uint64_t d0 = dense_off[r0];
     for (uint32_t r = tid; r <= nrows; r += kPairThreads) row_start[r] = (uint32_t)(dense_off[r0 + r] - d0);
     for (uint32_t r = tid; r < nrows; r += kPairThreads) row_cls[r] = cls[r0 + r];
@@ -387,110 +431,200 @@ __global__ __launch_bounds__(kPairThreads) void pair_kernel(
         const uint32_t x = dense[d0 + e];
         const uint32_t b = bloom_block(x);
         atomicOr(&bloom[b], bloom_bits(x));
-        atomicAdd(&F[b + 2], 1u);
+        atomicAdd(&Fc[b + 2], 1u);
     }
     __syncthreads();
     {
-        const uint32_t c0 = F[4 * tid + 2], c1 = F[4 * tid + 3], c2 = F[4 * tid + 4], c3 = F[4 * tid + 5];
+        const uint32_t c0 = Fc[4 * tid + 2], c1 = Fc[4 * tid + 3], c2 = Fc[4 * tid + 4], c3 = Fc[4 * tid + 5];
         const uint32_t ex = block_scan_1024(c0 + c1 + c2 + c3, wave_tot);
         __syncthreads();
-        F[4 * tid + 1] = ex;  // F[b+1] = start of bucket b (F[0] = 0)
-        F[4 * tid + 2] = ex + c0;
-        F[4 * tid + 3] = ex + c0 + c1;
-        F[4 * tid + 4] = ex + c0 + c1 + c2;
+        Fc[4 * tid + 1] = ex;  // Fc[b+1] = start of bucket b (Fc[0] = 0)
+        Fc[4 * tid + 2] = ex + c0;
+        Fc[4 * tid + 3] = ex + c0 + c1;
+        Fc[4 * tid + 4] = ex + c0 + c1 + c2;
     }
     __syncthreads();
     for (uint32_t r = wave; r < nrows; r += kPairWaves) {
         const uint32_t rb = row_start[r], re = row_start[r + 1];
         for (uint32_t e = rb + lane; e < re; e += 64) {
             const uint32_t x = dense[d0 + e];
-            const uint32_t pos = atomicAdd(&F[bloom_block(x) + 1], 1u);
+            const uint32_t pos = atomicAdd(&Fc[bloom_block(x) + 1], 1u);
             keys[pos] = x;
             rows[pos] = (uint8_t)r;
         }
     }
-    __syncthreads();  // bucket b = [F[b], F[b+1])
+    __syncthreads();  // Fc[b] .. Fc[b+1] = bucket b
+    for (uint32_t i = tid; i < kBuckets + 1; i += kPairThreads) F[i] = (uint16_t)Fc[i];
+    __syncthreads();
+    for (uint32_t i = tid; i < kPairWaves * kRowsMax; i += kPairThreads) scratch[i] = 0;  // hit counters
+    __syncthreads();
+    if (kAblate == 2) return;
+    uint32_t* cnt = scratch + wave * kRowsMax;
+    uint64_t* tm = tmask[wave];
+    uint32_t nbuf = 0;  // wave-uniform fill of the wave's edge buffer
+    uint32_t sink = 0;
 
-    for (uint32_t q = qfirst + wave; q < it.col_end; q += kPairWaves) {
-        ColRegs nxt;
-        col_load(nxt, dense, dense_off, q + kPairWaves, it.col_end, lane);
-        const uint32_t len = cur.len;
+    // flush the wave's edge buffer to HBM: one global atomic per kEdgeBuf edges
+    auto flush = [&]() {
+        if (nbuf == 0) return;
+        unsigned long long first = 0;
+        if (lane == 0) first = atomicAdd(count, (unsigned long long)nbuf);
+        first = __shfl(first, 0);
+        for (uint32_t e = lane; e < nbuf; e += 64) {
+            const unsigned long long pos = first + e;
+            if (pos < cap) {
+                out_p[pos] = ebuf[wave][0][e];
+                out_q[pos] = ebuf[wave][1][e];
+                out_w[pos] = ebuf[wave][2][e];
+            }
+        }
+        nbuf = 0;
+    };
+
+    // probe 64*C k-mers x[] of column q (lanes/registers past len are ignored)
+    auto probe = [&](uint32_t q, uint32_t len, uint32_t base, const uint32_t (&x)[C], bool& hit_any) {
         const uint32_t lim = min(q - r0, nrows);  // rows with p < q
-        for (uint32_t base = 0; base < len; base += 64 * kColRegs) {
-            uint32_t x[kColRegs];
-            if (base == 0) {
+        if (kAblate == 1) {
 #pragma unroll
-                for (uint32_t i = 0; i < kColRegs; ++i) x[i] = cur.x[i];
-            } else {
+            for (uint32_t i = 0; i < C; ++i) sink += x[i];
+            return;
+        }
+        uint64_t word[C], want[C];
+        uint32_t blk[C];
 #pragma unroll
-                for (uint32_t i = 0; i < kColRegs; ++i) {
-                    const uint32_t e = base + lane + 64 * i;
-                    x[i] = e < len ? dense[cur.start + e] : 0u;
-                }
-            }
-            uint64_t word[kColRegs], want[kColRegs];
-            uint32_t blk[kColRegs];
+        for (uint32_t i = 0; i < C; ++i) {
+            blk[i] = bloom_block(x[i]);
+            want[i] = bloom_bits(x[i]);
+            word[i] = bloom[blk[i]];
+        }
+        bool any = false;
+        bool pass[C];
 #pragma unroll
-            for (uint32_t i = 0; i < kColRegs; ++i) {
-                blk[i] = bloom_block(x[i]);
-                want[i] = bloom_bits(x[i]);
-                word[i] = bloom[blk[i]];
-            }
-            bool any = false;
-            bool pass[kColRegs];
+        for (uint32_t i = 0; i < C; ++i) {
+            pass[i] = base + lane + 64 * i < len && (word[i] & want[i]) == want[i];
+            any |= pass[i];
+        }
+        if (kAblate == 3) {
+            sink += any;
+            return;
+        }
+        if (__ballot(any) == 0) return;
 #pragma unroll
-            for (uint32_t i = 0; i < kColRegs; ++i) {
-                pass[i] = base + lane + 64 * i < len && (word[i] & want[i]) == want[i];
-                any |= pass[i];
-            }
-            if (__ballot(any) == 0) continue;
+        for (uint32_t i = 0; i < C; ++i) {
+            if (!pass[i]) continue;
+            const uint32_t be = F[blk[i] + 1];
+            for (uint32_t s0 = F[blk[i]]; s0 < be; s0 += 4) {
+                uint32_t kk[4];
 #pragma unroll
-            for (uint32_t i = 0; i < kColRegs; ++i) {
-                if (!pass[i]) continue;
-                const uint32_t be = F[blk[i] + 1];
-                for (uint32_t s = F[blk[i]]; s < be; ++s) {
-                    if (keys[s] != x[i]) continue;
-                    const uint32_t r = rows[s];
-                    if (r < lim && atomicAdd(&cnt[wave][r], 1u) == 0u) {
-                        const uint32_t t = atomicAdd(&ntouched[wave], 1u);
-                        touched[wave][t] = (uint8_t)r;
+                for (uint32_t u = 0; u < 4; ++u) kk[u] = s0 + u < be ? keys[s0 + u] : ~x[i];
+#pragma unroll
+                for (uint32_t u = 0; u < 4; ++u) {
+                    if (kk[u] != x[i]) continue;
+                    const uint32_t r = rows[s0 + u];
+                    if (r < lim) {
+                        atomicAdd(&cnt[r], 1u);  // no return: nothing waits
+                        atomicOr(&tm[r >> 6], 1ull << (r & 63u));
+                        hit_any = true;
                     }
                 }
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        const uint32_t nt = ntouched[wave];
-        if (nt != 0) {
-            const uint16_t cq = cls[q];
-            for (uint32_t t0 = 0; t0 < nt; t0 += 64) {
-                const uint32_t t = t0 + lane;
+    };
+
+    // emit the rows touched by column q (class cq) into the wave's edge buffer
+    auto epilogue = [&](uint32_t q, uint32_t cq, bool hit_any) {
+        if (__ballot(hit_any) != 0) {
+#pragma unroll
+            for (uint32_t i = 0; i < kRowsMax / 64; ++i) {
+                const uint64_t m = tm[i];  // same word for every lane
+                if (m == 0) continue;
+                const uint32_t r = 64 * i + lane;
                 bool ok = false;
-                uint32_t r = 0, wv = 0;
-                if (t < nt) {
-                    r = touched[wave][t];
-                    wv = cnt[wave][r];
-                    cnt[wave][r] = 0;
+                uint32_t wv = 0;
+                if ((m >> lane) & 1ull) {
+                    wv = cnt[r];
+                    cnt[r] = 0;
                     ok = wv >= min_shared && (!require_diff || row_cls[r] != cq);
                 }
-                const uint64_t m = __ballot(ok);
-                if (m) {
-                    unsigned long long first = 0;
-                    if (lane == 0) first = atomicAdd(count, (unsigned long long)__popcll(m));
-                    first = __shfl(first, 0);
-                    const unsigned long long pos = first + mask_rank(m);
-                    if (ok && pos < cap) {
-                        out_p[pos] = r0 + r;
-                        out_q[pos] = q;
-                        out_w[pos] = wv;
-                    }
+                const uint64_t okm = __ballot(ok);
+                const uint32_t nok = (uint32_t)__popcll(okm);
+                if (nok == 0) continue;
+                if (nbuf + nok > kEdgeBuf) flush();
+                if (ok) {
+                    const uint32_t slot = nbuf + mask_rank(okm);
+                    ebuf[wave][0][slot] = r0 + r;
+                    ebuf[wave][1][slot] = q;
+                    ebuf[wave][2][slot] = wv;
                 }
+                nbuf += nok;
             }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            if (lane == 0) ntouched[wave] = 0;
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            if (lane < kRowsMax / 64) tm[lane] = 0;
         }
-        cur = nxt;
+    };
+
+    // a column held entirely in registers (len <= 64*C): no global load
+    auto column_short = [&](uint32_t q, uint32_t len, uint32_t cq, const uint32_t (&x)[C]) {
+        bool hit_any = false;
+        probe(q, len, 0, x, hit_any);
+        epilogue(q, cq, hit_any);
+    };
+    // any column, loaded here (used after the batches only)
+    auto column_long = [&](uint32_t q) {
+        const uint64_t s = dense_off[q];
+        const uint32_t len = (uint32_t)(dense_off[q + 1] - s);
+        bool hit_any = false;
+        for (uint32_t base = 0; base < len; base += 64 * C) {
+            uint32_t x[C];
+#pragma unroll
+            for (uint32_t i = 0; i < C; ++i) {
+                const uint32_t e = base + lane + 64 * i;
+                x[i] = e < len ? dense[s + e] : 0u;
+            }
+            probe(q, len, base, x, hit_any);
+        }
+        epilogue(q, cls[q], hit_any);
+    };
+
+    // pair iterations: issue B -> probe A -> issue next A -> probe B -> rotate meta
+    uint32_t ndefer = 0;  // columns longer than the register window (probed after the loop)
+    auto probe_batch = [&](const BatchX<B, C>& cur, uint32_t t0, uint32_t j0) {
+#pragma unroll
+        for (uint32_t j = 0; j < B; ++j) {
+            const uint32_t t = t0 + j;
+            if (t >= ncol) break;
+            const uint64_t s = readlane64(mcur.beg, j0 + j);
+            const uint32_t len = (uint32_t)(readlane64(mcur.end, j0 + j) - s);
+            if (len == 0) continue;
+            const uint32_t q = qw + kPairWaves * t;
+            if (len > 64 * C) {
+                if (ndefer < kDefer && lane == 0) defer[wave][ndefer] = q;
+                ++ndefer;
+                continue;
+            }
+            column_short(q, len, __builtin_amdgcn_readlane(mcur.cls, j0 + j), cur.x[j]);
+        }
+    };
+    for (uint32_t t0 = 0; t0 < ncol; t0 += 2 * B) {
+        batch_issue(xb, dense, mcur, B, lane);        // batch t0+B
+        probe_batch(xa, t0, 0);                       // batch t0
+        batch_issue(xa, dense, mnext, 0, lane);       // batch t0+2B
+        probe_batch(xb, t0 + B, B);                   // batch t0+B
+        mcur = mnext;
+        meta_load(mnext, dense_off, cls, qw, t0 + 4 * B, ncol, lane);
     }
+    // deferred long columns (their k-mers are loaded here, in order)
+    for (uint32_t d = 0; d < min(ndefer, kDefer); ++d) column_long(defer[wave][d]);
+    if (ndefer > kDefer) {
+        // list overflowed: walk the wave's columns again and probe every long one beyond it
+        uint32_t seen = 0;
+        for (uint32_t t = 0; t < ncol; ++t) {
+            const uint32_t q = qw + kPairWaves * t;
+            const uint32_t len = (uint32_t)(dense_off[q + 1] - dense_off[q]);
+            if (len > 64 * C && seen++ >= kDefer) column_long(q);
+        }
+    }
+    flush();
+    if (kAblate != 0 && sink == 0xFFFFFFFFu) out_w[0] = sink;  // keep the ablated work alive
 }
 
 // ------------------------------------------------------------------------------------
@@ -702,6 +836,21 @@ int kmp_order_items_xcd(const kmp_work_item* in, uint64_t n, kmp_work_item* out,
     return KMP_OK;
 }
 
+uint32_t kmp_pair_col_window(const uint32_t* set_len, uint32_t n) {
+    if (!set_len || n == 0) return 0;
+    // smallest window class that holds >= 97 % of the non-empty columns (the rest are deferred)
+    const uint32_t classes[3] = {192, 384, 768};
+    uint64_t nonempty = 0, fit[3] = {0, 0, 0};
+    for (uint32_t p = 0; p < n; ++p) {
+        if (set_len[p] == 0) continue;
+        ++nonempty;
+        for (int c = 0; c < 3; ++c) fit[c] += set_len[p] <= classes[c];
+    }
+    for (int c = 0; c < 3; ++c)
+        if (fit[c] * 100 >= nonempty * 97) return classes[c];
+    return classes[2];
+}
+
 int kmp_dev_pack_dense(const uint32_t* d_rep, const uint64_t* d_res_off, const uint64_t* d_dense_off, uint32_t n,
                        uint32_t* d_dense, void* stream) {
     if (n == 0) return KMP_OK;
@@ -711,17 +860,45 @@ int kmp_dev_pack_dense(const uint32_t* d_rep, const uint64_t* d_res_off, const u
 }
 
 int kmp_dev_pairs(const uint32_t* d_dense, const uint64_t* d_dense_off, const uint16_t* d_class, uint32_t n,
-                  const kmp_work_item* d_items, uint64_t n_items, uint32_t min_shared, int require_class_diff,
-                  uint32_t* d_p, uint32_t* d_q, uint32_t* d_w, uint64_t cap, unsigned long long* d_count,
-                  void* stream) {
+                  const kmp_work_item* d_items, uint64_t n_items, uint32_t col_window, uint32_t min_shared,
+                  int require_class_diff, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w, uint64_t cap,
+                  unsigned long long* d_count, void* stream) {
     (void)n;
     if (n_items == 0) return KMP_OK;
     if (!d_dense || !d_dense_off || !d_class || !d_items || !d_count || (cap && (!d_p || !d_q || !d_w)))
         return KMP_EINVAL;
     if (n_items > 0x7FFFFFFFull) return KMP_EINVAL;
     if (min_shared < 1) min_shared = 1;
-    pair_kernel<<<(uint32_t)n_items, kPairThreads, 0, as_stream(stream)>>>(
-        d_dense, d_dense_off, d_class, d_items, min_shared, require_class_diff, d_p, d_q, d_w, cap, d_count);
+    static const int ablate = [] {
+        const char* v = std::getenv("KMP_PAIR_ABLATE");
+        return v ? std::atoi(v) : 0;
+    }();
+    const dim3 grid((uint32_t)n_items), block(kPairThreads);
+    hipStream_t st = as_stream(stream);
+#define KMP_PAIR_LAUNCH(A, CC, BB)                                                                          \
+    pair_kernel<A, CC, BB><<<grid, block, 0, st>>>(d_dense, d_dense_off, d_class, d_items, min_shared,      \
+                                                   require_class_diff, d_p, d_q, d_w, cap, d_count)
+    // register window: 64*C k-mers per column, B columns per batch (2*B*C VGPRs in flight)
+    static const uint32_t force_window = [] {
+        const char* v = std::getenv("KMP_PAIR_WINDOW");  // diagnostic override
+        return v ? (uint32_t)std::atoi(v) : 0u;
+    }();
+    if (force_window) col_window = force_window;
+    const uint32_t w = col_window <= 192 ? 3u : col_window <= 384 ? 6u : 12u;
+#define KMP_PAIR_BY_WINDOW(A)                 \
+    do {                                      \
+        if (w == 3) KMP_PAIR_LAUNCH(A, 3, 8); \
+        else if (w == 6) KMP_PAIR_LAUNCH(A, 6, 3); \
+        else KMP_PAIR_LAUNCH(A, 12, 1);       \
+    } while (0)
+    switch (ablate) {
+        case 1: KMP_PAIR_BY_WINDOW(1); break;
+        case 2: KMP_PAIR_BY_WINDOW(2); break;
+        case 3: KMP_PAIR_BY_WINDOW(3); break;
+        default: KMP_PAIR_BY_WINDOW(0); break;
+    }
+#undef KMP_PAIR_BY_WINDOW
+#undef KMP_PAIR_LAUNCH
     return hip_status(hipGetLastError());
 }
 

@@ -152,6 +152,7 @@ class DevicePipeline:
         long_ids = np.flatnonzero(rep_len > tile_cap).astype(np.uint32)
         plan_len = np.where(rep_len > tile_cap, 0, rep_len).astype(np.uint32)
         plan = Plan(plan_len, chunk_cost)
+        self.col_window = int(lib().kmp_pair_col_window(_np(plan_len), len(plan_len)))
         mine = order_xcd(plan.share(rank, world))
         self.long_rank = rank == world - 1  # the (rare) long-protein pairs run on one rank
         dev = self.dev
@@ -175,7 +176,7 @@ class DevicePipeline:
         for _ in range(2):
             self.count.zero_()
             check(lib().kmp_dev_pairs(_p(self.dense), _p(self.dense_off), _p(self.cls), self.n, _p(self.items),
-                                      self.n_items, min_shared, int(require_class_diff), _p(self.ep), _p(self.eq),
+                                      self.n_items, self.col_window, min_shared, int(require_class_diff), _p(self.ep), _p(self.eq),
                                       _p(self.ew), self.edge_cap, _p(self.count), _stream()), "kmp_dev_pairs")
             if self.n_long and (self.long_rank is None or self.long_rank):
                 check(lib().kmp_dev_pairs_long(_p(self.rep), _p(self.rep_len), _p(self.off), _p(self.cls), self.n,
