@@ -49,6 +49,13 @@ enum { KMP_LEN_NORMAL300 = 0, KMP_LEN_LOGUNIFORM = 1 };
 /* pair scores (kmp_pair_opts.score) */
 enum { KMP_SCORE_COUNT = 0, KMP_SCORE_JACCARD = 1 };
 
+/* pair engines (kmp_pair_opts.engine); every engine returns the same edges */
+enum {
+    KMP_ENGINE_AUTO = 0,      /* postings, with the tiled kernel taking over very frequent k-mers */
+    KMP_ENGINE_POSTINGS = 1,  /* sort / expand Σ C(df,2) incidences / reduce (the reference's algorithm) */
+    KMP_ENGINE_TILES = 2      /* LDS-tiled all-pairs intersection over the N x N upper triangle */
+};
+
 typedef struct kmp_ctx kmp_ctx;
 typedef struct kmp_edges kmp_edges;
 
@@ -71,9 +78,10 @@ typedef struct {
     int32_t require_class_diff;  /* 1: drop same-AMR-class pairs (mod.rs:549-697); 0: keep */
     uint32_t align_threshold;    /* alignment candidates: w > threshold (mod.rs:242: 10) */
     int32_t score;               /* KMP_SCORE_COUNT | KMP_SCORE_JACCARD (build extension) */
+    int32_t engine;              /* KMP_ENGINE_* */
 } kmp_pair_opts;
 
-/* defaults: min_shared 1, require_class_diff 1, align_threshold 10, score COUNT */
+/* defaults: min_shared 1, require_class_diff 1, align_threshold 10, score COUNT, engine AUTO */
 void kmp_pair_opts_default(kmp_pair_opts* opts);
 
 /* ------------------------------------------------------------------ context -------- */
@@ -209,6 +217,35 @@ int kmp_dev_pairs_long(const uint32_t* d_rep, const uint32_t* d_rep_len, const u
                        const uint16_t* d_class, uint32_t n, const uint32_t* d_long_ids, uint32_t n_long,
                        uint32_t min_shared, int require_class_diff, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w,
                        uint64_t cap, unsigned long long* d_count, void* stream);
+
+/* The postings engine (kmp_postings.hip): one radix sort of (k-mer, protein) keys over all
+ * K(p) slots (runs = distinct k-mers, run length = df), expansion of the Σ C(df,2) incidences
+ * of every run with df <= heavy_df (class test fused, graph/mod.rs:39-193 + :549-697), radix
+ * sort + run-length encoding of the pair keys (combine_edges, mod.rs:322-546).  Writes the
+ * edges (p, q, w), w >= min_shared, ALREADY in canonical (p, q) order; *n_edges = count
+ * (KMP_EOVERFLOW if cap is smaller: resize and rerun).  Reads the unfiltered K(p) slots
+ * (d_set, slots = buffer capacity in elements).  Synchronises `stream` (device counts are
+ * read back between phases).  The workspace grows on first use and is reused afterwards.
+ * Pairs that share k-mers with df > heavy_df get only their light share here (see
+ * kmp_pairs, engine AUTO). */
+typedef struct kmp_postings kmp_postings;
+typedef struct {
+    uint64_t sum_S;           /* Σ |K(p)| */
+    uint64_t distinct;        /* distinct k-mers (runs) */
+    uint64_t repeat;          /* runs with df >= 2 */
+    uint64_t sum_cdf2_light;  /* Σ C(df,2) over runs with df <= heavy_df */
+    uint64_t max_df;
+    uint64_t heavy_entries;   /* Σ df over runs with df > heavy_df */
+    uint64_t incidences;      /* class-filtered incidences expanded */
+    uint64_t pairs;           /* distinct pairs among them (before min_shared) */
+} kmp_postings_stats;
+int kmp_postings_create(kmp_postings** ws);
+void kmp_postings_destroy(kmp_postings* ws);
+int kmp_dev_pairs_postings(kmp_postings* ws, const uint32_t* d_set, const uint32_t* d_set_len,
+                           const uint64_t* d_res_off, const uint16_t* d_class, uint32_t n, int k, uint64_t slots,
+                           uint32_t heavy_df, uint32_t min_shared, int require_class_diff, uint32_t* d_p,
+                           uint32_t* d_q, uint32_t* d_w, uint64_t cap, uint64_t* n_edges,
+                           kmp_postings_stats* stats, void* stream);
 
 /* Canonical order: sorts n edges by (p, q).  Keys/values are read from d_p/d_q/d_w and the
  * sorted result is written back to them.  d_tmp: kmp_dev_sort_edges_tmp_bytes(n, N) bytes. */

@@ -28,18 +28,23 @@ def assert_edges(edges, p, q, w):
     np.testing.assert_array_equal(edges.w, w)
 
 
+ENGINES = [_lib.KMP_ENGINE_POSTINGS, _lib.KMP_ENGINE_TILES]
+ENGINE_IDS = ["postings", "tiles"]
+
+
 @pytest.fixture(scope="module")
 def uni():
     res, off, cls, _ = uniprot()
     return res, off, cls
 
 
+@pytest.mark.parametrize("eng", ENGINES, ids=ENGINE_IDS)
 @pytest.mark.parametrize("k", [5, 7])
-def test_tiny_golden(engine, k):
+def test_tiny_golden(engine, k, eng):
     res, off, cls, _ = tiny()
     engine.load(batch(res, off, cls))
     engine.build_sets(k)
-    e = engine.pairs()
+    e = engine.pairs(engine=eng)
     assert_edges(e, *read_edges_tsv(f"tiny_k{k}_edges.tsv"))
     c = engine.counters()
     for key, val in load_json("tiny_counters.json")[str(k)].items():
@@ -67,13 +72,14 @@ def test_kmers_and_sets_match_oracle(engine, oracle_mod, uni, k):
         assert c[key] == oc[key], key
 
 
+@pytest.mark.parametrize("eng", ENGINES, ids=ENGINE_IDS)
 @pytest.mark.parametrize("k", [5, 7])
-def test_uniprot_edges_bit_exact(engine, uni, k):
+def test_uniprot_edges_bit_exact(engine, uni, k, eng):
     res, off, cls = uni
     g = load_json("uniprot_counters.json")[str(k)]
     engine.load(batch(res, off, cls))
     engine.build_sets(k)
-    e = engine.pairs()
+    e = engine.pairs(engine=eng)
     assert len(e) == g["n_edges"]
     assert edges_sha256(e.p, e.q, e.w) == g["edges_sha256"]
     c = engine.counters()
@@ -81,7 +87,8 @@ def test_uniprot_edges_bit_exact(engine, uni, k):
         assert c[key] == g[key], key
 
 
-def test_uniprot_options_match_oracle(engine, oracle_mod, uni):
+@pytest.mark.parametrize("eng", ENGINES, ids=ENGINE_IDS)
+def test_uniprot_options_match_oracle(engine, oracle_mod, uni, eng):
     res, off, cls = uni
     idx = np.arange(0, len(off) - 1, 3)
     r2, o2, c2 = slice_proteins(res, off, cls, idx)
@@ -89,7 +96,7 @@ def test_uniprot_options_match_oracle(engine, oracle_mod, uni):
     engine.load(batch(r2, o2, c2))
     engine.build_sets(5)
     for min_shared, diff in ((1, False), (4, True), (11, False)):
-        e = engine.pairs(min_shared=min_shared, require_class_diff=diff)
+        e = engine.pairs(min_shared=min_shared, require_class_diff=diff, engine=eng)
         assert_edges(e, *o.pairs(min_shared=min_shared, require_class_diff=diff))
 
 
@@ -107,27 +114,29 @@ def test_jaccard_scores(engine, oracle_mod, uni):
     assert np.all((e.score > 0) & (e.score <= 1))
 
 
+@pytest.mark.parametrize("eng", ENGINES, ids=ENGINE_IDS)
 @pytest.mark.parametrize("n,seed,law,k", [(10000, 2, 0, 7), (3000, 5, 1, 5), (3000, 5, 1, 7)])
-def test_synthetic_bit_exact(engine, oracle_mod, n, seed, law, k):
+def test_synthetic_bit_exact(engine, oracle_mod, n, seed, law, k, eng):
     b = K.synth(n, seed, law)
     o = oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=k, threads=8)
     engine.load(b)
     engine.build_sets(k)
-    e = engine.pairs()
+    e = engine.pairs(engine=eng)
     assert_edges(e, *o.pairs())
     assert len(e) > 0
 
 
 def test_config3_full_size_bit_exact(engine, oracle_mod):
-    """Config 3 (100k synthetic, len~300, k=7) against the oracle, end to end."""
+    """Config 3 (100k synthetic, len~300, k=7) against the oracle, end to end, both engines."""
     b = K.synth(100000, 3)
     o = oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=7, threads=16)
     engine.load(b)
     engine.build_sets(7)
-    e = engine.pairs()
     p, q, w = o.pairs()
-    assert len(e) == len(p) and len(e) > 1_000_000
-    assert_edges(e, p, q, w)
+    for eng in ENGINES:
+        e = engine.pairs(engine=eng)
+        assert len(e) == len(p) and len(e) > 1_000_000
+        assert_edges(e, p, q, w)
     c, oc = engine.counters(), o.counters()
     for key in ("distinct", "repeat", "sum_cdf2", "sum_w_diff", "n_edges", "n_align"):
         assert c[key] == oc[key], key
@@ -154,11 +163,12 @@ def test_long_proteins_global_sort_path(engine, oracle_mod):
     rc, _ = o.repeat()
     rep_len = [int(np.isin(sv[so[p]:so[p + 1]], rc).sum()) for p in range(len(seqs))]
     assert sum(r > K._lib.geometry().tile_cap for r in rep_len) >= 2  # the long path really runs
-    for diff in (False, True):
-        assert_edges(engine.pairs(require_class_diff=diff), *o.pairs(require_class_diff=diff))
-    for ms in (1, 50, 3000):
-        assert_edges(engine.pairs(min_shared=ms, require_class_diff=False),
-                     *o.pairs(min_shared=ms, require_class_diff=False))
+    for eng in ENGINES:
+        for diff in (False, True):
+            assert_edges(engine.pairs(require_class_diff=diff, engine=eng), *o.pairs(require_class_diff=diff))
+        for ms in (1, 50, 3000):
+            assert_edges(engine.pairs(min_shared=ms, require_class_diff=False, engine=eng),
+                         *o.pairs(min_shared=ms, require_class_diff=False))
 
 
 def test_edge_cases(engine, oracle_mod):
@@ -170,13 +180,15 @@ def test_edge_cases(engine, oracle_mod):
         for k in (1, 2, 5, 7):
             o = oracle_mod.Oracle(res, off, cls, k=k)
             engine.build_sets(k)
-            assert_edges(engine.pairs(), *o.pairs())
-            assert_edges(engine.pairs(require_class_diff=False), *o.pairs(require_class_diff=False))
+            for eng in ENGINES:
+                assert_edges(engine.pairs(engine=eng), *o.pairs())
+                assert_edges(engine.pairs(require_class_diff=False, engine=eng), *o.pairs(require_class_diff=False))
     # empty batch
     res, off, cls = make_batch([], [])
     engine.load(batch(res, off, cls))
     engine.build_sets(5)
-    assert len(engine.pairs()) == 0
+    for eng in ENGINES:
+        assert len(engine.pairs(engine=eng)) == 0
 
 
 def test_errors(engine):
@@ -196,7 +208,7 @@ def test_device_pipeline_matches_oracle(oracle_mod):
     b = K.synth(20000, 9)
     o = oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=7, threads=8)
     pipe = DevicePipeline(b, 7, "cuda:0", edge_cap=1024)  # forces the overflow/rerun path
-    n = pipe.step()
+    n = pipe.step(engine="tiles")
     torch.cuda.synchronize()
     p, q, w = o.pairs()
     assert n == len(p)
@@ -204,9 +216,20 @@ def test_device_pipeline_matches_oracle(oracle_mod):
     np.testing.assert_array_equal(ep, p)
     np.testing.assert_array_equal(eq, q)
     np.testing.assert_array_equal(ew, w)
-    # a second step on the same buffers is identical (no stale state)
-    assert pipe.step() == n
+    # a second step on the same buffers is identical (no stale state); the postings engine too
+    assert pipe.step(engine="tiles") == n
     np.testing.assert_array_equal(pipe.edges()[2], w)
+    pipe._alloc_edges(1024)
+    for _ in range(2):
+        assert pipe.step(engine="postings") == n
+        ep, eq, ew = pipe.edges()
+        np.testing.assert_array_equal(ep, p)
+        np.testing.assert_array_equal(eq, q)
+        np.testing.assert_array_equal(ew, w)
+    st = pipe.postings_stats.as_dict()
+    c = o.counters()
+    assert st["distinct"] == c["distinct"] and st["repeat"] == c["repeat"] and st["max_df"] == c["max_df"]
+    assert st["sum_cdf2_light"] == c["sum_cdf2"] and st["incidences"] == c["sum_w_diff"]
     # sliced set build (multi-GPU shape): two halves == one launch
     pipe.set.zero_()
     pipe.build_sets(0, 7000)

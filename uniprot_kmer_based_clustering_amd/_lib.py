@@ -17,6 +17,7 @@ HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "kmerpair.h")
 KMP_OK, KMP_EINVAL, KMP_ENOMEM, KMP_EDEVICE, KMP_ERCCL, KMP_EOVERFLOW, KMP_ESTATE, KMP_EIO = range(8)
 KMP_LEN_NORMAL300, KMP_LEN_LOGUNIFORM = 0, 1
 KMP_SCORE_COUNT, KMP_SCORE_JACCARD = 0, 1
+KMP_ENGINE_AUTO, KMP_ENGINE_POSTINGS, KMP_ENGINE_TILES = 0, 1, 2
 KMP_LDS_SORT_MAX = 4096
 
 
@@ -40,7 +41,15 @@ class Counters(C.Structure):
 
 class PairOpts(C.Structure):
     _fields_ = [("min_shared", C.c_uint32), ("require_class_diff", C.c_int32),
-                ("align_threshold", C.c_uint32), ("score", C.c_int32)]
+                ("align_threshold", C.c_uint32), ("score", C.c_int32), ("engine", C.c_int32)]
+
+
+class PostingsStats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in (
+        "sum_S", "distinct", "repeat", "sum_cdf2_light", "max_df", "heavy_entries", "incidences", "pairs")]
+
+    def as_dict(self):
+        return {n: int(getattr(self, n)) for n, _ in self._fields_}
 
 
 class WorkItem(C.Structure):
@@ -90,6 +99,10 @@ SIGNATURES = {
     "kmp_pair_col_window": (C.c_uint32, [P, C.c_uint32]),
     "kmp_dev_pairs_long": (C.c_int, [P, P, P, P, C.c_uint32, P, C.c_uint32, C.c_uint32, C.c_int,
                                      P, P, P, C.c_uint64, P, P]),
+    "kmp_postings_create": (C.c_int, [C.POINTER(P)]),
+    "kmp_postings_destroy": (None, [P]),
+    "kmp_dev_pairs_postings": (C.c_int, [P, P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32,
+                                         C.c_uint32, C.c_int, P, P, P, C.c_uint64, U64P, P, P]),
     "kmp_dev_sort_edges_tmp_bytes": (C.c_uint64, [C.c_uint64, C.c_uint32]),
     "kmp_dev_sort_edges": (C.c_int, [P, P, P, C.c_uint64, C.c_uint32, P, C.c_uint64, P]),
     "kmp_read_fasta": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint32), C.POINTER(P), C.POINTER(P),

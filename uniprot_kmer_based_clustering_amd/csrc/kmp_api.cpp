@@ -70,6 +70,8 @@ struct kmp_ctx {
 
     DevBuf items, dense_off, dense, long_ids, ep, eq, ew, ecount, sort_tmp;
     uint64_t edge_cap = 0;
+    kmp_postings* postings = nullptr;
+    ~kmp_ctx() { kmp_postings_destroy(postings); }
 };
 
 struct kmp_edges {
@@ -115,6 +117,45 @@ int use_device(kmp_ctx* c) {
 
 uint64_t protein_len(const kmp_ctx* c, uint32_t p) { return c->h_off[p + 1] - c->h_off[p]; }
 
+// canonical order (tiles: device sort; postings: already sorted), copy out, scores, counters
+int finish_edges(kmp_ctx* c, const kmp_pair_opts& o, uint64_t count, bool needs_sort, kmp_edges** out) {
+    if (needs_sort) {
+        const uint64_t tmp = kmp_dev_sort_edges_tmp_bytes(count, c->n);
+        KMP_HIP(c, c->sort_tmp.reserve(tmp));
+        KMP_TRY(c, kmp_dev_sort_edges(c->ep.as<uint32_t>(), c->eq.as<uint32_t>(), c->ew.as<uint32_t>(), count, c->n,
+                                      c->sort_tmp.p, c->sort_tmp.bytes, c->stream));
+    }
+    std::unique_ptr<kmp_edges> e(new (std::nothrow) kmp_edges);
+    if (!e) return fail(c, KMP_ENOMEM, "edges");
+    e->p.resize(count);
+    e->q.resize(count);
+    e->w.resize(count);
+    if (count) {
+        KMP_HIP(c, hipMemcpyAsync(e->p.data(), c->ep.p, count * 4, hipMemcpyDeviceToHost, c->stream));
+        KMP_HIP(c, hipMemcpyAsync(e->q.data(), c->eq.p, count * 4, hipMemcpyDeviceToHost, c->stream));
+        KMP_HIP(c, hipMemcpyAsync(e->w.data(), c->ew.p, count * 4, hipMemcpyDeviceToHost, c->stream));
+    }
+    KMP_HIP(c, hipStreamSynchronize(c->stream));
+    e->score.resize(count);
+    uint64_t wdiff = 0, nalign = 0;
+    for (uint64_t i = 0; i < count; ++i) {
+        const uint32_t p = e->p[i], q = e->q[i], w = e->w[i];
+        if (c->h_cls[p] != c->h_cls[q]) wdiff += w;
+        if (w > o.align_threshold) ++nalign;
+        if (o.score == KMP_SCORE_JACCARD) {
+            const uint64_t uni = (uint64_t)c->h_set_len[p] + c->h_set_len[q] - w;
+            e->score[i] = uni ? (float)w / (float)uni : 0.0f;  // exact operands (< 2^24), one rounding
+        } else {
+            e->score[i] = (float)w;
+        }
+    }
+    c->counters.n_edges = count;
+    c->counters.n_align = nalign;
+    c->counters.sum_w_diff = wdiff;
+    *out = e.release();
+    return KMP_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -141,6 +182,7 @@ void kmp_pair_opts_default(kmp_pair_opts* o) {
     o->require_class_diff = 1;
     o->align_threshold = 10;
     o->score = KMP_SCORE_COUNT;
+    o->engine = KMP_ENGINE_AUTO;
 }
 
 int kmp_ctx_create(kmp_ctx** out, int device, int cpu_threads) {
@@ -323,7 +365,34 @@ int kmp_pairs(kmp_ctx* c, const kmp_pair_opts* opts, kmp_edges** out) {
     kmp_pair_opts_default(&o);
     if (opts) o = *opts;
     if (o.score != KMP_SCORE_COUNT && o.score != KMP_SCORE_JACCARD) return fail(c, KMP_EINVAL, "unknown score %d", o.score);
+    if (o.engine < KMP_ENGINE_AUTO || o.engine > KMP_ENGINE_TILES) return fail(c, KMP_EINVAL, "unknown engine %d", o.engine);
     KMP_TRY(c, use_device(c));
+    if (c->edge_cap == 0) c->edge_cap = std::max<uint64_t>(1u << 20, 4ull * c->n);
+    unsigned long long count = 0;
+    if (o.engine != KMP_ENGINE_TILES) {
+        if (!c->postings) KMP_TRY(c, kmp_postings_create(&c->postings));
+        const uint64_t slots = kmp_set_capacity(c->n, c->total_res);
+        for (int attempt = 0; attempt < 2; ++attempt) {
+            KMP_HIP(c, c->ep.reserve(c->edge_cap * sizeof(uint32_t)));
+            KMP_HIP(c, c->eq.reserve(c->edge_cap * sizeof(uint32_t)));
+            KMP_HIP(c, c->ew.reserve(c->edge_cap * sizeof(uint32_t)));
+            uint64_t ne = 0;
+            const int st = kmp_dev_pairs_postings(c->postings, c->set.as<uint32_t>(), c->set_len.as<uint32_t>(),
+                                                  c->off.as<uint64_t>(), c->cls.as<uint16_t>(), c->n, c->k_sets,
+                                                  slots, 0xFFFFFFFFu, o.min_shared, o.require_class_diff,
+                                                  c->ep.as<uint32_t>(), c->eq.as<uint32_t>(), c->ew.as<uint32_t>(),
+                                                  c->edge_cap, &ne, nullptr, c->stream);
+            count = ne;
+            if (st == KMP_EOVERFLOW) {
+                c->edge_cap = ne + ne / 8 + 1024;
+                continue;
+            }
+            if (st != KMP_OK) return fail(c, st, "postings engine: %s", kmp_status_string(st));
+            break;
+        }
+        if (count > c->edge_cap) return fail(c, KMP_EDEVICE, "edge count unstable across reruns");
+        return finish_edges(c, o, count, false, out);
+    }
 
     // plan (host): dense CSR offsets, row tiles x column chunks, XCD-aware launch order
     // sets longer than a row tile take the long-protein kernel; they are planned with length 0
@@ -358,9 +427,7 @@ int kmp_pairs(kmp_ctx* c, const kmp_pair_opts* opts, kmp_edges** out) {
                                   hipMemcpyHostToDevice, c->stream));
     KMP_TRY(c, kmp_dev_pack_dense(c->rep.as<uint32_t>(), c->off.as<uint64_t>(), c->dense_off.as<uint64_t>(), c->n,
                                   c->dense.as<uint32_t>(), c->stream));
-    if (c->edge_cap == 0) c->edge_cap = std::max<uint64_t>(1u << 20, 4ull * c->n);
     KMP_HIP(c, c->ecount.reserve(sizeof(unsigned long long)));
-    unsigned long long count = 0;
     for (int attempt = 0; attempt < 2; ++attempt) {
         KMP_HIP(c, c->ep.reserve(c->edge_cap * sizeof(uint32_t)));
         KMP_HIP(c, c->eq.reserve(c->edge_cap * sizeof(uint32_t)));
@@ -381,39 +448,7 @@ int kmp_pairs(kmp_ctx* c, const kmp_pair_opts* opts, kmp_edges** out) {
         c->edge_cap = count + count / 8 + 1024;
     }
     if (count > c->edge_cap) return fail(c, KMP_EDEVICE, "edge count unstable across reruns");
-    const uint64_t tmp = kmp_dev_sort_edges_tmp_bytes(count, c->n);
-    KMP_HIP(c, c->sort_tmp.reserve(tmp));
-    KMP_TRY(c, kmp_dev_sort_edges(c->ep.as<uint32_t>(), c->eq.as<uint32_t>(), c->ew.as<uint32_t>(), count, c->n,
-                                  c->sort_tmp.p, c->sort_tmp.bytes, c->stream));
-    std::unique_ptr<kmp_edges> e(new (std::nothrow) kmp_edges);
-    if (!e) return fail(c, KMP_ENOMEM, "edges");
-    e->p.resize(count);
-    e->q.resize(count);
-    e->w.resize(count);
-    if (count) {
-        KMP_HIP(c, hipMemcpyAsync(e->p.data(), c->ep.p, count * 4, hipMemcpyDeviceToHost, c->stream));
-        KMP_HIP(c, hipMemcpyAsync(e->q.data(), c->eq.p, count * 4, hipMemcpyDeviceToHost, c->stream));
-        KMP_HIP(c, hipMemcpyAsync(e->w.data(), c->ew.p, count * 4, hipMemcpyDeviceToHost, c->stream));
-    }
-    KMP_HIP(c, hipStreamSynchronize(c->stream));
-    e->score.resize(count);
-    uint64_t wdiff = 0, nalign = 0;
-    for (uint64_t i = 0; i < count; ++i) {
-        const uint32_t p = e->p[i], q = e->q[i], w = e->w[i];
-        if (c->h_cls[p] != c->h_cls[q]) wdiff += w;
-        if (w > o.align_threshold) ++nalign;
-        if (o.score == KMP_SCORE_JACCARD) {
-            const uint64_t uni = (uint64_t)c->h_set_len[p] + c->h_set_len[q] - w;
-            e->score[i] = uni ? (float)w / (float)uni : 0.0f;  // exact operands (< 2^24), one rounding
-        } else {
-            e->score[i] = (float)w;
-        }
-    }
-    c->counters.n_edges = count;
-    c->counters.n_align = nalign;
-    c->counters.sum_w_diff = wdiff;
-    *out = e.release();
-    return KMP_OK;
+    return finish_edges(c, o, count, true, out);
 }
 
 int kmp_edges_count(const kmp_edges* e, uint64_t* n) {

@@ -123,6 +123,8 @@ class DevicePipeline:
         self.n_long = 0
         self.long_ids = None
         self.long_rank = None
+        self._postings = None
+        self.postings_stats = _lib.PostingsStats()
 
     def _alloc_edges(self, cap):
         self.edge_cap = cap
@@ -201,14 +203,48 @@ class DevicePipeline:
         check(L.kmp_dev_sort_edges(_p(self.ep), _p(self.eq), _p(self.ew), n, self.n, _p(self._sort_tmp),
                                    self._sort_tmp.numel(), _stream()), "kmp_dev_sort_edges")
 
-    def step(self, min_shared: int = 1, require_class_diff: bool = True) -> int:
-        """The whole single-GPU path: sets -> filter -> plan -> pairs -> canonical sort."""
+    def postings(self, min_shared: int = 1, require_class_diff: bool = True,
+                 heavy_df: int = 0xFFFFFFFF) -> int:
+        """Postings engine over the K(p) slots: canonical edges into ep/eq/ew (syncs)."""
+        if self._postings is None:
+            ws = C.c_void_p()
+            check(lib().kmp_postings_create(C.byref(ws)), "kmp_postings_create")
+            self._postings = ws
+        slots = int(lib().kmp_set_capacity(self.n, self.total))
+        for _ in range(2):
+            ne = C.c_uint64()
+            st = lib().kmp_dev_pairs_postings(self._postings, _p(self.set), _p(self.set_len), _p(self.off),
+                                              _p(self.cls), self.n, self.k, slots, heavy_df, min_shared,
+                                              int(require_class_diff), _p(self.ep), _p(self.eq), _p(self.ew),
+                                              self.edge_cap, C.byref(ne), C.byref(self.postings_stats),
+                                              _stream())
+            if st == _lib.KMP_EOVERFLOW:
+                self._alloc_edges(ne.value + ne.value // 8 + 1024)
+                continue
+            check(st, "kmp_dev_pairs_postings")
+            self.n_edges = ne.value
+            return self.n_edges
+        raise RuntimeError("edge count unstable across reruns")
+
+    def step(self, min_shared: int = 1, require_class_diff: bool = True, engine: str = "postings") -> int:
+        """The whole single-GPU path.  postings: sets -> sort/expand/reduce (canonical order);
+        tiles: sets -> repeat filter -> plan -> tiled pair kernel -> canonical sort."""
         self.build_sets()
+        if engine == "postings":
+            return self.postings(min_shared, require_class_diff)
         self.filter()
         self.plan()
         n = self.pairs(min_shared, require_class_diff)
         self.sort(n)
         return n
+
+    def __del__(self):
+        if getattr(self, "_postings", None) is not None:
+            try:
+                lib().kmp_postings_destroy(self._postings)
+            except Exception:
+                pass
+            self._postings = None
 
     def edges(self):
         n = self.n_edges

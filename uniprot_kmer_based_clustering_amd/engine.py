@@ -155,8 +155,8 @@ class KmerPairEngine:
         return c.as_dict()
 
     def pairs(self, min_shared=1, require_class_diff=True, align_threshold=10,
-              score=_lib.KMP_SCORE_COUNT) -> Edges:
-        o = _lib.PairOpts(min_shared, int(require_class_diff), align_threshold, score)
+              score=_lib.KMP_SCORE_COUNT, engine=_lib.KMP_ENGINE_AUTO) -> Edges:
+        o = _lib.PairOpts(min_shared, int(require_class_diff), align_threshold, score, engine)
         e = C.c_void_p()
         self._check(lib().kmp_pairs(self._ctx, C.byref(o), C.byref(e)), "kmp_pairs")
         try:
