@@ -53,7 +53,8 @@ enum { KMP_SCORE_COUNT = 0, KMP_SCORE_JACCARD = 1 };
 enum {
     KMP_ENGINE_AUTO = 0,      /* postings, with the tiled kernel taking over very frequent k-mers */
     KMP_ENGINE_POSTINGS = 1,  /* sort / expand Σ C(df,2) incidences / reduce (the reference's algorithm) */
-    KMP_ENGINE_TILES = 2      /* LDS-tiled all-pairs intersection over the N x N upper triangle */
+    KMP_ENGINE_TILES = 2,     /* LDS-tiled all-pairs intersection over the N x N upper triangle */
+    KMP_ENGINE_RESIDUES = 3   /* postings fed by the k-mer windows of the residues (kmp_dev_pairs_residues) */
 };
 
 typedef struct kmp_ctx kmp_ctx;
@@ -229,6 +230,7 @@ int kmp_dev_pairs_long(const uint32_t* d_rep, const uint32_t* d_rep_len, const u
  * Pairs that share k-mers with df > heavy_df get only their light share here (see
  * kmp_pairs, engine AUTO). */
 typedef struct kmp_postings kmp_postings;
+#define KMP_POSTINGS_STAGES 6
 typedef struct {
     uint64_t sum_S;           /* Σ |K(p)| */
     uint64_t distinct;        /* distinct k-mers (runs) */
@@ -238,14 +240,29 @@ typedef struct {
     uint64_t heavy_entries;   /* Σ df over runs with df > heavy_df */
     uint64_t incidences;      /* class-filtered incidences expanded */
     uint64_t pairs;           /* distinct pairs among them (before min_shared) */
+    float stage_ms[KMP_POSTINGS_STAGES]; /* per-stage device time (kmp_postings_set_timing), else 0:
+                                            keys, code sort, count + offsets, write, pair sort,
+                                            run-length encode + emit */
 } kmp_postings_stats;
 int kmp_postings_create(kmp_postings** ws);
 void kmp_postings_destroy(kmp_postings* ws);
+/* Records HIP events between the stages on the call's stream (stats->stage_ms). */
+int kmp_postings_set_timing(kmp_postings* ws, int enable);
 int kmp_dev_pairs_postings(kmp_postings* ws, const uint32_t* d_set, const uint32_t* d_set_len,
                            const uint64_t* d_res_off, const uint16_t* d_class, uint32_t n, int k, uint64_t slots,
                            uint32_t heavy_df, uint32_t min_shared, int require_class_diff, uint32_t* d_p,
                            uint32_t* d_q, uint32_t* d_w, uint64_t cap, uint64_t* n_edges,
                            kmp_postings_stats* stats, void* stream);
+
+/* The postings engine straight from the packed residues (the fused device path): one key per
+ * k-mer window (Protein::new, protein.rs:82-94) in the same slot layout, so the per-protein
+ * sort + dedup of K(p) (main.rs:280-282) is never materialised — duplicate windows of one
+ * protein are adjacent after the stable code sort and count once.  Same output contract and
+ * edges as kmp_dev_pairs_postings; stats->sum_S = Σ |K(p)|.  slots = kmp_set_capacity(N, ΣL). */
+int kmp_dev_pairs_residues(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off,
+                           const uint16_t* d_class, uint32_t n, int k, uint64_t slots, uint32_t heavy_df,
+                           uint32_t min_shared, int require_class_diff, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w,
+                           uint64_t cap, uint64_t* n_edges, kmp_postings_stats* stats, void* stream);
 
 /* Canonical order: sorts n edges by (p, q).  Keys/values are read from d_p/d_q/d_w and the
  * sorted result is written back to them.  d_tmp: kmp_dev_sort_edges_tmp_bytes(n, N) bytes. */

@@ -28,8 +28,8 @@ def assert_edges(edges, p, q, w):
     np.testing.assert_array_equal(edges.w, w)
 
 
-ENGINES = [_lib.KMP_ENGINE_POSTINGS, _lib.KMP_ENGINE_TILES]
-ENGINE_IDS = ["postings", "tiles"]
+ENGINES = [_lib.KMP_ENGINE_POSTINGS, _lib.KMP_ENGINE_TILES, _lib.KMP_ENGINE_RESIDUES]
+ENGINE_IDS = ["postings", "tiles", "residues"]
 
 
 @pytest.fixture(scope="module")
@@ -219,17 +219,25 @@ def test_device_pipeline_matches_oracle(oracle_mod):
     # a second step on the same buffers is identical (no stale state); the postings engine too
     assert pipe.step(engine="tiles") == n
     np.testing.assert_array_equal(pipe.edges()[2], w)
-    pipe._alloc_edges(1024)
-    for _ in range(2):
-        assert pipe.step(engine="postings") == n
-        ep, eq, ew = pipe.edges()
-        np.testing.assert_array_equal(ep, p)
-        np.testing.assert_array_equal(eq, q)
-        np.testing.assert_array_equal(ew, w)
-    st = pipe.postings_stats.as_dict()
     c = o.counters()
-    assert st["distinct"] == c["distinct"] and st["repeat"] == c["repeat"] and st["max_df"] == c["max_df"]
-    assert st["sum_cdf2_light"] == c["sum_cdf2"] and st["incidences"] == c["sum_w_diff"]
+    for eng in ("postings", "residues"):
+        pipe._alloc_edges(1024)
+        for _ in range(2):
+            assert pipe.step(engine=eng) == n
+            ep, eq, ew = pipe.edges()
+            np.testing.assert_array_equal(ep, p)
+            np.testing.assert_array_equal(eq, q)
+            np.testing.assert_array_equal(ew, w)
+        st = pipe.postings_stats.as_dict()
+        assert st["distinct"] == c["distinct"] and st["repeat"] == c["repeat"] and st["max_df"] == c["max_df"]
+        assert st["sum_cdf2_light"] == c["sum_cdf2"] and st["incidences"] == c["sum_w_diff"]
+        assert st["sum_S"] == c["sum_S"] and st["pairs"] == n
+    # stage timing: six non-negative stage times that add up to about one step
+    pipe.set_stage_timing(True)
+    assert pipe.step(engine="residues") == n
+    stages = pipe.postings_stats.stages()
+    assert len(stages) == 6 and all(v >= 0 for v in stages.values()) and sum(stages.values()) > 0
+    pipe.set_stage_timing(False)
     # sliced set build (multi-GPU shape): two halves == one launch
     pipe.set.zero_()
     pipe.build_sets(0, 7000)

@@ -17,7 +17,7 @@ from uniprot_kmer_based_clustering_amd.device import DevicePipeline  # noqa: E40
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 100000
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
-    engines = sys.argv[3].split(",") if len(sys.argv) > 3 else ["postings", "tiles"]
+    engines = sys.argv[3].split(",") if len(sys.argv) > 3 else ["residues", "postings", "tiles"]
     b = K.synth(n, 3)
     pipe = DevicePipeline(b, 7, "cuda:0")
     for eng in engines:
@@ -29,8 +29,14 @@ def main():
             m = pipe.step(engine=eng)
             torch.cuda.synchronize()
             t.append((time.perf_counter() - t0) * 1e3)
+        post = eng in ("postings", "residues")
         print(f"engine={eng} n={n} edges={m} median_ms={np.median(t):.3f} min_ms={min(t):.3f} "
-              f"stats={pipe.postings_stats.as_dict() if eng == 'postings' else ''}")
+              f"stats={pipe.postings_stats.as_dict() if post else ''}")
+        if post:
+            pipe.set_stage_timing(True)
+            pipe.step(engine=eng)
+            print("  stages_ms", {k: round(v, 3) for k, v in pipe.postings_stats.stages().items()})
+            pipe.set_stage_timing(False)
 
 
 if __name__ == "__main__":

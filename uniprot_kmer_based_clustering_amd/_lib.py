@@ -17,7 +17,7 @@ HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "kmerpair.h")
 KMP_OK, KMP_EINVAL, KMP_ENOMEM, KMP_EDEVICE, KMP_ERCCL, KMP_EOVERFLOW, KMP_ESTATE, KMP_EIO = range(8)
 KMP_LEN_NORMAL300, KMP_LEN_LOGUNIFORM = 0, 1
 KMP_SCORE_COUNT, KMP_SCORE_JACCARD = 0, 1
-KMP_ENGINE_AUTO, KMP_ENGINE_POSTINGS, KMP_ENGINE_TILES = 0, 1, 2
+KMP_ENGINE_AUTO, KMP_ENGINE_POSTINGS, KMP_ENGINE_TILES, KMP_ENGINE_RESIDUES = 0, 1, 2, 3
 KMP_LDS_SORT_MAX = 4096
 
 
@@ -44,12 +44,20 @@ class PairOpts(C.Structure):
                 ("align_threshold", C.c_uint32), ("score", C.c_int32), ("engine", C.c_int32)]
 
 
+KMP_POSTINGS_STAGES = 6
+POSTINGS_STAGE_NAMES = ("keys", "code_sort", "count", "write", "pair_sort", "rle_emit")
+
+
 class PostingsStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
-        "sum_S", "distinct", "repeat", "sum_cdf2_light", "max_df", "heavy_entries", "incidences", "pairs")]
+        "sum_S", "distinct", "repeat", "sum_cdf2_light", "max_df", "heavy_entries", "incidences", "pairs")] + [
+        ("stage_ms", C.c_float * KMP_POSTINGS_STAGES)]
 
     def as_dict(self):
-        return {n: int(getattr(self, n)) for n, _ in self._fields_}
+        return {n: int(getattr(self, n)) for n, _ in self._fields_ if n != "stage_ms"}
+
+    def stages(self) -> dict:
+        return dict(zip(POSTINGS_STAGE_NAMES, (float(x) for x in self.stage_ms)))
 
 
 class WorkItem(C.Structure):
@@ -102,6 +110,9 @@ SIGNATURES = {
     "kmp_postings_create": (C.c_int, [C.POINTER(P)]),
     "kmp_postings_destroy": (None, [P]),
     "kmp_dev_pairs_postings": (C.c_int, [P, P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32,
+                                         C.c_uint32, C.c_int, P, P, P, C.c_uint64, U64P, P, P]),
+    "kmp_postings_set_timing": (C.c_int, [P, C.c_int]),
+    "kmp_dev_pairs_residues": (C.c_int, [P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32,
                                          C.c_uint32, C.c_int, P, P, P, C.c_uint64, U64P, P, P]),
     "kmp_dev_sort_edges_tmp_bytes": (C.c_uint64, [C.c_uint64, C.c_uint32]),
     "kmp_dev_sort_edges": (C.c_int, [P, P, P, C.c_uint64, C.c_uint32, P, C.c_uint64, P]),

@@ -365,7 +365,7 @@ int kmp_pairs(kmp_ctx* c, const kmp_pair_opts* opts, kmp_edges** out) {
     kmp_pair_opts_default(&o);
     if (opts) o = *opts;
     if (o.score != KMP_SCORE_COUNT && o.score != KMP_SCORE_JACCARD) return fail(c, KMP_EINVAL, "unknown score %d", o.score);
-    if (o.engine < KMP_ENGINE_AUTO || o.engine > KMP_ENGINE_TILES) return fail(c, KMP_EINVAL, "unknown engine %d", o.engine);
+    if (o.engine < KMP_ENGINE_AUTO || o.engine > KMP_ENGINE_RESIDUES) return fail(c, KMP_EINVAL, "unknown engine %d", o.engine);
     KMP_TRY(c, use_device(c));
     if (c->edge_cap == 0) c->edge_cap = std::max<uint64_t>(1u << 20, 4ull * c->n);
     unsigned long long count = 0;
@@ -377,11 +377,18 @@ int kmp_pairs(kmp_ctx* c, const kmp_pair_opts* opts, kmp_edges** out) {
             KMP_HIP(c, c->eq.reserve(c->edge_cap * sizeof(uint32_t)));
             KMP_HIP(c, c->ew.reserve(c->edge_cap * sizeof(uint32_t)));
             uint64_t ne = 0;
-            const int st = kmp_dev_pairs_postings(c->postings, c->set.as<uint32_t>(), c->set_len.as<uint32_t>(),
-                                                  c->off.as<uint64_t>(), c->cls.as<uint16_t>(), c->n, c->k_sets,
-                                                  slots, 0xFFFFFFFFu, o.min_shared, o.require_class_diff,
-                                                  c->ep.as<uint32_t>(), c->eq.as<uint32_t>(), c->ew.as<uint32_t>(),
-                                                  c->edge_cap, &ne, nullptr, c->stream);
+            const int st =
+                o.engine == KMP_ENGINE_RESIDUES
+                    ? kmp_dev_pairs_residues(c->postings, c->res.as<uint8_t>(), c->off.as<uint64_t>(),
+                                             c->cls.as<uint16_t>(), c->n, c->k_sets, slots, 0xFFFFFFFFu,
+                                             o.min_shared, o.require_class_diff, c->ep.as<uint32_t>(),
+                                             c->eq.as<uint32_t>(), c->ew.as<uint32_t>(), c->edge_cap, &ne, nullptr,
+                                             c->stream)
+                    : kmp_dev_pairs_postings(c->postings, c->set.as<uint32_t>(), c->set_len.as<uint32_t>(),
+                                             c->off.as<uint64_t>(), c->cls.as<uint16_t>(), c->n, c->k_sets, slots,
+                                             0xFFFFFFFFu, o.min_shared, o.require_class_diff, c->ep.as<uint32_t>(),
+                                             c->eq.as<uint32_t>(), c->ew.as<uint32_t>(), c->edge_cap, &ne, nullptr,
+                                             c->stream);
             count = ne;
             if (st == KMP_EOVERFLOW) {
                 c->edge_cap = ne + ne / 8 + 1024;

@@ -22,6 +22,23 @@ inline uint64_t pow21(int k) {
     return v;
 }
 
+// byte -> residue code (amino_acid_to_bits, protein.rs:49-54): unknown bytes -> 20
+struct CodeLut {
+    uint8_t v[256];
+};
+constexpr CodeLut make_lut() {
+    CodeLut l{};
+    for (int b = 0; b < 256; ++b) {
+        l.v[b] = 20;
+        for (int i = 0; i < 21; ++i)
+            if ((uint8_t)kAminoAcids[i] == (uint8_t)b) {
+                l.v[b] = (uint8_t)i;
+                break;
+            }
+    }
+    return l;
+}
+
 // windows j in [0, L-k] (protein.rs:114); L < k yields none (documented deviation: the
 // reference wraps usize for L < 4 and panics)
 inline uint64_t n_windows(uint64_t L, int k) { return L >= (uint64_t)k ? L - k + 1 : 0; }

@@ -27,18 +27,6 @@ using namespace kmp;
 
 namespace {
 
-struct CodeLut {
-    uint8_t v[256];
-};
-constexpr CodeLut make_lut() {
-    CodeLut l{};
-    for (int b = 0; b < 256; ++b) {
-        l.v[b] = 20;  // amino_acid_to_bits: unknown -> 20 (protein.rs:50-51)
-        for (int i = 0; i < 21; ++i)
-            if ((uint8_t)kAminoAcids[i] == (uint8_t)b) { l.v[b] = (uint8_t)i; break; }
-    }
-    return l;
-}
 __constant__ CodeLut c_lut = make_lut();
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }

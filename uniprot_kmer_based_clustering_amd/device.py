@@ -203,21 +203,36 @@ class DevicePipeline:
         check(L.kmp_dev_sort_edges(_p(self.ep), _p(self.eq), _p(self.ew), n, self.n, _p(self._sort_tmp),
                                    self._sort_tmp.numel(), _stream()), "kmp_dev_sort_edges")
 
-    def postings(self, min_shared: int = 1, require_class_diff: bool = True,
-                 heavy_df: int = 0xFFFFFFFF) -> int:
-        """Postings engine over the K(p) slots: canonical edges into ep/eq/ew (syncs)."""
+    def _workspace(self):
         if self._postings is None:
             ws = C.c_void_p()
             check(lib().kmp_postings_create(C.byref(ws)), "kmp_postings_create")
             self._postings = ws
+        return self._postings
+
+    def set_stage_timing(self, enable: bool = True) -> None:
+        """Per-stage HIP-event times of the postings engine into postings_stats.stage_ms."""
+        check(lib().kmp_postings_set_timing(self._workspace(), int(enable)), "kmp_postings_set_timing")
+
+    def postings(self, min_shared: int = 1, require_class_diff: bool = True,
+                 heavy_df: int = 0xFFFFFFFF, from_residues: bool = False) -> int:
+        """Postings engine: canonical edges into ep/eq/ew (syncs).  Reads the K(p) slots
+        (after build_sets), or with from_residues the packed residues directly (fused path)."""
+        ws = self._workspace()
         slots = int(lib().kmp_set_capacity(self.n, self.total))
         for _ in range(2):
             ne = C.c_uint64()
-            st = lib().kmp_dev_pairs_postings(self._postings, _p(self.set), _p(self.set_len), _p(self.off),
-                                              _p(self.cls), self.n, self.k, slots, heavy_df, min_shared,
-                                              int(require_class_diff), _p(self.ep), _p(self.eq), _p(self.ew),
-                                              self.edge_cap, C.byref(ne), C.byref(self.postings_stats),
-                                              _stream())
+            if from_residues:
+                st = lib().kmp_dev_pairs_residues(ws, _p(self.res), _p(self.off), _p(self.cls), self.n, self.k,
+                                                  slots, heavy_df, min_shared, int(require_class_diff),
+                                                  _p(self.ep), _p(self.eq), _p(self.ew), self.edge_cap,
+                                                  C.byref(ne), C.byref(self.postings_stats), _stream())
+            else:
+                st = lib().kmp_dev_pairs_postings(ws, _p(self.set), _p(self.set_len), _p(self.off),
+                                                  _p(self.cls), self.n, self.k, slots, heavy_df, min_shared,
+                                                  int(require_class_diff), _p(self.ep), _p(self.eq), _p(self.ew),
+                                                  self.edge_cap, C.byref(ne), C.byref(self.postings_stats),
+                                                  _stream())
             if st == _lib.KMP_EOVERFLOW:
                 self._alloc_edges(ne.value + ne.value // 8 + 1024)
                 continue
@@ -226,9 +241,13 @@ class DevicePipeline:
             return self.n_edges
         raise RuntimeError("edge count unstable across reruns")
 
-    def step(self, min_shared: int = 1, require_class_diff: bool = True, engine: str = "postings") -> int:
-        """The whole single-GPU path.  postings: sets -> sort/expand/reduce (canonical order);
-        tiles: sets -> repeat filter -> plan -> tiled pair kernel -> canonical sort."""
+    def step(self, min_shared: int = 1, require_class_diff: bool = True, engine: str = "residues") -> int:
+        """The whole single-GPU path, packed residues in HBM -> canonical edges in HBM.
+        residues: windows -> sort/expand/reduce (kmp_dev_pairs_residues, fused);
+        postings: K(p) sets -> sort/expand/reduce;
+        tiles: K(p) sets -> repeat filter -> plan -> tiled pair kernel -> canonical sort."""
+        if engine == "residues":
+            return self.postings(min_shared, require_class_diff, from_residues=True)
         self.build_sets()
         if engine == "postings":
             return self.postings(min_shared, require_class_diff)
