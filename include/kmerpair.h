@@ -248,6 +248,12 @@ int kmp_postings_create(kmp_postings** ws);
 void kmp_postings_destroy(kmp_postings* ws);
 /* Records HIP events between the stages on the call's stream (stats->stage_ms). */
 int kmp_postings_set_timing(kmp_postings* ws, int enable);
+/* Key layout.  bucketed (default 1): keys sorted on a 2^b-bucket hash of the k-mer only, then one
+ * workgroup per bucket groups, deduplicates and expands its k-mers in LDS; buckets that do not
+ * fit (very frequent k-mers) make the call rerun on the flat layout.  0: always flat (full code
+ * sort, scan-based expansion).  kmp_postings_last_layout: 1 if the last call ran bucketed. */
+int kmp_postings_set_layout(kmp_postings* ws, int bucketed);
+int kmp_postings_last_layout(const kmp_postings* ws);
 int kmp_dev_pairs_postings(kmp_postings* ws, const uint32_t* d_set, const uint32_t* d_set_len,
                            const uint64_t* d_res_off, const uint16_t* d_class, uint32_t n, int k, uint64_t slots,
                            uint32_t heavy_df, uint32_t min_shared, int require_class_diff, uint32_t* d_p,

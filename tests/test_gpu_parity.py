@@ -191,6 +191,27 @@ def test_edge_cases(engine, oracle_mod):
         assert len(engine.pairs(engine=eng)) == 0
 
 
+def test_bucketed_fallback_on_frequent_kmers(oracle_mod):
+    """A k-mer shared by thousands of proteins overflows an LDS sub-bucket: the bucketed layout
+    hands the call to the flat layout and the edges stay exact."""
+    import torch
+    from uniprot_kmer_based_clustering_amd.device import DevicePipeline
+    rng = np.random.default_rng(11)
+    alpha = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", dtype=np.uint8)
+    seqs = [alpha[rng.integers(0, 20, 120)].tobytes() + b"WWWWWWW" for _ in range(3000)]
+    res, off, cls = make_batch(seqs, [str(i % 7) for i in range(3000)])
+    o = oracle_mod.Oracle(res, off, cls, k=7, threads=8)
+    pipe = DevicePipeline(K.Proteins(res, off, cls), 7, "cuda:0")
+    for eng in ("postings", "residues"):
+        m = pipe.step(engine=eng)
+        torch.cuda.synchronize()
+        assert pipe.last_layout() == "flat"
+        p, q, w = o.pairs()
+        assert m == len(p)
+        np.testing.assert_array_equal(pipe.edges()[0], p)
+        np.testing.assert_array_equal(pipe.edges()[2], w)
+
+
 def test_errors(engine):
     with pytest.raises(_lib.KmpError) as e:
         engine.build_sets(9)
@@ -232,6 +253,15 @@ def test_device_pipeline_matches_oracle(oracle_mod):
         assert st["distinct"] == c["distinct"] and st["repeat"] == c["repeat"] and st["max_df"] == c["max_df"]
         assert st["sum_cdf2_light"] == c["sum_cdf2"] and st["incidences"] == c["sum_w_diff"]
         assert st["sum_S"] == c["sum_S"] and st["pairs"] == n
+    # both key layouts, both entry points: identical edges; config-shaped input runs bucketed
+    for bucketed in (True, False):
+        pipe.set_layout(bucketed)
+        for eng in ("postings", "residues"):
+            assert pipe.step(engine=eng) == n
+            np.testing.assert_array_equal(pipe.edges()[1], q)
+            np.testing.assert_array_equal(pipe.edges()[2], w)
+            assert pipe.last_layout() == ("bucketed" if bucketed else "flat")
+    pipe.set_layout(True)
     # stage timing: six non-negative stage times that add up to about one step
     pipe.set_stage_timing(True)
     assert pipe.step(engine="residues") == n

@@ -27,6 +27,7 @@
 #include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdint>
 #include <vector>
 
@@ -50,28 +51,62 @@ unsigned bits_for(uint64_t v) {  // bits needed for values < v
 constexpr unsigned long long kNoKey = ~0ull;
 constexpr unsigned kClsBits = 16;
 
+// Two key layouts (u64, kNoKey = all ones is the padding of every layout):
+//   flat     [ code | class (16 bits, when it fits) | p ]       sorted on the code bits (stable)
+//   bucketed [ 0 | h(code) (32) | p | class (cb bits) ]         h(code) = code * A mod 2^32 is a
+//            bijection, so h identifies the k-mer; bucket = top bbits of h (equal k-mers share a
+//            bucket); keys are sorted on bits [bucket .. 64): the zero top bit makes the padding
+//            sort last.  cb = 31 - pbits (16 at most); a class id that does not fit sends the
+//            call to the flat layout.
 struct Layout {
-    unsigned pbits;   // protein index bits
-    unsigned shift;   // code starts here: pbits (+ kClsBits when the class is in the key)
-    unsigned end_bit; // shift + code bits
-    bool cls_in_key;
+    unsigned pbits;    // protein index bits
+    unsigned cbits;    // code bits
+    unsigned shift;    // flat: code starts here
+    bool cls_in_key;   // flat: class bits between code and p
+    bool bucketed;
+    unsigned bbits;    // bucketed: bucket index bits
+    unsigned clsbits;  // bucketed: class bits (bits [0, clsbits))
+    unsigned hshift;   // bucketed: h(code) starts here (= pbits + clsbits)
+    unsigned sort_lo, sort_hi;  // radix-sorted bit range
 };
 
-Layout make_layout(uint32_t n, int k) {
-    Layout l;
+constexpr uint32_t kBucketTarget = 1024;  // mean keys per bucket
+constexpr uint32_t kHashA = 0x9E3779B1u;  // odd: code -> h(code) is a bijection of u32
+
+Layout make_layout(uint32_t n, int k, uint64_t slots, bool bucketed) {
+    Layout l{};
     l.pbits = bits_for(n);
-    const unsigned cbits = bits_for(pow21(k));
-    l.cls_in_key = l.pbits + kClsBits + cbits <= 64;
+    l.cbits = bits_for(pow21(k));
+    if (bucketed && l.pbits <= 30) {
+        unsigned bb = 1;
+        while (bb < 20 && (slots >> bb) > kBucketTarget) ++bb;  // bb + sub bits <= 32
+        l.bucketed = true;
+        l.bbits = bb;
+        l.clsbits = std::min(16u, 31u - l.pbits);
+        l.hshift = l.pbits + l.clsbits;
+        l.sort_lo = l.hshift + 32 - bb;
+        l.sort_hi = 64;
+        return l;
+    }
+    l.cls_in_key = l.pbits + kClsBits + l.cbits <= 64;
     l.shift = l.pbits + (l.cls_in_key ? kClsBits : 0);
-    l.end_bit = l.shift + cbits;
+    l.sort_lo = l.shift;
+    l.sort_hi = l.shift + l.cbits;
     return l;
 }
 
-__device__ __forceinline__ unsigned long long make_key(uint32_t code, uint16_t c, uint32_t p, unsigned pbits,
-                                                       unsigned shift, bool cls_in_key) {
-    unsigned long long x = ((unsigned long long)code << shift) | p;
-    if (cls_in_key) x |= (unsigned long long)c << pbits;
+__device__ __forceinline__ unsigned long long make_key(uint32_t code, uint16_t c, uint32_t p, const Layout& l) {
+    if (l.bucketed)
+        return ((unsigned long long)(code * kHashA) << l.hshift) | ((unsigned long long)p << l.clsbits) |
+               (c & ((1u << l.clsbits) - 1));
+    unsigned long long x = ((unsigned long long)code << l.shift) | p;
+    if (l.cls_in_key) x |= (unsigned long long)c << l.pbits;
     return x;
+}
+
+// class ids wider than the bucketed layout's class field -> flat layout
+__device__ __forceinline__ void check_class(uint16_t c, const Layout& l, uint32_t* flags) {
+    if (l.bucketed && l.clsbits < 16 && (c >> l.clsbits)) flags[1] = 1;
 }
 
 // keys of the unfiltered K(p) slots: K(p)[t] for t < |K(p)|, kNoKey for the rest of the region;
@@ -80,7 +115,8 @@ __global__ __launch_bounds__(256) void set_keys_kernel(const uint32_t* __restric
                                                        const uint32_t* __restrict__ set_len,
                                                        const uint64_t* __restrict__ res_off,
                                                        const uint16_t* __restrict__ cls, uint32_t n, uint64_t slots,
-                                                       Layout lay, unsigned long long* __restrict__ keys) {
+                                                       Layout lay, unsigned long long* __restrict__ keys,
+                                                       uint32_t* __restrict__ flags) {
     const uint32_t p = blockIdx.x;
     if (p == n) {
         for (uint64_t i = set_base(res_off[n], n) + threadIdx.x; i < slots; i += 256) keys[i] = kNoKey;
@@ -89,38 +125,51 @@ __global__ __launch_bounds__(256) void set_keys_kernel(const uint32_t* __restric
     const uint64_t b = set_base(res_off[p], p), e = set_base(res_off[p + 1], p + 1);
     const uint32_t len = set_len[p];
     const uint16_t c = cls[p];
+    if (threadIdx.x == 0) check_class(c, lay, flags);
     for (uint64_t i = b + threadIdx.x; i < e; i += 256) {
         const uint64_t o = i - b;
-        keys[i] = o < len ? make_key(set[i], c, p, lay.pbits, lay.shift, lay.cls_in_key) : kNoKey;
+        keys[i] = o < len ? make_key(set[i], c, p, lay) : kNoKey;
     }
 }
 
 // one key per window straight from the residues (Protein::new, protein.rs:82-94: window j of
-// protein p is residues [j, j+k), radix-21, first residue most significant); same slot layout
+// protein p is residues [j, j+k), radix-21, first residue most significant); same slot layout.
+// The residues are recoded once into LDS (byte -> code through an LDS copy of the table), the
+// windows are formed from LDS.
 constexpr int kResThreads = 256;
+constexpr int kResChunk = 2048;  // windows per LDS chunk
 __global__ __launch_bounds__(kResThreads) void residue_keys_kernel(const uint8_t* __restrict__ res,
                                                                    const uint64_t* __restrict__ res_off,
                                                                    const uint16_t* __restrict__ cls, uint32_t n,
                                                                    int k, uint64_t slots, Layout lay,
-                                                                   unsigned long long* __restrict__ keys) {
+                                                                   unsigned long long* __restrict__ keys,
+                                                                   uint32_t* __restrict__ flags) {
+    __shared__ uint8_t lut[256];
+    __shared__ uint8_t rc[kResChunk + kMaxK];
     const uint32_t p = blockIdx.x;
+    const int tid = threadIdx.x;
     if (p == n) {
-        for (uint64_t i = set_base(res_off[n], n) + threadIdx.x; i < slots; i += kResThreads) keys[i] = kNoKey;
+        for (uint64_t i = set_base(res_off[n], n) + tid; i < slots; i += kResThreads) keys[i] = kNoKey;
         return;
     }
+    lut[tid] = c_lut.v[tid];
     const uint64_t off = res_off[p], L = res_off[p + 1] - off;
     const uint64_t nw = L >= (uint64_t)k ? L - k + 1 : 0;
     const uint64_t b = set_base(off, p), e = set_base(res_off[p + 1], p + 1);
     const uint16_t c = cls[p];
-    for (uint64_t i = b + threadIdx.x; i < e; i += kResThreads) {
-        const uint64_t j = i - b;
-        unsigned long long x = kNoKey;
-        if (j < nw) {
+    if (tid == 0) check_class(c, lay, flags);
+    for (uint64_t i = b + nw + tid; i < e; i += kResThreads) keys[i] = kNoKey;
+    for (uint64_t c0 = 0; c0 < nw; c0 += kResChunk) {
+        const uint32_t w = (uint32_t)std::min<uint64_t>(kResChunk, nw - c0);
+        const uint32_t r = w + k - 1;
+        __syncthreads();
+        for (uint32_t t = tid; t < r; t += kResThreads) rc[t] = lut[res[off + c0 + t]];
+        __syncthreads();
+        for (uint32_t j = tid; j < w; j += kResThreads) {
             uint32_t v = 0;
-            for (int t = 0; t < k; ++t) v = v * kRadix + c_lut.v[res[off + j + t]];
-            x = make_key(v, c, p, lay.pbits, lay.shift, lay.cls_in_key);
+            for (int t = 0; t < k; ++t) v = v * kRadix + rc[j + t];
+            keys[b + c0 + j] = make_key(v, c, p, lay);
         }
-        keys[i] = x;
     }
 }
 
@@ -293,6 +342,301 @@ __global__ __launch_bounds__(1024) void reduce_stats_kernel(const unsigned long 
     }
 }
 
+// ---------------------------------------------------------------- bucketed layout ----------
+// Bucket b occupies [bstart[b], bstart[b+1]) of the keys sorted on bits [sort_lo, 64); the
+// padding starts at bstart[nb].
+__global__ void bucket_bounds_kernel(const unsigned long long* __restrict__ k, uint64_t slots, unsigned sort_lo,
+                                     uint32_t nb, uint32_t* __restrict__ bstart) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b > nb) return;
+    uint64_t lo = 0, hi = slots;  // first key whose field >= b
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if ((k[mid] >> sort_lo) < b) lo = mid + 1;
+        else hi = mid;
+    }
+    bstart[b] = (uint32_t)lo;
+}
+
+constexpr uint32_t kHeavySub = 128;  // larger sub-buckets (very frequent k-mers) -> flat layout
+constexpr int kShards = 64;          // output cursors (one per bucket residue mod kShards)
+
+template <int kThreads>
+__device__ __forceinline__ void block_scan_n(uint32_t v, uint32_t& excl, uint32_t& total, uint32_t* wave_tot) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wave_tot[w] = x;
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < kThreads / 64; ++i) {
+        const uint32_t t = wave_tot[i];
+        before += i < w ? t : 0;
+        tot += t;
+    }
+    __syncthreads();
+    excl = before + x - v;
+    total = tot;
+}
+
+// One workgroup per bucket with lo < size <= kCap.  The bucket's keys are grouped in LDS by a
+// counting sort on the next kSubBits bits of h(code) (below the bucket bits), as two u32 planes:
+// Bh = h(code), Bl = p << cb | class.  Per sub-bucket:
+//   duplicate windows of one protein (identical keys) count once (the K(p) dedup, main.rs:280-282);
+//   df = distinct proteins with the k-mer; head = first element of its k-mer in the sub-bucket;
+//   every element pairs with the later non-duplicate elements of its k-mer (vertex.rs:103-137),
+//   class test fused (mod.rs:580-587); pair key = min(p,q) * N + max(p,q).
+// Thread tid owns positions tid + e*kThreads of the grouped bucket in every phase, so its
+// per-position state stays in registers.  Output: the workgroup reserves its range on
+// cursor[b % kShards] (one agent-scope atomic) inside that shard's region; the pair sort makes
+// the order irrelevant.  Statistics -> gstats[b % kShards].  flags[0]: a bucket above the large capacity
+// or a sub-bucket above kHeavySub (the caller reruns on the flat layout).
+template <int kCap, int kThreads, int kSubBits, int kAblate = 0>
+__device__ __forceinline__ void process_bucket(
+    const uint32_t b, const unsigned long long* __restrict__ sorted, const uint32_t* __restrict__ bstart,
+    const Layout& lay, uint32_t n_prot, int require_diff, uint32_t heavy_df, bool small,
+    unsigned long long* __restrict__ out, uint64_t shard_cap, unsigned long long* __restrict__ cursor,
+    unsigned long long* __restrict__ gstats, uint32_t* __restrict__ flags, uint32_t* __restrict__ list,
+    uint32_t* __restrict__ list_count) {
+    constexpr int kE = kCap / kThreads;
+    constexpr uint32_t kSub = 1u << kSubBits;
+    constexpr int kPer = kSub / kThreads;
+    static_assert(kE * kThreads == kCap && kPer == 4, "geometry: four sub-buckets per thread");
+    __shared__ uint32_t Bh[kCap], Bl[kCap];
+    __shared__ __attribute__((aligned(16))) uint32_t H[kSub + 4];  // sub-bucket sizes, then starts
+    __shared__ uint32_t SZ[kHeavySub + 1];                           // sub-buckets per size, then starts
+    __shared__ uint8_t HS[kSub];                                     // sub-bucket sizes (<= kHeavySub)
+    __shared__ uint32_t dupw[kCap / 32];
+    __shared__ uint32_t wave_tot[kThreads / 64];
+    __shared__ uint32_t red[kThreads / 64][8];
+    __shared__ unsigned long long sbase;
+    __shared__ uint32_t heavy;
+    const uint32_t s0 = bstart[b], n = bstart[b + 1] - s0;
+    const int tid = threadIdx.x;
+    if (n == 0) return;
+    if (n > (uint32_t)kCap) {
+        if (tid == 0) {
+            if (small) list[atomicAdd(list_count, 1u)] = b;  // the large kernel takes it
+            else flags[0] = 1;                                // too big: flat layout
+        }
+        return;
+    }
+    __syncthreads();  // LDS reuse across the buckets of one workgroup
+    const unsigned hshift = lay.hshift, cb = lay.clsbits;
+    const unsigned subshift = 32 - lay.bbits - kSubBits;  // sub-hash: the h bits below the bucket
+    const uint32_t lmask = (1u << hshift) - 1, cmask = (1u << cb) - 1;
+    reinterpret_cast<uint4*>(H)[tid] = make_uint4(0, 0, 0, 0);
+    if (tid == 0) H[kSub] = 0;
+    for (uint32_t i = tid; i <= kHeavySub; i += kThreads) SZ[i] = 0;
+    for (uint32_t i = tid; i < kCap / 32; i += kThreads) dupw[i] = 0;
+    if (tid == 0) heavy = 0;
+    __syncthreads();
+    // 1. counting sort on the sub-hash: ranks from LDS atomics, offsets from one workgroup scan
+    uint32_t xh[kE], xl[kE], rk[kE];
+#pragma unroll
+    for (int e = 0; e < kE; ++e) {
+        const uint32_t i = tid + e * kThreads;
+        const unsigned long long x = i < n ? sorted[s0 + i] : 0ull;
+        xh[e] = (uint32_t)(x >> hshift);
+        xl[e] = (uint32_t)x & lmask;
+    }
+    if (kAblate == 1) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int e = 0; e < kE; ++e) v ^= xh[e] + xl[e];
+        if (v == 42) flags[3] = 1;
+        return;
+    }
+#pragma unroll
+    for (int e = 0; e < kE; ++e)
+        rk[e] = tid + e * kThreads < n ? atomicAdd(&H[(xh[e] >> subshift) & (kSub - 1)], 1u) : 0u;
+    __syncthreads();
+    // sub-buckets are laid out by size, largest first, so that the lanes of a wave scan
+    // sub-buckets of (nearly) equal size in the phases below: rank each non-empty sub-bucket in
+    // its size class, then one scan over the size classes (descending) gives the class starts
+    uint32_t c4[kPer], r4[kPer];
+    {
+        const uint4 v = reinterpret_cast<const uint4*>(H)[tid];
+        c4[0] = v.x, c4[1] = v.y, c4[2] = v.z, c4[3] = v.w;
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) {
+            if (c4[q] > kHeavySub) heavy = 1;
+            r4[q] = c4[q] && c4[q] <= kHeavySub ? atomicAdd(&SZ[c4[q]], 1u) : 0u;
+        }
+    }
+    __syncthreads();
+    if (heavy) {
+        if (tid == 0) flags[0] = 1;
+        return;
+    }
+    {
+        const uint32_t m = tid <= (int)kHeavySub ? kHeavySub - tid : 0;  // size class of this thread
+        const uint32_t v = tid <= (int)kHeavySub ? m * SZ[m] : 0u;
+        uint32_t excl, total;
+        block_scan_n<kThreads>(v, excl, total, wave_tot);
+        if (tid <= (int)kHeavySub) SZ[m] = excl;  // first position of size class m
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+        H[tid * kPer + q] = c4[q] ? SZ[c4[q]] + r4[q] * c4[q] : 0u;
+        HS[tid * kPer + q] = (uint8_t)c4[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < kE; ++e)
+        if (tid + e * kThreads < n) {
+            const uint32_t pos = H[(xh[e] >> subshift) & (kSub - 1)] + rk[e];
+            Bh[pos] = xh[e];
+            Bl[pos] = xl[e];
+        }
+    __syncthreads();
+    if (kAblate == 2) return;
+    // 2. per position: its key, sub-bucket bounds, duplicate flag
+    uint32_t s[kE], en[kE];
+#pragma unroll
+    for (int e = 0; e < kE; ++e) {
+        const uint32_t i = tid + e * kThreads;
+        s[e] = en[e] = 0;
+        if (i >= n) continue;
+        xh[e] = Bh[i];
+        xl[e] = Bl[i];
+        const uint32_t sb = (xh[e] >> subshift) & (kSub - 1);
+        s[e] = H[sb];
+        en[e] = s[e] + HS[sb];
+        for (uint32_t j = s[e]; j < i; ++j)
+            if (Bh[j] == xh[e] && Bl[j] == xl[e]) {
+                atomicOr(&dupw[i >> 5], 1u << (i & 31));
+                break;
+            }
+    }
+    __syncthreads();
+    if (kAblate == 3) return;
+    auto is_dup = [&](uint32_t j) { return (dupw[j >> 5] >> (j & 31)) & 1u; };
+    // 3. df, head, kept-partner count
+    uint32_t cnt[kE];
+    uint32_t st_sum = 0, st_dist = 0, st_rep = 0, st_cdf2 = 0, st_max = 0, st_heavy = 0, mine = 0;
+#pragma unroll
+    for (int e = 0; e < kE; ++e) {
+        const uint32_t i = tid + e * kThreads;
+        cnt[e] = 0;
+        if (i >= n || is_dup(i)) continue;
+        uint32_t f = 0, c = 0;
+        bool head = true;
+        for (uint32_t j = s[e]; j < en[e]; ++j) {
+            if (Bh[j] != xh[e]) continue;
+            if (j < i) head = false;
+            if (is_dup(j)) continue;
+            ++f;
+            if (j > i && (!require_diff || ((Bl[j] ^ xl[e]) & cmask))) ++c;
+        }
+        if (f > heavy_df) c = 0;
+        st_sum += 1;
+        if (head) {
+            st_dist += 1;
+            st_rep += f >= 2;
+            if (f <= heavy_df) st_cdf2 += f * (f - 1) / 2;
+            else st_heavy += f;
+            st_max = max(st_max, f);
+        }
+        cnt[e] = c;
+        mine += c;
+    }
+    if (kAblate == 4) {
+        if (mine == 0xFFFFFFFF) flags[3] = 1;
+        return;
+    }
+    // 4. reserve the workgroup's output range, write the pair keys
+    uint32_t excl, total;
+    block_scan_n<kThreads>(mine, excl, total, wave_tot);
+    const uint32_t shard = b % kShards;
+    if (tid == 0) sbase = total ? atomicAdd(&cursor[shard], (unsigned long long)total) : 0ull;
+    __syncthreads();
+    if (mine && kAblate != 5) {
+        unsigned long long pos = sbase + excl;
+        unsigned long long* dst = out + (uint64_t)shard * shard_cap;
+#pragma unroll
+        for (int e = 0; e < kE; ++e) {
+            if (!cnt[e]) continue;
+            const uint32_t i = tid + e * kThreads;
+            const uint32_t p = xl[e] >> cb;
+            for (uint32_t j = i + 1; j < en[e]; ++j) {
+                if (Bh[j] != xh[e] || is_dup(j)) continue;
+                const uint32_t lj = Bl[j];
+                if (require_diff && !((lj ^ xl[e]) & cmask)) continue;
+                const uint32_t q = lj >> cb;
+                if (pos < shard_cap) dst[pos] = (unsigned long long)min(p, q) * n_prot + max(p, q);
+                ++pos;
+            }
+        }
+    }
+    // 5. statistics (u32 per workgroup; the bucket is at most kCap keys)
+    uint32_t sv[kStN] = {st_sum, st_dist, st_rep, st_cdf2, st_max, st_heavy, mine};
+#pragma unroll
+    for (int t = 0; t < kStN; ++t) {
+        uint32_t v = sv[t];
+        for (int sh = 32; sh > 0; sh >>= 1) {
+            const uint32_t u = __shfl_down(v, sh);
+            v = t == kStMaxDf ? max(u, v) : u + v;
+        }
+        if ((tid & 63) == 0) red[tid >> 6][t] = v;
+    }
+    __syncthreads();
+    if (tid < kStN) {
+        uint32_t v = red[0][tid];
+        for (int w = 1; w < kThreads / 64; ++w) v = tid == kStMaxDf ? max(v, red[w][tid]) : v + red[w][tid];
+        unsigned long long* g = gstats + (uint64_t)(b % kShards) * 8 + tid;  // sharded: no hot word
+        if (tid == kStMaxDf) atomicMax(g, (unsigned long long)v);
+        else if (v) atomicAdd(g, (unsigned long long)v);
+    }
+}
+
+template <int kCap, int kThreads, int kSubBits, int kAblate = 0>
+__global__ __launch_bounds__(kThreads) void bucket_small_kernel(
+    const unsigned long long* __restrict__ sorted, const uint32_t* __restrict__ bstart, Layout lay,
+    uint32_t n_prot, int require_diff, uint32_t heavy_df, unsigned long long* __restrict__ out, uint64_t shard_cap,
+    unsigned long long* __restrict__ cursor, unsigned long long* __restrict__ gstats, uint32_t* __restrict__ flags,
+    uint32_t* __restrict__ list, uint32_t* __restrict__ list_count) {
+    process_bucket<kCap, kThreads, kSubBits, kAblate>(blockIdx.x, sorted, bstart, lay, n_prot, require_diff,
+                                                      heavy_df, true, out, shard_cap, cursor, gstats, flags, list,
+                                                      list_count);
+}
+
+// the buckets the small kernel listed (above its capacity), a grid-stride loop over the list
+template <int kCap, int kThreads, int kSubBits>
+__global__ __launch_bounds__(kThreads) void bucket_large_kernel(
+    const unsigned long long* __restrict__ sorted, const uint32_t* __restrict__ bstart, Layout lay,
+    uint32_t n_prot, int require_diff, uint32_t heavy_df, unsigned long long* __restrict__ out, uint64_t shard_cap,
+    unsigned long long* __restrict__ cursor, unsigned long long* __restrict__ gstats, uint32_t* __restrict__ flags,
+    uint32_t* __restrict__ list, const uint32_t* __restrict__ list_count) {
+    const uint32_t m = *list_count;
+    for (uint32_t i = blockIdx.x; i < m; i += gridDim.x)
+        process_bucket<kCap, kThreads, kSubBits>(list[i], sorted, bstart, lay, n_prot, require_diff, heavy_df, false,
+                                                 out, shard_cap, cursor, gstats, flags, nullptr, nullptr);
+}
+
+// shard regions -> one contiguous array (shard order)
+__global__ void gather_shards_kernel(const unsigned long long* __restrict__ src, uint64_t shard_cap,
+                                     const unsigned long long* __restrict__ cursor,
+                                     unsigned long long* __restrict__ dst) {
+    const int s = blockIdx.y;
+    unsigned long long off = 0;
+    for (int t = 0; t < s; ++t) off += cursor[t];
+    const unsigned long long m = cursor[s];
+    for (unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; i < m;
+         i += (unsigned long long)gridDim.x * blockDim.x)
+        dst[off + i] = src[(uint64_t)s * shard_cap + i];
+}
+
+constexpr int kBucketSmallCap = 2048, kBucketSmallThreads = 256, kBucketSmallSub = 10;
+constexpr int kBucketLargeCap = 8192, kBucketLargeThreads = 1024, kBucketLargeSub = 12;
+
+
 // (pair key, w) runs -> edges with w >= min_shared, canonical order kept
 __global__ void emit_edges_kernel(const unsigned long long* __restrict__ uniq, const uint32_t* __restrict__ w,
                                   const uint32_t* __restrict__ nuniq, uint32_t n_prot, uint32_t min_shared,
@@ -340,14 +684,18 @@ struct Grow {
 
 struct kmp_postings {
     Grow<unsigned long long> keys, sorted, inc, inc_sorted, uniq, bstats, btot, boff;
-    Grow<uint32_t> w, keep, pos, small, cnt;
+    Grow<uint32_t> w, keep, pos, small, cnt, flags;  // flags: [0] bucket overflow, [1] class width, [2] list count
     Grow<char> tmp;
     bool timing = false;
+    bool bucketed = true;       // try the bucketed layout first
+    bool last_bucketed = false; // layout the last call ran on
+    uint64_t shard_cap = 0;     // bucketed: capacity of each output shard region
+    int ablate = getenv("KMP_BUCKET_ABLATE") ? atoi(getenv("KMP_BUCKET_ABLATE")) : 0;  // diagnostics
     hipEvent_t ev[KMP_POSTINGS_STAGES + 1] = {};
     ~kmp_postings() {
         keys.release(); sorted.release(); inc.release(); inc_sorted.release(); uniq.release();
         bstats.release(); btot.release(); boff.release();
-        w.release(); keep.release(); pos.release(); small.release(); cnt.release(); tmp.release();
+        w.release(); keep.release(); pos.release(); small.release(); cnt.release(); flags.release(); tmp.release();
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
     }
@@ -364,22 +712,30 @@ struct kmp_postings {
 
 namespace {
 
-// Everything after the keys are in ws->keys: stable code sort, count/scan/write, pair sort,
-// run-length encode, min_shared filter, unpack.  Stage marks: 1 keys done, 2 code sort,
-// 3 count + offsets, 4 write, 5 pair sort, 6 run-length encode + emit.
-int postings_core(kmp_postings* ws, uint64_t slots, const Layout& lay, const uint16_t* d_class, uint32_t n,
-                  uint32_t heavy_df, uint32_t min_shared, int require_class_diff, uint32_t* d_p, uint32_t* d_q,
-                  uint32_t* d_w, uint64_t cap, uint64_t* n_edges, kmp_postings_stats* stats, hipStream_t st) {
-    // 1. stable sort on the code bits: runs = distinct k-mers, proteins ascending inside a run
+void fill_stats(kmp_postings_stats* stats, const unsigned long long* acc) {
+    if (!stats) return;
+    stats->sum_S = acc[kStSumS];
+    stats->distinct = acc[kStDistinct];
+    stats->repeat = acc[kStRepeat];
+    stats->sum_cdf2_light = acc[kStCdf2];
+    stats->max_df = acc[kStMaxDf];
+    stats->heavy_entries = acc[kStHeavy];
+    stats->incidences = acc[kStInc];
+}
+
+// Flat front end (keys already in ws->keys): stable code sort, count pass, offsets, write pass.
+// Marks 2 (sort), 3 (count + offsets), 4 (write).  On return ws->inc holds *n_inc pair keys.
+int front_flat(kmp_postings* ws, uint64_t slots, const Layout& lay, const uint16_t* d_class, uint32_t n,
+               uint32_t heavy_df, int require_class_diff, unsigned long long* n_inc, kmp_postings_stats* stats,
+               hipStream_t st) {
     size_t t_sort = 0;
-    PG(rocprim::radix_sort_keys(nullptr, t_sort, ws->keys.p, ws->sorted.p, (size_t)slots, lay.shift, lay.end_bit,
+    PG(rocprim::radix_sort_keys(nullptr, t_sort, ws->keys.p, ws->sorted.p, (size_t)slots, lay.sort_lo, lay.sort_hi,
                                 st));
     PG(ws->tmp.reserve(std::max(t_sort, ws->tmp.n)));
-    PG(rocprim::radix_sort_keys(ws->tmp.p, t_sort, ws->keys.p, ws->sorted.p, (size_t)slots, lay.shift, lay.end_bit,
-                                st));
+    PG(rocprim::radix_sort_keys(ws->tmp.p, t_sort, ws->keys.p, ws->sorted.p, (size_t)slots, lay.sort_lo,
+                                lay.sort_hi, st));
     ws->mark(2, st);
 
-    // 2. count pass (+ df statistics), workgroup offsets
     const uint64_t nb64 = (slots + kExpChunk - 1) / kExpChunk;
     if (nb64 > 0x7FFFFFFFull) return KMP_EINVAL;
     const uint32_t nb = (uint32_t)nb64;
@@ -407,37 +763,119 @@ int postings_core(kmp_postings* ws, uint64_t slots, const Layout& lay, const uin
     unsigned long long acc[kStN];
     PG(hipMemcpyAsync(acc, acc_d, sizeof acc, hipMemcpyDeviceToHost, st));
     PG(hipStreamSynchronize(st));
-    const unsigned long long n_inc = acc[kStInc];
-    if (stats) {
-        stats->sum_S = acc[kStSumS];
-        stats->distinct = acc[kStDistinct];
-        stats->repeat = acc[kStRepeat];
-        stats->sum_cdf2_light = acc[kStCdf2];
-        stats->max_df = acc[kStMaxDf];
-        stats->heavy_entries = acc[kStHeavy];
-        stats->incidences = n_inc;
+    fill_stats(stats, acc);
+    *n_inc = acc[kStInc];
+    if (*n_inc && *n_inc <= 0xFFFFFFFFull) {
+        PG(ws->inc.reserve(*n_inc));
+        if (lay.cls_in_key)
+            expand_kernel<true, true><<<nb, kExpThreads, 0, st>>>(ws->sorted.p, slots, lay, d_class, n,
+                                                                  require_class_diff, heavy_df, ws->cnt.p, nullptr,
+                                                                  nullptr, ws->boff.p, ws->inc.p);
+        else
+            expand_kernel<true, false><<<nb, kExpThreads, 0, st>>>(ws->sorted.p, slots, lay, d_class, n,
+                                                                   require_class_diff, heavy_df, ws->cnt.p, nullptr,
+                                                                   nullptr, ws->boff.p, ws->inc.p);
     }
+    ws->mark(4, st);
+    return KMP_OK;
+}
+
+// Bucketed front end (keys in ws->keys, flags[0..1] written by the key kernel): sort on the
+// bucket field, bucket bounds, LDS group + expand per bucket into kShards regions, gather into
+// ws->inc.  Marks 2 (sort), 3 (group + expand), 4 (gather).  *fallback = true when a bucket
+// does not fit or a class id is too wide (the caller reruns on the flat layout).
+int front_bucketed(kmp_postings* ws, uint64_t slots, const Layout& lay, uint32_t n, uint32_t heavy_df,
+                   int require_class_diff, unsigned long long* n_inc, bool* fallback, kmp_postings_stats* stats,
+                   hipStream_t st) {
+    *fallback = false;
+    size_t t_sort = 0;
+    PG(rocprim::radix_sort_keys(nullptr, t_sort, ws->keys.p, ws->sorted.p, (size_t)slots, lay.sort_lo, lay.sort_hi,
+                                st));
+    PG(ws->tmp.reserve(std::max(t_sort, ws->tmp.n)));
+    PG(rocprim::radix_sort_keys(ws->tmp.p, t_sort, ws->keys.p, ws->sorted.p, (size_t)slots, lay.sort_lo,
+                                lay.sort_hi, st));
+    ws->mark(2, st);
+    const uint32_t nb = 1u << lay.bbits;
+    PG(ws->cnt.reserve(2 * (uint64_t)nb + 2));  // bucket starts, large-bucket list + its count
+    PG(ws->bstats.reserve(kShards * 8 + kShards));
+    uint32_t* bstart = ws->cnt.p;
+    uint32_t* list = ws->cnt.p + nb + 1;
+    uint32_t* list_count = ws->flags.p + 2;
+    uint32_t* flags = ws->flags.p;
+    unsigned long long* gstats = ws->bstats.p;          // kShards x 8 (kSt* slots)
+    unsigned long long* cursor = gstats + kShards * 8;  // kShards
+    bucket_bounds_kernel<<<(nb + 1 + 255) / 256, 256, 0, st>>>(ws->sorted.p, slots, lay.sort_lo, nb, bstart);
+    if (ws->shard_cap == 0) ws->shard_cap = slots / 2 / kShards + 4096;
+    for (int attempt = 0; attempt < 3; ++attempt) {
+        PG(ws->inc_sorted.reserve(ws->shard_cap * kShards));  // shard regions
+        PG(hipMemsetAsync(gstats, 0, (kShards * 8 + kShards) * sizeof(unsigned long long), st));
+        PG(hipMemsetAsync(list_count, 0, sizeof(uint32_t), st));
+#define KMP_SMALL(A)                                                                                          \
+    bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallSub, A>                             \
+        <<<nb, kBucketSmallThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,     \
+                                             ws->inc_sorted.p, ws->shard_cap, cursor, gstats, flags, list, list_count)
+        switch (ws->ablate) {  // diagnostics (KMP_BUCKET_ABLATE): phase cut-offs, results invalid
+            case 1: KMP_SMALL(1); break;
+            case 2: KMP_SMALL(2); break;
+            case 3: KMP_SMALL(3); break;
+            case 4: KMP_SMALL(4); break;
+            case 5: KMP_SMALL(5); break;
+            default: KMP_SMALL(0);
+        }
+#undef KMP_SMALL
+        bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeSub>
+            <<<256, kBucketLargeThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
+                                                  ws->inc_sorted.p, ws->shard_cap, cursor, gstats, flags, list,
+                                                  list_count);
+        ws->mark(3, st);
+        unsigned long long g[kShards * 8 + kShards];
+        uint32_t h_flags[2] = {0, 0};
+        PG(hipMemcpyAsync(g, gstats, sizeof g, hipMemcpyDeviceToHost, st));
+        PG(hipMemcpyAsync(h_flags, flags, sizeof h_flags, hipMemcpyDeviceToHost, st));
+        PG(hipStreamSynchronize(st));
+        if (h_flags[0] || h_flags[1]) {
+            *fallback = true;
+            return KMP_OK;
+        }
+        unsigned long long acc[kStN + kShards] = {};
+        for (int sh = 0; sh < kShards; ++sh) {
+            for (int t = 0; t < kStN; ++t)
+                acc[t] = t == kStMaxDf ? std::max(acc[t], g[sh * 8 + t]) : acc[t] + g[sh * 8 + t];
+            acc[kStN + sh] = g[kShards * 8 + sh];
+        }
+        fill_stats(stats, acc);
+        *n_inc = acc[kStInc];
+        unsigned long long most = 0;
+        for (int s = 0; s < kShards; ++s) most = std::max(most, acc[kStN + s]);
+        if (most <= ws->shard_cap) {
+            if (*n_inc > 0xFFFFFFFFull) return KMP_ENOMEM;
+            PG(ws->inc.reserve(std::max<unsigned long long>(1, *n_inc)));
+            if (*n_inc) {
+                const uint32_t gx = (uint32_t)std::min<uint64_t>((most + 255) / 256, 1024);
+                gather_shards_kernel<<<dim3(gx, kShards), 256, 0, st>>>(ws->inc_sorted.p, ws->shard_cap, cursor,
+                                                                        ws->inc.p);
+            }
+            ws->mark(4, st);
+            return KMP_OK;
+        }
+        ws->shard_cap = most + most / 4 + 4096;  // grow the regions and rerun the expansion
+    }
+    return KMP_EDEVICE;
+}
+
+// Shared tail: sort the pair keys, run-length encode -> (pair, w) in canonical order, keep
+// w >= min_shared, unpack.  Marks 5 (pair sort) and 6 (encode + emit).
+int tail(kmp_postings* ws, unsigned long long n_inc, uint32_t n, uint32_t min_shared, uint32_t* d_p, uint32_t* d_q,
+         uint32_t* d_w, uint64_t cap, uint64_t* n_edges, kmp_postings_stats* stats, hipStream_t st) {
+    if (stats) stats->incidences = n_inc;
     if (n_inc == 0) {
-        for (int s = 4; s <= KMP_POSTINGS_STAGES; ++s) ws->mark(s, st);
+        ws->mark(5, st);
+        ws->mark(6, st);
         return KMP_OK;
     }
     if (n_inc > 0xFFFFFFFFull) return KMP_ENOMEM;  // run-length counts are u32
-
-    // 3. write pass
-    PG(ws->inc.reserve(n_inc));
-    PG(ws->inc_sorted.reserve(n_inc));
-    if (lay.cls_in_key)
-        expand_kernel<true, true><<<nb, kExpThreads, 0, st>>>(ws->sorted.p, slots, lay, d_class, n, require_class_diff,
-                                                              heavy_df, ws->cnt.p, nullptr, nullptr, ws->boff.p,
-                                                              ws->inc.p);
-    else
-        expand_kernel<true, false><<<nb, kExpThreads, 0, st>>>(ws->sorted.p, slots, lay, d_class, n,
-                                                               require_class_diff, heavy_df, ws->cnt.p, nullptr,
-                                                               nullptr, ws->boff.p, ws->inc.p);
-    ws->mark(4, st);
-
-    // 4. sort pair keys p*N+q, run-length encode -> (pair, w) in canonical order
     const unsigned pair_bits = bits_for((uint64_t)n * n);
+    PG(ws->inc_sorted.reserve(n_inc));
     PG(ws->uniq.reserve(n_inc));
     PG(ws->w.reserve(n_inc));
     PG(ws->small.reserve(16));
@@ -458,7 +896,6 @@ int postings_core(kmp_postings* ws, uint64_t slots, const Layout& lay, const uin
     ws->mark(5, st);
     PG(rocprim::run_length_encode(ws->tmp.p, t3, ws->inc_sorted.p, (unsigned int)n_inc, ws->uniq.p, ws->w.p,
                                   ws->small.p + 1, st));
-    // 5. keep w >= min_shared (order preserved) and unpack
     const uint32_t kb = (uint32_t)std::min<uint64_t>((n_inc + 255) / 256, 8192);
     uint32_t h_uniq = 0, last_pos = 0, last_keep = 0;
     if (filter_w) {
@@ -499,6 +936,42 @@ int postings_args(kmp_postings* ws, int k, uint64_t* n_edges, kmp_postings_stats
     return KMP_OK;
 }
 
+// Both entry points: keys from `make_keys(layout)`, bucketed front end (flat on fallback), tail.
+template <class MakeKeys>
+int run_postings(kmp_postings* ws, MakeKeys make_keys, uint32_t n, int k, uint64_t slots, const uint16_t* d_class,
+                 uint32_t heavy_df, uint32_t min_shared, int require_class_diff, uint32_t* d_p, uint32_t* d_q,
+                 uint32_t* d_w, uint64_t cap, uint64_t* n_edges, kmp_postings_stats* stats, hipStream_t st) {
+    if (heavy_df < 2) heavy_df = 2;
+    if (min_shared < 1) min_shared = 1;
+    PG(ws->keys.reserve(slots));
+    PG(ws->sorted.reserve(slots));
+    PG(ws->flags.reserve(4));
+    PG(hipMemsetAsync(ws->flags.p, 0, 4 * sizeof(uint32_t), st));
+    unsigned long long n_inc = 0;
+    Layout lay = make_layout(n, k, slots, ws->bucketed);
+    bool fallback = true;
+    if (lay.bucketed) {
+        ws->mark(0, st);
+        make_keys(lay);
+        ws->mark(1, st);
+        int rc = front_bucketed(ws, slots, lay, n, heavy_df, require_class_diff, &n_inc, &fallback, stats, st);
+        if (rc != KMP_OK) return rc;
+    }
+    if (fallback) {
+        lay = make_layout(n, k, slots, false);
+        if (lay.sort_hi > 64) return KMP_EINVAL;
+        ws->mark(0, st);
+        make_keys(lay);
+        ws->mark(1, st);
+        int rc = front_flat(ws, slots, lay, d_class, n, heavy_df, require_class_diff, &n_inc, stats, st);
+        if (rc != KMP_OK) return rc;
+    }
+    ws->last_bucketed = !fallback;
+    int rc = tail(ws, n_inc, n, min_shared, d_p, d_q, d_w, cap, n_edges, stats, st);
+    if (rc == KMP_OK) finish_timing(ws, stats, st);
+    return rc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -519,6 +992,14 @@ int kmp_postings_set_timing(kmp_postings* ws, int enable) {
     return KMP_OK;
 }
 
+int kmp_postings_set_layout(kmp_postings* ws, int bucketed) {
+    if (!ws) return KMP_EINVAL;
+    ws->bucketed = bucketed != 0;
+    return KMP_OK;
+}
+
+int kmp_postings_last_layout(const kmp_postings* ws) { return ws && ws->last_bucketed ? 1 : 0; }
+
 int kmp_dev_pairs_postings(kmp_postings* ws, const uint32_t* d_set, const uint32_t* d_set_len,
                            const uint64_t* d_res_off, const uint16_t* d_class, uint32_t n, int k, uint64_t slots,
                            uint32_t heavy_df, uint32_t min_shared, int require_class_diff, uint32_t* d_p,
@@ -527,18 +1008,13 @@ int kmp_dev_pairs_postings(kmp_postings* ws, const uint32_t* d_set, const uint32
     int rc = postings_args(ws, k, n_edges, stats, d_p, d_q, d_w, cap);
     if (rc != KMP_OK || n < 2) return rc;
     if (!d_set || !d_set_len || !d_res_off || !d_class) return KMP_EINVAL;
-    const Layout lay = make_layout(n, k);
-    if (lay.end_bit > 64) return KMP_EINVAL;
     hipStream_t st = as_stream(stream);
-    PG(ws->keys.reserve(slots));
-    PG(ws->sorted.reserve(slots));
-    ws->mark(0, st);
-    set_keys_kernel<<<n + 1, 256, 0, st>>>(d_set, d_set_len, d_res_off, d_class, n, slots, lay, ws->keys.p);
-    ws->mark(1, st);
-    rc = postings_core(ws, slots, lay, d_class, n, heavy_df < 2 ? 2 : heavy_df, min_shared < 1 ? 1 : min_shared,
-                       require_class_diff, d_p, d_q, d_w, cap, n_edges, stats, st);
-    if (rc == KMP_OK) finish_timing(ws, stats, st);
-    return rc;
+    auto keys = [&](const Layout& lay) {
+        set_keys_kernel<<<n + 1, 256, 0, st>>>(d_set, d_set_len, d_res_off, d_class, n, slots, lay, ws->keys.p,
+                                               ws->flags.p);
+    };
+    return run_postings(ws, keys, n, k, slots, d_class, heavy_df, min_shared, require_class_diff, d_p, d_q, d_w, cap,
+                        n_edges, stats, st);
 }
 
 int kmp_dev_pairs_residues(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off,
@@ -548,18 +1024,13 @@ int kmp_dev_pairs_residues(kmp_postings* ws, const uint8_t* d_res, const uint64_
     int rc = postings_args(ws, k, n_edges, stats, d_p, d_q, d_w, cap);
     if (rc != KMP_OK || n < 2) return rc;
     if (!d_res || !d_res_off || !d_class) return KMP_EINVAL;
-    const Layout lay = make_layout(n, k);
-    if (lay.end_bit > 64) return KMP_EINVAL;
     hipStream_t st = as_stream(stream);
-    PG(ws->keys.reserve(slots));
-    PG(ws->sorted.reserve(slots));
-    ws->mark(0, st);
-    residue_keys_kernel<<<n + 1, kResThreads, 0, st>>>(d_res, d_res_off, d_class, n, k, slots, lay, ws->keys.p);
-    ws->mark(1, st);
-    rc = postings_core(ws, slots, lay, d_class, n, heavy_df < 2 ? 2 : heavy_df, min_shared < 1 ? 1 : min_shared,
-                       require_class_diff, d_p, d_q, d_w, cap, n_edges, stats, st);
-    if (rc == KMP_OK) finish_timing(ws, stats, st);
-    return rc;
+    auto keys = [&](const Layout& lay) {
+        residue_keys_kernel<<<n + 1, kResThreads, 0, st>>>(d_res, d_res_off, d_class, n, k, slots, lay, ws->keys.p,
+                                                           ws->flags.p);
+    };
+    return run_postings(ws, keys, n, k, slots, d_class, heavy_df, min_shared, require_class_diff, d_p, d_q, d_w, cap,
+                        n_edges, stats, st);
 }
 
 }  // extern "C"

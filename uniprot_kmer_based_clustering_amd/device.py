@@ -214,6 +214,13 @@ class DevicePipeline:
         """Per-stage HIP-event times of the postings engine into postings_stats.stage_ms."""
         check(lib().kmp_postings_set_timing(self._workspace(), int(enable)), "kmp_postings_set_timing")
 
+    def set_layout(self, bucketed: bool = True) -> None:
+        """Postings key layout: bucketed (LDS group + expand per hash bucket) or flat."""
+        check(lib().kmp_postings_set_layout(self._workspace(), int(bucketed)), "kmp_postings_set_layout")
+
+    def last_layout(self) -> str:
+        return "bucketed" if lib().kmp_postings_last_layout(self._workspace()) else "flat"
+
     def postings(self, min_shared: int = 1, require_class_diff: bool = True,
                  heavy_df: int = 0xFFFFFFFF, from_residues: bool = False) -> int:
         """Postings engine: canonical edges into ep/eq/ew (syncs).  Reads the K(p) slots
