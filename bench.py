@@ -1,13 +1,14 @@
 """Benchmark of the k-mer pair path (BASELINE.json metric: protein pairs/sec + edges/sec,
 100k x 300 aa synthetic proteins, k = 7, 1/2/4/8 MI355X).
 
-One step = one pass of the hot path over the resident batch: per-protein k-mer sets
-(extract + sort + dedup), repeat filter, pair planning, the tiled pair kernel over the whole
-N x N upper triangle, and the canonical (p, q) edge sort — from packed residues resident in
-HBM to the canonical edge list resident in HBM (rank 0).  Inputs are synthetic (SURVEY.md §8d,
-config 3: N = 100,000, seed 3, len ~ N(300, 30^2), k = 7).
+One step = one pass of the hot path over the resident batch, packed residues in HBM ->
+canonical (p, q, w) edge list in HBM: k-mer windows (radix-21 codes), the grouping of equal
+k-mers (the reference's df pass), duplicate-window removal (K(p) dedup), the Σ C(df,2)
+(k-mer, pair) incidence expansion with the AMR class filter, and the per-pair reduction to
+w = |K(p) ∩ K(q)| in canonical order (Graph::new + remove_uninteresting_edges + combine_edges).
+Inputs are synthetic (N = 100,000, seed 3, len ~ N(300, 30^2), k = 7).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--engine residues|postings|tiles]
   N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
 from __future__ import annotations
@@ -23,7 +24,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 
 CONFIGS = {
     # name: (N, seed, length law, k)
@@ -35,17 +36,19 @@ CONFIGS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="config3", choices=sorted(CONFIGS))
+    ap.add_argument("--engine", default="residues", choices=["residues", "postings", "tiles"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="oracle threads (0: min(16, cores))")
     return ap.parse_args()
 
 
 def cpu_baseline(proteins, k, threads):
-    """The reference algorithm restated in C (oracle/, posting-list expansion + class filter +
-    per-pair collapse), timed on this host over the full workload."""
+    """The reference algorithm restated in C (oracle/: windows, per-protein sort + dedup, df,
+    Σ C(df,2) posting-list expansion, class filter, per-pair collapse), timed on this host over
+    the full workload (about 1 s at 16 threads)."""
     from oracle.oracle import Oracle
     t0 = time.perf_counter()
     o = Oracle(proteins.residues, proteins.offsets, proteins.class_id, k=k, threads=threads)
@@ -53,9 +56,22 @@ def cpu_baseline(proteins, k, threads):
     dt = time.perf_counter() - t0
     n = proteins.n
     return {"value": n * (n - 1) / 2 / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
-            "sample": f"full workload ({n} proteins, k={k}): windows, sets, df, Σ C(df,2) "
-                      f"posting-list expansion, class filter, per-pair collapse; {dt:.2f} s",
+            "sample": f"full workload ({n} proteins, k={k}): windows, K(p) sort+dedup, df, Σ C(df,2) "
+                      f"posting-list expansion, class filter, per-pair collapse; one run, {dt:.2f} s",
             "seconds": dt, "edges": int(len(p))}
+
+
+def stage_bytes(n_res, slots, n_inc, n_edges, n_uniq):
+    """Algorithmic HBM bytes of each postings stage (one read of every input, one write of
+    every output)."""
+    return {
+        "keys": n_res + 8 * slots,                      # residues in, one u64 key per slot out
+        "code_sort": 16 * slots,                        # keys read once + written once
+        "count": 8 * slots + 8 * n_inc,                 # bucketed: keys in, pair keys out
+        "write": 16 * n_inc,                            # shard gather (bucketed) / write pass (flat)
+        "pair_sort": 16 * n_inc,                        # pair keys read once + written once
+        "rle_emit": 8 * n_inc + 12 * n_uniq + 12 * n_edges,
+    }
 
 
 def main():
@@ -64,16 +80,16 @@ def main():
     import torch.distributed as dist
 
     import uniprot_kmer_based_clustering_amd as K
+    from uniprot_kmer_based_clustering_amd import _lib
     from uniprot_kmer_based_clustering_amd.device import DevicePipeline
     from uniprot_kmer_based_clustering_amd.dist import distributed_step
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            print("run N>1 under torch.distributed.run (one process per GPU)", file=sys.stderr)
-            sys.exit(2)
+    if world != args.gpus and world == 1 and args.gpus > 1:
+        print("run N>1 under torch.distributed.run (one process per GPU)", file=sys.stderr)
+        sys.exit(2)
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -82,53 +98,40 @@ def main():
     proteins = K.synth(n, seed, law)
     pipe = DevicePipeline(proteins, k, f"cuda:{local}")
     torch.cuda.synchronize()
+    postings = args.engine in ("residues", "postings")
 
-    ev_pairs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                for _ in range(args.steps)]
-
-    def one_step(i=None):
-        timers = {"pairs": ev_pairs[i]} if i is not None else None
+    def one_step():
         if world > 1:
-            return distributed_step(pipe, rank, world, timers=timers)
-        pipe.build_sets()
-        pipe.filter()
-        pipe.plan()
-        if timers:
-            timers["pairs"][0].record()
-        m = pipe.pairs()
-        if timers:
-            timers["pairs"][1].record()
-        pipe.sort(m)
-        return m
+            return distributed_step(pipe, rank, world, engine=args.engine)
+        return pipe.step(engine=args.engine)
 
     for _ in range(args.warmup):
         one_step()
+    stage_sum = None
+    if postings and world == 1:
+        pipe.set_stage_timing(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        n_edges = one_step(i)
+    for _ in range(args.steps):
+        n_edges = one_step()
+        if postings and world == 1:
+            st = np.array(pipe.postings_stats.stage_ms[:], dtype=np.float64)
+            stage_sum = st if stage_sum is None else stage_sum + st
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    if postings and world == 1:
+        pipe.set_stage_timing(False)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
-    pair_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_pairs]))
     ms = dt / args.steps * 1e3
     pairs_total = n * (n - 1) / 2
-    rep_len = pipe.rep_len_host.astype(np.int64)
-    set_len = pipe.set_len[:n].cpu().numpy().astype(np.int64)
-    # algorithmic bytes of this rank's pair launches (4·(S_p + S_q) per pair
-    # over the sets the kernel intersects, the repeat-filtered K(p)); rank share by item cost
-    b_alg_all = 4.0 * (n - 1) * rep_len.sum()
-    share = 1.0 / world
-    achieved = b_alg_all * share / (pair_ms * 1e-3) / 1e9
-
     out = None
     if rank == 0:
         out = {
@@ -143,17 +146,35 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "u32",
-            "data": "synthetic (SURVEY.md §8d generator, seeded; random families)",
+            "data": "synthetic (SURVEY.md §8d generator, seeded; protein families, 15 AMR classes)",
             "config": {"workload": f"{args.config}: N={n}, seed={seed}, len~N(300,30^2), k={k}",
                        "proteins": n, "k": k, "pairs": int(pairs_total), "edges": int(n_edges),
-                       "parallelism": f"pair-space tiles x{world}"},
+                       "engine": args.engine,
+                       "parallelism": "single GPU" if world == 1 else f"k-mer buckets x{world}"},
             "edges_per_s": n_edges / (dt / args.steps),
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "pair_kernel", "kernel_ms": pair_ms,
-                         "alg_bytes_per_launch": b_alg_all * share,
-                         "alg_bytes_unfiltered_sets": 4.0 * (n - 1) * set_len.sum() * share},
         }
+        if stage_sum is not None:
+            ps = pipe.postings_stats.as_dict()
+            slots = int(_lib.lib().kmp_set_capacity(n, int(proteins.offsets[-1])))
+            byts = stage_bytes(int(proteins.offsets[-1]), slots, ps["incidences"], n_edges, ps["pairs"])
+            stage_ms = dict(zip(_lib.POSTINGS_STAGE_NAMES, (stage_sum / args.steps).tolist()))
+            stages = {s: {"ms": stage_ms[s], "alg_bytes": byts[s],
+                          "GBs": byts[s] / (stage_ms[s] * 1e-3) / 1e9 if stage_ms[s] > 0 else None}
+                      for s in stage_ms}
+            dom = max(stage_ms, key=stage_ms.get)
+            ach = stages[dom]["GBs"]
+            out["roofline"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": ach / HBM_PEAK_GBS, "traffic": None, "kernel": dom,
+                               "kernel_ms": stage_ms[dom], "alg_bytes_per_launch": byts[dom],
+                               "layout": pipe.last_layout(), "stages": stages,
+                               "step_alg_bytes": sum(byts.values()),
+                               "step_GBs": sum(byts.values()) / (ms * 1e-3) / 1e9}
+            # SURVEY.md §8d model: 4·(S_p + S_q) bytes per pair, i.e. a merge-intersection of every
+            # pair's sets; the postings engine never touches non-sharing pairs, so this is an
+            # effective figure far above the HBM peak
+            b_model = 4.0 * (n - 1) * ps["sum_S"]
+            out["roofline"]["pairs_model_GBs"] = b_model / (ms * 1e-3) / 1e9
+            out["postings_stats"] = ps
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         out["cpu_baseline"] = cpu_baseline(proteins, k, threads)

@@ -270,6 +270,35 @@ int kmp_dev_pairs_residues(kmp_postings* ws, const uint8_t* d_res, const uint64_
                            uint32_t min_shared, int require_class_diff, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w,
                            uint64_t cap, uint64_t* n_edges, kmp_postings_stats* stats, void* stream);
 
+/* Multi-GPU split of the postings engine (one process per GPU; dist.py does the exchanges).
+ * K-mer buckets are split into `parts` contiguous ranges (part j = buckets [j*nb/parts,
+ * (j+1)*nb/parts)), proteins into contiguous p ranges (part j = p in [ceil(j*N/parts),
+ * ceil((j+1)*N/parts))).
+ *   1. kmp_dev_keys_part: keys of the k-mer windows of proteins [lo, hi) (their slots
+ *      [slot_lo, slot_hi) = [kmp_set_base(off[lo], lo), kmp_set_base(off[hi], hi))), sorted by
+ *      bucket into d_out; part_counts[j] = keys bound for bucket part j (they are contiguous, in
+ *      part order, at the front of d_out).  slots = kmp_set_capacity(N, ΣL) of the whole batch
+ *      (it fixes the key layout, identical on every rank).
+ *   2. all-to-all of the keys; kmp_dev_pairs_keys on the m received keys: group + expand
+ *      (the bucketed engine), the n_inc pair keys p*N+q sorted into d_out (KMP_EOVERFLOW with
+ *      *n_inc set if out_cap is smaller); part_counts[j] = pair keys of p-range part j.
+ *   3. all-to-all of the pair keys; kmp_dev_edges_pairkeys: the received runs -> the edges
+ *      (p, q, w >= min_shared) of this p range in canonical order.  Concatenating the ranks'
+ *      edges in rank order gives the canonical edge list.
+ * KMP_ESTATE: the batch needs the flat layout (a class id wider than the key's class field, or a
+ * k-mer too frequent for the LDS buckets); use the single-GPU path. */
+int kmp_dev_keys_part(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
+                      uint32_t n, int k, uint64_t slots, uint32_t lo, uint32_t hi, uint64_t slot_lo,
+                      uint64_t slot_hi, uint32_t parts, unsigned long long* d_out, uint64_t out_cap,
+                      uint64_t* part_counts, void* stream);
+int kmp_dev_pairs_keys(kmp_postings* ws, const unsigned long long* d_keys, uint64_t m, uint32_t n, int k,
+                       uint64_t slots, uint32_t heavy_df, int require_class_diff, uint32_t parts,
+                       unsigned long long* d_out, uint64_t out_cap, uint64_t* n_inc, uint64_t* part_counts,
+                       kmp_postings_stats* stats, void* stream);
+int kmp_dev_edges_pairkeys(kmp_postings* ws, const unsigned long long* d_pk, uint64_t m, uint32_t n,
+                           uint32_t min_shared, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w, uint64_t cap,
+                           uint64_t* n_edges, uint64_t* n_pairs, void* stream);
+
 /* Canonical order: sorts n edges by (p, q).  Keys/values are read from d_p/d_q/d_w and the
  * sorted result is written back to them.  d_tmp: kmp_dev_sort_edges_tmp_bytes(n, N) bytes. */
 uint64_t kmp_dev_sort_edges_tmp_bytes(uint64_t n, uint32_t n_proteins);

@@ -87,6 +87,87 @@ def worker(rank, world, port, out_q):
         dist.destroy_process_group()
 
 
+class OracleStages:
+    """CPU stand-in for the three device stages of dist.distributed_postings, built on the
+    oracle's K(p) sets: keys = code << 20 | p routed by code % parts; pair keys p*N+q of every
+    class-differing pair of a k-mer's proteins, routed by p range; edges = runs of pair keys.
+    Exercises the exchanges and the canonical concatenation, not the kernels."""
+
+    def __init__(self, o, cls, n):
+        self.so, self.sv = o.sets()
+        self.cls = np.asarray(cls)
+        self.n = n
+
+    def keys_part(self, lo, hi, parts):
+        keys = np.concatenate([(self.sv[self.so[p]:self.so[p + 1]].astype(np.int64) << 20) | p
+                               for p in range(lo, hi)] + [np.zeros(0, np.int64)])
+        part = (keys >> 20) % parts
+        order = np.argsort(part, kind="stable")
+        return torch.from_numpy(keys[order]), np.bincount(part, minlength=parts).tolist()
+
+    def pairs_keys(self, keys, parts):
+        k = keys.numpy()
+        k = k[np.argsort(k, kind="stable")]
+        code, p = k >> 20, k & ((1 << 20) - 1)
+        out = []
+        for s, e in zip(*[np.flatnonzero(np.r_[True, code[1:] != code[:-1]]),
+                          np.r_[np.flatnonzero(code[1:] != code[:-1]) + 1, len(code)]]):
+            ps = p[s:e]
+            for i in range(len(ps)):
+                for j in range(i + 1, len(ps)):
+                    if self.cls[ps[i]] != self.cls[ps[j]]:
+                        a, b = sorted((int(ps[i]), int(ps[j])))
+                        out.append(a * self.n + b)
+        pk = np.sort(np.array(out, dtype=np.int64))
+        bounds = [-(-j * self.n // parts) * self.n for j in range(parts + 1)]
+        counts = [int(((pk >= bounds[j]) & (pk < bounds[j + 1])).sum()) for j in range(parts)]
+        return torch.from_numpy(pk), counts
+
+    def edges_pairkeys(self, pk):
+        u, w = np.unique(pk.numpy(), return_counts=True)
+        t = lambda a: torch.from_numpy(a.astype(np.int32))  # noqa: E731
+        return t(u // self.n), t(u % self.n), t(w), len(u)
+
+
+def postings_worker(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, ROOT)
+        from uniprot_kmer_based_clustering_amd.dist import distributed_postings
+        b, o = build_case()
+        got, m = distributed_postings(OracleStages(o, b.class_id, b.n), b.offsets, rank, world)
+        if rank == 0:
+            P, Q, W = o.pairs()
+            gp, gq, gw = (t.numpy().view(np.uint32) for t in got)
+            out_q.put(("edges", np.array_equal(gp, P) and np.array_equal(gq, Q) and np.array_equal(gw, W),
+                       len(P)))
+        out_q.put(("count", rank, m))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_distributed_postings_exchanges(world):
+    """Rank-order concatenation of the p-range owners' edges is the canonical edge list."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=postings_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    msgs = [q.get(timeout=300) for _ in range(world + 1)]  # drain before join: a queued message blocks exit
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    edges = [m for m in msgs if m[0] == "edges"]
+    counts = [m for m in msgs if m[0] == "count"]
+    assert len(edges) == 1 and edges[0][1] and edges[0][2] > 100, edges
+    assert sum(m[2] for m in counts) == edges[0][2]
+    assert all(m[2] > 0 for m in counts)  # every rank owns part of the edge list
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_distributed_split_is_invariant(world):
     ctx = mp.get_context("spawn")
@@ -95,10 +176,10 @@ def test_distributed_split_is_invariant(world):
     procs = [ctx.Process(target=worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
+    msgs = [q.get(timeout=300) for _ in range(world + 1)]  # drain before join: a queued message blocks exit
     for p in procs:
-        p.join(timeout=300)
+        p.join(timeout=60)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
-    msgs = [q.get(timeout=10) for _ in range(world + 1)]
     sets = [m for m in msgs if m[0] == "sets"]
     edges = [m for m in msgs if m[0] == "edges"]
     assert len(sets) == world and all(m[2] for m in sets), sets

@@ -275,3 +275,54 @@ def test_device_pipeline_matches_oracle(oracle_mod):
     so, sv = o.sets()
     for pr in (0, 6999, 7000, 7001, 19999):
         np.testing.assert_array_equal(pipe.set_of(pr), sv[so[pr]:so[pr + 1]])
+
+
+def _dist_gpu_worker(rank, world, port, out_q):
+    """One rank of the distributed postings flow; all ranks share cuda:0, gloo moves the data."""
+    import os
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import uniprot_kmer_based_clustering_amd as KK
+        from uniprot_kmer_based_clustering_amd.device import DevicePipeline
+        from uniprot_kmer_based_clustering_amd.dist import distributed_step
+        b = KK.synth(20000, 9)
+        pipe = DevicePipeline(b, 7, "cuda:0")
+        for _ in range(2):  # a second pass reuses every buffer
+            n = distributed_step(pipe, rank, world, engine="residues")
+        torch.cuda.synchronize()
+        if rank == 0:
+            out_q.put(("edges", n, [a.tolist() for a in pipe.edges()]))
+        else:
+            out_q.put(("rank", rank, n))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_distributed_postings_on_device(oracle_mod, world):
+    """The multi-GPU postings flow (bucket-range and p-range all-to-alls) with the real device
+    stages, `world` ranks on one GPU: rank 0's edge list equals the oracle's."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dist_gpu_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    msgs = [q.get(timeout=300) for _ in range(world)]  # drain before join: a queued message blocks exit
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    got = [m for m in msgs if m[0] == "edges"][0]
+    b = K.synth(20000, 9)
+    p, qq, w = oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=7, threads=8).pairs()
+    assert got[1] == len(p)
+    np.testing.assert_array_equal(np.array(got[2][0], dtype=np.uint32), p)
+    np.testing.assert_array_equal(np.array(got[2][1], dtype=np.uint32), qq)
+    np.testing.assert_array_equal(np.array(got[2][2], dtype=np.uint32), w)

@@ -116,6 +116,12 @@ SIGNATURES = {
     "kmp_postings_last_layout": (C.c_int, [P]),
     "kmp_dev_pairs_residues": (C.c_int, [P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32,
                                          C.c_uint32, C.c_int, P, P, P, C.c_uint64, U64P, P, P]),
+    "kmp_dev_keys_part": (C.c_int, [P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32, C.c_uint32,
+                                    C.c_uint64, C.c_uint64, C.c_uint32, P, C.c_uint64, U64P, P]),
+    "kmp_dev_pairs_keys": (C.c_int, [P, P, C.c_uint64, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32, C.c_int,
+                                     C.c_uint32, P, C.c_uint64, U64P, U64P, P, P]),
+    "kmp_dev_edges_pairkeys": (C.c_int, [P, P, C.c_uint64, C.c_uint32, C.c_uint32, P, P, P, C.c_uint64, U64P,
+                                         U64P, P]),
     "kmp_dev_sort_edges_tmp_bytes": (C.c_uint64, [C.c_uint64, C.c_uint32]),
     "kmp_dev_sort_edges": (C.c_int, [P, P, P, C.c_uint64, C.c_uint32, P, C.c_uint64, P]),
     "kmp_read_fasta": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint32), C.POINTER(P), C.POINTER(P),

@@ -143,11 +143,15 @@ __global__ __launch_bounds__(kResThreads) void residue_keys_kernel(const uint8_t
                                                                    const uint16_t* __restrict__ cls, uint32_t n,
                                                                    int k, uint64_t slots, Layout lay,
                                                                    unsigned long long* __restrict__ keys,
-                                                                   uint32_t* __restrict__ flags) {
+                                                                   uint32_t* __restrict__ flags, uint32_t p0 = 0,
+                                                                   uint64_t slot0 = 0) {
+    // proteins p0 + blockIdx.x; keys[i - slot0] for slot i (a slice starts at slot0 = its first
+    // protein's set_base); the block with p == n fills the buffer's tail up to `slots`
     __shared__ uint8_t lut[256];
     __shared__ uint8_t rc[kResChunk + kMaxK];
-    const uint32_t p = blockIdx.x;
+    const uint32_t p = p0 + blockIdx.x;
     const int tid = threadIdx.x;
+    keys -= slot0;
     if (p == n) {
         for (uint64_t i = set_base(res_off[n], n) + tid; i < slots; i += kResThreads) keys[i] = kNoKey;
         return;
@@ -356,6 +360,23 @@ __global__ void bucket_bounds_kernel(const unsigned long long* __restrict__ k, u
         else hi = mid;
     }
     bstart[b] = (uint32_t)lo;
+}
+
+// Partition bounds of sorted keys: bounds[j] = first index whose (key >> shift) >= T_j with
+// T_j = ceil(j * total / parts) * unit (j < parts) and T_parts = total * unit.
+__global__ void part_bounds_kernel(const unsigned long long* __restrict__ k, uint64_t m, unsigned shift,
+                                   unsigned long long total, unsigned long long unit, uint32_t parts,
+                                   unsigned long long* __restrict__ bounds) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j > parts) return;
+    const unsigned long long t = (j == parts ? total : (j * total + parts - 1) / parts) * unit;
+    uint64_t lo = 0, hi = m;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if ((k[mid] >> shift) < t) lo = mid + 1;
+        else hi = mid;
+    }
+    bounds[j] = lo;
 }
 
 constexpr uint32_t kHeavySub = 128;  // larger sub-buckets (very frequent k-mers) -> flat layout
@@ -784,16 +805,16 @@ int front_flat(kmp_postings* ws, uint64_t slots, const Layout& lay, const uint16
 // bucket field, bucket bounds, LDS group + expand per bucket into kShards regions, gather into
 // ws->inc.  Marks 2 (sort), 3 (group + expand), 4 (gather).  *fallback = true when a bucket
 // does not fit or a class id is too wide (the caller reruns on the flat layout).
-int front_bucketed(kmp_postings* ws, uint64_t slots, const Layout& lay, uint32_t n, uint32_t heavy_df,
+int front_bucketed(kmp_postings* ws, const unsigned long long* in, uint64_t slots, const Layout& lay, uint32_t n,
+                   uint32_t heavy_df,
                    int require_class_diff, unsigned long long* n_inc, bool* fallback, kmp_postings_stats* stats,
                    hipStream_t st) {
     *fallback = false;
     size_t t_sort = 0;
-    PG(rocprim::radix_sort_keys(nullptr, t_sort, ws->keys.p, ws->sorted.p, (size_t)slots, lay.sort_lo, lay.sort_hi,
-                                st));
+    PG(ws->sorted.reserve(slots));
+    PG(rocprim::radix_sort_keys(nullptr, t_sort, in, ws->sorted.p, (size_t)slots, lay.sort_lo, lay.sort_hi, st));
     PG(ws->tmp.reserve(std::max(t_sort, ws->tmp.n)));
-    PG(rocprim::radix_sort_keys(ws->tmp.p, t_sort, ws->keys.p, ws->sorted.p, (size_t)slots, lay.sort_lo,
-                                lay.sort_hi, st));
+    PG(rocprim::radix_sort_keys(ws->tmp.p, t_sort, in, ws->sorted.p, (size_t)slots, lay.sort_lo, lay.sort_hi, st));
     ws->mark(2, st);
     const uint32_t nb = 1u << lay.bbits;
     PG(ws->cnt.reserve(2 * (uint64_t)nb + 2));  // bucket starts, large-bucket list + its count
@@ -865,7 +886,8 @@ int front_bucketed(kmp_postings* ws, uint64_t slots, const Layout& lay, uint32_t
 
 // Shared tail: sort the pair keys, run-length encode -> (pair, w) in canonical order, keep
 // w >= min_shared, unpack.  Marks 5 (pair sort) and 6 (encode + emit).
-int tail(kmp_postings* ws, unsigned long long n_inc, uint32_t n, uint32_t min_shared, uint32_t* d_p, uint32_t* d_q,
+int tail(kmp_postings* ws, const unsigned long long* in, unsigned long long n_inc, uint32_t n, uint32_t min_shared,
+         uint32_t* d_p, uint32_t* d_q,
          uint32_t* d_w, uint64_t cap, uint64_t* n_edges, kmp_postings_stats* stats, hipStream_t st) {
     if (stats) stats->incidences = n_inc;
     if (n_inc == 0) {
@@ -885,14 +907,14 @@ int tail(kmp_postings* ws, unsigned long long n_inc, uint32_t n, uint32_t min_sh
         PG(ws->pos.reserve(n_inc));
     }
     size_t t2 = 0, t3 = 0, t4 = 0;
-    PG(rocprim::radix_sort_keys(nullptr, t2, ws->inc.p, ws->inc_sorted.p, (size_t)n_inc, 0u, pair_bits, st));
+    PG(rocprim::radix_sort_keys(nullptr, t2, in, ws->inc_sorted.p, (size_t)n_inc, 0u, pair_bits, st));
     PG(rocprim::run_length_encode(nullptr, t3, ws->inc_sorted.p, (unsigned int)n_inc, ws->uniq.p, ws->w.p,
                                   ws->small.p + 1, st));
     if (filter_w)
         PG(rocprim::exclusive_scan(nullptr, t4, ws->keep.p, ws->pos.p, 0u, (size_t)n_inc, rocprim::plus<uint32_t>(),
                                    st));
     PG(ws->tmp.reserve(std::max({t2, t3, t4, ws->tmp.n})));
-    PG(rocprim::radix_sort_keys(ws->tmp.p, t2, ws->inc.p, ws->inc_sorted.p, (size_t)n_inc, 0u, pair_bits, st));
+    PG(rocprim::radix_sort_keys(ws->tmp.p, t2, in, ws->inc_sorted.p, (size_t)n_inc, 0u, pair_bits, st));
     ws->mark(5, st);
     PG(rocprim::run_length_encode(ws->tmp.p, t3, ws->inc_sorted.p, (unsigned int)n_inc, ws->uniq.p, ws->w.p,
                                   ws->small.p + 1, st));
@@ -954,7 +976,8 @@ int run_postings(kmp_postings* ws, MakeKeys make_keys, uint32_t n, int k, uint64
         ws->mark(0, st);
         make_keys(lay);
         ws->mark(1, st);
-        int rc = front_bucketed(ws, slots, lay, n, heavy_df, require_class_diff, &n_inc, &fallback, stats, st);
+        int rc = front_bucketed(ws, ws->keys.p, slots, lay, n, heavy_df, require_class_diff, &n_inc, &fallback, stats,
+                                st);
         if (rc != KMP_OK) return rc;
     }
     if (fallback) {
@@ -967,7 +990,7 @@ int run_postings(kmp_postings* ws, MakeKeys make_keys, uint32_t n, int k, uint64
         if (rc != KMP_OK) return rc;
     }
     ws->last_bucketed = !fallback;
-    int rc = tail(ws, n_inc, n, min_shared, d_p, d_q, d_w, cap, n_edges, stats, st);
+    int rc = tail(ws, ws->inc.p, n_inc, n, min_shared, d_p, d_q, d_w, cap, n_edges, stats, st);
     if (rc == KMP_OK) finish_timing(ws, stats, st);
     return rc;
 }
@@ -1033,6 +1056,101 @@ int kmp_dev_pairs_residues(kmp_postings* ws, const uint8_t* d_res, const uint64_
                         n_edges, stats, st);
 }
 
+// ------------------------------------------------------------- multi-GPU split -------------
+// (dist.py) keys of a protein slice, routed by k-mer bucket range -> group + expand on the
+// bucket owner -> pair keys routed by p range -> edges on the p-range owner.
+
+static int part_bounds(kmp_postings* ws, const unsigned long long* d_sorted, uint64_t m, unsigned shift,
+                       unsigned long long total, unsigned long long unit, uint32_t parts, uint64_t* counts,
+                       hipStream_t st) {
+    PG(ws->bstats.reserve(std::max<uint64_t>(ws->bstats.n, kShards * 8 + kShards + parts + 1)));
+    unsigned long long* d_b = ws->bstats.p + kShards * 8 + kShards;
+    part_bounds_kernel<<<(parts + 1 + 63) / 64, 64, 0, st>>>(d_sorted, m, shift, total, unit, parts, d_b);
+    std::vector<unsigned long long> h(parts + 1);
+    PG(hipMemcpyAsync(h.data(), d_b, (parts + 1) * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    PG(hipStreamSynchronize(st));
+    for (uint32_t j = 0; j < parts; ++j) counts[j] = h[j + 1] - h[j];
+    return KMP_OK;
+}
+
+int kmp_dev_keys_part(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
+                      uint32_t n, int k, uint64_t slots, uint32_t lo, uint32_t hi, uint64_t slot_lo,
+                      uint64_t slot_hi, uint32_t parts, unsigned long long* d_out, uint64_t out_cap,
+                      uint64_t* part_counts, void* stream) {
+    if (!ws || !part_counts || parts < 1 || k < 1 || k > kMaxK || lo > hi || hi > n || slot_hi < slot_lo)
+        return KMP_EINVAL;
+    for (uint32_t j = 0; j < parts; ++j) part_counts[j] = 0;
+    const uint64_t m = slot_hi - slot_lo;
+    if (hi == lo || m == 0) return KMP_OK;
+    if (!d_res || !d_res_off || !d_class || !d_out || out_cap < m) return KMP_EINVAL;
+    const Layout lay = make_layout(n, k, slots, true);
+    if (!lay.bucketed) return KMP_ESTATE;
+    hipStream_t st = as_stream(stream);
+    PG(ws->keys.reserve(m));
+    PG(ws->flags.reserve(4));
+    PG(hipMemsetAsync(ws->flags.p, 0, 4 * sizeof(uint32_t), st));
+    residue_keys_kernel<<<hi - lo, kResThreads, 0, st>>>(d_res, d_res_off, d_class, n, k, slots, lay, ws->keys.p,
+                                                         ws->flags.p, lo, slot_lo);
+    size_t t_sort = 0;
+    PG(rocprim::radix_sort_keys(nullptr, t_sort, ws->keys.p, d_out, (size_t)m, lay.sort_lo, lay.sort_hi, st));
+    PG(ws->tmp.reserve(std::max(t_sort, ws->tmp.n)));
+    PG(rocprim::radix_sort_keys(ws->tmp.p, t_sort, ws->keys.p, d_out, (size_t)m, lay.sort_lo, lay.sort_hi, st));
+    int rc = part_bounds(ws, d_out, m, lay.sort_lo, 1ull << lay.bbits, 1, parts, part_counts, st);
+    if (rc != KMP_OK) return rc;
+    uint32_t h_flags[2] = {0, 0};
+    PG(hipMemcpy(h_flags, ws->flags.p, sizeof h_flags, hipMemcpyDeviceToHost));
+    return h_flags[1] ? KMP_ESTATE : KMP_OK;
+}
+
+int kmp_dev_pairs_keys(kmp_postings* ws, const unsigned long long* d_keys, uint64_t m, uint32_t n, int k,
+                       uint64_t slots, uint32_t heavy_df, int require_class_diff, uint32_t parts,
+                       unsigned long long* d_out, uint64_t out_cap, uint64_t* n_inc, uint64_t* part_counts,
+                       kmp_postings_stats* stats, void* stream) {
+    if (!ws || !n_inc || !part_counts || parts < 1 || k < 1 || k > kMaxK) return KMP_EINVAL;
+    *n_inc = 0;
+    for (uint32_t j = 0; j < parts; ++j) part_counts[j] = 0;
+    if (stats) *stats = kmp_postings_stats{};
+    if (m == 0 || n < 2) return KMP_OK;
+    if (!d_keys) return KMP_EINVAL;
+    const Layout lay = make_layout(n, k, slots, true);
+    if (!lay.bucketed) return KMP_ESTATE;
+    hipStream_t st = as_stream(stream);
+    PG(ws->flags.reserve(4));
+    PG(hipMemsetAsync(ws->flags.p, 0, 4 * sizeof(uint32_t), st));
+    unsigned long long ni = 0;
+    bool fallback = false;
+    int rc = front_bucketed(ws, d_keys, m, lay, n, heavy_df < 2 ? 2 : heavy_df, require_class_diff, &ni, &fallback,
+                            stats, st);
+    if (rc != KMP_OK) return rc;
+    if (fallback) return KMP_ESTATE;  // a k-mer too frequent for the LDS buckets
+    *n_inc = ni;
+    if (stats) stats->incidences = ni;
+    if (ni == 0) return KMP_OK;
+    if (ni > out_cap || !d_out) return KMP_EOVERFLOW;
+    const unsigned pair_bits = bits_for((uint64_t)n * n);
+    size_t t2 = 0;
+    PG(rocprim::radix_sort_keys(nullptr, t2, ws->inc.p, d_out, (size_t)ni, 0u, pair_bits, st));
+    PG(ws->tmp.reserve(std::max(t2, ws->tmp.n)));
+    PG(rocprim::radix_sort_keys(ws->tmp.p, t2, ws->inc.p, d_out, (size_t)ni, 0u, pair_bits, st));
+    return part_bounds(ws, d_out, ni, 0, n, n, parts, part_counts, st);
+}
+
+int kmp_dev_edges_pairkeys(kmp_postings* ws, const unsigned long long* d_pk, uint64_t m, uint32_t n,
+                           uint32_t min_shared, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w, uint64_t cap,
+                           uint64_t* n_edges, uint64_t* n_pairs, void* stream) {
+    if (!ws || !n_edges || (cap && (!d_p || !d_q || !d_w))) return KMP_EINVAL;
+    *n_edges = 0;
+    if (n_pairs) *n_pairs = 0;
+    if (m == 0) return KMP_OK;
+    if (!d_pk) return KMP_EINVAL;
+    kmp_postings_stats s{};
+    const int rc = tail(ws, d_pk, m, n, min_shared < 1 ? 1 : min_shared, d_p, d_q, d_w, cap, n_edges, &s,
+                        as_stream(stream));
+    if (n_pairs) *n_pairs = s.pairs;
+    return rc;
+}
+
 }  // extern "C"
+
 
 #undef PG

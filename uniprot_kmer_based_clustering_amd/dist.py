@@ -1,6 +1,19 @@
 """Multi-GPU split of the pair path: one process per GPU, torch.distributed over RCCL.
 
-The N x N pair space shards with one real exchange step:
+Postings engines (default; ``distributed_postings``) — the reference's algorithm sharded by
+k-mer, two all-to-all exchanges:
+  1. rank r turns the k-mer windows of its protein slice into keys, sorted by k-mer bucket
+     (kmp_dev_keys_part);
+  2. all-to-all: every key goes to the owner of its bucket range (RCCL over xGMI);
+  3. the owner groups, deduplicates and expands its k-mers into (p, q) pair keys
+     (kmp_dev_pairs_keys; the bucketed engine on 1/G of the keys), sorted;
+  4. all-to-all: every pair key goes to the owner of its p range;
+  5. the owner reduces the runs to edges w(p, q) (kmp_dev_edges_pairkeys): its p range of the
+     canonical edge list;
+  6. edges are gathered to rank 0 in rank order — already canonical, no final sort.
+
+Tiles engine (``distributed_step(engine="tiles")``) — the N x N pair space shards with one
+exchange step:
   1. rank r builds K(p) for its contiguous protein slice (balanced by residue count);
   2. all-gather of the slices' set slots and set sizes (RCCL over xGMI) -> every rank holds
      every K(p) in the same layout;
@@ -69,6 +82,9 @@ def gather_edges(ep: torch.Tensor, eq: torch.Tensor, ew: torch.Tensor, count: in
     """All ranks' (p, q, w) concatenated in rank order on rank 0 (None elsewhere)."""
     world = dist.get_world_size(group)
     dev = ep.device
+    if _staged(ep, group):
+        got = gather_edges(ep[:count].cpu(), eq[:count].cpu(), ew[:count].cpu(), count, rank, group)
+        return None if got is None else tuple(t.to(dev) for t in got)
     cnt = torch.tensor([count], dtype=torch.int64, device=dev)
     counts = [torch.zeros_like(cnt) for _ in range(world)]
     dist.all_gather(counts, cnt, group=group)
@@ -86,10 +102,122 @@ def gather_edges(ep: torch.Tensor, eq: torch.Tensor, ew: torch.Tensor, count: in
     return out[0].contiguous(), out[1].contiguous(), out[2].contiguous()
 
 
+def _staged(t: torch.Tensor, group) -> bool:
+    """gloo moves CPU tensors only: device tensors are staged through the host."""
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
+def exchange(send: torch.Tensor, counts: list, group=None) -> torch.Tensor:
+    """all-to-all with uneven splits: send[sum(counts[:j]) : sum(counts[:j+1])] goes to rank j;
+    returns what every rank sent to this one, in source-rank order."""
+    dev = send.device
+    staged = _staged(send, group)
+    cdev = torch.device("cpu") if staged or not send.is_cuda else dev
+    cnt = torch.tensor([int(c) for c in counts], dtype=torch.int64, device=cdev)
+    rcnt = torch.empty_like(cnt)
+    dist.all_to_all_single(rcnt, cnt, group=group)
+    rc = [int(x) for x in rcnt.tolist()]
+    src = send[:sum(int(c) for c in counts)]
+    if staged:
+        src = src.cpu()
+    recv = torch.empty(sum(rc), dtype=send.dtype, device=src.device)
+    dist.all_to_all_single(recv, src, rc, [int(c) for c in counts], group=group)
+    return recv.to(dev) if staged else recv
+
+
+class DeviceStages:
+    """The three device stages of the distributed postings flow on a DevicePipeline (the
+    kmp_dev_keys_part / kmp_dev_pairs_keys / kmp_dev_edges_pairkeys entry points)."""
+
+    def __init__(self, pipe, min_shared: int = 1, require_class_diff: bool = True):
+        import ctypes as C
+        self.C = C
+        self.pipe = pipe
+        self.L = _lib.lib()
+        self.ws = pipe._workspace()
+        self.slots = int(self.L.kmp_set_capacity(pipe.n, pipe.total))
+        self.min_shared = min_shared
+        self.require_class_diff = require_class_diff
+        self.pk_cap = 1 << 20
+        self.stats = _lib.PostingsStats()
+
+    def _stream(self):
+        return self.C.c_void_p(torch.cuda.current_stream(self.pipe.dev).cuda_stream)
+
+    def _ptr(self, t):
+        return self.C.c_void_p(t.data_ptr())
+
+    def keys_part(self, lo: int, hi: int, parts: int):
+        C, L, p = self.C, self.L, self.pipe
+        off = p.offsets_host
+        slot_lo = int(L.kmp_set_base(int(off[lo]), lo))
+        slot_hi = int(L.kmp_set_base(int(off[hi]), hi))
+        out = torch.empty(max(1, slot_hi - slot_lo), dtype=torch.int64, device=p.dev)
+        counts = (C.c_uint64 * parts)()
+        _lib.check(L.kmp_dev_keys_part(self.ws, self._ptr(p.res), self._ptr(p.off), self._ptr(p.cls), p.n, p.k,
+                                       self.slots, lo, hi, slot_lo, slot_hi, parts, self._ptr(out), out.numel(),
+                                       counts, self._stream()), "kmp_dev_keys_part")
+        return out, [int(c) for c in counts]
+
+    def pairs_keys(self, keys: torch.Tensor, parts: int):
+        C, L, p = self.C, self.L, self.pipe
+        counts = (C.c_uint64 * parts)()
+        ni = C.c_uint64()
+        for _ in range(3):
+            out = torch.empty(max(1, self.pk_cap), dtype=torch.int64, device=p.dev)
+            st = L.kmp_dev_pairs_keys(self.ws, self._ptr(keys), keys.numel(), p.n, p.k, self.slots, 0xFFFFFFFF,
+                                      int(self.require_class_diff), parts, self._ptr(out), out.numel(),
+                                      C.byref(ni), counts, C.byref(self.stats), self._stream())
+            if st == _lib.KMP_EOVERFLOW:
+                self.pk_cap = ni.value + ni.value // 8 + 1024
+                continue
+            _lib.check(st, "kmp_dev_pairs_keys")
+            return out[:ni.value], [int(c) for c in counts]
+        raise RuntimeError("pair-key count unstable across reruns")
+
+    def edges_pairkeys(self, pk: torch.Tensor):
+        C, L, p = self.C, self.L, self.pipe
+        m = pk.numel()  # every edge is at least one incidence: m bounds the edge count
+        ep, eq, ew = (torch.empty(max(1, m), dtype=torch.int32, device=p.dev) for _ in range(3))
+        ne, npairs = C.c_uint64(), C.c_uint64()
+        _lib.check(L.kmp_dev_edges_pairkeys(self.ws, self._ptr(pk), m, p.n, self.min_shared, self._ptr(ep),
+                                            self._ptr(eq), self._ptr(ew), max(1, m), C.byref(ne), C.byref(npairs),
+                                            self._stream()), "kmp_dev_edges_pairkeys")
+        return ep, eq, ew, ne.value
+
+
+def distributed_postings(stages, offsets: np.ndarray, rank: int, world: int, group=None):
+    """The postings flow above on `stages` (DeviceStages, or a stand-in with the same three
+    methods).  Returns rank 0's gathered canonical edges (p, q, w) and None elsewhere, plus this
+    rank's edge count."""
+    lo, hi = protein_slices(offsets, world)[rank]
+    keys, kc = stages.keys_part(lo, hi, world)
+    mine = exchange(keys, kc, group)
+    pk, pc = stages.pairs_keys(mine, world)
+    pk_mine = exchange(pk, pc, group)
+    ep, eq, ew, m = stages.edges_pairkeys(pk_mine)
+    return gather_edges(ep, eq, ew, m, rank, group), m
+
+
 def distributed_step(pipe, rank: int, world: int, group=None, min_shared: int = 1,
-                     require_class_diff: bool = True, timers: dict | None = None) -> int:
+                     require_class_diff: bool = True, timers: dict | None = None, engine: str = "residues") -> int:
     """One multi-GPU pass of the path on a DevicePipeline holding the whole batch.
     Returns the canonical edge count (rank 0) or this rank's share (others)."""
+    if engine in ("residues", "postings"):
+        stages = getattr(pipe, "_dist_stages", None)
+        if stages is None or stages.min_shared != min_shared or stages.require_class_diff != require_class_diff:
+            stages = pipe._dist_stages = DeviceStages(pipe, min_shared, require_class_diff)
+        got, m = distributed_postings(stages, pipe.offsets_host, rank, world, group)
+        if rank == 0:
+            n = got[0].numel()
+            if n > pipe.edge_cap:
+                pipe._alloc_edges(n + n // 8 + 1024)
+            pipe.ep[:n] = got[0]
+            pipe.eq[:n] = got[1]
+            pipe.ew[:n] = got[2]
+            pipe.n_edges = n
+            return n
+        return m
     slices = protein_slices(pipe.offsets_host, world)
     lo, hi = slices[rank]
     pipe.build_sets(lo, hi)
