@@ -14,8 +14,10 @@
  *  - Calls are synchronous, like the reference's graph methods (each spawns and joins
  *    its own pool before returning, mod.rs:81-124).  One host thread per kmp_ctx.
  *  - Device-stage API (kmp_dev_*): plain device pointers + an optional hipStream_t passed
- *    as void*; no allocation, no synchronisation inside, so a multi-GPU host (one process
- *    per GPU, RCCL all-gather between stages) can drive the stages on its own streams.
+ *    as void*, so a multi-GPU host (one process per GPU, RCCL between stages) can drive the
+ *    stages on its own streams.  The set/tile stages allocate nothing and do not
+ *    synchronise; the postings stages own their scratch in a kmp_postings workspace and
+ *    synchronise the stream where they read device counts back (documented per call).
  *  - Proteins are indexed 0..N-1 in input (file) order; edges are (p, q, w) with p < q,
  *    sorted by (p, q) — the reference's post-combine_edges graph with orientation [p, q]
  *    (single-thread visitor order, vertex.rs:100).
@@ -51,7 +53,7 @@ enum { KMP_SCORE_COUNT = 0, KMP_SCORE_JACCARD = 1 };
 
 /* pair engines (kmp_pair_opts.engine); every engine returns the same edges */
 enum {
-    KMP_ENGINE_AUTO = 0,      /* postings, with the tiled kernel taking over very frequent k-mers */
+    KMP_ENGINE_AUTO = 0,      /* the fastest engine for the batch: currently RESIDUES */
     KMP_ENGINE_POSTINGS = 1,  /* sort / expand Σ C(df,2) incidences / reduce (the reference's algorithm) */
     KMP_ENGINE_TILES = 2,     /* LDS-tiled all-pairs intersection over the N x N upper triangle */
     KMP_ENGINE_RESIDUES = 3   /* postings fed by the k-mer windows of the residues (kmp_dev_pairs_residues) */

@@ -378,7 +378,7 @@ int kmp_pairs(kmp_ctx* c, const kmp_pair_opts* opts, kmp_edges** out) {
             KMP_HIP(c, c->ew.reserve(c->edge_cap * sizeof(uint32_t)));
             uint64_t ne = 0;
             const int st =
-                o.engine == KMP_ENGINE_RESIDUES
+                (o.engine == KMP_ENGINE_RESIDUES || o.engine == KMP_ENGINE_AUTO)
                     ? kmp_dev_pairs_residues(c->postings, c->res.as<uint8_t>(), c->off.as<uint64_t>(),
                                              c->cls.as<uint16_t>(), c->n, c->k_sets, slots, 0xFFFFFFFFu,
                                              o.min_shared, o.require_class_diff, c->ep.as<uint32_t>(),
