@@ -61,9 +61,20 @@ def cpu_baseline(proteins, k, threads):
             "seconds": dt, "edges": int(len(p))}
 
 
-def stage_bytes(n_res, slots, n_inc, n_edges, n_uniq):
+def stage_bytes(n_res, slots, n_inc, n_edges, n_uniq, tail="sort"):
     """Algorithmic HBM bytes of each postings stage (one read of every input, one write of
-    every output)."""
+    every output).  The six timing slots of the p-shard tail are keys, bucket sort,
+    group + expand (pair keys written to their row ranges), -, row-range reduce (+ offsets),
+    compaction."""
+    if tail == "pshard":
+        return {
+            "keys": n_res + 8 * slots,
+            "code_sort": 16 * slots,
+            "count": 8 * slots + 8 * n_inc,
+            "write": 0,
+            "pair_sort": 8 * n_inc + 12 * n_edges,
+            "rle_emit": 24 * n_edges,
+        }
     return {
         "keys": n_res + 8 * slots,                      # residues in, one u64 key per slot out
         "code_sort": 16 * slots,                        # keys read once + written once
@@ -156,8 +167,11 @@ def main():
         if stage_sum is not None:
             ps = pipe.postings_stats.as_dict()
             slots = int(_lib.lib().kmp_set_capacity(n, int(proteins.offsets[-1])))
-            byts = stage_bytes(int(proteins.offsets[-1]), slots, ps["incidences"], n_edges, ps["pairs"])
-            stage_ms = dict(zip(_lib.POSTINGS_STAGE_NAMES, (stage_sum / args.steps).tolist()))
+            tail = pipe.last_tail()
+            byts = stage_bytes(int(proteins.offsets[-1]), slots, ps["incidences"], n_edges, ps["pairs"], tail)
+            names = _lib.POSTINGS_STAGE_NAMES if tail == "sort" else (
+                "keys", "code_sort", "count", "write", "pair_sort", "rle_emit")
+            stage_ms = dict(zip(names, (stage_sum / args.steps).tolist()))
             stages = {s: {"ms": stage_ms[s], "alg_bytes": byts[s],
                           "GBs": byts[s] / (stage_ms[s] * 1e-3) / 1e9 if stage_ms[s] > 0 else None}
                       for s in stage_ms}
@@ -166,7 +180,7 @@ def main():
             out["roofline"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": ach / HBM_PEAK_GBS, "traffic": None, "kernel": dom,
                                "kernel_ms": stage_ms[dom], "alg_bytes_per_launch": byts[dom],
-                               "layout": pipe.last_layout(), "stages": stages,
+                               "layout": pipe.last_layout(), "tail": tail, "stages": stages,
                                "step_alg_bytes": sum(byts.values()),
                                "step_GBs": sum(byts.values()) / (ms * 1e-3) / 1e9}
             # SURVEY.md §8d model: 4·(S_p + S_q) bytes per pair, i.e. a merge-intersection of every

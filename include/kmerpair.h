@@ -253,9 +253,15 @@ int kmp_postings_set_timing(kmp_postings* ws, int enable);
 /* Key layout.  bucketed (default 1): keys sorted on a 2^b-bucket hash of the k-mer only, then one
  * workgroup per bucket groups, deduplicates and expands its k-mers in LDS; buckets that do not
  * fit (very frequent k-mers) make the call rerun on the flat layout.  0: always flat (full code
- * sort, scan-based expansion).  kmp_postings_last_layout: 1 if the last call ran bucketed. */
+ * sort, scan-based expansion).  kmp_postings_last_layout: 0 flat, 1 bucketed with the pair-key
+ * sort tail, 2 bucketed with the row-range (p-shard) tail.
+ * kmp_postings_set_pshard (default 0): 1 makes the bucketed expansion write each pair key into the
+ * region of its row range (p >> r), and one workgroup per range sorts, run-length encodes and
+ * filters it in LDS instead of the global pair-key sort; ranges above the LDS capacity fall back to
+ * the sort tail.  Measured slower at config 3 (per-key cursor atomics), kept for experiments. */
 int kmp_postings_set_layout(kmp_postings* ws, int bucketed);
 int kmp_postings_last_layout(const kmp_postings* ws);
+int kmp_postings_set_pshard(kmp_postings* ws, int enable);
 int kmp_dev_pairs_postings(kmp_postings* ws, const uint32_t* d_set, const uint32_t* d_set_len,
                            const uint64_t* d_res_off, const uint16_t* d_class, uint32_t n, int k, uint64_t slots,
                            uint32_t heavy_df, uint32_t min_shared, int require_class_diff, uint32_t* d_p,

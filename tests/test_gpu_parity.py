@@ -191,6 +191,49 @@ def test_edge_cases(engine, oracle_mod):
         assert len(engine.pairs(engine=eng)) == 0
 
 
+@pytest.mark.parametrize("n", [700, 3000, 60000])
+def test_bucketed_small_batches(oracle_mod, n):
+    """Small and mid-size batches (below rocprim's 1M-key merge-sort threshold) stay on the
+    bucketed layout and are exact: regression for the rocprim 4.2 default-config sort defect on
+    bit ranges [b, 64) (kmp_postings.hip SortCfg, tools/sort_check.hip)."""
+    import torch
+    from uniprot_kmer_based_clustering_amd.device import DevicePipeline
+    b = K.synth(n, 13)
+    p, q, w = oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=7, threads=8).pairs()
+    pipe = DevicePipeline(b, 7, "cuda:0")
+    for _ in range(2):
+        m = pipe.step(engine="residues")
+        torch.cuda.synchronize()
+        assert pipe.last_layout() == "bucketed" and m == len(p)
+        np.testing.assert_array_equal(pipe.edges()[0], p)
+        np.testing.assert_array_equal(pipe.edges()[1], q)
+        np.testing.assert_array_equal(pipe.edges()[2], w)
+
+
+def test_pshard_long_rows(oracle_mod):
+    """One protein sharing a distinct k-mer with each of ~650 others: its row of the p-shard
+    reduction is longer than the rank-sort limit, so that range is bitonic-sorted in LDS."""
+    import torch
+    from uniprot_kmer_based_clustering_amd.device import DevicePipeline
+    rng = np.random.default_rng(5)
+    alpha = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", dtype=np.uint8)
+    rnd = lambda m: alpha[rng.integers(0, 20, m)].tobytes()  # noqa: E731
+    base = rnd(700)
+    seqs = [base] + [rnd(40) + base[i:i + 7] + rnd(40) for i in range(650)]
+    res, off, cls = make_batch(seqs, ["a"] + ["b"] * 650)
+    o = oracle_mod.Oracle(res, off, cls, k=7, threads=8)
+    p, q, w = o.pairs()
+    assert (p == 0).sum() > 600
+    pipe = DevicePipeline(K.Proteins(res, off, cls), 7, "cuda:0")
+    pipe.set_pshard(True)
+    m = pipe.step(engine="residues")
+    torch.cuda.synchronize()
+    assert pipe.last_tail() == "pshard" and m == len(p)
+    np.testing.assert_array_equal(pipe.edges()[0], p)
+    np.testing.assert_array_equal(pipe.edges()[1], q)
+    np.testing.assert_array_equal(pipe.edges()[2], w)
+
+
 def test_bucketed_fallback_on_frequent_kmers(oracle_mod):
     """A k-mer shared by thousands of proteins overflows an LDS sub-bucket: the bucketed layout
     hands the call to the flat layout and the edges stay exact."""
@@ -253,15 +296,24 @@ def test_device_pipeline_matches_oracle(oracle_mod):
         assert st["distinct"] == c["distinct"] and st["repeat"] == c["repeat"] and st["max_df"] == c["max_df"]
         assert st["sum_cdf2_light"] == c["sum_cdf2"] and st["incidences"] == c["sum_w_diff"]
         assert st["sum_S"] == c["sum_S"] and st["pairs"] == n
-    # both key layouts, both entry points: identical edges; config-shaped input runs bucketed
-    for bucketed in (True, False):
+    # both key layouts, both tails, both entry points: identical edges; config-shaped input runs
+    # bucketed with the p-shard tail
+    for bucketed, pshard in ((True, True), (True, False), (False, True)):
         pipe.set_layout(bucketed)
+        pipe.set_pshard(pshard)
         for eng in ("postings", "residues"):
             assert pipe.step(engine=eng) == n
+            np.testing.assert_array_equal(pipe.edges()[0], p)
             np.testing.assert_array_equal(pipe.edges()[1], q)
             np.testing.assert_array_equal(pipe.edges()[2], w)
             assert pipe.last_layout() == ("bucketed" if bucketed else "flat")
+            assert pipe.last_tail() == ("pshard" if bucketed and pshard else "sort")
+        for ms in (2, 5):  # min_shared filter inside both tails
+            keep = w >= ms
+            assert pipe.step(min_shared=ms, engine="residues") == int(keep.sum())
+            np.testing.assert_array_equal(pipe.edges()[1], q[keep])
     pipe.set_layout(True)
+    pipe.set_pshard(False)
     # stage timing: six non-negative stage times that add up to about one step
     pipe.set_stage_timing(True)
     assert pipe.step(engine="residues") == n

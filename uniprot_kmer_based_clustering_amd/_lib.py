@@ -114,6 +114,7 @@ SIGNATURES = {
     "kmp_postings_set_timing": (C.c_int, [P, C.c_int]),
     "kmp_postings_set_layout": (C.c_int, [P, C.c_int]),
     "kmp_postings_last_layout": (C.c_int, [P]),
+    "kmp_postings_set_pshard": (C.c_int, [P, C.c_int]),
     "kmp_dev_pairs_residues": (C.c_int, [P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32,
                                          C.c_uint32, C.c_int, P, P, P, C.c_uint64, U64P, P, P]),
     "kmp_dev_keys_part": (C.c_int, [P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32, C.c_uint32,

@@ -27,6 +27,7 @@
 #include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstdint>
 #include <vector>
@@ -49,6 +50,13 @@ unsigned bits_for(uint64_t v) {  // bits needed for values < v
 }
 
 constexpr unsigned long long kNoKey = ~0ull;
+
+// rocprim 4.2 (ROCm 7.2): with the default config, radix_sort_keys on fewer than 1M keys takes a
+// merge-sort path that returns unsorted, non-permuted data for bit ranges [b, 64) with b > 0
+// (tools/sort_check.hip reproduces it).  Onesweep (merge-sort limit 0) is correct for every range
+// and size, so every sort here uses it.
+using SortCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                           rocprim::default_config, 0>;
 constexpr unsigned kClsBits = 16;
 
 // Two key layouts (u64, kNoKey = all ones is the padding of every layout):
@@ -417,13 +425,23 @@ __device__ __forceinline__ void block_scan_n(uint32_t v, uint32_t& excl, uint32_
 // cursor[b % kShards] (one agent-scope atomic) inside that shard's region; the pair sort makes
 // the order irrelevant.  Statistics -> gstats[b % kShards].  flags[0]: a bucket above the large capacity
 // or a sub-bucket above kHeavySub (the caller reruns on the flat layout).
-template <int kCap, int kThreads, int kSubBits, int kAblate = 0>
+// p-shard output mode: every pair key goes to the region of its row range (p >> row_bits),
+// reserved key by key on that shard's cursor; shard_reduce_kernel then finishes each range in LDS
+struct PShard {
+    unsigned row_bits;
+    uint32_t n_shards;
+    uint64_t cap;                       // keys per shard region
+    uint32_t* cursor;                   // n_shards
+    unsigned long long* region;         // n_shards * cap, key = p << 32 | q
+};
+
+template <int kCap, int kThreads, int kSubBits, int kAblate = 0, bool kPShard = false>
 __device__ __forceinline__ void process_bucket(
     const uint32_t b, const unsigned long long* __restrict__ sorted, const uint32_t* __restrict__ bstart,
     const Layout& lay, uint32_t n_prot, int require_diff, uint32_t heavy_df, bool small,
     unsigned long long* __restrict__ out, uint64_t shard_cap, unsigned long long* __restrict__ cursor,
     unsigned long long* __restrict__ gstats, uint32_t* __restrict__ flags, uint32_t* __restrict__ list,
-    uint32_t* __restrict__ list_count) {
+    uint32_t* __restrict__ list_count, const PShard& ps) {
     constexpr int kE = kCap / kThreads;
     constexpr uint32_t kSub = 1u << kSubBits;
     constexpr int kPer = kSub / kThreads;
@@ -572,27 +590,49 @@ __device__ __forceinline__ void process_bucket(
         if (mine == 0xFFFFFFFF) flags[3] = 1;
         return;
     }
-    // 4. reserve the workgroup's output range, write the pair keys
-    uint32_t excl, total;
-    block_scan_n<kThreads>(mine, excl, total, wave_tot);
-    const uint32_t shard = b % kShards;
-    if (tid == 0) sbase = total ? atomicAdd(&cursor[shard], (unsigned long long)total) : 0ull;
-    __syncthreads();
-    if (mine && kAblate != 5) {
-        unsigned long long pos = sbase + excl;
-        unsigned long long* dst = out + (uint64_t)shard * shard_cap;
+    // 4. write the pair keys: p-shard mode reserves each key on its row range's cursor; otherwise
+    //    the workgroup reserves one range on cursor[b % kShards]
+    if (kPShard) {
+        if (mine && kAblate != 5) {
 #pragma unroll
-        for (int e = 0; e < kE; ++e) {
-            if (!cnt[e]) continue;
-            const uint32_t i = tid + e * kThreads;
-            const uint32_t p = xl[e] >> cb;
-            for (uint32_t j = i + 1; j < en[e]; ++j) {
-                if (Bh[j] != xh[e] || is_dup(j)) continue;
-                const uint32_t lj = Bl[j];
-                if (require_diff && !((lj ^ xl[e]) & cmask)) continue;
-                const uint32_t q = lj >> cb;
-                if (pos < shard_cap) dst[pos] = (unsigned long long)min(p, q) * n_prot + max(p, q);
-                ++pos;
+            for (int e = 0; e < kE; ++e) {
+                if (!cnt[e]) continue;
+                const uint32_t i = tid + e * kThreads;
+                const uint32_t p = xl[e] >> cb;
+                for (uint32_t j = i + 1; j < en[e]; ++j) {
+                    if (Bh[j] != xh[e] || is_dup(j)) continue;
+                    const uint32_t lj = Bl[j];
+                    if (require_diff && !((lj ^ xl[e]) & cmask)) continue;
+                    const uint32_t q = lj >> cb;
+                    const uint32_t a = min(p, q), c = max(p, q);
+                    const uint32_t sh = a >> ps.row_bits;
+                    const uint32_t slot = atomicAdd(&ps.cursor[sh], 1u);
+                    if (slot < ps.cap) ps.region[(uint64_t)sh * ps.cap + slot] = ((unsigned long long)a << 32) | c;
+                }
+            }
+        }
+    } else {
+        uint32_t excl, total;
+        block_scan_n<kThreads>(mine, excl, total, wave_tot);
+        const uint32_t shard = b % kShards;
+        if (tid == 0) sbase = total ? atomicAdd(&cursor[shard], (unsigned long long)total) : 0ull;
+        __syncthreads();
+        if (mine && kAblate != 5) {
+            unsigned long long pos = sbase + excl;
+            unsigned long long* dst = out + (uint64_t)shard * shard_cap;
+#pragma unroll
+            for (int e = 0; e < kE; ++e) {
+                if (!cnt[e]) continue;
+                const uint32_t i = tid + e * kThreads;
+                const uint32_t p = xl[e] >> cb;
+                for (uint32_t j = i + 1; j < en[e]; ++j) {
+                    if (Bh[j] != xh[e] || is_dup(j)) continue;
+                    const uint32_t lj = Bl[j];
+                    if (require_diff && !((lj ^ xl[e]) & cmask)) continue;
+                    const uint32_t q = lj >> cb;
+                    if (pos < shard_cap) dst[pos] = (unsigned long long)min(p, q) * n_prot + max(p, q);
+                    ++pos;
+                }
             }
         }
     }
@@ -617,28 +657,169 @@ __device__ __forceinline__ void process_bucket(
     }
 }
 
-template <int kCap, int kThreads, int kSubBits, int kAblate = 0>
+template <int kCap, int kThreads, int kSubBits, int kAblate = 0, bool kPShard = false>
 __global__ __launch_bounds__(kThreads) void bucket_small_kernel(
     const unsigned long long* __restrict__ sorted, const uint32_t* __restrict__ bstart, Layout lay,
     uint32_t n_prot, int require_diff, uint32_t heavy_df, unsigned long long* __restrict__ out, uint64_t shard_cap,
     unsigned long long* __restrict__ cursor, unsigned long long* __restrict__ gstats, uint32_t* __restrict__ flags,
-    uint32_t* __restrict__ list, uint32_t* __restrict__ list_count) {
-    process_bucket<kCap, kThreads, kSubBits, kAblate>(blockIdx.x, sorted, bstart, lay, n_prot, require_diff,
-                                                      heavy_df, true, out, shard_cap, cursor, gstats, flags, list,
-                                                      list_count);
+    uint32_t* __restrict__ list, uint32_t* __restrict__ list_count, PShard ps) {
+    process_bucket<kCap, kThreads, kSubBits, kAblate, kPShard>(blockIdx.x, sorted, bstart, lay, n_prot,
+                                                               require_diff, heavy_df, true, out, shard_cap, cursor,
+                                                               gstats, flags, list, list_count, ps);
 }
 
 // the buckets the small kernel listed (above its capacity), a grid-stride loop over the list
-template <int kCap, int kThreads, int kSubBits>
+template <int kCap, int kThreads, int kSubBits, bool kPShard = false>
 __global__ __launch_bounds__(kThreads) void bucket_large_kernel(
     const unsigned long long* __restrict__ sorted, const uint32_t* __restrict__ bstart, Layout lay,
     uint32_t n_prot, int require_diff, uint32_t heavy_df, unsigned long long* __restrict__ out, uint64_t shard_cap,
     unsigned long long* __restrict__ cursor, unsigned long long* __restrict__ gstats, uint32_t* __restrict__ flags,
-    uint32_t* __restrict__ list, const uint32_t* __restrict__ list_count) {
+    uint32_t* __restrict__ list, const uint32_t* __restrict__ list_count, PShard ps) {
     const uint32_t m = *list_count;
     for (uint32_t i = blockIdx.x; i < m; i += gridDim.x)
-        process_bucket<kCap, kThreads, kSubBits>(list[i], sorted, bstart, lay, n_prot, require_diff, heavy_df, false,
-                                                 out, shard_cap, cursor, gstats, flags, nullptr, nullptr);
+        process_bucket<kCap, kThreads, kSubBits, 0, kPShard>(list[i], sorted, bstart, lay, n_prot, require_diff,
+                                                             heavy_df, false, out, shard_cap, cursor, gstats, flags,
+                                                             nullptr, nullptr, ps);
+}
+
+// ---------------------------------------------------------------- p-shard reduction --------
+// One workgroup per row range [s << row_bits, (s+1) << row_bits) (combine_edges, mod.rs:322-546):
+// its m pair keys (p << 32 | q) as v = row << 24 | q in LDS, counting sort by row, rank sort by q
+// inside each row (rows are short), runs of equal v = one pair, run length = w; pairs with
+// w >= min_shared go to the shard's edge region in (p, q) order.  ecount[s] = edges,
+// npairs[s] = pairs before the min_shared filter.
+constexpr int kReduceCap = 8192, kReduceThreads = 256, kReduceRowsMax = 256;
+constexpr uint32_t kRankRowMax = 512;  // longer rows: bitonic sort of the whole shard instead
+__global__ __launch_bounds__(kReduceThreads) void shard_reduce_kernel(
+    const unsigned long long* __restrict__ region, const uint32_t* __restrict__ cursor, uint64_t cap,
+    unsigned row_bits, uint32_t min_shared, uint32_t* __restrict__ ep, uint32_t* __restrict__ eq,
+    uint32_t* __restrict__ ew, uint32_t* __restrict__ ecount, uint32_t* __restrict__ npairs) {
+    __shared__ uint32_t A[kReduceCap], Bv[kReduceCap];
+    __shared__ uint32_t rc[kReduceRowsMax + 1], cur[kReduceRowsMax];
+    __shared__ uint32_t wave_tot[kReduceThreads / 64];
+    __shared__ uint32_t big;
+    const uint32_t s = blockIdx.x;
+    const int tid = threadIdx.x;
+    const uint32_t m = (uint32_t)min((uint64_t)cursor[s], cap);
+    const uint32_t rows = 1u << row_bits;
+    const uint32_t p0 = s << row_bits;
+    const unsigned long long* src = region + (uint64_t)s * cap;
+    if (m == 0) {
+        if (tid == 0) ecount[s] = npairs[s] = 0;
+        return;
+    }
+    if (tid <= (int)rows) rc[tid] = 0;
+    if (tid == 0) big = 0;
+    __syncthreads();
+    // 1. v = row << 24 | q, row histogram
+    for (uint32_t i = tid; i < m; i += kReduceThreads) {
+        const unsigned long long x = src[i];
+        const uint32_t row = (uint32_t)(x >> 32) - p0;
+        A[i] = (row << 24) | (uint32_t)x;
+        atomicAdd(&rc[row], 1u);
+    }
+    __syncthreads();
+    {
+        const uint32_t v = tid < (int)rows ? rc[tid] : 0u;
+        if (v > kRankRowMax) big = 1;
+        uint32_t excl, total;
+        block_scan_n<kReduceThreads>(v, excl, total, wave_tot);
+        if (tid < (int)rows) rc[tid] = cur[tid] = excl;
+        if (tid == 0) rc[rows] = m;
+    }
+    __syncthreads();
+    if (!big) {
+        // 2. group by row, then rank sort inside each row (position = row start + #smaller or
+        //    equal-and-earlier)
+        for (uint32_t i = tid; i < m; i += kReduceThreads) {
+            const uint32_t v = A[i];
+            Bv[atomicAdd(&cur[v >> 24], 1u)] = v;
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < m; i += kReduceThreads) {
+            const uint32_t v = Bv[i];
+            const uint32_t rs = rc[v >> 24], re = rc[(v >> 24) + 1];
+            uint32_t rank = 0;
+            for (uint32_t j = rs; j < re; ++j) {
+                const uint32_t u = Bv[j];
+                rank += u < v || (u == v && j < i);
+            }
+            A[rs + rank] = v;
+        }
+    } else {
+        // a long row: bitonic sort of the whole shard (padding sorts last)
+        uint32_t np = 1;
+        while (np < m) np <<= 1;
+        for (uint32_t i = m + tid; i < np; i += kReduceThreads) A[i] = 0xFFFFFFFFu;
+        __syncthreads();
+        for (uint32_t k2 = 2; k2 <= np; k2 <<= 1)
+            for (uint32_t j = k2 >> 1; j > 0; j >>= 1) {
+                for (uint32_t i = tid; i < np; i += kReduceThreads) {
+                    const uint32_t l = i ^ j;
+                    if (l > i) {
+                        const uint32_t x = A[i], y = A[l];
+                        if (((i & k2) == 0) == (x > y)) {
+                            A[i] = y;
+                            A[l] = x;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+    }
+    __syncthreads();
+    // 3. runs of equal v = one pair, w = run length; contiguous chunks per thread keep the
+    //    output in (p, q) order
+    const uint32_t chunk = (m + kReduceThreads - 1) / kReduceThreads;
+    const uint32_t c0 = min(m, tid * chunk), c1 = min(m, c0 + chunk);
+    uint32_t kept = 0, heads = 0;
+    for (uint32_t i = c0; i < c1; ++i) {
+        const uint32_t v = A[i];
+        if (i > 0 && A[i - 1] == v) continue;
+        uint32_t e = i + 1;
+        while (e < m && A[e] == v) ++e;
+        ++heads;
+        kept += e - i >= min_shared;
+    }
+    uint32_t excl, total, hx, htotal;
+    block_scan_n<kReduceThreads>(kept, excl, total, wave_tot);
+    block_scan_n<kReduceThreads>(heads, hx, htotal, wave_tot);
+    if (tid == 0) {
+        ecount[s] = total;
+        npairs[s] = htotal;
+    }
+    uint32_t* const op = ep + (uint64_t)s * cap;
+    uint32_t* const oq = eq + (uint64_t)s * cap;
+    uint32_t* const ow = ew + (uint64_t)s * cap;
+    for (uint32_t i = c0; i < c1; ++i) {
+        const uint32_t v = A[i];
+        if (i > 0 && A[i - 1] == v) continue;
+        uint32_t e = i + 1;
+        while (e < m && A[e] == v) ++e;
+        if (e - i < min_shared) continue;
+        op[excl] = p0 + (v >> 24);
+        oq[excl] = v & 0xFFFFFFu;
+        ow[excl] = e - i;
+        ++excl;
+    }
+}
+
+// shard edge regions -> the caller's (p, q, w) arrays at the shards' exclusive offsets
+__global__ void compact_edges_kernel(const uint32_t* __restrict__ ep, const uint32_t* __restrict__ eq,
+                                     const uint32_t* __restrict__ ew, uint64_t cap,
+                                     const uint32_t* __restrict__ ecount, const unsigned long long* __restrict__ eoff,
+                                     uint32_t* __restrict__ out_p, uint32_t* __restrict__ out_q,
+                                     uint32_t* __restrict__ out_w, uint64_t out_cap) {
+    const uint32_t s = blockIdx.x;
+    const uint32_t m = ecount[s];
+    const unsigned long long o = eoff[s];
+    for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
+        if (o + i >= out_cap) break;
+        const uint64_t k = (uint64_t)s * cap + i;
+        out_p[o + i] = ep[k];
+        out_q[o + i] = eq[k];
+        out_w[o + i] = ew[k];
+    }
 }
 
 // shard regions -> one contiguous array (shard order)
@@ -710,13 +891,21 @@ struct kmp_postings {
     bool timing = false;
     bool bucketed = true;       // try the bucketed layout first
     bool last_bucketed = false; // layout the last call ran on
+    bool last_pshard = false;   // ... and whether it finished with the p-shard tail
     uint64_t shard_cap = 0;     // bucketed: capacity of each output shard region
+    uint64_t ps_cap = 0;        // p-shard: keys per row-range region
+    bool ps_ok = false;         // the last bucketed front end left its keys in row-range regions
+    bool pshard = false;        // use the p-shard tail when the row ranges fit (opt-in: slower)
+    PShard ps{};
+    Grow<uint32_t> ps_cursor, e3, ecnt;
+    Grow<unsigned long long> eoff;
     int ablate = getenv("KMP_BUCKET_ABLATE") ? atoi(getenv("KMP_BUCKET_ABLATE")) : 0;  // diagnostics
     hipEvent_t ev[KMP_POSTINGS_STAGES + 1] = {};
     ~kmp_postings() {
         keys.release(); sorted.release(); inc.release(); inc_sorted.release(); uniq.release();
         bstats.release(); btot.release(); boff.release();
         w.release(); keep.release(); pos.release(); small.release(); cnt.release(); flags.release(); tmp.release();
+        ps_cursor.release(); e3.release(); ecnt.release(); eoff.release();
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
     }
@@ -750,10 +939,10 @@ int front_flat(kmp_postings* ws, uint64_t slots, const Layout& lay, const uint16
                uint32_t heavy_df, int require_class_diff, unsigned long long* n_inc, kmp_postings_stats* stats,
                hipStream_t st) {
     size_t t_sort = 0;
-    PG(rocprim::radix_sort_keys(nullptr, t_sort, ws->keys.p, ws->sorted.p, (size_t)slots, lay.sort_lo, lay.sort_hi,
+    PG(rocprim::radix_sort_keys<SortCfg>(nullptr, t_sort, ws->keys.p, ws->sorted.p, (size_t)slots, lay.sort_lo, lay.sort_hi,
                                 st));
     PG(ws->tmp.reserve(std::max(t_sort, ws->tmp.n)));
-    PG(rocprim::radix_sort_keys(ws->tmp.p, t_sort, ws->keys.p, ws->sorted.p, (size_t)slots, lay.sort_lo,
+    PG(rocprim::radix_sort_keys<SortCfg>(ws->tmp.p, t_sort, ws->keys.p, ws->sorted.p, (size_t)slots, lay.sort_lo,
                                 lay.sort_hi, st));
     ws->mark(2, st);
 
@@ -801,24 +990,37 @@ int front_flat(kmp_postings* ws, uint64_t slots, const Layout& lay, const uint16
     return KMP_OK;
 }
 
-// Bucketed front end (keys in ws->keys, flags[0..1] written by the key kernel): sort on the
-// bucket field, bucket bounds, LDS group + expand per bucket into kShards regions, gather into
-// ws->inc.  Marks 2 (sort), 3 (group + expand), 4 (gather).  *fallback = true when a bucket
-// does not fit or a class id is too wide (the caller reruns on the flat layout).
+// p-shard geometry for n proteins: rows per shard 2^row_bits (<= kReduceRowsMax), q < 2^24
+bool pshard_geometry(uint32_t n, unsigned* row_bits, uint32_t* n_shards) {
+    if (n >= (1u << 24)) return false;
+    const unsigned pb = bits_for(n);
+    const unsigned r = pb > 12 ? std::min(8u, pb - 12) : 0u;
+    *row_bits = r;
+    *n_shards = (n + (1u << r) - 1) >> r;
+    return true;
+}
+
+// Bucketed front end (keys `in`, flags[0..1] written by the key kernel): sort on the bucket
+// field, bucket bounds, LDS group + expand per bucket.  Output modes:
+//   pshard == false: pair keys p*N+q into kShards regions, gathered into ws->inc (*n_inc keys);
+//   pshard == true:  pair keys p<<32|q into the row-range regions of ws->ps (ws->ps_ok tells
+//                    whether every range fit; if not the caller uses pshard == false).
+// Marks 2 (sort), 3 (group + expand), 4 (gather).  *fallback = true when a bucket does not fit
+// or a class id is too wide (the caller reruns on the flat layout).
 int front_bucketed(kmp_postings* ws, const unsigned long long* in, uint64_t slots, const Layout& lay, uint32_t n,
-                   uint32_t heavy_df,
-                   int require_class_diff, unsigned long long* n_inc, bool* fallback, kmp_postings_stats* stats,
-                   hipStream_t st) {
+                   uint32_t heavy_df, int require_class_diff, bool pshard, unsigned long long* n_inc,
+                   bool* fallback, kmp_postings_stats* stats, hipStream_t st) {
     *fallback = false;
+    ws->ps_ok = false;
     size_t t_sort = 0;
     PG(ws->sorted.reserve(slots));
-    PG(rocprim::radix_sort_keys(nullptr, t_sort, in, ws->sorted.p, (size_t)slots, lay.sort_lo, lay.sort_hi, st));
+    PG(rocprim::radix_sort_keys<SortCfg>(nullptr, t_sort, in, ws->sorted.p, (size_t)slots, lay.sort_lo, lay.sort_hi, st));
     PG(ws->tmp.reserve(std::max(t_sort, ws->tmp.n)));
-    PG(rocprim::radix_sort_keys(ws->tmp.p, t_sort, in, ws->sorted.p, (size_t)slots, lay.sort_lo, lay.sort_hi, st));
+    PG(rocprim::radix_sort_keys<SortCfg>(ws->tmp.p, t_sort, in, ws->sorted.p, (size_t)slots, lay.sort_lo, lay.sort_hi, st));
     ws->mark(2, st);
     const uint32_t nb = 1u << lay.bbits;
-    PG(ws->cnt.reserve(2 * (uint64_t)nb + 2));  // bucket starts, large-bucket list + its count
-    PG(ws->bstats.reserve(kShards * 8 + kShards));
+    PG(ws->cnt.reserve(2 * (uint64_t)nb + 2));  // bucket starts, large-bucket list
+    PG(ws->bstats.reserve(std::max<uint64_t>(ws->bstats.n, kShards * 8 + kShards)));
     uint32_t* bstart = ws->cnt.p;
     uint32_t* list = ws->cnt.p + nb + 1;
     uint32_t* list_count = ws->flags.p + 2;
@@ -826,35 +1028,75 @@ int front_bucketed(kmp_postings* ws, const unsigned long long* in, uint64_t slot
     unsigned long long* gstats = ws->bstats.p;          // kShards x 8 (kSt* slots)
     unsigned long long* cursor = gstats + kShards * 8;  // kShards
     bucket_bounds_kernel<<<(nb + 1 + 255) / 256, 256, 0, st>>>(ws->sorted.p, slots, lay.sort_lo, nb, bstart);
-    if (ws->shard_cap == 0) ws->shard_cap = slots / 2 / kShards + 4096;
+    PShard ps{};
+    if (pshard) {
+        if (!pshard_geometry(n, &ps.row_bits, &ps.n_shards)) pshard = false;
+    }
+    if (pshard) {
+        if (ws->ps_cap == 0) ws->ps_cap = std::min<uint64_t>(kReduceCap, slots / 4 / ps.n_shards + 256);
+        PG(ws->ps_cursor.reserve(ps.n_shards));
+        ps.cursor = ws->ps_cursor.p;
+    } else if (ws->shard_cap == 0) {
+        ws->shard_cap = slots / 2 / kShards + 4096;
+    }
     for (int attempt = 0; attempt < 3; ++attempt) {
-        PG(ws->inc_sorted.reserve(ws->shard_cap * kShards));  // shard regions
+        if (pshard) {
+            ps.cap = ws->ps_cap;
+            PG(ws->inc_sorted.reserve(ps.cap * ps.n_shards));  // row-range regions
+            ps.region = ws->inc_sorted.p;
+            PG(hipMemsetAsync(ps.cursor, 0, ps.n_shards * sizeof(uint32_t), st));
+        } else {
+            PG(ws->inc_sorted.reserve(ws->shard_cap * kShards));  // shard regions
+        }
         PG(hipMemsetAsync(gstats, 0, (kShards * 8 + kShards) * sizeof(unsigned long long), st));
         PG(hipMemsetAsync(list_count, 0, sizeof(uint32_t), st));
-#define KMP_SMALL(A)                                                                                          \
-    bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallSub, A>                             \
+#define KMP_SMALL(A, P)                                                                                       \
+    bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallSub, A, P>                          \
         <<<nb, kBucketSmallThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,     \
-                                             ws->inc_sorted.p, ws->shard_cap, cursor, gstats, flags, list, list_count)
-        switch (ws->ablate) {  // diagnostics (KMP_BUCKET_ABLATE): phase cut-offs, results invalid
-            case 1: KMP_SMALL(1); break;
-            case 2: KMP_SMALL(2); break;
-            case 3: KMP_SMALL(3); break;
-            case 4: KMP_SMALL(4); break;
-            case 5: KMP_SMALL(5); break;
-            default: KMP_SMALL(0);
+                                             ws->inc_sorted.p, ws->shard_cap, cursor, gstats, flags, list,    \
+                                             list_count, ps)
+        if (pshard) {
+            KMP_SMALL(0, true);
+            bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeSub, true>
+                <<<256, kBucketLargeThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
+                                                      ws->inc_sorted.p, ws->shard_cap, cursor, gstats, flags, list,
+                                                      list_count, ps);
+        } else {
+            switch (ws->ablate) {  // diagnostics (KMP_BUCKET_ABLATE): phase cut-offs, results invalid
+                case 1: KMP_SMALL(1, false); break;
+                case 2: KMP_SMALL(2, false); break;
+                case 3: KMP_SMALL(3, false); break;
+                case 4: KMP_SMALL(4, false); break;
+                case 5: KMP_SMALL(5, false); break;
+                default: KMP_SMALL(0, false);
+            }
+            bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeSub, false>
+                <<<256, kBucketLargeThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
+                                                      ws->inc_sorted.p, ws->shard_cap, cursor, gstats, flags, list,
+                                                      list_count, ps);
         }
 #undef KMP_SMALL
-        bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeSub>
-            <<<256, kBucketLargeThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
-                                                  ws->inc_sorted.p, ws->shard_cap, cursor, gstats, flags, list,
-                                                  list_count);
         ws->mark(3, st);
         unsigned long long g[kShards * 8 + kShards];
         uint32_t h_flags[2] = {0, 0};
         PG(hipMemcpyAsync(g, gstats, sizeof g, hipMemcpyDeviceToHost, st));
         PG(hipMemcpyAsync(h_flags, flags, sizeof h_flags, hipMemcpyDeviceToHost, st));
+        std::vector<uint32_t> pc;
+        if (pshard) {
+            pc.resize(ps.n_shards);
+            PG(hipMemcpyAsync(pc.data(), ps.cursor, ps.n_shards * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        }
         PG(hipStreamSynchronize(st));
         if (h_flags[0] || h_flags[1]) {
+            if (getenv("KMP_DEBUG")) {
+                std::vector<uint32_t> bs(nb + 1);
+                (void)hipMemcpy(bs.data(), bstart, (nb + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost);
+                uint32_t mx = 0;
+                for (uint32_t b = 0; b < nb; ++b) mx = std::max(mx, bs[b + 1] - bs[b]);
+                fprintf(stderr, "kmp: bucketed -> flat (bucket/sub-bucket overflow %u, class width %u; nb %u, "
+                        "largest bucket %u, keys %u of %llu slots, sort bits [%u,%u))\n", h_flags[0], h_flags[1], nb,
+                        mx, bs[nb], (unsigned long long)slots, lay.sort_lo, lay.sort_hi);
+            }
             *fallback = true;
             return KMP_OK;
         }
@@ -866,6 +1108,27 @@ int front_bucketed(kmp_postings* ws, const unsigned long long* in, uint64_t slot
         }
         fill_stats(stats, acc);
         *n_inc = acc[kStInc];
+        if (pshard && getenv("KMP_DEBUG")) {
+            uint32_t most = pc.empty() ? 0u : *std::max_element(pc.begin(), pc.end());
+            fprintf(stderr, "kmp: p-shard attempt %d: shards %u cap %llu most %u\n", attempt, ps.n_shards,
+                    (unsigned long long)ps.cap, most);
+        }
+        if (pshard) {
+            const uint32_t most = pc.empty() ? 0u : *std::max_element(pc.begin(), pc.end());
+            if (most <= ps.cap) {
+                ws->ps_ok = true;
+                ws->ps = ps;
+                ws->mark(4, st);
+                return KMP_OK;
+            }
+            if (most > (uint32_t)kReduceCap) {  // a row range too large for LDS: key-sort tail
+                pshard = false;
+                if (ws->shard_cap == 0) ws->shard_cap = slots / 2 / kShards + 4096;
+                continue;
+            }
+            ws->ps_cap = std::min<uint64_t>(kReduceCap, most + most / 4 + 64);  // grow, rerun
+            continue;
+        }
         unsigned long long most = 0;
         for (int s = 0; s < kShards; ++s) most = std::max(most, acc[kStN + s]);
         if (most <= ws->shard_cap) {
@@ -882,6 +1145,45 @@ int front_bucketed(kmp_postings* ws, const unsigned long long* in, uint64_t slot
         ws->shard_cap = most + most / 4 + 4096;  // grow the regions and rerun the expansion
     }
     return KMP_EDEVICE;
+}
+
+// p-shard tail: LDS reduce per row range, offsets, compaction.  Marks 5 (reduce), 6 (emit).
+int tail_pshard(kmp_postings* ws, uint32_t min_shared, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w, uint64_t cap,
+                uint64_t* n_edges, kmp_postings_stats* stats, hipStream_t st) {
+    const PShard& ps = ws->ps;
+    const uint32_t S = ps.n_shards;
+    PG(ws->e3.reserve(3 * ps.cap * S));
+    PG(ws->ecnt.reserve(2 * (uint64_t)S));
+    PG(ws->eoff.reserve(S));
+    uint32_t* ep = ws->e3.p;
+    uint32_t* eq = ep + ps.cap * S;
+    uint32_t* ew = eq + ps.cap * S;
+    uint32_t* ecount = ws->ecnt.p;
+    uint32_t* npairs = ws->ecnt.p + S;
+    shard_reduce_kernel<<<S, kReduceThreads, 0, st>>>(ps.region, ps.cursor, ps.cap, ps.row_bits, min_shared, ep, eq,
+                                                      ew, ecount, npairs);
+    size_t t_scan = 0;
+    PG(rocprim::exclusive_scan(nullptr, t_scan, ecount, ws->eoff.p, 0ull, (size_t)S,
+                               rocprim::plus<unsigned long long>(), st));
+    PG(ws->tmp.reserve(std::max(t_scan, ws->tmp.n)));
+    PG(rocprim::exclusive_scan(ws->tmp.p, t_scan, ecount, ws->eoff.p, 0ull, (size_t)S,
+                               rocprim::plus<unsigned long long>(), st));
+    ws->mark(5, st);
+    std::vector<uint32_t> h(2 * (size_t)S);
+    PG(hipMemcpyAsync(h.data(), ecount, 2 * (size_t)S * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    PG(hipStreamSynchronize(st));
+    uint64_t ne = 0, np = 0;
+    for (uint32_t s = 0; s < S; ++s) {
+        ne += h[s];
+        np += h[S + s];
+    }
+    if (stats) stats->pairs = np;
+    *n_edges = ne;
+    if (ne > cap) return KMP_EOVERFLOW;
+    if (ne) compact_edges_kernel<<<S, 256, 0, st>>>(ep, eq, ew, ps.cap, ecount, ws->eoff.p, d_p, d_q, d_w, cap);
+    ws->mark(6, st);
+    PG(hipGetLastError());
+    return KMP_OK;
 }
 
 // Shared tail: sort the pair keys, run-length encode -> (pair, w) in canonical order, keep
@@ -907,14 +1209,14 @@ int tail(kmp_postings* ws, const unsigned long long* in, unsigned long long n_in
         PG(ws->pos.reserve(n_inc));
     }
     size_t t2 = 0, t3 = 0, t4 = 0;
-    PG(rocprim::radix_sort_keys(nullptr, t2, in, ws->inc_sorted.p, (size_t)n_inc, 0u, pair_bits, st));
+    PG(rocprim::radix_sort_keys<SortCfg>(nullptr, t2, in, ws->inc_sorted.p, (size_t)n_inc, 0u, pair_bits, st));
     PG(rocprim::run_length_encode(nullptr, t3, ws->inc_sorted.p, (unsigned int)n_inc, ws->uniq.p, ws->w.p,
                                   ws->small.p + 1, st));
     if (filter_w)
         PG(rocprim::exclusive_scan(nullptr, t4, ws->keep.p, ws->pos.p, 0u, (size_t)n_inc, rocprim::plus<uint32_t>(),
                                    st));
     PG(ws->tmp.reserve(std::max({t2, t3, t4, ws->tmp.n})));
-    PG(rocprim::radix_sort_keys(ws->tmp.p, t2, in, ws->inc_sorted.p, (size_t)n_inc, 0u, pair_bits, st));
+    PG(rocprim::radix_sort_keys<SortCfg>(ws->tmp.p, t2, in, ws->inc_sorted.p, (size_t)n_inc, 0u, pair_bits, st));
     ws->mark(5, st);
     PG(rocprim::run_length_encode(ws->tmp.p, t3, ws->inc_sorted.p, (unsigned int)n_inc, ws->uniq.p, ws->w.p,
                                   ws->small.p + 1, st));
@@ -976,8 +1278,8 @@ int run_postings(kmp_postings* ws, MakeKeys make_keys, uint32_t n, int k, uint64
         ws->mark(0, st);
         make_keys(lay);
         ws->mark(1, st);
-        int rc = front_bucketed(ws, ws->keys.p, slots, lay, n, heavy_df, require_class_diff, &n_inc, &fallback, stats,
-                                st);
+        int rc = front_bucketed(ws, ws->keys.p, slots, lay, n, heavy_df, require_class_diff, ws->pshard, &n_inc,
+                                &fallback, stats, st);
         if (rc != KMP_OK) return rc;
     }
     if (fallback) {
@@ -990,7 +1292,9 @@ int run_postings(kmp_postings* ws, MakeKeys make_keys, uint32_t n, int k, uint64
         if (rc != KMP_OK) return rc;
     }
     ws->last_bucketed = !fallback;
-    int rc = tail(ws, ws->inc.p, n_inc, n, min_shared, d_p, d_q, d_w, cap, n_edges, stats, st);
+    ws->last_pshard = !fallback && ws->ps_ok;
+    int rc = ws->last_pshard ? tail_pshard(ws, min_shared, d_p, d_q, d_w, cap, n_edges, stats, st)
+                             : tail(ws, ws->inc.p, n_inc, n, min_shared, d_p, d_q, d_w, cap, n_edges, stats, st);
     if (rc == KMP_OK) finish_timing(ws, stats, st);
     return rc;
 }
@@ -1021,7 +1325,16 @@ int kmp_postings_set_layout(kmp_postings* ws, int bucketed) {
     return KMP_OK;
 }
 
-int kmp_postings_last_layout(const kmp_postings* ws) { return ws && ws->last_bucketed ? 1 : 0; }
+int kmp_postings_last_layout(const kmp_postings* ws) {
+    if (!ws || !ws->last_bucketed) return 0;
+    return ws->last_pshard ? 2 : 1;
+}
+
+int kmp_postings_set_pshard(kmp_postings* ws, int enable) {
+    if (!ws) return KMP_EINVAL;
+    ws->pshard = enable != 0;
+    return KMP_OK;
+}
 
 int kmp_dev_pairs_postings(kmp_postings* ws, const uint32_t* d_set, const uint32_t* d_set_len,
                            const uint64_t* d_res_off, const uint16_t* d_class, uint32_t n, int k, uint64_t slots,
@@ -1092,9 +1405,9 @@ int kmp_dev_keys_part(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_
     residue_keys_kernel<<<hi - lo, kResThreads, 0, st>>>(d_res, d_res_off, d_class, n, k, slots, lay, ws->keys.p,
                                                          ws->flags.p, lo, slot_lo);
     size_t t_sort = 0;
-    PG(rocprim::radix_sort_keys(nullptr, t_sort, ws->keys.p, d_out, (size_t)m, lay.sort_lo, lay.sort_hi, st));
+    PG(rocprim::radix_sort_keys<SortCfg>(nullptr, t_sort, ws->keys.p, d_out, (size_t)m, lay.sort_lo, lay.sort_hi, st));
     PG(ws->tmp.reserve(std::max(t_sort, ws->tmp.n)));
-    PG(rocprim::radix_sort_keys(ws->tmp.p, t_sort, ws->keys.p, d_out, (size_t)m, lay.sort_lo, lay.sort_hi, st));
+    PG(rocprim::radix_sort_keys<SortCfg>(ws->tmp.p, t_sort, ws->keys.p, d_out, (size_t)m, lay.sort_lo, lay.sort_hi, st));
     int rc = part_bounds(ws, d_out, m, lay.sort_lo, 1ull << lay.bbits, 1, parts, part_counts, st);
     if (rc != KMP_OK) return rc;
     uint32_t h_flags[2] = {0, 0};
@@ -1119,8 +1432,8 @@ int kmp_dev_pairs_keys(kmp_postings* ws, const unsigned long long* d_keys, uint6
     PG(hipMemsetAsync(ws->flags.p, 0, 4 * sizeof(uint32_t), st));
     unsigned long long ni = 0;
     bool fallback = false;
-    int rc = front_bucketed(ws, d_keys, m, lay, n, heavy_df < 2 ? 2 : heavy_df, require_class_diff, &ni, &fallback,
-                            stats, st);
+    int rc = front_bucketed(ws, d_keys, m, lay, n, heavy_df < 2 ? 2 : heavy_df, require_class_diff, false, &ni,
+                            &fallback, stats, st);
     if (rc != KMP_OK) return rc;
     if (fallback) return KMP_ESTATE;  // a k-mer too frequent for the LDS buckets
     *n_inc = ni;
@@ -1129,9 +1442,9 @@ int kmp_dev_pairs_keys(kmp_postings* ws, const unsigned long long* d_keys, uint6
     if (ni > out_cap || !d_out) return KMP_EOVERFLOW;
     const unsigned pair_bits = bits_for((uint64_t)n * n);
     size_t t2 = 0;
-    PG(rocprim::radix_sort_keys(nullptr, t2, ws->inc.p, d_out, (size_t)ni, 0u, pair_bits, st));
+    PG(rocprim::radix_sort_keys<SortCfg>(nullptr, t2, ws->inc.p, d_out, (size_t)ni, 0u, pair_bits, st));
     PG(ws->tmp.reserve(std::max(t2, ws->tmp.n)));
-    PG(rocprim::radix_sort_keys(ws->tmp.p, t2, ws->inc.p, d_out, (size_t)ni, 0u, pair_bits, st));
+    PG(rocprim::radix_sort_keys<SortCfg>(ws->tmp.p, t2, ws->inc.p, d_out, (size_t)ni, 0u, pair_bits, st));
     return part_bounds(ws, d_out, ni, 0, n, n, parts, part_counts, st);
 }
 

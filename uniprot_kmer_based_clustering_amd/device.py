@@ -218,8 +218,17 @@ class DevicePipeline:
         """Postings key layout: bucketed (LDS group + expand per hash bucket) or flat."""
         check(lib().kmp_postings_set_layout(self._workspace(), int(bucketed)), "kmp_postings_set_layout")
 
+    def set_pshard(self, enable: bool = True) -> None:
+        """Bucketed layout: finish with the row-range (p-shard) LDS reduction (default) or the
+        global pair-key sort."""
+        check(lib().kmp_postings_set_pshard(self._workspace(), int(enable)), "kmp_postings_set_pshard")
+
     def last_layout(self) -> str:
         return "bucketed" if lib().kmp_postings_last_layout(self._workspace()) else "flat"
+
+    def last_tail(self) -> str:
+        """How the last postings call reduced its pair keys: 'pshard' or 'sort'."""
+        return "pshard" if lib().kmp_postings_last_layout(self._workspace()) == 2 else "sort"
 
     def postings(self, min_shared: int = 1, require_class_diff: bool = True,
                  heavy_df: int = 0xFFFFFFFF, from_residues: bool = False) -> int:
