@@ -85,6 +85,18 @@ def stage_bytes(n_res, slots, n_inc, n_edges, n_uniq, tail="sort"):
     }
 
 
+def pmc_traffic(stage: str):
+    """HBM bytes per step of `stage` from the newest committed PMC table (profiles/r*_pmc_traffic.json,
+    made by tools/pmc_traffic.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of
+    this bench on config 3, FETCH_SIZE doubled per the gfx950 note in MI355X_MICROARCH.md)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return None, None
+    st = json.load(open(files[-1]))["stages"].get(stage)
+    return (st["bytes"] if st else None), os.path.relpath(files[-1], ROOT)
+
+
 def main():
     args = parse()
     import torch
@@ -177,8 +189,11 @@ def main():
                       for s in stage_ms}
             dom = max(stage_ms, key=stage_ms.get)
             ach = stages[dom]["GBs"]
+            traffic, source = (pmc_traffic(dom) if args.config == "config3" and args.engine == "residues"
+                               and tail == "sort" else (None, None))
             out["roofline"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                               "frac": ach / HBM_PEAK_GBS, "traffic": None, "kernel": dom,
+                               "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": source,
+                               "traffic_over_alg": traffic / byts[dom] if traffic else None, "kernel": dom,
                                "kernel_ms": stage_ms[dom], "alg_bytes_per_launch": byts[dom],
                                "layout": pipe.last_layout(), "tail": tail, "stages": stages,
                                "step_alg_bytes": sum(byts.values()),

@@ -1,0 +1,76 @@
+"""Per-kernel HBM traffic from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE; KiB per
+dispatch).  gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE counts half the bytes of a
+wide streaming read, so it is doubled; WRITE_SIZE is taken as is.
+Usage: python tools/pmc_traffic.py FETCH.csv WRITE.csv [calls_per_step]"""
+import collections
+import csv
+import json
+import sys
+
+sys.path.insert(0, __file__.rsplit("/", 1)[0])
+from prof_summary import short  # noqa: E402
+
+
+def load(path):
+    out = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        out[(short(r["Kernel_Name"]), int(r["Grid_Size"]))].append(float(r["Counter_Value"]) * 1024.0)
+    return out
+
+
+def main():
+    fetch, write = load(sys.argv[1]), load(sys.argv[2])
+    rows = []
+    for key in sorted(set(fetch) | set(write), key=lambda k: -(sum(fetch.get(k, [0])) + sum(write.get(k, [0])))):
+        f, w = fetch.get(key, []), write.get(key, [])
+        n = max(len(f), len(w))
+        fb = 2.0 * sum(f) / max(1, len(f))
+        wb = sum(w) / max(1, len(w))
+        rows.append({"kernel": key[0], "grid": key[1], "dispatches": n, "read_bytes": fb, "write_bytes": wb,
+                     "bytes": fb + wb})
+    print(f"{'kernel':<52} {'grid':>10} {'disp':>5} {'read MB':>9} {'write MB':>9}")
+    for r in rows[:20]:
+        print(f"{r['kernel'][:52]:<52} {r['grid']:>10} {r['dispatches']:>5} {r['read_bytes']/1e6:>9.1f} "
+              f"{r['write_bytes']/1e6:>9.1f}")
+    # per-step traffic of the postings stages (bucketed layout, sort tail): calls = residue_keys
+    # dispatches; of the two radix sorts the one with the larger grid is the bucket (code) sort
+    calls = max([r["dispatches"] for r in rows if r["kernel"] == "residue_keys_kernel"] or [1])
+    sort_grids = sorted({r["grid"] for r in rows if r["kernel"] == "rocprim::radix_sort_onesweep_iteration"})
+    code_grid = sort_grids[-1] if sort_grids else -1
+
+    def stage(r):
+        k = r["kernel"]
+        if k == "residue_keys_kernel" or k == "set_keys_kernel":
+            return "keys"
+        if k.startswith("rocprim::radix_sort_onesweep"):
+            same = [g for g in sort_grids]
+            if k.endswith("iteration"):
+                return "code_sort" if r["grid"] == code_grid else "pair_sort"
+            # histogram kernels: match by the iteration grid they precede (largest = code sort)
+            hist = sorted({x["grid"] for x in rows if x["kernel"] == k and x["read_bytes"] > 0})
+            return "code_sort" if hist and r["grid"] == hist[-1] else ("pair_sort" if r["read_bytes"] > 0 else None)
+        if "bucket_" in k:
+            return "count"
+        if k == "gather_shards_kernel":
+            return "write"
+        if "reduce_by_key" in k or k == "emit_edges_kernel":
+            return "rle_emit"
+        return None
+
+    stages = collections.defaultdict(lambda: {"read_bytes": 0.0, "write_bytes": 0.0})
+    for r in rows:
+        st = stage(r)
+        if st:
+            per_step = r["dispatches"] / calls
+            stages[st]["read_bytes"] += r["read_bytes"] * per_step
+            stages[st]["write_bytes"] += r["write_bytes"] * per_step
+    for st in stages.values():
+        st["bytes"] = st["read_bytes"] + st["write_bytes"]
+    print("per-step stage traffic (MB):", {k: round(v["bytes"] / 1e6, 1) for k, v in stages.items()})
+    if len(sys.argv) > 3:
+        json.dump({"calls": calls, "correction": "FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; KiB counters",
+                   "stages": stages, "kernels": rows}, open(sys.argv[3], "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
