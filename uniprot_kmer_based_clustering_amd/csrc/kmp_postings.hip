@@ -2,7 +2,7 @@
 // GPU as sort / expand / reduce.
 //
 //   reference (file:line)                                  here
-//   Protein::new windows + codes (protein.rs:82-94)        residue_keys_kernel: one key per window
+//   Protein::new windows + codes (protein.rs:82-94)        residue_keys_chunk_kernel: one key per window
 //   per-protein sort + dedup (main.rs:280-282)             duplicates of (k-mer, p) end up adjacent
 //                                                          after the stable code sort; skipped there
 //   global df: sorted Vec<(kmer, df)> (main.rs:77-122)     radix sort of the keys on the code bits;
@@ -141,47 +141,95 @@ __global__ __launch_bounds__(256) void set_keys_kernel(const uint32_t* __restric
 }
 
 // one key per window straight from the residues (Protein::new, protein.rs:82-94: window j of
-// protein p is residues [j, j+k), radix-21, first residue most significant); same slot layout.
-// The residues are recoded once into LDS (byte -> code through an LDS copy of the table), the
-// windows are formed from LDS.
-constexpr int kResThreads = 256;
-constexpr int kResChunk = 2048;  // windows per LDS chunk
-__global__ __launch_bounds__(kResThreads) void residue_keys_kernel(const uint8_t* __restrict__ res,
-                                                                   const uint64_t* __restrict__ res_off,
-                                                                   const uint16_t* __restrict__ cls, uint32_t n,
-                                                                   int k, uint64_t slots, Layout lay,
-                                                                   unsigned long long* __restrict__ keys,
-                                                                   uint32_t* __restrict__ flags, uint32_t p0 = 0,
-                                                                   uint64_t slot0 = 0) {
-    // proteins p0 + blockIdx.x; keys[i - slot0] for slot i (a slice starts at slot0 = its first
-    // protein's set_base); the block with p == n fills the buffer's tail up to `slots`
+// protein p is residues [j, j+k), radix-21, first residue most significant), same slot layout.
+// Workgroup g owns slots [slot_begin + g*kKeyChunk, ... + kKeyChunk) of proteins
+// [p_lo, p_hi) (about 13 proteins per chunk at L ~ 300).  It finds them by binary search on
+// set_base, recodes just the residue span its windows need into LDS (byte -> code), and writes the
+// chunk's keys coalesced; slots past a protein's windows (and past the last region) get kNoKey.
+// keys[i - slot_begin] for slot i.
+constexpr int kKeyThreads = 256;
+constexpr uint32_t kKeyChunk = 4096;
+constexpr uint32_t kKeyProtMax = kKeyChunk / 4 + 2;                // a region spans >= 4 slots
+// residues a chunk can need: a protein's region is longer than its residue count, so the span is
+// at most the chunk plus the last window's k - 1 residues
+constexpr uint32_t kKeyResMax = kKeyChunk + 64;
+
+// first[c] = the protein whose region holds the chunk's first slot (p_hi: the tail past the last
+// region); one thread per protein writes the chunk starts that fall in its region
+__global__ void chunk_first_kernel(const uint64_t* __restrict__ res_off, uint32_t p_lo, uint32_t p_hi,
+                                   uint64_t slot_begin, uint64_t slot_end, uint32_t n_chunks,
+                                   uint32_t* __restrict__ first) {
+    const uint32_t p = p_lo + blockIdx.x * blockDim.x + threadIdx.x;
+    if (p > p_hi) return;
+    const uint64_t b = set_base(res_off[p], p) - slot_begin;
+    const uint64_t e = (p < p_hi ? set_base(res_off[p + 1], p + 1) : slot_end) - slot_begin;
+    for (uint64_t c = (b + kKeyChunk - 1) / kKeyChunk; c * kKeyChunk < e && c < n_chunks; ++c) first[c] = p;
+}
+
+__global__ __launch_bounds__(kKeyThreads) void residue_keys_chunk_kernel(
+    const uint8_t* __restrict__ res, const uint64_t* __restrict__ res_off, const uint16_t* __restrict__ cls,
+    int k, uint32_t p_hi, uint64_t slot_begin, uint64_t slot_end, const uint32_t* __restrict__ chunk_first,
+    Layout lay, unsigned long long* __restrict__ keys, uint32_t* __restrict__ flags) {
     __shared__ uint8_t lut[256];
-    __shared__ uint8_t rc[kResChunk + kMaxK];
-    const uint32_t p = p0 + blockIdx.x;
+    __shared__ uint8_t rc[kKeyResMax];
+    __shared__ uint32_t pb[kKeyProtMax + 1];   // region start of each protein, relative to c0 (may wrap)
+    __shared__ int32_t pr[kKeyProtMax];        // LDS index of the protein's residue 0 (may be < 0)
+    __shared__ uint32_t pw[kKeyProtMax];       // window count
+    __shared__ uint16_t pc[kKeyProtMax];       // class
+    __shared__ uint32_t s_np;
+    __shared__ uint64_t s_r0, s_r1;
     const int tid = threadIdx.x;
-    keys -= slot0;
-    if (p == n) {
-        for (uint64_t i = set_base(res_off[n], n) + tid; i < slots; i += kResThreads) keys[i] = kNoKey;
-        return;
-    }
+    const uint64_t c0 = slot_begin + (uint64_t)blockIdx.x * kKeyChunk;
+    const uint64_t c1 = min(c0 + kKeyChunk, slot_end);
+    const uint32_t first = chunk_first[blockIdx.x];
     lut[tid] = c_lut.v[tid];
-    const uint64_t off = res_off[p], L = res_off[p + 1] - off;
-    const uint64_t nw = L >= (uint64_t)k ? L - k + 1 : 0;
-    const uint64_t b = set_base(off, p), e = set_base(res_off[p + 1], p + 1);
-    const uint16_t c = cls[p];
-    if (tid == 0) check_class(c, lay, flags);
-    for (uint64_t i = b + nw + tid; i < e; i += kResThreads) keys[i] = kNoKey;
-    for (uint64_t c0 = 0; c0 < nw; c0 += kResChunk) {
-        const uint32_t w = (uint32_t)std::min<uint64_t>(kResChunk, nw - c0);
-        const uint32_t r = w + k - 1;
-        __syncthreads();
-        for (uint32_t t = tid; t < r; t += kResThreads) rc[t] = lut[res[off + c0 + t]];
-        __syncthreads();
-        for (uint32_t j = tid; j < w; j += kResThreads) {
-            uint32_t v = 0;
-            for (int t = 0; t < k; ++t) v = v * kRadix + rc[j + t];
-            keys[b + c0 + j] = make_key(v, c, p, lay);
+    if (tid == 0) {
+        s_np = 0;
+        s_r0 = s_r1 = 0;
+    }
+    __syncthreads();
+    // the chunk's proteins: first + t while its region starts before c1 (one parallel round)
+    for (uint32_t t = tid; t < kKeyProtMax && first + t < p_hi; t += kKeyThreads) {
+        const uint32_t p = first + t;
+        const uint64_t off = res_off[p], L = res_off[p + 1] - off;
+        const uint64_t b = set_base(off, p);
+        if (b >= c1) break;
+        const uint32_t nw = L >= (uint64_t)k ? (uint32_t)(L - k + 1) : 0u;
+        pb[t] = (uint32_t)(b - c0);  // wraps for the first protein when it starts before c0
+        pw[t] = nw;
+        pc[t] = cls[p];
+        check_class(pc[t], lay, flags);
+        atomicMax(&s_np, t + 1);
+        const uint64_t j0 = c0 > b ? c0 - b : 0;
+        const uint64_t j1 = min<uint64_t>(nw, c1 - b);
+        if (t == 0) s_r0 = off + min<uint64_t>(j0, L);
+        if (j1 > j0) atomicMax((unsigned long long*)&s_r1, (unsigned long long)(off + j1 + k - 1));
+    }
+    __syncthreads();
+    const uint32_t np = s_np;
+    const uint64_t r0 = s_r0, r1 = max(s_r0, s_r1);
+    for (uint64_t i = r0 + tid; i < r1; i += kKeyThreads) rc[i - r0] = lut[res[i]];
+    for (uint32_t t = tid; t < np; t += kKeyThreads) pr[t] = (int32_t)((int64_t)res_off[first + t] - (int64_t)r0);
+    __syncthreads();
+    for (uint32_t i = tid; i < (uint32_t)(c1 - c0); i += kKeyThreads) {
+        unsigned long long x = kNoKey;
+        if (np) {
+            // protein of slot c0 + i: last t with region start <= c0 + i (t = 0 may start before c0)
+            uint32_t a = 0, b = np;
+            while (a + 1 < b) {
+                const uint32_t mid = (a + b) >> 1;
+                if (pb[mid] <= i) a = mid;
+                else b = mid;
+            }
+            const uint32_t j = i - pb[a];  // window index (pb[0] wraps: i - pb[0] = c0 + i - b0)
+            if (j < pw[a]) {
+                const uint8_t* w = rc + (pr[a] + (int32_t)j);
+                uint32_t v = 0;
+                for (int t = 0; t < k; ++t) v = v * kRadix + w[t];
+                x = make_key(v, pc[a], first + a, lay);
+            }
         }
+        keys[c0 + i - slot_begin] = x;
     }
 }
 
@@ -897,7 +945,7 @@ struct kmp_postings {
     bool ps_ok = false;         // the last bucketed front end left its keys in row-range regions
     bool pshard = false;        // use the p-shard tail when the row ranges fit (opt-in: slower)
     PShard ps{};
-    Grow<uint32_t> ps_cursor, e3, ecnt;
+    Grow<uint32_t> ps_cursor, e3, ecnt, chunk_first;
     Grow<unsigned long long> eoff;
     int ablate = getenv("KMP_BUCKET_ABLATE") ? atoi(getenv("KMP_BUCKET_ABLATE")) : 0;  // diagnostics
     hipEvent_t ev[KMP_POSTINGS_STAGES + 1] = {};
@@ -905,7 +953,7 @@ struct kmp_postings {
         keys.release(); sorted.release(); inc.release(); inc_sorted.release(); uniq.release();
         bstats.release(); btot.release(); boff.release();
         w.release(); keep.release(); pos.release(); small.release(); cnt.release(); flags.release(); tmp.release();
-        ps_cursor.release(); e3.release(); ecnt.release(); eoff.release();
+        ps_cursor.release(); e3.release(); ecnt.release(); eoff.release(); chunk_first.release();
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
     }
@@ -1260,6 +1308,20 @@ int postings_args(kmp_postings* ws, int k, uint64_t* n_edges, kmp_postings_stats
     return KMP_OK;
 }
 
+// keys of proteins [p_lo, p_hi) into ws->keys (slots [slot_begin, slot_end) of the batch layout)
+hipError_t launch_residue_keys(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off,
+                               const uint16_t* d_class, int k, uint32_t p_lo, uint32_t p_hi, uint64_t slot_begin,
+                               uint64_t slot_end, const Layout& lay, hipStream_t st) {
+    const uint32_t g = (uint32_t)((slot_end - slot_begin + kKeyChunk - 1) / kKeyChunk);
+    hipError_t e = ws->chunk_first.reserve(g + 1);
+    if (e != hipSuccess) return e;
+    chunk_first_kernel<<<(p_hi - p_lo + 1 + 255) / 256, 256, 0, st>>>(d_res_off, p_lo, p_hi, slot_begin, slot_end, g,
+                                                                      ws->chunk_first.p);
+    residue_keys_chunk_kernel<<<g, kKeyThreads, 0, st>>>(d_res, d_res_off, d_class, k, p_hi, slot_begin, slot_end,
+                                                          ws->chunk_first.p, lay, ws->keys.p, ws->flags.p);
+    return hipGetLastError();
+}
+
 // Both entry points: keys from `make_keys(layout)`, bucketed front end (flat on fallback), tail.
 template <class MakeKeys>
 int run_postings(kmp_postings* ws, MakeKeys make_keys, uint32_t n, int k, uint64_t slots, const uint16_t* d_class,
@@ -1276,7 +1338,7 @@ int run_postings(kmp_postings* ws, MakeKeys make_keys, uint32_t n, int k, uint64
     bool fallback = true;
     if (lay.bucketed) {
         ws->mark(0, st);
-        make_keys(lay);
+        PG(make_keys(lay));
         ws->mark(1, st);
         int rc = front_bucketed(ws, ws->keys.p, slots, lay, n, heavy_df, require_class_diff, ws->pshard, &n_inc,
                                 &fallback, stats, st);
@@ -1286,7 +1348,7 @@ int run_postings(kmp_postings* ws, MakeKeys make_keys, uint32_t n, int k, uint64
         lay = make_layout(n, k, slots, false);
         if (lay.sort_hi > 64) return KMP_EINVAL;
         ws->mark(0, st);
-        make_keys(lay);
+        PG(make_keys(lay));
         ws->mark(1, st);
         int rc = front_flat(ws, slots, lay, d_class, n, heavy_df, require_class_diff, &n_inc, stats, st);
         if (rc != KMP_OK) return rc;
@@ -1348,6 +1410,7 @@ int kmp_dev_pairs_postings(kmp_postings* ws, const uint32_t* d_set, const uint32
     auto keys = [&](const Layout& lay) {
         set_keys_kernel<<<n + 1, 256, 0, st>>>(d_set, d_set_len, d_res_off, d_class, n, slots, lay, ws->keys.p,
                                                ws->flags.p);
+        return hipGetLastError();
     };
     return run_postings(ws, keys, n, k, slots, d_class, heavy_df, min_shared, require_class_diff, d_p, d_q, d_w, cap,
                         n_edges, stats, st);
@@ -1362,8 +1425,7 @@ int kmp_dev_pairs_residues(kmp_postings* ws, const uint8_t* d_res, const uint64_
     if (!d_res || !d_res_off || !d_class) return KMP_EINVAL;
     hipStream_t st = as_stream(stream);
     auto keys = [&](const Layout& lay) {
-        residue_keys_kernel<<<n + 1, kResThreads, 0, st>>>(d_res, d_res_off, d_class, n, k, slots, lay, ws->keys.p,
-                                                           ws->flags.p);
+        return launch_residue_keys(ws, d_res, d_res_off, d_class, k, 0u, n, 0ull, slots, lay, st);
     };
     return run_postings(ws, keys, n, k, slots, d_class, heavy_df, min_shared, require_class_diff, d_p, d_q, d_w, cap,
                         n_edges, stats, st);
@@ -1402,8 +1464,7 @@ int kmp_dev_keys_part(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_
     PG(ws->keys.reserve(m));
     PG(ws->flags.reserve(4));
     PG(hipMemsetAsync(ws->flags.p, 0, 4 * sizeof(uint32_t), st));
-    residue_keys_kernel<<<hi - lo, kResThreads, 0, st>>>(d_res, d_res_off, d_class, n, k, slots, lay, ws->keys.p,
-                                                         ws->flags.p, lo, slot_lo);
+    PG(launch_residue_keys(ws, d_res, d_res_off, d_class, k, lo, hi, slot_lo, slot_hi, lay, st));
     size_t t_sort = 0;
     PG(rocprim::radix_sort_keys<SortCfg>(nullptr, t_sort, ws->keys.p, d_out, (size_t)m, lay.sort_lo, lay.sort_hi, st));
     PG(ws->tmp.reserve(std::max(t_sort, ws->tmp.n)));
