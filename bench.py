@@ -66,6 +66,15 @@ def stage_bytes(n_res, slots, n_inc, n_edges, n_uniq, tail="sort"):
     every output).  The six timing slots of the p-shard tail are keys, bucket sort,
     group + expand (pair keys written to their row ranges), -, row-range reduce (+ offsets),
     compaction."""
+    if tail == "fused":
+        return {
+            "keys": n_res + 8 * slots,
+            "code_sort": 16 * slots,
+            "count": 8 * slots + 8 * n_inc,                 # keys in, pair keys out to the shards
+            "write": 0,                                     # padding of the shard tails
+            "pair_sort": 16 * n_inc,
+            "rle_emit": 8 * n_inc + 12 * n_uniq + 12 * n_edges,
+        }
     if tail == "pshard":
         return {
             "keys": n_res + 8 * slots,
@@ -181,8 +190,7 @@ def main():
             slots = int(_lib.lib().kmp_set_capacity(n, int(proteins.offsets[-1])))
             tail = pipe.last_tail()
             byts = stage_bytes(int(proteins.offsets[-1]), slots, ps["incidences"], n_edges, ps["pairs"], tail)
-            names = _lib.POSTINGS_STAGE_NAMES if tail == "sort" else (
-                "keys", "code_sort", "count", "write", "pair_sort", "rle_emit")
+            names = ("keys", "code_sort", "count", "write", "pair_sort", "rle_emit")
             stage_ms = dict(zip(names, (stage_sum / args.steps).tolist()))
             stages = {s: {"ms": stage_ms[s], "alg_bytes": byts[s],
                           "GBs": byts[s] / (stage_ms[s] * 1e-3) / 1e9 if stage_ms[s] > 0 else None}
@@ -190,7 +198,7 @@ def main():
             dom = max(stage_ms, key=stage_ms.get)
             ach = stages[dom]["GBs"]
             traffic, source = (pmc_traffic(dom) if args.config == "config3" and args.engine == "residues"
-                               and tail == "sort" else (None, None))
+                               and dom in ("code_sort", "keys") else (None, None))
             out["roofline"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": source,
                                "traffic_over_alg": traffic / byts[dom] if traffic else None, "kernel": dom,

@@ -307,7 +307,7 @@ def test_device_pipeline_matches_oracle(oracle_mod):
             np.testing.assert_array_equal(pipe.edges()[1], q)
             np.testing.assert_array_equal(pipe.edges()[2], w)
             assert pipe.last_layout() == ("bucketed" if bucketed else "flat")
-            assert pipe.last_tail() == ("pshard" if bucketed and pshard else "sort")
+            assert pipe.last_tail() == ("sort" if not bucketed else "pshard" if pshard else "fused")
         for ms in (2, 5):  # min_shared filter inside both tails
             keep = w >= ms
             assert pipe.step(min_shared=ms, engine="residues") == int(keep.sum())

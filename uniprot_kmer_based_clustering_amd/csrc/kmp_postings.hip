@@ -870,6 +870,30 @@ __global__ void compact_edges_kernel(const uint32_t* __restrict__ ep, const uint
     }
 }
 
+// unused tail of every shard region -> kNoKey (sorts after every pair key)
+__global__ void pad_shards_kernel(unsigned long long* __restrict__ region, uint64_t shard_cap,
+                                  const unsigned long long* __restrict__ cursor) {
+    const int s = blockIdx.y;
+    const unsigned long long m = cursor[s];
+    for (uint64_t i = m + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < shard_cap;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        region[(uint64_t)s * shard_cap + i] = kNoKey;
+}
+
+// (pair key, w) runs -> edges, w >= 1 (the padding run, key kNoKey, is last and skipped)
+__global__ void emit_runs_kernel(const unsigned long long* __restrict__ uniq, const uint32_t* __restrict__ w,
+                                 const uint32_t* __restrict__ nuniq, uint32_t n_prot, uint32_t* __restrict__ out_p,
+                                 uint32_t* __restrict__ out_q, uint32_t* __restrict__ out_w, uint64_t cap) {
+    const uint32_t U = *nuniq;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < U; i += gridDim.x * blockDim.x) {
+        const unsigned long long x = uniq[i];
+        if (x == kNoKey || i >= cap) continue;
+        out_p[i] = (uint32_t)(x / n_prot);
+        out_q[i] = (uint32_t)(x % n_prot);
+        out_w[i] = w[i];
+    }
+}
+
 // shard regions -> one contiguous array (shard order)
 __global__ void gather_shards_kernel(const unsigned long long* __restrict__ src, uint64_t shard_cap,
                                      const unsigned long long* __restrict__ cursor,
@@ -940,6 +964,7 @@ struct kmp_postings {
     bool bucketed = true;       // try the bucketed layout first
     bool last_bucketed = false; // layout the last call ran on
     bool last_pshard = false;   // ... and whether it finished with the p-shard tail
+    bool last_fused = false;    // ... or with the single-synchronisation bucketed path
     uint64_t shard_cap = 0;     // bucketed: capacity of each output shard region
     uint64_t ps_cap = 0;        // p-shard: keys per row-range region
     bool ps_ok = false;         // the last bucketed front end left its keys in row-range regions
@@ -1234,6 +1259,98 @@ int tail_pshard(kmp_postings* ws, uint32_t min_shared, uint32_t* d_p, uint32_t* 
     return KMP_OK;
 }
 
+// Bucketed, min_shared == 1, one host synchronisation: bucket sort, group + expand into the
+// kShards regions, the regions' unused tails padded with kNoKey, one radix sort of the whole
+// padded buffer (its capacity is learned call to call, so it stays within a few % of the
+// incidence count), run-length encode, emit.  Stats, flags and the shard counts are read back
+// once at the end; a bucket that does not fit -> *fallback (flat rerun), a shard region
+// overflow -> grow and rerun.  Marks 2 (sort), 3 (group + expand), 4 (pad), 5 (pair sort),
+// 6 (encode + emit + read-back).
+int run_bucketed_fused(kmp_postings* ws, uint64_t slots, const Layout& lay, uint32_t n, uint32_t heavy_df,
+                       int require_class_diff, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w, uint64_t cap,
+                       uint64_t* n_edges, bool* fallback, kmp_postings_stats* stats, hipStream_t st) {
+    *fallback = false;
+    size_t t_sort = 0;
+    PG(rocprim::radix_sort_keys<SortCfg>(nullptr, t_sort, ws->keys.p, ws->sorted.p, (size_t)slots, lay.sort_lo,
+                                         lay.sort_hi, st));
+    PG(ws->tmp.reserve(std::max(t_sort, ws->tmp.n)));
+    PG(rocprim::radix_sort_keys<SortCfg>(ws->tmp.p, t_sort, ws->keys.p, ws->sorted.p, (size_t)slots, lay.sort_lo,
+                                         lay.sort_hi, st));
+    ws->mark(2, st);
+    const uint32_t nb = 1u << lay.bbits;
+    PG(ws->cnt.reserve(2 * (uint64_t)nb + 2));
+    PG(ws->bstats.reserve(std::max<uint64_t>(ws->bstats.n, kShards * 8 + kShards)));
+    PG(ws->small.reserve(16));
+    uint32_t* bstart = ws->cnt.p;
+    uint32_t* list = ws->cnt.p + nb + 1;
+    uint32_t* list_count = ws->flags.p + 2;
+    uint32_t* flags = ws->flags.p;
+    unsigned long long* gstats = ws->bstats.p;
+    unsigned long long* cursor = gstats + kShards * 8;
+    bucket_bounds_kernel<<<(nb + 1 + 255) / 256, 256, 0, st>>>(ws->sorted.p, slots, lay.sort_lo, nb, bstart);
+    if (ws->shard_cap == 0) ws->shard_cap = slots / 4 / kShards + 4096;
+    PShard ps{};
+    const unsigned pair_bits = bits_for((uint64_t)n * n);
+    for (int attempt = 0; attempt < 3; ++attempt) {
+        const uint64_t sc = ws->shard_cap, total = sc * kShards;
+        PG(ws->inc_sorted.reserve(total));
+        PG(ws->inc.reserve(total));
+        PG(ws->uniq.reserve(total));
+        PG(ws->w.reserve(total));
+        PG(hipMemsetAsync(gstats, 0, (kShards * 8 + kShards) * sizeof(unsigned long long), st));
+        PG(hipMemsetAsync(list_count, 0, sizeof(uint32_t), st));
+        bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallSub, 0, false>
+            <<<nb, kBucketSmallThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
+                                                 ws->inc_sorted.p, sc, cursor, gstats, flags, list, list_count, ps);
+        bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeSub, false>
+            <<<256, kBucketLargeThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
+                                                  ws->inc_sorted.p, sc, cursor, gstats, flags, list, list_count, ps);
+        ws->mark(3, st);
+        pad_shards_kernel<<<dim3(64, kShards), 256, 0, st>>>(ws->inc_sorted.p, sc, cursor);
+        ws->mark(4, st);
+        size_t t2 = 0, t3 = 0;
+        PG(rocprim::radix_sort_keys<SortCfg>(nullptr, t2, ws->inc_sorted.p, ws->inc.p, (size_t)total, 0u, pair_bits,
+                                             st));
+        PG(rocprim::run_length_encode(nullptr, t3, ws->inc.p, (unsigned int)total, ws->uniq.p, ws->w.p,
+                                      ws->small.p + 1, st));
+        PG(ws->tmp.reserve(std::max({t2, t3, ws->tmp.n})));
+        PG(rocprim::radix_sort_keys<SortCfg>(ws->tmp.p, t2, ws->inc_sorted.p, ws->inc.p, (size_t)total, 0u,
+                                             pair_bits, st));
+        ws->mark(5, st);
+        PG(rocprim::run_length_encode(ws->tmp.p, t3, ws->inc.p, (unsigned int)total, ws->uniq.p, ws->w.p,
+                                      ws->small.p + 1, st));
+        const uint32_t kb = (uint32_t)std::min<uint64_t>((total + 255) / 256, 8192);
+        emit_runs_kernel<<<kb, 256, 0, st>>>(ws->uniq.p, ws->w.p, ws->small.p + 1, n, d_p, d_q, d_w, cap);
+        unsigned long long g[kShards * 8 + kShards];
+        uint32_t h_flags[2] = {0, 0}, h_uniq = 0;
+        PG(hipMemcpyAsync(g, gstats, sizeof g, hipMemcpyDeviceToHost, st));
+        PG(hipMemcpyAsync(h_flags, flags, sizeof h_flags, hipMemcpyDeviceToHost, st));
+        PG(hipMemcpyAsync(&h_uniq, ws->small.p + 1, sizeof h_uniq, hipMemcpyDeviceToHost, st));
+        PG(hipStreamSynchronize(st));
+        ws->mark(6, st);
+        if (h_flags[0] || h_flags[1]) {
+            *fallback = true;
+            return KMP_OK;
+        }
+        unsigned long long acc[kStN] = {}, most = 0, n_inc = 0;
+        for (int sh = 0; sh < kShards; ++sh) {
+            for (int t = 0; t < kStN; ++t)
+                acc[t] = t == kStMaxDf ? std::max(acc[t], g[sh * 8 + t]) : acc[t] + g[sh * 8 + t];
+            most = std::max(most, g[kShards * 8 + sh]);
+            n_inc += g[kShards * 8 + sh];
+        }
+        ws->shard_cap = most + most / 64 + 256;  // learned capacity for the next call (or the rerun)
+        if (most > sc) continue;                 // a region overflowed: rerun with the new capacity
+        fill_stats(stats, acc);
+        if (stats) stats->incidences = n_inc;
+        const uint64_t ne = h_uniq - (n_inc < total ? 1u : 0u);  // the padding run
+        if (stats) stats->pairs = ne;
+        *n_edges = ne;
+        return ne > cap ? KMP_EOVERFLOW : KMP_OK;
+    }
+    return KMP_EDEVICE;
+}
+
 // Shared tail: sort the pair keys, run-length encode -> (pair, w) in canonical order, keep
 // w >= min_shared, unpack.  Marks 5 (pair sort) and 6 (encode + emit).
 int tail(kmp_postings* ws, const unsigned long long* in, unsigned long long n_inc, uint32_t n, uint32_t min_shared,
@@ -1336,7 +1453,20 @@ int run_postings(kmp_postings* ws, MakeKeys make_keys, uint32_t n, int k, uint64
     unsigned long long n_inc = 0;
     Layout lay = make_layout(n, k, slots, ws->bucketed);
     bool fallback = true;
-    if (lay.bucketed) {
+    if (lay.bucketed && min_shared == 1 && !ws->pshard) {
+        ws->mark(0, st);
+        PG(make_keys(lay));
+        ws->mark(1, st);
+        int rc = run_bucketed_fused(ws, slots, lay, n, heavy_df, require_class_diff, d_p, d_q, d_w, cap, n_edges,
+                                    &fallback, stats, st);
+        if (!fallback) {
+            ws->last_bucketed = true;
+            ws->last_pshard = false;
+            ws->last_fused = true;
+            if (rc == KMP_OK) finish_timing(ws, stats, st);
+            return rc;
+        }
+    } else if (lay.bucketed) {
         ws->mark(0, st);
         PG(make_keys(lay));
         ws->mark(1, st);
@@ -1355,6 +1485,7 @@ int run_postings(kmp_postings* ws, MakeKeys make_keys, uint32_t n, int k, uint64
     }
     ws->last_bucketed = !fallback;
     ws->last_pshard = !fallback && ws->ps_ok;
+    ws->last_fused = false;
     int rc = ws->last_pshard ? tail_pshard(ws, min_shared, d_p, d_q, d_w, cap, n_edges, stats, st)
                              : tail(ws, ws->inc.p, n_inc, n, min_shared, d_p, d_q, d_w, cap, n_edges, stats, st);
     if (rc == KMP_OK) finish_timing(ws, stats, st);
@@ -1389,7 +1520,7 @@ int kmp_postings_set_layout(kmp_postings* ws, int bucketed) {
 
 int kmp_postings_last_layout(const kmp_postings* ws) {
     if (!ws || !ws->last_bucketed) return 0;
-    return ws->last_pshard ? 2 : 1;
+    return ws->last_fused ? 3 : ws->last_pshard ? 2 : 1;
 }
 
 int kmp_postings_set_pshard(kmp_postings* ws, int enable) {

@@ -227,8 +227,9 @@ class DevicePipeline:
         return "bucketed" if lib().kmp_postings_last_layout(self._workspace()) else "flat"
 
     def last_tail(self) -> str:
-        """How the last postings call reduced its pair keys: 'pshard' or 'sort'."""
-        return "pshard" if lib().kmp_postings_last_layout(self._workspace()) == 2 else "sort"
+        """How the last postings call reduced its pair keys: 'fused' (bucketed, one host
+        synchronisation), 'pshard' (row-range LDS reduction) or 'sort' (gathered pair-key sort)."""
+        return {3: "fused", 2: "pshard"}.get(lib().kmp_postings_last_layout(self._workspace()), "sort")
 
     def postings(self, min_shared: int = 1, require_class_diff: bool = True,
                  heavy_df: int = 0xFFFFFFFF, from_residues: bool = False) -> int:
