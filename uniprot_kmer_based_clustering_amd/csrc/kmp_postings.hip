@@ -461,18 +461,21 @@ __device__ __forceinline__ void block_scan_n(uint32_t v, uint32_t& excl, uint32_
     total = tot;
 }
 
-// One workgroup per bucket with lo < size <= kCap.  The bucket's keys are grouped in LDS by a
-// counting sort on the next kSubBits bits of h(code) (below the bucket bits), as two u32 planes:
-// Bh = h(code), Bl = p << cb | class.  Per sub-bucket:
-//   duplicate windows of one protein (identical keys) count once (the K(p) dedup, main.rs:280-282);
-//   df = distinct proteins with the k-mer; head = first element of its k-mer in the sub-bucket;
-//   every element pairs with the later non-duplicate elements of its k-mer (vertex.rs:103-137),
-//   class test fused (mod.rs:580-587); pair key = min(p,q) * N + max(p,q).
-// Thread tid owns positions tid + e*kThreads of the grouped bucket in every phase, so its
-// per-position state stays in registers.  Output: the workgroup reserves its range on
-// cursor[b % kShards] (one agent-scope atomic) inside that shard's region; the pair sort makes
-// the order irrelevant.  Statistics -> gstats[b % kShards].  flags[0]: a bucket above the large capacity
-// or a sub-bucket above kHeavySub (the caller reruns on the flat layout).
+// One workgroup per bucket with size <= kCap (the bucket: keys with the same top bbits of
+// h(code)).  In LDS:
+//   A. exact k-mer groups: an open-addressing table on h (kTab >= kCap slots, the empty mark can
+//      not be an h of this bucket) gives every key its group slot; LDS atomics rank it in the group;
+//   B. groups are laid out by size, largest first (a counting sort over the size classes), so the
+//      lanes of a wave walk groups of equal size in the loops below; singletons walk none;
+//   C. scatter: Bl[pos] = p << cb | class, and per position its group (start << 8 | size);
+//   D. duplicate windows of one protein (same p twice in a group) count once (main.rs:280-282);
+//   E. df = distinct proteins of the group; every element pairs with the later non-duplicate
+//      elements of its group (vertex.rs:103-137), class test fused (mod.rs:580-587);
+//   F. output: the workgroup reserves its range on cursor[b % kShards] (p-shard mode: every key on
+//      its row range's cursor) and writes the pair keys min(p,q) * N + max(p,q).
+// Thread tid owns positions tid + e*kThreads in C-F, so its per-position state stays in
+// registers.  Statistics -> gstats[b % kShards].  flags[0]: a bucket above the large capacity or
+// a group above kHeavySub (a very frequent k-mer; the caller reruns on the flat layout).
 // p-shard output mode: every pair key goes to the region of its row range (p >> row_bits),
 // reserved key by key on that shard's cursor; shard_reduce_kernel then finishes each range in LDS
 struct PShard {
@@ -483,7 +486,7 @@ struct PShard {
     unsigned long long* region;         // n_shards * cap, key = p << 32 | q
 };
 
-template <int kCap, int kThreads, int kSubBits, int kAblate = 0, bool kPShard = false>
+template <int kCap, int kThreads, int kTabBits, bool kPShard = false>
 __device__ __forceinline__ void process_bucket(
     const uint32_t b, const unsigned long long* __restrict__ sorted, const uint32_t* __restrict__ bstart,
     const Layout& lay, uint32_t n_prot, int require_diff, uint32_t heavy_df, bool small,
@@ -491,14 +494,14 @@ __device__ __forceinline__ void process_bucket(
     unsigned long long* __restrict__ gstats, uint32_t* __restrict__ flags, uint32_t* __restrict__ list,
     uint32_t* __restrict__ list_count, const PShard& ps) {
     constexpr int kE = kCap / kThreads;
-    constexpr uint32_t kSub = 1u << kSubBits;
-    constexpr int kPer = kSub / kThreads;
-    static_assert(kE * kThreads == kCap && kPer == 4, "geometry: four sub-buckets per thread");
-    __shared__ uint32_t Bh[kCap], Bl[kCap];
-    __shared__ __attribute__((aligned(16))) uint32_t H[kSub + 4];  // sub-bucket sizes, then starts
-    __shared__ uint32_t SZ[kHeavySub + 1];                           // sub-buckets per size, then starts
-    __shared__ uint8_t HS[kSub];                                     // sub-bucket sizes (<= kHeavySub)
+    constexpr uint32_t kTab = 1u << kTabBits;
+    constexpr int kPer = kTab / kThreads;
+    static_assert(kE * kThreads == kCap && kPer % 4 == 0 && kTab >= (uint32_t)kCap, "geometry");
+    __shared__ __attribute__((aligned(16))) uint32_t T[kTab];  // A: table of h; C-E: per position start<<8|size
+    __shared__ __attribute__((aligned(16))) uint32_t H[kTab];  // per slot: group size, then start<<8|size
+    __shared__ uint32_t Bl[kCap];                              // per position: p << cb | class
     __shared__ uint32_t dupw[kCap / 32];
+    __shared__ uint32_t SZ[kHeavySub + 1];
     __shared__ uint32_t wave_tot[kThreads / 64];
     __shared__ uint32_t red[kThreads / 64][8];
     __shared__ unsigned long long sbase;
@@ -515,41 +518,47 @@ __device__ __forceinline__ void process_bucket(
     }
     __syncthreads();  // LDS reuse across the buckets of one workgroup
     const unsigned hshift = lay.hshift, cb = lay.clsbits;
-    const unsigned subshift = 32 - lay.bbits - kSubBits;  // sub-hash: the h bits below the bucket
     const uint32_t lmask = (1u << hshift) - 1, cmask = (1u << cb) - 1;
-    reinterpret_cast<uint4*>(H)[tid] = make_uint4(0, 0, 0, 0);
-    if (tid == 0) H[kSub] = 0;
-    for (uint32_t i = tid; i <= kHeavySub; i += kThreads) SZ[i] = 0;
+    const uint32_t empty = ~b << (32 - lay.bbits);  // top bits differ from every h of bucket b
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+        T[tid * kPer + q] = empty;
+        H[tid * kPer + q] = 0;
+    }
     for (uint32_t i = tid; i < kCap / 32; i += kThreads) dupw[i] = 0;
+    for (uint32_t i = tid; i <= kHeavySub; i += kThreads) SZ[i] = 0;
     if (tid == 0) heavy = 0;
     __syncthreads();
-    // 1. counting sort on the sub-hash: ranks from LDS atomics, offsets from one workgroup scan
-    uint32_t xh[kE], xl[kE], rk[kE];
+    // A. group slot + rank of every key
+    uint32_t xl[kE], sl[kE], rk[kE];
 #pragma unroll
     for (int e = 0; e < kE; ++e) {
         const uint32_t i = tid + e * kThreads;
         const unsigned long long x = i < n ? sorted[s0 + i] : 0ull;
-        xh[e] = (uint32_t)(x >> hshift);
+        const uint32_t h = (uint32_t)(x >> hshift);
         xl[e] = (uint32_t)x & lmask;
+        sl[e] = 0;
+        rk[e] = 0;
+        if (i < n) {
+            uint32_t slot = (h * 0x85EBCA6Bu) >> (32 - kTabBits);
+            for (;;) {
+                const uint32_t old = atomicCAS(&T[slot], empty, h);
+                if (old == empty || old == h) break;
+                slot = (slot + 1) & (kTab - 1);
+            }
+            sl[e] = slot;
+            rk[e] = atomicAdd(&H[slot], 1u);
+        }
     }
-    if (kAblate == 1) {
-        uint32_t v = 0;
-#pragma unroll
-        for (int e = 0; e < kE; ++e) v ^= xh[e] + xl[e];
-        if (v == 42) flags[3] = 1;
-        return;
-    }
-#pragma unroll
-    for (int e = 0; e < kE; ++e)
-        rk[e] = tid + e * kThreads < n ? atomicAdd(&H[(xh[e] >> subshift) & (kSub - 1)], 1u) : 0u;
     __syncthreads();
-    // sub-buckets are laid out by size, largest first, so that the lanes of a wave scan
-    // sub-buckets of (nearly) equal size in the phases below: rank each non-empty sub-bucket in
-    // its size class, then one scan over the size classes (descending) gives the class starts
+    // B. size classes, largest first
     uint32_t c4[kPer], r4[kPer];
     {
-        const uint4 v = reinterpret_cast<const uint4*>(H)[tid];
-        c4[0] = v.x, c4[1] = v.y, c4[2] = v.z, c4[3] = v.w;
+#pragma unroll
+        for (int q4 = 0; q4 < kPer / 4; ++q4) {
+            const uint4 v = reinterpret_cast<const uint4*>(H)[tid * (kPer / 4) + q4];
+            c4[4 * q4] = v.x, c4[4 * q4 + 1] = v.y, c4[4 * q4 + 2] = v.z, c4[4 * q4 + 3] = v.w;
+        }
 #pragma unroll
         for (int q = 0; q < kPer; ++q) {
             if (c4[q] > kHeavySub) heavy = 1;
@@ -570,42 +579,40 @@ __device__ __forceinline__ void process_bucket(
     }
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < kPer; ++q) {
-        H[tid * kPer + q] = c4[q] ? SZ[c4[q]] + r4[q] * c4[q] : 0u;
-        HS[tid * kPer + q] = (uint8_t)c4[q];
-    }
+    for (int q = 0; q < kPer; ++q)
+        H[tid * kPer + q] = c4[q] ? ((SZ[c4[q]] + r4[q] * c4[q]) << 8) | c4[q] : 0u;
     __syncthreads();
+    // C. scatter (T now holds, per position, its group's start << 8 | size)
 #pragma unroll
     for (int e = 0; e < kE; ++e)
         if (tid + e * kThreads < n) {
-            const uint32_t pos = H[(xh[e] >> subshift) & (kSub - 1)] + rk[e];
-            Bh[pos] = xh[e];
+            const uint32_t g = H[sl[e]];
+            const uint32_t pos = (g >> 8) + rk[e];
             Bl[pos] = xl[e];
+            T[pos] = g;
         }
     __syncthreads();
-    if (kAblate == 2) return;
-    // 2. per position: its key, sub-bucket bounds, duplicate flag
+    // D. per position: group bounds, duplicate flag (same protein earlier in the group)
     uint32_t s[kE], en[kE];
 #pragma unroll
     for (int e = 0; e < kE; ++e) {
         const uint32_t i = tid + e * kThreads;
         s[e] = en[e] = 0;
         if (i >= n) continue;
-        xh[e] = Bh[i];
+        const uint32_t g = T[i];
+        s[e] = g >> 8;
+        en[e] = s[e] + (g & 255u);
         xl[e] = Bl[i];
-        const uint32_t sb = (xh[e] >> subshift) & (kSub - 1);
-        s[e] = H[sb];
-        en[e] = s[e] + HS[sb];
+        const uint32_t p = xl[e] >> cb;
         for (uint32_t j = s[e]; j < i; ++j)
-            if (Bh[j] == xh[e] && Bl[j] == xl[e]) {
+            if ((Bl[j] >> cb) == p) {
                 atomicOr(&dupw[i >> 5], 1u << (i & 31));
                 break;
             }
     }
     __syncthreads();
-    if (kAblate == 3) return;
     auto is_dup = [&](uint32_t j) { return (dupw[j >> 5] >> (j & 31)) & 1u; };
-    // 3. df, head, kept-partner count
+    // E. df, head, kept-partner count
     uint32_t cnt[kE];
     uint32_t st_sum = 0, st_dist = 0, st_rep = 0, st_cdf2 = 0, st_max = 0, st_heavy = 0, mine = 0;
 #pragma unroll
@@ -613,18 +620,18 @@ __device__ __forceinline__ void process_bucket(
         const uint32_t i = tid + e * kThreads;
         cnt[e] = 0;
         if (i >= n || is_dup(i)) continue;
-        uint32_t f = 0, c = 0;
-        bool head = true;
-        for (uint32_t j = s[e]; j < en[e]; ++j) {
-            if (Bh[j] != xh[e]) continue;
-            if (j < i) head = false;
-            if (is_dup(j)) continue;
-            ++f;
-            if (j > i && (!require_diff || ((Bl[j] ^ xl[e]) & cmask))) ++c;
+        uint32_t f = 1, c = 0;
+        if (en[e] - s[e] > 1) {
+            f = 0;
+            for (uint32_t j = s[e]; j < en[e]; ++j) {
+                if (is_dup(j)) continue;
+                ++f;
+                if (j > i && (!require_diff || ((Bl[j] ^ xl[e]) & cmask))) ++c;
+            }
+            if (f > heavy_df) c = 0;
         }
-        if (f > heavy_df) c = 0;
         st_sum += 1;
-        if (head) {
+        if (i == s[e]) {  // the group's first position is never a duplicate
             st_dist += 1;
             st_rep += f >= 2;
             if (f <= heavy_df) st_cdf2 += f * (f - 1) / 2;
@@ -634,21 +641,16 @@ __device__ __forceinline__ void process_bucket(
         cnt[e] = c;
         mine += c;
     }
-    if (kAblate == 4) {
-        if (mine == 0xFFFFFFFF) flags[3] = 1;
-        return;
-    }
-    // 4. write the pair keys: p-shard mode reserves each key on its row range's cursor; otherwise
-    //    the workgroup reserves one range on cursor[b % kShards]
+    // F. write the pair keys
     if (kPShard) {
-        if (mine && kAblate != 5) {
+        if (mine) {
 #pragma unroll
             for (int e = 0; e < kE; ++e) {
                 if (!cnt[e]) continue;
                 const uint32_t i = tid + e * kThreads;
                 const uint32_t p = xl[e] >> cb;
                 for (uint32_t j = i + 1; j < en[e]; ++j) {
-                    if (Bh[j] != xh[e] || is_dup(j)) continue;
+                    if (is_dup(j)) continue;
                     const uint32_t lj = Bl[j];
                     if (require_diff && !((lj ^ xl[e]) & cmask)) continue;
                     const uint32_t q = lj >> cb;
@@ -665,7 +667,7 @@ __device__ __forceinline__ void process_bucket(
         const uint32_t shard = b % kShards;
         if (tid == 0) sbase = total ? atomicAdd(&cursor[shard], (unsigned long long)total) : 0ull;
         __syncthreads();
-        if (mine && kAblate != 5) {
+        if (mine) {
             unsigned long long pos = sbase + excl;
             unsigned long long* dst = out + (uint64_t)shard * shard_cap;
 #pragma unroll
@@ -674,7 +676,7 @@ __device__ __forceinline__ void process_bucket(
                 const uint32_t i = tid + e * kThreads;
                 const uint32_t p = xl[e] >> cb;
                 for (uint32_t j = i + 1; j < en[e]; ++j) {
-                    if (Bh[j] != xh[e] || is_dup(j)) continue;
+                    if (is_dup(j)) continue;
                     const uint32_t lj = Bl[j];
                     if (require_diff && !((lj ^ xl[e]) & cmask)) continue;
                     const uint32_t q = lj >> cb;
@@ -684,7 +686,7 @@ __device__ __forceinline__ void process_bucket(
             }
         }
     }
-    // 5. statistics (u32 per workgroup; the bucket is at most kCap keys)
+    // statistics (u32 per workgroup; the bucket is at most kCap keys)
     uint32_t sv[kStN] = {st_sum, st_dist, st_rep, st_cdf2, st_max, st_heavy, mine};
 #pragma unroll
     for (int t = 0; t < kStN; ++t) {
@@ -705,19 +707,19 @@ __device__ __forceinline__ void process_bucket(
     }
 }
 
-template <int kCap, int kThreads, int kSubBits, int kAblate = 0, bool kPShard = false>
+template <int kCap, int kThreads, int kTabBits, bool kPShard = false>
 __global__ __launch_bounds__(kThreads) void bucket_small_kernel(
     const unsigned long long* __restrict__ sorted, const uint32_t* __restrict__ bstart, Layout lay,
     uint32_t n_prot, int require_diff, uint32_t heavy_df, unsigned long long* __restrict__ out, uint64_t shard_cap,
     unsigned long long* __restrict__ cursor, unsigned long long* __restrict__ gstats, uint32_t* __restrict__ flags,
     uint32_t* __restrict__ list, uint32_t* __restrict__ list_count, PShard ps) {
-    process_bucket<kCap, kThreads, kSubBits, kAblate, kPShard>(blockIdx.x, sorted, bstart, lay, n_prot,
-                                                               require_diff, heavy_df, true, out, shard_cap, cursor,
-                                                               gstats, flags, list, list_count, ps);
+    process_bucket<kCap, kThreads, kTabBits, kPShard>(blockIdx.x, sorted, bstart, lay, n_prot, require_diff, heavy_df,
+                                                      true, out, shard_cap, cursor, gstats, flags, list, list_count,
+                                                      ps);
 }
 
 // the buckets the small kernel listed (above its capacity), a grid-stride loop over the list
-template <int kCap, int kThreads, int kSubBits, bool kPShard = false>
+template <int kCap, int kThreads, int kTabBits, bool kPShard = false>
 __global__ __launch_bounds__(kThreads) void bucket_large_kernel(
     const unsigned long long* __restrict__ sorted, const uint32_t* __restrict__ bstart, Layout lay,
     uint32_t n_prot, int require_diff, uint32_t heavy_df, unsigned long long* __restrict__ out, uint64_t shard_cap,
@@ -725,9 +727,9 @@ __global__ __launch_bounds__(kThreads) void bucket_large_kernel(
     uint32_t* __restrict__ list, const uint32_t* __restrict__ list_count, PShard ps) {
     const uint32_t m = *list_count;
     for (uint32_t i = blockIdx.x; i < m; i += gridDim.x)
-        process_bucket<kCap, kThreads, kSubBits, 0, kPShard>(list[i], sorted, bstart, lay, n_prot, require_diff,
-                                                             heavy_df, false, out, shard_cap, cursor, gstats, flags,
-                                                             nullptr, nullptr, ps);
+        process_bucket<kCap, kThreads, kTabBits, kPShard>(list[i], sorted, bstart, lay, n_prot, require_diff,
+                                                          heavy_df, false, out, shard_cap, cursor, gstats, flags,
+                                                          nullptr, nullptr, ps);
 }
 
 // ---------------------------------------------------------------- p-shard reduction --------
@@ -907,8 +909,9 @@ __global__ void gather_shards_kernel(const unsigned long long* __restrict__ src,
         dst[off + i] = src[(uint64_t)s * shard_cap + i];
 }
 
-constexpr int kBucketSmallCap = 2048, kBucketSmallThreads = 256, kBucketSmallSub = 10;
-constexpr int kBucketLargeCap = 8192, kBucketLargeThreads = 1024, kBucketLargeSub = 12;
+// bucket kernels: capacity (keys), threads, log2 of the k-mer table (>= capacity)
+constexpr int kBucketSmallCap = 2048, kBucketSmallThreads = 256, kBucketSmallTab = 11;
+constexpr int kBucketLargeCap = 8192, kBucketLargeThreads = 1024, kBucketLargeTab = 13;
 
 
 // (pair key, w) runs -> edges with w >= min_shared, canonical order kept
@@ -1123,32 +1126,25 @@ int front_bucketed(kmp_postings* ws, const unsigned long long* in, uint64_t slot
         }
         PG(hipMemsetAsync(gstats, 0, (kShards * 8 + kShards) * sizeof(unsigned long long), st));
         PG(hipMemsetAsync(list_count, 0, sizeof(uint32_t), st));
-#define KMP_SMALL(A, P)                                                                                       \
-    bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallSub, A, P>                          \
-        <<<nb, kBucketSmallThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,     \
-                                             ws->inc_sorted.p, ws->shard_cap, cursor, gstats, flags, list,    \
-                                             list_count, ps)
         if (pshard) {
-            KMP_SMALL(0, true);
-            bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeSub, true>
+            bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallTab, true>
+                <<<nb, kBucketSmallThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
+                                                     ws->inc_sorted.p, ws->shard_cap, cursor, gstats, flags, list,
+                                                     list_count, ps);
+            bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeTab, true>
                 <<<256, kBucketLargeThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
                                                       ws->inc_sorted.p, ws->shard_cap, cursor, gstats, flags, list,
                                                       list_count, ps);
         } else {
-            switch (ws->ablate) {  // diagnostics (KMP_BUCKET_ABLATE): phase cut-offs, results invalid
-                case 1: KMP_SMALL(1, false); break;
-                case 2: KMP_SMALL(2, false); break;
-                case 3: KMP_SMALL(3, false); break;
-                case 4: KMP_SMALL(4, false); break;
-                case 5: KMP_SMALL(5, false); break;
-                default: KMP_SMALL(0, false);
-            }
-            bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeSub, false>
+            bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallTab, false>
+                <<<nb, kBucketSmallThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
+                                                     ws->inc_sorted.p, ws->shard_cap, cursor, gstats, flags, list,
+                                                     list_count, ps);
+            bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeTab, false>
                 <<<256, kBucketLargeThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
                                                       ws->inc_sorted.p, ws->shard_cap, cursor, gstats, flags, list,
                                                       list_count, ps);
         }
-#undef KMP_SMALL
         ws->mark(3, st);
         unsigned long long g[kShards * 8 + kShards];
         uint32_t h_flags[2] = {0, 0};
@@ -1299,10 +1295,10 @@ int run_bucketed_fused(kmp_postings* ws, uint64_t slots, const Layout& lay, uint
         PG(ws->w.reserve(total));
         PG(hipMemsetAsync(gstats, 0, (kShards * 8 + kShards) * sizeof(unsigned long long), st));
         PG(hipMemsetAsync(list_count, 0, sizeof(uint32_t), st));
-        bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallSub, 0, false>
+        bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallTab, false>
             <<<nb, kBucketSmallThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
                                                  ws->inc_sorted.p, sc, cursor, gstats, flags, list, list_count, ps);
-        bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeSub, false>
+        bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeTab, false>
             <<<256, kBucketLargeThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
                                                   ws->inc_sorted.p, sc, cursor, gstats, flags, list, list_count, ps);
         ws->mark(3, st);
