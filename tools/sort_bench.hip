@@ -48,7 +48,8 @@ void run(const char* name, unsigned long long* in, unsigned long long* out, size
 using namespace rocprim;
 template <unsigned R, unsigned BS, unsigned IPT>
 using OS = radix_sort_config<default_config, default_config,
-                             radix_sort_onesweep_config<kernel_config<256, 12>, kernel_config<BS, IPT>, R>>;
+                             radix_sort_onesweep_config<kernel_config<256, 12>, kernel_config<BS, IPT>, R>, 0>;
+using DEF0 = radix_sort_config<default_config, default_config, default_config, 0>;
 
 int main(int argc, char** argv) {
     size_t n = argc > 1 ? strtoull(argv[1], 0, 10) : 30400000;
@@ -58,20 +59,18 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&out, n * 8));
     fill<<<(n + 255) / 256, 256>>>(in, n, shift, 1);
     CK(hipDeviceSynchronize());
-    const unsigned b1 = shift + 31;
-    run<default_config>("default", in, out, n, shift, b1);
-    run<OS<8, 512, 8>>("r8 bs512 ipt8", in, out, n, shift, b1);
-    run<OS<8, 256, 16>>("r8 bs256 ipt16", in, out, n, shift, b1);
-    run<OS<8, 1024, 4>>("r8 bs1024 ipt4", in, out, n, shift, b1);
-    run<OS<11, 512, 8>>("r11 bs512 ipt8", in, out, n, shift, b1);
-    run<OS<11, 256, 16>>("r11 bs256 ipt16", in, out, n, shift, b1);
-    run<OS<11, 1024, 4>>("r11 bs1024 ipt4", in, out, n, shift, b1);
-    run<OS<10, 512, 8>>("r10 bs512 ipt8", in, out, n, shift, b1);
-    // pair-key sort shape: 5.3M keys, 34 bits
+    // bucket sort shape: 30.4M keys, 16-bit field at the top
+    run<DEF0>("code default(onesweep)", in, out, n, 48, 64);
+    run<OS<8, 256, 8>>("code r8 256x8", in, out, n, 48, 64);
+    run<OS<8, 512, 8>>("code r8 512x8", in, out, n, 48, 64);
+    run<OS<8, 1024, 4>>("code r8 1024x4", in, out, n, 48, 64);
+    // pair sort shape: 5.3M keys, 34 bits
     fill<<<(n + 255) / 256, 256>>>(in, n, 0, 7);
-    run<default_config>("pairs default", in, out, 5300000, 0, 34);
-    run<OS<12, 512, 8>>("pairs r12 bs512", in, out, 5300000, 0, 34);
-    run<OS<12, 1024, 4>>("pairs r12 bs1024", in, out, 5300000, 0, 34);
-    run<OS<9, 512, 8>>("pairs r9 bs512", in, out, 5300000, 0, 34);
+    run<DEF0>("pairs default(onesweep)", in, out, 5300000, 0, 34);
+    run<OS<9, 256, 8>>("pairs r9 256x8", in, out, 5300000, 0, 34);
+    run<OS<10, 256, 8>>("pairs r10 256x8", in, out, 5300000, 0, 34);
+    run<OS<12, 256, 8>>("pairs r12 256x8", in, out, 5300000, 0, 34);
+    run<OS<12, 256, 4>>("pairs r12 256x4", in, out, 5300000, 0, 34);
+    run<OS<9, 512, 8>>("pairs r9 512x8", in, out, 5300000, 0, 34);
     return 0;
 }
