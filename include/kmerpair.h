@@ -308,6 +308,27 @@ int kmp_dev_edges_pairkeys(kmp_postings* ws, const unsigned long long* d_pk, uin
                            uint32_t min_shared, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w, uint64_t cap,
                            uint64_t* n_edges, uint64_t* n_pairs, void* stream);
 
+/* The same split with fixed-capacity exchanges and no host synchronisation (dist.py's default):
+ * every exchange buffer holds `parts` regions of `cap` u64 keys, each region's unused tail is
+ * ~0 (padding sorts after every real key), and the caller's device array d_flags[8] (zeroed per
+ * step) collects what went wrong: [0] a part exceeded `cap` (sizes in [4] keys, [6] pair keys),
+ * [1] a class id too wide, [2] a k-mer group too large for the LDS buckets (both: use the
+ * single-GPU path), [3] a shard region exceeded shard_cap (size in [5]).  After a flagged step
+ * the caller grows the capacities and reruns.
+ *   kmp_dev_keys_route:  keys of proteins [lo, hi) bucket-sorted and routed by bucket range.
+ *   kmp_dev_pairs_route: the m received keys grouped + expanded, pair keys sorted and routed
+ *                        by p range (shard_cap: pair keys per expansion shard region).
+ *   kmp_dev_edges_route: the m received pair keys -> this p range's edges, count in *d_count. */
+int kmp_dev_keys_route(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
+                       uint32_t n, int k, uint64_t slots, uint32_t lo, uint32_t hi, uint64_t slot_lo, uint64_t slot_hi,
+                       uint32_t parts, uint64_t cap, unsigned long long* d_send, uint32_t* d_flags, void* stream);
+int kmp_dev_pairs_route(kmp_postings* ws, const unsigned long long* d_keys, uint64_t m, uint32_t n, int k,
+                        uint64_t slots, uint32_t heavy_df, int require_class_diff, uint64_t shard_cap, uint32_t parts,
+                        uint64_t cap, unsigned long long* d_send, uint32_t* d_flags, kmp_postings_stats* stats,
+                        void* stream);
+int kmp_dev_edges_route(kmp_postings* ws, const unsigned long long* d_pk, uint64_t m, uint32_t n, uint32_t* d_p,
+                        uint32_t* d_q, uint32_t* d_w, uint64_t cap, unsigned long long* d_count, void* stream);
+
 /* Canonical order: sorts n edges by (p, q).  Keys/values are read from d_p/d_q/d_w and the
  * sorted result is written back to them.  d_tmp: kmp_dev_sort_edges_tmp_bytes(n, N) bytes. */
 uint64_t kmp_dev_sort_edges_tmp_bytes(uint64_t n, uint32_t n_proteins);

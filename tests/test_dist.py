@@ -129,6 +129,129 @@ class OracleStages:
         return t(u // self.n), t(u % self.n), t(w), len(u)
 
 
+ALL = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+class OracleRouteStages:
+    """CPU stand-in for the fixed-capacity stages of dist.distributed_postings_padded (padding =
+    all-ones keys, overflow flags, learned capacities), built on the oracle's K(p) sets; the
+    initial capacities are tiny so the first attempt overflows and the flow reruns."""
+
+    def __init__(self, o, cls, n):
+        self.so, self.sv = o.sets()
+        self.cls = np.asarray(cls)
+        self.n = n
+        self.cap_keys = self.cap_pairs = 0
+        self.flags = np.zeros(8, np.int64)
+        self.count = 0
+        self.attempts = 0
+
+    def begin(self, world):
+        if self.cap_keys == 0:
+            self.cap_keys, self.cap_pairs = 64, 64
+        self.flags[:] = 0
+        self.attempts += 1
+
+    def _route(self, vals, part, parts, cap, slot):
+        send = np.full(parts * cap, ALL, dtype=np.uint64)
+        for d in range(parts):
+            v = vals[part == d]
+            self.flags[slot] = max(self.flags[slot], len(v))
+            if len(v) > cap:
+                self.flags[0] = 1
+            v = v[:cap]
+            send[d * cap:d * cap + len(v)] = v
+        return torch.from_numpy(send.view(np.int64))
+
+    def keys_route(self, lo, hi, parts):
+        keys = np.concatenate([(self.sv[self.so[p]:self.so[p + 1]].astype(np.uint64) << np.uint64(20)) | np.uint64(p)
+                               for p in range(lo, hi)] + [np.zeros(0, np.uint64)])
+        return self._route(keys, (keys >> np.uint64(20)) % np.uint64(parts), parts, self.cap_keys, 4)
+
+    def pairs_route(self, keys, parts):
+        k = keys.numpy().view(np.uint64)
+        k = np.sort(k[k != ALL])
+        code, p = k >> np.uint64(20), (k & np.uint64((1 << 20) - 1)).astype(np.int64)
+        out = []
+        heads = np.flatnonzero(np.r_[True, code[1:] != code[:-1]]) if len(k) else np.zeros(0, int)
+        for s_, e_ in zip(heads, np.r_[heads[1:], len(k)]):
+            ps = p[s_:e_]
+            for i in range(len(ps)):
+                for j in range(i + 1, len(ps)):
+                    if self.cls[ps[i]] != self.cls[ps[j]]:
+                        a, b = sorted((int(ps[i]), int(ps[j])))
+                        out.append(a * self.n + b)
+        pk = np.sort(np.array(out, dtype=np.uint64))
+        bounds = np.array([-(-j * self.n // parts) * self.n for j in range(parts + 1)], dtype=np.uint64)
+        part = np.searchsorted(bounds, pk, side="right") - 1
+        return self._route(pk, part, parts, self.cap_pairs, 6)
+
+    def edges_route(self, pk):
+        k = pk.numpy().view(np.uint64)
+        u, w = np.unique(k[k != ALL], return_counts=True)
+        self.count = len(u)
+        e = np.zeros((3, max(1, len(u))), np.int32)
+        e[0, :len(u)] = (u // np.uint64(self.n)).astype(np.int32)
+        e[1, :len(u)] = (u % np.uint64(self.n)).astype(np.int32)
+        e[2, :len(u)] = w
+        return torch.from_numpy(e), None
+
+    def status(self):
+        return torch.from_numpy(np.r_[self.flags, self.count].astype(np.int64))
+
+    def grow(self, worst):
+        if worst[0]:
+            self.cap_keys = max(self.cap_keys, int(worst[4]) + 16)
+            self.cap_pairs = max(self.cap_pairs, int(worst[6]) + 16)
+
+
+def padded_worker(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, ROOT)
+        from uniprot_kmer_based_clustering_amd.dist import distributed_postings_padded
+        b, o = build_case()
+        stages = OracleRouteStages(o, b.class_id, b.n)
+        got, counts = distributed_postings_padded(stages, b.offsets, rank, world)
+        if rank == 0:
+            P, Q, W = o.pairs()
+            g = got.numpy()
+            ep, eq, ew = [], [], []
+            off = 0
+            for c in counts:
+                blk = g[3 * off:3 * (off + c)].reshape(3, c)
+                ep.append(blk[0]), eq.append(blk[1]), ew.append(blk[2])
+                off += c
+            ep, eq, ew = (np.concatenate(x).view(np.uint32) for x in (ep, eq, ew))
+            ok = np.array_equal(ep, P) and np.array_equal(eq, Q) and np.array_equal(ew, W)
+            out_q.put(("edges", ok, len(P), stages.attempts))
+        out_q.put(("count", rank, counts[rank]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_distributed_postings_padded(world):
+    """Fixed-capacity exchanges: overflow on the first attempt, joint rerun with learned
+    capacities, rank-order concatenation = the canonical edge list."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=padded_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    msgs = [q.get(timeout=300) for _ in range(world + 1)]  # drain before join: a queued message blocks exit
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    edges = [m for m in msgs if m[0] == "edges"]
+    assert len(edges) == 1 and edges[0][1] and edges[0][2] > 100, edges
+    assert edges[0][3] in (2, 3)  # the tiny first capacities overflowed (keys, then pair keys)
+    assert sum(m[2] for m in msgs if m[0] == "count") == edges[0][2]
+
+
 def postings_worker(rank, world, port, out_q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)

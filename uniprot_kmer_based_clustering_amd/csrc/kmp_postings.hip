@@ -1651,7 +1651,176 @@ int kmp_dev_edges_pairkeys(kmp_postings* ws, const unsigned long long* d_pk, uin
     return rc;
 }
 
+// ------------------------------------------------ multi-GPU split, fixed-capacity exchanges ----
+// No host synchronisation: every exchange buffer holds `parts` regions of `cap` keys, the unused
+// tail of each region is kNoKey (it sorts after every real key in every stage), and overflow or
+// fallback conditions accumulate in the caller's device flags (read once per step):
+//   flags[0] a part exceeded its region (rerun with cap >= flags[4] / flags[6])
+//   flags[1] a class id wider than the key's class field (needs the single-GPU flat layout)
+//   flags[2] a bucket or k-mer group too large for LDS (needs the single-GPU flat layout)
+//   flags[3] a pair-key shard region overflowed (rerun with shard_cap >= flags[5])
+//   flags[4] largest key part, flags[5] largest shard, flags[6] largest pair-key part
+
+// region d of `send` <- sorted[bounds[d], bounds[d+1]), padded with kNoKey
+__global__ void route_kernel(const unsigned long long* __restrict__ sorted,
+                             const unsigned long long* __restrict__ bounds, uint64_t cap,
+                             unsigned long long* __restrict__ send, uint32_t* __restrict__ flags, int max_slot) {
+    const uint32_t d = blockIdx.y;
+    const unsigned long long b0 = bounds[d], cnt = bounds[d + 1] - b0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        atomicMax(&flags[max_slot], (uint32_t)min(cnt, 0xFFFFFFFFull));
+        if (cnt > cap) atomicOr(&flags[0], 1u);
+    }
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * blockDim.x)
+        send[d * cap + i] = i < cnt ? sorted[b0 + i] : kNoKey;
+}
+
+// largest shard cursor -> flags[5]; overflow -> flags[3]
+__global__ void check_shards_kernel(const unsigned long long* __restrict__ cursor, uint64_t shard_cap,
+                                    uint32_t* __restrict__ flags) {
+    const unsigned long long c = cursor[threadIdx.x];
+    atomicMax(&flags[5], (uint32_t)min(c, 0xFFFFFFFFull));
+    if (c > shard_cap) atomicOr(&flags[3], 1u);
+}
+
+// copies flags[0] (bucket overflow of the bucket kernels) into flags[2]
+__global__ void bucket_flag_kernel(uint32_t* __restrict__ ws_flags, uint32_t* __restrict__ flags) {
+    if (ws_flags[0]) atomicOr(&flags[2], 1u);
+    if (ws_flags[1]) atomicOr(&flags[1], 1u);
+}
+
+// edge count of an encoded run list whose last run may be the kNoKey padding
+__global__ void run_count_kernel(const unsigned long long* __restrict__ uniq, const uint32_t* __restrict__ nuniq,
+                                 unsigned long long* __restrict__ count) {
+    const uint32_t u = *nuniq;
+    *count = u && uniq[u - 1] == kNoKey ? u - 1 : u;
+}
+
+static int sort_keys(kmp_postings* ws, const unsigned long long* in, unsigned long long* out, uint64_t m,
+                     unsigned lo, unsigned hi, hipStream_t st) {
+    size_t t = 0;
+    PG(rocprim::radix_sort_keys<SortCfg>(nullptr, t, in, out, (size_t)m, lo, hi, st));
+    PG(ws->tmp.reserve(std::max(t, ws->tmp.n)));
+    PG(rocprim::radix_sort_keys<SortCfg>(ws->tmp.p, t, in, out, (size_t)m, lo, hi, st));
+    return KMP_OK;
+}
+
+int kmp_dev_keys_route(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
+                       uint32_t n, int k, uint64_t slots, uint32_t lo, uint32_t hi, uint64_t slot_lo, uint64_t slot_hi,
+                       uint32_t parts, uint64_t cap, unsigned long long* d_send, uint32_t* d_flags, void* stream) {
+    if (!ws || !d_send || !d_flags || parts < 1 || cap < 1 || k < 1 || k > kMaxK || lo > hi || hi > n ||
+        slot_hi < slot_lo)
+        return KMP_EINVAL;
+    const Layout lay = make_layout(n, k, slots, true);
+    if (!lay.bucketed) return KMP_ESTATE;
+    hipStream_t st = as_stream(stream);
+    const uint64_t m = slot_hi - slot_lo;
+    PG(ws->bstats.reserve(std::max<uint64_t>(ws->bstats.n, kShards * 8 + kShards + parts + 1)));
+    unsigned long long* d_b = ws->bstats.p + kShards * 8 + kShards;
+    if (m == 0 || hi == lo) {
+        PG(hipMemsetAsync(d_b, 0, (parts + 1) * sizeof(unsigned long long), st));
+        route_kernel<<<dim3(64, parts), 256, 0, st>>>(ws->sorted.p, d_b, cap, d_send, d_flags, 4);
+        return KMP_OK;
+    }
+    PG(ws->keys.reserve(m));
+    PG(ws->sorted.reserve(m));
+    PG(ws->flags.reserve(4));
+    PG(hipMemsetAsync(ws->flags.p, 0, 4 * sizeof(uint32_t), st));
+    PG(launch_residue_keys(ws, d_res, d_res_off, d_class, k, lo, hi, slot_lo, slot_hi, lay, st));
+    int rc = sort_keys(ws, ws->keys.p, ws->sorted.p, m, lay.sort_lo, lay.sort_hi, st);
+    if (rc != KMP_OK) return rc;
+    part_bounds_kernel<<<(parts + 1 + 63) / 64, 64, 0, st>>>(ws->sorted.p, m, lay.sort_lo, 1ull << lay.bbits, 1,
+                                                              parts, d_b);
+    route_kernel<<<dim3(64, parts), 256, 0, st>>>(ws->sorted.p, d_b, cap, d_send, d_flags, 4);
+    bucket_flag_kernel<<<1, 1, 0, st>>>(ws->flags.p, d_flags);
+    PG(hipGetLastError());
+    return KMP_OK;
+}
+
+int kmp_dev_pairs_route(kmp_postings* ws, const unsigned long long* d_keys, uint64_t m, uint32_t n, int k,
+                        uint64_t slots, uint32_t heavy_df, int require_class_diff, uint64_t shard_cap, uint32_t parts,
+                        uint64_t cap, unsigned long long* d_send, uint32_t* d_flags, kmp_postings_stats* stats,
+                        void* stream) {
+    if (!ws || !d_send || !d_flags || parts < 1 || cap < 1 || shard_cap < 1 || k < 1 || k > kMaxK) return KMP_EINVAL;
+    if (stats) *stats = kmp_postings_stats{};
+    const Layout lay = make_layout(n, k, slots, true);
+    if (!lay.bucketed) return KMP_ESTATE;
+    hipStream_t st = as_stream(stream);
+    if (heavy_df < 2) heavy_df = 2;
+    PG(ws->flags.reserve(4));
+    PG(hipMemsetAsync(ws->flags.p, 0, 4 * sizeof(uint32_t), st));
+    // group + expand (the fused path's kernels, no read-back)
+    PG(ws->sorted.reserve(std::max<uint64_t>(1, m)));
+    if (m) {
+        int rc = sort_keys(ws, d_keys, ws->sorted.p, m, lay.sort_lo, lay.sort_hi, st);
+        if (rc != KMP_OK) return rc;
+    }
+    const uint32_t nb = 1u << lay.bbits;
+    PG(ws->cnt.reserve(2 * (uint64_t)nb + 2));
+    PG(ws->bstats.reserve(std::max<uint64_t>(ws->bstats.n, kShards * 8 + kShards + parts + 1)));
+    uint32_t* bstart = ws->cnt.p;
+    uint32_t* list = ws->cnt.p + nb + 1;
+    uint32_t* list_count = ws->flags.p + 2;
+    unsigned long long* gstats = ws->bstats.p;
+    unsigned long long* cursor = gstats + kShards * 8;
+    unsigned long long* d_b = cursor + kShards;
+    const uint64_t total = shard_cap * kShards;
+    PG(ws->inc_sorted.reserve(total));
+    PG(ws->inc.reserve(total));
+    PG(hipMemsetAsync(gstats, 0, (kShards * 8 + kShards) * sizeof(unsigned long long), st));
+    bucket_bounds_kernel<<<(nb + 1 + 255) / 256, 256, 0, st>>>(ws->sorted.p, m, lay.sort_lo, nb, bstart);
+    PShard ps{};
+    bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallTab, false>
+        <<<nb, kBucketSmallThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
+                                             ws->inc_sorted.p, shard_cap, cursor, gstats, ws->flags.p, list,
+                                             list_count, ps);
+    bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeTab, false>
+        <<<256, kBucketLargeThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
+                                              ws->inc_sorted.p, shard_cap, cursor, gstats, ws->flags.p, list,
+                                              list_count, ps);
+    check_shards_kernel<<<1, kShards, 0, st>>>(cursor, shard_cap, d_flags);
+    bucket_flag_kernel<<<1, 1, 0, st>>>(ws->flags.p, d_flags);
+    pad_shards_kernel<<<dim3(64, kShards), 256, 0, st>>>(ws->inc_sorted.p, shard_cap, cursor);
+    // sorted pair keys, routed by p range
+    const unsigned pair_bits = bits_for((uint64_t)n * n);
+    int rc = sort_keys(ws, ws->inc_sorted.p, ws->inc.p, total, 0, pair_bits, st);
+    if (rc != KMP_OK) return rc;
+    part_bounds_kernel<<<(parts + 1 + 63) / 64, 64, 0, st>>>(ws->inc.p, total, 0, n, n, parts, d_b);
+    route_kernel<<<dim3(64, parts), 256, 0, st>>>(ws->inc.p, d_b, cap, d_send, d_flags, 6);
+    PG(hipGetLastError());
+    return KMP_OK;
+}
+
+int kmp_dev_edges_route(kmp_postings* ws, const unsigned long long* d_pk, uint64_t m, uint32_t n, uint32_t* d_p,
+                        uint32_t* d_q, uint32_t* d_w, uint64_t cap, unsigned long long* d_count, void* stream) {
+    if (!ws || !d_count || (m && (!d_pk || !d_p || !d_q || !d_w))) return KMP_EINVAL;
+    hipStream_t st = as_stream(stream);
+    if (m == 0) {
+        PG(hipMemsetAsync(d_count, 0, sizeof(unsigned long long), st));
+        return KMP_OK;
+    }
+    PG(ws->inc_sorted.reserve(m));
+    PG(ws->uniq.reserve(m));
+    PG(ws->w.reserve(m));
+    PG(ws->small.reserve(16));
+    const unsigned pair_bits = bits_for((uint64_t)n * n);
+    int rc = sort_keys(ws, d_pk, ws->inc_sorted.p, m, 0, pair_bits, st);
+    if (rc != KMP_OK) return rc;
+    size_t t3 = 0;
+    PG(rocprim::run_length_encode(nullptr, t3, ws->inc_sorted.p, (unsigned int)m, ws->uniq.p, ws->w.p,
+                                  ws->small.p + 1, st));
+    PG(ws->tmp.reserve(std::max(t3, ws->tmp.n)));
+    PG(rocprim::run_length_encode(ws->tmp.p, t3, ws->inc_sorted.p, (unsigned int)m, ws->uniq.p, ws->w.p,
+                                  ws->small.p + 1, st));
+    const uint32_t kb = (uint32_t)std::min<uint64_t>((m + 255) / 256, 8192);
+    emit_runs_kernel<<<kb, 256, 0, st>>>(ws->uniq.p, ws->w.p, ws->small.p + 1, n, d_p, d_q, d_w, cap);
+    run_count_kernel<<<1, 1, 0, st>>>(ws->uniq.p, ws->small.p + 1, d_count);
+    PG(hipGetLastError());
+    return KMP_OK;
+}
+
 }  // extern "C"
+
 
 
 #undef PG

@@ -199,10 +199,170 @@ def distributed_postings(stages, offsets: np.ndarray, rank: int, world: int, gro
     return gather_edges(ep, eq, ew, m, rank, group), m
 
 
+def exchange_equal(send: torch.Tensor, group=None) -> torch.Tensor:
+    """all-to-all of `world` equal regions (region j -> rank j); no count exchange."""
+    dev = send.device
+    staged = _staged(send, group)
+    src = send.cpu() if staged else send
+    recv = torch.empty_like(src)
+    dist.all_to_all_single(recv, src, group=group)
+    return recv.to(dev) if staged else recv
+
+
+def gather_to_rank0(flat: torch.Tensor, count: int, counts: list, rank: int, group=None):
+    """Rank r's first `count` elements -> rank 0, concatenated in rank order (one uneven
+    all-to-all: every rank sends only to rank 0)."""
+    world = len(counts)
+    dev = flat.device
+    staged = _staged(flat, group)
+    src = flat[:count].cpu() if staged else flat[:count]
+    in_splits = [count] + [0] * (world - 1)
+    out_splits = counts if rank == 0 else [0] * world
+    recv = torch.empty(sum(out_splits), dtype=flat.dtype, device=src.device)
+    dist.all_to_all_single(recv, src.contiguous(), out_splits, in_splits, group=group)
+    return (recv.to(dev) if staged else recv) if rank == 0 else None
+
+
+class DeviceRouteStages:
+    """The fixed-capacity device stages (kmp_dev_keys_route / kmp_dev_pairs_route /
+    kmp_dev_edges_route) on a DevicePipeline.  Capacities are learned: a flagged step reports
+    the sizes it needed and the caller reruns after grow()."""
+
+    def __init__(self, pipe, require_class_diff: bool = True):
+        import ctypes as C
+        self.C = C
+        self.pipe = pipe
+        self.L = _lib.lib()
+        self.ws = pipe._workspace()
+        self.slots = int(self.L.kmp_set_capacity(pipe.n, pipe.total))
+        self.require_class_diff = require_class_diff
+        self.cap_keys = 0
+        self.cap_pairs = 0
+        self.shard_cap = 0
+        self.flags = torch.zeros(8, dtype=torch.int32, device=pipe.dev)
+        self.count = torch.zeros(1, dtype=torch.int64, device=pipe.dev)
+        self.stats = _lib.PostingsStats()
+
+    def _stream(self):
+        return self.C.c_void_p(torch.cuda.current_stream(self.pipe.dev).cuda_stream)
+
+    def _ptr(self, t):
+        return self.C.c_void_p(t.data_ptr())
+
+    def begin(self, world: int):
+        p = self.pipe
+        if self.cap_keys == 0:  # first guesses: an even split + 10 %
+            self.cap_keys = self.slots // (world * world) + self.slots // (10 * world * world) + 4096
+            self.shard_cap = self.slots // (4 * 64 * world) + 4096
+            self.cap_pairs = self.slots // (4 * world * world) + 4096
+        self.flags.zero_()
+
+    def keys_route(self, lo: int, hi: int, parts: int) -> torch.Tensor:
+        L, p = self.L, self.pipe
+        off = p.offsets_host
+        slot_lo = int(L.kmp_set_base(int(off[lo]), lo))
+        slot_hi = int(L.kmp_set_base(int(off[hi]), hi))
+        send = torch.empty(parts * self.cap_keys, dtype=torch.int64, device=p.dev)
+        _lib.check(L.kmp_dev_keys_route(self.ws, self._ptr(p.res), self._ptr(p.off), self._ptr(p.cls), p.n, p.k,
+                                        self.slots, lo, hi, slot_lo, slot_hi, parts, self.cap_keys,
+                                        self._ptr(send), self._ptr(self.flags), self._stream()),
+                   "kmp_dev_keys_route")
+        return send
+
+    def pairs_route(self, keys: torch.Tensor, parts: int) -> torch.Tensor:
+        L, p = self.L, self.pipe
+        send = torch.empty(parts * self.cap_pairs, dtype=torch.int64, device=p.dev)
+        _lib.check(L.kmp_dev_pairs_route(self.ws, self._ptr(keys), keys.numel(), p.n, p.k, self.slots, 0xFFFFFFFF,
+                                         int(self.require_class_diff), self.shard_cap, parts, self.cap_pairs,
+                                         self._ptr(send), self._ptr(self.flags), self.C.byref(self.stats),
+                                         self._stream()), "kmp_dev_pairs_route")
+        return send
+
+    def edges_route(self, pk: torch.Tensor):
+        """(p, q, w) interleaved as an int32 [m, 3] buffer and the edge count (device)."""
+        L, p = self.L, self.pipe
+        m = pk.numel()
+        e = torch.empty((3, max(1, m)), dtype=torch.int32, device=p.dev)
+        _lib.check(L.kmp_dev_edges_route(self.ws, self._ptr(pk), m, p.n, self._ptr(e[0]), self._ptr(e[1]),
+                                         self._ptr(e[2]), max(1, m), self._ptr(self.count), self._stream()),
+                   "kmp_dev_edges_route")
+        return e, self.count
+
+    def status(self) -> torch.Tensor:
+        """flags[0..7] + edge count, as one int64 device tensor (gathered across ranks)."""
+        return torch.cat([self.flags.to(torch.int64), self.count])
+
+    def grow(self, worst: np.ndarray) -> None:
+        """worst = element-wise max of every rank's flags."""
+        if worst[0]:
+            self.cap_keys = max(self.cap_keys, int(worst[4]) + int(worst[4]) // 16 + 1024)
+            self.cap_pairs = max(self.cap_pairs, int(worst[6]) + int(worst[6]) // 16 + 1024)
+        if worst[3]:
+            self.shard_cap = max(self.shard_cap, int(worst[5]) + int(worst[5]) // 16 + 1024)
+
+
+class RouteFallback(RuntimeError):
+    """The batch needs the single-GPU flat layout (a very frequent k-mer or wide class ids)."""
+
+
+def distributed_postings_padded(stages, offsets: np.ndarray, rank: int, world: int, group=None,
+                                max_attempts: int = 4):
+    """The fixed-capacity flow: keys routed by bucket range, pair keys routed by p range, edges
+    to rank 0 in rank order (= canonical).  One host synchronisation per attempt: the all-gather
+    of every rank's flags and edge count.  Returns rank 0's flat (p, q, w) int32 tensor (rank r's
+    block of 3 * count_r values is [p..., q..., w...]) and the per-rank counts; None elsewhere."""
+    lo, hi = protein_slices(offsets, world)[rank]
+    for _ in range(max_attempts):
+        stages.begin(world)
+        mine = exchange_equal(stages.keys_route(lo, hi, world), group)
+        pk = exchange_equal(stages.pairs_route(mine, world), group)
+        e, count = stages.edges_route(pk)
+        st = stages.status()
+        parts = [torch.empty_like(st) for _ in range(world)]
+        if _staged(st, group):
+            cpu = [torch.empty_like(st, device="cpu") for _ in range(world)]
+            dist.all_gather(cpu, st.cpu(), group=group)
+            table = torch.stack(cpu).numpy()
+        else:
+            dist.all_gather(parts, st, group=group)
+            table = torch.stack(parts).cpu().numpy()  # the step's one host synchronisation
+        worst = table[:, :8].max(axis=0)
+        if worst[1] or worst[2]:
+            raise RouteFallback("batch needs the single-GPU flat layout (frequent k-mer or wide class id)")
+        if worst[0] or worst[3]:
+            stages.grow(worst)
+            continue
+        counts = [int(c) for c in table[:, 8]]
+        c = counts[rank]
+        flat = e[:, :c].contiguous().view(-1) if c else e[:, :0].contiguous().view(-1)
+        got = gather_to_rank0(flat, 3 * c, [3 * x for x in counts], rank, group)
+        return got, counts
+    raise RuntimeError("exchange capacities did not converge")
+
+
 def distributed_step(pipe, rank: int, world: int, group=None, min_shared: int = 1,
                      require_class_diff: bool = True, timers: dict | None = None, engine: str = "residues") -> int:
     """One multi-GPU pass of the path on a DevicePipeline holding the whole batch.
     Returns the canonical edge count (rank 0) or this rank's share (others)."""
+    if engine in ("residues", "postings") and min_shared == 1:
+        stages = getattr(pipe, "_route_stages", None)
+        if stages is None or stages.require_class_diff != require_class_diff:
+            stages = pipe._route_stages = DeviceRouteStages(pipe, require_class_diff)
+        got, counts = distributed_postings_padded(stages, pipe.offsets_host, rank, world, group)
+        if rank == 0:
+            n = sum(counts)
+            if n > pipe.edge_cap:
+                pipe._alloc_edges(n + n // 8 + 1024)
+            o = 0
+            for c in counts:  # rank r's block: p[c], q[c], w[c]
+                blk = got[3 * o:3 * (o + c)].view(3, c)
+                pipe.ep[o:o + c] = blk[0]
+                pipe.eq[o:o + c] = blk[1]
+                pipe.ew[o:o + c] = blk[2]
+                o += c
+            pipe.n_edges = n
+            return n
+        return counts[rank]
     if engine in ("residues", "postings"):
         stages = getattr(pipe, "_dist_stages", None)
         if stages is None or stages.min_shared != min_shared or stages.require_class_diff != require_class_diff:
