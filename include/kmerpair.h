@@ -315,17 +315,23 @@ int kmp_dev_edges_pairkeys(kmp_postings* ws, const unsigned long long* d_pk, uin
  * [1] a class id too wide, [2] a k-mer group too large for the LDS buckets (both: use the
  * single-GPU path), [3] a shard region exceeded shard_cap (size in [5]).  After a flagged step
  * the caller grows the capacities and reruns.
- *   kmp_dev_keys_route:  keys of proteins [lo, hi) bucket-sorted and routed by bucket range.
- *   kmp_dev_pairs_route: the m received keys grouped + expanded, pair keys sorted and routed
- *                        by p range (shard_cap: pair keys per expansion shard region).
+ *   kmp_dev_keys_route:  keys of proteins [lo, hi) routed by bucket range (not sorted: every
+ *                        receiver sorts).
+ *   kmp_dev_pairs_route: the m received keys (bucket part `part` of `parts`) grouped +
+ *                        expanded, pair keys routed by row range (kmp_row_split; shard_cap: pair
+ *                        keys per expansion shard region).
  *   kmp_dev_edges_route: the m received pair keys -> this p range's edges, count in *d_count. */
+/* Row ranges of the pair split: range d = [start[d], start[d+1]) with start[d] =
+ * floor(N (1 - sqrt(1 - d/parts))): a pair belongs to its smaller protein, so the ranges hold about
+ * equal pair counts.  start has parts + 1 entries, parts <= 64. */
+void kmp_row_split(uint32_t n, uint32_t parts, uint32_t* start);
 int kmp_dev_keys_route(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
                        uint32_t n, int k, uint64_t slots, uint32_t lo, uint32_t hi, uint64_t slot_lo, uint64_t slot_hi,
                        uint32_t parts, uint64_t cap, unsigned long long* d_send, uint32_t* d_flags, void* stream);
 int kmp_dev_pairs_route(kmp_postings* ws, const unsigned long long* d_keys, uint64_t m, uint32_t n, int k,
-                        uint64_t slots, uint32_t heavy_df, int require_class_diff, uint64_t shard_cap, uint32_t parts,
-                        uint64_t cap, unsigned long long* d_send, uint32_t* d_flags, kmp_postings_stats* stats,
-                        void* stream);
+                        uint64_t slots, uint32_t heavy_df, int require_class_diff, uint64_t shard_cap, uint32_t part,
+                        uint32_t parts, uint64_t cap, unsigned long long* d_send, uint32_t* d_flags,
+                        kmp_postings_stats* stats, void* stream);
 int kmp_dev_edges_route(kmp_postings* ws, const unsigned long long* d_pk, uint64_t m, uint32_t n, uint32_t* d_p,
                         uint32_t* d_q, uint32_t* d_w, uint64_t cap, unsigned long long* d_count, void* stream);
 

@@ -168,7 +168,7 @@ class OracleRouteStages:
                                for p in range(lo, hi)] + [np.zeros(0, np.uint64)])
         return self._route(keys, (keys >> np.uint64(20)) % np.uint64(parts), parts, self.cap_keys, 4)
 
-    def pairs_route(self, keys, parts):
+    def pairs_route(self, keys, part, parts):
         k = keys.numpy().view(np.uint64)
         k = np.sort(k[k != ALL])
         code, p = k >> np.uint64(20), (k & np.uint64((1 << 20) - 1)).astype(np.int64)

@@ -169,3 +169,18 @@ def test_planner_rejects_oversized_set():
     with pytest.raises(_lib.KmpError) as e:
         plan(lens, 4)
     assert e.value.status == _lib.KMP_EINVAL
+
+
+def test_row_split_balances_pairs():
+    """kmp_row_split: monotone row ranges covering [0, N) whose expected pair counts (row p owns
+    N - 1 - p pairs) are within a few % of each other."""
+    import ctypes as C
+    L = K._lib.lib()
+    for n, parts in ((100000, 8), (100000, 3), (10619, 2), (7, 4), (1, 1)):
+        st = (C.c_uint32 * (parts + 1))()
+        L.kmp_row_split(n, parts, st)
+        s = list(st)
+        assert s[0] == 0 and s[-1] == n and all(a <= b for a, b in zip(s, s[1:]))
+        if n >= 1000:
+            load = [sum(n - 1 - p for p in range(a, b)) for a, b in zip(s, s[1:])]
+            assert max(load) / min(load) < 1.01, load

@@ -123,10 +123,11 @@ SIGNATURES = {
                                      C.c_uint32, P, C.c_uint64, U64P, U64P, P, P]),
     "kmp_dev_edges_pairkeys": (C.c_int, [P, P, C.c_uint64, C.c_uint32, C.c_uint32, P, P, P, C.c_uint64, U64P,
                                          U64P, P]),
+    "kmp_row_split": (None, [C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]),
     "kmp_dev_keys_route": (C.c_int, [P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32, C.c_uint32,
                                      C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64, P, P, P]),
     "kmp_dev_pairs_route": (C.c_int, [P, P, C.c_uint64, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32, C.c_int,
-                                      C.c_uint64, C.c_uint32, C.c_uint64, P, P, P, P]),
+                                      C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, P, P, P, P]),
     "kmp_dev_edges_route": (C.c_int, [P, P, C.c_uint64, C.c_uint32, P, P, P, C.c_uint64, P, P]),
     "kmp_dev_sort_edges_tmp_bytes": (C.c_uint64, [C.c_uint64, C.c_uint32]),
     "kmp_dev_sort_edges": (C.c_int, [P, P, P, C.c_uint64, C.c_uint32, P, C.c_uint64, P]),

@@ -27,6 +27,7 @@
 #include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstdint>
@@ -50,6 +51,9 @@ unsigned bits_for(uint64_t v) {  // bits needed for values < v
 }
 
 constexpr unsigned long long kNoKey = ~0ull;
+
+// blocks per region for the region copy/fill kernels (about 1024 keys per block)
+inline uint32_t route_blocks(uint64_t cap) { return (uint32_t)std::min<uint64_t>((cap + 1023) / 1024, 4096); }
 
 // rocprim 4.2 (ROCm 7.2): with the default config, radix_sort_keys on fewer than 1M keys takes a
 // merge-sort path that returns unsorted, non-permuted data for bit ranges [b, 64) with b > 0
@@ -712,10 +716,11 @@ __global__ __launch_bounds__(kThreads) void bucket_small_kernel(
     const unsigned long long* __restrict__ sorted, const uint32_t* __restrict__ bstart, Layout lay,
     uint32_t n_prot, int require_diff, uint32_t heavy_df, unsigned long long* __restrict__ out, uint64_t shard_cap,
     unsigned long long* __restrict__ cursor, unsigned long long* __restrict__ gstats, uint32_t* __restrict__ flags,
-    uint32_t* __restrict__ list, uint32_t* __restrict__ list_count, PShard ps) {
-    process_bucket<kCap, kThreads, kTabBits, kPShard>(blockIdx.x, sorted, bstart, lay, n_prot, require_diff, heavy_df,
-                                                      true, out, shard_cap, cursor, gstats, flags, list, list_count,
-                                                      ps);
+    uint32_t* __restrict__ list, uint32_t* __restrict__ list_count, PShard ps, uint32_t b0 = 0) {
+    // buckets b0 + blockIdx.x (a multi-GPU rank launches only its bucket range)
+    process_bucket<kCap, kThreads, kTabBits, kPShard>(b0 + blockIdx.x, sorted, bstart, lay, n_prot, require_diff,
+                                                      heavy_df, true, out, shard_cap, cursor, gstats, flags, list,
+                                                      list_count, ps);
 }
 
 // the buckets the small kernel listed (above its capacity), a grid-stride loop over the list
@@ -1302,7 +1307,7 @@ int run_bucketed_fused(kmp_postings* ws, uint64_t slots, const Layout& lay, uint
             <<<256, kBucketLargeThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
                                                   ws->inc_sorted.p, sc, cursor, gstats, flags, list, list_count, ps);
         ws->mark(3, st);
-        pad_shards_kernel<<<dim3(64, kShards), 256, 0, st>>>(ws->inc_sorted.p, sc, cursor);
+        pad_shards_kernel<<<dim3(route_blocks(sc), kShards), 256, 0, st>>>(ws->inc_sorted.p, sc, cursor);
         ws->mark(4, st);
         size_t t2 = 0, t3 = 0;
         PG(rocprim::radix_sort_keys<SortCfg>(nullptr, t2, ws->inc_sorted.p, ws->inc.p, (size_t)total, 0u, pair_bits,
@@ -1675,6 +1680,99 @@ __global__ void route_kernel(const unsigned long long* __restrict__ sorted,
         send[d * cap + i] = i < cnt ? sorted[b0 + i] : kNoKey;
 }
 
+// Partition into `parts` padded regions without sorting.  Destination of a key:
+//   kPairs == false (k-mer keys):  bucket = key >> shift, valid iff bucket < total,
+//                                  dest = bucket * parts / total (contiguous bucket ranges);
+//   kPairs == true  (pair keys):   valid iff key != kNoKey, p = key / total, dest = the row range
+//                                  [rows[d], rows[d+1]) holding p (contiguous row ranges, so the
+//                                  rank-order concatenation stays canonical).
+// Each workgroup ranks its 4096 keys per destination in LDS and reserves one range per
+// destination on dcursor[d]; pad_regions_kernel then fills the tails and raises the flags.
+}  // extern "C"
+namespace {
+constexpr int kPartThreads = 256, kPartIPT = 16, kPartMax = 64;
+struct RowSplit {
+    uint32_t start[kPartMax + 1];  // row range d = [start[d], start[d+1])
+};
+template <bool kPairs>
+__global__ __launch_bounds__(kPartThreads) void partition_kernel(const unsigned long long* __restrict__ in,
+                                                                 uint64_t m, unsigned shift, unsigned long long total,
+                                                                 uint32_t parts, uint64_t cap,
+                                                                 unsigned long long* __restrict__ send,
+                                                                 unsigned long long* __restrict__ dcursor,
+                                                                 RowSplit rows) {
+    __shared__ uint32_t lcnt[kPartMax];
+    __shared__ unsigned long long base[kPartMax];
+    const int tid = threadIdx.x;
+    const uint64_t c0 = blockIdx.x * (uint64_t)(kPartThreads * kPartIPT);
+    if (tid < kPartMax) lcnt[tid] = 0;
+    __syncthreads();
+    unsigned long long x[kPartIPT];
+    uint32_t dr[kPartIPT];  // dest << 24 | rank, or ~0 for padding
+#pragma unroll
+    for (int j = 0; j < kPartIPT; ++j) {
+        const uint64_t i = c0 + (uint64_t)j * kPartThreads + tid;
+        x[j] = i < m ? in[i] : kNoKey;
+        dr[j] = ~0u;
+        bool valid;
+        unsigned long long v;
+        if (kPairs) {
+            valid = x[j] != kNoKey;
+            v = valid ? x[j] / total : 0;
+        } else {
+            v = x[j] >> shift;
+            valid = i < m && v < total;
+        }
+        if (valid) {
+            uint32_t d;
+            if (kPairs) {
+                d = 0;
+                while (d + 1 < parts && v >= rows.start[d + 1]) ++d;
+            } else {
+                d = (uint32_t)(v * parts / total);
+            }
+            dr[j] = (d << 24) | atomicAdd(&lcnt[d], 1u);
+        }
+    }
+    __syncthreads();
+    if (tid < (int)parts) base[tid] = lcnt[tid] ? atomicAdd(&dcursor[tid], (unsigned long long)lcnt[tid]) : 0ull;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kPartIPT; ++j) {
+        if (dr[j] == ~0u) continue;
+        const uint32_t d = dr[j] >> 24;
+        const unsigned long long pos = base[d] + (dr[j] & 0xFFFFFFu);
+        if (pos < cap) send[d * cap + pos] = x[j];
+    }
+}
+
+}  // namespace
+extern "C" {
+
+// Row ranges of the multi-GPU pair split: a pair belongs to its smaller protein, so row p owns
+// about N - p pairs; range d starts at N * (1 - sqrt(1 - d/parts)) (equal expected pair counts).
+void kmp_row_split(uint32_t n, uint32_t parts, uint32_t* start) {
+    for (uint32_t d = 0; d <= parts; ++d) {
+        const double x = 1.0 - std::sqrt(1.0 - (double)d / parts);
+        start[d] = d == parts ? n : (uint32_t)std::min<double>(n, std::floor(x * n));
+    }
+}
+
+// region tails -> kNoKey; largest region -> flags[max_slot], overflow -> flags[0]
+__global__ void pad_regions_kernel(unsigned long long* __restrict__ send, uint64_t cap,
+                                   const unsigned long long* __restrict__ dcursor, uint32_t* __restrict__ flags,
+                                   int max_slot) {
+    const uint32_t d = blockIdx.y;
+    const unsigned long long cnt = dcursor[d];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        atomicMax(&flags[max_slot], (uint32_t)min(cnt, 0xFFFFFFFFull));
+        if (cnt > cap) atomicOr(&flags[0], 1u);
+    }
+    for (uint64_t i = cnt + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        send[d * cap + i] = kNoKey;
+}
+
 // largest shard cursor -> flags[5]; overflow -> flags[3]
 __global__ void check_shards_kernel(const unsigned long long* __restrict__ cursor, uint64_t shard_cap,
                                     uint32_t* __restrict__ flags) {
@@ -1708,7 +1806,8 @@ static int sort_keys(kmp_postings* ws, const unsigned long long* in, unsigned lo
 int kmp_dev_keys_route(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
                        uint32_t n, int k, uint64_t slots, uint32_t lo, uint32_t hi, uint64_t slot_lo, uint64_t slot_hi,
                        uint32_t parts, uint64_t cap, unsigned long long* d_send, uint32_t* d_flags, void* stream) {
-    if (!ws || !d_send || !d_flags || parts < 1 || cap < 1 || k < 1 || k > kMaxK || lo > hi || hi > n ||
+    if (!ws || !d_send || !d_flags || parts < 1 || parts > (uint32_t)kPartMax || cap < 1 || k < 1 || k > kMaxK ||
+        lo > hi || hi > n ||
         slot_hi < slot_lo)
         return KMP_EINVAL;
     const Layout lay = make_layout(n, k, slots, true);
@@ -1719,7 +1818,7 @@ int kmp_dev_keys_route(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d
     unsigned long long* d_b = ws->bstats.p + kShards * 8 + kShards;
     if (m == 0 || hi == lo) {
         PG(hipMemsetAsync(d_b, 0, (parts + 1) * sizeof(unsigned long long), st));
-        route_kernel<<<dim3(64, parts), 256, 0, st>>>(ws->sorted.p, d_b, cap, d_send, d_flags, 4);
+        pad_regions_kernel<<<dim3(route_blocks(cap), parts), 256, 0, st>>>(d_send, cap, d_b, d_flags, 4);
         return KMP_OK;
     }
     PG(ws->keys.reserve(m));
@@ -1727,21 +1826,23 @@ int kmp_dev_keys_route(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d
     PG(ws->flags.reserve(4));
     PG(hipMemsetAsync(ws->flags.p, 0, 4 * sizeof(uint32_t), st));
     PG(launch_residue_keys(ws, d_res, d_res_off, d_class, k, lo, hi, slot_lo, slot_hi, lay, st));
-    int rc = sort_keys(ws, ws->keys.p, ws->sorted.p, m, lay.sort_lo, lay.sort_hi, st);
-    if (rc != KMP_OK) return rc;
-    part_bounds_kernel<<<(parts + 1 + 63) / 64, 64, 0, st>>>(ws->sorted.p, m, lay.sort_lo, 1ull << lay.bbits, 1,
-                                                              parts, d_b);
-    route_kernel<<<dim3(64, parts), 256, 0, st>>>(ws->sorted.p, d_b, cap, d_send, d_flags, 4);
+    unsigned long long* dcur = d_b;  // parts destination cursors
+    PG(hipMemsetAsync(dcur, 0, parts * sizeof(unsigned long long), st));
+    partition_kernel<false><<<(uint32_t)((m + 4095) / 4096), kPartThreads, 0, st>>>(
+        ws->keys.p, m, lay.sort_lo, 1ull << lay.bbits, parts, cap, d_send, dcur, RowSplit{});
+    pad_regions_kernel<<<dim3(route_blocks(cap), parts), 256, 0, st>>>(d_send, cap, dcur, d_flags, 4);
     bucket_flag_kernel<<<1, 1, 0, st>>>(ws->flags.p, d_flags);
     PG(hipGetLastError());
     return KMP_OK;
 }
 
 int kmp_dev_pairs_route(kmp_postings* ws, const unsigned long long* d_keys, uint64_t m, uint32_t n, int k,
-                        uint64_t slots, uint32_t heavy_df, int require_class_diff, uint64_t shard_cap, uint32_t parts,
-                        uint64_t cap, unsigned long long* d_send, uint32_t* d_flags, kmp_postings_stats* stats,
-                        void* stream) {
-    if (!ws || !d_send || !d_flags || parts < 1 || cap < 1 || shard_cap < 1 || k < 1 || k > kMaxK) return KMP_EINVAL;
+                        uint64_t slots, uint32_t heavy_df, int require_class_diff, uint64_t shard_cap, uint32_t part,
+                        uint32_t parts, uint64_t cap, unsigned long long* d_send, uint32_t* d_flags,
+                        kmp_postings_stats* stats, void* stream) {
+    if (!ws || !d_send || !d_flags || parts < 1 || parts > (uint32_t)kPartMax || part >= parts || cap < 1 ||
+        shard_cap < 1 || k < 1 || k > kMaxK)
+        return KMP_EINVAL;
     if (stats) *stats = kmp_postings_stats{};
     const Layout lay = make_layout(n, k, slots, true);
     if (!lay.bucketed) return KMP_ESTATE;
@@ -1770,23 +1871,28 @@ int kmp_dev_pairs_route(kmp_postings* ws, const unsigned long long* d_keys, uint
     PG(hipMemsetAsync(gstats, 0, (kShards * 8 + kShards) * sizeof(unsigned long long), st));
     bucket_bounds_kernel<<<(nb + 1 + 255) / 256, 256, 0, st>>>(ws->sorted.p, m, lay.sort_lo, nb, bstart);
     PShard ps{};
-    bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallTab, false>
-        <<<nb, kBucketSmallThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
-                                             ws->inc_sorted.p, shard_cap, cursor, gstats, ws->flags.p, list,
-                                             list_count, ps);
+    // this part's bucket range (the keys routed here hold no others)
+    const uint32_t b0 = (uint32_t)(((uint64_t)part * nb + parts - 1) / parts);
+    const uint32_t b1 = (uint32_t)(((uint64_t)(part + 1) * nb + parts - 1) / parts);
+    if (b1 > b0)
+        bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallTab, false>
+            <<<b1 - b0, kBucketSmallThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
+                                                      ws->inc_sorted.p, shard_cap, cursor, gstats, ws->flags.p, list,
+                                                      list_count, ps, b0);
     bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeTab, false>
         <<<256, kBucketLargeThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
                                               ws->inc_sorted.p, shard_cap, cursor, gstats, ws->flags.p, list,
                                               list_count, ps);
     check_shards_kernel<<<1, kShards, 0, st>>>(cursor, shard_cap, d_flags);
     bucket_flag_kernel<<<1, 1, 0, st>>>(ws->flags.p, d_flags);
-    pad_shards_kernel<<<dim3(64, kShards), 256, 0, st>>>(ws->inc_sorted.p, shard_cap, cursor);
-    // sorted pair keys, routed by p range
-    const unsigned pair_bits = bits_for((uint64_t)n * n);
-    int rc = sort_keys(ws, ws->inc_sorted.p, ws->inc.p, total, 0, pair_bits, st);
-    if (rc != KMP_OK) return rc;
-    part_bounds_kernel<<<(parts + 1 + 63) / 64, 64, 0, st>>>(ws->inc.p, total, 0, n, n, parts, d_b);
-    route_kernel<<<dim3(64, parts), 256, 0, st>>>(ws->inc.p, d_b, cap, d_send, d_flags, 6);
+    pad_shards_kernel<<<dim3(route_blocks(shard_cap), kShards), 256, 0, st>>>(ws->inc_sorted.p, shard_cap, cursor);
+    // pair keys routed by row range (no sort: every receiver sorts its runs)
+    PG(hipMemsetAsync(d_b, 0, parts * sizeof(unsigned long long), st));
+    RowSplit rows{};
+    kmp_row_split(n, parts, rows.start);
+    partition_kernel<true><<<(uint32_t)((total + 4095) / 4096), kPartThreads, 0, st>>>(
+        ws->inc_sorted.p, total, 0, n, parts, cap, d_send, d_b, rows);
+    pad_regions_kernel<<<dim3(route_blocks(cap), parts), 256, 0, st>>>(d_send, cap, d_b, d_flags, 6);
     PG(hipGetLastError());
     return KMP_OK;
 }

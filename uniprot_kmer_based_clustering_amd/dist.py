@@ -269,11 +269,11 @@ class DeviceRouteStages:
                    "kmp_dev_keys_route")
         return send
 
-    def pairs_route(self, keys: torch.Tensor, parts: int) -> torch.Tensor:
+    def pairs_route(self, keys: torch.Tensor, part: int, parts: int) -> torch.Tensor:
         L, p = self.L, self.pipe
         send = torch.empty(parts * self.cap_pairs, dtype=torch.int64, device=p.dev)
         _lib.check(L.kmp_dev_pairs_route(self.ws, self._ptr(keys), keys.numel(), p.n, p.k, self.slots, 0xFFFFFFFF,
-                                         int(self.require_class_diff), self.shard_cap, parts, self.cap_pairs,
+                                         int(self.require_class_diff), self.shard_cap, part, parts, self.cap_pairs,
                                          self._ptr(send), self._ptr(self.flags), self.C.byref(self.stats),
                                          self._stream()), "kmp_dev_pairs_route")
         return send
@@ -315,7 +315,7 @@ def distributed_postings_padded(stages, offsets: np.ndarray, rank: int, world: i
     for _ in range(max_attempts):
         stages.begin(world)
         mine = exchange_equal(stages.keys_route(lo, hi, world), group)
-        pk = exchange_equal(stages.pairs_route(mine, world), group)
+        pk = exchange_equal(stages.pairs_route(mine, rank, world), group)
         e, count = stages.edges_route(pk)
         st = stages.status()
         parts = [torch.empty_like(st) for _ in range(world)]
