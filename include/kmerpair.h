@@ -61,6 +61,7 @@ enum {
 
 typedef struct kmp_ctx kmp_ctx;
 typedef struct kmp_edges kmp_edges;
+typedef struct kmp_mphf kmp_mphf;
 
 /* The reference's stderr counters (graph/mod.rs:50,51,545,695) plus set statistics. */
 typedef struct {
@@ -116,6 +117,41 @@ int kmp_get_kmers(kmp_ctx* ctx, uint32_t protein, uint32_t* out, uint64_t cap, u
 int kmp_build_sets(kmp_ctx* ctx, int k);
 int kmp_get_set(kmp_ctx* ctx, uint32_t protein, uint32_t* out, uint64_t cap, uint64_t* n);
 int kmp_counters_get(kmp_ctx* ctx, kmp_counters* out);
+
+/* ------------------------------------------------------------------ repeat index --- */
+/* The repeat k-mers (df >= 2) of the last kmp_build_sets, indexed by a device minimal perfect
+ * hash (main.rs:127-149: Mphf::new(3.0, &five_mer_repeat)); built on first use, kept until the
+ * next kmp_load_proteins / kmp_build_sets.  Ids are dense, 0 .. repeat-1, but not boomphf's
+ * (SURVEY.md §8c): they are internal indices, and code_by_id / df_by_id give their meaning.
+ *   kmp_get_df: df_by_id[repeat] = five_mer_hash_freq (main.rs:154,187-193);
+ *   kmp_get_repeat_codes: code_by_id[repeat], the inverse of the hash;
+ *   kmp_get_hash_kmers: hash_five_mers of protein p (remove_unique_five_mers +
+ *     modify_hash_five_mer, protein.rs:151-174; get_five_hash, :146): the ids of p's repeat
+ *     windows in first-occurrence order, duplicates dropped;
+ *   kmp_get_hash_kmers_all: the same for every protein, CSR: ids[offsets[p] .. offsets[p+1]),
+ *     offsets has n+1 entries (may be NULL to query the total in *n);
+ *   kmp_repeat_mphf: the context-owned MPHF (valid until the index is rebuilt) for lookups.
+ * All copy up to cap entries, set *n to the total and return KMP_EOVERFLOW if cap < total. */
+int kmp_get_df(kmp_ctx* ctx, uint32_t* df_by_id, uint64_t cap, uint64_t* n);
+int kmp_get_repeat_codes(kmp_ctx* ctx, uint32_t* code_by_id, uint64_t cap, uint64_t* n);
+int kmp_get_hash_kmers(kmp_ctx* ctx, uint32_t protein, uint32_t* ids, uint64_t cap, uint64_t* n);
+int kmp_get_hash_kmers_all(kmp_ctx* ctx, uint32_t* ids, uint64_t cap, uint64_t* offsets, uint64_t* n);
+int kmp_repeat_mphf(kmp_ctx* ctx, const kmp_mphf** out);
+
+/* ------------------------------------------------------------------ MPHF ----------- */
+/* boomphf's Mphf<u32> surface (Mphf::new(gamma, &keys) / hash(&key), main.rs:139-140,145,192;
+ * protein.rs:154,168) on the device: a BBHash of levelled bit vectors, about gamma bits per key
+ * per level, ranks by popcount prefix.  keys must be distinct (KMP_EINVAL otherwise, where
+ * boomphf would not terminate); ids of the n keys are a permutation of 0 .. n-1.  A key outside
+ * the set gets an arbitrary id or UINT64_MAX, as with boomphf.  Host buffers; the build and
+ * lookups run on the context's device.  kmp_mphf_dev_lookup takes device buffers and a
+ * hipStream_t (NULL: default stream).  gamma in [1, 100]. */
+int kmp_mphf_build(kmp_ctx* ctx, const uint32_t* keys, uint64_t n, double gamma, kmp_mphf** out);
+int kmp_mphf_lookup(const kmp_mphf* m, const uint32_t* keys, uint64_t n, uint64_t* ids);
+int kmp_mphf_dev_lookup(const kmp_mphf* m, const uint32_t* d_keys, uint64_t n, uint64_t* d_ids, void* stream);
+/* n keys, levels used, total level bits, keys in the fallback table; any pointer may be NULL */
+int kmp_mphf_info(const kmp_mphf* m, uint64_t* n, uint32_t* levels, uint64_t* bits, uint64_t* n_fallback);
+void kmp_mphf_free(kmp_mphf* m);
 
 /* ------------------------------------------------------------------ pairs ---------- */
 /* Fused Graph::new (mod.rs:39-193) + remove_uninteresting_edges (mod.rs:549-697) +

@@ -114,6 +114,23 @@ class Oracle:
         r = L.orc_n_repeat(self._ctx)
         return _view(L.orc_rep_codes(self._ctx), r, np.uint32), _view(L.orc_rep_df(self._ctx), r, np.uint32)
 
+    def hash_order(self):
+        """Per protein, its repeat k-mers in first-occurrence order, duplicates dropped: the codes
+        behind Protein.hash_five_mers (remove_unique_five_mers, protein.rs:151-162, then
+        modify_hash_five_mer, protein.rs:165-174).  CSR (codes, offsets[n+1]); a numpy loop over
+        proteins, for small batches."""
+        codes, woff = self.codes(), self.win_off()
+        rep, _ = self.repeat()
+        keep = np.isin(codes, rep)
+        out, offs = [], [0]
+        for p in range(self.n):
+            c = codes[woff[p]:woff[p + 1]][keep[woff[p]:woff[p + 1]]]
+            _, first = np.unique(c, return_index=True)
+            c = c[np.sort(first)]
+            out.append(c)
+            offs.append(offs[-1] + len(c))
+        return (np.concatenate(out) if out else np.zeros(0, np.uint32)).astype(np.uint32), np.array(offs, np.uint64)
+
     def distinct(self):
         L = lib()
         d = L.orc_n_distinct(self._ctx)

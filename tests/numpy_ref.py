@@ -49,3 +49,27 @@ def pair_weights(res, off, cls, k, require_class_diff=True, min_shared=1):
         "sum_S": int(len(allc)),
     }
     return p[o].astype(np.uint32), q[o].astype(np.uint32), w[o].astype(np.uint32), counters
+
+
+def hash_order(res, off, k):
+    """Literal restatement of main.rs:127-193 for one batch: the df of each k-mer over the
+    per-protein sets, then per protein remove_unique_five_mers (protein.rs:151-162: drop windows
+    whose k-mer has df == 1, order kept) and modify_hash_five_mer (protein.rs:165-174: first
+    occurrence wins).  Returns per-protein lists of codes (ids replaced by their codes) and a
+    {code: df} map of the repeat k-mers (five_mer_hash_freq keyed by code)."""
+    n = len(off) - 1
+    wins = [window_codes(bytes(res[int(off[p]):int(off[p + 1])]), k) for p in range(n)]
+    df = {}
+    for w in wins:
+        for c in set(w.tolist()):
+            df[c] = df.get(c, 0) + 1
+    out = []
+    for w in wins:
+        five_mers = [c for c in w.tolist() if df[c] != 1]
+        seen, hashed = set(), []
+        for c in five_mers:
+            if c not in seen:
+                seen.add(c)
+                hashed.append(c)
+        out.append(hashed)
+    return out, {c: f for c, f in df.items() if f >= 2}

@@ -104,3 +104,19 @@ def test_min_shared_and_threads_invariance(oracle_mod):
     for a, b in zip(base, multi):
         np.testing.assert_array_equal(a, b)
     assert np.all(base[2] >= 3)
+
+
+@pytest.mark.parametrize("k", [5, 7])
+def test_hash_order_vs_literal(oracle_mod, k):
+    """oracle.hash_order (the codes behind hash_five_mers) and the repeat df against the
+    element-by-element restatement of remove_unique_five_mers + modify_hash_five_mer."""
+    res, off, cls, _ = tiny()
+    sub = slice_proteins(*uniprot()[:3], np.arange(120))
+    for r, o_, c in ((res, off, cls), sub):
+        o = oracle_mod.Oracle(r, o_, c, k=k)
+        codes, offs = o.hash_order()
+        want, rep = numpy_ref.hash_order(r, o_, k)
+        assert offs.tolist() == np.cumsum([0] + [len(x) for x in want]).tolist()
+        assert codes.tolist() == [c for x in want for c in x]
+        rc, rdf = o.repeat()
+        assert dict(zip(rc.tolist(), rdf.tolist())) == rep

@@ -88,6 +88,16 @@ SIGNATURES = {
     "kmp_build_sets": (C.c_int, [P, C.c_int]),
     "kmp_get_set": (C.c_int, [P, C.c_uint32, P, C.c_uint64, U64P]),
     "kmp_counters_get": (C.c_int, [P, P]),
+    "kmp_get_df": (C.c_int, [P, P, C.c_uint64, U64P]),
+    "kmp_get_repeat_codes": (C.c_int, [P, P, C.c_uint64, U64P]),
+    "kmp_get_hash_kmers": (C.c_int, [P, C.c_uint32, P, C.c_uint64, U64P]),
+    "kmp_get_hash_kmers_all": (C.c_int, [P, P, C.c_uint64, P, U64P]),
+    "kmp_repeat_mphf": (C.c_int, [P, C.POINTER(P)]),
+    "kmp_mphf_build": (C.c_int, [P, P, C.c_uint64, C.c_double, C.POINTER(P)]),
+    "kmp_mphf_lookup": (C.c_int, [P, P, C.c_uint64, P]),
+    "kmp_mphf_dev_lookup": (C.c_int, [P, P, C.c_uint64, P, P]),
+    "kmp_mphf_info": (C.c_int, [P, U64P, C.POINTER(C.c_uint32), U64P, U64P]),
+    "kmp_mphf_free": (None, [P]),
     "kmp_pairs": (C.c_int, [P, P, C.POINTER(P)]),
     "kmp_edges_count": (C.c_int, [P, U64P]),
     "kmp_edges_get": (C.c_int, [P, P, P, P, P, C.c_uint64, U64P]),

@@ -15,6 +15,7 @@
 #include "kmerpair.h"
 #include "kmp_df.hpp"
 #include "kmp_internal.hpp"
+#include "kmp_mphf.hpp"
 
 using namespace kmp;
 
@@ -42,6 +43,11 @@ struct DevBuf {
     }
     template <class T>
     T* as() const { return static_cast<T*>(p); }
+    void adopt(void* q, size_t b) {  // take ownership of a hipMalloc'd buffer
+        release();
+        p = q;
+        bytes = q ? b : 0;
+    }
 };
 
 }  // namespace
@@ -71,7 +77,27 @@ struct kmp_ctx {
     DevBuf items, dense_off, dense, long_ids, ep, eq, ew, ecount, sort_tmp;
     uint64_t edge_cap = 0;
     kmp_postings* postings = nullptr;
-    ~kmp_ctx() { kmp_postings_destroy(postings); }
+
+    // repeat index of the current sets (kmp_get_df …): MPHF over the df >= 2 codes
+    bool rep_index = false, hash_kmers = false;
+    kmp_mphf* rep_mphf = nullptr;
+    uint64_t n_repeat = 0;
+    DevBuf code_by_id, df_by_id, hk_ids;
+    std::vector<uint64_t> h_hk_off;
+    void drop_repeat_index() {
+        kmp_mphf_free(rep_mphf);
+        rep_mphf = nullptr;
+        rep_index = hash_kmers = false;
+        n_repeat = 0;
+        code_by_id.release();
+        df_by_id.release();
+        hk_ids.release();
+        h_hk_off.clear();
+    }
+    ~kmp_ctx() {
+        kmp_postings_destroy(postings);
+        kmp_mphf_free(rep_mphf);
+    }
 };
 
 struct kmp_edges {
@@ -156,6 +182,60 @@ int finish_edges(kmp_ctx* c, const kmp_pair_opts& o, uint64_t count, bool needs_
     return KMP_OK;
 }
 
+
+// the repeat MPHF and code/df by id (main.rs:127-149,187-193), from a df pass that keeps its runs
+int ensure_repeat_index(kmp_ctx* c) {
+    if (c->rep_index) return KMP_OK;
+    DfCounters dc{};
+    uint32_t *uniq = nullptr, *counts = nullptr;
+    KMP_TRY(c, device_df_counters(c->set.as<uint32_t>(), c->h_set_len.data(), c->h_off.data(), c->off.as<uint64_t>(),
+                                  c->n, c->k_sets, c->stream, &dc, c->err, &uniq, &counts));
+    kmp_mphf* m = nullptr;
+    uint32_t *cb = nullptr, *db = nullptr;
+    uint64_t R = 0;
+    const int rc = repeat_mphf_build(uniq, counts, dc.distinct, 3.0, c->stream, &m, &cb, &db, &R);
+    if (uniq) (void)hipFree(uniq);
+    if (counts) (void)hipFree(counts);
+    if (rc != KMP_OK) return fail(c, rc, "repeat MPHF build: %s", kmp_status_string(rc));
+    c->rep_mphf = m;
+    c->n_repeat = R;
+    c->code_by_id.adopt(cb, R * 4);
+    c->df_by_id.adopt(db, R * 4);
+    c->rep_index = true;
+    return KMP_OK;
+}
+
+int ensure_hash_kmers(kmp_ctx* c) {
+    KMP_TRY(c, ensure_repeat_index(c));
+    if (c->hash_kmers) return KMP_OK;
+    uint32_t* ids = nullptr;
+    const int rc = hash_kmers_device(c->rep_mphf, c->res.as<uint8_t>(), c->off.as<uint64_t>(), c->h_off.data(), c->n,
+                                     c->k_sets, c->code_by_id.as<uint32_t>(), c->n_repeat, c->stream, &ids, c->h_hk_off);
+    if (rc != KMP_OK) return fail(c, rc, "hash k-mers: %s", kmp_status_string(rc));
+    c->hk_ids.adopt(ids, c->h_hk_off.back() * 4);
+    c->hash_kmers = true;
+    return KMP_OK;
+}
+
+// copy `total` u32 from device to a caller buffer with the cap / EOVERFLOW convention
+int copy_out_u32(kmp_ctx* c, const uint32_t* src, uint64_t total, uint32_t* out, uint64_t cap, uint64_t* n) {
+    *n = total;
+    if (cap < total) return KMP_EOVERFLOW;
+    if (total == 0) return KMP_OK;
+    if (!out) return fail(c, KMP_EINVAL, "out is NULL");
+    KMP_HIP(c, hipMemcpyAsync(out, src, total * 4, hipMemcpyDeviceToHost, c->stream));
+    KMP_HIP(c, hipStreamSynchronize(c->stream));
+    return KMP_OK;
+}
+
+int repeat_prologue(kmp_ctx* c, const void* n) {
+    if (!c || !n) return KMP_EINVAL;
+    c->err.clear();
+    if (!c->k_sets) return fail(c, KMP_ESTATE, "kmp_build_sets first");
+    KMP_TRY(c, use_device(c));
+    return KMP_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -228,6 +308,7 @@ int kmp_load_proteins(kmp_ctx* c, const uint8_t* residues, const uint64_t* offse
     KMP_TRY(c, use_device(c));
     c->loaded = false;
     c->k_codes = c->k_sets = 0;
+    c->drop_repeat_index();
     c->n = n;
     c->total_res = total;
     c->h_off.resize(n + 1);
@@ -290,6 +371,7 @@ int kmp_build_sets(kmp_ctx* c, int k) {
     if (k < 1 || k > kMaxK) return fail(c, KMP_EINVAL, "k must be in 1..7, got %d", k);
     KMP_TRY(c, use_device(c));
     c->k_sets = 0;
+    c->drop_repeat_index();
     const uint64_t capacity = kmp_set_capacity(c->n, c->total_res);
     const uint64_t words = kmp_dev_repeat_bitmap_words(k);
     KMP_HIP(c, c->set.reserve(capacity * sizeof(uint32_t)));
@@ -353,6 +435,55 @@ int kmp_get_set(kmp_ctx* c, uint32_t p, uint32_t* out, uint64_t cap, uint64_t* n
 int kmp_counters_get(kmp_ctx* c, kmp_counters* out) {
     if (!c || !out) return KMP_EINVAL;
     *out = c->counters;
+    return KMP_OK;
+}
+
+int kmp_get_df(kmp_ctx* c, uint32_t* df_by_id, uint64_t cap, uint64_t* n) {
+    KMP_TRY(c, repeat_prologue(c, n));
+    KMP_TRY(c, ensure_repeat_index(c));
+    return copy_out_u32(c, c->df_by_id.as<uint32_t>(), c->n_repeat, df_by_id, cap, n);
+}
+
+int kmp_get_repeat_codes(kmp_ctx* c, uint32_t* code_by_id, uint64_t cap, uint64_t* n) {
+    KMP_TRY(c, repeat_prologue(c, n));
+    KMP_TRY(c, ensure_repeat_index(c));
+    return copy_out_u32(c, c->code_by_id.as<uint32_t>(), c->n_repeat, code_by_id, cap, n);
+}
+
+int kmp_get_hash_kmers(kmp_ctx* c, uint32_t p, uint32_t* ids, uint64_t cap, uint64_t* n) {
+    KMP_TRY(c, repeat_prologue(c, n));
+    if (p >= c->n) return fail(c, KMP_EINVAL, "protein %u out of range", p);
+    KMP_TRY(c, ensure_hash_kmers(c));
+    const uint64_t b = c->h_hk_off[p];
+    return copy_out_u32(c, c->hk_ids.as<uint32_t>() + b, c->h_hk_off[p + 1] - b, ids, cap, n);
+}
+
+int kmp_get_hash_kmers_all(kmp_ctx* c, uint32_t* ids, uint64_t cap, uint64_t* offsets, uint64_t* n) {
+    KMP_TRY(c, repeat_prologue(c, n));
+    KMP_TRY(c, ensure_hash_kmers(c));
+    if (offsets) std::copy(c->h_hk_off.begin(), c->h_hk_off.end(), offsets);
+    return copy_out_u32(c, c->hk_ids.as<uint32_t>(), c->h_hk_off.back(), ids, cap, n);
+}
+
+int kmp_repeat_mphf(kmp_ctx* c, const kmp_mphf** out) {
+    KMP_TRY(c, repeat_prologue(c, out));
+    KMP_TRY(c, ensure_repeat_index(c));
+    *out = c->rep_mphf;
+    return KMP_OK;
+}
+
+int kmp_mphf_build(kmp_ctx* c, const uint32_t* keys, uint64_t n, double gamma, kmp_mphf** out) {
+    if (!c || !out) return KMP_EINVAL;
+    c->err.clear();
+    *out = nullptr;
+    if (n && !keys) return fail(c, KMP_EINVAL, "keys is NULL");
+    KMP_TRY(c, use_device(c));
+    DevBuf d;
+    KMP_HIP(c, d.reserve(n * 4));
+    if (n) KMP_HIP(c, hipMemcpyAsync(d.p, keys, n * 4, hipMemcpyHostToDevice, c->stream));
+    const int rc = mphf_build_device(d.as<uint32_t>(), n, gamma, c->stream, out);
+    if (rc == KMP_EINVAL) return fail(c, rc, "MPHF build: gamma must be in [1, 100] and keys distinct");
+    if (rc != KMP_OK) return fail(c, rc, "MPHF build: %s", kmp_status_string(rc));
     return KMP_OK;
 }
 

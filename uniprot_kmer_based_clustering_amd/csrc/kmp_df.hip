@@ -55,7 +55,14 @@ unsigned bits_for(uint64_t v) {
 struct Scratch {
     std::vector<void*> ptrs;
     ~Scratch() {
-        for (void* p : ptrs) (void)hipFree(p);
+        for (void* p : ptrs)
+            if (p) (void)hipFree(p);
+    }
+    template <class T>
+    T* release(T* p) {  // hand one buffer to the caller
+        for (auto& q : ptrs)
+            if (q == p) q = nullptr;
+        return p;
     }
     template <class T>
     hipError_t alloc(T** p, size_t bytes) {
@@ -71,9 +78,11 @@ struct Scratch {
 
 int device_df_counters(const uint32_t* d_set, const uint32_t* h_set_len, const uint64_t* h_off,
                        const uint64_t* d_res_off, uint32_t n, int k, hipStream_t st, DfCounters* out,
-                       std::string& err) {
+                       std::string& err, uint32_t** keep_uniq, uint32_t** keep_counts) {
     (void)h_off;
     *out = DfCounters{};
+    if (keep_uniq) *keep_uniq = nullptr;
+    if (keep_counts) *keep_counts = nullptr;
     if (n == 0) return KMP_OK;
     std::vector<uint64_t> dofs(n + 1, 0);
     for (uint32_t p = 0; p < n; ++p) dofs[p + 1] = dofs[p] + h_set_len[p];
@@ -126,6 +135,8 @@ int device_df_counters(const uint32_t* d_set, const uint32_t* h_set_len, const u
     out->repeat = h_acc[0];
     out->sum_cdf2 = h_acc[1];
     out->max_df = h_acc[2];
+    if (keep_uniq) *keep_uniq = sc.release(uniq);
+    if (keep_counts) *keep_counts = sc.release(counts);
     return KMP_OK;
 }
 

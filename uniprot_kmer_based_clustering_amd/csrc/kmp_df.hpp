@@ -13,9 +13,11 @@ struct DfCounters {
 };
 
 // d_set: per-protein sorted distinct codes in set_base slots; h_set_len/h_off: host copies
-// of the set lengths and residue offsets; d_res_off: device residue offsets.
+// of the set lengths and residue offsets; d_res_off: device residue offsets.  With keep_uniq /
+// keep_counts the distinct codes (ascending) and their df (out->distinct entries each) are handed
+// to the caller (hipFree); they stay null when there are no set entries.
 int device_df_counters(const uint32_t* d_set, const uint32_t* h_set_len, const uint64_t* h_off,
                        const uint64_t* d_res_off, uint32_t n, int k, hipStream_t stream, DfCounters* out,
-                       std::string& err);
+                       std::string& err, uint32_t** keep_uniq = nullptr, uint32_t** keep_counts = nullptr);
 
 }  // namespace kmp

@@ -149,6 +149,53 @@ class KmerPairEngine:
     def get_set(self, p: int) -> np.ndarray:
         return self._get(lib().kmp_get_set, "kmp_get_set", p)
 
+    # ---- repeat index (main.rs:127-149,187-193; protein.rs:151-174) ----
+    def _get_all(self, fn, name):
+        n = C.c_uint64()
+        st = fn(self._ctx, None, 0, C.byref(n))
+        if st not in (_lib.KMP_OK, _lib.KMP_EOVERFLOW):
+            self._check(st, name)
+        out = np.zeros(n.value, dtype=np.uint32)
+        self._check(fn(self._ctx, _ptr(out), n.value, C.byref(n)), name)
+        return out
+
+    def get_df(self) -> np.ndarray:
+        """five_mer_hash_freq: df of each repeat k-mer, indexed by its repeat-MPHF id."""
+        return self._get_all(lib().kmp_get_df, "kmp_get_df")
+
+    def get_repeat_codes(self) -> np.ndarray:
+        """code of each repeat-MPHF id (the inverse of Mphf::hash over the repeat k-mers)."""
+        return self._get_all(lib().kmp_get_repeat_codes, "kmp_get_repeat_codes")
+
+    def get_hash_kmers(self, p: int) -> np.ndarray:
+        """Protein.hash_five_mers (get_five_hash, protein.rs:146): repeat ids, first occurrence."""
+        return self._get(lib().kmp_get_hash_kmers, "kmp_get_hash_kmers", p)
+
+    def get_hash_kmers_all(self) -> tuple[np.ndarray, np.ndarray]:
+        """hash_five_mers of every protein as CSR (ids, offsets[n+1])."""
+        n = C.c_uint64()
+        off = np.zeros(self.n + 1, dtype=np.uint64)
+        st = lib().kmp_get_hash_kmers_all(self._ctx, None, 0, _ptr(off), C.byref(n))
+        if st not in (_lib.KMP_OK, _lib.KMP_EOVERFLOW):
+            self._check(st, "kmp_get_hash_kmers_all")
+        ids = np.zeros(n.value, dtype=np.uint32)
+        self._check(lib().kmp_get_hash_kmers_all(self._ctx, _ptr(ids), n.value, _ptr(off), C.byref(n)),
+                    "kmp_get_hash_kmers_all")
+        return ids, off
+
+    def repeat_mphf(self) -> "Mphf":
+        """The context's repeat-k-mer MPHF (valid until the next load / build_sets)."""
+        m = C.c_void_p()
+        self._check(lib().kmp_repeat_mphf(self._ctx, C.byref(m)), "kmp_repeat_mphf")
+        return Mphf(m, owner=self)
+
+    def mphf(self, keys, gamma: float = 3.0) -> "Mphf":
+        """Mphf::new(gamma, &keys) on this context's device."""
+        k = np.ascontiguousarray(keys, dtype=np.uint32)
+        m = C.c_void_p()
+        self._check(lib().kmp_mphf_build(self._ctx, _ptr(k), len(k), gamma, C.byref(m)), "kmp_mphf_build")
+        return Mphf(m)
+
     def counters(self) -> dict:
         c = _lib.Counters()
         self._check(lib().kmp_counters_get(self._ctx, C.byref(c)), "kmp_counters_get")
@@ -172,3 +219,45 @@ class KmerPairEngine:
         finally:
             lib().kmp_edges_free(e)
         return Edges(p, q, w, s)
+
+
+class Mphf:
+    """boomphf ``Mphf<u32>`` surface over the device MPHF (include/kmerpair.h "MPHF").
+    ``owner`` set: a context-owned MPHF (kmp_repeat_mphf), never freed here."""
+
+    def __init__(self, handle: C.c_void_p, owner=None):
+        self._m = handle
+        self._owner = owner
+
+    def hash(self, keys) -> np.ndarray:
+        k = np.ascontiguousarray(np.atleast_1d(keys), dtype=np.uint32)
+        ids = np.zeros(len(k), dtype=np.uint64)
+        check(lib().kmp_mphf_lookup(self._m, _ptr(k), len(k), _ptr(ids)), "kmp_mphf_lookup")
+        return ids
+
+    def dev_hash(self, keys, stream=None):
+        """ids (int64 torch tensor) of a uint32-valued device tensor, on ``stream``."""
+        import torch
+        k = keys.contiguous()
+        ids = torch.empty(k.numel(), dtype=torch.int64, device=k.device)
+        s = stream if stream is not None else torch.cuda.current_stream(k.device)
+        check(lib().kmp_mphf_dev_lookup(self._m, C.c_void_p(k.data_ptr()), k.numel(),
+                                        C.c_void_p(ids.data_ptr()), C.c_void_p(s.cuda_stream)),
+              "kmp_mphf_dev_lookup")
+        return ids
+
+    def info(self) -> dict:
+        n, lv, bits, fb = C.c_uint64(), C.c_uint32(), C.c_uint64(), C.c_uint64()
+        check(lib().kmp_mphf_info(self._m, C.byref(n), C.byref(lv), C.byref(bits), C.byref(fb)), "kmp_mphf_info")
+        return {"n": n.value, "levels": lv.value, "bits": bits.value, "fallback": fb.value}
+
+    def close(self):
+        if self._m and self._owner is None:
+            lib().kmp_mphf_free(self._m)
+        self._m = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
