@@ -166,6 +166,42 @@ int kmp_edges_get(const kmp_edges* e, uint32_t* p, uint32_t* q, uint32_t* w, flo
                   uint64_t cap, uint64_t* n);
 void kmp_edges_free(kmp_edges* e);
 
+/* ------------------------------------------------------------------ edge k-mers ---- */
+/* The shared k-mers behind each edge's w: KmerEdge::get_kmers (edge.rs:119-124), i.e. the
+ * KmerEdgeGroup.kmers that combine_edges concatenates (mod.rs:415-417; edge.rs:67-81).
+ * kmp_edges_kmers computes them on the device from the context's current sets (the
+ * kmp_build_sets the edges came from; KMP_EINVAL if an edge's intersection is not w long) and
+ * attaches them to e:
+ *   KMP_KMERS_CODES: radix-21 codes, ascending;
+ *   KMP_KMERS_IDS: repeat-MPHF ids (kmp_get_df's id space), ascending as in the reference; also
+ *     sets each edge's reference key, its index in the reference's final edge list, ordered by
+ *     (min shared id, p, q) (combine_edges with one thread).
+ * kmp_edges_get_kmers: CSR, edge i owns kmers[offsets[i] .. offsets[i+1]) (offsets: count+1,
+ * may be NULL); kmp_edges_reference_keys: count keys (IDS lists only, else KMP_ESTATE). */
+enum { KMP_KMERS_CODES = 0, KMP_KMERS_IDS = 1 };
+int kmp_edges_kmers(kmp_ctx* ctx, kmp_edges* e, int space);
+int kmp_edges_get_kmers(const kmp_edges* e, uint64_t* offsets, uint32_t* kmers, uint64_t cap, uint64_t* n);
+int kmp_edges_reference_keys(const kmp_edges* e, uint64_t* keys, uint64_t cap, uint64_t* n);
+
+/* ------------------------------------------------------------------ outputs -------- */
+/* align_and_output_pairs' files (mod.rs:195-319, the diamond runs out of scope): for every edge
+ * with w > threshold (mod.rs:242; reference 10), out_dir/fasta_files/{edge_key}_{prefix}.fasta
+ * for p then q, each ">{id}\n{seq}" with no trailing newline (mod.rs:253-261,273-280), where
+ * prefix = id.split_once('|').0 and edge_key is the reference key with IDS lists, the edge index
+ * otherwise; out_dir/db_files/ (empty, for diamond makedb) and out_dir/blastp_output.tsv holding
+ * the header line of mod.rs:304.  out_dir NULL: ".".  Existing directories are reused, not
+ * removed (the reference runs `rm -r` first).  residues/offsets[n+1]: the loaded batch; ids:
+ * NUL-separated record ids (kmp_read_fasta).  An id without '|' is KMP_EINVAL (the reference
+ * panics).  threads: writer threads.  *n_written: candidate edges. */
+int kmp_write_candidates(const kmp_edges* e, const uint8_t* residues, const uint64_t* offsets, uint32_t n,
+                         const char* ids, uint64_t ids_bytes, uint32_t threshold, const char* out_dir, int threads,
+                         uint64_t* n_written);
+/* `println!("Graph right now:\n{graph:#?}")` (main.rs:234; Debug of Graph, KmerEdge, ProteinVertex:
+ * mod.rs:700-708, edge.rs:158-174, vertex.rs:159-165): edges in reference order as "Single Kmer"
+ * (w == 1) / "Kmer Group" with their MPHF ids, then n "Protein { key, size = degree }".  Needs
+ * IDS lists.  path NULL or "-": stdout. */
+int kmp_write_graph_debug(const kmp_edges* e, uint32_t n, const char* path, int threads);
+
 /* ------------------------------------------------------------------ device stages -- */
 /* Device layout.  Every per-protein u32 array (window codes, K(p), repeat-filtered K(p))
  * lives in one buffer of kmp_set_capacity(N, ΣL) elements; protein p owns the 16-B

@@ -18,6 +18,7 @@ KMP_OK, KMP_EINVAL, KMP_ENOMEM, KMP_EDEVICE, KMP_ERCCL, KMP_EOVERFLOW, KMP_ESTAT
 KMP_LEN_NORMAL300, KMP_LEN_LOGUNIFORM = 0, 1
 KMP_SCORE_COUNT, KMP_SCORE_JACCARD = 0, 1
 KMP_ENGINE_AUTO, KMP_ENGINE_POSTINGS, KMP_ENGINE_TILES, KMP_ENGINE_RESIDUES = 0, 1, 2, 3
+KMP_KMERS_CODES, KMP_KMERS_IDS = 0, 1
 KMP_LDS_SORT_MAX = 4096
 
 
@@ -93,6 +94,11 @@ SIGNATURES = {
     "kmp_get_hash_kmers": (C.c_int, [P, C.c_uint32, P, C.c_uint64, U64P]),
     "kmp_get_hash_kmers_all": (C.c_int, [P, P, C.c_uint64, P, U64P]),
     "kmp_repeat_mphf": (C.c_int, [P, C.POINTER(P)]),
+    "kmp_edges_kmers": (C.c_int, [P, P, C.c_int]),
+    "kmp_edges_get_kmers": (C.c_int, [P, P, P, C.c_uint64, U64P]),
+    "kmp_edges_reference_keys": (C.c_int, [P, P, C.c_uint64, U64P]),
+    "kmp_write_candidates": (C.c_int, [P, P, P, C.c_uint32, P, C.c_uint64, C.c_uint32, C.c_char_p, C.c_int, U64P]),
+    "kmp_write_graph_debug": (C.c_int, [P, C.c_uint32, C.c_char_p, C.c_int]),
     "kmp_mphf_build": (C.c_int, [P, P, C.c_uint64, C.c_double, C.POINTER(P)]),
     "kmp_mphf_lookup": (C.c_int, [P, P, C.c_uint64, P]),
     "kmp_mphf_dev_lookup": (C.c_int, [P, P, C.c_uint64, P, P]),

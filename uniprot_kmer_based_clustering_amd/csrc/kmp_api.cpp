@@ -14,6 +14,7 @@
 
 #include "kmerpair.h"
 #include "kmp_df.hpp"
+#include "kmp_edges.hpp"
 #include "kmp_internal.hpp"
 #include "kmp_mphf.hpp"
 
@@ -100,10 +101,6 @@ struct kmp_ctx {
     }
 };
 
-struct kmp_edges {
-    std::vector<uint32_t> p, q, w;
-    std::vector<float> score;
-};
 
 namespace {
 
@@ -605,6 +602,78 @@ int kmp_edges_get(const kmp_edges* e, uint32_t* p, uint32_t* q, uint32_t* w, flo
     if (q) std::copy(e->q.begin(), e->q.end(), q);
     if (w) std::copy(e->w.begin(), e->w.end(), w);
     if (score) std::copy(e->score.begin(), e->score.end(), score);
+    return KMP_OK;
+}
+
+int kmp_edges_kmers(kmp_ctx* c, kmp_edges* e, int space) {
+    if (!c || !e) return KMP_EINVAL;
+    c->err.clear();
+    if (space != KMP_KMERS_CODES && space != KMP_KMERS_IDS) return fail(c, KMP_EINVAL, "space must be CODES or IDS");
+    if (!c->k_sets) return fail(c, KMP_ESTATE, "kmp_build_sets first");
+    KMP_TRY(c, use_device(c));
+    const uint64_t count = e->p.size();
+    std::vector<uint64_t> kofs(count + 1, 0);
+    for (uint64_t i = 0; i < count; ++i) {
+        if (e->p[i] >= c->n || e->q[i] >= c->n) return fail(c, KMP_EINVAL, "edge %llu names a protein out of range",
+                                                             (unsigned long long)i);
+        kofs[i + 1] = kofs[i] + e->w[i];
+    }
+    const uint64_t total = kofs[count];
+    if (space == KMP_KMERS_IDS) KMP_TRY(c, ensure_repeat_index(c));
+    DevBuf dp, dq, dk, dout, dref;
+    KMP_HIP(c, dp.reserve(count * 4));
+    KMP_HIP(c, dq.reserve(count * 4));
+    KMP_HIP(c, dk.reserve((count + 1) * 8));
+    KMP_HIP(c, dout.reserve(total * 4));
+    if (space == KMP_KMERS_IDS) KMP_HIP(c, dref.reserve(count * 8));
+    if (count) {
+        KMP_HIP(c, hipMemcpyAsync(dp.p, e->p.data(), count * 4, hipMemcpyHostToDevice, c->stream));
+        KMP_HIP(c, hipMemcpyAsync(dq.p, e->q.data(), count * 4, hipMemcpyHostToDevice, c->stream));
+    }
+    KMP_HIP(c, hipMemcpyAsync(dk.p, kofs.data(), (count + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    int rc = edge_kmers_device(c->rep.as<uint32_t>(), c->rep_len.as<uint32_t>(), c->off.as<uint64_t>(), dp.as<uint32_t>(),
+                               dq.as<uint32_t>(), dk.as<uint64_t>(), count, dout.as<uint32_t>(), c->stream);
+    if (rc == KMP_EINVAL) return fail(c, rc, "edge weights do not match the context's sets (edges of another build?)");
+    if (rc != KMP_OK) return fail(c, rc, "edge k-mers: %s", kmp_status_string(rc));
+    if (space == KMP_KMERS_IDS) {
+        rc = edge_kmers_to_ids(c->rep_mphf, dk.as<uint64_t>(), count, total, dout.as<uint32_t>(), dref.as<uint64_t>(),
+                               c->stream);
+        if (rc != KMP_OK) return fail(c, rc, "edge k-mer ids: %s", kmp_status_string(rc));
+    }
+    std::vector<uint32_t> kmers(total);
+    std::vector<uint64_t> ref(space == KMP_KMERS_IDS ? count : 0);
+    if (total) KMP_HIP(c, hipMemcpyAsync(kmers.data(), dout.p, total * 4, hipMemcpyDeviceToHost, c->stream));
+    if (!ref.empty()) KMP_HIP(c, hipMemcpyAsync(ref.data(), dref.p, count * 8, hipMemcpyDeviceToHost, c->stream));
+    KMP_HIP(c, hipStreamSynchronize(c->stream));
+    e->kofs.swap(kofs);
+    e->kmers.swap(kmers);
+    e->ref_key.swap(ref);
+    e->kspace = space;
+    return KMP_OK;
+}
+
+int kmp_edges_get_kmers(const kmp_edges* e, uint64_t* offsets, uint32_t* kmers, uint64_t cap, uint64_t* n) {
+    if (!e || !n) return KMP_EINVAL;
+    if (e->kspace < 0) return KMP_ESTATE;
+    *n = e->kmers.size();
+    if (offsets) std::copy(e->kofs.begin(), e->kofs.end(), offsets);
+    if (cap < e->kmers.size()) return KMP_EOVERFLOW;
+    if (!e->kmers.empty()) {
+        if (!kmers) return KMP_EINVAL;
+        std::copy(e->kmers.begin(), e->kmers.end(), kmers);
+    }
+    return KMP_OK;
+}
+
+int kmp_edges_reference_keys(const kmp_edges* e, uint64_t* keys, uint64_t cap, uint64_t* n) {
+    if (!e || !n) return KMP_EINVAL;
+    if (e->kspace != KMP_KMERS_IDS) return KMP_ESTATE;
+    *n = e->ref_key.size();
+    if (cap < e->ref_key.size()) return KMP_EOVERFLOW;
+    if (!e->ref_key.empty()) {
+        if (!keys) return KMP_EINVAL;
+        std::copy(e->ref_key.begin(), e->ref_key.end(), keys);
+    }
     return KMP_OK;
 }
 

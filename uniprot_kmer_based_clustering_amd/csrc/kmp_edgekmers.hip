@@ -1,0 +1,183 @@
+// kmp_edgekmers.hip — the shared k-mers of every emitted edge: the
+// KmerEdgeGroup.kmers list (edge.rs:48-81; concatenated in ascending key order by combine_edges,
+// mod.rs:415-417) that the postings engine reduces to its length w.
+//   edge_kmers_device: one wavefront per edge intersects the repeat-filtered sets of p and q
+//     (every shared k-mer is a repeat k-mer, main.rs:127-162): each lane takes one code of the
+//     shorter set, binary-searches the longer one, and a ballot + popcount places the hits, so
+//     the list comes out ascending.  The output range of edge i is kofs[i] .. kofs[i+1]
+//     (exclusive scan of w), and a length other than w flags the edge list as foreign.
+//   edge_kmers_to_ids: codes -> repeat-MPHF ids, ascending within each edge (one 64-bit sort of
+//     (edge, id)), and each edge's rank in the reference's final edge order, ascending
+//     (min shared id, p, q) (combine_edges with one thread).
+#include <hip/hip_runtime.h>
+
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include <algorithm>
+
+#include "kmerpair.h"
+#include "kmp_internal.hpp"
+#include "kmp_mphf.hpp"
+
+namespace kmp {
+namespace {
+
+constexpr uint32_t kWaves = 4;  // wavefronts (edges in flight) per 256-thread block
+
+__global__ __launch_bounds__(256) void edge_kmers_kernel(const uint32_t* __restrict__ rep,
+                                                         const uint32_t* __restrict__ rep_len,
+                                                         const uint64_t* __restrict__ off,
+                                                         const uint32_t* __restrict__ ep, const uint32_t* __restrict__ eq,
+                                                         const uint64_t* __restrict__ kofs, uint64_t count,
+                                                         uint32_t* __restrict__ out, unsigned int* __restrict__ bad) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t below = (1ull << lane) - 1;
+    for (uint64_t e = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); e < count; e += (uint64_t)gridDim.x * kWaves) {
+        const uint32_t a = ep[e], b = eq[e];
+        const uint32_t* A = rep + set_base(off[a], a);
+        const uint32_t* B = rep + set_base(off[b], b);
+        uint32_t la = rep_len[a], lb = rep_len[b];
+        if (la > lb) {
+            const uint32_t* t = A;
+            A = B;
+            B = t;
+            const uint32_t u = la;
+            la = lb;
+            lb = u;
+        }
+        const uint64_t o = kofs[e], w = kofs[e + 1] - o;
+        uint64_t wr = 0;
+        for (uint32_t c = 0; c < la; c += 64) {
+            const uint32_t i = c + lane;
+            bool hit = false;
+            uint32_t x = 0;
+            if (i < la) {
+                x = A[i];
+                uint32_t lo = 0, hi = lb;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (B[mid] < x) lo = mid + 1;
+                    else hi = mid;
+                }
+                hit = lo < lb && B[lo] == x;
+            }
+            const uint64_t mask = __ballot(hit);
+            if (hit) {
+                const uint64_t pos = wr + __popcll(mask & below);
+                if (pos < w) out[o + pos] = x;
+            }
+            wr += __popcll(mask);
+        }
+        if (lane == 0 && wr != w) atomicOr(bad, 1u);
+    }
+}
+
+// (edge, id) keys: the edge owning entry j is the largest e with kofs[e] <= j
+__global__ void edge_id_keys_kernel(const uint64_t* __restrict__ ids, uint64_t total, const uint64_t* __restrict__ kofs,
+                                    uint64_t count, unsigned long long* __restrict__ keys) {
+    for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < total; j += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t lo = 0, hi = count;
+        while (hi - lo > 1) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (kofs[mid] <= j) lo = mid;
+            else hi = mid;
+        }
+        keys[j] = (unsigned long long)lo << 32 | (ids[j] & 0xFFFFFFFFull);
+    }
+}
+
+__global__ void low_words_kernel(const unsigned long long* __restrict__ keys, uint64_t total, uint32_t* __restrict__ out) {
+    for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < total; j += (uint64_t)gridDim.x * blockDim.x)
+        out[j] = (uint32_t)keys[j];
+}
+
+// (min shared id, edge index): edges are in (p, q) order, so the index breaks ties as (p, q) does
+__global__ void min_id_keys_kernel(const uint32_t* __restrict__ ids, const uint64_t* __restrict__ kofs, uint64_t count,
+                                   unsigned long long* __restrict__ keys) {
+    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < count; e += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned long long m = kofs[e + 1] > kofs[e] ? ids[kofs[e]] : 0xFFFFFFFFull;
+        keys[e] = m << 32 | e;
+    }
+}
+
+__global__ void rank_scatter_kernel(const unsigned long long* __restrict__ sorted, uint64_t count,
+                                    uint64_t* __restrict__ ref_key) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < count; i += (uint64_t)gridDim.x * blockDim.x)
+        ref_key[sorted[i] & 0xFFFFFFFFull] = i;
+}
+
+inline uint32_t grid_for(uint64_t m) { return (uint32_t)std::min<uint64_t>((m + 255) / 256, 65536); }
+
+template <class T>
+hipError_t dmalloc(T** p, size_t n) {
+    return hipMalloc(reinterpret_cast<void**>(p), std::max<size_t>(1, n) * sizeof(T));
+}
+
+}  // namespace
+
+int edge_kmers_device(const uint32_t* d_rep, const uint32_t* d_rep_len, const uint64_t* d_off, const uint32_t* d_p,
+                      const uint32_t* d_q, const uint64_t* d_kofs, uint64_t count, uint32_t* d_out, hipStream_t st) {
+    if (count == 0) return KMP_OK;
+    unsigned int* bad = nullptr;
+    if (dmalloc(&bad, 1) != hipSuccess) return KMP_ENOMEM;
+    int rc = KMP_OK;
+    unsigned int h_bad = 0;
+    if (hipMemsetAsync(bad, 0, 4, st) != hipSuccess) rc = KMP_EDEVICE;
+    if (rc == KMP_OK) {
+        const uint32_t blocks = (uint32_t)std::min<uint64_t>((count + kWaves - 1) / kWaves, 1u << 20);
+        edge_kmers_kernel<<<blocks, 256, 0, st>>>(d_rep, d_rep_len, d_off, d_p, d_q, d_kofs, count, d_out, bad);
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpyAsync(&h_bad, bad, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            rc = KMP_EDEVICE;
+    }
+    (void)hipFree(bad);
+    if (rc == KMP_OK && h_bad) rc = KMP_EINVAL;  // w does not match the sets: edges of another build
+    return rc;
+}
+
+int edge_kmers_to_ids(const kmp_mphf* m, const uint64_t* d_kofs, uint64_t count, uint64_t total, uint32_t* d_inout,
+                      uint64_t* d_ref_key, hipStream_t st) {
+    if (count == 0) return KMP_OK;
+    if (count >= 0xFFFFFFFFull) return KMP_EINVAL;  // edge index must fit the high key half
+    uint64_t* ids = nullptr;
+    unsigned long long *ka = nullptr, *kb = nullptr;
+    void* scratch = nullptr;
+    const uint64_t nk = std::max(total, count);
+    auto done = [&](int r) {
+        for (void* q : {(void*)ids, (void*)ka, (void*)kb, scratch})
+            if (q) (void)hipFree(q);
+        return r;
+    };
+#define EB(x)                                                                          \
+    do {                                                                               \
+        hipError_t e_ = (x);                                                           \
+        if (e_ != hipSuccess) return done(e_ == hipErrorOutOfMemory ? KMP_ENOMEM : KMP_EDEVICE); \
+    } while (0)
+    EB(dmalloc(&ids, total));
+    EB(dmalloc(&ka, nk));
+    EB(dmalloc(&kb, nk));
+    size_t need = 0;
+    EB(rocprim::radix_sort_keys(nullptr, need, ka, kb, (size_t)nk, 0u, 64u, st));
+    EB(hipMalloc(&scratch, std::max<size_t>(need, 16)));
+    if (total) {
+        const int rc = mphf_lookup_device(m, d_inout, total, ids, st);
+        if (rc != KMP_OK) return done(rc);
+        edge_id_keys_kernel<<<grid_for(total), 256, 0, st>>>(ids, total, d_kofs, count, ka);
+        size_t n1 = need;
+        EB(rocprim::radix_sort_keys(scratch, n1, ka, kb, (size_t)total, 0u, 64u, st));
+        low_words_kernel<<<grid_for(total), 256, 0, st>>>(kb, total, d_inout);
+    }
+    if (d_ref_key) {
+        min_id_keys_kernel<<<grid_for(count), 256, 0, st>>>(d_inout, d_kofs, count, ka);
+        size_t n2 = need;
+        EB(rocprim::radix_sort_keys(scratch, n2, ka, kb, (size_t)count, 0u, 64u, st));
+        rank_scatter_kernel<<<grid_for(count), 256, 0, st>>>(kb, count, d_ref_key);
+    }
+    EB(hipGetLastError());
+    EB(hipStreamSynchronize(st));
+#undef EB
+    return done(KMP_OK);
+}
+
+}  // namespace kmp

@@ -28,4 +28,14 @@ int hash_kmers_device(const kmp_mphf* m, const uint8_t* d_res, const uint64_t* d
                       uint32_t n, int k, const uint32_t* d_code_by_id, uint64_t repeat, hipStream_t st,
                       uint32_t** d_ids, std::vector<uint64_t>& h_ids_off);
 
+// shared k-mers of each edge (p[i], q[i]) (kmp_edgekmers.hip): w[i] = kofs[i+1] - kofs[i]
+// ascending codes at out[kofs[i] ..), from the repeat-filtered sets.  KMP_EINVAL when an edge's
+// intersection is not w long (edges of another kmp_build_sets).
+int edge_kmers_device(const uint32_t* d_rep, const uint32_t* d_rep_len, const uint64_t* d_off, const uint32_t* d_p,
+                      const uint32_t* d_q, const uint64_t* d_kofs, uint64_t count, uint32_t* d_out, hipStream_t st);
+// codes -> repeat-MPHF ids in place, ascending within each edge; with d_ref_key, each edge's
+// index in the reference's final order (ascending (min shared id, p, q)).
+int edge_kmers_to_ids(const kmp_mphf* m, const uint64_t* d_kofs, uint64_t count, uint64_t total, uint32_t* d_inout,
+                      uint64_t* d_ref_key, hipStream_t st);
+
 }  // namespace kmp

@@ -201,24 +201,18 @@ class KmerPairEngine:
         self._check(lib().kmp_counters_get(self._ctx, C.byref(c)), "kmp_counters_get")
         return c.as_dict()
 
-    def pairs(self, min_shared=1, require_class_diff=True, align_threshold=10,
-              score=_lib.KMP_SCORE_COUNT, engine=_lib.KMP_ENGINE_AUTO) -> Edges:
+    def edge_set(self, min_shared=1, require_class_diff=True, align_threshold=10,
+                 score=_lib.KMP_SCORE_COUNT, engine=_lib.KMP_ENGINE_AUTO) -> "EdgeSet":
+        """kmp_pairs, keeping the library-owned edge list for the k-mer lists and the writers."""
         o = _lib.PairOpts(min_shared, int(require_class_diff), align_threshold, score, engine)
         e = C.c_void_p()
         self._check(lib().kmp_pairs(self._ctx, C.byref(o), C.byref(e)), "kmp_pairs")
-        try:
-            n = C.c_uint64()
-            check(lib().kmp_edges_count(e, C.byref(n)), "kmp_edges_count")
-            m = n.value
-            p = np.zeros(m, np.uint32)
-            q = np.zeros(m, np.uint32)
-            w = np.zeros(m, np.uint32)
-            s = np.zeros(m, np.float32)
-            check(lib().kmp_edges_get(e, _ptr(p), _ptr(q), _ptr(w), _ptr(s), m, C.byref(n)),
-                  "kmp_edges_get")
-        finally:
-            lib().kmp_edges_free(e)
-        return Edges(p, q, w, s)
+        return EdgeSet(self, e)
+
+    def pairs(self, min_shared=1, require_class_diff=True, align_threshold=10,
+              score=_lib.KMP_SCORE_COUNT, engine=_lib.KMP_ENGINE_AUTO) -> Edges:
+        with self.edge_set(min_shared, require_class_diff, align_threshold, score, engine) as es:
+            return es.get()
 
 
 class Mphf:
@@ -261,3 +255,81 @@ class Mphf:
             self.close()
         except Exception:
             pass
+
+
+class EdgeSet:
+    """A library-owned edge list (kmp_edges) and what the reference derives from its edges:
+    shared k-mer lists (KmerEdge::get_kmers), the reference edge order, the w > 10 candidate
+    files of align_and_output_pairs and the Debug dump of the final graph."""
+
+    def __init__(self, engine: KmerPairEngine, handle: C.c_void_p):
+        self._engine = engine
+        self._e = handle
+
+    def close(self):
+        if self._e:
+            lib().kmp_edges_free(self._e)
+            self._e = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __len__(self):
+        n = C.c_uint64()
+        check(lib().kmp_edges_count(self._e, C.byref(n)), "kmp_edges_count")
+        return n.value
+
+    def get(self) -> Edges:
+        m = len(self)
+        n = C.c_uint64()
+        p, q, w = (np.zeros(m, np.uint32) for _ in range(3))
+        s = np.zeros(m, np.float32)
+        check(lib().kmp_edges_get(self._e, _ptr(p), _ptr(q), _ptr(w), _ptr(s), m, C.byref(n)), "kmp_edges_get")
+        return Edges(p, q, w, s)
+
+    def kmers(self, space: str = "ids") -> tuple[np.ndarray, np.ndarray]:
+        """(kmers, offsets[count+1]): edge i's shared k-mers, ascending MPHF ids or codes."""
+        sp = {"ids": _lib.KMP_KMERS_IDS, "codes": _lib.KMP_KMERS_CODES}[space]
+        self._engine._check(lib().kmp_edges_kmers(self._engine._ctx, self._e, sp), "kmp_edges_kmers")
+        off = np.zeros(len(self) + 1, np.uint64)
+        n = C.c_uint64()
+        st = lib().kmp_edges_get_kmers(self._e, _ptr(off), None, 0, C.byref(n))
+        if st not in (_lib.KMP_OK, _lib.KMP_EOVERFLOW):
+            check(st, "kmp_edges_get_kmers")
+        km = np.zeros(n.value, np.uint32)
+        check(lib().kmp_edges_get_kmers(self._e, _ptr(off), _ptr(km), n.value, C.byref(n)), "kmp_edges_get_kmers")
+        return km, off
+
+    def reference_keys(self) -> np.ndarray:
+        """Each edge's index in the reference's final edge list (needs kmers("ids"))."""
+        m = len(self)
+        out = np.zeros(m, np.uint64)
+        n = C.c_uint64()
+        check(lib().kmp_edges_reference_keys(self._e, _ptr(out), m, C.byref(n)), "kmp_edges_reference_keys")
+        return out
+
+    def write_candidates(self, proteins: Proteins, out_dir: str, threshold: int = 10, threads: int = 4) -> int:
+        """fasta_files/{edge_key}_{prefix}.fasta pairs + blastp_output.tsv header (mod.rs:195-319)."""
+        if proteins.ids is None:
+            raise ValueError("write_candidates needs protein ids (read_fasta)")
+        blob = b"\0".join(i.encode() for i in proteins.ids) + b"\0"
+        buf = np.frombuffer(blob, np.uint8).copy()
+        res = np.ascontiguousarray(proteins.residues, np.uint8)
+        off = np.ascontiguousarray(proteins.offsets, np.uint64)
+        n = C.c_uint64()
+        check(lib().kmp_write_candidates(self._e, _ptr(res), _ptr(off), proteins.n, _ptr(buf), len(blob), threshold,
+                                         out_dir.encode(), threads, C.byref(n)), "kmp_write_candidates")
+        return n.value
+
+    def write_debug(self, path: str, n_proteins: int, threads: int = 4) -> None:
+        """The reference's final `println!("Graph right now:\\n{graph:#?}")` (needs kmers("ids"))."""
+        check(lib().kmp_write_graph_debug(self._e, n_proteins, path.encode(), threads), "kmp_write_graph_debug")
