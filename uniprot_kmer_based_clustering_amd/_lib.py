@@ -11,7 +11,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libkmerpair.so")
+# KMP_LIB: an alternative build of the same library (tools/build_variants.sh A/B timing only)
+LIB_PATH = os.environ.get("KMP_LIB") or os.path.join(HERE, "lib", "libkmerpair.so")
 HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "kmerpair.h")
 
 KMP_OK, KMP_EINVAL, KMP_ENOMEM, KMP_EDEVICE, KMP_ERCCL, KMP_EOVERFLOW, KMP_ESTATE, KMP_EIO = range(8)

@@ -82,7 +82,10 @@ struct Layout {
     unsigned sort_lo, sort_hi;  // radix-sorted bit range
 };
 
-constexpr uint32_t kBucketTarget = 1024;  // mean keys per bucket
+#ifndef KMP_BUCKET_TARGET
+#define KMP_BUCKET_TARGET 1024
+#endif
+constexpr uint32_t kBucketTarget = KMP_BUCKET_TARGET;  // mean keys per bucket
 constexpr uint32_t kHashA = 0x9E3779B1u;  // odd: code -> h(code) is a bijection of u32
 
 Layout make_layout(uint32_t n, int k, uint64_t slots, bool bucketed) {
@@ -439,6 +442,9 @@ __global__ void part_bounds_kernel(const unsigned long long* __restrict__ k, uin
     bounds[j] = lo;
 }
 
+#ifndef KMP_BUCKET_STOP
+#define KMP_BUCKET_STOP 0  // timing ablation only (tools/build_variants.sh): stop after phase 1..5
+#endif
 constexpr uint32_t kHeavySub = 128;  // larger sub-buckets (very frequent k-mers) -> flat layout
 constexpr int kShards = 64;          // output cursors (one per bucket residue mod kShards)
 
@@ -490,7 +496,12 @@ struct PShard {
     unsigned long long* region;         // n_shards * cap, key = p << 32 | q
 };
 
-template <int kCap, int kThreads, int kTabBits, bool kPShard = false>
+// kMerge (bucket field >= kMergeMinBits): one slot word holds h's low 32 - bbits bits and the group
+// count above them (the top bits of h are the bucket, equal for every key), so the table of h
+// and the count table share H, and T shrinks to the per-position array: 18.9 KB of LDS at the
+// small geometry, 8 workgroups (32 waves) per CU instead of 6
+constexpr unsigned kMergeMinBits = 11;
+template <int kCap, int kThreads, int kTabBits, bool kPShard = false, bool kMerge = false>
 __device__ __forceinline__ void process_bucket(
     const uint32_t b, const unsigned long long* __restrict__ sorted, const uint32_t* __restrict__ bstart,
     const Layout& lay, uint32_t n_prot, int require_diff, uint32_t heavy_df, bool small,
@@ -501,8 +512,11 @@ __device__ __forceinline__ void process_bucket(
     constexpr uint32_t kTab = 1u << kTabBits;
     constexpr int kPer = kTab / kThreads;
     static_assert(kE * kThreads == kCap && kPer % 4 == 0 && kTab >= (uint32_t)kCap, "geometry");
-    __shared__ __attribute__((aligned(16))) uint32_t T[kTab];  // A: table of h; C-E: per position start<<8|size
-    __shared__ __attribute__((aligned(16))) uint32_t H[kTab];  // per slot: group size, then start<<8|size
+    static_assert(!kMerge || kCap < (1 << kMergeMinBits) - 1, "merged count field");
+    // T: (unmerged) A: table of h; C-E: per position start<<8|size
+    __shared__ __attribute__((aligned(16))) uint32_t T[kMerge ? kCap : kTab];
+    // H: per slot: (merged: h low bits | count << hb) / group size, then start<<8|size
+    __shared__ __attribute__((aligned(16))) uint32_t H[kTab];
     __shared__ uint32_t Bl[kCap];                              // per position: p << cb | class
     __shared__ uint32_t dupw[kCap / 32];
     __shared__ uint32_t SZ[kHeavySub + 1];
@@ -524,10 +538,13 @@ __device__ __forceinline__ void process_bucket(
     const unsigned hshift = lay.hshift, cb = lay.clsbits;
     const uint32_t lmask = (1u << hshift) - 1, cmask = (1u << cb) - 1;
     const uint32_t empty = ~b << (32 - lay.bbits);  // top bits differ from every h of bucket b
+    const unsigned hb = 32 - lay.bbits;             // merged: low h bits kept in a slot
+    const uint32_t hm = (1u << hb) - 1;
+    constexpr uint32_t kFree = 0xFFFFFFFFu;          // merged empty slot (count field never all ones)
 #pragma unroll
     for (int q = 0; q < kPer; ++q) {
-        T[tid * kPer + q] = empty;
-        H[tid * kPer + q] = 0;
+        if (!kMerge) T[tid * kPer + q] = empty;
+        H[tid * kPer + q] = kMerge ? kFree : 0u;
     }
     for (uint32_t i = tid; i < kCap / 32; i += kThreads) dupw[i] = 0;
     for (uint32_t i = tid; i <= kHeavySub; i += kThreads) SZ[i] = 0;
@@ -545,16 +562,31 @@ __device__ __forceinline__ void process_bucket(
         rk[e] = 0;
         if (i < n) {
             uint32_t slot = (h * 0x85EBCA6Bu) >> (32 - kTabBits);
-            for (;;) {
-                const uint32_t old = atomicCAS(&T[slot], empty, h);
-                if (old == empty || old == h) break;
-                slot = (slot + 1) & (kTab - 1);
+            if (kMerge) {
+                const uint32_t hl = h & hm;
+                for (;;) {
+                    const uint32_t old = atomicCAS(&H[slot], kFree, hl);
+                    if (old == kFree || (old & hm) == hl) break;
+                    slot = (slot + 1) & (kTab - 1);
+                }
+                sl[e] = slot;
+                rk[e] = atomicAdd(&H[slot], 1u << hb) >> hb;
+            } else {
+                for (;;) {
+                    const uint32_t old = atomicCAS(&T[slot], empty, h);
+                    if (old == empty || old == h) break;
+                    slot = (slot + 1) & (kTab - 1);
+                }
+                sl[e] = slot;
+                rk[e] = atomicAdd(&H[slot], 1u);
             }
-            sl[e] = slot;
-            rk[e] = atomicAdd(&H[slot], 1u);
         }
     }
     __syncthreads();
+    if (KMP_BUCKET_STOP == 1) {
+        if (tid == 0 && T[0] == 0xFFFFFFFFu && H[1] == 7u) flags[3] = 1;
+        return;
+    }
     // B. size classes, largest first
     uint32_t c4[kPer], r4[kPer];
     {
@@ -562,6 +594,10 @@ __device__ __forceinline__ void process_bucket(
         for (int q4 = 0; q4 < kPer / 4; ++q4) {
             const uint4 v = reinterpret_cast<const uint4*>(H)[tid * (kPer / 4) + q4];
             c4[4 * q4] = v.x, c4[4 * q4 + 1] = v.y, c4[4 * q4 + 2] = v.z, c4[4 * q4 + 3] = v.w;
+        }
+        if (kMerge) {
+#pragma unroll
+            for (int q = 0; q < kPer; ++q) c4[q] = c4[q] == kFree ? 0u : c4[q] >> hb;
         }
 #pragma unroll
         for (int q = 0; q < kPer; ++q) {
@@ -586,6 +622,10 @@ __device__ __forceinline__ void process_bucket(
     for (int q = 0; q < kPer; ++q)
         H[tid * kPer + q] = c4[q] ? ((SZ[c4[q]] + r4[q] * c4[q]) << 8) | c4[q] : 0u;
     __syncthreads();
+    if (KMP_BUCKET_STOP == 2) {
+        if (tid == 0 && T[0] == 0xFFFFFFFFu && H[1] == 7u) flags[3] = 1;
+        return;
+    }
     // C. scatter (T now holds, per position, its group's start << 8 | size)
 #pragma unroll
     for (int e = 0; e < kE; ++e)
@@ -596,6 +636,10 @@ __device__ __forceinline__ void process_bucket(
             T[pos] = g;
         }
     __syncthreads();
+    if (KMP_BUCKET_STOP == 3) {
+        if (tid == 0 && T[0] == 0xFFFFFFFFu && H[1] == 7u) flags[3] = 1;
+        return;
+    }
     // D. per position: group bounds, duplicate flag (same protein earlier in the group)
     uint32_t s[kE], en[kE];
 #pragma unroll
@@ -615,6 +659,10 @@ __device__ __forceinline__ void process_bucket(
             }
     }
     __syncthreads();
+    if (KMP_BUCKET_STOP == 4) {
+        if (tid == 0 && T[0] == 0xFFFFFFFFu && H[1] == 7u) flags[3] = 1;
+        return;
+    }
     auto is_dup = [&](uint32_t j) { return (dupw[j >> 5] >> (j & 31)) & 1u; };
     // E. df, head, kept-partner count
     uint32_t cnt[kE];
@@ -644,6 +692,10 @@ __device__ __forceinline__ void process_bucket(
         }
         cnt[e] = c;
         mine += c;
+    }
+    if (KMP_BUCKET_STOP == 5) {
+        if (tid == 0 && mine == 0xFFFFFFFFu) flags[3] = 1;
+        return;
     }
     // F. write the pair keys
     if (kPShard) {
@@ -711,14 +763,14 @@ __device__ __forceinline__ void process_bucket(
     }
 }
 
-template <int kCap, int kThreads, int kTabBits, bool kPShard = false>
+template <int kCap, int kThreads, int kTabBits, bool kPShard = false, bool kMerge = false>
 __global__ __launch_bounds__(kThreads) void bucket_small_kernel(
     const unsigned long long* __restrict__ sorted, const uint32_t* __restrict__ bstart, Layout lay,
     uint32_t n_prot, int require_diff, uint32_t heavy_df, unsigned long long* __restrict__ out, uint64_t shard_cap,
     unsigned long long* __restrict__ cursor, unsigned long long* __restrict__ gstats, uint32_t* __restrict__ flags,
     uint32_t* __restrict__ list, uint32_t* __restrict__ list_count, PShard ps, uint32_t b0 = 0) {
     // buckets b0 + blockIdx.x (a multi-GPU rank launches only its bucket range)
-    process_bucket<kCap, kThreads, kTabBits, kPShard>(b0 + blockIdx.x, sorted, bstart, lay, n_prot, require_diff,
+    process_bucket<kCap, kThreads, kTabBits, kPShard, kMerge>(b0 + blockIdx.x, sorted, bstart, lay, n_prot, require_diff,
                                                       heavy_df, true, out, shard_cap, cursor, gstats, flags, list,
                                                       list_count, ps);
 }
@@ -915,8 +967,29 @@ __global__ void gather_shards_kernel(const unsigned long long* __restrict__ src,
 }
 
 // bucket kernels: capacity (keys), threads, log2 of the k-mer table (>= capacity)
-constexpr int kBucketSmallCap = 2048, kBucketSmallThreads = 256, kBucketSmallTab = 11;
+#ifndef KMP_SMALL_GEOM
+#define KMP_SMALL_GEOM 1280, 256, 11
+#endif
+constexpr int kSmallGeom[3] = {KMP_SMALL_GEOM};
+constexpr int kBucketSmallCap = kSmallGeom[0], kBucketSmallThreads = kSmallGeom[1], kBucketSmallTab = kSmallGeom[2];
 constexpr int kBucketLargeCap = 8192, kBucketLargeThreads = 1024, kBucketLargeTab = 13;
+
+// the small bucket kernel for this layout: merged slot words when the bucket field is wide enough
+template <bool kPShard>
+void launch_bucket_small(uint32_t grid, hipStream_t st, const unsigned long long* sorted, const uint32_t* bstart,
+                         const Layout& lay, uint32_t n, int require_diff, uint32_t heavy_df,
+                         unsigned long long* out, uint64_t shard_cap, unsigned long long* cursor,
+                         unsigned long long* gstats, uint32_t* flags, uint32_t* list, uint32_t* list_count,
+                         const PShard& ps, uint32_t b0 = 0) {
+    if (lay.bbits >= kMergeMinBits)
+        bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallTab, kPShard, true>
+            <<<grid, kBucketSmallThreads, 0, st>>>(sorted, bstart, lay, n, require_diff, heavy_df, out, shard_cap,
+                                                   cursor, gstats, flags, list, list_count, ps, b0);
+    else
+        bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallTab, kPShard, false>
+            <<<grid, kBucketSmallThreads, 0, st>>>(sorted, bstart, lay, n, require_diff, heavy_df, out, shard_cap,
+                                                   cursor, gstats, flags, list, list_count, ps, b0);
+}
 
 
 // (pair key, w) runs -> edges with w >= min_shared, canonical order kept
@@ -1132,19 +1205,13 @@ int front_bucketed(kmp_postings* ws, const unsigned long long* in, uint64_t slot
         PG(hipMemsetAsync(gstats, 0, (kShards * 8 + kShards) * sizeof(unsigned long long), st));
         PG(hipMemsetAsync(list_count, 0, sizeof(uint32_t), st));
         if (pshard) {
-            bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallTab, true>
-                <<<nb, kBucketSmallThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
-                                                     ws->inc_sorted.p, ws->shard_cap, cursor, gstats, flags, list,
-                                                     list_count, ps);
+            launch_bucket_small<true>(nb, st, ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df, ws->inc_sorted.p, ws->shard_cap, cursor, gstats, flags, list, list_count, ps);
             bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeTab, true>
                 <<<256, kBucketLargeThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
                                                       ws->inc_sorted.p, ws->shard_cap, cursor, gstats, flags, list,
                                                       list_count, ps);
         } else {
-            bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallTab, false>
-                <<<nb, kBucketSmallThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
-                                                     ws->inc_sorted.p, ws->shard_cap, cursor, gstats, flags, list,
-                                                     list_count, ps);
+            launch_bucket_small<false>(nb, st, ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df, ws->inc_sorted.p, ws->shard_cap, cursor, gstats, flags, list, list_count, ps);
             bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeTab, false>
                 <<<256, kBucketLargeThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
                                                       ws->inc_sorted.p, ws->shard_cap, cursor, gstats, flags, list,
@@ -1300,9 +1367,7 @@ int run_bucketed_fused(kmp_postings* ws, uint64_t slots, const Layout& lay, uint
         PG(ws->w.reserve(total));
         PG(hipMemsetAsync(gstats, 0, (kShards * 8 + kShards) * sizeof(unsigned long long), st));
         PG(hipMemsetAsync(list_count, 0, sizeof(uint32_t), st));
-        bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallTab, false>
-            <<<nb, kBucketSmallThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
-                                                 ws->inc_sorted.p, sc, cursor, gstats, flags, list, list_count, ps);
+        launch_bucket_small<false>(nb, st, ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df, ws->inc_sorted.p, sc, cursor, gstats, flags, list, list_count, ps);
         bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeTab, false>
             <<<256, kBucketLargeThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
                                                   ws->inc_sorted.p, sc, cursor, gstats, flags, list, list_count, ps);
@@ -1875,10 +1940,7 @@ int kmp_dev_pairs_route(kmp_postings* ws, const unsigned long long* d_keys, uint
     const uint32_t b0 = (uint32_t)(((uint64_t)part * nb + parts - 1) / parts);
     const uint32_t b1 = (uint32_t)(((uint64_t)(part + 1) * nb + parts - 1) / parts);
     if (b1 > b0)
-        bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallTab, false>
-            <<<b1 - b0, kBucketSmallThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
-                                                      ws->inc_sorted.p, shard_cap, cursor, gstats, ws->flags.p, list,
-                                                      list_count, ps, b0);
+        launch_bucket_small<false>(b1 - b0, st, ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df, ws->inc_sorted.p, shard_cap, cursor, gstats, ws->flags.p, list, list_count, ps, b0);
     bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeTab, false>
         <<<256, kBucketLargeThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
                                               ws->inc_sorted.p, shard_cap, cursor, gstats, ws->flags.p, list,
