@@ -14,4 +14,5 @@ for spec in "$@"; do
   name=${spec%%:*}
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../build_variants/libkmerpair_$name.so $OBJS ../../build_variants/kmp_postings_$name.o
 done
+rm -f ../../build_variants/*.o
 ls ../../build_variants/*.so

@@ -442,6 +442,9 @@ __global__ void part_bounds_kernel(const unsigned long long* __restrict__ k, uin
     bounds[j] = lo;
 }
 
+#ifndef KMP_F_EARLY
+#define KMP_F_EARLY 1
+#endif
 #ifndef KMP_BUCKET_STOP
 #define KMP_BUCKET_STOP 0  // timing ablation only (tools/build_variants.sh): stop after phase 1..5
 #endif
@@ -588,7 +591,7 @@ __device__ __forceinline__ void process_bucket(
         return;
     }
     // B. size classes, largest first
-    uint32_t c4[kPer], r4[kPer];
+    uint32_t c4[kPer], r4[kPer], single = 0;
     {
 #pragma unroll
         for (int q4 = 0; q4 < kPer / 4; ++q4) {
@@ -599,10 +602,13 @@ __device__ __forceinline__ void process_bucket(
 #pragma unroll
             for (int q = 0; q < kPer; ++q) c4[q] = c4[q] == kFree ? 0u : c4[q] >> hb;
         }
+        // singleton groups (one key: most groups) only count toward sum_S / distinct; they take
+        // no size-class rank and no position
 #pragma unroll
         for (int q = 0; q < kPer; ++q) {
             if (c4[q] > kHeavySub) heavy = 1;
-            r4[q] = c4[q] && c4[q] <= kHeavySub ? atomicAdd(&SZ[c4[q]], 1u) : 0u;
+            single += c4[q] == 1;
+            r4[q] = c4[q] >= 2 && c4[q] <= kHeavySub ? atomicAdd(&SZ[c4[q]], 1u) : 0u;
         }
     }
     __syncthreads();
@@ -610,17 +616,19 @@ __device__ __forceinline__ void process_bucket(
         if (tid == 0) flags[0] = 1;
         return;
     }
+    uint32_t nm;  // keys in groups of two or more: positions [0, nm)
     {
-        const uint32_t m = tid <= (int)kHeavySub ? kHeavySub - tid : 0;  // size class of this thread
-        const uint32_t v = tid <= (int)kHeavySub ? m * SZ[m] : 0u;
-        uint32_t excl, total;
-        block_scan_n<kThreads>(v, excl, total, wave_tot);
-        if (tid <= (int)kHeavySub) SZ[m] = excl;  // first position of size class m
+        const bool cls = tid + 2 <= (int)kHeavySub;                       // classes kHeavySub .. 2
+        const uint32_t m = cls ? kHeavySub - tid : 0;
+        const uint32_t v = cls ? m * SZ[m] : 0u;
+        uint32_t excl;
+        block_scan_n<kThreads>(v, excl, nm, wave_tot);
+        if (cls) SZ[m] = excl;  // first position of size class m
     }
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < kPer; ++q)
-        H[tid * kPer + q] = c4[q] ? ((SZ[c4[q]] + r4[q] * c4[q]) << 8) | c4[q] : 0u;
+        H[tid * kPer + q] = c4[q] >= 2 ? ((SZ[c4[q]] + r4[q] * c4[q]) << 8) | c4[q] : c4[q];  // singleton: 1
     __syncthreads();
     if (KMP_BUCKET_STOP == 2) {
         if (tid == 0 && T[0] == 0xFFFFFFFFu && H[1] == 7u) flags[3] = 1;
@@ -631,6 +639,7 @@ __device__ __forceinline__ void process_bucket(
     for (int e = 0; e < kE; ++e)
         if (tid + e * kThreads < n) {
             const uint32_t g = H[sl[e]];
+            if ((g & 255u) < 2) continue;  // singleton
             const uint32_t pos = (g >> 8) + rk[e];
             Bl[pos] = xl[e];
             T[pos] = g;
@@ -646,7 +655,7 @@ __device__ __forceinline__ void process_bucket(
     for (int e = 0; e < kE; ++e) {
         const uint32_t i = tid + e * kThreads;
         s[e] = en[e] = 0;
-        if (i >= n) continue;
+        if (i >= nm) continue;
         const uint32_t g = T[i];
         s[e] = g >> 8;
         en[e] = s[e] + (g & 255u);
@@ -666,12 +675,13 @@ __device__ __forceinline__ void process_bucket(
     auto is_dup = [&](uint32_t j) { return (dupw[j >> 5] >> (j & 31)) & 1u; };
     // E. df, head, kept-partner count
     uint32_t cnt[kE];
-    uint32_t st_sum = 0, st_dist = 0, st_rep = 0, st_cdf2 = 0, st_max = 0, st_heavy = 0, mine = 0;
+    uint32_t st_sum = single, st_dist = single, st_rep = 0, st_cdf2 = 0, st_max = single ? 1u : 0u, st_heavy = 0,
+             mine = 0;
 #pragma unroll
     for (int e = 0; e < kE; ++e) {
         const uint32_t i = tid + e * kThreads;
         cnt[e] = 0;
-        if (i >= n || is_dup(i)) continue;
+        if (i >= nm || is_dup(i)) continue;
         uint32_t f = 1, c = 0;
         if (en[e] - s[e] > 1) {
             f = 0;
@@ -697,6 +707,29 @@ __device__ __forceinline__ void process_bucket(
         if (tid == 0 && mine == 0xFFFFFFFFu) flags[3] = 1;
         return;
     }
+    // statistics (u32 per workgroup; the bucket is at most kCap keys): wave partials -> red, then
+    // kStN threads sum them and post one (sharded) atomic each
+    auto wave_stats = [&]() {
+        uint32_t sv[kStN] = {st_sum, st_dist, st_rep, st_cdf2, st_max, st_heavy, mine};
+#pragma unroll
+        for (int t = 0; t < kStN; ++t) {
+            uint32_t v = sv[t];
+            for (int sh = 32; sh > 0; sh >>= 1) {
+                const uint32_t u = __shfl_down(v, sh);
+                v = t == kStMaxDf ? max(u, v) : u + v;
+            }
+            if ((tid & 63) == 0) red[tid >> 6][t] = v;
+        }
+    };
+    auto post_stats = [&]() {
+        if (tid < kStN) {
+            uint32_t v = red[0][tid];
+            for (int w = 1; w < kThreads / 64; ++w) v = tid == kStMaxDf ? max(v, red[w][tid]) : v + red[w][tid];
+            unsigned long long* g = gstats + (uint64_t)(b % kShards) * 8 + tid;  // sharded: no hot word
+            if (tid == kStMaxDf) atomicMax(g, (unsigned long long)v);
+            else if (v) atomicAdd(g, (unsigned long long)v);
+        }
+    };
     // F. write the pair keys
     if (kPShard) {
         if (mine) {
@@ -718,10 +751,15 @@ __device__ __forceinline__ void process_bucket(
             }
         }
     } else {
+        // KMP_F_EARLY: the statistics ride on the scan's barriers, and the output reservation is made
+        // by the last wave while wave 0 posts them
+        if (KMP_F_EARLY) wave_stats();
         uint32_t excl, total;
         block_scan_n<kThreads>(mine, excl, total, wave_tot);
         const uint32_t shard = b % kShards;
-        if (tid == 0) sbase = total ? atomicAdd(&cursor[shard], (unsigned long long)total) : 0ull;
+        constexpr int kRes = KMP_F_EARLY ? kThreads - 64 : 0;
+        if (tid == kRes) sbase = total ? atomicAdd(&cursor[shard], (unsigned long long)total) : 0ull;
+        if (KMP_F_EARLY) post_stats();
         __syncthreads();
         if (mine) {
             unsigned long long pos = sbase + excl;
@@ -742,25 +780,10 @@ __device__ __forceinline__ void process_bucket(
             }
         }
     }
-    // statistics (u32 per workgroup; the bucket is at most kCap keys)
-    uint32_t sv[kStN] = {st_sum, st_dist, st_rep, st_cdf2, st_max, st_heavy, mine};
-#pragma unroll
-    for (int t = 0; t < kStN; ++t) {
-        uint32_t v = sv[t];
-        for (int sh = 32; sh > 0; sh >>= 1) {
-            const uint32_t u = __shfl_down(v, sh);
-            v = t == kStMaxDf ? max(u, v) : u + v;
-        }
-        if ((tid & 63) == 0) red[tid >> 6][t] = v;
-    }
+    if (!kPShard && KMP_F_EARLY) return;  // statistics already posted
+    wave_stats();
     __syncthreads();
-    if (tid < kStN) {
-        uint32_t v = red[0][tid];
-        for (int w = 1; w < kThreads / 64; ++w) v = tid == kStMaxDf ? max(v, red[w][tid]) : v + red[w][tid];
-        unsigned long long* g = gstats + (uint64_t)(b % kShards) * 8 + tid;  // sharded: no hot word
-        if (tid == kStMaxDf) atomicMax(g, (unsigned long long)v);
-        else if (v) atomicAdd(g, (unsigned long long)v);
-    }
+    post_stats();
 }
 
 template <int kCap, int kThreads, int kTabBits, bool kPShard = false, bool kMerge = false>
