@@ -61,6 +61,14 @@ inline uint32_t route_blocks(uint64_t cap) { return (uint32_t)std::min<uint64_t>
 // and size, so every sort here uses it.
 using SortCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
                                            rocprim::default_config, 0>;
+// Pair keys (p * N + q, 34 bits at N = 100k): 9-bit digits in 1024 x 8 workgroups take 4 onesweep
+// passes instead of 5 (tools/radix_bits_bench.hip: 0.209 vs 0.269 ms for 5.4 M keys); 10-bit
+// digits are slower and 11 bits exceed the LDS.  Merge-sort limit 0, as for SortCfg.
+using PairSortCfg = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<512, 12>, rocprim::kernel_config<1024, 8>, 9,
+                                        rocprim::block_radix_rank_algorithm::match>,
+    0>;
 constexpr unsigned kClsBits = 16;
 
 // Two key layouts (u64, kNoKey = all ones is the padding of every layout):
@@ -1398,13 +1406,13 @@ int run_bucketed_fused(kmp_postings* ws, uint64_t slots, const Layout& lay, uint
         pad_shards_kernel<<<dim3(route_blocks(sc), kShards), 256, 0, st>>>(ws->inc_sorted.p, sc, cursor);
         ws->mark(4, st);
         size_t t2 = 0, t3 = 0;
-        PG(rocprim::radix_sort_keys<SortCfg>(nullptr, t2, ws->inc_sorted.p, ws->inc.p, (size_t)total, 0u, pair_bits,
+        PG(rocprim::radix_sort_keys<PairSortCfg>(nullptr, t2, ws->inc_sorted.p, ws->inc.p, (size_t)total, 0u, pair_bits,
                                              st));
         PG(rocprim::run_length_encode(nullptr, t3, ws->inc.p, (unsigned int)total, ws->uniq.p, ws->w.p,
                                       ws->small.p + 1, st));
         PG(ws->tmp.reserve(std::max({t2, t3, ws->tmp.n})));
-        PG(rocprim::radix_sort_keys<SortCfg>(ws->tmp.p, t2, ws->inc_sorted.p, ws->inc.p, (size_t)total, 0u,
-                                             pair_bits, st));
+        PG(rocprim::radix_sort_keys<PairSortCfg>(ws->tmp.p, t2, ws->inc_sorted.p, ws->inc.p, (size_t)total, 0u,
+                                                 pair_bits, st));
         ws->mark(5, st);
         PG(rocprim::run_length_encode(ws->tmp.p, t3, ws->inc.p, (unsigned int)total, ws->uniq.p, ws->w.p,
                                       ws->small.p + 1, st));
@@ -1463,14 +1471,14 @@ int tail(kmp_postings* ws, const unsigned long long* in, unsigned long long n_in
         PG(ws->pos.reserve(n_inc));
     }
     size_t t2 = 0, t3 = 0, t4 = 0;
-    PG(rocprim::radix_sort_keys<SortCfg>(nullptr, t2, in, ws->inc_sorted.p, (size_t)n_inc, 0u, pair_bits, st));
+    PG(rocprim::radix_sort_keys<PairSortCfg>(nullptr, t2, in, ws->inc_sorted.p, (size_t)n_inc, 0u, pair_bits, st));
     PG(rocprim::run_length_encode(nullptr, t3, ws->inc_sorted.p, (unsigned int)n_inc, ws->uniq.p, ws->w.p,
                                   ws->small.p + 1, st));
     if (filter_w)
         PG(rocprim::exclusive_scan(nullptr, t4, ws->keep.p, ws->pos.p, 0u, (size_t)n_inc, rocprim::plus<uint32_t>(),
                                    st));
     PG(ws->tmp.reserve(std::max({t2, t3, t4, ws->tmp.n})));
-    PG(rocprim::radix_sort_keys<SortCfg>(ws->tmp.p, t2, in, ws->inc_sorted.p, (size_t)n_inc, 0u, pair_bits, st));
+    PG(rocprim::radix_sort_keys<PairSortCfg>(ws->tmp.p, t2, in, ws->inc_sorted.p, (size_t)n_inc, 0u, pair_bits, st));
     ws->mark(5, st);
     PG(rocprim::run_length_encode(ws->tmp.p, t3, ws->inc_sorted.p, (unsigned int)n_inc, ws->uniq.p, ws->w.p,
                                   ws->small.p + 1, st));
@@ -1723,9 +1731,9 @@ int kmp_dev_pairs_keys(kmp_postings* ws, const unsigned long long* d_keys, uint6
     if (ni > out_cap || !d_out) return KMP_EOVERFLOW;
     const unsigned pair_bits = bits_for((uint64_t)n * n);
     size_t t2 = 0;
-    PG(rocprim::radix_sort_keys<SortCfg>(nullptr, t2, ws->inc.p, d_out, (size_t)ni, 0u, pair_bits, st));
+    PG(rocprim::radix_sort_keys<PairSortCfg>(nullptr, t2, ws->inc.p, d_out, (size_t)ni, 0u, pair_bits, st));
     PG(ws->tmp.reserve(std::max(t2, ws->tmp.n)));
-    PG(rocprim::radix_sort_keys<SortCfg>(ws->tmp.p, t2, ws->inc.p, d_out, (size_t)ni, 0u, pair_bits, st));
+    PG(rocprim::radix_sort_keys<PairSortCfg>(ws->tmp.p, t2, ws->inc.p, d_out, (size_t)ni, 0u, pair_bits, st));
     return part_bounds(ws, d_out, ni, 0, n, n, parts, part_counts, st);
 }
 
@@ -1882,14 +1890,19 @@ __global__ void run_count_kernel(const unsigned long long* __restrict__ uniq, co
     *count = u && uniq[u - 1] == kNoKey ? u - 1 : u;
 }
 
+}  // extern "C"
+
+template <class Cfg = SortCfg>
 static int sort_keys(kmp_postings* ws, const unsigned long long* in, unsigned long long* out, uint64_t m,
                      unsigned lo, unsigned hi, hipStream_t st) {
     size_t t = 0;
-    PG(rocprim::radix_sort_keys<SortCfg>(nullptr, t, in, out, (size_t)m, lo, hi, st));
+    PG(rocprim::radix_sort_keys<Cfg>(nullptr, t, in, out, (size_t)m, lo, hi, st));
     PG(ws->tmp.reserve(std::max(t, ws->tmp.n)));
-    PG(rocprim::radix_sort_keys<SortCfg>(ws->tmp.p, t, in, out, (size_t)m, lo, hi, st));
+    PG(rocprim::radix_sort_keys<Cfg>(ws->tmp.p, t, in, out, (size_t)m, lo, hi, st));
     return KMP_OK;
 }
+
+extern "C" {
 
 int kmp_dev_keys_route(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
                        uint32_t n, int k, uint64_t slots, uint32_t lo, uint32_t hi, uint64_t slot_lo, uint64_t slot_hi,
@@ -1995,7 +2008,7 @@ int kmp_dev_edges_route(kmp_postings* ws, const unsigned long long* d_pk, uint64
     PG(ws->w.reserve(m));
     PG(ws->small.reserve(16));
     const unsigned pair_bits = bits_for((uint64_t)n * n);
-    int rc = sort_keys(ws, d_pk, ws->inc_sorted.p, m, 0, pair_bits, st);
+    int rc = sort_keys<PairSortCfg>(ws, d_pk, ws->inc_sorted.p, m, 0, pair_bits, st);
     if (rc != KMP_OK) return rc;
     size_t t3 = 0;
     PG(rocprim::run_length_encode(nullptr, t3, ws->inc_sorted.p, (unsigned int)m, ws->uniq.p, ws->w.p,
