@@ -186,7 +186,7 @@ __global__ __launch_bounds__(kKeyThreads) void residue_keys_chunk_kernel(
     int k, uint32_t p_hi, uint64_t slot_begin, uint64_t slot_end, const uint32_t* __restrict__ chunk_first,
     Layout lay, unsigned long long* __restrict__ keys, uint32_t* __restrict__ flags) {
     __shared__ uint8_t lut[256];
-    __shared__ uint8_t rc[kKeyResMax];
+    __shared__ __attribute__((aligned(16))) uint8_t rc[kKeyResMax + 32];  // residue codes from a0 = r0 & ~15
     __shared__ uint32_t pb[kKeyProtMax + 1];   // region start of each protein, relative to c0 (may wrap)
     __shared__ int32_t pr[kKeyProtMax];        // LDS index of the protein's residue 0 (may be < 0)
     __shared__ uint32_t pw[kKeyProtMax];       // window count
@@ -223,8 +223,36 @@ __global__ __launch_bounds__(kKeyThreads) void residue_keys_chunk_kernel(
     __syncthreads();
     const uint32_t np = s_np;
     const uint64_t r0 = s_r0, r1 = max(s_r0, s_r1);
-    for (uint64_t i = r0 + tid; i < r1; i += kKeyThreads) rc[i - r0] = lut[res[i]];
-    for (uint32_t t = tid; t < np; t += kKeyThreads) pr[t] = (int32_t)((int64_t)res_off[first + t] - (int64_t)r0);
+    // stage the span with independent 16-byte loads (byte loads where a vector would pass the end
+    // of the range's residues or the base is unaligned), recoded through the LUT, one 16-byte LDS
+    // store per vector
+    const uint64_t a0 = r0 & ~15ull, res_end = res_off[p_hi];
+    const bool vec_ok = ((uintptr_t)res & 15u) == 0;
+    const uint32_t nv = (uint32_t)((r1 - a0 + 15) >> 4);
+    for (uint32_t v = tid; v < nv; v += kKeyThreads) {
+        const uint64_t g = a0 + 16ull * v;
+        uint32_t w[4];
+        if (vec_ok && g + 16 <= res_end) {
+            const uint4 q = *reinterpret_cast<const uint4*>(res + g);
+            w[0] = q.x, w[1] = q.y, w[2] = q.z, w[3] = q.w;
+        } else {
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                w[d] = 0;
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const uint64_t i = g + 4 * d + b;
+                    w[d] |= (uint32_t)(i < res_end ? res[i] : 0) << (8 * b);
+                }
+            }
+        }
+        auto code4 = [&](uint32_t x) {
+            return (uint32_t)lut[x & 255u] | (uint32_t)lut[(x >> 8) & 255u] << 8 |
+                   (uint32_t)lut[(x >> 16) & 255u] << 16 | (uint32_t)lut[x >> 24] << 24;
+        };
+        *reinterpret_cast<uint4*>(rc + 16 * v) = make_uint4(code4(w[0]), code4(w[1]), code4(w[2]), code4(w[3]));
+    }
+    for (uint32_t t = tid; t < np; t += kKeyThreads) pr[t] = (int32_t)((int64_t)res_off[first + t] - (int64_t)a0);
     __syncthreads();
     for (uint32_t i = tid; i < (uint32_t)(c1 - c0); i += kKeyThreads) {
         unsigned long long x = kNoKey;
