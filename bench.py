@@ -137,11 +137,11 @@ def main():
             return distributed_step(pipe, rank, world, engine=args.engine)
         return pipe.step(engine=args.engine)
 
-    for _ in range(args.warmup):
-        one_step()
     stage_sum = None
     if postings and world == 1:
-        pipe.set_stage_timing(True)
+        pipe.set_stage_timing(True)  # before the warm-up: the timed steps replay the same graph
+    for _ in range(args.warmup):
+        one_step()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

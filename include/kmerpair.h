@@ -335,6 +335,15 @@ int kmp_postings_set_timing(kmp_postings* ws, int enable);
 int kmp_postings_set_layout(kmp_postings* ws, int bucketed);
 int kmp_postings_last_layout(const kmp_postings* ws);
 int kmp_postings_set_pshard(kmp_postings* ws, int enable);
+/* Residue entry point, bucketed layout: 1 (default) groups the keys by bucket with a two-level
+ * counting partition computed straight from the residues (no materialised keys, no radix sort);
+ * 0 writes every key and radix-sorts the bucket field.  Same edges either way. */
+int kmp_postings_set_partition(kmp_postings* ws, int enable);
+/* Single-synchronisation residue path as a HIP graph (default 1): captured on the second call
+ * with an unchanged shape (pointers, sizes, options, workspace buffers), replayed after that.
+ * kmp_postings_graph_replays: calls served by a replay so far. */
+int kmp_postings_set_graph(kmp_postings* ws, int enable);
+uint64_t kmp_postings_graph_replays(const kmp_postings* ws);
 int kmp_dev_pairs_postings(kmp_postings* ws, const uint32_t* d_set, const uint32_t* d_set_len,
                            const uint64_t* d_res_off, const uint16_t* d_class, uint32_t n, int k, uint64_t slots,
                            uint32_t heavy_df, uint32_t min_shared, int require_class_diff, uint32_t* d_p,

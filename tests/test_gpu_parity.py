@@ -210,6 +210,38 @@ def test_bucketed_small_batches(oracle_mod, n):
         np.testing.assert_array_equal(pipe.edges()[2], w)
 
 
+@pytest.mark.parametrize("partition", [True, False], ids=["partition", "keysort"])
+def test_residue_graph_replay(oracle_mod, partition):
+    """The single-synchronisation residue step replayed from its HIP graph: every replay (stage
+    timing off and on) is bit-exact, for both bucket-grouping front ends; an edge buffer that
+    moves (overflow rerun) forces a new capture and stays exact."""
+    import torch
+    from uniprot_kmer_based_clustering_amd.device import DevicePipeline
+    b = K.synth(20000, 21)
+    p, q, w = oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=7, threads=8).pairs()
+    pipe = DevicePipeline(b, 7, "cuda:0")
+    pipe.set_partition(partition)
+    for timing in (False, True):
+        pipe.set_stage_timing(timing)
+        for _ in range(4):
+            assert pipe.step(engine="residues") == len(p)
+            torch.cuda.synchronize()
+            assert pipe.last_tail() == "fused"
+            ep, eq, ew = pipe.edges()
+            np.testing.assert_array_equal(ep, p)
+            np.testing.assert_array_equal(eq, q)
+            np.testing.assert_array_equal(ew, w)
+    assert pipe.graph_replays() >= 2
+    pipe._alloc_edges(1024)  # too small: EOVERFLOW, new buffers, new shape
+    for _ in range(3):
+        assert pipe.step(engine="residues") == len(p)
+        np.testing.assert_array_equal(pipe.edges()[1], q)
+    pipe.set_graph(False)
+    r = pipe.graph_replays()
+    assert pipe.step(engine="residues") == len(p) and pipe.graph_replays() == r
+    np.testing.assert_array_equal(pipe.edges()[2], w)
+
+
 def test_pshard_long_rows(oracle_mod):
     """One protein sharing a distinct k-mer with each of ~650 others: its row of the p-shard
     reduction is longer than the rank-sort limit, so that range is bitonic-sorted in LDS."""

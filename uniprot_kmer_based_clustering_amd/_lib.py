@@ -132,6 +132,9 @@ SIGNATURES = {
     "kmp_postings_set_layout": (C.c_int, [P, C.c_int]),
     "kmp_postings_last_layout": (C.c_int, [P]),
     "kmp_postings_set_pshard": (C.c_int, [P, C.c_int]),
+    "kmp_postings_set_partition": (C.c_int, [P, C.c_int]),
+    "kmp_postings_set_graph": (C.c_int, [P, C.c_int]),
+    "kmp_postings_graph_replays": (C.c_uint64, [P]),
     "kmp_dev_pairs_residues": (C.c_int, [P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32,
                                          C.c_uint32, C.c_int, P, P, P, C.c_uint64, U64P, P, P]),
     "kmp_dev_keys_part": (C.c_int, [P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32, C.c_uint32,

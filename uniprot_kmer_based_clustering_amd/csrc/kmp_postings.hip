@@ -181,26 +181,30 @@ __global__ void chunk_first_kernel(const uint64_t* __restrict__ res_off, uint32_
     for (uint64_t c = (b + kKeyChunk - 1) / kKeyChunk; c * kKeyChunk < e && c < n_chunks; ++c) first[c] = p;
 }
 
-__global__ __launch_bounds__(kKeyThreads) void residue_keys_chunk_kernel(
-    const uint8_t* __restrict__ res, const uint64_t* __restrict__ res_off, const uint16_t* __restrict__ cls,
-    int k, uint32_t p_hi, uint64_t slot_begin, uint64_t slot_end, const uint32_t* __restrict__ chunk_first,
-    Layout lay, unsigned long long* __restrict__ keys, uint32_t* __restrict__ flags) {
-    __shared__ uint8_t lut[256];
-    __shared__ __attribute__((aligned(16))) uint8_t rc[kKeyResMax + 32];  // residue codes from a0 = r0 & ~15
-    __shared__ uint32_t pb[kKeyProtMax + 1];   // region start of each protein, relative to c0 (may wrap)
-    __shared__ int32_t pr[kKeyProtMax];        // LDS index of the protein's residue 0 (may be < 0)
-    __shared__ uint32_t pw[kKeyProtMax];       // window count
-    __shared__ uint16_t pc[kKeyProtMax];       // class
-    __shared__ uint32_t s_np;
-    __shared__ uint64_t s_r0, s_r1;
+// LDS state of one key chunk: residue codes of the chunk's span and its proteins' geometry
+struct KeyChunk {
+    uint8_t lut[256];
+    __attribute__((aligned(16))) uint8_t rc[kKeyResMax + 32];  // residue codes from a0 = r0 & ~15
+    uint32_t pb[kKeyProtMax + 1];   // region start of each protein, relative to c0 (may wrap)
+    int32_t pr[kKeyProtMax];        // LDS index of the protein's residue 0 (may be < 0)
+    uint32_t pw[kKeyProtMax];       // window count
+    uint16_t pc[kKeyProtMax];       // class
+    uint32_t np;
+    uint64_t r0, r1;
+};
+
+// Stage chunk [c0, c1) of proteins [first, p_hi): the proteins whose regions overlap it and the
+// residue span their windows need, recoded into LDS.  Ends with a barrier.
+__device__ __forceinline__ void key_chunk_load(KeyChunk& s, const uint8_t* __restrict__ res,
+                                               const uint64_t* __restrict__ res_off,
+                                               const uint16_t* __restrict__ cls, int k, uint32_t p_hi,
+                                               uint64_t c0, uint64_t c1, uint32_t first, const Layout& lay,
+                                               uint32_t* __restrict__ flags) {
     const int tid = threadIdx.x;
-    const uint64_t c0 = slot_begin + (uint64_t)blockIdx.x * kKeyChunk;
-    const uint64_t c1 = min(c0 + kKeyChunk, slot_end);
-    const uint32_t first = chunk_first[blockIdx.x];
-    lut[tid] = c_lut.v[tid];
+    s.lut[tid] = c_lut.v[tid];
     if (tid == 0) {
-        s_np = 0;
-        s_r0 = s_r1 = 0;
+        s.np = 0;
+        s.r0 = s.r1 = 0;
     }
     __syncthreads();
     // the chunk's proteins: first + t while its region starts before c1 (one parallel round)
@@ -210,19 +214,19 @@ __global__ __launch_bounds__(kKeyThreads) void residue_keys_chunk_kernel(
         const uint64_t b = set_base(off, p);
         if (b >= c1) break;
         const uint32_t nw = L >= (uint64_t)k ? (uint32_t)(L - k + 1) : 0u;
-        pb[t] = (uint32_t)(b - c0);  // wraps for the first protein when it starts before c0
-        pw[t] = nw;
-        pc[t] = cls[p];
-        check_class(pc[t], lay, flags);
-        atomicMax(&s_np, t + 1);
+        s.pb[t] = (uint32_t)(b - c0);  // wraps for the first protein when it starts before c0
+        s.pw[t] = nw;
+        s.pc[t] = cls[p];
+        check_class(s.pc[t], lay, flags);
+        atomicMax(&s.np, t + 1);
         const uint64_t j0 = c0 > b ? c0 - b : 0;
         const uint64_t j1 = min<uint64_t>(nw, c1 - b);
-        if (t == 0) s_r0 = off + min<uint64_t>(j0, L);
-        if (j1 > j0) atomicMax((unsigned long long*)&s_r1, (unsigned long long)(off + j1 + k - 1));
+        if (t == 0) s.r0 = off + min<uint64_t>(j0, L);
+        if (j1 > j0) atomicMax((unsigned long long*)&s.r1, (unsigned long long)(off + j1 + k - 1));
     }
     __syncthreads();
-    const uint32_t np = s_np;
-    const uint64_t r0 = s_r0, r1 = max(s_r0, s_r1);
+    const uint32_t np = s.np;
+    const uint64_t r0 = s.r0, r1 = max(s.r0, s.r1);
     // stage the span with independent 16-byte loads (byte loads where a vector would pass the end
     // of the range's residues or the base is unaligned), recoded through the LUT, one 16-byte LDS
     // store per vector
@@ -247,33 +251,103 @@ __global__ __launch_bounds__(kKeyThreads) void residue_keys_chunk_kernel(
             }
         }
         auto code4 = [&](uint32_t x) {
-            return (uint32_t)lut[x & 255u] | (uint32_t)lut[(x >> 8) & 255u] << 8 |
-                   (uint32_t)lut[(x >> 16) & 255u] << 16 | (uint32_t)lut[x >> 24] << 24;
+            return (uint32_t)s.lut[x & 255u] | (uint32_t)s.lut[(x >> 8) & 255u] << 8 |
+                   (uint32_t)s.lut[(x >> 16) & 255u] << 16 | (uint32_t)s.lut[x >> 24] << 24;
         };
-        *reinterpret_cast<uint4*>(rc + 16 * v) = make_uint4(code4(w[0]), code4(w[1]), code4(w[2]), code4(w[3]));
+        *reinterpret_cast<uint4*>(s.rc + 16 * v) =
+            make_uint4(code4(w[0]), code4(w[1]), code4(w[2]), code4(w[3]));
     }
-    for (uint32_t t = tid; t < np; t += kKeyThreads) pr[t] = (int32_t)((int64_t)res_off[first + t] - (int64_t)a0);
+    for (uint32_t t = tid; t < np; t += kKeyThreads) s.pr[t] = (int32_t)((int64_t)res_off[first + t] - (int64_t)a0);
     __syncthreads();
-    for (uint32_t i = tid; i < (uint32_t)(c1 - c0); i += kKeyThreads) {
-        unsigned long long x = kNoKey;
-        if (np) {
-            // protein of slot c0 + i: last t with region start <= c0 + i (t = 0 may start before c0)
-            uint32_t a = 0, b = np;
-            while (a + 1 < b) {
-                const uint32_t mid = (a + b) >> 1;
-                if (pb[mid] <= i) a = mid;
-                else b = mid;
-            }
-            const uint32_t j = i - pb[a];  // window index (pb[0] wraps: i - pb[0] = c0 + i - b0)
-            if (j < pw[a]) {
-                const uint8_t* w = rc + (pr[a] + (int32_t)j);
-                uint32_t v = 0;
-                for (int t = 0; t < k; ++t) v = v * kRadix + w[t];
-                x = make_key(v, pc[a], first + a, lay);
+}
+
+// key of chunk slot c0 + i (kNoKey past a protein's windows)
+__device__ __forceinline__ unsigned long long key_chunk_key(const KeyChunk& s, uint32_t i, int k, uint32_t first,
+                                                            const Layout& lay) {
+    const uint32_t np = s.np;
+    if (!np) return kNoKey;
+    // protein of slot c0 + i: last t with region start <= c0 + i (t = 0 may start before c0)
+    uint32_t a = 0, b = np;
+    while (a + 1 < b) {
+        const uint32_t mid = (a + b) >> 1;
+        if (s.pb[mid] <= i) a = mid;
+        else b = mid;
+    }
+    const uint32_t j = i - s.pb[a];  // window index (pb[0] wraps: i - pb[0] = c0 + i - b0)
+    if (j >= s.pw[a]) return kNoKey;
+    const uint8_t* w = s.rc + (s.pr[a] + (int32_t)j);
+    uint32_t v = 0;
+    for (int t = 0; t < k; ++t) v = v * kRadix + w[t];
+    return make_key(v, s.pc[a], first + a, lay);
+}
+
+// The kPer consecutive chunk slots i0 .. i0 + kPer - 1: one binary search, then the protein's
+// state in registers (reloaded at a region start: regions are >= 4 slots, so at most one per
+// slot) and the radix-21 code rolled window to window (two LDS reads instead of k).
+// emit(e, valid, h, lo) per slot: h = h(code), lo = the key's p | class bits; the key is
+// (u64)h << hshift | lo.  pw21 = 21^(k-1).
+template <uint32_t kPer, class Emit>
+__device__ __forceinline__ void key_chunk_run(const KeyChunk& s, uint32_t i0, uint32_t n_slots, int k, uint32_t pw21,
+                                              uint32_t first, const Layout& lay, Emit emit) {
+    const uint32_t np = s.np;
+    if (!np) {
+#pragma unroll
+        for (uint32_t e = 0; e < kPer; ++e) emit(e, false, 0u, 0ull);
+        return;
+    }
+    uint32_t a = 0, b = np;
+    while (a + 1 < b) {
+        const uint32_t mid = (a + b) >> 1;
+        if (s.pb[mid] <= i0) a = mid;
+        else b = mid;
+    }
+    const uint32_t cmask = (1u << lay.clsbits) - 1;
+    uint32_t nxt = a + 1 < np ? s.pb[a + 1] : 0xFFFFFFFFu;  // first slot of protein a + 1
+    uint32_t j = i0 - s.pb[a];                              // window index (pb[0] may wrap)
+    uint32_t nw = s.pw[a];
+    int32_t r = s.pr[a] + (int32_t)j;                       // LDS index of window j's first residue
+    unsigned long long lo = ((unsigned long long)(first + a) << lay.clsbits) | (s.pc[a] & cmask);
+    uint32_t v = 0;
+    bool have = false;  // v holds the code of window j - 1
+#pragma unroll
+    for (uint32_t e = 0; e < kPer; ++e) {
+        const uint32_t i = i0 + e;
+        if (i == nxt) {
+            ++a;
+            nxt = a + 1 < np ? s.pb[a + 1] : 0xFFFFFFFFu;
+            j = 0;
+            nw = s.pw[a];
+            r = s.pr[a];
+            lo = ((unsigned long long)(first + a) << lay.clsbits) | (s.pc[a] & cmask);
+            have = false;
+        }
+        const bool valid = j < nw && i < n_slots;
+        if (valid) {
+            if (have) {
+                v = (v - s.rc[r - 1] * pw21) * kRadix + s.rc[r + k - 1];
+            } else {
+                v = 0;
+                for (int t = 0; t < k; ++t) v = v * kRadix + s.rc[r + t];
             }
         }
-        keys[c0 + i - slot_begin] = x;
+        have = valid;
+        emit(e, valid, v * kHashA, lo);
+        ++j;
+        ++r;
     }
+}
+
+__global__ __launch_bounds__(kKeyThreads) void residue_keys_chunk_kernel(
+    const uint8_t* __restrict__ res, const uint64_t* __restrict__ res_off, const uint16_t* __restrict__ cls,
+    int k, uint32_t p_hi, uint64_t slot_begin, uint64_t slot_end, const uint32_t* __restrict__ chunk_first,
+    Layout lay, unsigned long long* __restrict__ keys, uint32_t* __restrict__ flags) {
+    __shared__ KeyChunk s;
+    const uint64_t c0 = slot_begin + (uint64_t)blockIdx.x * kKeyChunk;
+    const uint64_t c1 = min(c0 + kKeyChunk, slot_end);
+    const uint32_t first = chunk_first[blockIdx.x];
+    key_chunk_load(s, res, res_off, cls, k, p_hi, c0, c1, first, lay, flags);
+    for (uint32_t i = threadIdx.x; i < (uint32_t)(c1 - c0); i += kKeyThreads)
+        keys[c0 + i - slot_begin] = key_chunk_key(s, i, k, first, lay);
 }
 
 enum : int { kStSumS, kStDistinct, kStRepeat, kStCdf2, kStMaxDf, kStHeavy, kStInc, kStN };
@@ -1033,6 +1107,333 @@ constexpr int kSmallGeom[3] = {KMP_SMALL_GEOM};
 constexpr int kBucketSmallCap = kSmallGeom[0], kBucketSmallThreads = kSmallGeom[1], kBucketSmallTab = kSmallGeom[2];
 constexpr int kBucketLargeCap = 8192, kBucketLargeThreads = 1024, kBucketLargeTab = 13;
 
+// ------------------------------------------------------------- bucket partition ------------
+// The residue path groups its keys by bucket (the top bbits of h) with two counting passes
+// instead of materialising every key and radix sorting it (0.09 ms of key writes + 0.46 ms of
+// onesweep at config 3): bucket = digit1 (high d1 bits) : digit2 (low d2 bits).
+//   level 1 (bp_hist1 -> column scan -> bp_scatter1): each 4,096-slot key chunk computes its keys
+//     from the residues twice, once to count them per digit1 and once to write them, ranked in
+//     LDS, as one contiguous run per digit1 at the offset the column scan gave that (digit, chunk);
+//     padding slots are dropped.  Output: keys grouped by digit1 ("coarse bins"), in ws->keys.
+//   level 2 (bp_hist2 -> per-coarse-bin scan -> bp_scatter2): 4,096-key tiles of each coarse bin,
+//     counted and scattered the same way on digit2.  Output: keys grouped by bucket, in
+//     ws->sorted, and bstart[] for the bucket kernels straight from the scan.
+// Order inside a bucket is unspecified (LDS atomics rank the keys); the bucket kernel does not
+// need one.  A coarse bin above its tile budget (a k-mer with ~10^5 copies) raises flags[0], the
+// same fallback as a bucket above the large kernel's capacity.
+constexpr uint32_t kBpTile = 4096;            // level-2 tile (level 1 uses the key chunk, also 4,096)
+constexpr uint32_t kBpPer = kBpTile / kKeyThreads;
+constexpr uint32_t kBpMaxBins = 1024;         // digit widths <= 10 bits
+constexpr uint32_t kBpRowGroup = 64;          // rows per partial sum of the level-1 column scan
+constexpr uint32_t kBpAlign = 16;             // coarse bins start on 128-B lines of the level-1 array
+static_assert(kKeyChunk == kBpTile, "one tile geometry for both levels");
+
+struct BpDigits {
+    unsigned sh1, sh2;   // digit1 = x >> sh1; digit2 = (x >> sh2) & m2
+    uint32_t nb1, nb2, m2;
+};
+
+BpDigits bp_digits(const Layout& lay) {
+    BpDigits d{};
+    const unsigned d2 = lay.bbits / 2, d1 = lay.bbits - d2;
+    d.sh2 = lay.sort_lo;
+    d.sh1 = lay.sort_lo + d2;
+    d.nb1 = 1u << d1;
+    d.nb2 = 1u << d2;
+    d.m2 = d.nb2 - 1;
+    return d;
+}
+
+// exclusive scan of lh[0, nb) in place (nb <= kBpMaxBins, kThreads threads); ends with a barrier
+template <int kThreads = kKeyThreads>
+__device__ __forceinline__ void lds_bins_scan(uint32_t* lh, uint32_t nb, uint32_t* wave_tot) {
+    const uint32_t q = (nb + kThreads - 1) / kThreads, b0 = threadIdx.x * q;
+    uint32_t v = 0;
+    for (uint32_t t = 0; t < q; ++t)
+        if (b0 + t < nb) v += lh[b0 + t];
+    uint32_t excl, total;
+    block_scan_n<kThreads>(v, excl, total, wave_tot);  // barriers inside
+    for (uint32_t t = 0; t < q; ++t)
+        if (b0 + t < nb) {
+            const uint32_t c = lh[b0 + t];
+            lh[b0 + t] = excl;
+            excl += c;
+        }
+    __syncthreads();
+}
+
+// level 1, pass 1: per-chunk digit1 histogram -> H1[chunk][digit]
+__global__ __launch_bounds__(kKeyThreads) void bp_hist1_kernel(
+    const uint8_t* __restrict__ res, const uint64_t* __restrict__ res_off, const uint16_t* __restrict__ cls, int k,
+    uint32_t p_hi, uint64_t slots, const uint32_t* __restrict__ chunk_first, Layout lay, BpDigits dg, uint32_t pw21,
+    uint32_t* __restrict__ H1, uint32_t* __restrict__ flags) {
+    __shared__ KeyChunk s;
+    __shared__ uint32_t lh[kBpMaxBins];
+    const uint64_t c0 = (uint64_t)blockIdx.x * kKeyChunk, c1 = min(c0 + kKeyChunk, slots);
+    for (uint32_t d = threadIdx.x; d < dg.nb1; d += kKeyThreads) lh[d] = 0;
+    const uint32_t first = chunk_first[blockIdx.x];
+    key_chunk_load(s, res, res_off, cls, k, p_hi, c0, c1, first, lay, flags);
+    const unsigned hs1 = dg.sh1 - lay.hshift;  // digit1 = the top d1 bits of h
+    key_chunk_run<kBpPer>(s, threadIdx.x * kBpPer, (uint32_t)(c1 - c0), k, pw21, first, lay,
+                          [&](uint32_t, bool valid, uint32_t h, unsigned long long) {
+                              if (valid) atomicAdd(&lh[h >> hs1], 1u);
+                          });
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < dg.nb1; d += kKeyThreads) H1[(uint64_t)blockIdx.x * dg.nb1 + d] = lh[d];
+}
+
+// level-1 column scan, 1 of 3: R[g][c] = sum of M[r][c] over the kBpRowGroup rows of group g
+__global__ __launch_bounds__(256) void bp_colsum_kernel(const uint32_t* __restrict__ M, uint32_t rows, uint32_t cols,
+                                                        uint32_t* __restrict__ R) {
+    const uint32_t r0 = blockIdx.x * kBpRowGroup, r1 = min(rows, r0 + kBpRowGroup);
+    for (uint32_t c = threadIdx.x; c < cols; c += blockDim.x) {
+        uint32_t v = 0;
+#pragma unroll 8
+        for (uint32_t r = r0; r < r1; ++r) v += M[(uint64_t)r * cols + c];
+        R[(uint64_t)blockIdx.x * cols + c] = v;
+    }
+}
+
+// 2 of 3 (one workgroup): per column an exclusive scan down the groups; the column totals
+// scanned across columns twice: rounded up to kBpAlign keys -> colstart[c] (where column c's run
+// starts in the level-1 array, added to every R[g][c]) and exact -> colstart[cols + 1 + c]
+// (compact starts; [cols] and [2 cols + 1] are the grand totals).
+// cols is a power of two <= 1024; each column's groups are split over 1024 / cols threads.
+constexpr int kColThreads = 1024;
+__global__ __launch_bounds__(kColThreads) void bp_colscan_kernel(uint32_t* __restrict__ R, uint32_t groups,
+                                                                 uint32_t cols, uint32_t* __restrict__ colstart) {
+    __shared__ uint32_t part[kColThreads];
+    __shared__ uint32_t tot[kBpMaxBins], cmp[kBpMaxBins];
+    __shared__ uint32_t wave_tot[kColThreads / 64];
+    const uint32_t splits = max(1u, kColThreads / cols);
+    const uint32_t c = threadIdx.x % cols, sp = threadIdx.x / cols;
+    const bool act = sp < splits;
+    const uint32_t gq = (groups + splits - 1) / splits, g0 = min(groups, sp * gq), g1 = min(groups, g0 + gq);
+    uint32_t v = 0;
+    if (act) {
+#pragma unroll 4
+        for (uint32_t g = g0; g < g1; ++g) v += R[(uint64_t)g * cols + c];
+    }
+    part[threadIdx.x] = v;
+    __syncthreads();
+    uint32_t before = 0;  // this split's offset inside its column
+    if (act) {
+        uint32_t t = 0;
+        for (uint32_t s = 0; s < splits; ++s) {
+            const uint32_t y = part[s * cols + c];
+            before += s < sp ? y : 0u;
+            t += y;
+        }
+        if (sp == 0) {
+            tot[c] = (t + kBpAlign - 1) & ~(kBpAlign - 1);
+            cmp[c] = t;
+        }
+    }
+    __syncthreads();
+    uint32_t last = 0, last_c = 0;
+    if (threadIdx.x == 0) {
+        last = tot[cols - 1];
+        last_c = cmp[cols - 1];
+    }
+    lds_bins_scan<kColThreads>(tot, cols, wave_tot);
+    lds_bins_scan<kColThreads>(cmp, cols, wave_tot);
+    if (act) {
+        if (sp == 0) {
+            colstart[c] = tot[c];
+            colstart[cols + 1 + c] = cmp[c];
+        }
+        uint32_t run = tot[c] + before;
+        for (uint32_t g = g0; g < g1; ++g) {
+            const uint32_t x = R[(uint64_t)g * cols + c];
+            R[(uint64_t)g * cols + c] = run;
+            run += x;
+        }
+    }
+    if (threadIdx.x == 0) {
+        colstart[cols] = tot[cols - 1] + last;
+        colstart[2 * cols + 1] = cmp[cols - 1] + last_c;
+    }
+}
+
+// 3 of 3: P[r][c] = R[group(r)][c] + the rows of the group before r
+__global__ __launch_bounds__(256) void bp_colprefix_kernel(const uint32_t* __restrict__ M, uint32_t rows,
+                                                           uint32_t cols, const uint32_t* __restrict__ R,
+                                                           uint32_t* __restrict__ P) {
+    const uint32_t r0 = blockIdx.x * kBpRowGroup, r1 = min(rows, r0 + kBpRowGroup);
+    for (uint32_t c = threadIdx.x; c < cols; c += blockDim.x) {
+        uint32_t run = R[(uint64_t)blockIdx.x * cols + c];
+        for (uint32_t r = r0; r < r1; ++r) {
+            P[(uint64_t)r * cols + c] = run;
+            run += M[(uint64_t)r * cols + c];
+        }
+    }
+}
+
+// rank every key of the workgroup's tile by digit in LDS (x[e] = element tid + e*kKeyThreads),
+// place the tile digit-major into S and write each digit's run at base[digit] (global offset of
+// the tile's run, from the scan).  lh holds the tile histogram on entry (zeroed, then counted by
+// the caller's ranks); shared by both scatter levels.
+template <class Digit>
+__device__ __forceinline__ void bp_place(const unsigned long long (&x)[kBpPer], const uint32_t (&r)[kBpPer],
+                                         uint32_t n_in, uint32_t nb, Digit digit, uint32_t* lh, uint32_t* wave_tot,
+                                         unsigned long long* S, const uint32_t* __restrict__ prow,
+                                         unsigned long long* __restrict__ out) {
+    lds_bins_scan(lh, nb, wave_tot);
+#pragma unroll
+    for (uint32_t e = 0; e < kBpPer; ++e)
+        if (x[e] != kNoKey) S[lh[digit(x[e])] + r[e]] = x[e];
+    __syncthreads();
+    // lh[d] -> global base of the digit's run minus its tile start: out[lh[d] + i] for S[i]
+    for (uint32_t d = threadIdx.x; d < nb; d += kKeyThreads) lh[d] = prow[d] - lh[d];
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n_in; i += kKeyThreads) {
+        const unsigned long long y = S[i];
+        out[lh[digit(y)] + i] = y;
+    }
+}
+
+// level 1, pass 2: the chunk's keys again, grouped by digit1 at P1[chunk][digit]
+__global__ __launch_bounds__(kKeyThreads) void bp_scatter1_kernel(
+    const uint8_t* __restrict__ res, const uint64_t* __restrict__ res_off, const uint16_t* __restrict__ cls, int k,
+    uint32_t p_hi, uint64_t slots, const uint32_t* __restrict__ chunk_first, Layout lay, BpDigits dg, uint32_t pw21,
+    const uint32_t* __restrict__ P1, unsigned long long* __restrict__ out, uint32_t* __restrict__ flags) {
+    __shared__ union {
+        KeyChunk kc;
+        unsigned long long S[kKeyChunk];
+    } u;
+    __shared__ uint32_t lh[kBpMaxBins];
+    __shared__ uint32_t wave_tot[kKeyThreads / 64];
+    __shared__ uint32_t s_n;
+    const uint64_t c0 = (uint64_t)blockIdx.x * kKeyChunk, c1 = min(c0 + kKeyChunk, slots);
+    for (uint32_t d = threadIdx.x; d < dg.nb1; d += kKeyThreads) lh[d] = 0;
+    if (threadIdx.x == 0) s_n = 0;
+    const uint32_t first = chunk_first[blockIdx.x];
+    key_chunk_load(u.kc, res, res_off, cls, k, p_hi, c0, c1, first, lay, flags);
+    unsigned long long x[kBpPer];
+    uint32_t r[kBpPer], nk = 0;
+    auto digit = [&](unsigned long long y) { return (uint32_t)(y >> dg.sh1); };
+    const unsigned hs1 = dg.sh1 - lay.hshift;
+    key_chunk_run<kBpPer>(u.kc, threadIdx.x * kBpPer, (uint32_t)(c1 - c0), k, pw21, first, lay,
+                          [&](uint32_t e, bool valid, uint32_t h, unsigned long long lo) {
+                              x[e] = valid ? ((unsigned long long)h << lay.hshift) | lo : kNoKey;
+                              r[e] = valid ? atomicAdd(&lh[h >> hs1], 1u) : 0u;
+                              nk += valid;
+                          });
+    if (nk) atomicAdd(&s_n, nk);
+    __syncthreads();  // the chunk's staging (u.kc) is dead from here: u.S reuses it
+    bp_place(x, r, s_n, dg.nb1, digit, lh, wave_tot, u.S, P1 + (uint64_t)blockIdx.x * dg.nb1, out);
+}
+
+// level-2 tile (j, c) of coarse bin c: keys [a + j*kBpTile, a + min(n, (j+1)*kBpTile)) of the
+// level-1 array, a = C1[c] (aligned start), n = the bin's key count (compact starts C1[nb1+1+c]);
+// false past the bin's last tile, and for every tile of a bin above its budget of J tiles
+__device__ __forceinline__ bool bp_tile(const uint32_t* __restrict__ C1, uint32_t nb1, uint32_t c, uint32_t j,
+                                        uint32_t J, uint32_t& t0, uint32_t& tn) {
+    const uint32_t n = C1[nb1 + 2 + c] - C1[nb1 + 1 + c];
+    if (n > J * kBpTile || j * kBpTile >= n) return false;
+    t0 = C1[c] + j * kBpTile;
+    tn = min(kBpTile, n - j * kBpTile);
+    return true;
+}
+
+// level 2, pass 1: per-tile digit2 histogram -> H2[c][j][digit]
+__global__ __launch_bounds__(kKeyThreads) void bp_hist2_kernel(const unsigned long long* __restrict__ in,
+                                                               const uint32_t* __restrict__ C1, uint32_t J,
+                                                               BpDigits dg, uint32_t* __restrict__ H2) {
+    __shared__ uint32_t lh[kBpMaxBins];
+    const uint32_t j = blockIdx.x, c = blockIdx.y;
+    uint32_t t0, tn;
+    if (!bp_tile(C1, dg.nb1, c, j, J, t0, tn)) return;
+    for (uint32_t d = threadIdx.x; d < dg.nb2; d += kKeyThreads) lh[d] = 0;
+    __syncthreads();
+    // t0 is even (aligned bins): two keys per 16-byte load
+    for (uint32_t i = 2 * threadIdx.x; i < tn; i += 2 * kKeyThreads) {
+        if (i + 1 < tn) {
+            const ulonglong2 y = *reinterpret_cast<const ulonglong2*>(in + t0 + i);
+            atomicAdd(&lh[(uint32_t)(y.x >> dg.sh2) & dg.m2], 1u);
+            atomicAdd(&lh[(uint32_t)(y.y >> dg.sh2) & dg.m2], 1u);
+        } else {
+            atomicAdd(&lh[(uint32_t)(in[t0 + i] >> dg.sh2) & dg.m2], 1u);
+        }
+    }
+    __syncthreads();
+    uint32_t* row = H2 + ((uint64_t)c * J + j) * dg.nb2;
+    for (uint32_t d = threadIdx.x; d < dg.nb2; d += kKeyThreads) row[d] = lh[d];
+}
+
+// level-2 scan, one workgroup per coarse bin c: per digit the total over the bin's tiles, scanned
+// across digits -> bstart of buckets c*nb2 .. c*nb2 + nb2 - 1; then per digit an exclusive scan
+// down the tiles, in place (H2 -> P2).  A bin with more tiles than J raises flags[0].
+__global__ __launch_bounds__(kKeyThreads) void bp_scan2_kernel(uint32_t* __restrict__ H2,
+                                                               const uint32_t* __restrict__ C1, uint32_t J,
+                                                               BpDigits dg, uint32_t* __restrict__ bstart,
+                                                               uint32_t* __restrict__ flags) {
+    __shared__ uint32_t tot[kBpMaxBins];
+    __shared__ uint32_t wave_tot[kKeyThreads / 64];
+    const uint32_t c = blockIdx.x;
+    const uint32_t b0 = C1[dg.nb1 + 1 + c], n = C1[dg.nb1 + 2 + c] - b0;  // compact start, key count
+    const uint32_t nt = (n + kBpTile - 1) / kBpTile;
+    if (nt > J) {  // no tile of this bin was written: its buckets read as empty, the call falls back
+        if (threadIdx.x == 0) flags[0] = 1;
+        for (uint32_t d = threadIdx.x; d < dg.nb2; d += kKeyThreads) bstart[c * dg.nb2 + d] = b0;
+        if (c == gridDim.x - 1 && threadIdx.x == 0) bstart[gridDim.x * dg.nb2] = b0;
+        return;
+    }
+    uint32_t* base = H2 + (uint64_t)c * J * dg.nb2;
+    for (uint32_t d = threadIdx.x; d < dg.nb2; d += kKeyThreads) {
+        uint32_t v = 0;
+#pragma unroll 8
+        for (uint32_t j = 0; j < nt; ++j) v += base[(uint64_t)j * dg.nb2 + d];
+        tot[d] = v;
+    }
+    __syncthreads();
+    lds_bins_scan(tot, dg.nb2, wave_tot);
+    for (uint32_t d = threadIdx.x; d < dg.nb2; d += kKeyThreads) {
+        uint32_t run = b0 + tot[d];
+        bstart[c * dg.nb2 + d] = run;
+        for (uint32_t j = 0; j < nt; ++j) {
+            const uint32_t v = base[(uint64_t)j * dg.nb2 + d];
+            base[(uint64_t)j * dg.nb2 + d] = run;
+            run += v;
+        }
+    }
+    if (c == gridDim.x - 1 && threadIdx.x == 0) bstart[gridDim.x * dg.nb2] = b0 + n;
+}
+
+// level 2, pass 2: the tile's keys grouped by digit2 at P2[c][j][digit]
+__global__ __launch_bounds__(kKeyThreads) void bp_scatter2_kernel(const unsigned long long* __restrict__ in,
+                                                                  const uint32_t* __restrict__ C1, uint32_t J,
+                                                                  BpDigits dg, const uint32_t* __restrict__ P2,
+                                                                  unsigned long long* __restrict__ out) {
+    __shared__ unsigned long long S[kBpTile];
+    __shared__ uint32_t lh[kBpMaxBins];
+    __shared__ uint32_t wave_tot[kKeyThreads / 64];
+    const uint32_t j = blockIdx.x, c = blockIdx.y;
+    uint32_t t0, tn;
+    if (!bp_tile(C1, dg.nb1, c, j, J, t0, tn)) return;
+    for (uint32_t d = threadIdx.x; d < dg.nb2; d += kKeyThreads) lh[d] = 0;
+    __syncthreads();
+    unsigned long long x[kBpPer];
+    uint32_t r[kBpPer];
+    auto digit = [&](unsigned long long y) { return (uint32_t)(y >> dg.sh2) & dg.m2; };
+#pragma unroll
+    for (uint32_t e = 0; e < kBpPer; e += 2) {  // t0 is even: two keys per 16-byte load
+        const uint32_t i = 2 * threadIdx.x + e * kKeyThreads;
+        if (i + 1 < tn) {
+            const ulonglong2 y = *reinterpret_cast<const ulonglong2*>(in + t0 + i);
+            x[e] = y.x;
+            x[e + 1] = y.y;
+        } else {
+            x[e] = i < tn ? in[t0 + i] : kNoKey;
+            x[e + 1] = kNoKey;
+        }
+    }
+#pragma unroll
+    for (uint32_t e = 0; e < kBpPer; ++e) r[e] = x[e] != kNoKey ? atomicAdd(&lh[digit(x[e])], 1u) : 0u;
+    __syncthreads();
+    bp_place(x, r, tn, dg.nb2, digit, lh, wave_tot, S, P2 + ((uint64_t)c * J + j) * dg.nb2, out);
+}
+
 // the small bucket kernel for this layout: merged slot words when the bucket field is wide enough
 template <bool kPShard>
 void launch_bucket_small(uint32_t grid, hipStream_t st, const unsigned long long* sorted, const uint32_t* bstart,
@@ -1074,12 +1475,17 @@ __global__ void keep_flags_kernel(const uint32_t* __restrict__ w, const uint32_t
         keep[i] = i < U && w[i] >= min_shared;
 }
 
+// bumped on every reallocation of a workspace buffer: a captured step graph is valid only for the
+// generation it was captured in
+unsigned long long g_grow_gen = 0;
+
 template <class T>
 struct Grow {
     T* p = nullptr;
     size_t n = 0;
     hipError_t reserve(size_t m) {
         if (m <= n && p) return hipSuccess;
+        ++g_grow_gen;
         if (p) (void)hipFree(p);
         p = nullptr;
         n = 0;
@@ -1112,15 +1518,33 @@ struct kmp_postings {
     PShard ps{};
     Grow<uint32_t> ps_cursor, e3, ecnt, chunk_first;
     Grow<unsigned long long> eoff;
+    Grow<uint32_t> bp;          // bucket partition: H1 | P1 | R | C1 | H2 (see bp_level1)
+    uint32_t bp_J = 0;          // level-2 tiles per coarse bin
+    bool partition = !getenv("KMP_PARTITION") || atoi(getenv("KMP_PARTITION")) != 0;  // residue keys: counting partition
+    bool parted = false;        // ws->keys holds level-1 output (bp_level1 ran for this call)
+    // fused residue step as a HIP graph: captured on the second call with the same shape
+    // (every buffer already sized), replayed after that
+    bool graph_on = !getenv("KMP_GRAPH") || atoi(getenv("KMP_GRAPH")) != 0;
+    hipGraphExec_t gexec = nullptr;
+    hipStream_t cst = nullptr;  // capture stream
+    std::vector<unsigned long long> gkey, gkey_seen;
+    uint64_t graph_replays = 0;
+    // read-back of the fused step: gstats | cursors | flags[0..1] | run count, one D2H copy
+    Grow<unsigned long long> rb;
+    unsigned long long* hrb = nullptr;  // pinned
     int ablate = getenv("KMP_BUCKET_ABLATE") ? atoi(getenv("KMP_BUCKET_ABLATE")) : 0;  // diagnostics
     hipEvent_t ev[KMP_POSTINGS_STAGES + 1] = {};
     ~kmp_postings() {
         keys.release(); sorted.release(); inc.release(); inc_sorted.release(); uniq.release();
         bstats.release(); btot.release(); boff.release();
         w.release(); keep.release(); pos.release(); small.release(); cnt.release(); flags.release(); tmp.release();
-        ps_cursor.release(); e3.release(); ecnt.release(); eoff.release(); chunk_first.release();
+        ps_cursor.release(); e3.release(); ecnt.release(); eoff.release(); chunk_first.release(); bp.release();
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
+        rb.release();
+        if (hrb) (void)hipHostFree(hrb);
+        if (gexec) (void)hipGraphExecDestroy(gexec);
+        if (cst) (void)hipStreamDestroy(cst);
     }
     void mark(int stage, hipStream_t st) {
         if (timing) (void)hipEventRecord(ev[stage], st);
@@ -1144,6 +1568,74 @@ void fill_stats(kmp_postings_stats* stats, const unsigned long long* acc) {
     stats->max_df = acc[kStMaxDf];
     stats->heavy_entries = acc[kStHeavy];
     stats->incidences = acc[kStInc];
+}
+
+// Level 1 of the bucket partition for proteins [0, n): ws->keys = the valid keys grouped by
+// digit1; C1 = coarse bin starts (C1[nb1] = key count) in ws->bp for level 2.
+hipError_t bp_level1(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
+                     int k, uint32_t n, uint64_t slots, const Layout& lay, hipStream_t st) {
+    const BpDigits dg = bp_digits(lay);
+    const uint64_t G64 = (slots + kKeyChunk - 1) / kKeyChunk;
+    if (G64 * dg.nb1 > 0xFFFFFFFFull || slots > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    const uint32_t G = (uint32_t)G64, groups = (G + kBpRowGroup - 1) / kBpRowGroup;
+    // coarse bins are hash-uniform: a budget of 1.25x the mean plus two tiles
+    ws->bp_J = (uint32_t)((slots / dg.nb1 * 5 / 4 + kBpTile - 1) / kBpTile) + 2;
+    const uint64_t h1 = (uint64_t)G * dg.nb1, r = (uint64_t)groups * dg.nb1;
+    const uint64_t need = 2 * h1 + r + 2 * (dg.nb1 + 1) + (uint64_t)dg.nb1 * ws->bp_J * dg.nb2;
+    hipError_t e = ws->bp.reserve(need);
+    if (e == hipSuccess) e = ws->keys.reserve(slots + (uint64_t)kBpAlign * dg.nb1);  // + alignment gaps
+    if (e == hipSuccess) e = ws->chunk_first.reserve(G + 1);
+    if (e != hipSuccess) return e;
+    uint32_t *H1 = ws->bp.p, *P1 = H1 + h1, *R = P1 + h1, *C1 = R + r;
+    chunk_first_kernel<<<(n + 1 + 255) / 256, 256, 0, st>>>(d_res_off, 0u, n, 0ull, slots, G, ws->chunk_first.p);
+    const uint32_t pw21 = (uint32_t)pow21(k - 1);
+    bp_hist1_kernel<<<G, kKeyThreads, 0, st>>>(d_res, d_res_off, d_class, k, n, slots, ws->chunk_first.p, lay, dg,
+                                                pw21, H1, ws->flags.p);
+    bp_colsum_kernel<<<groups, 256, 0, st>>>(H1, G, dg.nb1, R);
+    bp_colscan_kernel<<<1, kColThreads, 0, st>>>(R, groups, dg.nb1, C1);
+    bp_colprefix_kernel<<<groups, 256, 0, st>>>(H1, G, dg.nb1, R, P1);
+    bp_scatter1_kernel<<<G, kKeyThreads, 0, st>>>(d_res, d_res_off, d_class, k, n, slots, ws->chunk_first.p, lay, dg,
+                                                   pw21, P1, ws->keys.p, ws->flags.p);
+    return hipGetLastError();
+}
+
+// Level 2: ws->keys (level 1) -> ws->sorted grouped by bucket, bstart[0..nb] in ws->cnt.
+int bp_level2(kmp_postings* ws, uint64_t slots, const Layout& lay, hipStream_t st) {
+    const BpDigits dg = bp_digits(lay);
+    const uint32_t G = (uint32_t)((slots + kKeyChunk - 1) / kKeyChunk), groups = (G + kBpRowGroup - 1) / kBpRowGroup;
+    const uint64_t h1 = (uint64_t)G * dg.nb1, r = (uint64_t)groups * dg.nb1;
+    uint32_t* C1 = ws->bp.p + 2 * h1 + r;
+    uint32_t* H2 = C1 + 2 * (dg.nb1 + 1);
+    const uint32_t nb = 1u << lay.bbits, J = ws->bp_J;
+    PG(ws->cnt.reserve(2 * (uint64_t)nb + 2));
+    bp_hist2_kernel<<<dim3(J, dg.nb1), kKeyThreads, 0, st>>>(ws->keys.p, C1, J, dg, H2);
+    bp_scan2_kernel<<<dg.nb1, kKeyThreads, 0, st>>>(H2, C1, J, dg, ws->cnt.p, ws->flags.p);
+    bp_scatter2_kernel<<<dim3(J, dg.nb1), kKeyThreads, 0, st>>>(ws->keys.p, C1, J, dg, H2, ws->sorted.p);
+    PG(hipGetLastError());
+    return KMP_OK;
+}
+
+// Bucketed front: keys `in` grouped by bucket into ws->sorted, bstart[0..nb] in ws->cnt.  After
+// bp_level1 (ws->parted) that is level 2; otherwise a radix sort on the bucket field and a binary
+// search per bucket.  Marks 2 after the grouping.
+int bucket_group(kmp_postings* ws, const unsigned long long* in, uint64_t slots, const Layout& lay, hipStream_t st) {
+    const uint32_t nb = 1u << lay.bbits;
+    PG(ws->sorted.reserve(slots));
+    if (ws->parted && in == ws->keys.p) {
+        ws->parted = false;
+        int rc = bp_level2(ws, slots, lay, st);
+        ws->mark(2, st);
+        return rc;
+    }
+    size_t t_sort = 0;
+    PG(rocprim::radix_sort_keys<SortCfg>(nullptr, t_sort, in, ws->sorted.p, (size_t)slots, lay.sort_lo, lay.sort_hi, st));
+    PG(ws->tmp.reserve(std::max(t_sort, ws->tmp.n)));
+    PG(rocprim::radix_sort_keys<SortCfg>(ws->tmp.p, t_sort, in, ws->sorted.p, (size_t)slots, lay.sort_lo, lay.sort_hi, st));
+    ws->mark(2, st);
+    PG(ws->cnt.reserve(2 * (uint64_t)nb + 2));
+    bucket_bounds_kernel<<<(nb + 1 + 255) / 256, 256, 0, st>>>(ws->sorted.p, slots, lay.sort_lo, nb, ws->cnt.p);
+    PG(hipGetLastError());
+    return KMP_OK;
 }
 
 // Flat front end (keys already in ws->keys): stable code sort, count pass, offsets, write pass.
@@ -1225,14 +1717,11 @@ int front_bucketed(kmp_postings* ws, const unsigned long long* in, uint64_t slot
                    bool* fallback, kmp_postings_stats* stats, hipStream_t st) {
     *fallback = false;
     ws->ps_ok = false;
-    size_t t_sort = 0;
-    PG(ws->sorted.reserve(slots));
-    PG(rocprim::radix_sort_keys<SortCfg>(nullptr, t_sort, in, ws->sorted.p, (size_t)slots, lay.sort_lo, lay.sort_hi, st));
-    PG(ws->tmp.reserve(std::max(t_sort, ws->tmp.n)));
-    PG(rocprim::radix_sort_keys<SortCfg>(ws->tmp.p, t_sort, in, ws->sorted.p, (size_t)slots, lay.sort_lo, lay.sort_hi, st));
-    ws->mark(2, st);
     const uint32_t nb = 1u << lay.bbits;
-    PG(ws->cnt.reserve(2 * (uint64_t)nb + 2));  // bucket starts, large-bucket list
+    {
+        int rc = bucket_group(ws, in, slots, lay, st);  // bucket starts + room for the large-bucket list
+        if (rc != KMP_OK) return rc;
+    }
     PG(ws->bstats.reserve(std::max<uint64_t>(ws->bstats.n, kShards * 8 + kShards)));
     uint32_t* bstart = ws->cnt.p;
     uint32_t* list = ws->cnt.p + nb + 1;
@@ -1240,7 +1729,6 @@ int front_bucketed(kmp_postings* ws, const unsigned long long* in, uint64_t slot
     uint32_t* flags = ws->flags.p;
     unsigned long long* gstats = ws->bstats.p;          // kShards x 8 (kSt* slots)
     unsigned long long* cursor = gstats + kShards * 8;  // kShards
-    bucket_bounds_kernel<<<(nb + 1 + 255) / 256, 256, 0, st>>>(ws->sorted.p, slots, lay.sort_lo, nb, bstart);
     PShard ps{};
     if (pshard) {
         if (!pshard_geometry(n, &ps.row_bits, &ps.n_shards)) pshard = false;
@@ -1386,74 +1874,183 @@ int tail_pshard(kmp_postings* ws, uint32_t min_shared, uint32_t* d_p, uint32_t* 
     return KMP_OK;
 }
 
-// Bucketed, min_shared == 1, one host synchronisation: bucket sort, group + expand into the
-// kShards regions, the regions' unused tails padded with kNoKey, one radix sort of the whole
-// padded buffer (its capacity is learned call to call, so it stays within a few % of the
-// incidence count), run-length encode, emit.  Stats, flags and the shard counts are read back
-// once at the end; a bucket that does not fit -> *fallback (flat rerun), a shard region
-// overflow -> grow and rerun.  Marks 2 (sort), 3 (group + expand), 4 (pad), 5 (pair sort),
-// 6 (encode + emit + read-back).
-int run_bucketed_fused(kmp_postings* ws, uint64_t slots, const Layout& lay, uint32_t n, uint32_t heavy_df,
-                       int require_class_diff, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w, uint64_t cap,
-                       uint64_t* n_edges, bool* fallback, kmp_postings_stats* stats, hipStream_t st) {
-    *fallback = false;
-    size_t t_sort = 0;
-    PG(rocprim::radix_sort_keys<SortCfg>(nullptr, t_sort, ws->keys.p, ws->sorted.p, (size_t)slots, lay.sort_lo,
-                                         lay.sort_hi, st));
-    PG(ws->tmp.reserve(std::max(t_sort, ws->tmp.n)));
-    PG(rocprim::radix_sort_keys<SortCfg>(ws->tmp.p, t_sort, ws->keys.p, ws->sorted.p, (size_t)slots, lay.sort_lo,
-                                         lay.sort_hi, st));
-    ws->mark(2, st);
-    const uint32_t nb = 1u << lay.bbits;
-    PG(ws->cnt.reserve(2 * (uint64_t)nb + 2));
+// ------------------------------------------------------------- fused residue step ----------
+// Bucketed, min_shared == 1, one host synchronisation per call: keys, bucket grouping, group +
+// expand into the kShards regions, the regions' unused tails padded with kNoKey, one radix sort
+// of the whole padded buffer (its capacity is learned call to call, so it stays within a few %
+// of the incidence count), run-length encode, emit, and ONE read-back of statistics, shard
+// counts, flags and the run count.  fused_enqueue issues all of it with no host wait, so it can
+// be captured as a HIP graph; run_fused replays that graph once the shape repeats.  A bucket that
+// does not fit -> *fallback (flat rerun); a shard region overflow -> grow and rerun.
+// Marks 0 (start), 1 (keys / level 1), 2 (bucket grouping), 3 (group + expand), 4 (pad),
+// 5 (pair sort), 6 (encode + emit + read-back).
+constexpr uint32_t kRbWords = kShards * 9 + 3;  // gstats (8 per shard) | cursors | flags[0..1] | runs
+
+__global__ void fused_clear_kernel(uint32_t* __restrict__ flags, unsigned long long* __restrict__ gstats) {
+    for (uint32_t i = threadIdx.x; i < kShards * 9; i += blockDim.x) gstats[i] = 0;
+    if (threadIdx.x < 4) flags[threadIdx.x] = 0;
+}
+
+__global__ void fused_pack_kernel(const unsigned long long* __restrict__ gstats, const uint32_t* __restrict__ flags,
+                                  const uint32_t* __restrict__ runs, unsigned long long* __restrict__ rb) {
+    for (uint32_t i = threadIdx.x; i < kShards * 9; i += blockDim.x) rb[i] = gstats[i];
+    if (threadIdx.x == 0) {
+        rb[kShards * 9] = flags[0];
+        rb[kShards * 9 + 1] = flags[1];
+        rb[kShards * 9 + 2] = *runs;
+    }
+}
+
+// buffers of one fused step (reserved before any launch, so a capture allocates nothing)
+int fused_reserve(kmp_postings* ws, uint64_t slots, const Layout& lay, uint32_t n) {
+    const uint64_t total = ws->shard_cap * kShards;
+    const unsigned pair_bits = bits_for((uint64_t)n * n);
+    PG(ws->keys.reserve(slots));
+    PG(ws->sorted.reserve(slots));
+    PG(ws->flags.reserve(4));
+    PG(ws->cnt.reserve(2 * ((uint64_t)1 << lay.bbits) + 2));
     PG(ws->bstats.reserve(std::max<uint64_t>(ws->bstats.n, kShards * 8 + kShards)));
     PG(ws->small.reserve(16));
-    uint32_t* bstart = ws->cnt.p;
-    uint32_t* list = ws->cnt.p + nb + 1;
-    uint32_t* list_count = ws->flags.p + 2;
+    PG(ws->inc_sorted.reserve(total));
+    PG(ws->inc.reserve(total));
+    PG(ws->uniq.reserve(total));
+    PG(ws->w.reserve(total));
+    PG(ws->rb.reserve(kRbWords));
+    if (!ws->hrb) PG(hipHostMalloc((void**)&ws->hrb, kRbWords * sizeof(unsigned long long), hipHostMallocDefault));
+    size_t t2 = 0, t3 = 0;
+    PG(rocprim::radix_sort_keys<PairSortCfg>(nullptr, t2, ws->inc_sorted.p, ws->inc.p, (size_t)total, 0u, pair_bits,
+                                             (hipStream_t)0));
+    PG(rocprim::run_length_encode(nullptr, t3, ws->inc.p, (unsigned int)total, ws->uniq.p, ws->w.p, ws->small.p + 1,
+                                  (hipStream_t)0));
+    PG(ws->tmp.reserve(std::max({t2, t3, ws->tmp.n})));
+    return KMP_OK;
+}
+
+// one attempt of the fused step, keys included, up to the read-back copy into ws->hrb; no host
+// wait, no allocation (fused_reserve ran first)
+template <class MakeKeys>
+int fused_enqueue(kmp_postings* ws, MakeKeys& make_keys, uint64_t slots, const Layout& lay, uint32_t n,
+                  uint32_t heavy_df, int require_class_diff, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w,
+                  uint64_t cap, hipStream_t st) {
+    const uint32_t nb = 1u << lay.bbits;
+    const uint64_t sc = ws->shard_cap, total = sc * kShards;
+    const unsigned pair_bits = bits_for((uint64_t)n * n);
     uint32_t* flags = ws->flags.p;
+    uint32_t* list_count = flags + 2;
     unsigned long long* gstats = ws->bstats.p;
     unsigned long long* cursor = gstats + kShards * 8;
-    bucket_bounds_kernel<<<(nb + 1 + 255) / 256, 256, 0, st>>>(ws->sorted.p, slots, lay.sort_lo, nb, bstart);
-    if (ws->shard_cap == 0) ws->shard_cap = slots / 4 / kShards + 4096;
+    fused_clear_kernel<<<1, 256, 0, st>>>(flags, gstats);
+    ws->mark(0, st);
+    PG(make_keys(lay, st));
+    ws->mark(1, st);
+    {
+        int rc = bucket_group(ws, ws->keys.p, slots, lay, st);
+        if (rc != KMP_OK) return rc;
+    }
+    uint32_t* bstart = ws->cnt.p;
+    uint32_t* list = ws->cnt.p + nb + 1;
     PShard ps{};
-    const unsigned pair_bits = bits_for((uint64_t)n * n);
+    launch_bucket_small<false>(nb, st, ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df, ws->inc_sorted.p, sc,
+                               cursor, gstats, flags, list, list_count, ps);
+    bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeTab, false>
+        <<<256, kBucketLargeThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
+                                              ws->inc_sorted.p, sc, cursor, gstats, flags, list, list_count, ps);
+    ws->mark(3, st);
+    pad_shards_kernel<<<dim3(route_blocks(sc), kShards), 256, 0, st>>>(ws->inc_sorted.p, sc, cursor);
+    ws->mark(4, st);
+    size_t t2 = ws->tmp.n, t3 = ws->tmp.n;
+    PG(rocprim::radix_sort_keys<PairSortCfg>(ws->tmp.p, t2, ws->inc_sorted.p, ws->inc.p, (size_t)total, 0u,
+                                             pair_bits, st));
+    ws->mark(5, st);
+    PG(rocprim::run_length_encode(ws->tmp.p, t3, ws->inc.p, (unsigned int)total, ws->uniq.p, ws->w.p,
+                                  ws->small.p + 1, st));
+    const uint32_t kb = (uint32_t)std::min<uint64_t>((total + 255) / 256, 8192);
+    emit_runs_kernel<<<kb, 256, 0, st>>>(ws->uniq.p, ws->w.p, ws->small.p + 1, n, d_p, d_q, d_w, cap);
+    fused_pack_kernel<<<1, 256, 0, st>>>(gstats, flags, ws->small.p + 1, ws->rb.p);
+    PG(hipMemcpyAsync(ws->hrb, ws->rb.p, kRbWords * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    ws->mark(6, st);
+    PG(hipGetLastError());
+    return KMP_OK;
+}
+
+// enqueue the step: replay the captured graph when the shape matches the capture, capture it
+// when the shape repeats a plain run (buffers sized), else run plain
+template <class MakeKeys>
+int fused_launch(kmp_postings* ws, MakeKeys& make_keys, const std::vector<unsigned long long>& key, uint64_t slots,
+                 const Layout& lay, uint32_t n, uint32_t heavy_df, int require_class_diff, uint32_t* d_p,
+                 uint32_t* d_q, uint32_t* d_w, uint64_t cap, hipStream_t st) {
+    auto plain = [&]() {
+        return fused_enqueue(ws, make_keys, slots, lay, n, heavy_df, require_class_diff, d_p, d_q, d_w, cap, st);
+    };
+    if (!ws->graph_on) return plain();
+    if (ws->gexec && ws->gkey == key) {
+        PG(hipGraphLaunch(ws->gexec, st));
+        ++ws->graph_replays;
+        return KMP_OK;
+    }
+    if (ws->gkey_seen != key) {
+        ws->gkey_seen = key;
+        return plain();
+    }
+    if (ws->gexec) {
+        (void)hipGraphExecDestroy(ws->gexec);
+        ws->gexec = nullptr;
+        ws->gkey.clear();
+    }
+    const unsigned long long gen = g_grow_gen;
+    hipGraph_t g = nullptr;
+    // captured on a private stream (the caller's may be the legacy null stream, which cannot be
+    // captured), launched on the caller's
+    if (!ws->cst && hipStreamCreateWithFlags(&ws->cst, hipStreamNonBlocking) != hipSuccess) ws->cst = nullptr;
+    if (!ws->cst || hipStreamBeginCapture(ws->cst, hipStreamCaptureModeRelaxed) != hipSuccess) {
+        (void)hipGetLastError();
+        ws->graph_on = false;
+        return plain();
+    }
+    int rc = fused_enqueue(ws, make_keys, slots, lay, n, heavy_df, require_class_diff, d_p, d_q, d_w, cap, ws->cst);
+    hipError_t e = hipStreamEndCapture(ws->cst, &g);
+    hipGraphExec_t ex = nullptr;
+    if (rc == KMP_OK && e == hipSuccess && g && gen == g_grow_gen)
+        e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+    else if (e == hipSuccess)
+        e = hipErrorUnknown;
+    if (g) (void)hipGraphDestroy(g);
+    if (e != hipSuccess || !ex) {  // capture not usable: plain from now on
+        (void)hipGetLastError();
+        if (getenv("KMP_DEBUG"))
+            fprintf(stderr, "kmp: step graph capture failed (rc %d, %s); plain launches from now on\n", rc,
+                    hipGetErrorString(e));
+        ws->graph_on = false;
+        return plain();
+    }
+    ws->gexec = ex;
+    ws->gkey = key;
+    PG(hipGraphLaunch(ws->gexec, st));
+    return KMP_OK;
+}
+
+template <class MakeKeys>
+int run_fused(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long long> key, uint64_t slots,
+              const Layout& lay, uint32_t n, uint32_t heavy_df, int require_class_diff, uint32_t* d_p, uint32_t* d_q,
+              uint32_t* d_w, uint64_t cap, uint64_t* n_edges, bool* fallback, kmp_postings_stats* stats,
+              hipStream_t st) {
+    *fallback = false;
+    if (ws->shard_cap == 0) ws->shard_cap = slots / 4 / kShards + 4096;
     for (int attempt = 0; attempt < 3; ++attempt) {
         const uint64_t sc = ws->shard_cap, total = sc * kShards;
-        PG(ws->inc_sorted.reserve(total));
-        PG(ws->inc.reserve(total));
-        PG(ws->uniq.reserve(total));
-        PG(ws->w.reserve(total));
-        PG(hipMemsetAsync(gstats, 0, (kShards * 8 + kShards) * sizeof(unsigned long long), st));
-        PG(hipMemsetAsync(list_count, 0, sizeof(uint32_t), st));
-        launch_bucket_small<false>(nb, st, ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df, ws->inc_sorted.p, sc, cursor, gstats, flags, list, list_count, ps);
-        bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeTab, false>
-            <<<256, kBucketLargeThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
-                                                  ws->inc_sorted.p, sc, cursor, gstats, flags, list, list_count, ps);
-        ws->mark(3, st);
-        pad_shards_kernel<<<dim3(route_blocks(sc), kShards), 256, 0, st>>>(ws->inc_sorted.p, sc, cursor);
-        ws->mark(4, st);
-        size_t t2 = 0, t3 = 0;
-        PG(rocprim::radix_sort_keys<PairSortCfg>(nullptr, t2, ws->inc_sorted.p, ws->inc.p, (size_t)total, 0u, pair_bits,
-                                             st));
-        PG(rocprim::run_length_encode(nullptr, t3, ws->inc.p, (unsigned int)total, ws->uniq.p, ws->w.p,
-                                      ws->small.p + 1, st));
-        PG(ws->tmp.reserve(std::max({t2, t3, ws->tmp.n})));
-        PG(rocprim::radix_sort_keys<PairSortCfg>(ws->tmp.p, t2, ws->inc_sorted.p, ws->inc.p, (size_t)total, 0u,
-                                                 pair_bits, st));
-        ws->mark(5, st);
-        PG(rocprim::run_length_encode(ws->tmp.p, t3, ws->inc.p, (unsigned int)total, ws->uniq.p, ws->w.p,
-                                      ws->small.p + 1, st));
-        const uint32_t kb = (uint32_t)std::min<uint64_t>((total + 255) / 256, 8192);
-        emit_runs_kernel<<<kb, 256, 0, st>>>(ws->uniq.p, ws->w.p, ws->small.p + 1, n, d_p, d_q, d_w, cap);
-        unsigned long long g[kShards * 8 + kShards];
-        uint32_t h_flags[2] = {0, 0}, h_uniq = 0;
-        PG(hipMemcpyAsync(g, gstats, sizeof g, hipMemcpyDeviceToHost, st));
-        PG(hipMemcpyAsync(h_flags, flags, sizeof h_flags, hipMemcpyDeviceToHost, st));
-        PG(hipMemcpyAsync(&h_uniq, ws->small.p + 1, sizeof h_uniq, hipMemcpyDeviceToHost, st));
+        {
+            int rc = fused_reserve(ws, slots, lay, n);
+            if (rc != KMP_OK) return rc;
+        }
+        key.push_back(sc);
+        key.push_back(ws->timing);
+        key.push_back(g_grow_gen);
+        int rc = fused_launch(ws, make_keys, key, slots, lay, n, heavy_df, require_class_diff, d_p, d_q, d_w, cap, st);
+        key.resize(key.size() - 3);
+        if (rc != KMP_OK) return rc;
         PG(hipStreamSynchronize(st));
-        ws->mark(6, st);
-        if (h_flags[0] || h_flags[1]) {
+        const unsigned long long* g = ws->hrb;
+        if (g[kShards * 9] || g[kShards * 9 + 1]) {
             *fallback = true;
             return KMP_OK;
         }
@@ -1464,6 +2061,7 @@ int run_bucketed_fused(kmp_postings* ws, uint64_t slots, const Layout& lay, uint
             most = std::max(most, g[kShards * 8 + sh]);
             n_inc += g[kShards * 8 + sh];
         }
+        const uint64_t h_uniq = g[kShards * 9 + 2];
         ws->shard_cap = most + most / 64 + 256;  // learned capacity for the next call (or the rerun)
         if (most > sc) continue;                 // a region overflowed: rerun with the new capacity
         fill_stats(stats, acc);
@@ -1566,24 +2164,29 @@ hipError_t launch_residue_keys(kmp_postings* ws, const uint8_t* d_res, const uin
 
 // Both entry points: keys from `make_keys(layout)`, bucketed front end (flat on fallback), tail.
 template <class MakeKeys>
-int run_postings(kmp_postings* ws, MakeKeys make_keys, uint32_t n, int k, uint64_t slots, const uint16_t* d_class,
-                 uint32_t heavy_df, uint32_t min_shared, int require_class_diff, uint32_t* d_p, uint32_t* d_q,
-                 uint32_t* d_w, uint64_t cap, uint64_t* n_edges, kmp_postings_stats* stats, hipStream_t st) {
+int run_postings(kmp_postings* ws, MakeKeys make_keys, const std::vector<unsigned long long>& key_extra, uint32_t n,
+                 int k, uint64_t slots, const uint16_t* d_class, uint32_t heavy_df, uint32_t min_shared,
+                 int require_class_diff, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w, uint64_t cap, uint64_t* n_edges,
+                 kmp_postings_stats* stats, hipStream_t st) {
     if (heavy_df < 2) heavy_df = 2;
     if (min_shared < 1) min_shared = 1;
     PG(ws->keys.reserve(slots));
     PG(ws->sorted.reserve(slots));
     PG(ws->flags.reserve(4));
-    PG(hipMemsetAsync(ws->flags.p, 0, 4 * sizeof(uint32_t), st));
     unsigned long long n_inc = 0;
+    ws->parted = false;
     Layout lay = make_layout(n, k, slots, ws->bucketed);
     bool fallback = true;
     if (lay.bucketed && min_shared == 1 && !ws->pshard) {
-        ws->mark(0, st);
-        PG(make_keys(lay));
-        ws->mark(1, st);
-        int rc = run_bucketed_fused(ws, slots, lay, n, heavy_df, require_class_diff, d_p, d_q, d_w, cap, n_edges,
-                                    &fallback, stats, st);
+        // graph key: the call's shape and pointers (run_fused adds the shard capacity, the timing
+        // switch and the buffer generation)
+        std::vector<unsigned long long> key = {n, (unsigned long long)k, slots, heavy_df,
+                                               (unsigned long long)require_class_diff, cap,
+                                               (unsigned long long)(uintptr_t)d_p, (unsigned long long)(uintptr_t)d_q,
+                                               (unsigned long long)(uintptr_t)d_w};
+        key.insert(key.end(), key_extra.begin(), key_extra.end());
+        int rc = run_fused(ws, make_keys, key, slots, lay, n, heavy_df, require_class_diff, d_p, d_q, d_w, cap,
+                           n_edges, &fallback, stats, st);
         if (!fallback) {
             ws->last_bucketed = true;
             ws->last_pshard = false;
@@ -1592,8 +2195,9 @@ int run_postings(kmp_postings* ws, MakeKeys make_keys, uint32_t n, int k, uint64
             return rc;
         }
     } else if (lay.bucketed) {
+        PG(hipMemsetAsync(ws->flags.p, 0, 4 * sizeof(uint32_t), st));
         ws->mark(0, st);
-        PG(make_keys(lay));
+        PG(make_keys(lay, st));
         ws->mark(1, st);
         int rc = front_bucketed(ws, ws->keys.p, slots, lay, n, heavy_df, require_class_diff, ws->pshard, &n_inc,
                                 &fallback, stats, st);
@@ -1602,8 +2206,10 @@ int run_postings(kmp_postings* ws, MakeKeys make_keys, uint32_t n, int k, uint64
     if (fallback) {
         lay = make_layout(n, k, slots, false);
         if (lay.sort_hi > 64) return KMP_EINVAL;
+        ws->parted = false;
+        PG(hipMemsetAsync(ws->flags.p, 0, 4 * sizeof(uint32_t), st));
         ws->mark(0, st);
-        PG(make_keys(lay));
+        PG(make_keys(lay, st));
         ws->mark(1, st);
         int rc = front_flat(ws, slots, lay, d_class, n, heavy_df, require_class_diff, &n_inc, stats, st);
         if (rc != KMP_OK) return rc;
@@ -1654,6 +2260,26 @@ int kmp_postings_set_pshard(kmp_postings* ws, int enable) {
     return KMP_OK;
 }
 
+int kmp_postings_set_partition(kmp_postings* ws, int enable) {
+    if (!ws) return KMP_EINVAL;
+    ws->partition = enable != 0;
+    return KMP_OK;
+}
+
+int kmp_postings_set_graph(kmp_postings* ws, int enable) {
+    if (!ws) return KMP_EINVAL;
+    ws->graph_on = enable != 0;
+    if (!ws->graph_on && ws->gexec) {
+        (void)hipGraphExecDestroy(ws->gexec);
+        ws->gexec = nullptr;
+        ws->gkey.clear();
+    }
+    ws->gkey_seen.clear();
+    return KMP_OK;
+}
+
+uint64_t kmp_postings_graph_replays(const kmp_postings* ws) { return ws ? ws->graph_replays : 0; }
+
 int kmp_dev_pairs_postings(kmp_postings* ws, const uint32_t* d_set, const uint32_t* d_set_len,
                            const uint64_t* d_res_off, const uint16_t* d_class, uint32_t n, int k, uint64_t slots,
                            uint32_t heavy_df, uint32_t min_shared, int require_class_diff, uint32_t* d_p,
@@ -1663,13 +2289,15 @@ int kmp_dev_pairs_postings(kmp_postings* ws, const uint32_t* d_set, const uint32
     if (rc != KMP_OK || n < 2) return rc;
     if (!d_set || !d_set_len || !d_res_off || !d_class) return KMP_EINVAL;
     hipStream_t st = as_stream(stream);
-    auto keys = [&](const Layout& lay) {
+    auto keys = [&](const Layout& lay, hipStream_t st) {
         set_keys_kernel<<<n + 1, 256, 0, st>>>(d_set, d_set_len, d_res_off, d_class, n, slots, lay, ws->keys.p,
                                                ws->flags.p);
         return hipGetLastError();
     };
-    return run_postings(ws, keys, n, k, slots, d_class, heavy_df, min_shared, require_class_diff, d_p, d_q, d_w, cap,
-                        n_edges, stats, st);
+    const std::vector<unsigned long long> key_extra = {0, (uintptr_t)d_set, (uintptr_t)d_set_len, (uintptr_t)d_res_off,
+                                                       (uintptr_t)d_class};
+    return run_postings(ws, keys, key_extra, n, k, slots, d_class, heavy_df, min_shared, require_class_diff, d_p, d_q,
+                        d_w, cap, n_edges, stats, st);
 }
 
 int kmp_dev_pairs_residues(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off,
@@ -1680,11 +2308,17 @@ int kmp_dev_pairs_residues(kmp_postings* ws, const uint8_t* d_res, const uint64_
     if (rc != KMP_OK || n < 2) return rc;
     if (!d_res || !d_res_off || !d_class) return KMP_EINVAL;
     hipStream_t st = as_stream(stream);
-    auto keys = [&](const Layout& lay) {
+    auto keys = [&](const Layout& lay, hipStream_t st) {
+        if (lay.bucketed && ws->partition) {
+            ws->parted = true;
+            return bp_level1(ws, d_res, d_res_off, d_class, k, n, slots, lay, st);
+        }
         return launch_residue_keys(ws, d_res, d_res_off, d_class, k, 0u, n, 0ull, slots, lay, st);
     };
-    return run_postings(ws, keys, n, k, slots, d_class, heavy_df, min_shared, require_class_diff, d_p, d_q, d_w, cap,
-                        n_edges, stats, st);
+    const std::vector<unsigned long long> key_extra = {1, (uintptr_t)d_res, (uintptr_t)d_res_off, (uintptr_t)d_class,
+                                                       ws->partition};
+    return run_postings(ws, keys, key_extra, n, k, slots, d_class, heavy_df, min_shared, require_class_diff, d_p, d_q,
+                        d_w, cap, n_edges, stats, st);
 }
 
 // ------------------------------------------------------------- multi-GPU split -------------

@@ -223,6 +223,18 @@ class DevicePipeline:
         global pair-key sort."""
         check(lib().kmp_postings_set_pshard(self._workspace(), int(enable)), "kmp_postings_set_pshard")
 
+    def set_partition(self, enable: bool = True) -> None:
+        """Residue path: group keys by bucket with the two-level counting partition (default) or
+        write every key and radix-sort the bucket field."""
+        check(lib().kmp_postings_set_partition(self._workspace(), int(enable)), "kmp_postings_set_partition")
+
+    def set_graph(self, enable: bool = True) -> None:
+        """Residue path: capture the single-synchronisation step as a HIP graph and replay it."""
+        check(lib().kmp_postings_set_graph(self._workspace(), int(enable)), "kmp_postings_set_graph")
+
+    def graph_replays(self) -> int:
+        return int(lib().kmp_postings_graph_replays(self._workspace()))
+
     def last_layout(self) -> str:
         return "bucketed" if lib().kmp_postings_last_layout(self._workspace()) else "flat"
 
