@@ -242,6 +242,35 @@ def test_residue_graph_replay(oracle_mod, partition):
     np.testing.assert_array_equal(pipe.edges()[2], w)
 
 
+def test_rowtail_overflow_falls_back(oracle_mod):
+    """A protein whose row holds more pair keys than one row block of the fused step's LDS
+    reduction (kPtCap) sends the call to the global pair-key sort tail; edges stay exact, and the
+    row-block tail handles the same shape when rows are short."""
+    import torch
+    from uniprot_kmer_based_clustering_amd.device import DevicePipeline
+    rng = np.random.default_rng(7)
+    alpha = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", dtype=np.uint8)
+    rnd = lambda m: alpha[rng.integers(0, 20, m)].tobytes()  # noqa: E731
+    base = rnd(15000)
+    seqs = [base] + [rnd(30) + base[60 * i:60 * i + 60] + rnd(30) for i in range(220)]
+    res, off, cls = make_batch(seqs, ["a"] + ["b"] * 220)
+    p, q, w = oracle_mod.Oracle(res, off, cls, k=7, threads=8).pairs()
+    assert int(w[p == 0].sum()) > 8192
+    for shuffle_first in (False, True):
+        if shuffle_first:  # the long row last instead of first: every row short enough
+            seqs2 = seqs[1:] + seqs[:1]
+            res, off, cls = make_batch(seqs2, ["b"] * 220 + ["a"])
+            p, q, w = oracle_mod.Oracle(res, off, cls, k=7, threads=8).pairs()
+        pipe = DevicePipeline(K.Proteins(res, off, cls), 7, "cuda:0")
+        for _ in range(3):
+            m = pipe.step(engine="residues")
+            torch.cuda.synchronize()
+            assert pipe.last_tail() == "fused" and m == len(p)
+            np.testing.assert_array_equal(pipe.edges()[0], p)
+            np.testing.assert_array_equal(pipe.edges()[1], q)
+            np.testing.assert_array_equal(pipe.edges()[2], w)
+
+
 def test_pshard_long_rows(oracle_mod):
     """One protein sharing a distinct k-mer with each of ~650 others: its row of the p-shard
     reduction is longer than the rank-sort limit, so that range is bitonic-sorted in LDS."""

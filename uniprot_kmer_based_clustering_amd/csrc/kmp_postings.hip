@@ -22,6 +22,7 @@
 // proteins ascending.  Carrying the class in the key keeps the expansion free of random loads.
 #include <hip/hip_runtime.h>
 
+#include <rocprim/block/block_radix_sort.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_run_length_encode.hpp>
 #include <rocprim/device/device_scan.hpp>
@@ -1182,11 +1183,12 @@ __global__ __launch_bounds__(kKeyThreads) void bp_hist1_kernel(
     for (uint32_t d = threadIdx.x; d < dg.nb1; d += kKeyThreads) H1[(uint64_t)blockIdx.x * dg.nb1 + d] = lh[d];
 }
 
-// level-1 column scan, 1 of 3: R[g][c] = sum of M[r][c] over the kBpRowGroup rows of group g
+// column scan of a [rows][cols] count matrix, 1 of 3: R[g][c] = sum of M[r][c] over the
+// kBpRowGroup rows of group g (grid: groups x ceil(cols / 256))
 __global__ __launch_bounds__(256) void bp_colsum_kernel(const uint32_t* __restrict__ M, uint32_t rows, uint32_t cols,
                                                         uint32_t* __restrict__ R) {
     const uint32_t r0 = blockIdx.x * kBpRowGroup, r1 = min(rows, r0 + kBpRowGroup);
-    for (uint32_t c = threadIdx.x; c < cols; c += blockDim.x) {
+    for (uint32_t c = blockIdx.y * 256 + threadIdx.x; c < cols; c += gridDim.y * 256) {
         uint32_t v = 0;
 #pragma unroll 8
         for (uint32_t r = r0; r < r1; ++r) v += M[(uint64_t)r * cols + c];
@@ -1260,8 +1262,9 @@ __global__ __launch_bounds__(256) void bp_colprefix_kernel(const uint32_t* __res
                                                            uint32_t cols, const uint32_t* __restrict__ R,
                                                            uint32_t* __restrict__ P) {
     const uint32_t r0 = blockIdx.x * kBpRowGroup, r1 = min(rows, r0 + kBpRowGroup);
-    for (uint32_t c = threadIdx.x; c < cols; c += blockDim.x) {
+    for (uint32_t c = blockIdx.y * 256 + threadIdx.x; c < cols; c += gridDim.y * 256) {
         uint32_t run = R[(uint64_t)blockIdx.x * cols + c];
+#pragma unroll 8
         for (uint32_t r = r0; r < r1; ++r) {
             P[(uint64_t)r * cols + c] = run;
             run += M[(uint64_t)r * cols + c];
@@ -1519,6 +1522,10 @@ struct kmp_postings {
     Grow<uint32_t> ps_cursor, e3, ecnt, chunk_first;
     Grow<unsigned long long> eoff;
     Grow<uint32_t> bp;          // bucket partition: H1 | P1 | R | C1 | H2 (see bp_level1)
+    Grow<uint32_t> pt;          // row-block tail (pt_bufs)
+    bool pt_on = !getenv("KMP_ROWTAIL") || atoi(getenv("KMP_ROWTAIL")) != 0;  // fused step: row-block tail
+    uint64_t pt_inc = 0;        // incidences of the last fused call (row-block sizing)
+    unsigned pt_rb_max = 16;    // rows-per-block bound learned from overflowing row blocks
     uint32_t bp_J = 0;          // level-2 tiles per coarse bin
     bool partition = !getenv("KMP_PARTITION") || atoi(getenv("KMP_PARTITION")) != 0;  // residue keys: counting partition
     bool parted = false;        // ws->keys holds level-1 output (bp_level1 ran for this call)
@@ -1538,7 +1545,7 @@ struct kmp_postings {
         keys.release(); sorted.release(); inc.release(); inc_sorted.release(); uniq.release();
         bstats.release(); btot.release(); boff.release();
         w.release(); keep.release(); pos.release(); small.release(); cnt.release(); flags.release(); tmp.release();
-        ps_cursor.release(); e3.release(); ecnt.release(); eoff.release(); chunk_first.release(); bp.release();
+        ps_cursor.release(); e3.release(); ecnt.release(); eoff.release(); chunk_first.release(); bp.release(); pt.release();
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
         rb.release();
@@ -1591,9 +1598,9 @@ hipError_t bp_level1(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_r
     const uint32_t pw21 = (uint32_t)pow21(k - 1);
     bp_hist1_kernel<<<G, kKeyThreads, 0, st>>>(d_res, d_res_off, d_class, k, n, slots, ws->chunk_first.p, lay, dg,
                                                 pw21, H1, ws->flags.p);
-    bp_colsum_kernel<<<groups, 256, 0, st>>>(H1, G, dg.nb1, R);
+    bp_colsum_kernel<<<dim3(groups, (dg.nb1 + 255) / 256), 256, 0, st>>>(H1, G, dg.nb1, R);
     bp_colscan_kernel<<<1, kColThreads, 0, st>>>(R, groups, dg.nb1, C1);
-    bp_colprefix_kernel<<<groups, 256, 0, st>>>(H1, G, dg.nb1, R, P1);
+    bp_colprefix_kernel<<<dim3(groups, (dg.nb1 + 255) / 256), 256, 0, st>>>(H1, G, dg.nb1, R, P1);
     bp_scatter1_kernel<<<G, kKeyThreads, 0, st>>>(d_res, d_res_off, d_class, k, n, slots, ws->chunk_first.p, lay, dg,
                                                    pw21, P1, ws->keys.p, ws->flags.p);
     return hipGetLastError();
@@ -1874,6 +1881,280 @@ int tail_pshard(kmp_postings* ws, uint32_t min_shared, uint32_t* d_p, uint32_t* 
     return KMP_OK;
 }
 
+// ------------------------------------------------------------- row-block tail -------------
+// combine_edges (mod.rs:322-546) for the fused step without a global pair-key sort.  Pair keys
+// are p << pbits | q (p < q); row block r = rows [r << rbits, (r + 1) << rbits).
+//   pt_hist     per 8,192-key tile of each shard region: row-block histogram -> H[tile][r]
+//   column scan (bp_colsum, pt_colscan, bp_colprefix) -> P[tile][r] and the block starts
+//   pt_scatter  per tile: keys ranked by row block in LDS and written as u32
+//               (p_local << pbits | q), one run per row block at P[tile][r]
+//   pt_reduce   one workgroup per row block: LDS radix sort of its keys (rocprim
+//               block_radix_sort), run-length encode (run = one (p, q) pair, length = w); runs
+//               staged at the block's input offset, run count per block
+//   pt_offsets  one workgroup: exclusive scan of the run counts -> edge offsets and the total
+//   pt_emit     one workgroup per row block: staged runs -> (d_p, d_q, d_w) at its offset
+// A row block above kPtCap keys (a protein pairing with thousands of later proteins) raises
+// flags[3]; the call then reruns on the global-sort tail.
+constexpr uint32_t kPtThreads = 1024, kPtPer = 16, kPtTile = kPtThreads * kPtPer;  // partition tiles: 16,384 keys
+constexpr uint32_t kPtRThreads = 512, kPtCap = 8192;  // pt_reduce: up to 16 keys per thread
+constexpr uint32_t kPtMaxBlocks = 8192;  // row blocks (LDS histogram of pt_hist / pt_scatter)
+
+struct PtGeom {
+    unsigned pbits, rbits;  // key = p << pbits | q; rows per block = 1 << rbits
+    uint32_t nrb;           // row blocks
+    uint32_t jt;            // tiles per shard region
+    uint64_t sc;            // shard region capacity
+};
+
+__device__ __forceinline__ uint32_t pt_tile_keys(const unsigned long long* __restrict__ cursor, const PtGeom& g,
+                                                 uint32_t s, uint32_t j, uint32_t& t0) {
+    const uint64_t ns = min<unsigned long long>(cursor[s], g.sc);
+    t0 = j * kPtTile;
+    return t0 < ns ? (uint32_t)min<uint64_t>(kPtTile, ns - t0) : 0u;
+}
+
+__global__ __launch_bounds__(kPtThreads) void pt_hist_kernel(const unsigned long long* __restrict__ in,
+                                                             const unsigned long long* __restrict__ cursor, PtGeom g,
+                                                             uint32_t* __restrict__ H) {
+    __shared__ uint32_t lh[kPtMaxBlocks];
+    const uint32_t j = blockIdx.x, s = blockIdx.y;
+    for (uint32_t r = threadIdx.x; r < g.nrb; r += kPtThreads) lh[r] = 0;
+    __syncthreads();
+    uint32_t t0;
+    const uint32_t m = pt_tile_keys(cursor, g, s, j, t0);
+    const unsigned long long* src = in + s * g.sc + t0;
+    const unsigned sh = g.pbits + g.rbits;
+    for (uint32_t i = threadIdx.x; i < m; i += kPtThreads) atomicAdd(&lh[(uint32_t)(src[i] >> sh)], 1u);
+    __syncthreads();
+    uint32_t* row = H + (uint64_t)(s * g.jt + j) * g.nrb;
+    for (uint32_t r = threadIdx.x; r < g.nrb; r += kPtThreads) row[r] = lh[r];
+}
+
+// column starts of a [rows][cols] matrix already summed into row groups (R, bp_colsum): per
+// column an exclusive scan down the groups plus the column's start, in place; colstart[c] and
+// colstart[cols] = total; *colmax = the largest column total.  cols <= 8 * 1024 (each thread owns
+// up to 8 consecutive columns).
+constexpr int kPtScanThreads = 1024;
+__global__ __launch_bounds__(kPtScanThreads) void pt_colscan_kernel(uint32_t* __restrict__ R, uint32_t groups,
+                                                                    uint32_t cols, uint32_t* __restrict__ colstart,
+                                                                    uint32_t* __restrict__ colmax) {
+    __shared__ uint32_t wave_tot[kPtScanThreads / 64];
+    __shared__ uint32_t s_max;
+    if (threadIdx.x == 0) s_max = 0;
+    const uint32_t q = (cols + kPtScanThreads - 1) / kPtScanThreads, c0 = threadIdx.x * q;
+    uint32_t tot[8], sum = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) {
+        tot[i] = 0;
+        const uint32_t c = c0 + i;
+        if (i >= q || c >= cols) continue;
+        for (uint32_t gi = 0; gi < groups; ++gi) {
+            const uint32_t v = R[(uint64_t)gi * cols + c];
+            R[(uint64_t)gi * cols + c] = tot[i];
+            tot[i] += v;
+        }
+        sum += tot[i];
+    }
+    uint32_t mx = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) mx = max(mx, tot[i]);
+    __syncthreads();
+    if (mx) atomicMax(&s_max, mx);
+    uint32_t excl, total;
+    block_scan_n<kPtScanThreads>(sum, excl, total, wave_tot);  // barriers: s_max complete
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) {
+        const uint32_t c = c0 + i;
+        if (i >= q || c >= cols) continue;
+        colstart[c] = excl;
+        for (uint32_t gi = 0; gi < groups; ++gi) R[(uint64_t)gi * cols + c] += excl;
+        excl += tot[i];
+    }
+    if (threadIdx.x == 0) {
+        colstart[cols] = total;
+        *colmax = s_max;
+    }
+}
+
+__global__ __launch_bounds__(kPtThreads) void pt_scatter_kernel(const unsigned long long* __restrict__ in,
+                                                                const unsigned long long* __restrict__ cursor,
+                                                                PtGeom g, const uint32_t* __restrict__ P,
+                                                                uint32_t* __restrict__ out) {
+    __shared__ uint32_t lh[kPtMaxBlocks];
+    __shared__ uint32_t S[kPtTile];
+    __shared__ uint16_t SR[kPtTile];
+    __shared__ uint32_t wave_tot[kPtThreads / 64];
+    const uint32_t j = blockIdx.x, s = blockIdx.y;
+    uint32_t t0;
+    const uint32_t m = pt_tile_keys(cursor, g, s, j, t0);
+    if (m == 0) return;
+    for (uint32_t r = threadIdx.x; r < g.nrb; r += kPtThreads) lh[r] = 0;
+    __syncthreads();
+    const unsigned long long* src = in + s * g.sc + t0;
+    const unsigned sh = g.pbits + g.rbits;
+    const unsigned long long lowm = (1ull << sh) - 1;
+    unsigned long long x[kPtPer];
+    uint32_t rk[kPtPer];
+#pragma unroll
+    for (uint32_t e = 0; e < kPtPer; ++e) {
+        const uint32_t i = threadIdx.x + e * kPtThreads;
+        x[e] = i < m ? src[i] : kNoKey;
+    }
+#pragma unroll
+    for (uint32_t e = 0; e < kPtPer; ++e) rk[e] = x[e] != kNoKey ? atomicAdd(&lh[(uint32_t)(x[e] >> sh)], 1u) : 0u;
+    __syncthreads();
+    lds_bins_scan<kPtThreads>(lh, g.nrb, wave_tot);
+#pragma unroll
+    for (uint32_t e = 0; e < kPtPer; ++e)
+        if (x[e] != kNoKey) {
+            const uint32_t r = (uint32_t)(x[e] >> sh), pos = lh[r] + rk[e];
+            S[pos] = (uint32_t)(x[e] & lowm);
+            SR[pos] = (uint16_t)r;
+        }
+    __syncthreads();
+    const uint32_t* prow = P + (uint64_t)(s * g.jt + j) * g.nrb;
+    for (uint32_t r = threadIdx.x; r < g.nrb; r += kPtThreads) lh[r] = prow[r] - lh[r];
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < m; i += kPtThreads) out[lh[SR[i]] + i] = S[i];
+}
+
+template <uint32_t kE>
+using PtSort = rocprim::block_radix_sort<uint32_t, kPtRThreads, kE>;
+
+struct PtRuns {
+    uint32_t hs[kPtCap + 1];  // rank of each run's first key
+    uint32_t hk[kPtCap];      // the run's key
+};
+union PtReduceLds {
+    typename PtSort<2>::storage_type s2;
+    typename PtSort<4>::storage_type s4;
+    typename PtSort<8>::storage_type s8;
+    typename PtSort<16>::storage_type s16;
+    PtRuns runs;
+};
+
+// row block r's n keys (n <= kE * kPtRThreads): sort, run-length encode, stage the runs
+template <uint32_t kE>
+__device__ __forceinline__ void pt_reduce_block(PtReduceLds& u, typename PtSort<kE>::storage_type& st,
+                                                uint32_t* last, uint32_t* wave_tot, const uint32_t* __restrict__ keys,
+                                                uint32_t r, uint32_t s0, uint32_t n, const PtGeom& g,
+                                                uint32_t* __restrict__ stage_p, uint32_t* __restrict__ stage_q,
+                                                uint32_t* __restrict__ stage_w, uint32_t* __restrict__ counts) {
+    uint32_t k[kE];
+#pragma unroll
+    for (uint32_t e = 0; e < kE; ++e) {
+        const uint32_t i = threadIdx.x + e * kPtRThreads;
+        k[e] = i < n ? keys[s0 + i] : 0xFFFFFFFFu;
+    }
+    PtSort<kE>().sort(k, st, 0, g.pbits + g.rbits);  // blocked: thread t holds ranks t*kE + e
+    last[threadIdx.x] = k[kE - 1];
+    __syncthreads();
+    const uint32_t rank0 = threadIdx.x * kE;
+    uint32_t prev = threadIdx.x ? last[threadIdx.x - 1] : 0u, nh = 0;
+    bool head[kE];
+#pragma unroll
+    for (uint32_t e = 0; e < kE; ++e) {
+        const uint32_t rank = rank0 + e;
+        head[e] = rank < n && (rank == 0 || k[e] != prev);
+        prev = k[e];
+        nh += head[e];
+    }
+    uint32_t base, nruns;
+    block_scan_n<kPtRThreads>(nh, base, nruns, wave_tot);  // barriers: the sort storage is dead
+#pragma unroll
+    for (uint32_t e = 0; e < kE; ++e)
+        if (head[e]) {
+            u.runs.hs[base] = rank0 + e;
+            u.runs.hk[base] = k[e];
+            ++base;
+        }
+    if (threadIdx.x == 0) {
+        u.runs.hs[nruns] = n;
+        counts[r] = nruns;
+    }
+    __syncthreads();
+    const uint32_t qm = (1u << g.pbits) - 1;
+    for (uint32_t i = threadIdx.x; i < nruns; i += kPtRThreads) {
+        const uint32_t key = u.runs.hk[i];
+        stage_p[s0 + i] = (r << g.rbits) | (key >> g.pbits);
+        stage_q[s0 + i] = key & qm;
+        stage_w[s0 + i] = u.runs.hs[i + 1] - u.runs.hs[i];
+    }
+}
+
+// one workgroup per row block; the sort width follows the block's size
+__global__ __launch_bounds__(kPtRThreads) void pt_reduce_kernel(const uint32_t* __restrict__ keys,
+                                                                const uint32_t* __restrict__ bst, PtGeom g,
+                                                                uint32_t* __restrict__ flags,
+                                                                uint32_t* __restrict__ stage_p,
+                                                                uint32_t* __restrict__ stage_q,
+                                                                uint32_t* __restrict__ stage_w,
+                                                                uint32_t* __restrict__ counts) {
+    __shared__ PtReduceLds u;
+    __shared__ uint32_t last[kPtRThreads];
+    __shared__ uint32_t wave_tot[kPtRThreads / 64];
+    const uint32_t r = blockIdx.x, s0 = bst[r], n = bst[r + 1] - s0;
+    if (n == 0 || n > kPtCap) {
+        if (threadIdx.x == 0) {
+            counts[r] = 0;
+            if (n) flags[3] = 1;
+        }
+        return;
+    }
+    if (n <= 2 * kPtRThreads)
+        pt_reduce_block<2>(u, u.s2, last, wave_tot, keys, r, s0, n, g, stage_p, stage_q, stage_w, counts);
+    else if (n <= 4 * kPtRThreads)
+        pt_reduce_block<4>(u, u.s4, last, wave_tot, keys, r, s0, n, g, stage_p, stage_q, stage_w, counts);
+    else if (n <= 8 * kPtRThreads)
+        pt_reduce_block<8>(u, u.s8, last, wave_tot, keys, r, s0, n, g, stage_p, stage_q, stage_w, counts);
+    else
+        pt_reduce_block<16>(u, u.s16, last, wave_tot, keys, r, s0, n, g, stage_p, stage_q, stage_w, counts);
+}
+
+// exclusive scan of the nrb run counts (nrb <= 8 * 1024) -> eoff; eoff[nrb] and *total = edges
+__global__ __launch_bounds__(kPtScanThreads) void pt_offsets_kernel(const uint32_t* __restrict__ counts, uint32_t nrb,
+                                                                    uint32_t* __restrict__ eoff,
+                                                                    uint32_t* __restrict__ total) {
+    __shared__ uint32_t wave_tot[kPtScanThreads / 64];
+    const uint32_t q = (nrb + kPtScanThreads - 1) / kPtScanThreads, c0 = threadIdx.x * q;
+    uint32_t v[8], sum = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) {
+        v[i] = i < q && c0 + i < nrb ? counts[c0 + i] : 0u;
+        sum += v[i];
+    }
+    uint32_t excl, tot;
+    block_scan_n<kPtScanThreads>(sum, excl, tot, wave_tot);
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i)
+        if (i < q && c0 + i < nrb) {
+            eoff[c0 + i] = excl;
+            excl += v[i];
+        }
+    if (threadIdx.x == 0) {
+        eoff[nrb] = tot;
+        *total = tot;
+    }
+}
+
+__global__ __launch_bounds__(256) void pt_emit_kernel(const uint32_t* __restrict__ stage_p,
+                                                      const uint32_t* __restrict__ stage_q,
+                                                      const uint32_t* __restrict__ stage_w,
+                                                      const uint32_t* __restrict__ bst,
+                                                      const uint32_t* __restrict__ counts,
+                                                      const uint32_t* __restrict__ eoff, uint32_t* __restrict__ d_p,
+                                                      uint32_t* __restrict__ d_q, uint32_t* __restrict__ d_w,
+                                                      uint64_t cap) {
+    const uint32_t r = blockIdx.x, s0 = bst[r], m = counts[r];
+    const uint64_t o = eoff[r];
+    for (uint32_t i = threadIdx.x; i < m; i += 256) {
+        if (o + i >= cap) break;
+        d_p[o + i] = stage_p[s0 + i];
+        d_q[o + i] = stage_q[s0 + i];
+        d_w[o + i] = stage_w[s0 + i];
+    }
+}
+
 // ------------------------------------------------------------- fused residue step ----------
 // Bucketed, min_shared == 1, one host synchronisation per call: keys, bucket grouping, group +
 // expand into the kShards regions, the regions' unused tails padded with kNoKey, one radix sort
@@ -1884,7 +2165,7 @@ int tail_pshard(kmp_postings* ws, uint32_t min_shared, uint32_t* d_p, uint32_t* 
 // does not fit -> *fallback (flat rerun); a shard region overflow -> grow and rerun.
 // Marks 0 (start), 1 (keys / level 1), 2 (bucket grouping), 3 (group + expand), 4 (pad),
 // 5 (pair sort), 6 (encode + emit + read-back).
-constexpr uint32_t kRbWords = kShards * 9 + 3;  // gstats (8 per shard) | cursors | flags[0..1] | runs
+constexpr uint32_t kRbWords = kShards * 9 + 5;  // gstats (8 per shard) | cursors | flags[0..1] | runs | flags[3] | row-block max
 
 __global__ void fused_clear_kernel(uint32_t* __restrict__ flags, unsigned long long* __restrict__ gstats) {
     for (uint32_t i = threadIdx.x; i < kShards * 9; i += blockDim.x) gstats[i] = 0;
@@ -1893,12 +2174,57 @@ __global__ void fused_clear_kernel(uint32_t* __restrict__ flags, unsigned long l
 
 __global__ void fused_pack_kernel(const unsigned long long* __restrict__ gstats, const uint32_t* __restrict__ flags,
                                   const uint32_t* __restrict__ runs, unsigned long long* __restrict__ rb) {
+    // runs[0]: run count; runs[1]: largest row block (row-block tail)
     for (uint32_t i = threadIdx.x; i < kShards * 9; i += blockDim.x) rb[i] = gstats[i];
     if (threadIdx.x == 0) {
         rb[kShards * 9] = flags[0];
         rb[kShards * 9 + 1] = flags[1];
         rb[kShards * 9 + 2] = *runs;
+        rb[kShards * 9 + 3] = flags[3];
+        rb[kShards * 9 + 4] = runs[1];
     }
+}
+
+// row-block tail geometry: rows per block so that an average block holds about a quarter of
+// kPtCap keys (from the last call's incidence count, or a guess from the slots); false when the
+// tail does not apply (switched off, an earlier overflow, or keys wider than 32 bits)
+bool pt_geometry(const kmp_postings* ws, uint64_t slots, uint32_t n, PtGeom* g) {
+    if (!ws->pt_on) return false;
+    g->pbits = bits_for(n);
+    const uint64_t est = std::max<uint64_t>(1, ws->pt_inc ? ws->pt_inc : slots / 4);
+    // rows per block ~ (kPtCap / 2.4) * n / est, to the nearest power of two: an average block
+    // of 2.4-4.8K keys; the first rows (p is the smaller index) hold about twice the average
+    const double rows = (double)kPtCap / 2.4 * n / est;
+    unsigned rb = 0;
+    while (rb < 16 && (double)(1u << rb) * 1.41421356 < rows) ++rb;
+    rb = std::min(rb, ws->pt_rb_max);  // learned from overflowing blocks
+    while (rb < 16 && ((n + (1ull << rb) - 1) >> rb) > kPtMaxBlocks) ++rb;
+    if (g->pbits + rb > 32) return false;
+    g->rbits = rb;
+    g->nrb = (uint32_t)((n + (1ull << rb) - 1) >> rb);
+    g->sc = ws->shard_cap;
+    g->jt = (uint32_t)((g->sc + kPtTile - 1) / kPtTile);
+    return true;
+}
+
+// ws->pt: H | P | R | block starts (nrb + 1) | run counts (nrb) | edge offsets (nrb + 1)
+struct PtBufs {
+    uint32_t *H, *P, *R, *bst, *counts, *eoff;
+    uint32_t rows, groups;
+};
+PtBufs pt_bufs(kmp_postings* ws, const PtGeom& g, bool reserve, hipError_t* e) {
+    PtBufs b{};
+    b.rows = kShards * g.jt;
+    b.groups = (b.rows + kBpRowGroup - 1) / kBpRowGroup;
+    const uint64_t h = (uint64_t)b.rows * g.nrb, r = (uint64_t)b.groups * g.nrb;
+    if (reserve) *e = ws->pt.reserve(2 * h + r + 3 * (uint64_t)g.nrb + 2);
+    b.H = ws->pt.p;
+    b.P = b.H + h;
+    b.R = b.P + h;
+    b.bst = b.R + r;
+    b.counts = b.bst + g.nrb + 1;
+    b.eoff = b.counts + g.nrb;
+    return b;
 }
 
 // buffers of one fused step (reserved before any launch, so a capture allocates nothing)
@@ -1910,12 +2236,18 @@ int fused_reserve(kmp_postings* ws, uint64_t slots, const Layout& lay, uint32_t 
     PG(ws->flags.reserve(4));
     PG(ws->cnt.reserve(2 * ((uint64_t)1 << lay.bbits) + 2));
     PG(ws->bstats.reserve(std::max<uint64_t>(ws->bstats.n, kShards * 8 + kShards)));
-    PG(ws->small.reserve(16));
+    PG(ws->small.reserve(16));  // [1] run count, [2] largest row block
     PG(ws->inc_sorted.reserve(total));
     PG(ws->inc.reserve(total));
     PG(ws->uniq.reserve(total));
     PG(ws->w.reserve(total));
     PG(ws->rb.reserve(kRbWords));
+    PtGeom g;
+    if (pt_geometry(ws, slots, n, &g)) {
+        hipError_t e = hipSuccess;
+        pt_bufs(ws, g, true, &e);
+        PG(e);
+    }
     if (!ws->hrb) PG(hipHostMalloc((void**)&ws->hrb, kRbWords * sizeof(unsigned long long), hipHostMallocDefault));
     size_t t2 = 0, t3 = 0;
     PG(rocprim::radix_sort_keys<PairSortCfg>(nullptr, t2, ws->inc_sorted.p, ws->inc.p, (size_t)total, 0u, pair_bits,
@@ -1950,12 +2282,37 @@ int fused_enqueue(kmp_postings* ws, MakeKeys& make_keys, uint64_t slots, const L
     uint32_t* bstart = ws->cnt.p;
     uint32_t* list = ws->cnt.p + nb + 1;
     PShard ps{};
-    launch_bucket_small<false>(nb, st, ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df, ws->inc_sorted.p, sc,
-                               cursor, gstats, flags, list, list_count, ps);
+    PtGeom g;
+    const bool pt = pt_geometry(ws, slots, n, &g);
+    const uint32_t mul = pt ? 1u << g.pbits : n;  // pair key p * mul + q
+    launch_bucket_small<false>(nb, st, ws->sorted.p, bstart, lay, mul, require_class_diff, heavy_df, ws->inc_sorted.p,
+                               sc, cursor, gstats, flags, list, list_count, ps);
     bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeTab, false>
-        <<<256, kBucketLargeThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
+        <<<256, kBucketLargeThreads, 0, st>>>(ws->sorted.p, bstart, lay, mul, require_class_diff, heavy_df,
                                               ws->inc_sorted.p, sc, cursor, gstats, flags, list, list_count, ps);
     ws->mark(3, st);
+    if (pt) {
+        hipError_t e = hipSuccess;
+        const PtBufs b = pt_bufs(ws, g, false, &e);
+        uint32_t* keys32 = reinterpret_cast<uint32_t*>(ws->inc.p);
+        uint32_t* stage_p = reinterpret_cast<uint32_t*>(ws->uniq.p);
+        uint32_t* stage_q = stage_p + total;
+        pt_hist_kernel<<<dim3(g.jt, kShards), kPtThreads, 0, st>>>(ws->inc_sorted.p, cursor, g, b.H);
+        bp_colsum_kernel<<<dim3(b.groups, (g.nrb + 255) / 256), 256, 0, st>>>(b.H, b.rows, g.nrb, b.R);
+        pt_colscan_kernel<<<1, kPtScanThreads, 0, st>>>(b.R, b.groups, g.nrb, b.bst, ws->small.p + 2);
+        bp_colprefix_kernel<<<dim3(b.groups, (g.nrb + 255) / 256), 256, 0, st>>>(b.H, b.rows, g.nrb, b.R, b.P);
+        ws->mark(4, st);
+        pt_scatter_kernel<<<dim3(g.jt, kShards), kPtThreads, 0, st>>>(ws->inc_sorted.p, cursor, g, b.P, keys32);
+        pt_reduce_kernel<<<g.nrb, kPtRThreads, 0, st>>>(keys32, b.bst, g, flags, stage_p, stage_q, ws->w.p, b.counts);
+        ws->mark(5, st);
+        pt_offsets_kernel<<<1, kPtScanThreads, 0, st>>>(b.counts, g.nrb, b.eoff, ws->small.p + 1);
+        pt_emit_kernel<<<g.nrb, 256, 0, st>>>(stage_p, stage_q, ws->w.p, b.bst, b.counts, b.eoff, d_p, d_q, d_w, cap);
+        fused_pack_kernel<<<1, 256, 0, st>>>(gstats, flags, ws->small.p + 1, ws->rb.p);
+        PG(hipMemcpyAsync(ws->hrb, ws->rb.p, kRbWords * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+        ws->mark(6, st);
+        PG(hipGetLastError());
+        return KMP_OK;
+    }
     pad_shards_kernel<<<dim3(route_blocks(sc), kShards), 256, 0, st>>>(ws->inc_sorted.p, sc, cursor);
     ws->mark(4, st);
     size_t t2 = ws->tmp.n, t3 = ws->tmp.n;
@@ -2036,23 +2393,41 @@ int run_fused(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long l
               hipStream_t st) {
     *fallback = false;
     if (ws->shard_cap == 0) ws->shard_cap = slots / 4 / kShards + 4096;
-    for (int attempt = 0; attempt < 3; ++attempt) {
+    // every rerun grows the shard capacity, shrinks the row blocks or leaves the row-block tail,
+    // so a handful of attempts always suffices
+    for (int attempt = 0; attempt < 16; ++attempt) {
         const uint64_t sc = ws->shard_cap, total = sc * kShards;
         {
             int rc = fused_reserve(ws, slots, lay, n);
             if (rc != KMP_OK) return rc;
         }
+        PtGeom pg;
+        const bool pt = pt_geometry(ws, slots, n, &pg);
         key.push_back(sc);
         key.push_back(ws->timing);
+        key.push_back(pt ? pg.rbits + 1 : 0);
         key.push_back(g_grow_gen);
         int rc = fused_launch(ws, make_keys, key, slots, lay, n, heavy_df, require_class_diff, d_p, d_q, d_w, cap, st);
-        key.resize(key.size() - 3);
+        key.resize(key.size() - 4);
         if (rc != KMP_OK) return rc;
         PG(hipStreamSynchronize(st));
         const unsigned long long* g = ws->hrb;
         if (g[kShards * 9] || g[kShards * 9 + 1]) {
             *fallback = true;
             return KMP_OK;
+        }
+        if (pt && g[kShards * 9 + 3]) {
+            // a row block above kPtCap: fewer rows per block (sized from the largest block), or
+            // the global-sort tail from now on when a single row is already too long
+            const double over = (double)g[kShards * 9 + 4] / (0.8 * kPtCap);
+            unsigned shrink = 1;
+            while (shrink < 16 && (double)(1u << shrink) < over) ++shrink;
+            if (pg.rbits == 0) ws->pt_on = false;
+            else ws->pt_rb_max = pg.rbits > shrink ? pg.rbits - shrink : 0u;
+            if (getenv("KMP_DEBUG"))
+                fprintf(stderr, "kmp: row block of %llu keys (rbits %u): rbits bound %u, row tail %d\n",
+                        (unsigned long long)g[kShards * 9 + 4], pg.rbits, ws->pt_rb_max, (int)ws->pt_on);
+            continue;
         }
         unsigned long long acc[kStN] = {}, most = 0, n_inc = 0;
         for (int sh = 0; sh < kShards; ++sh) {
@@ -2063,10 +2438,15 @@ int run_fused(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long l
         }
         const uint64_t h_uniq = g[kShards * 9 + 2];
         ws->shard_cap = most + most / 64 + 256;  // learned capacity for the next call (or the rerun)
-        if (most > sc) continue;                 // a region overflowed: rerun with the new capacity
+        if (most > sc) {                          // a region overflowed: rerun with the new capacity
+            if (getenv("KMP_DEBUG"))
+                fprintf(stderr, "kmp: shard region of %llu keys > %llu: rerun\n", most, (unsigned long long)sc);
+            continue;
+        }
         fill_stats(stats, acc);
         if (stats) stats->incidences = n_inc;
-        const uint64_t ne = h_uniq - (n_inc < total ? 1u : 0u);  // the padding run
+        ws->pt_inc = n_inc;  // sizes the next call's row blocks
+        const uint64_t ne = pt ? h_uniq : h_uniq - (n_inc < total ? 1u : 0u);  // sort tail: the padding run
         if (stats) stats->pairs = ne;
         *n_edges = ne;
         return ne > cap ? KMP_EOVERFLOW : KMP_OK;
