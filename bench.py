@@ -61,11 +61,30 @@ def cpu_baseline(proteins, k, threads):
             "seconds": dt, "edges": int(len(p))}
 
 
-def stage_bytes(n_res, slots, n_inc, n_edges, n_uniq, tail="sort"):
+# names of the six stage-timing slots (kmp_postings_stats.stage_ms) per tail
+STAGE_NAMES = {
+    "rows": ("keys_level1", "buckets_level2", "group_expand", "pair_partition", "pair_sort_rle", "emit"),
+}
+STAGE_NAMES_DEFAULT = ("keys", "code_sort", "count", "write", "pair_sort", "rle_emit")
+
+
+def stage_bytes(n_res, slots, n_inc, n_edges, n_uniq, tail="sort", n_win=None):
     """Algorithmic HBM bytes of each postings stage (one read of every input, one write of
     every output).  The six timing slots of the p-shard tail are keys, bucket sort,
     group + expand (pair keys written to their row ranges), -, row-range reduce (+ offsets),
-    compaction."""
+    compaction.  'rows' (the default residue step): level-1 partition (residues in, one u64 key
+    per window out), level-2 partition (keys in and out), group + expand (keys in, pair keys out),
+    pair-key row-block histogram (pair keys in), scatter + LDS sort + run-length encode (pair keys
+    in, runs out), emit (runs in, edges out)."""
+    if tail == "rows":
+        return {
+            "keys_level1": n_res + 8 * n_win,
+            "buckets_level2": 16 * n_win,
+            "group_expand": 8 * n_win + 8 * n_inc,
+            "pair_partition": 8 * n_inc,
+            "pair_sort_rle": 8 * n_inc + 12 * n_uniq,
+            "emit": 12 * n_uniq + 12 * n_edges,
+        }
     if tail == "fused":
         return {
             "keys": n_res + 8 * slots,
@@ -189,8 +208,11 @@ def main():
             ps = pipe.postings_stats.as_dict()
             slots = int(_lib.lib().kmp_set_capacity(n, int(proteins.offsets[-1])))
             tail = pipe.last_tail()
-            byts = stage_bytes(int(proteins.offsets[-1]), slots, ps["incidences"], n_edges, ps["pairs"], tail)
-            names = ("keys", "code_sort", "count", "write", "pair_sort", "rle_emit")
+            lens = np.diff(np.asarray(proteins.offsets, dtype=np.int64))
+            n_win = int(np.maximum(lens - k + 1, 0).sum())  # windows = keys of the residue path
+            byts = stage_bytes(int(proteins.offsets[-1]), slots, ps["incidences"], n_edges, ps["pairs"], tail,
+                               n_win)
+            names = STAGE_NAMES.get(tail, STAGE_NAMES_DEFAULT)
             stage_ms = dict(zip(names, (stage_sum / args.steps).tolist()))
             stages = {s: {"ms": stage_ms[s], "alg_bytes": byts[s],
                           "GBs": byts[s] / (stage_ms[s] * 1e-3) / 1e9 if stage_ms[s] > 0 else None}
@@ -198,7 +220,7 @@ def main():
             dom = max(stage_ms, key=stage_ms.get)
             ach = stages[dom]["GBs"]
             traffic, source = (pmc_traffic(dom) if args.config == "config3" and args.engine == "residues"
-                               and dom in ("code_sort", "keys") else (None, None))
+                               else (None, None))
             out["roofline"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": source,
                                "traffic_over_alg": traffic / byts[dom] if traffic else None, "kernel": dom,

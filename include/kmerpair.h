@@ -327,7 +327,9 @@ int kmp_postings_set_timing(kmp_postings* ws, int enable);
  * fit (very frequent k-mers) make the call rerun on the flat layout.  0: always flat (full code
  * sort, scan-based expansion).  kmp_postings_last_layout: 0 flat, 1 bucketed with the pair-key
  * sort tail, 2 bucketed with the row-range (p-shard) tail, 3 bucketed single-synchronisation path
- * (min_shared == 1: padded shard regions sorted in place of the gather, one read-back).
+ * (min_shared == 1: padded shard regions sorted in place of the gather, one read-back), 4 the same
+ * single-synchronisation path with the row-block tail (pair keys partitioned by p range, each
+ * range sorted and run-length encoded in LDS; rows too long for LDS send the call to 3).
  * kmp_postings_set_pshard (default 0): 1 makes the bucketed expansion write each pair key into the
  * region of its row range (p >> r), and one workgroup per range sorts, run-length encodes and
  * filters it in LDS instead of the global pair-key sort; ranges above the LDS capacity fall back to

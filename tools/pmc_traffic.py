@@ -32,30 +32,24 @@ def main():
     for r in rows[:20]:
         print(f"{r['kernel'][:52]:<52} {r['grid']:>10} {r['dispatches']:>5} {r['read_bytes']/1e6:>9.1f} "
               f"{r['write_bytes']/1e6:>9.1f}")
-    # per-step traffic of the postings stages (bucketed layout, sort tail): calls = residue_keys
-    # dispatches; of the two radix sorts the one with the larger grid is the bucket (code) sort
-    calls = max([r["dispatches"] for r in rows if r["kernel"] == "residue_keys_kernel"] or [1])
-    sort_grids = sorted({r["grid"] for r in rows if r["kernel"] == "rocprim::radix_sort_onesweep_iteration"})
-    code_grid = sort_grids[-1] if sort_grids else -1
+    # per-step traffic of the residue step's stages (bench.py STAGE_NAMES["rows"]); one
+    # bp_scatter1_kernel dispatch per step
+    calls = max([r["dispatches"] for r in rows if r["kernel"] == "bp_scatter1_kernel"] or [1])
+    by_kernel = {
+        "chunk_first_kernel": "keys_level1", "bp_hist1_kernel": "keys_level1", "bp_colscan_kernel": "keys_level1",
+        "bp_scatter1_kernel": "keys_level1", "bp_colsum_kernel": "keys_level1", "bp_colprefix_kernel": "keys_level1",
+        "bp_hist2_kernel": "buckets_level2", "bp_scan2_kernel": "buckets_level2",
+        "bp_scatter2_kernel": "buckets_level2",
+        "pt_hist_kernel": "pair_partition", "pt_colscan_kernel": "pair_partition",
+        "pt_scatter_kernel": "pair_sort_rle", "pt_reduce_kernel": "pair_sort_rle",
+        "pt_offsets_kernel": "emit", "pt_emit_kernel": "emit", "fused_pack_kernel": "emit",
+    }
 
     def stage(r):
         k = r["kernel"]
-        if k == "residue_keys_kernel" or k == "set_keys_kernel":
-            return "keys"
-        if k.startswith("rocprim::radix_sort_onesweep"):
-            same = [g for g in sort_grids]
-            if k.endswith("iteration"):
-                return "code_sort" if r["grid"] == code_grid else "pair_sort"
-            # histogram kernels: match by the iteration grid they precede (largest = code sort)
-            hist = sorted({x["grid"] for x in rows if x["kernel"] == k and x["read_bytes"] > 0})
-            return "code_sort" if hist and r["grid"] == hist[-1] else ("pair_sort" if r["read_bytes"] > 0 else None)
-        if "bucket_" in k:
-            return "count"
-        if k == "gather_shards_kernel":
-            return "write"
-        if "reduce_by_key" in k or k == "emit_edges_kernel":
-            return "rle_emit"
-        return None
+        if "bucket_small_kernel" in k or "bucket_large_kernel" in k:
+            return "group_expand"
+        return by_kernel.get(k)
 
     stages = collections.defaultdict(lambda: {"read_bytes": 0.0, "write_bytes": 0.0})
     for r in rows:

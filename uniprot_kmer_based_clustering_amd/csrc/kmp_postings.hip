@@ -1163,6 +1163,25 @@ __device__ __forceinline__ void lds_bins_scan(uint32_t* lh, uint32_t nb, uint32_
     __syncthreads();
 }
 
+// in place: x[i * stride] <- run + (exclusive prefix of x[0 .. i)), for i < m; returns the end
+// value.  Loads go out in batches of 8 ahead of the stores (the in-place stores would otherwise
+// serialise every load behind the previous store).
+__device__ __forceinline__ uint32_t col_prefix_inplace(uint32_t* __restrict__ x, uint64_t stride, uint32_t m,
+                                                       uint32_t run) {
+    for (uint32_t i = 0; i < m; i += 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (uint32_t t = 0; t < 8; ++t) v[t] = i + t < m ? x[(i + t) * stride] : 0u;
+#pragma unroll
+        for (uint32_t t = 0; t < 8; ++t)
+            if (i + t < m) {
+                x[(i + t) * stride] = run;
+                run += v[t];
+            }
+    }
+    return run;
+}
+
 // level 1, pass 1: per-chunk digit1 histogram -> H1[chunk][digit]
 __global__ __launch_bounds__(kKeyThreads) void bp_hist1_kernel(
     const uint8_t* __restrict__ res, const uint64_t* __restrict__ res_off, const uint16_t* __restrict__ cls, int k,
@@ -1244,12 +1263,7 @@ __global__ __launch_bounds__(kColThreads) void bp_colscan_kernel(uint32_t* __res
             colstart[c] = tot[c];
             colstart[cols + 1 + c] = cmp[c];
         }
-        uint32_t run = tot[c] + before;
-        for (uint32_t g = g0; g < g1; ++g) {
-            const uint32_t x = R[(uint64_t)g * cols + c];
-            R[(uint64_t)g * cols + c] = run;
-            run += x;
-        }
+        col_prefix_inplace(R + (uint64_t)g0 * cols + c, cols, g1 - g0, tot[c] + before);
     }
     if (threadIdx.x == 0) {
         colstart[cols] = tot[cols - 1] + last;
@@ -1392,13 +1406,9 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scan2_kernel(uint32_t* __restr
     __syncthreads();
     lds_bins_scan(tot, dg.nb2, wave_tot);
     for (uint32_t d = threadIdx.x; d < dg.nb2; d += kKeyThreads) {
-        uint32_t run = b0 + tot[d];
+        const uint32_t run = b0 + tot[d];
         bstart[c * dg.nb2 + d] = run;
-        for (uint32_t j = 0; j < nt; ++j) {
-            const uint32_t v = base[(uint64_t)j * dg.nb2 + d];
-            base[(uint64_t)j * dg.nb2 + d] = run;
-            run += v;
-        }
+        col_prefix_inplace(base + d, dg.nb2, nt, run);
     }
     if (c == gridDim.x - 1 && threadIdx.x == 0) bstart[gridDim.x * dg.nb2] = b0 + n;
 }
@@ -1514,6 +1524,7 @@ struct kmp_postings {
     bool last_bucketed = false; // layout the last call ran on
     bool last_pshard = false;   // ... and whether it finished with the p-shard tail
     bool last_fused = false;    // ... or with the single-synchronisation bucketed path
+    bool last_rows = false;     // ... whose pair keys went through the row-block tail
     uint64_t shard_cap = 0;     // bucketed: capacity of each output shard region
     uint64_t ps_cap = 0;        // p-shard: keys per row-range region
     bool ps_ok = false;         // the last bucketed front end left its keys in row-range regions
@@ -1948,11 +1959,8 @@ __global__ __launch_bounds__(kPtScanThreads) void pt_colscan_kernel(uint32_t* __
         tot[i] = 0;
         const uint32_t c = c0 + i;
         if (i >= q || c >= cols) continue;
-        for (uint32_t gi = 0; gi < groups; ++gi) {
-            const uint32_t v = R[(uint64_t)gi * cols + c];
-            R[(uint64_t)gi * cols + c] = tot[i];
-            tot[i] += v;
-        }
+#pragma unroll 8
+        for (uint32_t gi = 0; gi < groups; ++gi) tot[i] += R[(uint64_t)gi * cols + c];
         sum += tot[i];
     }
     uint32_t mx = 0;
@@ -1967,7 +1975,7 @@ __global__ __launch_bounds__(kPtScanThreads) void pt_colscan_kernel(uint32_t* __
         const uint32_t c = c0 + i;
         if (i >= q || c >= cols) continue;
         colstart[c] = excl;
-        for (uint32_t gi = 0; gi < groups; ++gi) R[(uint64_t)gi * cols + c] += excl;
+        col_prefix_inplace(R + c, cols, groups, excl);
         excl += tot[i];
     }
     if (threadIdx.x == 0) {
@@ -2447,6 +2455,7 @@ int run_fused(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long l
         if (stats) stats->incidences = n_inc;
         ws->pt_inc = n_inc;  // sizes the next call's row blocks
         const uint64_t ne = pt ? h_uniq : h_uniq - (n_inc < total ? 1u : 0u);  // sort tail: the padding run
+        ws->last_rows = pt;
         if (stats) stats->pairs = ne;
         *n_edges = ne;
         return ne > cap ? KMP_EOVERFLOW : KMP_OK;
@@ -2631,7 +2640,7 @@ int kmp_postings_set_layout(kmp_postings* ws, int bucketed) {
 
 int kmp_postings_last_layout(const kmp_postings* ws) {
     if (!ws || !ws->last_bucketed) return 0;
-    return ws->last_fused ? 3 : ws->last_pshard ? 2 : 1;
+    return ws->last_fused ? (ws->last_rows ? 4 : 3) : ws->last_pshard ? 2 : 1;
 }
 
 int kmp_postings_set_pshard(kmp_postings* ws, int enable) {

@@ -239,9 +239,10 @@ class DevicePipeline:
         return "bucketed" if lib().kmp_postings_last_layout(self._workspace()) else "flat"
 
     def last_tail(self) -> str:
-        """How the last postings call reduced its pair keys: 'fused' (bucketed, one host
-        synchronisation), 'pshard' (row-range LDS reduction) or 'sort' (gathered pair-key sort)."""
-        return {3: "fused", 2: "pshard"}.get(lib().kmp_postings_last_layout(self._workspace()), "sort")
+        """How the last postings call reduced its pair keys: 'rows' (bucketed, one host
+        synchronisation, row-block LDS sort tail), 'fused' (the same step with the global pair-key
+        sort tail), 'pshard' (row-range LDS reduction) or 'sort' (gathered pair-key sort)."""
+        return {4: "rows", 3: "fused", 2: "pshard"}.get(lib().kmp_postings_last_layout(self._workspace()), "sort")
 
     def postings(self, min_shared: int = 1, require_class_diff: bool = True,
                  heavy_df: int = 0xFFFFFFFF, from_residues: bool = False) -> int:
