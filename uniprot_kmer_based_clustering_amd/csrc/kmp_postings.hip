@@ -89,6 +89,7 @@ struct Layout {
     unsigned clsbits;  // bucketed: class bits (bits [0, clsbits))
     unsigned hshift;   // bucketed: h(code) starts here (= pbits + clsbits)
     unsigned sort_lo, sort_hi;  // radix-sorted bit range
+    uint32_t mean_keys;         // bucketed: expected keys per bucket (windows / buckets)
 };
 
 #ifndef KMP_BUCKET_TARGET
@@ -110,6 +111,10 @@ Layout make_layout(uint32_t n, int k, uint64_t slots, bool bucketed) {
         l.hshift = l.pbits + l.clsbits;
         l.sort_lo = l.hshift + 32 - bb;
         l.sort_hi = 64;
+        // a protein's slot region (L + 4 slots and more) holds L - k + 1 windows: k + 3 slots at
+        // least hold none, so this is an upper bound of the mean
+        const uint64_t spare = (uint64_t)(k + 3) * n;
+        l.mean_keys = (uint32_t)((slots > spare ? slots - spare : 0ull) >> bb);
         return l;
     }
     l.cls_in_key = l.pbits + kClsBits + l.cbits <= 64;
@@ -632,10 +637,11 @@ __device__ __forceinline__ void process_bucket(
     // H: per slot: (merged: h low bits | count << hb) / group size, then start<<8|size
     __shared__ __attribute__((aligned(16))) uint32_t H[kTab];
     __shared__ uint32_t Bl[kCap];                              // per position: p << cb | class
-    __shared__ uint32_t dupw[kCap / 32];
+    __shared__ uint32_t dupw[kCap / 32];   // per position: a later occurrence of a protein in its group
+    __shared__ uint32_t gdupw[kCap / 32];  // per group start: the group holds such a duplicate
     __shared__ uint32_t SZ[kHeavySub + 1];
     __shared__ uint32_t wave_tot[kThreads / 64];
-    __shared__ uint32_t red[kThreads / 64][8];
+    __shared__ unsigned long long red[kThreads / 64][3];
     __shared__ unsigned long long sbase;
     __shared__ uint32_t heavy;
     const uint32_t s0 = bstart[b], n = bstart[b + 1] - s0;
@@ -660,7 +666,7 @@ __device__ __forceinline__ void process_bucket(
         if (!kMerge) T[tid * kPer + q] = empty;
         H[tid * kPer + q] = kMerge ? kFree : 0u;
     }
-    for (uint32_t i = tid; i < kCap / 32; i += kThreads) dupw[i] = 0;
+    for (uint32_t i = tid; i < kCap / 32; i += kThreads) dupw[i] = gdupw[i] = 0;
     for (uint32_t i = tid; i <= kHeavySub; i += kThreads) SZ[i] = 0;
     if (tid == 0) heavy = 0;
     __syncthreads();
@@ -677,14 +683,18 @@ __device__ __forceinline__ void process_bucket(
         if (i < n) {
             uint32_t slot = (h * 0x85EBCA6Bu) >> (32 - kTabBits);
             if (kMerge) {
+                // a new k-mer goes in with its count already 1 (one atomic: most keys are the
+                // first or only one of their k-mer); a later key of it adds to the count
+                // (inserting a new k-mer with its count already 1 saves an atomic for most keys but
+                // measured 6 % slower: the divergent two-exit loop)
                 const uint32_t hl = h & hm;
                 for (;;) {
                     const uint32_t old = atomicCAS(&H[slot], kFree, hl);
                     if (old == kFree || (old & hm) == hl) break;
                     slot = (slot + 1) & (kTab - 1);
                 }
-                sl[e] = slot;
                 rk[e] = atomicAdd(&H[slot], 1u << hb) >> hb;
+                sl[e] = slot;
             } else {
                 for (;;) {
                     const uint32_t old = atomicCAS(&T[slot], empty, h);
@@ -760,7 +770,8 @@ __device__ __forceinline__ void process_bucket(
         if (tid == 0 && T[0] == 0xFFFFFFFFu && H[1] == 7u) flags[3] = 1;
         return;
     }
-    // D. per position: group bounds, duplicate flag (same protein earlier in the group)
+    // D. per position: group bounds, duplicate flag (same protein earlier in the group: the same
+    // p << cb | class word); a group holding one marks its start in gdupw
     uint32_t s[kE], en[kE];
 #pragma unroll
     for (int e = 0; e < kE; ++e) {
@@ -771,10 +782,10 @@ __device__ __forceinline__ void process_bucket(
         s[e] = g >> 8;
         en[e] = s[e] + (g & 255u);
         xl[e] = Bl[i];
-        const uint32_t p = xl[e] >> cb;
         for (uint32_t j = s[e]; j < i; ++j)
-            if ((Bl[j] >> cb) == p) {
+            if (Bl[j] == xl[e]) {
                 atomicOr(&dupw[i >> 5], 1u << (i & 31));
+                atomicOr(&gdupw[s[e] >> 5], 1u << (s[e] & 31));
                 break;
             }
     }
@@ -784,25 +795,37 @@ __device__ __forceinline__ void process_bucket(
         return;
     }
     auto is_dup = [&](uint32_t j) { return (dupw[j >> 5] >> (j & 31)) & 1u; };
-    // E. df, head, kept-partner count
+    // E. df, head, kept-partner count.  A group without duplicates (almost all) has df = its size
+    // and counts its partners after i only; a group with one walks the whole group.
     uint32_t cnt[kE];
+    bool gd[kE];
     uint32_t st_sum = single, st_dist = single, st_rep = 0, st_cdf2 = 0, st_max = single ? 1u : 0u, st_heavy = 0,
              mine = 0;
 #pragma unroll
     for (int e = 0; e < kE; ++e) {
         const uint32_t i = tid + e * kThreads;
         cnt[e] = 0;
-        if (i >= nm || is_dup(i)) continue;
-        uint32_t f = 1, c = 0;
-        if (en[e] - s[e] > 1) {
+        gd[e] = false;
+        if (i >= nm) continue;
+        gd[e] = (gdupw[s[e] >> 5] >> (s[e] & 31)) & 1u;
+        if (gd[e] && is_dup(i)) continue;
+        uint32_t f, c = 0;
+        if (!gd[e]) {
+            f = en[e] - s[e];
+            if (require_diff) {
+                for (uint32_t j = i + 1; j < en[e]; ++j) c += ((Bl[j] ^ xl[e]) & cmask) != 0u;
+            } else {
+                c = en[e] - 1 - i;
+            }
+        } else {
             f = 0;
             for (uint32_t j = s[e]; j < en[e]; ++j) {
                 if (is_dup(j)) continue;
                 ++f;
                 if (j > i && (!require_diff || ((Bl[j] ^ xl[e]) & cmask))) ++c;
             }
-            if (f > heavy_df) c = 0;
         }
+        if (f > heavy_df) c = 0;
         st_sum += 1;
         if (i == s[e]) {  // the group's first position is never a duplicate
             st_dist += 1;
@@ -818,27 +841,42 @@ __device__ __forceinline__ void process_bucket(
         if (tid == 0 && mine == 0xFFFFFFFFu) flags[3] = 1;
         return;
     }
-    // statistics (u32 per workgroup; the bucket is at most kCap keys): wave partials -> red, then
-    // kStN threads sum them and post one (sharded) atomic each
+    // statistics: three wave reductions of packed words (per workgroup every count is at most
+    // kCap, so 16-bit fields cannot carry; C(df,2) and the incidences stay below 2^32), wave
+    // partials -> red, then kStN threads unpack, sum and post one (sharded) atomic each
     auto wave_stats = [&]() {
-        uint32_t sv[kStN] = {st_sum, st_dist, st_rep, st_cdf2, st_max, st_heavy, mine};
-#pragma unroll
-        for (int t = 0; t < kStN; ++t) {
-            uint32_t v = sv[t];
-            for (int sh = 32; sh > 0; sh >>= 1) {
-                const uint32_t u = __shfl_down(v, sh);
-                v = t == kStMaxDf ? max(u, v) : u + v;
-            }
-            if ((tid & 63) == 0) red[tid >> 6][t] = v;
+        unsigned long long a = st_sum | (unsigned long long)st_dist << 16 | (unsigned long long)st_rep << 32 |
+                               (unsigned long long)st_heavy << 48;
+        unsigned long long c2 = st_cdf2 | (unsigned long long)mine << 32;
+        uint32_t mx = st_max;
+        for (int sh = 32; sh > 0; sh >>= 1) {
+            a += __shfl_down(a, sh);
+            c2 += __shfl_down(c2, sh);
+            mx = max(mx, (uint32_t)__shfl_down(mx, sh));
+        }
+        if ((tid & 63) == 0) {
+            red[tid >> 6][0] = a;
+            red[tid >> 6][1] = c2;
+            red[tid >> 6][2] = mx;
         }
     };
     auto post_stats = [&]() {
         if (tid < kStN) {
-            uint32_t v = red[0][tid];
-            for (int w = 1; w < kThreads / 64; ++w) v = tid == kStMaxDf ? max(v, red[w][tid]) : v + red[w][tid];
+            unsigned long long v = 0;
+            for (int w = 0; w < kThreads / 64; ++w) {
+                const unsigned long long a = red[w][0], c2 = red[w][1], mx = red[w][2];
+                const unsigned long long x = tid == kStSumS     ? a & 0xFFFF
+                                             : tid == kStDistinct ? (a >> 16) & 0xFFFF
+                                             : tid == kStRepeat   ? (a >> 32) & 0xFFFF
+                                             : tid == kStHeavy    ? a >> 48
+                                             : tid == kStCdf2     ? c2 & 0xFFFFFFFFull
+                                             : tid == kStInc      ? c2 >> 32
+                                                                  : mx;
+                v = tid == kStMaxDf ? (v > x ? v : x) : v + x;
+            }
             unsigned long long* g = gstats + (uint64_t)(b % kShards) * 8 + tid;  // sharded: no hot word
-            if (tid == kStMaxDf) atomicMax(g, (unsigned long long)v);
-            else if (v) atomicAdd(g, (unsigned long long)v);
+            if (tid == kStMaxDf) atomicMax(g, v);
+            else if (v) atomicAdd(g, v);
         }
     };
     // F. write the pair keys
@@ -850,7 +888,7 @@ __device__ __forceinline__ void process_bucket(
                 const uint32_t i = tid + e * kThreads;
                 const uint32_t p = xl[e] >> cb;
                 for (uint32_t j = i + 1; j < en[e]; ++j) {
-                    if (is_dup(j)) continue;
+                    if (gd[e] && is_dup(j)) continue;
                     const uint32_t lj = Bl[j];
                     if (require_diff && !((lj ^ xl[e]) & cmask)) continue;
                     const uint32_t q = lj >> cb;
@@ -881,7 +919,7 @@ __device__ __forceinline__ void process_bucket(
                 const uint32_t i = tid + e * kThreads;
                 const uint32_t p = xl[e] >> cb;
                 for (uint32_t j = i + 1; j < en[e]; ++j) {
-                    if (is_dup(j)) continue;
+                    if (gd[e] && is_dup(j)) continue;
                     const uint32_t lj = Bl[j];
                     if (require_diff && !((lj ^ xl[e]) & cmask)) continue;
                     const uint32_t q = lj >> cb;
@@ -1447,14 +1485,24 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scatter2_kernel(const unsigned
     bp_place(x, r, tn, dg.nb2, digit, lh, wave_tot, S, P2 + ((uint64_t)c * J + j) * dg.nb2, out);
 }
 
-// the small bucket kernel for this layout: merged slot words when the bucket field is wide enough
+// the small bucket kernel for this layout: merged slot words when the bucket field is wide enough;
+// a 1,024-key capacity (four keys per thread) when the mean bucket is small enough that a bucket
+// above it is a > 4-sigma event (the large kernel takes those)
+#ifndef KMP_CAP1024_MEAN
+#define KMP_CAP1024_MEAN 800  // at config 3 (mean 897) the 1,280 variant measured faster
+#endif
+constexpr uint32_t kBucketCap1024Mean = KMP_CAP1024_MEAN;
 template <bool kPShard>
 void launch_bucket_small(uint32_t grid, hipStream_t st, const unsigned long long* sorted, const uint32_t* bstart,
                          const Layout& lay, uint32_t n, int require_diff, uint32_t heavy_df,
                          unsigned long long* out, uint64_t shard_cap, unsigned long long* cursor,
                          unsigned long long* gstats, uint32_t* flags, uint32_t* list, uint32_t* list_count,
                          const PShard& ps, uint32_t b0 = 0) {
-    if (lay.bbits >= kMergeMinBits)
+    if (lay.bbits >= kMergeMinBits && lay.mean_keys <= kBucketCap1024Mean)  // four keys per thread
+        bucket_small_kernel<1024, kBucketSmallThreads, kBucketSmallTab, kPShard, true>
+            <<<grid, kBucketSmallThreads, 0, st>>>(sorted, bstart, lay, n, require_diff, heavy_df, out, shard_cap,
+                                                   cursor, gstats, flags, list, list_count, ps, b0);
+    else if (lay.bbits >= kMergeMinBits)
         bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallTab, kPShard, true>
             <<<grid, kBucketSmallThreads, 0, st>>>(sorted, bstart, lay, n, require_diff, heavy_df, out, shard_cap,
                                                    cursor, gstats, flags, list, list_count, ps, b0);
