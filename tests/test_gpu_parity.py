@@ -412,6 +412,10 @@ def _dist_gpu_worker(rank, world, port, out_q):
             out_q.put(("edges", n, [a.tolist() for a in pipe.edges()]))
         else:
             out_q.put(("rank", rank, n))
+    except Exception as e:  # report instead of leaving the test waiting on its queue
+        import traceback
+        out_q.put(("error", rank, f"{e!r}\n{traceback.format_exc()}"))
+        raise
     finally:
         dist.destroy_process_group()
 
@@ -430,7 +434,15 @@ def test_distributed_postings_on_device(oracle_mod, world):
     procs = [ctx.Process(target=_dist_gpu_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    msgs = [q.get(timeout=300) for _ in range(world)]  # drain before join: a queued message blocks exit
+    msgs = []
+    for _ in range(world):  # drain before join: a queued message blocks exit
+        msgs.append(q.get(timeout=150))
+        if msgs[-1][0] == "error":
+            for p in procs:
+                p.join(timeout=30)
+                if p.is_alive():
+                    p.kill()
+            pytest.fail(f"rank {msgs[-1][1]}: {msgs[-1][2]}")
     for p in procs:
         p.join(timeout=60)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]

@@ -43,7 +43,7 @@ def main():
             sends2 = [st.pairs_route(recvs[r], r, world).clone() for r in range(world)]
             cp = st.cap_pairs
             recv2 = torch.cat([s[0:cp] for s in sends2])
-            e, cnt = st.edges_route(recv2)
+            e, cnt = st.edges_route(recv2, 0, world)
             flags = st.flags.cpu().numpy()
             if flags[0] or flags[3]:
                 st.grow(flags)
@@ -52,7 +52,7 @@ def main():
         lo, hi = sl[0]
         t1, _ = timed(lambda: st.keys_route(lo, hi, world))
         t2, _ = timed(lambda: st.pairs_route(recvs[0], 0, world))
-        t3, _ = timed(lambda: st.edges_route(recv2))
+        t3, _ = timed(lambda: st.edges_route(recv2, 0, world))
         print(f"world={world} rank0: keys_route {t1:.3f} ms  pairs_route {t2:.3f} ms  edges_route {t3:.3f} ms  "
               f"total {t1 + t2 + t3:.3f} ms | exchange bytes/rank: keys {world * ck * 8 / 1e6:.1f} MB, "
               f"pairs {world * cp * 8 / 1e6:.1f} MB | edges rank0 {int(cnt.item())}")

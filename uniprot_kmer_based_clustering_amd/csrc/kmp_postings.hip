@@ -1485,6 +1485,52 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scatter2_kernel(const unsigned
     bp_place(x, r, tn, dg.nb2, digit, lh, wave_tot, S, P2 + ((uint64_t)c * J + j) * dg.nb2, out);
 }
 
+// Level 1 from a key array instead of the residues (the multi-GPU owner's received keys, kNoKey
+// padding skipped): 4,096-key tiles, digit1 histogram -> H1[tile][digit], then the same column
+// scan and an LDS-ranked scatter into digit-major runs.
+__global__ __launch_bounds__(kKeyThreads) void bp_hist_arr_kernel(const unsigned long long* __restrict__ in,
+                                                                  uint64_t m, BpDigits dg, uint32_t* __restrict__ H1) {
+    __shared__ uint32_t lh[kBpMaxBins];
+    const uint64_t t0 = (uint64_t)blockIdx.x * kBpTile;
+    const uint32_t tn = (uint32_t)min<uint64_t>(kBpTile, m - t0);
+    for (uint32_t d = threadIdx.x; d < dg.nb1; d += kKeyThreads) lh[d] = 0;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < tn; i += kKeyThreads) {
+        const unsigned long long x = in[t0 + i];
+        if (x != kNoKey) atomicAdd(&lh[(uint32_t)(x >> dg.sh1)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < dg.nb1; d += kKeyThreads) H1[(uint64_t)blockIdx.x * dg.nb1 + d] = lh[d];
+}
+
+__global__ __launch_bounds__(kKeyThreads) void bp_scatter_arr_kernel(const unsigned long long* __restrict__ in,
+                                                                     uint64_t m, BpDigits dg,
+                                                                     const uint32_t* __restrict__ P1,
+                                                                     unsigned long long* __restrict__ out) {
+    __shared__ unsigned long long S[kBpTile];
+    __shared__ uint32_t lh[kBpMaxBins];
+    __shared__ uint32_t wave_tot[kKeyThreads / 64];
+    __shared__ uint32_t s_n;
+    const uint64_t t0 = (uint64_t)blockIdx.x * kBpTile;
+    const uint32_t tn = (uint32_t)min<uint64_t>(kBpTile, m - t0);
+    for (uint32_t d = threadIdx.x; d < dg.nb1; d += kKeyThreads) lh[d] = 0;
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
+    unsigned long long x[kBpPer];
+    uint32_t r[kBpPer], nk = 0;
+    auto digit = [&](unsigned long long y) { return (uint32_t)(y >> dg.sh1); };
+#pragma unroll
+    for (uint32_t e = 0; e < kBpPer; ++e) {
+        const uint32_t i = threadIdx.x + e * kKeyThreads;
+        x[e] = i < tn ? in[t0 + i] : kNoKey;
+        r[e] = x[e] != kNoKey ? atomicAdd(&lh[digit(x[e])], 1u) : 0u;
+        nk += x[e] != kNoKey;
+    }
+    if (nk) atomicAdd(&s_n, nk);
+    __syncthreads();
+    bp_place(x, r, s_n, dg.nb1, digit, lh, wave_tot, S, P1 + (uint64_t)blockIdx.x * dg.nb1, out);
+}
+
 // the small bucket kernel for this layout: merged slot words when the bucket field is wide enough;
 // a 1,024-key capacity (four keys per thread) when the mean bucket is small enough that a bucket
 // above it is a > 4-sigma event (the large kernel takes those)
@@ -1586,6 +1632,7 @@ struct kmp_postings {
     uint64_t pt_inc = 0;        // incidences of the last fused call (row-block sizing)
     unsigned pt_rb_max = 16;    // rows-per-block bound learned from overflowing row blocks
     uint32_t bp_J = 0;          // level-2 tiles per coarse bin
+    uint64_t bp_c1 = 0;         // offset of C1 (coarse bin starts) in ws->bp
     bool partition = !getenv("KMP_PARTITION") || atoi(getenv("KMP_PARTITION")) != 0;  // residue keys: counting partition
     bool parted = false;        // ws->keys holds level-1 output (bp_level1 ran for this call)
     // fused residue step as a HIP graph: captured on the second call with the same shape
@@ -1653,6 +1700,7 @@ hipError_t bp_level1(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_r
     if (e == hipSuccess) e = ws->chunk_first.reserve(G + 1);
     if (e != hipSuccess) return e;
     uint32_t *H1 = ws->bp.p, *P1 = H1 + h1, *R = P1 + h1, *C1 = R + r;
+    ws->bp_c1 = 2 * h1 + r;
     chunk_first_kernel<<<(n + 1 + 255) / 256, 256, 0, st>>>(d_res_off, 0u, n, 0ull, slots, G, ws->chunk_first.p);
     const uint32_t pw21 = (uint32_t)pow21(k - 1);
     bp_hist1_kernel<<<G, kKeyThreads, 0, st>>>(d_res, d_res_off, d_class, k, n, slots, ws->chunk_first.p, lay, dg,
@@ -1665,12 +1713,36 @@ hipError_t bp_level1(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_r
     return hipGetLastError();
 }
 
-// Level 2: ws->keys (level 1) -> ws->sorted grouped by bucket, bstart[0..nb] in ws->cnt.
-int bp_level2(kmp_postings* ws, uint64_t slots, const Layout& lay, hipStream_t st) {
+// Level 1 from a key array of m entries (kNoKey padding skipped) -> ws->keys, C1 for level 2.
+// The keys fall in `bins` of the nb1 coarse bins (a multi-GPU owner holds only its bucket
+// range), which sets level 2's tile budget per bin.
+hipError_t bp_level1_array(kmp_postings* ws, const unsigned long long* d_keys, uint64_t m, const Layout& lay,
+                           uint32_t bins, hipStream_t st) {
     const BpDigits dg = bp_digits(lay);
-    const uint32_t G = (uint32_t)((slots + kKeyChunk - 1) / kKeyChunk), groups = (G + kBpRowGroup - 1) / kBpRowGroup;
-    const uint64_t h1 = (uint64_t)G * dg.nb1, r = (uint64_t)groups * dg.nb1;
-    uint32_t* C1 = ws->bp.p + 2 * h1 + r;
+    const uint64_t T64 = (m + kBpTile - 1) / kBpTile;
+    if (T64 * dg.nb1 > 0xFFFFFFFFull || m > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    const uint32_t T = (uint32_t)T64, groups = (T + kBpRowGroup - 1) / kBpRowGroup;
+    bins = std::max(1u, std::min(bins, dg.nb1));
+    ws->bp_J = (uint32_t)((m / bins * 5 / 4 + kBpTile - 1) / kBpTile) + 2;
+    const uint64_t h1 = (uint64_t)T * dg.nb1, r = (uint64_t)groups * dg.nb1;
+    const uint64_t need = 2 * h1 + r + 2 * (dg.nb1 + 1) + (uint64_t)dg.nb1 * ws->bp_J * dg.nb2;
+    hipError_t e = ws->bp.reserve(need);
+    if (e == hipSuccess) e = ws->keys.reserve(m + (uint64_t)kBpAlign * dg.nb1);
+    if (e != hipSuccess) return e;
+    uint32_t *H1 = ws->bp.p, *P1 = H1 + h1, *R = P1 + h1, *C1 = R + r;
+    ws->bp_c1 = 2 * h1 + r;
+    bp_hist_arr_kernel<<<T, kKeyThreads, 0, st>>>(d_keys, m, dg, H1);
+    bp_colsum_kernel<<<dim3(groups, (dg.nb1 + 255) / 256), 256, 0, st>>>(H1, T, dg.nb1, R);
+    bp_colscan_kernel<<<1, kColThreads, 0, st>>>(R, groups, dg.nb1, C1);
+    bp_colprefix_kernel<<<dim3(groups, (dg.nb1 + 255) / 256), 256, 0, st>>>(H1, T, dg.nb1, R, P1);
+    bp_scatter_arr_kernel<<<T, kKeyThreads, 0, st>>>(d_keys, m, dg, P1, ws->keys.p);
+    return hipGetLastError();
+}
+
+// Level 2: ws->keys (level 1) -> ws->sorted grouped by bucket, bstart[0..nb] in ws->cnt.
+int bp_level2(kmp_postings* ws, const Layout& lay, hipStream_t st) {
+    const BpDigits dg = bp_digits(lay);
+    uint32_t* C1 = ws->bp.p + ws->bp_c1;
     uint32_t* H2 = C1 + 2 * (dg.nb1 + 1);
     const uint32_t nb = 1u << lay.bbits, J = ws->bp_J;
     PG(ws->cnt.reserve(2 * (uint64_t)nb + 2));
@@ -1689,7 +1761,7 @@ int bucket_group(kmp_postings* ws, const unsigned long long* in, uint64_t slots,
     PG(ws->sorted.reserve(slots));
     if (ws->parted && in == ws->keys.p) {
         ws->parted = false;
-        int rc = bp_level2(ws, slots, lay, st);
+        int rc = bp_level2(ws, lay, st);
         ws->mark(2, st);
         return rc;
     }
@@ -1960,14 +2032,17 @@ constexpr uint32_t kPtMaxBlocks = 8192;  // row blocks (LDS histogram of pt_hist
 
 struct PtGeom {
     unsigned pbits, rbits;  // key = p << pbits | q; rows per block = 1 << rbits
-    uint32_t nrb;           // row blocks
+    uint32_t nrb;           // row blocks, from row row0
     uint32_t jt;            // tiles per shard region
     uint64_t sc;            // shard region capacity
+    uint32_t nshards;       // shard regions (kShards), or 1 for a flat array
+    uint32_t row0;          // first row (a multi-GPU owner's row range)
+    uint64_t flat_n;        // nonzero: one region of flat_n keys with kNoKey padding (no cursors)
 };
 
 __device__ __forceinline__ uint32_t pt_tile_keys(const unsigned long long* __restrict__ cursor, const PtGeom& g,
                                                  uint32_t s, uint32_t j, uint32_t& t0) {
-    const uint64_t ns = min<unsigned long long>(cursor[s], g.sc);
+    const uint64_t ns = g.flat_n ? g.flat_n : min<unsigned long long>(cursor[s], g.sc);
     t0 = j * kPtTile;
     return t0 < ns ? (uint32_t)min<uint64_t>(kPtTile, ns - t0) : 0u;
 }
@@ -1983,7 +2058,11 @@ __global__ __launch_bounds__(kPtThreads) void pt_hist_kernel(const unsigned long
     const uint32_t m = pt_tile_keys(cursor, g, s, j, t0);
     const unsigned long long* src = in + s * g.sc + t0;
     const unsigned sh = g.pbits + g.rbits;
-    for (uint32_t i = threadIdx.x; i < m; i += kPtThreads) atomicAdd(&lh[(uint32_t)(src[i] >> sh)], 1u);
+    const unsigned long long base = (unsigned long long)g.row0 << g.pbits;
+    for (uint32_t i = threadIdx.x; i < m; i += kPtThreads) {
+        const unsigned long long x = src[i];
+        if (x != kNoKey) atomicAdd(&lh[(uint32_t)((x - base) >> sh)], 1u);
+    }
     __syncthreads();
     uint32_t* row = H + (uint64_t)(s * g.jt + j) * g.nrb;
     for (uint32_t r = threadIdx.x; r < g.nrb; r += kPtThreads) row[r] = lh[r];
@@ -2040,24 +2119,33 @@ __global__ __launch_bounds__(kPtThreads) void pt_scatter_kernel(const unsigned l
     __shared__ uint32_t S[kPtTile];
     __shared__ uint16_t SR[kPtTile];
     __shared__ uint32_t wave_tot[kPtThreads / 64];
+    __shared__ uint32_t s_n;
     const uint32_t j = blockIdx.x, s = blockIdx.y;
     uint32_t t0;
     const uint32_t m = pt_tile_keys(cursor, g, s, j, t0);
     if (m == 0) return;
     for (uint32_t r = threadIdx.x; r < g.nrb; r += kPtThreads) lh[r] = 0;
+    if (threadIdx.x == 0) s_n = 0;
     __syncthreads();
     const unsigned long long* src = in + s * g.sc + t0;
     const unsigned sh = g.pbits + g.rbits;
     const unsigned long long lowm = (1ull << sh) - 1;
+    const unsigned long long base = (unsigned long long)g.row0 << g.pbits;
     unsigned long long x[kPtPer];
     uint32_t rk[kPtPer];
 #pragma unroll
     for (uint32_t e = 0; e < kPtPer; ++e) {
         const uint32_t i = threadIdx.x + e * kPtThreads;
         x[e] = i < m ? src[i] : kNoKey;
+        if (x[e] != kNoKey) x[e] -= base;  // rows from row0
     }
+    uint32_t nk = 0;
 #pragma unroll
-    for (uint32_t e = 0; e < kPtPer; ++e) rk[e] = x[e] != kNoKey ? atomicAdd(&lh[(uint32_t)(x[e] >> sh)], 1u) : 0u;
+    for (uint32_t e = 0; e < kPtPer; ++e) {
+        rk[e] = x[e] != kNoKey ? atomicAdd(&lh[(uint32_t)(x[e] >> sh)], 1u) : 0u;
+        nk += x[e] != kNoKey;
+    }
+    if (nk) atomicAdd(&s_n, nk);
     __syncthreads();
     lds_bins_scan<kPtThreads>(lh, g.nrb, wave_tot);
 #pragma unroll
@@ -2071,7 +2159,8 @@ __global__ __launch_bounds__(kPtThreads) void pt_scatter_kernel(const unsigned l
     const uint32_t* prow = P + (uint64_t)(s * g.jt + j) * g.nrb;
     for (uint32_t r = threadIdx.x; r < g.nrb; r += kPtThreads) lh[r] = prow[r] - lh[r];
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < m; i += kPtThreads) out[lh[SR[i]] + i] = S[i];
+    const uint32_t placed = s_n;  // m counts the kNoKey padding of a flat array too
+    for (uint32_t i = threadIdx.x; i < placed; i += kPtThreads) out[lh[SR[i]] + i] = S[i];
 }
 
 template <uint32_t kE>
@@ -2132,7 +2221,7 @@ __device__ __forceinline__ void pt_reduce_block(PtReduceLds& u, typename PtSort<
     const uint32_t qm = (1u << g.pbits) - 1;
     for (uint32_t i = threadIdx.x; i < nruns; i += kPtRThreads) {
         const uint32_t key = u.runs.hk[i];
-        stage_p[s0 + i] = (r << g.rbits) | (key >> g.pbits);
+        stage_p[s0 + i] = g.row0 + ((r << g.rbits) | (key >> g.pbits));
         stage_q[s0 + i] = key & qm;
         stage_w[s0 + i] = u.runs.hs[i + 1] - u.runs.hs[i];
     }
@@ -2170,7 +2259,8 @@ __global__ __launch_bounds__(kPtRThreads) void pt_reduce_kernel(const uint32_t* 
 // exclusive scan of the nrb run counts (nrb <= 8 * 1024) -> eoff; eoff[nrb] and *total = edges
 __global__ __launch_bounds__(kPtScanThreads) void pt_offsets_kernel(const uint32_t* __restrict__ counts, uint32_t nrb,
                                                                     uint32_t* __restrict__ eoff,
-                                                                    uint32_t* __restrict__ total) {
+                                                                    uint32_t* __restrict__ total,
+                                                                    unsigned long long* __restrict__ total64 = nullptr) {
     __shared__ uint32_t wave_tot[kPtScanThreads / 64];
     const uint32_t q = (nrb + kPtScanThreads - 1) / kPtScanThreads, c0 = threadIdx.x * q;
     uint32_t v[8], sum = 0;
@@ -2190,6 +2280,7 @@ __global__ __launch_bounds__(kPtScanThreads) void pt_offsets_kernel(const uint32
     if (threadIdx.x == 0) {
         eoff[nrb] = tot;
         *total = tot;
+        if (total64) *total64 = tot;
     }
 }
 
@@ -2260,6 +2351,9 @@ bool pt_geometry(const kmp_postings* ws, uint64_t slots, uint32_t n, PtGeom* g) 
     g->nrb = (uint32_t)((n + (1ull << rb) - 1) >> rb);
     g->sc = ws->shard_cap;
     g->jt = (uint32_t)((g->sc + kPtTile - 1) / kPtTile);
+    g->nshards = kShards;
+    g->row0 = 0;
+    g->flat_n = 0;
     return true;
 }
 
@@ -2270,7 +2364,7 @@ struct PtBufs {
 };
 PtBufs pt_bufs(kmp_postings* ws, const PtGeom& g, bool reserve, hipError_t* e) {
     PtBufs b{};
-    b.rows = kShards * g.jt;
+    b.rows = g.nshards * g.jt;
     b.groups = (b.rows + kBpRowGroup - 1) / kBpRowGroup;
     const uint64_t h = (uint64_t)b.rows * g.nrb, r = (uint64_t)b.groups * g.nrb;
     if (reserve) *e = ws->pt.reserve(2 * h + r + 3 * (uint64_t)g.nrb + 2);
@@ -2353,12 +2447,12 @@ int fused_enqueue(kmp_postings* ws, MakeKeys& make_keys, uint64_t slots, const L
         uint32_t* keys32 = reinterpret_cast<uint32_t*>(ws->inc.p);
         uint32_t* stage_p = reinterpret_cast<uint32_t*>(ws->uniq.p);
         uint32_t* stage_q = stage_p + total;
-        pt_hist_kernel<<<dim3(g.jt, kShards), kPtThreads, 0, st>>>(ws->inc_sorted.p, cursor, g, b.H);
+        pt_hist_kernel<<<dim3(g.jt, g.nshards), kPtThreads, 0, st>>>(ws->inc_sorted.p, cursor, g, b.H);
         bp_colsum_kernel<<<dim3(b.groups, (g.nrb + 255) / 256), 256, 0, st>>>(b.H, b.rows, g.nrb, b.R);
         pt_colscan_kernel<<<1, kPtScanThreads, 0, st>>>(b.R, b.groups, g.nrb, b.bst, ws->small.p + 2);
         bp_colprefix_kernel<<<dim3(b.groups, (g.nrb + 255) / 256), 256, 0, st>>>(b.H, b.rows, g.nrb, b.R, b.P);
         ws->mark(4, st);
-        pt_scatter_kernel<<<dim3(g.jt, kShards), kPtThreads, 0, st>>>(ws->inc_sorted.p, cursor, g, b.P, keys32);
+        pt_scatter_kernel<<<dim3(g.jt, g.nshards), kPtThreads, 0, st>>>(ws->inc_sorted.p, cursor, g, b.P, keys32);
         pt_reduce_kernel<<<g.nrb, kPtRThreads, 0, st>>>(keys32, b.bst, g, flags, stage_p, stage_q, ws->w.p, b.counts);
         ws->mark(5, st);
         pt_offsets_kernel<<<1, kPtScanThreads, 0, st>>>(b.counts, g.nrb, b.eoff, ws->small.p + 1);
@@ -2878,7 +2972,7 @@ __global__ void route_kernel(const unsigned long long* __restrict__ sorted,
 // Partition into `parts` padded regions without sorting.  Destination of a key:
 //   kPairs == false (k-mer keys):  bucket = key >> shift, valid iff bucket < total,
 //                                  dest = bucket * parts / total (contiguous bucket ranges);
-//   kPairs == true  (pair keys):   valid iff key != kNoKey, p = key / total, dest = the row range
+//   kPairs == true  (pair keys):   valid iff key != kNoKey, p = key >> shift, dest = the row range
 //                                  [rows[d], rows[d+1]) holding p (contiguous row ranges, so the
 //                                  rank-order concatenation stays canonical).
 // Each workgroup ranks its 4096 keys per destination in LDS and reserves one range per
@@ -2913,7 +3007,7 @@ __global__ __launch_bounds__(kPartThreads) void partition_kernel(const unsigned 
         unsigned long long v;
         if (kPairs) {
             valid = x[j] != kNoKey;
-            v = valid ? x[j] / total : 0;
+            v = valid ? x[j] >> shift : 0;
         } else {
             v = x[j] >> shift;
             valid = i < m && v < total;
@@ -3050,14 +3144,23 @@ int kmp_dev_pairs_route(kmp_postings* ws, const unsigned long long* d_keys, uint
     if (heavy_df < 2) heavy_df = 2;
     PG(ws->flags.reserve(4));
     PG(hipMemsetAsync(ws->flags.p, 0, 4 * sizeof(uint32_t), st));
-    // group + expand (the fused path's kernels, no read-back)
-    PG(ws->sorted.reserve(std::max<uint64_t>(1, m)));
-    if (m) {
-        int rc = sort_keys(ws, d_keys, ws->sorted.p, m, lay.sort_lo, lay.sort_hi, st);
-        if (rc != KMP_OK) return rc;
-    }
+    // group + expand (the fused path's kernels, no read-back): the received keys grouped by
+    // bucket with the counting partition (level 1 from the array, then level 2)
     const uint32_t nb = 1u << lay.bbits;
+    PG(ws->sorted.reserve(std::max<uint64_t>(1, m)));
     PG(ws->cnt.reserve(2 * (uint64_t)nb + 2));
+    // this part's bucket range (the keys routed here hold no others)
+    const uint32_t b0 = (uint32_t)(((uint64_t)part * nb + parts - 1) / parts);
+    const uint32_t b1 = (uint32_t)(((uint64_t)(part + 1) * nb + parts - 1) / parts);
+    if (m) {
+        const unsigned d2 = lay.bbits / 2;  // bp_digits: coarse bin = bucket >> d2
+        const uint32_t bins = b1 > b0 ? ((b1 - 1) >> d2) - (b0 >> d2) + 1 : 1u;
+        PG(bp_level1_array(ws, d_keys, m, lay, bins, st));
+        int rc = bp_level2(ws, lay, st);
+        if (rc != KMP_OK) return rc;
+    } else {
+        PG(hipMemsetAsync(ws->cnt.p, 0, (nb + 1) * sizeof(uint32_t), st));
+    }
     PG(ws->bstats.reserve(std::max<uint64_t>(ws->bstats.n, kShards * 8 + kShards + parts + 1)));
     uint32_t* bstart = ws->cnt.p;
     uint32_t* list = ws->cnt.p + nb + 1;
@@ -3069,15 +3172,14 @@ int kmp_dev_pairs_route(kmp_postings* ws, const unsigned long long* d_keys, uint
     PG(ws->inc_sorted.reserve(total));
     PG(ws->inc.reserve(total));
     PG(hipMemsetAsync(gstats, 0, (kShards * 8 + kShards) * sizeof(unsigned long long), st));
-    bucket_bounds_kernel<<<(nb + 1 + 255) / 256, 256, 0, st>>>(ws->sorted.p, m, lay.sort_lo, nb, bstart);
     PShard ps{};
-    // this part's bucket range (the keys routed here hold no others)
-    const uint32_t b0 = (uint32_t)(((uint64_t)part * nb + parts - 1) / parts);
-    const uint32_t b1 = (uint32_t)(((uint64_t)(part + 1) * nb + parts - 1) / parts);
+    const unsigned pbits = bits_for(n);
+    const uint32_t mul = 1u << pbits;  // pair keys p << pbits | q (kmp_dev_edges_rows)
     if (b1 > b0)
-        launch_bucket_small<false>(b1 - b0, st, ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df, ws->inc_sorted.p, shard_cap, cursor, gstats, ws->flags.p, list, list_count, ps, b0);
+        launch_bucket_small<false>(b1 - b0, st, ws->sorted.p, bstart, lay, mul, require_class_diff, heavy_df,
+                                   ws->inc_sorted.p, shard_cap, cursor, gstats, ws->flags.p, list, list_count, ps, b0);
     bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeTab, false>
-        <<<256, kBucketLargeThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
+        <<<256, kBucketLargeThreads, 0, st>>>(ws->sorted.p, bstart, lay, mul, require_class_diff, heavy_df,
                                               ws->inc_sorted.p, shard_cap, cursor, gstats, ws->flags.p, list,
                                               list_count, ps);
     check_shards_kernel<<<1, kShards, 0, st>>>(cursor, shard_cap, d_flags);
@@ -3088,7 +3190,7 @@ int kmp_dev_pairs_route(kmp_postings* ws, const unsigned long long* d_keys, uint
     RowSplit rows{};
     kmp_row_split(n, parts, rows.start);
     partition_kernel<true><<<(uint32_t)((total + 4095) / 4096), kPartThreads, 0, st>>>(
-        ws->inc_sorted.p, total, 0, n, parts, cap, d_send, d_b, rows);
+        ws->inc_sorted.p, total, pbits, n, parts, cap, d_send, d_b, rows);
     pad_regions_kernel<<<dim3(route_blocks(cap), parts), 256, 0, st>>>(d_send, cap, d_b, d_flags, 6);
     PG(hipGetLastError());
     return KMP_OK;
@@ -3106,7 +3208,7 @@ int kmp_dev_edges_route(kmp_postings* ws, const unsigned long long* d_pk, uint64
     PG(ws->uniq.reserve(m));
     PG(ws->w.reserve(m));
     PG(ws->small.reserve(16));
-    const unsigned pair_bits = bits_for((uint64_t)n * n);
+    const unsigned pbits = bits_for(n), pair_bits = 2 * pbits;  // keys p << pbits | q (kmp_dev_pairs_route)
     int rc = sort_keys<PairSortCfg>(ws, d_pk, ws->inc_sorted.p, m, 0, pair_bits, st);
     if (rc != KMP_OK) return rc;
     size_t t3 = 0;
@@ -3116,9 +3218,75 @@ int kmp_dev_edges_route(kmp_postings* ws, const unsigned long long* d_pk, uint64
     PG(rocprim::run_length_encode(ws->tmp.p, t3, ws->inc_sorted.p, (unsigned int)m, ws->uniq.p, ws->w.p,
                                   ws->small.p + 1, st));
     const uint32_t kb = (uint32_t)std::min<uint64_t>((m + 255) / 256, 8192);
-    emit_runs_kernel<<<kb, 256, 0, st>>>(ws->uniq.p, ws->w.p, ws->small.p + 1, n, d_p, d_q, d_w, cap);
+    emit_runs_kernel<<<kb, 256, 0, st>>>(ws->uniq.p, ws->w.p, ws->small.p + 1, 1u << pbits, d_p, d_q, d_w, cap);
     run_count_kernel<<<1, 1, 0, st>>>(ws->uniq.p, ws->small.p + 1, d_count);
     PG(hipGetLastError());
+    return KMP_OK;
+}
+
+// Multi-GPU owner of rows [row_lo, row_hi): the row-block tail (§3.1.3) over its m received pair
+// keys (kNoKey padding skipped, no cursors), rows counted from row_lo.  A row block above the
+// LDS capacity leaves *d_count = KMP_EDGES_RETRY; the caller switches the workspace to the sort
+// tail (kmp_postings_set_rowtail(ws, 0)) and reruns.
+__global__ void rowtail_check_kernel(const uint32_t* __restrict__ flags, unsigned long long* __restrict__ d_count) {
+    if (flags[3]) *d_count = KMP_EDGES_RETRY;
+}
+
+int kmp_dev_edges_rows(kmp_postings* ws, const unsigned long long* d_pk, uint64_t m, uint32_t n, uint32_t row_lo,
+                       uint32_t row_hi, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w, uint64_t cap,
+                       unsigned long long* d_count, void* stream) {
+    if (!ws || !d_count || row_lo > row_hi || row_hi > n || (m && (!d_pk || !d_p || !d_q || !d_w)))
+        return KMP_EINVAL;
+    const unsigned pbits = bits_for(n);
+    const uint32_t rows = row_hi - row_lo;
+    if (!ws->pt_on || m == 0 || rows == 0 || m > 0xFFFFFFFFull)
+        return kmp_dev_edges_route(ws, d_pk, m, n, d_p, d_q, d_w, cap, d_count, stream);
+    hipStream_t st = as_stream(stream);
+    PtGeom g{};
+    g.pbits = pbits;
+    // rows per block: an average of about a quarter of kPtCap keys (rows are skewed: a pair
+    // belongs to its smaller protein)
+    const double rpb = (double)(kPtCap / 4) * rows / (double)m;
+    unsigned rb = 0;
+    while (rb < 16 && (double)(2u << rb) <= rpb) ++rb;
+    rb = std::min(rb, ws->pt_rb_max);
+    while (rb < 16 && ((rows + (1ull << rb) - 1) >> rb) > kPtMaxBlocks) ++rb;
+    if (pbits + rb > 32) return kmp_dev_edges_route(ws, d_pk, m, n, d_p, d_q, d_w, cap, d_count, stream);
+    g.rbits = rb;
+    g.nrb = (uint32_t)((rows + (1ull << rb) - 1) >> rb);
+    g.sc = m;
+    g.jt = (uint32_t)((m + kPtTile - 1) / kPtTile);
+    g.nshards = 1;
+    g.row0 = row_lo;
+    g.flat_n = m;
+    hipError_t e = hipSuccess;
+    const PtBufs b = pt_bufs(ws, g, true, &e);
+    PG(e);
+    PG(ws->inc.reserve(m));
+    PG(ws->uniq.reserve(m));
+    PG(ws->w.reserve(m));
+    PG(ws->small.reserve(16));
+    PG(ws->flags.reserve(4));
+    PG(hipMemsetAsync(ws->flags.p, 0, 4 * sizeof(uint32_t), st));
+    uint32_t* keys32 = reinterpret_cast<uint32_t*>(ws->inc.p);
+    uint32_t* stage_p = reinterpret_cast<uint32_t*>(ws->uniq.p);
+    uint32_t* stage_q = stage_p + m;
+    pt_hist_kernel<<<dim3(g.jt, 1), kPtThreads, 0, st>>>(d_pk, nullptr, g, b.H);
+    bp_colsum_kernel<<<dim3(b.groups, (g.nrb + 255) / 256), 256, 0, st>>>(b.H, b.rows, g.nrb, b.R);
+    pt_colscan_kernel<<<1, kPtScanThreads, 0, st>>>(b.R, b.groups, g.nrb, b.bst, ws->small.p + 2);
+    bp_colprefix_kernel<<<dim3(b.groups, (g.nrb + 255) / 256), 256, 0, st>>>(b.H, b.rows, g.nrb, b.R, b.P);
+    pt_scatter_kernel<<<dim3(g.jt, 1), kPtThreads, 0, st>>>(d_pk, nullptr, g, b.P, keys32);
+    pt_reduce_kernel<<<g.nrb, kPtRThreads, 0, st>>>(keys32, b.bst, g, ws->flags.p, stage_p, stage_q, ws->w.p, b.counts);
+    pt_offsets_kernel<<<1, kPtScanThreads, 0, st>>>(b.counts, g.nrb, b.eoff, ws->small.p + 1, d_count);
+    pt_emit_kernel<<<g.nrb, 256, 0, st>>>(stage_p, stage_q, ws->w.p, b.bst, b.counts, b.eoff, d_p, d_q, d_w, cap);
+    rowtail_check_kernel<<<1, 1, 0, st>>>(ws->flags.p, d_count);
+    PG(hipGetLastError());
+    return KMP_OK;
+}
+
+int kmp_postings_set_rowtail(kmp_postings* ws, int enable) {
+    if (!ws) return KMP_EINVAL;
+    ws->pt_on = enable != 0;
     return KMP_OK;
 }
 

@@ -278,15 +278,23 @@ class DeviceRouteStages:
                                          self._stream()), "kmp_dev_pairs_route")
         return send
 
-    def edges_route(self, pk: torch.Tensor):
-        """(p, q, w) interleaved as an int32 [m, 3] buffer and the edge count (device)."""
+    def edges_route(self, pk: torch.Tensor, part: int, parts: int):
+        """(p, q, w) as an int32 [3, m] buffer and the edge count (device): the row-block tail over
+        this part's rows (kmp_dev_edges_rows; the count is KMP_EDGES_RETRY when a row block did not
+        fit in LDS, see disable_rowtail)."""
         L, p = self.L, self.pipe
         m = pk.numel()
         e = torch.empty((3, max(1, m)), dtype=torch.int32, device=p.dev)
-        _lib.check(L.kmp_dev_edges_route(self.ws, self._ptr(pk), m, p.n, self._ptr(e[0]), self._ptr(e[1]),
-                                         self._ptr(e[2]), max(1, m), self._ptr(self.count), self._stream()),
-                   "kmp_dev_edges_route")
+        rows = (self.C.c_uint32 * (parts + 1))()
+        L.kmp_row_split(p.n, parts, rows)
+        _lib.check(L.kmp_dev_edges_rows(self.ws, self._ptr(pk), m, p.n, rows[part], rows[part + 1], self._ptr(e[0]),
+                                        self._ptr(e[1]), self._ptr(e[2]), max(1, m), self._ptr(self.count),
+                                        self._stream()), "kmp_dev_edges_rows")
         return e, self.count
+
+    def disable_rowtail(self) -> None:
+        """A row block exceeded the LDS capacity somewhere: reduce with the global sort tail."""
+        _lib.check(self.L.kmp_postings_set_rowtail(self.ws, 0), "kmp_postings_set_rowtail")
 
     def status(self) -> torch.Tensor:
         """flags[0..7] + edge count, as one int64 device tensor (gathered across ranks)."""
@@ -299,6 +307,9 @@ class DeviceRouteStages:
             self.cap_pairs = max(self.cap_pairs, int(worst[6]) + int(worst[6]) // 16 + 1024)
         if worst[3]:
             self.shard_cap = max(self.shard_cap, int(worst[5]) + int(worst[5]) // 16 + 1024)
+
+
+EDGES_RETRY = 1 << 62  # KMP_EDGES_RETRY (kmerpair.h)
 
 
 class RouteFallback(RuntimeError):
@@ -316,7 +327,7 @@ def distributed_postings_padded(stages, offsets: np.ndarray, rank: int, world: i
         stages.begin(world)
         mine = exchange_equal(stages.keys_route(lo, hi, world), group)
         pk = exchange_equal(stages.pairs_route(mine, rank, world), group)
-        e, count = stages.edges_route(pk)
+        e, count = stages.edges_route(pk, rank, world)
         st = stages.status()
         parts = [torch.empty_like(st) for _ in range(world)]
         if _staged(st, group):
@@ -331,6 +342,9 @@ def distributed_postings_padded(stages, offsets: np.ndarray, rank: int, world: i
             raise RouteFallback("batch needs the single-GPU flat layout (frequent k-mer or wide class id)")
         if worst[0] or worst[3]:
             stages.grow(worst)
+            continue
+        if (table[:, 8] >= EDGES_RETRY).any():  # a row too long for the LDS row-block tail
+            stages.disable_rowtail()
             continue
         counts = [int(c) for c in table[:, 8]]
         c = counts[rank]
