@@ -2168,7 +2168,6 @@ using PtSort = rocprim::block_radix_sort<uint32_t, kPtRThreads, kE>;
 
 struct PtRuns {
     uint32_t hs[kPtCap + 1];  // rank of each run's first key
-    uint32_t hk[kPtCap];      // the run's key
 };
 union PtReduceLds {
     typename PtSort<2>::storage_type s2;
@@ -2206,11 +2205,14 @@ __device__ __forceinline__ void pt_reduce_block(PtReduceLds& u, typename PtSort<
     }
     uint32_t base, nruns;
     block_scan_n<kPtRThreads>(nh, base, nruns, wave_tot);  // barriers: the sort storage is dead
+    // heads write (p, q) from registers; w = the distance to the next run's first rank
+    const uint32_t qm = (1u << g.pbits) - 1;
 #pragma unroll
     for (uint32_t e = 0; e < kE; ++e)
         if (head[e]) {
             u.runs.hs[base] = rank0 + e;
-            u.runs.hk[base] = k[e];
+            stage_p[s0 + base] = g.row0 + ((r << g.rbits) | (k[e] >> g.pbits));
+            stage_q[s0 + base] = k[e] & qm;
             ++base;
         }
     if (threadIdx.x == 0) {
@@ -2218,13 +2220,7 @@ __device__ __forceinline__ void pt_reduce_block(PtReduceLds& u, typename PtSort<
         counts[r] = nruns;
     }
     __syncthreads();
-    const uint32_t qm = (1u << g.pbits) - 1;
-    for (uint32_t i = threadIdx.x; i < nruns; i += kPtRThreads) {
-        const uint32_t key = u.runs.hk[i];
-        stage_p[s0 + i] = g.row0 + ((r << g.rbits) | (key >> g.pbits));
-        stage_q[s0 + i] = key & qm;
-        stage_w[s0 + i] = u.runs.hs[i + 1] - u.runs.hs[i];
-    }
+    for (uint32_t i = threadIdx.x; i < nruns; i += kPtRThreads) stage_w[s0 + i] = u.runs.hs[i + 1] - u.runs.hs[i];
 }
 
 // one workgroup per row block; the sort width follows the block's size
@@ -2392,13 +2388,14 @@ int fused_reserve(kmp_postings* ws, uint64_t slots, const Layout& lay, uint32_t 
     PG(ws->uniq.reserve(total));
     PG(ws->w.reserve(total));
     PG(ws->rb.reserve(kRbWords));
+    if (!ws->hrb) PG(hipHostMalloc((void**)&ws->hrb, kRbWords * sizeof(unsigned long long), hipHostMallocDefault));
     PtGeom g;
-    if (pt_geometry(ws, slots, n, &g)) {
+    if (pt_geometry(ws, slots, n, &g)) {  // the row-block tail: no rocprim scratch to size
         hipError_t e = hipSuccess;
         pt_bufs(ws, g, true, &e);
         PG(e);
+        return KMP_OK;
     }
-    if (!ws->hrb) PG(hipHostMalloc((void**)&ws->hrb, kRbWords * sizeof(unsigned long long), hipHostMallocDefault));
     size_t t2 = 0, t3 = 0;
     PG(rocprim::radix_sort_keys<PairSortCfg>(nullptr, t2, ws->inc_sorted.p, ws->inc.p, (size_t)total, 0u, pair_bits,
                                              (hipStream_t)0));
@@ -3035,6 +3032,48 @@ __global__ __launch_bounds__(kPartThreads) void partition_kernel(const unsigned 
     }
 }
 
+// keys of chunk slots computed with the rolling chunk kernel (as bp_scatter1) and routed to
+// their destination (contiguous bucket ranges of `parts`) in the same pass: per chunk, ranks per
+// destination in LDS, one reservation per destination on dcursor[d], runs of ~4096/parts keys
+__global__ __launch_bounds__(kKeyThreads) void route_keys_kernel(
+    const uint8_t* __restrict__ res, const uint64_t* __restrict__ res_off, const uint16_t* __restrict__ cls, int k,
+    uint32_t p_hi, uint64_t slot_begin, uint64_t slot_end, const uint32_t* __restrict__ chunk_first, Layout lay,
+    uint32_t pw21, uint32_t parts, uint64_t cap, unsigned long long* __restrict__ send,
+    unsigned long long* __restrict__ dcursor, uint32_t* __restrict__ flags) {
+    __shared__ KeyChunk s;
+    __shared__ uint32_t lcnt[kPartMax];
+    __shared__ unsigned long long base[kPartMax];
+    const int tid = threadIdx.x;
+    const uint64_t c0 = slot_begin + (uint64_t)blockIdx.x * kKeyChunk;
+    const uint64_t c1 = min(c0 + kKeyChunk, slot_end);
+    if (tid < kPartMax) lcnt[tid] = 0;
+    const uint32_t first = chunk_first[blockIdx.x];
+    key_chunk_load(s, res, res_off, cls, k, p_hi, c0, c1, first, lay, flags);
+    unsigned long long x[kBpPer];
+    uint32_t dr[kBpPer];  // dest << 24 | rank, ~0 for no key
+    const unsigned bs = 32 - lay.bbits;  // bucket = h >> bs
+    const uint64_t nb = 1ull << lay.bbits;
+    key_chunk_run<kBpPer>(s, tid * kBpPer, (uint32_t)(c1 - c0), k, pw21, first, lay,
+                          [&](uint32_t e, bool valid, uint32_t h, unsigned long long lo) {
+                              x[e] = ((unsigned long long)h << lay.hshift) | lo;
+                              dr[e] = ~0u;
+                              if (valid) {
+                                  const uint32_t d = (uint32_t)((uint64_t)(h >> bs) * parts / nb);
+                                  dr[e] = (d << 24) | atomicAdd(&lcnt[d], 1u);
+                              }
+                          });
+    __syncthreads();
+    if (tid < (int)parts) base[tid] = lcnt[tid] ? atomicAdd(&dcursor[tid], (unsigned long long)lcnt[tid]) : 0ull;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t e = 0; e < kBpPer; ++e) {
+        if (dr[e] == ~0u) continue;
+        const uint32_t d = dr[e] >> 24;
+        const unsigned long long pos = base[d] + (dr[e] & 0xFFFFFFu);
+        if (pos < cap) send[d * cap + pos] = x[e];
+    }
+}
+
 }  // namespace
 extern "C" {
 
@@ -3115,15 +3154,18 @@ int kmp_dev_keys_route(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d
         pad_regions_kernel<<<dim3(route_blocks(cap), parts), 256, 0, st>>>(d_send, cap, d_b, d_flags, 4);
         return KMP_OK;
     }
-    PG(ws->keys.reserve(m));
-    PG(ws->sorted.reserve(m));
     PG(ws->flags.reserve(4));
     PG(hipMemsetAsync(ws->flags.p, 0, 4 * sizeof(uint32_t), st));
-    PG(launch_residue_keys(ws, d_res, d_res_off, d_class, k, lo, hi, slot_lo, slot_hi, lay, st));
     unsigned long long* dcur = d_b;  // parts destination cursors
     PG(hipMemsetAsync(dcur, 0, parts * sizeof(unsigned long long), st));
-    partition_kernel<false><<<(uint32_t)((m + 4095) / 4096), kPartThreads, 0, st>>>(
-        ws->keys.p, m, lay.sort_lo, 1ull << lay.bbits, parts, cap, d_send, dcur, RowSplit{});
+    // keys computed and routed in one pass (no key array)
+    const uint32_t g = (uint32_t)((m + kKeyChunk - 1) / kKeyChunk);
+    PG(ws->chunk_first.reserve(g + 1));
+    chunk_first_kernel<<<(hi - lo + 1 + 255) / 256, 256, 0, st>>>(d_res_off, lo, hi, slot_lo, slot_hi, g,
+                                                                  ws->chunk_first.p);
+    route_keys_kernel<<<g, kKeyThreads, 0, st>>>(d_res, d_res_off, d_class, k, hi, slot_lo, slot_hi,
+                                                  ws->chunk_first.p, lay, (uint32_t)pow21(k - 1), parts, cap, d_send,
+                                                  dcur, ws->flags.p);
     pad_regions_kernel<<<dim3(route_blocks(cap), parts), 256, 0, st>>>(d_send, cap, dcur, d_flags, 4);
     bucket_flag_kernel<<<1, 1, 0, st>>>(ws->flags.p, d_flags);
     PG(hipGetLastError());
