@@ -418,15 +418,17 @@ int kmp_dev_pairs_route(kmp_postings* ws, const unsigned long long* d_keys, uint
 int kmp_dev_edges_route(kmp_postings* ws, const unsigned long long* d_pk, uint64_t m, uint32_t n, uint32_t* d_p,
                         uint32_t* d_q, uint32_t* d_w, uint64_t cap, unsigned long long* d_count, void* stream);
 /* kmp_dev_edges_rows: as kmp_dev_edges_route for the owner of rows [row_lo, row_hi) (the
- * kmp_row_split range of its part), reduced with the row-block tail (pair keys partitioned by
+ * kmp_row_split range of its part), edges written as interleaved (p, q, w) u32 triples
+ * (d_edges[3i .. 3i+2], cap triples) so a rank's block is contiguous for the gather to rank 0;
+ * reduced with the row-block tail (pair keys partitioned by
  * row block, LDS radix sort + run-length encode per block) instead of a global sort.  A row block
  * above the LDS capacity leaves *d_count = KMP_EDGES_RETRY: switch the workspace to the sort tail
  * (kmp_postings_set_rowtail(ws, 0)) and rerun.  Pair keys from kmp_dev_pairs_route are
  * p << bits(n) | q. */
 #define KMP_EDGES_RETRY (1ull << 62)
 int kmp_dev_edges_rows(kmp_postings* ws, const unsigned long long* d_pk, uint64_t m, uint32_t n, uint32_t row_lo,
-                       uint32_t row_hi, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w, uint64_t cap,
-                       unsigned long long* d_count, void* stream);
+                       uint32_t row_hi, uint32_t* d_edges, uint64_t cap, unsigned long long* d_count,
+                       void* stream);
 /* Row-block tail on (default) or off for the fused residue step and kmp_dev_edges_rows; the
  * workspace turns it off by itself after a row too long for LDS. */
 int kmp_postings_set_rowtail(kmp_postings* ws, int enable);

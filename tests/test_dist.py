@@ -197,11 +197,11 @@ class OracleRouteStages:
         self.count = len(u)
         if self.retry_rowtail:  # emulate a row block too long for the LDS row-block tail
             self.count = 1 << 62
-        e = np.zeros((3, max(1, len(u))), np.int32)
-        e[0, :len(u)] = (u // np.uint64(self.n)).astype(np.int32)
-        e[1, :len(u)] = (u % np.uint64(self.n)).astype(np.int32)
-        e[2, :len(u)] = w
-        return torch.from_numpy(e), None
+        e = np.zeros((max(1, len(u)), 3), np.int32)  # interleaved (p, q, w) triples
+        e[:len(u), 0] = (u // np.uint64(self.n)).astype(np.int32)
+        e[:len(u), 1] = (u % np.uint64(self.n)).astype(np.int32)
+        e[:len(u), 2] = w
+        return torch.from_numpy(e.reshape(-1)), None
 
     def status(self):
         return torch.from_numpy(np.r_[self.flags, self.count].astype(np.int64))
@@ -225,14 +225,8 @@ def padded_worker(rank, world, port, out_q):
         got, counts = distributed_postings_padded(stages, b.offsets, rank, world, max_attempts=6)
         if rank == 0:
             P, Q, W = o.pairs()
-            g = got.numpy()
-            ep, eq, ew = [], [], []
-            off = 0
-            for c in counts:
-                blk = g[3 * off:3 * (off + c)].reshape(3, c)
-                ep.append(blk[0]), eq.append(blk[1]), ew.append(blk[2])
-                off += c
-            ep, eq, ew = (np.concatenate(x).view(np.uint32) for x in (ep, eq, ew))
+            tri = got.numpy().reshape(-1, 3)  # interleaved triples of every rank, rank order
+            ep, eq, ew = (np.ascontiguousarray(tri[:, j]).view(np.uint32) for j in range(3))
             ok = np.array_equal(ep, P) and np.array_equal(eq, Q) and np.array_equal(ew, W)
             out_q.put(("edges", ok, len(P), stages.attempts))
         out_q.put(("count", rank, counts[rank]))

@@ -150,8 +150,7 @@ SIGNATURES = {
     "kmp_dev_pairs_route": (C.c_int, [P, P, C.c_uint64, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32, C.c_int,
                                       C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, P, P, P, P]),
     "kmp_dev_edges_route": (C.c_int, [P, P, C.c_uint64, C.c_uint32, P, P, P, C.c_uint64, P, P]),
-    "kmp_dev_edges_rows": (C.c_int, [P, P, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, P, P, P, C.c_uint64, P,
-                                     P]),
+    "kmp_dev_edges_rows": (C.c_int, [P, P, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, P, C.c_uint64, P, P]),
     "kmp_dev_sort_edges_tmp_bytes": (C.c_uint64, [C.c_uint64, C.c_uint32]),
     "kmp_dev_sort_edges": (C.c_int, [P, P, P, C.c_uint64, C.c_uint32, P, C.c_uint64, P]),
     "kmp_read_fasta": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint32), C.POINTER(P), C.POINTER(P),

@@ -1114,14 +1114,15 @@ __global__ void pad_shards_kernel(unsigned long long* __restrict__ region, uint6
 // (pair key, w) runs -> edges, w >= 1 (the padding run, key kNoKey, is last and skipped)
 __global__ void emit_runs_kernel(const unsigned long long* __restrict__ uniq, const uint32_t* __restrict__ w,
                                  const uint32_t* __restrict__ nuniq, uint32_t n_prot, uint32_t* __restrict__ out_p,
-                                 uint32_t* __restrict__ out_q, uint32_t* __restrict__ out_w, uint64_t cap) {
+                                 uint32_t* __restrict__ out_q, uint32_t* __restrict__ out_w, uint64_t cap,
+                                 uint32_t stride = 1) {
     const uint32_t U = *nuniq;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < U; i += gridDim.x * blockDim.x) {
         const unsigned long long x = uniq[i];
         if (x == kNoKey || i >= cap) continue;
-        out_p[i] = (uint32_t)(x / n_prot);
-        out_q[i] = (uint32_t)(x % n_prot);
-        out_w[i] = w[i];
+        out_p[(uint64_t)i * stride] = (uint32_t)(x / n_prot);
+        out_q[(uint64_t)i * stride] = (uint32_t)(x % n_prot);
+        out_w[(uint64_t)i * stride] = w[i];
     }
 }
 
@@ -2287,14 +2288,14 @@ __global__ __launch_bounds__(256) void pt_emit_kernel(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ counts,
                                                       const uint32_t* __restrict__ eoff, uint32_t* __restrict__ d_p,
                                                       uint32_t* __restrict__ d_q, uint32_t* __restrict__ d_w,
-                                                      uint64_t cap) {
+                                                      uint64_t cap, uint32_t stride = 1) {
     const uint32_t r = blockIdx.x, s0 = bst[r], m = counts[r];
     const uint64_t o = eoff[r];
     for (uint32_t i = threadIdx.x; i < m; i += 256) {
         if (o + i >= cap) break;
-        d_p[o + i] = stage_p[s0 + i];
-        d_q[o + i] = stage_q[s0 + i];
-        d_w[o + i] = stage_w[s0 + i];
+        d_p[(o + i) * stride] = stage_p[s0 + i];
+        d_q[(o + i) * stride] = stage_q[s0 + i];
+        d_w[(o + i) * stride] = stage_w[s0 + i];
     }
 }
 
@@ -3238,8 +3239,10 @@ int kmp_dev_pairs_route(kmp_postings* ws, const unsigned long long* d_keys, uint
     return KMP_OK;
 }
 
-int kmp_dev_edges_route(kmp_postings* ws, const unsigned long long* d_pk, uint64_t m, uint32_t n, uint32_t* d_p,
-                        uint32_t* d_q, uint32_t* d_w, uint64_t cap, unsigned long long* d_count, void* stream) {
+}  // extern "C"
+static int edges_route_impl(kmp_postings* ws, const unsigned long long* d_pk, uint64_t m, uint32_t n, uint32_t* d_p,
+                            uint32_t* d_q, uint32_t* d_w, uint32_t stride, uint64_t cap,
+                            unsigned long long* d_count, void* stream) {
     if (!ws || !d_count || (m && (!d_pk || !d_p || !d_q || !d_w))) return KMP_EINVAL;
     hipStream_t st = as_stream(stream);
     if (m == 0) {
@@ -3260,10 +3263,18 @@ int kmp_dev_edges_route(kmp_postings* ws, const unsigned long long* d_pk, uint64
     PG(rocprim::run_length_encode(ws->tmp.p, t3, ws->inc_sorted.p, (unsigned int)m, ws->uniq.p, ws->w.p,
                                   ws->small.p + 1, st));
     const uint32_t kb = (uint32_t)std::min<uint64_t>((m + 255) / 256, 8192);
-    emit_runs_kernel<<<kb, 256, 0, st>>>(ws->uniq.p, ws->w.p, ws->small.p + 1, 1u << pbits, d_p, d_q, d_w, cap);
+    emit_runs_kernel<<<kb, 256, 0, st>>>(ws->uniq.p, ws->w.p, ws->small.p + 1, 1u << pbits, d_p, d_q, d_w, cap,
+                                         stride);
     run_count_kernel<<<1, 1, 0, st>>>(ws->uniq.p, ws->small.p + 1, d_count);
     PG(hipGetLastError());
     return KMP_OK;
+}
+
+extern "C" {
+
+int kmp_dev_edges_route(kmp_postings* ws, const unsigned long long* d_pk, uint64_t m, uint32_t n, uint32_t* d_p,
+                        uint32_t* d_q, uint32_t* d_w, uint64_t cap, unsigned long long* d_count, void* stream) {
+    return edges_route_impl(ws, d_pk, m, n, d_p, d_q, d_w, 1, cap, d_count, stream);
 }
 
 // Multi-GPU owner of rows [row_lo, row_hi): the row-block tail (§3.1.3) over its m received pair
@@ -3275,14 +3286,14 @@ __global__ void rowtail_check_kernel(const uint32_t* __restrict__ flags, unsigne
 }
 
 int kmp_dev_edges_rows(kmp_postings* ws, const unsigned long long* d_pk, uint64_t m, uint32_t n, uint32_t row_lo,
-                       uint32_t row_hi, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w, uint64_t cap,
-                       unsigned long long* d_count, void* stream) {
-    if (!ws || !d_count || row_lo > row_hi || row_hi > n || (m && (!d_pk || !d_p || !d_q || !d_w)))
-        return KMP_EINVAL;
+                       uint32_t row_hi, uint32_t* d_edges, uint64_t cap, unsigned long long* d_count,
+                       void* stream) {
+    if (!ws || !d_count || row_lo > row_hi || row_hi > n || (m && (!d_pk || !d_edges))) return KMP_EINVAL;
     const unsigned pbits = bits_for(n);
     const uint32_t rows = row_hi - row_lo;
+    uint32_t *d_p = d_edges, *d_q = d_edges + 1, *d_w = d_edges + 2;  // interleaved triples
     if (!ws->pt_on || m == 0 || rows == 0 || m > 0xFFFFFFFFull)
-        return kmp_dev_edges_route(ws, d_pk, m, n, d_p, d_q, d_w, cap, d_count, stream);
+        return edges_route_impl(ws, d_pk, m, n, d_p, d_q, d_w, 3, cap, d_count, stream);
     hipStream_t st = as_stream(stream);
     PtGeom g{};
     g.pbits = pbits;
@@ -3293,7 +3304,7 @@ int kmp_dev_edges_rows(kmp_postings* ws, const unsigned long long* d_pk, uint64_
     while (rb < 16 && (double)(2u << rb) <= rpb) ++rb;
     rb = std::min(rb, ws->pt_rb_max);
     while (rb < 16 && ((rows + (1ull << rb) - 1) >> rb) > kPtMaxBlocks) ++rb;
-    if (pbits + rb > 32) return kmp_dev_edges_route(ws, d_pk, m, n, d_p, d_q, d_w, cap, d_count, stream);
+    if (pbits + rb > 32) return edges_route_impl(ws, d_pk, m, n, d_p, d_q, d_w, 3, cap, d_count, stream);
     g.rbits = rb;
     g.nrb = (uint32_t)((rows + (1ull << rb) - 1) >> rb);
     g.sc = m;
@@ -3320,7 +3331,7 @@ int kmp_dev_edges_rows(kmp_postings* ws, const unsigned long long* d_pk, uint64_
     pt_scatter_kernel<<<dim3(g.jt, 1), kPtThreads, 0, st>>>(d_pk, nullptr, g, b.P, keys32);
     pt_reduce_kernel<<<g.nrb, kPtRThreads, 0, st>>>(keys32, b.bst, g, ws->flags.p, stage_p, stage_q, ws->w.p, b.counts);
     pt_offsets_kernel<<<1, kPtScanThreads, 0, st>>>(b.counts, g.nrb, b.eoff, ws->small.p + 1, d_count);
-    pt_emit_kernel<<<g.nrb, 256, 0, st>>>(stage_p, stage_q, ws->w.p, b.bst, b.counts, b.eoff, d_p, d_q, d_w, cap);
+    pt_emit_kernel<<<g.nrb, 256, 0, st>>>(stage_p, stage_q, ws->w.p, b.bst, b.counts, b.eoff, d_p, d_q, d_w, cap, 3);
     rowtail_check_kernel<<<1, 1, 0, st>>>(ws->flags.p, d_count);
     PG(hipGetLastError());
     return KMP_OK;

@@ -279,17 +279,16 @@ class DeviceRouteStages:
         return send
 
     def edges_route(self, pk: torch.Tensor, part: int, parts: int):
-        """(p, q, w) as an int32 [3, m] buffer and the edge count (device): the row-block tail over
-        this part's rows (kmp_dev_edges_rows; the count is KMP_EDGES_RETRY when a row block did not
-        fit in LDS, see disable_rowtail)."""
+        """Interleaved (p, q, w) int32 triples (a flat [3 m] buffer) and the edge count (device): the
+        row-block tail over this part's rows (kmp_dev_edges_rows; the count is KMP_EDGES_RETRY when a
+        row block did not fit in LDS, see disable_rowtail)."""
         L, p = self.L, self.pipe
         m = pk.numel()
-        e = torch.empty((3, max(1, m)), dtype=torch.int32, device=p.dev)
+        e = torch.empty(3 * max(1, m), dtype=torch.int32, device=p.dev)
         rows = (self.C.c_uint32 * (parts + 1))()
         L.kmp_row_split(p.n, parts, rows)
-        _lib.check(L.kmp_dev_edges_rows(self.ws, self._ptr(pk), m, p.n, rows[part], rows[part + 1], self._ptr(e[0]),
-                                        self._ptr(e[1]), self._ptr(e[2]), max(1, m), self._ptr(self.count),
-                                        self._stream()), "kmp_dev_edges_rows")
+        _lib.check(L.kmp_dev_edges_rows(self.ws, self._ptr(pk), m, p.n, rows[part], rows[part + 1], self._ptr(e),
+                                        max(1, m), self._ptr(self.count), self._stream()), "kmp_dev_edges_rows")
         return e, self.count
 
     def disable_rowtail(self) -> None:
@@ -320,8 +319,8 @@ def distributed_postings_padded(stages, offsets: np.ndarray, rank: int, world: i
                                 max_attempts: int = 4):
     """The fixed-capacity flow: keys routed by bucket range, pair keys routed by p range, edges
     to rank 0 in rank order (= canonical).  One host synchronisation per attempt: the all-gather
-    of every rank's flags and edge count.  Returns rank 0's flat (p, q, w) int32 tensor (rank r's
-    block of 3 * count_r values is [p..., q..., w...]) and the per-rank counts; None elsewhere."""
+    of every rank's flags and edge count.  Returns rank 0's flat int32 tensor of interleaved
+    (p, q, w) triples (all ranks' edges, canonical order) and the per-rank counts; None elsewhere."""
     lo, hi = protein_slices(offsets, world)[rank]
     for _ in range(max_attempts):
         stages.begin(world)
@@ -348,8 +347,7 @@ def distributed_postings_padded(stages, offsets: np.ndarray, rank: int, world: i
             continue
         counts = [int(c) for c in table[:, 8]]
         c = counts[rank]
-        flat = e[:, :c].contiguous().view(-1) if c else e[:, :0].contiguous().view(-1)
-        got = gather_to_rank0(flat, 3 * c, [3 * x for x in counts], rank, group)
+        got = gather_to_rank0(e, 3 * c, [3 * x for x in counts], rank, group)  # triples: no repacking
         return got, counts
     raise RuntimeError("exchange capacities did not converge")
 
@@ -367,13 +365,10 @@ def distributed_step(pipe, rank: int, world: int, group=None, min_shared: int = 
             n = sum(counts)
             if n > pipe.edge_cap:
                 pipe._alloc_edges(n + n // 8 + 1024)
-            o = 0
-            for c in counts:  # rank r's block: p[c], q[c], w[c]
-                blk = got[3 * o:3 * (o + c)].view(3, c)
-                pipe.ep[o:o + c] = blk[0]
-                pipe.eq[o:o + c] = blk[1]
-                pipe.ew[o:o + c] = blk[2]
-                o += c
+            tri = got[:3 * n].view(n, 3)  # interleaved triples, already in canonical order
+            pipe.ep[:n] = tri[:, 0]
+            pipe.eq[:n] = tri[:, 1]
+            pipe.ew[:n] = tri[:, 2]
             pipe.n_edges = n
             return n
         return counts[rank]
