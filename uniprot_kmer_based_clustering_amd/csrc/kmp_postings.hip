@@ -711,25 +711,21 @@ __device__ __forceinline__ void process_bucket(
         if (tid == 0 && T[0] == 0xFFFFFFFFu && H[1] == 7u) flags[3] = 1;
         return;
     }
-    // B. size classes, largest first
-    uint32_t c4[kPer], r4[kPer], single = 0;
-    {
+    // B. size classes, largest first.  Each group's first key (rank 0) stands for it (count from
+    // its slot word, size-class rank, position rewrite), so the pass is per key, not over all kTab
+    // table slots (measured 6 % faster); singleton groups (most) take no rank and no position
+    uint32_t single = 0;
+    uint32_t cn[kE], rr[kE];
 #pragma unroll
-        for (int q4 = 0; q4 < kPer / 4; ++q4) {
-            const uint4 v = reinterpret_cast<const uint4*>(H)[tid * (kPer / 4) + q4];
-            c4[4 * q4] = v.x, c4[4 * q4 + 1] = v.y, c4[4 * q4 + 2] = v.z, c4[4 * q4 + 3] = v.w;
-        }
-        if (kMerge) {
-#pragma unroll
-            for (int q = 0; q < kPer; ++q) c4[q] = c4[q] == kFree ? 0u : c4[q] >> hb;
-        }
-        // singleton groups (one key: most groups) only count toward sum_S / distinct; they take
-        // no size-class rank and no position
-#pragma unroll
-        for (int q = 0; q < kPer; ++q) {
-            if (c4[q] > kHeavySub) heavy = 1;
-            single += c4[q] == 1;
-            r4[q] = c4[q] >= 2 && c4[q] <= kHeavySub ? atomicAdd(&SZ[c4[q]], 1u) : 0u;
+    for (int e = 0; e < kE; ++e) {
+        cn[e] = rr[e] = 0;
+        if (tid + e * kThreads >= n) continue;
+        const uint32_t w = H[sl[e]];
+        cn[e] = kMerge ? w >> hb : w;
+        if (rk[e] == 0) {
+            if (cn[e] > kHeavySub) heavy = 1;
+            else if (cn[e] == 1) ++single;
+            else rr[e] = atomicAdd(&SZ[cn[e]], 1u);
         }
     }
     __syncthreads();
@@ -748,8 +744,8 @@ __device__ __forceinline__ void process_bucket(
     }
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < kPer; ++q)
-        H[tid * kPer + q] = c4[q] >= 2 ? ((SZ[c4[q]] + r4[q] * c4[q]) << 8) | c4[q] : c4[q];  // singleton: 1
+    for (int e = 0; e < kE; ++e)
+        if (rk[e] == 0 && cn[e] >= 2) H[sl[e]] = ((SZ[cn[e]] + rr[e] * cn[e]) << 8) | cn[e];
     __syncthreads();
     if (KMP_BUCKET_STOP == 2) {
         if (tid == 0 && T[0] == 0xFFFFFFFFu && H[1] == 7u) flags[3] = 1;
@@ -759,8 +755,8 @@ __device__ __forceinline__ void process_bucket(
 #pragma unroll
     for (int e = 0; e < kE; ++e)
         if (tid + e * kThreads < n) {
+            if (cn[e] < 2) continue;  // singleton
             const uint32_t g = H[sl[e]];
-            if ((g & 255u) < 2) continue;  // singleton
             const uint32_t pos = (g >> 8) + rk[e];
             Bl[pos] = xl[e];
             T[pos] = g;
@@ -1202,6 +1198,20 @@ __device__ __forceinline__ void lds_bins_scan(uint32_t* lh, uint32_t nb, uint32_
     __syncthreads();
 }
 
+// sum of x[i * stride], i < m, with the loads issued in batches of 8 (an accumulation loop would
+// otherwise wait on every load in turn)
+__device__ __forceinline__ uint32_t col_sum(const uint32_t* __restrict__ x, uint64_t stride, uint32_t m) {
+    uint32_t s = 0;
+    for (uint32_t i = 0; i < m; i += 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (uint32_t t = 0; t < 8; ++t) v[t] = i + t < m ? x[(i + t) * stride] : 0u;
+#pragma unroll
+        for (uint32_t t = 0; t < 8; ++t) s += v[t];
+    }
+    return s;
+}
+
 // in place: x[i * stride] <- run + (exclusive prefix of x[0 .. i)), for i < m; returns the end
 // value.  Loads go out in batches of 8 ahead of the stores (the in-place stores would otherwise
 // serialise every load behind the previous store).
@@ -1247,10 +1257,7 @@ __global__ __launch_bounds__(256) void bp_colsum_kernel(const uint32_t* __restri
                                                         uint32_t* __restrict__ R) {
     const uint32_t r0 = blockIdx.x * kBpRowGroup, r1 = min(rows, r0 + kBpRowGroup);
     for (uint32_t c = blockIdx.y * 256 + threadIdx.x; c < cols; c += gridDim.y * 256) {
-        uint32_t v = 0;
-#pragma unroll 8
-        for (uint32_t r = r0; r < r1; ++r) v += M[(uint64_t)r * cols + c];
-        R[(uint64_t)blockIdx.x * cols + c] = v;
+        R[(uint64_t)blockIdx.x * cols + c] = col_sum(M + (uint64_t)r0 * cols + c, cols, r1 - r0);
     }
 }
 
@@ -1269,11 +1276,7 @@ __global__ __launch_bounds__(kColThreads) void bp_colscan_kernel(uint32_t* __res
     const uint32_t c = threadIdx.x % cols, sp = threadIdx.x / cols;
     const bool act = sp < splits;
     const uint32_t gq = (groups + splits - 1) / splits, g0 = min(groups, sp * gq), g1 = min(groups, g0 + gq);
-    uint32_t v = 0;
-    if (act) {
-#pragma unroll 4
-        for (uint32_t g = g0; g < g1; ++g) v += R[(uint64_t)g * cols + c];
-    }
+    const uint32_t v = act ? col_sum(R + (uint64_t)g0 * cols + c, cols, g1 - g0) : 0u;
     part[threadIdx.x] = v;
     __syncthreads();
     uint32_t before = 0;  // this split's offset inside its column
@@ -1437,10 +1440,7 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scan2_kernel(uint32_t* __restr
     }
     uint32_t* base = H2 + (uint64_t)c * J * dg.nb2;
     for (uint32_t d = threadIdx.x; d < dg.nb2; d += kKeyThreads) {
-        uint32_t v = 0;
-#pragma unroll 8
-        for (uint32_t j = 0; j < nt; ++j) v += base[(uint64_t)j * dg.nb2 + d];
-        tot[d] = v;
+        tot[d] = col_sum(base + d, dg.nb2, nt);
     }
     __syncthreads();
     lds_bins_scan(tot, dg.nb2, wave_tot);
@@ -1643,9 +1643,9 @@ struct kmp_postings {
     hipStream_t cst = nullptr;  // capture stream
     std::vector<unsigned long long> gkey, gkey_seen;
     uint64_t graph_replays = 0;
-    // read-back of the fused step: gstats | cursors | flags[0..1] | run count, one D2H copy
-    Grow<unsigned long long> rb;
-    unsigned long long* hrb = nullptr;  // pinned
+    // read-back of the fused step (kRbWords: gstats | cursors | flags | run count | largest row
+    // block), written by fused_pack_kernel into coherent pinned host memory
+    unsigned long long* hrb = nullptr;
     int ablate = getenv("KMP_BUCKET_ABLATE") ? atoi(getenv("KMP_BUCKET_ABLATE")) : 0;  // diagnostics
     hipEvent_t ev[KMP_POSTINGS_STAGES + 1] = {};
     ~kmp_postings() {
@@ -1655,7 +1655,6 @@ struct kmp_postings {
         ps_cursor.release(); e3.release(); ecnt.release(); eoff.release(); chunk_first.release(); bp.release(); pt.release();
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
-        rb.release();
         if (hrb) (void)hipHostFree(hrb);
         if (gexec) (void)hipGraphExecDestroy(gexec);
         if (cst) (void)hipStreamDestroy(cst);
@@ -2087,8 +2086,7 @@ __global__ __launch_bounds__(kPtScanThreads) void pt_colscan_kernel(uint32_t* __
         tot[i] = 0;
         const uint32_t c = c0 + i;
         if (i >= q || c >= cols) continue;
-#pragma unroll 8
-        for (uint32_t gi = 0; gi < groups; ++gi) tot[i] += R[(uint64_t)gi * cols + c];
+        tot[i] = col_sum(R + c, cols, groups);
         sum += tot[i];
     }
     uint32_t mx = 0;
@@ -2327,6 +2325,7 @@ __global__ void fused_pack_kernel(const unsigned long long* __restrict__ gstats,
         rb[kShards * 9 + 3] = flags[3];
         rb[kShards * 9 + 4] = runs[1];
     }
+    __threadfence_system();  // rb is host memory, read after the stream synchronises
 }
 
 // row-block tail geometry: rows per block so that an average block holds about a quarter of
@@ -2388,8 +2387,8 @@ int fused_reserve(kmp_postings* ws, uint64_t slots, const Layout& lay, uint32_t 
     PG(ws->inc.reserve(total));
     PG(ws->uniq.reserve(total));
     PG(ws->w.reserve(total));
-    PG(ws->rb.reserve(kRbWords));
-    if (!ws->hrb) PG(hipHostMalloc((void**)&ws->hrb, kRbWords * sizeof(unsigned long long), hipHostMallocDefault));
+    // coherent pinned memory: fused_pack_kernel writes the read-back straight into it (no copy)
+    if (!ws->hrb) PG(hipHostMalloc((void**)&ws->hrb, kRbWords * sizeof(unsigned long long), hipHostMallocCoherent));
     PtGeom g;
     if (pt_geometry(ws, slots, n, &g)) {  // the row-block tail: no rocprim scratch to size
         hipError_t e = hipSuccess;
@@ -2455,8 +2454,7 @@ int fused_enqueue(kmp_postings* ws, MakeKeys& make_keys, uint64_t slots, const L
         ws->mark(5, st);
         pt_offsets_kernel<<<1, kPtScanThreads, 0, st>>>(b.counts, g.nrb, b.eoff, ws->small.p + 1);
         pt_emit_kernel<<<g.nrb, 256, 0, st>>>(stage_p, stage_q, ws->w.p, b.bst, b.counts, b.eoff, d_p, d_q, d_w, cap);
-        fused_pack_kernel<<<1, 256, 0, st>>>(gstats, flags, ws->small.p + 1, ws->rb.p);
-        PG(hipMemcpyAsync(ws->hrb, ws->rb.p, kRbWords * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+        fused_pack_kernel<<<1, 256, 0, st>>>(gstats, flags, ws->small.p + 1, ws->hrb);
         ws->mark(6, st);
         PG(hipGetLastError());
         return KMP_OK;
@@ -2471,8 +2469,7 @@ int fused_enqueue(kmp_postings* ws, MakeKeys& make_keys, uint64_t slots, const L
                                   ws->small.p + 1, st));
     const uint32_t kb = (uint32_t)std::min<uint64_t>((total + 255) / 256, 8192);
     emit_runs_kernel<<<kb, 256, 0, st>>>(ws->uniq.p, ws->w.p, ws->small.p + 1, n, d_p, d_q, d_w, cap);
-    fused_pack_kernel<<<1, 256, 0, st>>>(gstats, flags, ws->small.p + 1, ws->rb.p);
-    PG(hipMemcpyAsync(ws->hrb, ws->rb.p, kRbWords * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    fused_pack_kernel<<<1, 256, 0, st>>>(gstats, flags, ws->small.p + 1, ws->hrb);
     ws->mark(6, st);
     PG(hipGetLastError());
     return KMP_OK;
