@@ -48,8 +48,13 @@ typedef enum {
 /* length laws of the synthetic generator */
 enum { KMP_LEN_NORMAL300 = 0, KMP_LEN_LOGUNIFORM = 1 };
 
-/* pair scores (kmp_pair_opts.score) */
-enum { KMP_SCORE_COUNT = 0, KMP_SCORE_JACCARD = 1 };
+/* pair scores (kmp_pair_opts.score), build extensions (the reference computes neither, so their
+ * parity is unpinned):
+ *   COUNT    score = w
+ *   JACCARD  score = w / (|K(p)| + |K(q)| - w), one correctly rounded f32 divide
+ *   BLOSUM   score = Σ over the shared k-mers x of Σ_i B62[x_i][x_i] (the BLOSUM62 diagonal of
+ *            blosum.rs:8-30 in residue-code order; code 20 scores 0), an exact integer in f32 */
+enum { KMP_SCORE_COUNT = 0, KMP_SCORE_JACCARD = 1, KMP_SCORE_BLOSUM = 2 };
 
 /* pair engines (kmp_pair_opts.engine); every engine returns the same edges */
 enum {
@@ -81,7 +86,7 @@ typedef struct {
     uint32_t min_shared;         /* emit iff w >= min_shared (reference: 1) */
     int32_t require_class_diff;  /* 1: drop same-AMR-class pairs (mod.rs:549-697); 0: keep */
     uint32_t align_threshold;    /* alignment candidates: w > threshold (mod.rs:242: 10) */
-    int32_t score;               /* KMP_SCORE_COUNT | KMP_SCORE_JACCARD (build extension) */
+    int32_t score;               /* KMP_SCORE_COUNT | KMP_SCORE_JACCARD | KMP_SCORE_BLOSUM (build extensions) */
     int32_t engine;              /* KMP_ENGINE_* */
 } kmp_pair_opts;
 

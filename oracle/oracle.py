@@ -150,6 +150,21 @@ class Oracle:
             L.orc_free(ptr)
         return out
 
+    def blosum_scores(self, p, q):
+        """BLOSUM-weighted score of each pair (p[i], q[i]) (a build
+        extension, parity unpinned): Σ over the shared k-mers x of Σ_j B62[x_j][x_j], the diagonal
+        of blosum.rs:8-30 in residue-code order (C S T A G P D E Q N H R K M I L V W Y F,
+        AMINO_ACID_LIST of protein.rs:9-13), code 20 scored 0.  A loop over pairs, small batches."""
+        out = np.zeros(len(p), dtype=np.int64)
+        for i, (a, b) in enumerate(zip(np.asarray(p).tolist(), np.asarray(q).tolist())):
+            x = self.shared(a, b).astype(np.int64)
+            s = 0
+            for _ in range(self.k):
+                s += int(B62_DIAG[x % 21].sum())
+                x //= 21
+            out[i] = s
+        return out
+
     def shared(self, p, q):
         buf = np.zeros(4096, dtype=np.uint32)
         m = lib().orc_shared(self._ctx, p, q, buf.ctypes.data, buf.size)
@@ -157,6 +172,11 @@ class Oracle:
             buf = np.zeros(m, dtype=np.uint32)
             lib().orc_shared(self._ctx, p, q, buf.ctypes.data, buf.size)
         return buf[:m].copy()
+
+
+# BLOSUM62 diagonal (blosum.rs:8-30: C 9, S 4, T 5, A 4, G 6, P 7, D 6, E 5, Q 5, N 6, H 8, R 5,
+# K 5, M 5, I 4, L 4, V 4, W 11, Y 7, F 6), indexed by residue code; code 20 ('*', unknown) -> 0
+B62_DIAG = np.array([9, 4, 5, 4, 6, 7, 6, 5, 5, 6, 8, 5, 5, 5, 4, 4, 4, 11, 7, 6, 0], dtype=np.int64)
 
 
 def residue_code(b: int) -> int:

@@ -114,6 +114,31 @@ def test_jaccard_scores(engine, oracle_mod, uni):
     assert np.all((e.score > 0) & (e.score <= 1))
 
 
+@pytest.mark.parametrize("k", [5, 7])
+def test_blosum_scores(engine, oracle_mod, k):
+    """KMP_SCORE_BLOSUM (SURVEY.md §8d config-5 scoring, a build extension): every edge's score
+    equals the oracle's Σ over shared k-mers of the BLOSUM62 diagonal, exactly (integers in f32),
+    for every engine; plus the hand-checked batch of test_oracle.py."""
+    b = K.synth(3000, 5, 1)  # config-5 length law (log-uniform 50-2000)
+    o = oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=k, threads=8)
+    p, q, w = o.pairs()
+    want = o.blosum_scores(p, q).astype(np.float32)
+    engine.load(b)
+    engine.build_sets(k)
+    for eng in ENGINES:
+        e = engine.pairs(score=_lib.KMP_SCORE_BLOSUM, engine=eng)
+        assert_edges(e, p, q, w)
+        np.testing.assert_array_equal(e.score, want)
+    assert len(p) > 100
+    seqs = [b"CCCCCAWWWWW", b"GGCCCCCGG", b"WWWWWPP", b"XCCCC*", b"XCCCC*A"]
+    res, off, cls = make_batch(seqs, ["a", "b", "c", "d", "e"])
+    engine.load(batch(res, off, cls))
+    engine.build_sets(5)
+    e = engine.pairs(score=_lib.KMP_SCORE_BLOSUM)
+    got = dict(zip(zip(e.p.tolist(), e.q.tolist()), e.score.tolist()))
+    assert got == {(0, 1): 45.0, (0, 2): 55.0, (3, 4): 72.0}
+
+
 @pytest.mark.parametrize("eng", ENGINES, ids=ENGINE_IDS)
 @pytest.mark.parametrize("n,seed,law,k", [(10000, 2, 0, 7), (3000, 5, 1, 5), (3000, 5, 1, 7)])
 def test_synthetic_bit_exact(engine, oracle_mod, n, seed, law, k, eng):

@@ -120,3 +120,19 @@ def test_hash_order_vs_literal(oracle_mod, k):
         assert codes.tolist() == [c for x in want for c in x]
         rc, rdf = o.repeat()
         assert dict(zip(rc.tolist(), rdf.tolist())) == rep
+
+
+def test_blosum_scores_known_answers(oracle_mod):
+    """BLOSUM-weighted scores (SURVEY.md §8d build extension; parity unpinned, so pinned here by
+    hand): the self-scores of blosum.rs:8-30's diagonal summed over each shared k-mer's residues;
+    '*' and unknown residues (code 20) score 0."""
+    seqs = [b"CCCCCAWWWWW", b"GGCCCCCGG", b"WWWWWPP", b"XCCCC*", b"XCCCC*A"]
+    res, off, cls = make_batch(seqs, ["a", "b", "c", "d", "e"])
+    o = oracle_mod.Oracle(res, off, cls, k=5, threads=1)
+    p, q, w = o.pairs()
+    got = dict(zip(zip(p.tolist(), q.tolist()), o.blosum_scores(p, q).tolist()))
+    assert got[(0, 1)] == 5 * 9           # CCCCC
+    assert got[(0, 2)] == 5 * 11          # WWWWW
+    assert w[(p == 3) & (q == 4)][0] == 2
+    assert got[(3, 4)] == 2 * 4 * 9       # XCCCC (X -> 0) and CCCC* ('*' -> 0): 36 each
+    assert set(got) == {(0, 1), (0, 2), (3, 4)}

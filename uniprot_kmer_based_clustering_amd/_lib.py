@@ -17,7 +17,7 @@ HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "kmerpair.h")
 
 KMP_OK, KMP_EINVAL, KMP_ENOMEM, KMP_EDEVICE, KMP_ERCCL, KMP_EOVERFLOW, KMP_ESTATE, KMP_EIO = range(8)
 KMP_LEN_NORMAL300, KMP_LEN_LOGUNIFORM = 0, 1
-KMP_SCORE_COUNT, KMP_SCORE_JACCARD = 0, 1
+KMP_SCORE_COUNT, KMP_SCORE_JACCARD, KMP_SCORE_BLOSUM = 0, 1, 2
 KMP_ENGINE_AUTO, KMP_ENGINE_POSTINGS, KMP_ENGINE_TILES, KMP_ENGINE_RESIDUES = 0, 1, 2, 3
 KMP_KMERS_CODES, KMP_KMERS_IDS = 0, 1
 KMP_LDS_SORT_MAX = 4096

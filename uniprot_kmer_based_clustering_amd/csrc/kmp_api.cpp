@@ -72,6 +72,7 @@ struct kmp_ctx {
 
     int k_sets = 0;
     DevBuf set, set_len, rep, rep_len, bits, scratch;
+    DevBuf escore;  // per-edge scores computed on the device (KMP_SCORE_BLOSUM)
     std::vector<uint32_t> h_set_len, h_rep_len;
     kmp_counters counters{};
 
@@ -158,6 +159,15 @@ int finish_edges(kmp_ctx* c, const kmp_pair_opts& o, uint64_t count, bool needs_
         KMP_HIP(c, hipMemcpyAsync(e->q.data(), c->eq.p, count * 4, hipMemcpyDeviceToHost, c->stream));
         KMP_HIP(c, hipMemcpyAsync(e->w.data(), c->ew.p, count * 4, hipMemcpyDeviceToHost, c->stream));
     }
+    if (o.score == KMP_SCORE_BLOSUM && count) {
+        KMP_HIP(c, c->escore.reserve(count * sizeof(float)));
+        e->score.resize(count);
+        KMP_TRY(c, edge_blosum_device(c->rep.as<uint32_t>(), c->rep_len.as<uint32_t>(), c->off.as<uint64_t>(),
+                                      c->ep.as<uint32_t>(), c->eq.as<uint32_t>(), c->ew.as<uint32_t>(), count,
+                                      c->k_sets, c->escore.as<float>(), c->stream));
+        KMP_HIP(c, hipMemcpyAsync(e->score.data(), c->escore.p, count * sizeof(float), hipMemcpyDeviceToHost,
+                                  c->stream));
+    }
     KMP_HIP(c, hipStreamSynchronize(c->stream));
     e->score.resize(count);
     uint64_t wdiff = 0, nalign = 0;
@@ -168,6 +178,8 @@ int finish_edges(kmp_ctx* c, const kmp_pair_opts& o, uint64_t count, bool needs_
         if (o.score == KMP_SCORE_JACCARD) {
             const uint64_t uni = (uint64_t)c->h_set_len[p] + c->h_set_len[q] - w;
             e->score[i] = uni ? (float)w / (float)uni : 0.0f;  // exact operands (< 2^24), one rounding
+        } else if (o.score == KMP_SCORE_BLOSUM) {
+            // computed on the device above
         } else {
             e->score[i] = (float)w;
         }
@@ -492,7 +504,8 @@ int kmp_pairs(kmp_ctx* c, const kmp_pair_opts* opts, kmp_edges** out) {
     kmp_pair_opts o;
     kmp_pair_opts_default(&o);
     if (opts) o = *opts;
-    if (o.score != KMP_SCORE_COUNT && o.score != KMP_SCORE_JACCARD) return fail(c, KMP_EINVAL, "unknown score %d", o.score);
+    if (o.score != KMP_SCORE_COUNT && o.score != KMP_SCORE_JACCARD && o.score != KMP_SCORE_BLOSUM)
+        return fail(c, KMP_EINVAL, "unknown score %d", o.score);
     if (o.engine < KMP_ENGINE_AUTO || o.engine > KMP_ENGINE_RESIDUES) return fail(c, KMP_EINVAL, "unknown engine %d", o.engine);
     KMP_TRY(c, use_device(c));
     if (c->edge_cap == 0) c->edge_cap = std::max<uint64_t>(1u << 20, 4ull * c->n);

@@ -6,6 +6,7 @@
 //     shorter set, binary-searches the longer one, and a ballot + popcount places the hits, so
 //     the list comes out ascending.  The output range of edge i is kofs[i] .. kofs[i+1]
 //     (exclusive scan of w), and a length other than w flags the edge list as foreign.
+//   edge_blosum_device: the BLOSUM-weighted score of every edge over the same intersection.
 //   edge_kmers_to_ids: codes -> repeat-MPHF ids, ascending within each edge (one 64-bit sort of
 //     (edge, id)), and each edge's rank in the reference's final edge order, ascending
 //     (min shared id, p, q) (combine_edges with one thread).
@@ -72,6 +73,68 @@ __global__ __launch_bounds__(256) void edge_kmers_kernel(const uint32_t* __restr
     }
 }
 
+// BLOSUM62 self-scores in residue-code order (the diagonal of blosum.rs:8-30, whose rows follow
+// the same C S T A G P D E Q N H R K M I L V W Y F order as AMINO_ACID_LIST); code 20 ('*' and
+// unknown residues) scores 0
+__constant__ int8_t c_b62_diag[21] = {9, 4, 5, 4, 6, 7, 6, 5, 5, 6, 8, 5, 5, 5, 4, 4, 4, 11, 7, 6, 0};
+
+// BLOSUM-weighted score of every edge (a build extension, parity
+// unpinned): score = Σ over the shared k-mers x of Σ_i B62[x_i][x_i].  One wavefront per edge
+// intersects the repeat-filtered sets as edge_kmers_kernel does; each hit adds its k-mer's
+// self-score (radix-21 digits of the code), a wave reduction sums them.  hits != w flags the
+// edge list as foreign.
+__global__ __launch_bounds__(256) void edge_blosum_kernel(const uint32_t* __restrict__ rep,
+                                                          const uint32_t* __restrict__ rep_len,
+                                                          const uint64_t* __restrict__ off,
+                                                          const uint32_t* __restrict__ ep,
+                                                          const uint32_t* __restrict__ eq,
+                                                          const uint32_t* __restrict__ ew, uint64_t count, int k,
+                                                          float* __restrict__ score, unsigned int* __restrict__ bad) {
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint64_t e = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); e < count; e += (uint64_t)gridDim.x * kWaves) {
+        const uint32_t a = ep[e], b = eq[e];
+        const uint32_t* A = rep + set_base(off[a], a);
+        const uint32_t* B = rep + set_base(off[b], b);
+        uint32_t la = rep_len[a], lb = rep_len[b];
+        if (la > lb) {
+            const uint32_t* t = A;
+            A = B;
+            B = t;
+            const uint32_t u = la;
+            la = lb;
+            lb = u;
+        }
+        int sum = 0, hits = 0;
+        for (uint32_t c = 0; c < la; c += 64) {
+            const uint32_t i = c + lane;
+            if (i >= la) continue;
+            const uint32_t x = A[i];
+            uint32_t lo = 0, hi = lb;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (B[mid] < x) lo = mid + 1;
+                else hi = mid;
+            }
+            if (lo < lb && B[lo] == x) {
+                uint32_t v = x;
+                for (int t = 0; t < k; ++t) {
+                    sum += c_b62_diag[v % kRadix];
+                    v /= kRadix;
+                }
+                ++hits;
+            }
+        }
+        for (int sh = 32; sh > 0; sh >>= 1) {
+            sum += __shfl_down(sum, sh);
+            hits += __shfl_down(hits, sh);
+        }
+        if (lane == 0) {
+            score[e] = (float)sum;  // an integer below 2^24: exact
+            if ((uint32_t)hits != ew[e]) atomicOr(bad, 1u);
+        }
+    }
+}
+
 // (edge, id) keys: the edge owning entry j is the largest e with kofs[e] <= j
 __global__ void edge_id_keys_kernel(const uint64_t* __restrict__ ids, uint64_t total, const uint64_t* __restrict__ kofs,
                                     uint64_t count, unsigned long long* __restrict__ keys) {
@@ -133,6 +196,28 @@ int edge_kmers_device(const uint32_t* d_rep, const uint32_t* d_rep_len, const ui
     }
     (void)hipFree(bad);
     if (rc == KMP_OK && h_bad) rc = KMP_EINVAL;  // w does not match the sets: edges of another build
+    return rc;
+}
+
+int edge_blosum_device(const uint32_t* d_rep, const uint32_t* d_rep_len, const uint64_t* d_off, const uint32_t* d_p,
+                       const uint32_t* d_q, const uint32_t* d_w, uint64_t count, int k, float* d_score,
+                       hipStream_t st) {
+    if (count == 0) return KMP_OK;
+    unsigned int* bad = nullptr;
+    if (dmalloc(&bad, 1) != hipSuccess) return KMP_ENOMEM;
+    int rc = KMP_OK;
+    unsigned int h_bad = 0;
+    if (hipMemsetAsync(bad, 0, 4, st) != hipSuccess) rc = KMP_EDEVICE;
+    if (rc == KMP_OK) {
+        const uint32_t blocks = (uint32_t)std::min<uint64_t>((count + kWaves - 1) / kWaves, 1u << 20);
+        edge_blosum_kernel<<<blocks, 256, 0, st>>>(d_rep, d_rep_len, d_off, d_p, d_q, d_w, count, k, d_score, bad);
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpyAsync(&h_bad, bad, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            rc = KMP_EDEVICE;
+    }
+    (void)hipFree(bad);
+    if (rc == KMP_OK && h_bad) rc = KMP_EINVAL;
     return rc;
 }
 

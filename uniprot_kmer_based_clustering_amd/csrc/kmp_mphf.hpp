@@ -31,6 +31,9 @@ int hash_kmers_device(const kmp_mphf* m, const uint8_t* d_res, const uint64_t* d
 // shared k-mers of each edge (p[i], q[i]) (kmp_edgekmers.hip): w[i] = kofs[i+1] - kofs[i]
 // ascending codes at out[kofs[i] ..), from the repeat-filtered sets.  KMP_EINVAL when an edge's
 // intersection is not w long (edges of another kmp_build_sets).
+int edge_blosum_device(const uint32_t* d_rep, const uint32_t* d_rep_len, const uint64_t* d_off, const uint32_t* d_p,
+                       const uint32_t* d_q, const uint32_t* d_w, uint64_t count, int k, float* d_score,
+                       hipStream_t st);
 int edge_kmers_device(const uint32_t* d_rep, const uint32_t* d_rep_len, const uint64_t* d_off, const uint32_t* d_p,
                       const uint32_t* d_q, const uint64_t* d_kofs, uint64_t count, uint32_t* d_out, hipStream_t st);
 // codes -> repeat-MPHF ids in place, ascending within each edge; with d_ref_key, each edge's
