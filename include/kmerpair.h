@@ -169,6 +169,17 @@ int kmp_edges_count(const kmp_edges* e, uint64_t* n);
  * may be NULL.  score[] is w for KMP_SCORE_COUNT, Jaccard w/(S_p+S_q-w) otherwise. */
 int kmp_edges_get(const kmp_edges* e, uint32_t* p, uint32_t* q, uint32_t* w, float* score,
                   uint64_t cap, uint64_t* n);
+
+/* Config 5 of SURVEY.md §8d (k = 5 and k = 7 combined): w_k is computed independently for each k
+ * in ks[0..nk) (nk <= KMP_MULTI_K_MAX, distinct k in 1..7), and an edge is emitted when any w_k
+ * >= min_shared (classes differing as opts asks).  The per-k canonical lists are merged by
+ * (p, q): w = Σ_k w_k, score = Σ_k score_k (COUNT or BLOSUM; JACCARD -> KMP_EINVAL).  Runs
+ * kmp_build_sets for every k in turn: the context's sets are those of ks[nk-1] afterwards.
+ * kmp_edges_get_wk: the weights w_{ks[j]} of every merged edge (0 where that k shares none).
+ * A build extension: the reference has one k per run (main.rs), so parity is unpinned. */
+#define KMP_MULTI_K_MAX 4
+int kmp_pairs_multi_k(kmp_ctx* ctx, const kmp_pair_opts* opts, const int* ks, uint32_t nk, kmp_edges** out);
+int kmp_edges_get_wk(const kmp_edges* e, uint32_t j, uint32_t* wk, uint64_t cap, uint64_t* n);
 void kmp_edges_free(kmp_edges* e);
 
 /* ------------------------------------------------------------------ edge k-mers ---- */

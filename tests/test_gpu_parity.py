@@ -139,6 +139,34 @@ def test_blosum_scores(engine, oracle_mod, k):
     assert got == {(0, 1): 45.0, (0, 2): 55.0, (3, 4): 72.0}
 
 
+def test_multi_k_config5(engine, oracle_mod):
+    """Config-5 shape (log-uniform lengths, k = 5 and 7 combined, BLOSUM score): the union of the
+    per-k oracle edge lists with w_5, w_7 kept, w = w_5 + w_7, score = Σ_k BLOSUM score."""
+    b = K.synth(4000, 5, 1)
+    want = {}
+    for k in (5, 7):
+        o = oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=k, threads=8)
+        p, q, w = o.pairs()
+        s = o.blosum_scores(p, q)
+        for a, c, x, y in zip(p.tolist(), q.tolist(), w.tolist(), s.tolist()):
+            d = want.setdefault((a, c), {5: 0, 7: 0, "s": 0})
+            d[k] = x
+            d["s"] += y
+    engine.load(b)
+    e, wk = engine.pairs_multi_k((5, 7), score=_lib.KMP_SCORE_BLOSUM)
+    keys = sorted(want)
+    assert len(e) == len(keys) and len(keys) > 100
+    np.testing.assert_array_equal(e.p, np.array([a for a, _ in keys], np.uint32))
+    np.testing.assert_array_equal(e.q, np.array([c for _, c in keys], np.uint32))
+    np.testing.assert_array_equal(wk[5], np.array([want[x][5] for x in keys], np.uint32))
+    np.testing.assert_array_equal(wk[7], np.array([want[x][7] for x in keys], np.uint32))
+    np.testing.assert_array_equal(e.w, wk[5] + wk[7])
+    np.testing.assert_array_equal(e.score, np.array([want[x]["s"] for x in keys], np.float32))
+    assert (wk[7] > 0).sum() < (wk[5] > 0).sum()  # k = 7 shares less
+    with pytest.raises(_lib.KmpError):
+        engine.pairs_multi_k((5, 5))
+
+
 @pytest.mark.parametrize("eng", ENGINES, ids=ENGINE_IDS)
 @pytest.mark.parametrize("n,seed,law,k", [(10000, 2, 0, 7), (3000, 5, 1, 5), (3000, 5, 1, 7)])
 def test_synthetic_bit_exact(engine, oracle_mod, n, seed, law, k, eng):

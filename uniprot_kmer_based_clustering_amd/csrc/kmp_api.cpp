@@ -618,10 +618,87 @@ int kmp_edges_get(const kmp_edges* e, uint32_t* p, uint32_t* q, uint32_t* w, flo
     return KMP_OK;
 }
 
+// Config 5 of SURVEY.md §8d: w_k computed independently for each k; an edge is emitted when any
+// w_k >= min_shared (and, with require_class_diff, the classes differ).  Each k runs the whole
+// path (kmp_build_sets + kmp_pairs, which leave the context's sets at the last k), then the
+// canonical lists are merged by (p, q): w = Σ_k w_k, score = Σ_k score_k (COUNT / BLOSUM).
+int kmp_pairs_multi_k(kmp_ctx* c, const kmp_pair_opts* opts, const int* ks, uint32_t nk, kmp_edges** out) {
+    if (!c || !out || !ks || nk < 1 || nk > KMP_MULTI_K_MAX) return KMP_EINVAL;
+    *out = nullptr;
+    c->err.clear();
+    kmp_pair_opts o;
+    kmp_pair_opts_default(&o);
+    if (opts) o = *opts;
+    if (o.score == KMP_SCORE_JACCARD) return fail(c, KMP_EINVAL, "JACCARD does not sum over k");
+    for (uint32_t j = 0; j < nk; ++j) {
+        if (ks[j] < 1 || ks[j] > kMaxK) return fail(c, KMP_EINVAL, "k = %d", ks[j]);
+        for (uint32_t i = 0; i < j; ++i)
+            if (ks[i] == ks[j]) return fail(c, KMP_EINVAL, "k = %d twice", ks[j]);
+    }
+    std::vector<std::unique_ptr<kmp_edges>> lists;
+    for (uint32_t j = 0; j < nk; ++j) {
+        KMP_TRY(c, kmp_build_sets(c, ks[j]));
+        kmp_edges* e = nullptr;
+        KMP_TRY(c, kmp_pairs(c, &o, &e));
+        lists.emplace_back(e);
+    }
+    std::unique_ptr<kmp_edges> m(new (std::nothrow) kmp_edges);
+    if (!m) return fail(c, KMP_ENOMEM, "edges");
+    // nk-way merge of (p, q)-sorted lists
+    std::vector<size_t> at(nk, 0);
+    const uint64_t key_end = ~0ull;
+    auto key = [&](uint32_t j) {
+        const kmp_edges& e = *lists[j];
+        return at[j] < e.p.size() ? (uint64_t)e.p[at[j]] << 32 | e.q[at[j]] : key_end;
+    };
+    std::vector<std::vector<uint32_t>> wk(nk);
+    uint64_t nalign = 0;
+    for (;;) {
+        uint64_t best = key_end;
+        for (uint32_t j = 0; j < nk; ++j) best = std::min(best, key(j));
+        if (best == key_end) break;
+        uint32_t w = 0;
+        float s = 0.0f;
+        for (uint32_t j = 0; j < nk; ++j) {
+            uint32_t wj = 0;
+            if (key(j) == best) {
+                wj = lists[j]->w[at[j]];
+                s += lists[j]->score[at[j]];
+                ++at[j];
+            }
+            wk[j].push_back(wj);
+            w += wj;
+        }
+        m->p.push_back((uint32_t)(best >> 32));
+        m->q.push_back((uint32_t)best);
+        m->w.push_back(w);
+        m->score.push_back(s);
+        if (w > o.align_threshold) ++nalign;
+    }
+    m->ks.assign(ks, ks + nk);
+    for (uint32_t j = 0; j < nk; ++j) m->wk.insert(m->wk.end(), wk[j].begin(), wk[j].end());
+    c->counters.n_edges = m->p.size();
+    c->counters.n_align = nalign;
+    *out = m.release();
+    return KMP_OK;
+}
+
+int kmp_edges_get_wk(const kmp_edges* e, uint32_t j, uint32_t* wk, uint64_t cap, uint64_t* n) {
+    if (!e || !n) return KMP_EINVAL;
+    const uint64_t count = e->p.size();
+    *n = count;
+    if (j >= e->ks.size()) return KMP_EINVAL;
+    if (cap < count) return KMP_EOVERFLOW;
+    if (count && !wk) return KMP_EINVAL;
+    std::copy(e->wk.begin() + j * count, e->wk.begin() + (j + 1) * count, wk);
+    return KMP_OK;
+}
+
 int kmp_edges_kmers(kmp_ctx* c, kmp_edges* e, int space) {
     if (!c || !e) return KMP_EINVAL;
     c->err.clear();
     if (space != KMP_KMERS_CODES && space != KMP_KMERS_IDS) return fail(c, KMP_EINVAL, "space must be CODES or IDS");
+    if (e->ks.size() > 1) return fail(c, KMP_ESTATE, "k-mer lists of a multi-k edge set are per k: use one k");
     if (!c->k_sets) return fail(c, KMP_ESTATE, "kmp_build_sets first");
     KMP_TRY(c, use_device(c));
     const uint64_t count = e->p.size();

@@ -12,4 +12,7 @@ struct kmp_edges {
     std::vector<uint64_t> kofs;
     std::vector<uint32_t> kmers;
     std::vector<uint64_t> ref_key;  // IDS only: index in the reference's final edge order
+    // kmp_pairs_multi_k: the k of each merged list and the per-k weights (k-major: wk[j*count + i])
+    std::vector<int> ks;
+    std::vector<uint32_t> wk;
 };

@@ -214,6 +214,24 @@ class KmerPairEngine:
         with self.edge_set(min_shared, require_class_diff, align_threshold, score, engine) as es:
             return es.get()
 
+    def pairs_multi_k(self, ks=(5, 7), min_shared=1, require_class_diff=True, align_threshold=10,
+                      score=_lib.KMP_SCORE_COUNT, engine=_lib.KMP_ENGINE_AUTO):
+        """kmp_pairs_multi_k: the union over k of the per-k edge lists,
+        w = Σ_k w_k, score = Σ_k score_k.  Returns (Edges, {k: w_k array})."""
+        o = _lib.PairOpts(min_shared, int(require_class_diff), align_threshold, score, engine)
+        karr = (C.c_int * len(ks))(*ks)
+        h = C.c_void_p()
+        self._check(lib().kmp_pairs_multi_k(self._ctx, C.byref(o), karr, len(ks), C.byref(h)), "kmp_pairs_multi_k")
+        with EdgeSet(self, h) as es:
+            edges = es.get()
+            wk = {}
+            for j, k in enumerate(ks):
+                w = np.zeros(len(edges), np.uint32)
+                n = C.c_uint64()
+                check(lib().kmp_edges_get_wk(h, j, _ptr(w), len(w), C.byref(n)), "kmp_edges_get_wk")
+                wk[k] = w
+        return edges, wk
+
 
 class Mphf:
     """boomphf ``Mphf<u32>`` surface over the device MPHF (include/kmerpair.h "MPHF").
