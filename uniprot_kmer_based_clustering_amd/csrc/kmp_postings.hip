@@ -1142,6 +1142,8 @@ __global__ void gather_shards_kernel(const unsigned long long* __restrict__ src,
 constexpr int kSmallGeom[3] = {KMP_SMALL_GEOM};
 constexpr int kBucketSmallCap = kSmallGeom[0], kBucketSmallThreads = kSmallGeom[1], kBucketSmallTab = kSmallGeom[2];
 constexpr int kBucketLargeCap = 8192, kBucketLargeThreads = 1024, kBucketLargeTab = 13;
+// the large kernel grid-strides the (usually empty or short) list of large buckets
+constexpr int kBucketLargeGrid = 32;
 
 // ------------------------------------------------------------- bucket partition ------------
 // The residue path groups its keys by bucket (the top bbits of h) with two counting passes
@@ -2080,13 +2082,28 @@ __global__ __launch_bounds__(kPtScanThreads) void pt_colscan_kernel(uint32_t* __
     __shared__ uint32_t s_max;
     if (threadIdx.x == 0) s_max = 0;
     const uint32_t q = (cols + kPtScanThreads - 1) / kPtScanThreads, c0 = threadIdx.x * q;
+    constexpr uint32_t kG = 8;  // up to kG row groups: every load of the thread in flight at once
+    const bool small = groups <= kG;
+    uint32_t v[8][kG];
     uint32_t tot[8], sum = 0;
 #pragma unroll
     for (uint32_t i = 0; i < 8; ++i) {
         tot[i] = 0;
         const uint32_t c = c0 + i;
+        const bool on = i < q && c < cols;
+#pragma unroll
+        for (uint32_t g = 0; g < kG; ++g) v[i][g] = small && on && g < groups ? R[(uint64_t)g * cols + c] : 0u;
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) {
+        const uint32_t c = c0 + i;
         if (i >= q || c >= cols) continue;
-        tot[i] = col_sum(R + c, cols, groups);
+        if (small) {
+#pragma unroll
+            for (uint32_t g = 0; g < kG; ++g) tot[i] += v[i][g];
+        } else {
+            tot[i] = col_sum(R + c, cols, groups);
+        }
         sum += tot[i];
     }
     uint32_t mx = 0;
@@ -2101,7 +2118,17 @@ __global__ __launch_bounds__(kPtScanThreads) void pt_colscan_kernel(uint32_t* __
         const uint32_t c = c0 + i;
         if (i >= q || c >= cols) continue;
         colstart[c] = excl;
-        col_prefix_inplace(R + c, cols, groups, excl);
+        if (small) {
+            uint32_t run = excl;
+#pragma unroll
+            for (uint32_t g = 0; g < kG; ++g)
+                if (g < groups) {
+                    R[(uint64_t)g * cols + c] = run;
+                    run += v[i][g];
+                }
+        } else {
+            col_prefix_inplace(R + c, cols, groups, excl);
+        }
         excl += tot[i];
     }
     if (threadIdx.x == 0) {
@@ -2435,8 +2462,9 @@ int fused_enqueue(kmp_postings* ws, MakeKeys& make_keys, uint64_t slots, const L
     launch_bucket_small<false>(nb, st, ws->sorted.p, bstart, lay, mul, require_class_diff, heavy_df, ws->inc_sorted.p,
                                sc, cursor, gstats, flags, list, list_count, ps);
     bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeTab, false>
-        <<<256, kBucketLargeThreads, 0, st>>>(ws->sorted.p, bstart, lay, mul, require_class_diff, heavy_df,
-                                              ws->inc_sorted.p, sc, cursor, gstats, flags, list, list_count, ps);
+        <<<kBucketLargeGrid, kBucketLargeThreads, 0, st>>>(ws->sorted.p, bstart, lay, mul, require_class_diff,
+                                                           heavy_df, ws->inc_sorted.p, sc, cursor, gstats, flags, list,
+                                                           list_count, ps);
     ws->mark(3, st);
     if (pt) {
         hipError_t e = hipSuccess;
