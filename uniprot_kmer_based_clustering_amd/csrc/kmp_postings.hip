@@ -1347,9 +1347,23 @@ __device__ __forceinline__ void bp_place(const unsigned long long (&x)[kBpPer], 
     // lh[d] -> global base of the digit's run minus its tile start: out[lh[d] + i] for S[i]
     for (uint32_t d = threadIdx.x; d < nb; d += kKeyThreads) lh[d] = prow[d] - lh[d];
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < n_in; i += kKeyThreads) {
-        const unsigned long long y = S[i];
-        out[lh[digit(y)] + i] = y;
+    // pairs (i, i+1), i even: one 16-byte store when both keys belong to the same run and its
+    // destination is 16-byte aligned (S is 16-byte aligned, i even), else two 8-byte stores
+    for (uint32_t i = 2 * threadIdx.x; i < n_in; i += 2 * kKeyThreads) {
+        if (i + 1 < n_in) {
+            const ulonglong2 y = *reinterpret_cast<const ulonglong2*>(S + i);
+            const uint32_t d0 = digit(y.x), d1 = digit(y.y);
+            const uint64_t a0 = (uint64_t)lh[d0] + i;
+            if (d0 == d1 && !(a0 & 1)) {
+                *reinterpret_cast<ulonglong2*>(out + a0) = y;
+            } else {
+                out[a0] = y.x;
+                out[(uint64_t)lh[d1] + i + 1] = y.y;
+            }
+        } else {
+            const unsigned long long y = S[i];
+            out[lh[digit(y)] + i] = y;
+        }
     }
 }
 
@@ -1459,7 +1473,7 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scatter2_kernel(const unsigned
                                                                   const uint32_t* __restrict__ C1, uint32_t J,
                                                                   BpDigits dg, const uint32_t* __restrict__ P2,
                                                                   unsigned long long* __restrict__ out) {
-    __shared__ unsigned long long S[kBpTile];
+    __shared__ __attribute__((aligned(16))) unsigned long long S[kBpTile];
     __shared__ uint32_t lh[kBpMaxBins];
     __shared__ uint32_t wave_tot[kKeyThreads / 64];
     const uint32_t j = blockIdx.x, c = blockIdx.y;
@@ -1510,7 +1524,7 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scatter_arr_kernel(const unsig
                                                                      uint64_t m, BpDigits dg,
                                                                      const uint32_t* __restrict__ P1,
                                                                      unsigned long long* __restrict__ out) {
-    __shared__ unsigned long long S[kBpTile];
+    __shared__ __attribute__((aligned(16))) unsigned long long S[kBpTile];
     __shared__ uint32_t lh[kBpMaxBins];
     __shared__ uint32_t wave_tot[kKeyThreads / 64];
     __shared__ uint32_t s_n;
