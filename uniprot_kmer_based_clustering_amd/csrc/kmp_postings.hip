@@ -949,12 +949,16 @@ __global__ __launch_bounds__(kThreads) void bucket_large_kernel(
     const unsigned long long* __restrict__ sorted, const uint32_t* __restrict__ bstart, Layout lay,
     uint32_t n_prot, int require_diff, uint32_t heavy_df, unsigned long long* __restrict__ out, uint64_t shard_cap,
     unsigned long long* __restrict__ cursor, unsigned long long* __restrict__ gstats, uint32_t* __restrict__ flags,
-    uint32_t* __restrict__ list, const uint32_t* __restrict__ list_count, PShard ps) {
+    uint32_t* __restrict__ list, const uint32_t* __restrict__ list_count, PShard ps, uint32_t lo = 0,
+    uint32_t hi = 0xFFFFFFFFu) {
+    // [lo, hi): the buckets of this launch (a pipelined chunk); the list may hold earlier chunks'
     const uint32_t m = *list_count;
-    for (uint32_t i = blockIdx.x; i < m; i += gridDim.x)
-        process_bucket<kCap, kThreads, kTabBits, kPShard>(list[i], sorted, bstart, lay, n_prot, require_diff,
-                                                          heavy_df, false, out, shard_cap, cursor, gstats, flags,
-                                                          nullptr, nullptr, ps);
+    for (uint32_t i = blockIdx.x; i < m; i += gridDim.x) {
+        const uint32_t b = list[i];
+        if (b < lo || b >= hi) continue;
+        process_bucket<kCap, kThreads, kTabBits, kPShard>(b, sorted, bstart, lay, n_prot, require_diff, heavy_df, false,
+                                                          out, shard_cap, cursor, gstats, flags, nullptr, nullptr, ps);
+    }
 }
 
 // ---------------------------------------------------------------- p-shard reduction --------
@@ -1414,9 +1418,10 @@ __device__ __forceinline__ bool bp_tile(const uint32_t* __restrict__ C1, uint32_
 // level 2, pass 1: per-tile digit2 histogram -> H2[c][j][digit]
 __global__ __launch_bounds__(kKeyThreads) void bp_hist2_kernel(const unsigned long long* __restrict__ in,
                                                                const uint32_t* __restrict__ C1, uint32_t J,
-                                                               BpDigits dg, uint32_t* __restrict__ H2) {
+                                                               BpDigits dg, uint32_t* __restrict__ H2,
+                                                               uint32_t c0) {
     __shared__ uint32_t lh[kBpMaxBins];
-    const uint32_t j = blockIdx.x, c = blockIdx.y;
+    const uint32_t j = blockIdx.x, c = c0 + blockIdx.y;
     uint32_t t0, tn;
     if (!bp_tile(C1, dg.nb1, c, j, J, t0, tn)) return;
     for (uint32_t d = threadIdx.x; d < dg.nb2; d += kKeyThreads) lh[d] = 0;
@@ -1442,16 +1447,16 @@ __global__ __launch_bounds__(kKeyThreads) void bp_hist2_kernel(const unsigned lo
 __global__ __launch_bounds__(kKeyThreads) void bp_scan2_kernel(uint32_t* __restrict__ H2,
                                                                const uint32_t* __restrict__ C1, uint32_t J,
                                                                BpDigits dg, uint32_t* __restrict__ bstart,
-                                                               uint32_t* __restrict__ flags) {
+                                                               uint32_t* __restrict__ flags, uint32_t c0) {
     __shared__ uint32_t tot[kBpMaxBins];
     __shared__ uint32_t wave_tot[kKeyThreads / 64];
-    const uint32_t c = blockIdx.x;
+    const uint32_t c = c0 + blockIdx.x;
     const uint32_t b0 = C1[dg.nb1 + 1 + c], n = C1[dg.nb1 + 2 + c] - b0;  // compact start, key count
     const uint32_t nt = (n + kBpTile - 1) / kBpTile;
     if (nt > J) {  // no tile of this bin was written: its buckets read as empty, the call falls back
         if (threadIdx.x == 0) flags[0] = 1;
         for (uint32_t d = threadIdx.x; d < dg.nb2; d += kKeyThreads) bstart[c * dg.nb2 + d] = b0;
-        if (c == gridDim.x - 1 && threadIdx.x == 0) bstart[gridDim.x * dg.nb2] = b0;
+        if (threadIdx.x == 0) bstart[(c + 1) * dg.nb2] = b0 + n;  // the bin's end (= the next bin's start)
         return;
     }
     uint32_t* base = H2 + (uint64_t)c * J * dg.nb2;
@@ -1465,18 +1470,20 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scan2_kernel(uint32_t* __restr
         bstart[c * dg.nb2 + d] = run;
         col_prefix_inplace(base + d, dg.nb2, nt, run);
     }
-    if (c == gridDim.x - 1 && threadIdx.x == 0) bstart[gridDim.x * dg.nb2] = b0 + n;
+    // the bin's end, which the next bin's scan writes too (same value): a chunk of bins is
+    // complete without the scan of the next chunk (pipelined level 2)
+    if (threadIdx.x == 0) bstart[(c + 1) * dg.nb2] = b0 + n;
 }
 
 // level 2, pass 2: the tile's keys grouped by digit2 at P2[c][j][digit]
 __global__ __launch_bounds__(kKeyThreads) void bp_scatter2_kernel(const unsigned long long* __restrict__ in,
                                                                   const uint32_t* __restrict__ C1, uint32_t J,
                                                                   BpDigits dg, const uint32_t* __restrict__ P2,
-                                                                  unsigned long long* __restrict__ out) {
+                                                                  unsigned long long* __restrict__ out, uint32_t c0) {
     __shared__ __attribute__((aligned(16))) unsigned long long S[kBpTile];
     __shared__ uint32_t lh[kBpMaxBins];
     __shared__ uint32_t wave_tot[kKeyThreads / 64];
-    const uint32_t j = blockIdx.x, c = blockIdx.y;
+    const uint32_t j = blockIdx.x, c = c0 + blockIdx.y;
     uint32_t t0, tn;
     if (!bp_tile(C1, dg.nb1, c, j, J, t0, tn)) return;
     for (uint32_t d = threadIdx.x; d < dg.nb2; d += kKeyThreads) lh[d] = 0;
@@ -1626,6 +1633,8 @@ struct Grow {
 
 }  // namespace
 
+constexpr uint32_t kPipeMax = 16;  // coarse-bin chunks of the pipelined fused step, at most
+
 struct kmp_postings {
     Grow<unsigned long long> keys, sorted, inc, inc_sorted, uniq, bstats, btot, boff;
     Grow<uint32_t> w, keep, pos, small, cnt, flags;  // flags: [0] bucket overflow, [1] class width, [2] list count
@@ -1659,6 +1668,11 @@ struct kmp_postings {
     hipStream_t cst = nullptr;  // capture stream
     std::vector<unsigned long long> gkey, gkey_seen;
     uint64_t graph_replays = 0;
+    // fused step: level 2 and the bucket kernels pipelined over pipe_k coarse-bin chunks on a
+    // second stream (1 = serial, the default: pipelining measured slower)
+    int pipe_k = getenv("KMP_PIPE") ? atoi(getenv("KMP_PIPE")) : 1;
+    hipStream_t pst = nullptr;
+    hipEvent_t pev[kPipeMax + 2] = {};
     // read-back of the fused step (kRbWords: gstats | cursors | flags | run count | largest row
     // block), written by fused_pack_kernel into coherent pinned host memory
     unsigned long long* hrb = nullptr;
@@ -1674,6 +1688,9 @@ struct kmp_postings {
         if (hrb) (void)hipHostFree(hrb);
         if (gexec) (void)hipGraphExecDestroy(gexec);
         if (cst) (void)hipStreamDestroy(cst);
+        for (auto& e : pev)
+            if (e) (void)hipEventDestroy(e);
+        if (pst) (void)hipStreamDestroy(pst);
     }
     void mark(int stage, hipStream_t st) {
         if (timing) (void)hipEventRecord(ev[stage], st);
@@ -1756,15 +1773,16 @@ hipError_t bp_level1_array(kmp_postings* ws, const unsigned long long* d_keys, u
 }
 
 // Level 2: ws->keys (level 1) -> ws->sorted grouped by bucket, bstart[0..nb] in ws->cnt.
-int bp_level2(kmp_postings* ws, const Layout& lay, hipStream_t st) {
+int bp_level2(kmp_postings* ws, const Layout& lay, hipStream_t st, uint32_t c0 = 0, uint32_t bins = 0) {
     const BpDigits dg = bp_digits(lay);
     uint32_t* C1 = ws->bp.p + ws->bp_c1;
     uint32_t* H2 = C1 + 2 * (dg.nb1 + 1);
     const uint32_t nb = 1u << lay.bbits, J = ws->bp_J;
+    if (bins == 0) bins = dg.nb1 - c0;  // coarse bins [c0, c0 + bins)
     PG(ws->cnt.reserve(2 * (uint64_t)nb + 2));
-    bp_hist2_kernel<<<dim3(J, dg.nb1), kKeyThreads, 0, st>>>(ws->keys.p, C1, J, dg, H2);
-    bp_scan2_kernel<<<dg.nb1, kKeyThreads, 0, st>>>(H2, C1, J, dg, ws->cnt.p, ws->flags.p);
-    bp_scatter2_kernel<<<dim3(J, dg.nb1), kKeyThreads, 0, st>>>(ws->keys.p, C1, J, dg, H2, ws->sorted.p);
+    bp_hist2_kernel<<<dim3(J, bins), kKeyThreads, 0, st>>>(ws->keys.p, C1, J, dg, H2, c0);
+    bp_scan2_kernel<<<bins, kKeyThreads, 0, st>>>(H2, C1, J, dg, ws->cnt.p, ws->flags.p, c0);
+    bp_scatter2_kernel<<<dim3(J, bins), kKeyThreads, 0, st>>>(ws->keys.p, C1, J, dg, H2, ws->sorted.p, c0);
     PG(hipGetLastError());
     return KMP_OK;
 }
@@ -2054,6 +2072,7 @@ struct PtGeom {
     uint32_t nshards;       // shard regions (kShards), or 1 for a flat array
     uint32_t row0;          // first row (a multi-GPU owner's row range)
     uint64_t flat_n;        // nonzero: one region of flat_n keys with kNoKey padding (no cursors)
+    uint32_t rank;          // pt_reduce: counting sort by row + rank sort in the row when rows are short
 };
 
 __device__ __forceinline__ uint32_t pt_tile_keys(const unsigned long long* __restrict__ cursor, const PtGeom& g,
@@ -2463,22 +2482,51 @@ int fused_enqueue(kmp_postings* ws, MakeKeys& make_keys, uint64_t slots, const L
     ws->mark(0, st);
     PG(make_keys(lay, st));
     ws->mark(1, st);
-    {
-        int rc = bucket_group(ws, ws->keys.p, slots, lay, st);
-        if (rc != KMP_OK) return rc;
-    }
-    uint32_t* bstart = ws->cnt.p;
-    uint32_t* list = ws->cnt.p + nb + 1;
     PShard ps{};
     PtGeom g;
     const bool pt = pt_geometry(ws, slots, n, &g);
     const uint32_t mul = pt ? 1u << g.pbits : n;  // pair key p * mul + q
-    launch_bucket_small<false>(nb, st, ws->sorted.p, bstart, lay, mul, require_class_diff, heavy_df, ws->inc_sorted.p,
-                               sc, cursor, gstats, flags, list, list_count, ps);
-    bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeTab, false>
-        <<<kBucketLargeGrid, kBucketLargeThreads, 0, st>>>(ws->sorted.p, bstart, lay, mul, require_class_diff,
-                                                           heavy_df, ws->inc_sorted.p, sc, cursor, gstats, flags, list,
-                                                           list_count, ps);
+    const BpDigits dg = bp_digits(lay);
+    const uint32_t K = ws->parted ? std::min<uint32_t>((uint32_t)std::max(ws->pipe_k, 1), std::min(dg.nb1, kPipeMax))
+                                  : 1u;
+    PG(ws->sorted.reserve(slots));
+    PG(ws->cnt.reserve(2 * (uint64_t)nb + 2));
+    uint32_t* bstart = ws->cnt.p;
+    uint32_t* list = ws->cnt.p + nb + 1;
+    // group + expand buckets [b_lo, b_hi) on stream s
+    auto group_range = [&](uint32_t b_lo, uint32_t b_hi, hipStream_t s) {
+        launch_bucket_small<false>(b_hi - b_lo, s, ws->sorted.p, bstart, lay, mul, require_class_diff, heavy_df,
+                                   ws->inc_sorted.p, sc, cursor, gstats, flags, list, list_count, ps, b_lo);
+        bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeTab, false>
+            <<<kBucketLargeGrid, kBucketLargeThreads, 0, s>>>(ws->sorted.p, bstart, lay, mul, require_class_diff,
+                                                              heavy_df, ws->inc_sorted.p, sc, cursor, gstats, flags,
+                                                              list, list_count, ps, b_lo, b_hi);
+    };
+    if (K <= 1) {
+        int rc = bucket_group(ws, ws->keys.p, slots, lay, st);
+        if (rc != KMP_OK) return rc;
+        group_range(0, nb, st);
+    } else {
+        // level 2 (HBM-bound scatter) of coarse-bin chunk i+1 runs on st while chunk i's buckets
+        // (VALU-bound) are grouped on ws->pst: a fork / join captured into the step graph
+        ws->parted = false;
+        if (!ws->pst) PG(hipStreamCreateWithFlags(&ws->pst, hipStreamNonBlocking));
+        for (uint32_t i = 0; i <= K + 1; ++i)
+            if (!ws->pev[i]) PG(hipEventCreateWithFlags(&ws->pev[i], hipEventDisableTiming));
+        PG(hipEventRecord(ws->pev[0], st));
+        PG(hipStreamWaitEvent(ws->pst, ws->pev[0], 0));
+        for (uint32_t i = 0; i < K; ++i) {
+            const uint32_t c0 = (uint32_t)((uint64_t)dg.nb1 * i / K), c1 = (uint32_t)((uint64_t)dg.nb1 * (i + 1) / K);
+            int rc = bp_level2(ws, lay, st, c0, c1 - c0);
+            if (rc != KMP_OK) return rc;
+            PG(hipEventRecord(ws->pev[1 + i], st));
+            PG(hipStreamWaitEvent(ws->pst, ws->pev[1 + i], 0));
+            group_range(c0 * dg.nb2, c1 * dg.nb2, ws->pst);
+        }
+        ws->mark(2, st);
+        PG(hipEventRecord(ws->pev[K + 1], ws->pst));
+        PG(hipStreamWaitEvent(st, ws->pev[K + 1], 0));
+    }
     ws->mark(3, st);
     if (pt) {
         hipError_t e = hipSuccess;
