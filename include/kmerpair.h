@@ -448,6 +448,10 @@ int kmp_dev_edges_rows(kmp_postings* ws, const unsigned long long* d_pk, uint64_
 /* Row-block tail on (default) or off for the fused residue step and kmp_dev_edges_rows; the
  * workspace turns it off by itself after a row too long for LDS. */
 int kmp_postings_set_rowtail(kmp_postings* ws, int enable);
+/* Row-block tail, in-block sort (combine_edges, mod.rs:322-546): 1 counts a block's keys by row
+ * and rank-sorts each row in LDS when every row holds at most 512 keys, else the block radix
+ * sort; 0 (default; env KMP_PT_RANK=1 turns 1 on) always the block radix sort.  Same edges. */
+int kmp_postings_set_rowrank(kmp_postings* ws, int enable);
 
 /* Canonical order: sorts n edges by (p, q).  Keys/values are read from d_p/d_q/d_w and the
  * sorted result is written back to them.  d_tmp: kmp_dev_sort_edges_tmp_bytes(n, N) bytes. */

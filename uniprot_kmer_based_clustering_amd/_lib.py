@@ -134,6 +134,7 @@ SIGNATURES = {
     "kmp_postings_set_pshard": (C.c_int, [P, C.c_int]),
     "kmp_postings_set_partition": (C.c_int, [P, C.c_int]),
     "kmp_postings_set_rowtail": (C.c_int, [P, C.c_int]),
+    "kmp_postings_set_rowrank": (C.c_int, [P, C.c_int]),
     "kmp_pairs_multi_k": (C.c_int, [P, P, C.POINTER(C.c_int), C.c_uint32, C.POINTER(P)]),
     "kmp_edges_get_wk": (C.c_int, [P, C.c_uint32, P, C.c_uint64, C.POINTER(C.c_uint64)]),
     "kmp_postings_set_graph": (C.c_int, [P, C.c_int]),

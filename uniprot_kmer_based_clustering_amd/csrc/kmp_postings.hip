@@ -1657,6 +1657,9 @@ struct kmp_postings {
     bool pt_on = !getenv("KMP_ROWTAIL") || atoi(getenv("KMP_ROWTAIL")) != 0;  // fused step: row-block tail
     uint64_t pt_inc = 0;        // incidences of the last fused call (row-block sizing)
     unsigned pt_rb_max = 16;    // rows-per-block bound learned from overflowing row blocks
+    // row-block tail: rank sort inside short rows instead of the block radix sort (opt-in,
+    // KMP_PT_RANK=1: measured slower)
+    uint32_t pt_rank = getenv("KMP_PT_RANK") && atoi(getenv("KMP_PT_RANK")) != 0;
     uint32_t bp_J = 0;          // level-2 tiles per coarse bin
     uint64_t bp_c1 = 0;         // offset of C1 (coarse bin starts) in ws->bp
     bool partition = !getenv("KMP_PARTITION") || atoi(getenv("KMP_PARTITION")) != 0;  // residue keys: counting partition
@@ -2228,18 +2231,78 @@ using PtSort = rocprim::block_radix_sort<uint32_t, kPtRThreads, kE>;
 struct PtRuns {
     uint32_t hs[kPtCap + 1];  // rank of each run's first key
 };
+struct PtRank {
+    __attribute__((aligned(16))) uint32_t B[kPtCap + 4];  // the block's keys grouped by row (+ padding)
+    __attribute__((aligned(16))) uint32_t A[kPtCap];      // ... sorted
+};
 union PtReduceLds {
     typename PtSort<2>::storage_type s2;
     typename PtSort<4>::storage_type s4;
     typename PtSort<8>::storage_type s8;
     typename PtSort<16>::storage_type s16;
     PtRuns runs;
+    PtRank rk;
 };
+constexpr uint32_t kPtRankRows = 1024;   // rank sort: rows per block (LDS row cursors) ...
+constexpr uint32_t kPtRankRowMax = 512;  // ... and keys per row at most
+
+// Sort of a row block's keys for short rows (config 3: ~50 keys per row, 64 rows per block):
+// a counting sort by row (LDS cursors), then a rank sort inside each row, rank = the row's
+// smaller keys + its equal keys at earlier positions.  Rows are runs of B in row order, so
+// every key before the row is smaller and every key after it larger: each thread counts over
+// [row start rounded down to 4, row end) with 16-byte broadcast loads and subtracts the
+// earlier rows' keys.  O(row length) per key, against the three 8-bit passes of the block
+// radix sort.  On return k[] is blocked (thread t holds ranks t*kE + e, padding 0xFFFFFFFF) as
+// after the radix sort; false, with nothing written to s, when a row is longer than
+// kPtRankRowMax.
+template <uint32_t kE>
+__device__ __forceinline__ bool pt_rank_sort(PtRank& s, uint32_t* rc, uint32_t* wave_tot, uint32_t* s_big,
+                                             uint32_t (&k)[kE], uint32_t n, const PtGeom& g) {
+    const uint32_t nrows = 1u << g.rbits;
+    for (uint32_t t = threadIdx.x; t < nrows; t += kPtRThreads) rc[t] = 0;
+    if (threadIdx.x == 0) {
+        *s_big = 0;
+        rc[nrows] = n;
+    }
+    __syncthreads();
+    uint32_t rk[kE];
+#pragma unroll
+    for (uint32_t e = 0; e < kE; ++e)
+        rk[e] = threadIdx.x + e * kPtRThreads < n ? atomicAdd(&rc[k[e] >> g.pbits], 1u) : 0u;
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < nrows; t += kPtRThreads)
+        if (rc[t] > kPtRankRowMax) *s_big = 1;
+    lds_bins_scan<kPtRThreads>(rc, nrows, wave_tot);  // ends with a barrier
+    if (*s_big) return false;
+#pragma unroll
+    for (uint32_t e = 0; e < kE; ++e)
+        if (threadIdx.x + e * kPtRThreads < n) s.B[rc[k[e] >> g.pbits] + rk[e]] = k[e];
+    if (threadIdx.x < 4) s.B[n + threadIdx.x] = 0xFFFFFFFFu;  // past the last row: larger than any key
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += kPtRThreads) {
+        const uint32_t v = s.B[i], row = v >> g.pbits, r0 = rc[row], r1 = rc[row + 1], j0 = r0 & ~3u;
+        uint32_t less = 0, eq = 0;
+        for (uint32_t j = j0; j < r1; j += 4) {
+            const uint4 x = *reinterpret_cast<const uint4*>(s.B + j);
+            less += (x.x < v) + (x.y < v) + (x.z < v) + (x.w < v);
+            eq += (x.x == v && j < i) + (x.y == v && j + 1 < i) + (x.z == v && j + 2 < i) + (x.w == v && j + 3 < i);
+        }
+        s.A[j0 + less + eq] = v;  // r0 + (less - (r0 - j0)) + eq
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t e = 0; e < kE; ++e) {
+        const uint32_t idx = threadIdx.x * kE + e;
+        k[e] = idx < n ? s.A[idx] : 0xFFFFFFFFu;
+    }
+    return true;
+}
 
 // row block r's n keys (n <= kE * kPtRThreads): sort, run-length encode, stage the runs
 template <uint32_t kE>
 __device__ __forceinline__ void pt_reduce_block(PtReduceLds& u, typename PtSort<kE>::storage_type& st,
-                                                uint32_t* last, uint32_t* wave_tot, const uint32_t* __restrict__ keys,
+                                                uint32_t* last, uint32_t* wave_tot, uint32_t* rc, uint32_t* s_big,
+                                                const uint32_t* __restrict__ keys,
                                                 uint32_t r, uint32_t s0, uint32_t n, const PtGeom& g,
                                                 uint32_t* __restrict__ stage_p, uint32_t* __restrict__ stage_q,
                                                 uint32_t* __restrict__ stage_w, uint32_t* __restrict__ counts) {
@@ -2249,7 +2312,9 @@ __device__ __forceinline__ void pt_reduce_block(PtReduceLds& u, typename PtSort<
         const uint32_t i = threadIdx.x + e * kPtRThreads;
         k[e] = i < n ? keys[s0 + i] : 0xFFFFFFFFu;
     }
-    PtSort<kE>().sort(k, st, 0, g.pbits + g.rbits);  // blocked: thread t holds ranks t*kE + e
+    // blocked: thread t holds ranks t*kE + e
+    if (!(g.rank && (1u << g.rbits) <= kPtRankRows && pt_rank_sort<kE>(u.rk, rc, wave_tot, s_big, k, n, g)))
+        PtSort<kE>().sort(k, st, 0, g.pbits + g.rbits);
     last[threadIdx.x] = k[kE - 1];
     __syncthreads();
     const uint32_t rank0 = threadIdx.x * kE;
@@ -2293,6 +2358,8 @@ __global__ __launch_bounds__(kPtRThreads) void pt_reduce_kernel(const uint32_t* 
     __shared__ PtReduceLds u;
     __shared__ uint32_t last[kPtRThreads];
     __shared__ uint32_t wave_tot[kPtRThreads / 64];
+    __shared__ uint32_t rc[kPtRankRows + 1];
+    __shared__ uint32_t s_big;
     const uint32_t r = blockIdx.x, s0 = bst[r], n = bst[r + 1] - s0;
     if (n == 0 || n > kPtCap) {
         if (threadIdx.x == 0) {
@@ -2302,13 +2369,14 @@ __global__ __launch_bounds__(kPtRThreads) void pt_reduce_kernel(const uint32_t* 
         return;
     }
     if (n <= 2 * kPtRThreads)
-        pt_reduce_block<2>(u, u.s2, last, wave_tot, keys, r, s0, n, g, stage_p, stage_q, stage_w, counts);
+        pt_reduce_block<2>(u, u.s2, last, wave_tot, rc, &s_big, keys, r, s0, n, g, stage_p, stage_q, stage_w, counts);
     else if (n <= 4 * kPtRThreads)
-        pt_reduce_block<4>(u, u.s4, last, wave_tot, keys, r, s0, n, g, stage_p, stage_q, stage_w, counts);
+        pt_reduce_block<4>(u, u.s4, last, wave_tot, rc, &s_big, keys, r, s0, n, g, stage_p, stage_q, stage_w, counts);
     else if (n <= 8 * kPtRThreads)
-        pt_reduce_block<8>(u, u.s8, last, wave_tot, keys, r, s0, n, g, stage_p, stage_q, stage_w, counts);
+        pt_reduce_block<8>(u, u.s8, last, wave_tot, rc, &s_big, keys, r, s0, n, g, stage_p, stage_q, stage_w, counts);
     else
-        pt_reduce_block<16>(u, u.s16, last, wave_tot, keys, r, s0, n, g, stage_p, stage_q, stage_w, counts);
+        pt_reduce_block<16>(u, u.s16, last, wave_tot, rc, &s_big, keys, r, s0, n, g, stage_p, stage_q, stage_w,
+                            counts);
 }
 
 // exclusive scan of the nrb run counts (nrb <= 8 * 1024) -> eoff; eoff[nrb] and *total = edges
@@ -2410,6 +2478,7 @@ bool pt_geometry(const kmp_postings* ws, uint64_t slots, uint32_t n, PtGeom* g) 
     g->nshards = kShards;
     g->row0 = 0;
     g->flat_n = 0;
+    g->rank = ws->pt_rank;
     return true;
 }
 
@@ -2640,7 +2709,7 @@ int run_fused(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long l
         const bool pt = pt_geometry(ws, slots, n, &pg);
         key.push_back(sc);
         key.push_back(ws->timing);
-        key.push_back(pt ? pg.rbits + 1 : 0);
+        key.push_back(pt ? (pg.rbits + 1) | pg.rank << 8 : 0);
         key.push_back(g_grow_gen);
         int rc = fused_launch(ws, make_keys, key, slots, lay, n, heavy_df, require_class_diff, d_p, d_q, d_w, cap, st);
         key.resize(key.size() - 4);
@@ -3399,6 +3468,7 @@ int kmp_dev_edges_rows(kmp_postings* ws, const unsigned long long* d_pk, uint64_
     g.nshards = 1;
     g.row0 = row_lo;
     g.flat_n = m;
+    g.rank = ws->pt_rank;
     hipError_t e = hipSuccess;
     const PtBufs b = pt_bufs(ws, g, true, &e);
     PG(e);
@@ -3427,6 +3497,12 @@ int kmp_dev_edges_rows(kmp_postings* ws, const unsigned long long* d_pk, uint64_
 int kmp_postings_set_rowtail(kmp_postings* ws, int enable) {
     if (!ws) return KMP_EINVAL;
     ws->pt_on = enable != 0;
+    return KMP_OK;
+}
+
+int kmp_postings_set_rowrank(kmp_postings* ws, int enable) {
+    if (!ws) return KMP_EINVAL;
+    ws->pt_rank = enable != 0;
     return KMP_OK;
 }
 

@@ -223,6 +223,11 @@ class DevicePipeline:
         global pair-key sort."""
         check(lib().kmp_postings_set_pshard(self._workspace(), int(enable)), "kmp_postings_set_pshard")
 
+    def set_rowrank(self, enable: bool = True) -> None:
+        """Row-block tail: rank-sort short rows in LDS, or always use the block radix sort
+        (default: measured faster)."""
+        check(lib().kmp_postings_set_rowrank(self._workspace(), int(enable)), "kmp_postings_set_rowrank")
+
     def set_partition(self, enable: bool = True) -> None:
         """Residue path: group keys by bucket with the two-level counting partition (default) or
         write every key and radix-sort the bucket field."""
