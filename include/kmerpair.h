@@ -338,27 +338,23 @@ int kmp_postings_create(kmp_postings** ws);
 void kmp_postings_destroy(kmp_postings* ws);
 /* Records HIP events between the stages on the call's stream (stats->stage_ms). */
 int kmp_postings_set_timing(kmp_postings* ws, int enable);
-/* Key layout.  bucketed (default 1): keys sorted on a 2^b-bucket hash of the k-mer only, then one
- * workgroup per bucket groups, deduplicates and expands its k-mers in LDS; buckets that do not
- * fit (very frequent k-mers) make the call rerun on the flat layout.  0: always flat (full code
- * sort, scan-based expansion).  kmp_postings_last_layout: 0 flat, 1 bucketed with the pair-key
- * sort tail, 2 bucketed with the row-range (p-shard) tail, 3 bucketed single-synchronisation path
- * (min_shared == 1: padded shard regions sorted in place of the gather, one read-back), 4 the same
- * single-synchronisation path with the row-block tail (pair keys partitioned by p range, each
- * range sorted and run-length encoded in LDS; rows too long for LDS send the call to 3).
- * kmp_postings_set_pshard (default 0): 1 makes the bucketed expansion write each pair key into the
- * region of its row range (p >> r), and one workgroup per range sorts, run-length encodes and
- * filters it in LDS instead of the global pair-key sort; ranges above the LDS capacity fall back to
- * the sort tail.  Measured slower at config 3 (per-key cursor atomics), kept for experiments. */
+/* Key layout.  bucketed (default 1): keys grouped by a 2^b-bucket hash of the k-mer (a two-level
+ * counting partition from the residues), then one workgroup per bucket groups, deduplicates and
+ * expands its k-mers in LDS; a frequent k-mer (more than 128 keys) is spilled whole to the heavy
+ * path (sorted, split into tiles of its C(df,2) pairs across workgroups), so no df is too large.
+ * 0: always flat (full code sort, scan-based expansion; also the fallback for class ids wider
+ * than the bucketed key's class field, 31 - bits(N) bits).
+ * kmp_postings_last_layout: KMP_LAYOUT_FLAT, KMP_LAYOUT_BUCKETED (single-synchronisation step,
+ * graph-captured from the second call of a shape) or KMP_LAYOUT_BUCKETED_HEAVY (the batch spilled
+ * frequent k-mers: the split step with the heavy path).  kmp_postings_last_overflow_blocks: row
+ * blocks of the pair tail above the LDS capacity (a protein pairing with thousands of later
+ * proteins) that the last call finished with the segmented sort. */
+enum { KMP_LAYOUT_FLAT = 0, KMP_LAYOUT_BUCKETED = 1, KMP_LAYOUT_BUCKETED_HEAVY = 2 };
 int kmp_postings_set_layout(kmp_postings* ws, int bucketed);
 int kmp_postings_last_layout(const kmp_postings* ws);
-int kmp_postings_set_pshard(kmp_postings* ws, int enable);
-/* Residue entry point, bucketed layout: 1 (default) groups the keys by bucket with a two-level
- * counting partition computed straight from the residues (no materialised keys, no radix sort);
- * 0 writes every key and radix-sorts the bucket field.  Same edges either way. */
-int kmp_postings_set_partition(kmp_postings* ws, int enable);
-/* Single-synchronisation residue path as a HIP graph (default 1): captured on the second call
- * with an unchanged shape (pointers, sizes, options, workspace buffers), replayed after that.
+uint32_t kmp_postings_last_overflow_blocks(const kmp_postings* ws);
+/* The bucketed step as a HIP graph (default 1): captured on the second call with an unchanged
+ * shape (pointers, sizes, options, workspace buffers), replayed after that.
  * kmp_postings_graph_replays: calls served by a replay so far. */
 int kmp_postings_set_graph(kmp_postings* ws, int enable);
 uint64_t kmp_postings_graph_replays(const kmp_postings* ws);
@@ -378,80 +374,20 @@ int kmp_dev_pairs_residues(kmp_postings* ws, const uint8_t* d_res, const uint64_
                            uint32_t min_shared, int require_class_diff, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w,
                            uint64_t cap, uint64_t* n_edges, kmp_postings_stats* stats, void* stream);
 
-/* Multi-GPU split of the postings engine (one process per GPU; dist.py does the exchanges).
- * K-mer buckets are split into `parts` contiguous ranges (part j = buckets [j*nb/parts,
- * (j+1)*nb/parts)), proteins into contiguous p ranges (part j = p in [ceil(j*N/parts),
- * ceil((j+1)*N/parts))).
- *   1. kmp_dev_keys_part: keys of the k-mer windows of proteins [lo, hi) (their slots
- *      [slot_lo, slot_hi) = [kmp_set_base(off[lo], lo), kmp_set_base(off[hi], hi))), sorted by
- *      bucket into d_out; part_counts[j] = keys bound for bucket part j (they are contiguous, in
- *      part order, at the front of d_out).  slots = kmp_set_capacity(N, ΣL) of the whole batch
- *      (it fixes the key layout, identical on every rank).
- *   2. all-to-all of the keys; kmp_dev_pairs_keys on the m received keys: group + expand
- *      (the bucketed engine), the n_inc pair keys p*N+q sorted into d_out (KMP_EOVERFLOW with
- *      *n_inc set if out_cap is smaller); part_counts[j] = pair keys of p-range part j.
- *   3. all-to-all of the pair keys; kmp_dev_edges_pairkeys: the received runs -> the edges
- *      (p, q, w >= min_shared) of this p range in canonical order.  Concatenating the ranks'
- *      edges in rank order gives the canonical edge list.
- * KMP_ESTATE: the batch needs the flat layout (a class id wider than the key's class field, or a
- * k-mer too frequent for the LDS buckets); use the single-GPU path. */
-int kmp_dev_keys_part(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
-                      uint32_t n, int k, uint64_t slots, uint32_t lo, uint32_t hi, uint64_t slot_lo,
-                      uint64_t slot_hi, uint32_t parts, unsigned long long* d_out, uint64_t out_cap,
-                      uint64_t* part_counts, void* stream);
-int kmp_dev_pairs_keys(kmp_postings* ws, const unsigned long long* d_keys, uint64_t m, uint32_t n, int k,
-                       uint64_t slots, uint32_t heavy_df, int require_class_diff, uint32_t parts,
-                       unsigned long long* d_out, uint64_t out_cap, uint64_t* n_inc, uint64_t* part_counts,
-                       kmp_postings_stats* stats, void* stream);
-int kmp_dev_edges_pairkeys(kmp_postings* ws, const unsigned long long* d_pk, uint64_t m, uint32_t n,
-                           uint32_t min_shared, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w, uint64_t cap,
-                           uint64_t* n_edges, uint64_t* n_pairs, void* stream);
-
-/* The same split with fixed-capacity exchanges and no host synchronisation (dist.py's default):
- * every exchange buffer holds `parts` regions of `cap` u64 keys, each region's unused tail is
- * ~0 (padding sorts after every real key), and the caller's device array d_flags[8] (zeroed per
- * step) collects what went wrong: [0] a part exceeded `cap` (sizes in [4] keys, [6] pair keys),
- * [1] a class id too wide, [2] a k-mer group too large for the LDS buckets (both: use the
- * single-GPU path), [3] a shard region exceeded shard_cap (size in [5]).  After a flagged step
- * the caller grows the capacities and reruns.
- *   kmp_dev_keys_route:  keys of proteins [lo, hi) routed by bucket range (not sorted: every
- *                        receiver sorts).
- *   kmp_dev_pairs_route: the m received keys (bucket part `part` of `parts`) grouped +
- *                        expanded, pair keys routed by row range (kmp_row_split; shard_cap: pair
- *                        keys per expansion shard region).
- *   kmp_dev_edges_route: the m received pair keys -> this p range's edges, count in *d_count. */
-/* Row ranges of the pair split: range d = [start[d], start[d+1]) with start[d] =
+/* The residue path restricted to rows [row_lo, row_hi): only the pairs (p, q), p < q, whose
+ * smaller protein p lies in the range (every k-mer group still grouped in full, so each pair's
+ * w is complete).  The edges come out in canonical order; concatenating the calls of
+ * consecutive ranges gives the canonical list.  This is the unit a rank of the multi-GPU split
+ * and a pass of the bounded-memory mode run.  KMP_ESTATE: the batch needs the flat layout
+ * (class ids too wide), which has no row filter. */
+int kmp_dev_pairs_rows(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
+                       uint32_t n, int k, uint64_t slots, uint32_t heavy_df, uint32_t min_shared,
+                       int require_class_diff, uint32_t row_lo, uint32_t row_hi, uint32_t* d_p, uint32_t* d_q,
+                       uint32_t* d_w, uint64_t cap, uint64_t* n_edges, kmp_postings_stats* stats, void* stream);
+/* Row ranges of a split of the pair space: range d = [start[d], start[d+1]) with start[d] =
  * floor(N (1 - sqrt(1 - d/parts))): a pair belongs to its smaller protein, so the ranges hold about
- * equal pair counts.  start has parts + 1 entries, parts <= 64. */
+ * equal pair counts.  start has parts + 1 entries. */
 void kmp_row_split(uint32_t n, uint32_t parts, uint32_t* start);
-int kmp_dev_keys_route(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
-                       uint32_t n, int k, uint64_t slots, uint32_t lo, uint32_t hi, uint64_t slot_lo, uint64_t slot_hi,
-                       uint32_t parts, uint64_t cap, unsigned long long* d_send, uint32_t* d_flags, void* stream);
-int kmp_dev_pairs_route(kmp_postings* ws, const unsigned long long* d_keys, uint64_t m, uint32_t n, int k,
-                        uint64_t slots, uint32_t heavy_df, int require_class_diff, uint64_t shard_cap, uint32_t part,
-                        uint32_t parts, uint64_t cap, unsigned long long* d_send, uint32_t* d_flags,
-                        kmp_postings_stats* stats, void* stream);
-int kmp_dev_edges_route(kmp_postings* ws, const unsigned long long* d_pk, uint64_t m, uint32_t n, uint32_t* d_p,
-                        uint32_t* d_q, uint32_t* d_w, uint64_t cap, unsigned long long* d_count, void* stream);
-/* kmp_dev_edges_rows: as kmp_dev_edges_route for the owner of rows [row_lo, row_hi) (the
- * kmp_row_split range of its part), edges written as interleaved (p, q, w) u32 triples
- * (d_edges[3i .. 3i+2], cap triples) so a rank's block is contiguous for the gather to rank 0;
- * reduced with the row-block tail (pair keys partitioned by
- * row block, LDS radix sort + run-length encode per block) instead of a global sort.  A row block
- * above the LDS capacity leaves *d_count = KMP_EDGES_RETRY: switch the workspace to the sort tail
- * (kmp_postings_set_rowtail(ws, 0)) and rerun.  Pair keys from kmp_dev_pairs_route are
- * p << bits(n) | q. */
-#define KMP_EDGES_RETRY (1ull << 62)
-int kmp_dev_edges_rows(kmp_postings* ws, const unsigned long long* d_pk, uint64_t m, uint32_t n, uint32_t row_lo,
-                       uint32_t row_hi, uint32_t* d_edges, uint64_t cap, unsigned long long* d_count,
-                       void* stream);
-/* Row-block tail on (default) or off for the fused residue step and kmp_dev_edges_rows; the
- * workspace turns it off by itself after a row too long for LDS. */
-int kmp_postings_set_rowtail(kmp_postings* ws, int enable);
-/* Row-block tail, in-block sort (combine_edges, mod.rs:322-546): 1 counts a block's keys by row
- * and rank-sorts each row in LDS when every row holds at most 512 keys, else the block radix
- * sort; 0 (default; env KMP_PT_RANK=1 turns 1 on) always the block radix sort.  Same edges. */
-int kmp_postings_set_rowrank(kmp_postings* ws, int enable);
 
 /* Canonical order: sorts n edges by (p, q).  Keys/values are read from d_p/d_q/d_w and the
  * sorted result is written back to them.  d_tmp: kmp_dev_sort_edges_tmp_bytes(n, N) bytes. */

@@ -1,9 +1,10 @@
-"""The multi-GPU split (uniprot_kmer_based_clustering_amd/dist.py) on CPU: world_size 2 and 3
-over gloo.  Every rank contributes its protein slice of the set buffer and its share of the
-pair items; the test checks that the all-gathered sets equal the single-process sets and
-that the edges gathered to rank 0 (each rank's edges = the oracle's edges restricted to the
-rank's items) re-sort into exactly the single-process edge list — i.e. the result is
-invariant to the number of ranks.  The pair kernel itself needs a GPU (tests/test_gpu_*)."""
+"""The multi-GPU row split (uniprot_kmer_based_clustering_amd/dist.py) on CPU: world_size 2 and
+3 over gloo.  Each rank's device stage (kmp_dev_pairs_rows, GPU-only) is stood in for by the
+oracle's edge list restricted to the rank's rows; the test checks that the ranks' blocks,
+gathered in place to rank 0, concatenate to exactly the single-process canonical list (the
+result is invariant to the number of ranks), including empty blocks and a rank-0 destination
+that has to grow.  The device stage itself: tests/test_gpu_parity.py::test_row_ranges_concatenate
+and tests/test_gpu_multi.py."""
 import os
 import socket
 
@@ -13,7 +14,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from common import ROOT, slice_proteins, uniprot
+from common import ROOT
 
 
 def free_port():
@@ -30,295 +31,86 @@ def build_case():
     return b, o
 
 
+class OraclePipe:
+    """CPU stand-in for DevicePipeline.rows: the oracle's edges of rows [lo, hi) into ep/eq/ew."""
+
+    def __init__(self, n, p, q, w, cap):
+        self.n, self.P, self.Q, self.W = n, p, q, w
+        self._alloc_edges(cap)
+
+    def _alloc_edges(self, cap):
+        self.edge_cap = cap
+        self.ep = torch.zeros(cap, dtype=torch.int32)
+        self.eq = torch.zeros(cap, dtype=torch.int32)
+        self.ew = torch.zeros(cap, dtype=torch.int32)
+
+    def rows(self, lo, hi, min_shared=1, require_class_diff=True):
+        keep = (self.P >= lo) & (self.P < hi) & (self.W >= min_shared)
+        m = int(keep.sum())
+        if m > self.edge_cap:
+            self._alloc_edges(m)
+        for dst, src in zip((self.ep, self.eq, self.ew), (self.P, self.Q, self.W)):
+            dst[:m] = torch.from_numpy(src[keep].view(np.int32).copy())
+        return m
+
+
 def worker(rank, world, port, out_q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import sys
         sys.path.insert(0, ROOT)
-        from uniprot_kmer_based_clustering_amd import _lib
-        from uniprot_kmer_based_clustering_amd.device import Plan
-        from uniprot_kmer_based_clustering_amd.dist import (allgather_sets, gather_edges, protein_slices,
-                                                            slot_range)
+        from uniprot_kmer_based_clustering_amd.dist import distributed_step, row_ranges
         b, o = build_case()
-        n = b.n
-        L = _lib.lib()
-        so, sv = o.sets()
-        cap = int(L.kmp_set_capacity(n, int(b.offsets[-1])))
-        full = np.full(cap, -1, dtype=np.int32)
-        lens = np.diff(so).astype(np.int32)
-        for p in range(n):
-            base = int(L.kmp_set_base(int(b.offsets[p]), p))
-            full[base:base + lens[p]] = sv[so[p]:so[p + 1]].view(np.int32)
-        slices = protein_slices(b.offsets, world)
-        lo, hi = slices[rank]
-        # this rank only holds its slice (the rest is garbage before the all-gather)
-        buf = torch.full((cap,), -7, dtype=torch.int32)
-        sl_lo, sl_hi = slot_range(b.offsets, lo, hi)
-        buf[sl_lo:sl_hi] = torch.from_numpy(full[sl_lo:sl_hi])
-        ln = torch.full((n,), -3, dtype=torch.int32)
-        ln[lo:hi] = torch.from_numpy(lens[lo:hi])
-        allgather_sets(buf, ln, b.offsets, slices, rank)
-        ok_sets = bool(torch.equal(ln, torch.from_numpy(lens)))
-        for p in range(n):
-            base = int(L.kmp_set_base(int(b.offsets[p]), p))
-            ok_sets &= bool(torch.equal(buf[base:base + lens[p]], torch.from_numpy(full[base:base + lens[p]])))
-
-        # pair share: the oracle's edges restricted to this rank's items (repeat-filtered sizes)
-        rc, _ = o.repeat()
-        rep_len = np.array([np.isin(sv[so[p]:so[p + 1]], rc).sum() for p in range(n)], dtype=np.uint32)
-        mine = Plan(rep_len, 20000).share(rank, world)
         P, Q, W = o.pairs()
-        keep = np.zeros(len(P), dtype=bool)
-        for r0, r1, c0, c1 in mine.astype(np.int64):
-            keep |= (P >= r0) & (P < r1) & (Q >= c0) & (Q < c1) & (Q > P)
-        ep = torch.from_numpy(P[keep].view(np.int32).copy())
-        eq = torch.from_numpy(Q[keep].view(np.int32).copy())
-        ew = torch.from_numpy(W[keep].view(np.int32).copy())
-        got = gather_edges(ep, eq, ew, int(keep.sum()), rank)
-        if rank == 0:
-            gp, gq, gw = (t.numpy().view(np.uint32) for t in got)
-            order = np.lexsort((gq, gp))
-            ok_edges = (np.array_equal(gp[order], P) and np.array_equal(gq[order], Q)
-                        and np.array_equal(gw[order], W))
-            out_q.put(("edges", ok_edges, len(P), int(keep.sum())))
-        out_q.put(("sets", rank, ok_sets))
-    finally:
-        dist.destroy_process_group()
-
-
-class OracleStages:
-    """CPU stand-in for the three device stages of dist.distributed_postings, built on the
-    oracle's K(p) sets: keys = code << 20 | p routed by code % parts; pair keys p*N+q of every
-    class-differing pair of a k-mer's proteins, routed by p range; edges = runs of pair keys.
-    Exercises the exchanges and the canonical concatenation, not the kernels."""
-
-    def __init__(self, o, cls, n):
-        self.so, self.sv = o.sets()
-        self.cls = np.asarray(cls)
-        self.n = n
-
-    def keys_part(self, lo, hi, parts):
-        keys = np.concatenate([(self.sv[self.so[p]:self.so[p + 1]].astype(np.int64) << 20) | p
-                               for p in range(lo, hi)] + [np.zeros(0, np.int64)])
-        part = (keys >> 20) % parts
-        order = np.argsort(part, kind="stable")
-        return torch.from_numpy(keys[order]), np.bincount(part, minlength=parts).tolist()
-
-    def pairs_keys(self, keys, parts):
-        k = keys.numpy()
-        k = k[np.argsort(k, kind="stable")]
-        code, p = k >> 20, k & ((1 << 20) - 1)
-        out = []
-        for s, e in zip(*[np.flatnonzero(np.r_[True, code[1:] != code[:-1]]),
-                          np.r_[np.flatnonzero(code[1:] != code[:-1]) + 1, len(code)]]):
-            ps = p[s:e]
-            for i in range(len(ps)):
-                for j in range(i + 1, len(ps)):
-                    if self.cls[ps[i]] != self.cls[ps[j]]:
-                        a, b = sorted((int(ps[i]), int(ps[j])))
-                        out.append(a * self.n + b)
-        pk = np.sort(np.array(out, dtype=np.int64))
-        bounds = [-(-j * self.n // parts) * self.n for j in range(parts + 1)]
-        counts = [int(((pk >= bounds[j]) & (pk < bounds[j + 1])).sum()) for j in range(parts)]
-        return torch.from_numpy(pk), counts
-
-    def edges_pairkeys(self, pk):
-        u, w = np.unique(pk.numpy(), return_counts=True)
-        t = lambda a: torch.from_numpy(a.astype(np.int32))  # noqa: E731
-        return t(u // self.n), t(u % self.n), t(w), len(u)
-
-
-ALL = np.uint64(0xFFFFFFFFFFFFFFFF)
-
-
-class OracleRouteStages:
-    """CPU stand-in for the fixed-capacity stages of dist.distributed_postings_padded (padding =
-    all-ones keys, overflow flags, learned capacities), built on the oracle's K(p) sets; the
-    initial capacities are tiny so the first attempt overflows and the flow reruns."""
-
-    def __init__(self, o, cls, n):
-        self.so, self.sv = o.sets()
-        self.cls = np.asarray(cls)
-        self.n = n
-        self.cap_keys = self.cap_pairs = 0
-        self.flags = np.zeros(8, np.int64)
-        self.count = 0
-        self.attempts = 0
-        self.retry_rowtail = False
-
-    def disable_rowtail(self):
-        self.retry_rowtail = False
-        self.rowtail_disabled = True
-
-    def begin(self, world):
-        if self.cap_keys == 0:
-            self.cap_keys, self.cap_pairs = 64, 64
-        self.flags[:] = 0
-        self.attempts += 1
-
-    def _route(self, vals, part, parts, cap, slot):
-        send = np.full(parts * cap, ALL, dtype=np.uint64)
-        for d in range(parts):
-            v = vals[part == d]
-            self.flags[slot] = max(self.flags[slot], len(v))
-            if len(v) > cap:
-                self.flags[0] = 1
-            v = v[:cap]
-            send[d * cap:d * cap + len(v)] = v
-        return torch.from_numpy(send.view(np.int64))
-
-    def keys_route(self, lo, hi, parts):
-        keys = np.concatenate([(self.sv[self.so[p]:self.so[p + 1]].astype(np.uint64) << np.uint64(20)) | np.uint64(p)
-                               for p in range(lo, hi)] + [np.zeros(0, np.uint64)])
-        return self._route(keys, (keys >> np.uint64(20)) % np.uint64(parts), parts, self.cap_keys, 4)
-
-    def pairs_route(self, keys, part, parts):
-        k = keys.numpy().view(np.uint64)
-        k = np.sort(k[k != ALL])
-        code, p = k >> np.uint64(20), (k & np.uint64((1 << 20) - 1)).astype(np.int64)
-        out = []
-        heads = np.flatnonzero(np.r_[True, code[1:] != code[:-1]]) if len(k) else np.zeros(0, int)
-        for s_, e_ in zip(heads, np.r_[heads[1:], len(k)]):
-            ps = p[s_:e_]
-            for i in range(len(ps)):
-                for j in range(i + 1, len(ps)):
-                    if self.cls[ps[i]] != self.cls[ps[j]]:
-                        a, b = sorted((int(ps[i]), int(ps[j])))
-                        out.append(a * self.n + b)
-        pk = np.sort(np.array(out, dtype=np.uint64))
-        bounds = np.array([-(-j * self.n // parts) * self.n for j in range(parts + 1)], dtype=np.uint64)
-        part = np.searchsorted(bounds, pk, side="right") - 1
-        return self._route(pk, part, parts, self.cap_pairs, 6)
-
-    def edges_route(self, pk, part=0, parts=1):
-        k = pk.numpy().view(np.uint64)
-        u, w = np.unique(k[k != ALL], return_counts=True)
-        self.count = len(u)
-        if self.retry_rowtail:  # emulate a row block too long for the LDS row-block tail
-            self.count = 1 << 62
-        e = np.zeros((max(1, len(u)), 3), np.int32)  # interleaved (p, q, w) triples
-        e[:len(u), 0] = (u // np.uint64(self.n)).astype(np.int32)
-        e[:len(u), 1] = (u % np.uint64(self.n)).astype(np.int32)
-        e[:len(u), 2] = w
-        return torch.from_numpy(e.reshape(-1)), None
-
-    def status(self):
-        return torch.from_numpy(np.r_[self.flags, self.count].astype(np.int64))
-
-    def grow(self, worst):
-        if worst[0]:
-            self.cap_keys = max(self.cap_keys, int(worst[4]) + 16)
-            self.cap_pairs = max(self.cap_pairs, int(worst[6]) + 16)
-
-
-def padded_worker(rank, world, port, out_q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        import sys
-        sys.path.insert(0, ROOT)
-        from uniprot_kmer_based_clustering_amd.dist import distributed_postings_padded
-        b, o = build_case()
-        stages = OracleRouteStages(o, b.class_id, b.n)
-        stages.retry_rowtail = rank == world - 1  # that rank's row-block tail "overflows" once
-        got, counts = distributed_postings_padded(stages, b.offsets, rank, world, max_attempts=6)
-        if rank == 0:
-            P, Q, W = o.pairs()
-            tri = got.numpy().reshape(-1, 3)  # interleaved triples of every rank, rank order
-            ep, eq, ew = (np.ascontiguousarray(tri[:, j]).view(np.uint32) for j in range(3))
-            ok = np.array_equal(ep, P) and np.array_equal(eq, Q) and np.array_equal(ew, W)
-            out_q.put(("edges", ok, len(P), stages.attempts))
-        out_q.put(("count", rank, counts[rank]))
+        # rank 0 starts with a destination smaller than the gathered list: it has to grow
+        pipe = OraclePipe(b.n, P, Q, W, cap=16 if rank == 0 else 1 << 20)
+        ranges = row_ranges(b.n, world)
+        for ms in (1, 3, 10 ** 6):  # the last one: every block empty
+            n = distributed_step(pipe, rank, world, min_shared=ms)
+            if rank == 0:
+                keep = W >= ms
+                ok = (n == int(keep.sum())
+                      and np.array_equal(pipe.ep[:n].numpy().view(np.uint32), P[keep])
+                      and np.array_equal(pipe.eq[:n].numpy().view(np.uint32), Q[keep])
+                      and np.array_equal(pipe.ew[:n].numpy().view(np.uint32), W[keep]))
+                out_q.put(("edges", ms, ok, n))
+        out_q.put(("ranges", rank, ranges))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_distributed_postings_padded(world):
-    """Fixed-capacity exchanges: overflow on the first attempt, joint rerun with learned
-    capacities, one more rerun after a row-block-tail overflow on the last rank (every rank
-    switches to the sort tail), rank-order concatenation = the canonical edge list."""
+def test_row_split_gather(world):
+    port = free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = free_port()
-    procs = [ctx.Process(target=padded_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    msgs = [q.get(timeout=300) for _ in range(world + 1)]  # drain before join: a queued message blocks exit
-    for p in procs:
-        p.join(timeout=60)
-    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
-    edges = [m for m in msgs if m[0] == "edges"]
-    assert len(edges) == 1 and edges[0][1] and edges[0][2] > 100, edges
-    assert edges[0][3] in (3, 4)  # tiny first capacities overflowed (keys, then pair keys); row-tail retry
-    assert sum(m[2] for m in msgs if m[0] == "count") == edges[0][2]
-
-
-def postings_worker(rank, world, port, out_q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        import sys
-        sys.path.insert(0, ROOT)
-        from uniprot_kmer_based_clustering_amd.dist import distributed_postings
-        b, o = build_case()
-        got, m = distributed_postings(OracleStages(o, b.class_id, b.n), b.offsets, rank, world)
-        if rank == 0:
-            P, Q, W = o.pairs()
-            gp, gq, gw = (t.numpy().view(np.uint32) for t in got)
-            out_q.put(("edges", np.array_equal(gp, P) and np.array_equal(gq, Q) and np.array_equal(gw, W),
-                       len(P)))
-        out_q.put(("count", rank, m))
-    finally:
-        dist.destroy_process_group()
-
-
-@pytest.mark.parametrize("world", [2, 3])
-def test_distributed_postings_exchanges(world):
-    """Rank-order concatenation of the p-range owners' edges is the canonical edge list."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = free_port()
-    procs = [ctx.Process(target=postings_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    msgs = [q.get(timeout=300) for _ in range(world + 1)]  # drain before join: a queued message blocks exit
-    for p in procs:
-        p.join(timeout=60)
-    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
-    edges = [m for m in msgs if m[0] == "edges"]
-    counts = [m for m in msgs if m[0] == "count"]
-    assert len(edges) == 1 and edges[0][1] and edges[0][2] > 100, edges
-    assert sum(m[2] for m in counts) == edges[0][2]
-    assert all(m[2] > 0 for m in counts)  # every rank owns part of the edge list
-
-
-@pytest.mark.parametrize("world", [2, 3])
-def test_distributed_split_is_invariant(world):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = free_port()
     procs = [ctx.Process(target=worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    msgs = [q.get(timeout=300) for _ in range(world + 1)]  # drain before join: a queued message blocks exit
+    msgs = [q.get(timeout=300) for _ in range(3 + world)]
     for p in procs:
         p.join(timeout=60)
-    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
-    sets = [m for m in msgs if m[0] == "sets"]
+    assert all(p.exitcode == 0 for p in procs)
     edges = [m for m in msgs if m[0] == "edges"]
-    assert len(sets) == world and all(m[2] for m in sets), sets
-    assert len(edges) == 1 and edges[0][1], edges
-    assert edges[0][2] > 100
+    assert len(edges) == 3 and all(m[2] for m in edges), edges
+    assert edges[0][3] > 1000 and edges[2][3] == 0
+    ranges = [m[2] for m in msgs if m[0] == "ranges"]
+    assert all(r == ranges[0] for r in ranges)
+    r = ranges[0]
+    assert r[0][0] == 0 and r[-1][1] == 3000 and all(a[1] == b[0] for a, b in zip(r, r[1:]))
 
 
-def test_protein_slices_balance():
-    from uniprot_kmer_based_clustering_amd.dist import protein_slices
-    res, off, cls, _ = uniprot()
-    for world in (1, 2, 4, 8):
-        sl = protein_slices(off, world)
-        assert sl[0][0] == 0 and sl[-1][1] == len(off) - 1
-        assert all(sl[i][1] == sl[i + 1][0] for i in range(world - 1))
-        sizes = [int(off[h]) - int(off[l]) for l, h in sl]
-        assert max(sizes) - min(sizes) <= 2 * int(np.diff(off).max())
+def test_row_split_balance():
+    """kmp_row_split: range d starts at N (1 - sqrt(1 - d/parts)), so the expected pair counts
+    (row p holds N - 1 - p pairs) are equal within one row's worth."""
+    from uniprot_kmer_based_clustering_amd import _lib
+    n = 100_000
+    for parts in (1, 2, 4, 8, 64):
+        s = _lib.row_split(n, parts).astype(np.int64)
+        assert s[0] == 0 and s[-1] == n and np.all(np.diff(s) > 0)
+        pairs = [(s[d + 1] - s[d]) * (n - 1) - (s[d + 1] * (s[d + 1] - 1) - s[d] * (s[d] - 1)) // 2
+                 for d in range(parts)]
+        total = n * (n - 1) // 2
+        assert sum(pairs) == total
+        assert max(abs(x - total / parts) for x in pairs) <= n

@@ -263,17 +263,15 @@ def test_bucketed_small_batches(oracle_mod, n):
         np.testing.assert_array_equal(pipe.edges()[2], w)
 
 
-@pytest.mark.parametrize("partition", [True, False], ids=["partition", "keysort"])
-def test_residue_graph_replay(oracle_mod, partition):
+def test_residue_graph_replay(oracle_mod):
     """The single-synchronisation residue step replayed from its HIP graph: every replay (stage
-    timing off and on) is bit-exact, for both bucket-grouping front ends; an edge buffer that
-    moves (overflow rerun) forces a new capture and stays exact."""
+    timing off and on) is bit-exact; an edge buffer that moves (overflow rerun) forces a new
+    capture and stays exact."""
     import torch
     from uniprot_kmer_based_clustering_amd.device import DevicePipeline
     b = K.synth(20000, 21)
     p, q, w = oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=7, threads=8).pairs()
     pipe = DevicePipeline(b, 7, "cuda:0")
-    pipe.set_partition(partition)
     for timing in (False, True):
         pipe.set_stage_timing(timing)
         for _ in range(4):
@@ -295,10 +293,10 @@ def test_residue_graph_replay(oracle_mod, partition):
     np.testing.assert_array_equal(pipe.edges()[2], w)
 
 
-def test_rowtail_overflow_falls_back(oracle_mod):
-    """A protein whose row holds more pair keys than one row block of the fused step's LDS
-    reduction (kPtCap) sends the call to the global pair-key sort tail; edges stay exact, and the
-    row-block tail handles the same shape when rows are short."""
+def test_rowtail_overflow_blocks(oracle_mod):
+    """A protein whose row holds more pair keys than one row block of the LDS reduction (kPtCap):
+    its block is listed and finished by the segmented sort, the rest stay on the LDS path; edges
+    exact with the long row first (overflow) and last (every block short)."""
     import torch
     from uniprot_kmer_based_clustering_amd.device import DevicePipeline
     rng = np.random.default_rng(7)
@@ -309,66 +307,104 @@ def test_rowtail_overflow_falls_back(oracle_mod):
     res, off, cls = make_batch(seqs, ["a"] + ["b"] * 220)
     p, q, w = oracle_mod.Oracle(res, off, cls, k=7, threads=8).pairs()
     assert int(w[p == 0].sum()) > 8192
-    for shuffle_first in (False, True):
-        if shuffle_first:  # the long row last instead of first: every row short enough
+    for long_first in (True, False):
+        if not long_first:  # the long row last instead of first: every row short enough
             seqs2 = seqs[1:] + seqs[:1]
             res, off, cls = make_batch(seqs2, ["b"] * 220 + ["a"])
             p, q, w = oracle_mod.Oracle(res, off, cls, k=7, threads=8).pairs()
         pipe = DevicePipeline(K.Proteins(res, off, cls), 7, "cuda:0")
-        for _ in range(3):
+        for it in range(3):
             m = pipe.step(engine="residues")
             torch.cuda.synchronize()
-            assert pipe.last_tail() in ("rows", "fused") and m == len(p)
-            # the long row sends its batch to the global-sort tail; short rows stay on the row tail
-            assert pipe.last_tail() == ("rows" if shuffle_first else "fused")
+            assert pipe.last_tail() == "rows" and m == len(p)
+            if it == 0:
+                assert (pipe.overflow_blocks() > 0) == long_first
             np.testing.assert_array_equal(pipe.edges()[0], p)
             np.testing.assert_array_equal(pipe.edges()[1], q)
             np.testing.assert_array_equal(pipe.edges()[2], w)
+        for ms in (2, 30):  # min_shared inside the overflow encoder too
+            keep = w >= ms
+            assert pipe.step(min_shared=ms, engine="residues") == int(keep.sum())
+            np.testing.assert_array_equal(pipe.edges()[1], q[keep])
+            np.testing.assert_array_equal(pipe.edges()[2], w[keep])
 
 
-def test_pshard_long_rows(oracle_mod):
-    """One protein sharing a distinct k-mer with each of ~650 others: its row of the p-shard
-    reduction is longer than the rank-sort limit, so that range is bitonic-sorted in LDS."""
-    import torch
-    from uniprot_kmer_based_clustering_amd.device import DevicePipeline
-    rng = np.random.default_rng(5)
-    alpha = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", dtype=np.uint8)
-    rnd = lambda m: alpha[rng.integers(0, 20, m)].tobytes()  # noqa: E731
-    base = rnd(700)
-    seqs = [base] + [rnd(40) + base[i:i + 7] + rnd(40) for i in range(650)]
-    res, off, cls = make_batch(seqs, ["a"] + ["b"] * 650)
-    o = oracle_mod.Oracle(res, off, cls, k=7, threads=8)
-    p, q, w = o.pairs()
-    assert (p == 0).sum() > 600
-    pipe = DevicePipeline(K.Proteins(res, off, cls), 7, "cuda:0")
-    pipe.set_pshard(True)
-    m = pipe.step(engine="residues")
-    torch.cuda.synchronize()
-    assert pipe.last_tail() == "pshard" and m == len(p)
-    np.testing.assert_array_equal(pipe.edges()[0], p)
-    np.testing.assert_array_equal(pipe.edges()[1], q)
-    np.testing.assert_array_equal(pipe.edges()[2], w)
-
-
-def test_bucketed_fallback_on_frequent_kmers(oracle_mod):
-    """A k-mer shared by thousands of proteins overflows an LDS sub-bucket: the bucketed layout
-    hands the call to the flat layout and the edges stay exact."""
+@pytest.mark.parametrize("copies", [3000, 12000])
+def test_frequent_kmers_heavy_path(oracle_mod, copies):
+    """A k-mer shared by thousands of proteins (a group above the LDS sub-bucket limit; at 12000
+    copies its bucket is above every LDS capacity and its level-2 bin above its tile budget):
+    the bucketed layout spills it to the heavy path and the edges stay exact, for both entry
+    points, with and without the class filter, and with min_shared."""
     import torch
     from uniprot_kmer_based_clustering_amd.device import DevicePipeline
     rng = np.random.default_rng(11)
     alpha = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", dtype=np.uint8)
-    seqs = [alpha[rng.integers(0, 20, 120)].tobytes() + b"WWWWWWW" for _ in range(3000)]
-    res, off, cls = make_batch(seqs, [str(i % 7) for i in range(3000)])
+    seqs = [alpha[rng.integers(0, 20, 120)].tobytes() + b"WWWWWWW" * (1 + i % 2) for i in range(copies)]
+    res, off, cls = make_batch(seqs, [str(i % 7) for i in range(copies)])
     o = oracle_mod.Oracle(res, off, cls, k=7, threads=8)
     pipe = DevicePipeline(K.Proteins(res, off, cls), 7, "cuda:0")
-    for eng in ("postings", "residues"):
-        m = pipe.step(engine=eng)
+    for eng in ("postings", "residues", "residues"):
+        for diff in (True, False):
+            m = pipe.step(require_class_diff=diff, engine=eng)
+            torch.cuda.synchronize()
+            assert pipe.last_layout() == "bucketed" and pipe.last_heavy()
+            p, q, w = o.pairs(require_class_diff=diff)
+            assert m == len(p)
+            np.testing.assert_array_equal(pipe.edges()[0], p)
+            np.testing.assert_array_equal(pipe.edges()[1], q)
+            np.testing.assert_array_equal(pipe.edges()[2], w)
+    st, c = pipe.postings_stats.as_dict(), o.counters()
+    assert st["max_df"] == c["max_df"] >= copies and st["distinct"] == c["distinct"]
+    assert st["sum_cdf2_light"] == c["sum_cdf2"] and st["repeat"] == c["repeat"]
+    p, q, w = o.pairs(min_shared=2)
+    assert pipe.step(min_shared=2, engine="residues") == len(p)
+    np.testing.assert_array_equal(pipe.edges()[1], q)
+
+
+def test_uniprot_k5_on_bucketed_heavy_path(oracle_mod, uni):
+    """The reference's dataset at k = 5 (max df 3,694): bucketed layout with the heavy path and
+    the row-block tail, edge list sha equal to the golden one (repeat: graph replay is not used
+    on the split step, every call recomputes)."""
+    import torch
+    from uniprot_kmer_based_clustering_amd.device import DevicePipeline
+    res, off, cls = uni
+    g = load_json("uniprot_counters.json")["5"]
+    pipe = DevicePipeline(K.Proteins(res, off, cls), 5, "cuda:0")
+    for _ in range(2):
+        m = pipe.step(engine="residues")
         torch.cuda.synchronize()
-        assert pipe.last_layout() == "flat"
-        p, q, w = o.pairs()
-        assert m == len(p)
-        np.testing.assert_array_equal(pipe.edges()[0], p)
-        np.testing.assert_array_equal(pipe.edges()[2], w)
+        assert pipe.last_layout() == "bucketed" and pipe.last_heavy() and pipe.last_tail() == "rows"
+        assert m == g["n_edges"]
+        assert edges_sha256(*pipe.edges()) == g["edges_sha256"]
+        st = pipe.postings_stats.as_dict()
+        assert st["max_df"] == g["max_df"] and st["sum_cdf2_light"] == g["sum_cdf2"]
+        assert st["incidences"] == g["sum_w_diff"] and st["distinct"] == g["distinct"]
+
+
+@pytest.mark.parametrize("k", [5, 7])
+def test_row_ranges_concatenate(oracle_mod, k):
+    """kmp_dev_pairs_rows: the edges of consecutive row ranges (the unit of a rank / a pass)
+    concatenate to the canonical list, on light (k = 7) and heavy (k = 5, frequent 5-mers)
+    batches; statistics of every range describe the whole batch."""
+    import torch
+    from uniprot_kmer_based_clustering_amd.device import DevicePipeline
+    b = K.synth(6000, 5, 1)
+    o = oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=k, threads=8)
+    p, q, w = o.pairs()
+    pipe = DevicePipeline(b, k, "cuda:0")
+    for parts in (1, 3, 8):
+        start = K._lib.row_split(b.n, parts)
+        got = [[], [], []]
+        for d in range(parts):
+            pipe.rows(int(start[d]), int(start[d + 1]))
+            torch.cuda.synchronize()
+            for a, x in zip(got, pipe.edges()):
+                a.append(x)
+            assert np.all((got[0][-1] >= start[d]) & (got[0][-1] < start[d + 1]))
+        np.testing.assert_array_equal(np.concatenate(got[0]), p)
+        np.testing.assert_array_equal(np.concatenate(got[1]), q)
+        np.testing.assert_array_equal(np.concatenate(got[2]), w)
+    assert pipe.rows(5, 5) == 0
 
 
 def test_errors(engine):
@@ -412,24 +448,21 @@ def test_device_pipeline_matches_oracle(oracle_mod):
         assert st["distinct"] == c["distinct"] and st["repeat"] == c["repeat"] and st["max_df"] == c["max_df"]
         assert st["sum_cdf2_light"] == c["sum_cdf2"] and st["incidences"] == c["sum_w_diff"]
         assert st["sum_S"] == c["sum_S"] and st["pairs"] == n
-    # both key layouts, both tails, both entry points: identical edges; config-shaped input runs
-    # bucketed with the p-shard tail
-    for bucketed, pshard in ((True, True), (True, False), (False, True)):
+    # both key layouts, both entry points: identical edges
+    for bucketed in (True, False):
         pipe.set_layout(bucketed)
-        pipe.set_pshard(pshard)
         for eng in ("postings", "residues"):
             assert pipe.step(engine=eng) == n
             np.testing.assert_array_equal(pipe.edges()[0], p)
             np.testing.assert_array_equal(pipe.edges()[1], q)
             np.testing.assert_array_equal(pipe.edges()[2], w)
             assert pipe.last_layout() == ("bucketed" if bucketed else "flat")
-            assert pipe.last_tail() == ("sort" if not bucketed else "pshard" if pshard else "rows")
+            assert pipe.last_tail() == ("rows" if bucketed else "sort")
         for ms in (2, 5):  # min_shared filter inside both tails
             keep = w >= ms
             assert pipe.step(min_shared=ms, engine="residues") == int(keep.sum())
             np.testing.assert_array_equal(pipe.edges()[1], q[keep])
     pipe.set_layout(True)
-    pipe.set_pshard(False)
     # stage timing: six non-negative stage times that add up to about one step
     pipe.set_stage_timing(True)
     assert pipe.step(engine="residues") == n
@@ -443,66 +476,3 @@ def test_device_pipeline_matches_oracle(oracle_mod):
     so, sv = o.sets()
     for pr in (0, 6999, 7000, 7001, 19999):
         np.testing.assert_array_equal(pipe.set_of(pr), sv[so[pr]:so[pr + 1]])
-
-
-def _dist_gpu_worker(rank, world, port, out_q):
-    """One rank of the distributed postings flow; all ranks share cuda:0, gloo moves the data."""
-    import os
-    import torch
-    import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        import uniprot_kmer_based_clustering_amd as KK
-        from uniprot_kmer_based_clustering_amd.device import DevicePipeline
-        from uniprot_kmer_based_clustering_amd.dist import distributed_step
-        b = KK.synth(20000, 9)
-        pipe = DevicePipeline(b, 7, "cuda:0")
-        for _ in range(2):  # a second pass reuses every buffer
-            n = distributed_step(pipe, rank, world, engine="residues")
-        torch.cuda.synchronize()
-        if rank == 0:
-            out_q.put(("edges", n, [a.tolist() for a in pipe.edges()]))
-        else:
-            out_q.put(("rank", rank, n))
-    except Exception as e:  # report instead of leaving the test waiting on its queue
-        import traceback
-        out_q.put(("error", rank, f"{e!r}\n{traceback.format_exc()}"))
-        raise
-    finally:
-        dist.destroy_process_group()
-
-
-@pytest.mark.parametrize("world", [2, 3])
-def test_distributed_postings_on_device(oracle_mod, world):
-    """The multi-GPU postings flow (bucket-range and p-range all-to-alls) with the real device
-    stages, `world` ranks on one GPU: rank 0's edge list equals the oracle's."""
-    import socket
-    import torch.multiprocessing as mp
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    procs = [ctx.Process(target=_dist_gpu_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    msgs = []
-    for _ in range(world):  # drain before join: a queued message blocks exit
-        msgs.append(q.get(timeout=150))
-        if msgs[-1][0] == "error":
-            for p in procs:
-                p.join(timeout=30)
-                if p.is_alive():
-                    p.kill()
-            pytest.fail(f"rank {msgs[-1][1]}: {msgs[-1][2]}")
-    for p in procs:
-        p.join(timeout=60)
-    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
-    got = [m for m in msgs if m[0] == "edges"][0]
-    b = K.synth(20000, 9)
-    p, qq, w = oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=7, threads=8).pairs()
-    assert got[1] == len(p)
-    np.testing.assert_array_equal(np.array(got[2][0], dtype=np.uint32), p)
-    np.testing.assert_array_equal(np.array(got[2][1], dtype=np.uint32), qq)
-    np.testing.assert_array_equal(np.array(got[2][2], dtype=np.uint32), w)

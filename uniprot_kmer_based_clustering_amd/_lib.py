@@ -20,6 +20,7 @@ KMP_LEN_NORMAL300, KMP_LEN_LOGUNIFORM = 0, 1
 KMP_SCORE_COUNT, KMP_SCORE_JACCARD, KMP_SCORE_BLOSUM = 0, 1, 2
 KMP_ENGINE_AUTO, KMP_ENGINE_POSTINGS, KMP_ENGINE_TILES, KMP_ENGINE_RESIDUES = 0, 1, 2, 3
 KMP_KMERS_CODES, KMP_KMERS_IDS = 0, 1
+KMP_LAYOUT_FLAT, KMP_LAYOUT_BUCKETED, KMP_LAYOUT_BUCKETED_HEAVY = 0, 1, 2
 KMP_LDS_SORT_MAX = 4096
 
 
@@ -131,29 +132,16 @@ SIGNATURES = {
     "kmp_postings_set_timing": (C.c_int, [P, C.c_int]),
     "kmp_postings_set_layout": (C.c_int, [P, C.c_int]),
     "kmp_postings_last_layout": (C.c_int, [P]),
-    "kmp_postings_set_pshard": (C.c_int, [P, C.c_int]),
-    "kmp_postings_set_partition": (C.c_int, [P, C.c_int]),
-    "kmp_postings_set_rowtail": (C.c_int, [P, C.c_int]),
-    "kmp_postings_set_rowrank": (C.c_int, [P, C.c_int]),
     "kmp_pairs_multi_k": (C.c_int, [P, P, C.POINTER(C.c_int), C.c_uint32, C.POINTER(P)]),
     "kmp_edges_get_wk": (C.c_int, [P, C.c_uint32, P, C.c_uint64, C.POINTER(C.c_uint64)]),
     "kmp_postings_set_graph": (C.c_int, [P, C.c_int]),
     "kmp_postings_graph_replays": (C.c_uint64, [P]),
     "kmp_dev_pairs_residues": (C.c_int, [P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32,
                                          C.c_uint32, C.c_int, P, P, P, C.c_uint64, U64P, P, P]),
-    "kmp_dev_keys_part": (C.c_int, [P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32, C.c_uint32,
-                                    C.c_uint64, C.c_uint64, C.c_uint32, P, C.c_uint64, U64P, P]),
-    "kmp_dev_pairs_keys": (C.c_int, [P, P, C.c_uint64, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32, C.c_int,
-                                     C.c_uint32, P, C.c_uint64, U64P, U64P, P, P]),
-    "kmp_dev_edges_pairkeys": (C.c_int, [P, P, C.c_uint64, C.c_uint32, C.c_uint32, P, P, P, C.c_uint64, U64P,
-                                         U64P, P]),
+    "kmp_dev_pairs_rows": (C.c_int, [P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32, C.c_uint32,
+                                     C.c_int, C.c_uint32, C.c_uint32, P, P, P, C.c_uint64, U64P, P, P]),
     "kmp_row_split": (None, [C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]),
-    "kmp_dev_keys_route": (C.c_int, [P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32, C.c_uint32,
-                                     C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64, P, P, P]),
-    "kmp_dev_pairs_route": (C.c_int, [P, P, C.c_uint64, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32, C.c_int,
-                                      C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, P, P, P, P]),
-    "kmp_dev_edges_route": (C.c_int, [P, P, C.c_uint64, C.c_uint32, P, P, P, C.c_uint64, P, P]),
-    "kmp_dev_edges_rows": (C.c_int, [P, P, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, P, C.c_uint64, P, P]),
+    "kmp_postings_last_overflow_blocks": (C.c_uint32, [P]),
     "kmp_dev_sort_edges_tmp_bytes": (C.c_uint64, [C.c_uint64, C.c_uint32]),
     "kmp_dev_sort_edges": (C.c_int, [P, P, P, C.c_uint64, C.c_uint32, P, C.c_uint64, P]),
     "kmp_read_fasta": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint32), C.POINTER(P), C.POINTER(P),
@@ -215,3 +203,11 @@ def geometry() -> PairGeometry:
     g = PairGeometry()
     lib().kmp_pair_geometry_get(C.byref(g))
     return g
+
+
+def row_split(n: int, parts: int):
+    """kmp_row_split: parts + 1 row boundaries of equal expected pair counts."""
+    import numpy as np
+    out = (C.c_uint32 * (parts + 1))()
+    lib().kmp_row_split(n, parts, out)
+    return np.array(out[:], dtype=np.uint32)

@@ -173,6 +173,8 @@ int finish_edges(kmp_ctx* c, const kmp_pair_opts& o, uint64_t count, bool needs_
     uint64_t wdiff = 0, nalign = 0;
     for (uint64_t i = 0; i < count; ++i) {
         const uint32_t p = e->p[i], q = e->q[i], w = e->w[i];
+        if (p >= q || q >= c->n) return fail(c, KMP_EDEVICE, "device edge %llu = (%u, %u) is not a pair of the batch",
+                                             (unsigned long long)i, p, q);
         if (c->h_cls[p] != c->h_cls[q]) wdiff += w;
         if (w > o.align_threshold) ++nalign;
         if (o.score == KMP_SCORE_JACCARD) {

@@ -24,6 +24,7 @@
 
 #include <rocprim/block/block_radix_sort.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_segmented_radix_sort.hpp>
 #include <rocprim/device/device_run_length_encode.hpp>
 #include <rocprim/device/device_scan.hpp>
 
@@ -53,8 +54,6 @@ unsigned bits_for(uint64_t v) {  // bits needed for values < v
 
 constexpr unsigned long long kNoKey = ~0ull;
 
-// blocks per region for the region copy/fill kernels (about 1024 keys per block)
-inline uint32_t route_blocks(uint64_t cap) { return (uint32_t)std::min<uint64_t>((cap + 1023) / 1024, 4096); }
 
 // rocprim 4.2 (ROCm 7.2): with the default config, radix_sort_keys on fewer than 1M keys takes a
 // merge-sort path that returns unsorted, non-permuted data for bit ranges [b, 64) with b > 0
@@ -541,29 +540,6 @@ __global__ void bucket_bounds_kernel(const unsigned long long* __restrict__ k, u
     bstart[b] = (uint32_t)lo;
 }
 
-// Partition bounds of sorted keys: bounds[j] = first index whose (key >> shift) >= T_j with
-// T_j = ceil(j * total / parts) * unit (j < parts) and T_parts = total * unit.
-__global__ void part_bounds_kernel(const unsigned long long* __restrict__ k, uint64_t m, unsigned shift,
-                                   unsigned long long total, unsigned long long unit, uint32_t parts,
-                                   unsigned long long* __restrict__ bounds) {
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j > parts) return;
-    const unsigned long long t = (j == parts ? total : (j * total + parts - 1) / parts) * unit;
-    uint64_t lo = 0, hi = m;
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if ((k[mid] >> shift) < t) lo = mid + 1;
-        else hi = mid;
-    }
-    bounds[j] = lo;
-}
-
-#ifndef KMP_F_EARLY
-#define KMP_F_EARLY 1
-#endif
-#ifndef KMP_BUCKET_STOP
-#define KMP_BUCKET_STOP 0  // timing ablation only (tools/build_variants.sh): stop after phase 1..5
-#endif
 constexpr uint32_t kHeavySub = 128;  // larger sub-buckets (very frequent k-mers) -> flat layout
 constexpr int kShards = 64;          // output cursors (one per bucket residue mod kShards)
 
@@ -590,46 +566,65 @@ __device__ __forceinline__ void block_scan_n(uint32_t v, uint32_t& excl, uint32_
     total = tot;
 }
 
+// Arguments of the bucket kernels (one struct, passed by value).
+//   out / shard_cap / cursor: kShards pair-key regions; a workgroup reserves its range on
+//     cursor[b % kShards] and writes the keys min(p,q) * mul + max(p,q) (writes past shard_cap are
+//     dropped, the cursor still counts them: the caller grows the regions and reruns);
+//   gstats: kShards x 8 statistics accumulators (kSt* slots);
+//   list / list_count: buckets above the small kernel's capacity (the large kernel takes them);
+//   spill / spill_cap / spill_cursor: the keys of heavy groups (more than kHeavySub keys: a
+//     frequent k-mer) and of buckets above the large capacity, one region of spill_cap keys per
+//     shard; the heavy path (heavy_* below) expands them.  spill == nullptr: heavy groups are
+//     skipped (an earlier pass of the same keys spilled them already);
+//   row_lo / row_hi (kRows): emit only the pairs whose smaller protein lies in [row_lo, row_hi)
+//     (a pass or a rank of the row split).
+struct BucketArgs {
+    const unsigned long long* sorted;
+    const uint32_t* bstart;
+    Layout lay;
+    uint32_t mul;
+    int require_diff;
+    uint32_t heavy_df;
+    uint32_t row_lo, row_hi;
+    unsigned long long* out;
+    uint64_t shard_cap;
+    unsigned long long* cursor;
+    unsigned long long* gstats;
+    uint32_t* flags;
+    uint32_t* list;
+    uint32_t* list_count;
+    unsigned long long* spill;
+    uint64_t spill_cap;
+    unsigned long long* spill_cursor;
+};
+
 // One workgroup per bucket with size <= kCap (the bucket: keys with the same top bbits of
 // h(code)).  In LDS:
 //   A. exact k-mer groups: an open-addressing table on h (kTab >= kCap slots, the empty mark can
 //      not be an h of this bucket) gives every key its group slot; LDS atomics rank it in the group;
 //   B. groups are laid out by size, largest first (a counting sort over the size classes), so the
-//      lanes of a wave walk groups of equal size in the loops below; singletons walk none;
+//      lanes of a wave walk groups of equal size in the loops below; singletons walk none; a group
+//      above kHeavySub keys (a frequent k-mer) is spilled whole to the heavy path instead;
 //   C. scatter: Bl[pos] = p << cb | class, and per position its group (start << 8 | size);
-//   D. duplicate windows of one protein (same p twice in a group) count once (main.rs:280-282);
+//   D. duplicate windows of one protein (same p twice in a group) count once (main.rs:99-100);
 //   E. df = distinct proteins of the group; every element pairs with the later non-duplicate
-//      elements of its group (vertex.rs:103-137), class test fused (mod.rs:580-587);
-//   F. output: the workgroup reserves its range on cursor[b % kShards] (p-shard mode: every key on
-//      its row range's cursor) and writes the pair keys min(p,q) * N + max(p,q).
+//      elements of its group (vertex.rs:103-137), class test fused (mod.rs:580-587).  kRows:
+//      instead every element pairs with the group's elements of a LARGER protein, and only
+//      elements whose protein lies in [row_lo, row_hi) emit (the row filter of a pass / rank);
+//   F. output: the workgroup reserves its range on cursor[b % kShards] and writes the pair keys.
 // Thread tid owns positions tid + e*kThreads in C-F, so its per-position state stays in
-// registers.  Statistics -> gstats[b % kShards].  flags[0]: a bucket above the large capacity or
-// a group above kHeavySub (a very frequent k-mer; the caller reruns on the flat layout).
-// p-shard output mode: every pair key goes to the region of its row range (p >> row_bits),
-// reserved key by key on that shard's cursor; shard_reduce_kernel then finishes each range in LDS
-struct PShard {
-    unsigned row_bits;
-    uint32_t n_shards;
-    uint64_t cap;                       // keys per shard region
-    uint32_t* cursor;                   // n_shards
-    unsigned long long* region;         // n_shards * cap, key = p << 32 | q
-};
-
+// registers.  Statistics -> gstats[b % kShards] (heavy groups: the heavy path's).
 // kMerge (bucket field >= kMergeMinBits): one slot word holds h's low 32 - bbits bits and the group
 // count above them (the top bits of h are the bucket, equal for every key), so the table of h
 // and the count table share H, and T shrinks to the per-position array: 18.9 KB of LDS at the
 // small geometry, 8 workgroups (32 waves) per CU instead of 6
 constexpr unsigned kMergeMinBits = 11;
-template <int kCap, int kThreads, int kTabBits, bool kPShard = false, bool kMerge = false>
-__device__ __forceinline__ void process_bucket(
-    const uint32_t b, const unsigned long long* __restrict__ sorted, const uint32_t* __restrict__ bstart,
-    const Layout& lay, uint32_t n_prot, int require_diff, uint32_t heavy_df, bool small,
-    unsigned long long* __restrict__ out, uint64_t shard_cap, unsigned long long* __restrict__ cursor,
-    unsigned long long* __restrict__ gstats, uint32_t* __restrict__ flags, uint32_t* __restrict__ list,
-    uint32_t* __restrict__ list_count, const PShard& ps) {
+template <int kCap, int kThreads, int kTabBits, bool kMerge, bool kRows>
+__device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArgs& a, bool small) {
     constexpr int kE = kCap / kThreads;
     constexpr uint32_t kTab = 1u << kTabBits;
     constexpr int kPer = kTab / kThreads;
+    constexpr int kMaxHeavy = kCap / (kHeavySub + 1) + 1;
     static_assert(kE * kThreads == kCap && kPer % 4 == 0 && kTab >= (uint32_t)kCap, "geometry");
     static_assert(!kMerge || kCap < (1 << kMergeMinBits) - 1, "merged count field");
     // T: (unmerged) A: table of h; C-E: per position start<<8|size
@@ -643,15 +638,26 @@ __device__ __forceinline__ void process_bucket(
     __shared__ uint32_t wave_tot[kThreads / 64];
     __shared__ unsigned long long red[kThreads / 64][3];
     __shared__ unsigned long long sbase;
-    __shared__ uint32_t heavy;
-    const uint32_t s0 = bstart[b], n = bstart[b + 1] - s0;
+    __shared__ unsigned long long hbase[kMaxHeavy];  // spill offset of each heavy group
+    __shared__ uint32_t nheavy, hkeys;
+    const uint32_t s0 = a.bstart[b], n = a.bstart[b + 1] - s0;
     const int tid = threadIdx.x;
+    const Layout& lay = a.lay;
     if (n == 0) return;
+    const uint32_t shard = b % kShards;
     if (n > (uint32_t)kCap) {
-        if (tid == 0) {
-            if (small) list[atomicAdd(list_count, 1u)] = b;  // the large kernel takes it
-            else flags[0] = 1;                                // too big: flat layout
+        if (small) {
+            if (tid == 0) a.list[atomicAdd(a.list_count, 1u)] = b;  // the large kernel takes it
+            return;
         }
+        // above every LDS capacity: the whole bucket goes to the heavy path
+        if (!a.spill) return;
+        __syncthreads();
+        if (tid == 0) sbase = atomicAdd(&a.spill_cursor[shard], (unsigned long long)n);
+        __syncthreads();
+        unsigned long long* dst = a.spill + (uint64_t)shard * a.spill_cap;
+        for (uint32_t i = tid; i < n; i += kThreads)
+            if (sbase + i < a.spill_cap) dst[sbase + i] = a.sorted[s0 + i];
         return;
     }
     __syncthreads();  // LDS reuse across the buckets of one workgroup
@@ -668,14 +674,14 @@ __device__ __forceinline__ void process_bucket(
     }
     for (uint32_t i = tid; i < kCap / 32; i += kThreads) dupw[i] = gdupw[i] = 0;
     for (uint32_t i = tid; i <= kHeavySub; i += kThreads) SZ[i] = 0;
-    if (tid == 0) heavy = 0;
+    if (tid == 0) nheavy = hkeys = 0;
     __syncthreads();
     // A. group slot + rank of every key
     uint32_t xl[kE], sl[kE], rk[kE];
 #pragma unroll
     for (int e = 0; e < kE; ++e) {
         const uint32_t i = tid + e * kThreads;
-        const unsigned long long x = i < n ? sorted[s0 + i] : 0ull;
+        const unsigned long long x = i < n ? a.sorted[s0 + i] : 0ull;
         const uint32_t h = (uint32_t)(x >> hshift);
         xl[e] = (uint32_t)x & lmask;
         sl[e] = 0;
@@ -707,13 +713,10 @@ __device__ __forceinline__ void process_bucket(
         }
     }
     __syncthreads();
-    if (KMP_BUCKET_STOP == 1) {
-        if (tid == 0 && T[0] == 0xFFFFFFFFu && H[1] == 7u) flags[3] = 1;
-        return;
-    }
     // B. size classes, largest first.  Each group's first key (rank 0) stands for it (count from
     // its slot word, size-class rank, position rewrite), so the pass is per key, not over all kTab
-    // table slots (measured 6 % faster); singleton groups (most) take no rank and no position
+    // table slots (measured 6 % faster); singleton groups (most) take no rank and no position.
+    // A heavy group's first key reserves its spill range (one returning atomic per bucket).
     uint32_t single = 0;
     uint32_t cn[kE], rr[kE];
 #pragma unroll
@@ -723,49 +726,54 @@ __device__ __forceinline__ void process_bucket(
         const uint32_t w = H[sl[e]];
         cn[e] = kMerge ? w >> hb : w;
         if (rk[e] == 0) {
-            if (cn[e] > kHeavySub) heavy = 1;
-            else if (cn[e] == 1) ++single;
-            else rr[e] = atomicAdd(&SZ[cn[e]], 1u);
+            if (cn[e] > kHeavySub) {
+                if (a.spill) {
+                    rr[e] = atomicAdd(&nheavy, 1u);
+                    hbase[rr[e]] = atomicAdd(&hkeys, cn[e]);  // offset inside the bucket's spill range
+                }
+            } else if (cn[e] == 1) {
+                ++single;
+            } else {
+                rr[e] = atomicAdd(&SZ[cn[e]], 1u);
+            }
         }
     }
     __syncthreads();
-    if (heavy) {
-        if (tid == 0) flags[0] = 1;
-        return;
-    }
+    if (tid == 0 && hkeys) sbase = atomicAdd(&a.spill_cursor[shard], (unsigned long long)hkeys);
     uint32_t nm;  // keys in groups of two or more: positions [0, nm)
     {
         const bool cls = tid + 2 <= (int)kHeavySub;                       // classes kHeavySub .. 2
         const uint32_t m = cls ? kHeavySub - tid : 0;
         const uint32_t v = cls ? m * SZ[m] : 0u;
         uint32_t excl;
-        block_scan_n<kThreads>(v, excl, nm, wave_tot);
+        block_scan_n<kThreads>(v, excl, nm, wave_tot);  // barriers: sbase visible after it
         if (cls) SZ[m] = excl;  // first position of size class m
     }
     __syncthreads();
 #pragma unroll
     for (int e = 0; e < kE; ++e)
-        if (rk[e] == 0 && cn[e] >= 2) H[sl[e]] = ((SZ[cn[e]] + rr[e] * cn[e]) << 8) | cn[e];
+        if (rk[e] == 0 && cn[e] >= 2) H[sl[e]] = cn[e] > kHeavySub ? rr[e] : ((SZ[cn[e]] + rr[e] * cn[e]) << 8) | cn[e];
     __syncthreads();
-    if (KMP_BUCKET_STOP == 2) {
-        if (tid == 0 && T[0] == 0xFFFFFFFFu && H[1] == 7u) flags[3] = 1;
-        return;
-    }
-    // C. scatter (T now holds, per position, its group's start << 8 | size)
+    // C. scatter (T now holds, per position, its group's start << 8 | size); heavy groups' keys
+    // go to the spill region
+    unsigned long long* spill_dst = a.spill ? a.spill + (uint64_t)shard * a.spill_cap : nullptr;
 #pragma unroll
-    for (int e = 0; e < kE; ++e)
-        if (tid + e * kThreads < n) {
-            if (cn[e] < 2) continue;  // singleton
-            const uint32_t g = H[sl[e]];
-            const uint32_t pos = (g >> 8) + rk[e];
-            Bl[pos] = xl[e];
-            T[pos] = g;
+    for (int e = 0; e < kE; ++e) {
+        const uint32_t i = tid + e * kThreads;
+        if (i >= n || cn[e] < 2) continue;  // singleton
+        const uint32_t g = H[sl[e]];
+        if (cn[e] > kHeavySub) {
+            if (spill_dst) {
+                const unsigned long long pos = sbase + hbase[g] + rk[e];
+                if (pos < a.spill_cap) spill_dst[pos] = a.sorted[s0 + i];
+            }
+            continue;
         }
-    __syncthreads();
-    if (KMP_BUCKET_STOP == 3) {
-        if (tid == 0 && T[0] == 0xFFFFFFFFu && H[1] == 7u) flags[3] = 1;
-        return;
+        const uint32_t pos = (g >> 8) + rk[e];
+        Bl[pos] = xl[e];
+        T[pos] = g;
     }
+    __syncthreads();
     // D. per position: group bounds, duplicate flag (same protein earlier in the group: the same
     // p << cb | class word); a group holding one marks its start in gdupw
     uint32_t s[kE], en[kE];
@@ -786,10 +794,6 @@ __device__ __forceinline__ void process_bucket(
             }
     }
     __syncthreads();
-    if (KMP_BUCKET_STOP == 4) {
-        if (tid == 0 && T[0] == 0xFFFFFFFFu && H[1] == 7u) flags[3] = 1;
-        return;
-    }
     auto is_dup = [&](uint32_t j) { return (dupw[j >> 5] >> (j & 31)) & 1u; };
     // E. df, head, kept-partner count.  A group without duplicates (almost all) has df = its size
     // and counts its partners after i only; a group with one walks the whole group.
@@ -806,9 +810,21 @@ __device__ __forceinline__ void process_bucket(
         gd[e] = (gdupw[s[e] >> 5] >> (s[e] & 31)) & 1u;
         if (gd[e] && is_dup(i)) continue;
         uint32_t f, c = 0;
-        if (!gd[e]) {
+        if (kRows) {
+            // df, and the partners of a larger protein when this element's protein is in the rows
+            const uint32_t p = xl[e] >> cb;
+            const bool emit = p >= a.row_lo && p < a.row_hi;
+            f = gd[e] ? 0u : en[e] - s[e];
+            if (emit || gd[e])
+                for (uint32_t j = s[e]; j < en[e]; ++j) {
+                    if (gd[e] && is_dup(j)) continue;
+                    f += gd[e];
+                    const uint32_t lj = Bl[j];
+                    c += emit && (lj >> cb) > p && (!a.require_diff || ((lj ^ xl[e]) & cmask));
+                }
+        } else if (!gd[e]) {
             f = en[e] - s[e];
-            if (require_diff) {
+            if (a.require_diff) {
                 for (uint32_t j = i + 1; j < en[e]; ++j) c += ((Bl[j] ^ xl[e]) & cmask) != 0u;
             } else {
                 c = en[e] - 1 - i;
@@ -818,312 +834,95 @@ __device__ __forceinline__ void process_bucket(
             for (uint32_t j = s[e]; j < en[e]; ++j) {
                 if (is_dup(j)) continue;
                 ++f;
-                if (j > i && (!require_diff || ((Bl[j] ^ xl[e]) & cmask))) ++c;
+                if (j > i && (!a.require_diff || ((Bl[j] ^ xl[e]) & cmask))) ++c;
             }
         }
-        if (f > heavy_df) c = 0;
+        if (f > a.heavy_df) c = 0;
         st_sum += 1;
         if (i == s[e]) {  // the group's first position is never a duplicate
             st_dist += 1;
             st_rep += f >= 2;
-            if (f <= heavy_df) st_cdf2 += f * (f - 1) / 2;
+            if (f <= a.heavy_df) st_cdf2 += f * (f - 1) / 2;
             else st_heavy += f;
             st_max = max(st_max, f);
         }
         cnt[e] = c;
         mine += c;
     }
-    if (KMP_BUCKET_STOP == 5) {
-        if (tid == 0 && mine == 0xFFFFFFFFu) flags[3] = 1;
-        return;
-    }
     // statistics: three wave reductions of packed words (per workgroup every count is at most
     // kCap, so 16-bit fields cannot carry; C(df,2) and the incidences stay below 2^32), wave
-    // partials -> red, then kStN threads unpack, sum and post one (sharded) atomic each
-    auto wave_stats = [&]() {
-        unsigned long long a = st_sum | (unsigned long long)st_dist << 16 | (unsigned long long)st_rep << 32 |
-                               (unsigned long long)st_heavy << 48;
+    // partials -> red, then kStN threads unpack, sum and post one (sharded) atomic each.  They
+    // ride on the output scan's barriers; the last wave reserves the output range meanwhile.
+    {
+        unsigned long long w0 = st_sum | (unsigned long long)st_dist << 16 | (unsigned long long)st_rep << 32 |
+                                (unsigned long long)st_heavy << 48;
         unsigned long long c2 = st_cdf2 | (unsigned long long)mine << 32;
         uint32_t mx = st_max;
         for (int sh = 32; sh > 0; sh >>= 1) {
-            a += __shfl_down(a, sh);
+            w0 += __shfl_down(w0, sh);
             c2 += __shfl_down(c2, sh);
             mx = max(mx, (uint32_t)__shfl_down(mx, sh));
         }
         if ((tid & 63) == 0) {
-            red[tid >> 6][0] = a;
+            red[tid >> 6][0] = w0;
             red[tid >> 6][1] = c2;
             red[tid >> 6][2] = mx;
         }
-    };
-    auto post_stats = [&]() {
-        if (tid < kStN) {
-            unsigned long long v = 0;
-            for (int w = 0; w < kThreads / 64; ++w) {
-                const unsigned long long a = red[w][0], c2 = red[w][1], mx = red[w][2];
-                const unsigned long long x = tid == kStSumS     ? a & 0xFFFF
-                                             : tid == kStDistinct ? (a >> 16) & 0xFFFF
-                                             : tid == kStRepeat   ? (a >> 32) & 0xFFFF
-                                             : tid == kStHeavy    ? a >> 48
-                                             : tid == kStCdf2     ? c2 & 0xFFFFFFFFull
-                                             : tid == kStInc      ? c2 >> 32
-                                                                  : mx;
-                v = tid == kStMaxDf ? (v > x ? v : x) : v + x;
-            }
-            unsigned long long* g = gstats + (uint64_t)(b % kShards) * 8 + tid;  // sharded: no hot word
-            if (tid == kStMaxDf) atomicMax(g, v);
-            else if (v) atomicAdd(g, v);
+    }
+    uint32_t excl, total;
+    block_scan_n<kThreads>(mine, excl, total, wave_tot);
+    if (tid == kThreads - 64) sbase = total ? atomicAdd(&a.cursor[shard], (unsigned long long)total) : 0ull;
+    if (tid < kStN) {
+        unsigned long long v = 0;
+        for (int w = 0; w < kThreads / 64; ++w) {
+            const unsigned long long w0 = red[w][0], c2 = red[w][1], mx = red[w][2];
+            const unsigned long long x = tid == kStSumS     ? w0 & 0xFFFF
+                                         : tid == kStDistinct ? (w0 >> 16) & 0xFFFF
+                                         : tid == kStRepeat   ? (w0 >> 32) & 0xFFFF
+                                         : tid == kStHeavy    ? w0 >> 48
+                                         : tid == kStCdf2     ? c2 & 0xFFFFFFFFull
+                                         : tid == kStInc      ? c2 >> 32
+                                                              : mx;
+            v = tid == kStMaxDf ? (v > x ? v : x) : v + x;
         }
-    };
+        unsigned long long* g = a.gstats + (uint64_t)shard * 8 + tid;  // sharded: no hot word
+        if (tid == kStMaxDf) atomicMax(g, v);
+        else if (v) atomicAdd(g, v);
+    }
+    __syncthreads();
     // F. write the pair keys
-    if (kPShard) {
-        if (mine) {
+    if (mine) {
+        unsigned long long pos = sbase + excl;
+        unsigned long long* dst = a.out + (uint64_t)shard * a.shard_cap;
 #pragma unroll
-            for (int e = 0; e < kE; ++e) {
-                if (!cnt[e]) continue;
-                const uint32_t i = tid + e * kThreads;
-                const uint32_t p = xl[e] >> cb;
-                for (uint32_t j = i + 1; j < en[e]; ++j) {
-                    if (gd[e] && is_dup(j)) continue;
-                    const uint32_t lj = Bl[j];
-                    if (require_diff && !((lj ^ xl[e]) & cmask)) continue;
-                    const uint32_t q = lj >> cb;
-                    const uint32_t a = min(p, q), c = max(p, q);
-                    const uint32_t sh = a >> ps.row_bits;
-                    const uint32_t slot = atomicAdd(&ps.cursor[sh], 1u);
-                    if (slot < ps.cap) ps.region[(uint64_t)sh * ps.cap + slot] = ((unsigned long long)a << 32) | c;
-                }
-            }
-        }
-    } else {
-        // KMP_F_EARLY: the statistics ride on the scan's barriers, and the output reservation is made
-        // by the last wave while wave 0 posts them
-        if (KMP_F_EARLY) wave_stats();
-        uint32_t excl, total;
-        block_scan_n<kThreads>(mine, excl, total, wave_tot);
-        const uint32_t shard = b % kShards;
-        constexpr int kRes = KMP_F_EARLY ? kThreads - 64 : 0;
-        if (tid == kRes) sbase = total ? atomicAdd(&cursor[shard], (unsigned long long)total) : 0ull;
-        if (KMP_F_EARLY) post_stats();
-        __syncthreads();
-        if (mine) {
-            unsigned long long pos = sbase + excl;
-            unsigned long long* dst = out + (uint64_t)shard * shard_cap;
-#pragma unroll
-            for (int e = 0; e < kE; ++e) {
-                if (!cnt[e]) continue;
-                const uint32_t i = tid + e * kThreads;
-                const uint32_t p = xl[e] >> cb;
-                for (uint32_t j = i + 1; j < en[e]; ++j) {
-                    if (gd[e] && is_dup(j)) continue;
-                    const uint32_t lj = Bl[j];
-                    if (require_diff && !((lj ^ xl[e]) & cmask)) continue;
-                    const uint32_t q = lj >> cb;
-                    if (pos < shard_cap) dst[pos] = (unsigned long long)min(p, q) * n_prot + max(p, q);
-                    ++pos;
-                }
+        for (int e = 0; e < kE; ++e) {
+            if (!cnt[e]) continue;
+            const uint32_t i = tid + e * kThreads;
+            const uint32_t p = xl[e] >> cb;
+            for (uint32_t j = kRows ? s[e] : i + 1; j < en[e]; ++j) {
+                if (gd[e] && is_dup(j)) continue;
+                const uint32_t lj = Bl[j];
+                if (a.require_diff && !((lj ^ xl[e]) & cmask)) continue;
+                const uint32_t q = lj >> cb;
+                if (kRows && q <= p) continue;
+                if (pos < a.shard_cap) dst[pos] = (unsigned long long)min(p, q) * a.mul + max(p, q);
+                ++pos;
             }
         }
     }
-    if (!kPShard && KMP_F_EARLY) return;  // statistics already posted
-    wave_stats();
-    __syncthreads();
-    post_stats();
 }
 
-template <int kCap, int kThreads, int kTabBits, bool kPShard = false, bool kMerge = false>
-__global__ __launch_bounds__(kThreads) void bucket_small_kernel(
-    const unsigned long long* __restrict__ sorted, const uint32_t* __restrict__ bstart, Layout lay,
-    uint32_t n_prot, int require_diff, uint32_t heavy_df, unsigned long long* __restrict__ out, uint64_t shard_cap,
-    unsigned long long* __restrict__ cursor, unsigned long long* __restrict__ gstats, uint32_t* __restrict__ flags,
-    uint32_t* __restrict__ list, uint32_t* __restrict__ list_count, PShard ps, uint32_t b0 = 0) {
-    // buckets b0 + blockIdx.x (a multi-GPU rank launches only its bucket range)
-    process_bucket<kCap, kThreads, kTabBits, kPShard, kMerge>(b0 + blockIdx.x, sorted, bstart, lay, n_prot, require_diff,
-                                                      heavy_df, true, out, shard_cap, cursor, gstats, flags, list,
-                                                      list_count, ps);
+template <int kCap, int kThreads, int kTabBits, bool kMerge, bool kRows>
+__global__ __launch_bounds__(kThreads) void bucket_small_kernel(BucketArgs a, uint32_t b0) {
+    process_bucket<kCap, kThreads, kTabBits, kMerge, kRows>(b0 + blockIdx.x, a, true);
 }
 
 // the buckets the small kernel listed (above its capacity), a grid-stride loop over the list
-template <int kCap, int kThreads, int kTabBits, bool kPShard = false>
-__global__ __launch_bounds__(kThreads) void bucket_large_kernel(
-    const unsigned long long* __restrict__ sorted, const uint32_t* __restrict__ bstart, Layout lay,
-    uint32_t n_prot, int require_diff, uint32_t heavy_df, unsigned long long* __restrict__ out, uint64_t shard_cap,
-    unsigned long long* __restrict__ cursor, unsigned long long* __restrict__ gstats, uint32_t* __restrict__ flags,
-    uint32_t* __restrict__ list, const uint32_t* __restrict__ list_count, PShard ps, uint32_t lo = 0,
-    uint32_t hi = 0xFFFFFFFFu) {
-    // [lo, hi): the buckets of this launch (a pipelined chunk); the list may hold earlier chunks'
-    const uint32_t m = *list_count;
-    for (uint32_t i = blockIdx.x; i < m; i += gridDim.x) {
-        const uint32_t b = list[i];
-        if (b < lo || b >= hi) continue;
-        process_bucket<kCap, kThreads, kTabBits, kPShard>(b, sorted, bstart, lay, n_prot, require_diff, heavy_df, false,
-                                                          out, shard_cap, cursor, gstats, flags, nullptr, nullptr, ps);
-    }
-}
-
-// ---------------------------------------------------------------- p-shard reduction --------
-// One workgroup per row range [s << row_bits, (s+1) << row_bits) (combine_edges, mod.rs:322-546):
-// its m pair keys (p << 32 | q) as v = row << 24 | q in LDS, counting sort by row, rank sort by q
-// inside each row (rows are short), runs of equal v = one pair, run length = w; pairs with
-// w >= min_shared go to the shard's edge region in (p, q) order.  ecount[s] = edges,
-// npairs[s] = pairs before the min_shared filter.
-constexpr int kReduceCap = 8192, kReduceThreads = 256, kReduceRowsMax = 256;
-constexpr uint32_t kRankRowMax = 512;  // longer rows: bitonic sort of the whole shard instead
-__global__ __launch_bounds__(kReduceThreads) void shard_reduce_kernel(
-    const unsigned long long* __restrict__ region, const uint32_t* __restrict__ cursor, uint64_t cap,
-    unsigned row_bits, uint32_t min_shared, uint32_t* __restrict__ ep, uint32_t* __restrict__ eq,
-    uint32_t* __restrict__ ew, uint32_t* __restrict__ ecount, uint32_t* __restrict__ npairs) {
-    __shared__ uint32_t A[kReduceCap], Bv[kReduceCap];
-    __shared__ uint32_t rc[kReduceRowsMax + 1], cur[kReduceRowsMax];
-    __shared__ uint32_t wave_tot[kReduceThreads / 64];
-    __shared__ uint32_t big;
-    const uint32_t s = blockIdx.x;
-    const int tid = threadIdx.x;
-    const uint32_t m = (uint32_t)min((uint64_t)cursor[s], cap);
-    const uint32_t rows = 1u << row_bits;
-    const uint32_t p0 = s << row_bits;
-    const unsigned long long* src = region + (uint64_t)s * cap;
-    if (m == 0) {
-        if (tid == 0) ecount[s] = npairs[s] = 0;
-        return;
-    }
-    if (tid <= (int)rows) rc[tid] = 0;
-    if (tid == 0) big = 0;
-    __syncthreads();
-    // 1. v = row << 24 | q, row histogram
-    for (uint32_t i = tid; i < m; i += kReduceThreads) {
-        const unsigned long long x = src[i];
-        const uint32_t row = (uint32_t)(x >> 32) - p0;
-        A[i] = (row << 24) | (uint32_t)x;
-        atomicAdd(&rc[row], 1u);
-    }
-    __syncthreads();
-    {
-        const uint32_t v = tid < (int)rows ? rc[tid] : 0u;
-        if (v > kRankRowMax) big = 1;
-        uint32_t excl, total;
-        block_scan_n<kReduceThreads>(v, excl, total, wave_tot);
-        if (tid < (int)rows) rc[tid] = cur[tid] = excl;
-        if (tid == 0) rc[rows] = m;
-    }
-    __syncthreads();
-    if (!big) {
-        // 2. group by row, then rank sort inside each row (position = row start + #smaller or
-        //    equal-and-earlier)
-        for (uint32_t i = tid; i < m; i += kReduceThreads) {
-            const uint32_t v = A[i];
-            Bv[atomicAdd(&cur[v >> 24], 1u)] = v;
-        }
-        __syncthreads();
-        for (uint32_t i = tid; i < m; i += kReduceThreads) {
-            const uint32_t v = Bv[i];
-            const uint32_t rs = rc[v >> 24], re = rc[(v >> 24) + 1];
-            uint32_t rank = 0;
-            for (uint32_t j = rs; j < re; ++j) {
-                const uint32_t u = Bv[j];
-                rank += u < v || (u == v && j < i);
-            }
-            A[rs + rank] = v;
-        }
-    } else {
-        // a long row: bitonic sort of the whole shard (padding sorts last)
-        uint32_t np = 1;
-        while (np < m) np <<= 1;
-        for (uint32_t i = m + tid; i < np; i += kReduceThreads) A[i] = 0xFFFFFFFFu;
-        __syncthreads();
-        for (uint32_t k2 = 2; k2 <= np; k2 <<= 1)
-            for (uint32_t j = k2 >> 1; j > 0; j >>= 1) {
-                for (uint32_t i = tid; i < np; i += kReduceThreads) {
-                    const uint32_t l = i ^ j;
-                    if (l > i) {
-                        const uint32_t x = A[i], y = A[l];
-                        if (((i & k2) == 0) == (x > y)) {
-                            A[i] = y;
-                            A[l] = x;
-                        }
-                    }
-                }
-                __syncthreads();
-            }
-    }
-    __syncthreads();
-    // 3. runs of equal v = one pair, w = run length; contiguous chunks per thread keep the
-    //    output in (p, q) order
-    const uint32_t chunk = (m + kReduceThreads - 1) / kReduceThreads;
-    const uint32_t c0 = min(m, tid * chunk), c1 = min(m, c0 + chunk);
-    uint32_t kept = 0, heads = 0;
-    for (uint32_t i = c0; i < c1; ++i) {
-        const uint32_t v = A[i];
-        if (i > 0 && A[i - 1] == v) continue;
-        uint32_t e = i + 1;
-        while (e < m && A[e] == v) ++e;
-        ++heads;
-        kept += e - i >= min_shared;
-    }
-    uint32_t excl, total, hx, htotal;
-    block_scan_n<kReduceThreads>(kept, excl, total, wave_tot);
-    block_scan_n<kReduceThreads>(heads, hx, htotal, wave_tot);
-    if (tid == 0) {
-        ecount[s] = total;
-        npairs[s] = htotal;
-    }
-    uint32_t* const op = ep + (uint64_t)s * cap;
-    uint32_t* const oq = eq + (uint64_t)s * cap;
-    uint32_t* const ow = ew + (uint64_t)s * cap;
-    for (uint32_t i = c0; i < c1; ++i) {
-        const uint32_t v = A[i];
-        if (i > 0 && A[i - 1] == v) continue;
-        uint32_t e = i + 1;
-        while (e < m && A[e] == v) ++e;
-        if (e - i < min_shared) continue;
-        op[excl] = p0 + (v >> 24);
-        oq[excl] = v & 0xFFFFFFu;
-        ow[excl] = e - i;
-        ++excl;
-    }
-}
-
-// shard edge regions -> the caller's (p, q, w) arrays at the shards' exclusive offsets
-__global__ void compact_edges_kernel(const uint32_t* __restrict__ ep, const uint32_t* __restrict__ eq,
-                                     const uint32_t* __restrict__ ew, uint64_t cap,
-                                     const uint32_t* __restrict__ ecount, const unsigned long long* __restrict__ eoff,
-                                     uint32_t* __restrict__ out_p, uint32_t* __restrict__ out_q,
-                                     uint32_t* __restrict__ out_w, uint64_t out_cap) {
-    const uint32_t s = blockIdx.x;
-    const uint32_t m = ecount[s];
-    const unsigned long long o = eoff[s];
-    for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
-        if (o + i >= out_cap) break;
-        const uint64_t k = (uint64_t)s * cap + i;
-        out_p[o + i] = ep[k];
-        out_q[o + i] = eq[k];
-        out_w[o + i] = ew[k];
-    }
-}
-
-// unused tail of every shard region -> kNoKey (sorts after every pair key)
-__global__ void pad_shards_kernel(unsigned long long* __restrict__ region, uint64_t shard_cap,
-                                  const unsigned long long* __restrict__ cursor) {
-    const int s = blockIdx.y;
-    const unsigned long long m = cursor[s];
-    for (uint64_t i = m + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < shard_cap;
-         i += (uint64_t)gridDim.x * blockDim.x)
-        region[(uint64_t)s * shard_cap + i] = kNoKey;
-}
-
-// (pair key, w) runs -> edges, w >= 1 (the padding run, key kNoKey, is last and skipped)
-__global__ void emit_runs_kernel(const unsigned long long* __restrict__ uniq, const uint32_t* __restrict__ w,
-                                 const uint32_t* __restrict__ nuniq, uint32_t n_prot, uint32_t* __restrict__ out_p,
-                                 uint32_t* __restrict__ out_q, uint32_t* __restrict__ out_w, uint64_t cap,
-                                 uint32_t stride = 1) {
-    const uint32_t U = *nuniq;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < U; i += gridDim.x * blockDim.x) {
-        const unsigned long long x = uniq[i];
-        if (x == kNoKey || i >= cap) continue;
-        out_p[(uint64_t)i * stride] = (uint32_t)(x / n_prot);
-        out_q[(uint64_t)i * stride] = (uint32_t)(x % n_prot);
-        out_w[(uint64_t)i * stride] = w[i];
-    }
+template <int kCap, int kThreads, int kTabBits, bool kRows>
+__global__ __launch_bounds__(kThreads) void bucket_large_kernel(BucketArgs a) {
+    const uint32_t m = *a.list_count;
+    for (uint32_t i = blockIdx.x; i < m; i += gridDim.x)
+        process_bucket<kCap, kThreads, kTabBits, false, kRows>(a.list[i], a, false);
 }
 
 // shard regions -> one contiguous array (shard order)
@@ -1137,6 +936,209 @@ __global__ void gather_shards_kernel(const unsigned long long* __restrict__ src,
     for (unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; i < m;
          i += (unsigned long long)gridDim.x * blockDim.x)
         dst[off + i] = src[(uint64_t)s * shard_cap + i];
+}
+
+// ------------------------------------------------------------- heavy path ------------------
+// Frequent k-mers (a group above kHeavySub keys) and buckets above every LDS capacity are
+// spilled by the bucket kernels (their keys, unchanged) and expanded here, with no cap on df:
+//   1. the spilled keys, gathered, are radix sorted on (h, p) (bits [clsbits, 63)): one run per
+//      k-mer, its proteins ascending, duplicate windows of one protein adjacent;
+//   2. heavy_scan / heavy_compact (4,096-key tiles + a scan of the tile counts): the distinct
+//      (k-mer, protein) elements E = p << cb | class, and each k-mer's start GS[g] in E;
+//      df(g) = GS[g+1] - GS[g] (main.rs:77-122 restated on the spill);
+//   3. heavy_plan (one thread per k-mer): statistics, the element range [i0, i1) whose proteins
+//      lie in the call's rows, and the tile count: element blocks of kHvI rows x partner chunks
+//      of kHvJ (the upper triangle of the k-mer's C(df,2) pairs, vertex.rs:103-137);
+//   4. heavy_expand (one workgroup per tile): the partner chunk in LDS, one row per thread, the
+//      class test (mod.rs:580-587) on every pair (p_i, p_j), j > i; a workgroup scan and one
+//      cursor reservation place the pair keys p_i * mul + p_j in the shard regions the bucket
+//      kernels fill.  A k-mer of df 10^4 is ~400 tiles: no workgroup walks a long posting list.
+constexpr uint32_t kHvTile = 4096, kHvThreads = 256, kHvPer = kHvTile / kHvThreads;
+constexpr uint32_t kHvI = 256, kHvJ = 2048;
+
+// per tile: distinct (h, p) elements and k-mer heads -> cnt[2 * t], cnt[2 * t + 1]
+__global__ __launch_bounds__(kHvThreads) void heavy_scan_kernel(const unsigned long long* __restrict__ x, uint64_t m,
+                                                                unsigned cb, unsigned hshift,
+                                                                uint32_t* __restrict__ ecnt,
+                                                                uint32_t* __restrict__ gcnt) {
+    __shared__ uint32_t s_e, s_g;
+    if (threadIdx.x == 0) s_e = s_g = 0;
+    __syncthreads();
+    const uint64_t t0 = (uint64_t)blockIdx.x * kHvTile;
+    uint32_t ne = 0, ng = 0;
+    for (uint32_t r = 0; r < kHvPer; ++r) {
+        const uint64_t i = t0 + r * kHvThreads + threadIdx.x;
+        if (i >= m) break;
+        const unsigned long long v = x[i], u = i ? x[i - 1] : ~0ull;
+        ne += (v >> cb) != (u >> cb);
+        ng += (v >> hshift) != (u >> hshift);
+    }
+    if (ne) atomicAdd(&s_e, ne);
+    if (ng) atomicAdd(&s_g, ng);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        ecnt[blockIdx.x] = s_e;
+        gcnt[blockIdx.x] = s_g;
+    }
+}
+
+// per tile: the elements at eoff[t] + their rank, the k-mer starts at goff[t] + rank
+__global__ __launch_bounds__(kHvThreads) void heavy_compact_kernel(const unsigned long long* __restrict__ x,
+                                                                   uint64_t m, unsigned cb, unsigned hshift,
+                                                                   const uint64_t* __restrict__ eoff,
+                                                                   const uint64_t* __restrict__ goff,
+                                                                   uint32_t* __restrict__ E,
+                                                                   uint64_t* __restrict__ GS) {
+    __shared__ uint32_t wave_tot[kHvThreads / 64];
+    const uint64_t t0 = (uint64_t)blockIdx.x * kHvTile;
+    uint64_t eb = eoff[blockIdx.x], gb = goff[blockIdx.x];
+    const unsigned long long lmask = (1ull << hshift) - 1;
+    for (uint32_t r = 0; r < kHvPer; ++r) {
+        const uint64_t i = t0 + r * kHvThreads + threadIdx.x;
+        bool ke = false, kg = false;
+        unsigned long long v = 0;
+        if (i < m) {
+            v = x[i];
+            const unsigned long long u = i ? x[i - 1] : ~0ull;
+            ke = (v >> cb) != (u >> cb);
+            kg = (v >> hshift) != (u >> hshift);
+        }
+        uint32_t xe, te, xg, tg;
+        block_scan_n<kHvThreads>(ke, xe, te, wave_tot);
+        block_scan_n<kHvThreads>(kg, xg, tg, wave_tot);
+        if (ke) E[eb + xe] = (uint32_t)(v & lmask);
+        if (kg) GS[gb + xg] = eb + xe;  // a k-mer head is always a new element
+        eb += te;
+        gb += tg;
+    }
+}
+
+// per k-mer: statistics (stats != 0), rows [i0, i1) of the call, tile count
+__global__ __launch_bounds__(256) void heavy_plan_kernel(const uint32_t* __restrict__ E,
+                                                         const uint64_t* __restrict__ GS, uint64_t ng,
+                                                         unsigned cb, uint32_t row_lo, uint32_t row_hi,
+                                                         uint32_t heavy_df, int stats,
+                                                         unsigned long long* __restrict__ gstats,
+                                                         uint32_t* __restrict__ gi,
+                                                         unsigned long long* __restrict__ tcount) {
+    const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    unsigned long long st[kStN] = {0, 0, 0, 0, 0, 0, 0};
+    if (g < ng) {
+        const uint64_t b = GS[g];
+        const uint32_t d = (uint32_t)(GS[g + 1] - b);
+        auto lower = [&](uint32_t row) {  // first element whose protein >= row
+            uint32_t lo = 0, hi = d;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if ((E[b + mid] >> cb) < row) lo = mid + 1;
+                else hi = mid;
+            }
+            return lo;
+        };
+        uint32_t i0 = 0, i1 = 0;
+        unsigned long long tiles = 0;
+        if (d >= 2 && d <= heavy_df) {
+            i0 = lower(row_lo);
+            i1 = lower(row_hi);
+            for (uint32_t r = i0; r < i1; r += kHvI) tiles += (d - (r + 1) + kHvJ - 1) / kHvJ;
+        }
+        gi[2 * g] = i0;
+        gi[2 * g + 1] = i1;
+        tcount[g] = tiles;
+        st[kStSumS] = d;
+        st[kStDistinct] = 1;
+        st[kStRepeat] = d >= 2;
+        if (d <= heavy_df) st[kStCdf2] = (unsigned long long)d * (d - 1) / 2;
+        else st[kStHeavy] = d;
+        st[kStMaxDf] = d;
+    }
+    if (!stats) return;
+    __shared__ unsigned long long red[4][kStN];
+#pragma unroll
+    for (int t = 0; t < kStN; ++t) {
+        unsigned long long v = st[t];
+        for (int s = 32; s > 0; s >>= 1) v = stat_op(t, v, __shfl_down(v, s));
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][t] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < kStN && threadIdx.x != kStInc) {
+        const int t = threadIdx.x;
+        unsigned long long v = red[0][t];
+        for (int w = 1; w < 4; ++w) v = stat_op(t, v, red[w][t]);
+        unsigned long long* gp = gstats + (uint64_t)(blockIdx.x % kShards) * 8 + t;
+        if (t == kStMaxDf) atomicMax(gp, v);
+        else if (v) atomicAdd(gp, v);
+    }
+}
+
+// one workgroup per tile (grid-stride): rows i of block r of k-mer g against partner chunk c
+__global__ __launch_bounds__(kHvI) void heavy_expand_kernel(const uint32_t* __restrict__ E,
+                                                            const uint64_t* __restrict__ GS,
+                                                            const uint32_t* __restrict__ gi,
+                                                            const unsigned long long* __restrict__ toff, uint64_t ng,
+                                                            const unsigned long long* __restrict__ ntiles,
+                                                            unsigned cb, uint32_t mul, int require_diff,
+                                                            unsigned long long* __restrict__ out, uint64_t shard_cap,
+                                                            unsigned long long* __restrict__ cursor,
+                                                            unsigned long long* __restrict__ gstats) {
+    __shared__ uint32_t J[kHvJ];
+    __shared__ uint32_t wave_tot[kHvI / 64];
+    __shared__ unsigned long long sbase;
+    const unsigned long long T = *ntiles;
+    const uint32_t cmask = (1u << cb) - 1;
+    for (unsigned long long t = blockIdx.x; t < T; t += gridDim.x) {
+        // k-mer g: the last with toff[g] <= t
+        uint64_t lo = 0, hi = ng;
+        while (lo + 1 < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (toff[mid] <= t) lo = mid;
+            else hi = mid;
+        }
+        const uint64_t g = lo, b = GS[g];
+        const uint32_t d = (uint32_t)(GS[g + 1] - b), i0 = gi[2 * g], i1 = gi[2 * g + 1];
+        unsigned long long local = t - toff[g];
+        uint32_t r = i0;  // row block start
+        while (r < i1) {
+            const unsigned long long c = (d - (r + 1) + kHvJ - 1) / kHvJ;
+            if (local < c) break;
+            local -= c;
+            r += kHvI;
+        }
+        if (r >= i1) continue;  // not reached with a consistent plan (uniform across the workgroup)
+        const uint32_t j0 = r + 1 + (uint32_t)local * kHvJ, j1 = min(d, j0 + kHvJ);
+        __syncthreads();  // J reuse
+        for (uint32_t j = j0 + threadIdx.x; j < j1; j += kHvI) J[j - j0] = E[b + j];
+        const uint32_t i = r + threadIdx.x;
+        const bool row = i < i1;
+        const uint32_t xi = row ? E[b + i] : 0u;
+        __syncthreads();
+        uint32_t c = 0;
+        const uint32_t js = row ? max(i + 1, j0) : j1;
+        if (require_diff) {
+            for (uint32_t j = js; j < j1; ++j) c += ((J[j - j0] ^ xi) & cmask) != 0u;
+        } else {
+            c = j1 - js;
+        }
+        uint32_t excl, total;
+        block_scan_n<kHvI>(c, excl, total, wave_tot);
+        const uint32_t shard = (uint32_t)(t % kShards);
+        if (threadIdx.x == 0) {
+            sbase = total ? atomicAdd(&cursor[shard], (unsigned long long)total) : 0ull;
+            if (total) atomicAdd(&gstats[(uint64_t)shard * 8 + kStInc], (unsigned long long)total);
+        }
+        __syncthreads();
+        if (c) {
+            unsigned long long pos = sbase + excl;
+            unsigned long long* dst = out + (uint64_t)shard * shard_cap;
+            const unsigned long long rowkey = (unsigned long long)(xi >> cb) * mul;
+            for (uint32_t j = js; j < j1; ++j) {
+                const uint32_t xj = J[j - j0];
+                if (require_diff && !((xj ^ xi) & cmask)) continue;
+                if (pos < shard_cap) dst[pos] = rowkey + (xj >> cb);
+                ++pos;
+            }
+        }
+    }
 }
 
 // bucket kernels: capacity (keys), threads, log2 of the k-mer table (>= capacity)
@@ -1161,8 +1163,8 @@ constexpr int kBucketLargeGrid = 32;
 //     counted and scattered the same way on digit2.  Output: keys grouped by bucket, in
 //     ws->sorted, and bstart[] for the bucket kernels straight from the scan.
 // Order inside a bucket is unspecified (LDS atomics rank the keys); the bucket kernel does not
-// need one.  A coarse bin above its tile budget (a k-mer with ~10^5 copies) raises flags[0], the
-// same fallback as a bucket above the large kernel's capacity.
+// need one.  A coarse bin above its tile budget (a k-mer with ~10^5 copies) raises flags[0] and
+// records the tiles it needs in flags[4]; the step reruns with that budget.
 constexpr uint32_t kBpTile = 4096;            // level-2 tile (level 1 uses the key chunk, also 4,096)
 constexpr uint32_t kBpPer = kBpTile / kKeyThreads;
 constexpr uint32_t kBpMaxBins = 1024;         // digit widths <= 10 bits
@@ -1453,8 +1455,11 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scan2_kernel(uint32_t* __restr
     const uint32_t c = c0 + blockIdx.x;
     const uint32_t b0 = C1[dg.nb1 + 1 + c], n = C1[dg.nb1 + 2 + c] - b0;  // compact start, key count
     const uint32_t nt = (n + kBpTile - 1) / kBpTile;
-    if (nt > J) {  // no tile of this bin was written: its buckets read as empty, the call falls back
-        if (threadIdx.x == 0) flags[0] = 1;
+    if (nt > J) {  // no tile of this bin was written: its buckets read as empty, the call reruns
+        if (threadIdx.x == 0) {
+            flags[0] = 1;
+            atomicMax(&flags[4], nt);  // the budget the rerun needs
+        }
         for (uint32_t d = threadIdx.x; d < dg.nb2; d += kKeyThreads) bstart[c * dg.nb2 + d] = b0;
         if (threadIdx.x == 0) bstart[(c + 1) * dg.nb2] = b0 + n;  // the bin's end (= the next bin's start)
         return;
@@ -1470,8 +1475,7 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scan2_kernel(uint32_t* __restr
         bstart[c * dg.nb2 + d] = run;
         col_prefix_inplace(base + d, dg.nb2, nt, run);
     }
-    // the bin's end, which the next bin's scan writes too (same value): a chunk of bins is
-    // complete without the scan of the next chunk (pipelined level 2)
+    // the bin's end, which the next bin's scan writes too (same value)
     if (threadIdx.x == 0) bstart[(c + 1) * dg.nb2] = b0 + n;
 }
 
@@ -1509,79 +1513,24 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scatter2_kernel(const unsigned
     bp_place(x, r, tn, dg.nb2, digit, lh, wave_tot, S, P2 + ((uint64_t)c * J + j) * dg.nb2, out);
 }
 
-// Level 1 from a key array instead of the residues (the multi-GPU owner's received keys, kNoKey
-// padding skipped): 4,096-key tiles, digit1 histogram -> H1[tile][digit], then the same column
-// scan and an LDS-ranked scatter into digit-major runs.
-__global__ __launch_bounds__(kKeyThreads) void bp_hist_arr_kernel(const unsigned long long* __restrict__ in,
-                                                                  uint64_t m, BpDigits dg, uint32_t* __restrict__ H1) {
-    __shared__ uint32_t lh[kBpMaxBins];
-    const uint64_t t0 = (uint64_t)blockIdx.x * kBpTile;
-    const uint32_t tn = (uint32_t)min<uint64_t>(kBpTile, m - t0);
-    for (uint32_t d = threadIdx.x; d < dg.nb1; d += kKeyThreads) lh[d] = 0;
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < tn; i += kKeyThreads) {
-        const unsigned long long x = in[t0 + i];
-        if (x != kNoKey) atomicAdd(&lh[(uint32_t)(x >> dg.sh1)], 1u);
-    }
-    __syncthreads();
-    for (uint32_t d = threadIdx.x; d < dg.nb1; d += kKeyThreads) H1[(uint64_t)blockIdx.x * dg.nb1 + d] = lh[d];
-}
-
-__global__ __launch_bounds__(kKeyThreads) void bp_scatter_arr_kernel(const unsigned long long* __restrict__ in,
-                                                                     uint64_t m, BpDigits dg,
-                                                                     const uint32_t* __restrict__ P1,
-                                                                     unsigned long long* __restrict__ out) {
-    __shared__ __attribute__((aligned(16))) unsigned long long S[kBpTile];
-    __shared__ uint32_t lh[kBpMaxBins];
-    __shared__ uint32_t wave_tot[kKeyThreads / 64];
-    __shared__ uint32_t s_n;
-    const uint64_t t0 = (uint64_t)blockIdx.x * kBpTile;
-    const uint32_t tn = (uint32_t)min<uint64_t>(kBpTile, m - t0);
-    for (uint32_t d = threadIdx.x; d < dg.nb1; d += kKeyThreads) lh[d] = 0;
-    if (threadIdx.x == 0) s_n = 0;
-    __syncthreads();
-    unsigned long long x[kBpPer];
-    uint32_t r[kBpPer], nk = 0;
-    auto digit = [&](unsigned long long y) { return (uint32_t)(y >> dg.sh1); };
-#pragma unroll
-    for (uint32_t e = 0; e < kBpPer; ++e) {
-        const uint32_t i = threadIdx.x + e * kKeyThreads;
-        x[e] = i < tn ? in[t0 + i] : kNoKey;
-        r[e] = x[e] != kNoKey ? atomicAdd(&lh[digit(x[e])], 1u) : 0u;
-        nk += x[e] != kNoKey;
-    }
-    if (nk) atomicAdd(&s_n, nk);
-    __syncthreads();
-    bp_place(x, r, s_n, dg.nb1, digit, lh, wave_tot, S, P1 + (uint64_t)blockIdx.x * dg.nb1, out);
-}
-
 // the small bucket kernel for this layout: merged slot words when the bucket field is wide enough;
 // a 1,024-key capacity (four keys per thread) when the mean bucket is small enough that a bucket
 // above it is a > 4-sigma event (the large kernel takes those)
-#ifndef KMP_CAP1024_MEAN
-#define KMP_CAP1024_MEAN 800  // at config 3 (mean 897) the 1,280 variant measured faster
-#endif
-constexpr uint32_t kBucketCap1024Mean = KMP_CAP1024_MEAN;
-template <bool kPShard>
-void launch_bucket_small(uint32_t grid, hipStream_t st, const unsigned long long* sorted, const uint32_t* bstart,
-                         const Layout& lay, uint32_t n, int require_diff, uint32_t heavy_df,
-                         unsigned long long* out, uint64_t shard_cap, unsigned long long* cursor,
-                         unsigned long long* gstats, uint32_t* flags, uint32_t* list, uint32_t* list_count,
-                         const PShard& ps, uint32_t b0 = 0) {
-    if (lay.bbits >= kMergeMinBits && lay.mean_keys <= kBucketCap1024Mean)  // four keys per thread
-        bucket_small_kernel<1024, kBucketSmallThreads, kBucketSmallTab, kPShard, true>
-            <<<grid, kBucketSmallThreads, 0, st>>>(sorted, bstart, lay, n, require_diff, heavy_df, out, shard_cap,
-                                                   cursor, gstats, flags, list, list_count, ps, b0);
-    else if (lay.bbits >= kMergeMinBits)
-        bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallTab, kPShard, true>
-            <<<grid, kBucketSmallThreads, 0, st>>>(sorted, bstart, lay, n, require_diff, heavy_df, out, shard_cap,
-                                                   cursor, gstats, flags, list, list_count, ps, b0);
+constexpr uint32_t kBucketCap1024Mean = 800;  // at config 3 (mean 897) the 1,280 variant measured faster
+template <bool kRows>
+void launch_buckets(const BucketArgs& a, uint32_t nb, hipStream_t st) {
+    if (a.lay.bbits >= kMergeMinBits && a.lay.mean_keys <= kBucketCap1024Mean)  // four keys per thread
+        bucket_small_kernel<1024, kBucketSmallThreads, kBucketSmallTab, true, kRows>
+            <<<nb, kBucketSmallThreads, 0, st>>>(a, 0u);
+    else if (a.lay.bbits >= kMergeMinBits)
+        bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallTab, true, kRows>
+            <<<nb, kBucketSmallThreads, 0, st>>>(a, 0u);
     else
-        bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallTab, kPShard, false>
-            <<<grid, kBucketSmallThreads, 0, st>>>(sorted, bstart, lay, n, require_diff, heavy_df, out, shard_cap,
-                                                   cursor, gstats, flags, list, list_count, ps, b0);
+        bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallTab, false, kRows>
+            <<<nb, kBucketSmallThreads, 0, st>>>(a, 0u);
+    bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeTab, kRows>
+        <<<kBucketLargeGrid, kBucketLargeThreads, 0, st>>>(a);
 }
-
 
 // (pair key, w) runs -> edges with w >= min_shared, canonical order kept
 __global__ void emit_edges_kernel(const unsigned long long* __restrict__ uniq, const uint32_t* __restrict__ w,
@@ -1633,67 +1582,59 @@ struct Grow {
 
 }  // namespace
 
-constexpr uint32_t kPipeMax = 16;  // coarse-bin chunks of the pipelined fused step, at most
-
 struct kmp_postings {
     Grow<unsigned long long> keys, sorted, inc, inc_sorted, uniq, bstats, btot, boff;
-    Grow<uint32_t> w, keep, pos, small, cnt, flags;  // flags: [0] bucket overflow, [1] class width, [2] list count
+    Grow<uint32_t> w, keep, pos, small, cnt, flags;  // flags: see kFl*
     Grow<char> tmp;
     bool timing = false;
     bool bucketed = true;       // try the bucketed layout first
     bool last_bucketed = false; // layout the last call ran on
-    bool last_pshard = false;   // ... and whether it finished with the p-shard tail
-    bool last_fused = false;    // ... or with the single-synchronisation bucketed path
-    bool last_rows = false;     // ... whose pair keys went through the row-block tail
-    uint64_t shard_cap = 0;     // bucketed: capacity of each output shard region
-    uint64_t ps_cap = 0;        // p-shard: keys per row-range region
-    bool ps_ok = false;         // the last bucketed front end left its keys in row-range regions
-    bool pshard = false;        // use the p-shard tail when the row ranges fit (opt-in: slower)
-    PShard ps{};
-    Grow<uint32_t> ps_cursor, e3, ecnt, chunk_first;
-    Grow<unsigned long long> eoff;
+    bool last_fused = false;    // ... single-synchronisation step (else the split step)
+    bool last_heavy = false;    // ... with spilled frequent k-mers
+    uint32_t last_ovf = 0;      // ... row blocks finished by the overflow sort
+    uint64_t shard_cap = 0;     // capacity of each pair-key shard region
+    Grow<uint32_t> chunk_first;
     Grow<uint32_t> bp;          // bucket partition: H1 | P1 | R | C1 | H2 (see bp_level1)
     Grow<uint32_t> pt;          // row-block tail (pt_bufs)
-    bool pt_on = !getenv("KMP_ROWTAIL") || atoi(getenv("KMP_ROWTAIL")) != 0;  // fused step: row-block tail
-    uint64_t pt_inc = 0;        // incidences of the last fused call (row-block sizing)
+    Grow<uint32_t> ovf;         // listed row blocks | segment starts | segment ends
+    Grow<uint32_t> ks;          // their keys, sorted
+    uint64_t pt_inc = 0;        // incidences of the last call (row-block sizing)
     unsigned pt_rb_max = 16;    // rows-per-block bound learned from overflowing row blocks
-    // row-block tail: rank sort inside short rows instead of the block radix sort (opt-in,
-    // KMP_PT_RANK=1: measured slower)
-    uint32_t pt_rank = getenv("KMP_PT_RANK") && atoi(getenv("KMP_PT_RANK")) != 0;
-    uint32_t bp_J = 0;          // level-2 tiles per coarse bin
+    uint32_t bp_J = 0;          // level-2 tiles per coarse bin ...
+    uint32_t bp_J_min = 0;      // ... at least (learned from an overflowing bin)
     uint64_t bp_c1 = 0;         // offset of C1 (coarse bin starts) in ws->bp
-    bool partition = !getenv("KMP_PARTITION") || atoi(getenv("KMP_PARTITION")) != 0;  // residue keys: counting partition
     bool parted = false;        // ws->keys holds level-1 output (bp_level1 ran for this call)
-    // fused residue step as a HIP graph: captured on the second call with the same shape
+    // heavy path (frequent k-mers): spill regions, the gathered + sorted spill, its elements,
+    // k-mer starts, per-k-mer row bounds / tile counts / tile offsets
+    Grow<unsigned long long> spill, hkeys, hsorted, hGS, htc, htoff, hoff;
+    Grow<uint32_t> hE, hgi, hcnt;
+    uint64_t spill_cap = 0;     // keys per spill shard region
+    bool heavy = false;         // this workspace's batches spill: run the split step
+    bool heavy_ready = false;   // hE / hGS hold the current front's compacted spill
+    uint64_t h_ne = 0, h_ng = 0;
+    std::vector<unsigned long long> shape;  // (n, slots, code bits, bucket bits) of the last batch
+    // single-synchronisation step as a HIP graph: captured on the second call with the same shape
     // (every buffer already sized), replayed after that
-    bool graph_on = !getenv("KMP_GRAPH") || atoi(getenv("KMP_GRAPH")) != 0;
+    bool graph_on = true;
     hipGraphExec_t gexec = nullptr;
     hipStream_t cst = nullptr;  // capture stream
     std::vector<unsigned long long> gkey, gkey_seen;
     uint64_t graph_replays = 0;
-    // fused step: level 2 and the bucket kernels pipelined over pipe_k coarse-bin chunks on a
-    // second stream (1 = serial, the default: pipelining measured slower)
-    int pipe_k = getenv("KMP_PIPE") ? atoi(getenv("KMP_PIPE")) : 1;
-    hipStream_t pst = nullptr;
-    hipEvent_t pev[kPipeMax + 2] = {};
-    // read-back of the fused step (kRbWords: gstats | cursors | flags | run count | largest row
-    // block), written by fused_pack_kernel into coherent pinned host memory
+    // read-back of a step (kRb* layout), written by the pack kernel into coherent pinned memory
     unsigned long long* hrb = nullptr;
-    int ablate = getenv("KMP_BUCKET_ABLATE") ? atoi(getenv("KMP_BUCKET_ABLATE")) : 0;  // diagnostics
     hipEvent_t ev[KMP_POSTINGS_STAGES + 1] = {};
     ~kmp_postings() {
-        keys.release(); sorted.release(); inc.release(); inc_sorted.release(); uniq.release();
-        bstats.release(); btot.release(); boff.release();
-        w.release(); keep.release(); pos.release(); small.release(); cnt.release(); flags.release(); tmp.release();
-        ps_cursor.release(); e3.release(); ecnt.release(); eoff.release(); chunk_first.release(); bp.release(); pt.release();
+        for (auto* g : {&keys, &sorted, &inc, &inc_sorted, &uniq, &bstats, &btot, &boff, &spill, &hkeys, &hsorted,
+                        &hGS, &htc, &htoff, &hoff})
+            g->release();
+        for (auto* g : {&w, &keep, &pos, &small, &cnt, &flags, &chunk_first, &bp, &pt, &ovf, &ks, &hE, &hgi, &hcnt})
+            g->release();
+        tmp.release();
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
         if (hrb) (void)hipHostFree(hrb);
         if (gexec) (void)hipGraphExecDestroy(gexec);
         if (cst) (void)hipStreamDestroy(cst);
-        for (auto& e : pev)
-            if (e) (void)hipEventDestroy(e);
-        if (pst) (void)hipStreamDestroy(pst);
     }
     void mark(int stage, hipStream_t st) {
         if (timing) (void)hipEventRecord(ev[stage], st);
@@ -1728,7 +1669,7 @@ hipError_t bp_level1(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_r
     if (G64 * dg.nb1 > 0xFFFFFFFFull || slots > 0xFFFFFFFFull) return hipErrorInvalidValue;
     const uint32_t G = (uint32_t)G64, groups = (G + kBpRowGroup - 1) / kBpRowGroup;
     // coarse bins are hash-uniform: a budget of 1.25x the mean plus two tiles
-    ws->bp_J = (uint32_t)((slots / dg.nb1 * 5 / 4 + kBpTile - 1) / kBpTile) + 2;
+    ws->bp_J = std::max(ws->bp_J_min, (uint32_t)((slots / dg.nb1 * 5 / 4 + kBpTile - 1) / kBpTile) + 2);
     const uint64_t h1 = (uint64_t)G * dg.nb1, r = (uint64_t)groups * dg.nb1;
     const uint64_t need = 2 * h1 + r + 2 * (dg.nb1 + 1) + (uint64_t)dg.nb1 * ws->bp_J * dg.nb2;
     hipError_t e = ws->bp.reserve(need);
@@ -1749,43 +1690,16 @@ hipError_t bp_level1(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_r
     return hipGetLastError();
 }
 
-// Level 1 from a key array of m entries (kNoKey padding skipped) -> ws->keys, C1 for level 2.
-// The keys fall in `bins` of the nb1 coarse bins (a multi-GPU owner holds only its bucket
-// range), which sets level 2's tile budget per bin.
-hipError_t bp_level1_array(kmp_postings* ws, const unsigned long long* d_keys, uint64_t m, const Layout& lay,
-                           uint32_t bins, hipStream_t st) {
-    const BpDigits dg = bp_digits(lay);
-    const uint64_t T64 = (m + kBpTile - 1) / kBpTile;
-    if (T64 * dg.nb1 > 0xFFFFFFFFull || m > 0xFFFFFFFFull) return hipErrorInvalidValue;
-    const uint32_t T = (uint32_t)T64, groups = (T + kBpRowGroup - 1) / kBpRowGroup;
-    bins = std::max(1u, std::min(bins, dg.nb1));
-    ws->bp_J = (uint32_t)((m / bins * 5 / 4 + kBpTile - 1) / kBpTile) + 2;
-    const uint64_t h1 = (uint64_t)T * dg.nb1, r = (uint64_t)groups * dg.nb1;
-    const uint64_t need = 2 * h1 + r + 2 * (dg.nb1 + 1) + (uint64_t)dg.nb1 * ws->bp_J * dg.nb2;
-    hipError_t e = ws->bp.reserve(need);
-    if (e == hipSuccess) e = ws->keys.reserve(m + (uint64_t)kBpAlign * dg.nb1);
-    if (e != hipSuccess) return e;
-    uint32_t *H1 = ws->bp.p, *P1 = H1 + h1, *R = P1 + h1, *C1 = R + r;
-    ws->bp_c1 = 2 * h1 + r;
-    bp_hist_arr_kernel<<<T, kKeyThreads, 0, st>>>(d_keys, m, dg, H1);
-    bp_colsum_kernel<<<dim3(groups, (dg.nb1 + 255) / 256), 256, 0, st>>>(H1, T, dg.nb1, R);
-    bp_colscan_kernel<<<1, kColThreads, 0, st>>>(R, groups, dg.nb1, C1);
-    bp_colprefix_kernel<<<dim3(groups, (dg.nb1 + 255) / 256), 256, 0, st>>>(H1, T, dg.nb1, R, P1);
-    bp_scatter_arr_kernel<<<T, kKeyThreads, 0, st>>>(d_keys, m, dg, P1, ws->keys.p);
-    return hipGetLastError();
-}
-
 // Level 2: ws->keys (level 1) -> ws->sorted grouped by bucket, bstart[0..nb] in ws->cnt.
-int bp_level2(kmp_postings* ws, const Layout& lay, hipStream_t st, uint32_t c0 = 0, uint32_t bins = 0) {
+int bp_level2(kmp_postings* ws, const Layout& lay, hipStream_t st) {
     const BpDigits dg = bp_digits(lay);
     uint32_t* C1 = ws->bp.p + ws->bp_c1;
     uint32_t* H2 = C1 + 2 * (dg.nb1 + 1);
     const uint32_t nb = 1u << lay.bbits, J = ws->bp_J;
-    if (bins == 0) bins = dg.nb1 - c0;  // coarse bins [c0, c0 + bins)
     PG(ws->cnt.reserve(2 * (uint64_t)nb + 2));
-    bp_hist2_kernel<<<dim3(J, bins), kKeyThreads, 0, st>>>(ws->keys.p, C1, J, dg, H2, c0);
-    bp_scan2_kernel<<<bins, kKeyThreads, 0, st>>>(H2, C1, J, dg, ws->cnt.p, ws->flags.p, c0);
-    bp_scatter2_kernel<<<dim3(J, bins), kKeyThreads, 0, st>>>(ws->keys.p, C1, J, dg, H2, ws->sorted.p, c0);
+    bp_hist2_kernel<<<dim3(J, dg.nb1), kKeyThreads, 0, st>>>(ws->keys.p, C1, J, dg, H2, 0u);
+    bp_scan2_kernel<<<dg.nb1, kKeyThreads, 0, st>>>(H2, C1, J, dg, ws->cnt.p, ws->flags.p, 0u);
+    bp_scatter2_kernel<<<dim3(J, dg.nb1), kKeyThreads, 0, st>>>(ws->keys.p, C1, J, dg, H2, ws->sorted.p, 0u);
     PG(hipGetLastError());
     return KMP_OK;
 }
@@ -1870,199 +1784,21 @@ int front_flat(kmp_postings* ws, uint64_t slots, const Layout& lay, const uint16
     return KMP_OK;
 }
 
-// p-shard geometry for n proteins: rows per shard 2^row_bits (<= kReduceRowsMax), q < 2^24
-bool pshard_geometry(uint32_t n, unsigned* row_bits, uint32_t* n_shards) {
-    if (n >= (1u << 24)) return false;
-    const unsigned pb = bits_for(n);
-    const unsigned r = pb > 12 ? std::min(8u, pb - 12) : 0u;
-    *row_bits = r;
-    *n_shards = (n + (1u << r) - 1) >> r;
-    return true;
-}
-
-// Bucketed front end (keys `in`, flags[0..1] written by the key kernel): sort on the bucket
-// field, bucket bounds, LDS group + expand per bucket.  Output modes:
-//   pshard == false: pair keys p*N+q into kShards regions, gathered into ws->inc (*n_inc keys);
-//   pshard == true:  pair keys p<<32|q into the row-range regions of ws->ps (ws->ps_ok tells
-//                    whether every range fit; if not the caller uses pshard == false).
-// Marks 2 (sort), 3 (group + expand), 4 (gather).  *fallback = true when a bucket does not fit
-// or a class id is too wide (the caller reruns on the flat layout).
-int front_bucketed(kmp_postings* ws, const unsigned long long* in, uint64_t slots, const Layout& lay, uint32_t n,
-                   uint32_t heavy_df, int require_class_diff, bool pshard, unsigned long long* n_inc,
-                   bool* fallback, kmp_postings_stats* stats, hipStream_t st) {
-    *fallback = false;
-    ws->ps_ok = false;
-    const uint32_t nb = 1u << lay.bbits;
-    {
-        int rc = bucket_group(ws, in, slots, lay, st);  // bucket starts + room for the large-bucket list
-        if (rc != KMP_OK) return rc;
-    }
-    PG(ws->bstats.reserve(std::max<uint64_t>(ws->bstats.n, kShards * 8 + kShards)));
-    uint32_t* bstart = ws->cnt.p;
-    uint32_t* list = ws->cnt.p + nb + 1;
-    uint32_t* list_count = ws->flags.p + 2;
-    uint32_t* flags = ws->flags.p;
-    unsigned long long* gstats = ws->bstats.p;          // kShards x 8 (kSt* slots)
-    unsigned long long* cursor = gstats + kShards * 8;  // kShards
-    PShard ps{};
-    if (pshard) {
-        if (!pshard_geometry(n, &ps.row_bits, &ps.n_shards)) pshard = false;
-    }
-    if (pshard) {
-        if (ws->ps_cap == 0) ws->ps_cap = std::min<uint64_t>(kReduceCap, slots / 4 / ps.n_shards + 256);
-        PG(ws->ps_cursor.reserve(ps.n_shards));
-        ps.cursor = ws->ps_cursor.p;
-    } else if (ws->shard_cap == 0) {
-        ws->shard_cap = slots / 2 / kShards + 4096;
-    }
-    for (int attempt = 0; attempt < 3; ++attempt) {
-        if (pshard) {
-            ps.cap = ws->ps_cap;
-            PG(ws->inc_sorted.reserve(ps.cap * ps.n_shards));  // row-range regions
-            ps.region = ws->inc_sorted.p;
-            PG(hipMemsetAsync(ps.cursor, 0, ps.n_shards * sizeof(uint32_t), st));
-        } else {
-            PG(ws->inc_sorted.reserve(ws->shard_cap * kShards));  // shard regions
-        }
-        PG(hipMemsetAsync(gstats, 0, (kShards * 8 + kShards) * sizeof(unsigned long long), st));
-        PG(hipMemsetAsync(list_count, 0, sizeof(uint32_t), st));
-        if (pshard) {
-            launch_bucket_small<true>(nb, st, ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df, ws->inc_sorted.p, ws->shard_cap, cursor, gstats, flags, list, list_count, ps);
-            bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeTab, true>
-                <<<256, kBucketLargeThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
-                                                      ws->inc_sorted.p, ws->shard_cap, cursor, gstats, flags, list,
-                                                      list_count, ps);
-        } else {
-            launch_bucket_small<false>(nb, st, ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df, ws->inc_sorted.p, ws->shard_cap, cursor, gstats, flags, list, list_count, ps);
-            bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeTab, false>
-                <<<256, kBucketLargeThreads, 0, st>>>(ws->sorted.p, bstart, lay, n, require_class_diff, heavy_df,
-                                                      ws->inc_sorted.p, ws->shard_cap, cursor, gstats, flags, list,
-                                                      list_count, ps);
-        }
-        ws->mark(3, st);
-        unsigned long long g[kShards * 8 + kShards];
-        uint32_t h_flags[2] = {0, 0};
-        PG(hipMemcpyAsync(g, gstats, sizeof g, hipMemcpyDeviceToHost, st));
-        PG(hipMemcpyAsync(h_flags, flags, sizeof h_flags, hipMemcpyDeviceToHost, st));
-        std::vector<uint32_t> pc;
-        if (pshard) {
-            pc.resize(ps.n_shards);
-            PG(hipMemcpyAsync(pc.data(), ps.cursor, ps.n_shards * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-        }
-        PG(hipStreamSynchronize(st));
-        if (h_flags[0] || h_flags[1]) {
-            if (getenv("KMP_DEBUG")) {
-                std::vector<uint32_t> bs(nb + 1);
-                (void)hipMemcpy(bs.data(), bstart, (nb + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost);
-                uint32_t mx = 0;
-                for (uint32_t b = 0; b < nb; ++b) mx = std::max(mx, bs[b + 1] - bs[b]);
-                fprintf(stderr, "kmp: bucketed -> flat (bucket/sub-bucket overflow %u, class width %u; nb %u, "
-                        "largest bucket %u, keys %u of %llu slots, sort bits [%u,%u))\n", h_flags[0], h_flags[1], nb,
-                        mx, bs[nb], (unsigned long long)slots, lay.sort_lo, lay.sort_hi);
-            }
-            *fallback = true;
-            return KMP_OK;
-        }
-        unsigned long long acc[kStN + kShards] = {};
-        for (int sh = 0; sh < kShards; ++sh) {
-            for (int t = 0; t < kStN; ++t)
-                acc[t] = t == kStMaxDf ? std::max(acc[t], g[sh * 8 + t]) : acc[t] + g[sh * 8 + t];
-            acc[kStN + sh] = g[kShards * 8 + sh];
-        }
-        fill_stats(stats, acc);
-        *n_inc = acc[kStInc];
-        if (pshard && getenv("KMP_DEBUG")) {
-            uint32_t most = pc.empty() ? 0u : *std::max_element(pc.begin(), pc.end());
-            fprintf(stderr, "kmp: p-shard attempt %d: shards %u cap %llu most %u\n", attempt, ps.n_shards,
-                    (unsigned long long)ps.cap, most);
-        }
-        if (pshard) {
-            const uint32_t most = pc.empty() ? 0u : *std::max_element(pc.begin(), pc.end());
-            if (most <= ps.cap) {
-                ws->ps_ok = true;
-                ws->ps = ps;
-                ws->mark(4, st);
-                return KMP_OK;
-            }
-            if (most > (uint32_t)kReduceCap) {  // a row range too large for LDS: key-sort tail
-                pshard = false;
-                if (ws->shard_cap == 0) ws->shard_cap = slots / 2 / kShards + 4096;
-                continue;
-            }
-            ws->ps_cap = std::min<uint64_t>(kReduceCap, most + most / 4 + 64);  // grow, rerun
-            continue;
-        }
-        unsigned long long most = 0;
-        for (int s = 0; s < kShards; ++s) most = std::max(most, acc[kStN + s]);
-        if (most <= ws->shard_cap) {
-            if (*n_inc > 0xFFFFFFFFull) return KMP_ENOMEM;
-            PG(ws->inc.reserve(std::max<unsigned long long>(1, *n_inc)));
-            if (*n_inc) {
-                const uint32_t gx = (uint32_t)std::min<uint64_t>((most + 255) / 256, 1024);
-                gather_shards_kernel<<<dim3(gx, kShards), 256, 0, st>>>(ws->inc_sorted.p, ws->shard_cap, cursor,
-                                                                        ws->inc.p);
-            }
-            ws->mark(4, st);
-            return KMP_OK;
-        }
-        ws->shard_cap = most + most / 4 + 4096;  // grow the regions and rerun the expansion
-    }
-    return KMP_EDEVICE;
-}
-
-// p-shard tail: LDS reduce per row range, offsets, compaction.  Marks 5 (reduce), 6 (emit).
-int tail_pshard(kmp_postings* ws, uint32_t min_shared, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w, uint64_t cap,
-                uint64_t* n_edges, kmp_postings_stats* stats, hipStream_t st) {
-    const PShard& ps = ws->ps;
-    const uint32_t S = ps.n_shards;
-    PG(ws->e3.reserve(3 * ps.cap * S));
-    PG(ws->ecnt.reserve(2 * (uint64_t)S));
-    PG(ws->eoff.reserve(S));
-    uint32_t* ep = ws->e3.p;
-    uint32_t* eq = ep + ps.cap * S;
-    uint32_t* ew = eq + ps.cap * S;
-    uint32_t* ecount = ws->ecnt.p;
-    uint32_t* npairs = ws->ecnt.p + S;
-    shard_reduce_kernel<<<S, kReduceThreads, 0, st>>>(ps.region, ps.cursor, ps.cap, ps.row_bits, min_shared, ep, eq,
-                                                      ew, ecount, npairs);
-    size_t t_scan = 0;
-    PG(rocprim::exclusive_scan(nullptr, t_scan, ecount, ws->eoff.p, 0ull, (size_t)S,
-                               rocprim::plus<unsigned long long>(), st));
-    PG(ws->tmp.reserve(std::max(t_scan, ws->tmp.n)));
-    PG(rocprim::exclusive_scan(ws->tmp.p, t_scan, ecount, ws->eoff.p, 0ull, (size_t)S,
-                               rocprim::plus<unsigned long long>(), st));
-    ws->mark(5, st);
-    std::vector<uint32_t> h(2 * (size_t)S);
-    PG(hipMemcpyAsync(h.data(), ecount, 2 * (size_t)S * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    PG(hipStreamSynchronize(st));
-    uint64_t ne = 0, np = 0;
-    for (uint32_t s = 0; s < S; ++s) {
-        ne += h[s];
-        np += h[S + s];
-    }
-    if (stats) stats->pairs = np;
-    *n_edges = ne;
-    if (ne > cap) return KMP_EOVERFLOW;
-    if (ne) compact_edges_kernel<<<S, 256, 0, st>>>(ep, eq, ew, ps.cap, ecount, ws->eoff.p, d_p, d_q, d_w, cap);
-    ws->mark(6, st);
-    PG(hipGetLastError());
-    return KMP_OK;
-}
-
 // ------------------------------------------------------------- row-block tail -------------
-// combine_edges (mod.rs:322-546) for the fused step without a global pair-key sort.  Pair keys
-// are p << pbits | q (p < q); row block r = rows [r << rbits, (r + 1) << rbits).
-//   pt_hist     per 8,192-key tile of each shard region: row-block histogram -> H[tile][r]
+// combine_edges (mod.rs:322-546) without a global pair-key sort.  Pair keys are p << pbits | q
+// (p < q); row block r = rows [row0 + (r << rbits), row0 + ((r + 1) << rbits)).
+//   pt_hist     per 16,384-key tile of each shard region: row-block histogram -> H[tile][r]
 //   column scan (bp_colsum, pt_colscan, bp_colprefix) -> P[tile][r] and the block starts
 //   pt_scatter  per tile: keys ranked by row block in LDS and written as u32
 //               (p_local << pbits | q), one run per row block at P[tile][r]
 //   pt_reduce   one workgroup per row block: LDS radix sort of its keys (rocprim
-//               block_radix_sort), run-length encode (run = one (p, q) pair, length = w); runs
-//               staged at the block's input offset, run count per block
+//               block_radix_sort), run-length encode (run = one (p, q) pair, length = w), runs
+//               with w >= min_shared staged at the block's input offset, kept-run count per block
 //   pt_offsets  one workgroup: exclusive scan of the run counts -> edge offsets and the total
 //   pt_emit     one workgroup per row block: staged runs -> (d_p, d_q, d_w) at its offset
-// A row block above kPtCap keys (a protein pairing with thousands of later proteins) raises
-// flags[3]; the call then reruns on the global-sort tail.
+// A row block above kPtCap keys (a protein pairing with thousands of later proteins: real data
+// at k = 5) is listed instead; the host sorts the listed blocks with one segmented radix sort
+// and pt_ovf_rle encodes them (pt_finish_overflow), then offsets and emit run again.
 constexpr uint32_t kPtThreads = 1024, kPtPer = 16, kPtTile = kPtThreads * kPtPer;  // partition tiles: 16,384 keys
 constexpr uint32_t kPtRThreads = 512, kPtCap = 8192;  // pt_reduce: up to 16 keys per thread
 constexpr uint32_t kPtMaxBlocks = 8192;  // row blocks (LDS histogram of pt_hist / pt_scatter)
@@ -2073,9 +1809,9 @@ struct PtGeom {
     uint32_t jt;            // tiles per shard region
     uint64_t sc;            // shard region capacity
     uint32_t nshards;       // shard regions (kShards), or 1 for a flat array
-    uint32_t row0;          // first row (a multi-GPU owner's row range)
+    uint32_t row0;          // first row (a pass's or rank's row range)
     uint64_t flat_n;        // nonzero: one region of flat_n keys with kNoKey padding (no cursors)
-    uint32_t rank;          // pt_reduce: counting sort by row + rank sort in the row when rows are short
+    uint32_t min_shared;    // runs with w < min_shared are dropped
 };
 
 __device__ __forceinline__ uint32_t pt_tile_keys(const unsigned long long* __restrict__ cursor, const PtGeom& g,
@@ -2228,81 +1964,19 @@ __global__ __launch_bounds__(kPtThreads) void pt_scatter_kernel(const unsigned l
 template <uint32_t kE>
 using PtSort = rocprim::block_radix_sort<uint32_t, kPtRThreads, kE>;
 
-struct PtRuns {
-    uint32_t hs[kPtCap + 1];  // rank of each run's first key
-};
-struct PtRank {
-    __attribute__((aligned(16))) uint32_t B[kPtCap + 4];  // the block's keys grouped by row (+ padding)
-    __attribute__((aligned(16))) uint32_t A[kPtCap];      // ... sorted
-};
 union PtReduceLds {
     typename PtSort<2>::storage_type s2;
     typename PtSort<4>::storage_type s4;
     typename PtSort<8>::storage_type s8;
     typename PtSort<16>::storage_type s16;
-    PtRuns runs;
-    PtRank rk;
+    uint32_t hs[kPtCap + 1];  // rank of each run's first key
 };
-constexpr uint32_t kPtRankRows = 1024;   // rank sort: rows per block (LDS row cursors) ...
-constexpr uint32_t kPtRankRowMax = 512;  // ... and keys per row at most
 
-// Sort of a row block's keys for short rows (config 3: ~50 keys per row, 64 rows per block):
-// a counting sort by row (LDS cursors), then a rank sort inside each row, rank = the row's
-// smaller keys + its equal keys at earlier positions.  Rows are runs of B in row order, so
-// every key before the row is smaller and every key after it larger: each thread counts over
-// [row start rounded down to 4, row end) with 16-byte broadcast loads and subtracts the
-// earlier rows' keys.  O(row length) per key, against the three 8-bit passes of the block
-// radix sort.  On return k[] is blocked (thread t holds ranks t*kE + e, padding 0xFFFFFFFF) as
-// after the radix sort; false, with nothing written to s, when a row is longer than
-// kPtRankRowMax.
-template <uint32_t kE>
-__device__ __forceinline__ bool pt_rank_sort(PtRank& s, uint32_t* rc, uint32_t* wave_tot, uint32_t* s_big,
-                                             uint32_t (&k)[kE], uint32_t n, const PtGeom& g) {
-    const uint32_t nrows = 1u << g.rbits;
-    for (uint32_t t = threadIdx.x; t < nrows; t += kPtRThreads) rc[t] = 0;
-    if (threadIdx.x == 0) {
-        *s_big = 0;
-        rc[nrows] = n;
-    }
-    __syncthreads();
-    uint32_t rk[kE];
-#pragma unroll
-    for (uint32_t e = 0; e < kE; ++e)
-        rk[e] = threadIdx.x + e * kPtRThreads < n ? atomicAdd(&rc[k[e] >> g.pbits], 1u) : 0u;
-    __syncthreads();
-    for (uint32_t t = threadIdx.x; t < nrows; t += kPtRThreads)
-        if (rc[t] > kPtRankRowMax) *s_big = 1;
-    lds_bins_scan<kPtRThreads>(rc, nrows, wave_tot);  // ends with a barrier
-    if (*s_big) return false;
-#pragma unroll
-    for (uint32_t e = 0; e < kE; ++e)
-        if (threadIdx.x + e * kPtRThreads < n) s.B[rc[k[e] >> g.pbits] + rk[e]] = k[e];
-    if (threadIdx.x < 4) s.B[n + threadIdx.x] = 0xFFFFFFFFu;  // past the last row: larger than any key
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < n; i += kPtRThreads) {
-        const uint32_t v = s.B[i], row = v >> g.pbits, r0 = rc[row], r1 = rc[row + 1], j0 = r0 & ~3u;
-        uint32_t less = 0, eq = 0;
-        for (uint32_t j = j0; j < r1; j += 4) {
-            const uint4 x = *reinterpret_cast<const uint4*>(s.B + j);
-            less += (x.x < v) + (x.y < v) + (x.z < v) + (x.w < v);
-            eq += (x.x == v && j < i) + (x.y == v && j + 1 < i) + (x.z == v && j + 2 < i) + (x.w == v && j + 3 < i);
-        }
-        s.A[j0 + less + eq] = v;  // r0 + (less - (r0 - j0)) + eq
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t e = 0; e < kE; ++e) {
-        const uint32_t idx = threadIdx.x * kE + e;
-        k[e] = idx < n ? s.A[idx] : 0xFFFFFFFFu;
-    }
-    return true;
-}
-
-// row block r's n keys (n <= kE * kPtRThreads): sort, run-length encode, stage the runs
+// row block r's n keys (n <= kE * kPtRThreads): sort, run-length encode, stage the runs with
+// w >= min_shared
 template <uint32_t kE>
 __device__ __forceinline__ void pt_reduce_block(PtReduceLds& u, typename PtSort<kE>::storage_type& st,
-                                                uint32_t* last, uint32_t* wave_tot, uint32_t* rc, uint32_t* s_big,
-                                                const uint32_t* __restrict__ keys,
+                                                uint32_t* last, uint32_t* wave_tot, const uint32_t* __restrict__ keys,
                                                 uint32_t r, uint32_t s0, uint32_t n, const PtGeom& g,
                                                 uint32_t* __restrict__ stage_p, uint32_t* __restrict__ stage_q,
                                                 uint32_t* __restrict__ stage_w, uint32_t* __restrict__ counts) {
@@ -2312,9 +1986,8 @@ __device__ __forceinline__ void pt_reduce_block(PtReduceLds& u, typename PtSort<
         const uint32_t i = threadIdx.x + e * kPtRThreads;
         k[e] = i < n ? keys[s0 + i] : 0xFFFFFFFFu;
     }
-    // blocked: thread t holds ranks t*kE + e
-    if (!(g.rank && (1u << g.rbits) <= kPtRankRows && pt_rank_sort<kE>(u.rk, rc, wave_tot, s_big, k, n, g)))
-        PtSort<kE>().sort(k, st, 0, g.pbits + g.rbits);
+    // bits [0, pbits + rbits] (one above the key): the padding (all ones) sorts after every key
+    PtSort<kE>().sort(k, st, 0, g.pbits + g.rbits + 1);  // blocked: thread t holds ranks t*kE + e
     last[threadIdx.x] = k[kE - 1];
     __syncthreads();
     const uint32_t rank0 = threadIdx.x * kE;
@@ -2329,28 +2002,64 @@ __device__ __forceinline__ void pt_reduce_block(PtReduceLds& u, typename PtSort<
     }
     uint32_t base, nruns;
     block_scan_n<kPtRThreads>(nh, base, nruns, wave_tot);  // barriers: the sort storage is dead
-    // heads write (p, q) from registers; w = the distance to the next run's first rank
     const uint32_t qm = (1u << g.pbits) - 1;
+    const uint32_t rowbase = g.row0 + (r << g.rbits);
+    if (g.min_shared <= 1) {
+        // heads write (p, q) from registers; w = the distance to the next run's first rank
+#pragma unroll
+        for (uint32_t e = 0; e < kE; ++e)
+            if (head[e]) {
+                u.hs[base] = rank0 + e;
+                stage_p[s0 + base] = rowbase + (k[e] >> g.pbits);
+                stage_q[s0 + base] = k[e] & qm;
+                ++base;
+            }
+        if (threadIdx.x == 0) {
+            u.hs[nruns] = n;
+            counts[r] = nruns;
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < nruns; i += kPtRThreads) stage_w[s0 + i] = u.hs[i + 1] - u.hs[i];
+        return;
+    }
+    // min_shared > 1: run keys staged in stage_p, then thread t keeps runs [t*kE, t*kE + kE) with
+    // w >= min_shared, in order (every read lands before the scan's barriers, every write after)
 #pragma unroll
     for (uint32_t e = 0; e < kE; ++e)
         if (head[e]) {
-            u.runs.hs[base] = rank0 + e;
-            stage_p[s0 + base] = g.row0 + ((r << g.rbits) | (k[e] >> g.pbits));
-            stage_q[s0 + base] = k[e] & qm;
+            u.hs[base] = rank0 + e;
+            stage_p[s0 + base] = k[e];
             ++base;
         }
-    if (threadIdx.x == 0) {
-        u.runs.hs[nruns] = n;
-        counts[r] = nruns;
-    }
+    if (threadIdx.x == 0) u.hs[nruns] = n;
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < nruns; i += kPtRThreads) stage_w[s0 + i] = u.runs.hs[i + 1] - u.runs.hs[i];
+    uint32_t kv[kE], wv[kE], kept = 0;
+#pragma unroll
+    for (uint32_t e = 0; e < kE; ++e) {
+        const uint32_t rr = rank0 + e;
+        wv[e] = rr < nruns ? u.hs[rr + 1] - u.hs[rr] : 0u;
+        kv[e] = rr < nruns ? stage_p[s0 + rr] : 0u;
+        kept += wv[e] >= g.min_shared;
+    }
+    uint32_t o, total;
+    block_scan_n<kPtRThreads>(kept, o, total, wave_tot);
+#pragma unroll
+    for (uint32_t e = 0; e < kE; ++e)
+        if (wv[e] >= g.min_shared) {
+            stage_p[s0 + o] = rowbase + (kv[e] >> g.pbits);
+            stage_q[s0 + o] = kv[e] & qm;
+            stage_w[s0 + o] = wv[e];
+            ++o;
+        }
+    if (threadIdx.x == 0) counts[r] = total;
 }
 
-// one workgroup per row block; the sort width follows the block's size
+// one workgroup per row block; the sort width follows the block's size.  A block above kPtCap
+// is listed in ovf (count in flags[3]) for pt_finish_overflow.
 __global__ __launch_bounds__(kPtRThreads) void pt_reduce_kernel(const uint32_t* __restrict__ keys,
                                                                 const uint32_t* __restrict__ bst, PtGeom g,
                                                                 uint32_t* __restrict__ flags,
+                                                                uint32_t* __restrict__ ovf,
                                                                 uint32_t* __restrict__ stage_p,
                                                                 uint32_t* __restrict__ stage_q,
                                                                 uint32_t* __restrict__ stage_w,
@@ -2358,25 +2067,78 @@ __global__ __launch_bounds__(kPtRThreads) void pt_reduce_kernel(const uint32_t* 
     __shared__ PtReduceLds u;
     __shared__ uint32_t last[kPtRThreads];
     __shared__ uint32_t wave_tot[kPtRThreads / 64];
-    __shared__ uint32_t rc[kPtRankRows + 1];
-    __shared__ uint32_t s_big;
     const uint32_t r = blockIdx.x, s0 = bst[r], n = bst[r + 1] - s0;
     if (n == 0 || n > kPtCap) {
         if (threadIdx.x == 0) {
             counts[r] = 0;
-            if (n) flags[3] = 1;
+            if (n) ovf[atomicAdd(&flags[3], 1u)] = r;
         }
         return;
     }
     if (n <= 2 * kPtRThreads)
-        pt_reduce_block<2>(u, u.s2, last, wave_tot, rc, &s_big, keys, r, s0, n, g, stage_p, stage_q, stage_w, counts);
+        pt_reduce_block<2>(u, u.s2, last, wave_tot, keys, r, s0, n, g, stage_p, stage_q, stage_w, counts);
     else if (n <= 4 * kPtRThreads)
-        pt_reduce_block<4>(u, u.s4, last, wave_tot, rc, &s_big, keys, r, s0, n, g, stage_p, stage_q, stage_w, counts);
+        pt_reduce_block<4>(u, u.s4, last, wave_tot, keys, r, s0, n, g, stage_p, stage_q, stage_w, counts);
     else if (n <= 8 * kPtRThreads)
-        pt_reduce_block<8>(u, u.s8, last, wave_tot, rc, &s_big, keys, r, s0, n, g, stage_p, stage_q, stage_w, counts);
+        pt_reduce_block<8>(u, u.s8, last, wave_tot, keys, r, s0, n, g, stage_p, stage_q, stage_w, counts);
     else
-        pt_reduce_block<16>(u, u.s16, last, wave_tot, rc, &s_big, keys, r, s0, n, g, stage_p, stage_q, stage_w,
-                            counts);
+        pt_reduce_block<16>(u, u.s16, last, wave_tot, keys, r, s0, n, g, stage_p, stage_q, stage_w, counts);
+}
+
+// segment bounds of the listed (overflowing) row blocks, for the segmented sort
+__global__ void pt_ovf_segments_kernel(const uint32_t* __restrict__ ovf, uint32_t m, const uint32_t* __restrict__ bst,
+                                       uint32_t* __restrict__ sb, uint32_t* __restrict__ se) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    sb[i] = bst[ovf[i]];
+    se[i] = bst[ovf[i] + 1];
+}
+
+// one workgroup per listed block, its keys already sorted in ks: run starts into tmp (the
+// block's unsorted input, dead after the sort), then the runs with w >= min_shared staged
+constexpr uint32_t kOvfThreads = 1024;
+__global__ __launch_bounds__(kOvfThreads) void pt_ovf_rle_kernel(const uint32_t* __restrict__ ovf,
+                                                                 const uint32_t* __restrict__ bst, PtGeom g,
+                                                                 const uint32_t* __restrict__ ks,
+                                                                 uint32_t* __restrict__ tmp,
+                                                                 uint32_t* __restrict__ stage_p,
+                                                                 uint32_t* __restrict__ stage_q,
+                                                                 uint32_t* __restrict__ stage_w,
+                                                                 uint32_t* __restrict__ counts) {
+    __shared__ uint32_t wave_tot[kOvfThreads / 64];
+    const uint32_t r = ovf[blockIdx.x], s0 = bst[r], n = bst[r + 1] - s0;
+    uint32_t runs = 0;
+    for (uint32_t c = 0; c < n; c += kOvfThreads) {
+        const uint32_t i = c + threadIdx.x;
+        const bool h = i < n && (i == 0 || ks[s0 + i] != ks[s0 + i - 1]);
+        uint32_t x, t;
+        block_scan_n<kOvfThreads>(h, x, t, wave_tot);
+        if (h) tmp[s0 + runs + x] = i;
+        runs += t;
+    }
+    __syncthreads();
+    const uint32_t qm = (1u << g.pbits) - 1;
+    const uint32_t rowbase = g.row0 + (r << g.rbits);
+    uint32_t kept = 0;
+    for (uint32_t c = 0; c < runs; c += kOvfThreads) {
+        const uint32_t j = c + threadIdx.x;
+        uint32_t w = 0, key = 0;
+        if (j < runs) {
+            const uint32_t a = tmp[s0 + j];
+            w = (j + 1 < runs ? tmp[s0 + j + 1] : n) - a;
+            key = ks[s0 + a];
+        }
+        const bool keep = j < runs && w >= g.min_shared;
+        uint32_t x, t;
+        block_scan_n<kOvfThreads>(keep, x, t, wave_tot);
+        if (keep) {
+            stage_p[s0 + kept + x] = rowbase + (key >> g.pbits);
+            stage_q[s0 + kept + x] = key & qm;
+            stage_w[s0 + kept + x] = w;
+        }
+        kept += t;
+    }
+    if (threadIdx.x == 0) counts[r] = kept;
 }
 
 // exclusive scan of the nrb run counts (nrb <= 8 * 1024) -> eoff; eoff[nrb] and *total = edges
@@ -2425,60 +2187,83 @@ __global__ __launch_bounds__(256) void pt_emit_kernel(const uint32_t* __restrict
     }
 }
 
-// ------------------------------------------------------------- fused residue step ----------
-// Bucketed, min_shared == 1, one host synchronisation per call: keys, bucket grouping, group +
-// expand into the kShards regions, the regions' unused tails padded with kNoKey, one radix sort
-// of the whole padded buffer (its capacity is learned call to call, so it stays within a few %
-// of the incidence count), run-length encode, emit, and ONE read-back of statistics, shard
-// counts, flags and the run count.  fused_enqueue issues all of it with no host wait, so it can
-// be captured as a HIP graph; run_fused replays that graph once the shape repeats.  A bucket that
-// does not fit -> *fallback (flat rerun); a shard region overflow -> grow and rerun.
-// Marks 0 (start), 1 (keys / level 1), 2 (bucket grouping), 3 (group + expand), 4 (pad),
-// 5 (pair sort), 6 (encode + emit + read-back).
-constexpr uint32_t kRbWords = kShards * 9 + 5;  // gstats (8 per shard) | cursors | flags[0..1] | runs | flags[3] | row-block max
+// ------------------------------------------------------------- the step --------------------
+// One call of the bucketed residue path (or of the set path: make_keys differs):
+//   front   keys (make_keys: the counting partition's level 1 for residues), level 2 / bucket
+//           sort, bucket kernels (group + expand, heavy groups spilled)
+//   heavy   the spilled frequent k-mers (heavy_phase; only when something spilled)
+//   tail    row-block tail into (d_p, d_q, d_w), canonical order
+// Fused step (nothing spilled, the usual case): all of it enqueued with no host wait and read
+// back once (one D2H of statistics, cursors, flags and the run count), captured as a HIP graph
+// from the second call of an unchanged shape and replayed after that.  Split step (the batch
+// spills, or the fused step found a spill): front, one read-back, heavy path, exact tail
+// geometry from the cursors, tail, read-back.  Overflowing buffers (shard regions, spill
+// regions, level-2 bins) grow to the measured need and the step reruns; row blocks above the
+// LDS capacity are finished by one segmented sort (pt_finish_overflow) without a rerun.
+// Marks 0 (start), 1 (keys / level 1), 2 (level 2), 3 (bucket kernels [+ heavy]), 4 (pair
+// partition), 5 (row-block sort + encode), 6 (emit + read-back).
+enum : uint32_t { kFlBin = 0, kFlClass = 1, kFlList = 2, kFlOvf = 3, kFlBinTiles = 4, kFlN = 8 };
+// read-back: gstats (8 per shard) | pair cursors | spill cursors | the words below
+enum : uint32_t {
+    kRbCursor = kShards * 8, kRbSpill = kShards * 9, kRbFlagBin = kShards * 10, kRbFlagClass, kRbRuns, kRbOvf,
+    kRbMaxBlock, kRbBinTiles, kRbWords
+};
+constexpr uint32_t kGsWords = kShards * 10;  // gstats | cursors | spill cursors (u64)
 
-__global__ void fused_clear_kernel(uint32_t* __restrict__ flags, unsigned long long* __restrict__ gstats) {
-    for (uint32_t i = threadIdx.x; i < kShards * 9; i += blockDim.x) gstats[i] = 0;
-    if (threadIdx.x < 4) flags[threadIdx.x] = 0;
+__global__ void step_clear_kernel(uint32_t* __restrict__ flags, unsigned long long* __restrict__ gstats) {
+    for (uint32_t i = threadIdx.x; i < kGsWords; i += blockDim.x) gstats[i] = 0;
+    if (threadIdx.x < kFlN) flags[threadIdx.x] = 0;
 }
 
-__global__ void fused_pack_kernel(const unsigned long long* __restrict__ gstats, const uint32_t* __restrict__ flags,
-                                  const uint32_t* __restrict__ runs, unsigned long long* __restrict__ rb) {
-    // runs[0]: run count; runs[1]: largest row block (row-block tail)
-    for (uint32_t i = threadIdx.x; i < kShards * 9; i += blockDim.x) rb[i] = gstats[i];
+__global__ void step_pack_kernel(const unsigned long long* __restrict__ gstats, const uint32_t* __restrict__ flags,
+                                 const uint32_t* __restrict__ runs, unsigned long long* __restrict__ rb) {
+    for (uint32_t i = threadIdx.x; i < kGsWords; i += blockDim.x) rb[i] = gstats[i];
     if (threadIdx.x == 0) {
-        rb[kShards * 9] = flags[0];
-        rb[kShards * 9 + 1] = flags[1];
-        rb[kShards * 9 + 2] = *runs;
-        rb[kShards * 9 + 3] = flags[3];
-        rb[kShards * 9 + 4] = runs[1];
+        rb[kRbFlagBin] = flags[kFlBin];
+        rb[kRbFlagClass] = flags[kFlClass];
+        rb[kRbRuns] = runs ? runs[0] : 0;
+        rb[kRbOvf] = flags[kFlOvf];
+        rb[kRbMaxBlock] = runs ? runs[1] : 0;
+        rb[kRbBinTiles] = flags[kFlBinTiles];
     }
     __threadfence_system();  // rb is host memory, read after the stream synchronises
 }
 
+// one call's parameters
+struct StepCfg {
+    uint64_t slots;
+    Layout lay;
+    uint32_t n, heavy_df, min_shared;
+    int require_diff;
+    bool ranged;              // pairs of rows [row_lo, row_hi) only
+    uint32_t row_lo, row_hi;
+    uint32_t *d_p, *d_q, *d_w;
+    uint64_t cap;
+    uint32_t stride;          // edge arrays' element stride (3: interleaved triples)
+};
+
 // row-block tail geometry: rows per block so that an average block holds about a quarter of
-// kPtCap keys (from the last call's incidence count, or a guess from the slots); false when the
-// tail does not apply (switched off, an earlier overflow, or keys wider than 32 bits)
-bool pt_geometry(const kmp_postings* ws, uint64_t slots, uint32_t n, PtGeom* g) {
-    if (!ws->pt_on) return false;
-    g->pbits = bits_for(n);
-    const uint64_t est = std::max<uint64_t>(1, ws->pt_inc ? ws->pt_inc : slots / 4);
-    // rows per block ~ (kPtCap / 2.4) * n / est, to the nearest power of two: an average block
+// kPtCap keys (from the expected incidence count)
+bool pt_geometry(const kmp_postings* ws, const StepCfg& c, uint64_t inc, PtGeom* g) {
+    g->pbits = bits_for(c.n);
+    const uint32_t rows = c.ranged ? c.row_hi - c.row_lo : c.n;
+    const uint64_t est = std::max<uint64_t>(1, inc);
+    // rows per block ~ (kPtCap / 2.4) * rows / est, to the nearest power of two: an average block
     // of 2.4-4.8K keys; the first rows (p is the smaller index) hold about twice the average
-    const double rows = (double)kPtCap / 2.4 * n / est;
+    const double want = (double)kPtCap / 2.4 * std::max<uint32_t>(rows, 1) / est;
     unsigned rb = 0;
-    while (rb < 16 && (double)(1u << rb) * 1.41421356 < rows) ++rb;
+    while (rb < 16 && (double)(1u << rb) * 1.41421356 < want) ++rb;
     rb = std::min(rb, ws->pt_rb_max);  // learned from overflowing blocks
-    while (rb < 16 && ((n + (1ull << rb) - 1) >> rb) > kPtMaxBlocks) ++rb;
-    if (g->pbits + rb > 32) return false;
+    while (rb < 31 && ((rows + (1ull << rb) - 1) >> rb) > kPtMaxBlocks) ++rb;
+    if (g->pbits + rb > 31) return false;  // the key and one padding bit in a u32
     g->rbits = rb;
-    g->nrb = (uint32_t)((n + (1ull << rb) - 1) >> rb);
+    g->nrb = std::max(1u, (uint32_t)((rows + (1ull << rb) - 1) >> rb));
     g->sc = ws->shard_cap;
     g->jt = (uint32_t)((g->sc + kPtTile - 1) / kPtTile);
     g->nshards = kShards;
-    g->row0 = 0;
+    g->row0 = c.ranged ? c.row_lo : 0;
     g->flat_n = 0;
-    g->rank = ws->pt_rank;
+    g->min_shared = std::max(1u, c.min_shared);
     return true;
 }
 
@@ -2502,148 +2287,229 @@ PtBufs pt_bufs(kmp_postings* ws, const PtGeom& g, bool reserve, hipError_t* e) {
     return b;
 }
 
-// buffers of one fused step (reserved before any launch, so a capture allocates nothing)
-int fused_reserve(kmp_postings* ws, uint64_t slots, const Layout& lay, uint32_t n) {
+BucketArgs bucket_args(kmp_postings* ws, const StepCfg& c, bool spill) {
+    BucketArgs a{};
+    const uint32_t nb = 1u << c.lay.bbits;
+    a.sorted = ws->sorted.p;
+    a.bstart = ws->cnt.p;
+    a.lay = c.lay;
+    a.mul = 1u << bits_for(c.n);  // pair key p << pbits | q (the row-block tail's key)
+    a.require_diff = c.require_diff;
+    a.heavy_df = c.heavy_df;
+    a.row_lo = c.ranged ? c.row_lo : 0;
+    a.row_hi = c.ranged ? c.row_hi : c.n;
+    a.out = ws->inc_sorted.p;
+    a.shard_cap = ws->shard_cap;
+    a.gstats = ws->bstats.p;
+    a.cursor = ws->bstats.p + kRbCursor;
+    a.flags = ws->flags.p;
+    a.list = ws->cnt.p + nb + 1;
+    a.list_count = ws->flags.p + kFlList;
+    a.spill = spill ? ws->spill.p : nullptr;
+    a.spill_cap = ws->spill_cap;
+    a.spill_cursor = ws->bstats.p + kRbSpill;
+    return a;
+}
+
+// buffers of one step (reserved before any launch, so a capture allocates nothing)
+int step_reserve(kmp_postings* ws, const StepCfg& c, const PtGeom& g) {
     const uint64_t total = ws->shard_cap * kShards;
-    const unsigned pair_bits = bits_for((uint64_t)n * n);
-    PG(ws->keys.reserve(slots));
-    PG(ws->sorted.reserve(slots));
-    PG(ws->flags.reserve(4));
-    PG(ws->cnt.reserve(2 * ((uint64_t)1 << lay.bbits) + 2));
-    PG(ws->bstats.reserve(std::max<uint64_t>(ws->bstats.n, kShards * 8 + kShards)));
+    PG(ws->keys.reserve(c.slots));
+    PG(ws->sorted.reserve(c.slots));
+    PG(ws->flags.reserve(kFlN));
+    PG(ws->cnt.reserve(2 * ((uint64_t)1 << c.lay.bbits) + 2));
+    PG(ws->bstats.reserve(kGsWords));
     PG(ws->small.reserve(16));  // [1] run count, [2] largest row block
     PG(ws->inc_sorted.reserve(total));
-    PG(ws->inc.reserve(total));
-    PG(ws->uniq.reserve(total));
-    PG(ws->w.reserve(total));
-    // coherent pinned memory: fused_pack_kernel writes the read-back straight into it (no copy)
+    PG(ws->inc.reserve(total));  // u32 row-block keys (pt_scatter) ...
+    PG(ws->uniq.reserve(total));  // ... staged p | q (u32 each)
+    PG(ws->w.reserve(total));     // ... staged w
+    PG(ws->spill.reserve(ws->spill_cap * kShards));
+    PG(ws->ovf.reserve(3 * (uint64_t)g.nrb + 3));
     if (!ws->hrb) PG(hipHostMalloc((void**)&ws->hrb, kRbWords * sizeof(unsigned long long), hipHostMallocCoherent));
-    PtGeom g;
-    if (pt_geometry(ws, slots, n, &g)) {  // the row-block tail: no rocprim scratch to size
-        hipError_t e = hipSuccess;
-        pt_bufs(ws, g, true, &e);
-        PG(e);
-        return KMP_OK;
-    }
-    size_t t2 = 0, t3 = 0;
-    PG(rocprim::radix_sort_keys<PairSortCfg>(nullptr, t2, ws->inc_sorted.p, ws->inc.p, (size_t)total, 0u, pair_bits,
-                                             (hipStream_t)0));
-    PG(rocprim::run_length_encode(nullptr, t3, ws->inc.p, (unsigned int)total, ws->uniq.p, ws->w.p, ws->small.p + 1,
-                                  (hipStream_t)0));
-    PG(ws->tmp.reserve(std::max({t2, t3, ws->tmp.n})));
+    hipError_t e = hipSuccess;
+    pt_bufs(ws, g, true, &e);
+    PG(e);
     return KMP_OK;
 }
 
-// one attempt of the fused step, keys included, up to the read-back copy into ws->hrb; no host
-// wait, no allocation (fused_reserve ran first)
+// front: clear, keys, level 2 (or the bucket sort), bucket kernels
 template <class MakeKeys>
-int fused_enqueue(kmp_postings* ws, MakeKeys& make_keys, uint64_t slots, const Layout& lay, uint32_t n,
-                  uint32_t heavy_df, int require_class_diff, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w,
-                  uint64_t cap, hipStream_t st) {
-    const uint32_t nb = 1u << lay.bbits;
-    const uint64_t sc = ws->shard_cap, total = sc * kShards;
-    const unsigned pair_bits = bits_for((uint64_t)n * n);
-    uint32_t* flags = ws->flags.p;
-    uint32_t* list_count = flags + 2;
-    unsigned long long* gstats = ws->bstats.p;
-    unsigned long long* cursor = gstats + kShards * 8;
-    fused_clear_kernel<<<1, 256, 0, st>>>(flags, gstats);
+int enqueue_front(kmp_postings* ws, MakeKeys& make_keys, const StepCfg& c, bool spill, hipStream_t st) {
+    step_clear_kernel<<<1, 256, 0, st>>>(ws->flags.p, ws->bstats.p);
     ws->mark(0, st);
-    PG(make_keys(lay, st));
+    PG(make_keys(c.lay, st));
     ws->mark(1, st);
-    PShard ps{};
-    PtGeom g;
-    const bool pt = pt_geometry(ws, slots, n, &g);
-    const uint32_t mul = pt ? 1u << g.pbits : n;  // pair key p * mul + q
-    const BpDigits dg = bp_digits(lay);
-    const uint32_t K = ws->parted ? std::min<uint32_t>((uint32_t)std::max(ws->pipe_k, 1), std::min(dg.nb1, kPipeMax))
-                                  : 1u;
-    PG(ws->sorted.reserve(slots));
-    PG(ws->cnt.reserve(2 * (uint64_t)nb + 2));
-    uint32_t* bstart = ws->cnt.p;
-    uint32_t* list = ws->cnt.p + nb + 1;
-    // group + expand buckets [b_lo, b_hi) on stream s
-    auto group_range = [&](uint32_t b_lo, uint32_t b_hi, hipStream_t s) {
-        launch_bucket_small<false>(b_hi - b_lo, s, ws->sorted.p, bstart, lay, mul, require_class_diff, heavy_df,
-                                   ws->inc_sorted.p, sc, cursor, gstats, flags, list, list_count, ps, b_lo);
-        bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeTab, false>
-            <<<kBucketLargeGrid, kBucketLargeThreads, 0, s>>>(ws->sorted.p, bstart, lay, mul, require_class_diff,
-                                                              heavy_df, ws->inc_sorted.p, sc, cursor, gstats, flags,
-                                                              list, list_count, ps, b_lo, b_hi);
-    };
-    if (K <= 1) {
-        int rc = bucket_group(ws, ws->keys.p, slots, lay, st);
+    {
+        int rc = bucket_group(ws, ws->keys.p, c.slots, c.lay, st);  // marks 2
         if (rc != KMP_OK) return rc;
-        group_range(0, nb, st);
-    } else {
-        // level 2 (HBM-bound scatter) of coarse-bin chunk i+1 runs on st while chunk i's buckets
-        // (VALU-bound) are grouped on ws->pst: a fork / join captured into the step graph
-        ws->parted = false;
-        if (!ws->pst) PG(hipStreamCreateWithFlags(&ws->pst, hipStreamNonBlocking));
-        for (uint32_t i = 0; i <= K + 1; ++i)
-            if (!ws->pev[i]) PG(hipEventCreateWithFlags(&ws->pev[i], hipEventDisableTiming));
-        PG(hipEventRecord(ws->pev[0], st));
-        PG(hipStreamWaitEvent(ws->pst, ws->pev[0], 0));
-        for (uint32_t i = 0; i < K; ++i) {
-            const uint32_t c0 = (uint32_t)((uint64_t)dg.nb1 * i / K), c1 = (uint32_t)((uint64_t)dg.nb1 * (i + 1) / K);
-            int rc = bp_level2(ws, lay, st, c0, c1 - c0);
-            if (rc != KMP_OK) return rc;
-            PG(hipEventRecord(ws->pev[1 + i], st));
-            PG(hipStreamWaitEvent(ws->pst, ws->pev[1 + i], 0));
-            group_range(c0 * dg.nb2, c1 * dg.nb2, ws->pst);
-        }
-        ws->mark(2, st);
-        PG(hipEventRecord(ws->pev[K + 1], ws->pst));
-        PG(hipStreamWaitEvent(st, ws->pev[K + 1], 0));
     }
-    ws->mark(3, st);
-    if (pt) {
-        hipError_t e = hipSuccess;
-        const PtBufs b = pt_bufs(ws, g, false, &e);
-        uint32_t* keys32 = reinterpret_cast<uint32_t*>(ws->inc.p);
-        uint32_t* stage_p = reinterpret_cast<uint32_t*>(ws->uniq.p);
-        uint32_t* stage_q = stage_p + total;
-        pt_hist_kernel<<<dim3(g.jt, g.nshards), kPtThreads, 0, st>>>(ws->inc_sorted.p, cursor, g, b.H);
-        bp_colsum_kernel<<<dim3(b.groups, (g.nrb + 255) / 256), 256, 0, st>>>(b.H, b.rows, g.nrb, b.R);
-        pt_colscan_kernel<<<1, kPtScanThreads, 0, st>>>(b.R, b.groups, g.nrb, b.bst, ws->small.p + 2);
-        bp_colprefix_kernel<<<dim3(b.groups, (g.nrb + 255) / 256), 256, 0, st>>>(b.H, b.rows, g.nrb, b.R, b.P);
-        ws->mark(4, st);
-        pt_scatter_kernel<<<dim3(g.jt, g.nshards), kPtThreads, 0, st>>>(ws->inc_sorted.p, cursor, g, b.P, keys32);
-        pt_reduce_kernel<<<g.nrb, kPtRThreads, 0, st>>>(keys32, b.bst, g, flags, stage_p, stage_q, ws->w.p, b.counts);
-        ws->mark(5, st);
-        pt_offsets_kernel<<<1, kPtScanThreads, 0, st>>>(b.counts, g.nrb, b.eoff, ws->small.p + 1);
-        pt_emit_kernel<<<g.nrb, 256, 0, st>>>(stage_p, stage_q, ws->w.p, b.bst, b.counts, b.eoff, d_p, d_q, d_w, cap);
-        fused_pack_kernel<<<1, 256, 0, st>>>(gstats, flags, ws->small.p + 1, ws->hrb);
-        ws->mark(6, st);
-        PG(hipGetLastError());
-        return KMP_OK;
-    }
-    pad_shards_kernel<<<dim3(route_blocks(sc), kShards), 256, 0, st>>>(ws->inc_sorted.p, sc, cursor);
+    const BucketArgs a = bucket_args(ws, c, spill);
+    const uint32_t nb = 1u << c.lay.bbits;
+    if (c.ranged) launch_buckets<true>(a, nb, st);
+    else launch_buckets<false>(a, nb, st);
+    PG(hipGetLastError());
+    return KMP_OK;
+}
+
+// tail over the shard regions, then the read-back; marks 4, 5, 6
+int enqueue_tail(kmp_postings* ws, const StepCfg& c, const PtGeom& g, hipStream_t st) {
+    hipError_t e = hipSuccess;
+    const PtBufs b = pt_bufs(ws, g, false, &e);
+    const uint64_t total = ws->shard_cap * kShards;
+    const unsigned long long* cursor = ws->bstats.p + kRbCursor;
+    uint32_t* keys32 = reinterpret_cast<uint32_t*>(ws->inc.p);
+    uint32_t* stage_p = reinterpret_cast<uint32_t*>(ws->uniq.p);
+    uint32_t* stage_q = stage_p + total;
+    pt_hist_kernel<<<dim3(g.jt, g.nshards), kPtThreads, 0, st>>>(ws->inc_sorted.p, cursor, g, b.H);
+    bp_colsum_kernel<<<dim3(b.groups, (g.nrb + 255) / 256), 256, 0, st>>>(b.H, b.rows, g.nrb, b.R);
+    pt_colscan_kernel<<<1, kPtScanThreads, 0, st>>>(b.R, b.groups, g.nrb, b.bst, ws->small.p + 2);
+    bp_colprefix_kernel<<<dim3(b.groups, (g.nrb + 255) / 256), 256, 0, st>>>(b.H, b.rows, g.nrb, b.R, b.P);
     ws->mark(4, st);
-    size_t t2 = ws->tmp.n, t3 = ws->tmp.n;
-    PG(rocprim::radix_sort_keys<PairSortCfg>(ws->tmp.p, t2, ws->inc_sorted.p, ws->inc.p, (size_t)total, 0u,
-                                             pair_bits, st));
+    pt_scatter_kernel<<<dim3(g.jt, g.nshards), kPtThreads, 0, st>>>(ws->inc_sorted.p, cursor, g, b.P, keys32);
+    pt_reduce_kernel<<<g.nrb, kPtRThreads, 0, st>>>(keys32, b.bst, g, ws->flags.p, ws->ovf.p, stage_p, stage_q,
+                                                    ws->w.p, b.counts);
     ws->mark(5, st);
-    PG(rocprim::run_length_encode(ws->tmp.p, t3, ws->inc.p, (unsigned int)total, ws->uniq.p, ws->w.p,
-                                  ws->small.p + 1, st));
-    const uint32_t kb = (uint32_t)std::min<uint64_t>((total + 255) / 256, 8192);
-    emit_runs_kernel<<<kb, 256, 0, st>>>(ws->uniq.p, ws->w.p, ws->small.p + 1, n, d_p, d_q, d_w, cap);
-    fused_pack_kernel<<<1, 256, 0, st>>>(gstats, flags, ws->small.p + 1, ws->hrb);
+    pt_offsets_kernel<<<1, kPtScanThreads, 0, st>>>(b.counts, g.nrb, b.eoff, ws->small.p + 1);
+    pt_emit_kernel<<<g.nrb, 256, 0, st>>>(stage_p, stage_q, ws->w.p, b.bst, b.counts, b.eoff, c.d_p, c.d_q, c.d_w,
+                                          c.cap, c.stride);
+    step_pack_kernel<<<1, 256, 0, st>>>(ws->bstats.p, ws->flags.p, ws->small.p + 1, ws->hrb);
     ws->mark(6, st);
     PG(hipGetLastError());
     return KMP_OK;
 }
 
-// enqueue the step: replay the captured graph when the shape matches the capture, capture it
-// when the shape repeats a plain run (buffers sized), else run plain
+// the listed row blocks (above kPtCap keys): one segmented radix sort, run-length encoding,
+// then offsets and emit again; host-synchronous, returns the edge count in *edges
+int pt_finish_overflow(kmp_postings* ws, const StepCfg& c, const PtGeom& g, uint32_t m, uint64_t* edges,
+                       hipStream_t st) {
+    hipError_t e = hipSuccess;
+    const PtBufs b = pt_bufs(ws, g, false, &e);
+    const uint64_t total = ws->shard_cap * kShards;
+    uint32_t* keys32 = reinterpret_cast<uint32_t*>(ws->inc.p);
+    uint32_t* stage_p = reinterpret_cast<uint32_t*>(ws->uniq.p);
+    uint32_t* stage_q = stage_p + total;
+    uint32_t* sb = ws->ovf.p + g.nrb + 1;
+    uint32_t* se = sb + g.nrb + 1;
+    PG(ws->ks.reserve(total));
+    pt_ovf_segments_kernel<<<(m + 255) / 256, 256, 0, st>>>(ws->ovf.p, m, b.bst, sb, se);
+    uint32_t nkeys = 0;
+    PG(hipMemcpyAsync(&nkeys, b.bst + g.nrb, 4, hipMemcpyDeviceToHost, st));
+    PG(hipStreamSynchronize(st));
+    size_t tb = 0;
+    PG(rocprim::segmented_radix_sort_keys(nullptr, tb, keys32, ws->ks.p, (unsigned)nkeys, m, sb, se, 0u,
+                                          g.pbits + g.rbits, st));
+    PG(ws->tmp.reserve(std::max(tb, ws->tmp.n)));
+    PG(rocprim::segmented_radix_sort_keys(ws->tmp.p, tb, keys32, ws->ks.p, (unsigned)nkeys, m, sb, se, 0u,
+                                          g.pbits + g.rbits, st));
+    pt_ovf_rle_kernel<<<m, kOvfThreads, 0, st>>>(ws->ovf.p, b.bst, g, ws->ks.p, keys32, stage_p, stage_q, ws->w.p,
+                                                 b.counts);
+    pt_offsets_kernel<<<1, kPtScanThreads, 0, st>>>(b.counts, g.nrb, b.eoff, ws->small.p + 1);
+    pt_emit_kernel<<<g.nrb, 256, 0, st>>>(stage_p, stage_q, ws->w.p, b.bst, b.counts, b.eoff, c.d_p, c.d_q, c.d_w,
+                                          c.cap, c.stride);
+    uint32_t ne = 0;
+    PG(hipMemcpyAsync(&ne, ws->small.p + 1, 4, hipMemcpyDeviceToHost, st));
+    PG(hipStreamSynchronize(st));
+    *edges = ne;
+    return KMP_OK;
+}
+
+// Heavy path (host-driven, after the front): gather, sort and compact the spill once per front;
+// plan and expand the rows of this call into the shard regions.  stats: post the heavy k-mers'
+// statistics (once per batch).
+int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipStream_t st) {
+    const Layout& lay = c.lay;
+    if (!ws->heavy_ready) {
+        PG(ws->hkeys.reserve(m));
+        PG(ws->hsorted.reserve(m));
+        const unsigned long long* spill_cursor = ws->bstats.p + kRbSpill;
+        gather_shards_kernel<<<dim3((uint32_t)std::min<uint64_t>((ws->spill_cap + 255) / 256, 1024), kShards), 256, 0,
+                               st>>>(ws->spill.p, ws->spill_cap, spill_cursor, ws->hkeys.p);
+        size_t tb = 0;
+        PG(rocprim::radix_sort_keys<SortCfg>(nullptr, tb, ws->hkeys.p, ws->hsorted.p, (size_t)m, lay.clsbits, 63u, st));
+        PG(ws->tmp.reserve(std::max(tb, ws->tmp.n)));
+        PG(rocprim::radix_sort_keys<SortCfg>(ws->tmp.p, tb, ws->hkeys.p, ws->hsorted.p, (size_t)m, lay.clsbits, 63u,
+                                             st));
+        const uint64_t nt = (m + kHvTile - 1) / kHvTile;
+        PG(ws->hcnt.reserve(2 * nt));
+        PG(ws->hoff.reserve(2 * nt + 2));
+        uint32_t* ecnt = ws->hcnt.p;
+        uint32_t* gcnt = ws->hcnt.p + nt;
+        unsigned long long* eoff = ws->hoff.p;
+        unsigned long long* goff = ws->hoff.p + nt + 1;
+        heavy_scan_kernel<<<(uint32_t)nt, kHvThreads, 0, st>>>(ws->hsorted.p, m, lay.clsbits, lay.hshift, ecnt, gcnt);
+        size_t t1 = 0;
+        PG(rocprim::exclusive_scan(nullptr, t1, ecnt, eoff, 0ull, (size_t)nt + 1, rocprim::plus<unsigned long long>(),
+                                   st));
+        PG(ws->tmp.reserve(std::max(t1, ws->tmp.n)));
+        PG(rocprim::exclusive_scan(ws->tmp.p, t1, ecnt, eoff, 0ull, (size_t)nt, rocprim::plus<unsigned long long>(),
+                                   st));
+        PG(rocprim::exclusive_scan(ws->tmp.p, t1, gcnt, goff, 0ull, (size_t)nt, rocprim::plus<unsigned long long>(),
+                                   st));
+        unsigned long long lastoff[2] = {0, 0};
+        uint32_t lastcnt[2] = {0, 0};
+        PG(hipMemcpyAsync(&lastoff[0], eoff + nt - 1, 8, hipMemcpyDeviceToHost, st));
+        PG(hipMemcpyAsync(&lastoff[1], goff + nt - 1, 8, hipMemcpyDeviceToHost, st));
+        PG(hipMemcpyAsync(&lastcnt[0], ecnt + nt - 1, 4, hipMemcpyDeviceToHost, st));
+        PG(hipMemcpyAsync(&lastcnt[1], gcnt + nt - 1, 4, hipMemcpyDeviceToHost, st));
+        PG(hipStreamSynchronize(st));
+        ws->h_ne = lastoff[0] + lastcnt[0];
+        ws->h_ng = lastoff[1] + lastcnt[1];
+        PG(ws->hE.reserve(ws->h_ne));
+        PG(ws->hGS.reserve(ws->h_ng + 1));
+        heavy_compact_kernel<<<(uint32_t)nt, kHvThreads, 0, st>>>(ws->hsorted.p, m, lay.clsbits, lay.hshift,
+                                                                  reinterpret_cast<const uint64_t*>(eoff),
+                                                                  reinterpret_cast<const uint64_t*>(goff), ws->hE.p,
+                                                                  reinterpret_cast<uint64_t*>(ws->hGS.p));
+        const unsigned long long ne = ws->h_ne;
+        PG(hipMemcpyAsync(ws->hGS.p + ws->h_ng, &ne, 8, hipMemcpyHostToDevice, st));
+        PG(hipGetLastError());
+        ws->heavy_ready = true;
+    }
+    const uint64_t ng = ws->h_ng;
+    if (ng == 0) return KMP_OK;
+    PG(ws->hgi.reserve(2 * ng));
+    PG(ws->htc.reserve(ng + 1));
+    PG(ws->htoff.reserve(ng + 1));
+    const uint32_t row_lo = c.ranged ? c.row_lo : 0, row_hi = c.ranged ? c.row_hi : c.n;
+    heavy_plan_kernel<<<(uint32_t)((ng + 255) / 256), 256, 0, st>>>(
+        ws->hE.p, reinterpret_cast<const uint64_t*>(ws->hGS.p), ng, lay.clsbits, row_lo, row_hi, c.heavy_df,
+        stats ? 1 : 0, ws->bstats.p, ws->hgi.p, ws->htc.p);
+    size_t t2 = 0;
+    PG(rocprim::exclusive_scan(nullptr, t2, ws->htc.p, ws->htoff.p, 0ull, (size_t)ng + 1,
+                               rocprim::plus<unsigned long long>(), st));
+    PG(ws->tmp.reserve(std::max(t2, ws->tmp.n)));
+    PG(hipMemsetAsync(ws->htc.p + ng, 0, 8, st));
+    PG(rocprim::exclusive_scan(ws->tmp.p, t2, ws->htc.p, ws->htoff.p, 0ull, (size_t)ng + 1,
+                               rocprim::plus<unsigned long long>(), st));
+    unsigned long long tiles = 0;
+    PG(hipMemcpyAsync(&tiles, ws->htoff.p + ng, 8, hipMemcpyDeviceToHost, st));
+    PG(hipStreamSynchronize(st));
+    if (tiles) {
+        const uint32_t grid = (uint32_t)std::min<unsigned long long>(tiles, 8192);
+        heavy_expand_kernel<<<grid, kHvI, 0, st>>>(ws->hE.p, reinterpret_cast<const uint64_t*>(ws->hGS.p), ws->hgi.p,
+                                                   ws->htoff.p, ng, ws->htoff.p + ng, lay.clsbits,
+                                                   1u << bits_for(c.n), c.require_diff, ws->inc_sorted.p,
+                                                   ws->shard_cap, ws->bstats.p + kRbCursor, ws->bstats.p);
+    }
+    PG(hipGetLastError());
+    return KMP_OK;
+}
+
+// enqueue the fused step: replay the captured graph when the shape matches the capture, capture
+// it when the shape repeats a plain run (buffers sized), else run plain
 template <class MakeKeys>
-int fused_launch(kmp_postings* ws, MakeKeys& make_keys, const std::vector<unsigned long long>& key, uint64_t slots,
-                 const Layout& lay, uint32_t n, uint32_t heavy_df, int require_class_diff, uint32_t* d_p,
-                 uint32_t* d_q, uint32_t* d_w, uint64_t cap, hipStream_t st) {
-    auto plain = [&]() {
-        return fused_enqueue(ws, make_keys, slots, lay, n, heavy_df, require_class_diff, d_p, d_q, d_w, cap, st);
+int fused_launch(kmp_postings* ws, MakeKeys& make_keys, const std::vector<unsigned long long>& key, const StepCfg& c,
+                 const PtGeom& g, hipStream_t st) {
+    auto enqueue = [&](hipStream_t s) {
+        int rc = enqueue_front(ws, make_keys, c, true, s);
+        if (rc == KMP_OK) {
+            ws->mark(3, s);
+            rc = enqueue_tail(ws, c, g, s);
+        }
+        return rc;
     };
-    if (!ws->graph_on) return plain();
+    if (!ws->graph_on) return enqueue(st);
     if (ws->gexec && ws->gkey == key) {
         PG(hipGraphLaunch(ws->gexec, st));
         ++ws->graph_replays;
@@ -2651,7 +2517,7 @@ int fused_launch(kmp_postings* ws, MakeKeys& make_keys, const std::vector<unsign
     }
     if (ws->gkey_seen != key) {
         ws->gkey_seen = key;
-        return plain();
+        return enqueue(st);
     }
     if (ws->gexec) {
         (void)hipGraphExecDestroy(ws->gexec);
@@ -2659,30 +2525,30 @@ int fused_launch(kmp_postings* ws, MakeKeys& make_keys, const std::vector<unsign
         ws->gkey.clear();
     }
     const unsigned long long gen = g_grow_gen;
-    hipGraph_t g = nullptr;
+    hipGraph_t gr = nullptr;
     // captured on a private stream (the caller's may be the legacy null stream, which cannot be
     // captured), launched on the caller's
     if (!ws->cst && hipStreamCreateWithFlags(&ws->cst, hipStreamNonBlocking) != hipSuccess) ws->cst = nullptr;
     if (!ws->cst || hipStreamBeginCapture(ws->cst, hipStreamCaptureModeRelaxed) != hipSuccess) {
         (void)hipGetLastError();
         ws->graph_on = false;
-        return plain();
+        return enqueue(st);
     }
-    int rc = fused_enqueue(ws, make_keys, slots, lay, n, heavy_df, require_class_diff, d_p, d_q, d_w, cap, ws->cst);
-    hipError_t e = hipStreamEndCapture(ws->cst, &g);
+    int rc = enqueue(ws->cst);
+    hipError_t e = hipStreamEndCapture(ws->cst, &gr);
     hipGraphExec_t ex = nullptr;
-    if (rc == KMP_OK && e == hipSuccess && g && gen == g_grow_gen)
-        e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+    if (rc == KMP_OK && e == hipSuccess && gr && gen == g_grow_gen)
+        e = hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0);
     else if (e == hipSuccess)
         e = hipErrorUnknown;
-    if (g) (void)hipGraphDestroy(g);
+    if (gr) (void)hipGraphDestroy(gr);
     if (e != hipSuccess || !ex) {  // capture not usable: plain from now on
         (void)hipGetLastError();
         if (getenv("KMP_DEBUG"))
             fprintf(stderr, "kmp: step graph capture failed (rc %d, %s); plain launches from now on\n", rc,
                     hipGetErrorString(e));
         ws->graph_on = false;
-        return plain();
+        return enqueue(st);
     }
     ws->gexec = ex;
     ws->gkey = key;
@@ -2690,71 +2556,143 @@ int fused_launch(kmp_postings* ws, MakeKeys& make_keys, const std::vector<unsign
     return KMP_OK;
 }
 
+void sum_stats(const unsigned long long* rb, unsigned long long* acc, unsigned long long* most,
+               unsigned long long* n_inc, unsigned long long* spill_most, unsigned long long* spill_total) {
+    for (int t = 0; t < kStN; ++t) acc[t] = 0;
+    *most = *n_inc = *spill_most = *spill_total = 0;
+    for (int sh = 0; sh < kShards; ++sh) {
+        for (int t = 0; t < kStN; ++t)
+            acc[t] = t == kStMaxDf ? std::max(acc[t], rb[sh * 8 + t]) : acc[t] + rb[sh * 8 + t];
+        *most = std::max(*most, rb[kRbCursor + sh]);
+        *n_inc += rb[kRbCursor + sh];
+        *spill_most = std::max(*spill_most, rb[kRbSpill + sh]);
+        *spill_total += rb[kRbSpill + sh];
+    }
+}
+
+// One call: the fused step, or the split step when the batch spills.  *fallback: a class id
+// wider than the key's class field (the caller reruns on the flat layout).
 template <class MakeKeys>
-int run_fused(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long long> key, uint64_t slots,
-              const Layout& lay, uint32_t n, uint32_t heavy_df, int require_class_diff, uint32_t* d_p, uint32_t* d_q,
-              uint32_t* d_w, uint64_t cap, uint64_t* n_edges, bool* fallback, kmp_postings_stats* stats,
-              hipStream_t st) {
+int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long long> key, const StepCfg& c,
+             uint64_t* n_edges, bool* fallback, kmp_postings_stats* stats, hipStream_t st) {
     *fallback = false;
-    if (ws->shard_cap == 0) ws->shard_cap = slots / 4 / kShards + 4096;
-    // every rerun grows the shard capacity, shrinks the row blocks or leaves the row-block tail,
-    // so a handful of attempts always suffices
+    const std::vector<unsigned long long> shape = {c.n, c.slots, (unsigned long long)c.lay.cbits, c.lay.bbits};
+    if (ws->shape != shape) {  // a new batch: forget what the last one taught the row tail and level 2
+        ws->shape = shape;
+        ws->pt_inc = 0;
+        ws->pt_rb_max = 16;
+        ws->bp_J_min = 0;
+        ws->heavy = false;
+    }
+    if (ws->shard_cap == 0) ws->shard_cap = c.slots / 4 / kShards + 4096;
+    if (ws->spill_cap == 0) ws->spill_cap = 1024;
+    const bool debug = getenv("KMP_DEBUG") != nullptr;
+    // every rerun grows a capacity to its measured need, so a handful of attempts suffices
     for (int attempt = 0; attempt < 16; ++attempt) {
-        const uint64_t sc = ws->shard_cap, total = sc * kShards;
+        PtGeom g;
+        if (!pt_geometry(ws, c, ws->pt_inc ? ws->pt_inc : c.slots / 4, &g)) return KMP_EINVAL;
         {
-            int rc = fused_reserve(ws, slots, lay, n);
+            int rc = step_reserve(ws, c, g);
             if (rc != KMP_OK) return rc;
         }
-        PtGeom pg;
-        const bool pt = pt_geometry(ws, slots, n, &pg);
-        key.push_back(sc);
-        key.push_back(ws->timing);
-        key.push_back(pt ? (pg.rbits + 1) | pg.rank << 8 : 0);
-        key.push_back(g_grow_gen);
-        int rc = fused_launch(ws, make_keys, key, slots, lay, n, heavy_df, require_class_diff, d_p, d_q, d_w, cap, st);
-        key.resize(key.size() - 4);
-        if (rc != KMP_OK) return rc;
-        PG(hipStreamSynchronize(st));
-        const unsigned long long* g = ws->hrb;
-        if (g[kShards * 9] || g[kShards * 9 + 1]) {
+        const unsigned long long* rb = ws->hrb;
+        unsigned long long acc[kStN], most, n_inc, spill_most, spill_total;
+        if (!ws->heavy) {
+            key.push_back(ws->shard_cap);
+            key.push_back(ws->spill_cap);
+            key.push_back(ws->timing);
+            key.push_back(g.rbits + 1);
+            key.push_back(g_grow_gen);
+            int rc = fused_launch(ws, make_keys, key, c, g, st);
+            key.resize(key.size() - 5);
+            if (rc != KMP_OK) return rc;
+            PG(hipStreamSynchronize(st));
+        } else {
+            ws->heavy_ready = false;
+            int rc = enqueue_front(ws, make_keys, c, true, st);
+            if (rc != KMP_OK) return rc;
+            step_pack_kernel<<<1, 256, 0, st>>>(ws->bstats.p, ws->flags.p, nullptr, ws->hrb);
+            PG(hipStreamSynchronize(st));
+        }
+        if (rb[kRbFlagClass]) {
             *fallback = true;
             return KMP_OK;
         }
-        if (pt && g[kShards * 9 + 3]) {
-            // a row block above kPtCap: fewer rows per block (sized from the largest block), or
-            // the global-sort tail from now on when a single row is already too long
-            const double over = (double)g[kShards * 9 + 4] / (0.8 * kPtCap);
-            unsigned shrink = 1;
-            while (shrink < 16 && (double)(1u << shrink) < over) ++shrink;
-            if (pg.rbits == 0) ws->pt_on = false;
-            else ws->pt_rb_max = pg.rbits > shrink ? pg.rbits - shrink : 0u;
-            if (getenv("KMP_DEBUG"))
-                fprintf(stderr, "kmp: row block of %llu keys (rbits %u): rbits bound %u, row tail %d\n",
-                        (unsigned long long)g[kShards * 9 + 4], pg.rbits, ws->pt_rb_max, (int)ws->pt_on);
+        sum_stats(rb, acc, &most, &n_inc, &spill_most, &spill_total);
+        bool rerun = false;
+        if (rb[kRbFlagBin]) {  // a coarse bin above its level-2 tile budget
+            ws->bp_J_min = (uint32_t)rb[kRbBinTiles] + 2;
+            rerun = true;
+        }
+        if (spill_most > ws->spill_cap) {
+            ws->spill_cap = spill_most + spill_most / 8 + 1024;
+            rerun = true;
+        }
+        if (spill_total && !ws->heavy) {  // frequent k-mers: the split step from now on
+            ws->heavy = true;
+            rerun = true;
+        }
+        if (!ws->heavy && most > ws->shard_cap) {
+            ws->shard_cap = most + most / 64 + 256;
+            rerun = true;
+        }
+        if (rerun) {
+            if (debug)
+                fprintf(stderr, "kmp: rerun (bin %llu tiles %llu, spill %llu/%llu, heavy %d, shard %llu/%llu)\n",
+                        rb[kRbFlagBin], rb[kRbBinTiles], spill_most, (unsigned long long)ws->spill_cap,
+                        (int)ws->heavy, most, (unsigned long long)ws->shard_cap);
             continue;
         }
-        unsigned long long acc[kStN] = {}, most = 0, n_inc = 0;
-        for (int sh = 0; sh < kShards; ++sh) {
-            for (int t = 0; t < kStN; ++t)
-                acc[t] = t == kStMaxDf ? std::max(acc[t], g[sh * 8 + t]) : acc[t] + g[sh * 8 + t];
-            most = std::max(most, g[kShards * 8 + sh]);
-            n_inc += g[kShards * 8 + sh];
+        if (ws->heavy) {
+            if (spill_total) {
+                ws->mark(3, st);
+                int rc = heavy_phase(ws, c, spill_total, true, st);
+                if (rc != KMP_OK) return rc;
+            }
+            step_pack_kernel<<<1, 256, 0, st>>>(ws->bstats.p, ws->flags.p, nullptr, ws->hrb);
+            PG(hipStreamSynchronize(st));
+            sum_stats(rb, acc, &most, &n_inc, &spill_most, &spill_total);
+            if (most > ws->shard_cap) {
+                ws->shard_cap = most + most / 64 + 256;
+                continue;
+            }
+            ws->pt_inc = n_inc;
+            if (!pt_geometry(ws, c, n_inc, &g)) return KMP_EINVAL;
+            int rc = step_reserve(ws, c, g);
+            if (rc != KMP_OK) return rc;
+            rc = enqueue_tail(ws, c, g, st);
+            if (rc != KMP_OK) return rc;
+            PG(hipStreamSynchronize(st));
         }
-        const uint64_t h_uniq = g[kShards * 9 + 2];
-        ws->shard_cap = most + most / 64 + 256;  // learned capacity for the next call (or the rerun)
-        if (most > sc) {                          // a region overflowed: rerun with the new capacity
-            if (getenv("KMP_DEBUG"))
-                fprintf(stderr, "kmp: shard region of %llu keys > %llu: rerun\n", most, (unsigned long long)sc);
-            continue;
+        ws->shard_cap = std::max<uint64_t>(ws->shard_cap, most + most / 64 + 256);  // learned for the next call
+        ws->pt_inc = n_inc;  // sizes the next call's row blocks
+        uint64_t ne = rb[kRbRuns];
+        ws->last_ovf = (uint32_t)rb[kRbOvf];
+        if (rb[kRbOvf]) {
+            // row blocks above the LDS capacity: finished by the segmented sort; the next call
+            // uses fewer rows per block when one row is not already the whole block
+            if (g.rbits > 0) {
+                const double over = (double)rb[kRbMaxBlock] / (0.8 * kPtCap);
+                unsigned shrink = 1;
+                while (shrink < 16 && (double)(1u << shrink) < over) ++shrink;
+                ws->pt_rb_max = g.rbits > shrink ? g.rbits - shrink : 0u;
+            }
+            int rc = pt_finish_overflow(ws, c, g, (uint32_t)rb[kRbOvf], &ne, st);
+            if (rc != KMP_OK) return rc;
+            if (debug)
+                fprintf(stderr, "kmp: %llu row blocks above %u keys (largest %llu) sorted apart; rbits bound %u\n",
+                        rb[kRbOvf], kPtCap, rb[kRbMaxBlock], ws->pt_rb_max);
         }
         fill_stats(stats, acc);
-        if (stats) stats->incidences = n_inc;
-        ws->pt_inc = n_inc;  // sizes the next call's row blocks
-        const uint64_t ne = pt ? h_uniq : h_uniq - (n_inc < total ? 1u : 0u);  // sort tail: the padding run
-        ws->last_rows = pt;
-        if (stats) stats->pairs = ne;
+        if (stats) {
+            stats->incidences = n_inc;
+            stats->pairs = ne;
+        }
+        ws->last_heavy = ws->heavy;
+        ws->last_fused = !ws->heavy;
+        if (ws->heavy && !spill_total) ws->heavy = false;  // nothing spilled: the fused step next call
         *n_edges = ne;
-        return ne > cap ? KMP_EOVERFLOW : KMP_OK;
+        return ne > c.cap ? KMP_EOVERFLOW : KMP_OK;
     }
     return KMP_EDEVICE;
 }
@@ -2847,63 +2785,66 @@ hipError_t launch_residue_keys(kmp_postings* ws, const uint8_t* d_res, const uin
     return hipGetLastError();
 }
 
-// Both entry points: keys from `make_keys(layout)`, bucketed front end (flat on fallback), tail.
+// Both entry points: keys from `make_keys(layout)`, the bucketed step (flat on fallback).
 template <class MakeKeys>
 int run_postings(kmp_postings* ws, MakeKeys make_keys, const std::vector<unsigned long long>& key_extra, uint32_t n,
                  int k, uint64_t slots, const uint16_t* d_class, uint32_t heavy_df, uint32_t min_shared,
-                 int require_class_diff, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w, uint64_t cap, uint64_t* n_edges,
-                 kmp_postings_stats* stats, hipStream_t st) {
+                 int require_class_diff, bool ranged, uint32_t row_lo, uint32_t row_hi, uint32_t* d_p, uint32_t* d_q,
+                 uint32_t* d_w, uint64_t cap, uint64_t* n_edges, kmp_postings_stats* stats, hipStream_t st) {
     if (heavy_df < 2) heavy_df = 2;
     if (min_shared < 1) min_shared = 1;
     PG(ws->keys.reserve(slots));
     PG(ws->sorted.reserve(slots));
-    PG(ws->flags.reserve(4));
-    unsigned long long n_inc = 0;
+    PG(ws->flags.reserve(kFlN));
     ws->parted = false;
     Layout lay = make_layout(n, k, slots, ws->bucketed);
-    bool fallback = true;
-    if (lay.bucketed && min_shared == 1 && !ws->pshard) {
-        // graph key: the call's shape and pointers (run_fused adds the shard capacity, the timing
-        // switch and the buffer generation)
-        std::vector<unsigned long long> key = {n, (unsigned long long)k, slots, heavy_df,
-                                               (unsigned long long)require_class_diff, cap,
+    if (lay.bucketed) {
+        StepCfg c{};
+        c.slots = slots;
+        c.lay = lay;
+        c.n = n;
+        c.heavy_df = heavy_df;
+        c.min_shared = min_shared;
+        c.require_diff = require_class_diff;
+        c.ranged = ranged;
+        c.row_lo = row_lo;
+        c.row_hi = row_hi;
+        c.d_p = d_p;
+        c.d_q = d_q;
+        c.d_w = d_w;
+        c.cap = cap;
+        c.stride = 1;
+        // graph key: the call's shape and pointers (run_step adds the capacities, the timing
+        // switch, the row-block geometry and the buffer generation)
+        std::vector<unsigned long long> key = {n, (unsigned long long)k, slots, heavy_df, min_shared,
+                                               (unsigned long long)require_class_diff, ranged, row_lo, row_hi, cap,
                                                (unsigned long long)(uintptr_t)d_p, (unsigned long long)(uintptr_t)d_q,
                                                (unsigned long long)(uintptr_t)d_w};
         key.insert(key.end(), key_extra.begin(), key_extra.end());
-        int rc = run_fused(ws, make_keys, key, slots, lay, n, heavy_df, require_class_diff, d_p, d_q, d_w, cap,
-                           n_edges, &fallback, stats, st);
+        bool fallback = false;
+        int rc = run_step(ws, make_keys, key, c, n_edges, &fallback, stats, st);
         if (!fallback) {
             ws->last_bucketed = true;
-            ws->last_pshard = false;
-            ws->last_fused = true;
             if (rc == KMP_OK) finish_timing(ws, stats, st);
             return rc;
         }
-    } else if (lay.bucketed) {
-        PG(hipMemsetAsync(ws->flags.p, 0, 4 * sizeof(uint32_t), st));
-        ws->mark(0, st);
-        PG(make_keys(lay, st));
-        ws->mark(1, st);
-        int rc = front_bucketed(ws, ws->keys.p, slots, lay, n, heavy_df, require_class_diff, ws->pshard, &n_inc,
-                                &fallback, stats, st);
-        if (rc != KMP_OK) return rc;
     }
-    if (fallback) {
-        lay = make_layout(n, k, slots, false);
-        if (lay.sort_hi > 64) return KMP_EINVAL;
-        ws->parted = false;
-        PG(hipMemsetAsync(ws->flags.p, 0, 4 * sizeof(uint32_t), st));
-        ws->mark(0, st);
-        PG(make_keys(lay, st));
-        ws->mark(1, st);
-        int rc = front_flat(ws, slots, lay, d_class, n, heavy_df, require_class_diff, &n_inc, stats, st);
-        if (rc != KMP_OK) return rc;
-    }
-    ws->last_bucketed = !fallback;
-    ws->last_pshard = !fallback && ws->ps_ok;
-    ws->last_fused = false;
-    int rc = ws->last_pshard ? tail_pshard(ws, min_shared, d_p, d_q, d_w, cap, n_edges, stats, st)
-                             : tail(ws, ws->inc.p, n_inc, n, min_shared, d_p, d_q, d_w, cap, n_edges, stats, st);
+    // flat layout: class ids wider than the bucketed key's class field (or the layout forced)
+    if (ranged) return KMP_ESTATE;  // no row filter on the flat layout
+    lay = make_layout(n, k, slots, false);
+    if (lay.sort_hi > 64) return KMP_EINVAL;
+    ws->parted = false;
+    PG(hipMemsetAsync(ws->flags.p, 0, kFlN * sizeof(uint32_t), st));
+    ws->mark(0, st);
+    PG(make_keys(lay, st));
+    ws->mark(1, st);
+    unsigned long long n_inc = 0;
+    int rc = front_flat(ws, slots, lay, d_class, n, heavy_df, require_class_diff, &n_inc, stats, st);
+    if (rc != KMP_OK) return rc;
+    ws->last_bucketed = false;
+    ws->last_fused = ws->last_heavy = false;
+    ws->last_ovf = 0;
+    rc = tail(ws, ws->inc.p, n_inc, n, min_shared, d_p, d_q, d_w, cap, n_edges, stats, st);
     if (rc == KMP_OK) finish_timing(ws, stats, st);
     return rc;
 }
@@ -2935,21 +2876,11 @@ int kmp_postings_set_layout(kmp_postings* ws, int bucketed) {
 }
 
 int kmp_postings_last_layout(const kmp_postings* ws) {
-    if (!ws || !ws->last_bucketed) return 0;
-    return ws->last_fused ? (ws->last_rows ? 4 : 3) : ws->last_pshard ? 2 : 1;
+    if (!ws || !ws->last_bucketed) return KMP_LAYOUT_FLAT;
+    return ws->last_heavy ? KMP_LAYOUT_BUCKETED_HEAVY : KMP_LAYOUT_BUCKETED;
 }
 
-int kmp_postings_set_pshard(kmp_postings* ws, int enable) {
-    if (!ws) return KMP_EINVAL;
-    ws->pshard = enable != 0;
-    return KMP_OK;
-}
-
-int kmp_postings_set_partition(kmp_postings* ws, int enable) {
-    if (!ws) return KMP_EINVAL;
-    ws->partition = enable != 0;
-    return KMP_OK;
-}
+uint32_t kmp_postings_last_overflow_blocks(const kmp_postings* ws) { return ws ? ws->last_ovf : 0u; }
 
 int kmp_postings_set_graph(kmp_postings* ws, int enable) {
     if (!ws) return KMP_EINVAL;
@@ -2981,260 +2912,53 @@ int kmp_dev_pairs_postings(kmp_postings* ws, const uint32_t* d_set, const uint32
     };
     const std::vector<unsigned long long> key_extra = {0, (uintptr_t)d_set, (uintptr_t)d_set_len, (uintptr_t)d_res_off,
                                                        (uintptr_t)d_class};
-    return run_postings(ws, keys, key_extra, n, k, slots, d_class, heavy_df, min_shared, require_class_diff, d_p, d_q,
-                        d_w, cap, n_edges, stats, st);
+    return run_postings(ws, keys, key_extra, n, k, slots, d_class, heavy_df, min_shared, require_class_diff, false, 0,
+                        n, d_p, d_q, d_w, cap, n_edges, stats, st);
+}
+
+static int residues_impl(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
+                         uint32_t n, int k, uint64_t slots, uint32_t heavy_df, uint32_t min_shared,
+                         int require_class_diff, bool ranged, uint32_t row_lo, uint32_t row_hi, uint32_t* d_p,
+                         uint32_t* d_q, uint32_t* d_w, uint64_t cap, uint64_t* n_edges, kmp_postings_stats* stats,
+                         void* stream) {
+    int rc = postings_args(ws, k, n_edges, stats, d_p, d_q, d_w, cap);
+    if (rc != KMP_OK || n < 2) return rc;
+    if (!d_res || !d_res_off || !d_class) return KMP_EINVAL;
+    hipStream_t st = as_stream(stream);
+    auto keys = [&](const Layout& lay, hipStream_t st) {
+        if (lay.bucketed) {
+            ws->parted = true;
+            return bp_level1(ws, d_res, d_res_off, d_class, k, n, slots, lay, st);
+        }
+        return launch_residue_keys(ws, d_res, d_res_off, d_class, k, 0u, n, 0ull, slots, lay, st);
+    };
+    const std::vector<unsigned long long> key_extra = {1, (uintptr_t)d_res, (uintptr_t)d_res_off, (uintptr_t)d_class};
+    return run_postings(ws, keys, key_extra, n, k, slots, d_class, heavy_df, min_shared, require_class_diff, ranged,
+                        row_lo, row_hi, d_p, d_q, d_w, cap, n_edges, stats, st);
 }
 
 int kmp_dev_pairs_residues(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off,
                            const uint16_t* d_class, uint32_t n, int k, uint64_t slots, uint32_t heavy_df,
                            uint32_t min_shared, int require_class_diff, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w,
                            uint64_t cap, uint64_t* n_edges, kmp_postings_stats* stats, void* stream) {
-    int rc = postings_args(ws, k, n_edges, stats, d_p, d_q, d_w, cap);
-    if (rc != KMP_OK || n < 2) return rc;
-    if (!d_res || !d_res_off || !d_class) return KMP_EINVAL;
-    hipStream_t st = as_stream(stream);
-    auto keys = [&](const Layout& lay, hipStream_t st) {
-        if (lay.bucketed && ws->partition) {
-            ws->parted = true;
-            return bp_level1(ws, d_res, d_res_off, d_class, k, n, slots, lay, st);
-        }
-        return launch_residue_keys(ws, d_res, d_res_off, d_class, k, 0u, n, 0ull, slots, lay, st);
-    };
-    const std::vector<unsigned long long> key_extra = {1, (uintptr_t)d_res, (uintptr_t)d_res_off, (uintptr_t)d_class,
-                                                       ws->partition};
-    return run_postings(ws, keys, key_extra, n, k, slots, d_class, heavy_df, min_shared, require_class_diff, d_p, d_q,
-                        d_w, cap, n_edges, stats, st);
+    return residues_impl(ws, d_res, d_res_off, d_class, n, k, slots, heavy_df, min_shared, require_class_diff, false,
+                         0, n, d_p, d_q, d_w, cap, n_edges, stats, stream);
 }
 
-// ------------------------------------------------------------- multi-GPU split -------------
-// (dist.py) keys of a protein slice, routed by k-mer bucket range -> group + expand on the
-// bucket owner -> pair keys routed by p range -> edges on the p-range owner.
-
-static int part_bounds(kmp_postings* ws, const unsigned long long* d_sorted, uint64_t m, unsigned shift,
-                       unsigned long long total, unsigned long long unit, uint32_t parts, uint64_t* counts,
-                       hipStream_t st) {
-    PG(ws->bstats.reserve(std::max<uint64_t>(ws->bstats.n, kShards * 8 + kShards + parts + 1)));
-    unsigned long long* d_b = ws->bstats.p + kShards * 8 + kShards;
-    part_bounds_kernel<<<(parts + 1 + 63) / 64, 64, 0, st>>>(d_sorted, m, shift, total, unit, parts, d_b);
-    std::vector<unsigned long long> h(parts + 1);
-    PG(hipMemcpyAsync(h.data(), d_b, (parts + 1) * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
-    PG(hipStreamSynchronize(st));
-    for (uint32_t j = 0; j < parts; ++j) counts[j] = h[j + 1] - h[j];
-    return KMP_OK;
-}
-
-int kmp_dev_keys_part(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
-                      uint32_t n, int k, uint64_t slots, uint32_t lo, uint32_t hi, uint64_t slot_lo,
-                      uint64_t slot_hi, uint32_t parts, unsigned long long* d_out, uint64_t out_cap,
-                      uint64_t* part_counts, void* stream) {
-    if (!ws || !part_counts || parts < 1 || k < 1 || k > kMaxK || lo > hi || hi > n || slot_hi < slot_lo)
-        return KMP_EINVAL;
-    for (uint32_t j = 0; j < parts; ++j) part_counts[j] = 0;
-    const uint64_t m = slot_hi - slot_lo;
-    if (hi == lo || m == 0) return KMP_OK;
-    if (!d_res || !d_res_off || !d_class || !d_out || out_cap < m) return KMP_EINVAL;
-    const Layout lay = make_layout(n, k, slots, true);
-    if (!lay.bucketed) return KMP_ESTATE;
-    hipStream_t st = as_stream(stream);
-    PG(ws->keys.reserve(m));
-    PG(ws->flags.reserve(4));
-    PG(hipMemsetAsync(ws->flags.p, 0, 4 * sizeof(uint32_t), st));
-    PG(launch_residue_keys(ws, d_res, d_res_off, d_class, k, lo, hi, slot_lo, slot_hi, lay, st));
-    size_t t_sort = 0;
-    PG(rocprim::radix_sort_keys<SortCfg>(nullptr, t_sort, ws->keys.p, d_out, (size_t)m, lay.sort_lo, lay.sort_hi, st));
-    PG(ws->tmp.reserve(std::max(t_sort, ws->tmp.n)));
-    PG(rocprim::radix_sort_keys<SortCfg>(ws->tmp.p, t_sort, ws->keys.p, d_out, (size_t)m, lay.sort_lo, lay.sort_hi, st));
-    int rc = part_bounds(ws, d_out, m, lay.sort_lo, 1ull << lay.bbits, 1, parts, part_counts, st);
-    if (rc != KMP_OK) return rc;
-    uint32_t h_flags[2] = {0, 0};
-    PG(hipMemcpy(h_flags, ws->flags.p, sizeof h_flags, hipMemcpyDeviceToHost));
-    return h_flags[1] ? KMP_ESTATE : KMP_OK;
-}
-
-int kmp_dev_pairs_keys(kmp_postings* ws, const unsigned long long* d_keys, uint64_t m, uint32_t n, int k,
-                       uint64_t slots, uint32_t heavy_df, int require_class_diff, uint32_t parts,
-                       unsigned long long* d_out, uint64_t out_cap, uint64_t* n_inc, uint64_t* part_counts,
-                       kmp_postings_stats* stats, void* stream) {
-    if (!ws || !n_inc || !part_counts || parts < 1 || k < 1 || k > kMaxK) return KMP_EINVAL;
-    *n_inc = 0;
-    for (uint32_t j = 0; j < parts; ++j) part_counts[j] = 0;
-    if (stats) *stats = kmp_postings_stats{};
-    if (m == 0 || n < 2) return KMP_OK;
-    if (!d_keys) return KMP_EINVAL;
-    const Layout lay = make_layout(n, k, slots, true);
-    if (!lay.bucketed) return KMP_ESTATE;
-    hipStream_t st = as_stream(stream);
-    PG(ws->flags.reserve(4));
-    PG(hipMemsetAsync(ws->flags.p, 0, 4 * sizeof(uint32_t), st));
-    unsigned long long ni = 0;
-    bool fallback = false;
-    int rc = front_bucketed(ws, d_keys, m, lay, n, heavy_df < 2 ? 2 : heavy_df, require_class_diff, false, &ni,
-                            &fallback, stats, st);
-    if (rc != KMP_OK) return rc;
-    if (fallback) return KMP_ESTATE;  // a k-mer too frequent for the LDS buckets
-    *n_inc = ni;
-    if (stats) stats->incidences = ni;
-    if (ni == 0) return KMP_OK;
-    if (ni > out_cap || !d_out) return KMP_EOVERFLOW;
-    const unsigned pair_bits = bits_for((uint64_t)n * n);
-    size_t t2 = 0;
-    PG(rocprim::radix_sort_keys<PairSortCfg>(nullptr, t2, ws->inc.p, d_out, (size_t)ni, 0u, pair_bits, st));
-    PG(ws->tmp.reserve(std::max(t2, ws->tmp.n)));
-    PG(rocprim::radix_sort_keys<PairSortCfg>(ws->tmp.p, t2, ws->inc.p, d_out, (size_t)ni, 0u, pair_bits, st));
-    return part_bounds(ws, d_out, ni, 0, n, n, parts, part_counts, st);
-}
-
-int kmp_dev_edges_pairkeys(kmp_postings* ws, const unsigned long long* d_pk, uint64_t m, uint32_t n,
-                           uint32_t min_shared, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w, uint64_t cap,
-                           uint64_t* n_edges, uint64_t* n_pairs, void* stream) {
-    if (!ws || !n_edges || (cap && (!d_p || !d_q || !d_w))) return KMP_EINVAL;
-    *n_edges = 0;
-    if (n_pairs) *n_pairs = 0;
-    if (m == 0) return KMP_OK;
-    if (!d_pk) return KMP_EINVAL;
-    kmp_postings_stats s{};
-    const int rc = tail(ws, d_pk, m, n, min_shared < 1 ? 1 : min_shared, d_p, d_q, d_w, cap, n_edges, &s,
-                        as_stream(stream));
-    if (n_pairs) *n_pairs = s.pairs;
-    return rc;
-}
-
-// ------------------------------------------------ multi-GPU split, fixed-capacity exchanges ----
-// No host synchronisation: every exchange buffer holds `parts` regions of `cap` keys, the unused
-// tail of each region is kNoKey (it sorts after every real key in every stage), and overflow or
-// fallback conditions accumulate in the caller's device flags (read once per step):
-//   flags[0] a part exceeded its region (rerun with cap >= flags[4] / flags[6])
-//   flags[1] a class id wider than the key's class field (needs the single-GPU flat layout)
-//   flags[2] a bucket or k-mer group too large for LDS (needs the single-GPU flat layout)
-//   flags[3] a pair-key shard region overflowed (rerun with shard_cap >= flags[5])
-//   flags[4] largest key part, flags[5] largest shard, flags[6] largest pair-key part
-
-// region d of `send` <- sorted[bounds[d], bounds[d+1]), padded with kNoKey
-__global__ void route_kernel(const unsigned long long* __restrict__ sorted,
-                             const unsigned long long* __restrict__ bounds, uint64_t cap,
-                             unsigned long long* __restrict__ send, uint32_t* __restrict__ flags, int max_slot) {
-    const uint32_t d = blockIdx.y;
-    const unsigned long long b0 = bounds[d], cnt = bounds[d + 1] - b0;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        atomicMax(&flags[max_slot], (uint32_t)min(cnt, 0xFFFFFFFFull));
-        if (cnt > cap) atomicOr(&flags[0], 1u);
+int kmp_dev_pairs_rows(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
+                       uint32_t n, int k, uint64_t slots, uint32_t heavy_df, uint32_t min_shared,
+                       int require_class_diff, uint32_t row_lo, uint32_t row_hi, uint32_t* d_p, uint32_t* d_q,
+                       uint32_t* d_w, uint64_t cap, uint64_t* n_edges, kmp_postings_stats* stats, void* stream) {
+    if (row_lo > row_hi || row_hi > n) return KMP_EINVAL;
+    if (row_lo == row_hi) {
+        int rc = postings_args(ws, k, n_edges, stats, d_p, d_q, d_w, cap);
+        return rc;
     }
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * blockDim.x)
-        send[d * cap + i] = i < cnt ? sorted[b0 + i] : kNoKey;
+    return residues_impl(ws, d_res, d_res_off, d_class, n, k, slots, heavy_df, min_shared, require_class_diff, true,
+                         row_lo, row_hi, d_p, d_q, d_w, cap, n_edges, stats, stream);
 }
 
-// Partition into `parts` padded regions without sorting.  Destination of a key:
-//   kPairs == false (k-mer keys):  bucket = key >> shift, valid iff bucket < total,
-//                                  dest = bucket * parts / total (contiguous bucket ranges);
-//   kPairs == true  (pair keys):   valid iff key != kNoKey, p = key >> shift, dest = the row range
-//                                  [rows[d], rows[d+1]) holding p (contiguous row ranges, so the
-//                                  rank-order concatenation stays canonical).
-// Each workgroup ranks its 4096 keys per destination in LDS and reserves one range per
-// destination on dcursor[d]; pad_regions_kernel then fills the tails and raises the flags.
-}  // extern "C"
-namespace {
-constexpr int kPartThreads = 256, kPartIPT = 16, kPartMax = 64;
-struct RowSplit {
-    uint32_t start[kPartMax + 1];  // row range d = [start[d], start[d+1])
-};
-template <bool kPairs>
-__global__ __launch_bounds__(kPartThreads) void partition_kernel(const unsigned long long* __restrict__ in,
-                                                                 uint64_t m, unsigned shift, unsigned long long total,
-                                                                 uint32_t parts, uint64_t cap,
-                                                                 unsigned long long* __restrict__ send,
-                                                                 unsigned long long* __restrict__ dcursor,
-                                                                 RowSplit rows) {
-    __shared__ uint32_t lcnt[kPartMax];
-    __shared__ unsigned long long base[kPartMax];
-    const int tid = threadIdx.x;
-    const uint64_t c0 = blockIdx.x * (uint64_t)(kPartThreads * kPartIPT);
-    if (tid < kPartMax) lcnt[tid] = 0;
-    __syncthreads();
-    unsigned long long x[kPartIPT];
-    uint32_t dr[kPartIPT];  // dest << 24 | rank, or ~0 for padding
-#pragma unroll
-    for (int j = 0; j < kPartIPT; ++j) {
-        const uint64_t i = c0 + (uint64_t)j * kPartThreads + tid;
-        x[j] = i < m ? in[i] : kNoKey;
-        dr[j] = ~0u;
-        bool valid;
-        unsigned long long v;
-        if (kPairs) {
-            valid = x[j] != kNoKey;
-            v = valid ? x[j] >> shift : 0;
-        } else {
-            v = x[j] >> shift;
-            valid = i < m && v < total;
-        }
-        if (valid) {
-            uint32_t d;
-            if (kPairs) {
-                d = 0;
-                while (d + 1 < parts && v >= rows.start[d + 1]) ++d;
-            } else {
-                d = (uint32_t)(v * parts / total);
-            }
-            dr[j] = (d << 24) | atomicAdd(&lcnt[d], 1u);
-        }
-    }
-    __syncthreads();
-    if (tid < (int)parts) base[tid] = lcnt[tid] ? atomicAdd(&dcursor[tid], (unsigned long long)lcnt[tid]) : 0ull;
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kPartIPT; ++j) {
-        if (dr[j] == ~0u) continue;
-        const uint32_t d = dr[j] >> 24;
-        const unsigned long long pos = base[d] + (dr[j] & 0xFFFFFFu);
-        if (pos < cap) send[d * cap + pos] = x[j];
-    }
-}
-
-// keys of chunk slots computed with the rolling chunk kernel (as bp_scatter1) and routed to
-// their destination (contiguous bucket ranges of `parts`) in the same pass: per chunk, ranks per
-// destination in LDS, one reservation per destination on dcursor[d], runs of ~4096/parts keys
-__global__ __launch_bounds__(kKeyThreads) void route_keys_kernel(
-    const uint8_t* __restrict__ res, const uint64_t* __restrict__ res_off, const uint16_t* __restrict__ cls, int k,
-    uint32_t p_hi, uint64_t slot_begin, uint64_t slot_end, const uint32_t* __restrict__ chunk_first, Layout lay,
-    uint32_t pw21, uint32_t parts, uint64_t cap, unsigned long long* __restrict__ send,
-    unsigned long long* __restrict__ dcursor, uint32_t* __restrict__ flags) {
-    __shared__ KeyChunk s;
-    __shared__ uint32_t lcnt[kPartMax];
-    __shared__ unsigned long long base[kPartMax];
-    const int tid = threadIdx.x;
-    const uint64_t c0 = slot_begin + (uint64_t)blockIdx.x * kKeyChunk;
-    const uint64_t c1 = min(c0 + kKeyChunk, slot_end);
-    if (tid < kPartMax) lcnt[tid] = 0;
-    const uint32_t first = chunk_first[blockIdx.x];
-    key_chunk_load(s, res, res_off, cls, k, p_hi, c0, c1, first, lay, flags);
-    unsigned long long x[kBpPer];
-    uint32_t dr[kBpPer];  // dest << 24 | rank, ~0 for no key
-    const unsigned bs = 32 - lay.bbits;  // bucket = h >> bs
-    const uint64_t nb = 1ull << lay.bbits;
-    key_chunk_run<kBpPer>(s, tid * kBpPer, (uint32_t)(c1 - c0), k, pw21, first, lay,
-                          [&](uint32_t e, bool valid, uint32_t h, unsigned long long lo) {
-                              x[e] = ((unsigned long long)h << lay.hshift) | lo;
-                              dr[e] = ~0u;
-                              if (valid) {
-                                  const uint32_t d = (uint32_t)((uint64_t)(h >> bs) * parts / nb);
-                                  dr[e] = (d << 24) | atomicAdd(&lcnt[d], 1u);
-                              }
-                          });
-    __syncthreads();
-    if (tid < (int)parts) base[tid] = lcnt[tid] ? atomicAdd(&dcursor[tid], (unsigned long long)lcnt[tid]) : 0ull;
-    __syncthreads();
-#pragma unroll
-    for (uint32_t e = 0; e < kBpPer; ++e) {
-        if (dr[e] == ~0u) continue;
-        const uint32_t d = dr[e] >> 24;
-        const unsigned long long pos = base[d] + (dr[e] & 0xFFFFFFu);
-        if (pos < cap) send[d * cap + pos] = x[e];
-    }
-}
-
-}  // namespace
-extern "C" {
-
-// Row ranges of the multi-GPU pair split: a pair belongs to its smaller protein, so row p owns
+// Row ranges of a split of the pair space: a pair belongs to its smaller protein, so row p owns
 // about N - p pairs; range d starts at N * (1 - sqrt(1 - d/parts)) (equal expected pair counts).
 void kmp_row_split(uint32_t n, uint32_t parts, uint32_t* start) {
     for (uint32_t d = 0; d <= parts; ++d) {
@@ -3243,271 +2967,6 @@ void kmp_row_split(uint32_t n, uint32_t parts, uint32_t* start) {
     }
 }
 
-// region tails -> kNoKey; largest region -> flags[max_slot], overflow -> flags[0]
-__global__ void pad_regions_kernel(unsigned long long* __restrict__ send, uint64_t cap,
-                                   const unsigned long long* __restrict__ dcursor, uint32_t* __restrict__ flags,
-                                   int max_slot) {
-    const uint32_t d = blockIdx.y;
-    const unsigned long long cnt = dcursor[d];
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        atomicMax(&flags[max_slot], (uint32_t)min(cnt, 0xFFFFFFFFull));
-        if (cnt > cap) atomicOr(&flags[0], 1u);
-    }
-    for (uint64_t i = cnt + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap;
-         i += (uint64_t)gridDim.x * blockDim.x)
-        send[d * cap + i] = kNoKey;
-}
-
-// largest shard cursor -> flags[5]; overflow -> flags[3]
-__global__ void check_shards_kernel(const unsigned long long* __restrict__ cursor, uint64_t shard_cap,
-                                    uint32_t* __restrict__ flags) {
-    const unsigned long long c = cursor[threadIdx.x];
-    atomicMax(&flags[5], (uint32_t)min(c, 0xFFFFFFFFull));
-    if (c > shard_cap) atomicOr(&flags[3], 1u);
-}
-
-// copies flags[0] (bucket overflow of the bucket kernels) into flags[2]
-__global__ void bucket_flag_kernel(uint32_t* __restrict__ ws_flags, uint32_t* __restrict__ flags) {
-    if (ws_flags[0]) atomicOr(&flags[2], 1u);
-    if (ws_flags[1]) atomicOr(&flags[1], 1u);
-}
-
-// edge count of an encoded run list whose last run may be the kNoKey padding
-__global__ void run_count_kernel(const unsigned long long* __restrict__ uniq, const uint32_t* __restrict__ nuniq,
-                                 unsigned long long* __restrict__ count) {
-    const uint32_t u = *nuniq;
-    *count = u && uniq[u - 1] == kNoKey ? u - 1 : u;
-}
-
 }  // extern "C"
-
-template <class Cfg = SortCfg>
-static int sort_keys(kmp_postings* ws, const unsigned long long* in, unsigned long long* out, uint64_t m,
-                     unsigned lo, unsigned hi, hipStream_t st) {
-    size_t t = 0;
-    PG(rocprim::radix_sort_keys<Cfg>(nullptr, t, in, out, (size_t)m, lo, hi, st));
-    PG(ws->tmp.reserve(std::max(t, ws->tmp.n)));
-    PG(rocprim::radix_sort_keys<Cfg>(ws->tmp.p, t, in, out, (size_t)m, lo, hi, st));
-    return KMP_OK;
-}
-
-extern "C" {
-
-int kmp_dev_keys_route(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
-                       uint32_t n, int k, uint64_t slots, uint32_t lo, uint32_t hi, uint64_t slot_lo, uint64_t slot_hi,
-                       uint32_t parts, uint64_t cap, unsigned long long* d_send, uint32_t* d_flags, void* stream) {
-    if (!ws || !d_send || !d_flags || parts < 1 || parts > (uint32_t)kPartMax || cap < 1 || k < 1 || k > kMaxK ||
-        lo > hi || hi > n ||
-        slot_hi < slot_lo)
-        return KMP_EINVAL;
-    const Layout lay = make_layout(n, k, slots, true);
-    if (!lay.bucketed) return KMP_ESTATE;
-    hipStream_t st = as_stream(stream);
-    const uint64_t m = slot_hi - slot_lo;
-    PG(ws->bstats.reserve(std::max<uint64_t>(ws->bstats.n, kShards * 8 + kShards + parts + 1)));
-    unsigned long long* d_b = ws->bstats.p + kShards * 8 + kShards;
-    if (m == 0 || hi == lo) {
-        PG(hipMemsetAsync(d_b, 0, (parts + 1) * sizeof(unsigned long long), st));
-        pad_regions_kernel<<<dim3(route_blocks(cap), parts), 256, 0, st>>>(d_send, cap, d_b, d_flags, 4);
-        return KMP_OK;
-    }
-    PG(ws->flags.reserve(4));
-    PG(hipMemsetAsync(ws->flags.p, 0, 4 * sizeof(uint32_t), st));
-    unsigned long long* dcur = d_b;  // parts destination cursors
-    PG(hipMemsetAsync(dcur, 0, parts * sizeof(unsigned long long), st));
-    // keys computed and routed in one pass (no key array)
-    const uint32_t g = (uint32_t)((m + kKeyChunk - 1) / kKeyChunk);
-    PG(ws->chunk_first.reserve(g + 1));
-    chunk_first_kernel<<<(hi - lo + 1 + 255) / 256, 256, 0, st>>>(d_res_off, lo, hi, slot_lo, slot_hi, g,
-                                                                  ws->chunk_first.p);
-    route_keys_kernel<<<g, kKeyThreads, 0, st>>>(d_res, d_res_off, d_class, k, hi, slot_lo, slot_hi,
-                                                  ws->chunk_first.p, lay, (uint32_t)pow21(k - 1), parts, cap, d_send,
-                                                  dcur, ws->flags.p);
-    pad_regions_kernel<<<dim3(route_blocks(cap), parts), 256, 0, st>>>(d_send, cap, dcur, d_flags, 4);
-    bucket_flag_kernel<<<1, 1, 0, st>>>(ws->flags.p, d_flags);
-    PG(hipGetLastError());
-    return KMP_OK;
-}
-
-int kmp_dev_pairs_route(kmp_postings* ws, const unsigned long long* d_keys, uint64_t m, uint32_t n, int k,
-                        uint64_t slots, uint32_t heavy_df, int require_class_diff, uint64_t shard_cap, uint32_t part,
-                        uint32_t parts, uint64_t cap, unsigned long long* d_send, uint32_t* d_flags,
-                        kmp_postings_stats* stats, void* stream) {
-    if (!ws || !d_send || !d_flags || parts < 1 || parts > (uint32_t)kPartMax || part >= parts || cap < 1 ||
-        shard_cap < 1 || k < 1 || k > kMaxK)
-        return KMP_EINVAL;
-    if (stats) *stats = kmp_postings_stats{};
-    const Layout lay = make_layout(n, k, slots, true);
-    if (!lay.bucketed) return KMP_ESTATE;
-    hipStream_t st = as_stream(stream);
-    if (heavy_df < 2) heavy_df = 2;
-    PG(ws->flags.reserve(4));
-    PG(hipMemsetAsync(ws->flags.p, 0, 4 * sizeof(uint32_t), st));
-    // group + expand (the fused path's kernels, no read-back): the received keys grouped by
-    // bucket with the counting partition (level 1 from the array, then level 2)
-    const uint32_t nb = 1u << lay.bbits;
-    PG(ws->sorted.reserve(std::max<uint64_t>(1, m)));
-    PG(ws->cnt.reserve(2 * (uint64_t)nb + 2));
-    // this part's bucket range (the keys routed here hold no others)
-    const uint32_t b0 = (uint32_t)(((uint64_t)part * nb + parts - 1) / parts);
-    const uint32_t b1 = (uint32_t)(((uint64_t)(part + 1) * nb + parts - 1) / parts);
-    if (m) {
-        const unsigned d2 = lay.bbits / 2;  // bp_digits: coarse bin = bucket >> d2
-        const uint32_t bins = b1 > b0 ? ((b1 - 1) >> d2) - (b0 >> d2) + 1 : 1u;
-        PG(bp_level1_array(ws, d_keys, m, lay, bins, st));
-        int rc = bp_level2(ws, lay, st);
-        if (rc != KMP_OK) return rc;
-    } else {
-        PG(hipMemsetAsync(ws->cnt.p, 0, (nb + 1) * sizeof(uint32_t), st));
-    }
-    PG(ws->bstats.reserve(std::max<uint64_t>(ws->bstats.n, kShards * 8 + kShards + parts + 1)));
-    uint32_t* bstart = ws->cnt.p;
-    uint32_t* list = ws->cnt.p + nb + 1;
-    uint32_t* list_count = ws->flags.p + 2;
-    unsigned long long* gstats = ws->bstats.p;
-    unsigned long long* cursor = gstats + kShards * 8;
-    unsigned long long* d_b = cursor + kShards;
-    const uint64_t total = shard_cap * kShards;
-    PG(ws->inc_sorted.reserve(total));
-    PG(ws->inc.reserve(total));
-    PG(hipMemsetAsync(gstats, 0, (kShards * 8 + kShards) * sizeof(unsigned long long), st));
-    PShard ps{};
-    const unsigned pbits = bits_for(n);
-    const uint32_t mul = 1u << pbits;  // pair keys p << pbits | q (kmp_dev_edges_rows)
-    if (b1 > b0)
-        launch_bucket_small<false>(b1 - b0, st, ws->sorted.p, bstart, lay, mul, require_class_diff, heavy_df,
-                                   ws->inc_sorted.p, shard_cap, cursor, gstats, ws->flags.p, list, list_count, ps, b0);
-    bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeTab, false>
-        <<<256, kBucketLargeThreads, 0, st>>>(ws->sorted.p, bstart, lay, mul, require_class_diff, heavy_df,
-                                              ws->inc_sorted.p, shard_cap, cursor, gstats, ws->flags.p, list,
-                                              list_count, ps);
-    check_shards_kernel<<<1, kShards, 0, st>>>(cursor, shard_cap, d_flags);
-    bucket_flag_kernel<<<1, 1, 0, st>>>(ws->flags.p, d_flags);
-    pad_shards_kernel<<<dim3(route_blocks(shard_cap), kShards), 256, 0, st>>>(ws->inc_sorted.p, shard_cap, cursor);
-    // pair keys routed by row range (no sort: every receiver sorts its runs)
-    PG(hipMemsetAsync(d_b, 0, parts * sizeof(unsigned long long), st));
-    RowSplit rows{};
-    kmp_row_split(n, parts, rows.start);
-    partition_kernel<true><<<(uint32_t)((total + 4095) / 4096), kPartThreads, 0, st>>>(
-        ws->inc_sorted.p, total, pbits, n, parts, cap, d_send, d_b, rows);
-    pad_regions_kernel<<<dim3(route_blocks(cap), parts), 256, 0, st>>>(d_send, cap, d_b, d_flags, 6);
-    PG(hipGetLastError());
-    return KMP_OK;
-}
-
-}  // extern "C"
-static int edges_route_impl(kmp_postings* ws, const unsigned long long* d_pk, uint64_t m, uint32_t n, uint32_t* d_p,
-                            uint32_t* d_q, uint32_t* d_w, uint32_t stride, uint64_t cap,
-                            unsigned long long* d_count, void* stream) {
-    if (!ws || !d_count || (m && (!d_pk || !d_p || !d_q || !d_w))) return KMP_EINVAL;
-    hipStream_t st = as_stream(stream);
-    if (m == 0) {
-        PG(hipMemsetAsync(d_count, 0, sizeof(unsigned long long), st));
-        return KMP_OK;
-    }
-    PG(ws->inc_sorted.reserve(m));
-    PG(ws->uniq.reserve(m));
-    PG(ws->w.reserve(m));
-    PG(ws->small.reserve(16));
-    const unsigned pbits = bits_for(n), pair_bits = 2 * pbits;  // keys p << pbits | q (kmp_dev_pairs_route)
-    int rc = sort_keys<PairSortCfg>(ws, d_pk, ws->inc_sorted.p, m, 0, pair_bits, st);
-    if (rc != KMP_OK) return rc;
-    size_t t3 = 0;
-    PG(rocprim::run_length_encode(nullptr, t3, ws->inc_sorted.p, (unsigned int)m, ws->uniq.p, ws->w.p,
-                                  ws->small.p + 1, st));
-    PG(ws->tmp.reserve(std::max(t3, ws->tmp.n)));
-    PG(rocprim::run_length_encode(ws->tmp.p, t3, ws->inc_sorted.p, (unsigned int)m, ws->uniq.p, ws->w.p,
-                                  ws->small.p + 1, st));
-    const uint32_t kb = (uint32_t)std::min<uint64_t>((m + 255) / 256, 8192);
-    emit_runs_kernel<<<kb, 256, 0, st>>>(ws->uniq.p, ws->w.p, ws->small.p + 1, 1u << pbits, d_p, d_q, d_w, cap,
-                                         stride);
-    run_count_kernel<<<1, 1, 0, st>>>(ws->uniq.p, ws->small.p + 1, d_count);
-    PG(hipGetLastError());
-    return KMP_OK;
-}
-
-extern "C" {
-
-int kmp_dev_edges_route(kmp_postings* ws, const unsigned long long* d_pk, uint64_t m, uint32_t n, uint32_t* d_p,
-                        uint32_t* d_q, uint32_t* d_w, uint64_t cap, unsigned long long* d_count, void* stream) {
-    return edges_route_impl(ws, d_pk, m, n, d_p, d_q, d_w, 1, cap, d_count, stream);
-}
-
-// Multi-GPU owner of rows [row_lo, row_hi): the row-block tail (§3.1.3) over its m received pair
-// keys (kNoKey padding skipped, no cursors), rows counted from row_lo.  A row block above the
-// LDS capacity leaves *d_count = KMP_EDGES_RETRY; the caller switches the workspace to the sort
-// tail (kmp_postings_set_rowtail(ws, 0)) and reruns.
-__global__ void rowtail_check_kernel(const uint32_t* __restrict__ flags, unsigned long long* __restrict__ d_count) {
-    if (flags[3]) *d_count = KMP_EDGES_RETRY;
-}
-
-int kmp_dev_edges_rows(kmp_postings* ws, const unsigned long long* d_pk, uint64_t m, uint32_t n, uint32_t row_lo,
-                       uint32_t row_hi, uint32_t* d_edges, uint64_t cap, unsigned long long* d_count,
-                       void* stream) {
-    if (!ws || !d_count || row_lo > row_hi || row_hi > n || (m && (!d_pk || !d_edges))) return KMP_EINVAL;
-    const unsigned pbits = bits_for(n);
-    const uint32_t rows = row_hi - row_lo;
-    uint32_t *d_p = d_edges, *d_q = d_edges + 1, *d_w = d_edges + 2;  // interleaved triples
-    if (!ws->pt_on || m == 0 || rows == 0 || m > 0xFFFFFFFFull)
-        return edges_route_impl(ws, d_pk, m, n, d_p, d_q, d_w, 3, cap, d_count, stream);
-    hipStream_t st = as_stream(stream);
-    PtGeom g{};
-    g.pbits = pbits;
-    // rows per block: an average of about a quarter of kPtCap keys (rows are skewed: a pair
-    // belongs to its smaller protein)
-    const double rpb = (double)(kPtCap / 4) * rows / (double)m;
-    unsigned rb = 0;
-    while (rb < 16 && (double)(2u << rb) <= rpb) ++rb;
-    rb = std::min(rb, ws->pt_rb_max);
-    while (rb < 16 && ((rows + (1ull << rb) - 1) >> rb) > kPtMaxBlocks) ++rb;
-    if (pbits + rb > 32) return edges_route_impl(ws, d_pk, m, n, d_p, d_q, d_w, 3, cap, d_count, stream);
-    g.rbits = rb;
-    g.nrb = (uint32_t)((rows + (1ull << rb) - 1) >> rb);
-    g.sc = m;
-    g.jt = (uint32_t)((m + kPtTile - 1) / kPtTile);
-    g.nshards = 1;
-    g.row0 = row_lo;
-    g.flat_n = m;
-    g.rank = ws->pt_rank;
-    hipError_t e = hipSuccess;
-    const PtBufs b = pt_bufs(ws, g, true, &e);
-    PG(e);
-    PG(ws->inc.reserve(m));
-    PG(ws->uniq.reserve(m));
-    PG(ws->w.reserve(m));
-    PG(ws->small.reserve(16));
-    PG(ws->flags.reserve(4));
-    PG(hipMemsetAsync(ws->flags.p, 0, 4 * sizeof(uint32_t), st));
-    uint32_t* keys32 = reinterpret_cast<uint32_t*>(ws->inc.p);
-    uint32_t* stage_p = reinterpret_cast<uint32_t*>(ws->uniq.p);
-    uint32_t* stage_q = stage_p + m;
-    pt_hist_kernel<<<dim3(g.jt, 1), kPtThreads, 0, st>>>(d_pk, nullptr, g, b.H);
-    bp_colsum_kernel<<<dim3(b.groups, (g.nrb + 255) / 256), 256, 0, st>>>(b.H, b.rows, g.nrb, b.R);
-    pt_colscan_kernel<<<1, kPtScanThreads, 0, st>>>(b.R, b.groups, g.nrb, b.bst, ws->small.p + 2);
-    bp_colprefix_kernel<<<dim3(b.groups, (g.nrb + 255) / 256), 256, 0, st>>>(b.H, b.rows, g.nrb, b.R, b.P);
-    pt_scatter_kernel<<<dim3(g.jt, 1), kPtThreads, 0, st>>>(d_pk, nullptr, g, b.P, keys32);
-    pt_reduce_kernel<<<g.nrb, kPtRThreads, 0, st>>>(keys32, b.bst, g, ws->flags.p, stage_p, stage_q, ws->w.p, b.counts);
-    pt_offsets_kernel<<<1, kPtScanThreads, 0, st>>>(b.counts, g.nrb, b.eoff, ws->small.p + 1, d_count);
-    pt_emit_kernel<<<g.nrb, 256, 0, st>>>(stage_p, stage_q, ws->w.p, b.bst, b.counts, b.eoff, d_p, d_q, d_w, cap, 3);
-    rowtail_check_kernel<<<1, 1, 0, st>>>(ws->flags.p, d_count);
-    PG(hipGetLastError());
-    return KMP_OK;
-}
-
-int kmp_postings_set_rowtail(kmp_postings* ws, int enable) {
-    if (!ws) return KMP_EINVAL;
-    ws->pt_on = enable != 0;
-    return KMP_OK;
-}
-
-int kmp_postings_set_rowrank(kmp_postings* ws, int enable) {
-    if (!ws) return KMP_EINVAL;
-    ws->pt_rank = enable != 0;
-    return KMP_OK;
-}
-
-}  // extern "C"
-
-
 
 #undef PG

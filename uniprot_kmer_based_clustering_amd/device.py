@@ -218,21 +218,6 @@ class DevicePipeline:
         """Postings key layout: bucketed (LDS group + expand per hash bucket) or flat."""
         check(lib().kmp_postings_set_layout(self._workspace(), int(bucketed)), "kmp_postings_set_layout")
 
-    def set_pshard(self, enable: bool = True) -> None:
-        """Bucketed layout: finish with the row-range (p-shard) LDS reduction (default) or the
-        global pair-key sort."""
-        check(lib().kmp_postings_set_pshard(self._workspace(), int(enable)), "kmp_postings_set_pshard")
-
-    def set_rowrank(self, enable: bool = True) -> None:
-        """Row-block tail: rank-sort short rows in LDS, or always use the block radix sort
-        (default: measured faster)."""
-        check(lib().kmp_postings_set_rowrank(self._workspace(), int(enable)), "kmp_postings_set_rowrank")
-
-    def set_partition(self, enable: bool = True) -> None:
-        """Residue path: group keys by bucket with the two-level counting partition (default) or
-        write every key and radix-sort the bucket field."""
-        check(lib().kmp_postings_set_partition(self._workspace(), int(enable)), "kmp_postings_set_partition")
-
     def set_graph(self, enable: bool = True) -> None:
         """Residue path: capture the single-synchronisation step as a HIP graph and replay it."""
         check(lib().kmp_postings_set_graph(self._workspace(), int(enable)), "kmp_postings_set_graph")
@@ -241,13 +226,41 @@ class DevicePipeline:
         return int(lib().kmp_postings_graph_replays(self._workspace()))
 
     def last_layout(self) -> str:
-        return "bucketed" if lib().kmp_postings_last_layout(self._workspace()) else "flat"
+        """Layout of the last postings call: 'bucketed' (LDS group + expand per hash bucket,
+        frequent k-mers on the heavy path) or 'flat' (the fallback for very wide class ids)."""
+        return "flat" if lib().kmp_postings_last_layout(self._workspace()) == _lib.KMP_LAYOUT_FLAT else "bucketed"
+
+    def last_heavy(self) -> bool:
+        """Whether the last call spilled frequent k-mers (df > 128) to the heavy path."""
+        return lib().kmp_postings_last_layout(self._workspace()) == _lib.KMP_LAYOUT_BUCKETED_HEAVY
 
     def last_tail(self) -> str:
-        """How the last postings call reduced its pair keys: 'rows' (bucketed, one host
-        synchronisation, row-block LDS sort tail), 'fused' (the same step with the global pair-key
-        sort tail), 'pshard' (row-range LDS reduction) or 'sort' (gathered pair-key sort)."""
-        return {4: "rows", 3: "fused", 2: "pshard"}.get(lib().kmp_postings_last_layout(self._workspace()), "sort")
+        """How the last postings call reduced its pair keys: 'rows' (row-block LDS sort tail,
+        bucketed layout) or 'sort' (global pair-key sort, flat layout)."""
+        return "sort" if self.last_layout() == "flat" else "rows"
+
+    def overflow_blocks(self) -> int:
+        """Row blocks of the last call above the LDS capacity (finished by the segmented sort)."""
+        return int(lib().kmp_postings_last_overflow_blocks(self._workspace()))
+
+    def rows(self, row_lo: int, row_hi: int, min_shared: int = 1, require_class_diff: bool = True,
+             heavy_df: int = 0xFFFFFFFF) -> int:
+        """Edges of rows [row_lo, row_hi) only (kmp_dev_pairs_rows), canonical, into ep/eq/ew."""
+        ws = self._workspace()
+        slots = int(lib().kmp_set_capacity(self.n, self.total))
+        for _ in range(2):
+            ne = C.c_uint64()
+            st = lib().kmp_dev_pairs_rows(ws, _p(self.res), _p(self.off), _p(self.cls), self.n, self.k, slots,
+                                          heavy_df, min_shared, int(require_class_diff), row_lo, row_hi,
+                                          _p(self.ep), _p(self.eq), _p(self.ew), self.edge_cap, C.byref(ne),
+                                          C.byref(self.postings_stats), _stream())
+            if st == _lib.KMP_EOVERFLOW:
+                self._alloc_edges(ne.value + ne.value // 8 + 1024)
+                continue
+            check(st, "kmp_dev_pairs_rows")
+            self.n_edges = ne.value
+            return self.n_edges
+        raise RuntimeError("edge count unstable across reruns")
 
     def postings(self, min_shared: int = 1, require_class_diff: bool = True,
                  heavy_df: int = 0xFFFFFFFF, from_residues: bool = False) -> int:
