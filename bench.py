@@ -27,10 +27,34 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 
 CONFIGS = {
-    # name: (N, seed, length law, k)
+    # name: (N, seed, length law, k); N = 0: the reference's own dataset (uniprot_arg.fasta)
     "config3": (100_000, 3, 0, 7),
     "config2": (10_000, 2, 0, 7),
+    "config1": (0, 0, 0, 5),
 }
+WORKLOADS = {
+    "config3": "config3: N=100000, seed=3, len~N(300,30^2), k=7",
+    "config2": "config2: N=10000, seed=2, len~N(300,30^2), k=7",
+    "config1": "config1: uniprot_arg.fasta (the reference's dataset, 10619 proteins), k=5",
+}
+
+
+def load_batch(name):
+    """The config's batch: synthetic (SURVEY.md §8d generator) or the reference's FASTA through
+    the library's own ingest (kmp_read_fasta)."""
+    import gzip
+    import tempfile
+
+    import uniprot_kmer_based_clustering_amd as K
+    n, seed, law, _ = CONFIGS[name]
+    if n:
+        return K.synth(n, seed, law)
+    with gzip.open(os.path.join(ROOT, "tests", "golden", "uniprot_arg.fasta.gz"), "rb") as f:
+        raw = f.read()
+    with tempfile.NamedTemporaryFile(suffix=".fasta") as t:
+        t.write(raw)
+        t.flush()
+        return K.read_fasta(t.name)
 
 
 def parse():
@@ -45,20 +69,36 @@ def parse():
     return ap.parse_args()
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(proteins, k, threads):
     """The reference algorithm restated in C (oracle/: windows, per-protein sort + dedup, df,
     Σ C(df,2) posting-list expansion, class filter, per-pair collapse), timed on this host over
-    the full workload (about 1 s at 16 threads)."""
+    the full workload: once single-threaded (the reference's threads = 1, run.sh's plumbing
+    config) and once on `threads` cores.  `value` is the multi-core run."""
     from oracle.oracle import Oracle
-    t0 = time.perf_counter()
-    o = Oracle(proteins.residues, proteins.offsets, proteins.class_id, k=k, threads=threads)
-    p, _, _ = o.pairs()
-    dt = time.perf_counter() - t0
     n = proteins.n
+    runs = {}
+    for t in (1, threads):
+        t0 = time.perf_counter()
+        o = Oracle(proteins.residues, proteins.offsets, proteins.class_id, k=k, threads=t)
+        p, _, _ = o.pairs()
+        runs[t] = (time.perf_counter() - t0, int(len(p)))
+    dt, ne = runs[threads]
     return {"value": n * (n - 1) / 2 / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
             "sample": f"full workload ({n} proteins, k={k}): windows, K(p) sort+dedup, df, Σ C(df,2) "
-                      f"posting-list expansion, class filter, per-pair collapse; one run, {dt:.2f} s",
-            "seconds": dt, "edges": int(len(p))}
+                      f"posting-list expansion, class filter, per-pair collapse; one run per thread count",
+            "seconds": dt, "edges": ne,
+            "single_thread": {"value": n * (n - 1) / 2 / runs[1][0], "seconds": runs[1][0], "cores": 1},
+            "nproc": os.cpu_count(), "cpu_model": cpu_model()}
 
 
 # names of the six stage-timing slots (kmp_postings_stats.stage_ms) per tail
@@ -145,15 +185,16 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    n, seed, law, k = CONFIGS[args.config]
-    proteins = K.synth(n, seed, law)
+    _, seed, law, k = CONFIGS[args.config]
+    proteins = load_batch(args.config)
+    n = proteins.n
     pipe = DevicePipeline(proteins, k, f"cuda:{local}")
     torch.cuda.synchronize()
     postings = args.engine in ("residues", "postings")
 
     def one_step():
         if world > 1:
-            return distributed_step(pipe, rank, world, engine=args.engine)
+            return distributed_step(pipe, rank, world)
         return pipe.step(engine=args.engine)
 
     stage_sum = None
@@ -187,6 +228,7 @@ def main():
     if rank == 0:
         out = {
             "metric": "protein pairs/sec (+ edges/sec), 100k x 300aa synthetic, k=7",
+            # config1 / config2 lines are extra workloads of the same metric (named in config)
             "value": pairs_total / (dt / args.steps),
             "unit": "pairs/s",
             "n_gpus": world,
@@ -197,13 +239,18 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "u32",
-            "data": "synthetic (SURVEY.md §8d generator, seeded; protein families, 15 AMR classes)",
-            "config": {"workload": f"{args.config}: N={n}, seed={seed}, len~N(300,30^2), k={k}",
+            "data": ("synthetic (SURVEY.md §8d generator, seeded; protein families, 15 AMR classes)"
+                     if CONFIGS[args.config][0] else "uniprot_arg.fasta (the reference's dataset)"),
+            "config": {"workload": WORKLOADS[args.config],
                        "proteins": n, "k": k, "pairs": int(pairs_total), "edges": int(n_edges),
                        "engine": args.engine,
-                       "parallelism": "single GPU" if world == 1 else f"k-mer buckets x{world}"},
+                       "parallelism": "single GPU" if world == 1 else f"row split x{world}"},
             "edges_per_s": n_edges / (dt / args.steps),
         }
+        if args.engine in ("residues", "postings"):
+            out["config"]["layout"] = pipe.last_layout()
+            out["config"]["heavy_path"] = pipe.last_heavy()
+            out["config"]["row_overflow_blocks"] = pipe.overflow_blocks()
         if stage_sum is not None:
             ps = pipe.postings_stats.as_dict()
             slots = int(_lib.lib().kmp_set_capacity(n, int(proteins.offsets[-1])))

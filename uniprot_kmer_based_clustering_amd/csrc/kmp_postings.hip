@@ -1147,9 +1147,12 @@ __global__ __launch_bounds__(kHvI) void heavy_expand_kernel(const uint32_t* __re
 #endif
 constexpr int kSmallGeom[3] = {KMP_SMALL_GEOM};
 constexpr int kBucketSmallCap = kSmallGeom[0], kBucketSmallThreads = kSmallGeom[1], kBucketSmallTab = kSmallGeom[2];
-constexpr int kBucketLargeCap = 8192, kBucketLargeThreads = 1024, kBucketLargeTab = 13;
-// the large kernel grid-strides the (usually empty or short) list of large buckets
-constexpr int kBucketLargeGrid = 32;
+// larger buckets (up to 4,096 keys: four per thread, no register spills) take the large kernel;
+// above that the whole bucket goes to the heavy path
+constexpr int kBucketLargeCap = 4096, kBucketLargeThreads = 1024, kBucketLargeTab = 12;
+// the large kernel grid-strides the list of large buckets (usually empty at config 3; most
+// buckets of a k = 5 batch of real proteins): one workgroup per CU
+constexpr int kBucketLargeGrid = 256;
 
 // ------------------------------------------------------------- bucket partition ------------
 // The residue path groups its keys by bucket (the top bbits of h) with two counting passes
@@ -1597,7 +1600,9 @@ struct kmp_postings {
     Grow<uint32_t> bp;          // bucket partition: H1 | P1 | R | C1 | H2 (see bp_level1)
     Grow<uint32_t> pt;          // row-block tail (pt_bufs)
     Grow<uint32_t> ovf;         // listed row blocks | segment starts | segment ends
-    Grow<uint32_t> ks;          // their keys, sorted
+    Grow<unsigned long long> ovk;  // their keys tagged, sorted, encoded (pt_finish_overflow)
+    Grow<unsigned long long> ovx;  // per listed block: offset of its keys
+    Grow<uint32_t> ovr;            // run lengths, kept flags and positions, first run per block
     uint64_t pt_inc = 0;        // incidences of the last call (row-block sizing)
     unsigned pt_rb_max = 16;    // rows-per-block bound learned from overflowing row blocks
     uint32_t bp_J = 0;          // level-2 tiles per coarse bin ...
@@ -1625,9 +1630,9 @@ struct kmp_postings {
     hipEvent_t ev[KMP_POSTINGS_STAGES + 1] = {};
     ~kmp_postings() {
         for (auto* g : {&keys, &sorted, &inc, &inc_sorted, &uniq, &bstats, &btot, &boff, &spill, &hkeys, &hsorted,
-                        &hGS, &htc, &htoff, &hoff})
+                        &hGS, &htc, &htoff, &hoff, &ovk, &ovx})
             g->release();
-        for (auto* g : {&w, &keep, &pos, &small, &cnt, &flags, &chunk_first, &bp, &pt, &ovf, &ks, &hE, &hgi, &hcnt})
+        for (auto* g : {&w, &keep, &pos, &small, &cnt, &flags, &chunk_first, &bp, &pt, &ovf, &ovr, &hE, &hgi, &hcnt})
             g->release();
         tmp.release();
         for (auto& e : ev)
@@ -2085,60 +2090,68 @@ __global__ __launch_bounds__(kPtRThreads) void pt_reduce_kernel(const uint32_t* 
         pt_reduce_block<16>(u, u.s16, last, wave_tot, keys, r, s0, n, g, stage_p, stage_q, stage_w, counts);
 }
 
-// segment bounds of the listed (overflowing) row blocks, for the segmented sort
-__global__ void pt_ovf_segments_kernel(const uint32_t* __restrict__ ovf, uint32_t m, const uint32_t* __restrict__ bst,
-                                       uint32_t* __restrict__ sb, uint32_t* __restrict__ se) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= m) return;
-    sb[i] = bst[ovf[i]];
-    se[i] = bst[ovf[i] + 1];
+// Row blocks above kPtCap (listed by pt_reduce): their keys, tagged with the list index j as
+// j << kb | key (kb = pbits + rbits key bits), are sorted together by one device-wide radix
+// sort and run-length encoded; each run (one (p, q) pair of block ovf[j], length w) is staged at
+// its block's offset.  Every step is multi-workgroup, so one very long row (real data at k = 5:
+// a protein sharing 5-mers with thousands of later ones) costs a sort of its keys, not one
+// workgroup walking them.
+__global__ void pt_ovf_sizes_kernel(const uint32_t* __restrict__ ovf, uint32_t m, const uint32_t* __restrict__ bst,
+                                    unsigned long long* __restrict__ sz) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < m) sz[j] = bst[ovf[j] + 1] - bst[ovf[j]];
+    if (j == m) sz[m] = 0;
 }
 
-// one workgroup per listed block, its keys already sorted in ks: run starts into tmp (the
-// block's unsorted input, dead after the sort), then the runs with w >= min_shared staged
-constexpr uint32_t kOvfThreads = 1024;
-__global__ __launch_bounds__(kOvfThreads) void pt_ovf_rle_kernel(const uint32_t* __restrict__ ovf,
-                                                                 const uint32_t* __restrict__ bst, PtGeom g,
-                                                                 const uint32_t* __restrict__ ks,
-                                                                 uint32_t* __restrict__ tmp,
-                                                                 uint32_t* __restrict__ stage_p,
-                                                                 uint32_t* __restrict__ stage_q,
-                                                                 uint32_t* __restrict__ stage_w,
-                                                                 uint32_t* __restrict__ counts) {
-    __shared__ uint32_t wave_tot[kOvfThreads / 64];
-    const uint32_t r = ovf[blockIdx.x], s0 = bst[r], n = bst[r + 1] - s0;
-    uint32_t runs = 0;
-    for (uint32_t c = 0; c < n; c += kOvfThreads) {
-        const uint32_t i = c + threadIdx.x;
-        const bool h = i < n && (i == 0 || ks[s0 + i] != ks[s0 + i - 1]);
-        uint32_t x, t;
-        block_scan_n<kOvfThreads>(h, x, t, wave_tot);
-        if (h) tmp[s0 + runs + x] = i;
-        runs += t;
+// one workgroup per listed block: its keys, tagged, at xoff[j]
+__global__ __launch_bounds__(256) void pt_ovf_gather_kernel(const uint32_t* __restrict__ ovf,
+                                                            const uint32_t* __restrict__ bst,
+                                                            const unsigned long long* __restrict__ xoff,
+                                                            const uint32_t* __restrict__ keys, unsigned kb,
+                                                            unsigned long long* __restrict__ x) {
+    const uint32_t j = blockIdx.y, r = ovf[j], s0 = bst[r], n = bst[r + 1] - s0;
+    const unsigned long long tag = (unsigned long long)j << kb, o = xoff[j];
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) x[o + i] = tag | keys[s0 + i];
+}
+
+// per run: kept (w >= min_shared) -> keep[u]; a run of a new block records the block's first run
+__global__ void pt_ovf_keep_kernel(const unsigned long long* __restrict__ uniq, const uint32_t* __restrict__ w,
+                                   const uint32_t* __restrict__ nruns, unsigned kb, uint32_t min_shared,
+                                   uint32_t* __restrict__ keep, uint32_t* __restrict__ first) {
+    const uint32_t U = *nruns;
+    for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u <= U; u += gridDim.x * blockDim.x) {
+        if (u == U) {
+            keep[u] = 0;
+            continue;
+        }
+        keep[u] = w[u] >= min_shared;
+        const uint32_t j = (uint32_t)(uniq[u] >> kb);
+        if (u == 0 || (uint32_t)(uniq[u - 1] >> kb) != j) first[j] = u;
     }
-    __syncthreads();
+}
+
+// kept runs -> stage at the block's offset; counts[ovf[j]] = the block's kept runs
+__global__ void pt_ovf_stage_kernel(const uint32_t* __restrict__ ovf, uint32_t m, const uint32_t* __restrict__ bst,
+                                    PtGeom g, const unsigned long long* __restrict__ uniq,
+                                    const uint32_t* __restrict__ w, const uint32_t* __restrict__ nruns,
+                                    const uint32_t* __restrict__ kpos, const uint32_t* __restrict__ first,
+                                    uint32_t* __restrict__ stage_p, uint32_t* __restrict__ stage_q,
+                                    uint32_t* __restrict__ stage_w, uint32_t* __restrict__ counts) {
+    const uint32_t U = *nruns;
+    const unsigned kb = g.pbits + g.rbits;
     const uint32_t qm = (1u << g.pbits) - 1;
-    const uint32_t rowbase = g.row0 + (r << g.rbits);
-    uint32_t kept = 0;
-    for (uint32_t c = 0; c < runs; c += kOvfThreads) {
-        const uint32_t j = c + threadIdx.x;
-        uint32_t w = 0, key = 0;
-        if (j < runs) {
-            const uint32_t a = tmp[s0 + j];
-            w = (j + 1 < runs ? tmp[s0 + j + 1] : n) - a;
-            key = ks[s0 + a];
-        }
-        const bool keep = j < runs && w >= g.min_shared;
-        uint32_t x, t;
-        block_scan_n<kOvfThreads>(keep, x, t, wave_tot);
-        if (keep) {
-            stage_p[s0 + kept + x] = rowbase + (key >> g.pbits);
-            stage_q[s0 + kept + x] = key & qm;
-            stage_w[s0 + kept + x] = w;
-        }
-        kept += t;
+    for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < U; u += gridDim.x * blockDim.x) {
+        const unsigned long long x = uniq[u];
+        const uint32_t j = (uint32_t)(x >> kb), r = ovf[j];
+        const uint32_t f = first[j];
+        const uint32_t nxt = j + 1 < m ? first[j + 1] : U;  // every listed block holds a run
+        if (u == f) counts[r] = kpos[nxt] - kpos[f];
+        if (w[u] < g.min_shared) continue;
+        const uint32_t key = (uint32_t)x & ((1u << kb) - 1), o = bst[r] + kpos[u] - kpos[f];
+        stage_p[o] = g.row0 + (r << g.rbits) + (key >> g.pbits);
+        stage_q[o] = key & qm;
+        stage_w[o] = w[u];
     }
-    if (threadIdx.x == 0) counts[r] = kept;
 }
 
 // exclusive scan of the nrb run counts (nrb <= 8 * 1024) -> eoff; eoff[nrb] and *total = edges
@@ -2325,7 +2338,7 @@ int step_reserve(kmp_postings* ws, const StepCfg& c, const PtGeom& g) {
     PG(ws->uniq.reserve(total));  // ... staged p | q (u32 each)
     PG(ws->w.reserve(total));     // ... staged w
     PG(ws->spill.reserve(ws->spill_cap * kShards));
-    PG(ws->ovf.reserve(3 * (uint64_t)g.nrb + 3));
+    PG(ws->ovf.reserve((uint64_t)g.nrb + 1));
     if (!ws->hrb) PG(hipHostMalloc((void**)&ws->hrb, kRbWords * sizeof(unsigned long long), hipHostMallocCoherent));
     hipError_t e = hipSuccess;
     pt_bufs(ws, g, true, &e);
@@ -2379,8 +2392,8 @@ int enqueue_tail(kmp_postings* ws, const StepCfg& c, const PtGeom& g, hipStream_
     return KMP_OK;
 }
 
-// the listed row blocks (above kPtCap keys): one segmented radix sort, run-length encoding,
-// then offsets and emit again; host-synchronous, returns the edge count in *edges
+// the listed row blocks (above kPtCap keys): the composite sort + encode above, then offsets
+// and emit again; host-synchronous, returns the edge count in *edges
 int pt_finish_overflow(kmp_postings* ws, const StepCfg& c, const PtGeom& g, uint32_t m, uint64_t* edges,
                        hipStream_t st) {
     hipError_t e = hipSuccess;
@@ -2389,21 +2402,39 @@ int pt_finish_overflow(kmp_postings* ws, const StepCfg& c, const PtGeom& g, uint
     uint32_t* keys32 = reinterpret_cast<uint32_t*>(ws->inc.p);
     uint32_t* stage_p = reinterpret_cast<uint32_t*>(ws->uniq.p);
     uint32_t* stage_q = stage_p + total;
-    uint32_t* sb = ws->ovf.p + g.nrb + 1;
-    uint32_t* se = sb + g.nrb + 1;
-    PG(ws->ks.reserve(total));
-    pt_ovf_segments_kernel<<<(m + 255) / 256, 256, 0, st>>>(ws->ovf.p, m, b.bst, sb, se);
-    uint32_t nkeys = 0;
-    PG(hipMemcpyAsync(&nkeys, b.bst + g.nrb, 4, hipMemcpyDeviceToHost, st));
+    const unsigned kb = g.pbits + g.rbits, mb = bits_for((uint64_t)m + 1);
+    if (kb + mb > 63) return KMP_EINVAL;
+    PG(ws->ovx.reserve(m + 1));
+    unsigned long long* xoff = ws->ovx.p;
+    pt_ovf_sizes_kernel<<<(m + 256) / 256, 256, 0, st>>>(ws->ovf.p, m, b.bst, xoff);
+    size_t t0 = 0;
+    PG(rocprim::exclusive_scan(nullptr, t0, xoff, xoff, 0ull, (size_t)m + 1, rocprim::plus<unsigned long long>(), st));
+    PG(ws->tmp.reserve(std::max(t0, ws->tmp.n)));
+    PG(rocprim::exclusive_scan(ws->tmp.p, t0, xoff, xoff, 0ull, (size_t)m + 1, rocprim::plus<unsigned long long>(),
+                               st));
+    unsigned long long nx = 0;
+    PG(hipMemcpyAsync(&nx, xoff + m, 8, hipMemcpyDeviceToHost, st));
     PG(hipStreamSynchronize(st));
-    size_t tb = 0;
-    PG(rocprim::segmented_radix_sort_keys(nullptr, tb, keys32, ws->ks.p, (unsigned)nkeys, m, sb, se, 0u,
-                                          g.pbits + g.rbits, st));
-    PG(ws->tmp.reserve(std::max(tb, ws->tmp.n)));
-    PG(rocprim::segmented_radix_sort_keys(ws->tmp.p, tb, keys32, ws->ks.p, (unsigned)nkeys, m, sb, se, 0u,
-                                          g.pbits + g.rbits, st));
-    pt_ovf_rle_kernel<<<m, kOvfThreads, 0, st>>>(ws->ovf.p, b.bst, g, ws->ks.p, keys32, stage_p, stage_q, ws->w.p,
-                                                 b.counts);
+    if (nx > 0xFFFFFFFFull) return KMP_ENOMEM;
+    PG(ws->ovk.reserve(3 * nx + 1));  // tagged keys | sorted | runs
+    PG(ws->ovr.reserve(3 * (nx + 1) + m + 1));  // w | keep | kept positions | first run per block
+    unsigned long long *x = ws->ovk.p, *xs = x + nx, *uq = xs + nx;
+    uint32_t *rw = ws->ovr.p, *keep = rw + nx + 1, *kpos = keep + nx + 1, *first = kpos + nx + 1;
+    uint32_t* nruns = ws->small.p + 4;
+    const uint32_t gx = (uint32_t)std::min<unsigned long long>((nx / m + 255) / 256 + 1, 64);
+    pt_ovf_gather_kernel<<<dim3(gx, m), 256, 0, st>>>(ws->ovf.p, b.bst, xoff, keys32, kb, x);
+    size_t t1 = 0, t2 = 0, t3 = 0;
+    PG(rocprim::radix_sort_keys<SortCfg>(nullptr, t1, x, xs, (size_t)nx, 0u, kb + mb, st));
+    PG(rocprim::run_length_encode(nullptr, t2, xs, (unsigned)nx, uq, rw, nruns, st));
+    PG(rocprim::exclusive_scan(nullptr, t3, keep, kpos, 0u, (size_t)nx + 1, rocprim::plus<uint32_t>(), st));
+    PG(ws->tmp.reserve(std::max({t1, t2, t3, ws->tmp.n})));
+    PG(rocprim::radix_sort_keys<SortCfg>(ws->tmp.p, t1, x, xs, (size_t)nx, 0u, kb + mb, st));
+    PG(rocprim::run_length_encode(ws->tmp.p, t2, xs, (unsigned)nx, uq, rw, nruns, st));
+    const uint32_t gr = (uint32_t)std::min<unsigned long long>((nx + 256) / 256, 4096);
+    pt_ovf_keep_kernel<<<gr, 256, 0, st>>>(uq, rw, nruns, kb, g.min_shared, keep, first);
+    PG(rocprim::exclusive_scan(ws->tmp.p, t3, keep, kpos, 0u, (size_t)nx + 1, rocprim::plus<uint32_t>(), st));
+    pt_ovf_stage_kernel<<<gr, 256, 0, st>>>(ws->ovf.p, m, b.bst, g, uq, rw, nruns, kpos, first, stage_p, stage_q,
+                                            ws->w.p, b.counts);
     pt_offsets_kernel<<<1, kPtScanThreads, 0, st>>>(b.counts, g.nrb, b.eoff, ws->small.p + 1);
     pt_emit_kernel<<<g.nrb, 256, 0, st>>>(stage_p, stage_q, ws->w.p, b.bst, b.counts, b.eoff, c.d_p, c.d_q, c.d_w,
                                           c.cap, c.stride);
@@ -2645,10 +2676,10 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
         }
         if (ws->heavy) {
             if (spill_total) {
-                ws->mark(3, st);
                 int rc = heavy_phase(ws, c, spill_total, true, st);
                 if (rc != KMP_OK) return rc;
             }
+            ws->mark(3, st);
             step_pack_kernel<<<1, 256, 0, st>>>(ws->bstats.p, ws->flags.p, nullptr, ws->hrb);
             PG(hipStreamSynchronize(st));
             sum_stats(rb, acc, &most, &n_inc, &spill_most, &spill_total);
@@ -2664,7 +2695,6 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
             if (rc != KMP_OK) return rc;
             PG(hipStreamSynchronize(st));
         }
-        ws->shard_cap = std::max<uint64_t>(ws->shard_cap, most + most / 64 + 256);  // learned for the next call
         ws->pt_inc = n_inc;  // sizes the next call's row blocks
         uint64_t ne = rb[kRbRuns];
         ws->last_ovf = (uint32_t)rb[kRbOvf];
@@ -2683,6 +2713,7 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
                 fprintf(stderr, "kmp: %llu row blocks above %u keys (largest %llu) sorted apart; rbits bound %u\n",
                         rb[kRbOvf], kPtCap, rb[kRbMaxBlock], ws->pt_rb_max);
         }
+        ws->shard_cap = most + most / 64 + 256;  // learned for the next call (after the last use of this one)
         fill_stats(stats, acc);
         if (stats) {
             stats->incidences = n_inc;
