@@ -39,7 +39,7 @@ typedef enum {
     KMP_EINVAL = 1,     /* bad argument (reference: panic / expect) */
     KMP_ENOMEM = 2,     /* host or device allocation failed */
     KMP_EDEVICE = 3,    /* HIP runtime error or no usable gfx950 device */
-    KMP_ERCCL = 4,      /* reserved: collective failure reported by a multi-GPU host */
+    KMP_ERCCL = 4,      /* RCCL unavailable or a collective failed (multi-GPU context) */
     KMP_EOVERFLOW = 5,  /* caller buffer too small; *n holds the size needed */
     KMP_ESTATE = 6,     /* call out of order (e.g. kmp_pairs before kmp_load_proteins) */
     KMP_EIO = 7         /* file could not be read / written */
@@ -98,6 +98,19 @@ int kmp_version(void);                         /* KMP_ABI_VERSION */
 const char* kmp_status_string(int status);
 /* device: HIP ordinal; cpu_threads: host threads for ingest / planning (reference: `threads`, main.rs:57-60) */
 int kmp_ctx_create(kmp_ctx** ctx, int device, int cpu_threads);
+/* Multi-GPU context (the reference's `threads` split of the same work, main.rs:57-60,
+ * graph/mod.rs:81-124): n_gpus ranks on the HIP devices devices[0..n_gpus) (NULL: 0..n_gpus-1),
+ * rank 0 on devices[0] doing everything a single-GPU context does.  kmp_load_proteins copies the
+ * batch to every rank; kmp_pairs (engine AUTO / RESIDUES) splits the pair space by rows
+ * (kmp_row_split: rank g expands the pairs whose smaller protein is in its rows, on its own device
+ * and host thread) and gathers the ranks' edges to device 0 in rank order, which is the canonical
+ * list.  The library owns the collective: distinct devices get RCCL communicators created
+ * in-process (ncclCommInitAll; KMP_ERCCL if RCCL is unavailable or a collective fails); a device
+ * listed more than once runs several ranks on one GPU and the gather uses device copies (for
+ * testing the split where RCCL admits one rank per device).  Other engines run on rank 0. */
+int kmp_ctx_create_multi(kmp_ctx** ctx, int n_gpus, const int* devices, int cpu_threads);
+int kmp_ctx_gpus(const kmp_ctx* ctx);               /* ranks (1 for kmp_ctx_create) */
+const char* kmp_ctx_transport(const kmp_ctx* ctx);  /* "local", "copy" or "rccl" */
 void kmp_ctx_destroy(kmp_ctx* ctx);
 const char* kmp_last_error(const kmp_ctx* ctx);
 

@@ -1,0 +1,100 @@
+"""GPU parity of the multi-GPU row split behind the C ABI (kmp_ctx_create_multi): G virtual ranks
+on one GPU (each rank its own stream, workspace and copy of the batch, one host thread per
+rank; the gather over device copies — RCCL admits one rank per device), against the oracle,
+bit-exact, on config-3 / config-4's workload (100k proteins, seed 3, k = 7) and on the heavy
+k = 5 dataset; the RCCL transport itself over the one real device (G = 1 communicator)."""
+import numpy as np
+import pytest
+
+from common import edges_sha256, load_json, uniprot
+import uniprot_kmer_based_clustering_amd as K
+from uniprot_kmer_based_clustering_amd import _lib
+
+pytestmark = pytest.mark.gpu
+
+
+def assert_edges(e, p, q, w):
+    np.testing.assert_array_equal(e.p, p)
+    np.testing.assert_array_equal(e.q, q)
+    np.testing.assert_array_equal(e.w, w)
+
+
+@pytest.fixture(scope="module")
+def config4(oracle_mod):
+    b = K.synth(100000, 3)
+    p, q, w = oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=7, threads=16).pairs()
+    return b, (p, q, w)
+
+
+@pytest.mark.parametrize("g", [2, 4, 8])
+def test_virtual_ranks_config4(config4, g):
+    """Config 4's workload split over G in {2, 4, 8} ranks: the gathered list equals the
+    oracle's canonical list (and so the single-GPU one): invariant to the number of ranks."""
+    b, (p, q, w) = config4
+    with K.KmerPairEngine(0, 4, devices=[0] * g) as e:
+        assert e.gpus == g and e.transport == "copy"
+        e.load(b)
+        e.build_sets(7)
+        for _ in range(2):  # second call: learned capacities, same result
+            got = e.pairs()
+            assert len(got) == len(p) > 1_000_000
+            assert_edges(got, p, q, w)
+        c = e.counters()
+        assert c["n_edges"] == len(p)
+
+
+def test_virtual_ranks_heavy_uniprot_k5():
+    """The reference's dataset at k = 5 (frequent 5-mers: every rank runs the heavy path and
+    the row-tail overflow sort on its rows) over 3 ranks: golden edge sha."""
+    res, off, cls, _ = uniprot()
+    g = load_json("uniprot_counters.json")["5"]
+    with K.KmerPairEngine(0, 4, devices=[0, 0, 0]) as e:
+        e.load(K.Proteins(res, off, cls))
+        e.build_sets(5)
+        got = e.pairs()
+        assert len(got) == g["n_edges"]
+        assert edges_sha256(got.p, got.q, got.w) == g["edges_sha256"]
+        c = e.counters()
+        assert c["sum_w_diff"] == g["sum_w_diff"] and c["n_align"] == g["n_align"]
+
+
+def test_virtual_ranks_options_and_scores(oracle_mod):
+    """min_shared, the class filter off, and BLOSUM scores (computed on rank 0 over the
+    gathered list) through the split; more ranks than proteins leaves ranks empty."""
+    b = K.synth(3000, 5, 1)
+    o = oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=5, threads=8)
+    with K.KmerPairEngine(0, 2, devices=[0, 0, 0, 0]) as e:
+        e.load(b)
+        e.build_sets(5)
+        for ms, diff in ((1, True), (3, False)):
+            assert_edges(e.pairs(min_shared=ms, require_class_diff=diff),
+                         *o.pairs(min_shared=ms, require_class_diff=diff))
+        p, q, w = o.pairs()
+        got = e.pairs(score=_lib.KMP_SCORE_BLOSUM)
+        assert_edges(got, p, q, w)
+        np.testing.assert_array_equal(got.score, o.blosum_scores(p, q).astype(np.float32))
+    seqs = K.synth(5, 1)
+    with K.KmerPairEngine(0, 1, devices=[0] * 8) as e:
+        e.load(seqs)
+        e.build_sets(5)
+        o = oracle_mod.Oracle(seqs.residues, seqs.offsets, seqs.class_id, k=5)
+        assert_edges(e.pairs(require_class_diff=False), *o.pairs(require_class_diff=False))
+
+
+def test_rccl_transport_single_device(oracle_mod):
+    """A one-device multi context (G = 1: no gather) and the RCCL transport: distinct devices
+    make library-owned RCCL communicators (ncclCommInitAll); with one GPU only G = 1 runs."""
+    b = K.synth(2000, 7)
+    p, q, w = oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=7).pairs()
+    with K.KmerPairEngine(0, 1, devices=[0]) as e:
+        assert e.gpus == 1 and e.transport == "local"
+        e.load(b)
+        e.build_sets(7)
+        assert_edges(e.pairs(), p, q, w)
+    import torch
+    if torch.cuda.device_count() >= 2:
+        with K.KmerPairEngine(0, 1, devices=[0, 1]) as e:
+            assert e.transport == "rccl"
+            e.load(b)
+            e.build_sets(7)
+            assert_edges(e.pairs(), p, q, w)

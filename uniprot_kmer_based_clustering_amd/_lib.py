@@ -125,6 +125,9 @@ SIGNATURES = {
     "kmp_pair_col_window": (C.c_uint32, [P, C.c_uint32]),
     "kmp_dev_pairs_long": (C.c_int, [P, P, P, P, C.c_uint32, P, C.c_uint32, C.c_uint32, C.c_int,
                                      P, P, P, C.c_uint64, P, P]),
+    "kmp_ctx_create_multi": (C.c_int, [C.POINTER(P), C.c_int, C.POINTER(C.c_int), C.c_int]),
+    "kmp_ctx_gpus": (C.c_int, [P]),
+    "kmp_ctx_transport": (C.c_char_p, [P]),
     "kmp_postings_create": (C.c_int, [C.POINTER(P)]),
     "kmp_postings_destroy": (None, [P]),
     "kmp_dev_pairs_postings": (C.c_int, [P, P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32,

@@ -10,6 +10,7 @@
 #include <memory>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "kmerpair.h"
@@ -17,6 +18,7 @@
 #include "kmp_edges.hpp"
 #include "kmp_internal.hpp"
 #include "kmp_mphf.hpp"
+#include "kmp_multi.hpp"
 
 using namespace kmp;
 
@@ -52,6 +54,31 @@ struct DevBuf {
 };
 
 }  // namespace
+
+// one rank of a multi-GPU context: its device, stream, workspace and pair buffers; ranks
+// other than 0 also hold their copy of the packed batch (rank 0 uses the context's)
+struct kmp_rank {
+    int device = 0;
+    hipStream_t stream = nullptr;  // rank 0: the context's
+    bool own_stream = false;
+    DevBuf res, off, cls, ep, eq, ew;
+    uint64_t cap = 0;
+    kmp_postings* ws = nullptr;
+    ~kmp_rank() {
+        (void)hipSetDevice(device);
+        if (own_stream && stream) {
+            (void)hipStreamSynchronize(stream);
+            (void)hipStreamDestroy(stream);
+        }
+        kmp_postings_destroy(ws);
+        res.release();
+        off.release();
+        cls.release();
+        ep.release();
+        eq.release();
+        ew.release();
+    }
+};
 
 struct kmp_ctx {
     int device = 0;
@@ -96,7 +123,13 @@ struct kmp_ctx {
         hk_ids.release();
         h_hk_off.clear();
     }
+    // multi-GPU (kmp_ctx_create_multi): the ranks of the row split and the gather's transport
+    std::vector<std::unique_ptr<kmp_rank>> ranks;
+    std::unique_ptr<kmp::Transport> transport;
     ~kmp_ctx() {
+        ranks.clear();
+        transport.reset();
+        (void)hipSetDevice(device);
         kmp_postings_destroy(postings);
         kmp_mphf_free(rep_mphf);
     }
@@ -297,6 +330,57 @@ int kmp_ctx_create(kmp_ctx** out, int device, int cpu_threads) {
     return KMP_OK;
 }
 
+int kmp_ctx_create_multi(kmp_ctx** out, int n_gpus, const int* devices, int cpu_threads) {
+    if (!out || n_gpus < 1 || n_gpus > 64) return KMP_EINVAL;
+    *out = nullptr;
+    std::vector<int> dev(n_gpus);
+    for (int g = 0; g < n_gpus; ++g) dev[g] = devices ? devices[g] : g;
+    kmp_ctx* c = nullptr;
+    int rc = kmp_ctx_create(&c, dev[0], cpu_threads);
+    if (rc != KMP_OK) return rc;
+    std::unique_ptr<kmp_ctx> guard(c);
+    bool distinct = true;
+    for (int g = 0; g < n_gpus; ++g) {
+        for (int h = 0; h < g; ++h) distinct &= dev[h] != dev[g];
+        if (g) {  // every device must pass the same checks as the first
+            kmp_ctx* probe = nullptr;
+            rc = kmp_ctx_create(&probe, dev[g], 1);
+            if (rc != KMP_OK) return rc;
+            kmp_ctx_destroy(probe);
+        }
+        std::unique_ptr<kmp_rank> r(new (std::nothrow) kmp_rank);
+        if (!r) return KMP_ENOMEM;
+        r->device = dev[g];
+        if (hipSetDevice(dev[g]) != hipSuccess) return KMP_EDEVICE;
+        if (g == 0) {
+            r->stream = c->stream;
+        } else {
+            if (hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess) return KMP_EDEVICE;
+            r->own_stream = true;
+        }
+        if (kmp_postings_create(&r->ws) != KMP_OK) return KMP_ENOMEM;
+        c->ranks.push_back(std::move(r));
+    }
+    (void)hipSetDevice(dev[0]);
+    if (n_gpus > 1) {
+        if (distinct) {
+            c->transport = kmp::make_rccl_transport(dev, &c->err);
+            if (!c->transport) return KMP_ERCCL;
+        } else {
+            c->transport = kmp::make_copy_transport(dev);
+        }
+    }
+    *out = guard.release();
+    return KMP_OK;
+}
+
+int kmp_ctx_gpus(const kmp_ctx* c) { return c ? std::max<int>(1, (int)c->ranks.size()) : 0; }
+
+const char* kmp_ctx_transport(const kmp_ctx* c) {
+    if (!c) return "none";
+    return c->transport ? c->transport->name() : "local";
+}
+
 void kmp_ctx_destroy(kmp_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
@@ -339,6 +423,18 @@ int kmp_load_proteins(kmp_ctx* c, const uint8_t* residues, const uint64_t* offse
     KMP_HIP(c, hipMemcpyAsync(c->off.p, c->h_off.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
     if (n) KMP_HIP(c, hipMemcpyAsync(c->cls.p, c->h_cls.data(), n * sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
     KMP_HIP(c, hipStreamSynchronize(c->stream));
+    for (size_t g = 1; g < c->ranks.size(); ++g) {  // multi-GPU: every rank holds the whole batch
+        kmp_rank& r = *c->ranks[g];
+        KMP_HIP(c, hipSetDevice(r.device));
+        KMP_HIP(c, r.res.reserve(total + 16));
+        KMP_HIP(c, r.off.reserve((n + 1) * sizeof(uint64_t)));
+        KMP_HIP(c, r.cls.reserve((n + 1) * sizeof(uint16_t)));
+        if (total) KMP_HIP(c, hipMemcpyAsync(r.res.p, residues + offsets[0], total, hipMemcpyHostToDevice, r.stream));
+        KMP_HIP(c, hipMemcpyAsync(r.off.p, c->h_off.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, r.stream));
+        if (n) KMP_HIP(c, hipMemcpyAsync(r.cls.p, c->h_cls.data(), n * sizeof(uint16_t), hipMemcpyHostToDevice, r.stream));
+        KMP_HIP(c, hipStreamSynchronize(r.stream));
+    }
+    KMP_TRY(c, use_device(c));
     c->counters = kmp_counters{};
     c->counters.n_proteins = n;
     c->loaded = true;
@@ -498,6 +594,73 @@ int kmp_mphf_build(kmp_ctx* c, const uint32_t* keys, uint64_t n, double gamma, k
     return KMP_OK;
 }
 
+// The multi-GPU row split: every rank expands its rows on its own device (one host thread per
+// rank), then the transport gathers the ranks' edges into the context's buffers in rank order.
+static int multi_pairs(kmp_ctx* c, const kmp_pair_opts& o, uint64_t* count) {
+    const uint32_t G = (uint32_t)c->ranks.size();
+    std::vector<uint32_t> start(G + 1);
+    kmp_row_split(c->n, G, start.data());
+    const uint64_t slots = kmp_set_capacity(c->n, c->total_res);
+    std::vector<int> status(G, KMP_OK);
+    std::vector<uint64_t> cnt(G, 0);
+    std::vector<std::string> why(G);
+    auto work = [&](uint32_t g) {
+        kmp_rank& r = *c->ranks[g];
+        if (hipSetDevice(r.device) != hipSuccess) {
+            status[g] = KMP_EDEVICE;
+            return;
+        }
+        const uint8_t* res = (g ? r.res : c->res).as<uint8_t>();
+        const uint64_t* off = (g ? r.off : c->off).as<uint64_t>();
+        const uint16_t* cls = (g ? r.cls : c->cls).as<uint16_t>();
+        if (r.cap == 0) r.cap = std::max<uint64_t>(1u << 16, 4ull * c->n / G);
+        for (int attempt = 0; attempt < 3; ++attempt) {
+            if (r.ep.reserve(r.cap * 4) != hipSuccess || r.eq.reserve(r.cap * 4) != hipSuccess ||
+                r.ew.reserve(r.cap * 4) != hipSuccess) {
+                status[g] = KMP_ENOMEM;
+                return;
+            }
+            uint64_t ne = 0;
+            status[g] = kmp_dev_pairs_rows(r.ws, res, off, cls, c->n, c->k_sets, slots, 0xFFFFFFFFu, o.min_shared,
+                                           o.require_class_diff, start[g], start[g + 1], r.ep.as<uint32_t>(),
+                                           r.eq.as<uint32_t>(), r.ew.as<uint32_t>(), r.cap, &ne, nullptr, r.stream);
+            cnt[g] = ne;
+            if (status[g] != KMP_EOVERFLOW) break;
+            r.cap = ne + ne / 8 + 1024;
+        }
+        if (status[g] == KMP_OK && cnt[g] > r.cap) status[g] = KMP_EDEVICE;
+    };
+    std::vector<std::thread> pool;
+    for (uint32_t g = 1; g < G; ++g) pool.emplace_back(work, g);
+    work(0);
+    for (auto& t : pool) t.join();
+    KMP_TRY(c, use_device(c));
+    for (uint32_t g = 0; g < G; ++g)
+        if (status[g] != KMP_OK)
+            return fail(c, status[g], "rank %u (device %d, rows [%u, %u)): %s", g, c->ranks[g]->device, start[g],
+                        start[g + 1], kmp_status_string(status[g]));
+    uint64_t total = 0;
+    for (uint64_t x : cnt) total += x;
+    if (total > c->edge_cap) c->edge_cap = total + total / 8 + 1024;
+    KMP_HIP(c, c->ep.reserve(c->edge_cap * sizeof(uint32_t)));
+    KMP_HIP(c, c->eq.reserve(c->edge_cap * sizeof(uint32_t)));
+    KMP_HIP(c, c->ew.reserve(c->edge_cap * sizeof(uint32_t)));
+    std::vector<kmp::EdgeArrays> src(G);
+    std::vector<hipStream_t> streams(G);
+    for (uint32_t g = 0; g < G; ++g) {
+        kmp_rank& r = *c->ranks[g];
+        src[g] = {r.ep.as<uint32_t>(), r.eq.as<uint32_t>(), r.ew.as<uint32_t>()};
+        streams[g] = r.stream;
+    }
+    std::string err;
+    const int rc = c->transport->gather(src, {c->ep.as<uint32_t>(), c->eq.as<uint32_t>(), c->ew.as<uint32_t>()}, cnt,
+                                        streams, &err);
+    KMP_TRY(c, use_device(c));
+    if (rc != KMP_OK) return fail(c, rc, "%s", err.c_str());
+    *count = total;
+    return KMP_OK;
+}
+
 int kmp_pairs(kmp_ctx* c, const kmp_pair_opts* opts, kmp_edges** out) {
     if (!c || !out) return KMP_EINVAL;
     *out = nullptr;
@@ -512,6 +675,11 @@ int kmp_pairs(kmp_ctx* c, const kmp_pair_opts* opts, kmp_edges** out) {
     KMP_TRY(c, use_device(c));
     if (c->edge_cap == 0) c->edge_cap = std::max<uint64_t>(1u << 20, 4ull * c->n);
     unsigned long long count = 0;
+    if (c->ranks.size() > 1 && (o.engine == KMP_ENGINE_AUTO || o.engine == KMP_ENGINE_RESIDUES)) {
+        uint64_t total = 0;
+        KMP_TRY(c, multi_pairs(c, o, &total));
+        return finish_edges(c, o, total, false, out);
+    }
     if (o.engine != KMP_ENGINE_TILES) {
         if (!c->postings) KMP_TRY(c, kmp_postings_create(&c->postings));
         const uint64_t slots = kmp_set_capacity(c->n, c->total_res);

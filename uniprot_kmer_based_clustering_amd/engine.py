@@ -96,9 +96,24 @@ class Edges:
 class KmerPairEngine:
     """One device context (kmp_ctx) holding a protein batch and its k-mer sets."""
 
-    def __init__(self, device: int = 0, cpu_threads: int = 1):
+    def __init__(self, device: int = 0, cpu_threads: int = 1, devices=None):
+        """devices: HIP ordinals of a multi-GPU context (kmp_ctx_create_multi; repeating one
+        runs several ranks on that GPU); None: the single-GPU context on `device`."""
         self._ctx = C.c_void_p()
-        check(lib().kmp_ctx_create(C.byref(self._ctx), device, cpu_threads), "kmp_ctx_create")
+        if devices is None:
+            check(lib().kmp_ctx_create(C.byref(self._ctx), device, cpu_threads), "kmp_ctx_create")
+        else:
+            arr = (C.c_int * len(devices))(*devices)
+            st = lib().kmp_ctx_create_multi(C.byref(self._ctx), len(devices), arr, cpu_threads)
+            check(st, "kmp_ctx_create_multi")
+
+    @property
+    def gpus(self) -> int:
+        return int(lib().kmp_ctx_gpus(self._ctx))
+
+    @property
+    def transport(self) -> str:
+        return lib().kmp_ctx_transport(self._ctx).decode()
 
     def close(self):
         if self._ctx:
