@@ -190,6 +190,17 @@ int kmp_edges_get(const kmp_edges* e, uint32_t* p, uint32_t* q, uint32_t* w, flo
  * kmp_build_sets for every k in turn: the context's sets are those of ks[nk-1] afterwards.
  * kmp_edges_get_wk: the weights w_{ks[j]} of every merged edge (0 where that k shares none).
  * A build extension: the reference has one k per run (main.rs), so parity is unpinned. */
+/* Bounded memory (config 5: 10^10-10^11 (k-mer, pair) incidences).  kmp_pairs (engine AUTO /
+ * RESIDUES on one GPU) and kmp_pairs_multi_k run the rows in passes of consecutive row ranges
+ * when the batch is large (more than 2^26 windows) or a pass budget is set: each pass expands
+ * only the pairs whose smaller protein lies in its rows, keeping the batch's keys, grouping and
+ * heavy-path compaction from the first pass (kmp_postings_set_reuse), and appends its edges
+ * (canonical: the ranges are consecutive).  The planner sizes each pass to 3/4 of `keys` pair
+ * keys from the densest incidence rate measured so far (the first pass is a probe of N/256
+ * rows).  keys = 0 (default): from the free device memory.  kmp_ctx_last_passes: passes of the
+ * last call. */
+int kmp_ctx_set_pass_keys(kmp_ctx* ctx, uint64_t keys);
+uint32_t kmp_ctx_last_passes(const kmp_ctx* ctx);
 #define KMP_MULTI_K_MAX 4
 int kmp_pairs_multi_k(kmp_ctx* ctx, const kmp_pair_opts* opts, const int* ks, uint32_t nk, kmp_edges** out);
 int kmp_edges_get_wk(const kmp_edges* e, uint32_t j, uint32_t* wk, uint64_t cap, uint64_t* n);
@@ -371,6 +382,12 @@ uint32_t kmp_postings_last_overflow_blocks(const kmp_postings* ws);
  * kmp_postings_graph_replays: calls served by a replay so far. */
 int kmp_postings_set_graph(kmp_postings* ws, int enable);
 uint64_t kmp_postings_graph_replays(const kmp_postings* ws);
+/* Front reuse (default 0).  1: a call on the same batch as the last successful call (same device
+ * pointers, n, k, slots, options; the caller guarantees the contents are unchanged) keeps that
+ * call's keys, bucket grouping and heavy-path compaction and runs only the bucket kernels, the
+ * heavy expansion and the tail of its rows — the passes of the bounded-memory mode and the
+ * per-k rows of kmp_pairs_multi_k call kmp_dev_pairs_rows this way. */
+int kmp_postings_set_reuse(kmp_postings* ws, int enable);
 int kmp_dev_pairs_postings(kmp_postings* ws, const uint32_t* d_set, const uint32_t* d_set_len,
                            const uint64_t* d_res_off, const uint16_t* d_class, uint32_t n, int k, uint64_t slots,
                            uint32_t heavy_df, uint32_t min_shared, int require_class_diff, uint32_t* d_p,

@@ -127,6 +127,8 @@ SIGNATURES = {
                                      P, P, P, C.c_uint64, P, P]),
     "kmp_ctx_create_multi": (C.c_int, [C.POINTER(P), C.c_int, C.POINTER(C.c_int), C.c_int]),
     "kmp_ctx_gpus": (C.c_int, [P]),
+    "kmp_ctx_set_pass_keys": (C.c_int, [P, C.c_uint64]),
+    "kmp_ctx_last_passes": (C.c_uint32, [P]),
     "kmp_ctx_transport": (C.c_char_p, [P]),
     "kmp_postings_create": (C.c_int, [C.POINTER(P)]),
     "kmp_postings_destroy": (None, [P]),
@@ -139,6 +141,7 @@ SIGNATURES = {
     "kmp_edges_get_wk": (C.c_int, [P, C.c_uint32, P, C.c_uint64, C.POINTER(C.c_uint64)]),
     "kmp_postings_set_graph": (C.c_int, [P, C.c_int]),
     "kmp_postings_graph_replays": (C.c_uint64, [P]),
+    "kmp_postings_set_reuse": (C.c_int, [P, C.c_int]),
     "kmp_dev_pairs_residues": (C.c_int, [P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32,
                                          C.c_uint32, C.c_int, P, P, P, C.c_uint64, U64P, P, P]),
     "kmp_dev_pairs_rows": (C.c_int, [P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32, C.c_uint32,

@@ -17,6 +17,7 @@
 #include "kmp_df.hpp"
 #include "kmp_edges.hpp"
 #include "kmp_internal.hpp"
+#include "kmp_merge.hpp"
 #include "kmp_mphf.hpp"
 #include "kmp_multi.hpp"
 
@@ -46,6 +47,10 @@ struct DevBuf {
     }
     template <class T>
     T* as() const { return static_cast<T*>(p); }
+    void swap(DevBuf& o) {
+        std::swap(p, o.p);
+        std::swap(bytes, o.bytes);
+    }
     void adopt(void* q, size_t b) {  // take ownership of a hipMalloc'd buffer
         release();
         p = q;
@@ -123,11 +128,29 @@ struct kmp_ctx {
         hk_ids.release();
         h_hk_off.clear();
     }
+    // bounded-memory passes: pair keys per pass (0: auto from free device memory), passes of the
+    // last kmp_pairs / kmp_pairs_multi_k
+    uint64_t pass_keys = 0;
+    uint32_t last_passes = 0;
+    // kmp_pairs_multi_k: per k, the sets (scores), a workspace (front kept across passes) and
+    // the pass's edges; the merged list
+    struct KSet {
+        int k = 0;
+        DevBuf set, set_len, rep, rep_len, ep, eq, ew, score;
+        uint64_t cap = 0;
+        std::vector<uint32_t> h_set_len, h_rep_len;
+        kmp_postings* ws = nullptr;
+        ~KSet() { kmp_postings_destroy(ws); }
+    };
+    std::vector<std::unique_ptr<KSet>> ksets;
+    DevBuf mscore, mwk, mscratch;
     // multi-GPU (kmp_ctx_create_multi): the ranks of the row split and the gather's transport
     std::vector<std::unique_ptr<kmp_rank>> ranks;
     std::unique_ptr<kmp::Transport> transport;
     ~kmp_ctx() {
         ranks.clear();
+        (void)hipSetDevice(device);
+        ksets.clear();
         transport.reset();
         (void)hipSetDevice(device);
         kmp_postings_destroy(postings);
@@ -594,6 +617,115 @@ int kmp_mphf_build(kmp_ctx* c, const uint32_t* keys, uint64_t n, double gamma, k
     return KMP_OK;
 }
 
+// Bounded-memory passes over the rows (Σ C(df,2) runs to 10^10-10^11
+// (k-mer, pair) incidences, far more than one pass of pair keys can hold).  A pair belongs to
+// its smaller protein, so row p carries about (N - 1 - p) units of the pair mass; the planner
+// measures incidences per unit on each pass (the first pass is a probe of N/256 rows) and sizes
+// the next pass to 3/4 of the key budget with the densest rate seen so far.
+struct PassPlan {
+    uint32_t n;
+    double budget;
+    double density = -1.0;
+    double mass(uint32_t a, uint32_t b) const {  // Σ_{p in [a, b)} (n - 1 - p)
+        const double A = a, B = b, N = n;
+        return (B - A) * (N - 1) - (B * (B - 1) - A * (A - 1)) / 2;
+    }
+    uint32_t next(uint32_t a) const {
+        if (a >= n) return n;
+        if (density < 0) return std::min<uint32_t>(n, a + std::max<uint32_t>(1, n / 256));
+        const double target = 0.75 * budget / std::max(density, 1e-12);
+        if (mass(a, n) <= target) return n;
+        uint32_t lo = a + 1, hi = n;
+        while (lo < hi) {
+            const uint32_t mid = lo + (hi - lo) / 2;
+            if (mass(a, mid) >= target) hi = mid;
+            else lo = mid + 1;
+        }
+        return lo;
+    }
+    void seen(uint32_t a, uint32_t b, uint64_t inc) {
+        const double m = mass(a, b);
+        if (m > 0) density = std::max(density, inc / m);
+    }
+};
+
+constexpr uint64_t kPassSlots = 1ull << 26;  // batches above ~67M windows run in passes by default
+
+uint64_t pass_budget(kmp_ctx* c) {
+    if (c->pass_keys) return c->pass_keys;
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 16ull << 30;
+    // ~96 B of device memory per pair key of a pass: shard regions (8), row-block keys (8),
+    // staged runs (12), and when every row block overflows (dense rows) the tagged-key sort (48)
+    // and its run arrays (12), with slack
+    return std::max<uint64_t>(1u << 20, std::min<uint64_t>(fr / 2 / 96, 3ull << 30));
+}
+
+// three u32 edge arrays of cap entries, grown to want entries keeping their first keep entries
+int grow_edges(kmp_ctx* c, DevBuf& ep, DevBuf& eq, DevBuf& ew, uint64_t& cap, uint64_t want, uint64_t keep) {
+    const uint64_t have = ep.p && eq.p && ew.p ? std::min({ep.bytes, eq.bytes, ew.bytes}) / 4 : 0;
+    if (have >= want) {
+        cap = have;
+        return KMP_OK;
+    }
+    for (DevBuf* b : {&ep, &eq, &ew}) {
+        DevBuf nb;
+        KMP_HIP(c, nb.reserve(want * sizeof(uint32_t)));
+        if (keep) KMP_HIP(c, hipMemcpyAsync(nb.p, b->p, keep * 4, hipMemcpyDeviceToDevice, c->stream));
+        KMP_HIP(c, hipStreamSynchronize(c->stream));
+        b->swap(nb);
+    }
+    cap = want;
+    return KMP_OK;
+}
+
+// rows [a, b) with workspace ws (front reuse on) into (ep, eq, ew) from entry off on; the
+// buffers grow, keeping [0, off), when the call reports an overflow
+int rows_into(kmp_ctx* c, kmp_postings* ws, int k, const kmp_pair_opts& o, uint32_t a, uint32_t b, DevBuf& ep,
+              DevBuf& eq, DevBuf& ew, uint64_t& cap, uint64_t off, uint64_t* ne, kmp_postings_stats* st) {
+    const uint64_t slots = kmp_set_capacity(c->n, c->total_res);
+    KMP_TRY(c, grow_edges(c, ep, eq, ew, cap, std::max<uint64_t>(cap, off + (1u << 16)), off));
+    for (int attempt = 0; attempt < 3; ++attempt) {
+        uint64_t m = 0;
+        const int rc = kmp_dev_pairs_rows(ws, c->res.as<uint8_t>(), c->off.as<uint64_t>(), c->cls.as<uint16_t>(), c->n,
+                                          k, slots, 0xFFFFFFFFu, o.min_shared, o.require_class_diff, a, b,
+                                          ep.as<uint32_t>() + off, eq.as<uint32_t>() + off, ew.as<uint32_t>() + off,
+                                          cap - off, &m, st, c->stream);
+        if (rc == KMP_EOVERFLOW) {
+            KMP_TRY(c, grow_edges(c, ep, eq, ew, cap, off + m + m / 8 + 1024, off));
+            continue;
+        }
+        if (rc != KMP_OK) return fail(c, rc, "rows [%u, %u): %s", a, b, kmp_status_string(rc));
+        *ne = m;
+        return KMP_OK;
+    }
+    return fail(c, KMP_EDEVICE, "rows [%u, %u): edge count unstable across reruns", a, b);
+}
+
+// single GPU, residue path, in passes: the pass edges land behind each other in the context's
+// buffers (already canonical: passes are consecutive row ranges)
+int pass_pairs(kmp_ctx* c, const kmp_pair_opts& o, uint64_t* count) {
+    KMP_TRY(c, kmp_postings_set_reuse(c->postings, 1));
+    PassPlan plan{c->n, (double)pass_budget(c)};
+    uint64_t off = 0;
+    uint32_t passes = 0;
+    int rc = KMP_OK;
+    for (uint32_t a = 0; a < c->n && rc == KMP_OK;) {
+        const uint32_t b = plan.next(a);
+        kmp_postings_stats st{};
+        uint64_t ne = 0;
+        rc = rows_into(c, c->postings, c->k_sets, o, a, b, c->ep, c->eq, c->ew, c->edge_cap, off, &ne, &st);
+        plan.seen(a, b, st.incidences);
+        off += ne;
+        a = b;
+        ++passes;
+    }
+    (void)kmp_postings_set_reuse(c->postings, 0);
+    c->last_passes = passes;
+    *count = off;
+    return rc;
+}
+
 // The multi-GPU row split: every rank expands its rows on its own device (one host thread per
 // rank), then the transport gathers the ranks' edges into the context's buffers in rank order.
 static int multi_pairs(kmp_ctx* c, const kmp_pair_opts& o, uint64_t* count) {
@@ -680,10 +812,17 @@ int kmp_pairs(kmp_ctx* c, const kmp_pair_opts* opts, kmp_edges** out) {
         KMP_TRY(c, multi_pairs(c, o, &total));
         return finish_edges(c, o, total, false, out);
     }
+    c->last_passes = 1;
     if (o.engine != KMP_ENGINE_TILES) {
         if (!c->postings) KMP_TRY(c, kmp_postings_create(&c->postings));
         const uint64_t slots = kmp_set_capacity(c->n, c->total_res);
-        for (int attempt = 0; attempt < 2; ++attempt) {
+        if ((o.engine == KMP_ENGINE_AUTO || o.engine == KMP_ENGINE_RESIDUES) && (c->pass_keys || slots > kPassSlots)) {
+            uint64_t total = 0;
+            KMP_TRY(c, pass_pairs(c, o, &total));
+            return finish_edges(c, o, total, false, out);
+        }
+        bool ok = false;
+        for (int attempt = 0; attempt < 3 && !ok; ++attempt) {
             KMP_HIP(c, c->ep.reserve(c->edge_cap * sizeof(uint32_t)));
             KMP_HIP(c, c->eq.reserve(c->edge_cap * sizeof(uint32_t)));
             KMP_HIP(c, c->ew.reserve(c->edge_cap * sizeof(uint32_t)));
@@ -701,14 +840,14 @@ int kmp_pairs(kmp_ctx* c, const kmp_pair_opts* opts, kmp_edges** out) {
                                              c->eq.as<uint32_t>(), c->ew.as<uint32_t>(), c->edge_cap, &ne, nullptr,
                                              c->stream);
             count = ne;
-            if (st == KMP_EOVERFLOW) {
+            if (st == KMP_EOVERFLOW) {  // the buffers were too small: grow them and rerun
                 c->edge_cap = ne + ne / 8 + 1024;
                 continue;
             }
             if (st != KMP_OK) return fail(c, st, "postings engine: %s", kmp_status_string(st));
-            break;
+            ok = count <= c->edge_cap;
         }
-        if (count > c->edge_cap) return fail(c, KMP_EDEVICE, "edge count unstable across reruns");
+        if (!ok) return fail(c, KMP_EDEVICE, "edge count unstable across reruns");
         return finish_edges(c, o, count, false, out);
     }
 
@@ -746,7 +885,8 @@ int kmp_pairs(kmp_ctx* c, const kmp_pair_opts* opts, kmp_edges** out) {
     KMP_TRY(c, kmp_dev_pack_dense(c->rep.as<uint32_t>(), c->off.as<uint64_t>(), c->dense_off.as<uint64_t>(), c->n,
                                   c->dense.as<uint32_t>(), c->stream));
     KMP_HIP(c, c->ecount.reserve(sizeof(unsigned long long)));
-    for (int attempt = 0; attempt < 2; ++attempt) {
+    bool ok = false;
+    for (int attempt = 0; attempt < 3 && !ok; ++attempt) {
         KMP_HIP(c, c->ep.reserve(c->edge_cap * sizeof(uint32_t)));
         KMP_HIP(c, c->eq.reserve(c->edge_cap * sizeof(uint32_t)));
         KMP_HIP(c, c->ew.reserve(c->edge_cap * sizeof(uint32_t)));
@@ -762,10 +902,10 @@ int kmp_pairs(kmp_ctx* c, const kmp_pair_opts* opts, kmp_edges** out) {
                                       c->ecount.as<unsigned long long>(), c->stream));
         KMP_HIP(c, hipMemcpyAsync(&count, c->ecount.p, sizeof count, hipMemcpyDeviceToHost, c->stream));
         KMP_HIP(c, hipStreamSynchronize(c->stream));
-        if (count <= c->edge_cap) break;
-        c->edge_cap = count + count / 8 + 1024;
+        ok = count <= c->edge_cap;  // else the buffers grow and the kernels rerun
+        if (!ok) c->edge_cap = count + count / 8 + 1024;
     }
-    if (count > c->edge_cap) return fail(c, KMP_EDEVICE, "edge count unstable across reruns");
+    if (!ok) return fail(c, KMP_EDEVICE, "edge count unstable across reruns");
     return finish_edges(c, o, count, true, out);
 }
 
@@ -789,9 +929,12 @@ int kmp_edges_get(const kmp_edges* e, uint32_t* p, uint32_t* q, uint32_t* w, flo
 }
 
 // Config 5 of SURVEY.md §8d: w_k computed independently for each k; an edge is emitted when any
-// w_k >= min_shared (and, with require_class_diff, the classes differ).  Each k runs the whole
-// path (kmp_build_sets + kmp_pairs, which leave the context's sets at the last k), then the
-// canonical lists are merged by (p, q): w = Σ_k w_k, score = Σ_k score_k (COUNT / BLOSUM).
+// w_k >= min_shared (and, with require_class_diff, the classes differ).  Each k's sets are built
+// and kept (for the scores), each k gets its own workspace whose front (keys, grouping, heavy
+// compaction) is kept across the passes, and the rows run in passes (one when the batch is
+// small): per pass, every k's edges of the pass's rows (kmp_dev_pairs_rows), their per-k scores
+// (BLOSUM on the device), and the device union (kmp_merge.hip): w = Σ_k w_k, score = Σ_k score_k
+// (COUNT: score = w).  The context's sets are left at the last k.
 int kmp_pairs_multi_k(kmp_ctx* c, const kmp_pair_opts* opts, const int* ks, uint32_t nk, kmp_edges** out) {
     if (!c || !out || !ks || nk < 1 || nk > KMP_MULTI_K_MAX) return KMP_EINVAL;
     *out = nullptr;
@@ -800,58 +943,168 @@ int kmp_pairs_multi_k(kmp_ctx* c, const kmp_pair_opts* opts, const int* ks, uint
     kmp_pair_opts_default(&o);
     if (opts) o = *opts;
     if (o.score == KMP_SCORE_JACCARD) return fail(c, KMP_EINVAL, "JACCARD does not sum over k");
+    if (o.score != KMP_SCORE_COUNT && o.score != KMP_SCORE_BLOSUM) return fail(c, KMP_EINVAL, "unknown score %d", o.score);
     for (uint32_t j = 0; j < nk; ++j) {
         if (ks[j] < 1 || ks[j] > kMaxK) return fail(c, KMP_EINVAL, "k = %d", ks[j]);
         for (uint32_t i = 0; i < j; ++i)
             if (ks[i] == ks[j]) return fail(c, KMP_EINVAL, "k = %d twice", ks[j]);
     }
-    std::vector<std::unique_ptr<kmp_edges>> lists;
+    if (!c->loaded) return fail(c, KMP_ESTATE, "kmp_load_proteins first");
+    KMP_TRY(c, use_device(c));
+    while (c->ksets.size() < nk) c->ksets.emplace_back(new kmp_ctx::KSet);
+    // every k's sets, stashed in its slot (the last k's are swapped back at the end)
     for (uint32_t j = 0; j < nk; ++j) {
         KMP_TRY(c, kmp_build_sets(c, ks[j]));
-        kmp_edges* e = nullptr;
-        KMP_TRY(c, kmp_pairs(c, &o, &e));
-        lists.emplace_back(e);
+        kmp_ctx::KSet& s = *c->ksets[j];
+        s.k = ks[j];
+        s.set.swap(c->set);
+        s.set_len.swap(c->set_len);
+        s.rep.swap(c->rep);
+        s.rep_len.swap(c->rep_len);
+        s.h_set_len.swap(c->h_set_len);
+        s.h_rep_len.swap(c->h_rep_len);
+        if (!s.ws) KMP_TRY(c, kmp_postings_create(&s.ws));
+        KMP_TRY(c, kmp_postings_set_reuse(s.ws, 1));
     }
-    std::unique_ptr<kmp_edges> m(new (std::nothrow) kmp_edges);
-    if (!m) return fail(c, KMP_ENOMEM, "edges");
-    // nk-way merge of (p, q)-sorted lists
-    std::vector<size_t> at(nk, 0);
-    const uint64_t key_end = ~0ull;
-    auto key = [&](uint32_t j) {
-        const kmp_edges& e = *lists[j];
-        return at[j] < e.p.size() ? (uint64_t)e.p[at[j]] << 32 | e.q[at[j]] : key_end;
+    auto restore = [&]() {  // the context keeps the last k's sets, as kmp_build_sets(ks[nk-1])
+        kmp_ctx::KSet& s = *c->ksets[nk - 1];
+        s.set.swap(c->set);
+        s.set_len.swap(c->set_len);
+        s.rep.swap(c->rep);
+        s.rep_len.swap(c->rep_len);
+        s.h_set_len.swap(c->h_set_len);
+        s.h_rep_len.swap(c->h_rep_len);
+        for (uint32_t j = 0; j < nk; ++j) (void)kmp_postings_set_reuse(c->ksets[j]->ws, 0);
     };
-    std::vector<std::vector<uint32_t>> wk(nk);
-    uint64_t nalign = 0;
-    for (;;) {
-        uint64_t best = key_end;
-        for (uint32_t j = 0; j < nk; ++j) best = std::min(best, key(j));
-        if (best == key_end) break;
-        uint32_t w = 0;
-        float s = 0.0f;
-        for (uint32_t j = 0; j < nk; ++j) {
-            uint32_t wj = 0;
-            if (key(j) == best) {
-                wj = lists[j]->w[at[j]];
-                s += lists[j]->score[at[j]];
-                ++at[j];
-            }
-            wk[j].push_back(wj);
-            w += wj;
-        }
-        m->p.push_back((uint32_t)(best >> 32));
-        m->q.push_back((uint32_t)best);
-        m->w.push_back(w);
-        m->score.push_back(s);
-        if (w > o.align_threshold) ++nalign;
+    const uint64_t slots = kmp_set_capacity(c->n, c->total_res);
+    PassPlan plan{c->n, (double)pass_budget(c)};
+    if (!c->pass_keys && slots <= kPassSlots) plan.density = 0;  // small batch: one pass
+    const bool blosum = o.score == KMP_SCORE_BLOSUM;
+    uint64_t off = 0, mcap = std::max<uint64_t>(c->edge_cap, 1u << 16);
+    int rc = KMP_OK;
+    uint32_t passes = 0;
+    auto grow_out = [&](uint64_t want) -> int {  // merged arrays: p q w (ctx), score, wk (nk x mcap)
+        if (want <= mcap && c->ep.p && c->mwk.p) return KMP_OK;
+        const uint64_t ncap = std::max(want, mcap);
+        uint64_t cap3 = mcap;
+        KMP_TRY(c, grow_edges(c, c->ep, c->eq, c->ew, cap3, ncap, off));
+        DevBuf ns, nw;
+        KMP_HIP(c, ns.reserve(ncap * 4));
+        KMP_HIP(c, nw.reserve((uint64_t)nk * ncap * 4));
+        if (off && c->mscore.p) KMP_HIP(c, hipMemcpyAsync(ns.p, c->mscore.p, off * 4, hipMemcpyDeviceToDevice, c->stream));
+        for (uint32_t j = 0; j < nk && off && c->mwk.p; ++j)
+            KMP_HIP(c, hipMemcpyAsync(nw.as<uint32_t>() + j * ncap, c->mwk.as<uint32_t>() + j * mcap, off * 4,
+                                      hipMemcpyDeviceToDevice, c->stream));
+        KMP_HIP(c, hipStreamSynchronize(c->stream));
+        c->mscore.swap(ns);
+        c->mwk.swap(nw);
+        mcap = ncap;
+        c->edge_cap = ncap;
+        return KMP_OK;
+    };
+    if ((rc = grow_out(mcap)) != KMP_OK) {
+        restore();
+        return rc;
     }
-    m->ks.assign(ks, ks + nk);
-    for (uint32_t j = 0; j < nk; ++j) m->wk.insert(m->wk.end(), wk[j].begin(), wk[j].end());
-    c->counters.n_edges = m->p.size();
+    c->edge_cap = mcap;
+    for (uint32_t a = 0; a < c->n && rc == KMP_OK;) {
+        const uint32_t b = plan.density == 0 ? c->n : plan.next(a);
+        MergeIn in{};
+        in.nk = nk;
+        uint64_t total = 0;
+        for (uint32_t j = 0; j < nk && rc == KMP_OK; ++j) {
+            kmp_ctx::KSet& s = *c->ksets[j];
+            kmp_postings_stats st{};
+            uint64_t ne = 0;
+            rc = rows_into(c, s.ws, s.k, o, a, b, s.ep, s.eq, s.ew, s.cap, 0, &ne, &st);
+            if (rc != KMP_OK) break;
+            if (plan.density != 0) plan.seen(a, b, st.incidences);
+            if (blosum && ne) {
+                if (s.score.bytes < ne * 4 && s.score.reserve(ne * 4) != hipSuccess) rc = fail(c, KMP_ENOMEM, "scores");
+                if (rc == KMP_OK)
+                    rc = edge_blosum_device(s.rep.as<uint32_t>(), s.rep_len.as<uint32_t>(), c->off.as<uint64_t>(),
+                                            s.ep.as<uint32_t>(), s.eq.as<uint32_t>(), s.ew.as<uint32_t>(), ne, s.k,
+                                            s.score.as<float>(), c->stream);
+                if (rc != KMP_OK) rc = fail(c, rc, "BLOSUM scores of k = %d: %s", s.k, kmp_status_string(rc));
+            }
+            in.p[j] = s.ep.as<uint32_t>();
+            in.q[j] = s.eq.as<uint32_t>();
+            in.w[j] = s.ew.as<uint32_t>();
+            in.s[j] = blosum ? s.score.as<float>() : nullptr;
+            in.off[j] = total;
+            total += ne;
+        }
+        if (rc != KMP_OK) break;
+        in.off[nk] = total;
+        if ((rc = grow_out(off + total)) != KMP_OK) break;
+        const uint64_t sb = merge_scratch_bytes(total);
+        if (c->mscratch.bytes < sb && c->mscratch.reserve(sb) != hipSuccess) {
+            rc = fail(c, KMP_ENOMEM, "merge scratch");
+            break;
+        }
+        MergeOut mo{};
+        mo.p = c->ep.as<uint32_t>() + off;
+        mo.q = c->eq.as<uint32_t>() + off;
+        mo.w = c->ew.as<uint32_t>() + off;
+        mo.s = blosum ? c->mscore.as<float>() + off : nullptr;
+        for (uint32_t j = 0; j < nk; ++j) mo.wk[j] = c->mwk.as<uint32_t>() + j * mcap + off;
+        mo.cap = mcap - off;
+        uint64_t m = 0;
+        rc = merge_edges_device(in, mo, c->mscratch.p, c->mscratch.bytes, &m, c->stream);
+        if (rc != KMP_OK) {
+            rc = fail(c, rc, "merge: %s", kmp_status_string(rc));
+            break;
+        }
+        off += m;
+        a = b;
+        ++passes;
+    }
+    restore();
+    if (rc != KMP_OK) return rc;
+    c->last_passes = passes;
+    std::unique_ptr<kmp_edges> e(new (std::nothrow) kmp_edges);
+    if (!e) return fail(c, KMP_ENOMEM, "edges");
+    const uint64_t count = off;
+    e->p.resize(count);
+    e->q.resize(count);
+    e->w.resize(count);
+    e->score.resize(count);
+    e->wk.resize((uint64_t)nk * count);
+    if (count) {
+        KMP_HIP(c, hipMemcpyAsync(e->p.data(), c->ep.p, count * 4, hipMemcpyDeviceToHost, c->stream));
+        KMP_HIP(c, hipMemcpyAsync(e->q.data(), c->eq.p, count * 4, hipMemcpyDeviceToHost, c->stream));
+        KMP_HIP(c, hipMemcpyAsync(e->w.data(), c->ew.p, count * 4, hipMemcpyDeviceToHost, c->stream));
+        if (blosum)
+            KMP_HIP(c, hipMemcpyAsync(e->score.data(), c->mscore.p, count * 4, hipMemcpyDeviceToHost, c->stream));
+        for (uint32_t j = 0; j < nk; ++j)
+            KMP_HIP(c, hipMemcpyAsync(e->wk.data() + j * count, c->mwk.as<uint32_t>() + j * mcap, count * 4,
+                                      hipMemcpyDeviceToHost, c->stream));
+    }
+    KMP_HIP(c, hipStreamSynchronize(c->stream));
+    uint64_t nalign = 0, wdiff = 0;
+    for (uint64_t i = 0; i < count; ++i) {
+        const uint32_t p = e->p[i], q = e->q[i];
+        if (p >= q || q >= c->n) return fail(c, KMP_EDEVICE, "device edge %llu = (%u, %u) is not a pair of the batch",
+                                             (unsigned long long)i, p, q);
+        if (!blosum) e->score[i] = (float)e->w[i];
+        if (e->w[i] > o.align_threshold) ++nalign;
+        if (c->h_cls[p] != c->h_cls[q]) wdiff += e->w[i];
+    }
+    e->ks.assign(ks, ks + nk);
+    c->counters.n_edges = count;
     c->counters.n_align = nalign;
-    *out = m.release();
+    c->counters.sum_w_diff = wdiff;
+    *out = e.release();
     return KMP_OK;
 }
+
+int kmp_ctx_set_pass_keys(kmp_ctx* c, uint64_t keys) {
+    if (!c) return KMP_EINVAL;
+    c->pass_keys = keys;
+    return KMP_OK;
+}
+
+uint32_t kmp_ctx_last_passes(const kmp_ctx* c) { return c ? c->last_passes : 0u; }
 
 int kmp_edges_get_wk(const kmp_edges* e, uint32_t j, uint32_t* wk, uint64_t cap, uint64_t* n) {
     if (!e || !n) return KMP_EINVAL;

@@ -1618,6 +1618,11 @@ struct kmp_postings {
     bool heavy_ready = false;   // hE / hGS hold the current front's compacted spill
     uint64_t h_ne = 0, h_ng = 0;
     std::vector<unsigned long long> shape;  // (n, slots, code bits, bucket bits) of the last batch
+    // front reuse (kmp_postings_set_reuse): a call on the same batch (front_key) keeps the keys,
+    // level 2 and the heavy compaction of the last successful call and runs only the buckets,
+    // the heavy expansion and the tail of its rows (the passes / ranks of one batch)
+    bool reuse = false, front_ok = false;
+    std::vector<unsigned long long> front_key;
     // single-synchronisation step as a HIP graph: captured on the second call with the same shape
     // (every buffer already sized), replayed after that
     bool graph_on = true;
@@ -2253,6 +2258,7 @@ struct StepCfg {
     uint32_t *d_p, *d_q, *d_w;
     uint64_t cap;
     uint32_t stride;          // edge arrays' element stride (3: interleaved triples)
+    const std::vector<unsigned long long>* front_key;  // the batch: pointers and shape
 };
 
 // row-block tail geometry: rows per block so that an average block holds about a quarter of
@@ -2348,14 +2354,18 @@ int step_reserve(kmp_postings* ws, const StepCfg& c, const PtGeom& g) {
 
 // front: clear, keys, level 2 (or the bucket sort), bucket kernels
 template <class MakeKeys>
-int enqueue_front(kmp_postings* ws, MakeKeys& make_keys, const StepCfg& c, bool spill, hipStream_t st) {
+int enqueue_front(kmp_postings* ws, MakeKeys& make_keys, const StepCfg& c, bool spill, hipStream_t st,
+                  bool keys = true) {
     step_clear_kernel<<<1, 256, 0, st>>>(ws->flags.p, ws->bstats.p);
     ws->mark(0, st);
-    PG(make_keys(c.lay, st));
-    ws->mark(1, st);
-    {
+    if (keys) {  // else: the keys grouped by bucket of the last call (front reuse)
+        PG(make_keys(c.lay, st));
+        ws->mark(1, st);
         int rc = bucket_group(ws, ws->keys.p, c.slots, c.lay, st);  // marks 2
         if (rc != KMP_OK) return rc;
+    } else {
+        ws->mark(1, st);
+        ws->mark(2, st);
     }
     const BucketArgs a = bucket_args(ws, c, spill);
     const uint32_t nb = 1u << c.lay.bbits;
@@ -2618,6 +2628,8 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
     if (ws->shard_cap == 0) ws->shard_cap = c.slots / 4 / kShards + 4096;
     if (ws->spill_cap == 0) ws->spill_cap = 1024;
     const bool debug = getenv("KMP_DEBUG") != nullptr;
+    const bool reuse = ws->reuse && ws->front_ok && c.front_key && *c.front_key == ws->front_key;
+    if (!reuse) ws->front_ok = false;
     // every rerun grows a capacity to its measured need, so a handful of attempts suffices
     for (int attempt = 0; attempt < 16; ++attempt) {
         PtGeom g;
@@ -2628,7 +2640,9 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
         }
         const unsigned long long* rb = ws->hrb;
         unsigned long long acc[kStN], most, n_inc, spill_most, spill_total;
-        if (!ws->heavy) {
+        const bool split = ws->heavy || reuse;
+        if (!reuse) ws->heavy_ready = false;  // a recomputed front: no compacted spill yet
+        if (!split) {
             key.push_back(ws->shard_cap);
             key.push_back(ws->spill_cap);
             key.push_back(ws->timing);
@@ -2639,8 +2653,7 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
             if (rc != KMP_OK) return rc;
             PG(hipStreamSynchronize(st));
         } else {
-            ws->heavy_ready = false;
-            int rc = enqueue_front(ws, make_keys, c, true, st);
+            int rc = enqueue_front(ws, make_keys, c, !ws->heavy_ready, st, !reuse);
             if (rc != KMP_OK) return rc;
             step_pack_kernel<<<1, 256, 0, st>>>(ws->bstats.p, ws->flags.p, nullptr, ws->hrb);
             PG(hipStreamSynchronize(st));
@@ -2659,11 +2672,11 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
             ws->spill_cap = spill_most + spill_most / 8 + 1024;
             rerun = true;
         }
-        if (spill_total && !ws->heavy) {  // frequent k-mers: the split step from now on
+        if (spill_total && !split) {  // frequent k-mers: the split step from now on
             ws->heavy = true;
             rerun = true;
         }
-        if (!ws->heavy && most > ws->shard_cap) {
+        if (!split && most > ws->shard_cap) {
             ws->shard_cap = most + most / 64 + 256;
             rerun = true;
         }
@@ -2674,8 +2687,8 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
                         (int)ws->heavy, most, (unsigned long long)ws->shard_cap);
             continue;
         }
-        if (ws->heavy) {
-            if (spill_total) {
+        if (split) {
+            if (spill_total || ws->heavy_ready) {
                 int rc = heavy_phase(ws, c, spill_total, true, st);
                 if (rc != KMP_OK) return rc;
             }
@@ -2719,9 +2732,13 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
             stats->incidences = n_inc;
             stats->pairs = ne;
         }
-        ws->last_heavy = ws->heavy;
-        ws->last_fused = !ws->heavy;
-        if (ws->heavy && !spill_total) ws->heavy = false;  // nothing spilled: the fused step next call
+        ws->last_heavy = ws->heavy_ready;
+        ws->last_fused = !split;
+        if (c.front_key) {
+            ws->front_ok = true;
+            ws->front_key = *c.front_key;
+        }
+        if (!reuse && ws->heavy && !spill_total) ws->heavy = false;  // nothing spilled: the fused step next
         *n_edges = ne;
         return ne > c.cap ? KMP_EOVERFLOW : KMP_OK;
     }
@@ -2829,6 +2846,9 @@ int run_postings(kmp_postings* ws, MakeKeys make_keys, const std::vector<unsigne
     PG(ws->flags.reserve(kFlN));
     ws->parted = false;
     Layout lay = make_layout(n, k, slots, ws->bucketed);
+    std::vector<unsigned long long> front_key = {n, (unsigned long long)k, slots, heavy_df,
+                                                 (unsigned long long)require_class_diff};
+    front_key.insert(front_key.end(), key_extra.begin(), key_extra.end());
     if (lay.bucketed) {
         StepCfg c{};
         c.slots = slots;
@@ -2845,6 +2865,7 @@ int run_postings(kmp_postings* ws, MakeKeys make_keys, const std::vector<unsigne
         c.d_w = d_w;
         c.cap = cap;
         c.stride = 1;
+        c.front_key = &front_key;
         // graph key: the call's shape and pointers (run_step adds the capacities, the timing
         // switch, the row-block geometry and the buffer generation)
         std::vector<unsigned long long> key = {n, (unsigned long long)k, slots, heavy_df, min_shared,
@@ -2861,6 +2882,7 @@ int run_postings(kmp_postings* ws, MakeKeys make_keys, const std::vector<unsigne
         }
     }
     // flat layout: class ids wider than the bucketed key's class field (or the layout forced)
+    ws->front_ok = false;
     if (ranged) return KMP_ESTATE;  // no row filter on the flat layout
     lay = make_layout(n, k, slots, false);
     if (lay.sort_hi > 64) return KMP_EINVAL;
@@ -2926,6 +2948,13 @@ int kmp_postings_set_graph(kmp_postings* ws, int enable) {
 }
 
 uint64_t kmp_postings_graph_replays(const kmp_postings* ws) { return ws ? ws->graph_replays : 0; }
+
+int kmp_postings_set_reuse(kmp_postings* ws, int enable) {
+    if (!ws) return KMP_EINVAL;
+    ws->reuse = enable != 0;
+    if (!ws->reuse) ws->front_ok = false;
+    return KMP_OK;
+}
 
 int kmp_dev_pairs_postings(kmp_postings* ws, const uint32_t* d_set, const uint32_t* d_set_len,
                            const uint64_t* d_res_off, const uint16_t* d_class, uint32_t n, int k, uint64_t slots,

@@ -222,6 +222,11 @@ class DevicePipeline:
         """Residue path: capture the single-synchronisation step as a HIP graph and replay it."""
         check(lib().kmp_postings_set_graph(self._workspace(), int(enable)), "kmp_postings_set_graph")
 
+    def set_reuse(self, enable: bool = True) -> None:
+        """Keep the batch's keys / grouping / heavy compaction across calls on the same batch
+        (the row passes of one step): kmp_postings_set_reuse."""
+        check(lib().kmp_postings_set_reuse(self._workspace(), int(enable)), "kmp_postings_set_reuse")
+
     def graph_replays(self) -> int:
         return int(lib().kmp_postings_graph_replays(self._workspace()))
 

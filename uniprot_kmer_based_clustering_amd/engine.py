@@ -115,6 +115,14 @@ class KmerPairEngine:
     def transport(self) -> str:
         return lib().kmp_ctx_transport(self._ctx).decode()
 
+    def set_pass_keys(self, keys: int) -> None:
+        """Bounded-memory passes: pair keys per pass (0: auto, from the free device memory)."""
+        self._check(lib().kmp_ctx_set_pass_keys(self._ctx, keys), "kmp_ctx_set_pass_keys")
+
+    @property
+    def last_passes(self) -> int:
+        return int(lib().kmp_ctx_last_passes(self._ctx))
+
     def close(self):
         if self._ctx:
             lib().kmp_ctx_destroy(self._ctx)
