@@ -73,7 +73,7 @@ typedef struct {
     uint64_t n_proteins;
     uint64_t n_windows;   /* Σ (L-k+1): Protein.five_mers total (protein.rs:114) */
     uint64_t sum_S;       /* Σ |K(p)|, distinct k-mers per protein */
-    uint64_t distinct;    /* distinct k-mers over all proteins (main.rs:318) */
+    uint64_t distinct;    /* distinct k-mers over all proteins (main.rs:137-140: five_mer_all) */
     uint64_t repeat;      /* df >= 2 k-mers: "Number of 5mers found in at least two proteins" (mod.rs:50) */
     uint64_t sum_cdf2;    /* Σ C(df,2): "Number of total edges" (mod.rs:51) */
     uint64_t sum_w_diff;  /* Σ w over class-differing pairs: edges after AMR filter (mod.rs:695) */
@@ -130,7 +130,7 @@ int kmp_extract(kmp_ctx* ctx, int k);
 int kmp_get_kmers(kmp_ctx* ctx, uint32_t protein, uint32_t* out, uint64_t cap, uint64_t* n);
 
 /* ------------------------------------------------------------------ sets ----------- */
-/* K(p): sorted distinct codes per protein (main.rs:280-282), plus the global repeat
+/* K(p): sorted distinct codes per protein (main.rs:99-101,187-189), plus the global repeat
  * (df >= 2) filter of remove_unique_five_mers (protein.rs:151-162). */
 int kmp_build_sets(kmp_ctx* ctx, int k);
 int kmp_get_set(kmp_ctx* ctx, uint32_t protein, uint32_t* out, uint64_t cap, uint64_t* n);
@@ -229,10 +229,11 @@ int kmp_edges_reference_keys(const kmp_edges* e, uint64_t* keys, uint64_t cap, u
  * for p then q, each ">{id}\n{seq}" with no trailing newline (mod.rs:253-261,273-280), where
  * prefix = id.split_once('|').0 and edge_key is the reference key with IDS lists, the edge index
  * otherwise; out_dir/db_files/ (empty, for diamond makedb) and out_dir/blastp_output.tsv holding
- * the header line of mod.rs:304.  out_dir NULL: ".".  Existing directories are reused, not
- * removed (the reference runs `rm -r` first).  residues/offsets[n+1]: the loaded batch; ids:
- * NUL-separated record ids (kmp_read_fasta).  An id without '|' is KMP_EINVAL (the reference
- * panics).  threads: writer threads.  *n_written: candidate edges. */
+ * the header line of mod.rs:304.  out_dir NULL: ".".  fasta_files/ and db_files/ are removed and
+ * recreated first, as the reference's `rm -r` + `mkdir` (mod.rs:202-220).  residues/offsets[n+1]:
+ * the loaded batch (residues NULL with candidates: KMP_EINVAL); ids: NUL-separated record ids
+ * (kmp_read_fasta).  An id without '|' is KMP_EINVAL (the reference panics).  threads: writer
+ * threads.  *n_written: candidate edges. */
 int kmp_write_candidates(const kmp_edges* e, const uint8_t* residues, const uint64_t* offsets, uint32_t n,
                          const char* ids, uint64_t ids_bytes, uint32_t threshold, const char* out_dir, int threads,
                          uint64_t* n_written);
@@ -396,7 +397,7 @@ int kmp_dev_pairs_postings(kmp_postings* ws, const uint32_t* d_set, const uint32
 
 /* The postings engine straight from the packed residues (the fused device path): one key per
  * k-mer window (Protein::new, protein.rs:82-94) in the same slot layout, so the per-protein
- * sort + dedup of K(p) (main.rs:280-282) is never materialised — duplicate windows of one
+ * sort + dedup of K(p) (main.rs:99-101,187-189) is never materialised — duplicate windows of one
  * protein are adjacent after the stable code sort and count once.  Same output contract and
  * edges as kmp_dev_pairs_postings; stats->sum_S = Σ |K(p)|.  slots = kmp_set_capacity(N, ΣL). */
 int kmp_dev_pairs_residues(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off,

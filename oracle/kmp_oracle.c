@@ -15,7 +15,7 @@
  *
  * Algorithm, phase for phase (file:line into /root/reference):
  *   windows + radix-21 codes ......... src/protein.rs:9-54 (codec), :107-132 (windows)
- *   per-protein sort+dedup ........... src/main.rs:280-282
+ *   per-protein sort+dedup ........... src/main.rs:99-101,187-189
  *   global df, df>=2 "repeat" split .. src/main.rs:77-122 (merge_sort :23-48), :127-149
  *   dense repeat ids (boomphf stand-in; ids differ from boomphf, unobservable in the
  *     edge list) ...................... src/main.rs:139-147, src/protein.rs:151-174
@@ -225,7 +225,7 @@ orc_ctx* orc_build(const uint8_t* res, const uint64_t* off, uint32_t n, const ui
     orc_extract(res, off, n, k, x->codes, x->win_off);
     x->c.n_windows = nw;
 
-    /* per-protein sort + dedup (main.rs:280-282) */
+    /* per-protein sort + dedup (main.rs:99-101,187-189) */
     x->set_val = (uint32_t*)malloc(sizeof(uint32_t) * (nw ? nw : 1));
     x->set_off = (uint64_t*)malloc(sizeof(uint64_t) * (n + 1));
     set_job sj = {x, 0};

@@ -107,6 +107,11 @@ HEADER = ("query id\tquery length\tsubject id\tsubject length\tquery alignment s
 def test_candidate_files(engine, tmp_path, threshold):
     res, off, cls, ids = uniprot()
     pr = load(engine, res, off, cls, ids, 5)
+    # files of an earlier run are removed (the reference's rm -r, mod.rs:202-210)
+    for d in ("fasta_files", "db_files"):
+        (tmp_path / d / "old").mkdir(parents=True)
+        (tmp_path / d / "old" / "stale.fasta").write_text(">x\nA")
+        (tmp_path / d / "stale.fasta").write_text(">x\nA")
     with engine.edge_set() as es:
         ed = es.get()
         es.kmers("ids")
@@ -119,7 +124,7 @@ def test_candidate_files(engine, tmp_path, threshold):
     for name in got[:: max(1, len(got) // 500)]:
         assert (tmp_path / "fasta_files" / name).read_bytes() == want[name], name
     assert (tmp_path / "blastp_output.tsv").read_text() == HEADER
-    assert (tmp_path / "db_files").is_dir()
+    assert (tmp_path / "db_files").is_dir() and not os.listdir(tmp_path / "db_files")
     # without IDS lists the edge index is the key
     with engine.edge_set() as es:
         out = tmp_path / "plain"

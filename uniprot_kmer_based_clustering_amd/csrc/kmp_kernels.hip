@@ -3,7 +3,7 @@
 //
 // Path (reference file:line it replaces):
 //   build_sets_kernel   Protein::new windows + radix-21 codes (src/protein.rs:29-37,107-132)
-//                       fused with the per-protein sort+dedup of src/main.rs:280-282
+//                       fused with the per-protein sort+dedup of src/main.rs:99-101,187-189
 //   mark/compact        remove_unique_five_mers (src/protein.rs:151-162) with the df>=2 test
 //                       of src/main.rs:127-149 as two bitmaps over the 21^k code space
 //   pair_kernel         Graph::new + remove_uninteresting_edges + combine_edges

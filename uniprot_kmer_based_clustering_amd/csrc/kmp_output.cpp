@@ -6,6 +6,7 @@
 //   kmp_write_graph_debug: `println!("Graph right now:\n{graph_ref:#?}")` (main.rs:234) with the
 //     Debug impls of Graph (mod.rs:700-708), KmerEdge (edge.rs:158-174) and ProteinVertex
 //     (vertex.rs:159-165), in the reference's final edge order.
+#include <ftw.h>
 #include <sys/stat.h>
 
 #include <algorithm>
@@ -38,6 +39,14 @@ bool split_ids(const char* ids, uint64_t bytes, uint32_t n, std::vector<std::pai
 }
 
 bool make_dir(const std::string& d) { return ::mkdir(d.c_str(), 0777) == 0 || errno == EEXIST; }
+
+// `rm -r d` (mod.rs:202-210): a missing directory is not an error, as the reference ignores rm's status
+bool remove_tree(const std::string& d) {
+    struct stat sb;
+    if (::lstat(d.c_str(), &sb) != 0) return errno == ENOENT;
+    auto rm = [](const char* path, const struct stat*, int, struct FTW*) -> int { return ::remove(path); };
+    return ::nftw(d.c_str(), rm, 16, FTW_DEPTH | FTW_PHYS) == 0;
+}
 
 bool write_file(const std::string& path, const std::string& text) {
     FILE* f = std::fopen(path.c_str(), "wb");
@@ -93,9 +102,12 @@ int kmp_write_candidates(const kmp_edges* e, const uint8_t* residues, const uint
             return KMP_EINVAL;
         cand.push_back(i);
     }
+    if (!cand.empty() && !residues) return KMP_EINVAL;
     const std::string root = out_dir && *out_dir ? std::string(out_dir) : std::string(".");
-    const std::string fdir = root + "/fasta_files";
-    if (!make_dir(root) || !make_dir(fdir) || !make_dir(root + "/db_files")) return KMP_EIO;
+    const std::string fdir = root + "/fasta_files", ddir = root + "/db_files";
+    // fresh directories, as the reference's rm -r + mkdir (mod.rs:202-220)
+    if (!make_dir(root) || !remove_tree(fdir) || !remove_tree(ddir) || !make_dir(fdir) || !make_dir(ddir))
+        return KMP_EIO;
     const bool ref_order = e->kspace == KMP_KMERS_IDS && e->ref_key.size() == e->p.size();
     std::atomic<uint64_t> next{0};
     std::atomic<int> err{KMP_OK};

@@ -3,7 +3,7 @@
 //
 //   reference (file:line)                                  here
 //   Protein::new windows + codes (protein.rs:82-94)        residue_keys_chunk_kernel: one key per window
-//   per-protein sort + dedup (main.rs:280-282)             duplicates of (k-mer, p) end up adjacent
+//   per-protein sort + dedup (main.rs:99-101,187-189)             duplicates of (k-mer, p) end up adjacent
 //                                                          after the stable code sort; skipped there
 //   global df: sorted Vec<(kmer, df)> (main.rs:77-122)     radix sort of the keys on the code bits;
 //                                                          one run per distinct k-mer, df = distinct

@@ -4,7 +4,7 @@ PyTorch is plumbing here: it owns the HBM buffers and the stream; every byte of 
 runs in libkmerpair's HIP kernels.  One ``DevicePipeline`` holds one protein batch resident
 on one GPU and runs the reference's hot path as stages:
 
-  build_sets   Protein::new + per-protein sort/dedup      (protein.rs:107-132, main.rs:280-282)
+  build_sets   Protein::new + per-protein sort/dedup      (protein.rs:107-132, main.rs:99-101,187-189)
   filter       remove_unique_five_mers (df >= 2)           (protein.rs:151-162, main.rs:127-149)
   plan         dense CSR of the filtered sets, column blocks, row tiles (host, from set sizes)
   pairs        Graph::new + remove_uninteresting_edges + combine_edges (graph/mod.rs)
