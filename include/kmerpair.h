@@ -383,6 +383,15 @@ uint32_t kmp_postings_last_overflow_blocks(const kmp_postings* ws);
  * kmp_postings_graph_replays: calls served by a replay so far. */
 int kmp_postings_set_graph(kmp_postings* ws, int enable);
 uint64_t kmp_postings_graph_replays(const kmp_postings* ws);
+/* Bucket partition of the residue path (level 1 is always the counting pass).  AUTO (default):
+ * level 2 by cursors — every run of keys reserved with one atomic in its bucket's fixed-capacity
+ * region (sized from the hash-uniform mean), no histogram / scan passes — and, for a shape where a
+ * region overflows (very frequent k-mers), the counting level 2 from then on.  COUNT: the counting
+ * level 2 only.  kmp_postings_last_partition: the level 2 the last call's bucketed front used
+ * (KMP_PARTITION_CURSOR or KMP_PARTITION_COUNT; -1 on the flat layout). */
+enum { KMP_PARTITION_AUTO = 0, KMP_PARTITION_COUNT = 1, KMP_PARTITION_CURSOR = 2 };
+int kmp_postings_set_partition(kmp_postings* ws, int mode);
+int kmp_postings_last_partition(const kmp_postings* ws);
 /* Front reuse (default 0).  1: a call on the same batch as the last successful call (same device
  * pointers, n, k, slots, options; the caller guarantees the contents are unchanged) keeps that
  * call's keys, bucket grouping and heavy-path compaction and runs only the bucket kernels, the

@@ -293,6 +293,39 @@ def test_residue_graph_replay(oracle_mod):
     np.testing.assert_array_equal(pipe.edges()[2], w)
 
 
+@pytest.mark.parametrize("case", ["synthetic", "uniprot5", "uniprot7"])
+def test_partitions_bit_exact(oracle_mod, uni, case):
+    """The cursor partition (fixed-capacity regions, one atomic per run) and the counting
+    partition group the same keys: bit-exact edges and statistics with either, repeated (graph
+    replay); a batch whose frequent k-mers overflow a bucket region (the uniprot families) falls
+    back to the counting partition and stays exact."""
+    import torch
+    from uniprot_kmer_based_clustering_amd.device import DevicePipeline
+    if case == "synthetic":
+        b, k = K.synth(30000, 23), 7
+    else:
+        b, k = K.Proteins(*uni), int(case[-1])
+    o = oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=k, threads=8)
+    p, q, w = o.pairs()
+    seen = {}
+    for mode in ("count", "auto"):
+        pipe = DevicePipeline(b, k, "cuda:0")
+        pipe.set_partition(mode)
+        for _ in range(4):
+            assert pipe.step(engine="residues") == len(p)
+            torch.cuda.synchronize()
+            assert pipe.last_layout() == "bucketed" and pipe.last_tail() == "rows"
+            np.testing.assert_array_equal(pipe.edges()[0], p)
+            np.testing.assert_array_equal(pipe.edges()[1], q)
+            np.testing.assert_array_equal(pipe.edges()[2], w)
+        st = pipe.postings_stats.as_dict()
+        assert st["distinct"] == o.counters()["distinct"] and st["max_df"] == o.counters()["max_df"]
+        seen[mode] = pipe.last_partition()
+    assert seen["count"] == "count"
+    if case == "synthetic":  # hash-uniform buckets; the real families of uniprot may overflow one
+        assert seen["auto"] == "cursor"
+
+
 def test_rowtail_overflow_blocks(oracle_mod):
     """A protein whose row holds more pair keys than one row block of the LDS reduction (kPtCap):
     its block is listed and finished by the segmented sort, the rest stay on the LDS path; edges

@@ -21,6 +21,7 @@ KMP_SCORE_COUNT, KMP_SCORE_JACCARD, KMP_SCORE_BLOSUM = 0, 1, 2
 KMP_ENGINE_AUTO, KMP_ENGINE_POSTINGS, KMP_ENGINE_TILES, KMP_ENGINE_RESIDUES = 0, 1, 2, 3
 KMP_KMERS_CODES, KMP_KMERS_IDS = 0, 1
 KMP_LAYOUT_FLAT, KMP_LAYOUT_BUCKETED, KMP_LAYOUT_BUCKETED_HEAVY = 0, 1, 2
+KMP_PARTITION_AUTO, KMP_PARTITION_COUNT, KMP_PARTITION_CURSOR = 0, 1, 2
 KMP_LDS_SORT_MAX = 4096
 
 
@@ -141,6 +142,8 @@ SIGNATURES = {
     "kmp_edges_get_wk": (C.c_int, [P, C.c_uint32, P, C.c_uint64, C.POINTER(C.c_uint64)]),
     "kmp_postings_set_graph": (C.c_int, [P, C.c_int]),
     "kmp_postings_graph_replays": (C.c_uint64, [P]),
+    "kmp_postings_set_partition": (C.c_int, [P, C.c_int]),
+    "kmp_postings_last_partition": (C.c_int, [P]),
     "kmp_postings_set_reuse": (C.c_int, [P, C.c_int]),
     "kmp_dev_pairs_residues": (C.c_int, [P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32,
                                          C.c_uint32, C.c_int, P, P, P, C.c_uint64, U64P, P, P]),

@@ -542,6 +542,10 @@ __global__ void bucket_bounds_kernel(const unsigned long long* __restrict__ k, u
 
 constexpr uint32_t kHeavySub = 128;  // larger sub-buckets (very frequent k-mers) -> flat layout
 constexpr int kShards = 64;          // output cursors (one per bucket residue mod kShards)
+// device flags of a step (ws->flags): a coarse bin above its level-2 tile budget, a class id too
+// wide for the key, the large-bucket list count, row blocks above the LDS capacity, the tile
+// budget an overflowing bin needs, a cursor-partition region overflow
+enum : uint32_t { kFlBin = 0, kFlClass = 1, kFlList = 2, kFlOvf = 3, kFlBinTiles = 4, kFlCur = 5, kFlN = 8 };
 
 template <int kThreads>
 __device__ __forceinline__ void block_scan_n(uint32_t v, uint32_t& excl, uint32_t& total, uint32_t* wave_tot) {
@@ -578,9 +582,12 @@ __device__ __forceinline__ void block_scan_n(uint32_t v, uint32_t& excl, uint32_
 //     skipped (an earlier pass of the same keys spilled them already);
 //   row_lo / row_hi (kRows): emit only the pairs whose smaller protein lies in [row_lo, row_hi)
 //     (a pass or a rank of the row split).
+//   capb: 0 -> bucket b is [bstart[b], bstart[b+1]) of sorted; else (cursor partition) bucket b
+//     is the region [b * capb, b * capb + bstart[b]) (bstart holds the counts)
 struct BucketArgs {
     const unsigned long long* sorted;
     const uint32_t* bstart;
+    uint32_t capb;
     Layout lay;
     uint32_t mul;
     int require_diff;
@@ -640,7 +647,15 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
     __shared__ unsigned long long sbase;
     __shared__ unsigned long long hbase[kMaxHeavy];  // spill offset of each heavy group
     __shared__ uint32_t nheavy, hkeys;
-    const uint32_t s0 = a.bstart[b], n = a.bstart[b + 1] - s0;
+    uint64_t s0;
+    uint32_t n;
+    if (a.capb) {
+        s0 = (uint64_t)b * a.capb;
+        n = min(a.bstart[b], a.capb);  // a larger count raised kFlCur: the call reruns
+    } else {
+        s0 = a.bstart[b];
+        n = a.bstart[b + 1] - (uint32_t)s0;
+    }
     const int tid = threadIdx.x;
     const Layout& lay = a.lay;
     if (n == 0) return;
@@ -1516,6 +1531,133 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scatter2_kernel(const unsigned
     bp_place(x, r, tn, dg.nb2, digit, lh, wave_tot, S, P2 + ((uint64_t)c * J + j) * dg.nb2, out);
 }
 
+// ------------------------------------------------------------- cursor level 2 --------------
+// Level 2 without its counting passes (bp_hist2 + bp_scan2, 45 us at config 3): every bucket
+// owns a fixed-capacity region of capb keys, and the workgroup that writes a run reserves it with
+// one returning atomic on the bucket's cursor (its count).  A bucket receives runs from ~30 tiles,
+// so the cursors see no queueing; order inside a bucket is unspecified, as with the counting
+// partition.  A run that would pass its region's end is dropped and raises kFlCur: the call
+// reruns with the counting level 2 (a skewed batch: a very frequent k-mer fills one bucket).
+// Regions are sized from the hash-uniform mean (capb ~ 2.6 x mean_keys: 0.6 GB at config 3).
+// Measured and rejected: the same reservation at level 1 (per-chunk runs into fixed-capacity
+// segments of each coarse bin, 8 / 32 / 64 cursor shards per bin instead of bp_hist1 and the
+// column scan): bp_scatter1 went from 139 us to 206 / 173 / 189 us — each of the 7,430
+// workgroups waits on its 256 returning atomics before it can write, which costs more than
+// the counting pass it replaces.
+struct CurGeom {
+    uint32_t capb;  // keys per bucket region
+};
+
+// lh holds the tile's digit histogram and r[e] every key's rank in its digit: reserve each digit's
+// run on cursor(d) (start of its region: region(d), cap keys), place the tile digit-major into S
+// and write each run at its reservation; keys past their region's end are dropped (kFlCur)
+template <class Digit, class Cursor, class Region>
+__device__ __forceinline__ void bp_place_cur(const unsigned long long (&x)[kBpPer], const uint32_t (&r)[kBpPer],
+                                             uint32_t n_in, uint32_t nb, Digit digit, Cursor cursor, Region region,
+                                             uint32_t cap, uint32_t* lh, uint32_t* wave_tot, unsigned long long* S,
+                                             unsigned long long* __restrict__ out, uint32_t* __restrict__ flags) {
+    constexpr uint32_t kQ = kBpMaxBins / kKeyThreads;
+    const uint32_t q = (nb + kKeyThreads - 1) / kKeyThreads, b0 = threadIdx.x * q;
+    uint32_t c[kQ], base[kQ], v = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < kQ; ++t) {
+        c[t] = t < q && b0 + t < nb ? lh[b0 + t] : 0u;
+        base[t] = c[t] ? atomicAdd(cursor(b0 + t), c[t]) : 0u;
+        v += c[t];
+    }
+    uint32_t excl, total;
+    block_scan_n<kKeyThreads>(v, excl, total, wave_tot);
+#pragma unroll
+    for (uint32_t t = 0; t < kQ; ++t)
+        if (t < q && b0 + t < nb) {
+            lh[b0 + t] = excl;
+            excl += c[t];
+        }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t e = 0; e < kBpPer; ++e)
+        if (x[e] != kNoKey) S[lh[digit(x[e])] + r[e]] = x[e];
+    __syncthreads();
+    // lh[d] -> global start of the digit's run minus its tile start; a run that does not fit
+    // starts at its region's end, so every one of its keys is dropped below
+    bool over = false;
+#pragma unroll
+    for (uint32_t t = 0; t < kQ; ++t)
+        if (t < q && b0 + t < nb) {
+            const bool fits = base[t] + c[t] <= cap;
+            over |= !fits;
+            lh[b0 + t] = region(b0 + t) + (fits ? base[t] : cap) - lh[b0 + t];
+        }
+    if (over) flags[kFlCur] = 1;
+    __syncthreads();
+    for (uint32_t i = 2 * threadIdx.x; i < n_in; i += 2 * kKeyThreads) {
+        const ulonglong2 y = *reinterpret_cast<const ulonglong2*>(S + i);
+        const uint32_t d0 = digit(y.x), a0 = lh[d0] + i, e0 = region(d0) + cap;
+        if (i + 1 < n_in) {
+            const uint32_t d1 = digit(y.y), a1 = lh[d1] + i + 1;
+            if (d0 == d1 && !(a0 & 1) && a1 < e0) {
+                *reinterpret_cast<ulonglong2*>(out + a0) = y;
+            } else {
+                if (a0 < e0) out[a0] = y.x;
+                if (a1 < region(d1) + cap) out[a1] = y.y;
+            }
+        } else if (a0 < e0) {
+            out[a0] = y.x;
+        }
+    }
+}
+
+// level 2, cursor variant: tile (j, c) of coarse bin c as bp_scatter2, each digit's run reserved
+// in its bucket's region; bcur[b] counts bucket b
+__global__ __launch_bounds__(kKeyThreads) void bp_scatter2c_kernel(const unsigned long long* __restrict__ in,
+                                                                   const uint32_t* __restrict__ C1, uint32_t J,
+                                                                   BpDigits dg, CurGeom cg,
+                                                                   uint32_t* __restrict__ bcur,
+                                                                   unsigned long long* __restrict__ out,
+                                                                   uint32_t* __restrict__ flags) {
+    __shared__ __attribute__((aligned(16))) unsigned long long S[kBpTile];
+    __shared__ uint32_t lh[kBpMaxBins];
+    __shared__ uint32_t wave_tot[kKeyThreads / 64];
+    const uint32_t j = blockIdx.x, c = blockIdx.y;
+    uint32_t t0, tn;
+    if (!bp_tile(C1, dg.nb1, c, j, J, t0, tn)) {
+        // a bin above its tile budget: no tile of it is written; its buckets are incomplete
+        if (j == 0 && threadIdx.x == 0 && C1[dg.nb1 + 2 + c] - C1[dg.nb1 + 1 + c] > J * kBpTile) {
+            flags[kFlBin] = 1;
+            atomicMax(&flags[kFlBinTiles], (C1[dg.nb1 + 2 + c] - C1[dg.nb1 + 1 + c] + kBpTile - 1) / kBpTile);
+        }
+        return;
+    }
+    for (uint32_t d = threadIdx.x; d < dg.nb2; d += kKeyThreads) lh[d] = 0;
+    __syncthreads();
+    unsigned long long x[kBpPer];
+    uint32_t r[kBpPer];
+    auto digit = [&](unsigned long long y) { return (uint32_t)(y >> dg.sh2) & dg.m2; };
+#pragma unroll
+    for (uint32_t e = 0; e < kBpPer; e += 2) {  // t0 is even: two keys per 16-byte load
+        const uint32_t i = 2 * threadIdx.x + e * kKeyThreads;
+        if (i + 1 < tn) {
+            const ulonglong2 y = *reinterpret_cast<const ulonglong2*>(in + t0 + i);
+            x[e] = y.x;
+            x[e + 1] = y.y;
+        } else {
+            x[e] = i < tn ? in[t0 + i] : kNoKey;
+            x[e + 1] = kNoKey;
+        }
+    }
+#pragma unroll
+    for (uint32_t e = 0; e < kBpPer; ++e) r[e] = x[e] != kNoKey ? atomicAdd(&lh[digit(x[e])], 1u) : 0u;
+    __syncthreads();
+    const uint32_t bb = c * dg.nb2;
+    bp_place_cur(
+        x, r, tn, dg.nb2, digit, [&](uint32_t d) { return &bcur[bb + d]; },
+        [&](uint32_t d) { return (bb + d) * cg.capb; }, cg.capb, lh, wave_tot, S, out, flags);
+}
+
+__global__ void bp_cur_clear_kernel(uint32_t* __restrict__ cur, uint32_t n) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) cur[i] = 0;
+}
+
 // the small bucket kernel for this layout: merged slot words when the bucket field is wide enough;
 // a 1,024-key capacity (four keys per thread) when the mean bucket is small enough that a bucket
 // above it is a > 4-sigma event (the large kernel takes those)
@@ -1609,6 +1751,12 @@ struct kmp_postings {
     uint32_t bp_J_min = 0;      // ... at least (learned from an overflowing bin)
     uint64_t bp_c1 = 0;         // offset of C1 (coarse bin starts) in ws->bp
     bool parted = false;        // ws->keys holds level-1 output (bp_level1 ran for this call)
+    // cursor level 2 (fixed-capacity bucket regions, no counting passes): tried first for a new
+    // shape (cur_on), dropped for the shape after a region overflow; cur_used: the buckets in
+    // ws->sorted came from it (ws->cur: bucket counts)
+    bool cur_mode = true, cur_on = true, cur_used = false;
+    Grow<uint32_t> cur;
+    CurGeom cg{};
     // heavy path (frequent k-mers): spill regions, the gathered + sorted spill, its elements,
     // k-mer starts, per-k-mer row bounds / tile counts / tile offsets
     Grow<unsigned long long> spill, hkeys, hsorted, hGS, htc, htoff, hoff;
@@ -1637,7 +1785,7 @@ struct kmp_postings {
         for (auto* g : {&keys, &sorted, &inc, &inc_sorted, &uniq, &bstats, &btot, &boff, &spill, &hkeys, &hsorted,
                         &hGS, &htc, &htoff, &hoff, &ovk, &ovx})
             g->release();
-        for (auto* g : {&w, &keep, &pos, &small, &cnt, &flags, &chunk_first, &bp, &pt, &ovf, &ovr, &hE, &hgi, &hcnt})
+        for (auto* g : {&w, &keep, &pos, &small, &cnt, &flags, &chunk_first, &bp, &pt, &ovf, &ovr, &hE, &hgi, &hcnt, &cur})
             g->release();
         tmp.release();
         for (auto& e : ev)
@@ -1714,6 +1862,31 @@ int bp_level2(kmp_postings* ws, const Layout& lay, hipStream_t st) {
     return KMP_OK;
 }
 
+// Cursor level-2 geometry from the hash-uniform mean bucket; false when the region offsets
+// would not fit the u32 arithmetic of the kernels
+bool cur_geometry(const Layout& lay, CurGeom* cg) {
+    const uint64_t nb = 1ull << lay.bbits;
+    const uint64_t capb = (std::max<uint64_t>(2ull * lay.mean_keys + 512, 1536) + 63) / 64 * 64;
+    if (nb * capb + capb >= (1ull << 32) - 2 * kBpTile) return false;
+    cg->capb = (uint32_t)capb;
+    return true;
+}
+
+// Level 2, cursor variant: ws->keys (level 1) -> the bucket regions of ws->sorted, counts in ws->cur.
+int bp_level2c(kmp_postings* ws, const Layout& lay, hipStream_t st) {
+    const BpDigits dg = bp_digits(lay);
+    const uint32_t nb = 1u << lay.bbits;
+    uint32_t* C1 = ws->bp.p + ws->bp_c1;
+    PG(ws->cur.reserve(nb));
+    PG(ws->sorted.reserve((uint64_t)nb * ws->cg.capb));
+    PG(ws->cnt.reserve(2 * (uint64_t)nb + 2));  // the large-bucket list
+    bp_cur_clear_kernel<<<std::min<uint32_t>((nb + 1023) / 1024, 1024), 1024, 0, st>>>(ws->cur.p, nb);
+    bp_scatter2c_kernel<<<dim3(ws->bp_J, dg.nb1), kKeyThreads, 0, st>>>(ws->keys.p, C1, ws->bp_J, dg, ws->cg,
+                                                                       ws->cur.p, ws->sorted.p, ws->flags.p);
+    PG(hipGetLastError());
+    return KMP_OK;
+}
+
 // Bucketed front: keys `in` grouped by bucket into ws->sorted, bstart[0..nb] in ws->cnt.  After
 // bp_level1 (ws->parted) that is level 2; otherwise a radix sort on the bucket field and a binary
 // search per bucket.  Marks 2 after the grouping.
@@ -1722,7 +1895,7 @@ int bucket_group(kmp_postings* ws, const unsigned long long* in, uint64_t slots,
     PG(ws->sorted.reserve(slots));
     if (ws->parted && in == ws->keys.p) {
         ws->parted = false;
-        int rc = bp_level2(ws, lay, st);
+        int rc = ws->cur_used ? bp_level2c(ws, lay, st) : bp_level2(ws, lay, st);
         ws->mark(2, st);
         return rc;
     }
@@ -2220,11 +2393,10 @@ __global__ __launch_bounds__(256) void pt_emit_kernel(const uint32_t* __restrict
 // LDS capacity are finished by one segmented sort (pt_finish_overflow) without a rerun.
 // Marks 0 (start), 1 (keys / level 1), 2 (level 2), 3 (bucket kernels [+ heavy]), 4 (pair
 // partition), 5 (row-block sort + encode), 6 (emit + read-back).
-enum : uint32_t { kFlBin = 0, kFlClass = 1, kFlList = 2, kFlOvf = 3, kFlBinTiles = 4, kFlN = 8 };
 // read-back: gstats (8 per shard) | pair cursors | spill cursors | the words below
 enum : uint32_t {
     kRbCursor = kShards * 8, kRbSpill = kShards * 9, kRbFlagBin = kShards * 10, kRbFlagClass, kRbRuns, kRbOvf,
-    kRbMaxBlock, kRbBinTiles, kRbWords
+    kRbMaxBlock, kRbBinTiles, kRbFlagCur, kRbWords
 };
 constexpr uint32_t kGsWords = kShards * 10;  // gstats | cursors | spill cursors (u64)
 
@@ -2243,6 +2415,7 @@ __global__ void step_pack_kernel(const unsigned long long* __restrict__ gstats, 
         rb[kRbOvf] = flags[kFlOvf];
         rb[kRbMaxBlock] = runs ? runs[1] : 0;
         rb[kRbBinTiles] = flags[kFlBinTiles];
+        rb[kRbFlagCur] = flags[kFlCur];
     }
     __threadfence_system();  // rb is host memory, read after the stream synchronises
 }
@@ -2311,6 +2484,10 @@ BucketArgs bucket_args(kmp_postings* ws, const StepCfg& c, bool spill) {
     const uint32_t nb = 1u << c.lay.bbits;
     a.sorted = ws->sorted.p;
     a.bstart = ws->cnt.p;
+    if (ws->cur_used) {
+        a.bstart = ws->cur.p;  // bucket counts
+        a.capb = ws->cg.capb;
+    }
     a.lay = c.lay;
     a.mul = 1u << bits_for(c.n);  // pair key p << pbits | q (the row-block tail's key)
     a.require_diff = c.require_diff;
@@ -2624,6 +2801,7 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
         ws->pt_rb_max = 16;
         ws->bp_J_min = 0;
         ws->heavy = false;
+        ws->cur_on = ws->cur_mode;
     }
     if (ws->shard_cap == 0) ws->shard_cap = c.slots / 4 / kShards + 4096;
     if (ws->spill_cap == 0) ws->spill_cap = 1024;
@@ -2648,8 +2826,9 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
             key.push_back(ws->timing);
             key.push_back(g.rbits + 1);
             key.push_back(g_grow_gen);
+            key.push_back(ws->cur_on);
             int rc = fused_launch(ws, make_keys, key, c, g, st);
-            key.resize(key.size() - 5);
+            key.resize(key.size() - 6);
             if (rc != KMP_OK) return rc;
             PG(hipStreamSynchronize(st));
         } else {
@@ -2664,6 +2843,10 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
         }
         sum_stats(rb, acc, &most, &n_inc, &spill_most, &spill_total);
         bool rerun = false;
+        if (rb[kRbFlagCur] && ws->cur_used) {  // a region of the cursor partition overflowed
+            ws->cur_on = false;
+            rerun = true;
+        }
         if (rb[kRbFlagBin]) {  // a coarse bin above its level-2 tile budget
             ws->bp_J_min = (uint32_t)rb[kRbBinTiles] + 2;
             rerun = true;
@@ -2949,6 +3132,19 @@ int kmp_postings_set_graph(kmp_postings* ws, int enable) {
 
 uint64_t kmp_postings_graph_replays(const kmp_postings* ws) { return ws ? ws->graph_replays : 0; }
 
+int kmp_postings_set_partition(kmp_postings* ws, int mode) {
+    if (!ws || (mode != KMP_PARTITION_AUTO && mode != KMP_PARTITION_COUNT)) return KMP_EINVAL;
+    ws->cur_mode = mode == KMP_PARTITION_AUTO;
+    ws->cur_on = ws->cur_mode;
+    ws->front_ok = false;
+    return KMP_OK;
+}
+
+int kmp_postings_last_partition(const kmp_postings* ws) {
+    if (!ws || !ws->last_bucketed) return -1;
+    return ws->cur_used ? KMP_PARTITION_CURSOR : KMP_PARTITION_COUNT;
+}
+
 int kmp_postings_set_reuse(kmp_postings* ws, int enable) {
     if (!ws) return KMP_EINVAL;
     ws->reuse = enable != 0;
@@ -2966,6 +3162,7 @@ int kmp_dev_pairs_postings(kmp_postings* ws, const uint32_t* d_set, const uint32
     if (!d_set || !d_set_len || !d_res_off || !d_class) return KMP_EINVAL;
     hipStream_t st = as_stream(stream);
     auto keys = [&](const Layout& lay, hipStream_t st) {
+        ws->cur_used = false;  // keys grouped by the bucket sort
         set_keys_kernel<<<n + 1, 256, 0, st>>>(d_set, d_set_len, d_res_off, d_class, n, slots, lay, ws->keys.p,
                                                ws->flags.p);
         return hipGetLastError();
@@ -2988,8 +3185,10 @@ static int residues_impl(kmp_postings* ws, const uint8_t* d_res, const uint64_t*
     auto keys = [&](const Layout& lay, hipStream_t st) {
         if (lay.bucketed) {
             ws->parted = true;
+            ws->cur_used = ws->cur_on && cur_geometry(lay, &ws->cg);
             return bp_level1(ws, d_res, d_res_off, d_class, k, n, slots, lay, st);
         }
+        ws->cur_used = false;
         return launch_residue_keys(ws, d_res, d_res_off, d_class, k, 0u, n, 0ull, slots, lay, st);
     };
     const std::vector<unsigned long long> key_extra = {1, (uintptr_t)d_res, (uintptr_t)d_res_off, (uintptr_t)d_class};

@@ -227,6 +227,17 @@ class DevicePipeline:
         (the row passes of one step): kmp_postings_set_reuse."""
         check(lib().kmp_postings_set_reuse(self._workspace(), int(enable)), "kmp_postings_set_reuse")
 
+    def set_partition(self, mode: str = "auto") -> None:
+        """Residue path's bucket partition: 'auto' (cursor partition, the counting partition for a
+        shape whose regions overflow) or 'count' (the counting partition only)."""
+        m = {"auto": _lib.KMP_PARTITION_AUTO, "count": _lib.KMP_PARTITION_COUNT}[mode]
+        check(lib().kmp_postings_set_partition(self._workspace(), m), "kmp_postings_set_partition")
+
+    def last_partition(self) -> str:
+        """Partition of the last bucketed call: 'cursor' or 'count' ('' on the flat layout)."""
+        r = lib().kmp_postings_last_partition(self._workspace())
+        return {_lib.KMP_PARTITION_CURSOR: "cursor", _lib.KMP_PARTITION_COUNT: "count"}.get(r, "")
+
     def graph_replays(self) -> int:
         return int(lib().kmp_postings_graph_replays(self._workspace()))
 
