@@ -9,7 +9,13 @@ w = |K(p) ∩ K(q)| in canonical order (Graph::new + remove_uninteresting_edges 
 Inputs are synthetic (N = 100,000, seed 3, len ~ N(300, 30^2), k = 7).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--engine residues|postings|tiles]
-  N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+  N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N [--split kmer|rows]
+
+N > 1 (config 4): one process per GPU over RCCL, the k-mer split (dist.kmer_split_step): each rank
+groups and expands its share of the k-mers, one all-to-all moves the pair keys to their row
+owners, each rank reduces its rows.  The step ends with every rank holding the canonical edges of
+its row range in HBM (rank order = canonical order); the gather of all of them onto one GPU is
+timed apart (gather_ms) and is not part of the step.
 """
 from __future__ import annotations
 
@@ -66,6 +72,7 @@ def parse():
     ap.add_argument("--engine", default="residues", choices=["residues", "postings", "tiles"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="oracle threads (0: min(16, cores))")
+    ap.add_argument("--split", default="kmer", choices=["kmer", "rows"], help="multi-GPU flow (N > 1)")
     return ap.parse_args()
 
 
@@ -173,7 +180,7 @@ def main():
     import uniprot_kmer_based_clustering_amd as K
     from uniprot_kmer_based_clustering_amd import _lib
     from uniprot_kmer_based_clustering_amd.device import DevicePipeline
-    from uniprot_kmer_based_clustering_amd.dist import distributed_step
+    from uniprot_kmer_based_clustering_amd.dist import distributed_step, kmer_split_step
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -192,7 +199,9 @@ def main():
     torch.cuda.synchronize()
     postings = args.engine in ("residues", "postings")
 
-    def one_step():
+    def one_step(timings=None, gather=False):
+        if world > 1 and args.split == "kmer":
+            return kmer_split_step(pipe, rank, world, gather=gather, timings=timings)
         if world > 1:
             return distributed_step(pipe, rank, world)
         return pipe.step(engine=args.engine)
@@ -217,10 +226,37 @@ def main():
     dt = time.perf_counter() - t0
     if postings and world == 1:
         pipe.set_stage_timing(False)
+    rank_info = None
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+        # untimed: the edge total over the ranks, per-rank phase times, and the gather to rank 0
+        ne = torch.tensor([n_edges], dtype=torch.int64, device=f"cuda:{local}")
+        if args.split == "kmer":
+            dist.all_reduce(ne)
+            stt = pipe._split_state.bufs[3].clone()
+            dist.all_reduce(stt)  # every rank's k-mers' statistics: the batch's
+            split_stats = [int(x) for x in stt.tolist()]
+            tims = []
+            for _ in range(5):
+                kmer_split_step(pipe, rank, world, timings=tims)
+            ph = torch.tensor(np.mean(np.array(tims), axis=0), dtype=torch.float64, device=f"cuda:{local}")
+            lo, hi = (int(x) for x in _lib.row_split(n, world)[rank:rank + 2])
+            mine = torch.tensor([rank, lo, hi, n_edges, *ph.tolist()], dtype=torch.float64, device=f"cuda:{local}")
+            allv = [torch.zeros_like(mine) for _ in range(world)]
+            dist.all_gather(allv, mine)
+            rank_info = [dict(zip(("rank", "row_lo", "row_hi", "edges", "expand_ms", "exchange_ms", "edges_ms"),
+                                  [int(v) if i < 4 else v for i, v in enumerate(x.tolist())])) for x in allv]
+            dist.barrier()
+            torch.cuda.synchronize()
+            g0 = time.perf_counter()
+            tot = kmer_split_step(pipe, rank, world, gather=True)
+            torch.cuda.synchronize()
+            gather_ms = (time.perf_counter() - g0) * 1e3
+            if rank == 0:
+                assert tot == int(ne.item()), (tot, int(ne.item()))
+        n_edges = int(ne.item())
 
     ms = dt / args.steps * 1e3
     pairs_total = n * (n - 1) / 2
@@ -244,9 +280,26 @@ def main():
             "config": {"workload": WORKLOADS[args.config],
                        "proteins": n, "k": k, "pairs": int(pairs_total), "edges": int(n_edges),
                        "engine": args.engine,
-                       "parallelism": "single GPU" if world == 1 else f"row split x{world}"},
+                       "parallelism": ("single GPU" if world == 1 else
+                                       f"k-mer split x{world} (all-to-all of pair keys)" if args.split == "kmer"
+                                       else f"row split x{world}")},
             "edges_per_s": n_edges / (dt / args.steps),
         }
+        if rank_info is not None:
+            # roofline of the whole multi-GPU step: its algorithmic bytes (the single-GPU stage
+            # model over all ranks' work plus the pair keys crossing the links) against N x peak
+            lens = np.diff(np.asarray(proteins.offsets, dtype=np.int64))
+            n_win = int(np.maximum(lens - k + 1, 0).sum())
+            n_inc = split_stats[6]
+            byts = sum(stage_bytes(int(proteins.offsets[-1]), 0, n_inc, n_edges, n_edges, "rows", n_win).values())
+            ach = byts / (ms * 1e-3) / 1e9
+            out["roofline"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
+                               "frac": ach / (HBM_PEAK_GBS * world), "traffic": None,
+                               "kernel": f"whole step over {world} GPUs", "alg_bytes_per_step": byts,
+                               "incidences": n_inc, "exchange_bytes": 8 * n_inc}
+            out["ranks"] = rank_info
+            out["gather_ms"] = gather_ms
+            out["edges_layout"] = "row-sharded across ranks (rank order = canonical); gather_ms = step + gather"
         if args.engine in ("residues", "postings"):
             out["config"]["layout"] = pipe.last_layout()
             out["config"]["heavy_path"] = pipe.last_heavy()

@@ -101,16 +101,23 @@ int kmp_ctx_create(kmp_ctx** ctx, int device, int cpu_threads);
 /* Multi-GPU context (the reference's `threads` split of the same work, main.rs:57-60,
  * graph/mod.rs:81-124): n_gpus ranks on the HIP devices devices[0..n_gpus) (NULL: 0..n_gpus-1),
  * rank 0 on devices[0] doing everything a single-GPU context does.  kmp_load_proteins copies the
- * batch to every rank; kmp_pairs (engine AUTO / RESIDUES) splits the pair space by rows
- * (kmp_row_split: rank g expands the pairs whose smaller protein is in its rows, on its own device
- * and host thread) and gathers the ranks' edges to device 0 in rank order, which is the canonical
- * list.  The library owns the collective: distinct devices get RCCL communicators created
+ * batch to every rank; kmp_pairs (engine AUTO / RESIDUES) leaves rank g with the canonical edges of
+ * its rows (kmp_row_split: the pairs whose smaller protein is in them) — by the k-mer split (rank g
+ * expands its share of the k-mers, an all-to-all routes each pair key to its row owner, which
+ * reduces it; kmp_dev_split_expand / kmp_dev_split_edges) or, when the batch spills frequent
+ * k-mers, by the row split (every rank groups every k-mer and expands its rows) — and gathers the
+ * ranks' edges to device 0 in rank order, which is the canonical list.  The library owns the
+ * collectives: distinct devices get RCCL communicators created
  * in-process (ncclCommInitAll; KMP_ERCCL if RCCL is unavailable or a collective fails); a device
  * listed more than once runs several ranks on one GPU and the gather uses device copies (for
  * testing the split where RCCL admits one rank per device).  Other engines run on rank 0. */
 int kmp_ctx_create_multi(kmp_ctx** ctx, int n_gpus, const int* devices, int cpu_threads);
 int kmp_ctx_gpus(const kmp_ctx* ctx);               /* ranks (1 for kmp_ctx_create) */
 const char* kmp_ctx_transport(const kmp_ctx* ctx);  /* "local", "copy" or "rccl" */
+/* the flow of the last multi-GPU kmp_pairs: "kmer" (the k-mer split: each rank expands its share of
+ * the k-mers, an all-to-all routes the pair keys to their row owners; kmp_dev_split_expand) or
+ * "rows" (the row split, for batches whose frequent k-mers spill); "" before one */
+const char* kmp_ctx_last_split(const kmp_ctx* ctx);
 void kmp_ctx_destroy(kmp_ctx* ctx);
 const char* kmp_last_error(const kmp_ctx* ctx);
 
@@ -424,6 +431,37 @@ int kmp_dev_pairs_rows(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d
                        uint32_t n, int k, uint64_t slots, uint32_t heavy_df, uint32_t min_shared,
                        int require_class_diff, uint32_t row_lo, uint32_t row_hi, uint32_t* d_p, uint32_t* d_q,
                        uint32_t* d_w, uint64_t cap, uint64_t* n_edges, kmp_postings_stats* stats, void* stream);
+/* The multi-GPU k-mer split (the reference's `threads` share the same work through
+ * one sorted k-mer list, main.rs:77-122 / mod.rs:81-124).  Rank `part` of `parts` (<= 64):
+ *   kmp_dev_split_expand  every window of the batch is keyed, the rank keeps the k-mers of its
+ *     share of the bucket hash range (a contiguous range of coarse bins), groups and expands them
+ *     (all rows), and routes each pair key (p << bits(N) | q) to the rank owning row p
+ *     (kmp_row_split): region d of d_send (cap keys, unused tail kNoKey) is rank d's.  No host
+ *     synchronisation; d_flags[KMP_SPLIT_FLAGS] and d_stats[8] (Σ|K(p)|, distinct, repeat,
+ *     Σ C(df,2), max df, heavy entries, incidences, 0 — this rank's k-mers) are written on `stream`.
+ *     learn: the previous call's flags reduced (max) over the ranks, or NULL for a first call;
+ *     every rank grows its capacities from them identically.
+ *   exchange (the caller's collective): region d of rank g's d_send -> region g of rank d's receive
+ *     buffer (an all-to-all of equal splits, cap keys each).
+ *   kmp_dev_split_edges   the m = parts * cap received keys -> the canonical edges of rows
+ *     [row_lo, row_hi) (the row-block tail), *n_edges; KMP_EOVERFLOW when cap is smaller (grow and
+ *     call again with the same keys).  Synchronises `stream`.
+ * The rank-order concatenation of the ranks' edges is the canonical list.  Flags: RERUN (a send
+ * region, pair-key shard or bucket region overflowed: call expand again with learn, after growing
+ * cap to at least MAX_PART when that is the cause), CLASS (class ids too wide: single GPU) and
+ * HEAVY (k-mers above the LDS group limit spilled: use the row split, kmp_dev_pairs_rows). */
+enum {
+    KMP_SPLIT_RERUN = 0, KMP_SPLIT_CLASS = 1, KMP_SPLIT_HEAVY = 2, KMP_SPLIT_MAX_PART = 3,
+    KMP_SPLIT_MAX_SHARD = 4, KMP_SPLIT_BIN_TILES = 5, KMP_SPLIT_CURSOR = 6, KMP_SPLIT_FLAGS = 8
+};
+int kmp_dev_split_expand(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
+                         uint32_t n, int k, uint64_t slots, uint32_t heavy_df, int require_class_diff, uint32_t part,
+                         uint32_t parts, uint64_t cap, const uint32_t* learn, unsigned long long* d_send,
+                         uint32_t* d_flags, unsigned long long* d_stats, void* stream);
+int kmp_dev_split_edges(kmp_postings* ws, const unsigned long long* d_keys, uint64_t m, uint32_t n, uint32_t row_lo,
+                        uint32_t row_hi, uint32_t min_shared, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w,
+                        uint64_t cap, uint64_t* n_edges, void* stream);
+
 /* Row ranges of a split of the pair space: range d = [start[d], start[d+1]) with start[d] =
  * floor(N (1 - sqrt(1 - d/parts))): a pair belongs to its smaller protein, so the ranges hold about
  * equal pair counts.  start has parts + 1 entries. */

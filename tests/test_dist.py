@@ -1,5 +1,6 @@
-"""The multi-GPU row split (uniprot_kmer_based_clustering_amd/dist.py) on CPU: world_size 2 and
-3 over gloo.  Each rank's device stage (kmp_dev_pairs_rows, GPU-only) is stood in for by the
+"""The multi-GPU flows (uniprot_kmer_based_clustering_amd/dist.py) on CPU: world_size 2 and 3
+over gloo — the row split and the k-mer split (kmer_split_step: all-to-all of the routed pair
+keys, flags reduced over the ranks, capacity reruns, row-split fallback).  Each rank's device stage (kmp_dev_pairs_rows, GPU-only) is stood in for by the
 oracle's edge list restricted to the rank's rows; the test checks that the ranks' blocks,
 gathered in place to rank 0, concatenate to exactly the single-process canonical list (the
 result is invariant to the number of ranks), including empty blocks and a rank-0 destination
@@ -78,6 +79,109 @@ def worker(rank, world, port, out_q):
         out_q.put(("ranges", rank, ranges))
     finally:
         dist.destroy_process_group()
+
+
+def bits_for(v):
+    b = 0
+    while b < 64 and (v - 1) >> b:
+        b += 1
+    return max(b, 1)
+
+
+class OracleSplitPipe(OraclePipe):
+    """CPU stand-in for the k-mer split stages.  split_expand: rank `part` owns a share of every
+    pair's w (w // parts, plus one for the first w % parts ranks: the shares of the k-mers of its
+    hash range), emits one pair key p << bits(N) | q per incidence and routes it to the row owner,
+    padded regions of cap keys (-1 = kNoKey), flags as the library's; split_edges: run-length
+    counts of the received keys of its rows, canonical order."""
+
+    def __init__(self, n, p, q, w, cap, heavy=False):
+        super().__init__(n, p, q, w, cap)
+        self.total = 300 * n
+        self.dev = torch.device("cpu")
+        self.heavy = heavy
+        self.pbits = bits_for(n)
+
+    def split_expand(self, part, parts, cap, send, flags, stats, learn=None, require_class_diff=True):
+        from uniprot_kmer_based_clustering_amd import _lib
+        from uniprot_kmer_based_clustering_amd.dist import row_ranges
+        share = self.W // parts + (part < self.W % parts)
+        keys = np.repeat((self.P.astype(np.int64) << self.pbits) | self.Q.astype(np.int64), share)
+        send.fill_(-1)
+        most = 0
+        for d, (lo, hi) in enumerate(row_ranges(self.n, parts)):
+            kd = keys[((keys >> self.pbits) >= lo) & ((keys >> self.pbits) < hi)][::-1]  # any order
+            most = max(most, len(kd))
+            send[d * cap:d * cap + min(cap, len(kd))] = torch.from_numpy(kd[:cap].copy())
+        flags.zero_()
+        flags[_lib.KMP_SPLIT_MAX_PART] = most
+        flags[_lib.KMP_SPLIT_RERUN] = int(most > cap)
+        flags[_lib.KMP_SPLIT_HEAVY] = int(self.heavy)
+        stats.zero_()
+        stats[6] = int(share.sum())
+
+    def split_edges(self, recv, lo, hi, min_shared=1):
+        x = recv.numpy()
+        x = x[x != -1]
+        assert np.all(((x >> self.pbits) >= lo) & ((x >> self.pbits) < hi))
+        u, c = np.unique(x, return_counts=True)
+        keep = c >= min_shared
+        u, c = u[keep], c[keep]
+        m = len(u)
+        if m > self.edge_cap:
+            self._alloc_edges(m)
+        self.ep[:m] = torch.from_numpy((u >> self.pbits).astype(np.int32))
+        self.eq[:m] = torch.from_numpy((u & ((1 << self.pbits) - 1)).astype(np.int32))
+        self.ew[:m] = torch.from_numpy(c.astype(np.int32))
+        self.n_edges = m
+        return m
+
+
+def split_worker(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, ROOT)
+        from uniprot_kmer_based_clustering_amd.dist import SplitState, kmer_split_step
+        b, o = build_case()
+        P, Q, W = o.pairs()
+        for heavy in (False, True):
+            pipe = OracleSplitPipe(b.n, P, Q, W, cap=16 if rank == 0 else 1 << 20, heavy=heavy)
+            state = SplitState()
+            state.cap = 64  # far too small: the first step reruns with the learned capacity
+            for ms in (1, 3):
+                n = kmer_split_step(pipe, rank, world, min_shared=ms, gather=True, state=state)
+                if rank == 0:
+                    keep = W >= ms
+                    ok = (n == int(keep.sum())
+                          and np.array_equal(pipe.ep[:n].numpy().view(np.uint32), P[keep])
+                          and np.array_equal(pipe.eq[:n].numpy().view(np.uint32), Q[keep])
+                          and np.array_equal(pipe.ew[:n].numpy().view(np.uint32), W[keep]))
+                    out_q.put(("split", heavy, ms, ok, n, state.reruns, state.row_split, state.cap))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_kmer_split_exchange(world):
+    """kmer_split_step over gloo: the all-to-all of routed pair keys and the per-rank reduction
+    give the canonical list gathered on rank 0; an undersized exchange capacity reruns once with
+    the capacity learned from the reduced flags; a spilling batch falls back to the row split."""
+    port = free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=split_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    msgs = [q.get(timeout=300) for _ in range(4)]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert all(m[3] for m in msgs), msgs
+    light = [m for m in msgs if not m[1]]
+    assert light[0][5] == 1 and not light[0][6] and light[0][7] > 64  # one rerun, then the learned cap
+    assert all(m[6] for m in msgs if m[1])  # heavy: the row split
 
 
 @pytest.mark.parametrize("world", [2, 3])

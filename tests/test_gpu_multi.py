@@ -39,6 +39,7 @@ def test_virtual_ranks_config4(config4, g):
             got = e.pairs()
             assert len(got) == len(p) > 1_000_000
             assert_edges(got, p, q, w)
+            assert e.last_split == "kmer"
         c = e.counters()
         assert c["n_edges"] == len(p)
 
@@ -52,7 +53,7 @@ def test_virtual_ranks_heavy_uniprot_k5():
         e.load(K.Proteins(res, off, cls))
         e.build_sets(5)
         got = e.pairs()
-        assert len(got) == g["n_edges"]
+        assert len(got) == g["n_edges"] and e.last_split == "rows"  # frequent 5-mers spill
         assert edges_sha256(got.p, got.q, got.w) == g["edges_sha256"]
         c = e.counters()
         assert c["sum_w_diff"] == g["sum_w_diff"] and c["n_align"] == g["n_align"]
@@ -98,3 +99,74 @@ def test_rccl_transport_single_device(oracle_mod):
             e.load(b)
             e.build_sets(7)
             assert_edges(e.pairs(), p, q, w)
+
+
+def emulate_kmer_split(b, k, G, cap=None, min_shared=1):
+    """The k-mer split's G ranks on one GPU, in one process: every rank's kmp_dev_split_expand on
+    its own DevicePipeline, the all-to-all done by slicing the send regions, every rank's
+    kmp_dev_split_edges; flags reduced (max) over the ranks and fed back as `learn` on a rerun,
+    as dist.kmer_split_step does over RCCL.  Returns the concatenated edges, the flags, the
+    summed statistics and the number of reruns."""
+    import torch
+    from uniprot_kmer_based_clustering_amd.device import DevicePipeline
+    pipes = [DevicePipeline(b, k, "cuda:0") for _ in range(G)]
+    start = _lib.row_split(b.n, G)
+    cap = cap or max(4096, pipes[0].total // 4 // (G * G))
+    learn, reruns = None, 0
+    for _ in range(6):
+        sends = [torch.empty(G * cap, dtype=torch.int64, device="cuda:0") for _ in range(G)]
+        flags = [torch.zeros(_lib.KMP_SPLIT_FLAGS, dtype=torch.int32, device="cuda:0") for _ in range(G)]
+        stats = [torch.zeros(8, dtype=torch.int64, device="cuda:0") for _ in range(G)]
+        for r in range(G):
+            pipes[r].split_expand(r, G, cap, sends[r], flags[r], stats[r], learn=learn)
+        fl = torch.stack(flags).max(dim=0).values.cpu().tolist()
+        out = [[], [], []]
+        for d in range(G):
+            recv = torch.cat([sends[r][d * cap:(d + 1) * cap] for r in range(G)])
+            pipes[d].split_edges(recv, int(start[d]), int(start[d + 1]), min_shared)
+            for a, x in zip(out, pipes[d].edges()):
+                a.append(x)
+        if fl[_lib.KMP_SPLIT_RERUN] and not (fl[_lib.KMP_SPLIT_HEAVY] or fl[_lib.KMP_SPLIT_CLASS]):
+            reruns += 1
+            learn = fl
+            cap = max(cap, fl[_lib.KMP_SPLIT_MAX_PART] + fl[_lib.KMP_SPLIT_MAX_PART] // 16 + 1024)
+            continue
+        st = torch.stack(stats).cpu().numpy()
+        tot = st.sum(axis=0)
+        tot[4] = st[:, 4].max()
+        return [np.concatenate(a) for a in out], fl, tot, reruns
+    raise AssertionError("capacities unstable")
+
+
+@pytest.mark.parametrize("g", [1, 2, 4, 8])
+def test_kmer_split_config4(config4, oracle_mod, g):
+    """Config 4's workload (100k proteins, k = 7) through the k-mer split's device stages at
+    G ranks: the rank-order concatenation of the ranks' edges equals the oracle's canonical list,
+    and the ranks' statistics add up to the whole batch's (Σ C(df,2), distinct, incidences)."""
+    b, (p, q, w) = config4
+    (ep, eq, ew), fl, tot, _ = emulate_kmer_split(b, 7, g)
+    assert not fl[_lib.KMP_SPLIT_HEAVY] and not fl[_lib.KMP_SPLIT_CLASS]
+    np.testing.assert_array_equal(ep, p)
+    np.testing.assert_array_equal(eq, q)
+    np.testing.assert_array_equal(ew, w)
+    c = oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=7, threads=16).counters()
+    assert tot[3] == c["sum_cdf2"] and tot[1] == c["distinct"] and tot[4] == c["max_df"]
+    assert tot[6] == int(w.sum())  # incidences after the class filter = Σ w of the canonical list
+
+
+def test_kmer_split_reruns_and_options(oracle_mod):
+    """An exchange capacity far too small reruns with the capacity learned from the reduced
+    flags (same edges); min_shared on the receiving side; the reference's dataset at k = 5
+    (frequent 5-mers spill) raises HEAVY, the caller's cue for the row split."""
+    b = K.synth(20000, 9)
+    o = oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=7, threads=8)
+    for ms in (1, 2):
+        (ep, eq, ew), fl, _, reruns = emulate_kmer_split(b, 7, 3, cap=64, min_shared=ms)
+        p, q, w = o.pairs(min_shared=ms)
+        assert reruns == 1
+        np.testing.assert_array_equal(ep, p)
+        np.testing.assert_array_equal(eq, q)
+        np.testing.assert_array_equal(ew, w)
+    res, off, cls, _ = uniprot()
+    _, fl, _, _ = emulate_kmer_split(K.Proteins(res, off, cls), 5, 2)
+    assert fl[_lib.KMP_SPLIT_HEAVY] == 1

@@ -1,8 +1,10 @@
-"""Per-rank compute of the multi-GPU row split, emulated on one GPU: for G = 1, 2, 4, 8 every
-rank's step (kmp_dev_pairs_rows over its kmp_row_split rows, graph-captured after its second
-call) is timed in turn on its own DevicePipeline; the slowest rank bounds the step.  The gather
-to rank 0 (point-to-point over xGMI) is not included.  Diagnostic tool:
-python tools/time_dist_rank.py [config3|config1]"""
+"""Per-rank device time of the two multi-GPU flows, emulated on one GPU (diagnostic):
+  rows   the row split: every rank's kmp_dev_pairs_rows over its kmp_row_split rows;
+  kmer   the k-mer split: every rank's kmp_dev_split_expand (its share of the bucket hash range,
+         pair keys routed by row owner) and kmp_dev_split_edges over the keys it would receive.
+For G = 1, 2, 4, 8 each rank's stages are timed in turn on its own DevicePipeline; the slowest
+rank bounds the step.  Exchanges (all-to-all, gather) are not included.
+python tools/time_dist_rank.py [config3|config1] [rows|kmer] [G ...]"""
 import json
 import os
 import sys
@@ -14,39 +16,69 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 from bench import load_batch, CONFIGS  # noqa: E402
+from uniprot_kmer_based_clustering_amd import _lib  # noqa: E402
 from uniprot_kmer_based_clustering_amd.device import DevicePipeline  # noqa: E402
 from uniprot_kmer_based_clustering_amd.dist import row_ranges  # noqa: E402
 
 
-def main():
-    name = sys.argv[1] if len(sys.argv) > 1 else "config3"
-    k = CONFIGS[name][3]
-    b = load_batch(name)
-    out = {"config": name, "n": b.n, "ranks": {}}
-    full = DevicePipeline(b, k, "cuda:0")
+def timed(fn, reps=10):
     for _ in range(3):
-        full.step()
+        fn()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(20):
-        full.step()
+    for _ in range(reps):
+        fn()
     torch.cuda.synchronize()
-    out["single_gpu_ms"] = (time.perf_counter() - t0) / 20 * 1e3
-    for g in (1, 2, 4, 8):
-        per = []
-        for r, (lo, hi) in enumerate(row_ranges(b.n, g)):
-            pipe = DevicePipeline(b, k, "cuda:0")
-            for _ in range(3):
-                m = pipe.rows(lo, hi)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(10):
-                m = pipe.rows(lo, hi)
-            torch.cuda.synchronize()
-            per.append({"rows": [lo, hi], "ms": (time.perf_counter() - t0) / 10 * 1e3, "edges": m})
-            del pipe
+    return (time.perf_counter() - t0) / reps * 1e3
+
+
+def kmer_ranks(b, k, g):
+    pipes = [DevicePipeline(b, k, "cuda:0") for _ in range(g)]
+    cap = max(4096, pipes[0].total // 4 // (g * g))
+    learn = None
+    for _ in range(4):  # learn the capacities
+        sends = [torch.empty(g * cap, dtype=torch.int64, device="cuda:0") for _ in range(g)]
+        flags = [torch.zeros(_lib.KMP_SPLIT_FLAGS, dtype=torch.int32, device="cuda:0") for _ in range(g)]
+        stats = [torch.zeros(8, dtype=torch.int64, device="cuda:0") for _ in range(g)]
+        for r in range(g):
+            pipes[r].split_expand(r, g, cap, sends[r], flags[r], stats[r], learn=learn)
+        fl = torch.stack(flags).max(dim=0).values.cpu().tolist()
+        if not fl[_lib.KMP_SPLIT_RERUN]:
+            break
+        learn = fl
+        cap = max(cap, fl[_lib.KMP_SPLIT_MAX_PART] * 17 // 16 + 1024)
+    recvs = [torch.cat([sends[r][d * cap:(d + 1) * cap] for r in range(g)]) for d in range(g)]
+    per = []
+    for r, (lo, hi) in enumerate(row_ranges(b.n, g)):
+        t1 = timed(lambda: pipes[r].split_expand(r, g, cap, sends[r], flags[r], stats[r]))
+        t2 = timed(lambda: pipes[r].split_edges(recvs[r], lo, hi))
+        per.append({"rows": [lo, hi], "expand_ms": t1, "edges_ms": t2, "ms": t1 + t2,
+                    "send_MB": g * cap * 8 / 1e6, "edges": pipes[r].n_edges})
+    return per
+
+
+def main():
+    name = sys.argv[1] if len(sys.argv) > 1 else "config3"
+    mode = sys.argv[2] if len(sys.argv) > 2 else "kmer"
+    k = CONFIGS[name][3]
+    b = load_batch(name)
+    out = {"config": name, "mode": mode, "n": b.n, "ranks": {}}
+    full = DevicePipeline(b, k, "cuda:0")
+    out["single_gpu_ms"] = timed(lambda: full.step(), 20)
+    print("single", round(out["single_gpu_ms"], 3), flush=True)
+    del full
+    for g in [int(x) for x in sys.argv[3:]] or (1, 2, 4, 8):
+        if mode == "kmer":
+            per = kmer_ranks(b, k, g)
+        else:
+            per = []
+            for r, (lo, hi) in enumerate(row_ranges(b.n, g)):
+                pipe = DevicePipeline(b, k, "cuda:0")
+                per.append({"rows": [lo, hi], "ms": timed(lambda: pipe.rows(lo, hi)), "edges": pipe.n_edges})
+                del pipe
         out["ranks"][g] = {"max_ms": max(x["ms"] for x in per), "per_rank": per}
-        print(g, out["ranks"][g]["max_ms"], [round(x["ms"], 3) for x in per], flush=True)
+        print(g, round(out["ranks"][g]["max_ms"], 3), [round(x["ms"], 3) for x in per], flush=True)
+        torch.cuda.empty_cache()
     print(json.dumps(out))
 
 

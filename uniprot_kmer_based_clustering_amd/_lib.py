@@ -22,6 +22,9 @@ KMP_ENGINE_AUTO, KMP_ENGINE_POSTINGS, KMP_ENGINE_TILES, KMP_ENGINE_RESIDUES = 0,
 KMP_KMERS_CODES, KMP_KMERS_IDS = 0, 1
 KMP_LAYOUT_FLAT, KMP_LAYOUT_BUCKETED, KMP_LAYOUT_BUCKETED_HEAVY = 0, 1, 2
 KMP_PARTITION_AUTO, KMP_PARTITION_COUNT, KMP_PARTITION_CURSOR = 0, 1, 2
+(KMP_SPLIT_RERUN, KMP_SPLIT_CLASS, KMP_SPLIT_HEAVY, KMP_SPLIT_MAX_PART, KMP_SPLIT_MAX_SHARD, KMP_SPLIT_BIN_TILES,
+ KMP_SPLIT_CURSOR) = range(7)
+KMP_SPLIT_FLAGS = 8
 KMP_LDS_SORT_MAX = 4096
 
 
@@ -131,6 +134,7 @@ SIGNATURES = {
     "kmp_ctx_set_pass_keys": (C.c_int, [P, C.c_uint64]),
     "kmp_ctx_last_passes": (C.c_uint32, [P]),
     "kmp_ctx_transport": (C.c_char_p, [P]),
+    "kmp_ctx_last_split": (C.c_char_p, [P]),
     "kmp_postings_create": (C.c_int, [C.POINTER(P)]),
     "kmp_postings_destroy": (None, [P]),
     "kmp_dev_pairs_postings": (C.c_int, [P, P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32,
@@ -147,6 +151,10 @@ SIGNATURES = {
     "kmp_postings_set_reuse": (C.c_int, [P, C.c_int]),
     "kmp_dev_pairs_residues": (C.c_int, [P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32,
                                          C.c_uint32, C.c_int, P, P, P, C.c_uint64, U64P, P, P]),
+    "kmp_dev_split_expand": (C.c_int, [P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32, C.c_int,
+                                        C.c_uint32, C.c_uint32, C.c_uint64, P, P, P, P, P]),
+    "kmp_dev_split_edges": (C.c_int, [P, P, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P, P, P,
+                                       C.c_uint64, U64P, P]),
     "kmp_dev_pairs_rows": (C.c_int, [P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32, C.c_uint32,
                                      C.c_int, C.c_uint32, C.c_uint32, P, P, P, C.c_uint64, U64P, P, P]),
     "kmp_row_split": (None, [C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]),

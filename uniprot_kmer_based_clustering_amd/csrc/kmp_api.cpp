@@ -67,6 +67,7 @@ struct kmp_rank {
     hipStream_t stream = nullptr;  // rank 0: the context's
     bool own_stream = false;
     DevBuf res, off, cls, ep, eq, ew;
+    DevBuf send, recv, sflags, sstats;  // k-mer split: exchange regions, flags, statistics
     uint64_t cap = 0;
     kmp_postings* ws = nullptr;
     ~kmp_rank() {
@@ -82,6 +83,10 @@ struct kmp_rank {
         ep.release();
         eq.release();
         ew.release();
+        send.release();
+        recv.release();
+        sflags.release();
+        sstats.release();
     }
 };
 
@@ -147,6 +152,9 @@ struct kmp_ctx {
     // multi-GPU (kmp_ctx_create_multi): the ranks of the row split and the gather's transport
     std::vector<std::unique_ptr<kmp_rank>> ranks;
     std::unique_ptr<kmp::Transport> transport;
+    uint64_t split_cap = 0;   // k-mer split: keys per exchange region (learned per batch)
+    const char* last_split = "";  // the flow of the last multi-GPU kmp_pairs: "kmer" or "rows"
+    bool split_rows = false;  // the batch spills frequent k-mers: the row split
     ~kmp_ctx() {
         ranks.clear();
         (void)hipSetDevice(device);
@@ -404,6 +412,8 @@ const char* kmp_ctx_transport(const kmp_ctx* c) {
     return c->transport ? c->transport->name() : "local";
 }
 
+const char* kmp_ctx_last_split(const kmp_ctx* c) { return c ? c->last_split : ""; }
+
 void kmp_ctx_destroy(kmp_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
@@ -461,6 +471,8 @@ int kmp_load_proteins(kmp_ctx* c, const uint8_t* residues, const uint64_t* offse
     c->counters = kmp_counters{};
     c->counters.n_proteins = n;
     c->loaded = true;
+    c->split_cap = 0;
+    c->split_rows = false;
     return KMP_OK;
 }
 
@@ -726,16 +738,108 @@ int pass_pairs(kmp_ctx* c, const kmp_pair_opts& o, uint64_t* count) {
     return rc;
 }
 
-// The multi-GPU row split: every rank expands its rows on its own device (one host thread per
-// rank), then the transport gathers the ranks' edges into the context's buffers in rank order.
-static int multi_pairs(kmp_ctx* c, const kmp_pair_opts& o, uint64_t* count) {
+// Multi-GPU: every rank's edges of its rows (kmp_row_split) into its own (ep, eq, ew), then the
+// transport gathers them into the context's buffers in rank order (the canonical list).
+//   k-mer split (default): phase 1 on every rank (kmp_dev_split_expand, enqueued from this
+//     thread), the all-to-all of the routed pair keys, the flags reduced on the host (a rerun grows
+//     the capacities identically on every rank), phase 2 on every rank (kmp_dev_split_edges, one
+//     host thread per rank: it synchronises);
+//   row split: every rank groups every k-mer and expands its rows (kmp_dev_pairs_rows, one host
+//     thread per rank), for batches whose frequent k-mers spill.
+constexpr int kSplitFallback = -1;
+
+static int split_rank_edges(kmp_ctx* c, const kmp_pair_opts& o, const std::vector<uint32_t>& start,
+                            std::vector<uint64_t>& cnt) {
     const uint32_t G = (uint32_t)c->ranks.size();
-    std::vector<uint32_t> start(G + 1);
-    kmp_row_split(c->n, G, start.data());
+    const uint64_t slots = kmp_set_capacity(c->n, c->total_res);
+    uint64_t cap = c->split_cap ? c->split_cap : std::max<uint64_t>(4096, c->total_res / 4 / ((uint64_t)G * G));
+    std::vector<uint32_t> learn(KMP_SPLIT_FLAGS, 0), fl(KMP_SPLIT_FLAGS, 0);
+    bool have_learn = false;
+    auto rank_buf = [&](uint32_t g) -> const uint8_t* { return (g ? c->ranks[g]->res : c->res).as<uint8_t>(); };
+    for (int attempt = 0; attempt < 6; ++attempt) {
+        std::vector<const char*> sendp(G);
+        std::vector<char*> recvp(G);
+        std::vector<hipStream_t> streams(G);
+        for (uint32_t g = 0; g < G; ++g) {
+            kmp_rank& r = *c->ranks[g];
+            KMP_HIP(c, hipSetDevice(r.device));
+            KMP_HIP(c, r.send.reserve((uint64_t)G * cap * 8));
+            KMP_HIP(c, r.recv.reserve((uint64_t)G * cap * 8));
+            KMP_HIP(c, r.sflags.reserve(KMP_SPLIT_FLAGS * sizeof(uint32_t)));
+            KMP_HIP(c, r.sstats.reserve(8 * sizeof(unsigned long long)));
+            const uint64_t* off = (g ? r.off : c->off).as<uint64_t>();
+            const uint16_t* cls = (g ? r.cls : c->cls).as<uint16_t>();
+            const int rc = kmp_dev_split_expand(r.ws, rank_buf(g), off, cls, c->n, c->k_sets, slots, 0xFFFFFFFFu,
+                                                o.require_class_diff, g, G, cap, have_learn ? learn.data() : nullptr,
+                                                r.send.as<unsigned long long>(), r.sflags.as<uint32_t>(),
+                                                r.sstats.as<unsigned long long>(), r.stream);
+            if (rc == KMP_ESTATE) return kSplitFallback;
+            if (rc != KMP_OK) return fail(c, rc, "rank %u: k-mer split expand: %s", g, kmp_status_string(rc));
+            sendp[g] = static_cast<const char*>(r.send.p);
+            recvp[g] = static_cast<char*>(r.recv.p);
+            streams[g] = r.stream;
+        }
+        std::string err;
+        const int rc = c->transport->alltoall(sendp, recvp, cap * 8, streams, &err);
+        if (rc != KMP_OK) return fail(c, rc, "%s", err.c_str());
+        std::fill(fl.begin(), fl.end(), 0u);
+        for (uint32_t g = 0; g < G; ++g) {  // the flags, reduced (max) over the ranks
+            kmp_rank& r = *c->ranks[g];
+            uint32_t h[KMP_SPLIT_FLAGS];
+            KMP_HIP(c, hipSetDevice(r.device));
+            KMP_HIP(c, hipMemcpy(h, r.sflags.p, sizeof h, hipMemcpyDeviceToHost));
+            for (int i = 0; i < KMP_SPLIT_FLAGS; ++i) fl[i] = std::max(fl[i], h[i]);
+        }
+        if (fl[KMP_SPLIT_CLASS] || fl[KMP_SPLIT_HEAVY]) return kSplitFallback;
+        if (fl[KMP_SPLIT_RERUN]) {
+            learn = fl;
+            have_learn = true;
+            if (fl[KMP_SPLIT_MAX_PART] > cap) cap = fl[KMP_SPLIT_MAX_PART] + fl[KMP_SPLIT_MAX_PART] / 16 + 1024;
+            continue;
+        }
+        c->split_cap = cap;
+        std::vector<int> status(G, KMP_OK);
+        auto work = [&](uint32_t g) {
+            kmp_rank& r = *c->ranks[g];
+            if (hipSetDevice(r.device) != hipSuccess) {
+                status[g] = KMP_EDEVICE;
+                return;
+            }
+            if (r.cap == 0) r.cap = std::max<uint64_t>(1u << 16, 4ull * c->n / G);
+            for (int a = 0; a < 3; ++a) {
+                if (r.ep.reserve(r.cap * 4) != hipSuccess || r.eq.reserve(r.cap * 4) != hipSuccess ||
+                    r.ew.reserve(r.cap * 4) != hipSuccess) {
+                    status[g] = KMP_ENOMEM;
+                    return;
+                }
+                uint64_t ne = 0;
+                status[g] = kmp_dev_split_edges(r.ws, r.recv.as<unsigned long long>(), (uint64_t)G * cap, c->n,
+                                                start[g], start[g + 1], o.min_shared, r.ep.as<uint32_t>(),
+                                                r.eq.as<uint32_t>(), r.ew.as<uint32_t>(), r.cap, &ne, r.stream);
+                cnt[g] = ne;
+                if (status[g] != KMP_EOVERFLOW) break;
+                r.cap = ne + ne / 8 + 1024;
+            }
+        };
+        std::vector<std::thread> pool;
+        for (uint32_t g = 1; g < G; ++g) pool.emplace_back(work, g);
+        work(0);
+        for (auto& t : pool) t.join();
+        KMP_TRY(c, use_device(c));
+        for (uint32_t g = 0; g < G; ++g)
+            if (status[g] != KMP_OK)
+                return fail(c, status[g], "rank %u (device %d, rows [%u, %u)): k-mer split edges: %s", g,
+                            c->ranks[g]->device, start[g], start[g + 1], kmp_status_string(status[g]));
+        return KMP_OK;
+    }
+    return fail(c, KMP_EDEVICE, "k-mer split: capacities unstable across reruns");
+}
+
+static int rows_rank_edges(kmp_ctx* c, const kmp_pair_opts& o, const std::vector<uint32_t>& start,
+                           std::vector<uint64_t>& cnt) {
+    const uint32_t G = (uint32_t)c->ranks.size();
     const uint64_t slots = kmp_set_capacity(c->n, c->total_res);
     std::vector<int> status(G, KMP_OK);
-    std::vector<uint64_t> cnt(G, 0);
-    std::vector<std::string> why(G);
     auto work = [&](uint32_t g) {
         kmp_rank& r = *c->ranks[g];
         if (hipSetDevice(r.device) != hipSuccess) {
@@ -771,6 +875,23 @@ static int multi_pairs(kmp_ctx* c, const kmp_pair_opts& o, uint64_t* count) {
         if (status[g] != KMP_OK)
             return fail(c, status[g], "rank %u (device %d, rows [%u, %u)): %s", g, c->ranks[g]->device, start[g],
                         start[g + 1], kmp_status_string(status[g]));
+    return KMP_OK;
+}
+
+static int multi_pairs(kmp_ctx* c, const kmp_pair_opts& o, uint64_t* count) {
+    const uint32_t G = (uint32_t)c->ranks.size();
+    std::vector<uint32_t> start(G + 1);
+    kmp_row_split(c->n, G, start.data());
+    std::vector<uint64_t> cnt(G, 0);
+    int rc = kSplitFallback;
+    if (!c->split_rows) rc = split_rank_edges(c, o, start, cnt);
+    if (rc == kSplitFallback) {
+        c->split_rows = true;  // for this batch
+        std::fill(cnt.begin(), cnt.end(), 0ull);
+        rc = rows_rank_edges(c, o, start, cnt);
+    }
+    if (rc != KMP_OK) return rc;
+    c->last_split = c->split_rows ? "rows" : "kmer";
     uint64_t total = 0;
     for (uint64_t x : cnt) total += x;
     if (total > c->edge_cap) c->edge_cap = total + total / 8 + 1024;
@@ -785,8 +906,8 @@ static int multi_pairs(kmp_ctx* c, const kmp_pair_opts& o, uint64_t* count) {
         streams[g] = r.stream;
     }
     std::string err;
-    const int rc = c->transport->gather(src, {c->ep.as<uint32_t>(), c->eq.as<uint32_t>(), c->ew.as<uint32_t>()}, cnt,
-                                        streams, &err);
+    rc = c->transport->gather(src, {c->ep.as<uint32_t>(), c->eq.as<uint32_t>(), c->ew.as<uint32_t>()}, cnt, streams,
+                              &err);
     KMP_TRY(c, use_device(c));
     if (rc != KMP_OK) return fail(c, rc, "%s", err.c_str());
     *count = total;

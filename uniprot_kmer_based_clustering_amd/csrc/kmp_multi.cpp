@@ -44,6 +44,39 @@ struct CopyTransport final : Transport {
         }
         return KMP_OK;
     }
+    int alltoall(const std::vector<const char*>& send, const std::vector<char*>& recv, uint64_t bytes,
+                 const std::vector<hipStream_t>& streams, std::string* err) override {
+        const size_t G = send.size();
+        for (size_t g = 0; g < G; ++g) {  // every rank's send regions complete
+            (void)hipSetDevice(dev[g]);
+            hipError_t e = hipStreamSynchronize(streams[g]);
+            if (e != hipSuccess) {
+                *err = std::string("all-to-all: ") + hipGetErrorString(e);
+                return KMP_EDEVICE;
+            }
+        }
+        for (size_t d = 0; d < G; ++d) {
+            (void)hipSetDevice(dev[d]);
+            for (size_t g = 0; g < G; ++g) {
+                hipError_t e = hipMemcpyPeerAsync(recv[d] + g * bytes, dev[d], send[g] + d * bytes, dev[g], bytes,
+                                                  streams[d]);
+                if (e != hipSuccess) {
+                    *err = std::string("hipMemcpyPeerAsync: ") + hipGetErrorString(e);
+                    return KMP_EDEVICE;
+                }
+            }
+        }
+        for (size_t d = 0; d < G; ++d) {
+            (void)hipSetDevice(dev[d]);
+            hipError_t e = hipStreamSynchronize(streams[d]);
+            if (e != hipSuccess) {
+                *err = std::string("all-to-all: ") + hipGetErrorString(e);
+                return KMP_EDEVICE;
+            }
+        }
+        (void)hipSetDevice(dev[0]);
+        return KMP_OK;
+    }
 };
 
 // librccl entry points, resolved once per process from /opt/rocm's librccl (RTLD_LOCAL: a
@@ -121,6 +154,45 @@ struct RcclTransport final : Transport {
             hipError_t e = hipStreamSynchronize(streams[g]);
             if (e != hipSuccess) {
                 *err = std::string("gather: ") + hipGetErrorString(e);
+                return KMP_EDEVICE;
+            }
+        }
+        (void)hipSetDevice(dev[0]);
+        return KMP_OK;
+    }
+    int alltoall(const std::vector<const char*>& send, const std::vector<char*>& recv, uint64_t bytes,
+                 const std::vector<hipStream_t>& streams, std::string* err) override {
+        const size_t G = send.size();
+        // a rank's own region: a device copy; the others: one grouped send / receive per pair,
+        // each ordered on its rank's stream after the expansion that filled it
+        for (size_t g = 0; g < G; ++g) {
+            (void)hipSetDevice(dev[g]);
+            hipError_t e = hipMemcpyAsync(recv[g] + g * bytes, send[g] + g * bytes, bytes, hipMemcpyDeviceToDevice,
+                                          streams[g]);
+            if (e != hipSuccess) {
+                *err = std::string("hipMemcpyAsync: ") + hipGetErrorString(e);
+                return KMP_EDEVICE;
+            }
+        }
+        ncclResult_t r = g_rccl.GroupStart();
+        for (size_t g = 0; g < G && r == ncclSuccess; ++g)
+            for (size_t d = 0; d < G && r == ncclSuccess; ++d) {
+                if (g == d) continue;
+                r = g_rccl.Send(send[g] + d * bytes, bytes / 8, ncclUint64, (int)d, comm[g], streams[g]);
+                if (r == ncclSuccess)
+                    r = g_rccl.Recv(recv[d] + g * bytes, bytes / 8, ncclUint64, (int)g, comm[d], streams[d]);
+            }
+        const ncclResult_t r2 = g_rccl.GroupEnd();
+        if (r == ncclSuccess) r = r2;
+        if (r != ncclSuccess) {
+            *err = std::string("RCCL all-to-all: ") + g_rccl.ErrorString(r);
+            return KMP_ERCCL;
+        }
+        for (size_t g = 0; g < G; ++g) {
+            (void)hipSetDevice(dev[g]);
+            hipError_t e = hipStreamSynchronize(streams[g]);
+            if (e != hipSuccess) {
+                *err = std::string("all-to-all: ") + hipGetErrorString(e);
                 return KMP_EDEVICE;
             }
         }

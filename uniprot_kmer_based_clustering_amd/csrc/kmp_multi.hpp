@@ -1,10 +1,14 @@
 // kmp_multi.hpp — the multi-GPU split behind the C ABI (kmp_ctx_create_multi).
 //
-// The pair space is split by rows: rank g expands the pairs (p, q), p < q, whose smaller protein
-// lies in rows [start[g], start[g+1]) (kmp_row_split), with kmp_dev_pairs_rows on its own device
-// and its own copy of the packed batch.  Ranks never exchange keys; the only collective is the
-// gather of every rank's edges to device 0 in rank order, which is already the canonical list.
-// The gather goes through a Transport, so the same flow runs over RCCL between GPUs
+// Two flows over the same ranks (each its own device, stream, workspace and copy of the packed
+// batch); rank g always ends with the canonical edges of rows [start[g], start[g+1])
+// (kmp_row_split), and the gather to device 0 in rank order is the canonical list:
+//   k-mer split (default): rank g expands its share of the k-mers (kmp_dev_split_expand), one
+//     all-to-all routes the pair keys to their row owners, each rank reduces its rows
+//     (kmp_dev_split_edges);
+//   row split (batches whose frequent k-mers spill, and the bounded-memory passes): rank g
+//     groups every k-mer and expands only its rows (kmp_dev_pairs_rows); no exchange.
+// The collectives go through a Transport, so the same flows run over RCCL between GPUs
 // (library-owned communicators, ncclCommInitAll in-process) and over device copies between
 // virtual ranks that share one GPU (tests; RCCL admits one rank per device).
 #pragma once
@@ -28,6 +32,10 @@ struct Transport {
     // Returns KMP_OK, KMP_ERCCL or KMP_EDEVICE; *err describes a failure.
     virtual int gather(const std::vector<EdgeArrays>& src, const EdgeArrays& dst, const std::vector<uint64_t>& counts,
                        const std::vector<hipStream_t>& streams, std::string* err) = 0;
+    // the k-mer split's exchange: recv[d] + g * bytes <- send[g] + d * bytes for every pair of
+    // ranks (g, d), ordered after the work already on the ranks' streams, complete on return
+    virtual int alltoall(const std::vector<const char*>& send, const std::vector<char*>& recv, uint64_t bytes,
+                         const std::vector<hipStream_t>& streams, std::string* err) = 0;
 };
 
 // device-to-device copies (hipMemcpyPeerAsync): any set of devices, repeated ones included

@@ -1285,7 +1285,7 @@ __device__ __forceinline__ uint32_t col_prefix_inplace(uint32_t* __restrict__ x,
 __global__ __launch_bounds__(kKeyThreads) void bp_hist1_kernel(
     const uint8_t* __restrict__ res, const uint64_t* __restrict__ res_off, const uint16_t* __restrict__ cls, int k,
     uint32_t p_hi, uint64_t slots, const uint32_t* __restrict__ chunk_first, Layout lay, BpDigits dg, uint32_t pw21,
-    uint32_t* __restrict__ H1, uint32_t* __restrict__ flags) {
+    uint32_t dlo, uint32_t dhi, uint32_t* __restrict__ H1, uint32_t* __restrict__ flags) {
     __shared__ KeyChunk s;
     __shared__ uint32_t lh[kBpMaxBins];
     const uint64_t c0 = (uint64_t)blockIdx.x * kKeyChunk, c1 = min(c0 + kKeyChunk, slots);
@@ -1295,7 +1295,8 @@ __global__ __launch_bounds__(kKeyThreads) void bp_hist1_kernel(
     const unsigned hs1 = dg.sh1 - lay.hshift;  // digit1 = the top d1 bits of h
     key_chunk_run<kBpPer>(s, threadIdx.x * kBpPer, (uint32_t)(c1 - c0), k, pw21, first, lay,
                           [&](uint32_t, bool valid, uint32_t h, unsigned long long) {
-                              if (valid) atomicAdd(&lh[h >> hs1], 1u);
+                              const uint32_t d = h >> hs1;
+                              if (valid && d >= dlo && d < dhi) atomicAdd(&lh[d], 1u);
                           });
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < dg.nb1; d += kKeyThreads) H1[(uint64_t)blockIdx.x * dg.nb1 + d] = lh[d];
@@ -1378,14 +1379,26 @@ __global__ __launch_bounds__(256) void bp_colprefix_kernel(const uint32_t* __res
     }
 }
 
+// the tile's row of run offsets (P1 / P2), digit tid + t * kKeyThreads in pre[t]: loaded at the
+// start of the scatter kernels so the load's latency hides behind the tile's own work (loaded
+// where it was used, after the tile scan, every workgroup waited on it)
+constexpr uint32_t kBpQ = kBpMaxBins / kKeyThreads;
+__device__ __forceinline__ void bp_prow_load(const uint32_t* __restrict__ prow, uint32_t nb, uint32_t (&pre)[kBpQ]) {
+#pragma unroll
+    for (uint32_t t = 0; t < kBpQ; ++t) {
+        const uint32_t d = threadIdx.x + t * kKeyThreads;
+        pre[t] = d < nb ? prow[d] : 0u;
+    }
+}
+
 // rank every key of the workgroup's tile by digit in LDS (x[e] = element tid + e*kKeyThreads),
 // place the tile digit-major into S and write each digit's run at base[digit] (global offset of
-// the tile's run, from the scan).  lh holds the tile histogram on entry (zeroed, then counted by
-// the caller's ranks); shared by both scatter levels.
+// the tile's run, from the scan; pre = bp_prow_load of it).  lh holds the tile histogram on
+// entry (zeroed, then counted by the caller's ranks); shared by both scatter levels.
 template <class Digit>
 __device__ __forceinline__ void bp_place(const unsigned long long (&x)[kBpPer], const uint32_t (&r)[kBpPer],
                                          uint32_t n_in, uint32_t nb, Digit digit, uint32_t* lh, uint32_t* wave_tot,
-                                         unsigned long long* S, const uint32_t* __restrict__ prow,
+                                         unsigned long long* S, const uint32_t (&pre)[kBpQ],
                                          unsigned long long* __restrict__ out) {
     lds_bins_scan(lh, nb, wave_tot);
 #pragma unroll
@@ -1393,7 +1406,11 @@ __device__ __forceinline__ void bp_place(const unsigned long long (&x)[kBpPer], 
         if (x[e] != kNoKey) S[lh[digit(x[e])] + r[e]] = x[e];
     __syncthreads();
     // lh[d] -> global base of the digit's run minus its tile start: out[lh[d] + i] for S[i]
-    for (uint32_t d = threadIdx.x; d < nb; d += kKeyThreads) lh[d] = prow[d] - lh[d];
+#pragma unroll
+    for (uint32_t t = 0; t < kBpQ; ++t) {
+        const uint32_t d = threadIdx.x + t * kKeyThreads;
+        if (d < nb) lh[d] = pre[t] - lh[d];
+    }
     __syncthreads();
     // pairs (i, i+1), i even: one 16-byte store when both keys belong to the same run and its
     // destination is 16-byte aligned (S is 16-byte aligned, i even), else two 8-byte stores
@@ -1419,7 +1436,8 @@ __device__ __forceinline__ void bp_place(const unsigned long long (&x)[kBpPer], 
 __global__ __launch_bounds__(kKeyThreads) void bp_scatter1_kernel(
     const uint8_t* __restrict__ res, const uint64_t* __restrict__ res_off, const uint16_t* __restrict__ cls, int k,
     uint32_t p_hi, uint64_t slots, const uint32_t* __restrict__ chunk_first, Layout lay, BpDigits dg, uint32_t pw21,
-    const uint32_t* __restrict__ P1, unsigned long long* __restrict__ out, uint32_t* __restrict__ flags) {
+    uint32_t dlo, uint32_t dhi, const uint32_t* __restrict__ P1, unsigned long long* __restrict__ out,
+    uint32_t* __restrict__ flags) {
     __shared__ union {
         KeyChunk kc;
         unsigned long long S[kKeyChunk];
@@ -1428,6 +1446,8 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scatter1_kernel(
     __shared__ uint32_t wave_tot[kKeyThreads / 64];
     __shared__ uint32_t s_n;
     const uint64_t c0 = (uint64_t)blockIdx.x * kKeyChunk, c1 = min(c0 + kKeyChunk, slots);
+    uint32_t pre[kBpQ];
+    bp_prow_load(P1 + (uint64_t)blockIdx.x * dg.nb1, dg.nb1, pre);
     for (uint32_t d = threadIdx.x; d < dg.nb1; d += kKeyThreads) lh[d] = 0;
     if (threadIdx.x == 0) s_n = 0;
     const uint32_t first = chunk_first[blockIdx.x];
@@ -1438,13 +1458,15 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scatter1_kernel(
     const unsigned hs1 = dg.sh1 - lay.hshift;
     key_chunk_run<kBpPer>(u.kc, threadIdx.x * kBpPer, (uint32_t)(c1 - c0), k, pw21, first, lay,
                           [&](uint32_t e, bool valid, uint32_t h, unsigned long long lo) {
-                              x[e] = valid ? ((unsigned long long)h << lay.hshift) | lo : kNoKey;
-                              r[e] = valid ? atomicAdd(&lh[h >> hs1], 1u) : 0u;
-                              nk += valid;
+                              const uint32_t d = h >> hs1;
+                              const bool mine = valid && d >= dlo && d < dhi;  // the call's coarse bins
+                              x[e] = mine ? ((unsigned long long)h << lay.hshift) | lo : kNoKey;
+                              r[e] = mine ? atomicAdd(&lh[d], 1u) : 0u;
+                              nk += mine;
                           });
     if (nk) atomicAdd(&s_n, nk);
     __syncthreads();  // the chunk's staging (u.kc) is dead from here: u.S reuses it
-    bp_place(x, r, s_n, dg.nb1, digit, lh, wave_tot, u.S, P1 + (uint64_t)blockIdx.x * dg.nb1, out);
+    bp_place(x, r, s_n, dg.nb1, digit, lh, wave_tot, u.S, pre, out);
 }
 
 // level-2 tile (j, c) of coarse bin c: keys [a + j*kBpTile, a + min(n, (j+1)*kBpTile)) of the
@@ -1532,6 +1554,8 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scatter2_kernel(const unsigned
     const uint32_t j = blockIdx.x, c = c0 + blockIdx.y;
     uint32_t t0, tn;
     if (!bp_tile(C1, dg.nb1, c, j, J, t0, tn)) return;
+    uint32_t pre[kBpQ];
+    bp_prow_load(P2 + ((uint64_t)c * J + j) * dg.nb2, dg.nb2, pre);
     for (uint32_t d = threadIdx.x; d < dg.nb2; d += kKeyThreads) lh[d] = 0;
     __syncthreads();
     unsigned long long x[kBpPer];
@@ -1552,7 +1576,7 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scatter2_kernel(const unsigned
 #pragma unroll
     for (uint32_t e = 0; e < kBpPer; ++e) r[e] = x[e] != kNoKey ? atomicAdd(&lh[digit(x[e])], 1u) : 0u;
     __syncthreads();
-    bp_place(x, r, tn, dg.nb2, digit, lh, wave_tot, S, P2 + ((uint64_t)c * J + j) * dg.nb2, out);
+    bp_place(x, r, tn, dg.nb2, digit, lh, wave_tot, S, pre, out);
 }
 
 // ------------------------------------------------------------- cursor level 2 --------------
@@ -1638,11 +1662,11 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scatter2c_kernel(const unsigne
                                                                    BpDigits dg, CurGeom cg,
                                                                    uint32_t* __restrict__ bcur,
                                                                    unsigned long long* __restrict__ out,
-                                                                   uint32_t* __restrict__ flags) {
+                                                                   uint32_t* __restrict__ flags, uint32_t c0) {
     __shared__ __attribute__((aligned(16))) unsigned long long S[kBpTile];
     __shared__ uint32_t lh[kBpMaxBins];
     __shared__ uint32_t wave_tot[kKeyThreads / 64];
-    const uint32_t j = blockIdx.x, c = blockIdx.y;
+    const uint32_t j = blockIdx.x, c = c0 + blockIdx.y;
     uint32_t t0, tn;
     if (!bp_tile(C1, dg.nb1, c, j, J, t0, tn)) {
         // a bin above its tile budget: no tile of it is written; its buckets are incomplete
@@ -1686,17 +1710,18 @@ __global__ void bp_cur_clear_kernel(uint32_t* __restrict__ cur, uint32_t n) {
 // a 1,024-key capacity (four keys per thread) when the mean bucket is small enough that a bucket
 // above it is a > 4-sigma event (the large kernel takes those)
 constexpr uint32_t kBucketCap1024Mean = 800;  // at config 3 (mean 897) the 1,280 variant measured faster
+// buckets [b0, b0 + nb)
 template <bool kRows>
-void launch_buckets(const BucketArgs& a, uint32_t nb, hipStream_t st) {
+void launch_buckets(const BucketArgs& a, uint32_t b0, uint32_t nb, hipStream_t st) {
     if (a.lay.bbits >= kMergeMinBits && a.lay.mean_keys <= kBucketCap1024Mean)  // four keys per thread
         bucket_small_kernel<1024, kBucketSmallThreads, kBucketSmallTab, true, kRows>
-            <<<nb, kBucketSmallThreads, 0, st>>>(a, 0u);
+            <<<nb, kBucketSmallThreads, 0, st>>>(a, b0);
     else if (a.lay.bbits >= kMergeMinBits)
         bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallTab, true, kRows>
-            <<<nb, kBucketSmallThreads, 0, st>>>(a, 0u);
+            <<<nb, kBucketSmallThreads, 0, st>>>(a, b0);
     else
         bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallTab, false, kRows>
-            <<<nb, kBucketSmallThreads, 0, st>>>(a, 0u);
+            <<<nb, kBucketSmallThreads, 0, st>>>(a, b0);
     bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeTab, kRows>
         <<<kBucketLargeGrid, kBucketLargeThreads, 0, st>>>(a);
 }
@@ -1770,11 +1795,16 @@ struct kmp_postings {
     Grow<unsigned long long> ovx;  // per listed block: offset of its keys
     Grow<uint32_t> ovr;            // run lengths, kept flags and positions, first run per block
     uint64_t pt_inc = 0;        // incidences of the last call (row-block sizing)
+    Grow<unsigned long long> split_cur;  // k-mer split: per-destination send cursors
+    std::vector<unsigned long long> split_shape;
     unsigned pt_rb_max = 16;    // rows-per-block bound learned from overflowing row blocks
     uint32_t bp_J = 0;          // level-2 tiles per coarse bin ...
     uint32_t bp_J_min = 0;      // ... at least (learned from an overflowing bin)
     uint64_t bp_c1 = 0;         // offset of C1 (coarse bin starts) in ws->bp
     bool parted = false;        // ws->keys holds level-1 output (bp_level1 ran for this call)
+    // coarse bins [bin_lo, bin_hi) of this call (bin_hi 0: all): the bucket-range share of a rank
+    // of the multi-GPU k-mer split (kmp_dev_split_expand); level 1 keeps only their keys
+    uint32_t bin_lo = 0, bin_hi = 0;
     // cursor level 2 (fixed-capacity bucket regions, no counting passes): tried first for a new
     // shape (cur_on), dropped for the shape after a region overflow; cur_used: the buckets in
     // ws->sorted came from it (ws->cur: bucket counts)
@@ -1807,7 +1837,7 @@ struct kmp_postings {
     hipEvent_t ev[KMP_POSTINGS_STAGES + 1] = {};
     ~kmp_postings() {
         for (auto* g : {&keys, &sorted, &inc, &inc_sorted, &uniq, &bstats, &btot, &boff, &spill, &hkeys, &hsorted,
-                        &hGS, &htc, &htoff, &hoff, &ovk, &ovx})
+                        &hGS, &htc, &htoff, &hoff, &ovk, &ovx, &split_cur})
             g->release();
         for (auto* g : {&w, &keep, &pos, &small, &cnt, &flags, &chunk_first, &bp, &pt, &ovf, &ovr, &hE, &hgi, &hcnt, &cur})
             g->release();
@@ -1844,9 +1874,17 @@ void fill_stats(kmp_postings_stats* stats, const unsigned long long* acc) {
 
 // Level 1 of the bucket partition for proteins [0, n): ws->keys = the valid keys grouped by
 // digit1; C1 = coarse bin starts (C1[nb1] = key count) in ws->bp for level 2.
+// the call's coarse bins [*lo, *hi)
+void own_bins(const kmp_postings* ws, const BpDigits& dg, uint32_t* lo, uint32_t* hi) {
+    *lo = ws->bin_hi ? ws->bin_lo : 0u;
+    *hi = ws->bin_hi ? std::min(ws->bin_hi, dg.nb1) : dg.nb1;
+}
+
 hipError_t bp_level1(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
                      int k, uint32_t n, uint64_t slots, const Layout& lay, hipStream_t st) {
     const BpDigits dg = bp_digits(lay);
+    uint32_t dlo, dhi;
+    own_bins(ws, dg, &dlo, &dhi);
     const uint64_t G64 = (slots + kKeyChunk - 1) / kKeyChunk;
     if (G64 * dg.nb1 > 0xFFFFFFFFull || slots > 0xFFFFFFFFull) return hipErrorInvalidValue;
     const uint32_t G = (uint32_t)G64, groups = (G + kBpRowGroup - 1) / kBpRowGroup;
@@ -1863,12 +1901,12 @@ hipError_t bp_level1(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_r
     chunk_first_kernel<<<(n + 1 + 255) / 256, 256, 0, st>>>(d_res_off, 0u, n, 0ull, slots, G, ws->chunk_first.p);
     const uint32_t pw21 = (uint32_t)pow21(k - 1);
     bp_hist1_kernel<<<G, kKeyThreads, 0, st>>>(d_res, d_res_off, d_class, k, n, slots, ws->chunk_first.p, lay, dg,
-                                                pw21, H1, ws->flags.p);
+                                                pw21, dlo, dhi, H1, ws->flags.p);
     bp_colsum_kernel<<<dim3(groups, (dg.nb1 + 255) / 256), 256, 0, st>>>(H1, G, dg.nb1, R);
     bp_colscan_kernel<<<1, kColThreads, 0, st>>>(R, groups, dg.nb1, C1);
     bp_colprefix_kernel<<<dim3(groups, (dg.nb1 + 255) / 256), 256, 0, st>>>(H1, G, dg.nb1, R, P1);
     bp_scatter1_kernel<<<G, kKeyThreads, 0, st>>>(d_res, d_res_off, d_class, k, n, slots, ws->chunk_first.p, lay, dg,
-                                                   pw21, P1, ws->keys.p, ws->flags.p);
+                                                   pw21, dlo, dhi, P1, ws->keys.p, ws->flags.p);
     return hipGetLastError();
 }
 
@@ -1878,10 +1916,14 @@ int bp_level2(kmp_postings* ws, const Layout& lay, hipStream_t st) {
     uint32_t* C1 = ws->bp.p + ws->bp_c1;
     uint32_t* H2 = C1 + 2 * (dg.nb1 + 1);
     const uint32_t nb = 1u << lay.bbits, J = ws->bp_J;
+    uint32_t c0, c1;
+    own_bins(ws, dg, &c0, &c1);
     PG(ws->cnt.reserve(2 * (uint64_t)nb + 2));
-    bp_hist2_kernel<<<dim3(J, dg.nb1), kKeyThreads, 0, st>>>(ws->keys.p, C1, J, dg, H2, 0u);
-    bp_scan2_kernel<<<dg.nb1, kKeyThreads, 0, st>>>(H2, C1, J, dg, ws->cnt.p, ws->flags.p, 0u);
-    bp_scatter2_kernel<<<dim3(J, dg.nb1), kKeyThreads, 0, st>>>(ws->keys.p, C1, J, dg, H2, ws->sorted.p, 0u);
+    if (c1 > c0) {
+        bp_hist2_kernel<<<dim3(J, c1 - c0), kKeyThreads, 0, st>>>(ws->keys.p, C1, J, dg, H2, c0);
+        bp_scan2_kernel<<<c1 - c0, kKeyThreads, 0, st>>>(H2, C1, J, dg, ws->cnt.p, ws->flags.p, c0);
+        bp_scatter2_kernel<<<dim3(J, c1 - c0), kKeyThreads, 0, st>>>(ws->keys.p, C1, J, dg, H2, ws->sorted.p, c0);
+    }
     PG(hipGetLastError());
     return KMP_OK;
 }
@@ -1904,9 +1946,12 @@ int bp_level2c(kmp_postings* ws, const Layout& lay, hipStream_t st) {
     PG(ws->cur.reserve(nb));
     PG(ws->sorted.reserve((uint64_t)nb * ws->cg.capb));
     PG(ws->cnt.reserve(2 * (uint64_t)nb + 2));  // the large-bucket list
+    uint32_t c0, c1;
+    own_bins(ws, dg, &c0, &c1);
     bp_cur_clear_kernel<<<std::min<uint32_t>((nb + 1023) / 1024, 1024), 1024, 0, st>>>(ws->cur.p, nb);
-    bp_scatter2c_kernel<<<dim3(ws->bp_J, dg.nb1), kKeyThreads, 0, st>>>(ws->keys.p, C1, ws->bp_J, dg, ws->cg,
-                                                                       ws->cur.p, ws->sorted.p, ws->flags.p);
+    if (c1 > c0)
+        bp_scatter2c_kernel<<<dim3(ws->bp_J, c1 - c0), kKeyThreads, 0, st>>>(ws->keys.p, C1, ws->bp_J, dg, ws->cg,
+                                                                            ws->cur.p, ws->sorted.p, ws->flags.p, c0);
     PG(hipGetLastError());
     return KMP_OK;
 }
@@ -2569,28 +2614,32 @@ int enqueue_front(kmp_postings* ws, MakeKeys& make_keys, const StepCfg& c, bool 
         ws->mark(2, st);
     }
     const BucketArgs a = bucket_args(ws, c, spill);
-    const uint32_t nb = 1u << c.lay.bbits;
-    if (c.ranged) launch_buckets<true>(a, nb, st);
-    else launch_buckets<false>(a, nb, st);
+    const BpDigits dg = bp_digits(c.lay);
+    uint32_t c0, c1;
+    own_bins(ws, dg, &c0, &c1);
+    const uint32_t b0 = c0 * dg.nb2, nbk = (c1 - c0) * dg.nb2;  // the call's buckets
+    if (c.ranged) launch_buckets<true>(a, b0, nbk, st);
+    else launch_buckets<false>(a, b0, nbk, st);
     PG(hipGetLastError());
     return KMP_OK;
 }
 
 // tail over the shard regions, then the read-back; marks 4, 5, 6
-int enqueue_tail(kmp_postings* ws, const StepCfg& c, const PtGeom& g, hipStream_t st) {
+// in: the pair keys (g.nshards regions of g.sc keys, counts in cursor; or, g.flat_n, one array
+// padded with kNoKey); total: capacity of the staging arrays (>= every key)
+int enqueue_tail_in(kmp_postings* ws, const StepCfg& c, const PtGeom& g, const unsigned long long* in,
+                    const unsigned long long* cursor, uint64_t total, hipStream_t st) {
     hipError_t e = hipSuccess;
     const PtBufs b = pt_bufs(ws, g, false, &e);
-    const uint64_t total = ws->shard_cap * kShards;
-    const unsigned long long* cursor = ws->bstats.p + kRbCursor;
     uint32_t* keys32 = reinterpret_cast<uint32_t*>(ws->inc.p);
     uint32_t* stage_p = reinterpret_cast<uint32_t*>(ws->uniq.p);
     uint32_t* stage_q = stage_p + total;
-    pt_hist_kernel<<<dim3(g.jt, g.nshards), kPtThreads, 0, st>>>(ws->inc_sorted.p, cursor, g, b.H);
+    pt_hist_kernel<<<dim3(g.jt, g.nshards), kPtThreads, 0, st>>>(in, cursor, g, b.H);
     bp_colsum_kernel<<<dim3(b.groups, (g.nrb + 255) / 256), 256, 0, st>>>(b.H, b.rows, g.nrb, b.R);
     pt_colscan_kernel<<<1, kPtScanThreads, 0, st>>>(b.R, b.groups, g.nrb, b.bst, ws->small.p + 2);
     bp_colprefix_kernel<<<dim3(b.groups, (g.nrb + 255) / 256), 256, 0, st>>>(b.H, b.rows, g.nrb, b.R, b.P);
     ws->mark(4, st);
-    pt_scatter_kernel<<<dim3(g.jt, g.nshards), kPtThreads, 0, st>>>(ws->inc_sorted.p, cursor, g, b.P, keys32);
+    pt_scatter_kernel<<<dim3(g.jt, g.nshards), kPtThreads, 0, st>>>(in, cursor, g, b.P, keys32);
     pt_reduce_kernel<<<g.nrb, kPtRThreads, 0, st>>>(keys32, b.bst, g, ws->flags.p, ws->ovf.p, stage_p, stage_q,
                                                     ws->w.p, b.counts);
     ws->mark(5, st);
@@ -2603,13 +2652,19 @@ int enqueue_tail(kmp_postings* ws, const StepCfg& c, const PtGeom& g, hipStream_
     return KMP_OK;
 }
 
+// the step's tail: the shard regions the bucket kernels filled
+int enqueue_tail(kmp_postings* ws, const StepCfg& c, const PtGeom& g, hipStream_t st) {
+    return enqueue_tail_in(ws, c, g, ws->inc_sorted.p, ws->bstats.p + kRbCursor, ws->shard_cap * kShards, st);
+}
+
 // the listed row blocks (above kPtCap keys): the composite sort + encode above, then offsets
 // and emit again; host-synchronous, returns the edge count in *edges
+
 int pt_finish_overflow(kmp_postings* ws, const StepCfg& c, const PtGeom& g, uint32_t m, uint64_t* edges,
-                       hipStream_t st) {
+                       hipStream_t st, uint64_t total = 0) {
     hipError_t e = hipSuccess;
     const PtBufs b = pt_bufs(ws, g, false, &e);
-    const uint64_t total = ws->shard_cap * kShards;
+    if (!total) total = ws->shard_cap * kShards;
     uint32_t* keys32 = reinterpret_cast<uint32_t*>(ws->inc.p);
     uint32_t* stage_p = reinterpret_cast<uint32_t*>(ws->uniq.p);
     uint32_t* stage_q = stage_p + total;
@@ -3048,6 +3103,7 @@ int run_postings(kmp_postings* ws, MakeKeys make_keys, const std::vector<unsigne
                  uint32_t* d_w, uint64_t cap, uint64_t* n_edges, kmp_postings_stats* stats, hipStream_t st) {
     if (heavy_df < 2) heavy_df = 2;
     if (min_shared < 1) min_shared = 1;
+    ws->bin_lo = ws->bin_hi = 0;  // every bucket (the k-mer split restricts its own calls)
     PG(ws->keys.reserve(slots));
     PG(ws->sorted.reserve(slots));
     PG(ws->flags.reserve(kFlN));
@@ -3107,6 +3163,112 @@ int run_postings(kmp_postings* ws, MakeKeys make_keys, const std::vector<unsigne
     rc = tail(ws, ws->inc.p, n_inc, n, min_shared, d_p, d_q, d_w, cap, n_edges, stats, st);
     if (rc == KMP_OK) finish_timing(ws, stats, st);
     return rc;
+}
+
+// ------------------------------------------------------------- multi-GPU k-mer split --------
+// kmp_dev_split_expand / kmp_dev_split_edges (kmerpair.h): rank `part` of `parts` groups and
+// expands only the k-mers of its coarse bins (a contiguous share of the bucket hash range; every
+// rank computes the windows of the whole batch and keeps its share at level 1), routes the pair
+// keys to the rank owning the row of their smaller protein, and that rank reduces them with the
+// row-block tail.  A pair's incidences from every k-mer meet on its row owner, so w is complete
+// there, and the ranks' row ranges are ordered: the rank-order concatenation is canonical.
+constexpr uint32_t kSplitMax = 64;  // ranks
+struct SplitRows {
+    uint32_t start[kSplitMax + 1];  // row range of rank d: [start[d], start[d+1])
+    uint32_t parts;
+};
+constexpr uint32_t kRtThreads = 256, kRtPer = 16, kRtTile = kRtThreads * kRtPer;
+
+// pair keys (p << pbits | q) of the shard regions -> region d (cap keys) of send, d = the rank
+// owning row p; one reservation per destination per 4,096-key tile on dcursor[d]
+__global__ __launch_bounds__(kRtThreads) void split_route_kernel(const unsigned long long* __restrict__ in,
+                                                                 const unsigned long long* __restrict__ cursor,
+                                                                 uint64_t sc, unsigned pbits, SplitRows rows,
+                                                                 uint64_t cap, unsigned long long* __restrict__ send,
+                                                                 unsigned long long* __restrict__ dcursor) {
+    __shared__ uint32_t lcnt[kSplitMax];
+    __shared__ unsigned long long base[kSplitMax];
+    const uint32_t s = blockIdx.y;
+    const uint64_t ns = min<unsigned long long>(cursor[s], sc), t0 = (uint64_t)blockIdx.x * kRtTile;
+    if (t0 >= ns) return;
+    const uint32_t m = (uint32_t)min<uint64_t>(kRtTile, ns - t0);
+    const unsigned long long* src = in + s * sc + t0;
+    if (threadIdx.x < kSplitMax) lcnt[threadIdx.x] = 0;
+    __syncthreads();
+    unsigned long long x[kRtPer];
+    uint32_t dr[kRtPer];  // destination << 24 | rank in the tile's run
+#pragma unroll
+    for (uint32_t e = 0; e < kRtPer; ++e) {
+        const uint32_t i = threadIdx.x + e * kRtThreads;
+        x[e] = i < m ? src[i] : kNoKey;
+    }
+#pragma unroll
+    for (uint32_t e = 0; e < kRtPer; ++e) {
+        dr[e] = ~0u;
+        if (x[e] == kNoKey) continue;
+        const uint32_t p = (uint32_t)(x[e] >> pbits);
+        uint32_t d = 0;
+        while (d + 1 < rows.parts && p >= rows.start[d + 1]) ++d;
+        dr[e] = d << 24 | atomicAdd(&lcnt[d], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < rows.parts)
+        base[threadIdx.x] =
+            lcnt[threadIdx.x] ? atomicAdd(&dcursor[threadIdx.x], (unsigned long long)lcnt[threadIdx.x]) : 0ull;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t e = 0; e < kRtPer; ++e) {
+        if (dr[e] == ~0u) continue;
+        const uint32_t d = dr[e] >> 24;
+        const unsigned long long pos = base[d] + (dr[e] & 0xFFFFFFu);
+        if (pos < cap) send[d * cap + pos] = x[e];
+    }
+}
+
+// the unused tail of every send region -> kNoKey (the receiver's tail skips it)
+__global__ void split_pad_kernel(unsigned long long* __restrict__ send, uint64_t cap,
+                                 const unsigned long long* __restrict__ dcursor) {
+    const uint32_t d = blockIdx.y;
+    for (uint64_t i = dcursor[d] + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        send[d * cap + i] = kNoKey;
+}
+
+__global__ void split_clear_kernel(unsigned long long* __restrict__ dcursor, uint32_t parts) {
+    if (threadIdx.x < parts) dcursor[threadIdx.x] = 0;
+}
+
+// the rank's flags (KMP_SPLIT_*) and statistics (kSt* order, summed over the shards)
+__global__ void split_finish_kernel(const unsigned long long* __restrict__ gstats,
+                                    const uint32_t* __restrict__ wflags, uint64_t sc,
+                                    const unsigned long long* __restrict__ dcursor, uint32_t parts, uint64_t cap,
+                                    uint32_t* __restrict__ out, unsigned long long* __restrict__ stats) {
+    const uint32_t t = threadIdx.x;
+    if (t < kStN) {
+        unsigned long long v = 0;
+        for (int sh = 0; sh < kShards; ++sh) {
+            const unsigned long long x = gstats[sh * 8 + t];
+            v = t == kStMaxDf ? max(v, x) : v + x;
+        }
+        stats[t] = v;
+    }
+    if (t == 0) {
+        unsigned long long shard = 0, spill = 0, part = 0;
+        for (int sh = 0; sh < kShards; ++sh) {
+            shard = max(shard, gstats[kRbCursor + sh]);
+            spill += gstats[kRbSpill + sh];
+        }
+        for (uint32_t d = 0; d < parts; ++d) part = max(part, dcursor[d]);
+        const uint32_t clamp = 0xFFFFFFFFu;
+        out[KMP_SPLIT_CLASS] = wflags[kFlClass];
+        out[KMP_SPLIT_HEAVY] = spill != 0;
+        out[KMP_SPLIT_MAX_PART] = (uint32_t)min<unsigned long long>(part, clamp);
+        out[KMP_SPLIT_MAX_SHARD] = (uint32_t)min<unsigned long long>(shard, clamp);
+        out[KMP_SPLIT_BIN_TILES] = wflags[kFlBin] ? wflags[kFlBinTiles] : 0u;
+        out[KMP_SPLIT_CURSOR] = wflags[kFlCur];
+        out[KMP_SPLIT_RERUN] = (part > cap || shard > sc || wflags[kFlBin] || wflags[kFlCur]) ? 1u : 0u;
+        for (uint32_t i = KMP_SPLIT_CURSOR + 1; i < KMP_SPLIT_FLAGS; ++i) out[i] = 0;
+    }
 }
 
 }  // namespace
@@ -3239,6 +3401,134 @@ int kmp_dev_pairs_rows(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d
     }
     return residues_impl(ws, d_res, d_res_off, d_class, n, k, slots, heavy_df, min_shared, require_class_diff, true,
                          row_lo, row_hi, d_p, d_q, d_w, cap, n_edges, stats, stream);
+}
+
+int kmp_dev_split_expand(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
+                         uint32_t n, int k, uint64_t slots, uint32_t heavy_df, int require_class_diff, uint32_t part,
+                         uint32_t parts, uint64_t cap, const uint32_t* learn, unsigned long long* d_send,
+                         uint32_t* d_flags, unsigned long long* d_stats, void* stream) {
+    if (!ws || !d_res || !d_res_off || !d_class || !d_send || !d_flags || !d_stats || k < 1 || k > kMaxK ||
+        parts < 1 || parts > kSplitMax || part >= parts || cap < 1)
+        return KMP_EINVAL;
+    hipStream_t st = as_stream(stream);
+    if (heavy_df < 2) heavy_df = 2;
+    const Layout lay = make_layout(n, k, slots, true);
+    if (!lay.bucketed) return KMP_ESTATE;
+    const std::vector<unsigned long long> shape = {n, slots, (unsigned long long)k, parts};
+    if (ws->split_shape != shape) {  // a new batch: learned capacities start over
+        ws->split_shape = shape;
+        ws->shard_cap = slots / 4 / kShards / parts + 4096;
+        ws->bp_J_min = 0;
+        ws->cur_on = ws->cur_mode;
+        ws->shape.clear();
+    }
+    if (learn) {  // the last call's flags, reduced over the ranks: every rank grows the same way
+        if (learn[KMP_SPLIT_MAX_SHARD] > ws->shard_cap)
+            ws->shard_cap = learn[KMP_SPLIT_MAX_SHARD] + learn[KMP_SPLIT_MAX_SHARD] / 32 + 256;
+        if (learn[KMP_SPLIT_BIN_TILES]) ws->bp_J_min = std::max(ws->bp_J_min, learn[KMP_SPLIT_BIN_TILES] + 2);
+        if (learn[KMP_SPLIT_CURSOR]) ws->cur_on = false;
+    }
+    if (ws->spill_cap == 0) ws->spill_cap = 1024;
+    ws->front_ok = false;  // the front below holds one bucket range only
+    StepCfg c{};
+    c.slots = slots;
+    c.lay = lay;
+    c.n = n;
+    c.heavy_df = heavy_df;
+    c.min_shared = 1;
+    c.require_diff = require_class_diff;
+    c.row_hi = n;
+    c.stride = 1;
+    PtGeom g;
+    if (!pt_geometry(ws, c, slots / 4, &g)) return KMP_EINVAL;
+    {
+        const int rc = step_reserve(ws, c, g);
+        if (rc != KMP_OK) return rc;
+    }
+    PG(ws->split_cur.reserve(kSplitMax));
+    const BpDigits dg = bp_digits(lay);
+    ws->bin_lo = (uint32_t)((uint64_t)part * dg.nb1 / parts);
+    ws->bin_hi = (uint32_t)((uint64_t)(part + 1) * dg.nb1 / parts);
+    auto make_keys = [&](const Layout& l, hipStream_t s) {
+        ws->parted = true;
+        ws->cur_used = ws->cur_on && cur_geometry(l, &ws->cg);
+        return bp_level1(ws, d_res, d_res_off, d_class, k, n, slots, l, s);
+    };
+    int rc = KMP_OK;
+    if (ws->bin_hi > ws->bin_lo) rc = enqueue_front(ws, make_keys, c, true, st);
+    else step_clear_kernel<<<1, 256, 0, st>>>(ws->flags.p, ws->bstats.p);  // no bins: nothing to expand
+    ws->bin_lo = ws->bin_hi = 0;
+    if (rc != KMP_OK) return rc;
+    SplitRows rows{};
+    rows.parts = parts;
+    kmp_row_split(n, parts, rows.start);
+    split_clear_kernel<<<1, kSplitMax, 0, st>>>(ws->split_cur.p, parts);
+    const unsigned long long* cursor = ws->bstats.p + kRbCursor;
+    split_route_kernel<<<dim3((uint32_t)((ws->shard_cap + kRtTile - 1) / kRtTile), kShards), kRtThreads, 0, st>>>(
+        ws->inc_sorted.p, cursor, ws->shard_cap, bits_for(n), rows, cap, d_send, ws->split_cur.p);
+    split_pad_kernel<<<dim3((uint32_t)std::min<uint64_t>((cap + 1023) / 1024, 256), parts), 256, 0, st>>>(
+        d_send, cap, ws->split_cur.p);
+    split_finish_kernel<<<1, 64, 0, st>>>(ws->bstats.p, ws->flags.p, ws->shard_cap, ws->split_cur.p, parts, cap,
+                                          d_flags, d_stats);
+    PG(hipGetLastError());
+    return KMP_OK;
+}
+
+int kmp_dev_split_edges(kmp_postings* ws, const unsigned long long* d_keys, uint64_t m, uint32_t n, uint32_t row_lo,
+                        uint32_t row_hi, uint32_t min_shared, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w,
+                        uint64_t cap, uint64_t* n_edges, void* stream) {
+    if (!ws || !n_edges || row_lo > row_hi || row_hi > n || (m && !d_keys) || (cap && (!d_p || !d_q || !d_w)))
+        return KMP_EINVAL;
+    *n_edges = 0;
+    if (m == 0 || row_lo == row_hi) return KMP_OK;
+    if (m > 0xFFFFFFFFull) return KMP_EINVAL;
+    hipStream_t st = as_stream(stream);
+    StepCfg c{};
+    c.n = n;
+    c.min_shared = std::max(1u, min_shared);
+    c.ranged = true;
+    c.row_lo = row_lo;
+    c.row_hi = row_hi;
+    c.d_p = d_p;
+    c.d_q = d_q;
+    c.d_w = d_w;
+    c.cap = cap;
+    c.stride = 1;
+    PtGeom g;
+    if (!pt_geometry(ws, c, m, &g)) return KMP_EINVAL;
+    g.flat_n = m;  // the received regions, padded with kNoKey, read as one array
+    g.nshards = 1;
+    g.sc = m;
+    g.jt = (uint32_t)((m + kPtTile - 1) / kPtTile);
+    hipError_t e = hipSuccess;
+    pt_bufs(ws, g, true, &e);
+    PG(e);
+    PG(ws->inc.reserve(m));  // u32 row-block keys
+    PG(ws->uniq.reserve(m));  // staged p | q (u32 each)
+    PG(ws->w.reserve(m));
+    PG(ws->ovf.reserve((uint64_t)g.nrb + 1));
+    PG(ws->small.reserve(16));
+    PG(ws->flags.reserve(kFlN));
+    PG(ws->bstats.reserve(kGsWords));
+    if (!ws->hrb) PG(hipHostMalloc((void**)&ws->hrb, kRbWords * sizeof(unsigned long long), hipHostMallocCoherent));
+    PG(hipMemsetAsync(ws->flags.p, 0, kFlN * sizeof(uint32_t), st));
+    int rc = enqueue_tail_in(ws, c, g, d_keys, nullptr, m, st);
+    if (rc != KMP_OK) return rc;
+    PG(hipStreamSynchronize(st));
+    const unsigned long long* rb = ws->hrb;
+    uint64_t ne = rb[kRbRuns];
+    if (rb[kRbOvf]) {  // row blocks above the LDS capacity: the segmented sort, fewer rows per block next time
+        if (g.rbits > 0) {
+            const double over = (double)rb[kRbMaxBlock] / (0.8 * kPtCap);
+            unsigned shrink = 1;
+            while (shrink < 16 && (double)(1u << shrink) < over) ++shrink;
+            ws->pt_rb_max = g.rbits > shrink ? g.rbits - shrink : 0u;
+        }
+        rc = pt_finish_overflow(ws, c, g, (uint32_t)rb[kRbOvf], &ne, st, m);
+        if (rc != KMP_OK) return rc;
+    }
+    *n_edges = ne;
+    return ne > cap ? KMP_EOVERFLOW : KMP_OK;
 }
 
 // Row ranges of a split of the pair space: a pair belongs to its smaller protein, so row p owns

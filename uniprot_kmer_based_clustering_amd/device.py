@@ -278,6 +278,35 @@ class DevicePipeline:
             return self.n_edges
         raise RuntimeError("edge count unstable across reruns")
 
+    def split_expand(self, part: int, parts: int, cap: int, send: torch.Tensor, flags: torch.Tensor,
+                     stats: torch.Tensor, learn=None, require_class_diff: bool = True,
+                     heavy_df: int = 0xFFFFFFFF) -> None:
+        """Multi-GPU k-mer split, phase 1 (kmp_dev_split_expand): this rank's share of the k-mers
+        grouped and expanded, pair keys routed to their row owners in `send` (parts regions of cap
+        keys, int64); flags (int32[KMP_SPLIT_FLAGS]) and stats (int64[8]) on the stream.  No host
+        synchronisation.  learn: the last call's flags reduced over the ranks (or None)."""
+        slots = int(lib().kmp_set_capacity(self.n, self.total))
+        lp = None if learn is None else (C.c_uint32 * _lib.KMP_SPLIT_FLAGS)(*[int(x) for x in learn])
+        check(lib().kmp_dev_split_expand(self._workspace(), _p(self.res), _p(self.off), _p(self.cls), self.n, self.k,
+                                         slots, heavy_df, int(require_class_diff), part, parts, cap, lp, _p(send),
+                                         _p(flags), _p(stats), _stream()), "kmp_dev_split_expand")
+
+    def split_edges(self, recv: torch.Tensor, row_lo: int, row_hi: int, min_shared: int = 1) -> int:
+        """Multi-GPU k-mer split, phase 2 (kmp_dev_split_edges): the received pair keys -> the
+        canonical edges of rows [row_lo, row_hi) in ep/eq/ew (syncs)."""
+        for _ in range(2):
+            ne = C.c_uint64()
+            st = lib().kmp_dev_split_edges(self._workspace(), _p(recv), recv.numel(), self.n, row_lo, row_hi,
+                                           min_shared, _p(self.ep), _p(self.eq), _p(self.ew), self.edge_cap,
+                                           C.byref(ne), _stream())
+            if st == _lib.KMP_EOVERFLOW:
+                self._alloc_edges(ne.value + ne.value // 8 + 1024)
+                continue
+            check(st, "kmp_dev_split_edges")
+            self.n_edges = ne.value
+            return self.n_edges
+        raise RuntimeError("edge count unstable across reruns")
+
     def postings(self, min_shared: int = 1, require_class_diff: bool = True,
                  heavy_df: int = 0xFFFFFFFF, from_residues: bool = False) -> int:
         """Postings engine: canonical edges into ep/eq/ew (syncs).  Reads the K(p) slots

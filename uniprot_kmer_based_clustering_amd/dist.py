@@ -17,6 +17,15 @@ config 5, far more than recomputing the grouping on each rank (≈ 5·10^8 windo
 
 The gather only moves tensors, so the same code runs on gloo with CPU tensors in the
 multi-process CPU tests (tests/test_dist.py).
+
+The k-mer split (``kmer_split_step``, the default of ``bench.py --gpus N``) divides the work
+instead of repeating the grouping on every rank: rank r keys every window but keeps only the
+k-mers of its share of the bucket hash range, groups and expands them, and routes each pair key
+to the rank owning the pair's row (kmp_dev_split_expand); one all-to-all of equal, padded splits
+moves the pair keys (42 MB in total per step at config 4, about 5 MB per rank at 8 ranks); every
+rank reduces its rows (kmp_dev_split_edges).  The row split stays the fallback for batches whose
+frequent k-mers spill (the heavy path is single-rank) and the bounded-memory mode: at config 5
+Σ C(df,2) ≈ 10^10-10^11 pair keys would cross the links, far more than recomputing the grouping.
 """
 from __future__ import annotations
 
@@ -73,6 +82,93 @@ def distributed_step(pipe, rank: int, world: int, group=None, min_shared: int = 
     lo, hi = row_ranges(pipe.n, world)[rank]
     m = pipe.rows(lo, hi, min_shared=min_shared, require_class_diff=require_class_diff)
     if world == 1:
+        return m
+
+    def grow(total):
+        old = (pipe.ep[:m].clone(), pipe.eq[:m].clone(), pipe.ew[:m].clone())
+        pipe._alloc_edges(total + total // 8)
+        for dst, src in zip((pipe.ep, pipe.eq, pipe.ew), old):
+            dst[:m].copy_(src)
+        return [pipe.ep, pipe.eq, pipe.ew]
+
+    total = gather_rows([pipe.ep, pipe.eq, pipe.ew], m, rank, world, group, grow)
+    if rank == 0:
+        pipe.n_edges = total
+    return total
+
+
+class SplitState:
+    """Learned state of the k-mer split, identical on every rank (it only changes from flags
+    reduced over the ranks): the per-destination send capacity, the flags to learn from on a
+    rerun, the exchange buffers, and whether the batch needs the row split."""
+
+    def __init__(self):
+        self.cap = 0
+        self.learn = None
+        self.bufs = None
+        self.row_split = False
+        self.reruns = 0
+
+
+def kmer_split_step(pipe, rank: int, world: int, group=None, min_shared: int = 1, require_class_diff: bool = True,
+                    gather: bool = False, state: SplitState | None = None, timings: list | None = None) -> int:
+    """One multi-GPU step of the k-mer split: expand this rank's k-mers, exchange the pair keys by
+    row owner (all-to-all), reduce this rank's rows.  Every rank ends holding the canonical edges
+    of its row range in pipe.ep/eq/ew (rank order = canonical order) and returns their count; with
+    gather, rank 0 also receives every rank's block behind its own and returns the total.  Falls
+    back to the row split (distributed_step) when the batch spills frequent k-mers.  timings: a
+    list to append this rank's (expand, exchange, edges) milliseconds to (CUDA events on the
+    current stream, which the library's stages and the collectives are ordered with)."""
+    st = state if state is not None else pipe.__dict__.setdefault("_split_state", SplitState())
+    if st.row_split:
+        return distributed_step(pipe, rank, world, group, min_shared, require_class_diff)
+    lo, hi = row_ranges(pipe.n, world)[rank]
+    dev = pipe.dev if hasattr(pipe, "dev") else torch.device("cpu")
+    if st.cap == 0:  # expected pair keys per (source, destination): a quarter of the windows / world^2
+        st.cap = max(4096, int(pipe.total // 4 // (world * world)))
+    m = 0
+    for _ in range(8):
+        if st.bufs is None or st.bufs[0].numel() != world * st.cap:
+            st.bufs = (torch.empty(world * st.cap, dtype=torch.int64, device=dev),
+                       torch.empty(world * st.cap, dtype=torch.int64, device=dev),
+                       torch.zeros(_lib.KMP_SPLIT_FLAGS, dtype=torch.int32, device=dev),
+                       torch.zeros(8, dtype=torch.int64, device=dev))
+        send, recv, flags, stats = st.bufs
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if timings is not None else None
+        if ev:
+            ev[0].record()
+        pipe.split_expand(rank, world, st.cap, send, flags, stats, learn=st.learn,
+                          require_class_diff=require_class_diff)
+        if ev:
+            ev[1].record()
+        if world > 1:
+            dist.all_to_all_single(recv, send, group=group)
+            dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=group)
+        else:
+            recv = send
+        if ev:
+            ev[2].record()
+        m = pipe.split_edges(recv, lo, hi, min_shared)
+        if ev:
+            ev[3].record()
+        fl = [int(x) for x in flags.cpu().tolist()]  # the step's one flag read-back
+        if fl[_lib.KMP_SPLIT_CLASS] or fl[_lib.KMP_SPLIT_HEAVY]:
+            st.row_split = True
+            return distributed_step(pipe, rank, world, group, min_shared, require_class_diff)
+        if fl[_lib.KMP_SPLIT_RERUN]:
+            st.reruns += 1
+            st.learn = fl
+            if fl[_lib.KMP_SPLIT_MAX_PART] > st.cap:
+                st.cap = fl[_lib.KMP_SPLIT_MAX_PART] + fl[_lib.KMP_SPLIT_MAX_PART] // 16 + 1024
+            continue
+        st.learn = None
+        if ev:
+            torch.cuda.synchronize()
+            timings.append(tuple(ev[i].elapsed_time(ev[i + 1]) for i in range(3)))
+        break
+    else:
+        raise RuntimeError("k-mer split: capacities unstable across reruns")
+    if not gather or world == 1:
         return m
 
     def grow(total):

@@ -115,6 +115,11 @@ class KmerPairEngine:
     def transport(self) -> str:
         return lib().kmp_ctx_transport(self._ctx).decode()
 
+    @property
+    def last_split(self) -> str:
+        """Flow of the last multi-GPU pairs call: 'kmer' (k-mer split) or 'rows' (row split)."""
+        return lib().kmp_ctx_last_split(self._ctx).decode()
+
     def set_pass_keys(self, keys: int) -> None:
         """Bounded-memory passes: pair keys per pass (0: auto, from the free device memory)."""
         self._check(lib().kmp_ctx_set_pass_keys(self._ctx, keys), "kmp_ctx_set_pass_keys")
