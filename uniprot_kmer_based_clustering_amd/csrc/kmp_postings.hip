@@ -1828,6 +1828,16 @@ struct kmp_postings {
     // single-synchronisation step as a HIP graph: captured on the second call with the same shape
     // (every buffer already sized), replayed after that
     bool graph_on = true;
+    struct GraphSlot {  // one captured sequence: its executable and the shape it was captured for
+        hipGraphExec_t gexec = nullptr;
+        std::vector<unsigned long long> key, seen;
+        void reset() {
+            if (gexec) (void)hipGraphExecDestroy(gexec);
+            gexec = nullptr;
+            key.clear();
+            seen.clear();
+        }
+    } split_g[2];  // the k-mer split's phases (expand, edges)
     hipGraphExec_t gexec = nullptr;
     hipStream_t cst = nullptr;  // capture stream
     std::vector<unsigned long long> gkey, gkey_seen;
@@ -1846,6 +1856,7 @@ struct kmp_postings {
             if (e) (void)hipEventDestroy(e);
         if (hrb) (void)hipHostFree(hrb);
         if (gexec) (void)hipGraphExecDestroy(gexec);
+        for (auto& g : split_g) g.reset();
         if (cst) (void)hipStreamDestroy(cst);
     }
     void mark(int stage, hipStream_t st) {
@@ -2510,8 +2521,11 @@ bool pt_geometry(const kmp_postings* ws, const StepCfg& c, uint64_t inc, PtGeom*
     const uint32_t rows = c.ranged ? c.row_hi - c.row_lo : c.n;
     const uint64_t est = std::max<uint64_t>(1, inc);
     // rows per block ~ (kPtCap / 2.4) * rows / est, to the nearest power of two: an average block
-    // of 2.4-4.8K keys; the first rows (p is the smaller index) hold about twice the average
-    const double want = (double)kPtCap / 2.4 * std::max<uint32_t>(rows, 1) / est;
+    // of 2.4-4.8K keys; the first rows (p is the smaller index) hold about twice the average.  A
+    // small call (a rank's rows of the k-mer split) takes smaller blocks, down to ~1K keys, so
+    // that ~1,000 workgroups still fill the GPU
+    const double per_block = std::min((double)kPtCap / 2.4, std::max(1024.0, (double)est / 1024));
+    const double want = per_block * std::max<uint32_t>(rows, 1) / est;
     unsigned rb = 0;
     while (rb < 16 && (double)(1u << rb) * 1.41421356 < want) ++rb;
     rb = std::min(rb, ws->pt_rb_max);  // learned from overflowing blocks
@@ -2795,6 +2809,49 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
 
 // enqueue the fused step: replay the captured graph when the shape matches the capture, capture
 // it when the shape repeats a plain run (buffers sized), else run plain
+// enqueue(s) on `st` as a HIP graph of `slot`: replayed when key matches its capture, captured when
+// key repeats the last plain run (every buffer sized by then), else run plain.  key must hold
+// every input of the sequence (shape, pointers, learned capacities, g_grow_gen).
+template <class Enqueue>
+int slot_launch(kmp_postings* ws, kmp_postings::GraphSlot& slot, std::vector<unsigned long long> key,
+                Enqueue enqueue, hipStream_t st) {
+    key.push_back(g_grow_gen);
+    if (!ws->graph_on) return enqueue(st);
+    if (slot.gexec && slot.key == key) {
+        PG(hipGraphLaunch(slot.gexec, st));
+        ++ws->graph_replays;
+        return KMP_OK;
+    }
+    if (slot.seen != key) {
+        slot.seen = key;
+        return enqueue(st);
+    }
+    if (slot.gexec) (void)hipGraphExecDestroy(slot.gexec);
+    slot.gexec = nullptr;
+    slot.key.clear();
+    if (!ws->cst && hipStreamCreateWithFlags(&ws->cst, hipStreamNonBlocking) != hipSuccess) ws->cst = nullptr;
+    hipGraph_t gr = nullptr;
+    if (!ws->cst || hipStreamBeginCapture(ws->cst, hipStreamCaptureModeRelaxed) != hipSuccess) {
+        (void)hipGetLastError();
+        return enqueue(st);
+    }
+    const unsigned long long gen = g_grow_gen;
+    int rc = enqueue(ws->cst);
+    hipError_t e = hipStreamEndCapture(ws->cst, &gr);
+    hipGraphExec_t ex = nullptr;
+    if (rc == KMP_OK && e == hipSuccess && gr && gen == g_grow_gen) e = hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0);
+    else if (e == hipSuccess) e = hipErrorUnknown;
+    if (gr) (void)hipGraphDestroy(gr);
+    if (e != hipSuccess || !ex) {  // not capturable this time: plain
+        (void)hipGetLastError();
+        return enqueue(st);
+    }
+    slot.gexec = ex;
+    slot.key = key;
+    PG(hipGraphLaunch(slot.gexec, st));
+    return KMP_OK;
+}
+
 template <class MakeKeys>
 int fused_launch(kmp_postings* ws, MakeKeys& make_keys, const std::vector<unsigned long long>& key, const StepCfg& c,
                  const PtGeom& g, hipStream_t st) {
@@ -3312,6 +3369,8 @@ int kmp_postings_set_graph(kmp_postings* ws, int enable) {
         ws->gexec = nullptr;
         ws->gkey.clear();
     }
+    if (!ws->graph_on)
+        for (auto& g : ws->split_g) g.reset();
     ws->gkey_seen.clear();
     return KMP_OK;
 }
@@ -3454,24 +3513,32 @@ int kmp_dev_split_expand(kmp_postings* ws, const uint8_t* d_res, const uint64_t*
         ws->cur_used = ws->cur_on && cur_geometry(l, &ws->cg);
         return bp_level1(ws, d_res, d_res_off, d_class, k, n, slots, l, s);
     };
-    int rc = KMP_OK;
-    if (ws->bin_hi > ws->bin_lo) rc = enqueue_front(ws, make_keys, c, true, st);
-    else step_clear_kernel<<<1, 256, 0, st>>>(ws->flags.p, ws->bstats.p);  // no bins: nothing to expand
-    ws->bin_lo = ws->bin_hi = 0;
-    if (rc != KMP_OK) return rc;
     SplitRows rows{};
     rows.parts = parts;
     kmp_row_split(n, parts, rows.start);
-    split_clear_kernel<<<1, kSplitMax, 0, st>>>(ws->split_cur.p, parts);
-    const unsigned long long* cursor = ws->bstats.p + kRbCursor;
-    split_route_kernel<<<dim3((uint32_t)((ws->shard_cap + kRtTile - 1) / kRtTile), kShards), kRtThreads, 0, st>>>(
-        ws->inc_sorted.p, cursor, ws->shard_cap, bits_for(n), rows, cap, d_send, ws->split_cur.p);
-    split_pad_kernel<<<dim3((uint32_t)std::min<uint64_t>((cap + 1023) / 1024, 256), parts), 256, 0, st>>>(
-        d_send, cap, ws->split_cur.p);
-    split_finish_kernel<<<1, 64, 0, st>>>(ws->bstats.p, ws->flags.p, ws->shard_cap, ws->split_cur.p, parts, cap,
-                                          d_flags, d_stats);
-    PG(hipGetLastError());
-    return KMP_OK;
+    auto enqueue = [&](hipStream_t s) -> int {
+        int rc = KMP_OK;
+        if (ws->bin_hi > ws->bin_lo) rc = enqueue_front(ws, make_keys, c, true, s);
+        else step_clear_kernel<<<1, 256, 0, s>>>(ws->flags.p, ws->bstats.p);  // no bins: nothing to expand
+        if (rc != KMP_OK) return rc;
+        split_clear_kernel<<<1, kSplitMax, 0, s>>>(ws->split_cur.p, parts);
+        const unsigned long long* cursor = ws->bstats.p + kRbCursor;
+        split_route_kernel<<<dim3((uint32_t)((ws->shard_cap + kRtTile - 1) / kRtTile), kShards), kRtThreads, 0, s>>>(
+            ws->inc_sorted.p, cursor, ws->shard_cap, bits_for(n), rows, cap, d_send, ws->split_cur.p);
+        split_pad_kernel<<<dim3((uint32_t)std::min<uint64_t>((cap + 1023) / 1024, 256), parts), 256, 0, s>>>(
+            d_send, cap, ws->split_cur.p);
+        split_finish_kernel<<<1, 64, 0, s>>>(ws->bstats.p, ws->flags.p, ws->shard_cap, ws->split_cur.p, parts, cap,
+                                              d_flags, d_stats);
+        PG(hipGetLastError());
+        return KMP_OK;
+    };
+    const std::vector<unsigned long long> key = {
+        n, slots, (unsigned long long)k, heavy_df, (unsigned long long)require_class_diff, part, parts, cap,
+        (uintptr_t)d_res, (uintptr_t)d_res_off, (uintptr_t)d_class, (uintptr_t)d_send, (uintptr_t)d_flags,
+        (uintptr_t)d_stats, ws->shard_cap, ws->spill_cap, ws->bp_J_min, ws->cur_on, ws->timing};
+    const int rc = slot_launch(ws, ws->split_g[0], key, enqueue, st);
+    ws->bin_lo = ws->bin_hi = 0;
+    return rc;
 }
 
 int kmp_dev_split_edges(kmp_postings* ws, const unsigned long long* d_keys, uint64_t m, uint32_t n, uint32_t row_lo,
@@ -3511,8 +3578,14 @@ int kmp_dev_split_edges(kmp_postings* ws, const unsigned long long* d_keys, uint
     PG(ws->flags.reserve(kFlN));
     PG(ws->bstats.reserve(kGsWords));
     if (!ws->hrb) PG(hipHostMalloc((void**)&ws->hrb, kRbWords * sizeof(unsigned long long), hipHostMallocCoherent));
-    PG(hipMemsetAsync(ws->flags.p, 0, kFlN * sizeof(uint32_t), st));
-    int rc = enqueue_tail_in(ws, c, g, d_keys, nullptr, m, st);
+    auto enqueue = [&](hipStream_t s) -> int {
+        step_clear_kernel<<<1, 256, 0, s>>>(ws->flags.p, ws->bstats.p);  // flags (the expand's stats are out)
+        return enqueue_tail_in(ws, c, g, d_keys, nullptr, m, s);
+    };
+    const std::vector<unsigned long long> key = {m, n, row_lo, row_hi, c.min_shared, cap, (uintptr_t)d_keys,
+                                                 (uintptr_t)d_p, (uintptr_t)d_q, (uintptr_t)d_w, g.rbits,
+                                                 ws->timing};
+    int rc = slot_launch(ws, ws->split_g[1], key, enqueue, st);
     if (rc != KMP_OK) return rc;
     PG(hipStreamSynchronize(st));
     const unsigned long long* rb = ws->hrb;
