@@ -1,4 +1,5 @@
-# kernel stats of the config-3 step for each KMP_LIB variant given (abvar/<name>.so), 8 steps each
+# kernel stats of the config-3 step for each KMP_LIB variant given (abvar/<name>.so: a build of the
+# library with changed kernels, copied there by hand), 8 steps each
 set -e
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out

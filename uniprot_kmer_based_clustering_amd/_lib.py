@@ -11,7 +11,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# KMP_LIB: an alternative build of the same library (tools/build_variants.sh A/B timing only)
+# KMP_LIB: an alternative build of the same library (tools/_ab_kernels.sh A/B timing only)
 LIB_PATH = os.environ.get("KMP_LIB") or os.path.join(HERE, "lib", "libkmerpair.so")
 HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "kmerpair.h")
 

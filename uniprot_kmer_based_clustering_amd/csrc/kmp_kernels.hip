@@ -366,10 +366,7 @@ __device__ __forceinline__ void batch_issue(BatchX<B, C>& b, const uint32_t* __r
     }
 }
 
-// kAblate (diagnostic builds only, selected by KMP_PAIR_ABLATE): 0 = the kernel; 1 = build the
-// tile + stream the columns, no probing; 2 = build the tile only; 3 = Bloom probes only (no
-// exact table, no counting).  Modes 1-3 produce wrong edges and exist to time the phases.
-template <int kAblate, uint32_t C, uint32_t B>
+template <uint32_t C, uint32_t B>
 __global__ __launch_bounds__(kPairThreads) void pair_kernel(
     const uint32_t* __restrict__ dense, const uint64_t* __restrict__ dense_off, const uint16_t* __restrict__ cls,
     const kmp_work_item* __restrict__ items, uint32_t min_shared, int require_diff, uint32_t* __restrict__ out_p,
@@ -446,11 +443,9 @@ __global__ __launch_bounds__(kPairThreads) void pair_kernel(
     __syncthreads();
     for (uint32_t i = tid; i < kPairWaves * kRowsMax; i += kPairThreads) scratch[i] = 0;  // hit counters
     __syncthreads();
-    if (kAblate == 2) return;
     uint32_t* cnt = scratch + wave * kRowsMax;
     uint64_t* tm = tmask[wave];
     uint32_t nbuf = 0;  // wave-uniform fill of the wave's edge buffer
-    uint32_t sink = 0;
 
     // flush the wave's edge buffer to HBM: one global atomic per kEdgeBuf edges
     auto flush = [&]() {
@@ -472,11 +467,6 @@ __global__ __launch_bounds__(kPairThreads) void pair_kernel(
     // probe 64*C k-mers x[] of column q (lanes/registers past len are ignored)
     auto probe = [&](uint32_t q, uint32_t len, uint32_t base, const uint32_t (&x)[C], bool& hit_any) {
         const uint32_t lim = min(q - r0, nrows);  // rows with p < q
-        if (kAblate == 1) {
-#pragma unroll
-            for (uint32_t i = 0; i < C; ++i) sink += x[i];
-            return;
-        }
         uint64_t word[C], want[C];
         uint32_t blk[C];
 #pragma unroll
@@ -491,10 +481,6 @@ __global__ __launch_bounds__(kPairThreads) void pair_kernel(
         for (uint32_t i = 0; i < C; ++i) {
             pass[i] = base + lane + 64 * i < len && (word[i] & want[i]) == want[i];
             any |= pass[i];
-        }
-        if (kAblate == 3) {
-            sink += any;
-            return;
         }
         if (__ballot(any) == 0) return;
 #pragma unroll
@@ -612,7 +598,6 @@ __global__ __launch_bounds__(kPairThreads) void pair_kernel(
         }
     }
     flush();
-    if (kAblate != 0 && sink == 0xFFFFFFFFu) out_w[0] = sink;  // keep the ablated work alive
 }
 
 // ------------------------------------------------------------------------------------
@@ -857,35 +842,16 @@ int kmp_dev_pairs(const uint32_t* d_dense, const uint64_t* d_dense_off, const ui
         return KMP_EINVAL;
     if (n_items > 0x7FFFFFFFull) return KMP_EINVAL;
     if (min_shared < 1) min_shared = 1;
-    static const int ablate = [] {
-        const char* v = std::getenv("KMP_PAIR_ABLATE");
-        return v ? std::atoi(v) : 0;
-    }();
     const dim3 grid((uint32_t)n_items), block(kPairThreads);
     hipStream_t st = as_stream(stream);
-#define KMP_PAIR_LAUNCH(A, CC, BB)                                                                          \
-    pair_kernel<A, CC, BB><<<grid, block, 0, st>>>(d_dense, d_dense_off, d_class, d_items, min_shared,      \
-                                                   require_class_diff, d_p, d_q, d_w, cap, d_count)
+#define KMP_PAIR_LAUNCH(CC, BB)                                                                             \
+    pair_kernel<CC, BB><<<grid, block, 0, st>>>(d_dense, d_dense_off, d_class, d_items, min_shared,          \
+                                                require_class_diff, d_p, d_q, d_w, cap, d_count)
     // register window: 64*C k-mers per column, B columns per batch (2*B*C VGPRs in flight)
-    static const uint32_t force_window = [] {
-        const char* v = std::getenv("KMP_PAIR_WINDOW");  // diagnostic override
-        return v ? (uint32_t)std::atoi(v) : 0u;
-    }();
-    if (force_window) col_window = force_window;
     const uint32_t w = col_window <= 192 ? 3u : col_window <= 384 ? 6u : 12u;
-#define KMP_PAIR_BY_WINDOW(A)                 \
-    do {                                      \
-        if (w == 3) KMP_PAIR_LAUNCH(A, 3, 8); \
-        else if (w == 6) KMP_PAIR_LAUNCH(A, 6, 3); \
-        else KMP_PAIR_LAUNCH(A, 12, 1);       \
-    } while (0)
-    switch (ablate) {
-        case 1: KMP_PAIR_BY_WINDOW(1); break;
-        case 2: KMP_PAIR_BY_WINDOW(2); break;
-        case 3: KMP_PAIR_BY_WINDOW(3); break;
-        default: KMP_PAIR_BY_WINDOW(0); break;
-    }
-#undef KMP_PAIR_BY_WINDOW
+    if (w == 3) KMP_PAIR_LAUNCH(3, 8);
+    else if (w == 6) KMP_PAIR_LAUNCH(6, 3);
+    else KMP_PAIR_LAUNCH(12, 1);
 #undef KMP_PAIR_LAUNCH
     return hip_status(hipGetLastError());
 }
