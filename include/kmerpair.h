@@ -477,9 +477,14 @@ int kmp_dev_sort_edges(uint32_t* d_p, uint32_t* d_q, uint32_t* d_w, uint64_t n, 
 /* FASTA ingest with seq_io semantics (main.rs:62-72): id = header up to the first space,
  * seq = the record's sequence bytes; AMR class = id.split_terminator('|')[3]
  * (protein.rs:135-138) interned to ids in order of first appearance.  Library-owned
- * output buffers; free each with kmp_free_host.  ids: NUL-separated id strings. */
+ * output buffers; free each with kmp_free_host.  ids: NUL-separated id strings.
+ * Multithreaded like the reference's parallel_fasta: the mapped file is cut into byte ranges,
+ * each thread parses the records whose header starts in its range; kmp_read_fasta uses
+ * min(16, hardware threads), kmp_read_fasta_threads the given count (0: the same default). */
 int kmp_read_fasta(const char* path, uint32_t* n, uint8_t** residues, uint64_t** offsets,
                    uint16_t** class_id, char** ids, uint64_t* ids_bytes, uint32_t* n_classes);
+int kmp_read_fasta_threads(const char* path, int threads, uint32_t* n, uint8_t** residues, uint64_t** offsets,
+                           uint16_t** class_id, char** ids, uint64_t* ids_bytes, uint32_t* n_classes);
 /* Synthetic sets of SURVEY.md §8d.  residues is malloc'd (free with kmp_free_host);
  * offsets[N+1], class_id[N], family[N] are caller buffers (class_id/family may be NULL). */
 int kmp_synth_packed(uint32_t n, uint64_t seed, int length_law, uint8_t** residues,

@@ -75,6 +75,34 @@ def test_fasta_edge_cases(tmp_path):
     np.testing.assert_array_equal(b.class_id, cls)
 
 
+def test_fasta_threads_match_independent_parser(tmp_path):
+    """The multithreaded reader (byte ranges per thread, records owned by the range their header
+    starts in) on a 6 MB file of wrapped, mixed LF / CRLF records with headers that straddle the
+    ranges: every thread count gives the independent parser's result."""
+    rng = np.random.default_rng(3)
+    alpha = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWYX*", dtype=np.uint8)
+    parts = [b"; leading comment line\n"]
+    for r in range(12000):
+        seq = alpha[rng.integers(0, len(alpha), int(rng.integers(0, 900)))].tobytes()
+        nl = b"\r\n" if r % 7 == 0 else b"\n"
+        width = int(rng.integers(40, 200))
+        body = nl.join(seq[i:i + width] for i in range(0, len(seq), width))
+        extra = b" desc text" if r % 3 == 0 else b""
+        end = b"" if r == 11999 else nl  # the last record without a final terminator
+        parts.append(b">sp|P%05d|x|class%d|g%d%s%s%s%s" % (r, r % 23, r, extra, nl, body, end))
+    data = b"".join(parts)
+    path = tmp_path / "wrapped.fasta"
+    path.write_bytes(data)
+    res, off, cls, ids = parse_fasta_bytes(data)
+    for t in (1, 3, 16, 64):
+        b = K.read_fasta(str(path), threads=t)
+        assert b.n == 12000
+        np.testing.assert_array_equal(b.offsets, off)
+        np.testing.assert_array_equal(b.residues, res)
+        np.testing.assert_array_equal(b.class_id, cls)
+        assert b.ids == ids and b.n_classes == 23
+
+
 def test_fasta_missing_class_field_is_an_error(tmp_path):
     path = tmp_path / "bad.fasta"
     path.write_bytes(b">a|b|c|\nACDE\n")   # split_terminator gives 3 fields -> reference panics

@@ -163,6 +163,8 @@ SIGNATURES = {
     "kmp_dev_sort_edges": (C.c_int, [P, P, P, C.c_uint64, C.c_uint32, P, C.c_uint64, P]),
     "kmp_read_fasta": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint32), C.POINTER(P), C.POINTER(P),
                                  C.POINTER(P), C.POINTER(P), U64P, C.POINTER(C.c_uint32)]),
+    "kmp_read_fasta_threads": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(C.c_uint32), C.POINTER(P), C.POINTER(P),
+                                         C.POINTER(P), C.POINTER(P), U64P, C.POINTER(C.c_uint32)]),
     "kmp_synth_packed": (C.c_int, [C.c_uint32, C.c_uint64, C.c_int, C.POINTER(P), P, P, P]),
     "kmp_synth_write_fasta": (C.c_int, [C.c_char_p, C.c_uint32, C.c_uint64, C.c_int]),
     "kmp_free_host": (None, [P]),

@@ -10,11 +10,20 @@
 //     field is not a field; fewer than four fields is an error (the reference panics).
 // Classes are interned to u16 ids in order of first appearance.  uniprot_arg.fasta is
 // single-line, LF-terminated; multi-line / CRLF inputs follow the rules above.
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <string_view>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -22,33 +31,54 @@
 
 namespace {
 
-bool read_file(const char* path, std::string& out) {
-    FILE* f = std::fopen(path, "rb");
-    if (!f) return false;
-    char buf[1 << 16];
-    size_t r;
-    while ((r = std::fread(buf, 1, sizeof buf, f)) > 0) out.append(buf, r);
-    const bool ok = !std::ferror(f);
-    std::fclose(f);
-    return ok;
-}
+// the file mapped read-only (empty files: an empty view)
+struct Mapped {
+    const char* p = nullptr;
+    size_t n = 0;
+    bool ok = false;
+    explicit Mapped(const char* path) {
+        const int fd = ::open(path, O_RDONLY);
+        if (fd < 0) return;
+        struct stat st;
+        if (::fstat(fd, &st) == 0) {
+            n = (size_t)st.st_size;
+            if (n == 0) {
+                ok = true;
+            } else {
+                void* m = ::mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
+                if (m != MAP_FAILED) {
+                    p = static_cast<const char*>(m);
+                    ok = true;
+                }
+            }
+        }
+        ::close(fd);
+    }
+    ~Mapped() {
+        if (p) ::munmap(const_cast<char*>(p), n);
+    }
+};
 
 // id.split_terminator('|')[3]
-bool amr_class(const std::string& id, std::string& cls) {
-    std::vector<std::string> fields;
+bool amr_class(std::string_view id, std::string_view& cls) {
     size_t b = 0;
+    int field = 0;
     for (;;) {
         const size_t e = id.find('|', b);
-        if (e == std::string::npos) {
-            if (b < id.size()) fields.push_back(id.substr(b));  // split_terminator: no trailing ""
-            break;
+        if (e == std::string_view::npos) {
+            if (b < id.size() && field == 3) {  // split_terminator: no trailing ""
+                cls = id.substr(b);
+                return true;
+            }
+            return false;
         }
-        fields.push_back(id.substr(b, e - b));
+        if (field == 3) {
+            cls = id.substr(b, e - b);
+            return true;
+        }
+        ++field;
         b = e + 1;
     }
-    if (fields.size() < 4) return false;
-    cls = fields[3];
-    return true;
 }
 
 template <class T>
@@ -58,71 +88,134 @@ T* dup(const std::vector<T>& v) {
     return p;
 }
 
+// one record: its id, class and raw sequence span [s0, s1) of the text
+struct Rec {
+    std::string_view id, cls;
+    size_t s0, s1;
+};
+
+// the records whose header line starts in [a, b) of text (a record starts at a '>' that begins a
+// line); false: a record without a class field (the reference panics)
+bool parse_range(const char* t, size_t N, size_t a, size_t b, std::vector<Rec>& out) {
+    size_t i = a;
+    while (i < b && !(t[i] == '>' && (i == 0 || t[i - 1] == '\n'))) {  // the range's first record
+        const void* nl = std::memchr(t + i, '\n', N - i);
+        i = nl ? (size_t)((const char*)nl - t) + 1 : N;
+    }
+    while (i < b) {
+        const void* nl = std::memchr(t + i, '\n', N - i);
+        const size_t e = nl ? (size_t)((const char*)nl - t) : N;
+        size_t he = e;
+        if (he > i + 1 && t[he - 1] == '\r') --he;
+        std::string_view head(t + i + 1, he - (i + 1));
+        const size_t sp = head.find(' ');
+        Rec r;
+        r.id = sp == std::string_view::npos ? head : head.substr(0, sp);
+        if (!amr_class(r.id, r.cls)) return false;
+        i = e < N ? e + 1 : N;
+        // sequence lines up to the next header: raw bytes, the last line's terminator dropped
+        r.s0 = r.s1 = i;
+        while (i < N && t[i] != '>') {
+            const void* ln = std::memchr(t + i, '\n', N - i);
+            const size_t le = ln ? (size_t)((const char*)ln - t) : N;
+            size_t ce = le;
+            if (ce > i && t[ce - 1] == '\r') --ce;
+            r.s1 = ce;
+            i = le < N ? le + 1 : N;
+        }
+        out.push_back(r);
+    }
+    return true;
+}
+
+int threads_for(int t) {
+    if (t > 0) return std::min(t, 256);
+    const unsigned h = std::thread::hardware_concurrency();
+    return (int)std::max(1u, std::min(h ? h : 1u, 16u));
+}
+
+template <class F>
+void parallel(int T, F f) {
+    std::vector<std::thread> pool;
+    for (int t = 1; t < T; ++t) pool.emplace_back(f, t);
+    f(0);
+    for (auto& th : pool) th.join();
+}
+
 }  // namespace
+
+// Multithreaded (the reference reads with parallel_fasta, main.rs:62-72): the mapped file is cut
+// into `threads` byte ranges, each thread parses the records whose header starts in its range,
+// classes are interned in file order of first appearance, and the residues and ids are copied in
+// parallel to their prefix-summed offsets.
+extern "C" int kmp_read_fasta_threads(const char* path, int threads, uint32_t* n, uint8_t** residues,
+                                      uint64_t** offsets, uint16_t** class_id, char** ids, uint64_t* ids_bytes,
+                                      uint32_t* n_classes) {
+    if (!path || !n || !residues || !offsets || !class_id) return KMP_EINVAL;
+    Mapped m(path);
+    if (!m.ok) return KMP_EIO;
+    const char* t = m.p;
+    const size_t N = m.n;
+    const int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)threads_for(threads), N / (1 << 16) + 1));
+    std::vector<std::vector<Rec>> recs(T);
+    std::vector<char> ok(T, 1);
+    parallel(T, [&](int k) { ok[k] = parse_range(t, N, N * k / T, N * (k + 1) / T, recs[k]); });
+    for (int k = 0; k < T; ++k)
+        if (!ok[k]) return KMP_EINVAL;
+    // record offsets per thread, class ids in order of first appearance
+    std::vector<size_t> rbase(T + 1, 0);
+    for (int k = 0; k < T; ++k) rbase[k + 1] = rbase[k] + recs[k].size();
+    const size_t R = rbase[T];
+    if (R > 0xFFFFFFFFull) return KMP_EINVAL;
+    std::vector<uint64_t> off(R + 1, 0), idoff(R + 1, 0);
+    std::vector<uint16_t> cls(R);
+    std::unordered_map<std::string_view, uint16_t> intern;
+    {
+        size_t r = 0;
+        for (int k = 0; k < T; ++k)
+            for (const Rec& x : recs[k]) {
+                auto it = intern.find(x.cls);
+                if (it == intern.end()) {
+                    if (intern.size() >= 65535) return KMP_EINVAL;
+                    it = intern.emplace(x.cls, (uint16_t)intern.size()).first;
+                }
+                cls[r] = it->second;
+                off[r + 1] = off[r] + (x.s1 - x.s0);
+                idoff[r + 1] = idoff[r] + x.id.size() + 1;
+                ++r;
+            }
+    }
+    uint8_t* res = static_cast<uint8_t*>(std::malloc(off[R] ? off[R] : 1));
+    char* idb = ids ? static_cast<char*>(std::malloc(idoff[R] + 1)) : nullptr;
+    if (!res || (ids && !idb)) {
+        std::free(res);
+        std::free(idb);
+        return KMP_ENOMEM;
+    }
+    parallel(T, [&](int k) {
+        size_t r = rbase[k];
+        for (const Rec& x : recs[k]) {
+            if (x.s1 > x.s0) std::memcpy(res + off[r], t + x.s0, x.s1 - x.s0);
+            if (idb) {
+                std::memcpy(idb + idoff[r], x.id.data(), x.id.size());
+                idb[idoff[r] + x.id.size()] = '\0';
+            }
+            ++r;
+        }
+    });
+    if (idb) idb[idoff[R]] = '\0';
+    *n = (uint32_t)R;
+    *residues = res;
+    *offsets = dup(off);
+    *class_id = dup(cls);
+    if (ids) *ids = idb;
+    if (ids_bytes) *ids_bytes = idoff[R];
+    if (n_classes) *n_classes = (uint32_t)intern.size();
+    if (!*offsets || !*class_id) return KMP_ENOMEM;
+    return KMP_OK;
+}
 
 extern "C" int kmp_read_fasta(const char* path, uint32_t* n, uint8_t** residues, uint64_t** offsets,
                               uint16_t** class_id, char** ids, uint64_t* ids_bytes, uint32_t* n_classes) {
-    if (!path || !n || !residues || !offsets || !class_id) return KMP_EINVAL;
-    std::string text;
-    if (!read_file(path, text)) return KMP_EIO;
-    std::vector<uint8_t> res;
-    std::vector<uint64_t> off;
-    std::vector<uint16_t> cls;
-    std::string idbuf;
-    std::unordered_map<std::string, uint16_t> intern;
-    res.reserve(text.size());
-    size_t i = 0;
-    const size_t N = text.size();
-    // skip anything before the first record header
-    while (i < N && text[i] != '>') {
-        const size_t e = text.find('\n', i);
-        i = e == std::string::npos ? N : e + 1;
-    }
-    while (i < N) {
-        // header line
-        size_t e = text.find('\n', i);
-        if (e == std::string::npos) e = N;
-        size_t he = e;
-        if (he > i + 1 && text[he - 1] == '\r') --he;
-        const std::string head = text.substr(i + 1, he - (i + 1));
-        const size_t sp = head.find(' ');
-        const std::string id = sp == std::string::npos ? head : head.substr(0, sp);
-        std::string c;
-        if (!amr_class(id, c)) return KMP_EINVAL;
-        auto it = intern.find(c);
-        if (it == intern.end()) {
-            if (intern.size() >= 65535) return KMP_EINVAL;
-            it = intern.emplace(c, (uint16_t)intern.size()).first;
-        }
-        cls.push_back(it->second);
-        idbuf.append(id);
-        idbuf.push_back('\0');
-        off.push_back(res.size());
-        i = e < N ? e + 1 : N;
-        // sequence lines up to the next header
-        size_t s0 = i, s1 = i;
-        while (i < N && text[i] != '>') {
-            size_t le = text.find('\n', i);
-            if (le == std::string::npos) le = N;
-            size_t content_end = le;
-            if (content_end > i && text[content_end - 1] == '\r') --content_end;
-            s1 = content_end;  // raw bytes up to the end of the last line's content
-            i = le < N ? le + 1 : N;
-        }
-        if (s1 > s0) res.insert(res.end(), text.begin() + s0, text.begin() + s1);
-    }
-    off.push_back(res.size());
-    if (off.size() - 1 > 0xFFFFFFFFull) return KMP_EINVAL;
-    *n = (uint32_t)(off.size() - 1);
-    *residues = dup(res);
-    *offsets = dup(off);
-    *class_id = dup(cls);
-    if (ids) {
-        *ids = static_cast<char*>(std::malloc(idbuf.size() + 1));
-        if (*ids) std::memcpy(*ids, idbuf.data(), idbuf.size() + 1);
-    }
-    if (ids_bytes) *ids_bytes = idbuf.size();
-    if (n_classes) *n_classes = (uint32_t)intern.size();
-    if (!*residues || !*offsets || !*class_id) return KMP_ENOMEM;
-    return KMP_OK;
+    return kmp_read_fasta_threads(path, 0, n, residues, offsets, class_id, ids, ids_bytes, n_classes);
 }

@@ -34,15 +34,16 @@ class Proteins:
         return len(self.offsets) - 1
 
 
-def read_fasta(path: str) -> Proteins:
-    """FASTA ingest with seq_io semantics (libkmerpair kmp_read_fasta)."""
+def read_fasta(path: str, threads: int = 0) -> Proteins:
+    """FASTA ingest with seq_io semantics (libkmerpair kmp_read_fasta_threads; threads 0: the
+    library's default, min(16, hardware threads))."""
     L = lib()
     n = C.c_uint32()
     res, off, cls, ids = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_void_p()
     ids_bytes = C.c_uint64()
     ncls = C.c_uint32()
-    st = L.kmp_read_fasta(path.encode(), C.byref(n), C.byref(res), C.byref(off), C.byref(cls),
-                          C.byref(ids), C.byref(ids_bytes), C.byref(ncls))
+    st = L.kmp_read_fasta_threads(path.encode(), threads, C.byref(n), C.byref(res), C.byref(off), C.byref(cls),
+                                  C.byref(ids), C.byref(ids_bytes), C.byref(ncls))
     check(st, f"kmp_read_fasta({path})")
     try:
         N = n.value
