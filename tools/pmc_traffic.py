@@ -39,7 +39,8 @@ def main():
         "chunk_first_kernel": "keys_level1", "bp_hist1_kernel": "keys_level1", "bp_colscan_kernel": "keys_level1",
         "bp_scatter1_kernel": "keys_level1", "bp_colsum_kernel": "keys_level1", "bp_colprefix_kernel": "keys_level1",
         "bp_hist2_kernel": "buckets_level2", "bp_scan2_kernel": "buckets_level2",
-        "bp_scatter2_kernel": "buckets_level2",
+        "bp_scatter2_kernel": "buckets_level2", "bp_scatter2c_kernel": "buckets_level2",
+        "bp_cur_clear_kernel": "buckets_level2", "step_clear_kernel": "keys_level1", "step_pack_kernel": "emit",
         "pt_hist_kernel": "pair_partition", "pt_colscan_kernel": "pair_partition",
         "pt_scatter_kernel": "pair_sort_rle", "pt_reduce_kernel": "pair_sort_rle",
         "pt_offsets_kernel": "emit", "pt_emit_kernel": "emit", "fused_pack_kernel": "emit",
