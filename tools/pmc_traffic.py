@@ -33,11 +33,12 @@ def main():
         print(f"{r['kernel'][:52]:<52} {r['grid']:>10} {r['dispatches']:>5} {r['read_bytes']/1e6:>9.1f} "
               f"{r['write_bytes']/1e6:>9.1f}")
     # per-step traffic of the residue step's stages (bench.py STAGE_NAMES["rows"]); one
-    # bp_scatter1_kernel dispatch per step
-    calls = max([r["dispatches"] for r in rows if r["kernel"] == "bp_scatter1_kernel"] or [1])
+    # level-1 scatter dispatch per step
+    calls = max([r["dispatches"] for r in rows if r["kernel"] in ("bp_scatter1_kernel", "bp_scatter1l_kernel")] or [1])
     by_kernel = {
         "chunk_first_kernel": "keys_level1", "bp_hist1_kernel": "keys_level1", "bp_colscan_kernel": "keys_level1",
-        "bp_scatter1_kernel": "keys_level1", "bp_colsum_kernel": "keys_level1", "bp_colprefix_kernel": "keys_level1",
+        "bp_scatter1_kernel": "keys_level1", "bp_scatter1l_kernel": "keys_level1", "bp_h1t_kernel": "keys_level1",
+        "bp_scatter2g_kernel": "buckets_level2", "bp_colsum_kernel": "keys_level1", "bp_colprefix_kernel": "keys_level1",
         "bp_hist2_kernel": "buckets_level2", "bp_scan2_kernel": "buckets_level2",
         "bp_scatter2_kernel": "buckets_level2", "bp_scatter2c_kernel": "buckets_level2",
         "bp_cur_clear_kernel": "buckets_level2", "step_clear_kernel": "keys_level1", "step_pack_kernel": "emit",

@@ -1706,6 +1706,175 @@ __global__ void bp_cur_clear_kernel(uint32_t* __restrict__ cur, uint32_t n) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) cur[i] = 0;
 }
 
+// ------------------------------------------------------------- local level 1 ---------------
+// With the cursor level 2 the coarse bins need not be contiguous: level 1 leaves each chunk's
+// keys in its own 4,096-key segment of ws->keys, grouped by digit1 (the chunk's runs, packed
+// start << 16 | count in H1[chunk][digit]), and a level-2 tile gathers the runs of one coarse bin
+// over a range of T chunks.  That drops bp_hist1 (every key computed a second time) and the
+// column scan, and level 1 writes whole segments.  The cursor level 2 is the only consumer; the
+// counting fallback (kFlCur) reruns with the counting level 1.
+constexpr uint32_t kBpGatherMax = 1024;  // chunks per level-2 tile (T)
+
+// level 1, local: the chunk's own-digit keys grouped by digit1 at out[chunk * kKeyChunk ...]
+__global__ __launch_bounds__(kKeyThreads) void bp_scatter1l_kernel(
+    const uint8_t* __restrict__ res, const uint64_t* __restrict__ res_off, const uint16_t* __restrict__ cls, int k,
+    uint32_t p_hi, uint64_t slots, const uint32_t* __restrict__ chunk_first, Layout lay, BpDigits dg, uint32_t pw21,
+    uint32_t dlo, uint32_t dhi, uint32_t* __restrict__ H1, unsigned long long* __restrict__ out,
+    uint32_t* __restrict__ flags) {
+    __shared__ union {
+        KeyChunk kc;
+        unsigned long long S[kKeyChunk];
+    } u;
+    __shared__ uint32_t lh[kBpMaxBins];
+    __shared__ uint32_t wave_tot[kKeyThreads / 64];
+    __shared__ uint32_t s_n;
+    const uint64_t c0 = (uint64_t)blockIdx.x * kKeyChunk, c1 = min(c0 + kKeyChunk, slots);
+    for (uint32_t d = threadIdx.x; d < dg.nb1; d += kKeyThreads) lh[d] = 0;
+    if (threadIdx.x == 0) s_n = 0;
+    const uint32_t first = chunk_first[blockIdx.x];
+    key_chunk_load(u.kc, res, res_off, cls, k, p_hi, c0, c1, first, lay, flags);
+    unsigned long long x[kBpPer];
+    uint32_t r[kBpPer], nk = 0;
+    const unsigned hs1 = dg.sh1 - lay.hshift;
+    key_chunk_run<kBpPer>(u.kc, threadIdx.x * kBpPer, (uint32_t)(c1 - c0), k, pw21, first, lay,
+                          [&](uint32_t e, bool valid, uint32_t h, unsigned long long lo) {
+                              const uint32_t d = h >> hs1;
+                              const bool mine = valid && d >= dlo && d < dhi;  // the call's coarse bins
+                              x[e] = mine ? ((unsigned long long)h << lay.hshift) | lo : kNoKey;
+                              r[e] = mine ? atomicAdd(&lh[d], 1u) : 0u;
+                              nk += mine;
+                          });
+    if (nk) atomicAdd(&s_n, nk);
+    __syncthreads();  // the chunk's staging (u.kc) is dead from here: u.S reuses it
+    uint32_t cnt[kBpQ];
+#pragma unroll
+    for (uint32_t t = 0; t < kBpQ; ++t) {
+        const uint32_t d = threadIdx.x + t * kKeyThreads;
+        cnt[t] = d < dg.nb1 ? lh[d] : 0u;
+    }
+    lds_bins_scan(lh, dg.nb1, wave_tot);
+    uint32_t* row = H1 + (uint64_t)blockIdx.x * dg.nb1;
+#pragma unroll
+    for (uint32_t t = 0; t < kBpQ; ++t) {
+        const uint32_t d = threadIdx.x + t * kKeyThreads;
+        if (d < dg.nb1) row[d] = lh[d] << 16 | cnt[t];
+    }
+#pragma unroll
+    for (uint32_t e = 0; e < kBpPer; ++e)
+        if (x[e] != kNoKey) u.S[lh[(uint32_t)(x[e] >> dg.sh1)] + r[e]] = x[e];
+    __syncthreads();
+    const uint32_t n_in = s_n;
+    unsigned long long* seg = out + c0;  // c0 = chunk * kKeyChunk: 16-byte aligned
+    for (uint32_t i = 2 * threadIdx.x; i < n_in; i += 2 * kKeyThreads) {
+        if (i + 1 < n_in)
+            *reinterpret_cast<ulonglong2*>(seg + i) = *reinterpret_cast<const ulonglong2*>(u.S + i);
+        else
+            seg[i] = u.S[i];
+    }
+}
+
+// H1[G][nb1] -> H1T[digit - dlo][G] for digits [dlo, dhi) (32 x 32 tiles through LDS)
+__global__ __launch_bounds__(256) void bp_h1t_kernel(const uint32_t* __restrict__ H1, uint32_t G, uint32_t nb1,
+                                                     uint32_t dlo, uint32_t dhi, uint32_t* __restrict__ H1T) {
+    __shared__ uint32_t tile[32][33];
+    const uint32_t g0 = blockIdx.x * 32, d0 = dlo + blockIdx.y * 32;
+    const uint32_t tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    for (uint32_t y = ty; y < 32; y += 8) {
+        const uint32_t g = g0 + y, d = d0 + tx;
+        tile[y][tx] = g < G && d < dhi ? H1[(uint64_t)g * nb1 + d] : 0u;
+    }
+    __syncthreads();
+    for (uint32_t y = ty; y < 32; y += 8) {
+        const uint32_t d = d0 + y, g = g0 + tx;
+        if (d < dhi && g < G) H1T[(uint64_t)(d - dlo) * G + g] = tile[tx][y];
+    }
+}
+
+// level 2 over the local level 1: tile (j, c) = coarse bin c's runs in chunks [j*T, j*T + T),
+// gathered and reserved in the bucket regions as bp_scatter2c.  The run table (off, src) and a
+// key -> run map live in S until the keys are in registers, so the loads go out coalesced
+// (element tid + e*kKeyThreads, as the other scatters).  A tile above kBpTile keys (a skewed
+// batch) goes in several rounds.  XCD-aware order: workgroup L runs on XCD L % 8, and XCD x
+// takes the tiles [x * per, (x + 1) * per) of the bin-major tile list, so neighbouring bins' tiles
+// of a chunk range (whose runs share the 128-B lines at their ends) run on one L2 at about the
+// same time.
+__global__ __launch_bounds__(kKeyThreads) void bp_scatter2g_kernel(const unsigned long long* __restrict__ in,
+                                                                   const uint32_t* __restrict__ H1T, uint32_t G,
+                                                                   uint32_t T, uint32_t ntiles, uint32_t nbins,
+                                                                   BpDigits dg, CurGeom cg,
+                                                                   uint32_t* __restrict__ bcur,
+                                                                   unsigned long long* __restrict__ out,
+                                                                   uint32_t* __restrict__ flags, uint32_t c0,
+                                                                   uint32_t dlo) {
+    __shared__ __attribute__((aligned(16))) unsigned long long S[kBpTile];
+    __shared__ uint32_t lh[kBpMaxBins];
+    __shared__ uint32_t wave_tot[kKeyThreads / 64];
+    // aliases in S, dead once the tile's keys are loaded: src[kBpGatherMax] (a run's segment
+    // offset minus its tile offset, mod 2^32) | map[kBpTile] (key -> run)
+    uint32_t* src = reinterpret_cast<uint32_t*>(S);
+    uint16_t* map = reinterpret_cast<uint16_t*>(src + kBpGatherMax);
+    static_assert(kBpGatherMax * 4 + kBpTile * 2 <= sizeof(S), "gather tables fit in S");
+    constexpr uint32_t kQ = kBpGatherMax / kKeyThreads;
+    const uint32_t total = ntiles * nbins, per = (total + 7) / 8;
+    const uint32_t w = (blockIdx.x % 8) * per + blockIdx.x / 8;
+    if (w >= total) return;
+    const uint32_t c = c0 + w / ntiles, ch0 = (w % ntiles) * T;
+    if (ch0 >= G) return;
+    const uint32_t nch = min(T, G - ch0);
+    const uint32_t* row = H1T + (uint64_t)(c - dlo) * G + ch0;
+    const uint32_t q = (nch + kKeyThreads - 1) / kKeyThreads, b0 = threadIdx.x * q;
+    uint32_t p[kQ], v = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < kQ; ++t) {
+        p[t] = t < q && b0 + t < nch ? row[b0 + t] : 0u;
+        v += p[t] & 0xFFFFu;
+    }
+    uint32_t excl0, tn;
+    block_scan_n<kKeyThreads>(v, excl0, tn, wave_tot);
+    auto digit = [&](unsigned long long y) { return (uint32_t)(y >> dg.sh2) & dg.m2; };
+    const uint32_t bb = c * dg.nb2;
+    for (uint32_t base = 0; base < tn; base += kBpTile) {
+        if (base) __syncthreads();  // the previous round's writes have read lh and S
+        const uint32_t n_in = min(kBpTile, tn - base);
+        for (uint32_t d = threadIdx.x; d < dg.nb2; d += kKeyThreads) lh[d] = 0;
+        uint32_t excl = excl0;
+#pragma unroll
+        for (uint32_t t = 0; t < kQ; ++t)
+            if (t < q && b0 + t < nch) {
+                src[b0 + t] = (ch0 + b0 + t) * kKeyChunk + (p[t] >> 16) - excl;
+                excl += p[t] & 0xFFFFu;
+            }
+        // key -> run map of the round's window [base, base + n_in)
+        excl = excl0;
+#pragma unroll
+        for (uint32_t t = 0; t < kQ; ++t)
+            if (t < q && b0 + t < nch) {
+                const uint32_t e1 = excl + (p[t] & 0xFFFFu);
+                const uint32_t lo = max(excl, base), hi = min(e1, base + n_in);
+                for (uint32_t i = lo; i < hi; ++i) map[i - base] = (uint16_t)(b0 + t);
+                excl = e1;
+            }
+        __syncthreads();
+        unsigned long long x[kBpPer];
+        uint32_t r[kBpPer];
+#pragma unroll
+        for (uint32_t e = 0; e < kBpPer; ++e) {
+            const uint32_t i = threadIdx.x + e * kKeyThreads;
+            if (i < n_in) {
+                x[e] = in[src[map[i]] + base + i];
+            } else {
+                x[e] = kNoKey;
+            }
+        }
+#pragma unroll
+        for (uint32_t e = 0; e < kBpPer; ++e) r[e] = x[e] != kNoKey ? atomicAdd(&lh[digit(x[e])], 1u) : 0u;
+        __syncthreads();  // every key loaded: S is free for the placement
+        bp_place_cur(
+            x, r, n_in, dg.nb2, digit, [&](uint32_t d) { return &bcur[bb + d]; },
+            [&](uint32_t d) { return (bb + d) * cg.capb; }, cg.capb, lh, wave_tot, S, out, flags);
+    }
+}
+
 // the small bucket kernel for this layout: merged slot words when the bucket field is wide enough;
 // a 1,024-key capacity (four keys per thread) when the mean bucket is small enough that a bucket
 // above it is a > 4-sigma event (the large kernel takes those)
@@ -1802,6 +1971,9 @@ struct kmp_postings {
     uint32_t bp_J_min = 0;      // ... at least (learned from an overflowing bin)
     uint64_t bp_c1 = 0;         // offset of C1 (coarse bin starts) in ws->bp
     bool parted = false;        // ws->keys holds level-1 output (bp_level1 ran for this call)
+    bool bp_local = false;      // ... in chunk segments (local level 1: H1T at bp + bp_h1t)
+    uint32_t bp_G = 0, bp_T = 0;
+    uint64_t bp_h1t = 0;
     // coarse bins [bin_lo, bin_hi) of this call (bin_hi 0: all): the bucket-range share of a rank
     // of the multi-GPU k-mer split (kmp_dev_split_expand); level 1 keeps only their keys
     uint32_t bin_lo = 0, bin_hi = 0;
@@ -1911,6 +2083,20 @@ hipError_t bp_level1(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_r
     ws->bp_c1 = 2 * h1 + r;
     chunk_first_kernel<<<(n + 1 + 255) / 256, 256, 0, st>>>(d_res_off, 0u, n, 0ull, slots, G, ws->chunk_first.p);
     const uint32_t pw21 = (uint32_t)pow21(k - 1);
+    ws->bp_local = ws->cur_used;
+    if (ws->bp_local) {  // local level 1 for the cursor level 2: H1 | H1T (own digits)
+        ws->bp_G = G;
+        ws->bp_h1t = h1;
+        // T chunks per level-2 tile: ~3/4 of a tile at the hash-uniform mean (kKeyChunk / nb1 keys
+        // per chunk and bin)
+        ws->bp_T = std::min<uint32_t>(kBpGatherMax, std::max<uint32_t>(1, kBpTile * 3 / 4 * dg.nb1 / kKeyChunk));
+        bp_scatter1l_kernel<<<G, kKeyThreads, 0, st>>>(d_res, d_res_off, d_class, k, n, slots, ws->chunk_first.p, lay,
+                                                        dg, pw21, dlo, dhi, H1, ws->keys.p, ws->flags.p);
+        if (dhi > dlo)
+            bp_h1t_kernel<<<dim3((G + 31) / 32, (dhi - dlo + 31) / 32), 256, 0, st>>>(H1, G, dg.nb1, dlo, dhi,
+                                                                                     H1 + h1);
+        return hipGetLastError();
+    }
     bp_hist1_kernel<<<G, kKeyThreads, 0, st>>>(d_res, d_res_off, d_class, k, n, slots, ws->chunk_first.p, lay, dg,
                                                 pw21, dlo, dhi, H1, ws->flags.p);
     bp_colsum_kernel<<<dim3(groups, (dg.nb1 + 255) / 256), 256, 0, st>>>(H1, G, dg.nb1, R);
@@ -1960,7 +2146,12 @@ int bp_level2c(kmp_postings* ws, const Layout& lay, hipStream_t st) {
     uint32_t c0, c1;
     own_bins(ws, dg, &c0, &c1);
     bp_cur_clear_kernel<<<std::min<uint32_t>((nb + 1023) / 1024, 1024), 1024, 0, st>>>(ws->cur.p, nb);
-    if (c1 > c0)
+    if (c1 > c0 && ws->bp_local) {
+        const uint32_t ntiles = (ws->bp_G + ws->bp_T - 1) / ws->bp_T, per = (ntiles * (c1 - c0) + 7) / 8;
+        bp_scatter2g_kernel<<<8 * per, kKeyThreads, 0, st>>>(ws->keys.p, ws->bp.p + ws->bp_h1t, ws->bp_G, ws->bp_T,
+                                                             ntiles, c1 - c0, dg, ws->cg, ws->cur.p, ws->sorted.p,
+                                                             ws->flags.p, c0, c0);
+    } else if (c1 > c0)
         bp_scatter2c_kernel<<<dim3(ws->bp_J, c1 - c0), kKeyThreads, 0, st>>>(ws->keys.p, C1, ws->bp_J, dg, ws->cg,
                                                                             ws->cur.p, ws->sorted.p, ws->flags.p, c0);
     PG(hipGetLastError());
