@@ -964,18 +964,6 @@ __global__ __launch_bounds__(kThreads) void bucket_large_kernel(BucketArgs a) {
         process_bucket<kCap, kThreads, kTabBits, false, kRows>(a.list[i], a, false);
 }
 
-// shard regions -> one contiguous array (shard order)
-__global__ void gather_shards_kernel(const unsigned long long* __restrict__ src, uint64_t shard_cap,
-                                     const unsigned long long* __restrict__ cursor,
-                                     unsigned long long* __restrict__ dst) {
-    const int s = blockIdx.y;
-    unsigned long long off = 0;
-    for (int t = 0; t < s; ++t) off += cursor[t];
-    const unsigned long long m = cursor[s];
-    for (unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; i < m;
-         i += (unsigned long long)gridDim.x * blockDim.x)
-        dst[off + i] = src[(uint64_t)s * shard_cap + i];
-}
 
 // ------------------------------------------------------------- heavy path ------------------
 // Frequent k-mers (a group above kHeavySub keys) and buckets above every LDS capacity are
@@ -993,75 +981,153 @@ __global__ void gather_shards_kernel(const unsigned long long* __restrict__ src,
 //      cursor reservation place the pair keys p_i * mul + p_j in the shard regions the bucket
 //      kernels fill.  A k-mer of df 10^4 is ~400 tiles: no workgroup walks a long posting list.
 constexpr uint32_t kHvTile = 4096, kHvThreads = 256, kHvPer = kHvTile / kHvThreads;
-constexpr uint32_t kHvI = 256, kHvJ = 2048;
+constexpr uint32_t kHvI = 256, kHvJ = 2048, kHvJWrite = 256;
 
-// per tile: distinct (h, p) elements and k-mer heads -> cnt[2 * t], cnt[2 * t + 1]
+// Heavy key order.  Plain: the spilled keys [h | p | class] sorted on (h, p).  Class order (the
+// class test is on): gather_shards rewrites them to [h | class | p] and the sort is on every bit,
+// so each k-mer's elements come in class runs, proteins ascending inside a run.  A pair of
+// different classes is then (row i, partner j) with j past the end of i's run: the expansion
+// walks only those — at k = 5 on uniprot_arg 98% of a frequent k-mer's pairs share a class and
+// were enumerated and tested one by one in the plain order.
+struct HeavyOrder {
+    unsigned cb, hshift, pbits;  // class bits, h shift, protein bits (hshift - cb)
+    int cls;                     // class order
+    uint32_t hj;                 // partners per tile (<= kHvJ)
+    // element-distinct test shift: plain keys drop the class (a function of p), class-ordered keys
+    // compare whole
+    __host__ __device__ unsigned eshift() const { return cls ? 0u : cb; }
+    // E value (p << cb | class) of a sorted key
+    __device__ uint32_t elem(unsigned long long v) const {
+        const unsigned long long lmask = (1ull << hshift) - 1;
+        if (!cls) return (uint32_t)(v & lmask);
+        const uint32_t pm = (uint32_t)((1ull << pbits) - 1), cm = (1u << cb) - 1;
+        return ((uint32_t)v & pm) << cb | ((uint32_t)(v >> pbits) & cm);
+    }
+};
+
+// spill shard regions -> one contiguous array (shard order); class order: keys rewritten to
+// [h | class | p]
+__global__ void gather_shards_kernel(const unsigned long long* __restrict__ src, uint64_t shard_cap,
+                                     const unsigned long long* __restrict__ cursor, HeavyOrder ho,
+                                     unsigned long long* __restrict__ dst) {
+    const int s = blockIdx.y;
+    unsigned long long off = 0;
+    for (int t = 0; t < s; ++t) off += cursor[t];
+    const unsigned long long m = cursor[s];
+    const unsigned long long cm = (1ull << ho.cb) - 1, hm = ~((1ull << ho.hshift) - 1);
+    for (unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; i < m;
+         i += (unsigned long long)gridDim.x * blockDim.x) {
+        const unsigned long long v = src[(uint64_t)s * shard_cap + i];
+        dst[off + i] = ho.cls ? (v & hm) | (v & cm) << ho.pbits | ((v & ~hm) >> ho.cb) : v;
+    }
+}
+
+// per tile: distinct (h, p) elements, k-mer heads and (class order) class-run heads
 __global__ __launch_bounds__(kHvThreads) void heavy_scan_kernel(const unsigned long long* __restrict__ x, uint64_t m,
-                                                                unsigned cb, unsigned hshift,
-                                                                uint32_t* __restrict__ ecnt,
-                                                                uint32_t* __restrict__ gcnt) {
-    __shared__ uint32_t s_e, s_g;
-    if (threadIdx.x == 0) s_e = s_g = 0;
+                                                                HeavyOrder ho, uint32_t* __restrict__ ecnt,
+                                                                uint32_t* __restrict__ gcnt,
+                                                                uint32_t* __restrict__ rcnt) {
+    __shared__ uint32_t s_e, s_g, s_r;
+    if (threadIdx.x == 0) s_e = s_g = s_r = 0;
     __syncthreads();
     const uint64_t t0 = (uint64_t)blockIdx.x * kHvTile;
-    uint32_t ne = 0, ng = 0;
+    const unsigned es = ho.eshift();
+    uint32_t ne = 0, ng = 0, nr = 0;
     for (uint32_t r = 0; r < kHvPer; ++r) {
         const uint64_t i = t0 + r * kHvThreads + threadIdx.x;
         if (i >= m) break;
         const unsigned long long v = x[i], u = i ? x[i - 1] : ~0ull;
-        ne += (v >> cb) != (u >> cb);
-        ng += (v >> hshift) != (u >> hshift);
+        ne += (v >> es) != (u >> es);
+        ng += (v >> ho.hshift) != (u >> ho.hshift);
+        nr += (v >> ho.pbits) != (u >> ho.pbits);
     }
     if (ne) atomicAdd(&s_e, ne);
     if (ng) atomicAdd(&s_g, ng);
+    if (nr && ho.cls) atomicAdd(&s_r, nr);
     __syncthreads();
     if (threadIdx.x == 0) {
         ecnt[blockIdx.x] = s_e;
         gcnt[blockIdx.x] = s_g;
+        if (ho.cls) rcnt[blockIdx.x] = s_r;
     }
 }
 
-// per tile: the elements at eoff[t] + their rank, the k-mer starts at goff[t] + rank
+// per tile: the elements at eoff[t] + their rank, the k-mer starts at goff[t] + rank; class order:
+// the class-run starts at roff[t] + rank (RH) and every element's run (RUN)
 __global__ __launch_bounds__(kHvThreads) void heavy_compact_kernel(const unsigned long long* __restrict__ x,
-                                                                   uint64_t m, unsigned cb, unsigned hshift,
+                                                                   uint64_t m, HeavyOrder ho,
                                                                    const uint64_t* __restrict__ eoff,
                                                                    const uint64_t* __restrict__ goff,
+                                                                   const uint64_t* __restrict__ roff,
                                                                    uint32_t* __restrict__ E,
-                                                                   uint64_t* __restrict__ GS) {
+                                                                   uint64_t* __restrict__ GS,
+                                                                   uint32_t* __restrict__ RUN,
+                                                                   uint64_t* __restrict__ RH) {
     __shared__ uint32_t wave_tot[kHvThreads / 64];
     const uint64_t t0 = (uint64_t)blockIdx.x * kHvTile;
-    uint64_t eb = eoff[blockIdx.x], gb = goff[blockIdx.x];
-    const unsigned long long lmask = (1ull << hshift) - 1;
+    uint64_t eb = eoff[blockIdx.x], gb = goff[blockIdx.x], rb = ho.cls ? roff[blockIdx.x] : 0;
+    const unsigned es = ho.eshift();
     for (uint32_t r = 0; r < kHvPer; ++r) {
         const uint64_t i = t0 + r * kHvThreads + threadIdx.x;
-        bool ke = false, kg = false;
+        bool ke = false, kg = false, kr = false;
         unsigned long long v = 0;
         if (i < m) {
             v = x[i];
             const unsigned long long u = i ? x[i - 1] : ~0ull;
-            ke = (v >> cb) != (u >> cb);
-            kg = (v >> hshift) != (u >> hshift);
+            ke = (v >> es) != (u >> es);
+            kg = (v >> ho.hshift) != (u >> ho.hshift);
+            kr = (v >> ho.pbits) != (u >> ho.pbits);
         }
         uint32_t xe, te, xg, tg;
         block_scan_n<kHvThreads>(ke, xe, te, wave_tot);
         block_scan_n<kHvThreads>(kg, xg, tg, wave_tot);
-        if (ke) E[eb + xe] = (uint32_t)(v & lmask);
+        if (ke) E[eb + xe] = ho.elem(v);
         if (kg) GS[gb + xg] = eb + xe;  // a k-mer head is always a new element
+        if (ho.cls) {
+            uint32_t xr, tr;
+            block_scan_n<kHvThreads>(kr, xr, tr, wave_tot);
+            if (kr) RH[rb + xr] = eb + xe;  // a run head too
+            if (ke) RUN[eb + xe] = (uint32_t)(rb + xr + kr - 1);
+            rb += tr;
+        }
         eb += te;
         gb += tg;
     }
 }
 
-// per k-mer: statistics (stats != 0), rows [i0, i1) of the call, tile count
+// Row blocks of kHvI elements: k-mer g's blocks are entries [bbase(g), bbase(g) + nblk) of the
+// block tables (GS[g] / kHvI + g: disjoint for consecutive k-mers), BT = the k-mer's tiles before
+// the block, BP = the block's partner start (its first row's).
+__device__ __forceinline__ uint64_t heavy_bbase(uint64_t gs, uint64_t g) { return gs / kHvI + g; }
+
+// a row's partner start (local index): past its class run (class order) or past itself
+__device__ __forceinline__ uint32_t heavy_pstart(uint32_t i, uint64_t b, const HeavyOrder& ho,
+                                                 const uint32_t* __restrict__ RUN,
+                                                 const uint64_t* __restrict__ RH) {
+    return ho.cls ? (uint32_t)(RH[RUN[b + i] + 1] - b) : i + 1;
+}
+
+// per k-mer: statistics (stats != 0), rows [i0, i1) of the call, the block tables and the tile
+// count.  Plain order: the rows whose protein lies in [row_lo, row_hi) (a contiguous range);
+// class order: every element (a ranged call tests each pair's smaller protein instead).
 __global__ __launch_bounds__(256) void heavy_plan_kernel(const uint32_t* __restrict__ E,
-                                                         const uint64_t* __restrict__ GS, uint64_t ng,
-                                                         unsigned cb, uint32_t row_lo, uint32_t row_hi,
-                                                         uint32_t heavy_df, int stats,
+                                                         const uint64_t* __restrict__ GS, uint64_t ngb,
+                                                         const unsigned long long* __restrict__ ng_dev,
+                                                         HeavyOrder ho, const uint32_t* __restrict__ RUN,
+                                                         const uint64_t* __restrict__ RH, uint32_t row_lo,
+                                                         uint32_t row_hi, uint32_t heavy_df, int stats,
                                                          unsigned long long* __restrict__ gstats,
-                                                         uint32_t* __restrict__ gi,
+                                                         uint32_t* __restrict__ gi, uint32_t* __restrict__ BT,
+                                                         uint32_t* __restrict__ BP,
                                                          unsigned long long* __restrict__ tcount) {
     const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const uint64_t ng = *ng_dev;  // k-mers; threads up to the bound ngb write empty plans
+    const unsigned cb = ho.cb;
     unsigned long long st[kStN] = {0, 0, 0, 0, 0, 0, 0};
+    if (g >= ng && g < ngb) {
+        gi[2 * g] = gi[2 * g + 1] = 0;
+        tcount[g] = 0;
+    }
     if (g < ng) {
         const uint64_t b = GS[g];
         const uint32_t d = (uint32_t)(GS[g + 1] - b);
@@ -1077,9 +1143,15 @@ __global__ __launch_bounds__(256) void heavy_plan_kernel(const uint32_t* __restr
         uint32_t i0 = 0, i1 = 0;
         unsigned long long tiles = 0;
         if (d >= 2 && d <= heavy_df) {
-            i0 = lower(row_lo);
-            i1 = lower(row_hi);
-            for (uint32_t r = i0; r < i1; r += kHvI) tiles += (d - (r + 1) + kHvJ - 1) / kHvJ;
+            i0 = ho.cls ? 0u : lower(row_lo);
+            i1 = ho.cls ? d : lower(row_hi);
+            const uint64_t bb = heavy_bbase(b, g);
+            for (uint32_t r = i0, k = 0; r < i1; r += kHvI, ++k) {
+                const uint32_t ps = heavy_pstart(r, b, ho, RUN, RH);
+                BT[bb + k] = (uint32_t)tiles;
+                BP[bb + k] = ps;
+                tiles += ps < d ? (d - ps + ho.hj - 1) / ho.hj : 0u;
+            }
         }
         gi[2 * g] = i0;
         gi[2 * g + 1] = i1;
@@ -1110,21 +1182,33 @@ __global__ __launch_bounds__(256) void heavy_plan_kernel(const uint32_t* __restr
     }
 }
 
-// one workgroup per tile (grid-stride): rows i of block r of k-mer g against partner chunk c
+// one workgroup per tile (grid-stride): rows i of block k of k-mer g against partner chunk
+// [j0, j0 + kHvJ).  Plain order: partners j > i, the class test per pair when require_diff.
+// Class order: partners past i's class run (every one of another class); a ranged call keeps the
+// pairs whose smaller protein lies in [row_lo, row_hi).  Keys min(p) * mul + max(p).
 __global__ __launch_bounds__(kHvI) void heavy_expand_kernel(const uint32_t* __restrict__ E,
                                                             const uint64_t* __restrict__ GS,
                                                             const uint32_t* __restrict__ gi,
-                                                            const unsigned long long* __restrict__ toff, uint64_t ng,
-                                                            const unsigned long long* __restrict__ ntiles,
-                                                            unsigned cb, uint32_t mul, int require_diff,
+                                                            const uint32_t* __restrict__ BT,
+                                                            const uint32_t* __restrict__ BP,
+                                                            const uint32_t* __restrict__ RUN,
+                                                            const uint64_t* __restrict__ RH,
+                                                            const unsigned long long* __restrict__ toff,
+                                                            const unsigned long long* __restrict__ ng_dev,
+                                                            HeavyOrder ho, uint32_t mul, int require_diff, int ranged,
+                                                            uint32_t row_lo, uint32_t row_hi,
                                                             unsigned long long* __restrict__ out, uint64_t shard_cap,
                                                             unsigned long long* __restrict__ cursor,
                                                             unsigned long long* __restrict__ gstats) {
     __shared__ uint32_t J[kHvJ];
+    __shared__ uint32_t s_ex[kHvI + 1], s_js[kHvI], s_p[kHvI];
     __shared__ uint32_t wave_tot[kHvI / 64];
     __shared__ unsigned long long sbase;
-    const unsigned long long T = *ntiles;
+    const uint64_t ng = *ng_dev;
+    const unsigned long long T = toff[ng];
+    const unsigned cb = ho.cb;
     const uint32_t cmask = (1u << cb) - 1;
+    const bool test_cls = require_diff && !ho.cls, test_row = ho.cls && ranged;
     for (unsigned long long t = blockIdx.x; t < T; t += gridDim.x) {
         // k-mer g: the last with toff[g] <= t
         uint64_t lo = 0, hi = ng;
@@ -1135,28 +1219,38 @@ __global__ __launch_bounds__(kHvI) void heavy_expand_kernel(const uint32_t* __re
         }
         const uint64_t g = lo, b = GS[g];
         const uint32_t d = (uint32_t)(GS[g + 1] - b), i0 = gi[2 * g], i1 = gi[2 * g + 1];
-        unsigned long long local = t - toff[g];
-        uint32_t r = i0;  // row block start
-        while (r < i1) {
-            const unsigned long long c = (d - (r + 1) + kHvJ - 1) / kHvJ;
-            if (local < c) break;
-            local -= c;
-            r += kHvI;
+        const uint32_t local = (uint32_t)(t - toff[g]);
+        // row block: the last with BT <= local (blocks without tiles share the next one's BT)
+        const uint64_t bb = heavy_bbase(b, g);
+        uint32_t klo = 0, khi = (i1 - i0 + kHvI - 1) / kHvI;
+        while (klo + 1 < khi) {
+            const uint32_t mid = (klo + khi) >> 1;
+            if (BT[bb + mid] <= local) klo = mid;
+            else khi = mid;
         }
-        if (r >= i1) continue;  // not reached with a consistent plan (uniform across the workgroup)
-        const uint32_t j0 = r + 1 + (uint32_t)local * kHvJ, j1 = min(d, j0 + kHvJ);
+        const uint32_t r = i0 + klo * kHvI;
+        const uint32_t j0 = BP[bb + klo] + (local - BT[bb + klo]) * ho.hj, j1 = min(d, j0 + ho.hj);
         __syncthreads();  // J reuse
         for (uint32_t j = j0 + threadIdx.x; j < j1; j += kHvI) J[j - j0] = E[b + j];
         const uint32_t i = r + threadIdx.x;
         const bool row = i < i1;
         const uint32_t xi = row ? E[b + i] : 0u;
+        const uint32_t js = row ? max(heavy_pstart(i, b, ho, RUN, RH), j0) : j1;
+        const uint32_t pi = xi >> cb;
         __syncthreads();
+        auto keep = [&](uint32_t xj) {
+            if (test_cls) return ((xj ^ xi) & cmask) != 0u;
+            if (test_row) {
+                const uint32_t pm = min(pi, xj >> cb);
+                return pm >= row_lo && pm < row_hi;
+            }
+            return true;
+        };
         uint32_t c = 0;
-        const uint32_t js = row ? max(i + 1, j0) : j1;
-        if (require_diff) {
-            for (uint32_t j = js; j < j1; ++j) c += ((J[j - j0] ^ xi) & cmask) != 0u;
+        if (test_cls || test_row) {
+            for (uint32_t j = js; j < j1; ++j) c += keep(J[j - j0]);
         } else {
-            c = j1 - js;
+            c = js < j1 ? j1 - js : 0u;
         }
         uint32_t excl, total;
         block_scan_n<kHvI>(c, excl, total, wave_tot);
@@ -1166,15 +1260,40 @@ __global__ __launch_bounds__(kHvI) void heavy_expand_kernel(const uint32_t* __re
             if (total) atomicAdd(&gstats[(uint64_t)shard * 8 + kStInc], (unsigned long long)total);
         }
         __syncthreads();
-        if (c) {
-            unsigned long long pos = sbase + excl;
-            unsigned long long* dst = out + (uint64_t)shard * shard_cap;
-            const unsigned long long rowkey = (unsigned long long)(xi >> cb) * mul;
-            for (uint32_t j = js; j < j1; ++j) {
-                const uint32_t xj = J[j - j0];
-                if (require_diff && !((xj ^ xi) & cmask)) continue;
-                if (pos < shard_cap) dst[pos] = rowkey + (xj >> cb);
-                ++pos;
+        unsigned long long* dst = out + (uint64_t)shard * shard_cap;
+        if (test_cls || test_row) {  // a filtered row: its kept partners in turn
+            if (c) {
+                unsigned long long pos = sbase + excl;
+                for (uint32_t j = js; j < j1; ++j) {
+                    const uint32_t xj = J[j - j0];
+                    if (!keep(xj)) continue;
+                    const uint32_t pj = xj >> cb;
+                    if (pos < shard_cap) dst[pos] = (unsigned long long)min(pi, pj) * mul + max(pi, pj);
+                    ++pos;
+                }
+            }
+        } else {
+            // every partner kept: the tile's output [0, total) in coalesced order, output o of row
+            // i (the last with s_ex[i] <= o) = partner js_i + o - s_ex[i]; a thread's rows only move
+            // forward as o grows
+            s_ex[threadIdx.x] = excl;
+            s_js[threadIdx.x] = js;
+            s_p[threadIdx.x] = pi;
+            if (threadIdx.x == 0) s_ex[kHvI] = total;
+            __syncthreads();
+            uint32_t i = 0, hi = kHvI;
+            if (threadIdx.x < total) {
+                while (i + 1 < hi) {
+                    const uint32_t mid = (i + hi) >> 1;
+                    if (s_ex[mid] <= threadIdx.x) i = mid;
+                    else hi = mid;
+                }
+            }
+            for (uint32_t o = threadIdx.x; o < total; o += kHvI) {
+                while (s_ex[i + 1] <= o) ++i;
+                const uint32_t pa = s_p[i], pj = J[s_js[i] + (o - s_ex[i]) - j0] >> cb;
+                const unsigned long long pos = sbase + o;
+                if (pos < shard_cap) dst[pos] = (unsigned long long)min(pa, pj) * mul + max(pa, pj);
             }
         }
     }
@@ -1599,8 +1718,8 @@ struct CurGeom {
 // lh holds the tile's digit histogram and r[e] every key's rank in its digit: reserve each digit's
 // run on cursor(d) (start of its region: region(d), cap keys), place the tile digit-major into S
 // and write each run at its reservation; keys past their region's end are dropped (kFlCur)
-template <class Digit, class Cursor, class Region>
-__device__ __forceinline__ void bp_place_cur(const unsigned long long (&x)[kBpPer], const uint32_t (&r)[kBpPer],
+template <uint32_t kPer, class Digit, class Cursor, class Region>
+__device__ __forceinline__ void bp_place_cur(const unsigned long long (&x)[kPer], const uint32_t (&r)[kPer],
                                              uint32_t n_in, uint32_t nb, Digit digit, Cursor cursor, Region region,
                                              uint32_t cap, uint32_t* lh, uint32_t* wave_tot, unsigned long long* S,
                                              unsigned long long* __restrict__ out, uint32_t* __restrict__ flags) {
@@ -1623,7 +1742,7 @@ __device__ __forceinline__ void bp_place_cur(const unsigned long long (&x)[kBpPe
         }
     __syncthreads();
 #pragma unroll
-    for (uint32_t e = 0; e < kBpPer; ++e)
+    for (uint32_t e = 0; e < kPer; ++e)
         if (x[e] != kNoKey) S[lh[digit(x[e])] + r[e]] = x[e];
     __syncthreads();
     // lh[d] -> global start of the digit's run minus its tile start; a run that does not fit
@@ -1714,6 +1833,7 @@ __global__ void bp_cur_clear_kernel(uint32_t* __restrict__ cur, uint32_t n) {
 // column scan, and level 1 writes whole segments.  The cursor level 2 is the only consumer; the
 // counting fallback (kFlCur) reruns with the counting level 1.
 constexpr uint32_t kBpGatherMax = 1024;  // chunks per level-2 tile (T)
+constexpr uint32_t kBpGatherTile = 4096;  // keys per round of a level-2 tile
 
 // level 1, local: the chunk's own-digit keys grouped by digit1 at out[chunk * kKeyChunk ...]
 __global__ __launch_bounds__(kKeyThreads) void bp_scatter1l_kernel(
@@ -1798,6 +1918,7 @@ __global__ __launch_bounds__(256) void bp_h1t_kernel(const uint32_t* __restrict_
 // takes the tiles [x * per, (x + 1) * per) of the bin-major tile list, so neighbouring bins' tiles
 // of a chunk range (whose runs share the 128-B lines at their ends) run on one L2 at about the
 // same time.
+template <uint32_t kPer>
 __global__ __launch_bounds__(kKeyThreads) void bp_scatter2g_kernel(const unsigned long long* __restrict__ in,
                                                                    const uint32_t* __restrict__ H1T, uint32_t G,
                                                                    uint32_t T, uint32_t ntiles, uint32_t nbins,
@@ -1806,14 +1927,15 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scatter2g_kernel(const unsigne
                                                                    unsigned long long* __restrict__ out,
                                                                    uint32_t* __restrict__ flags, uint32_t c0,
                                                                    uint32_t dlo) {
-    __shared__ __attribute__((aligned(16))) unsigned long long S[kBpTile];
+    constexpr uint32_t kTile = kPer * kKeyThreads;
+    __shared__ __attribute__((aligned(16))) unsigned long long S[kTile];
     __shared__ uint32_t lh[kBpMaxBins];
     __shared__ uint32_t wave_tot[kKeyThreads / 64];
     // aliases in S, dead once the tile's keys are loaded: src[kBpGatherMax] (a run's segment
     // offset minus its tile offset, mod 2^32) | map[kBpTile] (key -> run)
     uint32_t* src = reinterpret_cast<uint32_t*>(S);
     uint16_t* map = reinterpret_cast<uint16_t*>(src + kBpGatherMax);
-    static_assert(kBpGatherMax * 4 + kBpTile * 2 <= sizeof(S), "gather tables fit in S");
+    static_assert(kBpGatherMax * 4 + kTile * 2 <= sizeof(S), "gather tables fit in S");
     constexpr uint32_t kQ = kBpGatherMax / kKeyThreads;
     const uint32_t total = ntiles * nbins, per = (total + 7) / 8;
     const uint32_t w = (blockIdx.x % 8) * per + blockIdx.x / 8;
@@ -1833,9 +1955,9 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scatter2g_kernel(const unsigne
     block_scan_n<kKeyThreads>(v, excl0, tn, wave_tot);
     auto digit = [&](unsigned long long y) { return (uint32_t)(y >> dg.sh2) & dg.m2; };
     const uint32_t bb = c * dg.nb2;
-    for (uint32_t base = 0; base < tn; base += kBpTile) {
+    for (uint32_t base = 0; base < tn; base += kTile) {
         if (base) __syncthreads();  // the previous round's writes have read lh and S
-        const uint32_t n_in = min(kBpTile, tn - base);
+        const uint32_t n_in = min(kTile, tn - base);
         for (uint32_t d = threadIdx.x; d < dg.nb2; d += kKeyThreads) lh[d] = 0;
         uint32_t excl = excl0;
 #pragma unroll
@@ -1855,10 +1977,10 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scatter2g_kernel(const unsigne
                 excl = e1;
             }
         __syncthreads();
-        unsigned long long x[kBpPer];
-        uint32_t r[kBpPer];
+        unsigned long long x[kPer];
+        uint32_t r[kPer];
 #pragma unroll
-        for (uint32_t e = 0; e < kBpPer; ++e) {
+        for (uint32_t e = 0; e < kPer; ++e) {
             const uint32_t i = threadIdx.x + e * kKeyThreads;
             if (i < n_in) {
                 x[e] = in[src[map[i]] + base + i];
@@ -1867,7 +1989,7 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scatter2g_kernel(const unsigne
             }
         }
 #pragma unroll
-        for (uint32_t e = 0; e < kBpPer; ++e) r[e] = x[e] != kNoKey ? atomicAdd(&lh[digit(x[e])], 1u) : 0u;
+        for (uint32_t e = 0; e < kPer; ++e) r[e] = x[e] != kNoKey ? atomicAdd(&lh[digit(x[e])], 1u) : 0u;
         __syncthreads();  // every key loaded: S is free for the placement
         bp_place_cur(
             x, r, n_in, dg.nb2, digit, [&](uint32_t d) { return &bcur[bb + d]; },
@@ -1985,12 +2107,14 @@ struct kmp_postings {
     CurGeom cg{};
     // heavy path (frequent k-mers): spill regions, the gathered + sorted spill, its elements,
     // k-mer starts, per-k-mer row bounds / tile counts / tile offsets
-    Grow<unsigned long long> spill, hkeys, hsorted, hGS, htc, htoff, hoff;
-    Grow<uint32_t> hE, hgi, hcnt;
+    Grow<unsigned long long> spill, hkeys, hsorted, hGS, htc, htoff, hoff, hRH;
+    Grow<uint32_t> hE, hgi, hcnt, hrun, hblk;
     uint64_t spill_cap = 0;     // keys per spill shard region
     bool heavy = false;         // this workspace's batches spill: run the split step
     bool heavy_ready = false;   // hE / hGS hold the current front's compacted spill
-    uint64_t h_ne = 0, h_ng = 0;
+    uint64_t h_m = 0;                // spill keys behind hE (the bound on elements and k-mers)
+    int h_cls = 0;                   // hE in class order
+    unsigned long long* h_tot = nullptr;  // device: elements, k-mers, class runs
     std::vector<unsigned long long> shape;  // (n, slots, code bits, bucket bits) of the last batch
     // front reuse (kmp_postings_set_reuse): a call on the same batch (front_key) keeps the keys,
     // level 2 and the heavy compaction of the last successful call and runs only the buckets,
@@ -2019,9 +2143,9 @@ struct kmp_postings {
     hipEvent_t ev[KMP_POSTINGS_STAGES + 1] = {};
     ~kmp_postings() {
         for (auto* g : {&keys, &sorted, &inc, &inc_sorted, &uniq, &bstats, &btot, &boff, &spill, &hkeys, &hsorted,
-                        &hGS, &htc, &htoff, &hoff, &ovk, &ovx, &split_cur})
+                        &hGS, &htc, &htoff, &hoff, &hRH, &ovk, &ovx, &split_cur})
             g->release();
-        for (auto* g : {&w, &keep, &pos, &small, &cnt, &flags, &chunk_first, &bp, &pt, &ovf, &ovr, &hE, &hgi, &hcnt, &cur})
+        for (auto* g : {&w, &keep, &pos, &small, &cnt, &flags, &chunk_first, &bp, &pt, &ovf, &ovr, &hE, &hgi, &hcnt, &hrun, &hblk, &cur})
             g->release();
         tmp.release();
         for (auto& e : ev)
@@ -2089,7 +2213,7 @@ hipError_t bp_level1(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_r
         ws->bp_h1t = h1;
         // T chunks per level-2 tile: ~3/4 of a tile at the hash-uniform mean (kKeyChunk / nb1 keys
         // per chunk and bin)
-        ws->bp_T = std::min<uint32_t>(kBpGatherMax, std::max<uint32_t>(1, kBpTile * 3 / 4 * dg.nb1 / kKeyChunk));
+        ws->bp_T = std::min<uint32_t>(kBpGatherMax, std::max<uint32_t>(1, kBpGatherTile * 3 / 4 * dg.nb1 / kKeyChunk));
         bp_scatter1l_kernel<<<G, kKeyThreads, 0, st>>>(d_res, d_res_off, d_class, k, n, slots, ws->chunk_first.p, lay,
                                                         dg, pw21, dlo, dhi, H1, ws->keys.p, ws->flags.p);
         if (dhi > dlo)
@@ -2148,7 +2272,7 @@ int bp_level2c(kmp_postings* ws, const Layout& lay, hipStream_t st) {
     bp_cur_clear_kernel<<<std::min<uint32_t>((nb + 1023) / 1024, 1024), 1024, 0, st>>>(ws->cur.p, nb);
     if (c1 > c0 && ws->bp_local) {
         const uint32_t ntiles = (ws->bp_G + ws->bp_T - 1) / ws->bp_T, per = (ntiles * (c1 - c0) + 7) / 8;
-        bp_scatter2g_kernel<<<8 * per, kKeyThreads, 0, st>>>(ws->keys.p, ws->bp.p + ws->bp_h1t, ws->bp_G, ws->bp_T,
+        bp_scatter2g_kernel<kBpGatherTile / kKeyThreads><<<8 * per, kKeyThreads, 0, st>>>(ws->keys.p, ws->bp.p + ws->bp_h1t, ws->bp_G, ws->bp_T,
                                                              ntiles, c1 - c0, dg, ws->cg, ws->cur.p, ws->sorted.p,
                                                              ws->flags.p, c0, c0);
     } else if (c1 > c0)
@@ -2916,84 +3040,104 @@ int pt_finish_overflow(kmp_postings* ws, const StepCfg& c, const PtGeom& g, uint
     return KMP_OK;
 }
 
-// Heavy path (host-driven, after the front): gather, sort and compact the spill once per front;
-// plan and expand the rows of this call into the shard regions.  stats: post the heavy k-mers'
-// statistics (once per batch).
+// Heavy path (after the front): gather, sort and compact the spill once per front; plan and
+// expand the rows of this call into the shard regions.  stats: post the heavy k-mers' statistics
+// (once per batch).  No host round trip: the element, k-mer and run counts stay on the device
+// (hoff tail), the arrays are sized by the spill count m, and the plan and expansion grids cover
+// that bound.
+__global__ void heavy_totals_kernel(const uint32_t* __restrict__ cnt, const unsigned long long* __restrict__ off,
+                                    uint64_t nt, unsigned long long* __restrict__ tot) {
+    const uint32_t a = threadIdx.x;  // elements, k-mers, runs
+    if (a < 3) tot[a] = nt ? off[a * (nt + 1) + nt - 1] + cnt[a * nt + nt - 1] : 0ull;
+}
+__global__ void heavy_sentinel_kernel(const unsigned long long* __restrict__ tot, uint64_t* __restrict__ GS,
+                                      uint64_t* __restrict__ RH) {
+    if (threadIdx.x == 0) GS[tot[1]] = tot[0];
+    if (threadIdx.x == 1 && RH) RH[tot[2]] = tot[0];
+}
+
 int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipStream_t st) {
     const Layout& lay = c.lay;
+    HeavyOrder ho{};
+    ho.cb = lay.clsbits;
+    ho.hshift = lay.hshift;
+    ho.pbits = lay.hshift - lay.clsbits;
+    ho.cls = c.require_diff && lay.clsbits > 0;
+    // tiles whose every pair is written (no per-pair test) are cut finer: one workgroup's write
+    // stream is the bound of a tile, and a 256 x 2,048 block of pairs left one CU writing 4 MB
+    ho.hj = (ho.cls ? !c.ranged : !c.require_diff) ? kHvJWrite : kHvJ;
     if (!ws->heavy_ready) {
+        const uint64_t nt = (m + kHvTile - 1) / kHvTile;
         PG(ws->hkeys.reserve(m));
         PG(ws->hsorted.reserve(m));
+        PG(ws->hcnt.reserve(3 * nt + 1));
+        PG(ws->hoff.reserve(3 * (nt + 1) + 4));
+        PG(ws->hE.reserve(m + 1));
+        PG(ws->hGS.reserve(m + 1));
+        if (ho.cls) {
+            PG(ws->hrun.reserve(m + 1));
+            PG(ws->hRH.reserve(m + 1));
+        }
         const unsigned long long* spill_cursor = ws->bstats.p + kRbSpill;
         gather_shards_kernel<<<dim3((uint32_t)std::min<uint64_t>((ws->spill_cap + 255) / 256, 1024), kShards), 256, 0,
-                               st>>>(ws->spill.p, ws->spill_cap, spill_cursor, ws->hkeys.p);
+                               st>>>(ws->spill.p, ws->spill_cap, spill_cursor, ho, ws->hkeys.p);
+        const unsigned lo_bit = ho.eshift();
         size_t tb = 0;
-        PG(rocprim::radix_sort_keys<SortCfg>(nullptr, tb, ws->hkeys.p, ws->hsorted.p, (size_t)m, lay.clsbits, 63u, st));
+        PG(rocprim::radix_sort_keys<SortCfg>(nullptr, tb, ws->hkeys.p, ws->hsorted.p, (size_t)m, lo_bit, 63u, st));
         PG(ws->tmp.reserve(std::max(tb, ws->tmp.n)));
-        PG(rocprim::radix_sort_keys<SortCfg>(ws->tmp.p, tb, ws->hkeys.p, ws->hsorted.p, (size_t)m, lay.clsbits, 63u,
-                                             st));
-        const uint64_t nt = (m + kHvTile - 1) / kHvTile;
-        PG(ws->hcnt.reserve(2 * nt));
-        PG(ws->hoff.reserve(2 * nt + 2));
-        uint32_t* ecnt = ws->hcnt.p;
-        uint32_t* gcnt = ws->hcnt.p + nt;
-        unsigned long long* eoff = ws->hoff.p;
-        unsigned long long* goff = ws->hoff.p + nt + 1;
-        heavy_scan_kernel<<<(uint32_t)nt, kHvThreads, 0, st>>>(ws->hsorted.p, m, lay.clsbits, lay.hshift, ecnt, gcnt);
+        PG(rocprim::radix_sort_keys<SortCfg>(ws->tmp.p, tb, ws->hkeys.p, ws->hsorted.p, (size_t)m, lo_bit, 63u, st));
+        uint32_t* cnt = ws->hcnt.p;             // elements | k-mers | runs, nt each
+        unsigned long long* off = ws->hoff.p;   // their exclusive scans, nt + 1 apart
+        unsigned long long* tot = off + 3 * (nt + 1);
+        heavy_scan_kernel<<<(uint32_t)nt, kHvThreads, 0, st>>>(ws->hsorted.p, m, ho, cnt, cnt + nt, cnt + 2 * nt);
         size_t t1 = 0;
-        PG(rocprim::exclusive_scan(nullptr, t1, ecnt, eoff, 0ull, (size_t)nt + 1, rocprim::plus<unsigned long long>(),
-                                   st));
+        PG(rocprim::exclusive_scan(nullptr, t1, cnt, off, 0ull, (size_t)nt, rocprim::plus<unsigned long long>(), st));
         PG(ws->tmp.reserve(std::max(t1, ws->tmp.n)));
-        PG(rocprim::exclusive_scan(ws->tmp.p, t1, ecnt, eoff, 0ull, (size_t)nt, rocprim::plus<unsigned long long>(),
-                                   st));
-        PG(rocprim::exclusive_scan(ws->tmp.p, t1, gcnt, goff, 0ull, (size_t)nt, rocprim::plus<unsigned long long>(),
-                                   st));
-        unsigned long long lastoff[2] = {0, 0};
-        uint32_t lastcnt[2] = {0, 0};
-        PG(hipMemcpyAsync(&lastoff[0], eoff + nt - 1, 8, hipMemcpyDeviceToHost, st));
-        PG(hipMemcpyAsync(&lastoff[1], goff + nt - 1, 8, hipMemcpyDeviceToHost, st));
-        PG(hipMemcpyAsync(&lastcnt[0], ecnt + nt - 1, 4, hipMemcpyDeviceToHost, st));
-        PG(hipMemcpyAsync(&lastcnt[1], gcnt + nt - 1, 4, hipMemcpyDeviceToHost, st));
-        PG(hipStreamSynchronize(st));
-        ws->h_ne = lastoff[0] + lastcnt[0];
-        ws->h_ng = lastoff[1] + lastcnt[1];
-        PG(ws->hE.reserve(ws->h_ne));
-        PG(ws->hGS.reserve(ws->h_ng + 1));
-        heavy_compact_kernel<<<(uint32_t)nt, kHvThreads, 0, st>>>(ws->hsorted.p, m, lay.clsbits, lay.hshift,
-                                                                  reinterpret_cast<const uint64_t*>(eoff),
-                                                                  reinterpret_cast<const uint64_t*>(goff), ws->hE.p,
-                                                                  reinterpret_cast<uint64_t*>(ws->hGS.p));
-        const unsigned long long ne = ws->h_ne;
-        PG(hipMemcpyAsync(ws->hGS.p + ws->h_ng, &ne, 8, hipMemcpyHostToDevice, st));
+        for (int a = 0; a < (ho.cls ? 3 : 2); ++a)
+            PG(rocprim::exclusive_scan(ws->tmp.p, t1, cnt + a * nt, off + a * (nt + 1), 0ull, (size_t)nt,
+                                       rocprim::plus<unsigned long long>(), st));
+        heavy_totals_kernel<<<1, 64, 0, st>>>(cnt, off, nt, tot);
+        uint64_t* GS = reinterpret_cast<uint64_t*>(ws->hGS.p);
+        uint64_t* RH = ho.cls ? reinterpret_cast<uint64_t*>(ws->hRH.p) : nullptr;
+        heavy_compact_kernel<<<(uint32_t)nt, kHvThreads, 0, st>>>(
+            ws->hsorted.p, m, ho, reinterpret_cast<const uint64_t*>(off),
+            reinterpret_cast<const uint64_t*>(off + nt + 1), reinterpret_cast<const uint64_t*>(off + 2 * (nt + 1)),
+            ws->hE.p, GS, ho.cls ? ws->hrun.p : nullptr, RH);
+        heavy_sentinel_kernel<<<1, 64, 0, st>>>(tot, GS, RH);
         PG(hipGetLastError());
         ws->heavy_ready = true;
+        ws->h_m = m;
+        ws->h_cls = ho.cls;
+        ws->h_tot = tot;
     }
-    const uint64_t ng = ws->h_ng;
-    if (ng == 0) return KMP_OK;
-    PG(ws->hgi.reserve(2 * ng));
-    PG(ws->htc.reserve(ng + 1));
-    PG(ws->htoff.reserve(ng + 1));
+    if (ws->h_cls != ho.cls) return KMP_EINVAL;  // one front, one class mode
+    const uint64_t ngb = ws->h_m;  // bound on the k-mer count (device: h_tot[1])
+    if (ngb == 0) return KMP_OK;
+    PG(ws->hgi.reserve(2 * (ngb + 1)));
+    PG(ws->htc.reserve(ngb + 1));
+    PG(ws->htoff.reserve(ngb + 1));
+    PG(ws->hblk.reserve(2 * (ngb + ngb / kHvI + 2)));
+    uint32_t* BT = ws->hblk.p;
+    uint32_t* BP = BT + ngb + ngb / kHvI + 2;
     const uint32_t row_lo = c.ranged ? c.row_lo : 0, row_hi = c.ranged ? c.row_hi : c.n;
-    heavy_plan_kernel<<<(uint32_t)((ng + 255) / 256), 256, 0, st>>>(
-        ws->hE.p, reinterpret_cast<const uint64_t*>(ws->hGS.p), ng, lay.clsbits, row_lo, row_hi, c.heavy_df,
-        stats ? 1 : 0, ws->bstats.p, ws->hgi.p, ws->htc.p);
+    const uint64_t* GS = reinterpret_cast<const uint64_t*>(ws->hGS.p);
+    const uint64_t* RH = ho.cls ? reinterpret_cast<const uint64_t*>(ws->hRH.p) : nullptr;
+    const uint32_t* RUN = ho.cls ? ws->hrun.p : nullptr;
+    heavy_plan_kernel<<<(uint32_t)((ngb + 1 + 255) / 256), 256, 0, st>>>(
+        ws->hE.p, GS, ngb + 1, ws->h_tot + 1, ho, RUN, RH, row_lo, row_hi, c.heavy_df, stats ? 1 : 0, ws->bstats.p,
+        ws->hgi.p, BT, BP, ws->htc.p);
     size_t t2 = 0;
-    PG(rocprim::exclusive_scan(nullptr, t2, ws->htc.p, ws->htoff.p, 0ull, (size_t)ng + 1,
+    PG(rocprim::exclusive_scan(nullptr, t2, ws->htc.p, ws->htoff.p, 0ull, (size_t)ngb + 1,
                                rocprim::plus<unsigned long long>(), st));
     PG(ws->tmp.reserve(std::max(t2, ws->tmp.n)));
-    PG(hipMemsetAsync(ws->htc.p + ng, 0, 8, st));
-    PG(rocprim::exclusive_scan(ws->tmp.p, t2, ws->htc.p, ws->htoff.p, 0ull, (size_t)ng + 1,
+    PG(rocprim::exclusive_scan(ws->tmp.p, t2, ws->htc.p, ws->htoff.p, 0ull, (size_t)ngb + 1,
                                rocprim::plus<unsigned long long>(), st));
-    unsigned long long tiles = 0;
-    PG(hipMemcpyAsync(&tiles, ws->htoff.p + ng, 8, hipMemcpyDeviceToHost, st));
-    PG(hipStreamSynchronize(st));
-    if (tiles) {
-        const uint32_t grid = (uint32_t)std::min<unsigned long long>(tiles, 8192);
-        heavy_expand_kernel<<<grid, kHvI, 0, st>>>(ws->hE.p, reinterpret_cast<const uint64_t*>(ws->hGS.p), ws->hgi.p,
-                                                   ws->htoff.p, ng, ws->htoff.p + ng, lay.clsbits,
-                                                   1u << bits_for(c.n), c.require_diff, ws->inc_sorted.p,
-                                                   ws->shard_cap, ws->bstats.p + kRbCursor, ws->bstats.p);
-    }
+    // tiles = htoff[ng] (device); the grid strides them
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(ngb / 4, 256), 8192);
+    heavy_expand_kernel<<<grid, kHvI, 0, st>>>(ws->hE.p, GS, ws->hgi.p, BT, BP, RUN, RH, ws->htoff.p, ws->h_tot + 1,
+                                               ho, 1u << bits_for(c.n), c.require_diff, c.ranged ? 1 : 0, row_lo,
+                                               row_hi, ws->inc_sorted.p, ws->shard_cap, ws->bstats.p + kRbCursor,
+                                               ws->bstats.p);
     PG(hipGetLastError());
     return KMP_OK;
 }
