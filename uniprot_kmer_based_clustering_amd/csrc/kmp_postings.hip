@@ -542,10 +542,11 @@ __global__ void bucket_bounds_kernel(const unsigned long long* __restrict__ k, u
 
 constexpr uint32_t kHeavySub = 128;  // larger sub-buckets (very frequent k-mers) -> flat layout
 constexpr int kShards = 64;          // output cursors (one per bucket residue mod kShards)
+static_assert(kShards == 64, "the heavy tiles hash to a shard with a 6-bit shift");
 // device flags of a step (ws->flags): a coarse bin above its level-2 tile budget, a class id too
 // wide for the key, the large-bucket list count, row blocks above the LDS capacity, the tile
 // budget an overflowing bin needs, a cursor-partition region overflow
-enum : uint32_t { kFlBin = 0, kFlClass = 1, kFlList = 2, kFlOvf = 3, kFlBinTiles = 4, kFlCur = 5, kFlN = 8 };
+enum : uint32_t { kFlBin = 0, kFlClass = 1, kFlList = 2, kFlOvf = 3, kFlBinTiles = 4, kFlCur = 5, kFlSegs = 6, kFlSegMax = 7, kFlN = 8 };
 
 template <int kThreads>
 __device__ __forceinline__ void block_scan_n(uint32_t v, uint32_t& excl, uint32_t& total, uint32_t* wave_tot) {
@@ -603,7 +604,17 @@ struct BucketArgs {
     unsigned long long* spill;
     uint64_t spill_cap;
     unsigned long long* spill_cursor;
+    // spill segments (a heavy group, or a whole bucket): spill index | keys << 40, counted in
+    // flags[kFlSegs], the largest in flags[kFlSegMax]; the heavy path sorts each in LDS
+    unsigned long long* seg;
+    uint32_t seg_cap;
 };
+
+__device__ __forceinline__ void spill_segment(const BucketArgs& a, uint64_t pos, uint32_t keys) {
+    const uint32_t s = atomicAdd(&a.flags[kFlSegs], 1u);
+    if (s < a.seg_cap) a.seg[s] = pos | (unsigned long long)min(keys, 0xFFFFFFu) << 40;
+    atomicMax(&a.flags[kFlSegMax], keys);
+}
 
 // One workgroup per bucket with size <= kCap (the bucket: keys with the same top bbits of
 // h(code)).  In LDS:
@@ -668,7 +679,10 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
         // above every LDS capacity: the whole bucket goes to the heavy path
         if (!a.spill) return;
         __syncthreads();
-        if (tid == 0) sbase = atomicAdd(&a.spill_cursor[shard], (unsigned long long)n);
+        if (tid == 0) {
+            sbase = atomicAdd(&a.spill_cursor[shard], (unsigned long long)n);
+            spill_segment(a, (uint64_t)shard * a.spill_cap + sbase, n);
+        }
         __syncthreads();
         unsigned long long* dst = a.spill + (uint64_t)shard * a.spill_cap;
         for (uint32_t i = tid; i < n; i += kThreads)
@@ -789,6 +803,7 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
             if (spill_dst) {
                 const unsigned long long pos = sbase + hbase[g] + rk[e];
                 if (pos < a.spill_cap) spill_dst[pos] = xk[e];
+                if (rk[e] == 0) spill_segment(a, (uint64_t)shard * a.spill_cap + pos, cn[e]);
             }
             continue;
         }
@@ -982,6 +997,7 @@ __global__ __launch_bounds__(kThreads) void bucket_large_kernel(BucketArgs a) {
 //      kernels fill.  A k-mer of df 10^4 is ~400 tiles: no workgroup walks a long posting list.
 constexpr uint32_t kHvTile = 4096, kHvThreads = 256, kHvPer = kHvTile / kHvThreads;
 constexpr uint32_t kHvI = 256, kHvJ = 2048, kHvJWrite = 256;
+constexpr uint32_t kHvSpread = 64 * 256;  // a tile with this many pairs spreads them over the shards
 
 // Heavy key order.  Plain: the spilled keys [h | p | class] sorted on (h, p).  Class order (the
 // class test is on): gather_shards rewrites them to [h | class | p] and the sort is on every bit,
@@ -1020,6 +1036,54 @@ __global__ void gather_shards_kernel(const unsigned long long* __restrict__ src,
         const unsigned long long v = src[(uint64_t)s * shard_cap + i];
         dst[off + i] = ho.cls ? (v & hm) | (v & cm) << ho.pbits | ((v & ~hm) >> ho.cb) : v;
     }
+}
+
+// The spill is a list of segments (BucketArgs::seg): one heavy group (one k-mer) or one whole
+// bucket, each holding every key of its k-mers.  Each sorted alone, in LDS, and written where the
+// gather would have put it, is the whole sort the heavy path needs (k-mers contiguous, each
+// sorted): no global radix sort (eight onesweep passes over 1M keys at k = 5, 0.3 ms).  One
+// workgroup per segment of (kLo, kN] keys: a bitonic sort of the next power of two (1,024 threads
+// for the large segments: the stages are LDS-latency bound).
+constexpr uint32_t kSegSmall = 2048, kSegLarge = 8192;
+template <uint32_t kLo, uint32_t kN, uint32_t kSegThreads>
+__global__ __launch_bounds__(kSegThreads) void heavy_segsort_kernel(const unsigned long long* __restrict__ spill,
+                                                                    uint64_t spill_cap,
+                                                                    const unsigned long long* __restrict__ cursor,
+                                                                    const unsigned long long* __restrict__ seg,
+                                                                    HeavyOrder ho,
+                                                                    unsigned long long* __restrict__ out) {
+    __shared__ unsigned long long K[kN];
+    const unsigned long long sd = seg[blockIdx.x];
+    const uint32_t cnt = (uint32_t)(sd >> 40);
+    if (cnt <= kLo || cnt > kN) return;
+    const uint64_t pos = sd & ((1ull << 40) - 1), shard = pos / spill_cap;
+    uint64_t dst = pos - shard * spill_cap;
+    for (uint64_t t = 0; t < shard; ++t) dst += cursor[t];
+    uint32_t N = 1;
+    while (N < cnt) N <<= 1;
+    const unsigned long long cm = (1ull << ho.cb) - 1, hm = ~((1ull << ho.hshift) - 1);
+    for (uint32_t i = threadIdx.x; i < N; i += kSegThreads) {
+        unsigned long long v = ~0ull;  // padding sorts last
+        if (i < cnt) {
+            v = spill[pos + i];
+            if (ho.cls) v = (v & hm) | (v & cm) << ho.pbits | ((v & ~hm) >> ho.cb);
+        }
+        K[i] = v;
+    }
+    __syncthreads();
+    for (uint32_t k = 2; k <= N; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < N / 2; i += kSegThreads) {
+                const uint32_t lo = 2 * j * (i / j) + (i % j), hi = lo + j;
+                const unsigned long long x = K[lo], y = K[hi];
+                if ((x > y) == !(lo & k)) {
+                    K[lo] = y;
+                    K[hi] = x;
+                }
+            }
+            __syncthreads();
+        }
+    for (uint32_t i = threadIdx.x; i < cnt; i += kSegThreads) out[dst + i] = K[i];
 }
 
 // per tile: distinct (h, p) elements, k-mer heads and (class order) class-run heads
@@ -1202,6 +1266,7 @@ __global__ __launch_bounds__(kHvI) void heavy_expand_kernel(const uint32_t* __re
                                                             unsigned long long* __restrict__ gstats) {
     __shared__ uint32_t J[kHvJ];
     __shared__ uint32_t s_ex[kHvI + 1], s_js[kHvI], s_p[kHvI];
+    __shared__ unsigned long long s_sb[kShards];  // spread tile: shard base minus its first output
     __shared__ uint32_t wave_tot[kHvI / 64];
     __shared__ unsigned long long sbase;
     const uint64_t ng = *ng_dev;
@@ -1254,8 +1319,23 @@ __global__ __launch_bounds__(kHvI) void heavy_expand_kernel(const uint32_t* __re
         }
         uint32_t excl, total;
         block_scan_n<kHvI>(c, excl, total, wave_tot);
-        const uint32_t shard = (uint32_t)(t % kShards);
-        if (threadIdx.x == 0) {
+        // Shards, which size the next call's regions: a large unfiltered tile spreads its output
+        // evenly over all of them (output o in shard 64 o / total); another tile takes one shard from
+        // what it is (its k-mer's first element, block, chunk) — not from t: the k-mers' order in E
+        // follows the spill's (atomic) order, and the shard loads must not
+        const bool spread = !(test_cls || test_row) && total >= kHvSpread;
+        uint32_t hx = (E[b] * 0x9E3779B1u) ^ (klo * 0x85EBCA6Bu) ^ (local * 0xC2B2AE35u);
+        hx ^= hx >> 16;
+        const uint32_t shard = (hx * 0x7FEB352Du) >> 26;  // the top bits: kShards = 64
+        if (spread) {
+            if (threadIdx.x < kShards) {
+                const uint32_t sh = threadIdx.x;
+                const uint64_t a0 = ((uint64_t)sh * total + kShards - 1) / kShards;
+                const uint64_t a1 = ((uint64_t)(sh + 1) * total + kShards - 1) / kShards;
+                s_sb[sh] = atomicAdd(&cursor[sh], (unsigned long long)(a1 - a0)) - a0;  // pos = s_sb + o
+                if (a1 > a0) atomicAdd(&gstats[(uint64_t)sh * 8 + kStInc], (unsigned long long)(a1 - a0));
+            }
+        } else if (threadIdx.x == 0) {
             sbase = total ? atomicAdd(&cursor[shard], (unsigned long long)total) : 0ull;
             if (total) atomicAdd(&gstats[(uint64_t)shard * 8 + kStInc], (unsigned long long)total);
         }
@@ -1292,8 +1372,15 @@ __global__ __launch_bounds__(kHvI) void heavy_expand_kernel(const uint32_t* __re
             for (uint32_t o = threadIdx.x; o < total; o += kHvI) {
                 while (s_ex[i + 1] <= o) ++i;
                 const uint32_t pa = s_p[i], pj = J[s_js[i] + (o - s_ex[i]) - j0] >> cb;
-                const unsigned long long pos = sbase + o;
-                if (pos < shard_cap) dst[pos] = (unsigned long long)min(pa, pj) * mul + max(pa, pj);
+                const unsigned long long key = (unsigned long long)min(pa, pj) * mul + max(pa, pj);
+                if (spread) {
+                    const uint32_t sh = (uint32_t)((uint64_t)o * kShards / total);
+                    const unsigned long long pos = s_sb[sh] + o;
+                    if (pos < shard_cap) out[(uint64_t)sh * shard_cap + pos] = key;
+                } else {
+                    const unsigned long long pos = sbase + o;
+                    if (pos < shard_cap) dst[pos] = key;
+                }
             }
         }
     }
@@ -2107,12 +2194,13 @@ struct kmp_postings {
     CurGeom cg{};
     // heavy path (frequent k-mers): spill regions, the gathered + sorted spill, its elements,
     // k-mer starts, per-k-mer row bounds / tile counts / tile offsets
-    Grow<unsigned long long> spill, hkeys, hsorted, hGS, htc, htoff, hoff, hRH;
+    Grow<unsigned long long> spill, hkeys, hsorted, hGS, htc, htoff, hoff, hRH, hseg;
     Grow<uint32_t> hE, hgi, hcnt, hrun, hblk;
     uint64_t spill_cap = 0;     // keys per spill shard region
     bool heavy = false;         // this workspace's batches spill: run the split step
     bool heavy_ready = false;   // hE / hGS hold the current front's compacted spill
     uint64_t h_m = 0;                // spill keys behind hE (the bound on elements and k-mers)
+    uint64_t h_segs = 0, h_segmax = 0;  // the front's spill segments: count, largest (read-back)
     int h_cls = 0;                   // hE in class order
     unsigned long long* h_tot = nullptr;  // device: elements, k-mers, class runs
     std::vector<unsigned long long> shape;  // (n, slots, code bits, bucket bits) of the last batch
@@ -2143,7 +2231,7 @@ struct kmp_postings {
     hipEvent_t ev[KMP_POSTINGS_STAGES + 1] = {};
     ~kmp_postings() {
         for (auto* g : {&keys, &sorted, &inc, &inc_sorted, &uniq, &bstats, &btot, &boff, &spill, &hkeys, &hsorted,
-                        &hGS, &htc, &htoff, &hoff, &hRH, &ovk, &ovx, &split_cur})
+                        &hGS, &htc, &htoff, &hoff, &hRH, &hseg, &ovk, &ovx, &split_cur})
             g->release();
         for (auto* g : {&w, &keep, &pos, &small, &cnt, &flags, &chunk_first, &bp, &pt, &ovf, &ovr, &hE, &hgi, &hcnt, &hrun, &hblk, &cur})
             g->release();
@@ -2791,7 +2879,7 @@ __global__ __launch_bounds__(256) void pt_emit_kernel(const uint32_t* __restrict
 // read-back: gstats (8 per shard) | pair cursors | spill cursors | the words below
 enum : uint32_t {
     kRbCursor = kShards * 8, kRbSpill = kShards * 9, kRbFlagBin = kShards * 10, kRbFlagClass, kRbRuns, kRbOvf,
-    kRbMaxBlock, kRbBinTiles, kRbFlagCur, kRbWords
+    kRbMaxBlock, kRbBinTiles, kRbFlagCur, kRbSegs, kRbSegMax, kRbWords
 };
 constexpr uint32_t kGsWords = kShards * 10;  // gstats | cursors | spill cursors (u64)
 
@@ -2811,6 +2899,8 @@ __global__ void step_pack_kernel(const unsigned long long* __restrict__ gstats, 
         rb[kRbMaxBlock] = runs ? runs[1] : 0;
         rb[kRbBinTiles] = flags[kFlBinTiles];
         rb[kRbFlagCur] = flags[kFlCur];
+        rb[kRbSegs] = flags[kFlSegs];
+        rb[kRbSegMax] = flags[kFlSegMax];
     }
     __threadfence_system();  // rb is host memory, read after the stream synchronises
 }
@@ -2877,6 +2967,11 @@ PtBufs pt_bufs(kmp_postings* ws, const PtGeom& g, bool reserve, hipError_t* e) {
     return b;
 }
 
+// spill segments: every one holds more than kHeavySub keys (a heavy group, or a whole bucket)
+uint32_t seg_capacity(const kmp_postings* ws) {
+    return (uint32_t)std::min<uint64_t>(ws->spill_cap * kShards / kHeavySub + 64, 1u << 30);
+}
+
 BucketArgs bucket_args(kmp_postings* ws, const StepCfg& c, bool spill) {
     BucketArgs a{};
     const uint32_t nb = 1u << c.lay.bbits;
@@ -2902,6 +2997,8 @@ BucketArgs bucket_args(kmp_postings* ws, const StepCfg& c, bool spill) {
     a.spill = spill ? ws->spill.p : nullptr;
     a.spill_cap = ws->spill_cap;
     a.spill_cursor = ws->bstats.p + kRbSpill;
+    a.seg = ws->hseg.p;
+    a.seg_cap = seg_capacity(ws);
     return a;
 }
 
@@ -2919,6 +3016,7 @@ int step_reserve(kmp_postings* ws, const StepCfg& c, const PtGeom& g) {
     PG(ws->uniq.reserve(total));  // ... staged p | q (u32 each)
     PG(ws->w.reserve(total));     // ... staged w
     PG(ws->spill.reserve(ws->spill_cap * kShards));
+    PG(ws->hseg.reserve(seg_capacity(ws)));
     PG(ws->ovf.reserve((uint64_t)g.nrb + 1));
     if (!ws->hrb) PG(hipHostMalloc((void**)&ws->hrb, kRbWords * sizeof(unsigned long long), hipHostMallocCoherent));
     hipError_t e = hipSuccess;
@@ -3079,13 +3177,23 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
             PG(ws->hRH.reserve(m + 1));
         }
         const unsigned long long* spill_cursor = ws->bstats.p + kRbSpill;
-        gather_shards_kernel<<<dim3((uint32_t)std::min<uint64_t>((ws->spill_cap + 255) / 256, 1024), kShards), 256, 0,
-                               st>>>(ws->spill.p, ws->spill_cap, spill_cursor, ho, ws->hkeys.p);
-        const unsigned lo_bit = ho.eshift();
-        size_t tb = 0;
-        PG(rocprim::radix_sort_keys<SortCfg>(nullptr, tb, ws->hkeys.p, ws->hsorted.p, (size_t)m, lo_bit, 63u, st));
-        PG(ws->tmp.reserve(std::max(tb, ws->tmp.n)));
-        PG(rocprim::radix_sort_keys<SortCfg>(ws->tmp.p, tb, ws->hkeys.p, ws->hsorted.p, (size_t)m, lo_bit, 63u, st));
+        if (ws->h_segs && ws->h_segs <= seg_capacity(ws) && ws->h_segmax <= kSegLarge) {
+            const uint32_t ns = (uint32_t)ws->h_segs;
+            heavy_segsort_kernel<0, kSegSmall, 256><<<ns, 256, 0, st>>>(ws->spill.p, ws->spill_cap, spill_cursor,
+                                                                          ws->hseg.p, ho, ws->hsorted.p);
+            if (ws->h_segmax > kSegSmall)
+                heavy_segsort_kernel<kSegSmall, kSegLarge, 1024><<<ns, 1024, 0, st>>>(
+                    ws->spill.p, ws->spill_cap, spill_cursor, ws->hseg.p, ho, ws->hsorted.p);
+        } else {  // a segment above the LDS sort: gather and one radix sort
+            gather_shards_kernel<<<dim3((uint32_t)std::min<uint64_t>((ws->spill_cap + 255) / 256, 1024), kShards),
+                                   256, 0, st>>>(ws->spill.p, ws->spill_cap, spill_cursor, ho, ws->hkeys.p);
+            const unsigned lo_bit = ho.eshift();
+            size_t tb = 0;
+            PG(rocprim::radix_sort_keys<SortCfg>(nullptr, tb, ws->hkeys.p, ws->hsorted.p, (size_t)m, lo_bit, 63u, st));
+            PG(ws->tmp.reserve(std::max(tb, ws->tmp.n)));
+            PG(rocprim::radix_sort_keys<SortCfg>(ws->tmp.p, tb, ws->hkeys.p, ws->hsorted.p, (size_t)m, lo_bit, 63u,
+                                                 st));
+        }
         uint32_t* cnt = ws->hcnt.p;             // elements | k-mers | runs, nt each
         unsigned long long* off = ws->hoff.p;   // their exclusive scans, nt + 1 apart
         unsigned long long* tot = off + 3 * (nt + 1);
@@ -3343,6 +3451,8 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
         }
         if (split) {
             if (spill_total || ws->heavy_ready) {
+                ws->h_segs = rb[kRbSegs];
+                ws->h_segmax = rb[kRbSegMax];
                 int rc = heavy_phase(ws, c, spill_total, true, st);
                 if (rc != KMP_OK) return rc;
             }
@@ -3351,6 +3461,10 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
             PG(hipStreamSynchronize(st));
             sum_stats(rb, acc, &most, &n_inc, &spill_most, &spill_total);
             if (most > ws->shard_cap) {
+                if (debug)
+                    fprintf(stderr, "kmp: rerun after the heavy path (shard %llu/%llu, segments %llu, largest %llu)\n",
+                            most, (unsigned long long)ws->shard_cap, (unsigned long long)ws->h_segs,
+                            (unsigned long long)ws->h_segmax);
                 ws->shard_cap = most + most / 64 + 256;
                 continue;
             }
