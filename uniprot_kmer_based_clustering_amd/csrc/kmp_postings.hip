@@ -1369,12 +1369,18 @@ __global__ __launch_bounds__(kHvI) void heavy_expand_kernel(const uint32_t* __re
                     else hi = mid;
                 }
             }
+            // spread: output o's shard sh = 64 o / total, advanced as o grows (total < 2^26)
+            uint32_t sh = spread ? threadIdx.x * kShards / total : 0u;
+            uint32_t sh_end = spread ? ((sh + 1) * total + kShards - 1) / kShards : 0u;
             for (uint32_t o = threadIdx.x; o < total; o += kHvI) {
                 while (s_ex[i + 1] <= o) ++i;
                 const uint32_t pa = s_p[i], pj = J[s_js[i] + (o - s_ex[i]) - j0] >> cb;
                 const unsigned long long key = (unsigned long long)min(pa, pj) * mul + max(pa, pj);
                 if (spread) {
-                    const uint32_t sh = (uint32_t)((uint64_t)o * kShards / total);
+                    while (o >= sh_end) {
+                        ++sh;
+                        sh_end = ((sh + 1) * total + kShards - 1) / kShards;
+                    }
                     const unsigned long long pos = s_sb[sh] + o;
                     if (pos < shard_cap) out[(uint64_t)sh * shard_cap + pos] = key;
                 } else {
@@ -2815,6 +2821,69 @@ __global__ void pt_ovf_stage_kernel(const uint32_t* __restrict__ ovf, uint32_t m
     }
 }
 
+// Listed blocks whose key space is small (rbits + pbits <= 15: the next call's geometry after a
+// first overflow — one or two rows per block, e.g. a protein sharing 5-mers with thousands of
+// later ones): a histogram over the key (row in block, q) in LDS is the run-length encoding,
+// already in canonical order.  One workgroup per listed block (grid-stride over the device
+// count); no sort, no host round trip.
+constexpr uint32_t kRowHistBits = 15, kRowHistBins = 1u << kRowHistBits, kRowHistThreads = 1024, kRowHistGrid = 64;
+__host__ __device__ inline bool pt_rowhist_ok(const PtGeom& g) { return g.rbits + g.pbits <= kRowHistBits; }
+
+__global__ __launch_bounds__(kRowHistThreads) void pt_rowhist_kernel(const uint32_t* __restrict__ keys,
+                                                                     const uint32_t* __restrict__ bst, PtGeom g,
+                                                                     const uint32_t* __restrict__ flags,
+                                                                     const uint32_t* __restrict__ ovf,
+                                                                     uint32_t* __restrict__ stage_p,
+                                                                     uint32_t* __restrict__ stage_q,
+                                                                     uint32_t* __restrict__ stage_w,
+                                                                     uint32_t* __restrict__ counts) {
+    __shared__ uint32_t hist[kRowHistBins];  // 128 KB: one workgroup per CU
+    __shared__ uint32_t wave_tot[kRowHistThreads / 64];
+    const uint32_t m = flags[kFlOvf], nk = 1u << (g.rbits + g.pbits), km = nk - 1, qm = (1u << g.pbits) - 1;
+    constexpr uint32_t kQ = kRowHistBins / kRowHistThreads;
+    for (uint32_t j = blockIdx.x; j < m; j += gridDim.x) {
+        const uint32_t r = ovf[j], s0 = bst[r], n = bst[r + 1] - s0;
+        __syncthreads();  // the previous block's compaction has read hist
+        for (uint32_t x = threadIdx.x; x < nk; x += kRowHistThreads) hist[x] = 0;
+        __syncthreads();
+        // loads in batches of 8 ahead of their atomics (one workgroup walks the whole block)
+        for (uint32_t i0 = 0; i0 < n; i0 += 8 * kRowHistThreads) {
+            uint32_t v[8];
+#pragma unroll
+            for (uint32_t e = 0; e < 8; ++e) {
+                const uint32_t i = i0 + e * kRowHistThreads + threadIdx.x;
+                v[e] = i < n ? keys[s0 + i] : ~0u;
+            }
+#pragma unroll
+            for (uint32_t e = 0; e < 8; ++e)
+                if (v[e] != ~0u) atomicAdd(&hist[v[e] & km], 1u);
+        }
+        __syncthreads();
+        // thread t: keys [t * kQ, t * kQ + kQ), kept runs (w >= min_shared) in key order
+        const uint32_t x0 = threadIdx.x * kQ;
+        uint32_t kept = 0;
+#pragma unroll
+        for (uint32_t e = 0; e < kQ; ++e) {
+            const uint32_t w = x0 + e < nk ? hist[x0 + e] : 0u;
+            kept += w != 0 && w >= g.min_shared;
+        }
+        uint32_t o, total;
+        block_scan_n<kRowHistThreads>(kept, o, total, wave_tot);
+        const uint32_t rowbase = g.row0 + (r << g.rbits);
+#pragma unroll
+        for (uint32_t e = 0; e < kQ; ++e) {
+            const uint32_t x = x0 + e, w = x < nk ? hist[x] : 0u;
+            if (w != 0 && w >= g.min_shared) {
+                stage_p[s0 + o] = rowbase + (x >> g.pbits);
+                stage_q[s0 + o] = x & qm;
+                stage_w[s0 + o] = w;
+                ++o;
+            }
+        }
+        if (threadIdx.x == 0) counts[r] = total;
+    }
+}
+
 // exclusive scan of the nrb run counts (nrb <= 8 * 1024) -> eoff; eoff[nrb] and *total = edges
 __global__ __launch_bounds__(kPtScanThreads) void pt_offsets_kernel(const uint32_t* __restrict__ counts, uint32_t nrb,
                                                                     uint32_t* __restrict__ eoff,
@@ -3069,6 +3138,9 @@ int enqueue_tail_in(kmp_postings* ws, const StepCfg& c, const PtGeom& g, const u
     pt_scatter_kernel<<<dim3(g.jt, g.nshards), kPtThreads, 0, st>>>(in, cursor, g, b.P, keys32);
     pt_reduce_kernel<<<g.nrb, kPtRThreads, 0, st>>>(keys32, b.bst, g, ws->flags.p, ws->ovf.p, stage_p, stage_q,
                                                     ws->w.p, b.counts);
+    if (pt_rowhist_ok(g))  // one-row blocks above kPtCap: finished here (none listed: every workgroup exits)
+        pt_rowhist_kernel<<<kRowHistGrid, kRowHistThreads, 0, st>>>(keys32, b.bst, g, ws->flags.p, ws->ovf.p,
+                                                                    stage_p, stage_q, ws->w.p, b.counts);
     ws->mark(5, st);
     pt_offsets_kernel<<<1, kPtScanThreads, 0, st>>>(b.counts, g.nrb, b.eoff, ws->small.p + 1);
     pt_emit_kernel<<<g.nrb, 256, 0, st>>>(stage_p, stage_q, ws->w.p, b.bst, b.counts, b.eoff, c.d_p, c.d_q, c.d_w,
@@ -3479,7 +3551,7 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
         ws->pt_inc = n_inc;  // sizes the next call's row blocks
         uint64_t ne = rb[kRbRuns];
         ws->last_ovf = (uint32_t)rb[kRbOvf];
-        if (rb[kRbOvf]) {
+        if (rb[kRbOvf] && !pt_rowhist_ok(g)) {
             // row blocks above the LDS capacity: finished by the segmented sort; the next call
             // uses fewer rows per block when one row is not already the whole block
             if (g.rbits > 0) {
@@ -4039,7 +4111,7 @@ int kmp_dev_split_edges(kmp_postings* ws, const unsigned long long* d_keys, uint
     PG(hipStreamSynchronize(st));
     const unsigned long long* rb = ws->hrb;
     uint64_t ne = rb[kRbRuns];
-    if (rb[kRbOvf]) {  // row blocks above the LDS capacity: the segmented sort, fewer rows per block next time
+    if (rb[kRbOvf] && !pt_rowhist_ok(g)) {  // row blocks above the LDS capacity: the segmented sort, fewer rows per block next time
         if (g.rbits > 0) {
             const double over = (double)rb[kRbMaxBlock] / (0.8 * kPtCap);
             unsigned shrink = 1;
