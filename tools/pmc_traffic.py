@@ -34,7 +34,7 @@ def main():
               f"{r['write_bytes']/1e6:>9.1f}")
     # per-step traffic of the residue step's stages (bench.py STAGE_NAMES["rows"]); one
     # level-1 scatter dispatch per step
-    calls = max([r["dispatches"] for r in rows if r["kernel"] in ("bp_scatter1_kernel", "bp_scatter1l_kernel")] or [1])
+    calls = max([r["dispatches"] for r in rows if r["kernel"].split("<")[0] in ("bp_scatter1_kernel", "bp_scatter1l_kernel")] or [1])
     by_kernel = {
         "chunk_first_kernel": "keys_level1", "bp_hist1_kernel": "keys_level1", "bp_colscan_kernel": "keys_level1",
         "bp_scatter1_kernel": "keys_level1", "bp_scatter1l_kernel": "keys_level1", "bp_h1t_kernel": "keys_level1",
@@ -48,7 +48,7 @@ def main():
     }
 
     def stage(r):
-        k = r["kernel"]
+        k = r["kernel"].removeprefix("void ").split("<")[0]
         if "bucket_small_kernel" in k or "bucket_large_kernel" in k:
             return "group_expand"
         return by_kernel.get(k)
