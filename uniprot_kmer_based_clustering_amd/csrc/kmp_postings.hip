@@ -654,7 +654,8 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
     __shared__ uint32_t gdupw[kCap / 32];  // per group start: the group holds such a duplicate
     __shared__ uint32_t SZ[kHeavySub + 1];
     __shared__ uint32_t wave_tot[kThreads / 64];
-    __shared__ unsigned long long red[kThreads / 64][3];
+    __shared__ unsigned long long red[kThreads / 64][2];
+    __shared__ uint32_t s_cnt;  // F: keys in the LDS stage
     __shared__ unsigned long long sbase;
     __shared__ unsigned long long hbase[kMaxHeavy];  // spill offset of each heavy group
     __shared__ uint32_t nheavy, hkeys;
@@ -833,49 +834,28 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
     }
     __syncthreads();
     auto is_dup = [&](uint32_t j) { return (dupw[j >> 5] >> (j & 31)) & 1u; };
-    // E. df, head, kept-partner count.  A group without duplicates (almost all) has df = its size
-    // and counts its partners after i only; a group with one walks the whole group.
-    uint32_t cnt[kE];
-    bool gd[kE];
-    uint32_t st_sum = single, st_dist = single, st_rep = 0, st_cdf2 = 0, st_max = single ? 1u : 0u, st_heavy = 0,
-             mine = 0;
+    // E. df and head statistics; act[e]: the element expands (not a duplicate window, df within
+    // heavy_df, and with kRows its protein in the rows).  A group without duplicates (almost all)
+    // has df = its size; a group with one walks the whole group for it.
+    bool act[kE], gd[kE];
+    uint32_t st_sum = single, st_dist = single, st_rep = 0, st_cdf2 = 0, st_max = single ? 1u : 0u, st_heavy = 0;
 #pragma unroll
     for (int e = 0; e < kE; ++e) {
         const uint32_t i = tid + e * kThreads;
-        cnt[e] = 0;
-        gd[e] = false;
+        act[e] = gd[e] = false;
         if (i >= nm) continue;
         gd[e] = (gdupw[s[e] >> 5] >> (s[e] & 31)) & 1u;
         if (gd[e] && is_dup(i)) continue;
-        uint32_t f, c = 0;
-        if (kRows) {
-            // df, and the partners of a larger protein when this element's protein is in the rows
-            const uint32_t p = xl[e] >> cb;
-            const bool emit = p >= a.row_lo && p < a.row_hi;
-            f = gd[e] ? 0u : en[e] - s[e];
-            if (emit || gd[e])
-                for (uint32_t j = s[e]; j < en[e]; ++j) {
-                    if (gd[e] && is_dup(j)) continue;
-                    f += gd[e];
-                    const uint32_t lj = Bl[j];
-                    c += emit && (lj >> cb) > p && (!a.require_diff || ((lj ^ xl[e]) & cmask));
-                }
-        } else if (!gd[e]) {
-            f = en[e] - s[e];
-            if (a.require_diff) {
-                for (uint32_t j = i + 1; j < en[e]; ++j) c += ((Bl[j] ^ xl[e]) & cmask) != 0u;
-            } else {
-                c = en[e] - 1 - i;
-            }
-        } else {
+        uint32_t f = en[e] - s[e];
+        if (gd[e]) {
             f = 0;
-            for (uint32_t j = s[e]; j < en[e]; ++j) {
-                if (is_dup(j)) continue;
-                ++f;
-                if (j > i && (!a.require_diff || ((Bl[j] ^ xl[e]) & cmask))) ++c;
-            }
+            for (uint32_t j = s[e]; j < en[e]; ++j) f += !is_dup(j);
         }
-        if (f > a.heavy_df) c = 0;
+        act[e] = f <= a.heavy_df;
+        if (kRows) {
+            const uint32_t p = xl[e] >> cb;
+            act[e] = act[e] && p >= a.row_lo && p < a.row_hi;
+        }
         st_sum += 1;
         if (i == s[e]) {  // the group's first position is never a duplicate
             st_dist += 1;
@@ -884,59 +864,52 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
             else st_heavy += f;
             st_max = max(st_max, f);
         }
-        cnt[e] = c;
-        mine += c;
     }
-    // statistics: three wave reductions of packed words (per workgroup every count is at most
-    // kCap, so 16-bit fields cannot carry; C(df,2) and the incidences stay below 2^32), wave
-    // partials -> red, then kStN threads unpack, sum and post one (sharded) atomic each.  They
-    // ride on the output scan's barriers; the last wave reserves the output range meanwhile.
+    // statistics: two wave reductions of packed words (per workgroup every count is at most kCap,
+    // so 16-bit fields cannot carry; C(df,2) stays below 2^32), wave partials -> red, then kStN
+    // threads unpack, sum and post one (sharded) atomic each; the incidences are the stage count
     {
         unsigned long long w0 = st_sum | (unsigned long long)st_dist << 16 | (unsigned long long)st_rep << 32 |
                                 (unsigned long long)st_heavy << 48;
-        unsigned long long c2 = st_cdf2 | (unsigned long long)mine << 32;
-        uint32_t mx = st_max;
+        unsigned long long c2 = st_cdf2 | (unsigned long long)st_max << 32;
         for (int sh = 32; sh > 0; sh >>= 1) {
             w0 += __shfl_down(w0, sh);
-            c2 += __shfl_down(c2, sh);
-            mx = max(mx, (uint32_t)__shfl_down(mx, sh));
+            const unsigned long long o = __shfl_down(c2, sh);
+            c2 = ((c2 & 0xFFFFFFFFull) + (o & 0xFFFFFFFFull)) | (unsigned long long)max(c2 >> 32, o >> 32) << 32;
         }
         if ((tid & 63) == 0) {
             red[tid >> 6][0] = w0;
             red[tid >> 6][1] = c2;
-            red[tid >> 6][2] = mx;
         }
     }
-    uint32_t excl, total;
-    block_scan_n<kThreads>(mine, excl, total, wave_tot);
-    if (tid == kThreads - 64) sbase = total ? atomicAdd(&a.cursor[shard], (unsigned long long)total) : 0ull;
-    if (tid < kStN) {
+    if (tid == 0) s_cnt = 0;
+    __syncthreads();
+    if (tid < kStN && tid != kStInc) {
         unsigned long long v = 0;
         for (int w = 0; w < kThreads / 64; ++w) {
-            const unsigned long long w0 = red[w][0], c2 = red[w][1], mx = red[w][2];
+            const unsigned long long w0 = red[w][0], c2 = red[w][1];
             const unsigned long long x = tid == kStSumS     ? w0 & 0xFFFF
                                          : tid == kStDistinct ? (w0 >> 16) & 0xFFFF
                                          : tid == kStRepeat   ? (w0 >> 32) & 0xFFFF
                                          : tid == kStHeavy    ? w0 >> 48
                                          : tid == kStCdf2     ? c2 & 0xFFFFFFFFull
-                                         : tid == kStInc      ? c2 >> 32
-                                                              : mx;
+                                                              : c2 >> 32;
             v = tid == kStMaxDf ? (v > x ? v : x) : v + x;
         }
         unsigned long long* g = a.gstats + (uint64_t)shard * 8 + tid;  // sharded: no hot word
         if (tid == kStMaxDf) atomicMax(g, v);
         else if (v) atomicAdd(g, v);
     }
-    __syncthreads();
-    // F. write the pair keys.  When the bucket's keys fit (almost always) they are staged in LDS
-    // (H is dead after C) at each element's scanned offset and copied out coalesced; each lane
-    // writing its own short run straight to HBM cost one memory transaction per key (a bucket
-    // kernel without the partner loops ran 151 us instead of 236 us at config 3).
+    // F. the pair keys of every active element (partners j > i; kRows: every partner of a larger
+    // protein), class test fused (mod.rs:580-587).  Appended to an LDS stage (H is dead after C)
+    // with one LDS atomic per key and copied out coalesced with one cursor reservation: the
+    // bucket's order is free, so no count pass and no scan.  A bucket whose pairs pass the stage
+    // (rare) counts, scans and writes them straight to HBM instead.
     unsigned long long* dst = a.out + (uint64_t)shard * a.shard_cap;
     auto partners = [&](auto put) {
 #pragma unroll
         for (int e = 0; e < kE; ++e) {
-            if (!cnt[e]) continue;
+            if (!act[e]) continue;
             const uint32_t i = tid + e * kThreads;
             const uint32_t p = xl[e] >> cb;
             for (uint32_t j = kRows ? s[e] : i + 1; j < en[e]; ++j) {
@@ -950,14 +923,33 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
         }
     };
     constexpr uint32_t kStage = kTab / 2;
+    unsigned long long* stage = reinterpret_cast<unsigned long long*>(H);
+    partners([&](unsigned long long key) {
+        const uint32_t o = atomicAdd(&s_cnt, 1u);
+        if (o < kStage) stage[o] = key;
+    });
+    __syncthreads();
+    const uint32_t total = s_cnt;
     if (total <= kStage) {  // uniform over the workgroup
-        unsigned long long* stage = reinterpret_cast<unsigned long long*>(H);
-        uint32_t lpos = excl;
-        if (mine) partners([&](unsigned long long key) { stage[lpos++] = key; });
+        if (tid == 0 && total) {
+            sbase = atomicAdd(&a.cursor[shard], (unsigned long long)total);
+            atomicAdd(&a.gstats[(uint64_t)shard * 8 + kStInc], (unsigned long long)total);
+        }
         __syncthreads();
         for (uint32_t t = tid; t < total; t += kThreads)
             if (sbase + t < a.shard_cap) dst[sbase + t] = stage[t];
-    } else if (mine) {
+        return;
+    }
+    uint32_t mine = 0;
+    partners([&](unsigned long long) { ++mine; });
+    uint32_t excl, tot2;
+    block_scan_n<kThreads>(mine, excl, tot2, wave_tot);
+    if (tid == 0) {
+        sbase = atomicAdd(&a.cursor[shard], (unsigned long long)tot2);
+        atomicAdd(&a.gstats[(uint64_t)shard * 8 + kStInc], (unsigned long long)tot2);
+    }
+    __syncthreads();
+    if (mine) {
         unsigned long long pos = sbase + excl;
         partners([&](unsigned long long key) {
             if (pos < a.shard_cap) dst[pos] = key;
