@@ -610,9 +610,11 @@ struct BucketArgs {
     uint32_t seg_cap;
 };
 
-__device__ __forceinline__ void spill_segment(const BucketArgs& a, uint64_t pos, uint32_t keys) {
+// descriptor: spill index (40 bits) | keys (23 bits) << 40 | whole bucket (several k-mers) << 63
+__device__ __forceinline__ void spill_segment(const BucketArgs& a, uint64_t pos, uint32_t keys, bool whole) {
     const uint32_t s = atomicAdd(&a.flags[kFlSegs], 1u);
-    if (s < a.seg_cap) a.seg[s] = pos | (unsigned long long)min(keys, 0xFFFFFFu) << 40;
+    if (s < a.seg_cap)
+        a.seg[s] = pos | (unsigned long long)min(keys, 0x7FFFFFu) << 40 | (unsigned long long)whole << 63;
     atomicMax(&a.flags[kFlSegMax], keys);
 }
 
@@ -654,8 +656,7 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
     __shared__ uint32_t gdupw[kCap / 32];  // per group start: the group holds such a duplicate
     __shared__ uint32_t SZ[kHeavySub + 1];
     __shared__ uint32_t wave_tot[kThreads / 64];
-    __shared__ unsigned long long red[kThreads / 64][2];
-    __shared__ uint32_t s_cnt;  // F: keys in the LDS stage
+    __shared__ unsigned long long red[kThreads / 64][3];
     __shared__ unsigned long long sbase;
     __shared__ unsigned long long hbase[kMaxHeavy];  // spill offset of each heavy group
     __shared__ uint32_t nheavy, hkeys;
@@ -682,7 +683,7 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
         __syncthreads();
         if (tid == 0) {
             sbase = atomicAdd(&a.spill_cursor[shard], (unsigned long long)n);
-            spill_segment(a, (uint64_t)shard * a.spill_cap + sbase, n);
+            spill_segment(a, (uint64_t)shard * a.spill_cap + sbase, n, true);
         }
         __syncthreads();
         unsigned long long* dst = a.spill + (uint64_t)shard * a.spill_cap;
@@ -804,7 +805,7 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
             if (spill_dst) {
                 const unsigned long long pos = sbase + hbase[g] + rk[e];
                 if (pos < a.spill_cap) spill_dst[pos] = xk[e];
-                if (rk[e] == 0) spill_segment(a, (uint64_t)shard * a.spill_cap + pos, cn[e]);
+                if (rk[e] == 0) spill_segment(a, (uint64_t)shard * a.spill_cap + pos, cn[e], false);
             }
             continue;
         }
@@ -834,28 +835,49 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
     }
     __syncthreads();
     auto is_dup = [&](uint32_t j) { return (dupw[j >> 5] >> (j & 31)) & 1u; };
-    // E. df and head statistics; act[e]: the element expands (not a duplicate window, df within
-    // heavy_df, and with kRows its protein in the rows).  A group without duplicates (almost all)
-    // has df = its size; a group with one walks the whole group for it.
-    bool act[kE], gd[kE];
-    uint32_t st_sum = single, st_dist = single, st_rep = 0, st_cdf2 = 0, st_max = single ? 1u : 0u, st_heavy = 0;
+    // E. df, head, kept-partner count.  A group without duplicates (almost all) has df = its size
+    // and counts its partners after i only; a group with one walks the whole group.
+    uint32_t cnt[kE];
+    bool gd[kE];
+    uint32_t st_sum = single, st_dist = single, st_rep = 0, st_cdf2 = 0, st_max = single ? 1u : 0u, st_heavy = 0,
+             mine = 0;
 #pragma unroll
     for (int e = 0; e < kE; ++e) {
         const uint32_t i = tid + e * kThreads;
-        act[e] = gd[e] = false;
+        cnt[e] = 0;
+        gd[e] = false;
         if (i >= nm) continue;
         gd[e] = (gdupw[s[e] >> 5] >> (s[e] & 31)) & 1u;
         if (gd[e] && is_dup(i)) continue;
-        uint32_t f = en[e] - s[e];
-        if (gd[e]) {
-            f = 0;
-            for (uint32_t j = s[e]; j < en[e]; ++j) f += !is_dup(j);
-        }
-        act[e] = f <= a.heavy_df;
+        uint32_t f, c = 0;
         if (kRows) {
+            // df, and the partners of a larger protein when this element's protein is in the rows
             const uint32_t p = xl[e] >> cb;
-            act[e] = act[e] && p >= a.row_lo && p < a.row_hi;
+            const bool emit = p >= a.row_lo && p < a.row_hi;
+            f = gd[e] ? 0u : en[e] - s[e];
+            if (emit || gd[e])
+                for (uint32_t j = s[e]; j < en[e]; ++j) {
+                    if (gd[e] && is_dup(j)) continue;
+                    f += gd[e];
+                    const uint32_t lj = Bl[j];
+                    c += emit && (lj >> cb) > p && (!a.require_diff || ((lj ^ xl[e]) & cmask));
+                }
+        } else if (!gd[e]) {
+            f = en[e] - s[e];
+            if (a.require_diff) {
+                for (uint32_t j = i + 1; j < en[e]; ++j) c += ((Bl[j] ^ xl[e]) & cmask) != 0u;
+            } else {
+                c = en[e] - 1 - i;
+            }
+        } else {
+            f = 0;
+            for (uint32_t j = s[e]; j < en[e]; ++j) {
+                if (is_dup(j)) continue;
+                ++f;
+                if (j > i && (!a.require_diff || ((Bl[j] ^ xl[e]) & cmask))) ++c;
+            }
         }
+        if (f > a.heavy_df) c = 0;
         st_sum += 1;
         if (i == s[e]) {  // the group's first position is never a duplicate
             st_dist += 1;
@@ -864,52 +886,59 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
             else st_heavy += f;
             st_max = max(st_max, f);
         }
+        cnt[e] = c;
+        mine += c;
     }
-    // statistics: two wave reductions of packed words (per workgroup every count is at most kCap,
-    // so 16-bit fields cannot carry; C(df,2) stays below 2^32), wave partials -> red, then kStN
-    // threads unpack, sum and post one (sharded) atomic each; the incidences are the stage count
+    // statistics: three wave reductions of packed words (per workgroup every count is at most
+    // kCap, so 16-bit fields cannot carry; C(df,2) and the incidences stay below 2^32), wave
+    // partials -> red, then kStN threads unpack, sum and post one (sharded) atomic each.  They
+    // ride on the output scan's barriers; the last wave reserves the output range meanwhile.
     {
         unsigned long long w0 = st_sum | (unsigned long long)st_dist << 16 | (unsigned long long)st_rep << 32 |
                                 (unsigned long long)st_heavy << 48;
-        unsigned long long c2 = st_cdf2 | (unsigned long long)st_max << 32;
+        unsigned long long c2 = st_cdf2 | (unsigned long long)mine << 32;
+        uint32_t mx = st_max;
         for (int sh = 32; sh > 0; sh >>= 1) {
             w0 += __shfl_down(w0, sh);
-            const unsigned long long o = __shfl_down(c2, sh);
-            c2 = ((c2 & 0xFFFFFFFFull) + (o & 0xFFFFFFFFull)) | (unsigned long long)max(c2 >> 32, o >> 32) << 32;
+            c2 += __shfl_down(c2, sh);
+            mx = max(mx, (uint32_t)__shfl_down(mx, sh));
         }
         if ((tid & 63) == 0) {
             red[tid >> 6][0] = w0;
             red[tid >> 6][1] = c2;
+            red[tid >> 6][2] = mx;
         }
     }
-    if (tid == 0) s_cnt = 0;
-    __syncthreads();
-    if (tid < kStN && tid != kStInc) {
+    uint32_t excl, total;
+    block_scan_n<kThreads>(mine, excl, total, wave_tot);
+    if (tid == kThreads - 64) sbase = total ? atomicAdd(&a.cursor[shard], (unsigned long long)total) : 0ull;
+    if (tid < kStN) {
         unsigned long long v = 0;
         for (int w = 0; w < kThreads / 64; ++w) {
-            const unsigned long long w0 = red[w][0], c2 = red[w][1];
+            const unsigned long long w0 = red[w][0], c2 = red[w][1], mx = red[w][2];
             const unsigned long long x = tid == kStSumS     ? w0 & 0xFFFF
                                          : tid == kStDistinct ? (w0 >> 16) & 0xFFFF
                                          : tid == kStRepeat   ? (w0 >> 32) & 0xFFFF
                                          : tid == kStHeavy    ? w0 >> 48
                                          : tid == kStCdf2     ? c2 & 0xFFFFFFFFull
-                                                              : c2 >> 32;
+                                         : tid == kStInc      ? c2 >> 32
+                                                              : mx;
             v = tid == kStMaxDf ? (v > x ? v : x) : v + x;
         }
         unsigned long long* g = a.gstats + (uint64_t)shard * 8 + tid;  // sharded: no hot word
         if (tid == kStMaxDf) atomicMax(g, v);
         else if (v) atomicAdd(g, v);
     }
-    // F. the pair keys of every active element (partners j > i; kRows: every partner of a larger
-    // protein), class test fused (mod.rs:580-587).  Appended to an LDS stage (H is dead after C)
-    // with one LDS atomic per key and copied out coalesced with one cursor reservation: the
-    // bucket's order is free, so no count pass and no scan.  A bucket whose pairs pass the stage
-    // (rare) counts, scans and writes them straight to HBM instead.
+    __syncthreads();
+    // F. write the pair keys.  When the bucket's keys fit (almost always) they are staged in LDS
+    // (H is dead after C) at each element's scanned offset and copied out coalesced; each lane
+    // writing its own short run straight to HBM cost one memory transaction per key (a bucket
+    // kernel without the partner loops ran 151 us instead of 236 us at config 3).
     unsigned long long* dst = a.out + (uint64_t)shard * a.shard_cap;
     auto partners = [&](auto put) {
 #pragma unroll
         for (int e = 0; e < kE; ++e) {
-            if (!act[e]) continue;
+            if (!cnt[e]) continue;
             const uint32_t i = tid + e * kThreads;
             const uint32_t p = xl[e] >> cb;
             for (uint32_t j = kRows ? s[e] : i + 1; j < en[e]; ++j) {
@@ -923,33 +952,14 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
         }
     };
     constexpr uint32_t kStage = kTab / 2;
-    unsigned long long* stage = reinterpret_cast<unsigned long long*>(H);
-    partners([&](unsigned long long key) {
-        const uint32_t o = atomicAdd(&s_cnt, 1u);
-        if (o < kStage) stage[o] = key;
-    });
-    __syncthreads();
-    const uint32_t total = s_cnt;
     if (total <= kStage) {  // uniform over the workgroup
-        if (tid == 0 && total) {
-            sbase = atomicAdd(&a.cursor[shard], (unsigned long long)total);
-            atomicAdd(&a.gstats[(uint64_t)shard * 8 + kStInc], (unsigned long long)total);
-        }
+        unsigned long long* stage = reinterpret_cast<unsigned long long*>(H);
+        uint32_t lpos = excl;
+        if (mine) partners([&](unsigned long long key) { stage[lpos++] = key; });
         __syncthreads();
         for (uint32_t t = tid; t < total; t += kThreads)
             if (sbase + t < a.shard_cap) dst[sbase + t] = stage[t];
-        return;
-    }
-    uint32_t mine = 0;
-    partners([&](unsigned long long) { ++mine; });
-    uint32_t excl, tot2;
-    block_scan_n<kThreads>(mine, excl, tot2, wave_tot);
-    if (tid == 0) {
-        sbase = atomicAdd(&a.cursor[shard], (unsigned long long)tot2);
-        atomicAdd(&a.gstats[(uint64_t)shard * 8 + kStInc], (unsigned long long)tot2);
-    }
-    __syncthreads();
-    if (mine) {
+    } else if (mine) {
         unsigned long long pos = sbase + excl;
         partners([&](unsigned long long key) {
             if (pos < a.shard_cap) dst[pos] = key;
@@ -1034,27 +1044,65 @@ __global__ void gather_shards_kernel(const unsigned long long* __restrict__ src,
 // bucket, each holding every key of its k-mers.  Each sorted alone, in LDS, and written where the
 // gather would have put it, is the whole sort the heavy path needs (k-mers contiguous, each
 // sorted): no global radix sort (eight onesweep passes over 1M keys at k = 5, 0.3 ms).  One
-// workgroup per segment of (kLo, kN] keys: a bitonic sort of the next power of two (1,024 threads
-// for the large segments: the stages are LDS-latency bound).
-constexpr uint32_t kSegSmall = 2048, kSegLarge = 8192;
-template <uint32_t kLo, uint32_t kN, uint32_t kSegThreads>
-__global__ __launch_bounds__(kSegThreads) void heavy_segsort_kernel(const unsigned long long* __restrict__ spill,
-                                                                    uint64_t spill_cap,
-                                                                    const unsigned long long* __restrict__ cursor,
-                                                                    const unsigned long long* __restrict__ seg,
-                                                                    HeavyOrder ho,
-                                                                    unsigned long long* __restrict__ out) {
+// workgroup per segment.  Above kSegSmall keys: a block radix sort (rocprim, 8-bit digits,
+// 1,024 threads) of the key bits that differ — [0, hshift) for one k-mer (protein and class: four
+// passes instead of eight), every bit for a whole bucket (0.057 ms at config 1 against 0.074 ms
+// for a bitonic sort).
+constexpr uint32_t kSegSmall = 2048, kSegLarge = 8192, kSegItems = 8;
+template <uint32_t kLo, uint32_t kN>
+__global__ __launch_bounds__(kN / kSegItems) void heavy_segsort_kernel(const unsigned long long* __restrict__ spill,
+                                                                       uint64_t spill_cap,
+                                                                       const unsigned long long* __restrict__ cursor,
+                                                                       const unsigned long long* __restrict__ seg,
+                                                                       HeavyOrder ho,
+                                                                       unsigned long long* __restrict__ out) {
+    constexpr uint32_t kThreads = kN / kSegItems;
+    using Sort = rocprim::block_radix_sort<unsigned long long, kThreads, kSegItems>;
+    __shared__ typename Sort::storage_type st;
+    const unsigned long long sd = seg[blockIdx.x];
+    const uint32_t cnt = (uint32_t)(sd >> 40) & 0x7FFFFFu;
+    if (cnt <= kLo || cnt > kN) return;
+    const bool whole = sd >> 63;
+    const uint64_t pos = sd & ((1ull << 40) - 1), shard = pos / spill_cap;
+    uint64_t dst = pos - shard * spill_cap;
+    for (uint64_t t = 0; t < shard; ++t) dst += cursor[t];
+    const unsigned long long cm = (1ull << ho.cb) - 1, hm = ~((1ull << ho.hshift) - 1);
+    unsigned long long k[kSegItems];  // blocked: thread t holds keys t * kSegItems + e
+#pragma unroll
+    for (uint32_t e = 0; e < kSegItems; ++e) {
+        const uint32_t i = threadIdx.x * kSegItems + e;
+        unsigned long long v = ~0ull;  // padding: after every key (the sort is stable)
+        if (i < cnt) {
+            v = spill[pos + i];
+            if (ho.cls) v = (v & hm) | (v & cm) << ho.pbits | ((v & ~hm) >> ho.cb);
+        }
+        k[e] = v;
+    }
+    Sort().sort(k, st, 0, whole ? 64u : ho.hshift);
+#pragma unroll
+    for (uint32_t e = 0; e < kSegItems; ++e) {
+        const uint32_t i = threadIdx.x * kSegItems + e;
+        if (i < cnt) out[dst + i] = k[e];
+    }
+}
+
+// the small segments (<= kSegSmall keys): a bitonic sort of the next power of two, 256 threads
+// (the radix sort's four passes measured 0.081 ms there against 0.064 ms)
+template <uint32_t kN, uint32_t kThreads>
+__global__ __launch_bounds__(kThreads) void heavy_segsort_bitonic_kernel(
+    const unsigned long long* __restrict__ spill, uint64_t spill_cap, const unsigned long long* __restrict__ cursor,
+    const unsigned long long* __restrict__ seg, HeavyOrder ho, unsigned long long* __restrict__ out) {
     __shared__ unsigned long long K[kN];
     const unsigned long long sd = seg[blockIdx.x];
-    const uint32_t cnt = (uint32_t)(sd >> 40);
-    if (cnt <= kLo || cnt > kN) return;
+    const uint32_t cnt = (uint32_t)(sd >> 40) & 0x7FFFFFu;
+    if (cnt > kN) return;
     const uint64_t pos = sd & ((1ull << 40) - 1), shard = pos / spill_cap;
     uint64_t dst = pos - shard * spill_cap;
     for (uint64_t t = 0; t < shard; ++t) dst += cursor[t];
     uint32_t N = 1;
     while (N < cnt) N <<= 1;
     const unsigned long long cm = (1ull << ho.cb) - 1, hm = ~((1ull << ho.hshift) - 1);
-    for (uint32_t i = threadIdx.x; i < N; i += kSegThreads) {
+    for (uint32_t i = threadIdx.x; i < N; i += kThreads) {
         unsigned long long v = ~0ull;  // padding sorts last
         if (i < cnt) {
             v = spill[pos + i];
@@ -1065,7 +1113,7 @@ __global__ __launch_bounds__(kSegThreads) void heavy_segsort_kernel(const unsign
     __syncthreads();
     for (uint32_t k = 2; k <= N; k <<= 1)
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t i = threadIdx.x; i < N / 2; i += kSegThreads) {
+            for (uint32_t i = threadIdx.x; i < N / 2; i += kThreads) {
                 const uint32_t lo = 2 * j * (i / j) + (i % j), hi = lo + j;
                 const unsigned long long x = K[lo], y = K[hi];
                 if ((x > y) == !(lo & k)) {
@@ -1075,7 +1123,7 @@ __global__ __launch_bounds__(kSegThreads) void heavy_segsort_kernel(const unsign
             }
             __syncthreads();
         }
-    for (uint32_t i = threadIdx.x; i < cnt; i += kSegThreads) out[dst + i] = K[i];
+    for (uint32_t i = threadIdx.x; i < cnt; i += kThreads) out[dst + i] = K[i];
 }
 
 // per tile: distinct (h, p) elements, k-mer heads and (class order) class-run heads
@@ -3243,10 +3291,10 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
         const unsigned long long* spill_cursor = ws->bstats.p + kRbSpill;
         if (ws->h_segs && ws->h_segs <= seg_capacity(ws) && ws->h_segmax <= kSegLarge) {
             const uint32_t ns = (uint32_t)ws->h_segs;
-            heavy_segsort_kernel<0, kSegSmall, 256><<<ns, 256, 0, st>>>(ws->spill.p, ws->spill_cap, spill_cursor,
-                                                                          ws->hseg.p, ho, ws->hsorted.p);
+            heavy_segsort_bitonic_kernel<kSegSmall, 256><<<ns, 256, 0, st>>>(
+                ws->spill.p, ws->spill_cap, spill_cursor, ws->hseg.p, ho, ws->hsorted.p);
             if (ws->h_segmax > kSegSmall)
-                heavy_segsort_kernel<kSegSmall, kSegLarge, 1024><<<ns, 1024, 0, st>>>(
+                heavy_segsort_kernel<kSegSmall, kSegLarge><<<ns, kSegLarge / kSegItems, 0, st>>>(
                     ws->spill.p, ws->spill_cap, spill_cursor, ws->hseg.p, ho, ws->hsorted.p);
         } else {  // a segment above the LDS sort: gather and one radix sort
             gather_shards_kernel<<<dim3((uint32_t)std::min<uint64_t>((ws->spill_cap + 255) / 256, 1024), kShards),
