@@ -1000,6 +1000,10 @@ __global__ __launch_bounds__(kThreads) void bucket_large_kernel(BucketArgs a) {
 constexpr uint32_t kHvTile = 4096, kHvThreads = 256, kHvPer = kHvTile / kHvThreads;
 constexpr uint32_t kHvI = 256, kHvJ = 2048, kHvJWrite = 256;
 constexpr uint32_t kHvSpread = 64 * 256;  // a tile with this many pairs spreads them over the shards
+// flat tiles (class order, every pair kept, a k-mer of at most kHvFlatRuns class runs): the
+// k-mer's cross-class pairs (row of run r, any element past r's end) numbered run by run, row by
+// row, cut into kHvFlat-pair tiles: every tile full, nothing per row to plan
+constexpr uint32_t kHvFlat = 1024, kHvFlatRuns = 64, kHvFlatMark = 0xFFFFFFFFu;
 
 // Heavy key order.  Plain: the spilled keys [h | p | class] sorted on (h, p).  Class order (the
 // class test is on): gather_shards rewrites them to [h | class | p] and the sort is on every bit,
@@ -1218,8 +1222,9 @@ __global__ __launch_bounds__(256) void heavy_plan_kernel(const uint32_t* __restr
                                                          const uint64_t* __restrict__ GS, uint64_t ngb,
                                                          const unsigned long long* __restrict__ ng_dev,
                                                          HeavyOrder ho, const uint32_t* __restrict__ RUN,
-                                                         const uint64_t* __restrict__ RH, uint32_t row_lo,
-                                                         uint32_t row_hi, uint32_t heavy_df, int stats,
+                                                         const uint64_t* __restrict__ RH, int flat_ok,
+                                                         uint32_t row_lo, uint32_t row_hi, uint32_t heavy_df,
+                                                         int stats,
                                                          unsigned long long* __restrict__ gstats,
                                                          uint32_t* __restrict__ gi, uint32_t* __restrict__ BT,
                                                          uint32_t* __restrict__ BP,
@@ -1246,7 +1251,19 @@ __global__ __launch_bounds__(256) void heavy_plan_kernel(const uint32_t* __restr
         };
         uint32_t i0 = 0, i1 = 0;
         unsigned long long tiles = 0;
-        if (d >= 2 && d <= heavy_df) {
+        const uint32_t nruns = ho.cls && d ? RUN[b + d - 1] - RUN[b] + 1 : 0u;
+        if (d >= 2 && d <= heavy_df && flat_ok && nruns <= kHvFlatRuns) {
+            // flat: the k-mer's cross-class pairs as one index space, cut into kHvFlat-pair tiles
+            const uint32_t ra = RUN[b];
+            unsigned long long pairs = 0;
+            for (uint32_t r = 0; r < nruns; ++r) {
+                const uint64_t rs = RH[ra + r], re = RH[ra + r + 1];
+                pairs += (re - rs) * (b + d - re);
+            }
+            i0 = kHvFlatMark;
+            i1 = nruns;
+            tiles = (pairs + kHvFlat - 1) / kHvFlat;
+        } else if (d >= 2 && d <= heavy_df) {
             i0 = ho.cls ? 0u : lower(row_lo);
             i1 = ho.cls ? d : lower(row_hi);
             const uint64_t bb = heavy_bbase(b, g);
@@ -1307,6 +1324,8 @@ __global__ __launch_bounds__(kHvI) void heavy_expand_kernel(const uint32_t* __re
     __shared__ uint32_t J[kHvJ];
     __shared__ uint32_t s_ex[kHvI + 1], s_js[kHvI], s_p[kHvI];
     __shared__ unsigned long long s_sb[kShards];  // spread tile: shard base minus its first output
+    __shared__ uint32_t f_s[kHvFlatRuns], f_e[kHvFlatRuns];  // flat tile: the k-mer's runs (local)
+    __shared__ unsigned long long f_c[kHvFlatRuns + 1];       // ... and their first pair's index
     __shared__ uint32_t wave_tot[kHvI / 64];
     __shared__ unsigned long long sbase;
     const uint64_t ng = *ng_dev;
@@ -1314,25 +1333,91 @@ __global__ __launch_bounds__(kHvI) void heavy_expand_kernel(const uint32_t* __re
     const unsigned cb = ho.cb;
     const uint32_t cmask = (1u << cb) - 1;
     const bool test_cls = require_diff && !ho.cls, test_row = ho.cls && ranged;
-    for (unsigned long long t = blockIdx.x; t < T; t += gridDim.x) {
-        // k-mer g: the last with toff[g] <= t
-        uint64_t lo = 0, hi = ng;
+    // workgroup w takes the consecutive tiles [w * per, (w + 1) * per): one binary search for its
+    // first tile's k-mer, then the k-mer and row block advance (a search per tile was a chain of
+    // ~15 dependent loads, the bulk of a tile's time)
+    const unsigned long long per = (T + gridDim.x - 1) / gridDim.x, tb = blockIdx.x * per;
+    const unsigned long long te = min(T, tb + per);
+    uint64_t g = 0;
+    if (tb < te) {
+        uint64_t lo = 0, hi = ng;  // the last k-mer with toff[g] <= tb
         while (lo + 1 < hi) {
             const uint64_t mid = (lo + hi) >> 1;
-            if (toff[mid] <= t) lo = mid;
+            if (toff[mid] <= tb) lo = mid;
             else hi = mid;
         }
-        const uint64_t g = lo, b = GS[g];
+        g = lo;
+    }
+    uint32_t klo = 0;
+    for (unsigned long long t = tb; t < te; ++t) {
+        if (toff[g + 1] <= t) {  // the next k-mer with tiles (toff[ng] = T > t)
+            do ++g;
+            while (toff[g + 1] <= t);
+            klo = 0;
+        }
+        const uint64_t b = GS[g];
         const uint32_t d = (uint32_t)(GS[g + 1] - b), i0 = gi[2 * g], i1 = gi[2 * g + 1];
         const uint32_t local = (uint32_t)(t - toff[g]);
+        if (i0 == kHvFlatMark) {  // flat tile (uniform over the workgroup)
+            const uint32_t nr = i1, ra = RUN[b];
+            __syncthreads();  // the run table's reuse
+            unsigned long long pr = 0;
+            if (threadIdx.x < nr) {
+                const uint32_t rs = (uint32_t)(RH[ra + threadIdx.x] - b), re = (uint32_t)(RH[ra + threadIdx.x + 1] - b);
+                f_s[threadIdx.x] = rs;
+                f_e[threadIdx.x] = re;
+                pr = (unsigned long long)(re - rs) * (d - re);
+            }
+            if (threadIdx.x < 64) {  // exclusive scan of the runs' pair counts (nr <= 64: one wave)
+                unsigned long long incl = pr;
+                for (int sh = 1; sh < 64; sh <<= 1) {
+                    const unsigned long long y = __shfl_up(incl, sh);
+                    if ((int)threadIdx.x >= sh) incl += y;
+                }
+                if (threadIdx.x < nr) f_c[threadIdx.x] = incl - pr;
+                if (threadIdx.x == nr - 1) f_c[nr] = incl;
+            }
+            __syncthreads();
+            const unsigned long long o0 = (unsigned long long)local * kHvFlat, o1 = min(f_c[nr], o0 + kHvFlat);
+            const uint32_t total = (uint32_t)(o1 - o0);
+            uint32_t hx = (E[b] * 0x9E3779B1u) ^ (local * 0xC2B2AE35u) ^ 0x27D4EB2Fu;
+            hx ^= hx >> 16;
+            const uint32_t shard = (hx * 0x7FEB352Du) >> 26;
+            if (threadIdx.x == 0) {
+                sbase = atomicAdd(&cursor[shard], (unsigned long long)total);
+                atomicAdd(&gstats[(uint64_t)shard * 8 + kStInc], (unsigned long long)total);
+            }
+            __syncthreads();
+            unsigned long long* dst = out + (uint64_t)shard * shard_cap;
+            for (uint32_t u = threadIdx.x; u < total; u += kHvI) {
+                const unsigned long long o = o0 + u;
+                uint32_t r = 0, hi = nr;  // the last run with f_c[r] <= o
+                while (r + 1 < hi) {
+                    const uint32_t mid = (r + hi) >> 1;
+                    if (f_c[mid] <= o) r = mid;
+                    else hi = mid;
+                }
+                const unsigned long long off = o - f_c[r];
+                const uint32_t part = d - f_e[r];
+                const uint32_t row = f_s[r] + (uint32_t)(off / part), j = f_e[r] + (uint32_t)(off % part);
+                const uint32_t pa = E[b + row] >> cb, pj = E[b + j] >> cb;
+                const unsigned long long pos = sbase + u;
+                if (pos < shard_cap) dst[pos] = (unsigned long long)min(pa, pj) * mul + max(pa, pj);
+            }
+            continue;
+        }
         // row block: the last with BT <= local (blocks without tiles share the next one's BT)
         const uint64_t bb = heavy_bbase(b, g);
-        uint32_t klo = 0, khi = (i1 - i0 + kHvI - 1) / kHvI;
-        while (klo + 1 < khi) {
-            const uint32_t mid = (klo + khi) >> 1;
-            if (BT[bb + mid] <= local) klo = mid;
-            else khi = mid;
+        const uint32_t nblk = (i1 - i0 + kHvI - 1) / kHvI;
+        if (t == tb) {  // entered mid-k-mer: search
+            uint32_t khi = nblk;
+            while (klo + 1 < khi) {
+                const uint32_t mid = (klo + khi) >> 1;
+                if (BT[bb + mid] <= local) klo = mid;
+                else khi = mid;
+            }
         }
+        while (klo + 1 < nblk && BT[bb + klo + 1] <= local) ++klo;
         const uint32_t r = i0 + klo * kHvI;
         const uint32_t j0 = BP[bb + klo] + (local - BT[bb + klo]) * ho.hj, j1 = min(d, j0 + ho.hj);
         __syncthreads();  // J reuse
@@ -3344,7 +3429,8 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
     const uint64_t* RH = ho.cls ? reinterpret_cast<const uint64_t*>(ws->hRH.p) : nullptr;
     const uint32_t* RUN = ho.cls ? ws->hrun.p : nullptr;
     heavy_plan_kernel<<<(uint32_t)((ngb + 1 + 255) / 256), 256, 0, st>>>(
-        ws->hE.p, GS, ngb + 1, ws->h_tot + 1, ho, RUN, RH, row_lo, row_hi, c.heavy_df, stats ? 1 : 0, ws->bstats.p,
+        ws->hE.p, GS, ngb + 1, ws->h_tot + 1, ho, RUN, RH, ho.cls && !c.ranged ? 1 : 0, row_lo, row_hi, c.heavy_df,
+        stats ? 1 : 0, ws->bstats.p,
         ws->hgi.p, BT, BP, ws->htc.p);
     size_t t2 = 0;
     PG(rocprim::exclusive_scan(nullptr, t2, ws->htc.p, ws->htoff.p, 0ull, (size_t)ngb + 1,
