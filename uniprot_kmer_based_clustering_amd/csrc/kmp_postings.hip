@@ -2584,10 +2584,12 @@ int front_flat(kmp_postings* ws, uint64_t slots, const Layout& lay, const uint16
 // ------------------------------------------------------------- row-block tail -------------
 // combine_edges (mod.rs:322-546) without a global pair-key sort.  Pair keys are p << pbits | q
 // (p < q); row block r = rows [row0 + (r << rbits), row0 + ((r + 1) << rbits)).
-//   pt_hist     per 16,384-key tile of each shard region: row-block histogram -> H[tile][r]
-//   column scan (bp_colsum, pt_colscan, bp_colprefix) -> P[tile][r] and the block starts
+//   pt_hist     per 16,384-key tile of each shard region: row-block histogram added to the
+//               totals T[r]
+//   pt_tscan    one workgroup: block starts bst[r] and the scatter's cursors from T
 //   pt_scatter  per tile: keys ranked by row block in LDS and written as u32
-//               (p_local << pbits | q), one run per row block at P[tile][r]
+//               (p_local << pbits | q), one run per row block reserved on the block's cursor
+//               (the former per-tile column scan, three kernels, gone: pair partition 0.043 -> 0.026 ms at config 3)
 //   pt_reduce   one workgroup per row block: LDS radix sort of its keys (rocprim
 //               block_radix_sort), run-length encode (run = one (p, q) pair, length = w), runs
 //               with w >= min_shared staged at the block's input offset, kept-run count per block
@@ -2618,9 +2620,11 @@ __device__ __forceinline__ uint32_t pt_tile_keys(const unsigned long long* __res
     return t0 < ns ? (uint32_t)min<uint64_t>(kPtTile, ns - t0) : 0u;
 }
 
+// per 16,384-key tile of each shard region: its keys counted per row block in LDS and added to
+// the row-block totals T (one global atomic per nonzero count)
 __global__ __launch_bounds__(kPtThreads) void pt_hist_kernel(const unsigned long long* __restrict__ in,
                                                              const unsigned long long* __restrict__ cursor, PtGeom g,
-                                                             uint32_t* __restrict__ H) {
+                                                             uint32_t* __restrict__ T) {
     __shared__ uint32_t lh[kPtMaxBlocks];
     const uint32_t j = blockIdx.x, s = blockIdx.y;
     for (uint32_t r = threadIdx.x; r < g.nrb; r += kPtThreads) lh[r] = 0;
@@ -2635,80 +2639,53 @@ __global__ __launch_bounds__(kPtThreads) void pt_hist_kernel(const unsigned long
         if (x != kNoKey) atomicAdd(&lh[(uint32_t)((x - base) >> sh)], 1u);
     }
     __syncthreads();
-    uint32_t* row = H + (uint64_t)(s * g.jt + j) * g.nrb;
-    for (uint32_t r = threadIdx.x; r < g.nrb; r += kPtThreads) row[r] = lh[r];
+    for (uint32_t r = threadIdx.x; r < g.nrb; r += kPtThreads)
+        if (lh[r]) atomicAdd(&T[r], lh[r]);
 }
 
-// column starts of a [rows][cols] matrix already summed into row groups (R, bp_colsum): per
-// column an exclusive scan down the groups plus the column's start, in place; colstart[c] and
-// colstart[cols] = total; *colmax = the largest column total.  cols <= 8 * 1024 (each thread owns
-// up to 8 consecutive columns).
 constexpr int kPtScanThreads = 1024;
-__global__ __launch_bounds__(kPtScanThreads) void pt_colscan_kernel(uint32_t* __restrict__ R, uint32_t groups,
-                                                                    uint32_t cols, uint32_t* __restrict__ colstart,
-                                                                    uint32_t* __restrict__ colmax) {
+// row-block starts from the totals (one workgroup): bst[r] (bst[nrb] = total), the scatter's
+// cursors cur[r] = bst[r], *colmax = the largest block; T is zeroed for the next step (it is
+// zero when allocated, so pt_hist's atomics always start from zero)
+__global__ __launch_bounds__(kPtScanThreads) void pt_tscan_kernel(uint32_t* __restrict__ T, uint32_t nrb,
+                                                                  uint32_t* __restrict__ bst,
+                                                                  uint32_t* __restrict__ cur,
+                                                                  uint32_t* __restrict__ colmax) {
     __shared__ uint32_t wave_tot[kPtScanThreads / 64];
     __shared__ uint32_t s_max;
     if (threadIdx.x == 0) s_max = 0;
-    const uint32_t q = (cols + kPtScanThreads - 1) / kPtScanThreads, c0 = threadIdx.x * q;
-    constexpr uint32_t kG = 8;  // up to kG row groups: every load of the thread in flight at once
-    const bool small = groups <= kG;
-    uint32_t v[8][kG];
-    uint32_t tot[8], sum = 0;
+    const uint32_t q = (nrb + kPtScanThreads - 1) / kPtScanThreads, c0 = threadIdx.x * q;
+    uint32_t v[8], sum = 0, mx = 0;
 #pragma unroll
     for (uint32_t i = 0; i < 8; ++i) {
-        tot[i] = 0;
-        const uint32_t c = c0 + i;
-        const bool on = i < q && c < cols;
-#pragma unroll
-        for (uint32_t g = 0; g < kG; ++g) v[i][g] = small && on && g < groups ? R[(uint64_t)g * cols + c] : 0u;
+        v[i] = i < q && c0 + i < nrb ? T[c0 + i] : 0u;
+        sum += v[i];
+        mx = max(mx, v[i]);
     }
-#pragma unroll
-    for (uint32_t i = 0; i < 8; ++i) {
-        const uint32_t c = c0 + i;
-        if (i >= q || c >= cols) continue;
-        if (small) {
-#pragma unroll
-            for (uint32_t g = 0; g < kG; ++g) tot[i] += v[i][g];
-        } else {
-            tot[i] = col_sum(R + c, cols, groups);
-        }
-        sum += tot[i];
-    }
-    uint32_t mx = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < 8; ++i) mx = max(mx, tot[i]);
     __syncthreads();
     if (mx) atomicMax(&s_max, mx);
     uint32_t excl, total;
     block_scan_n<kPtScanThreads>(sum, excl, total, wave_tot);  // barriers: s_max complete
 #pragma unroll
-    for (uint32_t i = 0; i < 8; ++i) {
-        const uint32_t c = c0 + i;
-        if (i >= q || c >= cols) continue;
-        colstart[c] = excl;
-        if (small) {
-            uint32_t run = excl;
-#pragma unroll
-            for (uint32_t g = 0; g < kG; ++g)
-                if (g < groups) {
-                    R[(uint64_t)g * cols + c] = run;
-                    run += v[i][g];
-                }
-        } else {
-            col_prefix_inplace(R + c, cols, groups, excl);
+    for (uint32_t i = 0; i < 8; ++i)
+        if (i < q && c0 + i < nrb) {
+            bst[c0 + i] = excl;
+            cur[c0 + i] = excl;
+            T[c0 + i] = 0;
+            excl += v[i];
         }
-        excl += tot[i];
-    }
     if (threadIdx.x == 0) {
-        colstart[cols] = total;
+        bst[nrb] = total;
         *colmax = s_max;
     }
 }
 
+// the tile's keys ranked by row block in LDS, each block's run reserved with one returning
+// atomic on the block's cursor (order inside a block is free: pt_reduce sorts it), written as u32
+// (p - r * 2^rbits) << pbits | q
 __global__ __launch_bounds__(kPtThreads) void pt_scatter_kernel(const unsigned long long* __restrict__ in,
                                                                 const unsigned long long* __restrict__ cursor,
-                                                                PtGeom g, const uint32_t* __restrict__ P,
+                                                                PtGeom g, uint32_t* __restrict__ cur,
                                                                 uint32_t* __restrict__ out) {
     __shared__ uint32_t lh[kPtMaxBlocks];
     __shared__ uint32_t S[kPtTile];
@@ -2742,7 +2719,18 @@ __global__ __launch_bounds__(kPtThreads) void pt_scatter_kernel(const unsigned l
     }
     if (nk) atomicAdd(&s_n, nk);
     __syncthreads();
+    constexpr uint32_t kQ = kPtMaxBlocks / kPtThreads;
+    uint32_t cnt[kQ];
+#pragma unroll
+    for (uint32_t t = 0; t < kQ; ++t) {
+        const uint32_t r = threadIdx.x + t * kPtThreads;
+        cnt[t] = r < g.nrb ? lh[r] : 0u;
+    }
     lds_bins_scan<kPtThreads>(lh, g.nrb, wave_tot);
+    uint32_t rbase[kQ];
+#pragma unroll
+    for (uint32_t t = 0; t < kQ; ++t)  // reserved while the tile is placed
+        rbase[t] = cnt[t] ? atomicAdd(&cur[threadIdx.x + t * kPtThreads], cnt[t]) : 0u;
 #pragma unroll
     for (uint32_t e = 0; e < kPtPer; ++e)
         if (x[e] != kNoKey) {
@@ -2751,8 +2739,11 @@ __global__ __launch_bounds__(kPtThreads) void pt_scatter_kernel(const unsigned l
             SR[pos] = (uint16_t)r;
         }
     __syncthreads();
-    const uint32_t* prow = P + (uint64_t)(s * g.jt + j) * g.nrb;
-    for (uint32_t r = threadIdx.x; r < g.nrb; r += kPtThreads) lh[r] = prow[r] - lh[r];
+#pragma unroll
+    for (uint32_t t = 0; t < kQ; ++t) {
+        const uint32_t r = threadIdx.x + t * kPtThreads;
+        if (r < g.nrb) lh[r] = rbase[t] - lh[r];
+    }
     __syncthreads();
     const uint32_t placed = s_n;  // m counts the kNoKey padding of a flat array too
     for (uint32_t i = threadIdx.x; i < placed; i += kPtThreads) out[lh[SR[i]] + i] = S[i];
@@ -3143,19 +3134,19 @@ bool pt_geometry(const kmp_postings* ws, const StepCfg& c, uint64_t inc, PtGeom*
 
 // ws->pt: H | P | R | block starts (nrb + 1) | run counts (nrb) | edge offsets (nrb + 1)
 struct PtBufs {
-    uint32_t *H, *P, *R, *bst, *counts, *eoff;
-    uint32_t rows, groups;
+    uint32_t *T, *cur, *bst, *counts, *eoff;  // row-block totals | scatter cursors | starts | runs | edge offsets
 };
 PtBufs pt_bufs(kmp_postings* ws, const PtGeom& g, bool reserve, hipError_t* e) {
     PtBufs b{};
-    b.rows = g.nshards * g.jt;
-    b.groups = (b.rows + kBpRowGroup - 1) / kBpRowGroup;
-    const uint64_t h = (uint64_t)b.rows * g.nrb, r = (uint64_t)b.groups * g.nrb;
-    if (reserve) *e = ws->pt.reserve(2 * h + r + 3 * (uint64_t)g.nrb + 2);
-    b.H = ws->pt.p;
-    b.P = b.H + h;
-    b.R = b.P + h;
-    b.bst = b.R + r;
+    if (reserve) {
+        const void* before = ws->pt.p;
+        *e = ws->pt.reserve(2 * (uint64_t)kPtMaxBlocks + 3 * (uint64_t)g.nrb + 2);
+        // T (row-block totals) must be zero: pt_tscan re-zeroes what it used, a new buffer is cleared
+        if (*e == hipSuccess && ws->pt.p != before) *e = hipMemset(ws->pt.p, 0, kPtMaxBlocks * sizeof(uint32_t));
+    }
+    b.T = ws->pt.p;
+    b.cur = b.T + kPtMaxBlocks;
+    b.bst = b.cur + kPtMaxBlocks;
     b.counts = b.bst + g.nrb + 1;
     b.eoff = b.counts + g.nrb;
     return b;
@@ -3255,12 +3246,10 @@ int enqueue_tail_in(kmp_postings* ws, const StepCfg& c, const PtGeom& g, const u
     uint32_t* keys32 = reinterpret_cast<uint32_t*>(ws->inc.p);
     uint32_t* stage_p = reinterpret_cast<uint32_t*>(ws->uniq.p);
     uint32_t* stage_q = stage_p + total;
-    pt_hist_kernel<<<dim3(g.jt, g.nshards), kPtThreads, 0, st>>>(in, cursor, g, b.H);
-    bp_colsum_kernel<<<dim3(b.groups, (g.nrb + 255) / 256), 256, 0, st>>>(b.H, b.rows, g.nrb, b.R);
-    pt_colscan_kernel<<<1, kPtScanThreads, 0, st>>>(b.R, b.groups, g.nrb, b.bst, ws->small.p + 2);
-    bp_colprefix_kernel<<<dim3(b.groups, (g.nrb + 255) / 256), 256, 0, st>>>(b.H, b.rows, g.nrb, b.R, b.P);
+    pt_hist_kernel<<<dim3(g.jt, g.nshards), kPtThreads, 0, st>>>(in, cursor, g, b.T);
+    pt_tscan_kernel<<<1, kPtScanThreads, 0, st>>>(b.T, g.nrb, b.bst, b.cur, ws->small.p + 2);
     ws->mark(4, st);
-    pt_scatter_kernel<<<dim3(g.jt, g.nshards), kPtThreads, 0, st>>>(in, cursor, g, b.P, keys32);
+    pt_scatter_kernel<<<dim3(g.jt, g.nshards), kPtThreads, 0, st>>>(in, cursor, g, b.cur, keys32);
     pt_reduce_kernel<<<g.nrb, kPtRThreads, 0, st>>>(keys32, b.bst, g, ws->flags.p, ws->ovf.p, stage_p, stage_q,
                                                     ws->w.p, b.counts);
     if (pt_rowhist_ok(g))  // one-row blocks above kPtCap: finished here (none listed: every workgroup exits)
