@@ -186,6 +186,20 @@ __global__ void chunk_first_kernel(const uint64_t* __restrict__ res_off, uint32_
     for (uint64_t c = (b + kKeyChunk - 1) / kKeyChunk; c * kKeyChunk < e && c < n_chunks; ++c) first[c] = p;
 }
 
+// chunk_first_kernel (proteins [0, p_hi]) fused with the clear of the cursor level 2's bucket
+// counts (one launch less per step)
+__global__ void chunk_first_clear_kernel(const uint64_t* __restrict__ res_off, uint32_t p_hi, uint64_t slot_end,
+                                         uint32_t n_chunks, uint32_t* __restrict__ first,
+                                         uint32_t* __restrict__ cur, uint32_t ncur) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint32_t i = t; i < ncur; i += gridDim.x * blockDim.x) cur[i] = 0;
+    const uint32_t p = t;
+    if (p > p_hi) return;
+    const uint64_t b = set_base(res_off[p], p);
+    const uint64_t e = p < p_hi ? set_base(res_off[p + 1], p + 1) : slot_end;
+    for (uint64_t c = (b + kKeyChunk - 1) / kKeyChunk; c * kKeyChunk < e && c < n_chunks; ++c) first[c] = p;
+}
+
 // LDS state of one key chunk: residue codes of the chunk's span and its proteins' geometry
 struct KeyChunk {
     uint8_t lut[256];
@@ -2424,9 +2438,16 @@ hipError_t bp_level1(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_r
     if (e != hipSuccess) return e;
     uint32_t *H1 = ws->bp.p, *P1 = H1 + h1, *R = P1 + h1, *C1 = R + r;
     ws->bp_c1 = 2 * h1 + r;
-    chunk_first_kernel<<<(n + 1 + 255) / 256, 256, 0, st>>>(d_res_off, 0u, n, 0ull, slots, G, ws->chunk_first.p);
     const uint32_t pw21 = (uint32_t)pow21(k - 1);
     ws->bp_local = ws->cur_used;
+    const uint32_t nb = 1u << lay.bbits;
+    if (ws->bp_local) e = ws->cur.reserve(nb);
+    if (e != hipSuccess) return e;
+    if (ws->bp_local)  // the cursor level 2's bucket counts cleared here (bp_level2c does not)
+        chunk_first_clear_kernel<<<(n + 1 + 255) / 256, 256, 0, st>>>(d_res_off, n, slots, G, ws->chunk_first.p,
+                                                                    ws->cur.p, nb);
+    else
+        chunk_first_kernel<<<(n + 1 + 255) / 256, 256, 0, st>>>(d_res_off, 0u, n, 0ull, slots, G, ws->chunk_first.p);
     if (ws->bp_local) {  // local level 1 for the cursor level 2: H1 | H1T (own digits)
         ws->bp_G = G;
         ws->bp_h1t = h1;
@@ -2488,7 +2509,8 @@ int bp_level2c(kmp_postings* ws, const Layout& lay, hipStream_t st) {
     PG(ws->cnt.reserve(2 * (uint64_t)nb + 2));  // the large-bucket list
     uint32_t c0, c1;
     own_bins(ws, dg, &c0, &c1);
-    bp_cur_clear_kernel<<<std::min<uint32_t>((nb + 1023) / 1024, 1024), 1024, 0, st>>>(ws->cur.p, nb);
+    if (!ws->bp_local)  // the local level 1 cleared the counts with its chunk_first
+        bp_cur_clear_kernel<<<std::min<uint32_t>((nb + 1023) / 1024, 1024), 1024, 0, st>>>(ws->cur.p, nb);
     if (c1 > c0 && ws->bp_local) {
         const uint32_t ntiles = (ws->bp_G + ws->bp_T - 1) / ws->bp_T, per = (ntiles * (c1 - c0) + 7) / 8;
         bp_scatter2g_kernel<kBpGatherTile / kKeyThreads><<<8 * per, kKeyThreads, 0, st>>>(ws->keys.p, ws->bp.p + ws->bp_h1t, ws->bp_G, ws->bp_T,
