@@ -3050,6 +3050,18 @@ __global__ __launch_bounds__(kPtScanThreads) void pt_offsets_kernel(const uint32
     }
 }
 
+__device__ void step_pack_body(const unsigned long long* __restrict__ gstats, const uint32_t* __restrict__ flags,
+                               const uint32_t* __restrict__ runs, unsigned long long* __restrict__ rb);
+
+// pack: nonzero -> workgroup 0 also writes the step's read-back (step_pack_kernel's work: every
+// input of it is final once pt_offsets has run)
+struct PtPack {
+    const unsigned long long* gstats;
+    const uint32_t* flags;
+    const uint32_t* runs;
+    unsigned long long* rb;
+};
+
 __global__ __launch_bounds__(256) void pt_emit_kernel(const uint32_t* __restrict__ stage_p,
                                                       const uint32_t* __restrict__ stage_q,
                                                       const uint32_t* __restrict__ stage_w,
@@ -3057,7 +3069,8 @@ __global__ __launch_bounds__(256) void pt_emit_kernel(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ counts,
                                                       const uint32_t* __restrict__ eoff, uint32_t* __restrict__ d_p,
                                                       uint32_t* __restrict__ d_q, uint32_t* __restrict__ d_w,
-                                                      uint64_t cap, uint32_t stride = 1) {
+                                                      uint64_t cap, uint32_t stride = 1, PtPack pack = {}) {
+    if (pack.rb && blockIdx.x == 0) step_pack_body(pack.gstats, pack.flags, pack.runs, pack.rb);
     const uint32_t r = blockIdx.x, s0 = bst[r], m = counts[r];
     const uint64_t o = eoff[r];
     for (uint32_t i = threadIdx.x; i < m; i += 256) {
@@ -3097,6 +3110,11 @@ __global__ void step_clear_kernel(uint32_t* __restrict__ flags, unsigned long lo
 
 __global__ void step_pack_kernel(const unsigned long long* __restrict__ gstats, const uint32_t* __restrict__ flags,
                                  const uint32_t* __restrict__ runs, unsigned long long* __restrict__ rb) {
+    step_pack_body(gstats, flags, runs, rb);
+}
+
+__device__ void step_pack_body(const unsigned long long* __restrict__ gstats, const uint32_t* __restrict__ flags,
+                               const uint32_t* __restrict__ runs, unsigned long long* __restrict__ rb) {
     for (uint32_t i = threadIdx.x; i < kGsWords; i += blockDim.x) rb[i] = gstats[i];
     if (threadIdx.x == 0) {
         rb[kRbFlagBin] = flags[kFlBin];
@@ -3280,8 +3298,8 @@ int enqueue_tail_in(kmp_postings* ws, const StepCfg& c, const PtGeom& g, const u
     ws->mark(5, st);
     pt_offsets_kernel<<<1, kPtScanThreads, 0, st>>>(b.counts, g.nrb, b.eoff, ws->small.p + 1);
     pt_emit_kernel<<<g.nrb, 256, 0, st>>>(stage_p, stage_q, ws->w.p, b.bst, b.counts, b.eoff, c.d_p, c.d_q, c.d_w,
-                                          c.cap, c.stride);
-    step_pack_kernel<<<1, 256, 0, st>>>(ws->bstats.p, ws->flags.p, ws->small.p + 1, ws->hrb);
+                                          c.cap, c.stride,
+                                          PtPack{ws->bstats.p, ws->flags.p, ws->small.p + 1, ws->hrb});  // + read-back
     ws->mark(6, st);
     PG(hipGetLastError());
     return KMP_OK;
