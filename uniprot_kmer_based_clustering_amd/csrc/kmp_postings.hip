@@ -3069,10 +3069,26 @@ __global__ __launch_bounds__(256) void pt_emit_kernel(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ counts,
                                                       const uint32_t* __restrict__ eoff, uint32_t* __restrict__ d_p,
                                                       uint32_t* __restrict__ d_q, uint32_t* __restrict__ d_w,
-                                                      uint64_t cap, uint32_t stride = 1, PtPack pack = {}) {
-    if (pack.rb && blockIdx.x == 0) step_pack_body(pack.gstats, pack.flags, pack.runs, pack.rb);
+                                                      uint64_t cap, uint32_t stride = 1, PtPack pack = {},
+                                                      uint32_t* __restrict__ total_out = nullptr) {
     const uint32_t r = blockIdx.x, s0 = bst[r], m = counts[r];
-    const uint64_t o = eoff[r];
+    uint64_t o;
+    if (eoff) {
+        o = eoff[r];
+    } else {
+        // no pt_offsets: this block's offset = the runs of the blocks before it (block 0: the
+        // total, for the read-back)
+        __shared__ uint32_t wave_tot[256 / 64];
+        const uint32_t lim = r ? r : gridDim.x;
+        uint32_t v = 0;
+        for (uint32_t i = threadIdx.x; i < lim; i += 256) v += counts[i];
+        uint32_t excl, tot;
+        block_scan_n<256>(v, excl, tot, wave_tot);
+        o = r ? tot : 0u;
+        if (r == 0 && threadIdx.x == 0) *total_out = tot;
+        if (r == 0) __syncthreads();  // the total is in memory before the pack reads it
+    }
+    if (pack.rb && blockIdx.x == 0) step_pack_body(pack.gstats, pack.flags, pack.runs, pack.rb);
     for (uint32_t i = threadIdx.x; i < m; i += 256) {
         if (o + i >= cap) break;
         d_p[(o + i) * stride] = stage_p[s0 + i];
@@ -3296,10 +3312,10 @@ int enqueue_tail_in(kmp_postings* ws, const StepCfg& c, const PtGeom& g, const u
         pt_rowhist_kernel<<<kRowHistGrid, kRowHistThreads, 0, st>>>(keys32, b.bst, g, ws->flags.p, ws->ovf.p,
                                                                     stage_p, stage_q, ws->w.p, b.counts);
     ws->mark(5, st);
-    pt_offsets_kernel<<<1, kPtScanThreads, 0, st>>>(b.counts, g.nrb, b.eoff, ws->small.p + 1);
-    pt_emit_kernel<<<g.nrb, 256, 0, st>>>(stage_p, stage_q, ws->w.p, b.bst, b.counts, b.eoff, c.d_p, c.d_q, c.d_w,
-                                          c.cap, c.stride,
-                                          PtPack{ws->bstats.p, ws->flags.p, ws->small.p + 1, ws->hrb});  // + read-back
+    // edge offsets computed by the emit blocks themselves (no pt_offsets launch); + read-back
+    pt_emit_kernel<<<g.nrb, 256, 0, st>>>(stage_p, stage_q, ws->w.p, b.bst, b.counts, nullptr, c.d_p, c.d_q, c.d_w,
+                                          c.cap, c.stride, PtPack{ws->bstats.p, ws->flags.p, ws->small.p + 1, ws->hrb},
+                                          ws->small.p + 1);
     ws->mark(6, st);
     PG(hipGetLastError());
     return KMP_OK;
