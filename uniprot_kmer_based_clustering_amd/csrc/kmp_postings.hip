@@ -3396,6 +3396,46 @@ __global__ void heavy_sentinel_kernel(const unsigned long long* __restrict__ tot
     if (threadIdx.x == 1 && RH) RH[tot[2]] = tot[0];
 }
 
+// one workgroup: exclusive scans of the per-tile counts (elements | k-mers | runs, na arrays of nt
+// <= kHvScanMax), their totals in tot, and the sentinels GS[ng] = RH[nr] = ne (compact writes
+// the entries before them); in place of na device-wide scans + heavy_totals + heavy_sentinel
+constexpr uint32_t kHvScanThreads = 1024, kHvScanMax = 8 * kHvScanThreads;
+__global__ __launch_bounds__(kHvScanThreads) void heavy_tscan_kernel(const uint32_t* __restrict__ cnt, uint32_t nt,
+                                                                     uint32_t na, unsigned long long* __restrict__ off,
+                                                                     unsigned long long* __restrict__ tot,
+                                                                     uint64_t* __restrict__ GS,
+                                                                     uint64_t* __restrict__ RH) {
+    __shared__ uint32_t wave_tot[kHvScanThreads / 64];
+    __shared__ unsigned long long s_tot[3];
+    const uint32_t q = (nt + kHvScanThreads - 1) / kHvScanThreads, c0 = threadIdx.x * q;
+    for (uint32_t a = 0; a < na; ++a) {
+        uint32_t v[8], sum = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 8; ++i) {
+            v[i] = i < q && c0 + i < nt ? cnt[a * nt + c0 + i] : 0u;
+            sum += v[i];
+        }
+        uint32_t excl, total;  // per-tile counts are <= 4,096 and nt <= 8,192: u32 totals
+        block_scan_n<kHvScanThreads>(sum, excl, total, wave_tot);
+#pragma unroll
+        for (uint32_t i = 0; i < 8; ++i)
+            if (i < q && c0 + i < nt) {
+                off[a * (nt + 1) + c0 + i] = excl;
+                excl += v[i];
+            }
+        if (threadIdx.x == 0) {
+            tot[a] = total;
+            s_tot[a] = total;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (na < 3) tot[2] = 0;
+        GS[s_tot[1]] = s_tot[0];
+        if (RH && na == 3) RH[s_tot[2]] = s_tot[0];
+    }
+}
+
 int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipStream_t st) {
     const Layout& lay = c.lay;
     HeavyOrder ho{};
@@ -3440,20 +3480,27 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
         unsigned long long* off = ws->hoff.p;   // their exclusive scans, nt + 1 apart
         unsigned long long* tot = off + 3 * (nt + 1);
         heavy_scan_kernel<<<(uint32_t)nt, kHvThreads, 0, st>>>(ws->hsorted.p, m, ho, cnt, cnt + nt, cnt + 2 * nt);
-        size_t t1 = 0;
-        PG(rocprim::exclusive_scan(nullptr, t1, cnt, off, 0ull, (size_t)nt, rocprim::plus<unsigned long long>(), st));
-        PG(ws->tmp.reserve(std::max(t1, ws->tmp.n)));
-        for (int a = 0; a < (ho.cls ? 3 : 2); ++a)
-            PG(rocprim::exclusive_scan(ws->tmp.p, t1, cnt + a * nt, off + a * (nt + 1), 0ull, (size_t)nt,
-                                       rocprim::plus<unsigned long long>(), st));
-        heavy_totals_kernel<<<1, 64, 0, st>>>(cnt, off, nt, tot);
         uint64_t* GS = reinterpret_cast<uint64_t*>(ws->hGS.p);
         uint64_t* RH = ho.cls ? reinterpret_cast<uint64_t*>(ws->hRH.p) : nullptr;
+        const uint32_t na = ho.cls ? 3 : 2;
+        const bool one_wg = nt <= kHvScanMax;
+        if (one_wg) {
+            heavy_tscan_kernel<<<1, kHvScanThreads, 0, st>>>(cnt, (uint32_t)nt, na, off, tot, GS, RH);
+        } else {
+            size_t t1 = 0;
+            PG(rocprim::exclusive_scan(nullptr, t1, cnt, off, 0ull, (size_t)nt, rocprim::plus<unsigned long long>(),
+                                       st));
+            PG(ws->tmp.reserve(std::max(t1, ws->tmp.n)));
+            for (uint32_t a = 0; a < na; ++a)
+                PG(rocprim::exclusive_scan(ws->tmp.p, t1, cnt + a * nt, off + a * (nt + 1), 0ull, (size_t)nt,
+                                           rocprim::plus<unsigned long long>(), st));
+            heavy_totals_kernel<<<1, 64, 0, st>>>(cnt, off, nt, tot);
+        }
         heavy_compact_kernel<<<(uint32_t)nt, kHvThreads, 0, st>>>(
             ws->hsorted.p, m, ho, reinterpret_cast<const uint64_t*>(off),
             reinterpret_cast<const uint64_t*>(off + nt + 1), reinterpret_cast<const uint64_t*>(off + 2 * (nt + 1)),
             ws->hE.p, GS, ho.cls ? ws->hrun.p : nullptr, RH);
-        heavy_sentinel_kernel<<<1, 64, 0, st>>>(tot, GS, RH);
+        if (!one_wg) heavy_sentinel_kernel<<<1, 64, 0, st>>>(tot, GS, RH);
         PG(hipGetLastError());
         ws->heavy_ready = true;
         ws->h_m = m;
