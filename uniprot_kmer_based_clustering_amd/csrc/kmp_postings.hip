@@ -2374,6 +2374,8 @@ struct kmp_postings {
     // read-back of a step (kRb* layout), written by the pack kernel into coherent pinned memory
     unsigned long long* hrb = nullptr;
     hipEvent_t ev[KMP_POSTINGS_STAGES + 1] = {};
+    const uint32_t* pt_zero_p = nullptr;  // the pt allocation whose totals T were cleared
+    size_t pt_zero_n = 0;
     ~kmp_postings() {
         for (auto* g : {&keys, &sorted, &inc, &inc_sorted, &uniq, &bstats, &btot, &boff, &spill, &hkeys, &hsorted,
                         &hGS, &htc, &htoff, &hoff, &hRH, &hseg, &ovk, &ovx, &split_cur})
@@ -3195,10 +3197,14 @@ struct PtBufs {
 PtBufs pt_bufs(kmp_postings* ws, const PtGeom& g, bool reserve, hipError_t* e) {
     PtBufs b{};
     if (reserve) {
-        const void* before = ws->pt.p;
         *e = ws->pt.reserve(2 * (uint64_t)kPtMaxBlocks + 3 * (uint64_t)g.nrb + 2);
-        // T (row-block totals) must be zero: pt_tscan re-zeroes what it used, a new buffer is cleared
-        if (*e == hipSuccess && ws->pt.p != before) *e = hipMemset(ws->pt.p, 0, kPtMaxBlocks * sizeof(uint32_t));
+        // T (row-block totals) must be zero: pt_tscan re-zeroes what it used, a new allocation
+        // (a new pointer or capacity: reserve only reallocates to grow) is cleared once
+        if (*e == hipSuccess && (ws->pt_zero_p != ws->pt.p || ws->pt_zero_n != ws->pt.n)) {
+            *e = hipMemset(ws->pt.p, 0, kPtMaxBlocks * sizeof(uint32_t));
+            ws->pt_zero_p = ws->pt.p;
+            ws->pt_zero_n = ws->pt.n;
+        }
     }
     b.T = ws->pt.p;
     b.cur = b.T + kPtMaxBlocks;
