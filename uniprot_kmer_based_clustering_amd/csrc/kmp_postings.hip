@@ -2453,9 +2453,9 @@ hipError_t bp_level1(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_r
     if (ws->bp_local) {  // local level 1 for the cursor level 2: H1 | H1T (own digits)
         ws->bp_G = G;
         ws->bp_h1t = h1;
-        // T chunks per level-2 tile: ~7/8 of a tile at the hash-uniform mean (kKeyChunk / nb1 keys
+        // T chunks per level-2 tile: ~7/4 of a round at the hash-uniform mean (two rounds; kKeyChunk / nb1 keys
         // per chunk and bin)
-        ws->bp_T = std::min<uint32_t>(kBpGatherMax, std::max<uint32_t>(1, kBpGatherTile * 7 / 8 * dg.nb1 / kKeyChunk));
+        ws->bp_T = std::min<uint32_t>(kBpGatherMax, std::max<uint32_t>(1, kBpGatherTile * 7 / 4 * dg.nb1 / kKeyChunk));
         bp_scatter1l_kernel<<<G, kKeyThreads, 0, st>>>(d_res, d_res_off, d_class, k, n, slots, ws->chunk_first.p, lay,
                                                         dg, pw21, dlo, dhi, H1, ws->keys.p, ws->flags.p);
         if (dhi > dlo)
