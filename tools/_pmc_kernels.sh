@@ -1,9 +1,9 @@
-# one SQ counter pass (8 counters) over the config-3 bench for the kernels matching $1
+# one SQ counter pass (8 counters, PMC_COUNTERS overrides) over the config-3 bench for the kernels matching $1
 set -e
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 rm -rf gpurun_out/pmck
-timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVE_CYCLES --kernel-include-regex "$1" --output-format csv -d gpurun_out/pmck -o run -- python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/pmck.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc ${PMC_COUNTERS:-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVE_CYCLES} --kernel-include-regex "$1" --output-format csv -d gpurun_out/pmck -o run -- python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/pmck.log 2>&1
 python3 - <<'PY'
 import csv, glob, collections, sys
 sys.path.insert(0, 'tools')
