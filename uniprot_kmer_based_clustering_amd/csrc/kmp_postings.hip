@@ -850,9 +850,17 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
     __syncthreads();
     auto is_dup = [&](uint32_t j) { return (dupw[j >> 5] >> (j & 31)) & 1u; };
     // E. df, head, kept-partner count.  A group without duplicates (almost all) has df = its size
-    // and counts its partners after i only; a group with one walks the whole group.
+    // and counts its partners after i only; a group with one walks the whole group.  In a group of
+    // at most 33 keys without duplicates (nearly all), cnt holds the kept partners as a bit mask
+    // (bit t: position i + 1 + t) instead of their count, so F visits only the kept partners (at
+    // config 3 they are 5.3M of the 22.5M partners the class test looks at) without re-reading and
+    // re-testing the others.  The mode follows from s, en and gd (no register), and is the same for
+    // a whole group, so a wave walking one large group does not run both loops of F (deciding it per
+    // element, by the partners after i, measured 5 % slower at config 1).
     uint32_t cnt[kE];
     bool gd[kE];
+    constexpr bool kMask = !kRows && kThreads <= 256;  // the large kernel measured slower with it (74 -> 80 us, config 1)
+    auto mask_mode = [&](int e) { return kMask && !gd[e] && en[e] - s[e] <= 33u; };
     uint32_t st_sum = single, st_dist = single, st_rep = 0, st_cdf2 = 0, st_max = single ? 1u : 0u, st_heavy = 0,
              mine = 0;
 #pragma unroll
@@ -863,7 +871,7 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
         if (i >= nm) continue;
         gd[e] = (gdupw[s[e] >> 5] >> (s[e] & 31)) & 1u;
         if (gd[e] && is_dup(i)) continue;
-        uint32_t f, c = 0;
+        uint32_t f, c = 0, bits = 0;
         if (kRows) {
             // df, and the partners of a larger protein when this element's protein is in the rows
             const uint32_t p = xl[e] >> cb;
@@ -878,10 +886,19 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
                 }
         } else if (!gd[e]) {
             f = en[e] - s[e];
-            if (a.require_diff) {
+            const uint32_t span = en[e] - 1 - i;
+            if (kMask && en[e] - s[e] <= 33u) {
+                if (a.require_diff) {
+                    for (uint32_t j = i + 1; j < en[e]; ++j)
+                        bits |= (uint32_t)(((Bl[j] ^ xl[e]) & cmask) != 0u) << (j - i - 1);
+                } else {
+                    bits = span == 32u ? ~0u : (1u << span) - 1u;
+                }
+                c = __popc(bits);
+            } else if (a.require_diff) {
                 for (uint32_t j = i + 1; j < en[e]; ++j) c += ((Bl[j] ^ xl[e]) & cmask) != 0u;
             } else {
-                c = en[e] - 1 - i;
+                c = span;
             }
         } else {
             f = 0;
@@ -891,7 +908,7 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
                 if (j > i && (!a.require_diff || ((Bl[j] ^ xl[e]) & cmask))) ++c;
             }
         }
-        if (f > a.heavy_df) c = 0;
+        if (f > a.heavy_df) c = bits = 0;
         st_sum += 1;
         if (i == s[e]) {  // the group's first position is never a duplicate
             st_dist += 1;
@@ -900,7 +917,7 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
             else st_heavy += f;
             st_max = max(st_max, f);
         }
-        cnt[e] = c;
+        cnt[e] = mask_mode(e) ? bits : c;
         mine += c;
     }
     // statistics: three wave reductions of packed words (per workgroup every count is at most
@@ -955,6 +972,13 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
             if (!cnt[e]) continue;
             const uint32_t i = tid + e * kThreads;
             const uint32_t p = xl[e] >> cb;
+            if (mask_mode(e)) {
+                for (uint32_t m = cnt[e]; m; m &= m - 1) {
+                    const uint32_t q = Bl[i + 1 + __builtin_ctz(m)] >> cb;
+                    put((unsigned long long)min(p, q) * a.mul + max(p, q));
+                }
+                continue;
+            }
             for (uint32_t j = kRows ? s[e] : i + 1; j < en[e]; ++j) {
                 if (gd[e] && is_dup(j)) continue;
                 const uint32_t lj = Bl[j];
