@@ -37,11 +37,13 @@ CONFIGS = {
     "config3": (100_000, 3, 0, 7),
     "config2": (10_000, 2, 0, 7),
     "config1": (0, 0, 0, 5),
+    "config5": (1_000_000, 5, 1, 7),
 }
 WORKLOADS = {
     "config3": "config3: N=100000, seed=3, len~N(300,30^2), k=7",
     "config2": "config2: N=10000, seed=2, len~N(300,30^2), k=7",
     "config1": "config1: uniprot_arg.fasta (the reference's dataset, 10619 proteins), k=5",
+    "config5": "config5 at k=7: N=1000000, seed=5, len log-uniform 50-2000, k=7, BLOSUM scores, row passes",
 }
 
 
@@ -72,6 +74,7 @@ def parse():
     ap.add_argument("--engine", default="residues", choices=["residues", "postings", "tiles"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="oracle threads (0: min(16, cores))")
+    ap.add_argument("--score", default="blosum", choices=["blosum", "count"], help="config5: edge score")
     ap.add_argument("--split", default="kmer", choices=["kmer", "rows"], help="multi-GPU flow (N > 1)")
     return ap.parse_args()
 
@@ -172,8 +175,66 @@ def pmc_traffic(stage: str):
     return (st["bytes"] if st else None), os.path.relpath(files[-1], ROOT)
 
 
+def bench_config5(args):
+    """Config 5's batch at k = 7 through the C ABI (kmp_build_sets + kmp_pairs with BLOSUM scores):
+    1,000,000 proteins of log-uniform lengths 50-2,000 (~5.3e8 windows) do not fit one call, so the
+    library runs bounded-memory row passes.  One step = sets built from the resident
+    residues + every pass + the canonical edge list and its scores copied into the edge set's host
+    arrays (the C ABI hands edges to the caller: this line is PCIe-inclusive).  The k = 5 + 7 union at this size does not fit one GPU."""
+    import uniprot_kmer_based_clustering_amd as K
+    from uniprot_kmer_based_clustering_amd import _lib
+    n, seed, law, k = CONFIGS["config5"]
+    score = _lib.KMP_SCORE_BLOSUM if args.score == "blosum" else _lib.KMP_SCORE_COUNT
+    proteins = K.synth(n, seed, law)
+    with K.KmerPairEngine(0, 16) as e:
+        e.load(proteins)
+
+        def one_step():
+            e.build_sets(k)
+            with e.edge_set(score=score) as es:
+                return len(es)
+        for _ in range(args.warmup):
+            one_step()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            n_edges = one_step()
+        dt = time.perf_counter() - t0
+        passes = e.last_passes
+        c = e.counters()
+    ms = dt / args.steps * 1e3
+    pairs_total = n * (n - 1) / 2
+    out = {"metric": "protein pairs/sec (+ edges/sec), 100k x 300aa synthetic, k=7",
+           "value": pairs_total / (dt / args.steps), "unit": "pairs/s", "n_gpus": 1, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "strong",
+           "vs_baseline": None, "dtype": "u32",
+           "data": "synthetic (SURVEY.md §8d generator, seeded; log-uniform lengths 50-2000)",
+           "config": {"workload": WORKLOADS["config5"], "proteins": n, "k": k, "pairs": int(pairs_total),
+                      "edges": int(n_edges), "passes": passes, "score": args.score, "engine": "C ABI kmp_pairs",
+                      "edges_in": "host (PCIe-inclusive)"},
+           "edges_per_s": n_edges / (dt / args.steps),
+           "counters": c,
+           "roofline": None,
+           "roofline_note": "per-stage roofline on the config3 line; this line times whole C-ABI calls"}
+    if not args.no_cpu_baseline:
+        from oracle.oracle import Oracle
+        t0 = time.perf_counter()
+        o = Oracle(proteins.residues, proteins.offsets, proteins.class_id, k=k, threads=16)
+        p, _, _ = o.pairs()
+        cdt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": pairs_total / cdt, "unit": "pairs/s", "cores": 16, "kind": "port",
+                               "sample": f"full workload ({n} proteins, k={k}), 16 threads, no scores",
+                               "seconds": cdt, "edges": int(len(p)), "nproc": os.cpu_count(),
+                               "cpu_model": cpu_model()}
+    print(json.dumps(out))
+
+
 def main():
     args = parse()
+    if args.config == "config5":
+        if args.gpus != 1:
+            print("config5 is a single-GPU line", file=sys.stderr)
+            sys.exit(2)
+        return bench_config5(args)
     import torch
     import torch.distributed as dist
 

@@ -206,6 +206,39 @@ int use_device(kmp_ctx* c) {
 uint64_t protein_len(const kmp_ctx* c, uint32_t p) { return c->h_off[p + 1] - c->h_off[p]; }
 
 // canonical order (tiles: device sort; postings: already sorted), copy out, scores, counters
+// The host pass over a returned edge list (bounds check of every device edge, score fill, the
+// n_align / sum_w_diff counters), split over the context's host threads: at config 5 the list
+// holds ~5e8 edges and one thread spent seconds here.
+struct EdgeScan {
+    uint64_t nalign = 0, wdiff = 0, bad = ~0ull;
+};
+template <class F>
+EdgeScan scan_edges(uint64_t count, int threads, F body) {
+    const uint64_t kMinPer = 1u << 20;
+    int t = (int)std::min<uint64_t>(std::max(threads, 1), std::max<uint64_t>(1, count / kMinPer));
+    std::vector<EdgeScan> part(t);
+    auto run = [&](int r) {
+        const uint64_t a = count * r / t, b = count * (r + 1) / t;
+        EdgeScan& s = part[r];
+        for (uint64_t i = a; i < b; ++i)
+            if (!body(i, s)) {
+                s.bad = i;
+                return;
+            }
+    };
+    std::vector<std::thread> pool;
+    for (int r = 1; r < t; ++r) pool.emplace_back(run, r);
+    run(0);
+    for (auto& th : pool) th.join();
+    EdgeScan out;
+    for (const EdgeScan& s : part) {
+        out.nalign += s.nalign;
+        out.wdiff += s.wdiff;
+        out.bad = std::min(out.bad, s.bad);
+    }
+    return out;
+}
+
 int finish_edges(kmp_ctx* c, const kmp_pair_opts& o, uint64_t count, bool needs_sort, kmp_edges** out) {
     if (needs_sort) {
         const uint64_t tmp = kmp_dev_sort_edges_tmp_bytes(count, c->n);
@@ -234,25 +267,28 @@ int finish_edges(kmp_ctx* c, const kmp_pair_opts& o, uint64_t count, bool needs_
     }
     KMP_HIP(c, hipStreamSynchronize(c->stream));
     e->score.resize(count);
-    uint64_t wdiff = 0, nalign = 0;
-    for (uint64_t i = 0; i < count; ++i) {
-        const uint32_t p = e->p[i], q = e->q[i], w = e->w[i];
-        if (p >= q || q >= c->n) return fail(c, KMP_EDEVICE, "device edge %llu = (%u, %u) is not a pair of the batch",
-                                             (unsigned long long)i, p, q);
-        if (c->h_cls[p] != c->h_cls[q]) wdiff += w;
-        if (w > o.align_threshold) ++nalign;
+    kmp_edges* E = e.get();
+    const EdgeScan sc = scan_edges(count, c->threads, [&](uint64_t i, EdgeScan& s) {
+        const uint32_t p = E->p[i], q = E->q[i], w = E->w[i];
+        if (p >= q || q >= c->n) return false;
+        if (c->h_cls[p] != c->h_cls[q]) s.wdiff += w;
+        if (w > o.align_threshold) ++s.nalign;
         if (o.score == KMP_SCORE_JACCARD) {
             const uint64_t uni = (uint64_t)c->h_set_len[p] + c->h_set_len[q] - w;
-            e->score[i] = uni ? (float)w / (float)uni : 0.0f;  // exact operands (< 2^24), one rounding
+            E->score[i] = uni ? (float)w / (float)uni : 0.0f;  // exact operands (< 2^24), one rounding
         } else if (o.score == KMP_SCORE_BLOSUM) {
             // computed on the device above
         } else {
-            e->score[i] = (float)w;
+            E->score[i] = (float)w;
         }
-    }
+        return true;
+    });
+    if (sc.bad != ~0ull)
+        return fail(c, KMP_EDEVICE, "device edge %llu = (%u, %u) is not a pair of the batch",
+                    (unsigned long long)sc.bad, E->p[sc.bad], E->q[sc.bad]);
     c->counters.n_edges = count;
-    c->counters.n_align = nalign;
-    c->counters.sum_w_diff = wdiff;
+    c->counters.n_align = sc.nalign;
+    c->counters.sum_w_diff = sc.wdiff;
     *out = e.release();
     return KMP_OK;
 }
@@ -1202,19 +1238,22 @@ int kmp_pairs_multi_k(kmp_ctx* c, const kmp_pair_opts* opts, const int* ks, uint
                                       hipMemcpyDeviceToHost, c->stream));
     }
     KMP_HIP(c, hipStreamSynchronize(c->stream));
-    uint64_t nalign = 0, wdiff = 0;
-    for (uint64_t i = 0; i < count; ++i) {
-        const uint32_t p = e->p[i], q = e->q[i];
-        if (p >= q || q >= c->n) return fail(c, KMP_EDEVICE, "device edge %llu = (%u, %u) is not a pair of the batch",
-                                             (unsigned long long)i, p, q);
-        if (!blosum) e->score[i] = (float)e->w[i];
-        if (e->w[i] > o.align_threshold) ++nalign;
-        if (c->h_cls[p] != c->h_cls[q]) wdiff += e->w[i];
-    }
+    kmp_edges* E = e.get();
+    const EdgeScan sc = scan_edges(count, c->threads, [&](uint64_t i, EdgeScan& s) {
+        const uint32_t p = E->p[i], q = E->q[i], w = E->w[i];
+        if (p >= q || q >= c->n) return false;
+        if (!blosum) E->score[i] = (float)w;
+        if (w > o.align_threshold) ++s.nalign;
+        if (c->h_cls[p] != c->h_cls[q]) s.wdiff += w;
+        return true;
+    });
+    if (sc.bad != ~0ull)
+        return fail(c, KMP_EDEVICE, "device edge %llu = (%u, %u) is not a pair of the batch",
+                    (unsigned long long)sc.bad, E->p[sc.bad], E->q[sc.bad]);
     e->ks.assign(ks, ks + nk);
     c->counters.n_edges = count;
-    c->counters.n_align = nalign;
-    c->counters.sum_w_diff = wdiff;
+    c->counters.n_align = sc.nalign;
+    c->counters.sum_w_diff = sc.wdiff;
     *out = e.release();
     return KMP_OK;
 }
