@@ -6,7 +6,8 @@
 //     shorter set, binary-searches the longer one, and a ballot + popcount places the hits, so
 //     the list comes out ascending.  The output range of edge i is kofs[i] .. kofs[i+1]
 //     (exclusive scan of w), and a length other than w flags the edge list as foreign.
-//   edge_blosum_device: the BLOSUM-weighted score of every edge over the same intersection.
+//   edge_blosum_device: the BLOSUM-weighted score of every edge over the same intersection
+//     (set(p) staged in LDS per wave, set(q) streamed).
 //   edge_kmers_to_ids: codes -> repeat-MPHF ids, ascending within each edge (one 64-bit sort of
 //     (edge, id)), and each edge's rank in the reference's final edge order, ascending
 //     (min shared id, p, q) (combine_edges with one thread).
@@ -79,58 +80,84 @@ __global__ __launch_bounds__(256) void edge_kmers_kernel(const uint32_t* __restr
 __constant__ int8_t c_b62_diag[21] = {9, 4, 5, 4, 6, 7, 6, 5, 5, 6, 8, 5, 5, 5, 4, 4, 4, 11, 7, 6, 0};
 
 // BLOSUM-weighted score of every edge (a build extension, parity
-// unpinned): score = Σ over the shared k-mers x of Σ_i B62[x_i][x_i].  One wavefront per edge
-// intersects the repeat-filtered sets as edge_kmers_kernel does; each hit adds its k-mer's
-// self-score (radix-21 digits of the code), a wave reduction sums them.  hits != w flags the
-// edge list as foreign.
-__global__ __launch_bounds__(256) void edge_blosum_kernel(const uint32_t* __restrict__ rep,
-                                                          const uint32_t* __restrict__ rep_len,
-                                                          const uint64_t* __restrict__ off,
-                                                          const uint32_t* __restrict__ ep,
-                                                          const uint32_t* __restrict__ eq,
-                                                          const uint32_t* __restrict__ ew, uint64_t count, int k,
-                                                          float* __restrict__ score, unsigned int* __restrict__ bad) {
-    const uint32_t lane = threadIdx.x & 63;
-    for (uint64_t e = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); e < count; e += (uint64_t)gridDim.x * kWaves) {
-        const uint32_t a = ep[e], b = eq[e];
-        const uint32_t* A = rep + set_base(off[a], a);
-        const uint32_t* B = rep + set_base(off[b], b);
-        uint32_t la = rep_len[a], lb = rep_len[b];
-        if (la > lb) {
-            const uint32_t* t = A;
-            A = B;
-            B = t;
-            const uint32_t u = la;
-            la = lb;
-            lb = u;
-        }
-        int sum = 0, hits = 0;
-        for (uint32_t c = 0; c < la; c += 64) {
-            const uint32_t i = c + lane;
-            if (i >= la) continue;
-            const uint32_t x = A[i];
-            uint32_t lo = 0, hi = lb;
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (B[mid] < x) lo = mid + 1;
-                else hi = mid;
-            }
-            if (lo < lb && B[lo] == x) {
-                uint32_t v = x;
-                for (int t = 0; t < k; ++t) {
-                    sum += c_b62_diag[v % kRadix];
-                    v /= kRadix;
+// unpinned): score = Σ over the shared k-mers x of Σ_i B62[x_i][x_i] (radix-21 digits of the
+// code), over the intersection of the repeat-filtered sets; hits != w flags the edge list as
+// foreign.  Edges come in (p, q) order, so a wave takes 64 consecutive edges (one task), copies
+// set(p) into its own LDS slice whenever p changes (~500 edges share a p at config 5), and its
+// lanes walk set(q) with coalesced loads, each binary-searching the LDS copy (5e8 edges at config
+// 5, k = 7).  A search in global memory (round 2's first version) cost ~9 dependent L2/HBM loads
+// per code of the shorter set; here they are LDS reads.  An edge whose set(p) exceeds the slice
+// searches set(p) in global memory instead.
+constexpr uint32_t kBlWaves = 4, kBlSlice = 2048, kBlTask = 64;
+__global__ __launch_bounds__(256) void edge_blosum_lds_kernel(const uint32_t* __restrict__ rep,
+                                                              const uint32_t* __restrict__ rep_len,
+                                                              const uint64_t* __restrict__ off,
+                                                              const uint32_t* __restrict__ ep,
+                                                              const uint32_t* __restrict__ eq,
+                                                              const uint32_t* __restrict__ ew, uint64_t count, int k,
+                                                              float* __restrict__ score, unsigned int* __restrict__ bad) {
+    __shared__ uint32_t S[kBlWaves][kBlSlice];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t* P = S[wv];
+    const uint64_t tasks = (count + kBlTask - 1) / kBlTask;
+    for (uint64_t t = (uint64_t)blockIdx.x * kBlWaves + wv; t < tasks; t += (uint64_t)gridDim.x * kBlWaves) {
+        uint32_t cur = 0xFFFFFFFFu, lp = 0;
+        const uint64_t e1 = min(count, (t + 1) * kBlTask);
+        for (uint64_t e = t * kBlTask; e < e1; ++e) {
+            const uint32_t a = ep[e], b = eq[e];
+            const uint32_t la = rep_len[a], lb = rep_len[b];
+            int sum = 0, hits = 0;
+            auto add = [&](uint32_t x) {
+                for (int i = 0; i < k; ++i) {
+                    sum += c_b62_diag[x % kRadix];
+                    x /= kRadix;
                 }
                 ++hits;
+            };
+            if (la <= kBlSlice) {
+                if (a != cur) {
+                    __builtin_amdgcn_wave_barrier();  // every lane is done with the previous set
+                    const uint32_t* A = rep + set_base(off[a], a);
+                    for (uint32_t i = lane; i < la; i += 64) P[i] = A[i];
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    cur = a;
+                    lp = la;
+                }
+                const uint32_t* B = rep + set_base(off[b], b);
+                for (uint32_t i = lane; i < lb; i += 64) {
+                    const uint32_t x = B[i];
+                    uint32_t lo = 0, hi = lp;
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (P[mid] < x) lo = mid + 1;
+                        else hi = mid;
+                    }
+                    if (lo < lp && P[lo] == x) add(x);
+                }
+            } else {
+                const uint32_t* A = rep + set_base(off[a], a);
+                const uint32_t* B = rep + set_base(off[b], b);
+                for (uint32_t i = lane; i < lb; i += 64) {
+                    const uint32_t x = B[i];
+                    uint32_t lo = 0, hi = la;
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (A[mid] < x) lo = mid + 1;
+                        else hi = mid;
+                    }
+                    if (lo < la && A[lo] == x) add(x);
+                }
             }
-        }
-        for (int sh = 32; sh > 0; sh >>= 1) {
-            sum += __shfl_down(sum, sh);
-            hits += __shfl_down(hits, sh);
-        }
-        if (lane == 0) {
-            score[e] = (float)sum;  // an integer below 2^24: exact
-            if ((uint32_t)hits != ew[e]) atomicOr(bad, 1u);
+            for (int sh = 32; sh > 0; sh >>= 1) {
+                sum += __shfl_down(sum, sh);
+                hits += __shfl_down(hits, sh);
+            }
+            if (lane == 0) {
+                score[e] = (float)sum;  // an integer below 2^24: exact
+                if ((uint32_t)hits != ew[e]) atomicOr(bad, 1u);
+            }
         }
     }
 }
@@ -209,8 +236,10 @@ int edge_blosum_device(const uint32_t* d_rep, const uint32_t* d_rep_len, const u
     unsigned int h_bad = 0;
     if (hipMemsetAsync(bad, 0, 4, st) != hipSuccess) rc = KMP_EDEVICE;
     if (rc == KMP_OK) {
-        const uint32_t blocks = (uint32_t)std::min<uint64_t>((count + kWaves - 1) / kWaves, 1u << 20);
-        edge_blosum_kernel<<<blocks, 256, 0, st>>>(d_rep, d_rep_len, d_off, d_p, d_q, d_w, count, k, d_score, bad);
+        const uint64_t tasks = (count + kBlTask - 1) / kBlTask;
+        const uint32_t lblocks = (uint32_t)std::min<uint64_t>((tasks + kBlWaves - 1) / kBlWaves, 8192);
+        edge_blosum_lds_kernel<<<lblocks, 256, 0, st>>>(d_rep, d_rep_len, d_off, d_p, d_q, d_w, count, k, d_score,
+                                                         bad);
         if (hipGetLastError() != hipSuccess ||
             hipMemcpyAsync(&h_bad, bad, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
             hipStreamSynchronize(st) != hipSuccess)
