@@ -87,7 +87,9 @@ __constant__ int8_t c_b62_diag[21] = {9, 4, 5, 4, 6, 7, 6, 5, 5, 6, 8, 5, 5, 5, 
 // lanes walk set(q) with coalesced loads, each binary-searching the LDS copy (5e8 edges at config
 // 5, k = 7).  A search in global memory (round 2's first version) cost ~9 dependent L2/HBM loads
 // per code of the shorter set; here they are LDS reads.  An edge whose set(p) exceeds the slice
-// searches set(p) in global memory instead.
+// searches set(p) in global memory instead.  The walk of set(q) stops once the wave has seen the
+// edge's w hits (w = the shared k-mer count the pipeline computed): a list with fewer hits than its
+// w is still flagged, one with extra hits only if they fall in the chunk of 64 that reaches w.
 constexpr uint32_t kBlWaves = 4, kBlSlice = 2048, kBlTask = 64;
 __global__ __launch_bounds__(256) void edge_blosum_lds_kernel(const uint32_t* __restrict__ rep,
                                                               const uint32_t* __restrict__ rep_len,
@@ -105,7 +107,7 @@ __global__ __launch_bounds__(256) void edge_blosum_lds_kernel(const uint32_t* __
         const uint64_t e1 = min(count, (t + 1) * kBlTask);
         for (uint64_t e = t * kBlTask; e < e1; ++e) {
             const uint32_t a = ep[e], b = eq[e];
-            const uint32_t la = rep_len[a], lb = rep_len[b];
+            const uint32_t la = rep_len[a], lb = rep_len[b], w = ew[e];
             int sum = 0, hits = 0;
             auto add = [&](uint32_t x) {
                 for (int i = 0; i < k; ++i) {
@@ -126,28 +128,40 @@ __global__ __launch_bounds__(256) void edge_blosum_lds_kernel(const uint32_t* __
                     lp = la;
                 }
                 const uint32_t* B = rep + set_base(off[b], b);
-                for (uint32_t i = lane; i < lb; i += 64) {
-                    const uint32_t x = B[i];
-                    uint32_t lo = 0, hi = lp;
-                    while (lo < hi) {
-                        const uint32_t mid = (lo + hi) >> 1;
-                        if (P[mid] < x) lo = mid + 1;
-                        else hi = mid;
+                for (uint32_t c = 0, seen = 0; c < lb && seen < w; c += 64) {
+                    const uint32_t i = c + lane;
+                    bool hit = false;
+                    if (i < lb) {
+                        const uint32_t x = B[i];
+                        uint32_t lo = 0, hi = lp;
+                        while (lo < hi) {
+                            const uint32_t mid = (lo + hi) >> 1;
+                            if (P[mid] < x) lo = mid + 1;
+                            else hi = mid;
+                        }
+                        hit = lo < lp && P[lo] == x;
+                        if (hit) add(x);
                     }
-                    if (lo < lp && P[lo] == x) add(x);
+                    seen += __popcll(__ballot(hit));
                 }
             } else {
                 const uint32_t* A = rep + set_base(off[a], a);
                 const uint32_t* B = rep + set_base(off[b], b);
-                for (uint32_t i = lane; i < lb; i += 64) {
-                    const uint32_t x = B[i];
-                    uint32_t lo = 0, hi = la;
-                    while (lo < hi) {
-                        const uint32_t mid = (lo + hi) >> 1;
-                        if (A[mid] < x) lo = mid + 1;
-                        else hi = mid;
+                for (uint32_t c = 0, seen = 0; c < lb && seen < w; c += 64) {
+                    const uint32_t i = c + lane;
+                    bool hit = false;
+                    if (i < lb) {
+                        const uint32_t x = B[i];
+                        uint32_t lo = 0, hi = la;
+                        while (lo < hi) {
+                            const uint32_t mid = (lo + hi) >> 1;
+                            if (A[mid] < x) lo = mid + 1;
+                            else hi = mid;
+                        }
+                        hit = lo < la && A[lo] == x;
+                        if (hit) add(x);
                     }
-                    if (lo < la && A[lo] == x) add(x);
+                    seen += __popcll(__ballot(hit));
                 }
             }
             for (int sh = 32; sh > 0; sh >>= 1) {
@@ -156,7 +170,7 @@ __global__ __launch_bounds__(256) void edge_blosum_lds_kernel(const uint32_t* __
             }
             if (lane == 0) {
                 score[e] = (float)sum;  // an integer below 2^24: exact
-                if ((uint32_t)hits != ew[e]) atomicOr(bad, 1u);
+                if ((uint32_t)hits != w) atomicOr(bad, 1u);
             }
         }
     }
