@@ -128,12 +128,14 @@ __global__ __launch_bounds__(256) void edge_blosum_lds_kernel(const uint32_t* __
                     lp = la;
                 }
                 const uint32_t* B = rep + set_base(off[b], b);
-                for (uint32_t c = 0, seen = 0; c < lb && seen < w; c += 64) {
+                // set(q) is sorted: the last lane's insertion point bounds the next chunk's searches
+                for (uint32_t c = 0, seen = 0, base = 0; c < lb && seen < w; c += 64) {
                     const uint32_t i = c + lane;
                     bool hit = false;
+                    uint32_t lo = base;
                     if (i < lb) {
                         const uint32_t x = B[i];
-                        uint32_t lo = 0, hi = lp;
+                        uint32_t hi = lp;
                         while (lo < hi) {
                             const uint32_t mid = (lo + hi) >> 1;
                             if (P[mid] < x) lo = mid + 1;
@@ -143,6 +145,7 @@ __global__ __launch_bounds__(256) void edge_blosum_lds_kernel(const uint32_t* __
                         if (hit) add(x);
                     }
                     seen += __popcll(__ballot(hit));
+                    base = __shfl(lo, (int)min(63u, lb - 1 - c));
                 }
             } else {
                 const uint32_t* A = rep + set_base(off[a], a);
