@@ -213,6 +213,58 @@ int kmp_pairs_multi_k(kmp_ctx* ctx, const kmp_pair_opts* opts, const int* ks, ui
 int kmp_edges_get_wk(const kmp_edges* e, uint32_t j, uint32_t* wk, uint64_t cap, uint64_t* n);
 void kmp_edges_free(kmp_edges* e);
 
+/* ------------------------------------------------------------------ streamed pairs - */
+/* Edges streamed per row pass instead of returned whole (config 5, SURVEY.md §8d: at k = 5 the
+ * 10^6-protein batch has ~10^11 edges, more than one GPU's HBM or the host can hold).  The rows run
+ * in bounded-memory passes (kmp_ctx_set_pass_keys) as in kmp_pairs_multi_k; each pass's edges — the
+ * canonical list's consecutive block of the pairs whose smaller protein is in [row_lo, row_hi) —
+ * are handed to `sink` as one chunk, then the buffers are reused.  ks[0..nk): one k (nk = 1, the
+ * reference's kmp_pairs) or the config-5 union (w = Σ_k w_k, score = Σ_k score_k, w_k in wk[]).
+ * score: KMP_SCORE_COUNT (score = w) or KMP_SCORE_BLOSUM (the integer BLOSUM score, summed inside
+ * the pair reduction).  sink_on_device: 1 — the chunk's arrays are device pointers on
+ * chunk->device, valid during the call (the stream is synchronised before and after); 0 — host
+ * copies.  sink may be NULL (the summary only); a nonzero return from it stops the stream and is
+ * returned.  summary (may be NULL): the reference's counters over the whole list and a digest
+ * computed on the device (below).  Multi-GPU contexts: each rank streams its own rows (the row
+ * split, kmp_row_split), chunks arrive from one host thread per rank one at a time (the sink is
+ * never called concurrently) with chunk->rank set; per rank the chunks ascend. */
+#define KMP_DIGEST_SEGMENTS 64
+typedef struct {
+    uint32_t rank;            /* multi-GPU: the rank (0 on one GPU) */
+    int device;               /* HIP device of the arrays when on_device */
+    uint32_t row_lo, row_hi;  /* every edge (p, q) with row_lo <= p < row_hi, and only those */
+    uint64_t n;               /* edges in the chunk, canonical (p, q) order */
+    int on_device;
+    const uint32_t *p, *q, *w;
+    const uint32_t* score;    /* COUNT: w; BLOSUM: the integer score */
+    const uint32_t* wk[KMP_MULTI_K_MAX];  /* w of ks[j] (0 where that k shares none); NULL past nk */
+} kmp_edge_chunk;
+typedef int (*kmp_edge_sink)(void* user, const kmp_edge_chunk* chunk);
+/* Counters over the streamed list (mod.rs:545 n_edges, :695 sum_w_diff, :242 n_align) and its
+ * digest: Σ over the edges of kmp_edge_digest_term(p, q, w, score, w_{ks[0]}) mod 2^64, in total
+ * and per row segment (segment of p = p * KMP_DIGEST_SEGMENTS / N).  ordered = 1 when every chunk
+ * was strictly (p, q)-ascending inside its rows (then equal digests mean equal lists up to 64-bit
+ * collisions: an ascending list is determined by its set). */
+typedef struct {
+    uint64_t n_edges, sum_w, sum_score, n_align, sum_w_diff, incidences;
+    uint64_t digest;
+    uint64_t seg_edges[KMP_DIGEST_SEGMENTS];
+    uint64_t seg_digest[KMP_DIGEST_SEGMENTS];
+    uint32_t passes;
+    int32_t ordered;
+} kmp_stream_summary;
+int kmp_pairs_stream(kmp_ctx* ctx, const kmp_pair_opts* opts, const int* ks, uint32_t nk, int sink_on_device,
+                     kmp_edge_sink sink, void* user, kmp_stream_summary* summary);
+/* The rows kmp_pairs_stream covers: [row_lo, row_hi) (row_hi 0: every row, the default).  The unit
+ * of a multi-process split — one process per GPU, each streaming its kmp_row_split share of the
+ * pair space with no exchange (a multi-GPU context splits [row_lo, row_hi) over its ranks by
+ * equal pair mass instead). */
+int kmp_ctx_set_rows(kmp_ctx* ctx, uint32_t row_lo, uint32_t row_hi);
+/* The digest term of one edge: with a = p << 32 | q, b = w << 32 | score, m(z) = splitmix64's
+ * finaliser (z += 0x9E3779B97F4A7C15; z = (z ^ z >> 30) * 0xBF58476D1CE4E5B9;
+ * z = (z ^ z >> 27) * 0x94D049BB133111EB; z ^ z >> 31): m(a ^ m(b ^ m(w0))). */
+uint64_t kmp_edge_digest_term(uint32_t p, uint32_t q, uint32_t w, uint32_t score, uint32_t w0);
+
 /* ------------------------------------------------------------------ edge k-mers ---- */
 /* The shared k-mers behind each edge's w: KmerEdge::get_kmers (edge.rs:119-124), i.e. the
  * KmerEdgeGroup.kmers that combine_edges concatenates (mod.rs:415-417; edge.rs:67-81).
@@ -431,6 +483,34 @@ int kmp_dev_pairs_rows(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d
                        uint32_t n, int k, uint64_t slots, uint32_t heavy_df, uint32_t min_shared,
                        int require_class_diff, uint32_t row_lo, uint32_t row_hi, uint32_t* d_p, uint32_t* d_q,
                        uint32_t* d_w, uint64_t cap, uint64_t* n_edges, kmp_postings_stats* stats, void* stream);
+/* The scored residue path (config 5's BLOSUM score; a build extension, parity
+ * unpinned): as kmp_dev_pairs_rows, and d_score[i] = Σ over the shared k-mers x of edge i of
+ * Σ_j B62[x_j][x_j] (the BLOSUM62 diagonal of blosum.rs:8-30 in residue-code order, code 20 scored
+ * 0) as an exact integer.  The score is summed inside the pair reduction: every (k-mer, pair)
+ * incidence carries its k-mer's self-score (at most 7 x 11 = 77) in the pair key, so no per-edge
+ * set intersection runs.  row_lo = 0, row_hi = n: the whole batch (the unranged step).  A call
+ * covers at most kmp_dev_rows_max(n, 1) rows (the u32 row-block key holds the score bits too;
+ * 131,072 rows at n = 10^6); more is KMP_EINVAL. */
+uint32_t kmp_dev_rows_max(uint32_t n, int scored);  /* scored: 0 no score, 1 score, 2 multi-k (below) */
+int kmp_dev_pairs_rows_scored(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
+                              uint32_t n, int k, uint64_t slots, uint32_t heavy_df, uint32_t min_shared,
+                              int require_class_diff, uint32_t row_lo, uint32_t row_hi, uint32_t* d_p, uint32_t* d_q,
+                              uint32_t* d_w, uint32_t* d_score, uint64_t cap, uint64_t* n_edges,
+                              kmp_postings_stats* stats, void* stream);
+/* Config 5's union of two k in ONE reduction ("w5, w7 computed independently per
+ * pair; an edge is emitted if w5 >= 1 or w7 >= 1"): ws[j] (two distinct workspaces, kept across
+ * calls for front reuse) groups and expands the windows of ks[j], every (k-mer, pair) incidence
+ * keyed with its k bit and self-score, and one row-block tail reduces both sets of keys together:
+ * per pair w = w0 + w1 (w_j = the shared ks[j]-mers), score = Σ_j BLOSUM score_j, emitted when
+ * w0 >= min_shared or w1 >= min_shared (and the classes differ when required).  No per-k lists,
+ * no merge.  Rows as kmp_dev_pairs_rows, at most kmp_dev_rows_max(n, 2) per call (65,536 rows at
+ * n = 10^6). */
+int kmp_dev_pairs_rows_multi(kmp_postings* const* ws, const int* ks, uint32_t nk, const uint8_t* d_res,
+                             const uint64_t* d_res_off, const uint16_t* d_class, uint32_t n, uint64_t slots,
+                             uint32_t min_shared, int require_class_diff, uint32_t row_lo, uint32_t row_hi,
+                             uint32_t* d_p, uint32_t* d_q, uint32_t* d_w, uint32_t* d_score, uint32_t* d_w0,
+                             uint32_t* d_w1, uint64_t cap, uint64_t* n_edges, kmp_postings_stats* stats,
+                             void* stream);
 /* The multi-GPU k-mer split (the reference's `threads` share the same work through
  * one sorted k-mer list, main.rs:77-122 / mod.rs:81-124).  Rank `part` of `parts` (<= 64):
  *   kmp_dev_split_expand  every window of the batch is keyed, the rank keeps the k-mers of its

@@ -450,3 +450,281 @@ void orc_free_ctx(orc_ctx* x) {
     free(x->hid_val); free(x->hid_pos); free(x->post_off); free(x->post_val);
     free(x);
 }
+
+/* ======================================================================================
+ * Config 5 restated for streamed checking: the union over nk contexts (the
+ * same batch at distinct k) of the edges of rows [row_lo, row_hi), an edge (p, q) emitted when
+ * the classes differ (when required) and any w_j >= min_shared, with w = Σ_j w_j and
+ * score = Σ_j score_j (BLOSUM: Σ over the shared k-mers x of Σ_i B62[x_i][x_i], the diagonal of
+ * blosum.rs:8-30 in residue-code order, code 20 scored 0; COUNT: score = w).  Row p walks, per
+ * k, the posting list of each of its repeat k-mers past its own position (vertex.rs:103-137),
+ * exactly as orc_pairs does, and counts w_j and the score per later protein q.  Either the
+ * edges are collected (canonical order) or only summarised: the counters and the digest that
+ * kmp_pairs_stream reports (Σ of kmp_edge_digest_term over the edges, also per row segment
+ * p * 64 / N).  The digest term is restated here from its definition in kmerpair.h.
+ * ====================================================================================== */
+#define ORC_SEGMENTS 64
+
+static const uint8_t B62_DIAG[21] = {9, 4, 5, 4, 6, 7, 6, 5, 5, 6, 8, 5, 5, 5, 4, 4, 4, 11, 7, 6, 0};
+
+static uint32_t code_self_score(uint32_t code, int k) {
+    uint32_t s = 0;
+    for (int i = 0; i < k; ++i) {
+        s += B62_DIAG[code % 21u];
+        code /= 21u;
+    }
+    return s;
+}
+
+static inline uint64_t orc_mix(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+uint64_t orc_digest_term(uint32_t p, uint32_t q, uint32_t w, uint32_t s, uint32_t w0) {
+    uint64_t a = ((uint64_t)p << 32) | q, b = ((uint64_t)w << 32) | s;
+    return orc_mix(a ^ orc_mix(b ^ orc_mix((uint64_t)w0)));
+}
+
+typedef struct {
+    uint64_t n_edges, sum_w, sum_score, n_align, sum_w_diff, incidences, digest;
+    uint64_t seg_edges[ORC_SEGMENTS], seg_digest[ORC_SEGMENTS];
+} orc_digest;
+
+#define ORC_MAXK 4
+typedef struct {
+    orc_ctx* xs[ORC_MAXK];
+    uint32_t* hscore[ORC_MAXK];  /* self-score of each repeat id, per k */
+    int nk;
+    uint32_t row_lo, row_hi, min_shared, align_threshold;
+    int require_class_diff, blosum, collect;
+    _Atomic uint32_t cursor;
+    edge_buf* rows;              /* collect: one per row (q, w of the union) */
+    uint32_t** rs;               /* collect: per row, score and w_j arrays (1 + nk per edge) */
+    pthread_mutex_t lock;
+    orc_digest dg;
+} stream_job;
+
+static void* stream_worker(void* arg) {
+    stream_job* j = (stream_job*)arg;
+    orc_ctx* x0 = j->xs[0];
+    const uint32_t n = x0->n, nk = (uint32_t)j->nk;
+    uint32_t* cnt = (uint32_t*)calloc((size_t)nk * (n ? n : 1), sizeof(uint32_t));
+    uint32_t* sc = (uint32_t*)calloc(n ? n : 1, sizeof(uint32_t));
+    uint8_t* mark = (uint8_t*)calloc(n + 8, 1);
+    uint32_t* touched = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+    uint32_t* tmp = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+    orc_digest d;
+    memset(&d, 0, sizeof d);
+    for (;;) {
+        uint32_t r0 = atomic_fetch_add(&j->cursor, 16u);
+        if (r0 >= j->row_hi - j->row_lo) break;
+        uint32_t r1 = r0 + 16 < j->row_hi - j->row_lo ? r0 + 16 : j->row_hi - j->row_lo;
+        for (uint32_t pr = j->row_lo + r0; pr < j->row_lo + r1; ++pr) {
+            const uint32_t p = pr;
+            uint64_t nt = 0;
+            for (uint32_t k = 0; k < nk; ++k) {
+                orc_ctx* x = j->xs[k];
+                uint32_t* ck = cnt + (size_t)k * n;
+                for (uint64_t i = x->hid_off[p]; i < x->hid_off[p + 1]; ++i) {
+                    const uint32_t h = x->hid_val[i];
+                    const uint32_t s = j->blosum ? j->hscore[k][h] : 0u;
+                    const uint64_t b = x->post_off[h] + x->hid_pos[i] + 1, e = x->post_off[h + 1];
+                    for (uint64_t t = b; t < e; ++t) {
+                        const uint32_t q = x->post_val[t];
+                        ck[q]++;
+                        sc[q] += s;
+                        if (!mark[q]) {
+                            mark[q] = 1;
+                            touched[nt++] = q;
+                        }
+                        if (!j->require_class_diff || x->cls[p] != x->cls[q]) d.incidences++;
+                    }
+                }
+            }
+            /* ascending q: sort the touched list, or scan the marks when they are dense */
+            const uint64_t span = n - p;
+            int scan = nt * 16 > span / 8;
+            if (!scan) sort_u32(touched, tmp, nt);
+            uint64_t it = 0;
+            uint64_t qi = p + 1;
+            edge_buf* row = j->collect ? &j->rows[p - j->row_lo] : NULL;
+            for (;;) {
+                uint32_t q;
+                if (scan) {
+                    while (qi < n && !mark[qi]) {
+                        if ((qi & 7) == 0 && qi + 8 <= n) {
+                            uint64_t wd;
+                            memcpy(&wd, mark + qi, 8);
+                            if (!wd) { qi += 8; continue; }
+                        }
+                        ++qi;
+                    }
+                    if (qi >= n) break;
+                    q = (uint32_t)qi++;
+                } else {
+                    if (it >= nt) break;
+                    q = touched[it++];
+                }
+                mark[q] = 0;
+                uint32_t w = 0, any = 0, wj[ORC_MAXK];
+                for (uint32_t k = 0; k < nk; ++k) {
+                    wj[k] = cnt[(size_t)k * n + q];
+                    cnt[(size_t)k * n + q] = 0;
+                    w += wj[k];
+                    any |= wj[k] >= j->min_shared;
+                }
+                const uint32_t s = j->blosum ? sc[q] : w;
+                sc[q] = 0;
+                const int differ = x0->cls[p] != x0->cls[q]; /* mod.rs:580-587 */
+                if (!any || (j->require_class_diff && !differ)) continue;
+                d.n_edges++;
+                d.sum_w += w;
+                d.sum_score += s;
+                d.n_align += w > j->align_threshold;
+                if (differ) d.sum_w_diff += w;
+                const uint64_t term = orc_digest_term(p, q, w, s, wj[0]);
+                d.digest += term;
+                const uint32_t g = (uint32_t)((uint64_t)p * ORC_SEGMENTS / n);
+                d.seg_edges[g]++;
+                d.seg_digest[g] += term;
+                if (row) {
+                    if (row->n == row->cap) {
+                        row->cap = row->cap ? row->cap * 2 : 16;
+                        row->q = (uint32_t*)realloc(row->q, row->cap * sizeof(uint32_t));
+                        row->w = (uint32_t*)realloc(row->w, row->cap * sizeof(uint32_t));
+                        j->rs[p - j->row_lo] =
+                            (uint32_t*)realloc(j->rs[p - j->row_lo], row->cap * (1 + nk) * sizeof(uint32_t));
+                    }
+                    uint32_t* ex = j->rs[p - j->row_lo] + row->n * (1 + nk);
+                    ex[0] = s;
+                    for (uint32_t k = 0; k < nk; ++k) ex[1 + k] = wj[k];
+                    row->q[row->n] = q;
+                    row->w[row->n] = w;
+                    row->n++;
+                }
+            }
+        }
+    }
+    pthread_mutex_lock(&j->lock);
+    j->dg.n_edges += d.n_edges;
+    j->dg.sum_w += d.sum_w;
+    j->dg.sum_score += d.sum_score;
+    j->dg.n_align += d.n_align;
+    j->dg.sum_w_diff += d.sum_w_diff;
+    j->dg.incidences += d.incidences;
+    j->dg.digest += d.digest;
+    for (int g = 0; g < ORC_SEGMENTS; ++g) {
+        j->dg.seg_edges[g] += d.seg_edges[g];
+        j->dg.seg_digest[g] += d.seg_digest[g];
+    }
+    pthread_mutex_unlock(&j->lock);
+    free(cnt); free(sc); free(mark); free(touched); free(tmp);
+    return NULL;
+}
+
+/* collect != 0: the arrays P, Q, W, S (score) and WK (nk x n_edges, k-major) are malloc'd, canonical order. */
+int orc_stream(orc_ctx** xs, int nk, uint32_t row_lo, uint32_t row_hi, uint32_t min_shared,
+               int require_class_diff, uint32_t align_threshold, int blosum, int threads, int collect,
+               orc_digest* dg, uint32_t** P, uint32_t** Q, uint32_t** W, uint32_t** S, uint32_t** WK,
+               uint64_t* n_edges) {
+    if (nk < 1 || nk > ORC_MAXK || !xs || !xs[0] || row_lo > row_hi || row_hi > xs[0]->n) return ORC_EINVAL;
+    for (int k = 1; k < nk; ++k)
+        if (!xs[k] || xs[k]->n != xs[0]->n) return ORC_EINVAL;
+    stream_job j;
+    memset(&j, 0, sizeof j);
+    j.nk = nk;
+    for (int k = 0; k < nk; ++k) {
+        j.xs[k] = xs[k];
+        j.hscore[k] = (uint32_t*)malloc(sizeof(uint32_t) * (xs[k]->n_repeat ? xs[k]->n_repeat : 1));
+        for (uint64_t h = 0; h < xs[k]->n_repeat; ++h) j.hscore[k][h] = code_self_score(xs[k]->rep_codes[h], xs[k]->k);
+    }
+    j.row_lo = row_lo;
+    j.row_hi = row_hi;
+    j.min_shared = min_shared < 1 ? 1 : min_shared;
+    j.align_threshold = align_threshold;
+    j.require_class_diff = require_class_diff;
+    j.blosum = blosum;
+    j.collect = collect;
+    atomic_init(&j.cursor, 0);
+    pthread_mutex_init(&j.lock, NULL);
+    const uint32_t nr = row_hi - row_lo;
+    if (collect) {
+        j.rows = (edge_buf*)calloc(nr ? nr : 1, sizeof(edge_buf));
+        j.rs = (uint32_t**)calloc(nr ? nr : 1, sizeof(uint32_t*));
+    }
+    run_pool(threads < 1 ? 1 : threads, stream_worker, &j);
+    pthread_mutex_destroy(&j.lock);
+    for (int k = 0; k < nk; ++k) free(j.hscore[k]);
+    if (dg) *dg = j.dg;
+    if (n_edges) *n_edges = j.dg.n_edges;
+    if (collect) {
+        const uint64_t tot = j.dg.n_edges;
+        uint32_t* pp = (uint32_t*)malloc(sizeof(uint32_t) * (tot ? tot : 1));
+        uint32_t* qq = (uint32_t*)malloc(sizeof(uint32_t) * (tot ? tot : 1));
+        uint32_t* ww = (uint32_t*)malloc(sizeof(uint32_t) * (tot ? tot : 1));
+        uint32_t* ss = (uint32_t*)malloc(sizeof(uint32_t) * (tot ? tot : 1));
+        uint32_t* wk = (uint32_t*)malloc(sizeof(uint32_t) * (tot ? tot : 1) * nk);
+        uint64_t o = 0;
+        for (uint32_t r = 0; r < nr; ++r) {
+            edge_buf* b = &j.rows[r];
+            for (uint64_t t = 0; t < b->n; ++t) {
+                pp[o] = row_lo + r;
+                qq[o] = b->q[t];
+                ww[o] = b->w[t];
+                ss[o] = j.rs[r][t * (1 + nk)];
+                for (int k = 0; k < nk; ++k) wk[(uint64_t)k * tot + o] = j.rs[r][t * (1 + nk) + 1 + k];
+                ++o;
+            }
+            free(b->q); free(b->w); free(j.rs[r]);
+        }
+        free(j.rows); free(j.rs);
+        *P = pp; *Q = qq; *W = ww; *S = ss; *WK = wk;
+    }
+    return ORC_OK;
+}
+
+/* BLOSUM score of each pair (p[i], q[i]): Σ over the shared codes of their self-scores */
+typedef struct {
+    const orc_ctx* x;
+    const uint32_t *p, *q;
+    uint64_t n;
+    uint32_t* out;
+    _Atomic uint64_t cursor;
+} score_job;
+
+static void* score_worker(void* arg) {
+    score_job* j = (score_job*)arg;
+    const orc_ctx* x = j->x;
+    for (;;) {
+        uint64_t i0 = atomic_fetch_add(&j->cursor, 4096);
+        if (i0 >= j->n) break;
+        uint64_t i1 = i0 + 4096 < j->n ? i0 + 4096 : j->n;
+        for (uint64_t i = i0; i < i1; ++i) {
+            const uint32_t* a = x->set_val + x->set_off[j->p[i]];
+            const uint32_t* b = x->set_val + x->set_off[j->q[i]];
+            uint64_t na = x->set_off[j->p[i] + 1] - x->set_off[j->p[i]], nb = x->set_off[j->q[i] + 1] - x->set_off[j->q[i]];
+            uint64_t u = 0, v = 0;
+            uint32_t s = 0;
+            while (u < na && v < nb) {
+                if (a[u] < b[v]) ++u;
+                else if (a[u] > b[v]) ++v;
+                else { s += code_self_score(a[u], x->k); ++u; ++v; }
+            }
+            j->out[i] = s;
+        }
+    }
+    return NULL;
+}
+
+int orc_pair_scores(const orc_ctx* x, const uint32_t* p, const uint32_t* q, uint64_t n, uint32_t* out, int threads) {
+    if (!x) return ORC_EINVAL;
+    for (uint64_t i = 0; i < n; ++i)
+        if (p[i] >= x->n || q[i] >= x->n) return ORC_EINVAL;
+    score_job j = {x, p, q, n, out, 0};
+    atomic_init(&j.cursor, 0);
+    run_pool(threads < 1 ? 1 : threads, score_worker, &j);
+    return ORC_OK;
+}

@@ -17,6 +17,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "liboracle.so")
 _lib = None
+P = C.c_void_p
 
 
 class Counters(C.Structure):
@@ -26,6 +27,22 @@ class Counters(C.Structure):
 
     def as_dict(self):
         return {name: int(getattr(self, name)) for name, _ in self._fields_}
+
+
+SEGMENTS = 64
+
+
+class Digest(C.Structure):
+    """orc_digest: the counters and digest kmp_pairs_stream's summary reports."""
+    _fields_ = [(name, C.c_uint64) for name in (
+        "n_edges", "sum_w", "sum_score", "n_align", "sum_w_diff", "incidences", "digest")] + [
+        ("seg_edges", C.c_uint64 * SEGMENTS), ("seg_digest", C.c_uint64 * SEGMENTS)]
+
+    def as_dict(self):
+        d = {n: int(getattr(self, n)) for n, _ in self._fields_ if not n.startswith("seg_")}
+        d["seg_edges"] = [int(x) for x in self.seg_edges]
+        d["seg_digest"] = [int(x) for x in self.seg_digest]
+        return d
 
 
 def build() -> None:
@@ -56,6 +73,14 @@ def lib():
         L.orc_shared.argtypes = [P, C.c_uint32, C.c_uint32, P, C.c_uint64]
         L.orc_free.argtypes = [P]
         L.orc_free_ctx.argtypes = [P]
+        L.orc_stream.restype = C.c_int
+        L.orc_stream.argtypes = [C.POINTER(P), C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_uint32,
+                                 C.c_int, C.c_int, C.c_int, C.POINTER(Digest), C.POINTER(P), C.POINTER(P),
+                                 C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(C.c_uint64)]
+        L.orc_pair_scores.restype = C.c_int
+        L.orc_pair_scores.argtypes = [P, P, P, C.c_uint64, P, C.c_int]
+        L.orc_digest_term.restype = C.c_uint64
+        L.orc_digest_term.argtypes = [C.c_uint32] * 5
         L.orc_residue_code.restype = C.c_uint8
         L.orc_residue_code.argtypes = [C.c_uint8]
         L.orc_pack.restype = C.c_uint32
@@ -150,6 +175,17 @@ class Oracle:
             L.orc_free(ptr)
         return out
 
+    def pair_scores(self, p, q, threads=8):
+        """BLOSUM score of each pair (the C restatement of blosum_scores below, threaded)."""
+        p = np.ascontiguousarray(p, dtype=np.uint32)
+        q = np.ascontiguousarray(q, dtype=np.uint32)
+        out = np.zeros(len(p), dtype=np.uint32)
+        if len(p):
+            st = lib().orc_pair_scores(self._ctx, p.ctypes.data, q.ctypes.data, len(p), out.ctypes.data, threads)
+            if st != 0:
+                raise RuntimeError(f"orc_pair_scores status {st}")
+        return out
+
     def blosum_scores(self, p, q):
         """BLOSUM-weighted score of each pair (p[i], q[i]) (a build
         extension, parity unpinned): Σ over the shared k-mers x of Σ_j B62[x_j][x_j], the diagonal
@@ -172,6 +208,38 @@ class Oracle:
             buf = np.zeros(m, dtype=np.uint32)
             lib().orc_shared(self._ctx, p, q, buf.ctypes.data, buf.size)
         return buf[:m].copy()
+
+
+def stream(oracles, row_lo=0, row_hi=None, min_shared=1, require_class_diff=True, align_threshold=10,
+           blosum=True, threads=8, collect=False):
+    """The config-5 union over `oracles` (one Oracle per k, same batch) of rows [row_lo, row_hi):
+    the summary kmp_pairs_stream reports (counters, digest, per-segment digests) and, with
+    collect, the edges (p, q, w, score, [w_k per oracle]) in canonical order."""
+    L = lib()
+    nk = len(oracles)
+    arr = (P * nk)(*[o._ctx for o in oracles])
+    n = oracles[0].n
+    row_hi = n if row_hi is None else row_hi
+    dg = Digest()
+    ptrs = [P() for _ in range(5)]
+    ne = C.c_uint64()
+    st = L.orc_stream(arr, nk, row_lo, row_hi, min_shared, int(require_class_diff), align_threshold, int(blosum),
+                      threads, int(collect), C.byref(dg), *[C.byref(x) for x in ptrs], C.byref(ne))
+    if st != 0:
+        raise RuntimeError(f"orc_stream status {st}")
+    out = dg.as_dict()
+    if collect:
+        m = ne.value
+        p, q, w, s = (_view(x.value, m, np.uint32) for x in ptrs[:4])
+        wk = _view(ptrs[4].value, m * nk, np.uint32).reshape(nk, m) if m else np.zeros((nk, 0), np.uint32)
+        for x in ptrs:
+            L.orc_free(x)
+        return out, (p, q, w, s, list(wk))
+    return out
+
+
+def digest_term(p, q, w, s, w0) -> int:
+    return int(lib().orc_digest_term(p, q, w, s, w0))
 
 
 # BLOSUM62 diagonal (blosum.rs:8-30: C 9, S 4, T 5, A 4, G 6, P 7, D 6, E 5, Q 5, N 6, H 8, R 5,

@@ -67,6 +67,35 @@ class PostingsStats(C.Structure):
         return dict(zip(POSTINGS_STAGE_NAMES, (float(x) for x in self.stage_ms)))
 
 
+KMP_MULTI_K_MAX = 4
+KMP_DIGEST_SEGMENTS = 64
+
+
+class EdgeChunk(C.Structure):
+    """kmp_edge_chunk: one streamed pass of edges (kmp_pairs_stream)."""
+    _fields_ = [("rank", C.c_uint32), ("device", C.c_int), ("row_lo", C.c_uint32), ("row_hi", C.c_uint32),
+                ("n", C.c_uint64), ("on_device", C.c_int),
+                ("p", C.c_void_p), ("q", C.c_void_p), ("w", C.c_void_p), ("score", C.c_void_p),
+                ("wk", C.c_void_p * KMP_MULTI_K_MAX)]
+
+
+EDGE_SINK = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(EdgeChunk))
+
+
+class StreamSummary(C.Structure):
+    """kmp_stream_summary: counters and digest of a streamed edge list."""
+    _fields_ = [(n, C.c_uint64) for n in ("n_edges", "sum_w", "sum_score", "n_align", "sum_w_diff", "incidences",
+                                           "digest")] + [
+        ("seg_edges", C.c_uint64 * KMP_DIGEST_SEGMENTS), ("seg_digest", C.c_uint64 * KMP_DIGEST_SEGMENTS),
+        ("passes", C.c_uint32), ("ordered", C.c_int32)]
+
+    def as_dict(self):
+        d = {n: int(getattr(self, n)) for n, _ in self._fields_ if not n.startswith("seg_")}
+        d["seg_edges"] = [int(x) for x in self.seg_edges]
+        d["seg_digest"] = [int(x) for x in self.seg_digest]
+        return d
+
+
 class WorkItem(C.Structure):
     _fields_ = [("row_beg", C.c_uint32), ("row_end", C.c_uint32),
                 ("col_beg", C.c_uint32), ("col_end", C.c_uint32)]
@@ -158,6 +187,12 @@ SIGNATURES = {
     "kmp_dev_pairs_rows": (C.c_int, [P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32, C.c_uint32,
                                      C.c_int, C.c_uint32, C.c_uint32, P, P, P, C.c_uint64, U64P, P, P]),
     "kmp_row_split": (None, [C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]),
+    "kmp_dev_rows_max": (C.c_uint32, [C.c_uint32, C.c_int]),
+    "kmp_dev_pairs_rows_scored": (C.c_int, [P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32, C.c_uint32,
+                                            C.c_int, C.c_uint32, C.c_uint32, P, P, P, P, C.c_uint64, U64P, P, P]),
+    "kmp_pairs_stream": (C.c_int, [P, P, C.POINTER(C.c_int), C.c_uint32, C.c_int, EDGE_SINK, P, P]),
+    "kmp_edge_digest_term": (C.c_uint64, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
+    "kmp_ctx_set_rows": (C.c_int, [P, C.c_uint32, C.c_uint32]),
     "kmp_postings_last_overflow_blocks": (C.c_uint32, [P]),
     "kmp_dev_sort_edges_tmp_bytes": (C.c_uint64, [C.c_uint64, C.c_uint32]),
     "kmp_dev_sort_edges": (C.c_int, [P, P, P, C.c_uint64, C.c_uint32, P, C.c_uint64, P]),

@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <new>
 #include <string>
 #include <thread>
@@ -20,6 +21,8 @@
 #include "kmp_merge.hpp"
 #include "kmp_mphf.hpp"
 #include "kmp_multi.hpp"
+#include "kmp_stream.hpp"
+#include "kmp_threads.hpp"
 
 using namespace kmp;
 
@@ -60,6 +63,17 @@ struct DevBuf {
 
 }  // namespace
 
+// one k of a multi-k / streamed call: the sets (scores of the tiles engine), a workspace whose front
+// is kept across the passes, and the pass's edges
+struct kmp_kset {
+    int k = 0;
+    DevBuf set, set_len, rep, rep_len, ep, eq, ew, score;
+    uint64_t cap = 0;
+    std::vector<uint32_t> h_set_len, h_rep_len;
+    kmp_postings* ws = nullptr;
+    ~kmp_kset() { kmp_postings_destroy(ws); }
+};
+
 // one rank of a multi-GPU context: its device, stream, workspace and pair buffers; ranks
 // other than 0 also hold their copy of the packed batch (rank 0 uses the context's)
 struct kmp_rank {
@@ -70,8 +84,12 @@ struct kmp_rank {
     DevBuf send, recv, sflags, sstats;  // k-mer split: exchange regions, flags, statistics
     uint64_t cap = 0;
     kmp_postings* ws = nullptr;
+    // streamed passes (kmp_pairs_stream) of this rank's rows: per-k workspaces, merged arrays, summary
+    std::vector<std::unique_ptr<kmp_kset>> ksets;
+    DevBuf mscore, mwk, mscratch, dacc;
     ~kmp_rank() {
         (void)hipSetDevice(device);
+        ksets.clear();
         if (own_stream && stream) {
             (void)hipStreamSynchronize(stream);
             (void)hipStreamDestroy(stream);
@@ -94,6 +112,7 @@ struct kmp_ctx {
     int device = 0;
     int threads = 1;
     std::string err;
+    std::mutex err_mu;  // err is written from the rank threads of a multi-GPU stream
     hipStream_t stream = nullptr;
 
     uint32_t n = 0;
@@ -109,7 +128,7 @@ struct kmp_ctx {
 
     int k_sets = 0;
     DevBuf set, set_len, rep, rep_len, bits, scratch;
-    DevBuf escore;  // per-edge scores computed on the device (KMP_SCORE_BLOSUM)
+    DevBuf escore;  // per-edge BLOSUM scores (u32) from the scored reduction, or f32 from edge_blosum_device
     std::vector<uint32_t> h_set_len, h_rep_len;
     kmp_counters counters{};
 
@@ -137,16 +156,12 @@ struct kmp_ctx {
     // last kmp_pairs / kmp_pairs_multi_k
     uint64_t pass_keys = 0;
     uint32_t last_passes = 0;
+    // kmp_ctx_set_rows: the rows kmp_pairs_stream covers ([0, 0): all) — a process's share of a
+    // multi-process split (one process per GPU)
+    uint32_t rows_lo = 0, rows_hi = 0;
     // kmp_pairs_multi_k: per k, the sets (scores), a workspace (front kept across passes) and
     // the pass's edges; the merged list
-    struct KSet {
-        int k = 0;
-        DevBuf set, set_len, rep, rep_len, ep, eq, ew, score;
-        uint64_t cap = 0;
-        std::vector<uint32_t> h_set_len, h_rep_len;
-        kmp_postings* ws = nullptr;
-        ~KSet() { kmp_postings_destroy(ws); }
-    };
+    using KSet = kmp_kset;
     std::vector<std::unique_ptr<KSet>> ksets;
     DevBuf mscore, mwk, mscratch;
     // multi-GPU (kmp_ctx_create_multi): the ranks of the row split and the gather's transport
@@ -169,6 +184,12 @@ struct kmp_ctx {
 
 namespace {
 
+// the context's error text; the ranks of a multi-GPU stream report from their own threads
+void note_error(kmp_ctx* c, const std::string& msg, bool keep_first) {
+    std::lock_guard<std::mutex> lk(c->err_mu);
+    if (!keep_first || c->err.empty()) c->err = msg;
+}
+
 int fail(kmp_ctx* c, int status, const char* fmt, ...) {
     if (c) {
         char buf[512];
@@ -176,7 +197,7 @@ int fail(kmp_ctx* c, int status, const char* fmt, ...) {
         va_start(ap, fmt);
         std::vsnprintf(buf, sizeof buf, fmt, ap);
         va_end(ap);
-        c->err = buf;
+        note_error(c, buf, false);
     }
     return status;
 }
@@ -193,7 +214,7 @@ int fail(kmp_ctx* c, int status, const char* fmt, ...) {
     do {                                                                                      \
         int s_ = (expr);                                                                      \
         if (s_ != KMP_OK) {                                                                   \
-            if ((ctx)->err.empty()) (ctx)->err = std::string(#expr) + ": " + kmp_status_string(s_); \
+            note_error((ctx), std::string(#expr) + ": " + kmp_status_string(s_), true);       \
             return s_;                                                                        \
         }                                                                                     \
     } while (0)
@@ -226,10 +247,7 @@ EdgeScan scan_edges(uint64_t count, int threads, F body) {
                 return;
             }
     };
-    std::vector<std::thread> pool;
-    for (int r = 1; r < t; ++r) pool.emplace_back(run, r);
-    run(0);
-    for (auto& th : pool) th.join();
+    run_parts(t, run);
     EdgeScan out;
     for (const EdgeScan& s : part) {
         out.nalign += s.nalign;
@@ -239,7 +257,10 @@ EdgeScan scan_edges(uint64_t count, int threads, F body) {
     return out;
 }
 
-int finish_edges(kmp_ctx* c, const kmp_pair_opts& o, uint64_t count, bool needs_sort, kmp_edges** out) {
+// scored: the BLOSUM scores are in c->escore as u32 (the scored reduction); otherwise a BLOSUM
+// call computes them here per edge (edge_blosum_device: the tiles and set-postings engines)
+int finish_edges(kmp_ctx* c, const kmp_pair_opts& o, uint64_t count, bool needs_sort, kmp_edges** out,
+                 bool scored = false) {
     if (needs_sort) {
         const uint64_t tmp = kmp_dev_sort_edges_tmp_bytes(count, c->n);
         KMP_HIP(c, c->sort_tmp.reserve(tmp));
@@ -256,7 +277,12 @@ int finish_edges(kmp_ctx* c, const kmp_pair_opts& o, uint64_t count, bool needs_
         KMP_HIP(c, hipMemcpyAsync(e->q.data(), c->eq.p, count * 4, hipMemcpyDeviceToHost, c->stream));
         KMP_HIP(c, hipMemcpyAsync(e->w.data(), c->ew.p, count * 4, hipMemcpyDeviceToHost, c->stream));
     }
-    if (o.score == KMP_SCORE_BLOSUM && count) {
+    hvec<uint32_t> iscore;  // scored: the u32 scores, converted below
+    if (o.score == KMP_SCORE_BLOSUM && count && scored) {
+        iscore.resize(count);
+        KMP_HIP(c, hipMemcpyAsync(iscore.data(), c->escore.p, count * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                  c->stream));
+    } else if (o.score == KMP_SCORE_BLOSUM && count) {
         KMP_HIP(c, c->escore.reserve(count * sizeof(float)));
         e->score.resize(count);
         KMP_TRY(c, edge_blosum_device(c->rep.as<uint32_t>(), c->rep_len.as<uint32_t>(), c->off.as<uint64_t>(),
@@ -277,7 +303,7 @@ int finish_edges(kmp_ctx* c, const kmp_pair_opts& o, uint64_t count, bool needs_
             const uint64_t uni = (uint64_t)c->h_set_len[p] + c->h_set_len[q] - w;
             E->score[i] = uni ? (float)w / (float)uni : 0.0f;  // exact operands (< 2^24), one rounding
         } else if (o.score == KMP_SCORE_BLOSUM) {
-            // computed on the device above
+            if (scored) E->score[i] = (float)iscore[i];  // an integer below 2^24: exact
         } else {
             E->score[i] = (float)w;
         }
@@ -550,6 +576,10 @@ int kmp_build_sets(kmp_ctx* c, int k) {
     KMP_TRY(c, use_device(c));
     c->k_sets = 0;
     c->drop_repeat_index();
+    // the multi-GPU flow and exchange capacity are learned per (batch, k): a k that spills
+    // frequent k-mers must not pin the row split on another k of the same batch
+    c->split_cap = 0;
+    c->split_rows = false;
     const uint64_t capacity = kmp_set_capacity(c->n, c->total_res);
     const uint64_t words = kmp_dev_repeat_bitmap_words(k);
     KMP_HIP(c, c->set.reserve(capacity * sizeof(uint32_t)));
@@ -674,22 +704,26 @@ struct PassPlan {
     uint32_t n;
     double budget;
     double density = -1.0;
+    uint32_t max_rows = 0xFFFFFFFFu;  // rows one call may cover (scored: kmp_dev_rows_max)
+    uint32_t end = 0xFFFFFFFFu;       // the last row + 1 (a rank's share; default n)
     double mass(uint32_t a, uint32_t b) const {  // Σ_{p in [a, b)} (n - 1 - p)
         const double A = a, B = b, N = n;
         return (B - A) * (N - 1) - (B * (B - 1) - A * (A - 1)) / 2;
     }
     uint32_t next(uint32_t a) const {
-        if (a >= n) return n;
-        if (density < 0) return std::min<uint32_t>(n, a + std::max<uint32_t>(1, n / 256));
+        const uint32_t e = std::min(end, n);
+        if (a >= e) return e;
+        const uint32_t lim = (uint32_t)std::min<uint64_t>(e, (uint64_t)a + max_rows);
+        if (density < 0) return std::min<uint32_t>(lim, a + std::max<uint32_t>(1, n / 256));
         const double target = 0.75 * budget / std::max(density, 1e-12);
-        if (mass(a, n) <= target) return n;
-        uint32_t lo = a + 1, hi = n;
+        if (mass(a, e) <= target) return lim;
+        uint32_t lo = a + 1, hi = e;
         while (lo < hi) {
             const uint32_t mid = lo + (hi - lo) / 2;
             if (mass(a, mid) >= target) hi = mid;
             else lo = mid + 1;
         }
-        return lo;
+        return std::min(lo, lim);
     }
     void seen(uint32_t a, uint32_t b, uint64_t inc) {
         const double m = mass(a, b);
@@ -709,38 +743,58 @@ uint64_t pass_budget(kmp_ctx* c) {
     return std::max<uint64_t>(1u << 20, std::min<uint64_t>(fr / 2 / 96, 3ull << 30));
 }
 
-// three u32 edge arrays of cap entries, grown to want entries keeping their first keep entries
-int grow_edges(kmp_ctx* c, DevBuf& ep, DevBuf& eq, DevBuf& ew, uint64_t& cap, uint64_t want, uint64_t keep) {
-    const uint64_t have = ep.p && eq.p && ew.p ? std::min({ep.bytes, eq.bytes, ew.bytes}) / 4 : 0;
+// the batch and stream a pass runs on: the context's (nullptr) or a rank's copy
+struct Lane {
+    const uint8_t* res;
+    const uint64_t* off;
+    const uint16_t* cls;
+    hipStream_t stream;
+};
+
+// three (scored: four) u32 edge arrays of cap entries, grown to want entries keeping their first
+// keep entries
+int grow_edges(kmp_ctx* c, DevBuf& ep, DevBuf& eq, DevBuf& ew, uint64_t& cap, uint64_t want, uint64_t keep,
+               DevBuf* es = nullptr, hipStream_t stream = nullptr) {
+    if (!stream) stream = c->stream;
+    uint64_t have = ep.p && eq.p && ew.p ? std::min({ep.bytes, eq.bytes, ew.bytes}) / 4 : 0;
+    if (es) have = es->p ? std::min<uint64_t>(have, es->bytes / 4) : 0;
     if (have >= want) {
         cap = have;
         return KMP_OK;
     }
-    for (DevBuf* b : {&ep, &eq, &ew}) {
+    for (DevBuf* b : {&ep, &eq, &ew, es}) {
+        if (!b) continue;
         DevBuf nb;
         KMP_HIP(c, nb.reserve(want * sizeof(uint32_t)));
-        if (keep) KMP_HIP(c, hipMemcpyAsync(nb.p, b->p, keep * 4, hipMemcpyDeviceToDevice, c->stream));
-        KMP_HIP(c, hipStreamSynchronize(c->stream));
+        if (keep) KMP_HIP(c, hipMemcpyAsync(nb.p, b->p, keep * 4, hipMemcpyDeviceToDevice, stream));
+        KMP_HIP(c, hipStreamSynchronize(stream));
         b->swap(nb);
     }
     cap = want;
     return KMP_OK;
 }
 
-// rows [a, b) with workspace ws (front reuse on) into (ep, eq, ew) from entry off on; the
-// buffers grow, keeping [0, off), when the call reports an overflow
+// rows [a, b) with workspace ws (front reuse on) into (ep, eq, ew[, es]) from entry off on; the
+// buffers grow, keeping [0, off), when the call reports an overflow.  es: the scored reduction
+// (BLOSUM), its u32 scores into es
 int rows_into(kmp_ctx* c, kmp_postings* ws, int k, const kmp_pair_opts& o, uint32_t a, uint32_t b, DevBuf& ep,
-              DevBuf& eq, DevBuf& ew, uint64_t& cap, uint64_t off, uint64_t* ne, kmp_postings_stats* st) {
+              DevBuf& eq, DevBuf& ew, uint64_t& cap, uint64_t off, uint64_t* ne, kmp_postings_stats* st,
+              DevBuf* es = nullptr, const Lane* lane = nullptr) {
     const uint64_t slots = kmp_set_capacity(c->n, c->total_res);
-    KMP_TRY(c, grow_edges(c, ep, eq, ew, cap, std::max<uint64_t>(cap, off + (1u << 16)), off));
+    const Lane L = lane ? *lane : Lane{c->res.as<uint8_t>(), c->off.as<uint64_t>(), c->cls.as<uint16_t>(), c->stream};
+    KMP_TRY(c, grow_edges(c, ep, eq, ew, cap, std::max<uint64_t>(cap, off + (1u << 16)), off, es, L.stream));
     for (int attempt = 0; attempt < 3; ++attempt) {
         uint64_t m = 0;
-        const int rc = kmp_dev_pairs_rows(ws, c->res.as<uint8_t>(), c->off.as<uint64_t>(), c->cls.as<uint16_t>(), c->n,
-                                          k, slots, 0xFFFFFFFFu, o.min_shared, o.require_class_diff, a, b,
-                                          ep.as<uint32_t>() + off, eq.as<uint32_t>() + off, ew.as<uint32_t>() + off,
-                                          cap - off, &m, st, c->stream);
+        const int rc =
+            es ? kmp_dev_pairs_rows_scored(ws, L.res, L.off, L.cls, c->n, k, slots, 0xFFFFFFFFu, o.min_shared,
+                                           o.require_class_diff, a, b, ep.as<uint32_t>() + off, eq.as<uint32_t>() + off,
+                                           ew.as<uint32_t>() + off, es->as<uint32_t>() + off, cap - off, &m, st,
+                                           L.stream)
+               : kmp_dev_pairs_rows(ws, L.res, L.off, L.cls, c->n, k, slots, 0xFFFFFFFFu, o.min_shared,
+                                    o.require_class_diff, a, b, ep.as<uint32_t>() + off, eq.as<uint32_t>() + off,
+                                    ew.as<uint32_t>() + off, cap - off, &m, st, L.stream);
         if (rc == KMP_EOVERFLOW) {
-            KMP_TRY(c, grow_edges(c, ep, eq, ew, cap, off + m + m / 8 + 1024, off));
+            KMP_TRY(c, grow_edges(c, ep, eq, ew, cap, off + m + m / 8 + 1024, off, es, L.stream));
             continue;
         }
         if (rc != KMP_OK) return fail(c, rc, "rows [%u, %u): %s", a, b, kmp_status_string(rc));
@@ -752,9 +806,10 @@ int rows_into(kmp_ctx* c, kmp_postings* ws, int k, const kmp_pair_opts& o, uint3
 
 // single GPU, residue path, in passes: the pass edges land behind each other in the context's
 // buffers (already canonical: passes are consecutive row ranges)
-int pass_pairs(kmp_ctx* c, const kmp_pair_opts& o, uint64_t* count) {
+int pass_pairs(kmp_ctx* c, const kmp_pair_opts& o, uint64_t* count, bool scored) {
     KMP_TRY(c, kmp_postings_set_reuse(c->postings, 1));
     PassPlan plan{c->n, (double)pass_budget(c)};
+    if (scored) plan.max_rows = kmp_dev_rows_max(c->n, 1);
     uint64_t off = 0;
     uint32_t passes = 0;
     int rc = KMP_OK;
@@ -762,7 +817,8 @@ int pass_pairs(kmp_ctx* c, const kmp_pair_opts& o, uint64_t* count) {
         const uint32_t b = plan.next(a);
         kmp_postings_stats st{};
         uint64_t ne = 0;
-        rc = rows_into(c, c->postings, c->k_sets, o, a, b, c->ep, c->eq, c->ew, c->edge_cap, off, &ne, &st);
+        rc = rows_into(c, c->postings, c->k_sets, o, a, b, c->ep, c->eq, c->ew, c->edge_cap, off, &ne, &st,
+                       scored ? &c->escore : nullptr);
         plan.seen(a, b, st.incidences);
         off += ne;
         a = b;
@@ -857,10 +913,7 @@ static int split_rank_edges(kmp_ctx* c, const kmp_pair_opts& o, const std::vecto
                 r.cap = ne + ne / 8 + 1024;
             }
         };
-        std::vector<std::thread> pool;
-        for (uint32_t g = 1; g < G; ++g) pool.emplace_back(work, g);
-        work(0);
-        for (auto& t : pool) t.join();
+        run_parts((int)G, [&](int g) { work((uint32_t)g); });
         KMP_TRY(c, use_device(c));
         for (uint32_t g = 0; g < G; ++g)
             if (status[g] != KMP_OK)
@@ -902,10 +955,7 @@ static int rows_rank_edges(kmp_ctx* c, const kmp_pair_opts& o, const std::vector
         }
         if (status[g] == KMP_OK && cnt[g] > r.cap) status[g] = KMP_EDEVICE;
     };
-    std::vector<std::thread> pool;
-    for (uint32_t g = 1; g < G; ++g) pool.emplace_back(work, g);
-    work(0);
-    for (auto& t : pool) t.join();
+    run_parts((int)G, [&](int g) { work((uint32_t)g); });
     KMP_TRY(c, use_device(c));
     for (uint32_t g = 0; g < G; ++g)
         if (status[g] != KMP_OK)
@@ -973,10 +1023,19 @@ int kmp_pairs(kmp_ctx* c, const kmp_pair_opts* opts, kmp_edges** out) {
     if (o.engine != KMP_ENGINE_TILES) {
         if (!c->postings) KMP_TRY(c, kmp_postings_create(&c->postings));
         const uint64_t slots = kmp_set_capacity(c->n, c->total_res);
-        if ((o.engine == KMP_ENGINE_AUTO || o.engine == KMP_ENGINE_RESIDUES) && (c->pass_keys || slots > kPassSlots)) {
+        const bool residues = o.engine == KMP_ENGINE_AUTO || o.engine == KMP_ENGINE_RESIDUES;
+        const bool scored = residues && o.score == KMP_SCORE_BLOSUM;  // the score summed in the reduction
+        if (residues && (c->pass_keys || slots > kPassSlots || (scored && kmp_dev_rows_max(c->n, 1) < c->n))) {
             uint64_t total = 0;
-            KMP_TRY(c, pass_pairs(c, o, &total));
-            return finish_edges(c, o, total, false, out);
+            KMP_TRY(c, pass_pairs(c, o, &total, scored));
+            return finish_edges(c, o, total, false, out, scored);
+        }
+        if (scored) {
+            uint64_t total = 0;
+            KMP_TRY(c, kmp_postings_set_reuse(c->postings, 0));
+            KMP_TRY(c, rows_into(c, c->postings, c->k_sets, o, 0, c->n, c->ep, c->eq, c->ew, c->edge_cap, 0, &total,
+                                 nullptr, &c->escore));
+            return finish_edges(c, o, total, false, out, true);
         }
         bool ok = false;
         for (int attempt = 0; attempt < 3 && !ok; ++attempt) {
@@ -1085,31 +1144,38 @@ int kmp_edges_get(const kmp_edges* e, uint32_t* p, uint32_t* q, uint32_t* w, flo
     return KMP_OK;
 }
 
+}  // extern "C" (templates below)
+
+// ---- streamed passes (kmp_pairs_stream) and the config-5 union (kmp_pairs_multi_k) ----
 // Config 5 of SURVEY.md §8d: w_k computed independently for each k; an edge is emitted when any
 // w_k >= min_shared (and, with require_class_diff, the classes differ).  Each k's sets are built
-// and kept (for the scores), each k gets its own workspace whose front (keys, grouping, heavy
-// compaction) is kept across the passes, and the rows run in passes (one when the batch is
-// small): per pass, every k's edges of the pass's rows (kmp_dev_pairs_rows), their per-k scores
-// (BLOSUM on the device), and the device union (kmp_merge.hip): w = Σ_k w_k, score = Σ_k score_k
-// (COUNT: score = w).  The context's sets are left at the last k.
-int kmp_pairs_multi_k(kmp_ctx* c, const kmp_pair_opts* opts, const int* ks, uint32_t nk, kmp_edges** out) {
-    if (!c || !out || !ks || nk < 1 || nk > KMP_MULTI_K_MAX) return KMP_EINVAL;
-    *out = nullptr;
-    c->err.clear();
-    kmp_pair_opts o;
-    kmp_pair_opts_default(&o);
-    if (opts) o = *opts;
-    if (o.score == KMP_SCORE_JACCARD) return fail(c, KMP_EINVAL, "JACCARD does not sum over k");
-    if (o.score != KMP_SCORE_COUNT && o.score != KMP_SCORE_BLOSUM) return fail(c, KMP_EINVAL, "unknown score %d", o.score);
+// and kept, each k gets its own workspace whose front (keys, grouping, heavy compaction) is kept
+// across the passes, and the rows run in passes (one when the batch is small): per pass, every
+// k's edges of the pass's rows (kmp_dev_pairs_rows[_scored]: BLOSUM summed inside the reduction)
+// and, for nk > 1, the device union (kmp_merge.hip): w = Σ_k w_k, score = Σ_k score_k.  The pass's
+// chunk is summarised on the device (kmp_stream.hip) and handed to the sink; the buffers are then
+// reused, so the whole list is never resident.  The context's sets are left at the last k.
+
+static int opts_multi(kmp_ctx* c, const kmp_pair_opts* opts, const int* ks, uint32_t nk, kmp_pair_opts* o) {
+    if (!ks || nk < 1 || nk > KMP_MULTI_K_MAX) return fail(c, KMP_EINVAL, "need 1 to %d values of k", KMP_MULTI_K_MAX);
+    kmp_pair_opts_default(o);
+    if (opts) *o = *opts;
+    if (o->score == KMP_SCORE_JACCARD) return fail(c, KMP_EINVAL, "JACCARD does not sum over k");
+    if (o->score != KMP_SCORE_COUNT && o->score != KMP_SCORE_BLOSUM) return fail(c, KMP_EINVAL, "unknown score %d", o->score);
+    if (o->engine != KMP_ENGINE_AUTO && o->engine != KMP_ENGINE_RESIDUES)
+        return fail(c, KMP_EINVAL, "streamed pairs run the residues engine (engine %d)", o->engine);
     for (uint32_t j = 0; j < nk; ++j) {
         if (ks[j] < 1 || ks[j] > kMaxK) return fail(c, KMP_EINVAL, "k = %d", ks[j]);
         for (uint32_t i = 0; i < j; ++i)
             if (ks[i] == ks[j]) return fail(c, KMP_EINVAL, "k = %d twice", ks[j]);
     }
     if (!c->loaded) return fail(c, KMP_ESTATE, "kmp_load_proteins first");
-    KMP_TRY(c, use_device(c));
+    return KMP_OK;
+}
+
+// every k's sets, stashed in its KSet (the caller swaps the last k's back: restore_ksets)
+static int prepare_ksets(kmp_ctx* c, const int* ks, uint32_t nk) {
     while (c->ksets.size() < nk) c->ksets.emplace_back(new kmp_ctx::KSet);
-    // every k's sets, stashed in its slot (the last k's are swapped back at the end)
     for (uint32_t j = 0; j < nk; ++j) {
         KMP_TRY(c, kmp_build_sets(c, ks[j]));
         kmp_ctx::KSet& s = *c->ksets[j];
@@ -1123,137 +1189,493 @@ int kmp_pairs_multi_k(kmp_ctx* c, const kmp_pair_opts* opts, const int* ks, uint
         if (!s.ws) KMP_TRY(c, kmp_postings_create(&s.ws));
         KMP_TRY(c, kmp_postings_set_reuse(s.ws, 1));
     }
-    auto restore = [&]() {  // the context keeps the last k's sets, as kmp_build_sets(ks[nk-1])
-        kmp_ctx::KSet& s = *c->ksets[nk - 1];
-        s.set.swap(c->set);
-        s.set_len.swap(c->set_len);
-        s.rep.swap(c->rep);
-        s.rep_len.swap(c->rep_len);
-        s.h_set_len.swap(c->h_set_len);
-        s.h_rep_len.swap(c->h_rep_len);
-        for (uint32_t j = 0; j < nk; ++j) (void)kmp_postings_set_reuse(c->ksets[j]->ws, 0);
-    };
+    return KMP_OK;
+}
+
+static void restore_ksets(kmp_ctx* c, uint32_t nk) {  // the context keeps the last k's sets
+    kmp_ctx::KSet& s = *c->ksets[nk - 1];
+    s.set.swap(c->set);
+    s.set_len.swap(c->set_len);
+    s.rep.swap(c->rep);
+    s.rep_len.swap(c->rep_len);
+    s.h_set_len.swap(c->h_set_len);
+    s.h_rep_len.swap(c->h_rep_len);
+    for (uint32_t j = 0; j < nk; ++j) (void)kmp_postings_set_reuse(c->ksets[j]->ws, 0);
+}
+
+// pinned host staging of a chunk (a host sink)
+struct HostChunk {
+    void* p = nullptr;
+    size_t bytes = 0;
+    ~HostChunk() {
+        if (p) (void)hipHostFree(p);
+    }
+    hipError_t reserve(size_t b) {
+        if (b <= bytes && p) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        bytes = 0;
+        hipError_t e = hipHostMalloc(&p, b ? b : 16, hipHostMallocDefault);
+        if (e == hipSuccess) bytes = b ? b : 16;
+        return e;
+    }
+};
+
+// One lane of the streamed passes: a device, its copy of the batch and stream, the rows it owns,
+// per-k workspaces and pass edges, the merged arrays (nk > 1) and its summary accumulators.
+struct StreamLane {
+    Lane L;
+    int device = 0;
+    uint32_t rank = 0, row_lo = 0, row_hi = 0;
+    std::vector<std::unique_ptr<kmp_kset>>* ks = nullptr;
+    DevBuf *ep = nullptr, *eq = nullptr, *ew = nullptr, *mscore = nullptr, *mwk = nullptr, *mscratch = nullptr;
+    kmp::DigestAcc* acc = nullptr;
+    uint64_t incidences = 0;
+    uint32_t passes = 0;
+};
+
+// The passes of the lane's rows: for each, the chunk on the lane's device, its summary into
+// lane.acc (device), then on_chunk(chunk).  The lane's workspaces keep their front across passes.
+template <class OnChunk>
+static int stream_passes(kmp_ctx* c, const kmp_pair_opts& o, const int* ks, uint32_t nk, StreamLane& ln,
+                         OnChunk on_chunk) {
+    auto& kv = *ln.ks;
+    while (kv.size() < nk) kv.emplace_back(new kmp_kset);
+    for (uint32_t j = 0; j < nk; ++j) {
+        kv[j]->k = ks[j];
+        if (!kv[j]->ws) KMP_TRY(c, kmp_postings_create(&kv[j]->ws));
+        KMP_TRY(c, kmp_postings_set_reuse(kv[j]->ws, 1));
+    }
+    const bool blosum = o.score == KMP_SCORE_BLOSUM;
     const uint64_t slots = kmp_set_capacity(c->n, c->total_res);
     PassPlan plan{c->n, (double)pass_budget(c)};
-    if (!c->pass_keys && slots <= kPassSlots) plan.density = 0;  // small batch: one pass
-    const bool blosum = o.score == KMP_SCORE_BLOSUM;
-    uint64_t off = 0, mcap = std::max<uint64_t>(c->edge_cap, 1u << 16);
+    plan.end = ln.row_hi;
+    const bool fused = nk == 2;  // both k reduced together (kmp_dev_pairs_rows_multi): no merge
+    if (fused) plan.max_rows = kmp_dev_rows_max(c->n, 2);
+    else if (blosum) plan.max_rows = kmp_dev_rows_max(c->n, 1);
+    if (!c->pass_keys && slots <= kPassSlots && plan.max_rows >= ln.row_hi - ln.row_lo)
+        plan.density = 0;  // small batch: one pass
+    const hipStream_t st = ln.L.stream;
+    uint64_t mcap = 0;
     int rc = KMP_OK;
-    uint32_t passes = 0;
-    auto grow_out = [&](uint64_t want) -> int {  // merged arrays: p q w (ctx), score, wk (nk x mcap)
-        if (want <= mcap && c->ep.p && c->mwk.p) return KMP_OK;
-        const uint64_t ncap = std::max(want, mcap);
-        uint64_t cap3 = mcap;
-        KMP_TRY(c, grow_edges(c, c->ep, c->eq, c->ew, cap3, ncap, off));
-        DevBuf ns, nw;
-        KMP_HIP(c, ns.reserve(ncap * 4));
-        KMP_HIP(c, nw.reserve((uint64_t)nk * ncap * 4));
-        if (off && c->mscore.p) KMP_HIP(c, hipMemcpyAsync(ns.p, c->mscore.p, off * 4, hipMemcpyDeviceToDevice, c->stream));
-        for (uint32_t j = 0; j < nk && off && c->mwk.p; ++j)
-            KMP_HIP(c, hipMemcpyAsync(nw.as<uint32_t>() + j * ncap, c->mwk.as<uint32_t>() + j * mcap, off * 4,
-                                      hipMemcpyDeviceToDevice, c->stream));
-        KMP_HIP(c, hipStreamSynchronize(c->stream));
-        c->mscore.swap(ns);
-        c->mwk.swap(nw);
-        mcap = ncap;
-        c->edge_cap = ncap;
-        return KMP_OK;
-    };
-    if ((rc = grow_out(mcap)) != KMP_OK) {
-        restore();
-        return rc;
-    }
-    c->edge_cap = mcap;
-    for (uint32_t a = 0; a < c->n && rc == KMP_OK;) {
-        const uint32_t b = plan.density == 0 ? c->n : plan.next(a);
+    for (uint32_t a = ln.row_lo; a < ln.row_hi && rc == KMP_OK;) {
+        const uint32_t b = plan.density == 0 ? ln.row_hi : plan.next(a);
         MergeIn in{};
         in.nk = nk;
-        uint64_t total = 0;
-        for (uint32_t j = 0; j < nk && rc == KMP_OK; ++j) {
-            kmp_ctx::KSet& s = *c->ksets[j];
-            kmp_postings_stats st{};
-            uint64_t ne = 0;
-            rc = rows_into(c, s.ws, s.k, o, a, b, s.ep, s.eq, s.ew, s.cap, 0, &ne, &st);
-            if (rc != KMP_OK) break;
-            if (plan.density != 0) plan.seen(a, b, st.incidences);
-            if (blosum && ne) {
-                if (s.score.bytes < ne * 4 && s.score.reserve(ne * 4) != hipSuccess) rc = fail(c, KMP_ENOMEM, "scores");
-                if (rc == KMP_OK)
-                    rc = edge_blosum_device(s.rep.as<uint32_t>(), s.rep_len.as<uint32_t>(), c->off.as<uint64_t>(),
-                                            s.ep.as<uint32_t>(), s.eq.as<uint32_t>(), s.ew.as<uint32_t>(), ne, s.k,
-                                            s.score.as<float>(), c->stream);
-                if (rc != KMP_OK) rc = fail(c, rc, "BLOSUM scores of k = %d: %s", s.k, kmp_status_string(rc));
+        uint64_t total = 0, inc = 0;
+        kmp_edge_chunk ch{};
+        if (fused) {
+            // p q w (ln.ep/eq/ew), score (ln.mscore), w0 | w1 (ln.mwk), grown on overflow
+            kmp_postings* wsp[2] = {kv[0]->ws, kv[1]->ws};
+            // edges <= incidences: size the arrays from the densest incidence rate seen (no rerun
+            // of the pass's expansion when the estimate holds)
+            const double est = plan.density > 0 ? plan.density * plan.mass(a, b) : 0.0;
+            if (est * 1.02 + 4096 > (double)mcap) mcap = (uint64_t)(est * 1.02) + 4096;
+            for (int attempt = 0; attempt < 3; ++attempt) {
+                if (!mcap || !ln.mwk->p) mcap = std::max<uint64_t>(mcap, 1u << 20);
+                uint64_t cap3 = 0;
+                if ((rc = grow_edges(c, *ln.ep, *ln.eq, *ln.ew, cap3, mcap, 0, ln.mscore, st)) != KMP_OK) break;
+                if (ln.mwk->reserve(2 * mcap * 4) != hipSuccess) {
+                    rc = fail(c, KMP_ENOMEM, "pass weights (%llu)", (unsigned long long)mcap);
+                    break;
+                }
+                kmp_postings_stats pst{};
+                rc = kmp_dev_pairs_rows_multi(wsp, ks, 2, ln.L.res, ln.L.off, ln.L.cls, c->n, slots, o.min_shared,
+                                              o.require_class_diff, a, b, ln.ep->as<uint32_t>(), ln.eq->as<uint32_t>(),
+                                              ln.ew->as<uint32_t>(), ln.mscore->as<uint32_t>(), ln.mwk->as<uint32_t>(),
+                                              ln.mwk->as<uint32_t>() + mcap, mcap, &total, &pst, st);
+                inc = pst.incidences;
+                if (rc == KMP_EOVERFLOW) {
+                    mcap = total + total / 8 + 1024;
+                    rc = KMP_OK;
+                    continue;
+                }
+                if (rc != KMP_OK) rc = fail(c, rc, "rows [%u, %u) of k = %d + %d: %s", a, b, ks[0], ks[1],
+                                            kmp_status_string(rc));
+                break;
             }
+            if (rc == KMP_OK && total > mcap) rc = fail(c, KMP_EDEVICE, "rows [%u, %u): edge count unstable", a, b);
+            if (rc != KMP_OK) break;
+            ch.n = total;
+            ch.p = ln.ep->as<uint32_t>();
+            ch.q = ln.eq->as<uint32_t>();
+            ch.w = ln.ew->as<uint32_t>();
+            ch.score = blosum ? ln.mscore->as<uint32_t>() : ch.w;
+            ch.wk[0] = ln.mwk->as<uint32_t>();
+            ch.wk[1] = ln.mwk->as<uint32_t>() + mcap;
+        }
+        for (uint32_t j = 0; j < nk && rc == KMP_OK && !fused; ++j) {
+            kmp_kset& s = *kv[j];
+            kmp_postings_stats pst{};
+            uint64_t ne = 0;
+            // nk > 1: every w_j >= 1 (the true w_j of each kept pair), min_shared applied by the merge
+            kmp_pair_opts oj = o;
+            if (nk > 1) oj.min_shared = 1;
+            rc = rows_into(c, s.ws, s.k, oj, a, b, s.ep, s.eq, s.ew, s.cap, 0, &ne, &pst, blosum ? &s.score : nullptr,
+                           &ln.L);
+            if (rc != KMP_OK) break;
+            inc += pst.incidences;
             in.p[j] = s.ep.as<uint32_t>();
             in.q[j] = s.eq.as<uint32_t>();
             in.w[j] = s.ew.as<uint32_t>();
-            in.s[j] = blosum ? s.score.as<float>() : nullptr;
+            in.s[j] = blosum ? s.score.as<uint32_t>() : s.ew.as<uint32_t>();  // COUNT: the merge sums w
             in.off[j] = total;
             total += ne;
         }
         if (rc != KMP_OK) break;
         in.off[nk] = total;
-        if ((rc = grow_out(off + total)) != KMP_OK) break;
-        const uint64_t sb = merge_scratch_bytes(total);
-        if (c->mscratch.bytes < sb && c->mscratch.reserve(sb) != hipSuccess) {
-            rc = fail(c, KMP_ENOMEM, "merge scratch");
+        if (plan.density != 0) plan.seen(a, b, inc);
+        ln.incidences += inc;
+        ch.rank = ln.rank;
+        ch.device = ln.device;
+        ch.row_lo = a;
+        ch.row_hi = b;
+        ch.on_device = 1;
+        if (fused) {
+            // the chunk was filled by the fused reduction
+        } else if (nk == 1) {
+            kmp_kset& s = *kv[0];
+            ch.n = total;
+            ch.p = s.ep.as<uint32_t>();
+            ch.q = s.eq.as<uint32_t>();
+            ch.w = s.ew.as<uint32_t>();
+            ch.score = in.s[0];
+            ch.wk[0] = ch.w;
+        } else {
+            if (total > mcap || !ln.mwk->p) {  // merged arrays: p q w, score, wk (nk x mcap)
+                mcap = total + total / 8 + (1u << 16);
+                uint64_t cap3 = 0;
+                if ((rc = grow_edges(c, *ln.ep, *ln.eq, *ln.ew, cap3, mcap, 0, nullptr, st)) != KMP_OK) break;
+                if (ln.mscore->reserve(mcap * 4) != hipSuccess || ln.mwk->reserve((uint64_t)nk * mcap * 4) != hipSuccess) {
+                    rc = fail(c, KMP_ENOMEM, "merged edge arrays (%llu)", (unsigned long long)mcap);
+                    break;
+                }
+            }
+            const uint64_t sb = merge_scratch_bytes(total);
+            if (ln.mscratch->bytes < sb && ln.mscratch->reserve(sb) != hipSuccess) {
+                rc = fail(c, KMP_ENOMEM, "merge scratch");
+                break;
+            }
+            MergeOut mo{};
+            mo.p = ln.ep->as<uint32_t>();
+            mo.q = ln.eq->as<uint32_t>();
+            mo.w = ln.ew->as<uint32_t>();
+            mo.s = ln.mscore->as<uint32_t>();
+            for (uint32_t j = 0; j < nk; ++j) mo.wk[j] = ln.mwk->as<uint32_t>() + j * mcap;
+            mo.cap = mcap;
+            mo.min_shared = std::max(1u, o.min_shared);
+            uint64_t m = 0;
+            rc = merge_edges_device(in, mo, ln.mscratch->p, ln.mscratch->bytes, &m, st);
+            if (rc != KMP_OK) {
+                rc = fail(c, rc, "merge: %s", kmp_status_string(rc));
+                break;
+            }
+            ch.n = m;
+            ch.p = mo.p;
+            ch.q = mo.q;
+            ch.w = mo.w;
+            ch.score = mo.s;
+            for (uint32_t j = 0; j < nk; ++j) ch.wk[j] = mo.wk[j];
+        }
+        kmp::DigestIn di{};
+        di.p = ch.p;
+        di.q = ch.q;
+        di.w = ch.w;
+        di.s = ch.score;
+        di.w0 = ch.wk[0];
+        di.n = ch.n;
+        di.n_prot = c->n;
+        di.row_lo = a;
+        di.row_hi = b;
+        di.cls = o.require_class_diff ? nullptr : ln.L.cls;
+        di.align_threshold = o.align_threshold;
+        if (kmp::edge_digest_enqueue(di, ln.acc, st) != hipSuccess) {
+            rc = fail(c, KMP_EDEVICE, "edge digest");
             break;
         }
-        MergeOut mo{};
-        mo.p = c->ep.as<uint32_t>() + off;
-        mo.q = c->eq.as<uint32_t>() + off;
-        mo.w = c->ew.as<uint32_t>() + off;
-        mo.s = blosum ? c->mscore.as<float>() + off : nullptr;
-        for (uint32_t j = 0; j < nk; ++j) mo.wk[j] = c->mwk.as<uint32_t>() + j * mcap + off;
-        mo.cap = mcap - off;
-        uint64_t m = 0;
-        rc = merge_edges_device(in, mo, c->mscratch.p, c->mscratch.bytes, &m, c->stream);
-        if (rc != KMP_OK) {
-            rc = fail(c, rc, "merge: %s", kmp_status_string(rc));
+        if (hipStreamSynchronize(st) != hipSuccess) {
+            rc = fail(c, KMP_EDEVICE, "stream synchronise");
             break;
         }
-        off += m;
+        ++ln.passes;
+        rc = on_chunk(ch);
         a = b;
-        ++passes;
     }
-    restore();
+    for (uint32_t j = 0; j < nk; ++j) (void)kmp_postings_set_reuse(kv[j]->ws, 0);
+    return rc;
+}
+
+// the context's lane (rank 0 of a multi-GPU context too): its batch, stream and buffers
+static StreamLane ctx_lane(kmp_ctx* c, uint32_t lo, uint32_t hi, DevBuf& dacc) {
+    StreamLane ln;
+    ln.L = Lane{c->res.as<uint8_t>(), c->off.as<uint64_t>(), c->cls.as<uint16_t>(), c->stream};
+    ln.device = c->device;
+    ln.row_lo = lo;
+    ln.row_hi = hi;
+    ln.ks = &c->ksets;
+    ln.ep = &c->ep;
+    ln.eq = &c->eq;
+    ln.ew = &c->ew;
+    ln.mscore = &c->mscore;
+    ln.mwk = &c->mwk;
+    ln.mscratch = &c->mscratch;
+    ln.acc = dacc.as<kmp::DigestAcc>();
+    return ln;
+}
+
+// summary of the lanes' device accumulators (+ the counters the context reports)
+static int finish_summary(kmp_ctx* c, const kmp_pair_opts& o, const std::vector<StreamLane*>& lanes,
+                          kmp_stream_summary* out) {
+    kmp_stream_summary sm{};
+    bool bad = false;
+    for (StreamLane* ln : lanes) {
+        kmp::DigestAcc h{};
+        KMP_HIP(c, hipSetDevice(ln->device));
+        KMP_HIP(c, hipMemcpyAsync(&h, ln->acc, sizeof h, hipMemcpyDeviceToHost, ln->L.stream));
+        KMP_HIP(c, hipStreamSynchronize(ln->L.stream));
+        for (int i = 0; i < KMP_DIGEST_SEGMENTS; ++i) {
+            sm.seg_edges[i] += h.seg_edges[i];
+            sm.seg_digest[i] += h.seg_digest[i];
+            sm.n_edges += h.seg_edges[i];
+            sm.digest += h.seg_digest[i];
+        }
+        sm.sum_w += h.tot[0];
+        sm.sum_score += h.tot[1];
+        sm.n_align += h.tot[2];
+        sm.sum_w_diff += h.tot[3];
+        sm.incidences += ln->incidences;
+        sm.passes += ln->passes;
+        bad |= h.bad != 0;
+    }
+    KMP_TRY(c, use_device(c));
+    // Σ w over class-differing pairs: every edge when the class filter is on
+    if (o.require_class_diff) sm.sum_w_diff = sm.sum_w;
+    sm.ordered = bad ? 0 : 1;
+    c->last_passes = sm.passes;
+    c->counters.n_edges = sm.n_edges;
+    c->counters.n_align = sm.n_align;
+    c->counters.sum_w_diff = sm.sum_w_diff;
+    if (out) *out = sm;
+    if (bad) return fail(c, KMP_EDEVICE, "a streamed chunk was not in canonical order inside its rows");
+    return KMP_OK;
+}
+
+// host copies of a device chunk (p q w score, and the nk weights when nk > 1) for a host sink
+static int chunk_to_host(kmp_ctx* c, const kmp_edge_chunk& ch, uint32_t nk, HostChunk& host, hipStream_t st,
+                         kmp_edge_chunk* hc) {
+    const uint32_t na = 4 + (nk > 1 ? nk : 0);
+    if (host.reserve(std::max<uint64_t>(1, ch.n) * 4 * na) != hipSuccess) return fail(c, KMP_ENOMEM, "pinned chunk");
+    uint32_t* hb = static_cast<uint32_t*>(host.p);
+    const uint32_t* src[4 + KMP_MULTI_K_MAX] = {ch.p, ch.q, ch.w, ch.score, ch.wk[0], ch.wk[1], ch.wk[2], ch.wk[3]};
+    for (uint32_t i = 0; i < na; ++i)
+        if (ch.n && hipMemcpyAsync(hb + i * ch.n, src[i], ch.n * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+            return fail(c, KMP_EDEVICE, "chunk copy");
+    if (hipStreamSynchronize(st) != hipSuccess) return fail(c, KMP_EDEVICE, "chunk copy");
+    *hc = ch;
+    hc->on_device = 0;
+    hc->p = hb;
+    hc->q = hb + ch.n;
+    hc->w = hb + 2 * ch.n;
+    hc->score = hb + 3 * ch.n;
+    for (uint32_t j = 0; j < KMP_MULTI_K_MAX; ++j) hc->wk[j] = j < nk ? (nk > 1 ? hb + (4 + j) * ch.n : hc->w) : nullptr;
+    return KMP_OK;
+}
+
+// rows [lo, hi) cut into parts ranges of equal pair mass (a pair belongs to its smaller protein)
+static std::vector<uint32_t> mass_split(uint32_t n, uint32_t lo, uint32_t hi, uint32_t parts) {
+    PassPlan pm{n, 0.0};
+    std::vector<uint32_t> start(parts + 1, lo);
+    const double total = pm.mass(lo, hi);
+    for (uint32_t d = 1; d < parts; ++d) {
+        const double want = total * d / parts;
+        uint32_t a = start[d - 1], b = hi;
+        while (a < b) {
+            const uint32_t mid = a + (b - a) / 2;
+            if (pm.mass(lo, mid) >= want) b = mid;
+            else a = mid + 1;
+        }
+        start[d] = a;
+    }
+    start[parts] = hi;
+    return start;
+}
+
+// every rank streams its own rows (one host thread per rank); the sink is called under a mutex
+static int multi_stream(kmp_ctx* c, const kmp_pair_opts& o, const int* ks, uint32_t nk, int sink_on_device,
+                        kmp_edge_sink sink, void* user, kmp_stream_summary* summary, uint32_t lo, uint32_t hi) {
+    const uint32_t G = (uint32_t)c->ranks.size();
+    const std::vector<uint32_t> start =
+        lo == 0 && hi == c->n ? [&] {
+            std::vector<uint32_t> s(G + 1);
+            kmp_row_split(c->n, G, s.data());
+            return s;
+        }()
+                              : mass_split(c->n, lo, hi, G);
+    std::vector<StreamLane> lanes(G);
+    std::vector<HostChunk> host(G);
+    std::vector<int> status(G, KMP_OK);
+    std::mutex sink_mu;
+    int sink_rc = KMP_OK;
+    for (uint32_t g = 0; g < G; ++g) {
+        kmp_rank& r = *c->ranks[g];
+        KMP_HIP(c, hipSetDevice(r.device));
+        KMP_HIP(c, r.dacc.reserve(sizeof(kmp::DigestAcc)));
+        KMP_HIP(c, hipMemsetAsync(r.dacc.p, 0, sizeof(kmp::DigestAcc), r.stream));
+        StreamLane& ln = lanes[g];
+        if (g == 0) {
+            ln = ctx_lane(c, start[0], start[1], r.dacc);
+        } else {
+            ln.L = Lane{r.res.as<uint8_t>(), r.off.as<uint64_t>(), r.cls.as<uint16_t>(), r.stream};
+            ln.device = r.device;
+            ln.row_lo = start[g];
+            ln.row_hi = start[g + 1];
+            ln.ks = &r.ksets;
+            ln.ep = &r.ep;
+            ln.eq = &r.eq;
+            ln.ew = &r.ew;
+            ln.mscore = &r.mscore;
+            ln.mwk = &r.mwk;
+            ln.mscratch = &r.mscratch;
+            ln.acc = r.dacc.as<kmp::DigestAcc>();
+        }
+        ln.rank = g;
+    }
+    run_parts((int)G, [&](int gi) {
+        const uint32_t g = (uint32_t)gi;
+        StreamLane& ln = lanes[g];
+        if (hipSetDevice(ln.device) != hipSuccess) {
+            status[g] = KMP_EDEVICE;
+            return;
+        }
+        status[g] = stream_passes(c, o, ks, nk, ln, [&](const kmp_edge_chunk& ch) -> int {
+            if (!sink) return KMP_OK;
+            kmp_edge_chunk hc = ch;
+            if (!sink_on_device) {
+                const int rc = chunk_to_host(c, ch, nk, host[g], ln.L.stream, &hc);
+                if (rc != KMP_OK) return rc;
+            }
+            std::lock_guard<std::mutex> lk(sink_mu);
+            if (sink_rc != KMP_OK) return sink_rc;  // another rank's sink stopped the stream
+            const int rc = sink(user, &hc);
+            if (rc != KMP_OK) sink_rc = rc;
+            return rc;
+        });
+    });
+    KMP_TRY(c, use_device(c));
+    for (uint32_t g = 0; g < G; ++g)
+        if (status[g] != KMP_OK) {
+            if (status[g] == sink_rc) return sink_rc;
+            return fail(c, status[g], "rank %u (device %d, rows [%u, %u)): stream: %s (%s)", g, lanes[g].device,
+                        start[g], start[g + 1], kmp_status_string(status[g]), c->err.c_str());
+        }
+    std::vector<StreamLane*> lp;
+    for (auto& ln : lanes) lp.push_back(&ln);
+    return finish_summary(c, o, lp, summary);
+}
+
+extern "C" {
+
+int kmp_ctx_set_rows(kmp_ctx* c, uint32_t row_lo, uint32_t row_hi) {
+    if (!c) return KMP_EINVAL;
+    if (row_lo > row_hi) return fail(c, KMP_EINVAL, "rows [%u, %u)", row_lo, row_hi);
+    c->rows_lo = row_lo;
+    c->rows_hi = row_hi;
+    return KMP_OK;
+}
+
+int kmp_pairs_stream(kmp_ctx* c, const kmp_pair_opts* opts, const int* ks, uint32_t nk, int sink_on_device,
+                     kmp_edge_sink sink, void* user, kmp_stream_summary* summary) {
+    if (!c) return KMP_EINVAL;
+    c->err.clear();
+    kmp_pair_opts o;
+    KMP_TRY(c, opts_multi(c, opts, ks, nk, &o));
+    KMP_TRY(c, use_device(c));
+    uint32_t lo = 0, hi = c->n;
+    if (c->rows_hi) {
+        if (c->rows_hi > c->n) return fail(c, KMP_EINVAL, "rows [%u, %u) past the batch (%u)", c->rows_lo, c->rows_hi, c->n);
+        lo = c->rows_lo;
+        hi = c->rows_hi;
+    }
+    KMP_TRY(c, prepare_ksets(c, ks, nk));  // the reference's counters per k (kmp_build_sets)
+    restore_ksets(c, nk);
+    if (c->ranks.size() > 1) return multi_stream(c, o, ks, nk, sink_on_device, sink, user, summary, lo, hi);
+    DevBuf dacc;
+    KMP_HIP(c, dacc.reserve(sizeof(kmp::DigestAcc)));
+    KMP_HIP(c, hipMemsetAsync(dacc.p, 0, sizeof(kmp::DigestAcc), c->stream));
+    StreamLane ln = ctx_lane(c, lo, hi, dacc);
+    HostChunk host;
+    int rc = stream_passes(c, o, ks, nk, ln, [&](const kmp_edge_chunk& ch) -> int {
+        if (!sink) return KMP_OK;
+        if (sink_on_device) return sink(user, &ch);
+        kmp_edge_chunk hc{};
+        KMP_TRY(c, chunk_to_host(c, ch, nk, host, c->stream, &hc));
+        return sink(user, &hc);
+    });
     if (rc != KMP_OK) return rc;
-    c->last_passes = passes;
+    return finish_summary(c, o, {&ln}, summary);
+}
+
+// kmp_pairs_multi_k: the stream, collected into one device list (D2D appends), then copied out
+int kmp_pairs_multi_k(kmp_ctx* c, const kmp_pair_opts* opts, const int* ks, uint32_t nk, kmp_edges** out) {
+    if (!c || !out) return KMP_EINVAL;
+    *out = nullptr;
+    c->err.clear();
+    kmp_pair_opts o;
+    KMP_TRY(c, opts_multi(c, opts, ks, nk, &o));
+    KMP_TRY(c, use_device(c));
+    const bool blosum = o.score == KMP_SCORE_BLOSUM;
+    // collected device arrays: p q w score w_0 .. w_{nk-1}, each cap entries
+    const uint32_t na = 4 + nk;
+    DevBuf all;
+    uint64_t cap = 0, count = 0;
+    DevBuf dacc;
+    KMP_HIP(c, dacc.reserve(sizeof(kmp::DigestAcc)));
+    KMP_HIP(c, hipMemsetAsync(dacc.p, 0, sizeof(kmp::DigestAcc), c->stream));
+    KMP_TRY(c, prepare_ksets(c, ks, nk));
+    restore_ksets(c, nk);
+    StreamLane ln = ctx_lane(c, 0, c->n, dacc);
+    KMP_TRY(c, stream_passes(c, o, ks, nk, ln, [&](const kmp_edge_chunk& ch) -> int {
+        if (count + ch.n > cap) {
+            const uint64_t ncap = std::max<uint64_t>(1u << 16, (count + ch.n) + (count + ch.n) / 4);
+            DevBuf nb;
+            KMP_HIP(c, nb.reserve(ncap * 4 * na));
+            for (uint32_t i = 0; i < na && count; ++i)
+                KMP_HIP(c, hipMemcpyAsync(nb.as<uint32_t>() + i * ncap, all.as<uint32_t>() + i * cap, count * 4,
+                                          hipMemcpyDeviceToDevice, c->stream));
+            KMP_HIP(c, hipStreamSynchronize(c->stream));
+            all.swap(nb);
+            cap = ncap;
+        }
+        const uint32_t* src[4 + KMP_MULTI_K_MAX] = {ch.p, ch.q, ch.w, ch.score, ch.wk[0], ch.wk[1], ch.wk[2], ch.wk[3]};
+        for (uint32_t i = 0; i < na && ch.n; ++i)
+            KMP_HIP(c, hipMemcpyAsync(all.as<uint32_t>() + i * cap + count, src[i], ch.n * 4, hipMemcpyDeviceToDevice,
+                                      c->stream));
+        KMP_HIP(c, hipStreamSynchronize(c->stream));
+        count += ch.n;
+        return KMP_OK;
+    }));
+    KMP_TRY(c, finish_summary(c, o, {&ln}, nullptr));
     std::unique_ptr<kmp_edges> e(new (std::nothrow) kmp_edges);
     if (!e) return fail(c, KMP_ENOMEM, "edges");
-    const uint64_t count = off;
     e->p.resize(count);
     e->q.resize(count);
     e->w.resize(count);
     e->score.resize(count);
     e->wk.resize((uint64_t)nk * count);
+    hvec<uint32_t> iscore(count);
     if (count) {
-        KMP_HIP(c, hipMemcpyAsync(e->p.data(), c->ep.p, count * 4, hipMemcpyDeviceToHost, c->stream));
-        KMP_HIP(c, hipMemcpyAsync(e->q.data(), c->eq.p, count * 4, hipMemcpyDeviceToHost, c->stream));
-        KMP_HIP(c, hipMemcpyAsync(e->w.data(), c->ew.p, count * 4, hipMemcpyDeviceToHost, c->stream));
-        if (blosum)
-            KMP_HIP(c, hipMemcpyAsync(e->score.data(), c->mscore.p, count * 4, hipMemcpyDeviceToHost, c->stream));
+        const uint32_t* d = all.as<uint32_t>();
+        KMP_HIP(c, hipMemcpyAsync(e->p.data(), d, count * 4, hipMemcpyDeviceToHost, c->stream));
+        KMP_HIP(c, hipMemcpyAsync(e->q.data(), d + cap, count * 4, hipMemcpyDeviceToHost, c->stream));
+        KMP_HIP(c, hipMemcpyAsync(e->w.data(), d + 2 * cap, count * 4, hipMemcpyDeviceToHost, c->stream));
+        KMP_HIP(c, hipMemcpyAsync(iscore.data(), d + 3 * cap, count * 4, hipMemcpyDeviceToHost, c->stream));
         for (uint32_t j = 0; j < nk; ++j)
-            KMP_HIP(c, hipMemcpyAsync(e->wk.data() + j * count, c->mwk.as<uint32_t>() + j * mcap, count * 4,
-                                      hipMemcpyDeviceToHost, c->stream));
+            KMP_HIP(c, hipMemcpyAsync(e->wk.data() + j * count, d + (4 + j) * cap, count * 4, hipMemcpyDeviceToHost,
+                                      c->stream));
     }
     KMP_HIP(c, hipStreamSynchronize(c->stream));
-    kmp_edges* E = e.get();
-    const EdgeScan sc = scan_edges(count, c->threads, [&](uint64_t i, EdgeScan& s) {
-        const uint32_t p = E->p[i], q = E->q[i], w = E->w[i];
-        if (p >= q || q >= c->n) return false;
-        if (!blosum) E->score[i] = (float)w;
-        if (w > o.align_threshold) ++s.nalign;
-        if (c->h_cls[p] != c->h_cls[q]) s.wdiff += w;
-        return true;
-    });
-    if (sc.bad != ~0ull)
-        return fail(c, KMP_EDEVICE, "device edge %llu = (%u, %u) is not a pair of the batch",
-                    (unsigned long long)sc.bad, E->p[sc.bad], E->q[sc.bad]);
+    for (uint64_t i = 0; i < count; ++i) e->score[i] = blosum ? (float)iscore[i] : (float)e->w[i];
     e->ks.assign(ks, ks + nk);
-    c->counters.n_edges = count;
-    c->counters.n_align = sc.nalign;
-    c->counters.sum_w_diff = sc.wdiff;
     *out = e.release();
     return KMP_OK;
 }
@@ -1352,4 +1774,16 @@ int kmp_edges_reference_keys(const kmp_edges* e, uint64_t* keys, uint64_t cap, u
 
 void kmp_edges_free(kmp_edges* e) { delete e; }
 
+uint64_t kmp_edge_digest_term(uint32_t p, uint32_t q, uint32_t w, uint32_t score, uint32_t w0) {
+    auto m = [](uint64_t z) {
+        z += 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return z ^ (z >> 31);
+    };
+    const uint64_t a = (uint64_t)p << 32 | q, b = (uint64_t)w << 32 | score;
+    return m(a ^ m(b ^ m((uint64_t)w0)));
+}
+
 }  // extern "C"
+

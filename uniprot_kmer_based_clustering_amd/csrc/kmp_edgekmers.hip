@@ -13,6 +13,8 @@
 //     (min shared id, p, q) (combine_edges with one thread).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
@@ -89,7 +91,9 @@ __constant__ int8_t c_b62_diag[21] = {9, 4, 5, 4, 6, 7, 6, 5, 5, 6, 8, 5, 5, 5, 
 // per code of the shorter set; here they are LDS reads.  An edge whose set(p) exceeds the slice
 // searches set(p) in global memory instead.  The walk of set(q) stops once the wave has seen the
 // edge's w hits (w = the shared k-mer count the pipeline computed): a list with fewer hits than its
-// w is still flagged, one with extra hits only if they fall in the chunk of 64 that reaches w.
+// w is still flagged, one with extra hits only if they fall in the chunk of 64 that reaches w —
+// so w must be exact (as every engine's is).  full (KMP_DEBUG set): every set(q) is walked to its
+// end, and any hit count other than w flags the list as foreign.
 constexpr uint32_t kBlWaves = 4, kBlSlice = 2048, kBlTask = 64;
 __global__ __launch_bounds__(256) void edge_blosum_lds_kernel(const uint32_t* __restrict__ rep,
                                                               const uint32_t* __restrict__ rep_len,
@@ -97,7 +101,8 @@ __global__ __launch_bounds__(256) void edge_blosum_lds_kernel(const uint32_t* __
                                                               const uint32_t* __restrict__ ep,
                                                               const uint32_t* __restrict__ eq,
                                                               const uint32_t* __restrict__ ew, uint64_t count, int k,
-                                                              float* __restrict__ score, unsigned int* __restrict__ bad) {
+                                                              float* __restrict__ score, unsigned int* __restrict__ bad,
+                                                              int full) {
     __shared__ uint32_t S[kBlWaves][kBlSlice];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint32_t* P = S[wv];
@@ -129,7 +134,7 @@ __global__ __launch_bounds__(256) void edge_blosum_lds_kernel(const uint32_t* __
                 }
                 const uint32_t* B = rep + set_base(off[b], b);
                 // set(q) is sorted: the last lane's insertion point bounds the next chunk's searches
-                for (uint32_t c = 0, seen = 0, base = 0; c < lb && seen < w; c += 64) {
+                for (uint32_t c = 0, seen = 0, base = 0; c < lb && (full || seen < w); c += 64) {
                     const uint32_t i = c + lane;
                     bool hit = false;
                     uint32_t lo = base;
@@ -150,7 +155,7 @@ __global__ __launch_bounds__(256) void edge_blosum_lds_kernel(const uint32_t* __
             } else {
                 const uint32_t* A = rep + set_base(off[a], a);
                 const uint32_t* B = rep + set_base(off[b], b);
-                for (uint32_t c = 0, seen = 0; c < lb && seen < w; c += 64) {
+                for (uint32_t c = 0, seen = 0; c < lb && (full || seen < w); c += 64) {
                     const uint32_t i = c + lane;
                     bool hit = false;
                     if (i < lb) {
@@ -256,7 +261,7 @@ int edge_blosum_device(const uint32_t* d_rep, const uint32_t* d_rep_len, const u
         const uint64_t tasks = (count + kBlTask - 1) / kBlTask;
         const uint32_t lblocks = (uint32_t)std::min<uint64_t>((tasks + kBlWaves - 1) / kBlWaves, 8192);
         edge_blosum_lds_kernel<<<lblocks, 256, 0, st>>>(d_rep, d_rep_len, d_off, d_p, d_q, d_w, count, k, d_score,
-                                                         bad);
+                                                         bad, getenv("KMP_DEBUG") != nullptr ? 1 : 0);
         if (hipGetLastError() != hipSuccess ||
             hipMemcpyAsync(&h_bad, bad, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
             hipStreamSynchronize(st) != hipSuccess)

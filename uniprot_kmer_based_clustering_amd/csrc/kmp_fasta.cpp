@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "kmerpair.h"
+#include "kmp_threads.hpp"
 
 namespace {
 
@@ -136,10 +137,7 @@ int threads_for(int t) {
 
 template <class F>
 void parallel(int T, F f) {
-    std::vector<std::thread> pool;
-    for (int t = 1; t < T; ++t) pool.emplace_back(f, t);
-    f(0);
-    for (auto& th : pool) th.join();
+    kmp::run_parts(T, f);
 }
 
 }  // namespace

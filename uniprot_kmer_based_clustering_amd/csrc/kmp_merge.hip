@@ -32,10 +32,24 @@ __global__ void merge_keys_kernel(kmp::MergeIn in, uint64_t total, unsigned long
     }
 }
 
-__global__ void merge_heads_kernel(const unsigned long long* __restrict__ key, uint64_t total,
+// a head (first entry of a run = one pair) that some w_j reaches min_shared with
+__global__ void merge_heads_kernel(kmp::MergeIn in, const unsigned long long* __restrict__ key,
+                                   const uint32_t* __restrict__ val, uint64_t total, uint32_t min_shared,
                                    uint32_t* __restrict__ head) {
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i <= total; i += (uint64_t)gridDim.x * blockDim.x)
-        head[i] = i < total && (i == 0 || key[i] != key[i - 1]);
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i <= total; i += (uint64_t)gridDim.x * blockDim.x) {
+        bool h = i < total && (i == 0 || key[i] != key[i - 1]);
+        if (h && min_shared > 1) {
+            bool keep = false;
+            for (uint64_t t = i; t < total && key[t] == key[i]; ++t) {
+                const uint64_t g = val[t];
+                uint32_t j = 0;
+                while (j + 1 < in.nk && g >= in.off[j + 1]) ++j;
+                keep |= in.w[j][g - in.off[j]] >= min_shared;
+            }
+            h = keep;
+        }
+        head[i] = h;
+    }
 }
 
 __global__ void merge_write_kernel(kmp::MergeIn in, const unsigned long long* __restrict__ key,
@@ -43,10 +57,11 @@ __global__ void merge_write_kernel(kmp::MergeIn in, const unsigned long long* __
                                    kmp::MergeOut out) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
         if (i && key[i] == key[i - 1]) continue;  // not a head
+        if (pos[i + 1] == pos[i]) continue;      // a pair no w_j reaches min_shared with
         const uint64_t o = pos[i];
         if (o >= out.cap) continue;
         uint32_t wsum = 0;
-        float ssum = 0.0f;
+        uint32_t ssum = 0;
         uint32_t wk[KMP_MULTI_K_MAX] = {0, 0, 0, 0};
         for (uint64_t t = i; t < total && key[t] == key[i]; ++t) {
             const uint64_t g = val[t];
@@ -103,7 +118,7 @@ int merge_edges_device(const MergeIn& in, const MergeOut& out, void* scratch, ui
     merge_keys_kernel<<<grid, 256, 0, st>>>(in, total, k0, v0);
     if (rocprim::radix_sort_pairs<SortCfg>(tmp, tb, k0, k1, v0, v1, (size_t)total, 0u, 64u, st) != hipSuccess)
         return KMP_EDEVICE;
-    merge_heads_kernel<<<grid, 256, 0, st>>>(k1, total, head);
+    merge_heads_kernel<<<grid, 256, 0, st>>>(in, k1, v1, total, out.min_shared, head);
     tb = scratch_bytes - (uint64_t)(static_cast<char*>(tmp) - static_cast<char*>(scratch));
     if (rocprim::exclusive_scan(tmp, tb, head, pos, 0u, (size_t)total + 1, rocprim::plus<uint32_t>(), st) != hipSuccess)
         return KMP_EDEVICE;

@@ -20,6 +20,7 @@
 
 #include "kmerpair.h"
 #include "kmp_edges.hpp"
+#include "kmp_threads.hpp"
 
 namespace {
 
@@ -134,10 +135,7 @@ int kmp_write_candidates(const kmp_edges* e, const uint8_t* residues, const uint
         }
     };
     const int t = threads_for(threads);
-    std::vector<std::thread> pool;
-    for (int i = 1; i < t; ++i) pool.emplace_back(work);
-    work();
-    for (auto& th : pool) th.join();
+    kmp::run_parts(t, [&](int) { work(); });
     if (err.load() != KMP_OK) return err.load();
     static const char kHeader[] =
         "query id\tquery length\tsubject id\tsubject length\tquery alignment start\tquery alignment end\t"
@@ -171,17 +169,13 @@ int kmp_write_graph_debug(const kmp_edges* e, uint32_t n, const char* path, int 
     const uint64_t chunk = 1 << 16;
     for (uint64_t b = 0; b < count; b += chunk * t) {
         std::vector<std::string> part(t);
-        std::vector<std::thread> pool;
-        for (int j = 0; j < t; ++j) {
-            pool.emplace_back([&, j]() {
-                const uint64_t lo = b + j * chunk, hi = std::min<uint64_t>(lo + chunk, count);
-                for (uint64_t r = lo; r < hi; ++r) {
-                    const uint64_t i = order[r];
-                    format_edge(part[j], e->kmers.data() + e->kofs[i], e->kofs[i + 1] - e->kofs[i]);
-                }
-            });
-        }
-        for (auto& th : pool) th.join();
+        kmp::run_parts(t, [&](int j) {
+            const uint64_t lo = b + j * chunk, hi = std::min<uint64_t>(lo + chunk, count);
+            for (uint64_t r = lo; r < hi; ++r) {
+                const uint64_t i = order[r];
+                format_edge(part[j], e->kmers.data() + e->kofs[i], e->kofs[i + 1] - e->kofs[i]);
+            }
+        });
         for (auto& s : part) put(s);
     }
     std::string s;

@@ -24,11 +24,14 @@
 
 #include <rocprim/block/block_radix_sort.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_reduce_by_key.hpp>
 #include <rocprim/device/device_segmented_radix_sort.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
 #include <rocprim/device/device_run_length_encode.hpp>
 #include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -555,6 +558,27 @@ __global__ void bucket_bounds_kernel(const unsigned long long* __restrict__ k, u
 }
 
 constexpr uint32_t kHeavySub = 128;  // larger sub-buckets (very frequent k-mers) -> flat layout
+
+// ---- BLOSUM score carried in the pair key (a build extension) ----
+// A scored call writes every (k-mer, pair) incidence as (pair << sb) | sor | s(x): s(x) = Σ_i
+// B62[x_i][x_i] over the k residues of the shared k-mer x (the BLOSUM62 diagonal of blosum.rs:8-30
+// in residue-code order, code 20 scored 0; at most 7 x 11 = 77, kScoreBits bits) and sor the call's
+// k-index bit (kmp_pairs_multi_k's fused union: bit kScoreBits marks the second k).  The row-block
+// tail then sums s over each pair's run (score = Σ_{x in K(p) ∩ K(q)} s(x)) and counts the marked
+// entries (w of the second k), so no per-edge intersection runs at all.  h(code) = code * kHashA
+// is a bijection of u32: the k-mer's code is h * kHashAInv.
+constexpr unsigned kScoreBits = 7;
+constexpr uint32_t kHashAInv = 0x0E8B2F51u;  // kHashA^-1 mod 2^32
+__constant__ uint8_t c_b62_self[21] = {9, 4, 5, 4, 6, 7, 6, 5, 5, 6, 8, 5, 5, 5, 4, 4, 4, 11, 7, 6, 0};
+__device__ __forceinline__ uint32_t kmer_self_score(uint32_t h, int k) {
+    uint32_t x = h * kHashAInv, sc = 0;
+    for (int i = 0; i < k; ++i) {
+        const uint32_t q = x / 21u;
+        sc += c_b62_self[x - q * 21u];
+        x = q;
+    }
+    return sc;
+}
 constexpr int kShards = 64;          // output cursors (one per bucket residue mod kShards)
 static_assert(kShards == 64, "the heavy tiles hash to a shard with a 6-bit shift");
 // device flags of a step (ws->flags): a coarse bin above its level-2 tile budget, a class id too
@@ -622,6 +646,10 @@ struct BucketArgs {
     // flags[kFlSegs], the largest in flags[kFlSegMax]; the heavy path sorts each in LDS
     unsigned long long* seg;
     uint32_t seg_cap;
+    // scored calls (kScore kernels): pair keys (pair << sb) | sor | s(x), s(x) of the group's k-mer
+    int k;
+    unsigned sb;
+    uint32_t sor;
 };
 
 // descriptor: spill index (40 bits) | keys (23 bits) << 40 | whole bucket (several k-mers) << 63
@@ -653,7 +681,7 @@ __device__ __forceinline__ void spill_segment(const BucketArgs& a, uint64_t pos,
 // and the count table share H, and T shrinks to the per-position array: 18.9 KB of LDS at the
 // small geometry, 8 workgroups (32 waves) per CU instead of 6
 constexpr unsigned kMergeMinBits = 11;
-template <int kCap, int kThreads, int kTabBits, bool kMerge, bool kRows>
+template <int kCap, int kThreads, int kTabBits, bool kMerge, bool kRows, bool kScore>
 __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArgs& a, bool small) {
     constexpr int kE = kCap / kThreads;
     constexpr uint32_t kTab = 1u << kTabBits;
@@ -805,7 +833,11 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
     __syncthreads();
 #pragma unroll
     for (int e = 0; e < kE; ++e)
-        if (rk[e] == 0 && cn[e] >= 2) H[sl[e]] = cn[e] > kHeavySub ? rr[e] : ((SZ[cn[e]] + rr[e] * cn[e]) << 8) | cn[e];
+        if (rk[e] == 0 && cn[e] >= 2) {
+            // start << 8 | size (start < 4,096: 20 bits); scored: s(x) of the group's k-mer on top
+            const uint32_t sc = kScore && cn[e] <= kHeavySub ? kmer_self_score((uint32_t)(xk[e] >> hshift), a.k) << 24 : 0u;
+            H[sl[e]] = cn[e] > kHeavySub ? rr[e] : ((SZ[cn[e]] + rr[e] * cn[e]) << 8) | cn[e] | sc;
+        }
     __syncthreads();
     // C. scatter (T now holds, per position, its group's start << 8 | size); heavy groups' keys
     // go to the spill region
@@ -823,7 +855,7 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
             }
             continue;
         }
-        const uint32_t pos = (g >> 8) + rk[e];
+        const uint32_t pos = (kScore ? (g >> 8) & 0xFFFFu : g >> 8) + rk[e];
         Bl[pos] = xl[e];
         T[pos] = g;
     }
@@ -837,7 +869,7 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
         s[e] = en[e] = 0;
         if (i >= nm) continue;
         const uint32_t g = T[i];
-        s[e] = g >> 8;
+        s[e] = kScore ? (g >> 8) & 0xFFFFu : g >> 8;
         en[e] = s[e] + (g & 255u);
         xl[e] = Bl[i];
         for (uint32_t j = s[e]; j < i; ++j)
@@ -972,10 +1004,16 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
             if (!cnt[e]) continue;
             const uint32_t i = tid + e * kThreads;
             const uint32_t p = xl[e] >> cb;
+            // scored: every key of the element carries its k-mer's self-score and the call's k bit
+            const uint32_t sfield = kScore ? a.sor | T[s[e]] >> 24 : 0u;
+            auto pkey = [&](uint32_t q) {
+                const unsigned long long pk = (unsigned long long)min(p, q) * a.mul + max(p, q);
+                return kScore ? pk << a.sb | sfield : pk;
+            };
             if (mask_mode(e)) {
                 for (uint32_t m = cnt[e]; m; m &= m - 1) {
                     const uint32_t q = Bl[i + 1 + __builtin_ctz(m)] >> cb;
-                    put((unsigned long long)min(p, q) * a.mul + max(p, q));
+                    put(pkey(q));
                 }
                 continue;
             }
@@ -985,7 +1023,7 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
                 if (a.require_diff && !((lj ^ xl[e]) & cmask)) continue;
                 const uint32_t q = lj >> cb;
                 if (kRows && q <= p) continue;
-                put((unsigned long long)min(p, q) * a.mul + max(p, q));
+                put(pkey(q));
             }
         }
     };
@@ -1006,17 +1044,17 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
     }
 }
 
-template <int kCap, int kThreads, int kTabBits, bool kMerge, bool kRows>
+template <int kCap, int kThreads, int kTabBits, bool kMerge, bool kRows, bool kScore>
 __global__ __launch_bounds__(kThreads) void bucket_small_kernel(BucketArgs a, uint32_t b0) {
-    process_bucket<kCap, kThreads, kTabBits, kMerge, kRows>(b0 + blockIdx.x, a, true);
+    process_bucket<kCap, kThreads, kTabBits, kMerge, kRows, kScore>(b0 + blockIdx.x, a, true);
 }
 
 // the buckets the small kernel listed (above its capacity), a grid-stride loop over the list
-template <int kCap, int kThreads, int kTabBits, bool kRows>
+template <int kCap, int kThreads, int kTabBits, bool kRows, bool kScore>
 __global__ __launch_bounds__(kThreads) void bucket_large_kernel(BucketArgs a) {
     const uint32_t m = *a.list_count;
     for (uint32_t i = blockIdx.x; i < m; i += gridDim.x)
-        process_bucket<kCap, kThreads, kTabBits, false, kRows>(a.list[i], a, false);
+        process_bucket<kCap, kThreads, kTabBits, false, kRows, kScore>(a.list[i], a, false);
 }
 
 
@@ -1208,7 +1246,8 @@ __global__ __launch_bounds__(kHvThreads) void heavy_compact_kernel(const unsigne
                                                                    uint32_t* __restrict__ E,
                                                                    uint64_t* __restrict__ GS,
                                                                    uint32_t* __restrict__ RUN,
-                                                                   uint64_t* __restrict__ RH) {
+                                                                   uint64_t* __restrict__ RH,
+                                                                   uint32_t* __restrict__ GH) {
     __shared__ uint32_t wave_tot[kHvThreads / 64];
     const uint64_t t0 = (uint64_t)blockIdx.x * kHvTile;
     uint64_t eb = eoff[blockIdx.x], gb = goff[blockIdx.x], rb = ho.cls ? roff[blockIdx.x] : 0;
@@ -1228,7 +1267,10 @@ __global__ __launch_bounds__(kHvThreads) void heavy_compact_kernel(const unsigne
         block_scan_n<kHvThreads>(ke, xe, te, wave_tot);
         block_scan_n<kHvThreads>(kg, xg, tg, wave_tot);
         if (ke) E[eb + xe] = ho.elem(v);
-        if (kg) GS[gb + xg] = eb + xe;  // a k-mer head is always a new element
+        if (kg) {
+            GS[gb + xg] = eb + xe;  // a k-mer head is always a new element
+            GH[gb + xg] = (uint32_t)(v >> ho.hshift);  // the k-mer's h (scored calls: its self-score)
+        }
         if (ho.cls) {
             uint32_t xr, tr;
             block_scan_n<kHvThreads>(kr, xr, tr, wave_tot);
@@ -1358,7 +1400,9 @@ __global__ __launch_bounds__(kHvI) void heavy_expand_kernel(const uint32_t* __re
                                                             uint32_t row_lo, uint32_t row_hi,
                                                             unsigned long long* __restrict__ out, uint64_t shard_cap,
                                                             unsigned long long* __restrict__ cursor,
-                                                            unsigned long long* __restrict__ gstats) {
+                                                            unsigned long long* __restrict__ gstats,
+                                                            const uint32_t* __restrict__ GH, int k, unsigned sb,
+                                                            uint32_t sor) {
     __shared__ uint32_t J[kHvJ];
     __shared__ uint32_t s_ex[kHvI + 1], s_js[kHvI], s_p[kHvI];
     __shared__ unsigned long long s_sb[kShards];  // spread tile: shard base minus its first output
@@ -1396,6 +1440,11 @@ __global__ __launch_bounds__(kHvI) void heavy_expand_kernel(const uint32_t* __re
         const uint64_t b = GS[g];
         const uint32_t d = (uint32_t)(GS[g + 1] - b), i0 = gi[2 * g], i1 = gi[2 * g + 1];
         const uint32_t local = (uint32_t)(t - toff[g]);
+        // pair key; scored (sb > 0): (pair << sb) | sor | s(x) of this k-mer
+        const uint32_t sfield = sb ? sor | kmer_self_score(GH[g], k) : 0u;
+        auto mk = [&](uint32_t pa, uint32_t pb) {
+            return ((unsigned long long)min(pa, pb) * mul + max(pa, pb)) << sb | sfield;
+        };
         if (i0 == kHvFlatMark) {  // flat tile (uniform over the workgroup)
             const uint32_t nr = i1, ra = RUN[b];
             __syncthreads();  // the run table's reuse
@@ -1440,7 +1489,7 @@ __global__ __launch_bounds__(kHvI) void heavy_expand_kernel(const uint32_t* __re
                 const uint32_t row = f_s[r] + (uint32_t)(off / part), j = f_e[r] + (uint32_t)(off % part);
                 const uint32_t pa = E[b + row] >> cb, pj = E[b + j] >> cb;
                 const unsigned long long pos = sbase + u;
-                if (pos < shard_cap) dst[pos] = (unsigned long long)min(pa, pj) * mul + max(pa, pj);
+                if (pos < shard_cap) dst[pos] = mk(pa, pj);
             }
             continue;
         }
@@ -1511,7 +1560,7 @@ __global__ __launch_bounds__(kHvI) void heavy_expand_kernel(const uint32_t* __re
                     const uint32_t xj = J[j - j0];
                     if (!keep(xj)) continue;
                     const uint32_t pj = xj >> cb;
-                    if (pos < shard_cap) dst[pos] = (unsigned long long)min(pi, pj) * mul + max(pi, pj);
+                    if (pos < shard_cap) dst[pos] = mk(pi, pj);
                     ++pos;
                 }
             }
@@ -1538,7 +1587,7 @@ __global__ __launch_bounds__(kHvI) void heavy_expand_kernel(const uint32_t* __re
             for (uint32_t o = threadIdx.x; o < total; o += kHvI) {
                 while (s_ex[i + 1] <= o) ++i;
                 const uint32_t pa = s_p[i], pj = J[s_js[i] + (o - s_ex[i]) - j0] >> cb;
-                const unsigned long long key = (unsigned long long)min(pa, pj) * mul + max(pa, pj);
+                const unsigned long long key = mk(pa, pj);
                 if (spread) {
                     while (o >= sh_end) {
                         ++sh;
@@ -2258,18 +2307,18 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scatter2g_kernel(const unsigne
 // above it is a > 4-sigma event (the large kernel takes those)
 constexpr uint32_t kBucketCap1024Mean = 800;  // at config 3 (mean 897) the 1,280 variant measured faster
 // buckets [b0, b0 + nb)
-template <bool kRows>
+template <bool kRows, bool kScore>
 void launch_buckets(const BucketArgs& a, uint32_t b0, uint32_t nb, hipStream_t st) {
     if (a.lay.bbits >= kMergeMinBits && a.lay.mean_keys <= kBucketCap1024Mean)  // four keys per thread
-        bucket_small_kernel<1024, kBucketSmallThreads, kBucketSmallTab, true, kRows>
+        bucket_small_kernel<1024, kBucketSmallThreads, kBucketSmallTab, true, kRows, kScore>
             <<<nb, kBucketSmallThreads, 0, st>>>(a, b0);
     else if (a.lay.bbits >= kMergeMinBits)
-        bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallTab, true, kRows>
+        bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallTab, true, kRows, kScore>
             <<<nb, kBucketSmallThreads, 0, st>>>(a, b0);
     else
-        bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallTab, false, kRows>
+        bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallTab, false, kRows, kScore>
             <<<nb, kBucketSmallThreads, 0, st>>>(a, b0);
-    bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeTab, kRows>
+    bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeTab, kRows, kScore>
         <<<kBucketLargeGrid, kBucketLargeThreads, 0, st>>>(a);
 }
 
@@ -2297,8 +2346,9 @@ __global__ void keep_flags_kernel(const uint32_t* __restrict__ w, const uint32_t
 }
 
 // bumped on every reallocation of a workspace buffer: a captured step graph is valid only for the
-// generation it was captured in
-unsigned long long g_grow_gen = 0;
+// generation it was captured in.  Atomic: the ranks of a multi-GPU context reserve from one host
+// thread each at the same time (kmp_api.cpp split_rank_edges / rows_rank_edges)
+std::atomic<unsigned long long> g_grow_gen{0};
 
 template <class T>
 struct Grow {
@@ -2306,7 +2356,7 @@ struct Grow {
     size_t n = 0;
     hipError_t reserve(size_t m) {
         if (m <= n && p) return hipSuccess;
-        ++g_grow_gen;
+        g_grow_gen.fetch_add(1, std::memory_order_relaxed);
         if (p) (void)hipFree(p);
         p = nullptr;
         n = 0;
@@ -2341,7 +2391,10 @@ struct kmp_postings {
     Grow<unsigned long long> ovk;  // their keys tagged, sorted, encoded (pt_finish_overflow)
     Grow<unsigned long long> ovx;  // per listed block: offset of its keys
     Grow<uint32_t> ovr;            // run lengths, kept flags and positions, first run per block
+    Grow<uint32_t> ova;            // scored: per run (w, w1, score)
+    Grow<uint32_t> stg2;           // scored tail: staged scores | second-k weights
     uint64_t pt_inc = 0;        // incidences of the last call (row-block sizing)
+    uint64_t last_most = 0;     // expand-only call: the fullest shard region (sizes the next call's)
     Grow<unsigned long long> split_cur;  // k-mer split: per-destination send cursors
     std::vector<unsigned long long> split_shape;
     unsigned pt_rb_max = 16;    // rows-per-block bound learned from overflowing row blocks
@@ -2364,7 +2417,7 @@ struct kmp_postings {
     // heavy path (frequent k-mers): spill regions, the gathered + sorted spill, its elements,
     // k-mer starts, per-k-mer row bounds / tile counts / tile offsets
     Grow<unsigned long long> spill, hkeys, hsorted, hGS, htc, htoff, hoff, hRH, hseg;
-    Grow<uint32_t> hE, hgi, hcnt, hrun, hblk;
+    Grow<uint32_t> hE, hgi, hcnt, hrun, hblk, hGH;  // hGH: each heavy k-mer's h
     uint64_t spill_cap = 0;     // keys per spill shard region
     bool heavy = false;         // this workspace's batches spill: run the split step
     bool heavy_ready = false;   // hE / hGS hold the current front's compacted spill
@@ -2404,7 +2457,8 @@ struct kmp_postings {
         for (auto* g : {&keys, &sorted, &inc, &inc_sorted, &uniq, &bstats, &btot, &boff, &spill, &hkeys, &hsorted,
                         &hGS, &htc, &htoff, &hoff, &hRH, &hseg, &ovk, &ovx, &split_cur})
             g->release();
-        for (auto* g : {&w, &keep, &pos, &small, &cnt, &flags, &chunk_first, &bp, &pt, &ovf, &ovr, &hE, &hgi, &hcnt, &hrun, &hblk, &cur})
+        for (auto* g : {&w, &keep, &pos, &small, &cnt, &flags, &chunk_first, &bp, &pt, &ovf, &ovr, &ova, &stg2, &hE, &hgi, &hcnt,
+                        &hrun, &hblk, &cur, &hGH})
             g->release();
         tmp.release();
         for (auto& e : ev)
@@ -2652,6 +2706,8 @@ constexpr uint32_t kPtMaxBlocks = 8192;  // row blocks (LDS histogram of pt_hist
 
 struct PtGeom {
     unsigned pbits, rbits;  // key = p << pbits | q; rows per block = 1 << rbits
+    unsigned sbits;         // scored: the score field below the pair ((pair << sbits) | field), else 0
+    int kbit;               // scored multi-k: bit kScoreBits of the field marks the second k (w1 counted)
     uint32_t nrb;           // row blocks, from row row0
     uint32_t jt;            // tiles per shard region
     uint64_t sc;            // shard region capacity
@@ -2680,8 +2736,8 @@ __global__ __launch_bounds__(kPtThreads) void pt_hist_kernel(const unsigned long
     uint32_t t0;
     const uint32_t m = pt_tile_keys(cursor, g, s, j, t0);
     const unsigned long long* src = in + s * g.sc + t0;
-    const unsigned sh = g.pbits + g.rbits;
-    const unsigned long long base = (unsigned long long)g.row0 << g.pbits;
+    const unsigned sh = g.pbits + g.sbits + g.rbits;
+    const unsigned long long base = (unsigned long long)g.row0 << (g.pbits + g.sbits);
     for (uint32_t i = threadIdx.x; i < m; i += kPtThreads) {
         const unsigned long long x = src[i];
         if (x != kNoKey) atomicAdd(&lh[(uint32_t)((x - base) >> sh)], 1u);
@@ -2748,9 +2804,9 @@ __global__ __launch_bounds__(kPtThreads) void pt_scatter_kernel(const unsigned l
     if (threadIdx.x == 0) s_n = 0;
     __syncthreads();
     const unsigned long long* src = in + s * g.sc + t0;
-    const unsigned sh = g.pbits + g.rbits;
+    const unsigned sh = g.pbits + g.sbits + g.rbits;
     const unsigned long long lowm = (1ull << sh) - 1;
-    const unsigned long long base = (unsigned long long)g.row0 << g.pbits;
+    const unsigned long long base = (unsigned long long)g.row0 << (g.pbits + g.sbits);
     unsigned long long x[kPtPer];
     uint32_t rk[kPtPer];
 #pragma unroll
@@ -2921,6 +2977,161 @@ __global__ __launch_bounds__(kPtRThreads) void pt_reduce_kernel(const uint32_t* 
         pt_reduce_block<16>(u, u.s16, last, wave_tot, keys, r, s0, n, g, stage_p, stage_q, stage_w, counts);
 }
 
+// Scored row blocks (g.sbits > 0): the keys are (p_local << pbits | q) << sbits | field, field =
+// s(x) (low kScoreBits bits) | k bit; a run is one (p, q) pair (equal key >> sbits), w = its length,
+// score = Σ s over it (an exclusive block scan of the fields: run score = the scan at the next
+// run's head minus the scan at its own), w1 = the run's marked entries (kbit: the second k of
+// kmp_pairs_multi_k's fused union).  min_shared keeps a run when its w (single k) or either k's
+// count (multi-k: w - w1, w1) reaches it.
+template <bool kKbit>
+struct PtScoredLds {
+    union {
+        typename PtSort<2>::storage_type s2;
+        typename PtSort<4>::storage_type s4;
+        typename PtSort<8>::storage_type s8;
+        typename PtSort<16>::storage_type s16;
+        struct {
+            uint32_t hs[kPtCap + 1];  // rank of each run's first key
+            uint32_t ps[kPtCap + 1];  // score scan at each run's head
+            uint32_t pk[kKbit ? kPtCap + 1 : 1];  // k-bit scan at each run's head
+        } r;
+    };
+};
+
+template <uint32_t kE, bool kKbit>
+__device__ __forceinline__ void pt_reduce_scored_block(PtScoredLds<kKbit>& u, typename PtSort<kE>::storage_type& st,
+                                                       uint32_t* last, uint32_t* wave_tot,
+                                                       const uint32_t* __restrict__ keys, uint32_t r, uint32_t s0,
+                                                       uint32_t n, const PtGeom& g, uint32_t* __restrict__ stage_p,
+                                                       uint32_t* __restrict__ stage_q, uint32_t* __restrict__ stage_w,
+                                                       uint32_t* __restrict__ stage_s, uint32_t* __restrict__ stage_w1,
+                                                       uint32_t* __restrict__ counts) {
+    uint32_t k[kE];
+#pragma unroll
+    for (uint32_t e = 0; e < kE; ++e) {
+        const uint32_t i = threadIdx.x + e * kPtRThreads;
+        k[e] = i < n ? keys[s0 + i] : 0xFFFFFFFFu;
+    }
+    const unsigned sb = g.sbits;
+    PtSort<kE>().sort(k, st, 0, g.pbits + sb + g.rbits + 1);  // blocked: thread t holds ranks t*kE + e
+    last[threadIdx.x] = k[kE - 1] >> sb;
+    __syncthreads();
+    const uint32_t rank0 = threadIdx.x * kE;
+    const uint32_t smask = (1u << kScoreBits) - 1;
+    uint32_t prev = threadIdx.x ? last[threadIdx.x - 1] : 0u, nh = 0, ssum = 0, ksum = 0;
+    bool head[kE];
+#pragma unroll
+    for (uint32_t e = 0; e < kE; ++e) {
+        const uint32_t rank = rank0 + e, pk = k[e] >> sb;
+        head[e] = rank < n && (rank == 0 || pk != prev);
+        prev = pk;
+        nh += head[e];
+        if (rank < n) {
+            ssum += k[e] & smask;
+            if (kKbit) ksum += (k[e] >> kScoreBits) & 1u;
+        }
+    }
+    uint32_t base, nruns, sx, stot, kx = 0, ktot = 0;
+    block_scan_n<kPtRThreads>(nh, base, nruns, wave_tot);  // barriers: the sort storage is dead
+    block_scan_n<kPtRThreads>(ssum, sx, stot, wave_tot);
+    if (kKbit) block_scan_n<kPtRThreads>(ksum, kx, ktot, wave_tot);
+    const uint32_t qm = (1u << g.pbits) - 1;
+    const uint32_t rowbase = g.row0 + (r << g.rbits);
+    const bool filter = g.min_shared > 1;
+#pragma unroll
+    for (uint32_t e = 0; e < kE; ++e) {
+        if (head[e]) {
+            const uint32_t pk = k[e] >> sb;
+            u.r.hs[base] = rank0 + e;
+            u.r.ps[base] = sx;
+            if (kKbit) u.r.pk[base] = kx;
+            stage_p[s0 + base] = filter ? pk : rowbase + (pk >> g.pbits);
+            if (!filter) stage_q[s0 + base] = pk & qm;
+            ++base;
+        }
+        if (rank0 + e < n) {
+            sx += k[e] & smask;
+            if (kKbit) kx += (k[e] >> kScoreBits) & 1u;
+        }
+    }
+    if (threadIdx.x == 0) {
+        u.r.hs[nruns] = n;
+        u.r.ps[nruns] = stot;
+        if (kKbit) u.r.pk[nruns] = ktot;
+        if (!filter) counts[r] = nruns;
+    }
+    __syncthreads();
+    if (!filter) {
+        for (uint32_t i = threadIdx.x; i < nruns; i += kPtRThreads) {
+            stage_w[s0 + i] = u.r.hs[i + 1] - u.r.hs[i];
+            stage_s[s0 + i] = u.r.ps[i + 1] - u.r.ps[i];
+            if (kKbit) stage_w1[s0 + i] = u.r.pk[i + 1] - u.r.pk[i];
+        }
+        return;
+    }
+    // min_shared > 1: thread t keeps runs [t*kE, t*kE + kE) in order (reads before the scan's
+    // barriers, writes after)
+    uint32_t kv[kE], wv[kE], sv[kE], w1v[kE], kept = 0;
+#pragma unroll
+    for (uint32_t e = 0; e < kE; ++e) {
+        const uint32_t rr = rank0 + e;
+        const bool in = rr < nruns;
+        wv[e] = in ? u.r.hs[rr + 1] - u.r.hs[rr] : 0u;
+        sv[e] = in ? u.r.ps[rr + 1] - u.r.ps[rr] : 0u;
+        w1v[e] = in && kKbit ? u.r.pk[rr + 1] - u.r.pk[rr] : 0u;
+        kv[e] = in ? stage_p[s0 + rr] : 0u;
+        const bool keep = in && (kKbit ? (wv[e] - w1v[e] >= g.min_shared || w1v[e] >= g.min_shared)
+                                       : wv[e] >= g.min_shared);
+        if (!keep) wv[e] = 0;
+        kept += keep;
+    }
+    uint32_t o, total;
+    block_scan_n<kPtRThreads>(kept, o, total, wave_tot);
+#pragma unroll
+    for (uint32_t e = 0; e < kE; ++e)
+        if (wv[e]) {
+            stage_p[s0 + o] = rowbase + (kv[e] >> g.pbits);
+            stage_q[s0 + o] = kv[e] & qm;
+            stage_w[s0 + o] = wv[e];
+            stage_s[s0 + o] = sv[e];
+            if (kKbit) stage_w1[s0 + o] = w1v[e];
+            ++o;
+        }
+    if (threadIdx.x == 0) counts[r] = total;
+}
+
+template <bool kKbit>
+__global__ __launch_bounds__(kPtRThreads) void pt_reduce_scored_kernel(const uint32_t* __restrict__ keys,
+                                                                       const uint32_t* __restrict__ bst, PtGeom g,
+                                                                       uint32_t* __restrict__ flags,
+                                                                       uint32_t* __restrict__ ovf,
+                                                                       uint32_t* __restrict__ stage_p,
+                                                                       uint32_t* __restrict__ stage_q,
+                                                                       uint32_t* __restrict__ stage_w,
+                                                                       uint32_t* __restrict__ stage_s,
+                                                                       uint32_t* __restrict__ stage_w1,
+                                                                       uint32_t* __restrict__ counts) {
+    __shared__ PtScoredLds<kKbit> u;
+    __shared__ uint32_t last[kPtRThreads];
+    __shared__ uint32_t wave_tot[kPtRThreads / 64];
+    const uint32_t r = blockIdx.x, s0 = bst[r], n = bst[r + 1] - s0;
+    if (n == 0 || n > kPtCap) {
+        if (threadIdx.x == 0) {
+            counts[r] = 0;
+            if (n) ovf[atomicAdd(&flags[3], 1u)] = r;
+        }
+        return;
+    }
+#define PT_SCORED(E, S) \
+    pt_reduce_scored_block<E, kKbit>(u, u.S, last, wave_tot, keys, r, s0, n, g, stage_p, stage_q, stage_w, stage_s, \
+                                     stage_w1, counts)
+    if (n <= 2 * kPtRThreads) PT_SCORED(2, s2);
+    else if (n <= 4 * kPtRThreads) PT_SCORED(4, s4);
+    else if (n <= 8 * kPtRThreads) PT_SCORED(8, s8);
+    else PT_SCORED(16, s16);
+#undef PT_SCORED
+}
+
 // Row blocks above kPtCap (listed by pt_reduce): their keys, tagged with the list index j as
 // j << kb | key (kb = pbits + rbits key bits), are sorted together by one device-wide radix
 // sort and run-length encoded; each run (one (p, q) pair of block ovf[j], length w) is staged at
@@ -2985,13 +3196,77 @@ __global__ void pt_ovf_stage_kernel(const uint32_t* __restrict__ ovf, uint32_t m
     }
 }
 
+// scored listed blocks: runs of equal pair (tagged key >> sbits), reduced to (w, w1, score)
+struct RunAgg {
+    uint32_t w, w1, s;
+};
+struct RunAggPlus {
+    __host__ __device__ RunAgg operator()(const RunAgg& a, const RunAgg& b) const {
+        return RunAgg{a.w + b.w, a.w1 + b.w1, a.s + b.s};
+    }
+};
+struct PairOfKey {  // tagged scored key -> tagged pair
+    unsigned sb;
+    __host__ __device__ unsigned long long operator()(unsigned long long x) const { return x >> sb; }
+};
+struct AggOfKey {  // tagged scored key -> one entry's (1, k bit, s)
+    __host__ __device__ RunAgg operator()(unsigned long long x) const {
+        return RunAgg{1u, (uint32_t)(x >> kScoreBits) & 1u, (uint32_t)x & ((1u << kScoreBits) - 1)};
+    }
+};
+
+__global__ void pt_ovf_keep_scored_kernel(const unsigned long long* __restrict__ uniq, const RunAgg* __restrict__ agg,
+                                          const uint32_t* __restrict__ nruns, unsigned kb, uint32_t min_shared,
+                                          int kbit, uint32_t* __restrict__ keep, uint32_t* __restrict__ first) {
+    const uint32_t U = *nruns;
+    for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u <= U; u += gridDim.x * blockDim.x) {
+        if (u == U) {
+            keep[u] = 0;
+            continue;
+        }
+        const RunAgg a = agg[u];
+        keep[u] = kbit ? (a.w - a.w1 >= min_shared || a.w1 >= min_shared) : a.w >= min_shared;
+        const uint32_t j = (uint32_t)(uniq[u] >> kb);
+        if (u == 0 || (uint32_t)(uniq[u - 1] >> kb) != j) first[j] = u;
+    }
+}
+
+__global__ void pt_ovf_stage_scored_kernel(const uint32_t* __restrict__ ovf, uint32_t m,
+                                           const uint32_t* __restrict__ bst, PtGeom g,
+                                           const unsigned long long* __restrict__ uniq,
+                                           const RunAgg* __restrict__ agg, const uint32_t* __restrict__ nruns,
+                                           const uint32_t* __restrict__ keep, const uint32_t* __restrict__ kpos,
+                                           const uint32_t* __restrict__ first, uint32_t* __restrict__ stage_p,
+                                           uint32_t* __restrict__ stage_q, uint32_t* __restrict__ stage_w,
+                                           uint32_t* __restrict__ stage_s, uint32_t* __restrict__ stage_w1,
+                                           uint32_t* __restrict__ counts) {
+    const uint32_t U = *nruns;
+    const unsigned kb = g.pbits + g.rbits;  // the tag above the (unscored) pair key
+    const uint32_t qm = (1u << g.pbits) - 1;
+    for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < U; u += gridDim.x * blockDim.x) {
+        const unsigned long long x = uniq[u];
+        const uint32_t j = (uint32_t)(x >> kb), r = ovf[j];
+        const uint32_t f = first[j];
+        const uint32_t nxt = j + 1 < m ? first[j + 1] : U;
+        if (u == f) counts[r] = kpos[nxt] - kpos[f];
+        if (!keep[u]) continue;
+        const RunAgg a = agg[u];
+        const uint32_t key = (uint32_t)x & ((1u << kb) - 1), o = bst[r] + kpos[u] - kpos[f];
+        stage_p[o] = g.row0 + (r << g.rbits) + (key >> g.pbits);
+        stage_q[o] = key & qm;
+        stage_w[o] = a.w;
+        stage_s[o] = a.s;
+        if (g.kbit) stage_w1[o] = a.w1;
+    }
+}
+
 // Listed blocks whose key space is small (rbits + pbits <= 15: the next call's geometry after a
 // first overflow — one or two rows per block, e.g. a protein sharing 5-mers with thousands of
 // later ones): a histogram over the key (row in block, q) in LDS is the run-length encoding,
 // already in canonical order.  One workgroup per listed block (grid-stride over the device
 // count); no sort, no host round trip.
 constexpr uint32_t kRowHistBits = 15, kRowHistBins = 1u << kRowHistBits, kRowHistThreads = 1024, kRowHistGrid = 64;
-__host__ __device__ inline bool pt_rowhist_ok(const PtGeom& g) { return g.rbits + g.pbits <= kRowHistBits; }
+__host__ __device__ inline bool pt_rowhist_ok(const PtGeom& g) { return !g.sbits && g.rbits + g.pbits <= kRowHistBits; }
 
 __global__ __launch_bounds__(kRowHistThreads) void pt_rowhist_kernel(const uint32_t* __restrict__ keys,
                                                                      const uint32_t* __restrict__ bst, PtGeom g,
@@ -3088,6 +3363,15 @@ struct PtPack {
     unsigned long long* rb;
 };
 
+// scored calls: the staged scores / second-k weights and where they go (d_w1 nullptr: single k)
+struct PtScoreOut {
+    const uint32_t* stage_s;
+    const uint32_t* stage_w1;
+    uint32_t* d_s;
+    uint32_t* d_w1;
+    uint32_t* d_w0;  // multi-k: w of the first k (w - w1)
+};
+
 __global__ __launch_bounds__(256) void pt_emit_kernel(const uint32_t* __restrict__ stage_p,
                                                       const uint32_t* __restrict__ stage_q,
                                                       const uint32_t* __restrict__ stage_w,
@@ -3096,7 +3380,8 @@ __global__ __launch_bounds__(256) void pt_emit_kernel(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ eoff, uint32_t* __restrict__ d_p,
                                                       uint32_t* __restrict__ d_q, uint32_t* __restrict__ d_w,
                                                       uint64_t cap, uint32_t stride = 1, PtPack pack = {},
-                                                      uint32_t* __restrict__ total_out = nullptr) {
+                                                      uint32_t* __restrict__ total_out = nullptr,
+                                                      PtScoreOut so = {}) {
     const uint32_t r = blockIdx.x, s0 = bst[r], m = counts[r];
     uint64_t o;
     if (eoff) {
@@ -3120,6 +3405,12 @@ __global__ __launch_bounds__(256) void pt_emit_kernel(const uint32_t* __restrict
         d_p[(o + i) * stride] = stage_p[s0 + i];
         d_q[(o + i) * stride] = stage_q[s0 + i];
         d_w[(o + i) * stride] = stage_w[s0 + i];
+        if (so.d_s) so.d_s[(o + i) * stride] = so.stage_s[s0 + i];
+        if (so.d_w1) {
+            const uint32_t w1 = so.stage_w1[s0 + i];
+            so.d_w1[(o + i) * stride] = w1;
+            so.d_w0[(o + i) * stride] = stage_w[s0 + i] - w1;
+        }
     }
 }
 
@@ -3184,12 +3475,24 @@ struct StepCfg {
     uint64_t cap;
     uint32_t stride;          // edge arrays' element stride (3: interleaved triples)
     const std::vector<unsigned long long>* front_key;  // the batch: pointers and shape
+    // scored calls (sb > 0): pair keys carry the k-mer self-score (and sor: the k bit), the tail
+    // sums it into d_s (and counts the k bit into d_w1: the second k's w of a fused union)
+    int k;
+    unsigned sb;
+    uint32_t sor;
+    uint32_t *d_s, *d_w1, *d_w0;
+    // expand only (kmp_dev_pairs_rows_multi): front, buckets and heavy path into this workspace's
+    // shard regions, no tail; *n_inc_out = the pair keys written (the fused multi-k tail reads them)
+    bool expand_only;
+    uint64_t* n_inc_out;
 };
 
 // row-block tail geometry: rows per block so that an average block holds about a quarter of
 // kPtCap keys (from the expected incidence count)
 bool pt_geometry(const kmp_postings* ws, const StepCfg& c, uint64_t inc, PtGeom* g) {
     g->pbits = bits_for(c.n);
+    g->sbits = c.sb;
+    g->kbit = c.d_w1 != nullptr;
     const uint32_t rows = c.ranged ? c.row_hi - c.row_lo : c.n;
     const uint64_t est = std::max<uint64_t>(1, inc);
     // rows per block ~ (kPtCap / 2.4) * rows / est, to the nearest power of two: an average block
@@ -3202,7 +3505,7 @@ bool pt_geometry(const kmp_postings* ws, const StepCfg& c, uint64_t inc, PtGeom*
     while (rb < 16 && (double)(1u << rb) * 1.41421356 < want) ++rb;
     rb = std::min(rb, ws->pt_rb_max);  // learned from overflowing blocks
     while (rb < 31 && ((rows + (1ull << rb) - 1) >> rb) > kPtMaxBlocks) ++rb;
-    if (g->pbits + rb > 31) return false;  // the key and one padding bit in a u32
+    if (g->pbits + g->sbits + rb > 31) return false;  // the key and one padding bit in a u32
     g->rbits = rb;
     g->nrb = std::max(1u, (uint32_t)((rows + (1ull << rb) - 1) >> rb));
     g->sc = ws->shard_cap;
@@ -3270,6 +3573,9 @@ BucketArgs bucket_args(kmp_postings* ws, const StepCfg& c, bool spill) {
     a.spill_cursor = ws->bstats.p + kRbSpill;
     a.seg = ws->hseg.p;
     a.seg_cap = seg_capacity(ws);
+    a.k = c.k;
+    a.sb = c.sb;
+    a.sor = c.sor;
     return a;
 }
 
@@ -3286,6 +3592,7 @@ int step_reserve(kmp_postings* ws, const StepCfg& c, const PtGeom& g) {
     PG(ws->inc.reserve(total));  // u32 row-block keys (pt_scatter) ...
     PG(ws->uniq.reserve(total));  // ... staged p | q (u32 each)
     PG(ws->w.reserve(total));     // ... staged w
+    if (c.sb) PG(ws->stg2.reserve(2 * total));  // ... staged scores | second-k weights
     PG(ws->spill.reserve(ws->spill_cap * kShards));
     PG(ws->hseg.reserve(seg_capacity(ws)));
     PG(ws->ovf.reserve((uint64_t)g.nrb + 1));
@@ -3316,10 +3623,21 @@ int enqueue_front(kmp_postings* ws, MakeKeys& make_keys, const StepCfg& c, bool 
     uint32_t c0, c1;
     own_bins(ws, dg, &c0, &c1);
     const uint32_t b0 = c0 * dg.nb2, nbk = (c1 - c0) * dg.nb2;  // the call's buckets
-    if (c.ranged) launch_buckets<true>(a, b0, nbk, st);
-    else launch_buckets<false>(a, b0, nbk, st);
+    if (c.sb) {
+        if (c.ranged) launch_buckets<true, true>(a, b0, nbk, st);
+        else launch_buckets<false, true>(a, b0, nbk, st);
+    } else {
+        if (c.ranged) launch_buckets<true, false>(a, b0, nbk, st);
+        else launch_buckets<false, false>(a, b0, nbk, st);
+    }
     PG(hipGetLastError());
     return KMP_OK;
+}
+
+// the scored call's staging (ws->stg2: scores | second-k weights, total each) and outputs
+PtScoreOut pt_score_out(kmp_postings* ws, const StepCfg& c, uint64_t total) {
+    if (!c.sb) return PtScoreOut{};
+    return PtScoreOut{ws->stg2.p, ws->stg2.p + total, c.d_s, c.d_w1, c.d_w0};
 }
 
 // tail over the shard regions, then the read-back; marks 4, 5, 6
@@ -3336,8 +3654,17 @@ int enqueue_tail_in(kmp_postings* ws, const StepCfg& c, const PtGeom& g, const u
     pt_tscan_kernel<<<1, kPtScanThreads, 0, st>>>(b.T, g.nrb, b.bst, b.cur, ws->small.p + 2);
     ws->mark(4, st);
     pt_scatter_kernel<<<dim3(g.jt, g.nshards), kPtThreads, 0, st>>>(in, cursor, g, b.cur, keys32);
-    pt_reduce_kernel<<<g.nrb, kPtRThreads, 0, st>>>(keys32, b.bst, g, ws->flags.p, ws->ovf.p, stage_p, stage_q,
-                                                    ws->w.p, b.counts);
+    const PtScoreOut so = pt_score_out(ws, c, total);
+    if (g.sbits && g.kbit)
+        pt_reduce_scored_kernel<true><<<g.nrb, kPtRThreads, 0, st>>>(keys32, b.bst, g, ws->flags.p, ws->ovf.p, stage_p,
+                                                                     stage_q, ws->w.p, ws->stg2.p, ws->stg2.p + total,
+                                                                     b.counts);
+    else if (g.sbits)
+        pt_reduce_scored_kernel<false><<<g.nrb, kPtRThreads, 0, st>>>(keys32, b.bst, g, ws->flags.p, ws->ovf.p, stage_p,
+                                                                      stage_q, ws->w.p, ws->stg2.p, nullptr, b.counts);
+    else
+        pt_reduce_kernel<<<g.nrb, kPtRThreads, 0, st>>>(keys32, b.bst, g, ws->flags.p, ws->ovf.p, stage_p, stage_q,
+                                                        ws->w.p, b.counts);
     if (pt_rowhist_ok(g))  // one-row blocks above kPtCap: finished here (none listed: every workgroup exits)
         pt_rowhist_kernel<<<kRowHistGrid, kRowHistThreads, 0, st>>>(keys32, b.bst, g, ws->flags.p, ws->ovf.p,
                                                                     stage_p, stage_q, ws->w.p, b.counts);
@@ -3345,7 +3672,7 @@ int enqueue_tail_in(kmp_postings* ws, const StepCfg& c, const PtGeom& g, const u
     // edge offsets computed by the emit blocks themselves (no pt_offsets launch); + read-back
     pt_emit_kernel<<<g.nrb, 256, 0, st>>>(stage_p, stage_q, ws->w.p, b.bst, b.counts, nullptr, c.d_p, c.d_q, c.d_w,
                                           c.cap, c.stride, PtPack{ws->bstats.p, ws->flags.p, ws->small.p + 1, ws->hrb},
-                                          ws->small.p + 1);
+                                          ws->small.p + 1, so);
     ws->mark(6, st);
     PG(hipGetLastError());
     return KMP_OK;
@@ -3367,7 +3694,7 @@ int pt_finish_overflow(kmp_postings* ws, const StepCfg& c, const PtGeom& g, uint
     uint32_t* keys32 = reinterpret_cast<uint32_t*>(ws->inc.p);
     uint32_t* stage_p = reinterpret_cast<uint32_t*>(ws->uniq.p);
     uint32_t* stage_q = stage_p + total;
-    const unsigned kb = g.pbits + g.rbits, mb = bits_for((uint64_t)m + 1);
+    const unsigned kb = g.pbits + g.sbits + g.rbits, mb = bits_for((uint64_t)m + 1);
     if (kb + mb > 63) return KMP_EINVAL;
     PG(ws->ovx.reserve(m + 1));
     unsigned long long* xoff = ws->ovx.p;
@@ -3394,8 +3721,35 @@ int pt_finish_overflow(kmp_postings* ws, const StepCfg& c, const PtGeom& g, uint
     PG(rocprim::exclusive_scan(nullptr, t3, keep, kpos, 0u, (size_t)nx + 1, rocprim::plus<uint32_t>(), st));
     PG(ws->tmp.reserve(std::max({t1, t2, t3, ws->tmp.n})));
     PG(rocprim::radix_sort_keys<SortCfg>(ws->tmp.p, t1, x, xs, (size_t)nx, 0u, kb + mb, st));
-    PG(rocprim::run_length_encode(ws->tmp.p, t2, xs, (unsigned)nx, uq, rw, nruns, st));
     const uint32_t gr = (uint32_t)std::min<unsigned long long>((nx + 256) / 256, 4096);
+    if (g.sbits) {
+        // scored: runs of equal (tag, pair) = sorted key >> sbits, reduced to (w, w1, score)
+        PG(ws->ova.reserve(3 * (nx + 1)));
+        RunAgg* agg = reinterpret_cast<RunAgg*>(ws->ova.p);
+        auto kin = rocprim::make_transform_iterator(xs, PairOfKey{g.sbits});
+        auto vin = rocprim::make_transform_iterator(xs, AggOfKey{});
+        size_t t4 = 0;
+        PG(rocprim::reduce_by_key(nullptr, t4, kin, vin, (size_t)nx, uq, agg, nruns, RunAggPlus{},
+                                  rocprim::equal_to<unsigned long long>(), st));
+        PG(ws->tmp.reserve(std::max({t4, t3, ws->tmp.n})));
+        PG(rocprim::reduce_by_key(ws->tmp.p, t4, kin, vin, (size_t)nx, uq, agg, nruns, RunAggPlus{},
+                                  rocprim::equal_to<unsigned long long>(), st));
+        pt_ovf_keep_scored_kernel<<<gr, 256, 0, st>>>(uq, agg, nruns, kb - g.sbits, g.min_shared, g.kbit, keep, first);
+        PG(rocprim::exclusive_scan(ws->tmp.p, t3, keep, kpos, 0u, (size_t)nx + 1, rocprim::plus<uint32_t>(), st));
+        const PtScoreOut so = pt_score_out(ws, c, total);
+        pt_ovf_stage_scored_kernel<<<gr, 256, 0, st>>>(ws->ovf.p, m, b.bst, g, uq, agg, nruns, keep, kpos, first,
+                                                       stage_p, stage_q, ws->w.p, ws->stg2.p, ws->stg2.p + total,
+                                                       b.counts);
+        pt_offsets_kernel<<<1, kPtScanThreads, 0, st>>>(b.counts, g.nrb, b.eoff, ws->small.p + 1);
+        pt_emit_kernel<<<g.nrb, 256, 0, st>>>(stage_p, stage_q, ws->w.p, b.bst, b.counts, b.eoff, c.d_p, c.d_q, c.d_w,
+                                              c.cap, c.stride, PtPack{}, nullptr, so);
+        uint32_t ne = 0;
+        PG(hipMemcpyAsync(&ne, ws->small.p + 1, 4, hipMemcpyDeviceToHost, st));
+        PG(hipStreamSynchronize(st));
+        *edges = ne;
+        return KMP_OK;
+    }
+    PG(rocprim::run_length_encode(ws->tmp.p, t2, xs, (unsigned)nx, uq, rw, nruns, st));
     pt_ovf_keep_kernel<<<gr, 256, 0, st>>>(uq, rw, nruns, kb, g.min_shared, keep, first);
     PG(rocprim::exclusive_scan(ws->tmp.p, t3, keep, kpos, 0u, (size_t)nx + 1, rocprim::plus<uint32_t>(), st));
     pt_ovf_stage_kernel<<<gr, 256, 0, st>>>(ws->ovf.p, m, b.bst, g, uq, rw, nruns, kpos, first, stage_p, stage_q,
@@ -3484,6 +3838,7 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
         PG(ws->hoff.reserve(3 * (nt + 1) + 4));
         PG(ws->hE.reserve(m + 1));
         PG(ws->hGS.reserve(m + 1));
+        PG(ws->hGH.reserve(m + 1));
         if (ho.cls) {
             PG(ws->hrun.reserve(m + 1));
             PG(ws->hRH.reserve(m + 1));
@@ -3529,7 +3884,7 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
         heavy_compact_kernel<<<(uint32_t)nt, kHvThreads, 0, st>>>(
             ws->hsorted.p, m, ho, reinterpret_cast<const uint64_t*>(off),
             reinterpret_cast<const uint64_t*>(off + nt + 1), reinterpret_cast<const uint64_t*>(off + 2 * (nt + 1)),
-            ws->hE.p, GS, ho.cls ? ws->hrun.p : nullptr, RH);
+            ws->hE.p, GS, ho.cls ? ws->hrun.p : nullptr, RH, ws->hGH.p);
         if (!one_wg) heavy_sentinel_kernel<<<1, 64, 0, st>>>(tot, GS, RH);
         PG(hipGetLastError());
         ws->heavy_ready = true;
@@ -3565,7 +3920,7 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
     heavy_expand_kernel<<<grid, kHvI, 0, st>>>(ws->hE.p, GS, ws->hgi.p, BT, BP, RUN, RH, ws->htoff.p, ws->h_tot + 1,
                                                ho, 1u << bits_for(c.n), c.require_diff, c.ranged ? 1 : 0, row_lo,
                                                row_hi, ws->inc_sorted.p, ws->shard_cap, ws->bstats.p + kRbCursor,
-                                               ws->bstats.p);
+                                               ws->bstats.p, ws->hGH.p, c.k, c.sb, c.sor);
     PG(hipGetLastError());
     return KMP_OK;
 }
@@ -3578,7 +3933,7 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
 template <class Enqueue>
 int slot_launch(kmp_postings* ws, kmp_postings::GraphSlot& slot, std::vector<unsigned long long> key,
                 Enqueue enqueue, hipStream_t st) {
-    key.push_back(g_grow_gen);
+    key.push_back(g_grow_gen.load());
     if (!ws->graph_on) return enqueue(st);
     if (slot.gexec && slot.key == key) {
         PG(hipGraphLaunch(slot.gexec, st));
@@ -3598,11 +3953,11 @@ int slot_launch(kmp_postings* ws, kmp_postings::GraphSlot& slot, std::vector<uns
         (void)hipGetLastError();
         return enqueue(st);
     }
-    const unsigned long long gen = g_grow_gen;
+    const unsigned long long gen = g_grow_gen.load();
     int rc = enqueue(ws->cst);
     hipError_t e = hipStreamEndCapture(ws->cst, &gr);
     hipGraphExec_t ex = nullptr;
-    if (rc == KMP_OK && e == hipSuccess && gr && gen == g_grow_gen) e = hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0);
+    if (rc == KMP_OK && e == hipSuccess && gr && gen == g_grow_gen.load()) e = hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0);
     else if (e == hipSuccess) e = hipErrorUnknown;
     if (gr) (void)hipGraphDestroy(gr);
     if (e != hipSuccess || !ex) {  // not capturable this time: plain
@@ -3641,7 +3996,7 @@ int fused_launch(kmp_postings* ws, MakeKeys& make_keys, const std::vector<unsign
         ws->gexec = nullptr;
         ws->gkey.clear();
     }
-    const unsigned long long gen = g_grow_gen;
+    const unsigned long long gen = g_grow_gen.load();
     hipGraph_t gr = nullptr;
     // captured on a private stream (the caller's may be the legacy null stream, which cannot be
     // captured), launched on the caller's
@@ -3654,7 +4009,7 @@ int fused_launch(kmp_postings* ws, MakeKeys& make_keys, const std::vector<unsign
     int rc = enqueue(ws->cst);
     hipError_t e = hipStreamEndCapture(ws->cst, &gr);
     hipGraphExec_t ex = nullptr;
-    if (rc == KMP_OK && e == hipSuccess && gr && gen == g_grow_gen)
+    if (rc == KMP_OK && e == hipSuccess && gr && gen == g_grow_gen.load())
         e = hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0);
     else if (e == hipSuccess)
         e = hipErrorUnknown;
@@ -3717,14 +4072,14 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
         }
         const unsigned long long* rb = ws->hrb;
         unsigned long long acc[kStN], most, n_inc, spill_most, spill_total;
-        const bool split = ws->heavy || reuse;
+        const bool split = ws->heavy || reuse || c.expand_only;
         if (!reuse) ws->heavy_ready = false;  // a recomputed front: no compacted spill yet
         if (!split) {
             key.push_back(ws->shard_cap);
             key.push_back(ws->spill_cap);
             key.push_back(ws->timing);
             key.push_back(g.rbits + 1);
-            key.push_back(g_grow_gen);
+            key.push_back(g_grow_gen.load());
             key.push_back(ws->cur_on);
             int rc = fused_launch(ws, make_keys, key, c, g, st);
             key.resize(key.size() - 6);
@@ -3789,6 +4144,20 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
                 continue;
             }
             ws->pt_inc = n_inc;
+            if (c.expand_only) {  // the shard regions stay for the fused tail (shard_cap unchanged)
+                ws->last_most = most;
+                fill_stats(stats, acc);
+                if (stats) stats->incidences = n_inc;
+                ws->last_heavy = ws->heavy_ready;
+                ws->last_fused = false;
+                if (c.front_key) {
+                    ws->front_ok = true;
+                    ws->front_key = *c.front_key;
+                }
+                *c.n_inc_out = n_inc;
+                *n_edges = 0;
+                return KMP_OK;
+            }
             if (!pt_geometry(ws, c, n_inc, &g)) return KMP_EINVAL;
             int rc = step_reserve(ws, c, g);
             if (rc != KMP_OK) return rc;
@@ -3831,6 +4200,77 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
         return ne > c.cap ? KMP_EOVERFLOW : KMP_OK;
     }
     return KMP_EDEVICE;
+}
+
+// The fused multi-k tail (kmp_dev_pairs_rows_multi): the pair keys that every workspace's
+// expand-only call left in its shard regions (k bit and self-score in the field below the pair)
+// reduced together by the row-block tail of ws[0]: one run per pair over both k, w = its length,
+// w1 = its k-bit entries, score = Σ s — the union of the per-k lists without building or merging
+// them.  Host-synchronous; *n_edges = the kept pairs.
+int tail_multi(kmp_postings* const* ws, uint32_t nk, const StepCfg& c, const uint64_t* inc, uint64_t* n_edges,
+               kmp_postings_stats* stats, hipStream_t st) {
+    kmp_postings* w0 = ws[0];
+    uint64_t T = 0;
+    for (uint32_t j = 0; j < nk; ++j) T += inc[j];
+    PtGeom g;
+    if (!pt_geometry(w0, c, std::max<uint64_t>(T, 1), &g)) return KMP_EINVAL;
+    const uint64_t total = std::max<uint64_t>(T + 1, w0->shard_cap * kShards);  // staging capacity
+    PG(w0->inc.reserve(total));
+    PG(w0->uniq.reserve(total));
+    PG(w0->w.reserve(total));
+    PG(w0->stg2.reserve(2 * total));
+    PG(w0->ovf.reserve((uint64_t)g.nrb + 1));
+    PG(w0->small.reserve(16));
+    hipError_t e = hipSuccess;
+    const PtBufs b = pt_bufs(w0, g, true, &e);
+    PG(e);
+    PG(hipMemsetAsync(w0->flags.p + kFlOvf, 0, sizeof(uint32_t), st));
+    uint32_t* keys32 = reinterpret_cast<uint32_t*>(w0->inc.p);
+    uint32_t* stage_p = reinterpret_cast<uint32_t*>(w0->uniq.p);
+    uint32_t* stage_q = stage_p + total;
+    auto geo = [&](uint32_t j) {  // input j: its shard regions
+        PtGeom gj = g;
+        gj.sc = ws[j]->shard_cap;
+        gj.jt = (uint32_t)((gj.sc + kPtTile - 1) / kPtTile);
+        return gj;
+    };
+    for (uint32_t j = 0; j < nk; ++j)
+        pt_hist_kernel<<<dim3(geo(j).jt, kShards), kPtThreads, 0, st>>>(ws[j]->inc_sorted.p, ws[j]->bstats.p + kRbCursor,
+                                                                       geo(j), b.T);
+    pt_tscan_kernel<<<1, kPtScanThreads, 0, st>>>(b.T, g.nrb, b.bst, b.cur, w0->small.p + 2);
+    for (uint32_t j = 0; j < nk; ++j)
+        pt_scatter_kernel<<<dim3(geo(j).jt, kShards), kPtThreads, 0, st>>>(ws[j]->inc_sorted.p,
+                                                                          ws[j]->bstats.p + kRbCursor, geo(j), b.cur,
+                                                                          keys32);
+    if (g.kbit)
+        pt_reduce_scored_kernel<true><<<g.nrb, kPtRThreads, 0, st>>>(keys32, b.bst, g, w0->flags.p, w0->ovf.p, stage_p,
+                                                                     stage_q, w0->w.p, w0->stg2.p, w0->stg2.p + total,
+                                                                     b.counts);
+    else
+        pt_reduce_scored_kernel<false><<<g.nrb, kPtRThreads, 0, st>>>(keys32, b.bst, g, w0->flags.p, w0->ovf.p, stage_p,
+                                                                      stage_q, w0->w.p, w0->stg2.p, nullptr, b.counts);
+    pt_emit_kernel<<<g.nrb, 256, 0, st>>>(stage_p, stage_q, w0->w.p, b.bst, b.counts, nullptr, c.d_p, c.d_q, c.d_w,
+                                          c.cap, c.stride, PtPack{}, w0->small.p + 1, pt_score_out(w0, c, total));
+    PG(hipGetLastError());
+    uint32_t h[2] = {0, 0};
+    PG(hipMemcpyAsync(&h[0], w0->small.p + 1, 4, hipMemcpyDeviceToHost, st));
+    PG(hipMemcpyAsync(&h[1], w0->flags.p + kFlOvf, 4, hipMemcpyDeviceToHost, st));
+    PG(hipStreamSynchronize(st));
+    uint64_t ne = h[0];
+    w0->last_ovf = h[1];
+    if (h[1]) {
+        int rc = pt_finish_overflow(w0, c, g, h[1], &ne, st, total);
+        if (rc != KMP_OK) return rc;
+    }
+    for (uint32_t j = 0; j < nk; ++j)  // the next call's regions, learned now that the tail has read them
+        ws[j]->shard_cap = ws[j]->last_most + ws[j]->last_most / 64 + 256;
+    w0->pt_inc = T;
+    if (stats) {
+        stats->incidences = T;
+        stats->pairs = ne;
+    }
+    *n_edges = ne;
+    return ne > c.cap ? KMP_EOVERFLOW : KMP_OK;
 }
 
 // Shared tail: sort the pair keys, run-length encode -> (pair, w) in canonical order, keep
@@ -3926,7 +4366,9 @@ template <class MakeKeys>
 int run_postings(kmp_postings* ws, MakeKeys make_keys, const std::vector<unsigned long long>& key_extra, uint32_t n,
                  int k, uint64_t slots, const uint16_t* d_class, uint32_t heavy_df, uint32_t min_shared,
                  int require_class_diff, bool ranged, uint32_t row_lo, uint32_t row_hi, uint32_t* d_p, uint32_t* d_q,
-                 uint32_t* d_w, uint64_t cap, uint64_t* n_edges, kmp_postings_stats* stats, hipStream_t st) {
+                 uint32_t* d_w, uint64_t cap, uint64_t* n_edges, kmp_postings_stats* stats, hipStream_t st,
+                 unsigned sb = 0, uint32_t sor = 0, uint32_t* d_s = nullptr, uint32_t* d_w1 = nullptr,
+                 uint64_t* n_inc_out = nullptr) {
     if (heavy_df < 2) heavy_df = 2;
     if (min_shared < 1) min_shared = 1;
     ws->bin_lo = ws->bin_hi = 0;  // every bucket (the k-mer split restricts its own calls)
@@ -3955,12 +4397,20 @@ int run_postings(kmp_postings* ws, MakeKeys make_keys, const std::vector<unsigne
         c.cap = cap;
         c.stride = 1;
         c.front_key = &front_key;
+        c.k = k;
+        c.sb = sb;
+        c.sor = sor;
+        c.d_s = d_s;
+        c.d_w1 = d_w1;
+        c.expand_only = n_inc_out != nullptr;
+        c.n_inc_out = n_inc_out;
         // graph key: the call's shape and pointers (run_step adds the capacities, the timing
         // switch, the row-block geometry and the buffer generation)
         std::vector<unsigned long long> key = {n, (unsigned long long)k, slots, heavy_df, min_shared,
                                                (unsigned long long)require_class_diff, ranged, row_lo, row_hi, cap,
                                                (unsigned long long)(uintptr_t)d_p, (unsigned long long)(uintptr_t)d_q,
-                                               (unsigned long long)(uintptr_t)d_w};
+                                               (unsigned long long)(uintptr_t)d_w, sb, sor,
+                                               (unsigned long long)(uintptr_t)d_s, (unsigned long long)(uintptr_t)d_w1};
         key.insert(key.end(), key_extra.begin(), key_extra.end());
         bool fallback = false;
         int rc = run_step(ws, make_keys, key, c, n_edges, &fallback, stats, st);
@@ -3972,7 +4422,7 @@ int run_postings(kmp_postings* ws, MakeKeys make_keys, const std::vector<unsigne
     }
     // flat layout: class ids wider than the bucketed key's class field (or the layout forced)
     ws->front_ok = false;
-    if (ranged) return KMP_ESTATE;  // no row filter on the flat layout
+    if (ranged || sb || n_inc_out) return KMP_ESTATE;  // no row filter, scores or fused tail on the flat layout
     lay = make_layout(n, k, slots, false);
     if (lay.sort_hi > 64) return KMP_EINVAL;
     ws->parted = false;
@@ -4191,7 +4641,8 @@ static int residues_impl(kmp_postings* ws, const uint8_t* d_res, const uint64_t*
                          uint32_t n, int k, uint64_t slots, uint32_t heavy_df, uint32_t min_shared,
                          int require_class_diff, bool ranged, uint32_t row_lo, uint32_t row_hi, uint32_t* d_p,
                          uint32_t* d_q, uint32_t* d_w, uint64_t cap, uint64_t* n_edges, kmp_postings_stats* stats,
-                         void* stream) {
+                         void* stream, unsigned sb = 0, uint32_t sor = 0, uint32_t* d_s = nullptr,
+                         uint32_t* d_w1 = nullptr, uint64_t* n_inc_out = nullptr) {
     int rc = postings_args(ws, k, n_edges, stats, d_p, d_q, d_w, cap);
     if (rc != KMP_OK || n < 2) return rc;
     if (!d_res || !d_res_off || !d_class) return KMP_EINVAL;
@@ -4207,7 +4658,7 @@ static int residues_impl(kmp_postings* ws, const uint8_t* d_res, const uint64_t*
     };
     const std::vector<unsigned long long> key_extra = {1, (uintptr_t)d_res, (uintptr_t)d_res_off, (uintptr_t)d_class};
     return run_postings(ws, keys, key_extra, n, k, slots, d_class, heavy_df, min_shared, require_class_diff, ranged,
-                        row_lo, row_hi, d_p, d_q, d_w, cap, n_edges, stats, st);
+                        row_lo, row_hi, d_p, d_q, d_w, cap, n_edges, stats, st, sb, sor, d_s, d_w1, n_inc_out);
 }
 
 int kmp_dev_pairs_residues(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off,
@@ -4229,6 +4680,85 @@ int kmp_dev_pairs_rows(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d
     }
     return residues_impl(ws, d_res, d_res_off, d_class, n, k, slots, heavy_df, min_shared, require_class_diff, true,
                          row_lo, row_hi, d_p, d_q, d_w, cap, n_edges, stats, stream);
+}
+
+uint32_t kmp_dev_rows_max(uint32_t n, int scored) {
+    // the row-block tail's u32 key (p_local << pbits | q, scored << kScoreBits more, multi-k one k
+    // bit more, one padding bit) and its kPtMaxBlocks row blocks bound the rows of one call
+    const unsigned used = bits_for(n) + (scored ? kScoreBits : 0u) + (scored > 1 ? 1u : 0u);
+    if (used >= 31) return 0;
+    const uint64_t m = (uint64_t)kPtMaxBlocks << (31 - used);
+    return (uint32_t)std::min<uint64_t>(m, n);
+}
+
+int kmp_dev_pairs_rows_scored(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
+                              uint32_t n, int k, uint64_t slots, uint32_t heavy_df, uint32_t min_shared,
+                              int require_class_diff, uint32_t row_lo, uint32_t row_hi, uint32_t* d_p, uint32_t* d_q,
+                              uint32_t* d_w, uint32_t* d_score, uint64_t cap, uint64_t* n_edges,
+                              kmp_postings_stats* stats, void* stream) {
+    if (row_lo > row_hi || row_hi > n) return KMP_EINVAL;
+    if (cap && !d_score) return KMP_EINVAL;
+    if (row_hi - row_lo > kmp_dev_rows_max(n, 1)) return KMP_EINVAL;
+    if (row_lo == row_hi) return postings_args(ws, k, n_edges, stats, d_p, d_q, d_w, cap);
+    const bool ranged = !(row_lo == 0 && row_hi == n);
+    return residues_impl(ws, d_res, d_res_off, d_class, n, k, slots, heavy_df, min_shared, require_class_diff, ranged,
+                         row_lo, row_hi, d_p, d_q, d_w, cap, n_edges, stats, stream, kScoreBits, 0u, d_score, nullptr);
+}
+
+int kmp_dev_pairs_rows_multi(kmp_postings* const* ws, const int* ks, uint32_t nk, const uint8_t* d_res,
+                             const uint64_t* d_res_off, const uint16_t* d_class, uint32_t n, uint64_t slots,
+                             uint32_t min_shared, int require_class_diff, uint32_t row_lo, uint32_t row_hi,
+                             uint32_t* d_p, uint32_t* d_q, uint32_t* d_w, uint32_t* d_score, uint32_t* d_w0,
+                             uint32_t* d_w1, uint64_t cap, uint64_t* n_edges, kmp_postings_stats* stats,
+                             void* stream) {
+    if (!ws || !ks || nk != 2 || !n_edges || row_lo > row_hi || row_hi > n) return KMP_EINVAL;
+    if (!ws[0] || !ws[1] || ws[0] == ws[1] || ks[0] == ks[1]) return KMP_EINVAL;
+    for (uint32_t j = 0; j < nk; ++j)
+        if (ks[j] < 1 || ks[j] > kMaxK) return KMP_EINVAL;
+    if (cap && (!d_p || !d_q || !d_w || !d_score || !d_w0 || !d_w1)) return KMP_EINVAL;
+    if (row_hi - row_lo > kmp_dev_rows_max(n, 2)) return KMP_EINVAL;
+    *n_edges = 0;
+    if (stats) *stats = kmp_postings_stats{};
+    if (row_lo == row_hi || n < 2) return KMP_OK;
+    if (!d_res || !d_res_off || !d_class) return KMP_EINVAL;
+    hipStream_t st = as_stream(stream);
+    const bool ranged = !(row_lo == 0 && row_hi == n);
+    uint64_t inc[2] = {0, 0};
+    kmp_postings_stats s0{};
+    for (uint32_t j = 0; j < nk; ++j) {
+        // expand only: every incidence keyed (pair << 8) | j << 7 | s(x)
+        uint64_t unused = 0;
+        int rc = residues_impl(ws[j], d_res, d_res_off, d_class, n, ks[j], slots, 0xFFFFFFFFu, 1, require_class_diff,
+                               ranged, row_lo, row_hi, d_p, d_q, d_w, cap, &unused, j == 0 ? &s0 : nullptr, stream,
+                               kScoreBits + 1, j << kScoreBits, d_score, d_w1, &inc[j]);
+        if (rc != KMP_OK) return rc;
+    }
+    // the tail's geometry and outputs (the same StepCfg fields the step uses)
+    StepCfg c{};
+    c.n = n;
+    c.min_shared = std::max(1u, min_shared);
+    c.ranged = ranged;
+    c.row_lo = row_lo;
+    c.row_hi = row_hi;
+    c.d_p = d_p;
+    c.d_q = d_q;
+    c.d_w = d_w;
+    c.cap = cap;
+    c.stride = 1;
+    c.sb = kScoreBits + 1;
+    c.d_s = d_score;
+    c.d_w1 = d_w1;
+    c.d_w0 = d_w0;
+    int rc = tail_multi(ws, nk, c, inc, n_edges, stats, st);
+    if (stats) {  // the first k's front statistics
+        stats->sum_S = s0.sum_S;
+        stats->distinct = s0.distinct;
+        stats->repeat = s0.repeat;
+        stats->sum_cdf2_light = s0.sum_cdf2_light;
+        stats->max_df = s0.max_df;
+        stats->heavy_entries = s0.heavy_entries;
+    }
+    return rc;
 }
 
 int kmp_dev_split_expand(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,

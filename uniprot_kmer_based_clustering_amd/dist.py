@@ -102,12 +102,24 @@ class SplitState:
     reduced over the ranks): the per-destination send capacity, the flags to learn from on a
     rerun, the exchange buffers, and whether the batch needs the row split."""
 
-    def __init__(self):
+    def __init__(self, key=None):
+        self.key = key  # (n, total residues, k, residue buffer) of the batch it was learned on
         self.cap = 0
         self.learn = None
         self.bufs = None
         self.row_split = False
         self.reruns = 0
+
+
+def _pipe_state(pipe) -> SplitState:
+    """The pipe's cached SplitState, reset when its batch or k changed (a k that spills frequent
+    k-mers must not pin the row split, or its capacities, on another k of the same batch)."""
+    key = (pipe.n, pipe.total, pipe.k, pipe.res.data_ptr() if hasattr(pipe, "res") else 0)
+    st = pipe.__dict__.get("_split_state")
+    if st is None or st.key != key:
+        st = SplitState(key)
+        pipe.__dict__["_split_state"] = st
+    return st
 
 
 def kmer_split_step(pipe, rank: int, world: int, group=None, min_shared: int = 1, require_class_diff: bool = True,
@@ -119,7 +131,7 @@ def kmer_split_step(pipe, rank: int, world: int, group=None, min_shared: int = 1
     back to the row split (distributed_step) when the batch spills frequent k-mers.  timings: a
     list to append this rank's (expand, exchange, edges) milliseconds to (CUDA events on the
     current stream, which the library's stages and the collectives are ordered with)."""
-    st = state if state is not None else pipe.__dict__.setdefault("_split_state", SplitState())
+    st = state if state is not None else _pipe_state(pipe)
     if st.row_split:
         return distributed_step(pipe, rank, world, group, min_shared, require_class_diff)
     lo, hi = row_ranges(pipe.n, world)[rank]

@@ -125,6 +125,10 @@ class KmerPairEngine:
         """Bounded-memory passes: pair keys per pass (0: auto, from the free device memory)."""
         self._check(lib().kmp_ctx_set_pass_keys(self._ctx, keys), "kmp_ctx_set_pass_keys")
 
+    def set_rows(self, row_lo: int = 0, row_hi: int = 0) -> None:
+        """Rows kmp_pairs_stream covers ([0, 0): all): a process's share of a multi-process split."""
+        self._check(lib().kmp_ctx_set_rows(self._ctx, row_lo, row_hi), "kmp_ctx_set_rows")
+
     @property
     def last_passes(self) -> int:
         return int(lib().kmp_ctx_last_passes(self._ctx))
@@ -260,6 +264,50 @@ class KmerPairEngine:
                 check(lib().kmp_edges_get_wk(h, j, _ptr(w), len(w), C.byref(n)), "kmp_edges_get_wk")
                 wk[k] = w
         return edges, wk
+
+
+    def pairs_stream(self, ks=(5,), min_shared=1, require_class_diff=True, align_threshold=10,
+                     score=_lib.KMP_SCORE_COUNT, sink=None, on_device=False) -> dict:
+        """kmp_pairs_stream: the edges of ks (one k, or the config-5 union) in row passes, each
+        handed to ``sink(chunk)`` (a dict: rank, row_lo, row_hi, n, and numpy arrays p, q, w, score,
+        wk (list) when on_device is False; raw device pointers otherwise), never resident whole.
+        Returns the stream summary (counters, digest, per-segment digests, passes, ordered)."""
+        o = _lib.PairOpts(min_shared, int(require_class_diff), align_threshold, score, _lib.KMP_ENGINE_AUTO)
+        karr = (C.c_int * len(ks))(*ks)
+        err = []
+
+        def _sink(user, chp):
+            try:
+                ch = chp.contents
+                d = {"rank": ch.rank, "row_lo": ch.row_lo, "row_hi": ch.row_hi, "n": int(ch.n),
+                     "on_device": bool(ch.on_device), "device": ch.device}
+                if ch.on_device:
+                    d.update(p=ch.p, q=ch.q, w=ch.w, score=ch.score, wk=[ch.wk[j] for j in range(len(ks))])
+                else:
+                    def arr(ptr):
+                        if not ptr or ch.n == 0:
+                            return np.zeros(0, np.uint32)
+                        return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_uint32)), shape=(ch.n,)).copy()
+                    d.update(p=arr(ch.p), q=arr(ch.q), w=arr(ch.w), score=arr(ch.score),
+                             wk=[arr(ch.wk[j]) for j in range(len(ks))])
+                r = sink(d)
+                return int(r or 0)
+            except Exception as exc:  # surfaced after the call
+                err.append(exc)
+                return _lib.KMP_EINVAL
+        cb = _lib.EDGE_SINK(_sink) if sink is not None else _lib.EDGE_SINK()
+        sm = _lib.StreamSummary()
+        st = lib().kmp_pairs_stream(self._ctx, C.byref(o), karr, len(ks), int(bool(on_device)), cb, None,
+                                    C.byref(sm))
+        if err:
+            raise err[0]
+        self._check(st, "kmp_pairs_stream")
+        return sm.as_dict()
+
+
+def digest_term(p, q, w, s, w0) -> int:
+    """kmp_edge_digest_term of one edge (the stream digest's per-edge term)."""
+    return int(lib().kmp_edge_digest_term(p, q, w, s, w0))
 
 
 class Mphf:
