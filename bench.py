@@ -13,9 +13,12 @@ Inputs are synthetic (N = 100,000, seed 3, len ~ N(300
 
 N > 1 (config 4): one process per GPU over RCCL, the k-mer split (dist.kmer_split_step): each rank
 groups and expands its share of the k-mers, one all-to-all moves the pair keys to their row
-owners, each rank reduces its rows.  The step ends with every rank holding the canonical edges of
-its row range in HBM (rank order = canonical order); the gather of all of them onto one GPU is
-timed apart (gather_ms) and is not part of the step.
+owners, each rank reduces its rows, and rank 0 gathers every rank's row block behind its own (rank
+order = canonical order): the timed step ends with the canonical list resident on rank 0
+(SURVEY.md §8d); the row-sharded step without that gather is reported as a breakdown.
+
+--config config5: config 5 at its stated shape (1M proteins, k = 5 + 7, BLOSUM, streamed row
+passes; bench_config5); N > 1 splits its rows over the ranks with no data-path collective.
 """
 from __future__ import annotations
 
@@ -43,7 +46,7 @@ WORKLOADS = {
     "config3": "config3: N=100000, seed=3, len~N(300,30^2), k=7",
     "config2": "config2: N=10000, seed=2, len~N(300,30^2), k=7",
     "config1": "config1: uniprot_arg.fasta (the reference's dataset, 10619 proteins), k=5",
-    "config5": "config5 at k=7: N=1000000, seed=5, len log-uniform 50-2000, k=7, BLOSUM scores, row passes",
+    "config5": "config5: N=1000000, seed=5, len log-uniform 50-2000, k=5+7 combined, BLOSUM scores, streamed row passes",
 }
 
 
@@ -68,12 +71,12 @@ def load_batch(name):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default 20; config5: 1)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 3; config5: 0)")
     ap.add_argument("--config", default="config3", choices=sorted(CONFIGS))
     ap.add_argument("--engine", default="residues", choices=["residues", "postings", "tiles"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="oracle threads (0: min(16, cores))")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="oracle threads of the all-cores run (0: every usable core)")
     ap.add_argument("--score", default="blosum", choices=["blosum", "count"], help="config5: edge score")
     ap.add_argument("--split", default="kmer", choices=["kmer", "rows"], help="multi-GPU flow (N > 1)")
     return ap.parse_args()
@@ -89,77 +92,70 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(proteins, k, threads):
+def usable_cores() -> dict:
+    """The host's cores as this process can use them: nproc, the affinity mask, and the cgroup CPU
+    quota (cpu.max) when one is set; `all` = the smallest (a box shares its host, so nproc
+    overstates what a job gets)."""
+    n = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = n
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(-(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    allc = min(n, aff, quota or n)
+    return {"nproc": n, "affinity": aff, "cgroup_quota": quota, "all": allc}
+
+
+def cpu_baseline(proteins, k, threads=0):
     """The reference algorithm restated in C (oracle/: windows, per-protein sort + dedup, df,
     Σ C(df,2) posting-list expansion, class filter, per-pair collapse), timed on this host over
-    the full workload: once single-threaded (the reference's threads = 1, run.sh's plumbing
-    config) and once on `threads` cores.  `value` is the multi-core run."""
+    the full workload: single-threaded (the reference's threads = 1), on 32
+    threads (run.sh:16's `threads`) and on every usable host core.  `value` is the all-cores run
+    (`threads` overrides it)."""
     from oracle.oracle import Oracle
     n = proteins.n
+    cores = usable_cores()
+    allc = threads or cores["all"]
     runs = {}
-    for t in (1, threads):
+    for t in sorted({1, 32, allc}):
         t0 = time.perf_counter()
         o = Oracle(proteins.residues, proteins.offsets, proteins.class_id, k=k, threads=t)
         p, _, _ = o.pairs()
         runs[t] = (time.perf_counter() - t0, int(len(p)))
-    dt, ne = runs[threads]
-    return {"value": n * (n - 1) / 2 / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
+    dt, ne = runs[allc]
+    per = {str(t): {"value": n * (n - 1) / 2 / v[0], "seconds": v[0], "cores": t} for t, v in runs.items()}
+    return {"value": n * (n - 1) / 2 / dt, "unit": "pairs/s", "cores": allc, "kind": "port",
             "sample": f"full workload ({n} proteins, k={k}): windows, K(p) sort+dedup, df, Σ C(df,2) "
-                      f"posting-list expansion, class filter, per-pair collapse; one run per thread count",
-            "seconds": dt, "edges": ne,
-            "single_thread": {"value": n * (n - 1) / 2 / runs[1][0], "seconds": runs[1][0], "cores": 1},
-            "nproc": os.cpu_count(), "cpu_model": cpu_model()}
+                      f"posting-list expansion, class filter, per-pair collapse; runs at 1, 32 (run.sh:16) and "
+                      f"{allc} (all usable cores) threads",
+            "seconds": dt, "edges": ne, "runs": per,
+            "single_thread": per["1"], "threads_32": per["32"],
+            "host_cores": cores, "cpu_model": cpu_model()}
 
 
-# names of the six stage-timing slots (kmp_postings_stats.stage_ms) per tail
-STAGE_NAMES = {
-    "rows": ("keys_level1", "buckets_level2", "group_expand", "pair_partition", "pair_sort_rle", "emit"),
-}
-STAGE_NAMES_DEFAULT = ("keys", "code_sort", "count", "write", "pair_sort", "rle_emit")
+# names of the six stage-timing slots (kmp_postings_stats.stage_ms) of the bucketed residue step
+STAGE_NAMES = ("keys_level1", "buckets_level2", "group_expand", "pair_partition", "pair_sort_rle", "emit")
 
 
-def stage_bytes(n_res, slots, n_inc, n_edges, n_uniq, tail="sort", n_win=None):
-    """Algorithmic HBM bytes of each postings stage (one read of every input, one write of
-    every output).  The six timing slots of the p-shard tail are keys, bucket sort,
-    group + expand (pair keys written to their row ranges), -, row-range reduce (+ offsets),
-    compaction.  'rows' (the default residue step): level-1 partition (residues in, one u64 key
-    per window out), level-2 partition (keys in and out), group + expand (keys in, pair keys out),
-    pair-key row-block histogram (pair keys in), scatter + LDS sort + run-length encode (pair keys
-    in, runs out), emit (runs in, edges out)."""
-    if tail == "rows":
-        return {
-            "keys_level1": n_res + 8 * n_win,
-            "buckets_level2": 16 * n_win,
-            "group_expand": 8 * n_win + 8 * n_inc,
-            "pair_partition": 8 * n_inc,
-            "pair_sort_rle": 8 * n_inc + 12 * n_uniq,
-            "emit": 12 * n_uniq + 12 * n_edges,
-        }
-    if tail == "fused":
-        return {
-            "keys": n_res + 8 * slots,
-            "code_sort": 16 * slots,
-            "count": 8 * slots + 8 * n_inc,                 # keys in, pair keys out to the shards
-            "write": 0,                                     # padding of the shard tails
-            "pair_sort": 16 * n_inc,
-            "rle_emit": 8 * n_inc + 12 * n_uniq + 12 * n_edges,
-        }
-    if tail == "pshard":
-        return {
-            "keys": n_res + 8 * slots,
-            "code_sort": 16 * slots,
-            "count": 8 * slots + 8 * n_inc,
-            "write": 0,
-            "pair_sort": 8 * n_inc + 12 * n_edges,
-            "rle_emit": 24 * n_edges,
-        }
+def stage_bytes(n_res, n_inc, n_edges, n_uniq, n_win):
+    """Algorithmic HBM bytes of each stage of the residue step (one read of every input, one write
+    of every output): level-1 partition (residues in, one u64 key per window out),
+    level-2 partition (keys in and out), group + expand (keys in, pair keys out), pair-key row-block
+    histogram (pair keys in), scatter + LDS sort + run-length encode (pair keys in, runs out), emit
+    (runs in, edges out)."""
     return {
-        "keys": n_res + 8 * slots,                      # residues in, one u64 key per slot out
-        "code_sort": 16 * slots,                        # keys read once + written once
-        "count": 8 * slots + 8 * n_inc,                 # bucketed: keys in, pair keys out
-        "write": 16 * n_inc,                            # shard gather (bucketed) / write pass (flat)
-        "pair_sort": 16 * n_inc,                        # pair keys read once + written once
-        "rle_emit": 8 * n_inc + 12 * n_uniq + 12 * n_edges,
+        "keys_level1": n_res + 8 * n_win,
+        "buckets_level2": 16 * n_win,
+        "group_expand": 8 * n_win + 8 * n_inc,
+        "pair_partition": 8 * n_inc,
+        "pair_sort_rle": 8 * n_inc + 12 * n_uniq,
+        "emit": 12 * n_uniq + 12 * n_edges,
     }
 
 
@@ -175,66 +171,143 @@ def pmc_traffic(stage: str):
     return (st["bytes"] if st else None), os.path.relpath(files[-1], ROOT)
 
 
+def config5_cpu_baseline(threads):
+    """CPU baseline of config 5: the oracle's restatement of the reference algorithm
+    (posting lists, per-row expansion of every k, class filter, per-pair collapse, the BLOSUM score
+    summed per pair: oracle/kmp_oracle.c orc_build + orc_stream) on a bounded sample — the SAME
+    workload law at N = 100,000 (config 5's lengths, seed 5, k = 5 + 7, BLOSUM), run in full (about
+    30 s on 8 threads); pairs/s scales with the pair count since the incidences grow as N^2 too.
+    The full 10^6 run took 817 s on 8 threads of this container (tests/golden/
+    config5_1m_k5k7_blosum_digest.json)."""
+    from oracle import oracle as O
+    import uniprot_kmer_based_clustering_amd as K
+    n = 100_000
+    b = K.synth(n, 5, 1)
+    t0 = time.perf_counter()
+    orcs = [O.Oracle(b.residues, b.offsets, b.class_id, k=k, threads=threads) for k in (5, 7)]
+    d = O.stream(orcs, threads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": n * (n - 1) / 2 / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
+            "host_cores": usable_cores(),
+            "sample": f"config-5 law at N={n} (seed 5, log-uniform 50-2000), k=5+7, BLOSUM, full run: "
+                      f"{d['n_edges']} edges, {d['incidences']} incidences",
+            "seconds": dt, "edges": d["n_edges"], "nproc": os.cpu_count(), "cpu_model": cpu_model(),
+            "full_1m_seconds_8_threads_container": 817.4}
+
+
 def bench_config5(args):
-    """Config 5's batch at k = 7 through the C ABI (kmp_build_sets + kmp_pairs with BLOSUM scores):
-    1,000,000 proteins of log-uniform lengths 50-2,000 (~5.3e8 windows) do not fit one call, so the
-    library runs bounded-memory row passes.  One step = sets built from the resident
-    residues + every pass + the canonical edge list and its scores copied into the edge set's host
-    arrays (the C ABI hands edges to the caller: this line is PCIe-inclusive).  The k = 5 + 7 union at this size does not fit one GPU."""
+    """Config 5 at its stated shape (BASELINE.json configs[4]): 1,000,000 proteins of log-uniform
+    lengths 50-2,000 (~5.3e8 windows), k = 5 and 7 combined in one reduction, BLOSUM score, through
+    the C ABI's streamed passes (kmp_pairs_stream).  One step = sets per k built
+    from the resident residues + every bounded-memory row pass: grouping + expansion of both k, the
+    fused pair reduction, and the device summary of each pass's chunk (counters and digest) — each
+    pass's canonical edges are resident in HBM when it is summarised (8.4e10 edges in all: the list
+    never exists whole).  N > 1 (torch.distributed.run): each rank streams its kmp_row_split rows on
+    its own GPU (kmp_ctx_set_rows), no data-path collective; value = all ranks' pairs / max time."""
     import uniprot_kmer_based_clustering_amd as K
     from uniprot_kmer_based_clustering_amd import _lib
-    n, seed, law, k = CONFIGS["config5"]
+    import torch
+    import torch.distributed as dist
+    n, seed, law, _ = CONFIGS["config5"]
+    ks = (5, 7)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    steps = args.steps if args.steps is not None else 1
+    warmup = args.warmup if args.warmup is not None else 0
     score = _lib.KMP_SCORE_BLOSUM if args.score == "blosum" else _lib.KMP_SCORE_COUNT
     proteins = K.synth(n, seed, law)
-    with K.KmerPairEngine(0, 16) as e:
+    lo, hi = (int(x) for x in _lib.row_split(n, world)[rank:rank + 2])
+    with K.KmerPairEngine(local, 16) as e:
         e.load(proteins)
-
-        def one_step():
-            e.build_sets(k)
-            with e.edge_set(score=score) as es:
-                return len(es)
-        for _ in range(args.warmup):
-            one_step()
+        if world > 1:
+            e.set_rows(lo, hi)
+        for _ in range(warmup):
+            e.pairs_stream(ks, score=score)
+        if world > 1:
+            dist.barrier()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
-            n_edges = one_step()
+        for _ in range(steps):
+            sm = e.pairs_stream(ks, score=score)
         dt = time.perf_counter() - t0
-        passes = e.last_passes
-        c = e.counters()
-    ms = dt / args.steps * 1e3
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        keys = ("n_edges", "sum_w", "sum_score", "n_align", "incidences", "digest", "passes")
+        v = torch.tensor([sm[k] & 0x7FFFFFFFFFFFFFFF if k == "digest" else sm[k] for k in keys],
+                         dtype=torch.int64, device=f"cuda:{local}")
+        allv = [torch.zeros_like(v) for _ in range(world)]
+        dist.all_gather(allv, v)
+        st = torch.tensor(list(sm["stage_ms"].values()), dtype=torch.float64, device=f"cuda:{local}")
+        alls = [torch.zeros_like(st) for _ in range(world)]
+        dist.all_gather(alls, st)
+        ranks = [dict(zip(keys, [int(x) for x in a.tolist()]), stage_ms=dict(zip(sm["stage_ms"], b.tolist())),
+                      row_lo=int(_lib.row_split(n, world)[r]), row_hi=int(_lib.row_split(n, world)[r + 1]))
+                 for r, (a, b) in enumerate(zip(allv, alls))]
+        tot = {k: sum(r[k] for r in ranks) for k in ("n_edges", "sum_w", "sum_score", "n_align", "incidences", "passes")}
+        dist.destroy_process_group()
+        if rank != 0:
+            return
+    else:
+        ranks = None
+        tot = {k: sm[k] for k in ("n_edges", "sum_w", "sum_score", "n_align", "incidences", "passes")}
+    ms = dt / steps * 1e3
     pairs_total = n * (n - 1) / 2
-    out = {"metric": "protein pairs/sec (+ edges/sec), 100k x 300aa synthetic, k=7",
-           "value": pairs_total / (dt / args.steps), "unit": "pairs/s", "n_gpus": 1, "steps": args.steps,
-           "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "strong",
+    lens = np.diff(np.asarray(proteins.offsets, dtype=np.int64))
+    win = {k: int(np.maximum(lens - k + 1, 0).sum()) for k in ks}
+    stg = (ranks[0]["stage_ms"] if ranks else sm["stage_ms"])
+    # algorithmic bytes per stage (one read of every input, one write of every output), per rank 0
+    # or the single GPU: expand of k0 re-reads the grouped keys each pass and writes the pair keys;
+    # the reduce reads each pair key (partition, scatter), writes and re-reads the u32 row key, and
+    # writes the edges (p q w score w5 w7)
+    r0 = ranks[0] if ranks else {"incidences": sm["incidences"], "n_edges": sm["n_edges"], "passes": sm["passes"]}
+    alg = {"expand_k0": 8 * win[5] * r0["passes"] + 8 * r0["incidences"],
+           "reduce": 24 * r0["incidences"] + 24 * r0["n_edges"]}
+    stages = {s: {"ms": stg[s], "alg_bytes": alg.get(s),
+                  "GBs": alg[s] / (stg[s] * 1e-3) / 1e9 if s in alg and stg[s] > 0 else None} for s in stg}
+    dom = max(alg, key=lambda s: stg[s])
+    ach = stages[dom]["GBs"]
+    out = {"metric": "protein pairs/sec (+ edges/sec), config 5: 1M synthetic log-uniform 50-2000, k=5+7 combined, "
+                     "BLOSUM-weighted",
+           "value": pairs_total / (dt / steps), "unit": "pairs/s", "n_gpus": world, "steps": steps,
+           "warmup": warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "strong",
            "vs_baseline": None, "dtype": "u32",
-           "data": "synthetic (SURVEY.md §8d generator, seeded; log-uniform lengths 50-2000)",
-           "config": {"workload": WORKLOADS["config5"], "proteins": n, "k": k, "pairs": int(pairs_total),
-                      "edges": int(n_edges), "passes": passes, "score": args.score, "engine": "C ABI kmp_pairs",
-                      "edges_in": "host (PCIe-inclusive)"},
-           "edges_per_s": n_edges / (dt / args.steps),
-           "counters": c,
-           "roofline": None,
-           "roofline_note": "per-stage roofline on the config3 line; this line times whole C-ABI calls"}
-    if not args.no_cpu_baseline:
-        from oracle.oracle import Oracle
-        t0 = time.perf_counter()
-        o = Oracle(proteins.residues, proteins.offsets, proteins.class_id, k=k, threads=16)
-        p, _, _ = o.pairs()
-        cdt = time.perf_counter() - t0
-        out["cpu_baseline"] = {"value": pairs_total / cdt, "unit": "pairs/s", "cores": 16, "kind": "port",
-                               "sample": f"full workload ({n} proteins, k={k}), 16 threads, no scores",
-                               "seconds": cdt, "edges": int(len(p)), "nproc": os.cpu_count(),
-                               "cpu_model": cpu_model()}
+           "data": "synthetic (SURVEY.md §8d generator, seeded; log-uniform lengths 50-2000, 15 AMR classes)",
+           "config": {"workload": WORKLOADS["config5"], "proteins": n, "k": list(ks), "pairs": int(pairs_total),
+                      "edges": tot["n_edges"], "incidences": tot["incidences"], "passes": tot["passes"],
+                      "score": args.score, "engine": "C ABI kmp_pairs_stream (fused k=5+7 reduction)",
+                      "parallelism": "single GPU" if world == 1 else f"row split x{world} (kmp_ctx_set_rows per rank)",
+                      "edges_in": "device, per pass (summarised on the device; never copied whole)"},
+           "edges_per_s": tot["n_edges"] / (dt / steps),
+           "incidences_per_s": tot["incidences"] / (dt / steps),
+           "summary": {k: tot[k] for k in ("n_edges", "sum_w", "sum_score", "n_align")},
+           "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": ach / HBM_PEAK_GBS if ach else None, "traffic": None, "kernel": dom,
+                        "kernel_ms": stg[dom], "alg_bytes_per_launch": alg[dom], "stages": stages,
+                        "note": "stage times summed over the passes (HIP events on the stream); "
+                                "rank 0's when N > 1"}}
+    if ranks:
+        out["ranks"] = ranks
+    if world == 1:
+        if not ranks and "digest" in sm:
+            out["digest"] = str(sm["digest"])
+        if not args.no_cpu_baseline:
+            out["cpu_baseline"] = config5_cpu_baseline(args.cpu_threads or usable_cores()["all"])
     print(json.dumps(out))
 
 
 def main():
     args = parse()
     if args.config == "config5":
-        if args.gpus != 1:
-            print("config5 is a single-GPU line", file=sys.stderr)
-            sys.exit(2)
         return bench_config5(args)
+    if args.steps is None:
+        args.steps = 20
+    if args.warmup is None:
+        args.warmup = 3
     import torch
     import torch.distributed as dist
 
@@ -277,7 +350,9 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        n_edges = one_step()
+        # N > 1: the step ends with the canonical list on rank 0 (SURVEY.md §8d's clock), so it
+        # includes the rank-order gather of every rank's rows
+        n_edges = one_step(gather=True)
         if postings and world == 1:
             st = np.array(pipe.postings_stats.stage_ms[:], dtype=np.float64)
             stage_sum = st if stage_sum is None else stage_sum + st
@@ -292,10 +367,10 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-        # untimed: the edge total over the ranks, per-rank phase times, and the gather to rank 0
+        # untimed: per-rank phase times and the step without the gather (the breakdown)
         ne = torch.tensor([n_edges], dtype=torch.int64, device=f"cuda:{local}")
+        dist.broadcast(ne, 0)  # rank 0 holds the whole list: its count is the total
         if args.split == "kmer":
-            dist.all_reduce(ne)
             stt = pipe._split_state.bufs[3].clone()
             dist.all_reduce(stt)  # every rank's k-mers' statistics: the batch's
             split_stats = [int(x) for x in stt.tolist()]
@@ -312,11 +387,13 @@ def main():
             dist.barrier()
             torch.cuda.synchronize()
             g0 = time.perf_counter()
-            tot = kmer_split_step(pipe, rank, world, gather=True)
+            for _ in range(5):
+                kmer_split_step(pipe, rank, world, gather=False)
             torch.cuda.synchronize()
-            gather_ms = (time.perf_counter() - g0) * 1e3
-            if rank == 0:
-                assert tot == int(ne.item()), (tot, int(ne.item()))
+            dist.barrier()
+            t = torch.tensor([(time.perf_counter() - g0) / 5 * 1e3], dtype=torch.float64, device=f"cuda:{local}")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            no_gather_ms = float(t.item())
         n_edges = int(ne.item())
 
     ms = dt / args.steps * 1e3
@@ -352,28 +429,27 @@ def main():
             lens = np.diff(np.asarray(proteins.offsets, dtype=np.int64))
             n_win = int(np.maximum(lens - k + 1, 0).sum())
             n_inc = split_stats[6]
-            byts = sum(stage_bytes(int(proteins.offsets[-1]), 0, n_inc, n_edges, n_edges, "rows", n_win).values())
+            byts = sum(stage_bytes(int(proteins.offsets[-1]), n_inc, n_edges, n_edges, n_win).values())
             ach = byts / (ms * 1e-3) / 1e9
             out["roofline"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
                                "frac": ach / (HBM_PEAK_GBS * world), "traffic": None,
                                "kernel": f"whole step over {world} GPUs", "alg_bytes_per_step": byts,
                                "incidences": n_inc, "exchange_bytes": 8 * n_inc}
             out["ranks"] = rank_info
-            out["gather_ms"] = gather_ms
-            out["edges_layout"] = "row-sharded across ranks (rank order = canonical); gather_ms = step + gather"
+            out["step_without_gather_ms"] = no_gather_ms
+            out["gather_ms"] = ms - no_gather_ms
+            out["edges_layout"] = ("canonical list on rank 0 at the end of each timed step (the ranks' row blocks "
+                                   "gathered in rank order); step_without_gather_ms = the row-sharded step alone")
         if args.engine in ("residues", "postings"):
             out["config"]["layout"] = pipe.last_layout()
             out["config"]["heavy_path"] = pipe.last_heavy()
             out["config"]["row_overflow_blocks"] = pipe.overflow_blocks()
-        if stage_sum is not None:
+        if stage_sum is not None and pipe.last_tail() == "rows":  # the bucketed step's six stages
             ps = pipe.postings_stats.as_dict()
-            slots = int(_lib.lib().kmp_set_capacity(n, int(proteins.offsets[-1])))
-            tail = pipe.last_tail()
             lens = np.diff(np.asarray(proteins.offsets, dtype=np.int64))
             n_win = int(np.maximum(lens - k + 1, 0).sum())  # windows = keys of the residue path
-            byts = stage_bytes(int(proteins.offsets[-1]), slots, ps["incidences"], n_edges, ps["pairs"], tail,
-                               n_win)
-            names = STAGE_NAMES.get(tail, STAGE_NAMES_DEFAULT)
+            byts = stage_bytes(int(proteins.offsets[-1]), ps["incidences"], n_edges, ps["pairs"], n_win)
+            names = STAGE_NAMES
             stage_ms = dict(zip(names, (stage_sum / args.steps).tolist()))
             stages = {s: {"ms": stage_ms[s], "alg_bytes": byts[s],
                           "GBs": byts[s] / (stage_ms[s] * 1e-3) / 1e9 if stage_ms[s] > 0 else None}
@@ -386,7 +462,7 @@ def main():
                                "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": source,
                                "traffic_over_alg": traffic / byts[dom] if traffic else None, "kernel": dom,
                                "kernel_ms": stage_ms[dom], "alg_bytes_per_launch": byts[dom],
-                               "layout": pipe.last_layout(), "tail": tail, "stages": stages,
+                               "layout": pipe.last_layout(), "tail": "rows", "stages": stages,
                                "step_alg_bytes": sum(byts.values()),
                                "step_GBs": sum(byts.values()) / (ms * 1e-3) / 1e9}
             # SURVEY.md §8d model: 4·(S_p + S_q) bytes per pair, i.e. a merge-intersection of every
@@ -396,8 +472,7 @@ def main():
             out["roofline"]["pairs_model_GBs"] = b_model / (ms * 1e-3) / 1e9
             out["postings_stats"] = ps
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        out["cpu_baseline"] = cpu_baseline(proteins, k, threads)
+        out["cpu_baseline"] = cpu_baseline(proteins, k, args.cpu_threads)
     if rank == 0:
         print(json.dumps(out))
     if world > 1:

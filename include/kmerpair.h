@@ -252,6 +252,10 @@ typedef struct {
     uint64_t seg_digest[KMP_DIGEST_SEGMENTS];
     uint32_t passes;
     int32_t ordered;
+    /* device time summed over the passes (and ranks), HIP events on each lane's stream: the
+     * grouping + expansion of ks[0] (front, buckets, heavy path), of the other k, the pair
+     * reduction (row-block tail, overflow sort, emit; nk > 2: + merge), the summary kernel */
+    float stage_ms[4];
 } kmp_stream_summary;
 int kmp_pairs_stream(kmp_ctx* ctx, const kmp_pair_opts* opts, const int* ks, uint32_t nk, int sink_on_device,
                      kmp_edge_sink sink, void* user, kmp_stream_summary* summary);
@@ -505,6 +509,8 @@ int kmp_dev_pairs_rows_scored(kmp_postings* ws, const uint8_t* d_res, const uint
  * w0 >= min_shared or w1 >= min_shared (and the classes differ when required).  No per-k lists,
  * no merge.  Rows as kmp_dev_pairs_rows, at most kmp_dev_rows_max(n, 2) per call (65,536 rows at
  * n = 10^6). */
+/* stats (may be NULL): stage_ms[0] = the first k's grouping + expansion, [1] the second k's, [2] the
+ * fused reduction + emit (HIP events on `stream`); the front statistics are the first k's. */
 int kmp_dev_pairs_rows_multi(kmp_postings* const* ws, const int* ks, uint32_t nk, const uint8_t* d_res,
                              const uint64_t* d_res_off, const uint16_t* d_class, uint32_t n, uint64_t slots,
                              uint32_t min_shared, int require_class_diff, uint32_t row_lo, uint32_t row_hi,

@@ -728,3 +728,208 @@ int orc_pair_scores(const orc_ctx* x, const uint32_t* p, const uint32_t* q, uint
     run_pool(threads < 1 ? 1 : threads, score_worker, &j);
     return ORC_OK;
 }
+
+/* ======================================================================================
+ * Direct restatement for sampled rows (an independent check of orc_stream and of the library
+ * at sizes where the posting-list oracle is too slow to run live): for the few proteins p in
+ * [row_lo, row_hi) and every q > p of the batch, w_k(p, q) = |K_k(p) ∩ K_k(q)| straight from the
+ * definition (SURVEY.md §8 "Canonical result definition"; K(p) = the distinct window codes,
+ * protein.rs:107-132 + main.rs:99-101), the BLOSUM score Σ over the shared codes of their
+ * self-scores, the class filter of mod.rs:580-587 and the config-5 union rule.  Each q's windows
+ * are extracted, sorted and deduplicated, and each distinct code is looked up in the sorted
+ * (code, sample row) table of the sample's codes.  Edges in canonical order.
+ * ====================================================================================== */
+typedef struct {
+    const uint8_t* res;
+    const uint64_t* off;
+    const uint16_t* cls;
+    uint32_t n, lo, hi, nr;
+    int nk;
+    int ks[ORC_MAXK];
+    uint64_t* tab[ORC_MAXK];    /* sorted (code << 32 | sample row index) */
+    uint64_t ntab[ORC_MAXK];
+    uint32_t min_shared;
+    int require_class_diff, blosum;
+    _Atomic uint32_t cursor;
+    pthread_mutex_t lock;
+    uint64_t* out;              /* (p << 32 | q) keys, then per edge: w, s, w_k ... (2 + nk words) */
+    uint32_t* val;
+    uint64_t nout, capout;
+} direct_job;
+
+static int cmp_u64(const void* a, const void* b) {
+    uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
+    return x < y ? -1 : x > y;
+}
+
+static uint64_t distinct_codes(const uint8_t* s, uint64_t L, int k, const uint8_t* lut, uint32_t* buf,
+                               uint32_t* tmp) {
+    uint64_t nw = n_windows(L, k);
+    for (uint64_t j = 0; j < nw; ++j) {
+        uint32_t v = 0;
+        for (int i = 0; i < k; ++i) v = v * 21u + lut[s[j + i]];
+        buf[j] = v;
+    }
+    sort_u32(buf, tmp, nw);
+    return dedup_sorted(buf, nw);
+}
+
+static void* direct_worker(void* arg) {
+    direct_job* j = (direct_job*)arg;
+    uint8_t lut[256];
+    for (int b = 0; b < 256; ++b) lut[b] = orc_residue_code((uint8_t)b);
+    uint64_t maxl = 0;
+    for (uint32_t p = 0; p < j->n; ++p)
+        if (j->off[p + 1] - j->off[p] > maxl) maxl = j->off[p + 1] - j->off[p];
+    uint32_t* buf = (uint32_t*)malloc(sizeof(uint32_t) * (maxl + 1));
+    uint32_t* tmp = (uint32_t*)malloc(sizeof(uint32_t) * (maxl + 1));
+    uint32_t* w = (uint32_t*)calloc((size_t)j->nr * ORC_MAXK, sizeof(uint32_t));
+    uint32_t* sc = (uint32_t*)calloc(j->nr, sizeof(uint32_t));
+    uint32_t* touched = (uint32_t*)malloc(sizeof(uint32_t) * (j->nr ? j->nr : 1));
+    uint8_t* mk = (uint8_t*)calloc(j->nr ? j->nr : 1, 1);
+    uint64_t lcap = 1024, ln = 0;
+    uint64_t* lkey = (uint64_t*)malloc(sizeof(uint64_t) * lcap);
+    uint32_t* lval = (uint32_t*)malloc(sizeof(uint32_t) * lcap * (2 + j->nk));
+    const uint32_t first = j->lo + 1;
+    for (;;) {
+        uint32_t q0 = atomic_fetch_add(&j->cursor, 256u);
+        if ((uint64_t)first + q0 >= j->n) break;
+        uint32_t q1 = first + q0 + 256 < j->n ? first + q0 + 256 : j->n;
+        for (uint32_t q = first + q0; q < q1; ++q) {
+            uint32_t nt = 0;
+            for (int k = 0; k < j->nk; ++k) {
+                uint64_t m = distinct_codes(j->res + j->off[q], j->off[q + 1] - j->off[q], j->ks[k], lut, buf, tmp);
+                const uint64_t* T = j->tab[k];
+                const uint64_t nT = j->ntab[k];
+                for (uint64_t i = 0; i < m; ++i) {
+                    const uint64_t key = (uint64_t)buf[i] << 32;
+                    uint64_t a = 0, b = nT;  /* first entry >= key */
+                    while (a < b) {
+                        uint64_t mid = (a + b) >> 1;
+                        if (T[mid] < key) a = mid + 1; else b = mid;
+                    }
+                    for (; a < nT && (T[a] >> 32) == buf[i]; ++a) {
+                        const uint32_t r = (uint32_t)T[a];
+                        if (j->lo + r >= q) continue;  /* pairs p < q only */
+                        w[(size_t)r * ORC_MAXK + k]++;
+                        if (j->blosum) sc[r] += code_self_score(buf[i], j->ks[k]);
+                        if (!mk[r]) { mk[r] = 1; touched[nt++] = r; }
+                    }
+                }
+            }
+            for (uint32_t t = 0; t < nt; ++t) {
+                const uint32_t r = touched[t], p = j->lo + r;
+                mk[r] = 0;
+                uint32_t tot = 0, any = 0;
+                for (int k = 0; k < j->nk; ++k) {
+                    tot += w[(size_t)r * ORC_MAXK + k];
+                    any |= w[(size_t)r * ORC_MAXK + k] >= j->min_shared;
+                }
+                const int keep = any && (!j->require_class_diff || j->cls[p] != j->cls[q]);
+                if (keep) {
+                    if (ln == lcap) {
+                        lcap *= 2;
+                        lkey = (uint64_t*)realloc(lkey, sizeof(uint64_t) * lcap);
+                        lval = (uint32_t*)realloc(lval, sizeof(uint32_t) * lcap * (2 + j->nk));
+                    }
+                    lkey[ln] = ((uint64_t)p << 32) | q;
+                    uint32_t* v = lval + ln * (2 + j->nk);
+                    v[0] = tot;
+                    v[1] = j->blosum ? sc[r] : tot;
+                    for (int k = 0; k < j->nk; ++k) v[2 + k] = w[(size_t)r * ORC_MAXK + k];
+                    ++ln;
+                }
+                for (int k = 0; k < j->nk; ++k) w[(size_t)r * ORC_MAXK + k] = 0;
+                sc[r] = 0;
+            }
+        }
+    }
+    pthread_mutex_lock(&j->lock);
+    if (j->nout + ln > j->capout) {
+        j->capout = (j->nout + ln) * 2 + 1024;
+        j->out = (uint64_t*)realloc(j->out, sizeof(uint64_t) * j->capout);
+        j->val = (uint32_t*)realloc(j->val, sizeof(uint32_t) * j->capout * (2 + j->nk));
+    }
+    memcpy(j->out + j->nout, lkey, sizeof(uint64_t) * ln);
+    memcpy(j->val + j->nout * (2 + j->nk), lval, sizeof(uint32_t) * ln * (2 + j->nk));
+    j->nout += ln;
+    pthread_mutex_unlock(&j->lock);
+    free(buf); free(tmp); free(w); free(sc); free(touched); free(mk); free(lkey); free(lval);
+    return NULL;
+}
+
+/* Edges (p, q) of rows [row_lo, row_hi) (at most 65,536 rows) over ks[0..nk): P, Q, W, S and WK
+ * (nk x n, k-major) malloc'd, canonical order. */
+int orc_rows_direct(const uint8_t* res, const uint64_t* off, uint32_t n, const uint16_t* cls, const int* ks, int nk,
+                    uint32_t row_lo, uint32_t row_hi, uint32_t min_shared, int require_class_diff, int blosum,
+                    int threads, uint32_t** P, uint32_t** Q, uint32_t** W, uint32_t** S, uint32_t** WK,
+                    uint64_t* n_edges) {
+    if (nk < 1 || nk > ORC_MAXK || row_lo > row_hi || row_hi > n || row_hi - row_lo > 65536) return ORC_EINVAL;
+    direct_job j;
+    memset(&j, 0, sizeof j);
+    j.res = res; j.off = off; j.n = n; j.lo = row_lo; j.hi = row_hi; j.nr = row_hi - row_lo; j.nk = nk;
+    uint16_t* zero = NULL;
+    if (!cls) { zero = (uint16_t*)calloc(n ? n : 1, sizeof(uint16_t)); cls = zero; }
+    j.cls = cls;
+    j.min_shared = min_shared < 1 ? 1 : min_shared;
+    j.require_class_diff = require_class_diff;
+    j.blosum = blosum;
+    uint8_t lut[256];
+    for (int b = 0; b < 256; ++b) lut[b] = orc_residue_code((uint8_t)b);
+    uint64_t maxl = 0;
+    for (uint32_t p = row_lo; p < row_hi; ++p)
+        if (off[p + 1] - off[p] > maxl) maxl = off[p + 1] - off[p];
+    uint32_t* buf = (uint32_t*)malloc(sizeof(uint32_t) * (maxl + 1));
+    uint32_t* tmp = (uint32_t*)malloc(sizeof(uint32_t) * (maxl + 1));
+    for (int k = 0; k < nk; ++k) {
+        if (ks[k] < 1 || ks[k] > 7) return ORC_EINVAL;
+        j.ks[k] = ks[k];
+        uint64_t tot = 0, cap = 1024;
+        uint64_t* t = (uint64_t*)malloc(sizeof(uint64_t) * cap);
+        for (uint32_t p = row_lo; p < row_hi; ++p) {
+            uint64_t m = distinct_codes(res + off[p], off[p + 1] - off[p], ks[k], lut, buf, tmp);
+            if (tot + m > cap) { cap = (tot + m) * 2; t = (uint64_t*)realloc(t, sizeof(uint64_t) * cap); }
+            for (uint64_t i = 0; i < m; ++i) t[tot++] = ((uint64_t)buf[i] << 32) | (p - row_lo);
+        }
+        qsort(t, tot, sizeof(uint64_t), cmp_u64);
+        j.tab[k] = t;
+        j.ntab[k] = tot;
+    }
+    free(buf); free(tmp);
+    atomic_init(&j.cursor, 0);
+    pthread_mutex_init(&j.lock, NULL);
+    run_pool(threads < 1 ? 1 : threads, direct_worker, &j);
+    pthread_mutex_destroy(&j.lock);
+    /* canonical order: sort the keys with their value rows */
+    const uint64_t m = j.nout, vw = 2 + nk;
+    uint64_t* idx = (uint64_t*)malloc(sizeof(uint64_t) * (m ? m : 1));
+    for (uint64_t i = 0; i < m; ++i) idx[i] = i;
+    /* sort (key, index) pairs: keys are distinct, so sort 128-bit by key via an index array */
+    uint64_t* kk = j.out;
+    {   /* simple: pack to (key, idx) records and qsort */
+        typedef struct { uint64_t key, i; } rec;
+        rec* r = (rec*)malloc(sizeof(rec) * (m ? m : 1));
+        for (uint64_t i = 0; i < m; ++i) { r[i].key = kk[i]; r[i].i = i; }
+        qsort(r, m, sizeof(rec), cmp_u64);  /* key is the first field */
+        for (uint64_t i = 0; i < m; ++i) idx[i] = r[i].i;
+        free(r);
+    }
+    uint32_t* pp = (uint32_t*)malloc(sizeof(uint32_t) * (m ? m : 1));
+    uint32_t* qq = (uint32_t*)malloc(sizeof(uint32_t) * (m ? m : 1));
+    uint32_t* ww = (uint32_t*)malloc(sizeof(uint32_t) * (m ? m : 1));
+    uint32_t* ss = (uint32_t*)malloc(sizeof(uint32_t) * (m ? m : 1));
+    uint32_t* wk = (uint32_t*)malloc(sizeof(uint32_t) * (m ? m : 1) * nk);
+    for (uint64_t o = 0; o < m; ++o) {
+        const uint64_t i = idx[o];
+        pp[o] = (uint32_t)(kk[i] >> 32);
+        qq[o] = (uint32_t)kk[i];
+        const uint32_t* v = j.val + i * vw;
+        ww[o] = v[0];
+        ss[o] = v[1];
+        for (int k = 0; k < nk; ++k) wk[(uint64_t)k * m + o] = v[2 + k];
+    }
+    free(idx); free(j.out); free(j.val); free(zero);
+    for (int k = 0; k < nk; ++k) free(j.tab[k]);
+    *P = pp; *Q = qq; *W = ww; *S = ss; *WK = wk; *n_edges = m;
+    return ORC_OK;
+}

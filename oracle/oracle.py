@@ -81,6 +81,10 @@ def lib():
         L.orc_pair_scores.argtypes = [P, P, P, C.c_uint64, P, C.c_int]
         L.orc_digest_term.restype = C.c_uint64
         L.orc_digest_term.argtypes = [C.c_uint32] * 5
+        L.orc_rows_direct.restype = C.c_int
+        L.orc_rows_direct.argtypes = [P, P, C.c_uint32, P, P, C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int,
+                                      C.c_int, C.c_int, C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(P),
+                                      C.POINTER(P), C.POINTER(C.c_uint64)]
         L.orc_residue_code.restype = C.c_uint8
         L.orc_residue_code.argtypes = [C.c_uint8]
         L.orc_pack.restype = C.c_uint32
@@ -236,6 +240,32 @@ def stream(oracles, row_lo=0, row_hi=None, min_shared=1, require_class_diff=True
             L.orc_free(x)
         return out, (p, q, w, s, list(wk))
     return out
+
+
+def rows_direct(residues, offsets, class_id, ks, row_lo, row_hi, min_shared=1, require_class_diff=True, blosum=True,
+                threads=8):
+    """Edges of the few rows [row_lo, row_hi) over every q > p, from the definition w_k(p, q) =
+    |K_k(p) ∩ K_k(q)| (oracle/kmp_oracle.c orc_rows_direct; no posting lists, no global sort):
+    (p, q, w, score, [w_k]) in canonical order.  An independent check of the library (and of
+    orc_stream) at sizes where the posting-list oracle does not run live."""
+    L = lib()
+    res = np.ascontiguousarray(residues, dtype=np.uint8)
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    cls = None if class_id is None else np.ascontiguousarray(class_id, dtype=np.uint16)
+    karr = (C.c_int * len(ks))(*ks)
+    ptrs = [P() for _ in range(5)]
+    ne = C.c_uint64()
+    st = L.orc_rows_direct(res.ctypes.data, off.ctypes.data, len(off) - 1, None if cls is None else cls.ctypes.data,
+                           karr, len(ks), row_lo, row_hi, min_shared, int(require_class_diff), int(blosum), threads,
+                           *[C.byref(x) for x in ptrs], C.byref(ne))
+    if st != 0:
+        raise RuntimeError(f"orc_rows_direct status {st}")
+    m = ne.value
+    p, q, w, s = (_view(x.value, m, np.uint32) for x in ptrs[:4])
+    wk = _view(ptrs[4].value, m * len(ks), np.uint32).reshape(len(ks), m) if m else np.zeros((len(ks), 0), np.uint32)
+    for x in ptrs:
+        L.orc_free(x)
+    return p, q, w, s, list(wk)
 
 
 def digest_term(p, q, w, s, w0) -> int:

@@ -106,3 +106,33 @@ def test_config5_million_proteins_k7(oracle_mod):
     rng = np.random.default_rng(7)
     s = rng.choice(len(p), 2000, replace=False)
     np.testing.assert_array_equal(got.score[s], o.blosum_scores(p[s], q[s]).astype(np.float32))
+
+
+def test_config5_million_k5_k7_blosum_streamed(oracle_mod):
+    """Config 5 at its stated shape on one GPU: 1,000,000 proteins (seed 5, log-uniform 50-2000),
+    k = 5 and 7 combined in one reduction, BLOSUM score, streamed in bounded-memory row passes
+    (8.4e10 edges: the list never exists whole).  The device summary — counters, digest and the 64
+    per-row-segment digests of the canonical list — equals the oracle's (the posting-list
+    restatement, run in this container: tests/golden/config5_1m_k5k7_blosum_digest.json), and
+    sampled row ranges equal, edge by edge, the direct restatement w_k = |K_k(p) ∩ K_k(q)| run
+    live (oracle.rows_direct)."""
+    from common import load_json
+    g = load_json("config5_1m_k5k7_blosum_digest.json")
+    b = K.synth(1_000_000, 5, 1)
+    with K.KmerPairEngine(0, 16) as e:
+        e.load(b)
+        sm = e.pairs_stream((5, 7), score=_lib.KMP_SCORE_BLOSUM)
+        assert sm["passes"] > 10 and sm["ordered"] == 1
+        for key in ("n_edges", "sum_w", "sum_score", "n_align", "sum_w_diff", "incidences", "digest"):
+            assert sm[key] == g[key], key
+        assert sm["seg_edges"] == g["seg_edges"] and sm["seg_digest"] == g["seg_digest"]
+        for lo, hi in ((0, 16), (500_000, 500_016), (999_000, 999_100)):
+            chunks = []
+            e.set_rows(lo, hi)
+            e.pairs_stream((5, 7), score=_lib.KMP_SCORE_BLOSUM, sink=chunks.append)
+            p, q, w, s, wk = oracle_mod.rows_direct(b.residues, b.offsets, b.class_id, (5, 7), lo, hi, threads=16)
+            assert len(p) > 1000
+            for key, want in (("p", p), ("q", q), ("w", w), ("score", s)):
+                np.testing.assert_array_equal(np.concatenate([c[key] for c in chunks]), want)
+            for j in range(2):
+                np.testing.assert_array_equal(np.concatenate([c["wk"][j] for c in chunks]), wk[j])

@@ -87,12 +87,13 @@ class StreamSummary(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("n_edges", "sum_w", "sum_score", "n_align", "sum_w_diff", "incidences",
                                            "digest")] + [
         ("seg_edges", C.c_uint64 * KMP_DIGEST_SEGMENTS), ("seg_digest", C.c_uint64 * KMP_DIGEST_SEGMENTS),
-        ("passes", C.c_uint32), ("ordered", C.c_int32)]
+        ("passes", C.c_uint32), ("ordered", C.c_int32), ("stage_ms", C.c_float * 4)]
 
     def as_dict(self):
-        d = {n: int(getattr(self, n)) for n, _ in self._fields_ if not n.startswith("seg_")}
+        d = {n: int(getattr(self, n)) for n, _ in self._fields_ if not n.startswith("seg_") and n != "stage_ms"}
         d["seg_edges"] = [int(x) for x in self.seg_edges]
         d["seg_digest"] = [int(x) for x in self.seg_digest]
+        d["stage_ms"] = dict(zip(("expand_k0", "expand_k1", "reduce", "summary"), (float(x) for x in self.stage_ms)))
         return d
 
 

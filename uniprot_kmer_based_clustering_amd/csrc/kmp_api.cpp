@@ -1232,6 +1232,23 @@ struct StreamLane {
     kmp::DigestAcc* acc = nullptr;
     uint64_t incidences = 0;
     uint32_t passes = 0;
+    float stage_ms[4] = {0, 0, 0, 0};  // kmp_stream_summary.stage_ms
+};
+
+// two HIP events around the summary kernel of a pass (lane-local, created on first use)
+struct EventPair {
+    hipEvent_t a = nullptr, b = nullptr;
+    ~EventPair() {
+        if (a) (void)hipEventDestroy(a);
+        if (b) (void)hipEventDestroy(b);
+    }
+    bool ready() { return (a || hipEventCreate(&a) == hipSuccess) && (b || hipEventCreate(&b) == hipSuccess); }
+    float ms() {
+        float t = 0.f;
+        const bool ok = hipEventElapsedTime(&t, a, b) == hipSuccess;
+        if (!ok) (void)hipGetLastError();
+        return ok ? t : 0.f;
+    }
 };
 
 // The passes of the lane's rows: for each, the chunk on the lane's device, its summary into
@@ -1245,7 +1262,10 @@ static int stream_passes(kmp_ctx* c, const kmp_pair_opts& o, const int* ks, uint
         kv[j]->k = ks[j];
         if (!kv[j]->ws) KMP_TRY(c, kmp_postings_create(&kv[j]->ws));
         KMP_TRY(c, kmp_postings_set_reuse(kv[j]->ws, 1));
+        KMP_TRY(c, kmp_postings_set_timing(kv[j]->ws, 1));  // stage times of the summary
     }
+    EventPair dev;
+    if (!dev.ready()) return fail(c, KMP_EDEVICE, "events");
     const bool blosum = o.score == KMP_SCORE_BLOSUM;
     const uint64_t slots = kmp_set_capacity(c->n, c->total_res);
     PassPlan plan{c->n, (double)pass_budget(c)};
@@ -1285,6 +1305,7 @@ static int stream_passes(kmp_ctx* c, const kmp_pair_opts& o, const int* ks, uint
                                               ln.ew->as<uint32_t>(), ln.mscore->as<uint32_t>(), ln.mwk->as<uint32_t>(),
                                               ln.mwk->as<uint32_t>() + mcap, mcap, &total, &pst, st);
                 inc = pst.incidences;
+                for (int i = 0; i < 3; ++i) ln.stage_ms[i] += std::max(0.f, pst.stage_ms[i]);
                 if (rc == KMP_EOVERFLOW) {
                     mcap = total + total / 8 + 1024;
                     rc = KMP_OK;
@@ -1315,6 +1336,11 @@ static int stream_passes(kmp_ctx* c, const kmp_pair_opts& o, const int* ks, uint
                            &ln.L);
             if (rc != KMP_OK) break;
             inc += pst.incidences;
+            // stages 0-2 (keys, level 2, buckets + heavy) expand; 3-5 (partition, reduce, emit) reduce
+            ln.stage_ms[j ? 1 : 0] += std::max(0.f, pst.stage_ms[0]) + std::max(0.f, pst.stage_ms[1]) +
+                                      std::max(0.f, pst.stage_ms[2]);
+            ln.stage_ms[2] += std::max(0.f, pst.stage_ms[3]) + std::max(0.f, pst.stage_ms[4]) +
+                              std::max(0.f, pst.stage_ms[5]);
             in.p[j] = s.ep.as<uint32_t>();
             in.q[j] = s.eq.as<uint32_t>();
             in.w[j] = s.ew.as<uint32_t>();
@@ -1389,7 +1415,8 @@ static int stream_passes(kmp_ctx* c, const kmp_pair_opts& o, const int* ks, uint
         di.row_hi = b;
         di.cls = o.require_class_diff ? nullptr : ln.L.cls;
         di.align_threshold = o.align_threshold;
-        if (kmp::edge_digest_enqueue(di, ln.acc, st) != hipSuccess) {
+        if (hipEventRecord(dev.a, st) != hipSuccess || kmp::edge_digest_enqueue(di, ln.acc, st) != hipSuccess ||
+            hipEventRecord(dev.b, st) != hipSuccess) {
             rc = fail(c, KMP_EDEVICE, "edge digest");
             break;
         }
@@ -1397,11 +1424,15 @@ static int stream_passes(kmp_ctx* c, const kmp_pair_opts& o, const int* ks, uint
             rc = fail(c, KMP_EDEVICE, "stream synchronise");
             break;
         }
+        ln.stage_ms[3] += dev.ms();
         ++ln.passes;
         rc = on_chunk(ch);
         a = b;
     }
-    for (uint32_t j = 0; j < nk; ++j) (void)kmp_postings_set_reuse(kv[j]->ws, 0);
+    for (uint32_t j = 0; j < nk; ++j) {
+        (void)kmp_postings_set_reuse(kv[j]->ws, 0);
+        (void)kmp_postings_set_timing(kv[j]->ws, 0);
+    }
     return rc;
 }
 
@@ -1445,6 +1476,7 @@ static int finish_summary(kmp_ctx* c, const kmp_pair_opts& o, const std::vector<
         sm.sum_w_diff += h.tot[3];
         sm.incidences += ln->incidences;
         sm.passes += ln->passes;
+        for (int i = 0; i < 4; ++i) sm.stage_ms[i] += ln->stage_ms[i];
         bad |= h.bad != 0;
     }
     KMP_TRY(c, use_device(c));

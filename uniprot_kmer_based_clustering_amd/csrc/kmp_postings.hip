@@ -2416,7 +2416,8 @@ struct kmp_postings {
     CurGeom cg{};
     // heavy path (frequent k-mers): spill regions, the gathered + sorted spill, its elements,
     // k-mer starts, per-k-mer row bounds / tile counts / tile offsets
-    Grow<unsigned long long> spill, hkeys, hsorted, hGS, htc, htoff, hoff, hRH, hseg;
+    Grow<unsigned long long> spill, hkeys, hsorted, hGS, htc, htoff, hoff, hRH, hseg, hcur;
+    bool hcur_valid = false;  // hcur holds the current front's spill cursors
     Grow<uint32_t> hE, hgi, hcnt, hrun, hblk, hGH;  // hGH: each heavy k-mer's h
     uint64_t spill_cap = 0;     // keys per spill shard region
     bool heavy = false;         // this workspace's batches spill: run the split step
@@ -2451,17 +2452,20 @@ struct kmp_postings {
     // read-back of a step (kRb* layout), written by the pack kernel into coherent pinned memory
     unsigned long long* hrb = nullptr;
     hipEvent_t ev[KMP_POSTINGS_STAGES + 1] = {};
+    hipEvent_t mev[4] = {};  // kmp_dev_pairs_rows_multi: start, first k expanded, second k, tail done
     const uint32_t* pt_zero_p = nullptr;  // the pt allocation whose totals T were cleared
     size_t pt_zero_n = 0;
     ~kmp_postings() {
         for (auto* g : {&keys, &sorted, &inc, &inc_sorted, &uniq, &bstats, &btot, &boff, &spill, &hkeys, &hsorted,
-                        &hGS, &htc, &htoff, &hoff, &hRH, &hseg, &ovk, &ovx, &split_cur})
+                        &hGS, &htc, &htoff, &hoff, &hRH, &hseg, &hcur, &ovk, &ovx, &split_cur})
             g->release();
         for (auto* g : {&w, &keep, &pos, &small, &cnt, &flags, &chunk_first, &bp, &pt, &ovf, &ovr, &ova, &stg2, &hE, &hgi, &hcnt,
                         &hrun, &hblk, &cur, &hGH})
             g->release();
         tmp.release();
         for (auto& e : ev)
+            if (e) (void)hipEventDestroy(e);
+        for (auto& e : mev)
             if (e) (void)hipEventDestroy(e);
         if (hrb) (void)hipHostFree(hrb);
         if (gexec) (void)hipGraphExecDestroy(gexec);
@@ -2473,10 +2477,15 @@ struct kmp_postings {
     }
 };
 
-#define PG(x)                                                                   \
-    do {                                                                        \
-        hipError_t e_ = (x);                                                    \
-        if (e_ != hipSuccess) return e_ == hipErrorOutOfMemory ? KMP_ENOMEM : KMP_EDEVICE; \
+#define PG(x)                                                                                         \
+    do {                                                                                              \
+        hipError_t e_ = (x);                                                                          \
+        if (e_ != hipSuccess) {                                                                       \
+            if (getenv("KMP_DEBUG"))                                                                  \
+                fprintf(stderr, "kmp: %s failed: %s (kmp_postings.hip:%d)\n", #x, hipGetErrorString(e_), \
+                        __LINE__);                                                                    \
+            return e_ == hipErrorOutOfMemory ? KMP_ENOMEM : KMP_EDEVICE;                              \
+        }                                                                                             \
     } while (0)
 
 namespace {
@@ -3504,8 +3513,11 @@ bool pt_geometry(const kmp_postings* ws, const StepCfg& c, uint64_t inc, PtGeom*
     unsigned rb = 0;
     while (rb < 16 && (double)(1u << rb) * 1.41421356 < want) ++rb;
     rb = std::min(rb, ws->pt_rb_max);  // learned from overflowing blocks
+    // the key and one padding bit in a u32 (sparse rows would otherwise ask for wider blocks)
+    if (g->pbits + g->sbits > 31) return false;
+    rb = std::min(rb, 31 - g->pbits - g->sbits);
     while (rb < 31 && ((rows + (1ull << rb) - 1) >> rb) > kPtMaxBlocks) ++rb;
-    if (g->pbits + g->sbits + rb > 31) return false;  // the key and one padding bit in a u32
+    if (g->pbits + g->sbits + rb > 31) return false;  // too many rows for one call (kmp_dev_rows_max)
     g->rbits = rb;
     g->nrb = std::max(1u, (uint32_t)((rows + (1ull << rb) - 1) >> rb));
     g->sc = ws->shard_cap;
@@ -3826,7 +3838,15 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
     ho.cb = lay.clsbits;
     ho.hshift = lay.hshift;
     ho.pbits = lay.hshift - lay.clsbits;
-    ho.cls = c.require_diff && lay.clsbits > 0;
+    // class order skips same-class pairs without testing them, but puts the rows of a range
+    // anywhere in a k-mer's elements: a ranged call (a pass or a rank's rows) would walk every
+    // pair of every frequent k-mer on every pass.  Plain order keeps a range's rows contiguous, so
+    // a pass enumerates only its own rows' pairs (testing the class per pair).
+    ho.cls = c.require_diff && lay.clsbits > 0 && !c.ranged;
+    if (ws->heavy_ready && ws->h_cls != ho.cls) {  // the kept spill, compacted again in this order
+        ws->heavy_ready = false;
+        m = ws->h_m;
+    }
     // tiles whose every pair is written (no per-pair test) are cut finer: one workgroup's write
     // stream is the bound of a tile, and a 256 x 2,048 block of pairs left one CU writing 4 MB
     ho.hj = (ho.cls ? !c.ranged : !c.require_diff) ? kHvJWrite : kHvJ;
@@ -3843,7 +3863,15 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
             PG(ws->hrun.reserve(m + 1));
             PG(ws->hRH.reserve(m + 1));
         }
-        const unsigned long long* spill_cursor = ws->bstats.p + kRbSpill;
+        // the spill's region fill levels: this front's cursors, kept aside so that a reused front
+        // (its cursors cleared by the next call) can be compacted again in the other order
+        PG(ws->hcur.reserve(kShards));
+        if (!ws->hcur_valid) {
+            PG(hipMemcpyAsync(ws->hcur.p, ws->bstats.p + kRbSpill, kShards * sizeof(unsigned long long),
+                              hipMemcpyDeviceToDevice, st));
+            ws->hcur_valid = true;
+        }
+        const unsigned long long* spill_cursor = ws->hcur.p;
         if (ws->h_segs && ws->h_segs <= seg_capacity(ws) && ws->h_segmax <= kSegLarge) {
             const uint32_t ns = (uint32_t)ws->h_segs;
             heavy_segsort_bitonic_kernel<kSegSmall, 256><<<ns, 256, 0, st>>>(
@@ -3892,7 +3920,7 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
         ws->h_cls = ho.cls;
         ws->h_tot = tot;
     }
-    if (ws->h_cls != ho.cls) return KMP_EINVAL;  // one front, one class mode
+    if (ws->h_cls != ho.cls) return KMP_EINVAL;  // (compacted above in this call's order)
     const uint64_t ngb = ws->h_m;  // bound on the k-mer count (device: h_tot[1])
     if (ngb == 0) return KMP_OK;
     PG(ws->hgi.reserve(2 * (ngb + 1)));
@@ -4073,7 +4101,7 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
         const unsigned long long* rb = ws->hrb;
         unsigned long long acc[kStN], most, n_inc, spill_most, spill_total;
         const bool split = ws->heavy || reuse || c.expand_only;
-        if (!reuse) ws->heavy_ready = false;  // a recomputed front: no compacted spill yet
+        if (!reuse) ws->heavy_ready = ws->hcur_valid = false;  // a recomputed front: no compacted spill yet
         if (!split) {
             key.push_back(ws->shard_cap);
             key.push_back(ws->spill_cap);
@@ -4126,9 +4154,11 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
         }
         if (split) {
             if (spill_total || ws->heavy_ready) {
-                ws->h_segs = rb[kRbSegs];
-                ws->h_segmax = rb[kRbSegMax];
-                int rc = heavy_phase(ws, c, spill_total, true, st);
+                if (spill_total) {  // a new spill (a reused front spills nothing: keep its segments)
+                    ws->h_segs = rb[kRbSegs];
+                    ws->h_segmax = rb[kRbSegMax];
+                }
+                int rc = heavy_phase(ws, c, spill_total ? spill_total : ws->h_m, true, st);
                 if (rc != KMP_OK) return rc;
             }
             ws->mark(3, st);
@@ -4336,6 +4366,7 @@ void finish_timing(kmp_postings* ws, kmp_postings_stats* stats, hipStream_t st) 
         float ms = 0.f;
         stats->stage_ms[s] = hipEventElapsedTime(&ms, ws->ev[s], ws->ev[s + 1]) == hipSuccess ? ms : -1.f;
     }
+    (void)hipGetLastError();  // a stage the call did not run (never recorded) must not poison the next launch check
 }
 
 int postings_args(kmp_postings* ws, int k, uint64_t* n_edges, kmp_postings_stats* stats, uint32_t* d_p,
@@ -4725,6 +4756,10 @@ int kmp_dev_pairs_rows_multi(kmp_postings* const* ws, const int* ks, uint32_t nk
     const bool ranged = !(row_lo == 0 && row_hi == n);
     uint64_t inc[2] = {0, 0};
     kmp_postings_stats s0{};
+    const bool timed = stats != nullptr;  // stage_ms: [0] first k expanded, [1] second k, [2] the fused tail
+    if (timed && !ws[0]->mev[0])
+        for (auto& e : ws[0]->mev) PG(hipEventCreate(&e));
+    if (timed) PG(hipEventRecord(ws[0]->mev[0], st));
     for (uint32_t j = 0; j < nk; ++j) {
         // expand only: every incidence keyed (pair << 8) | j << 7 | s(x)
         uint64_t unused = 0;
@@ -4732,6 +4767,7 @@ int kmp_dev_pairs_rows_multi(kmp_postings* const* ws, const int* ks, uint32_t nk
                                ranged, row_lo, row_hi, d_p, d_q, d_w, cap, &unused, j == 0 ? &s0 : nullptr, stream,
                                kScoreBits + 1, j << kScoreBits, d_score, d_w1, &inc[j]);
         if (rc != KMP_OK) return rc;
+        if (timed) PG(hipEventRecord(ws[0]->mev[1 + j], st));
     }
     // the tail's geometry and outputs (the same StepCfg fields the step uses)
     StepCfg c{};
@@ -4750,6 +4786,16 @@ int kmp_dev_pairs_rows_multi(kmp_postings* const* ws, const int* ks, uint32_t nk
     c.d_w1 = d_w1;
     c.d_w0 = d_w0;
     int rc = tail_multi(ws, nk, c, inc, n_edges, stats, st);
+    if (timed && (rc == KMP_OK || rc == KMP_EOVERFLOW)) {
+        PG(hipEventRecord(ws[0]->mev[3], st));
+        PG(hipEventSynchronize(ws[0]->mev[3]));
+        for (int i = 0; i < 3; ++i) {
+            float ms = 0.f;
+            stats->stage_ms[i] = hipEventElapsedTime(&ms, ws[0]->mev[i], ws[0]->mev[i + 1]) == hipSuccess ? ms : -1.f;
+        }
+        (void)hipGetLastError();
+        for (int i = 3; i < KMP_POSTINGS_STAGES; ++i) stats->stage_ms[i] = 0.f;
+    }
     if (stats) {  // the first k's front statistics
         stats->sum_S = s0.sum_S;
         stats->distinct = s0.distinct;
