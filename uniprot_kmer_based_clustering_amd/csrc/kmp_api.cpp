@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -733,14 +734,15 @@ struct PassPlan {
 
 constexpr uint64_t kPassSlots = 1ull << 26;  // batches above ~67M windows run in passes by default
 
-uint64_t pass_budget(kmp_ctx* c) {
+uint64_t pass_budget(kmp_ctx* c, bool fused = false) {
     if (c->pass_keys) return c->pass_keys;
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 16ull << 30;
-    // ~96 B of device memory per pair key of a pass: shard regions (8), row-block keys (8),
-    // staged runs (12), and when every row block overflows (dense rows) the tagged-key sort (48)
-    // and its run arrays (12), with slack
-    return std::max<uint64_t>(1u << 20, std::min<uint64_t>(fr / 2 / 96, 3ull << 30));
+    // device memory per pair key of a pass: ~96 B when dense row blocks take the tagged-key sort
+    // (shard regions 8, row-block keys 8, staged runs 12, the sort's keys 48 and run arrays 12,
+    // slack); ~64 B in the fused tail, whose dense blocks are cut into LDS sub-blocks (shard regions
+    // with slack 10, row-block and sub-block keys 12, staged runs 20, the pass's edges 15, slack)
+    return std::max<uint64_t>(1u << 20, std::min<uint64_t>(fr / 2 / (fused ? 80 : 96), 3ull << 30));
 }
 
 // the batch and stream a pass runs on: the context's (nullptr) or a rank's copy
@@ -820,6 +822,22 @@ int pass_pairs(kmp_ctx* c, const kmp_pair_opts& o, uint64_t* count, bool scored)
         rc = rows_into(c, c->postings, c->k_sets, o, a, b, c->ep, c->eq, c->ew, c->edge_cap, off, &ne, &st,
                        scored ? &c->escore : nullptr);
         plan.seen(a, b, st.incidences);
+        if (rc == KMP_OK && getenv("KMP_DEBUG_PASSES")) {  // each pass's edges: rows in [a, b), p < q
+            std::vector<uint32_t> hp(ne), hq(ne);
+            (void)hipMemcpy(hp.data(), c->ep.as<uint32_t>() + off, ne * 4, hipMemcpyDeviceToHost);
+            (void)hipMemcpy(hq.data(), c->eq.as<uint32_t>() + off, ne * 4, hipMemcpyDeviceToHost);
+            uint64_t bad = 0, first = ~0ull;
+            for (uint64_t i = 0; i < ne; ++i)
+                if (hp[i] < a || hp[i] >= b || hp[i] >= hq[i] || (i && hp[i] < hp[i - 1])) {
+                    if (!bad++) first = i;
+                }
+            fprintf(stderr, "kmp: pass %u rows [%u, %u) edges %llu at %llu, incidences %llu, bad %llu first %lld\n",
+                    passes, a, b, (unsigned long long)ne, (unsigned long long)off,
+                    (unsigned long long)st.incidences, (unsigned long long)bad, (long long)first);
+            if (bad)
+                for (uint64_t i = first > 3 ? first - 3 : 0; i < std::min<uint64_t>(ne, first + 4); ++i)
+                    fprintf(stderr, "kmp:   %llu: (%u, %u)\n", (unsigned long long)i, hp[i], hq[i]);
+        }
         off += ne;
         a = b;
         ++passes;
@@ -879,7 +897,8 @@ static int split_rank_edges(kmp_ctx* c, const kmp_pair_opts& o, const std::vecto
             kmp_rank& r = *c->ranks[g];
             uint32_t h[KMP_SPLIT_FLAGS];
             KMP_HIP(c, hipSetDevice(r.device));
-            KMP_HIP(c, hipMemcpy(h, r.sflags.p, sizeof h, hipMemcpyDeviceToHost));
+            KMP_HIP(c, hipMemcpyAsync(h, r.sflags.p, sizeof h, hipMemcpyDeviceToHost, r.stream));
+            KMP_HIP(c, hipStreamSynchronize(r.stream));
             for (int i = 0; i < KMP_SPLIT_FLAGS; ++i) fl[i] = std::max(fl[i], h[i]);
         }
         if (fl[KMP_SPLIT_CLASS] || fl[KMP_SPLIT_HEAVY]) return kSplitFallback;
@@ -1268,7 +1287,7 @@ static int stream_passes(kmp_ctx* c, const kmp_pair_opts& o, const int* ks, uint
     if (!dev.ready()) return fail(c, KMP_EDEVICE, "events");
     const bool blosum = o.score == KMP_SCORE_BLOSUM;
     const uint64_t slots = kmp_set_capacity(c->n, c->total_res);
-    PassPlan plan{c->n, (double)pass_budget(c)};
+    PassPlan plan{c->n, (double)pass_budget(c, nk == 2)};
     plan.end = ln.row_hi;
     const bool fused = nk == 2;  // both k reduced together (kmp_dev_pairs_rows_multi): no merge
     if (fused) plan.max_rows = kmp_dev_rows_max(c->n, 2);
@@ -1277,6 +1296,8 @@ static int stream_passes(kmp_ctx* c, const kmp_pair_opts& o, const int* ks, uint
         plan.density = 0;  // small batch: one pass
     const hipStream_t st = ln.L.stream;
     uint64_t mcap = 0;
+    double edge_ratio = 1.0;  // the largest edges / incidences of a pass so far (after the first)
+    bool ratio_seen = false;
     int rc = KMP_OK;
     for (uint32_t a = ln.row_lo; a < ln.row_hi && rc == KMP_OK;) {
         const uint32_t b = plan.density == 0 ? ln.row_hi : plan.next(a);
@@ -1287,10 +1308,10 @@ static int stream_passes(kmp_ctx* c, const kmp_pair_opts& o, const int* ks, uint
         if (fused) {
             // p q w (ln.ep/eq/ew), score (ln.mscore), w0 | w1 (ln.mwk), grown on overflow
             kmp_postings* wsp[2] = {kv[0]->ws, kv[1]->ws};
-            // edges <= incidences: size the arrays from the densest incidence rate seen (no rerun
-            // of the pass's expansion when the estimate holds)
-            const double est = plan.density > 0 ? plan.density * plan.mass(a, b) : 0.0;
-            if (est * 1.02 + 4096 > (double)mcap) mcap = (uint64_t)(est * 1.02) + 4096;
+            // edges <= incidences: size the arrays from the densest incidence rate seen times the
+            // largest edges-per-incidence ratio seen (+10 %; an overflow reruns the pass)
+            const double est = plan.density > 0 ? plan.density * plan.mass(a, b) * std::min(1.0, edge_ratio * 1.1) : 0.0;
+            if (est + 4096 > (double)mcap) mcap = (uint64_t)est + 4096;
             for (int attempt = 0; attempt < 3; ++attempt) {
                 if (!mcap || !ln.mwk->p) mcap = std::max<uint64_t>(mcap, 1u << 20);
                 uint64_t cap3 = 0;
@@ -1304,7 +1325,7 @@ static int stream_passes(kmp_ctx* c, const kmp_pair_opts& o, const int* ks, uint
                                               o.require_class_diff, a, b, ln.ep->as<uint32_t>(), ln.eq->as<uint32_t>(),
                                               ln.ew->as<uint32_t>(), ln.mscore->as<uint32_t>(), ln.mwk->as<uint32_t>(),
                                               ln.mwk->as<uint32_t>() + mcap, mcap, &total, &pst, st);
-                inc = pst.incidences;
+                if (pst.incidences) inc = pst.incidences;  // (a re-emit after an overflow expands nothing)
                 for (int i = 0; i < 3; ++i) ln.stage_ms[i] += std::max(0.f, pst.stage_ms[i]);
                 if (rc == KMP_EOVERFLOW) {
                     mcap = total + total / 8 + 1024;
@@ -1351,6 +1372,11 @@ static int stream_passes(kmp_ctx* c, const kmp_pair_opts& o, const int* ks, uint
         if (rc != KMP_OK) break;
         in.off[nk] = total;
         if (plan.density != 0) plan.seen(a, b, inc);
+        if (inc) {
+            const double ratio = (double)total / (double)inc;
+            edge_ratio = ratio_seen ? std::max(edge_ratio, ratio) : ratio;
+            ratio_seen = true;
+        }
         ln.incidences += inc;
         ch.rank = ln.rank;
         ch.device = ln.device;
@@ -1425,6 +1451,12 @@ static int stream_passes(kmp_ctx* c, const kmp_pair_opts& o, const int* ks, uint
             break;
         }
         ln.stage_ms[3] += dev.ms();
+        if (getenv("KMP_DEBUG")) {
+            size_t fr = 0, tot = 0;
+            (void)hipMemGetInfo(&fr, &tot);
+            fprintf(stderr, "kmp: rank %u pass %u rows [%u, %u): %llu incidences, %llu edges, free %.1f GB\n", ln.rank,
+                    ln.passes, a, b, (unsigned long long)inc, (unsigned long long)ch.n, fr / 1e9);
+        }
         ++ln.passes;
         rc = on_chunk(ch);
         a = b;

@@ -2360,8 +2360,12 @@ struct Grow {
         if (p) (void)hipFree(p);
         p = nullptr;
         n = 0;
-        hipError_t e = hipMalloc(&p, std::max<size_t>(1, m) * sizeof(T));
-        if (e == hipSuccess) n = std::max<size_t>(1, m);
+        // a large buffer grows with a quarter of headroom: the passes of a stream vary in size, and
+        // every regrowth of a multi-GB buffer (a synchronous free + a fresh allocation) stalled the
+        // device for up to seconds
+        const size_t want = m > (size_t{1} << 26) ? m + m / 4 : std::max<size_t>(1, m);
+        hipError_t e = hipMalloc(&p, want * sizeof(T));
+        if (e == hipSuccess) n = want;
         return e;
     }
     void release() {
@@ -2393,8 +2397,14 @@ struct kmp_postings {
     Grow<uint32_t> ovr;            // run lengths, kept flags and positions, first run per block
     Grow<uint32_t> ova;            // scored: per run (w, w1, score)
     Grow<uint32_t> stg2;           // scored tail: staged scores | second-k weights
+    Grow<uint32_t> k2, dsc;        // fused tail's sub-blocks: keys by sub-block | descriptors, counts, offsets
     uint64_t pt_inc = 0;        // incidences of the last call (row-block sizing)
     uint64_t last_most = 0;     // expand-only call: the fullest shard region (sizes the next call's)
+    // tail_multi's staged result, kept for a re-emit into larger arrays: sub-blocks, staging
+    // capacity, edges, and the call it belongs to (rows, ks, n)
+    uint32_t pend_nd = 0;
+    uint64_t pend_total = 0, pend_ne = 0;
+    std::vector<unsigned long long> pend_key;
     Grow<unsigned long long> split_cur;  // k-mer split: per-destination send cursors
     std::vector<unsigned long long> split_shape;
     unsigned pt_rb_max = 16;    // rows-per-block bound learned from overflowing row blocks
@@ -2459,7 +2469,7 @@ struct kmp_postings {
         for (auto* g : {&keys, &sorted, &inc, &inc_sorted, &uniq, &bstats, &btot, &boff, &spill, &hkeys, &hsorted,
                         &hGS, &htc, &htoff, &hoff, &hRH, &hseg, &hcur, &ovk, &ovx, &split_cur})
             g->release();
-        for (auto* g : {&w, &keep, &pos, &small, &cnt, &flags, &chunk_first, &bp, &pt, &ovf, &ovr, &ova, &stg2, &hE, &hgi, &hcnt,
+        for (auto* g : {&w, &keep, &pos, &small, &cnt, &flags, &chunk_first, &bp, &pt, &ovf, &ovr, &ova, &stg2, &k2, &dsc, &hE, &hgi, &hcnt,
                         &hrun, &hblk, &cur, &hGH})
             g->release();
         tmp.release();
@@ -2725,6 +2735,25 @@ struct PtGeom {
     uint64_t flat_n;        // nonzero: one region of flat_n keys with kNoKey padding (no cursors)
     uint32_t min_shared;    // runs with w < min_shared are dropped
 };
+
+// The blocks a reduce runs over: row blocks (size == nullptr: block r is keys [start[r], start[r+1])
+// of row block r) or sub-blocks (block d is keys [start[d], start[d] + size[d]) of row block row[d]:
+// a row block above kPtCap cut by pt_split).
+struct BlkSrc {
+    const uint32_t* start;
+    const uint32_t* size;
+    const uint32_t* row;
+};
+__device__ __forceinline__ void blk_of(const BlkSrc& b, uint32_t i, uint32_t& s0, uint32_t& n, uint32_t& r) {
+    s0 = b.start[i];
+    if (b.size) {
+        n = b.size[i];
+        r = b.row[i];
+    } else {
+        n = b.start[i + 1] - s0;
+        r = i;
+    }
+}
 
 __device__ __forceinline__ uint32_t pt_tile_keys(const unsigned long long* __restrict__ cursor, const PtGeom& g,
                                                  uint32_t s, uint32_t j, uint32_t& t0) {
@@ -3010,8 +3039,9 @@ struct PtScoredLds {
 template <uint32_t kE, bool kKbit>
 __device__ __forceinline__ void pt_reduce_scored_block(PtScoredLds<kKbit>& u, typename PtSort<kE>::storage_type& st,
                                                        uint32_t* last, uint32_t* wave_tot,
-                                                       const uint32_t* __restrict__ keys, uint32_t r, uint32_t s0,
-                                                       uint32_t n, const PtGeom& g, uint32_t* __restrict__ stage_p,
+                                                       const uint32_t* __restrict__ keys, uint32_t r, uint32_t d,
+                                                       uint32_t s0, uint32_t n, const PtGeom& g,
+                                                       uint32_t* __restrict__ stage_p,
                                                        uint32_t* __restrict__ stage_q, uint32_t* __restrict__ stage_w,
                                                        uint32_t* __restrict__ stage_s, uint32_t* __restrict__ stage_w1,
                                                        uint32_t* __restrict__ counts) {
@@ -3067,7 +3097,7 @@ __device__ __forceinline__ void pt_reduce_scored_block(PtScoredLds<kKbit>& u, ty
         u.r.hs[nruns] = n;
         u.r.ps[nruns] = stot;
         if (kKbit) u.r.pk[nruns] = ktot;
-        if (!filter) counts[r] = nruns;
+        if (!filter) counts[d] = nruns;
     }
     __syncthreads();
     if (!filter) {
@@ -3106,12 +3136,12 @@ __device__ __forceinline__ void pt_reduce_scored_block(PtScoredLds<kKbit>& u, ty
             if (kKbit) stage_w1[s0 + o] = w1v[e];
             ++o;
         }
-    if (threadIdx.x == 0) counts[r] = total;
+    if (threadIdx.x == 0) counts[d] = total;
 }
 
 template <bool kKbit>
 __global__ __launch_bounds__(kPtRThreads) void pt_reduce_scored_kernel(const uint32_t* __restrict__ keys,
-                                                                       const uint32_t* __restrict__ bst, PtGeom g,
+                                                                       BlkSrc bs, PtGeom g,
                                                                        uint32_t* __restrict__ flags,
                                                                        uint32_t* __restrict__ ovf,
                                                                        uint32_t* __restrict__ stage_p,
@@ -3123,16 +3153,18 @@ __global__ __launch_bounds__(kPtRThreads) void pt_reduce_scored_kernel(const uin
     __shared__ PtScoredLds<kKbit> u;
     __shared__ uint32_t last[kPtRThreads];
     __shared__ uint32_t wave_tot[kPtRThreads / 64];
-    const uint32_t r = blockIdx.x, s0 = bst[r], n = bst[r + 1] - s0;
+    const uint32_t d = blockIdx.x;
+    uint32_t s0, n, r;
+    blk_of(bs, d, s0, n, r);
     if (n == 0 || n > kPtCap) {
         if (threadIdx.x == 0) {
-            counts[r] = 0;
-            if (n) ovf[atomicAdd(&flags[3], 1u)] = r;
+            counts[d] = 0;
+            if (n) ovf[atomicAdd(&flags[3], 1u)] = d;
         }
         return;
     }
 #define PT_SCORED(E, S) \
-    pt_reduce_scored_block<E, kKbit>(u, u.S, last, wave_tot, keys, r, s0, n, g, stage_p, stage_q, stage_w, stage_s, \
+    pt_reduce_scored_block<E, kKbit>(u, u.S, last, wave_tot, keys, r, d, s0, n, g, stage_p, stage_q, stage_w, stage_s, \
                                      stage_w1, counts)
     if (n <= 2 * kPtRThreads) PT_SCORED(2, s2);
     else if (n <= 4 * kPtRThreads) PT_SCORED(4, s4);
@@ -3147,20 +3179,25 @@ __global__ __launch_bounds__(kPtRThreads) void pt_reduce_scored_kernel(const uin
 // its block's offset.  Every step is multi-workgroup, so one very long row (real data at k = 5:
 // a protein sharing 5-mers with thousands of later ones) costs a sort of its keys, not one
 // workgroup walking them.
-__global__ void pt_ovf_sizes_kernel(const uint32_t* __restrict__ ovf, uint32_t m, const uint32_t* __restrict__ bst,
+__global__ void pt_ovf_sizes_kernel(const uint32_t* __restrict__ ovf, uint32_t m, BlkSrc bs,
                                     unsigned long long* __restrict__ sz) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j < m) sz[j] = bst[ovf[j] + 1] - bst[ovf[j]];
+    if (j < m) {
+        uint32_t s0, n, r;
+        blk_of(bs, ovf[j], s0, n, r);
+        sz[j] = n;
+    }
     if (j == m) sz[m] = 0;
 }
 
 // one workgroup per listed block: its keys, tagged, at xoff[j]
-__global__ __launch_bounds__(256) void pt_ovf_gather_kernel(const uint32_t* __restrict__ ovf,
-                                                            const uint32_t* __restrict__ bst,
+__global__ __launch_bounds__(256) void pt_ovf_gather_kernel(const uint32_t* __restrict__ ovf, BlkSrc bs,
                                                             const unsigned long long* __restrict__ xoff,
                                                             const uint32_t* __restrict__ keys, unsigned kb,
                                                             unsigned long long* __restrict__ x) {
-    const uint32_t j = blockIdx.y, r = ovf[j], s0 = bst[r], n = bst[r + 1] - s0;
+    const uint32_t j = blockIdx.y;
+    uint32_t s0, n, r;
+    blk_of(bs, ovf[j], s0, n, r);
     const unsigned long long tag = (unsigned long long)j << kb, o = xoff[j];
     for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) x[o + i] = tag | keys[s0 + i];
 }
@@ -3240,8 +3277,7 @@ __global__ void pt_ovf_keep_scored_kernel(const unsigned long long* __restrict__
     }
 }
 
-__global__ void pt_ovf_stage_scored_kernel(const uint32_t* __restrict__ ovf, uint32_t m,
-                                           const uint32_t* __restrict__ bst, PtGeom g,
+__global__ void pt_ovf_stage_scored_kernel(const uint32_t* __restrict__ ovf, uint32_t m, BlkSrc bs, PtGeom g,
                                            const unsigned long long* __restrict__ uniq,
                                            const RunAgg* __restrict__ agg, const uint32_t* __restrict__ nruns,
                                            const uint32_t* __restrict__ keep, const uint32_t* __restrict__ kpos,
@@ -3254,18 +3290,73 @@ __global__ void pt_ovf_stage_scored_kernel(const uint32_t* __restrict__ ovf, uin
     const uint32_t qm = (1u << g.pbits) - 1;
     for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < U; u += gridDim.x * blockDim.x) {
         const unsigned long long x = uniq[u];
-        const uint32_t j = (uint32_t)(x >> kb), r = ovf[j];
+        const uint32_t j = (uint32_t)(x >> kb), d = ovf[j];
+        uint32_t s0, n, r;
+        blk_of(bs, d, s0, n, r);
         const uint32_t f = first[j];
         const uint32_t nxt = j + 1 < m ? first[j + 1] : U;
-        if (u == f) counts[r] = kpos[nxt] - kpos[f];
+        if (u == f) counts[d] = kpos[nxt] - kpos[f];
         if (!keep[u]) continue;
         const RunAgg a = agg[u];
-        const uint32_t key = (uint32_t)x & ((1u << kb) - 1), o = bst[r] + kpos[u] - kpos[f];
+        const uint32_t key = (uint32_t)x & ((1u << kb) - 1), o = s0 + kpos[u] - kpos[f];
         stage_p[o] = g.row0 + (r << g.rbits) + (key >> g.pbits);
         stage_q[o] = key & qm;
         stage_w[o] = a.w;
         stage_s[o] = a.s;
         if (g.kbit) stage_w1[o] = a.w1;
+    }
+}
+
+// Sub-blocks (the fused multi-k tail): a row block above kPtCap keys — config 5 at k = 5, where one
+// protein pairs with ~10^5 later ones — is cut by the top bits of its local key (row in block, then
+// q) into nsub = 2^j sub-blocks of about kPtCap / 2 keys, each reduced in LDS like a row block, so
+// no device-wide sort of the pass's keys is needed.  One 1,024-thread workgroup per row block: count
+// the sub-block of every key in LDS, scan, write the sub-block descriptors, then scatter the keys
+// (an LDS cursor per sub-block) into keys2 at the same block offset.  A block that fits is one
+// sub-block (copied).  A sub-block still above kPtCap (a skewed q range) takes the overflow sort.
+constexpr uint32_t kSbThreads = 1024, kSbMaxLog = 12;
+__host__ __device__ inline unsigned pt_sub_log(uint32_t n, unsigned kbits) {
+    unsigned j = 0;
+    while (j < kSbMaxLog && j < kbits && ((uint64_t)(kPtCap / 2) << j) < n) ++j;
+    return n > kPtCap ? j : 0u;
+}
+
+__global__ __launch_bounds__(kSbThreads) void pt_split_kernel(const uint32_t* __restrict__ keys,
+                                                              const uint32_t* __restrict__ bst,
+                                                              const uint32_t* __restrict__ dbase, unsigned kbits,
+                                                              uint32_t* __restrict__ keys2,
+                                                              uint32_t* __restrict__ dstart,
+                                                              uint32_t* __restrict__ dsize,
+                                                              uint32_t* __restrict__ drow) {
+    __shared__ uint32_t cnt[1u << kSbMaxLog];
+    __shared__ uint32_t wave_tot[kSbThreads / 64];
+    const uint32_t r = blockIdx.x, s0 = bst[r], n = bst[r + 1] - s0;
+    const unsigned lj = pt_sub_log(n, kbits);
+    const uint32_t ns = 1u << lj, d0 = dbase[r];
+    const unsigned sh = kbits - lj;
+    if (lj == 0) {  // fits: one sub-block (the keys copied, so every sub-block reads keys2)
+        for (uint32_t i = threadIdx.x; i < n; i += kSbThreads) keys2[s0 + i] = keys[s0 + i];
+        if (threadIdx.x == 0) {
+            dstart[d0] = s0;
+            dsize[d0] = n;
+            drow[d0] = r;
+        }
+        return;
+    }
+    for (uint32_t i = threadIdx.x; i < ns; i += kSbThreads) cnt[i] = 0;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += kSbThreads) atomicAdd(&cnt[keys[s0 + i] >> sh], 1u);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < ns; i += kSbThreads) {  // descriptors (before the scan rewrites cnt)
+        dsize[d0 + i] = cnt[i];
+        drow[d0 + i] = r;
+    }
+    lds_bins_scan<kSbThreads>(cnt, ns, wave_tot);  // cnt[i] = first key of sub-block i
+    for (uint32_t i = threadIdx.x; i < ns; i += kSbThreads) dstart[d0 + i] = s0 + cnt[i];
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += kSbThreads) {
+        const uint32_t k = keys[s0 + i];
+        keys2[s0 + atomicAdd(&cnt[k >> sh], 1u)] = k;
     }
 }
 
@@ -3533,14 +3624,16 @@ bool pt_geometry(const kmp_postings* ws, const StepCfg& c, uint64_t inc, PtGeom*
 struct PtBufs {
     uint32_t *T, *cur, *bst, *counts, *eoff;  // row-block totals | scatter cursors | starts | runs | edge offsets
 };
-PtBufs pt_bufs(kmp_postings* ws, const PtGeom& g, bool reserve, hipError_t* e) {
+PtBufs pt_bufs(kmp_postings* ws, const PtGeom& g, bool reserve, hipError_t* e, hipStream_t st = nullptr) {
     PtBufs b{};
     if (reserve) {
         *e = ws->pt.reserve(2 * (uint64_t)kPtMaxBlocks + 3 * (uint64_t)g.nrb + 2);
         // T (row-block totals) must be zero: pt_tscan re-zeroes what it used, a new allocation
-        // (a new pointer or capacity: reserve only reallocates to grow) is cleared once
+        // (a new pointer or capacity: reserve only reallocates to grow) is cleared once, on the
+        // step's stream (a null-stream memset does not order with the non-blocking streams: the
+        // first pt_hist of a grown buffer could run before it)
         if (*e == hipSuccess && (ws->pt_zero_p != ws->pt.p || ws->pt_zero_n != ws->pt.n)) {
-            *e = hipMemset(ws->pt.p, 0, kPtMaxBlocks * sizeof(uint32_t));
+            *e = hipMemsetAsync(ws->pt.p, 0, kPtMaxBlocks * sizeof(uint32_t), st);
             ws->pt_zero_p = ws->pt.p;
             ws->pt_zero_n = ws->pt.n;
         }
@@ -3592,7 +3685,7 @@ BucketArgs bucket_args(kmp_postings* ws, const StepCfg& c, bool spill) {
 }
 
 // buffers of one step (reserved before any launch, so a capture allocates nothing)
-int step_reserve(kmp_postings* ws, const StepCfg& c, const PtGeom& g) {
+int step_reserve(kmp_postings* ws, const StepCfg& c, const PtGeom& g, hipStream_t st) {
     const uint64_t total = ws->shard_cap * kShards;
     PG(ws->keys.reserve(c.slots));
     PG(ws->sorted.reserve(c.slots));
@@ -3601,16 +3694,18 @@ int step_reserve(kmp_postings* ws, const StepCfg& c, const PtGeom& g) {
     PG(ws->bstats.reserve(kGsWords));
     PG(ws->small.reserve(16));  // [1] run count, [2] largest row block
     PG(ws->inc_sorted.reserve(total));
-    PG(ws->inc.reserve(total));  // u32 row-block keys (pt_scatter) ...
-    PG(ws->uniq.reserve(total));  // ... staged p | q (u32 each)
-    PG(ws->w.reserve(total));     // ... staged w
-    if (c.sb) PG(ws->stg2.reserve(2 * total));  // ... staged scores | second-k weights
+    if (!c.expand_only) {  // an expand-only call leaves the tail (and its staging) to tail_multi
+        PG(ws->inc.reserve(total));  // u32 row-block keys (pt_scatter) ...
+        PG(ws->uniq.reserve(total));  // ... staged p | q (u32 each)
+        PG(ws->w.reserve(total));     // ... staged w
+        if (c.sb) PG(ws->stg2.reserve(2 * total));  // ... staged scores | second-k weights
+    }
     PG(ws->spill.reserve(ws->spill_cap * kShards));
     PG(ws->hseg.reserve(seg_capacity(ws)));
     PG(ws->ovf.reserve((uint64_t)g.nrb + 1));
     if (!ws->hrb) PG(hipHostMalloc((void**)&ws->hrb, kRbWords * sizeof(unsigned long long), hipHostMallocCoherent));
     hipError_t e = hipSuccess;
-    pt_bufs(ws, g, true, &e);
+    pt_bufs(ws, g, true, &e, st);
     PG(e);
     return KMP_OK;
 }
@@ -3668,11 +3763,11 @@ int enqueue_tail_in(kmp_postings* ws, const StepCfg& c, const PtGeom& g, const u
     pt_scatter_kernel<<<dim3(g.jt, g.nshards), kPtThreads, 0, st>>>(in, cursor, g, b.cur, keys32);
     const PtScoreOut so = pt_score_out(ws, c, total);
     if (g.sbits && g.kbit)
-        pt_reduce_scored_kernel<true><<<g.nrb, kPtRThreads, 0, st>>>(keys32, b.bst, g, ws->flags.p, ws->ovf.p, stage_p,
+        pt_reduce_scored_kernel<true><<<g.nrb, kPtRThreads, 0, st>>>(keys32, BlkSrc{b.bst, nullptr, nullptr}, g, ws->flags.p, ws->ovf.p, stage_p,
                                                                      stage_q, ws->w.p, ws->stg2.p, ws->stg2.p + total,
                                                                      b.counts);
     else if (g.sbits)
-        pt_reduce_scored_kernel<false><<<g.nrb, kPtRThreads, 0, st>>>(keys32, b.bst, g, ws->flags.p, ws->ovf.p, stage_p,
+        pt_reduce_scored_kernel<false><<<g.nrb, kPtRThreads, 0, st>>>(keys32, BlkSrc{b.bst, nullptr, nullptr}, g, ws->flags.p, ws->ovf.p, stage_p,
                                                                       stage_q, ws->w.p, ws->stg2.p, nullptr, b.counts);
     else
         pt_reduce_kernel<<<g.nrb, kPtRThreads, 0, st>>>(keys32, b.bst, g, ws->flags.p, ws->ovf.p, stage_p, stage_q,
@@ -3698,19 +3793,28 @@ int enqueue_tail(kmp_postings* ws, const StepCfg& c, const PtGeom& g, hipStream_
 // the listed row blocks (above kPtCap keys): the composite sort + encode above, then offsets
 // and emit again; host-synchronous, returns the edge count in *edges
 
+// bsrc (sub-blocks; nullptr: the row blocks) / nblk, counts, eoff: the blocks the reduce ran over
+// and their run counts and edge offsets (sub-block mode: ws->dsc)
 int pt_finish_overflow(kmp_postings* ws, const StepCfg& c, const PtGeom& g, uint32_t m, uint64_t* edges,
-                       hipStream_t st, uint64_t total = 0) {
+                       hipStream_t st, uint64_t total = 0, const BlkSrc* bsrc = nullptr, uint32_t nblk = 0,
+                       uint32_t* bcounts = nullptr, uint32_t* beoff = nullptr, const uint32_t* bkeys = nullptr) {
     hipError_t e = hipSuccess;
-    const PtBufs b = pt_bufs(ws, g, false, &e);
+    PtBufs b = pt_bufs(ws, g, false, &e);
+    const BlkSrc bs = bsrc ? *bsrc : BlkSrc{b.bst, nullptr, nullptr};
+    const uint32_t nb = bsrc ? nblk : g.nrb;
+    if (bsrc) {
+        b.counts = bcounts;
+        b.eoff = beoff;
+    }
     if (!total) total = ws->shard_cap * kShards;
-    uint32_t* keys32 = reinterpret_cast<uint32_t*>(ws->inc.p);
+    const uint32_t* keys32 = bkeys ? bkeys : reinterpret_cast<uint32_t*>(ws->inc.p);
     uint32_t* stage_p = reinterpret_cast<uint32_t*>(ws->uniq.p);
     uint32_t* stage_q = stage_p + total;
     const unsigned kb = g.pbits + g.sbits + g.rbits, mb = bits_for((uint64_t)m + 1);
     if (kb + mb > 63) return KMP_EINVAL;
     PG(ws->ovx.reserve(m + 1));
     unsigned long long* xoff = ws->ovx.p;
-    pt_ovf_sizes_kernel<<<(m + 256) / 256, 256, 0, st>>>(ws->ovf.p, m, b.bst, xoff);
+    pt_ovf_sizes_kernel<<<(m + 256) / 256, 256, 0, st>>>(ws->ovf.p, m, bs, xoff);
     size_t t0 = 0;
     PG(rocprim::exclusive_scan(nullptr, t0, xoff, xoff, 0ull, (size_t)m + 1, rocprim::plus<unsigned long long>(), st));
     PG(ws->tmp.reserve(std::max(t0, ws->tmp.n)));
@@ -3726,7 +3830,7 @@ int pt_finish_overflow(kmp_postings* ws, const StepCfg& c, const PtGeom& g, uint
     uint32_t *rw = ws->ovr.p, *keep = rw + nx + 1, *kpos = keep + nx + 1, *first = kpos + nx + 1;
     uint32_t* nruns = ws->small.p + 4;
     const uint32_t gx = (uint32_t)std::min<unsigned long long>((nx / m + 255) / 256 + 1, 64);
-    pt_ovf_gather_kernel<<<dim3(gx, m), 256, 0, st>>>(ws->ovf.p, b.bst, xoff, keys32, kb, x);
+    pt_ovf_gather_kernel<<<dim3(gx, m), 256, 0, st>>>(ws->ovf.p, bs, xoff, keys32, kb, x);
     size_t t1 = 0, t2 = 0, t3 = 0;
     PG(rocprim::radix_sort_keys<SortCfg>(nullptr, t1, x, xs, (size_t)nx, 0u, kb + mb, st));
     PG(rocprim::run_length_encode(nullptr, t2, xs, (unsigned)nx, uq, rw, nruns, st));
@@ -3749,12 +3853,16 @@ int pt_finish_overflow(kmp_postings* ws, const StepCfg& c, const PtGeom& g, uint
         pt_ovf_keep_scored_kernel<<<gr, 256, 0, st>>>(uq, agg, nruns, kb - g.sbits, g.min_shared, g.kbit, keep, first);
         PG(rocprim::exclusive_scan(ws->tmp.p, t3, keep, kpos, 0u, (size_t)nx + 1, rocprim::plus<uint32_t>(), st));
         const PtScoreOut so = pt_score_out(ws, c, total);
-        pt_ovf_stage_scored_kernel<<<gr, 256, 0, st>>>(ws->ovf.p, m, b.bst, g, uq, agg, nruns, keep, kpos, first,
+        pt_ovf_stage_scored_kernel<<<gr, 256, 0, st>>>(ws->ovf.p, m, bs, g, uq, agg, nruns, keep, kpos, first,
                                                        stage_p, stage_q, ws->w.p, ws->stg2.p, ws->stg2.p + total,
                                                        b.counts);
-        pt_offsets_kernel<<<1, kPtScanThreads, 0, st>>>(b.counts, g.nrb, b.eoff, ws->small.p + 1);
-        pt_emit_kernel<<<g.nrb, 256, 0, st>>>(stage_p, stage_q, ws->w.p, b.bst, b.counts, b.eoff, c.d_p, c.d_q, c.d_w,
-                                              c.cap, c.stride, PtPack{}, nullptr, so);
+        if (bsrc) {  // the caller scans the sub-blocks' counts and emits
+            PG(hipStreamSynchronize(st));
+            return KMP_OK;
+        }
+        pt_offsets_kernel<<<1, kPtScanThreads, 0, st>>>(b.counts, nb, b.eoff, ws->small.p + 1);
+        pt_emit_kernel<<<nb, 256, 0, st>>>(stage_p, stage_q, ws->w.p, b.bst, b.counts, b.eoff, c.d_p, c.d_q, c.d_w,
+                                           c.cap, c.stride, PtPack{}, nullptr, so);
         uint32_t ne = 0;
         PG(hipMemcpyAsync(&ne, ws->small.p + 1, 4, hipMemcpyDeviceToHost, st));
         PG(hipStreamSynchronize(st));
@@ -4095,7 +4203,7 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
         PtGeom g;
         if (!pt_geometry(ws, c, ws->pt_inc ? ws->pt_inc : c.slots / 4, &g)) return KMP_EINVAL;
         {
-            int rc = step_reserve(ws, c, g);
+            int rc = step_reserve(ws, c, g, st);
             if (rc != KMP_OK) return rc;
         }
         const unsigned long long* rb = ws->hrb;
@@ -4189,7 +4297,7 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
                 return KMP_OK;
             }
             if (!pt_geometry(ws, c, n_inc, &g)) return KMP_EINVAL;
-            int rc = step_reserve(ws, c, g);
+            int rc = step_reserve(ws, c, g, st);
             if (rc != KMP_OK) return rc;
             rc = enqueue_tail(ws, c, g, st);
             if (rc != KMP_OK) return rc;
@@ -4244,15 +4352,15 @@ int tail_multi(kmp_postings* const* ws, uint32_t nk, const StepCfg& c, const uin
     for (uint32_t j = 0; j < nk; ++j) T += inc[j];
     PtGeom g;
     if (!pt_geometry(w0, c, std::max<uint64_t>(T, 1), &g)) return KMP_EINVAL;
-    const uint64_t total = std::max<uint64_t>(T + 1, w0->shard_cap * kShards);  // staging capacity
-    PG(w0->inc.reserve(total));
+    const uint64_t total = T + 1;  // staging capacity: every key of the pass (the row-block positions)
+    PG(w0->inc.reserve(total / 2 + 1));  // u32 keys in a u64 buffer
     PG(w0->uniq.reserve(total));
     PG(w0->w.reserve(total));
     PG(w0->stg2.reserve(2 * total));
     PG(w0->ovf.reserve((uint64_t)g.nrb + 1));
     PG(w0->small.reserve(16));
     hipError_t e = hipSuccess;
-    const PtBufs b = pt_bufs(w0, g, true, &e);
+    const PtBufs b = pt_bufs(w0, g, true, &e, st);
     PG(e);
     PG(hipMemsetAsync(w0->flags.p + kFlOvf, 0, sizeof(uint32_t), st));
     uint32_t* keys32 = reinterpret_cast<uint32_t*>(w0->inc.p);
@@ -4272,28 +4380,67 @@ int tail_multi(kmp_postings* const* ws, uint32_t nk, const StepCfg& c, const uin
         pt_scatter_kernel<<<dim3(geo(j).jt, kShards), kPtThreads, 0, st>>>(ws[j]->inc_sorted.p,
                                                                           ws[j]->bstats.p + kRbCursor, geo(j), b.cur,
                                                                           keys32);
-    if (g.kbit)
-        pt_reduce_scored_kernel<true><<<g.nrb, kPtRThreads, 0, st>>>(keys32, b.bst, g, w0->flags.p, w0->ovf.p, stage_p,
-                                                                     stage_q, w0->w.p, w0->stg2.p, w0->stg2.p + total,
-                                                                     b.counts);
-    else
-        pt_reduce_scored_kernel<false><<<g.nrb, kPtRThreads, 0, st>>>(keys32, b.bst, g, w0->flags.p, w0->ovf.p, stage_p,
-                                                                      stage_q, w0->w.p, w0->stg2.p, nullptr, b.counts);
-    pt_emit_kernel<<<g.nrb, 256, 0, st>>>(stage_p, stage_q, w0->w.p, b.bst, b.counts, nullptr, c.d_p, c.d_q, c.d_w,
-                                          c.cap, c.stride, PtPack{}, w0->small.p + 1, pt_score_out(w0, c, total));
-    PG(hipGetLastError());
-    uint32_t h[2] = {0, 0};
-    PG(hipMemcpyAsync(&h[0], w0->small.p + 1, 4, hipMemcpyDeviceToHost, st));
-    PG(hipMemcpyAsync(&h[1], w0->flags.p + kFlOvf, 4, hipMemcpyDeviceToHost, st));
+    // the row blocks' sizes -> sub-blocks (a block above kPtCap cut into pieces the LDS reduce takes)
+    std::vector<uint32_t> hb(g.nrb + 1), hd(g.nrb + 1);
+    PG(hipMemcpyAsync(hb.data(), b.bst, (g.nrb + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     PG(hipStreamSynchronize(st));
-    uint64_t ne = h[0];
-    w0->last_ovf = h[1];
-    if (h[1]) {
-        int rc = pt_finish_overflow(w0, c, g, h[1], &ne, st, total);
+    const unsigned kbits = g.pbits + g.sbits + g.rbits;
+    uint32_t nd = 0;
+    for (uint32_t r = 0; r < g.nrb; ++r) {
+        hd[r] = nd;
+        nd += 1u << pt_sub_log(hb[r + 1] - hb[r], kbits);
+    }
+    hd[g.nrb] = nd;
+    PG(w0->k2.reserve(total));
+    PG(w0->dsc.reserve(5 * (uint64_t)nd + 2 + g.nrb + 1));
+    // dstart | dsize | drow (nd each) | run counts (nd + 1: the scan's last input is 0) | edge offsets
+    // (nd + 1) | dbase (nrb + 1)
+    uint32_t *dstart = w0->dsc.p, *dsize = dstart + nd, *drow = dsize + nd, *dcnt = drow + nd, *deoff = dcnt + nd + 1,
+             *dbase = deoff + nd + 1;
+    PG(w0->ovf.reserve((uint64_t)std::max(nd, g.nrb) + 1));  // the sub-blocks the reduce lists
+    PG(hipMemcpyAsync(dbase, hd.data(), (g.nrb + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    pt_split_kernel<<<g.nrb, kSbThreads, 0, st>>>(keys32, b.bst, dbase, kbits, w0->k2.p, dstart, dsize, drow);
+    const BlkSrc bs{dstart, dsize, drow};
+    if (g.kbit)
+        pt_reduce_scored_kernel<true><<<nd, kPtRThreads, 0, st>>>(w0->k2.p, bs, g, w0->flags.p, w0->ovf.p, stage_p,
+                                                                  stage_q, w0->w.p, w0->stg2.p, w0->stg2.p + total,
+                                                                  dcnt);
+    else
+        pt_reduce_scored_kernel<false><<<nd, kPtRThreads, 0, st>>>(w0->k2.p, bs, g, w0->flags.p, w0->ovf.p, stage_p,
+                                                                   stage_q, w0->w.p, w0->stg2.p, nullptr, dcnt);
+    PG(hipGetLastError());
+    uint32_t h_ovf = 0;
+    PG(hipMemcpyAsync(&h_ovf, w0->flags.p + kFlOvf, 4, hipMemcpyDeviceToHost, st));
+    PG(hipStreamSynchronize(st));
+    w0->last_ovf = h_ovf;
+    if (h_ovf) {  // sub-blocks still above kPtCap: the tagged sort (their counts land in dcnt)
+        uint64_t unused = 0;
+        int rc = pt_finish_overflow(w0, c, g, h_ovf, &unused, st, total, &bs, nd, dcnt, deoff, w0->k2.p);
         if (rc != KMP_OK) return rc;
     }
-    for (uint32_t j = 0; j < nk; ++j)  // the next call's regions, learned now that the tail has read them
-        ws[j]->shard_cap = ws[j]->last_most + ws[j]->last_most / 64 + 256;
+    // edge offsets of the sub-blocks (canonical: row blocks in order, sub-blocks by key range)
+    size_t tscan = 0;
+    PG(rocprim::exclusive_scan(nullptr, tscan, dcnt, deoff, 0u, (size_t)nd + 1, rocprim::plus<uint32_t>(), st));
+    PG(w0->tmp.reserve(std::max(tscan, w0->tmp.n)));
+    PG(hipMemsetAsync(dcnt + nd, 0, sizeof(uint32_t), st));
+    PG(rocprim::exclusive_scan(w0->tmp.p, tscan, dcnt, deoff, 0u, (size_t)nd + 1, rocprim::plus<uint32_t>(), st));
+    uint32_t h_ne = 0;
+    PG(hipMemcpyAsync(&h_ne, deoff + nd, 4, hipMemcpyDeviceToHost, st));
+    PG(hipStreamSynchronize(st));
+    uint64_t ne = h_ne;
+    // the staged runs stay in w0: a caller that finds its arrays too small (KMP_EOVERFLOW) grows them
+    // and calls again with the same rows, and only the emit runs (tail_multi_emit)
+    w0->pend_nd = nd;
+    w0->pend_total = total;
+    w0->pend_ne = ne;
+    if (ne <= c.cap) {
+        pt_emit_kernel<<<nd, 256, 0, st>>>(stage_p, stage_q, w0->w.p, dstart, dcnt, deoff, c.d_p, c.d_q, c.d_w, c.cap,
+                                           c.stride, PtPack{}, nullptr, pt_score_out(w0, c, total));
+        PG(hipGetLastError());
+    }
+    // the next call's regions, learned now that the tail has read them; a quarter of slack (the
+    // passes' sizes and shard loads vary, and an overflow reruns the whole expansion)
+    for (uint32_t j = 0; j < nk; ++j) ws[j]->shard_cap = ws[j]->last_most + ws[j]->last_most / 4 + 256;
     w0->pt_inc = T;
     if (stats) {
         stats->incidences = T;
@@ -4301,6 +4448,21 @@ int tail_multi(kmp_postings* const* ws, uint32_t nk, const StepCfg& c, const uin
     }
     *n_edges = ne;
     return ne > c.cap ? KMP_EOVERFLOW : KMP_OK;
+}
+
+// the emit of the last tail_multi of w0 again, into larger arrays (its runs are still staged)
+int tail_multi_emit(kmp_postings* w0, const StepCfg& c, uint64_t* n_edges, hipStream_t st) {
+    const uint32_t nd = w0->pend_nd;
+    const uint64_t total = w0->pend_total;
+    uint32_t *dstart = w0->dsc.p, *dsize = dstart + nd, *drow = dsize + nd, *dcnt = drow + nd, *deoff = dcnt + nd + 1;
+    (void)drow;
+    uint32_t* stage_p = reinterpret_cast<uint32_t*>(w0->uniq.p);
+    *n_edges = w0->pend_ne;
+    if (w0->pend_ne > c.cap) return KMP_EOVERFLOW;
+    pt_emit_kernel<<<nd, 256, 0, st>>>(stage_p, stage_p + total, w0->w.p, dstart, dcnt, deoff, c.d_p, c.d_q, c.d_w,
+                                       c.cap, c.stride, PtPack{}, nullptr, pt_score_out(w0, c, total));
+    PG(hipGetLastError());
+    return KMP_OK;
 }
 
 // Shared tail: sort the pair keys, run-length encode -> (pair, w) in canonical order, keep
@@ -4754,21 +4916,6 @@ int kmp_dev_pairs_rows_multi(kmp_postings* const* ws, const int* ks, uint32_t nk
     if (!d_res || !d_res_off || !d_class) return KMP_EINVAL;
     hipStream_t st = as_stream(stream);
     const bool ranged = !(row_lo == 0 && row_hi == n);
-    uint64_t inc[2] = {0, 0};
-    kmp_postings_stats s0{};
-    const bool timed = stats != nullptr;  // stage_ms: [0] first k expanded, [1] second k, [2] the fused tail
-    if (timed && !ws[0]->mev[0])
-        for (auto& e : ws[0]->mev) PG(hipEventCreate(&e));
-    if (timed) PG(hipEventRecord(ws[0]->mev[0], st));
-    for (uint32_t j = 0; j < nk; ++j) {
-        // expand only: every incidence keyed (pair << 8) | j << 7 | s(x)
-        uint64_t unused = 0;
-        int rc = residues_impl(ws[j], d_res, d_res_off, d_class, n, ks[j], slots, 0xFFFFFFFFu, 1, require_class_diff,
-                               ranged, row_lo, row_hi, d_p, d_q, d_w, cap, &unused, j == 0 ? &s0 : nullptr, stream,
-                               kScoreBits + 1, j << kScoreBits, d_score, d_w1, &inc[j]);
-        if (rc != KMP_OK) return rc;
-        if (timed) PG(hipEventRecord(ws[0]->mev[1 + j], st));
-    }
     // the tail's geometry and outputs (the same StepCfg fields the step uses)
     StepCfg c{};
     c.n = n;
@@ -4785,7 +4932,32 @@ int kmp_dev_pairs_rows_multi(kmp_postings* const* ws, const int* ks, uint32_t nk
     c.d_s = d_score;
     c.d_w1 = d_w1;
     c.d_w0 = d_w0;
+    const std::vector<unsigned long long> call = {n, (unsigned long long)ks[0], (unsigned long long)ks[1], row_lo, row_hi,
+                                                  c.min_shared, (unsigned long long)require_class_diff, slots,
+                                                  (uintptr_t)d_res, (uintptr_t)ws[1]};
+    if (ws[0]->pend_key == call) {  // the same call after KMP_EOVERFLOW: emit the staged runs again
+        const int rc = tail_multi_emit(ws[0], c, n_edges, st);
+        if (rc == KMP_OK) ws[0]->pend_key.clear();
+        return rc;
+    }
+    ws[0]->pend_key.clear();
+    uint64_t inc[2] = {0, 0};
+    kmp_postings_stats s0{};
+    const bool timed = stats != nullptr;  // stage_ms: [0] first k expanded, [1] second k, [2] the fused tail
+    if (timed && !ws[0]->mev[0])
+        for (auto& e : ws[0]->mev) PG(hipEventCreate(&e));
+    if (timed) PG(hipEventRecord(ws[0]->mev[0], st));
+    for (uint32_t j = 0; j < nk; ++j) {
+        // expand only: every incidence keyed (pair << 8) | j << 7 | s(x)
+        uint64_t unused = 0;
+        int rc = residues_impl(ws[j], d_res, d_res_off, d_class, n, ks[j], slots, 0xFFFFFFFFu, 1, require_class_diff,
+                               ranged, row_lo, row_hi, d_p, d_q, d_w, cap, &unused, j == 0 ? &s0 : nullptr, stream,
+                               kScoreBits + 1, j << kScoreBits, d_score, d_w1, &inc[j]);
+        if (rc != KMP_OK) return rc;
+        if (timed) PG(hipEventRecord(ws[0]->mev[1 + j], st));
+    }
     int rc = tail_multi(ws, nk, c, inc, n_edges, stats, st);
+    if (rc == KMP_EOVERFLOW) ws[0]->pend_key = call;
     if (timed && (rc == KMP_OK || rc == KMP_EOVERFLOW)) {
         PG(hipEventRecord(ws[0]->mev[3], st));
         PG(hipEventSynchronize(ws[0]->mev[3]));
@@ -4846,7 +5018,7 @@ int kmp_dev_split_expand(kmp_postings* ws, const uint8_t* d_res, const uint64_t*
     PtGeom g;
     if (!pt_geometry(ws, c, slots / 4, &g)) return KMP_EINVAL;
     {
-        const int rc = step_reserve(ws, c, g);
+        const int rc = step_reserve(ws, c, g, st);
         if (rc != KMP_OK) return rc;
     }
     PG(ws->split_cur.reserve(kSplitMax));
@@ -4913,7 +5085,7 @@ int kmp_dev_split_edges(kmp_postings* ws, const unsigned long long* d_keys, uint
     g.sc = m;
     g.jt = (uint32_t)((m + kPtTile - 1) / kPtTile);
     hipError_t e = hipSuccess;
-    pt_bufs(ws, g, true, &e);
+    pt_bufs(ws, g, true, &e, st);
     PG(e);
     PG(ws->inc.reserve(m));  // u32 row-block keys
     PG(ws->uniq.reserve(m));  // staged p | q (u32 each)
