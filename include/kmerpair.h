@@ -104,8 +104,9 @@ int kmp_ctx_create(kmp_ctx** ctx, int device, int cpu_threads);
  * batch to every rank; kmp_pairs (engine AUTO / RESIDUES) leaves rank g with the canonical edges of
  * its rows (kmp_row_split: the pairs whose smaller protein is in them) — by the k-mer split (rank g
  * expands its share of the k-mers, an all-to-all routes each pair key to its row owner, which
- * reduces it; kmp_dev_split_expand / kmp_dev_split_edges) or, when the batch spills frequent
- * k-mers, by the row split (every rank groups every k-mer and expands its rows) — and gathers the
+ * reduces it; kmp_dev_split_expand / kmp_dev_split_edges; frequent k-mers through each rank's
+ * heavy path) or, when the class ids overflow the key or the split cannot run, by the row split
+ * (every rank groups every k-mer and expands its rows) — and gathers the
  * ranks' edges to device 0 in rank order, which is the canonical list.  The library owns the
  * collectives: distinct devices get RCCL communicators created
  * in-process (ncclCommInitAll; KMP_ERCCL if RCCL is unavailable or a collective fails); a device
@@ -116,7 +117,8 @@ int kmp_ctx_gpus(const kmp_ctx* ctx);               /* ranks (1 for kmp_ctx_crea
 const char* kmp_ctx_transport(const kmp_ctx* ctx);  /* "local", "copy" or "rccl" */
 /* the flow of the last multi-GPU kmp_pairs: "kmer" (the k-mer split: each rank expands its share of
  * the k-mers, an all-to-all routes the pair keys to their row owners; kmp_dev_split_expand) or
- * "rows" (the row split, for batches whose frequent k-mers spill); "" before one */
+ * "rows" (the row split: class ids wider than the key's field, or a batch the split cannot
+ * take); "" before one */
 const char* kmp_ctx_last_split(const kmp_ctx* ctx);
 void kmp_ctx_destroy(kmp_ctx* ctx);
 const char* kmp_last_error(const kmp_ctx* ctx);
@@ -461,6 +463,11 @@ int kmp_postings_last_partition(const kmp_postings* ws);
  * heavy expansion and the tail of its rows — the passes of the bounded-memory mode and the
  * per-k rows of kmp_pairs_multi_k call kmp_dev_pairs_rows this way. */
 int kmp_postings_set_reuse(kmp_postings* ws, int enable);
+/* Shard-region floor (default 0): the pair-key regions hold at least keys / 64 (+ a quarter) keys
+ * each from the next call on.  A stream whose passes are planned to ~keys pair keys sets it once,
+ * so its regions are sized before the first pass instead of regrown (a multi-GB reallocation idles
+ * the device) as the passes' measured sizes climb.  0: learned only. */
+int kmp_postings_set_shard_floor(kmp_postings* ws, uint64_t keys);
 int kmp_dev_pairs_postings(kmp_postings* ws, const uint32_t* d_set, const uint32_t* d_set_len,
                            const uint64_t* d_res_off, const uint16_t* d_class, uint32_t n, int k, uint64_t slots,
                            uint32_t heavy_df, uint32_t min_shared, int require_class_diff, uint32_t* d_p,
@@ -523,7 +530,9 @@ int kmp_dev_pairs_rows_multi(kmp_postings* const* ws, const int* ks, uint32_t nk
  *     share of the bucket hash range (a contiguous range of coarse bins), groups and expands them
  *     (all rows), and routes each pair key (p << bits(N) | q) to the rank owning row p
  *     (kmp_row_split): region d of d_send (cap keys, unused tail kNoKey) is rank d's.  No host
- *     synchronisation; d_flags[KMP_SPLIT_FLAGS] and d_stats[8] (Σ|K(p)|, distinct, repeat,
+ *     synchronisation (except with the heavy path on: one read-back of the front's spill, which
+ *     the rank compacts, plans and expands into its routed keys); d_flags[KMP_SPLIT_FLAGS] and
+ *     d_stats[8] (Σ|K(p)|, distinct, repeat,
  *     Σ C(df,2), max df, heavy entries, incidences, 0 — this rank's k-mers) are written on `stream`.
  *     learn: the previous call's flags reduced (max) over the ranks, or NULL for a first call;
  *     every rank grows its capacities from them identically.
@@ -535,7 +544,8 @@ int kmp_dev_pairs_rows_multi(kmp_postings* const* ws, const int* ks, uint32_t nk
  * The rank-order concatenation of the ranks' edges is the canonical list.  Flags: RERUN (a send
  * region, pair-key shard or bucket region overflowed: call expand again with learn, after growing
  * cap to at least MAX_PART when that is the cause), CLASS (class ids too wide: single GPU) and
- * HEAVY (k-mers above the LDS group limit spilled: use the row split, kmp_dev_pairs_rows). */
+ * HEAVY (k-mers above the LDS group limit spilled while the rank's heavy path was off: call expand
+ * again with learn — every rank turns its heavy path on for the batch, vertex.rs:59-140). */
 enum {
     KMP_SPLIT_RERUN = 0, KMP_SPLIT_CLASS = 1, KMP_SPLIT_HEAVY = 2, KMP_SPLIT_MAX_PART = 3,
     KMP_SPLIT_MAX_SHARD = 4, KMP_SPLIT_BIN_TILES = 5, KMP_SPLIT_CURSOR = 6, KMP_SPLIT_FLAGS = 8

@@ -100,6 +100,7 @@ class OracleSplitPipe(OraclePipe):
         self.total = 300 * n
         self.dev = torch.device("cpu")
         self.heavy = heavy
+        self.heavy_on = False
         self.pbits = bits_for(n)
 
     def split_expand(self, part, parts, cap, send, flags, stats, learn=None, require_class_diff=True):
@@ -116,7 +117,11 @@ class OracleSplitPipe(OraclePipe):
         flags.zero_()
         flags[_lib.KMP_SPLIT_MAX_PART] = most
         flags[_lib.KMP_SPLIT_RERUN] = int(most > cap)
-        flags[_lib.KMP_SPLIT_HEAVY] = int(self.heavy)
+        # a spilling batch raises HEAVY until the learned flags turn the heavy path on (the library
+        # keeps it on for the batch from then on)
+        if learn is not None and learn[_lib.KMP_SPLIT_HEAVY]:
+            self.heavy_on = True
+        flags[_lib.KMP_SPLIT_HEAVY] = int(self.heavy and not self.heavy_on)
         stats.zero_()
         stats[6] = int(share.sum())
 
@@ -167,7 +172,8 @@ def split_worker(rank, world, port, out_q):
 def test_kmer_split_exchange(world):
     """kmer_split_step over gloo: the all-to-all of routed pair keys and the per-rank reduction
     give the canonical list gathered on rank 0; an undersized exchange capacity reruns once with
-    the capacity learned from the reduced flags; a spilling batch falls back to the row split."""
+    the capacity learned from the reduced flags; a spilling batch reruns once with the heavy path
+    on and stays on the k-mer split."""
     port = free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -181,7 +187,9 @@ def test_kmer_split_exchange(world):
     assert all(m[3] for m in msgs), msgs
     light = [m for m in msgs if not m[1]]
     assert light[0][5] == 1 and not light[0][6] and light[0][7] > 64  # one rerun, then the learned cap
-    assert all(m[6] for m in msgs if m[1])  # heavy: the row split
+    heavy = [m for m in msgs if m[1]]
+    assert not any(m[6] for m in heavy)  # spilling: stays on the k-mer split, the heavy path on
+    assert heavy[0][5] >= 1  # (after a rerun that turned it on)
 
 
 @pytest.mark.parametrize("world", [2, 3])

@@ -3,7 +3,8 @@ processes sharing the one GPU of the test box: RCCL admits one rank per device, 
 collectives go over gloo through host copies (a shim with torch.distributed's signatures that
 bounces each tensor through the CPU).  The edges gathered on rank 0 equal the oracle's canonical
 list; the first step reruns once (an exchange capacity set far too small); the reference's
-dataset at k = 5 falls back to the row split."""
+dataset at k = 5 (frequent 5-mers) stays on the k-mer split: its first step reruns once with every
+rank's heavy path on, the second runs it without a rerun."""
 import os
 import socket
 
@@ -88,10 +89,11 @@ def worker(rank, world, port, out_q):
         g = load_json("uniprot_counters.json")["5"]
         pipe5 = DevicePipeline(K.Proteins(res, off, cls), 5, "cuda:0")
         state5 = D.SplitState()
-        n = D.kmer_split_step(pipe5, rank, world, gather=True, state=state5)
-        if rank == 0:
-            out_q.put(("rows", n == g["n_edges"] and edges_sha256(*pipe5.edges()) == g["edges_sha256"],
-                       state5.row_split))
+        for it in range(2):
+            n = D.kmer_split_step(pipe5, rank, world, gather=True, state=state5)
+            if rank == 0:
+                out_q.put(("heavy", n == g["n_edges"] and edges_sha256(*pipe5.edges()) == g["edges_sha256"],
+                           state5.row_split, state5.reruns))
     finally:
         dist.destroy_process_group()
 
@@ -104,11 +106,12 @@ def test_kmer_split_step_device_stages(world):
     procs = [ctx.Process(target=worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    msgs = [q.get(timeout=200) for _ in range(3)]
+    msgs = [q.get(timeout=200) for _ in range(4)]
     for p in procs:
         p.join(timeout=60)
     assert all(p.exitcode == 0 for p in procs)
     kmer = [m for m in msgs if m[0] == "kmer"]
     assert all(m[2] for m in kmer) and kmer[-1][3] == 1 and not kmer[-1][4], kmer
-    rows = [m for m in msgs if m[0] == "rows"][0]
-    assert rows[1] and rows[2], rows
+    heavy = [m for m in msgs if m[0] == "heavy"]
+    assert all(m[1] and not m[2] for m in heavy), heavy  # golden edges, never the row split
+    assert heavy[0][3] == heavy[1][3] >= 1, heavy  # the heavy path turned on once, then kept

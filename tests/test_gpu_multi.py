@@ -45,18 +45,21 @@ def test_virtual_ranks_config4(config4, g):
 
 
 def test_virtual_ranks_heavy_uniprot_k5():
-    """The reference's dataset at k = 5 (frequent 5-mers: every rank runs the heavy path and
-    the row-tail overflow sort on its rows) over 3 ranks: golden edge sha."""
+    """The reference's dataset at k = 5 (frequent 5-mers, max df 3,694) over 3 ranks on the k-mer
+    split: every rank compacts, plans and expands the spill of its own k-mers with the heavy path
+    and routes those pair keys with the light ones (vertex.rs:59-140); golden edge sha, twice (the
+    second call keeps the heavy path on without a rerun)."""
     res, off, cls, _ = uniprot()
     g = load_json("uniprot_counters.json")["5"]
     with K.KmerPairEngine(0, 4, devices=[0, 0, 0]) as e:
         e.load(K.Proteins(res, off, cls))
         e.build_sets(5)
-        got = e.pairs()
-        assert len(got) == g["n_edges"] and e.last_split == "rows"  # frequent 5-mers spill
-        assert edges_sha256(got.p, got.q, got.w) == g["edges_sha256"]
-        c = e.counters()
-        assert c["sum_w_diff"] == g["sum_w_diff"] and c["n_align"] == g["n_align"]
+        for _ in range(2):
+            got = e.pairs()
+            assert len(got) == g["n_edges"] and e.last_split == "kmer"
+            assert edges_sha256(got.p, got.q, got.w) == g["edges_sha256"]
+            c = e.counters()
+            assert c["sum_w_diff"] == g["sum_w_diff"] and c["n_align"] == g["n_align"]
 
 
 def test_virtual_ranks_options_and_scores(oracle_mod):
@@ -126,7 +129,7 @@ def emulate_kmer_split(b, k, G, cap=None, min_shared=1):
             pipes[d].split_edges(recv, int(start[d]), int(start[d + 1]), min_shared)
             for a, x in zip(out, pipes[d].edges()):
                 a.append(x)
-        if fl[_lib.KMP_SPLIT_RERUN] and not (fl[_lib.KMP_SPLIT_HEAVY] or fl[_lib.KMP_SPLIT_CLASS]):
+        if (fl[_lib.KMP_SPLIT_RERUN] or fl[_lib.KMP_SPLIT_HEAVY]) and not fl[_lib.KMP_SPLIT_CLASS]:
             reruns += 1
             learn = fl
             cap = max(cap, fl[_lib.KMP_SPLIT_MAX_PART] + fl[_lib.KMP_SPLIT_MAX_PART] // 16 + 1024)
@@ -157,7 +160,8 @@ def test_kmer_split_config4(config4, oracle_mod, g):
 def test_kmer_split_reruns_and_options(oracle_mod):
     """An exchange capacity far too small reruns with the capacity learned from the reduced
     flags (same edges); min_shared on the receiving side; the reference's dataset at k = 5
-    (frequent 5-mers spill) raises HEAVY, the caller's cue for the row split."""
+    (frequent 5-mers spill) raises HEAVY once, and the rerun with every rank's heavy path on gives
+    the golden edge list at G = 2 and 3."""
     b = K.synth(20000, 9)
     o = oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=7, threads=8)
     for ms in (1, 2):
@@ -168,5 +172,8 @@ def test_kmer_split_reruns_and_options(oracle_mod):
         np.testing.assert_array_equal(eq, q)
         np.testing.assert_array_equal(ew, w)
     res, off, cls, _ = uniprot()
-    _, fl, _, _ = emulate_kmer_split(K.Proteins(res, off, cls), 5, 2)
-    assert fl[_lib.KMP_SPLIT_HEAVY] == 1
+    g = load_json("uniprot_counters.json")["5"]
+    for G in (2, 3):
+        (ep, eq, ew), fl, tot, reruns = emulate_kmer_split(K.Proteins(res, off, cls), 5, G)
+        assert reruns >= 1 and not fl[_lib.KMP_SPLIT_HEAVY] and not fl[_lib.KMP_SPLIT_RERUN]
+        assert len(ep) == g["n_edges"] and edges_sha256(ep, eq, ew) == g["edges_sha256"]

@@ -1,7 +1,9 @@
 """Condenses a rocprofv3 --stats kernel_stats.csv into a short table (kernel names shortened,
-template noise dropped).  Usage: python tools/prof_summary.py run_kernel_stats.csv [steps]"""
+template noise dropped).  Usage: python tools/prof_summary.py run_kernel_stats.csv [steps]
+(or the results.db rocprofv3 writes without --output-format csv)"""
 import csv
 import re
+import sqlite3
 import sys
 
 
@@ -15,13 +17,24 @@ def short(name: str) -> str:
     if "init_lookback" in n:
         return "rocprim::init_lookback_scan_state_kernel"
     n = n.replace("(anonymous namespace)::", "")
-    return n.split("(")[0][:90]
+    n = n.replace("void ", "")
+    depth = 0
+    for i, ch in enumerate(n):  # the parameter list: the first '(' outside template brackets
+        depth += (ch == "<") - (ch == ">")
+        if ch == "(" and depth == 0:
+            return n[:i][:90]
+    return n[:90]
 
 
 def main():
     path = sys.argv[1]
     steps = float(sys.argv[2]) if len(sys.argv) > 2 else 0
-    rows = list(csv.DictReader(open(path)))
+    if path.endswith(".db"):  # rocprofv3's default output: the kernels view of its database
+        db = sqlite3.connect(path)
+        q = "select name, count(*), sum(end - start) from kernels group by name"
+        rows = [{"Name": n, "Calls": c, "TotalDurationNs": t} for n, c, t in db.execute(q)]
+    else:
+        rows = list(csv.DictReader(open(path)))
     agg = {}
     for r in rows:
         k = short(r["Name"])

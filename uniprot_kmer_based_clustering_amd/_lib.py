@@ -179,6 +179,7 @@ SIGNATURES = {
     "kmp_postings_set_partition": (C.c_int, [P, C.c_int]),
     "kmp_postings_last_partition": (C.c_int, [P]),
     "kmp_postings_set_reuse": (C.c_int, [P, C.c_int]),
+    "kmp_postings_set_shard_floor": (C.c_int, [P, C.c_uint64]),
     "kmp_dev_pairs_residues": (C.c_int, [P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32,
                                          C.c_uint32, C.c_int, P, P, P, C.c_uint64, U64P, P, P]),
     "kmp_dev_split_expand": (C.c_int, [P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32, C.c_int,

@@ -901,8 +901,8 @@ static int split_rank_edges(kmp_ctx* c, const kmp_pair_opts& o, const std::vecto
             KMP_HIP(c, hipStreamSynchronize(r.stream));
             for (int i = 0; i < KMP_SPLIT_FLAGS; ++i) fl[i] = std::max(fl[i], h[i]);
         }
-        if (fl[KMP_SPLIT_CLASS] || fl[KMP_SPLIT_HEAVY]) return kSplitFallback;
-        if (fl[KMP_SPLIT_RERUN]) {
+        if (fl[KMP_SPLIT_CLASS]) return kSplitFallback;
+        if (fl[KMP_SPLIT_RERUN] || fl[KMP_SPLIT_HEAVY]) {  // HEAVY: a rank spilled; every rank's heavy path on
             learn = fl;
             have_learn = true;
             if (fl[KMP_SPLIT_MAX_PART] > cap) cap = fl[KMP_SPLIT_MAX_PART] + fl[KMP_SPLIT_MAX_PART] / 16 + 1024;
@@ -1295,6 +1295,14 @@ static int stream_passes(kmp_ctx* c, const kmp_pair_opts& o, const int* ks, uint
     if (!c->pass_keys && slots <= kPassSlots && plan.max_rows >= ln.row_hi - ln.row_lo)
         plan.density = 0;  // small batch: one pass
     const hipStream_t st = ln.L.stream;
+    if (fused && plan.density != 0) {
+        // the smaller k carries most of a pass's incidences: its regions sized for the planned pass
+        // (3/4 of the budget) with the fullest region at up to twice the mean (measured 1.6x at
+        // config 5: frequent k-mers' tiles land on few shards)
+        const uint32_t big = ks[0] <= ks[1] ? 0 : 1;
+        KMP_TRY(c, kmp_postings_set_shard_floor(kv[big]->ws, (uint64_t)(2 * 0.75 * plan.budget)));
+        KMP_TRY(c, kmp_postings_set_shard_floor(kv[1 - big]->ws, 0));
+    }
     uint64_t mcap = 0;
     double edge_ratio = 1.0;  // the largest edges / incidences of a pass so far (after the first)
     bool ratio_seen = false;
@@ -1310,8 +1318,10 @@ static int stream_passes(kmp_ctx* c, const kmp_pair_opts& o, const int* ks, uint
             kmp_postings* wsp[2] = {kv[0]->ws, kv[1]->ws};
             // edges <= incidences: size the arrays from the densest incidence rate seen times the
             // largest edges-per-incidence ratio seen (+10 %; an overflow reruns the pass)
+            // a growth takes a quarter of headroom: reallocating six multi-GB arrays (a synchronous
+            // free and a fresh allocation each) stalled the device for seconds per growth
             const double est = plan.density > 0 ? plan.density * plan.mass(a, b) * std::min(1.0, edge_ratio * 1.1) : 0.0;
-            if (est + 4096 > (double)mcap) mcap = (uint64_t)est + 4096;
+            if (est + 4096 > (double)mcap) mcap = std::max<uint64_t>((uint64_t)est + 4096, mcap + mcap / 4);
             for (int attempt = 0; attempt < 3; ++attempt) {
                 if (!mcap || !ln.mwk->p) mcap = std::max<uint64_t>(mcap, 1u << 20);
                 uint64_t cap3 = 0;
@@ -1464,6 +1474,7 @@ static int stream_passes(kmp_ctx* c, const kmp_pair_opts& o, const int* ks, uint
     for (uint32_t j = 0; j < nk; ++j) {
         (void)kmp_postings_set_reuse(kv[j]->ws, 0);
         (void)kmp_postings_set_timing(kv[j]->ws, 0);
+        (void)kmp_postings_set_shard_floor(kv[j]->ws, 0);
     }
     return rc;
 }

@@ -36,6 +36,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstdint>
+#include <chrono>
 #include <vector>
 
 #include "kmerpair.h"
@@ -2357,6 +2358,7 @@ struct Grow {
     hipError_t reserve(size_t m) {
         if (m <= n && p) return hipSuccess;
         g_grow_gen.fetch_add(1, std::memory_order_relaxed);
+        const auto t0 = std::chrono::steady_clock::now();
         if (p) (void)hipFree(p);
         p = nullptr;
         n = 0;
@@ -2364,8 +2366,13 @@ struct Grow {
         // every regrowth of a multi-GB buffer (a synchronous free + a fresh allocation) stalled the
         // device for up to seconds
         const size_t want = m > (size_t{1} << 26) ? m + m / 4 : std::max<size_t>(1, m);
+        static const bool dbg = getenv("KMP_DEBUG_GROW") != nullptr;
         hipError_t e = hipMalloc(&p, want * sizeof(T));
         if (e == hipSuccess) n = want;
+        if (dbg && want * sizeof(T) >= (64u << 20))
+            fprintf(stderr, "kmp: grow %p to %.1f MB (%zu B elements) in %.1f ms\n", (void*)this,
+                    want * sizeof(T) / 1e6, sizeof(T),
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
         return e;
     }
     void release() {
@@ -2388,6 +2395,7 @@ struct kmp_postings {
     bool last_heavy = false;    // ... with spilled frequent k-mers
     uint32_t last_ovf = 0;      // ... row blocks finished by the overflow sort
     uint64_t shard_cap = 0;     // capacity of each pair-key shard region
+    uint64_t shard_floor = 0;   // ... at least (kmp_postings_set_shard_floor: a stream's planned pass size)
     Grow<uint32_t> chunk_first;
     Grow<uint32_t> bp;          // bucket partition: H1 | P1 | R | C1 | H2 (see bp_level1)
     Grow<uint32_t> pt;          // row-block tail (pt_bufs)
@@ -2407,6 +2415,7 @@ struct kmp_postings {
     std::vector<unsigned long long> pend_key;
     Grow<unsigned long long> split_cur;  // k-mer split: per-destination send cursors
     std::vector<unsigned long long> split_shape;
+    bool split_heavy = false;  // k-mer split: this batch spills, its heavy path runs on every call
     unsigned pt_rb_max = 16;    // rows-per-block bound learned from overflowing row blocks
     uint32_t bp_J = 0;          // level-2 tiles per coarse bin ...
     uint32_t bp_J_min = 0;      // ... at least (learned from an overflowing bin)
@@ -3308,32 +3317,38 @@ __global__ void pt_ovf_stage_scored_kernel(const uint32_t* __restrict__ ovf, uin
 }
 
 // Sub-blocks (the fused multi-k tail): a row block above kPtCap keys — config 5 at k = 5, where one
-// protein pairs with ~10^5 later ones — is cut by the top bits of its local key (row in block, then
-// q) into nsub = 2^j sub-blocks of about kPtCap / 2 keys, each reduced in LDS like a row block, so
-// no device-wide sort of the pass's keys is needed.  One 1,024-thread workgroup per row block: count
-// the sub-block of every key in LDS, scan, write the sub-block descriptors, then scatter the keys
-// (an LDS cursor per sub-block) into keys2 at the same block offset.  A block that fits is one
-// sub-block (copied).  A sub-block still above kPtCap (a skewed q range) takes the overflow sort.
-constexpr uint32_t kSbThreads = 1024, kSbMaxLog = 12;
-__host__ __device__ inline unsigned pt_sub_log(uint32_t n, unsigned kbits) {
-    unsigned j = 0;
-    while (j < kSbMaxLog && j < kbits && ((uint64_t)(kPtCap / 2) << j) < n) ++j;
-    return n > kPtCap ? j : 0u;
+// protein pairs with ~10^5 later ones — is cut into sub-blocks of at most about kPtCap keys, each
+// reduced in LDS like a row block, so no device-wide sort of the pass's keys is needed.  One
+// 1,024-thread workgroup per row block: the keys are counted into nf fine bins over the block's
+// pair range in (row in block, q) order — the linear position rl * span + (q - qlo), q in
+// (rowbase, n) — the bins scanned, and sub-block j takes the bins whose first key lies in
+// [j * kSbChunk, (j + 1) * kSbChunk): a monotone cut (canonical order kept) whose pieces are
+// balanced whatever the q distribution (cutting by the key's top bits left late passes, whose q
+// all share their top bits, in one piece).  Descriptors: nf per block (the unused ones empty);
+// the keys scattered to keys2 at their bin's cursor.  A block that fits is one sub-block (copied);
+// a sub-block still above kPtCap (one bin above kPtCap - kSbChunk keys) takes the overflow sort.
+constexpr uint32_t kSbThreads = 1024, kSbMaxLog = 14, kSbChunk = kPtCap * 3 / 4;
+__host__ __device__ inline unsigned pt_sub_log(uint32_t n) {
+    if (n <= kPtCap) return 0;
+    unsigned j = 1;  // nf * kSbChunk >= 4n: a bin holds a quarter of a sub-block on average
+    while (j < kSbMaxLog && ((uint64_t)kSbChunk << j) < 4ull * n) ++j;
+    return j;
 }
 
 __global__ __launch_bounds__(kSbThreads) void pt_split_kernel(const uint32_t* __restrict__ keys,
                                                               const uint32_t* __restrict__ bst,
-                                                              const uint32_t* __restrict__ dbase, unsigned kbits,
+                                                              const uint32_t* __restrict__ dbase, PtGeom g,
+                                                              uint32_t n_prot, uint32_t row_end,
                                                               uint32_t* __restrict__ keys2,
                                                               uint32_t* __restrict__ dstart,
                                                               uint32_t* __restrict__ dsize,
                                                               uint32_t* __restrict__ drow) {
-    __shared__ uint32_t cnt[1u << kSbMaxLog];
+    __shared__ uint32_t cnt[1u << kSbMaxLog];  // per bin: count, then first key (local), then cursor
+    __shared__ uint32_t lst[1u << kSbMaxLog];  // per sub-block: first key (local)
     __shared__ uint32_t wave_tot[kSbThreads / 64];
     const uint32_t r = blockIdx.x, s0 = bst[r], n = bst[r + 1] - s0;
-    const unsigned lj = pt_sub_log(n, kbits);
-    const uint32_t ns = 1u << lj, d0 = dbase[r];
-    const unsigned sh = kbits - lj;
+    const unsigned lj = pt_sub_log(n);
+    const uint32_t nf = 1u << lj, d0 = dbase[r];
     if (lj == 0) {  // fits: one sub-block (the keys copied, so every sub-block reads keys2)
         for (uint32_t i = threadIdx.x; i < n; i += kSbThreads) keys2[s0 + i] = keys[s0 + i];
         if (threadIdx.x == 0) {
@@ -3343,20 +3358,40 @@ __global__ __launch_bounds__(kSbThreads) void pt_split_kernel(const uint32_t* __
         }
         return;
     }
-    for (uint32_t i = threadIdx.x; i < ns; i += kSbThreads) cnt[i] = 0;
+    const uint32_t rowbase = g.row0 + (r << g.rbits);
+    const uint32_t rows = min(1u << g.rbits, row_end > rowbase ? row_end - rowbase : 1u);
+    const uint32_t qlo = rowbase + 1;  // q > p >= rowbase
+    const uint64_t span = n_prot > qlo ? n_prot - qlo : 1u, range = (uint64_t)rows * span;
+    const unsigned rs = g.pbits + g.sbits;
+    const uint32_t qm = (1u << g.pbits) - 1;
+    auto bin = [&](uint32_t k) -> uint32_t {
+        const uint32_t q = (k >> g.sbits) & qm;
+        const uint64_t pos = (uint64_t)(k >> rs) * span + (q > qlo ? q - qlo : 0u);
+        return (uint32_t)min<uint64_t>(pos * nf / range, nf - 1);
+    };
+    for (uint32_t i = threadIdx.x; i < nf; i += kSbThreads) cnt[i] = 0;
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < n; i += kSbThreads) atomicAdd(&cnt[keys[s0 + i] >> sh], 1u);
+    for (uint32_t i = threadIdx.x; i < n; i += kSbThreads) atomicAdd(&cnt[bin(keys[s0 + i])], 1u);
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < ns; i += kSbThreads) {  // descriptors (before the scan rewrites cnt)
-        dsize[d0 + i] = cnt[i];
-        drow[d0 + i] = r;
+    lds_bins_scan<kSbThreads>(cnt, nf, wave_tot);  // cnt[i] = first key of bin i
+    // sub-block of bin i: cnt[i] / kSbChunk (monotone); sub-block j starts at the first bin whose
+    // sub-block is >= j (a skipped j — one bin above kSbChunk — is empty)
+    const uint32_t used = cnt[nf - 1] / kSbChunk + 1;
+    for (uint32_t i = threadIdx.x; i < nf; i += kSbThreads) {
+        const uint32_t sj = cnt[i] / kSbChunk;
+        for (uint32_t j = i ? cnt[i - 1] / kSbChunk + 1 : 0u; j <= sj; ++j) lst[j] = cnt[i];
     }
-    lds_bins_scan<kSbThreads>(cnt, ns, wave_tot);  // cnt[i] = first key of sub-block i
-    for (uint32_t i = threadIdx.x; i < ns; i += kSbThreads) dstart[d0 + i] = s0 + cnt[i];
+    for (uint32_t j = used + threadIdx.x; j < nf; j += kSbThreads) lst[j] = n;
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < n; i += kSbThreads) {
+    for (uint32_t j = threadIdx.x; j < nf; j += kSbThreads) {
+        const uint32_t a = lst[j], e = j + 1 < nf ? lst[j + 1] : n;
+        dstart[d0 + j] = s0 + a;
+        dsize[d0 + j] = e - a;
+        drow[d0 + j] = r;
+    }
+    for (uint32_t i = threadIdx.x; i < n; i += kSbThreads) {  // a bin's keys stay inside its sub-block
         const uint32_t k = keys[s0 + i];
-        keys2[s0 + atomicAdd(&cnt[k >> sh], 1u)] = k;
+        keys2[s0 + atomicAdd(&cnt[bin(k)], 1u)] = k;
     }
 }
 
@@ -3686,6 +3721,7 @@ BucketArgs bucket_args(kmp_postings* ws, const StepCfg& c, bool spill) {
 
 // buffers of one step (reserved before any launch, so a capture allocates nothing)
 int step_reserve(kmp_postings* ws, const StepCfg& c, const PtGeom& g, hipStream_t st) {
+    if (ws->shard_cap < ws->shard_floor) ws->shard_cap = ws->shard_floor;
     const uint64_t total = ws->shard_cap * kShards;
     PG(ws->keys.reserve(c.slots));
     PG(ws->sorted.reserve(c.slots));
@@ -4384,11 +4420,10 @@ int tail_multi(kmp_postings* const* ws, uint32_t nk, const StepCfg& c, const uin
     std::vector<uint32_t> hb(g.nrb + 1), hd(g.nrb + 1);
     PG(hipMemcpyAsync(hb.data(), b.bst, (g.nrb + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     PG(hipStreamSynchronize(st));
-    const unsigned kbits = g.pbits + g.sbits + g.rbits;
     uint32_t nd = 0;
     for (uint32_t r = 0; r < g.nrb; ++r) {
         hd[r] = nd;
-        nd += 1u << pt_sub_log(hb[r + 1] - hb[r], kbits);
+        nd += 1u << pt_sub_log(hb[r + 1] - hb[r]);
     }
     hd[g.nrb] = nd;
     PG(w0->k2.reserve(total));
@@ -4399,7 +4434,8 @@ int tail_multi(kmp_postings* const* ws, uint32_t nk, const StepCfg& c, const uin
              *dbase = deoff + nd + 1;
     PG(w0->ovf.reserve((uint64_t)std::max(nd, g.nrb) + 1));  // the sub-blocks the reduce lists
     PG(hipMemcpyAsync(dbase, hd.data(), (g.nrb + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-    pt_split_kernel<<<g.nrb, kSbThreads, 0, st>>>(keys32, b.bst, dbase, kbits, w0->k2.p, dstart, dsize, drow);
+    pt_split_kernel<<<g.nrb, kSbThreads, 0, st>>>(keys32, b.bst, dbase, g, c.n, c.ranged ? c.row_hi : c.n,
+                                                  w0->k2.p, dstart, dsize, drow);
     const BlkSrc bs{dstart, dsize, drow};
     if (g.kbit)
         pt_reduce_scored_kernel<true><<<nd, kPtRThreads, 0, st>>>(w0->k2.p, bs, g, w0->flags.p, w0->ovf.p, stage_p,
@@ -4711,7 +4747,8 @@ __global__ void split_clear_kernel(unsigned long long* __restrict__ dcursor, uin
 __global__ void split_finish_kernel(const unsigned long long* __restrict__ gstats,
                                     const uint32_t* __restrict__ wflags, uint64_t sc,
                                     const unsigned long long* __restrict__ dcursor, uint32_t parts, uint64_t cap,
-                                    uint32_t* __restrict__ out, unsigned long long* __restrict__ stats) {
+                                    uint32_t* __restrict__ out, unsigned long long* __restrict__ stats,
+                                    int heavy_done) {
     const uint32_t t = threadIdx.x;
     if (t < kStN) {
         unsigned long long v = 0;
@@ -4730,7 +4767,7 @@ __global__ void split_finish_kernel(const unsigned long long* __restrict__ gstat
         for (uint32_t d = 0; d < parts; ++d) part = max(part, dcursor[d]);
         const uint32_t clamp = 0xFFFFFFFFu;
         out[KMP_SPLIT_CLASS] = wflags[kFlClass];
-        out[KMP_SPLIT_HEAVY] = spill != 0;
+        out[KMP_SPLIT_HEAVY] = spill != 0 && !heavy_done;  // spilled with the heavy path off: rerun with it on
         out[KMP_SPLIT_MAX_PART] = (uint32_t)min<unsigned long long>(part, clamp);
         out[KMP_SPLIT_MAX_SHARD] = (uint32_t)min<unsigned long long>(shard, clamp);
         out[KMP_SPLIT_BIN_TILES] = wflags[kFlBin] ? wflags[kFlBinTiles] : 0u;
@@ -4800,6 +4837,12 @@ int kmp_postings_set_partition(kmp_postings* ws, int mode) {
 int kmp_postings_last_partition(const kmp_postings* ws) {
     if (!ws || !ws->last_bucketed) return -1;
     return ws->cur_used ? KMP_PARTITION_CURSOR : KMP_PARTITION_COUNT;
+}
+
+int kmp_postings_set_shard_floor(kmp_postings* ws, uint64_t keys) {
+    if (!ws) return KMP_EINVAL;
+    ws->shard_floor = keys ? keys / kShards + keys / kShards / 4 + 256 : 0;
+    return KMP_OK;
 }
 
 int kmp_postings_set_reuse(kmp_postings* ws, int enable) {
@@ -4997,8 +5040,10 @@ int kmp_dev_split_expand(kmp_postings* ws, const uint8_t* d_res, const uint64_t*
         ws->bp_J_min = 0;
         ws->cur_on = ws->cur_mode;
         ws->shape.clear();
+        ws->split_heavy = false;
     }
     if (learn) {  // the last call's flags, reduced over the ranks: every rank grows the same way
+        if (learn[KMP_SPLIT_HEAVY]) ws->split_heavy = true;  // a rank spilled: the heavy path from now on
         if (learn[KMP_SPLIT_MAX_SHARD] > ws->shard_cap)
             ws->shard_cap = learn[KMP_SPLIT_MAX_SHARD] + learn[KMP_SPLIT_MAX_SHARD] / 32 + 256;
         if (learn[KMP_SPLIT_BIN_TILES]) ws->bp_J_min = std::max(ws->bp_J_min, learn[KMP_SPLIT_BIN_TILES] + 2);
@@ -5033,11 +5078,12 @@ int kmp_dev_split_expand(kmp_postings* ws, const uint8_t* d_res, const uint64_t*
     SplitRows rows{};
     rows.parts = parts;
     kmp_row_split(n, parts, rows.start);
-    auto enqueue = [&](hipStream_t s) -> int {
-        int rc = KMP_OK;
-        if (ws->bin_hi > ws->bin_lo) rc = enqueue_front(ws, make_keys, c, true, s);
-        else step_clear_kernel<<<1, 256, 0, s>>>(ws->flags.p, ws->bstats.p);  // no bins: nothing to expand
-        if (rc != KMP_OK) return rc;
+    auto front = [&](hipStream_t s) -> int {
+        if (ws->bin_hi > ws->bin_lo) return enqueue_front(ws, make_keys, c, true, s);
+        step_clear_kernel<<<1, 256, 0, s>>>(ws->flags.p, ws->bstats.p);  // no bins: nothing to expand
+        return KMP_OK;
+    };
+    auto route = [&](hipStream_t s, int heavy_done) -> int {
         split_clear_kernel<<<1, kSplitMax, 0, s>>>(ws->split_cur.p, parts);
         const unsigned long long* cursor = ws->bstats.p + kRbCursor;
         split_route_kernel<<<dim3((uint32_t)((ws->shard_cap + kRtTile - 1) / kRtTile), kShards), kRtThreads, 0, s>>>(
@@ -5045,9 +5091,45 @@ int kmp_dev_split_expand(kmp_postings* ws, const uint8_t* d_res, const uint64_t*
         split_pad_kernel<<<dim3((uint32_t)std::min<uint64_t>((cap + 1023) / 1024, 256), parts), 256, 0, s>>>(
             d_send, cap, ws->split_cur.p);
         split_finish_kernel<<<1, 64, 0, s>>>(ws->bstats.p, ws->flags.p, ws->shard_cap, ws->split_cur.p, parts, cap,
-                                              d_flags, d_stats);
+                                              d_flags, d_stats, heavy_done);
         PG(hipGetLastError());
         return KMP_OK;
+    };
+    if (ws->split_heavy) {
+        // frequent k-mers (vertex.rs:59-140 at k = 5): the rank's front, one read-back, its spill
+        // compacted, planned and expanded by the heavy path into the same shard regions (the heavy
+        // pairs of the rank's k-mers, all rows), then routed like the light keys.  The spill regions
+        // are the rank's own, so a spill overflow reruns the front here; every other capacity is
+        // reported in the flags and grown identically on every rank.  Host-synchronous.
+        int rc = KMP_OK;
+        for (int attempt = 0; attempt < 4; ++attempt) {
+            if ((rc = step_reserve(ws, c, g, st)) != KMP_OK) break;
+            if ((rc = front(st)) != KMP_OK) break;
+            step_pack_kernel<<<1, 256, 0, st>>>(ws->bstats.p, ws->flags.p, nullptr, ws->hrb);
+            PG(hipStreamSynchronize(st));
+            const unsigned long long* rb = ws->hrb;
+            unsigned long long acc[kStN], most, n_inc, spill_most, spill_total;
+            sum_stats(rb, acc, &most, &n_inc, &spill_most, &spill_total);
+            if (spill_most > ws->spill_cap) {
+                ws->spill_cap = spill_most + spill_most / 8 + 1024;
+                continue;
+            }
+            // a bin or cursor-region overflow: the flags rerun the step, no heavy work on it
+            if (spill_total && !rb[kRbFlagBin] && !(rb[kRbFlagCur] && ws->cur_used)) {
+                ws->heavy_ready = ws->hcur_valid = false;  // this call's front
+                ws->h_segs = rb[kRbSegs];
+                ws->h_segmax = rb[kRbSegMax];
+                if ((rc = heavy_phase(ws, c, spill_total, true, st)) != KMP_OK) break;
+            }
+            rc = route(st, 1);
+            break;
+        }
+        ws->bin_lo = ws->bin_hi = 0;
+        return rc;
+    }
+    auto enqueue = [&](hipStream_t s) -> int {
+        const int rc = front(s);
+        return rc != KMP_OK ? rc : route(s, 0);
     };
     const std::vector<unsigned long long> key = {
         n, slots, (unsigned long long)k, heavy_df, (unsigned long long)require_class_diff, part, parts, cap,

@@ -284,7 +284,8 @@ class DevicePipeline:
         """Multi-GPU k-mer split, phase 1 (kmp_dev_split_expand): this rank's share of the k-mers
         grouped and expanded, pair keys routed to their row owners in `send` (parts regions of cap
         keys, int64); flags (int32[KMP_SPLIT_FLAGS]) and stats (int64[8]) on the stream.  No host
-        synchronisation.  learn: the last call's flags reduced over the ranks (or None)."""
+        synchronisation (one with the heavy path on).  learn: the last call's flags reduced over the
+        ranks (or None); HEAVY in them turns the rank's heavy path on."""
         slots = int(lib().kmp_set_capacity(self.n, self.total))
         lp = None if learn is None else (C.c_uint32 * _lib.KMP_SPLIT_FLAGS)(*[int(x) for x in learn])
         check(lib().kmp_dev_split_expand(self._workspace(), _p(self.res), _p(self.off), _p(self.cls), self.n, self.k,

@@ -23,9 +23,12 @@ instead of repeating the grouping on every rank: rank r keys every window but ke
 k-mers of its share of the bucket hash range, groups and expands them, and routes each pair key
 to the rank owning the pair's row (kmp_dev_split_expand); one all-to-all of equal, padded splits
 moves the pair keys (42 MB in total per step at config 4, about 5 MB per rank at 8 ranks); every
-rank reduces its rows (kmp_dev_split_edges).  The row split stays the fallback for batches whose
-frequent k-mers spill (the heavy path is single-rank) and the bounded-memory mode: at config 5
-Σ C(df,2) ≈ 10^10-10^11 pair keys would cross the links, far more than recomputing the grouping.
+rank reduces its rows (kmp_dev_split_edges).  Frequent k-mers stay on the k-mer split: a rank
+whose share spills raises KMP_SPLIT_HEAVY, the step reruns with the heavy path on in every rank
+(each compacts, plans and expands the spill of its own k-mers into the keys it routes).  The row
+split stays the fallback for class ids wider than the key's field and the bounded-memory mode: at
+config 5 Σ C(df,2) ≈ 10^10-10^11 pair keys would cross the links, far more than recomputing the
+grouping.
 """
 from __future__ import annotations
 
@@ -127,8 +130,9 @@ def kmer_split_step(pipe, rank: int, world: int, group=None, min_shared: int = 1
     """One multi-GPU step of the k-mer split: expand this rank's k-mers, exchange the pair keys by
     row owner (all-to-all), reduce this rank's rows.  Every rank ends holding the canonical edges
     of its row range in pipe.ep/eq/ew (rank order = canonical order) and returns their count; with
-    gather, rank 0 also receives every rank's block behind its own and returns the total.  Falls
-    back to the row split (distributed_step) when the batch spills frequent k-mers.  timings: a
+    gather, rank 0 also receives every rank's block behind its own and returns the total.  A batch
+    that spills frequent k-mers reruns with the heavy path on (KMP_SPLIT_HEAVY in the reduced flags);
+    one whose class ids overflow the key falls back to the row split (distributed_step).  timings: a
     list to append this rank's (expand, exchange, edges) milliseconds to (CUDA events on the
     current stream, which the library's stages and the collectives are ordered with)."""
     st = state if state is not None else _pipe_state(pipe)
@@ -164,10 +168,10 @@ def kmer_split_step(pipe, rank: int, world: int, group=None, min_shared: int = 1
         if ev:
             ev[3].record()
         fl = [int(x) for x in flags.cpu().tolist()]  # the step's one flag read-back
-        if fl[_lib.KMP_SPLIT_CLASS] or fl[_lib.KMP_SPLIT_HEAVY]:
+        if fl[_lib.KMP_SPLIT_CLASS]:
             st.row_split = True
             return distributed_step(pipe, rank, world, group, min_shared, require_class_diff)
-        if fl[_lib.KMP_SPLIT_RERUN]:
+        if fl[_lib.KMP_SPLIT_RERUN] or fl[_lib.KMP_SPLIT_HEAVY]:  # HEAVY: the heavy path on every rank
             st.reruns += 1
             st.learn = fl
             if fl[_lib.KMP_SPLIT_MAX_PART] > st.cap:
