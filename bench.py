@@ -162,13 +162,16 @@ def stage_bytes(n_res, n_inc, n_edges, n_uniq, n_win):
 def pmc_traffic(stage: str):
     """HBM bytes per step of `stage` from the newest committed PMC table (profiles/r*_pmc_traffic.json,
     made by tools/pmc_traffic.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of
-    this bench on config 3, FETCH_SIZE doubled per the gfx950 note in MI355X_MICROARCH.md)."""
+    this bench on config 3; FETCH_SIZE divided by its measured factor, 0.5 at 4, 8 and 16 B per lane,
+    profiles/r03_pmc_calib.json).  Returns (corrected bytes, raw counter bytes or None, source)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
     if not files:
-        return None, None
+        return None, None, None
     st = json.load(open(files[-1]))["stages"].get(stage)
-    return (st["bytes"] if st else None), os.path.relpath(files[-1], ROOT)
+    if not st:
+        return None, None, os.path.relpath(files[-1], ROOT)
+    return st["bytes"], st.get("raw_bytes"), os.path.relpath(files[-1], ROOT)
 
 
 def config5_cpu_baseline(threads):
@@ -456,10 +459,11 @@ def main():
                       for s in stage_ms}
             dom = max(stage_ms, key=stage_ms.get)
             ach = stages[dom]["GBs"]
-            traffic, source = (pmc_traffic(dom) if args.config == "config3" and args.engine == "residues"
-                               else (None, None))
+            traffic, traffic_raw, source = (pmc_traffic(dom) if args.config == "config3" and args.engine == "residues"
+                                            else (None, None, None))
             out["roofline"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                               "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": source,
+                               "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "traffic_raw": traffic_raw,
+                               "traffic_source": source,
                                "traffic_over_alg": traffic / byts[dom] if traffic else None, "kernel": dom,
                                "kernel_ms": stage_ms[dom], "alg_bytes_per_launch": byts[dom],
                                "layout": pipe.last_layout(), "tail": "rows", "stages": stages,

@@ -8,6 +8,15 @@ import json
 import sys
 
 
+def width_of(name):
+    """access width of a calibration kernel: read_kernel<unsigned int> / <HIP_vector_type<unsigned int, 2u>> / 4u"""
+    if "2u>" in name:
+        return 8
+    if "4u>" in name:
+        return 16
+    return 4
+
+
 def per_kernel(path):
     out = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
@@ -22,12 +31,12 @@ def main():
     res = {"bytes_per_dispatch": nbytes, "read": {}, "write": {}}
     for name, vals in fetch.items():
         if name.startswith("read_kernel"):
-            width = {"unsigned int": 4, "uint2": 8, "uint4": 16}[name[name.index("<") + 1:-1]]
+            width = width_of(name)
             res["read"][width] = {"FETCH_SIZE_factor": sorted(vals)[len(vals) // 2] / nbytes,
                                   "dispatches": len(vals)}
     for name, vals in write.items():
         if name.startswith("write_kernel"):
-            width = {"unsigned int": 4, "uint2": 8, "uint4": 16}[name[name.index("<") + 1:-1]]
+            width = width_of(name)
             res["write"][width] = {"WRITE_SIZE_factor": sorted(vals)[len(vals) // 2] / nbytes,
                                    "dispatches": len(vals)}
     print(json.dumps(res, indent=1))

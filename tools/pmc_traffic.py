@@ -1,7 +1,9 @@
 """Per-kernel HBM traffic from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE; KiB per
-dispatch).  gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE counts half the bytes of a
-wide streaming read, so it is doubled; WRITE_SIZE is taken as is.
-Usage: python tools/pmc_traffic.py FETCH.csv WRITE.csv [calls_per_step]"""
+dispatch).  gfx950 correction: FETCH_SIZE counts half of the bytes read, WRITE_SIZE all of them
+— measured at 4, 8 and 16 B per lane against a known byte count (tools/pmc_calib.hip,
+profiles/r03_pmc_calib.json; MI355X_MICROARCH.md §HBM states it for 16 B) — so reads are divided
+by the calibrated factor (0.5) and writes taken as is.  Both raw and corrected bytes are written.
+Usage: python tools/pmc_traffic.py FETCH.csv WRITE.csv [out.json]"""
 import collections
 import csv
 import json
@@ -18,16 +20,30 @@ def load(path):
     return out
 
 
+def calib():
+    """(read factor, write factor) from the committed calibration (8-B-per-lane lines; every width
+    measured the same)"""
+    import os
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "r03_pmc_calib.json")
+    try:
+        c = json.load(open(path))
+        return c["read"]["8"]["FETCH_SIZE_factor"], c["write"]["8"]["WRITE_SIZE_factor"]
+    except (OSError, KeyError, ValueError):
+        return 0.5, 1.0
+
+
 def main():
     fetch, write = load(sys.argv[1]), load(sys.argv[2])
+    rf, wf = calib()
     rows = []
     for key in sorted(set(fetch) | set(write), key=lambda k: -(sum(fetch.get(k, [0])) + sum(write.get(k, [0])))):
         f, w = fetch.get(key, []), write.get(key, [])
         n = max(len(f), len(w))
-        fb = 2.0 * sum(f) / max(1, len(f))
-        wb = sum(w) / max(1, len(w))
+        fraw = sum(f) / max(1, len(f))
+        wraw = sum(w) / max(1, len(w))
+        fb, wb = fraw / rf, wraw / wf
         rows.append({"kernel": key[0], "grid": key[1], "dispatches": n, "read_bytes": fb, "write_bytes": wb,
-                     "bytes": fb + wb})
+                     "bytes": fb + wb, "raw_read_bytes": fraw, "raw_write_bytes": wraw, "raw_bytes": fraw + wraw})
     print(f"{'kernel':<52} {'grid':>10} {'disp':>5} {'read MB':>9} {'write MB':>9}")
     for r in rows[:20]:
         print(f"{r['kernel'][:52]:<52} {r['grid']:>10} {r['dispatches']:>5} {r['read_bytes']/1e6:>9.1f} "
@@ -53,18 +69,20 @@ def main():
             return "group_expand"
         return by_kernel.get(k)
 
-    stages = collections.defaultdict(lambda: {"read_bytes": 0.0, "write_bytes": 0.0})
+    stages = collections.defaultdict(lambda: {"read_bytes": 0.0, "write_bytes": 0.0, "raw_bytes": 0.0})
     for r in rows:
         st = stage(r)
         if st:
             per_step = r["dispatches"] / calls
             stages[st]["read_bytes"] += r["read_bytes"] * per_step
             stages[st]["write_bytes"] += r["write_bytes"] * per_step
+            stages[st]["raw_bytes"] += r["raw_bytes"] * per_step
     for st in stages.values():
         st["bytes"] = st["read_bytes"] + st["write_bytes"]
     print("per-step stage traffic (MB):", {k: round(v["bytes"] / 1e6, 1) for k, v in stages.items()})
     if len(sys.argv) > 3:
-        json.dump({"calls": calls, "correction": "FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; KiB counters",
+        json.dump({"calls": calls, "correction": f"FETCH_SIZE / {rf:.4f}, WRITE_SIZE / {wf:.4f} "
+                   "(profiles/r03_pmc_calib.json); KiB counters; raw_* uncorrected",
                    "stages": stages, "kernels": rows}, open(sys.argv[3], "w"), indent=1)
 
 

@@ -892,8 +892,9 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
     // element, by the partners after i, measured 5 % slower at config 1).
     uint32_t cnt[kE];
     bool gd[kE];
-    constexpr bool kMask = !kRows && kThreads <= 256;  // the large kernel measured slower with it (74 -> 80 us, config 1)
-    auto mask_mode = [&](int e) { return kMask && !gd[e] && en[e] - s[e] <= 33u; };
+    constexpr bool kMask = kThreads <= 256;  // the large kernel measured slower with it (74 -> 80 us, config 1)
+    // kRows: bit t = position s + t (every partner of a larger protein, anywhere in the group)
+    auto mask_mode = [&](int e) { return kMask && !gd[e] && en[e] - s[e] <= (kRows ? 32u : 33u); };
     uint32_t st_sum = single, st_dist = single, st_rep = 0, st_cdf2 = 0, st_max = single ? 1u : 0u, st_heavy = 0,
              mine = 0;
 #pragma unroll
@@ -915,7 +916,9 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
                     if (gd[e] && is_dup(j)) continue;
                     f += gd[e];
                     const uint32_t lj = Bl[j];
-                    c += emit && (lj >> cb) > p && (!a.require_diff || ((lj ^ xl[e]) & cmask));
+                    const bool k = emit && (lj >> cb) > p && (!a.require_diff || ((lj ^ xl[e]) & cmask));
+                    c += k;
+                    if (kMask && j - s[e] < 32u) bits |= (uint32_t)k << (j - s[e]);
                 }
         } else if (!gd[e]) {
             f = en[e] - s[e];
@@ -1012,8 +1015,9 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
                 return kScore ? pk << a.sb | sfield : pk;
             };
             if (mask_mode(e)) {
+                const uint32_t base = kRows ? s[e] : i + 1;
                 for (uint32_t m = cnt[e]; m; m &= m - 1) {
-                    const uint32_t q = Bl[i + 1 + __builtin_ctz(m)] >> cb;
+                    const uint32_t q = Bl[base + __builtin_ctz(m)] >> cb;
                     put(pkey(q));
                 }
                 continue;
@@ -1075,7 +1079,7 @@ __global__ __launch_bounds__(kThreads) void bucket_large_kernel(BucketArgs a) {
 //      cursor reservation place the pair keys p_i * mul + p_j in the shard regions the bucket
 //      kernels fill.  A k-mer of df 10^4 is ~400 tiles: no workgroup walks a long posting list.
 constexpr uint32_t kHvTile = 4096, kHvThreads = 256, kHvPer = kHvTile / kHvThreads;
-constexpr uint32_t kHvI = 256, kHvJ = 2048, kHvJWrite = 256;
+constexpr uint32_t kHvI = 256, kHvJ = 256, kHvMW = kHvJ / 32;
 constexpr uint32_t kHvSpread = 64 * 256;  // a tile with this many pairs spreads them over the shards
 // flat tiles (class order, every pair kept, a k-mer of at most kHvFlatRuns class runs): the
 // k-mer's cross-class pairs (row of run r, any element past r's end) numbered run by run, row by
@@ -1406,6 +1410,7 @@ __global__ __launch_bounds__(kHvI) void heavy_expand_kernel(const uint32_t* __re
                                                             uint32_t sor) {
     __shared__ uint32_t J[kHvJ];
     __shared__ uint32_t s_ex[kHvI + 1], s_js[kHvI], s_p[kHvI];
+    __shared__ uint32_t s_m[kHvI * kHvMW];  // filtered tile: each row's kept partners (bit j - j0)
     __shared__ unsigned long long s_sb[kShards];  // spread tile: shard base minus its first output
     __shared__ uint32_t f_s[kHvFlatRuns], f_e[kHvFlatRuns];  // flat tile: the k-mer's runs (local)
     __shared__ unsigned long long f_c[kHvFlatRuns + 1];       // ... and their first pair's index
@@ -1526,7 +1531,22 @@ __global__ __launch_bounds__(kHvI) void heavy_expand_kernel(const uint32_t* __re
         };
         uint32_t c = 0;
         if (test_cls || test_row) {
-            for (uint32_t j = js; j < j1; ++j) c += keep(J[j - j0]);
+            // the row's kept partners as a bit mask over the chunk (hj <= kHvJ): the emit below
+            // writes the tile's output coalesced (a row writing its own run, one lane per row, cost
+            // one memory transaction per key)
+            uint32_t* mrow = s_m + threadIdx.x * kHvMW;
+#pragma unroll
+            for (uint32_t w = 0; w < kHvMW; ++w) {
+                uint32_t bits = 0;
+                const uint32_t jw = j0 + w * 32;
+                if (jw < j1 && jw + 32 > js)
+                    for (uint32_t t = 0; t < 32; ++t) {
+                        const uint32_t j = jw + t;
+                        if (j >= js && j < j1 && keep(J[j - j0])) bits |= 1u << t;
+                    }
+                mrow[w] = bits;
+                c += __popc(bits);
+            }
         } else {
             c = js < j1 ? j1 - js : 0u;
         }
@@ -1554,16 +1574,41 @@ __global__ __launch_bounds__(kHvI) void heavy_expand_kernel(const uint32_t* __re
         }
         __syncthreads();
         unsigned long long* dst = out + (uint64_t)shard * shard_cap;
-        if (test_cls || test_row) {  // a filtered row: its kept partners in turn
-            if (c) {
-                unsigned long long pos = sbase + excl;
-                for (uint32_t j = js; j < j1; ++j) {
-                    const uint32_t xj = J[j - j0];
-                    if (!keep(xj)) continue;
-                    const uint32_t pj = xj >> cb;
-                    if (pos < shard_cap) dst[pos] = mk(pi, pj);
-                    ++pos;
+        if (test_cls || test_row) {
+            // filtered tile: output o of row i (the last with s_ex[i] <= o) is the row's
+            // (o - s_ex[i])-th kept partner, selected from its mask; consecutive lanes write
+            // consecutive keys
+            s_ex[threadIdx.x] = excl;
+            s_p[threadIdx.x] = pi;
+            if (threadIdx.x == 0) s_ex[kHvI] = total;
+            __syncthreads();
+            uint32_t i = 0, hi = kHvI;
+            if (threadIdx.x < total) {
+                while (i + 1 < hi) {
+                    const uint32_t mid = (i + hi) >> 1;
+                    if (s_ex[mid] <= threadIdx.x) i = mid;
+                    else hi = mid;
                 }
+            }
+            for (uint32_t o = threadIdx.x; o < total; o += kHvI) {
+                while (s_ex[i + 1] <= o) ++i;
+                uint32_t rk = o - s_ex[i], w = 0, x = s_m[i * kHvMW];
+                while (rk >= (uint32_t)__popc(x)) {  // the word holding it
+                    rk -= __popc(x);
+                    x = s_m[i * kHvMW + ++w];
+                }
+                uint32_t bit = 0;  // the rk-th set bit of x
+                for (uint32_t half = 16; half; half >>= 1) {
+                    const uint32_t low = __popc(x & ((1u << half) - 1));
+                    if (rk >= low) {
+                        rk -= low;
+                        x >>= half;
+                        bit += half;
+                    }
+                }
+                const uint32_t pj = J[w * 32 + bit] >> cb;
+                const unsigned long long pos = sbase + o;
+                if (pos < shard_cap) dst[pos] = mk(s_p[i], pj);
             }
         } else {
             // every partner kept: the tile's output [0, total) in coalesced order, output o of row
@@ -2743,6 +2788,9 @@ struct PtGeom {
     uint32_t row0;          // first row (a pass's or rank's row range)
     uint64_t flat_n;        // nonzero: one region of flat_n keys with kNoKey padding (no cursors)
     uint32_t min_shared;    // runs with w < min_shared are dropped
+    uint32_t nprot;         // proteins (q < nprot): the pair range of a row block (pt_bin_sort)
+    uint32_t rowend;        // the call's last row + 1
+    int binsort;            // the reduce sorts by bins (pt_bin_sort), else the block radix sort
 };
 
 // The blocks a reduce runs over: row blocks (size == nullptr: block r is keys [start[r], start[r+1])
@@ -2903,11 +2951,111 @@ __global__ __launch_bounds__(kPtThreads) void pt_scatter_kernel(const unsigned l
 template <uint32_t kE>
 using PtSort = rocprim::block_radix_sort<uint32_t, kPtRThreads, kE>;
 
+// Binned sort of a block's n keys (the row-block reduce; replaces a block radix sort over all
+// pbits + rbits (+ sbits) key bits, 6-8 passes of rank + scatter).  A run only needs its pair's
+// keys adjacent and the pairs in (row, q) order, so the keys are counted into nb >= 2n bins over
+// the block's own pair range — the monotone position rl * span + (q - qlo), q in (rowbase, nprot),
+// between its min and max (a sub-block covers a slice of it) — scattered to their bin's slice of
+// S, and each bin (half a key on average) insertion-sorted by its thread on the pair (key >> sbits;
+// the score field below it stays in arrival order).  A range of at most nb positions makes every
+// bin one pair: no sort at all.  A bin above kBinMax keys (a skewed block) makes the caller fall
+// back to the radix sort (k is untouched then).  On success k holds the sorted keys blocked
+// (thread t: ranks t * kE + e), the padding (all ones) last.
+constexpr uint32_t kBinMax = 64, kBinCap = 8192;
+struct PtBinLds {
+    uint32_t H[kBinCap];  // per bin: count, then first rank
+    uint32_t S[kPtCap];   // the keys by bin
+};
+template <uint32_t kE>
+__device__ __forceinline__ bool pt_bin_sort(uint32_t (&k)[kE], uint32_t n, const PtGeom& g, uint32_t rowbase,
+                                            PtBinLds& b, uint32_t* red, uint32_t* s_flag, uint32_t* wave_tot) {
+    constexpr uint32_t kT = kPtRThreads, kW = kT / 64;
+    const unsigned sb = g.sbits, rs = g.pbits + g.sbits;
+    const uint32_t qm = (1u << g.pbits) - 1, qlo = rowbase + 1;
+    const uint32_t span = g.nprot > qlo ? g.nprot - qlo : 1u;
+    auto pos = [&](uint32_t x) {
+        const uint32_t q = (x >> sb) & qm;
+        return (x >> rs) * span + (q > qlo ? q - qlo : 0u);
+    };
+    uint32_t lo = 0xFFFFFFFFu, hi = 0;
+#pragma unroll
+    for (uint32_t e = 0; e < kE; ++e)
+        if (threadIdx.x + e * kT < n) {
+            const uint32_t v = pos(k[e]);
+            lo = min(lo, v);
+            hi = max(hi, v);
+        }
+    for (int off = 32; off > 0; off >>= 1) {
+        lo = min(lo, (uint32_t)__shfl_xor(lo, off));
+        hi = max(hi, (uint32_t)__shfl_xor(hi, off));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[threadIdx.x >> 6] = lo;
+        red[kW + (threadIdx.x >> 6)] = hi;
+    }
+    uint32_t nb = 2;
+    while (nb < 2 * n && nb < kBinCap) nb <<= 1;
+    for (uint32_t i = threadIdx.x; i < nb; i += kT) b.H[i] = 0;
+    if (threadIdx.x == 0) *s_flag = 0;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t w = 0; w < kW; ++w) {
+        lo = min(lo, red[w]);
+        hi = max(hi, red[kW + w]);
+    }
+    const uint64_t range = (uint64_t)hi - lo + 1;
+    const bool exact = range <= nb;  // one pair per bin
+    uint32_t br[kE];                 // bin | rank in it << 16 (bins, ranks < 2^14)
+#pragma unroll
+    for (uint32_t e = 0; e < kE; ++e) {
+        br[e] = 0;
+        if (threadIdx.x + e * kT < n) {
+            const uint32_t v = pos(k[e]) - lo;
+            const uint32_t bin = exact ? v : (uint32_t)((uint64_t)v * nb / range);
+            br[e] = bin | atomicAdd(&b.H[bin], 1u) << 16;
+        }
+    }
+    __syncthreads();
+    lds_bins_scan<kT>(b.H, nb, wave_tot);  // H[bin] = its first rank
+#pragma unroll
+    for (uint32_t e = 0; e < kE; ++e)
+        if (threadIdx.x + e * kT < n) b.S[b.H[br[e] & 0xFFFFu] + (br[e] >> 16)] = k[e];
+    __syncthreads();
+    if (!exact)
+        for (uint32_t i = threadIdx.x; i < nb; i += kT) {
+            const uint32_t a = b.H[i], e = i + 1 < nb ? b.H[i + 1] : n;
+            if (e - a < 2) continue;
+            if (e - a > kBinMax) {
+                *s_flag = 1;
+                continue;
+            }
+            for (uint32_t j = a + 1; j < e; ++j) {
+                const uint32_t x = b.S[j], xp = x >> sb;
+                uint32_t t = j;
+                while (t > a && (b.S[t - 1] >> sb) > xp) {
+                    b.S[t] = b.S[t - 1];
+                    --t;
+                }
+                b.S[t] = x;
+            }
+        }
+    __syncthreads();
+    if (*s_flag) return false;  // (uniform) the radix sort on the untouched k
+#pragma unroll
+    for (uint32_t e = 0; e < kE; ++e) {
+        const uint32_t rank = threadIdx.x * kE + e;
+        k[e] = rank < n ? b.S[rank] : 0xFFFFFFFFu;
+    }
+    __syncthreads();  // S read before the caller reuses the LDS
+    return true;
+}
+
 union PtReduceLds {
     typename PtSort<2>::storage_type s2;
     typename PtSort<4>::storage_type s4;
     typename PtSort<8>::storage_type s8;
     typename PtSort<16>::storage_type s16;
+    PtBinLds b;
     uint32_t hs[kPtCap + 1];  // rank of each run's first key
 };
 
@@ -2926,7 +3074,8 @@ __device__ __forceinline__ void pt_reduce_block(PtReduceLds& u, typename PtSort<
         k[e] = i < n ? keys[s0 + i] : 0xFFFFFFFFu;
     }
     // bits [0, pbits + rbits] (one above the key): the padding (all ones) sorts after every key
-    PtSort<kE>().sort(k, st, 0, g.pbits + g.rbits + 1);  // blocked: thread t holds ranks t*kE + e
+    if (!g.binsort || !pt_bin_sort<kE>(k, n, g, g.row0 + (r << g.rbits), u.b, last, last + 2 * kPtRThreads / 64, wave_tot))
+        PtSort<kE>().sort(k, st, 0, g.pbits + g.rbits + 1);  // blocked: thread t holds ranks t*kE + e
     last[threadIdx.x] = k[kE - 1];
     __syncthreads();
     const uint32_t rank0 = threadIdx.x * kE;
@@ -3037,10 +3186,10 @@ struct PtScoredLds {
         typename PtSort<4>::storage_type s4;
         typename PtSort<8>::storage_type s8;
         typename PtSort<16>::storage_type s16;
+        PtBinLds b;
         struct {
-            uint32_t hs[kPtCap + 1];  // rank of each run's first key
+            uint32_t hs[kPtCap + 1];  // rank of each run's first key | k-bit scan at it << 16 (kKbit)
             uint32_t ps[kPtCap + 1];  // score scan at each run's head
-            uint32_t pk[kKbit ? kPtCap + 1 : 1];  // k-bit scan at each run's head
         } r;
     };
 };
@@ -3061,7 +3210,8 @@ __device__ __forceinline__ void pt_reduce_scored_block(PtScoredLds<kKbit>& u, ty
         k[e] = i < n ? keys[s0 + i] : 0xFFFFFFFFu;
     }
     const unsigned sb = g.sbits;
-    PtSort<kE>().sort(k, st, 0, g.pbits + sb + g.rbits + 1);  // blocked: thread t holds ranks t*kE + e
+    if (!g.binsort || !pt_bin_sort<kE>(k, n, g, g.row0 + (r << g.rbits), u.b, last, last + 2 * kPtRThreads / 64, wave_tot))
+        PtSort<kE>().sort(k, st, 0, g.pbits + sb + g.rbits + 1);  // blocked: thread t holds ranks t*kE + e
     last[threadIdx.x] = k[kE - 1] >> sb;
     __syncthreads();
     const uint32_t rank0 = threadIdx.x * kE;
@@ -3090,9 +3240,8 @@ __device__ __forceinline__ void pt_reduce_scored_block(PtScoredLds<kKbit>& u, ty
     for (uint32_t e = 0; e < kE; ++e) {
         if (head[e]) {
             const uint32_t pk = k[e] >> sb;
-            u.r.hs[base] = rank0 + e;
+            u.r.hs[base] = (rank0 + e) | (kKbit ? kx << 16 : 0u);
             u.r.ps[base] = sx;
-            if (kKbit) u.r.pk[base] = kx;
             stage_p[s0 + base] = filter ? pk : rowbase + (pk >> g.pbits);
             if (!filter) stage_q[s0 + base] = pk & qm;
             ++base;
@@ -3103,17 +3252,17 @@ __device__ __forceinline__ void pt_reduce_scored_block(PtScoredLds<kKbit>& u, ty
         }
     }
     if (threadIdx.x == 0) {
-        u.r.hs[nruns] = n;
+        u.r.hs[nruns] = n | (kKbit ? ktot << 16 : 0u);
         u.r.ps[nruns] = stot;
-        if (kKbit) u.r.pk[nruns] = ktot;
         if (!filter) counts[d] = nruns;
     }
     __syncthreads();
     if (!filter) {
         for (uint32_t i = threadIdx.x; i < nruns; i += kPtRThreads) {
-            stage_w[s0 + i] = u.r.hs[i + 1] - u.r.hs[i];
+            const uint32_t h0 = u.r.hs[i], h1 = u.r.hs[i + 1];
+            stage_w[s0 + i] = (h1 & 0xFFFFu) - (h0 & 0xFFFFu);
             stage_s[s0 + i] = u.r.ps[i + 1] - u.r.ps[i];
-            if (kKbit) stage_w1[s0 + i] = u.r.pk[i + 1] - u.r.pk[i];
+            if (kKbit) stage_w1[s0 + i] = (h1 >> 16) - (h0 >> 16);
         }
         return;
     }
@@ -3124,9 +3273,10 @@ __device__ __forceinline__ void pt_reduce_scored_block(PtScoredLds<kKbit>& u, ty
     for (uint32_t e = 0; e < kE; ++e) {
         const uint32_t rr = rank0 + e;
         const bool in = rr < nruns;
-        wv[e] = in ? u.r.hs[rr + 1] - u.r.hs[rr] : 0u;
+        const uint32_t h0 = in ? u.r.hs[rr] : 0u, h1 = in ? u.r.hs[rr + 1] : 0u;
+        wv[e] = in ? (h1 & 0xFFFFu) - (h0 & 0xFFFFu) : 0u;
         sv[e] = in ? u.r.ps[rr + 1] - u.r.ps[rr] : 0u;
-        w1v[e] = in && kKbit ? u.r.pk[rr + 1] - u.r.pk[rr] : 0u;
+        w1v[e] = in && kKbit ? (h1 >> 16) - (h0 >> 16) : 0u;
         kv[e] = in ? stage_p[s0 + rr] : 0u;
         const bool keep = in && (kKbit ? (wv[e] - w1v[e] >= g.min_shared || w1v[e] >= g.min_shared)
                                        : wv[e] >= g.min_shared);
@@ -3652,6 +3802,10 @@ bool pt_geometry(const kmp_postings* ws, const StepCfg& c, uint64_t inc, PtGeom*
     g->row0 = c.ranged ? c.row_lo : 0;
     g->flat_n = 0;
     g->min_shared = std::max(1u, c.min_shared);
+    g->nprot = c.n;
+    g->rowend = c.ranged ? c.row_hi : c.n;
+    static const int bs_mode = getenv("KMP_BINSORT") ? atoi(getenv("KMP_BINSORT")) : 1;  // A/B switch
+    g->binsort = bs_mode == 2 ? 1 : bs_mode == 0 ? 0 : (g->sbits != 0);
     return true;
 }
 
@@ -3991,9 +4145,10 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
         ws->heavy_ready = false;
         m = ws->h_m;
     }
-    // tiles whose every pair is written (no per-pair test) are cut finer: one workgroup's write
-    // stream is the bound of a tile, and a 256 x 2,048 block of pairs left one CU writing 4 MB
-    ho.hj = (ho.cls ? !c.ranged : !c.require_diff) ? kHvJWrite : kHvJ;
+    // 256 x 256 tiles: one workgroup's write stream bounds a tile (a 256 x 2,048 block of pairs
+    // left one CU writing 4 MB), and a filtered tile (the class test per pair) takes its kept
+    // partners through a per-row bit mask of the chunk (8 words a row)
+    ho.hj = kHvJ;
     if (!ws->heavy_ready) {
         const uint64_t nt = (m + kHvTile - 1) / kHvTile;
         PG(ws->hkeys.reserve(m));
