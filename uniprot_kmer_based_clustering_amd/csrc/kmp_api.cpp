@@ -1296,11 +1296,10 @@ static int stream_passes(kmp_ctx* c, const kmp_pair_opts& o, const int* ks, uint
         plan.density = 0;  // small batch: one pass
     const hipStream_t st = ln.L.stream;
     if (fused && plan.density != 0) {
-        // the smaller k carries most of a pass's incidences: its regions sized for the planned pass
-        // (3/4 of the budget) with the fullest region at up to twice the mean (measured 1.6x at
-        // config 5: frequent k-mers' tiles land on few shards)
+        // the smaller k carries most of a pass's incidences: its regions (and the fused tail's
+        // staging) sized for the planned pass, 3/4 of the budget
         const uint32_t big = ks[0] <= ks[1] ? 0 : 1;
-        KMP_TRY(c, kmp_postings_set_shard_floor(kv[big]->ws, (uint64_t)(2 * 0.75 * plan.budget)));
+        KMP_TRY(c, kmp_postings_set_shard_floor(kv[big]->ws, (uint64_t)(0.75 * plan.budget)));
         KMP_TRY(c, kmp_postings_set_shard_floor(kv[1 - big]->ws, 0));
     }
     uint64_t mcap = 0;
@@ -1320,7 +1319,10 @@ static int stream_passes(kmp_ctx* c, const kmp_pair_opts& o, const int* ks, uint
             // largest edges-per-incidence ratio seen (+10 %; an overflow reruns the pass)
             // a growth takes a quarter of headroom: reallocating six multi-GB arrays (a synchronous
             // free and a fresh allocation each) stalled the device for seconds per growth
-            const double est = plan.density > 0 ? plan.density * plan.mass(a, b) * std::min(1.0, edge_ratio * 1.1) : 0.0;
+            double est = plan.density > 0 ? plan.density * plan.mass(a, b) * std::min(1.0, edge_ratio * 1.1) : 0.0;
+            // once a pass has measured the edge ratio: the largest pass the planner aims for (3/4 of
+            // the key budget), so the arrays are allocated once instead of growing pass by pass
+            if (ratio_seen && plan.density > 0) est = std::max(est, 0.75 * plan.budget * std::min(1.0, edge_ratio * 1.1) * 1.1);
             if (est + 4096 > (double)mcap) mcap = std::max<uint64_t>((uint64_t)est + 4096, mcap + mcap / 4);
             for (int attempt = 0; attempt < 3; ++attempt) {
                 if (!mcap || !ln.mwk->p) mcap = std::max<uint64_t>(mcap, 1u << 20);

@@ -1049,8 +1049,12 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
     }
 }
 
+// KMP_BS_WAVES: an occupancy floor for the small kernel (waves per SIMD; 0: the compiler's choice)
+#ifndef KMP_BS_WAVES
+#define KMP_BS_WAVES 8  // 64 VGPRs: 8 workgroups per CU (LDS allows 8); group_expand 0.238 -> 0.222 ms at config 3
+#endif
 template <int kCap, int kThreads, int kTabBits, bool kMerge, bool kRows, bool kScore>
-__global__ __launch_bounds__(kThreads) void bucket_small_kernel(BucketArgs a, uint32_t b0) {
+__global__ __launch_bounds__(kThreads, KMP_BS_WAVES ? KMP_BS_WAVES * 256 / kThreads : 1) void bucket_small_kernel(BucketArgs a, uint32_t b0) {
     process_bucket<kCap, kThreads, kTabBits, kMerge, kRows, kScore>(b0 + blockIdx.x, a, true);
 }
 
@@ -2441,6 +2445,7 @@ struct kmp_postings {
     uint32_t last_ovf = 0;      // ... row blocks finished by the overflow sort
     uint64_t shard_cap = 0;     // capacity of each pair-key shard region
     uint64_t shard_floor = 0;   // ... at least (kmp_postings_set_shard_floor: a stream's planned pass size)
+    uint64_t stage_floor = 0;   // tail_multi's staging capacity at least (keys; same call)
     Grow<uint32_t> chunk_first;
     Grow<uint32_t> bp;          // bucket partition: H1 | P1 | R | C1 | H2 (see bp_level1)
     Grow<uint32_t> pt;          // row-block tail (pt_bufs)
@@ -3477,7 +3482,7 @@ __global__ void pt_ovf_stage_scored_kernel(const uint32_t* __restrict__ ovf, uin
 // all share their top bits, in one piece).  Descriptors: nf per block (the unused ones empty);
 // the keys scattered to keys2 at their bin's cursor.  A block that fits is one sub-block (copied);
 // a sub-block still above kPtCap (one bin above kPtCap - kSbChunk keys) takes the overflow sort.
-constexpr uint32_t kSbThreads = 1024, kSbMaxLog = 14, kSbChunk = kPtCap * 3 / 4;
+constexpr uint32_t kSbThreads = 1024, kSbMaxLog = 13, kSbChunk = kPtCap * 3 / 4;  // 64 KB of LDS: 2 workgroups per CU
 __host__ __device__ inline unsigned pt_sub_log(uint32_t n) {
     if (n <= kPtCap) return 0;
     unsigned j = 1;  // nf * kSbChunk >= 4n: a bin holds a quarter of a sub-block on average
@@ -4543,7 +4548,10 @@ int tail_multi(kmp_postings* const* ws, uint32_t nk, const StepCfg& c, const uin
     for (uint32_t j = 0; j < nk; ++j) T += inc[j];
     PtGeom g;
     if (!pt_geometry(w0, c, std::max<uint64_t>(T, 1), &g)) return KMP_EINVAL;
-    const uint64_t total = T + 1;  // staging capacity: every key of the pass (the row-block positions)
+    // staging capacity: every key of the pass (the row-block positions); a stream's planned pass
+    // size at least, so the staging arrays are allocated once, not regrown as the passes vary
+    uint64_t total = T + 1;
+    for (uint32_t j = 0; j < nk; ++j) total = std::max<uint64_t>(total, ws[j]->stage_floor);
     PG(w0->inc.reserve(total / 2 + 1));  // u32 keys in a u64 buffer
     PG(w0->uniq.reserve(total));
     PG(w0->w.reserve(total));
@@ -4996,7 +5004,10 @@ int kmp_postings_last_partition(const kmp_postings* ws) {
 
 int kmp_postings_set_shard_floor(kmp_postings* ws, uint64_t keys) {
     if (!ws) return KMP_EINVAL;
-    ws->shard_floor = keys ? keys / kShards + keys / kShards / 4 + 256 : 0;
+    // the fullest region at up to twice the mean (measured 1.6x at config 5: frequent k-mers' tiles
+    // land on few shards), a quarter of slack; the fused tail's staging for the pass + 15 %
+    ws->shard_floor = keys ? 2 * keys / kShards + 2 * keys / kShards / 4 + 256 : 0;
+    ws->stage_floor = keys + keys * 3 / 20;
     return KMP_OK;
 }
 
