@@ -740,9 +740,13 @@ uint64_t pass_budget(kmp_ctx* c, bool fused = false) {
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 16ull << 30;
     // device memory per pair key of a pass: ~96 B when dense row blocks take the tagged-key sort
     // (shard regions 8, row-block keys 8, staged runs 12, the sort's keys 48 and run arrays 12,
-    // slack); ~64 B in the fused tail, whose dense blocks are cut into LDS sub-blocks (shard regions
-    // with slack 10, row-block and sub-block keys 12, staged runs 20, the pass's edges 15, slack)
-    return std::max<uint64_t>(1u << 20, std::min<uint64_t>(fr / 2 / (fused ? 80 : 96), 3ull << 30));
+    // slack; half the free memory kept back); the fused tail, whose dense blocks are cut into LDS
+    // sub-blocks, sizes its buffers once per stream (kmp_postings_set_shard_floor): shard regions
+    // of the smaller k with a 2x fullest-region allowance 20, row-block and sub-block keys 8,
+    // staged runs 20, the pass's edges 17 (edges / incidences ~0.63), +25 % growth headroom:
+    // ~86 B per key of the 3/4-budget pass, so 3/4 of the free memory over 90 B leaves ~40 % free
+    if (fused) return std::max<uint64_t>(1u << 20, std::min<uint64_t>(fr / 4 * 3 / 90, 3ull << 30));
+    return std::max<uint64_t>(1u << 20, std::min<uint64_t>(fr / 2 / 96, 3ull << 30));
 }
 
 // the batch and stream a pass runs on: the context's (nullptr) or a rank's copy
