@@ -192,6 +192,9 @@ SIGNATURES = {
     "kmp_dev_rows_max": (C.c_uint32, [C.c_uint32, C.c_int]),
     "kmp_dev_pairs_rows_scored": (C.c_int, [P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32, C.c_uint32,
                                             C.c_int, C.c_uint32, C.c_uint32, P, P, P, P, C.c_uint64, U64P, P, P]),
+    "kmp_dev_pairs_rows_multi": (C.c_int, [P, C.POINTER(C.c_int), C.c_uint32, P, P, P, C.c_uint32, C.c_uint64,
+                                           C.c_uint32, C.c_int, C.c_uint32, C.c_uint32, P, P, P, P, P, P,
+                                           C.c_uint64, U64P, P, P]),
     "kmp_pairs_stream": (C.c_int, [P, P, C.POINTER(C.c_int), C.c_uint32, C.c_int, EDGE_SINK, P, P]),
     "kmp_edge_digest_term": (C.c_uint64, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
     "kmp_ctx_set_rows": (C.c_int, [P, C.c_uint32, C.c_uint32]),

@@ -682,6 +682,7 @@ __device__ __forceinline__ void spill_segment(const BucketArgs& a, uint64_t pos,
 // and the count table share H, and T shrinks to the per-position array: 18.9 KB of LDS at the
 // small geometry, 8 workgroups (32 waves) per CU instead of 6
 constexpr unsigned kMergeMinBits = 11;
+constexpr uint32_t kRunMin = 32;  // groups of at least this many keys are laid out in class runs (LDS: 640 B at 1,280 keys)
 template <int kCap, int kThreads, int kTabBits, bool kMerge, bool kRows, bool kScore>
 __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArgs& a, bool small) {
     constexpr int kE = kCap / kThreads;
@@ -703,6 +704,9 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
     __shared__ unsigned long long sbase;
     __shared__ unsigned long long hbase[kMaxHeavy];  // spill offset of each heavy group
     __shared__ uint32_t nheavy, hkeys;
+    // class runs (step C): per group of at least kRunMin keys (indexed by its start / kRunMin, unique
+    // since such groups start kRunMin apart) the keys of each of up to 16 classes, 8 bits a class
+    __shared__ uint32_t CC[kCap / kRunMin * 4];
     uint64_t s0;
     uint32_t n;
     if (a.capb) {
@@ -756,6 +760,10 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
     }
     for (uint32_t i = tid; i < kCap / 32; i += kThreads) dupw[i] = gdupw[i] = 0;
     for (uint32_t i = tid; i <= kHeavySub; i += kThreads) SZ[i] = 0;
+    // class runs: the class filter on, at most 16 classes, every pair of a group (not kRows)
+    const bool runs_on = !kRows && a.require_diff && cb >= 1 && cb <= 4;
+    if (runs_on)
+        for (uint32_t i = tid; i < kCap / kRunMin * 4; i += kThreads) CC[i] = 0;
     if (tid == 0) nheavy = hkeys = 0;
     __syncthreads();
     // A. group slot + rank of every key (the keys were loaded before the table clear)
@@ -856,11 +864,46 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
             }
             continue;
         }
-        const uint32_t pos = (kScore ? (g >> 8) & 0xFFFFu : g >> 8) + rk[e];
-        Bl[pos] = xl[e];
-        T[pos] = g;
+        const uint32_t gs = kScore ? (g >> 8) & 0xFFFFu : g >> 8;
+        T[gs + rk[e]] = g;
+        if (runs_on && cn[e] >= kRunMin) {  // its rank in its class; placed below by class
+            const uint32_t c = xl[e] & cmask, sh = 8 * (c & 3);
+            rr[e] = (atomicAdd(&CC[gs / kRunMin * 4 + (c >> 2)], 1u << sh) >> sh) & 0xFFu;
+        } else {
+            Bl[gs + rk[e]] = xl[e];
+        }
     }
     __syncthreads();
+    // keys of classes below c in the group starting at gs (class-run mode), and of class c
+    auto run_of = [&](uint32_t gs, uint32_t c, uint32_t& below, uint32_t& same) {
+        const uint32_t* cc = CC + gs / kRunMin * 4;
+        below = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < 4; ++w) {
+            const uint32_t x = cc[w];
+#pragma unroll
+            for (uint32_t t = 0; t < 4; ++t)
+                if (w * 4 + t < c) below += (x >> (8 * t)) & 0xFFu;
+        }
+        same = (cc[c >> 2] >> (8 * (c & 3))) & 0xFFu;
+    };
+    if (runs_on) {
+        // C'. a group of at least kRunMin keys laid out by class (ascending): an element's
+        // cross-class partners after it are then exactly the positions past its class run, so E
+        // counts them without a test and F writes them without one (config 1: 258M partners
+        // tested for 5.3M kept)
+#pragma unroll
+        for (int e = 0; e < kE; ++e) {
+            const uint32_t i = tid + e * kThreads;
+            if (i >= n || cn[e] < kRunMin || cn[e] > kHeavySub) continue;
+            const uint32_t g = H[sl[e]];
+            const uint32_t gs = kScore ? (g >> 8) & 0xFFFFu : g >> 8;
+            uint32_t below, same;
+            run_of(gs, xl[e] & cmask, below, same);
+            Bl[gs + below + rr[e]] = xl[e];
+        }
+        __syncthreads();
+    }
     // D. per position: group bounds, duplicate flag (same protein earlier in the group: the same
     // p << cb | class word); a group holding one marks its start in gdupw
     uint32_t s[kE], en[kE];
@@ -873,7 +916,13 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
         s[e] = kScore ? (g >> 8) & 0xFFFFu : g >> 8;
         en[e] = s[e] + (g & 255u);
         xl[e] = Bl[i];
-        for (uint32_t j = s[e]; j < i; ++j)
+        uint32_t j0 = s[e];
+        if (runs_on && en[e] - s[e] >= kRunMin) {  // a duplicate shares the class: its run only
+            uint32_t below, same;
+            run_of(s[e], xl[e] & cmask, below, same);
+            j0 = s[e] + below;
+        }
+        for (uint32_t j = j0; j < i; ++j)
             if (Bl[j] == xl[e]) {
                 atomicOr(&dupw[i >> 5], 1u << (i & 31));
                 atomicOr(&gdupw[s[e] >> 5], 1u << (s[e] & 31));
@@ -894,7 +943,8 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
     bool gd[kE];
     constexpr bool kMask = kThreads <= 256;  // the large kernel measured slower with it (74 -> 80 us, config 1)
     // kRows: bit t = position s + t (every partner of a larger protein, anywhere in the group)
-    auto mask_mode = [&](int e) { return kMask && !gd[e] && en[e] - s[e] <= (kRows ? 32u : 33u); };
+    auto run_mode = [&](int e) { return runs_on && !gd[e] && en[e] - s[e] >= kRunMin; };
+    auto mask_mode = [&](int e) { return kMask && !gd[e] && en[e] - s[e] <= (kRows ? 32u : 33u) && !run_mode(e); };
     uint32_t st_sum = single, st_dist = single, st_rep = 0, st_cdf2 = 0, st_max = single ? 1u : 0u, st_heavy = 0,
              mine = 0;
 #pragma unroll
@@ -920,6 +970,11 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
                     c += k;
                     if (kMask && j - s[e] < 32u) bits |= (uint32_t)k << (j - s[e]);
                 }
+        } else if (run_mode(e)) {  // class runs: the positions past its run, all kept
+            f = en[e] - s[e];
+            uint32_t below, same;
+            run_of(s[e], xl[e] & cmask, below, same);
+            c = en[e] - (s[e] + below + same);
         } else if (!gd[e]) {
             f = en[e] - s[e];
             const uint32_t span = en[e] - 1 - i;
@@ -1014,6 +1069,12 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
                 const unsigned long long pk = (unsigned long long)min(p, q) * a.mul + max(p, q);
                 return kScore ? pk << a.sb | sfield : pk;
             };
+            if (run_mode(e)) {
+                uint32_t below, same;
+                run_of(s[e], xl[e] & cmask, below, same);
+                for (uint32_t j = s[e] + below + same; j < en[e]; ++j) put(pkey(Bl[j] >> cb));
+                continue;
+            }
             if (mask_mode(e)) {
                 const uint32_t base = kRows ? s[e] : i + 1;
                 for (uint32_t m = cnt[e]; m; m &= m - 1) {
