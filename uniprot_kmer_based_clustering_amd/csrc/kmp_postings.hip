@@ -682,6 +682,12 @@ __device__ __forceinline__ void spill_segment(const BucketArgs& a, uint64_t pos,
 // and the count table share H, and T shrinks to the per-position array: 18.9 KB of LDS at the
 // small geometry, 8 workgroups (32 waves) per CU instead of 6
 constexpr unsigned kMergeMinBits = 11;
+// KMP_CLASS_RUNS: groups of kRunMin+ keys laid out by class (step C'), partners past the element's
+// class run taken without a test.  Off: measured slower at config 3 (group_expand 0.222 -> 0.238 ms:
+// the extra barrier and LDS) and at config 1 (0.443 -> 0.452 ms), whose time is not in the tests
+#ifndef KMP_CLASS_RUNS
+#define KMP_CLASS_RUNS 0
+#endif
 constexpr uint32_t kRunMin = 32;  // groups of at least this many keys are laid out in class runs (LDS: 640 B at 1,280 keys)
 template <int kCap, int kThreads, int kTabBits, bool kMerge, bool kRows, bool kScore>
 __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArgs& a, bool small) {
@@ -761,7 +767,7 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
     for (uint32_t i = tid; i < kCap / 32; i += kThreads) dupw[i] = gdupw[i] = 0;
     for (uint32_t i = tid; i <= kHeavySub; i += kThreads) SZ[i] = 0;
     // class runs: the class filter on, at most 16 classes, every pair of a group (not kRows)
-    const bool runs_on = !kRows && a.require_diff && cb >= 1 && cb <= 4;
+    const bool runs_on = KMP_CLASS_RUNS && !kRows && a.require_diff && cb >= 1 && cb <= 4;
     if (runs_on)
         for (uint32_t i = tid; i < kCap / kRunMin * 4; i += kThreads) CC[i] = 0;
     if (tid == 0) nheavy = hkeys = 0;
@@ -2839,7 +2845,13 @@ int front_flat(kmp_postings* ws, uint64_t slots, const Layout& lay, const uint16
 // A row block above kPtCap keys (a protein pairing with thousands of later proteins: real data
 // at k = 5) is listed instead; the host sorts the listed blocks with one segmented radix sort
 // and pt_ovf_rle encodes them (pt_finish_overflow), then offsets and emit run again.
-constexpr uint32_t kPtThreads = 1024, kPtPer = 16, kPtTile = kPtThreads * kPtPer;  // partition tiles: 16,384 keys
+#ifndef KMP_PT_PER
+#define KMP_PT_PER 16
+#endif
+#ifndef KMP_PT_RADIX_BITS
+#define KMP_PT_RADIX_BITS 0  // rocprim's choice (8 bits, match ranking, at 512 threads)
+#endif
+constexpr uint32_t kPtThreads = 1024, kPtPer = KMP_PT_PER, kPtTile = kPtThreads * kPtPer;  // partition tiles: 16,384 keys
 constexpr uint32_t kPtRThreads = 512, kPtCap = 8192;  // pt_reduce: up to 16 keys per thread
 constexpr uint32_t kPtMaxBlocks = 8192;  // row blocks (LDS histogram of pt_hist / pt_scatter)
 
@@ -3015,7 +3027,10 @@ __global__ __launch_bounds__(kPtThreads) void pt_scatter_kernel(const unsigned l
 }
 
 template <uint32_t kE>
-using PtSort = rocprim::block_radix_sort<uint32_t, kPtRThreads, kE>;
+using PtSort = rocprim::block_radix_sort<uint32_t, kPtRThreads, kE, rocprim::empty_type, 1, 1, KMP_PT_RADIX_BITS,
+                                         KMP_PT_RADIX_BITS == 4
+                                             ? rocprim::block_radix_rank_algorithm::basic_memoize
+                                             : rocprim::block_radix_rank_algorithm::default_for_radix_sort>;
 
 // Binned sort of a block's n keys (the row-block reduce; replaces a block radix sort over all
 // pbits + rbits (+ sbits) key bits, 6-8 passes of rank + scatter).  A run only needs its pair's
