@@ -383,15 +383,41 @@ __device__ __forceinline__ unsigned long long stat_op(int t, unsigned long long 
     return t == kStMaxDf ? (a > b ? a : b) : a + b;
 }
 
+// Wave64 inclusive scans on DPP (VALU only, no LDS crossbar round trips): row_shr 1/2/4/8 scan
+// each 16-lane row (bound_ctrl: a source before the row start reads 0), then row_bcast 15 / 31
+// carry the row totals into the later rows (rows outside the row mask keep the old value, 0).
+// Every lane of the wave must be active.
+template <int kCtrl, int kRowMask = 0xF>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, kCtrl, kRowMask, 0xF, true);
+}
+__device__ __forceinline__ uint32_t wave_iscan(uint32_t x) {
+    x += dpp_mov<0x111>(x);
+    x += dpp_mov<0x112>(x);
+    x += dpp_mov<0x114>(x);
+    x += dpp_mov<0x118>(x);
+    x += dpp_mov<0x142, 0xA>(x);
+    x += dpp_mov<0x143, 0xC>(x);
+    return x;
+}
+// the wave's maximum (every lane; values are unsigned, so the 0 of an invalid source is neutral)
+__device__ __forceinline__ uint32_t wave_max(uint32_t x) {
+    x = max(x, dpp_mov<0x111>(x));
+    x = max(x, dpp_mov<0x112>(x));
+    x = max(x, dpp_mov<0x114>(x));
+    x = max(x, dpp_mov<0x118>(x));
+    x = max(x, dpp_mov<0x142, 0xA>(x));
+    x = max(x, dpp_mov<0x143, 0xC>(x));
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_iscan(x), 63);
+}
+
 // exclusive scan of one value per thread over the workgroup; returns (prefix, total)
 __device__ __forceinline__ void block_scan(uint32_t v, uint32_t& excl, uint32_t& total, uint32_t* wave_tot) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o);
-        if (lane >= o) x += y;
-    }
+    const uint32_t x = wave_iscan(v);
     if (lane == 63) wave_tot[w] = x;
     __syncthreads();
     uint32_t before = 0, tot = 0;
@@ -590,12 +616,7 @@ enum : uint32_t { kFlBin = 0, kFlClass = 1, kFlList = 2, kFlOvf = 3, kFlBinTiles
 template <int kThreads>
 __device__ __forceinline__ void block_scan_n(uint32_t v, uint32_t& excl, uint32_t& total, uint32_t* wave_tot) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o);
-        if (lane >= o) x += y;
-    }
+    const uint32_t x = wave_iscan(v);
     if (lane == 63) wave_tot[w] = x;
     __syncthreads();
     uint32_t before = 0, tot = 0;
@@ -687,6 +708,11 @@ constexpr unsigned kMergeMinBits = 11;
 // the extra barrier and LDS) and at config 1 (0.443 -> 0.452 ms), whose time is not in the tests
 #ifndef KMP_CLASS_RUNS
 #define KMP_CLASS_RUNS 0
+#endif
+// KMP_BS_CUT (A/B timing builds only, wrong results): the small kernel returns after step
+// 1 = A, 2 = B, 3 = C, 4 = D, 5 = E + statistics (no output)
+#ifndef KMP_BS_CUT
+#define KMP_BS_CUT 0
 #endif
 constexpr uint32_t kRunMin = 32;  // groups of at least this many keys are laid out in class runs (LDS: 640 B at 1,280 keys)
 template <int kCap, int kThreads, int kTabBits, bool kMerge, bool kRows, bool kScore>
@@ -809,6 +835,7 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
         }
     }
     __syncthreads();
+    if (KMP_BS_CUT == 1 && small) return;
     // B. size classes, largest first.  Each group's first key (rank 0) stands for it (count from
     // its slot word, size-class rank, position rewrite), so the pass is per key, not over all kTab
     // table slots (measured 6 % faster); singleton groups (most) take no rank and no position.
@@ -854,6 +881,7 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
             H[sl[e]] = cn[e] > kHeavySub ? rr[e] : ((SZ[cn[e]] + rr[e] * cn[e]) << 8) | cn[e] | sc;
         }
     __syncthreads();
+    if (KMP_BS_CUT == 2 && small) return;
     // C. scatter (T now holds, per position, its group's start << 8 | size); heavy groups' keys
     // go to the spill region
     unsigned long long* spill_dst = a.spill ? a.spill + (uint64_t)shard * a.spill_cap : nullptr;
@@ -880,6 +908,7 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
         }
     }
     __syncthreads();
+    if (KMP_BS_CUT == 3 && small) return;
     // keys of classes below c in the group starting at gs (class-run mode), and of class c
     auto run_of = [&](uint32_t gs, uint32_t c, uint32_t& below, uint32_t& same) {
         const uint32_t* cc = CC + gs / kRunMin * 4;
@@ -936,6 +965,7 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
             }
     }
     __syncthreads();
+    if (KMP_BS_CUT == 4 && small) return;
     auto is_dup = [&](uint32_t j) { return (dupw[j >> 5] >> (j & 31)) & 1u; };
     // E. df, head, kept-partner count.  A group without duplicates (almost all) has df = its size
     // and counts its partners after i only; a group with one walks the whole group.  In a group of
@@ -1022,18 +1052,13 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
     // partials -> red, then kStN threads unpack, sum and post one (sharded) atomic each.  They
     // ride on the output scan's barriers; the last wave reserves the output range meanwhile.
     {
-        unsigned long long w0 = st_sum | (unsigned long long)st_dist << 16 | (unsigned long long)st_rep << 32 |
-                                (unsigned long long)st_heavy << 48;
-        unsigned long long c2 = st_cdf2 | (unsigned long long)mine << 32;
-        uint32_t mx = st_max;
-        for (int sh = 32; sh > 0; sh >>= 1) {
-            w0 += __shfl_down(w0, sh);
-            c2 += __shfl_down(c2, sh);
-            mx = max(mx, (uint32_t)__shfl_down(mx, sh));
-        }
+        // DPP wave sums of packed 16-bit fields (each at most kCap per workgroup); the incidences
+        // are the output scan's total
+        const uint32_t s0 = wave_sum(st_sum | st_dist << 16), s1 = wave_sum(st_rep | st_heavy << 16);
+        const uint32_t s2 = wave_sum(st_cdf2), mx = wave_max(st_max);
         if ((tid & 63) == 0) {
-            red[tid >> 6][0] = w0;
-            red[tid >> 6][1] = c2;
+            red[tid >> 6][0] = s0 | (unsigned long long)s1 << 32;
+            red[tid >> 6][1] = s2;
             red[tid >> 6][2] = mx;
         }
     }
@@ -1049,15 +1074,17 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
                                          : tid == kStRepeat   ? (w0 >> 32) & 0xFFFF
                                          : tid == kStHeavy    ? w0 >> 48
                                          : tid == kStCdf2     ? c2 & 0xFFFFFFFFull
-                                         : tid == kStInc      ? c2 >> 32
+                                         : tid == kStInc      ? 0ull
                                                               : mx;
             v = tid == kStMaxDf ? (v > x ? v : x) : v + x;
         }
+        if (tid == kStInc) v = total;
         unsigned long long* g = a.gstats + (uint64_t)shard * 8 + tid;  // sharded: no hot word
         if (tid == kStMaxDf) atomicMax(g, v);
         else if (v) atomicAdd(g, v);
     }
     __syncthreads();
+    if (KMP_BS_CUT == 5 && small) return;
     // F. write the pair keys.  When the bucket's keys fit (almost always) they are staged in LDS
     // (H is dead after C) at each element's scanned offset and copied out coalesced; each lane
     // writing its own short run straight to HBM cost one memory transaction per key (a bucket
