@@ -940,17 +940,46 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
         __syncthreads();
     }
     // D. per position: group bounds, duplicate flag (same protein earlier in the group: the same
-    // p << cb | class word); a group holding one marks its start in gdupw
-    uint32_t s[kE], en[kE];
+    // p << cb | class word); a group holding one marks its start in gdupw.
+    // fwd (every pair of a group, no class runs): one forward walk over the partners after i does
+    // both D and E's partner test — the kept partners go to cnt (a bit mask in a group of at most 33
+    // keys, else their count) and an equal word j > i marks j as a duplicate (rare: the group then
+    // takes E's walk over the whole group).  No separate backward duplicate scan (config 3: 62 VALU
+    // instructions per wave).
+    uint32_t s[kE], en[kE], cnt[kE];
+    constexpr bool kMask = kThreads <= 256;  // the large kernel measured slower with it (74 -> 80 us, config 1)
+    const bool fwd = !kRows && !runs_on;
 #pragma unroll
     for (int e = 0; e < kE; ++e) {
         const uint32_t i = tid + e * kThreads;
-        s[e] = en[e] = 0;
+        s[e] = en[e] = cnt[e] = 0;
         if (i >= nm) continue;
         const uint32_t g = T[i];
         s[e] = kScore ? (g >> 8) & 0xFFFFu : g >> 8;
         en[e] = s[e] + (g & 255u);
         xl[e] = Bl[i];
+        if (fwd) {
+            uint32_t acc = 0;
+            auto mark = [&](uint32_t j) {
+                atomicOr(&dupw[j >> 5], 1u << (j & 31));
+                atomicOr(&gdupw[s[e] >> 5], 1u << (s[e] & 31));
+            };
+            if (kMask && en[e] - s[e] <= 33u) {
+                for (uint32_t j = i + 1; j < en[e]; ++j) {
+                    const uint32_t lj = Bl[j];
+                    acc |= (uint32_t)(!a.require_diff || ((lj ^ xl[e]) & cmask) != 0u) << (j - i - 1);
+                    if (lj == xl[e]) mark(j);
+                }
+            } else {
+                for (uint32_t j = i + 1; j < en[e]; ++j) {
+                    const uint32_t lj = Bl[j];
+                    acc += !a.require_diff || ((lj ^ xl[e]) & cmask) != 0u;
+                    if (lj == xl[e]) mark(j);
+                }
+            }
+            cnt[e] = acc;
+            continue;
+        }
         uint32_t j0 = s[e];
         if (runs_on && en[e] - s[e] >= kRunMin) {  // a duplicate shares the class: its run only
             uint32_t below, same;
@@ -975,9 +1004,7 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
     // re-testing the others.  The mode follows from s, en and gd (no register), and is the same for
     // a whole group, so a wave walking one large group does not run both loops of F (deciding it per
     // element, by the partners after i, measured 5 % slower at config 1).
-    uint32_t cnt[kE];
     bool gd[kE];
-    constexpr bool kMask = kThreads <= 256;  // the large kernel measured slower with it (74 -> 80 us, config 1)
     // kRows: bit t = position s + t (every partner of a larger protein, anywhere in the group)
     auto run_mode = [&](int e) { return runs_on && !gd[e] && en[e] - s[e] >= kRunMin; };
     auto mask_mode = [&](int e) { return kMask && !gd[e] && en[e] - s[e] <= (kRows ? 32u : 33u) && !run_mode(e); };
@@ -986,6 +1013,7 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
 #pragma unroll
     for (int e = 0; e < kE; ++e) {
         const uint32_t i = tid + e * kThreads;
+        const uint32_t pre = cnt[e];  // fwd: D's kept partners (mask or count)
         cnt[e] = 0;
         gd[e] = false;
         if (i >= nm) continue;
@@ -1011,6 +1039,14 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
             uint32_t below, same;
             run_of(s[e], xl[e] & cmask, below, same);
             c = en[e] - (s[e] + below + same);
+        } else if (fwd && !gd[e]) {
+            f = en[e] - s[e];
+            if (kMask && en[e] - s[e] <= 33u) {
+                bits = pre;
+                c = __popc(bits);
+            } else {
+                c = pre;
+            }
         } else if (!gd[e]) {
             f = en[e] - s[e];
             const uint32_t span = en[e] - 1 - i;
