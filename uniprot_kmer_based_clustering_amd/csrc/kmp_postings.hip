@@ -727,7 +727,7 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
     __shared__ __attribute__((aligned(16))) uint32_t T[kMerge ? kCap : kTab];
     // H: per slot: (merged: h low bits | count << hb) / group size, then start<<8|size
     __shared__ __attribute__((aligned(16))) uint32_t H[kTab];
-    __shared__ uint32_t Bl[kCap];                              // per position: p << cb | class
+    __shared__ uint32_t Bl[kCap + 4];  // per position: p << cb | class (+4: the forward walk reads past a group)
     __shared__ uint32_t dupw[kCap / 32];   // per position: a later occurrence of a protein in its group
     __shared__ uint32_t gdupw[kCap / 32];  // per group start: the group holds such a duplicate
     __shared__ uint32_t SZ[kHeavySub + 1];
@@ -965,11 +965,22 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
                 atomicOr(&gdupw[s[e] >> 5], 1u << (s[e] & 31));
             };
             if (kMask && en[e] - s[e] <= 33u) {
-                for (uint32_t j = i + 1; j < en[e]; ++j) {
-                    const uint32_t lj = Bl[j];
-                    acc |= (uint32_t)(!a.require_diff || ((lj ^ xl[e]) & cmask) != 0u) << (j - i - 1);
-                    if (lj == xl[e]) mark(j);
+                // four partners per step (two ds_read2 of consecutive words; words past en are read
+                // and masked off: Bl is followed by other LDS arrays, never out of the allocation)
+                const uint32_t span = en[e] - 1 - i;
+                for (uint32_t j = i + 1; j < en[e]; j += 4) {
+                    const uint32_t l0 = Bl[j], l1 = Bl[j + 1], l2 = Bl[j + 2], l3 = Bl[j + 3];
+                    const uint32_t d = j - i - 1;
+                    auto kp = [&](uint32_t lj) { return (uint32_t)(!a.require_diff || ((lj ^ xl[e]) & cmask) != 0u); };
+                    acc |= (kp(l0) | kp(l1) << 1 | kp(l2) << 2 | kp(l3) << 3) << d;
+                    if ((l0 == xl[e]) | (l1 == xl[e]) | (l2 == xl[e]) | (l3 == xl[e])) {
+                        if (l0 == xl[e]) mark(j);
+                        if (l1 == xl[e] && j + 1 < en[e]) mark(j + 1);
+                        if (l2 == xl[e] && j + 2 < en[e]) mark(j + 2);
+                        if (l3 == xl[e] && j + 3 < en[e]) mark(j + 3);
+                    }
                 }
+                acc &= span >= 32u ? ~0u : (1u << span) - 1u;
             } else {
                 for (uint32_t j = i + 1; j < en[e]; ++j) {
                     const uint32_t lj = Bl[j];
