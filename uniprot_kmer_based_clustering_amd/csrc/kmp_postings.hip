@@ -218,20 +218,21 @@ struct KeyChunk {
 
 // Stage chunk [c0, c1) of proteins [first, p_hi): the proteins whose regions overlap it and the
 // residue span their windows need, recoded into LDS.  Ends with a barrier.
+template <uint32_t kThr = kKeyThreads>
 __device__ __forceinline__ void key_chunk_load(KeyChunk& s, const uint8_t* __restrict__ res,
                                                const uint64_t* __restrict__ res_off,
                                                const uint16_t* __restrict__ cls, int k, uint32_t p_hi,
                                                uint64_t c0, uint64_t c1, uint32_t first, const Layout& lay,
                                                uint32_t* __restrict__ flags) {
     const int tid = threadIdx.x;
-    s.lut[tid] = c_lut.v[tid];
+    if (tid < 256) s.lut[tid] = c_lut.v[tid];
     if (tid == 0) {
         s.np = 0;
         s.r0 = s.r1 = 0;
     }
     __syncthreads();
     // the chunk's proteins: first + t while its region starts before c1 (one parallel round)
-    for (uint32_t t = tid; t < kKeyProtMax && first + t < p_hi; t += kKeyThreads) {
+    for (uint32_t t = tid; t < kKeyProtMax && first + t < p_hi; t += kThr) {
         const uint32_t p = first + t;
         const uint64_t off = res_off[p], L = res_off[p + 1] - off;
         const uint64_t b = set_base(off, p);
@@ -256,7 +257,7 @@ __device__ __forceinline__ void key_chunk_load(KeyChunk& s, const uint8_t* __res
     const uint64_t a0 = r0 & ~15ull, res_end = res_off[p_hi];
     const bool vec_ok = ((uintptr_t)res & 15u) == 0;
     const uint32_t nv = (uint32_t)((r1 - a0 + 15) >> 4);
-    for (uint32_t v = tid; v < nv; v += kKeyThreads) {
+    for (uint32_t v = tid; v < nv; v += kThr) {
         const uint64_t g = a0 + 16ull * v;
         uint32_t w[4];
         if (vec_ok && g + 16 <= res_end) {
@@ -280,7 +281,7 @@ __device__ __forceinline__ void key_chunk_load(KeyChunk& s, const uint8_t* __res
         *reinterpret_cast<uint4*>(s.rc + 16 * v) =
             make_uint4(code4(w[0]), code4(w[1]), code4(w[2]), code4(w[3]));
     }
-    for (uint32_t t = tid; t < np; t += kKeyThreads) s.pr[t] = (int32_t)((int64_t)res_off[first + t] - (int64_t)a0);
+    for (uint32_t t = tid; t < np; t += kThr) s.pr[t] = (int32_t)((int64_t)res_off[first + t] - (int64_t)a0);
     __syncthreads();
 }
 
@@ -2214,13 +2215,13 @@ struct CurGeom {
 // lh holds the tile's digit histogram and r[e] every key's rank in its digit: reserve each digit's
 // run on cursor(d) (start of its region: region(d), cap keys), place the tile digit-major into S
 // and write each run at its reservation; keys past their region's end are dropped (kFlCur)
-template <uint32_t kPer, class Digit, class Cursor, class Region>
+template <uint32_t kPer, class Digit, class Cursor, class Region, uint32_t kThr = kKeyThreads>
 __device__ __forceinline__ void bp_place_cur(const unsigned long long (&x)[kPer], const uint32_t (&r)[kPer],
                                              uint32_t n_in, uint32_t nb, Digit digit, Cursor cursor, Region region,
                                              uint32_t cap, uint32_t* lh, uint32_t* wave_tot, unsigned long long* S,
                                              unsigned long long* __restrict__ out, uint32_t* __restrict__ flags) {
-    constexpr uint32_t kQ = kBpMaxBins / kKeyThreads;
-    const uint32_t q = (nb + kKeyThreads - 1) / kKeyThreads, b0 = threadIdx.x * q;
+    constexpr uint32_t kQ = kBpMaxBins / kThr;
+    const uint32_t q = (nb + kThr - 1) / kThr, b0 = threadIdx.x * q;
     uint32_t c[kQ], base[kQ], v = 0;
 #pragma unroll
     for (uint32_t t = 0; t < kQ; ++t) {
@@ -2229,7 +2230,7 @@ __device__ __forceinline__ void bp_place_cur(const unsigned long long (&x)[kPer]
         v += c[t];
     }
     uint32_t excl, total;
-    block_scan_n<kKeyThreads>(v, excl, total, wave_tot);
+    block_scan_n<kThr>(v, excl, total, wave_tot);
 #pragma unroll
     for (uint32_t t = 0; t < kQ; ++t)
         if (t < q && b0 + t < nb) {
@@ -2253,7 +2254,7 @@ __device__ __forceinline__ void bp_place_cur(const unsigned long long (&x)[kPer]
         }
     if (over) flags[kFlCur] = 1;
     __syncthreads();
-    for (uint32_t i = 2 * threadIdx.x; i < n_in; i += 2 * kKeyThreads) {
+    for (uint32_t i = 2 * threadIdx.x; i < n_in; i += 2 * kThr) {
         const ulonglong2 y = *reinterpret_cast<const ulonglong2*>(S + i);
         const uint32_t d0 = digit(y.x), a0 = lh[d0] + i, e0 = region(d0) + cap;
         if (i + 1 < n_in) {
@@ -2331,8 +2332,14 @@ __global__ void bp_cur_clear_kernel(uint32_t* __restrict__ cur, uint32_t n) {
 constexpr uint32_t kBpGatherMax = 1024;  // chunks per level-2 tile (T)
 constexpr uint32_t kBpGatherTile = 4096;  // keys per round of a level-2 tile
 
+// KMP_L1_THREADS: workgroup size of the local level 1 (a 4,096-slot chunk either way; 512 threads
+// own 8 slots each: twice the waves per CU at the same LDS; keys_level1 0.139 -> 0.127 ms at config 3)
+#ifndef KMP_L1_THREADS
+#define KMP_L1_THREADS 512
+#endif
 // level 1, local: the chunk's own-digit keys grouped by digit1 at out[chunk * kKeyChunk ...]
-__global__ __launch_bounds__(kKeyThreads) void bp_scatter1l_kernel(
+template <uint32_t kThr>
+__global__ __launch_bounds__(kThr) void bp_scatter1l_kernel(
     const uint8_t* __restrict__ res, const uint64_t* __restrict__ res_off, const uint16_t* __restrict__ cls, int k,
     uint32_t p_hi, uint64_t slots, const uint32_t* __restrict__ chunk_first, Layout lay, BpDigits dg, uint32_t pw21,
     uint32_t dlo, uint32_t dhi, uint32_t* __restrict__ H1, unsigned long long* __restrict__ out,
@@ -2342,17 +2349,18 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scatter1l_kernel(
         unsigned long long S[kKeyChunk];
     } u;
     __shared__ uint32_t lh[kBpMaxBins];
-    __shared__ uint32_t wave_tot[kKeyThreads / 64];
+    __shared__ uint32_t wave_tot[kThr / 64];
     __shared__ uint32_t s_n;
+    constexpr uint32_t kPer = kKeyChunk / kThr, kQ = kBpMaxBins / kThr;
     const uint64_t c0 = (uint64_t)blockIdx.x * kKeyChunk, c1 = min(c0 + kKeyChunk, slots);
-    for (uint32_t d = threadIdx.x; d < dg.nb1; d += kKeyThreads) lh[d] = 0;
+    for (uint32_t d = threadIdx.x; d < dg.nb1; d += kThr) lh[d] = 0;
     if (threadIdx.x == 0) s_n = 0;
     const uint32_t first = chunk_first[blockIdx.x];
-    key_chunk_load(u.kc, res, res_off, cls, k, p_hi, c0, c1, first, lay, flags);
-    unsigned long long x[kBpPer];
-    uint32_t r[kBpPer], nk = 0;
+    key_chunk_load<kThr>(u.kc, res, res_off, cls, k, p_hi, c0, c1, first, lay, flags);
+    unsigned long long x[kPer];
+    uint32_t r[kPer], nk = 0;
     const unsigned hs1 = dg.sh1 - lay.hshift;
-    key_chunk_run<kBpPer>(u.kc, threadIdx.x * kBpPer, (uint32_t)(c1 - c0), k, pw21, first, lay,
+    key_chunk_run<kPer>(u.kc, threadIdx.x * kPer, (uint32_t)(c1 - c0), k, pw21, first, lay,
                           [&](uint32_t e, bool valid, uint32_t h, unsigned long long lo) {
                               const uint32_t d = h >> hs1;
                               const bool mine = valid && d >= dlo && d < dhi;  // the call's coarse bins
@@ -2362,26 +2370,26 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scatter1l_kernel(
                           });
     if (nk) atomicAdd(&s_n, nk);
     __syncthreads();  // the chunk's staging (u.kc) is dead from here: u.S reuses it
-    uint32_t cnt[kBpQ];
+    uint32_t cnt[kQ];
 #pragma unroll
-    for (uint32_t t = 0; t < kBpQ; ++t) {
-        const uint32_t d = threadIdx.x + t * kKeyThreads;
+    for (uint32_t t = 0; t < kQ; ++t) {
+        const uint32_t d = threadIdx.x + t * kThr;
         cnt[t] = d < dg.nb1 ? lh[d] : 0u;
     }
-    lds_bins_scan(lh, dg.nb1, wave_tot);
+    lds_bins_scan<kThr>(lh, dg.nb1, wave_tot);
     uint32_t* row = H1 + (uint64_t)blockIdx.x * dg.nb1;
 #pragma unroll
-    for (uint32_t t = 0; t < kBpQ; ++t) {
-        const uint32_t d = threadIdx.x + t * kKeyThreads;
+    for (uint32_t t = 0; t < kQ; ++t) {
+        const uint32_t d = threadIdx.x + t * kThr;
         if (d < dg.nb1) row[d] = lh[d] << 16 | cnt[t];
     }
 #pragma unroll
-    for (uint32_t e = 0; e < kBpPer; ++e)
+    for (uint32_t e = 0; e < kPer; ++e)
         if (x[e] != kNoKey) u.S[lh[(uint32_t)(x[e] >> dg.sh1)] + r[e]] = x[e];
     __syncthreads();
     const uint32_t n_in = s_n;
     unsigned long long* seg = out + c0;  // c0 = chunk * kKeyChunk: 16-byte aligned
-    for (uint32_t i = 2 * threadIdx.x; i < n_in; i += 2 * kKeyThreads) {
+    for (uint32_t i = 2 * threadIdx.x; i < n_in; i += 2 * kThr) {
         if (i + 1 < n_in)
             *reinterpret_cast<ulonglong2*>(seg + i) = *reinterpret_cast<const ulonglong2*>(u.S + i);
         else
@@ -2414,8 +2422,8 @@ __global__ __launch_bounds__(256) void bp_h1t_kernel(const uint32_t* __restrict_
 // takes the tiles [x * per, (x + 1) * per) of the bin-major tile list, so neighbouring bins' tiles
 // of a chunk range (whose runs share the 128-B lines at their ends) run on one L2 at about the
 // same time.
-template <uint32_t kPer>
-__global__ __launch_bounds__(kKeyThreads) void bp_scatter2g_kernel(const unsigned long long* __restrict__ in,
+template <uint32_t kPer, uint32_t kThr>
+__global__ __launch_bounds__(kThr) void bp_scatter2g_kernel(const unsigned long long* __restrict__ in,
                                                                    const uint32_t* __restrict__ H1T, uint32_t G,
                                                                    uint32_t T, uint32_t ntiles, uint32_t nbins,
                                                                    BpDigits dg, CurGeom cg,
@@ -2423,16 +2431,16 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scatter2g_kernel(const unsigne
                                                                    unsigned long long* __restrict__ out,
                                                                    uint32_t* __restrict__ flags, uint32_t c0,
                                                                    uint32_t dlo) {
-    constexpr uint32_t kTile = kPer * kKeyThreads;
+    constexpr uint32_t kTile = kPer * kThr;
     __shared__ __attribute__((aligned(16))) unsigned long long S[kTile];
     __shared__ uint32_t lh[kBpMaxBins];
-    __shared__ uint32_t wave_tot[kKeyThreads / 64];
+    __shared__ uint32_t wave_tot[kThr / 64];
     // aliases in S, dead once the tile's keys are loaded: src[kBpGatherMax] (a run's segment
     // offset minus its tile offset, mod 2^32) | map[kBpTile] (key -> run)
     uint32_t* src = reinterpret_cast<uint32_t*>(S);
     uint16_t* map = reinterpret_cast<uint16_t*>(src + kBpGatherMax);
     static_assert(kBpGatherMax * 4 + kTile * 2 <= sizeof(S), "gather tables fit in S");
-    constexpr uint32_t kQ = kBpGatherMax / kKeyThreads;
+    constexpr uint32_t kQ = kBpGatherMax / kThr;
     const uint32_t total = ntiles * nbins, per = (total + 7) / 8;
     const uint32_t w = (blockIdx.x % 8) * per + blockIdx.x / 8;
     if (w >= total) return;
@@ -2440,7 +2448,7 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scatter2g_kernel(const unsigne
     if (ch0 >= G) return;
     const uint32_t nch = min(T, G - ch0);
     const uint32_t* row = H1T + (uint64_t)(c - dlo) * G + ch0;
-    const uint32_t q = (nch + kKeyThreads - 1) / kKeyThreads, b0 = threadIdx.x * q;
+    const uint32_t q = (nch + kThr - 1) / kThr, b0 = threadIdx.x * q;
     uint32_t p[kQ], v = 0;
 #pragma unroll
     for (uint32_t t = 0; t < kQ; ++t) {
@@ -2448,13 +2456,15 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scatter2g_kernel(const unsigne
         v += p[t] & 0xFFFFu;
     }
     uint32_t excl0, tn;
-    block_scan_n<kKeyThreads>(v, excl0, tn, wave_tot);
+    block_scan_n<kThr>(v, excl0, tn, wave_tot);
     auto digit = [&](unsigned long long y) { return (uint32_t)(y >> dg.sh2) & dg.m2; };
     const uint32_t bb = c * dg.nb2;
+    auto cursor = [&](uint32_t d) { return &bcur[bb + d]; };
+    auto region = [&](uint32_t d) { return (bb + d) * cg.capb; };
     for (uint32_t base = 0; base < tn; base += kTile) {
         if (base) __syncthreads();  // the previous round's writes have read lh and S
         const uint32_t n_in = min(kTile, tn - base);
-        for (uint32_t d = threadIdx.x; d < dg.nb2; d += kKeyThreads) lh[d] = 0;
+        for (uint32_t d = threadIdx.x; d < dg.nb2; d += kThr) lh[d] = 0;
         uint32_t excl = excl0;
 #pragma unroll
         for (uint32_t t = 0; t < kQ; ++t)
@@ -2477,7 +2487,7 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scatter2g_kernel(const unsigne
         uint32_t r[kPer];
 #pragma unroll
         for (uint32_t e = 0; e < kPer; ++e) {
-            const uint32_t i = threadIdx.x + e * kKeyThreads;
+            const uint32_t i = threadIdx.x + e * kThr;
             if (i < n_in) {
                 x[e] = in[src[map[i]] + base + i];
             } else {
@@ -2487,9 +2497,8 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scatter2g_kernel(const unsigne
 #pragma unroll
         for (uint32_t e = 0; e < kPer; ++e) r[e] = x[e] != kNoKey ? atomicAdd(&lh[digit(x[e])], 1u) : 0u;
         __syncthreads();  // every key loaded: S is free for the placement
-        bp_place_cur(
-            x, r, n_in, dg.nb2, digit, [&](uint32_t d) { return &bcur[bb + d]; },
-            [&](uint32_t d) { return (bb + d) * cg.capb; }, cg.capb, lh, wave_tot, S, out, flags);
+        bp_place_cur<kPer, decltype(digit), decltype(cursor), decltype(region), kThr>(
+            x, r, n_in, dg.nb2, digit, cursor, region, cg.capb, lh, wave_tot, S, out, flags);
     }
 }
 
@@ -2753,7 +2762,7 @@ hipError_t bp_level1(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_r
         // T chunks per level-2 tile: ~7/4 of a round at the hash-uniform mean (two rounds; kKeyChunk / nb1 keys
         // per chunk and bin)
         ws->bp_T = std::min<uint32_t>(kBpGatherMax, std::max<uint32_t>(1, kBpGatherTile * 7 / 4 * dg.nb1 / kKeyChunk));
-        bp_scatter1l_kernel<<<G, kKeyThreads, 0, st>>>(d_res, d_res_off, d_class, k, n, slots, ws->chunk_first.p, lay,
+        bp_scatter1l_kernel<KMP_L1_THREADS><<<G, KMP_L1_THREADS, 0, st>>>(d_res, d_res_off, d_class, k, n, slots, ws->chunk_first.p, lay,
                                                         dg, pw21, dlo, dhi, H1, ws->keys.p, ws->flags.p);
         if (dhi > dlo)
             bp_h1t_kernel<<<dim3((G + 31) / 32, (dhi - dlo + 31) / 32), 256, 0, st>>>(H1, G, dg.nb1, dlo, dhi,
@@ -2798,6 +2807,12 @@ bool cur_geometry(const Layout& lay, CurGeom* cg) {
     return true;
 }
 
+// KMP_GATHER_THREADS: workgroup size of the level-2 gather (a 4,096-key round either way).  512
+// threads x 8 keys (82 VGPRs, 6 waves per SIMD instead of 3) measured no faster at config 3
+// (buckets_level2 0.159-0.164 ms vs 0.149-0.160 ms), so 256 x 16 stays
+#ifndef KMP_GATHER_THREADS
+#define KMP_GATHER_THREADS 256
+#endif
 // Level 2, cursor variant: ws->keys (level 1) -> the bucket regions of ws->sorted, counts in ws->cur.
 int bp_level2c(kmp_postings* ws, const Layout& lay, hipStream_t st) {
     const BpDigits dg = bp_digits(lay);
@@ -2812,7 +2827,7 @@ int bp_level2c(kmp_postings* ws, const Layout& lay, hipStream_t st) {
         bp_cur_clear_kernel<<<std::min<uint32_t>((nb + 1023) / 1024, 1024), 1024, 0, st>>>(ws->cur.p, nb);
     if (c1 > c0 && ws->bp_local) {
         const uint32_t ntiles = (ws->bp_G + ws->bp_T - 1) / ws->bp_T, per = (ntiles * (c1 - c0) + 7) / 8;
-        bp_scatter2g_kernel<kBpGatherTile / kKeyThreads><<<8 * per, kKeyThreads, 0, st>>>(ws->keys.p, ws->bp.p + ws->bp_h1t, ws->bp_G, ws->bp_T,
+        bp_scatter2g_kernel<kBpGatherTile / KMP_GATHER_THREADS, KMP_GATHER_THREADS><<<8 * per, KMP_GATHER_THREADS, 0, st>>>(ws->keys.p, ws->bp.p + ws->bp_h1t, ws->bp_G, ws->bp_T,
                                                              ntiles, c1 - c0, dg, ws->cg, ws->cur.p, ws->sorted.p,
                                                              ws->flags.p, c0, c0);
     } else if (c1 > c0)
