@@ -799,7 +799,9 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
         for (uint32_t i = tid; i < kCap / kRunMin * 4; i += kThreads) CC[i] = 0;
     if (tid == 0) nheavy = hkeys = 0;
     __syncthreads();
-    // A. group slot + rank of every key (the keys were loaded before the table clear)
+    // A. group slot + rank of every key (the keys were loaded before the table clear).  (Issuing
+    // every key's first probe before using any result, then the collisions, then the counts, was
+    // measured slower: 643 -> 651 VALU per wave, group_expand 0.176 -> 0.180 ms at config 3)
     uint32_t xl[kE], sl[kE], rk[kE];
 #pragma unroll
     for (int e = 0; e < kE; ++e) {
@@ -1100,13 +1102,26 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
     // partials -> red, then kStN threads unpack, sum and post one (sharded) atomic each.  They
     // ride on the output scan's barriers; the last wave reserves the output range meanwhile.
     {
-        // DPP wave sums of packed 16-bit fields (each at most kCap per workgroup); the incidences
-        // are the output scan's total
-        const uint32_t s0 = wave_sum(st_sum | st_dist << 16), s1 = wave_sum(st_rep | st_heavy << 16);
-        const uint32_t s2 = wave_sum(st_cdf2), mx = wave_max(st_max);
+        // DPP wave sums of packed fields (the incidences are the output scan's total).  kCap below
+        // 2^11: Σ|K| | distinct << 11 | repeat << 22 (each at most kCap, repeat at most kCap / 2)
+        // and C(df,2) | heavy << 17 (at most kCap / 128 groups of C(128,2) < 2^17) in two sums;
+        // else 16-bit fields in three
+        const uint32_t mx = wave_max(st_max);
+        unsigned long long w0, c2;
+        if (kCap < 2048) {
+            const uint32_t s0 = wave_sum(st_sum | st_dist << 11 | st_rep << 22);
+            const uint32_t s1 = wave_sum(st_cdf2 | st_heavy << 17);
+            w0 = (s0 & 0x7FFu) | (unsigned long long)((s0 >> 11) & 0x7FFu) << 16 |
+                 (unsigned long long)(s0 >> 22) << 32 | (unsigned long long)(s1 >> 17) << 48;
+            c2 = s1 & 0x1FFFFu;
+        } else {
+            const uint32_t s0 = wave_sum(st_sum | st_dist << 16), s1 = wave_sum(st_rep | st_heavy << 16);
+            w0 = s0 | (unsigned long long)s1 << 32;
+            c2 = wave_sum(st_cdf2);
+        }
         if ((tid & 63) == 0) {
-            red[tid >> 6][0] = s0 | (unsigned long long)s1 << 32;
-            red[tid >> 6][1] = s2;
+            red[tid >> 6][0] = w0;
+            red[tid >> 6][1] = c2;
             red[tid >> 6][2] = mx;
         }
     }
