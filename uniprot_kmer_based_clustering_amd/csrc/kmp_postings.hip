@@ -733,7 +733,7 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
     __shared__ uint32_t gdupw[kCap / 32];  // per group start: the group holds such a duplicate
     __shared__ uint32_t SZ[kHeavySub + 1];
     __shared__ uint32_t wave_tot[kThreads / 64];
-    __shared__ unsigned long long red[kThreads / 64][3];
+    __shared__ uint32_t red[kThreads / 64][kStN];  // per wave: the statistics, unpacked
     __shared__ unsigned long long sbase;
     __shared__ unsigned long long hbase[kMaxHeavy];  // spill offset of each heavy group
     __shared__ uint32_t nheavy, hkeys;
@@ -849,19 +849,21 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
     for (int e = 0; e < kE; ++e) {
         cn[e] = rr[e] = 0;
         if (tid + e * kThreads >= n) continue;
+        if (rk[e] != 0) {  // a later key of a group of two or more: step C's word gives its size
+            cn[e] = 2;
+            continue;
+        }
         const uint32_t w = H[sl[e]];
         cn[e] = kMerge ? w >> hb : w;
-        if (rk[e] == 0) {
-            if (cn[e] > kHeavySub) {
-                if (a.spill) {
-                    rr[e] = atomicAdd(&nheavy, 1u);
-                    hbase[rr[e]] = atomicAdd(&hkeys, cn[e]);  // offset inside the bucket's spill range
-                }
-            } else if (cn[e] == 1) {
-                ++single;
-            } else {
-                rr[e] = atomicAdd(&SZ[cn[e]], 1u);
+        if (cn[e] > kHeavySub) {
+            if (a.spill) {
+                rr[e] = atomicAdd(&nheavy, 1u);
+                hbase[rr[e]] = atomicAdd(&hkeys, cn[e]);  // offset inside the bucket's spill range
             }
+        } else if (cn[e] == 1) {
+            ++single;
+        } else {
+            rr[e] = atomicAdd(&SZ[cn[e]], 1u);
         }
     }
     __syncthreads();
@@ -879,9 +881,10 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
 #pragma unroll
     for (int e = 0; e < kE; ++e)
         if (rk[e] == 0 && cn[e] >= 2) {
-            // start << 8 | size (start < 4,096: 20 bits); scored: s(x) of the group's k-mer on top
+            // start << 8 | size (start < 4,096: 20 bits); scored: s(x) of the group's k-mer in bits
+            // 24-30; a heavy group: bit 31 | its index in hbase
             const uint32_t sc = kScore && cn[e] <= kHeavySub ? kmer_self_score((uint32_t)(xk[e] >> hshift), a.k) << 24 : 0u;
-            H[sl[e]] = cn[e] > kHeavySub ? rr[e] : ((SZ[cn[e]] + rr[e] * cn[e]) << 8) | cn[e] | sc;
+            H[sl[e]] = cn[e] > kHeavySub ? 0x80000000u | rr[e] : ((SZ[cn[e]] + rr[e] * cn[e]) << 8) | cn[e] | sc;
         }
     __syncthreads();
     if (KMP_BS_CUT == 2 && small) return;
@@ -893,14 +896,16 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
         const uint32_t i = tid + e * kThreads;
         if (i >= n || cn[e] < 2) continue;  // singleton
         const uint32_t g = H[sl[e]];
-        if (cn[e] > kHeavySub) {
+        if (g >> 31) {  // heavy
             if (spill_dst) {
-                const unsigned long long pos = sbase + hbase[g] + rk[e];
+                const unsigned long long pos = sbase + hbase[g & 0x7FFFFFFFu] + rk[e];
                 if (pos < a.spill_cap) spill_dst[pos] = xk[e];
                 if (rk[e] == 0) spill_segment(a, (uint64_t)shard * a.spill_cap + pos, cn[e], false);
             }
+            cn[e] = kHeavySub + 1;
             continue;
         }
+        cn[e] = g & 255u;
         const uint32_t gs = kScore ? (g >> 8) & 0xFFFFu : g >> 8;
         T[gs + rk[e]] = g;
         if (runs_on && cn[e] >= kRunMin) {  // its rank in its class; placed below by class
@@ -1107,44 +1112,35 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
         // and C(df,2) | heavy << 17 (at most kCap / 128 groups of C(128,2) < 2^17) in two sums;
         // else 16-bit fields in three
         const uint32_t mx = wave_max(st_max);
-        unsigned long long w0, c2;
+        uint32_t v0, v1, v2, v3, v4;  // Σ|K|, distinct, repeat, heavy, C(df,2)
         if (kCap < 2048) {
             const uint32_t s0 = wave_sum(st_sum | st_dist << 11 | st_rep << 22);
             const uint32_t s1 = wave_sum(st_cdf2 | st_heavy << 17);
-            w0 = (s0 & 0x7FFu) | (unsigned long long)((s0 >> 11) & 0x7FFu) << 16 |
-                 (unsigned long long)(s0 >> 22) << 32 | (unsigned long long)(s1 >> 17) << 48;
-            c2 = s1 & 0x1FFFFu;
+            v0 = s0 & 0x7FFu, v1 = (s0 >> 11) & 0x7FFu, v2 = s0 >> 22, v3 = s1 >> 17, v4 = s1 & 0x1FFFFu;
         } else {
             const uint32_t s0 = wave_sum(st_sum | st_dist << 16), s1 = wave_sum(st_rep | st_heavy << 16);
-            w0 = s0 | (unsigned long long)s1 << 32;
-            c2 = wave_sum(st_cdf2);
+            v0 = s0 & 0xFFFFu, v1 = s0 >> 16, v2 = s1 & 0xFFFFu, v3 = s1 >> 16, v4 = wave_sum(st_cdf2);
         }
         if ((tid & 63) == 0) {
-            red[tid >> 6][0] = w0;
-            red[tid >> 6][1] = c2;
-            red[tid >> 6][2] = mx;
+            uint32_t* rw = red[tid >> 6];
+            rw[kStSumS] = v0, rw[kStDistinct] = v1, rw[kStRepeat] = v2, rw[kStHeavy] = v3, rw[kStCdf2] = v4;
+            rw[kStMaxDf] = mx, rw[kStInc] = 0;
         }
     }
     uint32_t excl, total;
     block_scan_n<kThreads>(mine, excl, total, wave_tot);
     if (tid == kThreads - 64) sbase = total ? atomicAdd(&a.cursor[shard], (unsigned long long)total) : 0ull;
     if (tid < kStN) {
-        unsigned long long v = 0;
+        uint32_t v = 0;
+#pragma unroll
         for (int w = 0; w < kThreads / 64; ++w) {
-            const unsigned long long w0 = red[w][0], c2 = red[w][1], mx = red[w][2];
-            const unsigned long long x = tid == kStSumS     ? w0 & 0xFFFF
-                                         : tid == kStDistinct ? (w0 >> 16) & 0xFFFF
-                                         : tid == kStRepeat   ? (w0 >> 32) & 0xFFFF
-                                         : tid == kStHeavy    ? w0 >> 48
-                                         : tid == kStCdf2     ? c2 & 0xFFFFFFFFull
-                                         : tid == kStInc      ? 0ull
-                                                              : mx;
-            v = tid == kStMaxDf ? (v > x ? v : x) : v + x;
+            const uint32_t x = red[w][tid];
+            v = tid == kStMaxDf ? max(v, x) : v + x;
         }
         if (tid == kStInc) v = total;
         unsigned long long* g = a.gstats + (uint64_t)shard * 8 + tid;  // sharded: no hot word
-        if (tid == kStMaxDf) atomicMax(g, v);
-        else if (v) atomicAdd(g, v);
+        if (tid == kStMaxDf) atomicMax(g, (unsigned long long)v);
+        else if (v) atomicAdd(g, (unsigned long long)v);
     }
     __syncthreads();
     if (KMP_BS_CUT == 5 && small) return;
