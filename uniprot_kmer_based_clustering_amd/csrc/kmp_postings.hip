@@ -737,6 +737,7 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
     __shared__ unsigned long long sbase;
     __shared__ unsigned long long hbase[kMaxHeavy];  // spill offset of each heavy group
     __shared__ uint32_t nheavy, hkeys;
+    __shared__ uint32_t anydup;  // some group of the bucket holds a duplicate window (gdupw nonzero)
     // class runs (step C): per group of at least kRunMin keys (indexed by its start / kRunMin, unique
     // since such groups start kRunMin apart) the keys of each of up to 16 classes, 8 bits a class
     __shared__ uint32_t CC[kCap / kRunMin * 4];
@@ -797,7 +798,7 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
     const bool runs_on = KMP_CLASS_RUNS && !kRows && a.require_diff && cb >= 1 && cb <= 4;
     if (runs_on)
         for (uint32_t i = tid; i < kCap / kRunMin * 4; i += kThreads) CC[i] = 0;
-    if (tid == 0) nheavy = hkeys = 0;
+    if (tid == 0) nheavy = hkeys = anydup = 0;
     __syncthreads();
     // A. group slot + rank of every key (the keys were loaded before the table clear).  (Issuing
     // every key's first probe before using any result, then the collisions, then the counts, was
@@ -971,6 +972,7 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
             auto mark = [&](uint32_t j) {
                 atomicOr(&dupw[j >> 5], 1u << (j & 31));
                 atomicOr(&gdupw[s[e] >> 5], 1u << (s[e] & 31));
+                anydup = 1;
             };
             if (kMask && en[e] - s[e] <= 33u) {
                 // four partners per step (two ds_read2 of consecutive words; words past en are read
@@ -1009,6 +1011,7 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
             if (Bl[j] == xl[e]) {
                 atomicOr(&dupw[i >> 5], 1u << (i & 31));
                 atomicOr(&gdupw[s[e] >> 5], 1u << (s[e] & 31));
+                anydup = 1;
                 break;
             }
     }
@@ -1027,6 +1030,7 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
     // kRows: bit t = position s + t (every partner of a larger protein, anywhere in the group)
     auto run_mode = [&](int e) { return runs_on && !gd[e] && en[e] - s[e] >= kRunMin; };
     auto mask_mode = [&](int e) { return kMask && !gd[e] && en[e] - s[e] <= (kRows ? 32u : 33u) && !run_mode(e); };
+    const bool anyd = anydup;  // (uniform) most buckets hold no duplicate window: no gdupw reads
     uint32_t st_sum = single, st_dist = single, st_rep = 0, st_cdf2 = 0, st_max = single ? 1u : 0u, st_heavy = 0,
              mine = 0;
 #pragma unroll
@@ -1036,7 +1040,7 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
         cnt[e] = 0;
         gd[e] = false;
         if (i >= nm) continue;
-        gd[e] = (gdupw[s[e] >> 5] >> (s[e] & 31)) & 1u;
+        gd[e] = anyd && ((gdupw[s[e] >> 5] >> (s[e] & 31)) & 1u);
         if (gd[e] && is_dup(i)) continue;
         uint32_t f, c = 0, bits = 0;
         if (kRows) {
