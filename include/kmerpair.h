@@ -443,6 +443,16 @@ enum { KMP_LAYOUT_FLAT = 0, KMP_LAYOUT_BUCKETED = 1, KMP_LAYOUT_BUCKETED_HEAVY =
 int kmp_postings_set_layout(kmp_postings* ws, int bucketed);
 int kmp_postings_last_layout(const kmp_postings* ws);
 uint32_t kmp_postings_last_overflow_blocks(const kmp_postings* ws);
+/* The row-block tail the last call reduced its pair keys with (combine_edges, graph/mod.rs:322-546):
+ * KMP_TAIL_FAST (unscored calls: pair keys into fixed row-block regions, one LDS hash-aggregate +
+ * rank per block writing the edges in canonical order at offsets from a decoupled look-back),
+ * KMP_TAIL_COUNT (histogram, scan, scatter, block sort, emit: scored / multi-k calls, and a shape
+ * whose row-block regions overflowed), or -1 (the flat layout's global sort). */
+enum { KMP_TAIL_COUNT = 0, KMP_TAIL_FAST = 1 };
+int kmp_postings_last_tail(const kmp_postings* ws);
+/* kmp_postings_set_tail: KMP_TAIL_FAST (default: the fast tail where it applies) or KMP_TAIL_COUNT
+ * (the counting tail only).  Same edges either way. */
+int kmp_postings_set_tail(kmp_postings* ws, int mode);
 /* The bucketed step as a HIP graph (default 1): captured on the second call with an unchanged
  * shape (pointers, sizes, options, workspace buffers), replayed after that.
  * kmp_postings_graph_replays: calls served by a replay so far. */
@@ -535,7 +545,8 @@ int kmp_dev_pairs_rows_multi(kmp_postings* const* ws, const int* ks, uint32_t nk
  *     d_stats[8] (Σ|K(p)|, distinct, repeat,
  *     Σ C(df,2), max df, heavy entries, incidences, 0 — this rank's k-mers) are written on `stream`.
  *     learn: the previous call's flags reduced (max) over the ranks, or NULL for a first call;
- *     every rank grows its capacities from them identically.
+ *     every rank grows its capacities from them identically.  KMP_EOVERFLOW (heavy path only):
+ *     the rank's spill regions kept overflowing; d_send and d_flags were not written (call again). 
  *   exchange (the caller's collective): region d of rank g's d_send -> region g of rank d's receive
  *     buffer (an all-to-all of equal splits, cap keys each).
  *   kmp_dev_split_edges   the m = parts * cap received keys -> the canonical edges of rows

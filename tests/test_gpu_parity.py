@@ -263,21 +263,24 @@ def test_bucketed_small_batches(oracle_mod, n):
         np.testing.assert_array_equal(pipe.edges()[2], w)
 
 
-def test_residue_graph_replay(oracle_mod):
+@pytest.mark.parametrize("tail", ["fast", "count"])
+def test_residue_graph_replay(oracle_mod, tail):
     """The single-synchronisation residue step replayed from its HIP graph: every replay (stage
-    timing off and on) is bit-exact; an edge buffer that moves (overflow rerun) forces a new
+    timing off and on) is bit-exact, with either row-block tail (the fast tail's look-back words
+    and cursors are reused across replays); an edge buffer that moves (overflow rerun) forces a new
     capture and stays exact."""
     import torch
     from uniprot_kmer_based_clustering_amd.device import DevicePipeline
     b = K.synth(20000, 21)
     p, q, w = oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=7, threads=8).pairs()
     pipe = DevicePipeline(b, 7, "cuda:0")
+    pipe.set_tail(tail)
     for timing in (False, True):
         pipe.set_stage_timing(timing)
         for _ in range(4):
             assert pipe.step(engine="residues") == len(p)
             torch.cuda.synchronize()
-            assert pipe.last_tail() == "rows"
+            assert pipe.last_tail() == ("fast" if tail == "fast" else "rows")
             ep, eq, ew = pipe.edges()
             np.testing.assert_array_equal(ep, p)
             np.testing.assert_array_equal(eq, q)
@@ -314,7 +317,7 @@ def test_partitions_bit_exact(oracle_mod, uni, case):
         for _ in range(4):
             assert pipe.step(engine="residues") == len(p)
             torch.cuda.synchronize()
-            assert pipe.last_layout() == "bucketed" and pipe.last_tail() == "rows"
+            assert pipe.last_layout() == "bucketed" and pipe.last_tail() in ("rows", "fast")
             np.testing.assert_array_equal(pipe.edges()[0], p)
             np.testing.assert_array_equal(pipe.edges()[1], q)
             np.testing.assert_array_equal(pipe.edges()[2], w)
@@ -349,7 +352,8 @@ def test_rowtail_overflow_blocks(oracle_mod):
         for it in range(3):
             m = pipe.step(engine="residues")
             torch.cuda.synchronize()
-            assert pipe.last_tail() == "rows" and m == len(p)
+            # the long row passes a fast-tail region: the counting tail (learned for the shape)
+            assert pipe.last_tail() == ("rows" if long_first else "fast") and m == len(p)
             if it == 0:
                 assert (pipe.overflow_blocks() > 0) == long_first
             np.testing.assert_array_equal(pipe.edges()[0], p)
@@ -406,7 +410,7 @@ def test_uniprot_k5_on_bucketed_heavy_path(oracle_mod, uni):
     for _ in range(2):
         m = pipe.step(engine="residues")
         torch.cuda.synchronize()
-        assert pipe.last_layout() == "bucketed" and pipe.last_heavy() and pipe.last_tail() == "rows"
+        assert pipe.last_layout() == "bucketed" and pipe.last_heavy() and pipe.last_tail() in ("rows", "fast")
         assert m == g["n_edges"]
         assert edges_sha256(*pipe.edges()) == g["edges_sha256"]
         st = pipe.postings_stats.as_dict()
@@ -490,7 +494,7 @@ def test_device_pipeline_matches_oracle(oracle_mod):
             np.testing.assert_array_equal(pipe.edges()[1], q)
             np.testing.assert_array_equal(pipe.edges()[2], w)
             assert pipe.last_layout() == ("bucketed" if bucketed else "flat")
-            assert pipe.last_tail() == ("rows" if bucketed else "sort")
+            assert pipe.last_tail() in (("rows", "fast") if bucketed else ("sort",))
         for ms in (2, 5):  # min_shared filter inside both tails
             keep = w >= ms
             assert pipe.step(min_shared=ms, engine="residues") == int(keep.sum())
@@ -509,3 +513,66 @@ def test_device_pipeline_matches_oracle(oracle_mod):
     so, sv = o.sets()
     for pr in (0, 6999, 7000, 7001, 19999):
         np.testing.assert_array_equal(pipe.set_of(pr), sv[so[pr]:so[pr + 1]])
+
+
+def _shared_kmer_batch(n, seed):
+    """n random proteins (~300 aa) that all carry one 7-mer: every pair shares it (w >= 1), so row p
+    holds ~n - p distinct partners of other classes — rows far past the fast tail's rank bound."""
+    rng = np.random.default_rng(seed)
+    alpha = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", dtype=np.uint8)
+    seqs, classes = [], []
+    for _ in range(n):
+        s = alpha[rng.integers(0, 20, 300)].tobytes()
+        at = int(rng.integers(0, 290))
+        seqs.append(s[:at] + b"WCWCWCW" + s[at + 7:])
+        classes.append(f"c{int(rng.integers(0, 15))}")
+    return make_batch(seqs, classes)
+
+
+@pytest.mark.parametrize("tail", ["fast", "count"])
+def test_fast_tail_sort_fallback(oracle_mod, tail):
+    """Rows with more distinct partners than the fast tail's per-row rank bound (kFtRankMax = 256):
+    those row blocks sort their keys (block radix sort + run-length encoding) inside the fast
+    reduce; edges equal the oracle's with either tail, min_shared 1 and 2, over graph replays."""
+    import torch
+    from uniprot_kmer_based_clustering_amd.device import DevicePipeline
+    res, off, cls = _shared_kmer_batch(700, 31)
+    o = oracle_mod.Oracle(res, off, cls, k=7, threads=8)
+    p, q, w = o.pairs()
+    assert np.bincount(p).max() > 256  # a row past the rank bound
+    pipe = DevicePipeline(K.Proteins(res, off, cls), 7, "cuda:0")
+    pipe.set_tail(tail)
+    for ms in (1, 2, 1):
+        keep = w >= ms
+        for _ in range(3):
+            assert pipe.step(min_shared=ms, engine="residues") == int(keep.sum())
+            torch.cuda.synchronize()
+            assert pipe.last_tail() == ("fast" if tail == "fast" else "rows")
+            ep, eq, ew = pipe.edges()
+            np.testing.assert_array_equal(ep, p[keep])
+            np.testing.assert_array_equal(eq, q[keep])
+            np.testing.assert_array_equal(ew, w[keep])
+
+
+@pytest.mark.parametrize("ms", [2, 3, 7])
+def test_fast_tail_min_shared_synthetic(oracle_mod, ms):
+    """min_shared > 1 on the fast tail (pairs below it dropped before the rank, so the kept pairs stay
+    canonical and contiguous), against the oracle and the counting tail on a 30k synthetic batch."""
+    import torch
+    from uniprot_kmer_based_clustering_amd.device import DevicePipeline
+    b = K.synth(30000, 29)
+    p, q, w = oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=7, threads=8).pairs()
+    keep = w >= ms
+    got = {}
+    for tail in ("fast", "count"):
+        pipe = DevicePipeline(b, 7, "cuda:0")
+        pipe.set_tail(tail)
+        for _ in range(2):
+            assert pipe.step(min_shared=ms, engine="residues") == int(keep.sum())
+        torch.cuda.synchronize()
+        got[tail] = pipe.edges()
+        assert pipe.last_tail() == ("fast" if tail == "fast" else "rows")
+    for t in got.values():
+        np.testing.assert_array_equal(t[0], p[keep])
+        np.testing.assert_array_equal(t[1], q[keep])
+        np.testing.assert_array_equal(t[2], w[keep])

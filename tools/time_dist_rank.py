@@ -3,7 +3,9 @@
   kmer   the k-mer split: every rank's kmp_dev_split_expand (its share of the bucket hash range,
          pair keys routed by row owner) and kmp_dev_split_edges over the keys it would receive.
 For G = 1, 2, 4, 8 each rank's stages are timed in turn on its own DevicePipeline; the slowest
-rank bounds the step.  Exchanges (all-to-all, gather) are not included.
+rank bounds the step.  Exchanges (all-to-all, gather) are not included.  Each phase is reported as
+wall time (host clock over back-to-back calls: launches and the edges phase's read-back included)
+and device time (HIP events around each call on its stream).
 python tools/time_dist_rank.py [config3|config1] [rows|kmer] [G ...]"""
 import json
 import os
@@ -22,6 +24,8 @@ from uniprot_kmer_based_clustering_amd.dist import row_ranges  # noqa: E402
 
 
 def timed(fn, reps=10):
+    """(wall ms per call, device ms per call): wall = host clock over reps back-to-back calls;
+    device = HIP events recorded around each call on the stream its kernels run on."""
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
@@ -29,7 +33,14 @@ def timed(fn, reps=10):
     for _ in range(reps):
         fn()
     torch.cuda.synchronize()
-    return (time.perf_counter() - t0) / reps * 1e3
+    wall = (time.perf_counter() - t0) / reps * 1e3
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in ev:
+        a.record()
+        fn()
+        b.record()
+    torch.cuda.synchronize()
+    return wall, sum(a.elapsed_time(b) for a, b in ev) / reps
 
 
 def kmer_ranks(b, k, g):
@@ -43,17 +54,18 @@ def kmer_ranks(b, k, g):
         for r in range(g):
             pipes[r].split_expand(r, g, cap, sends[r], flags[r], stats[r], learn=learn)
         fl = torch.stack(flags).max(dim=0).values.cpu().tolist()
-        if not fl[_lib.KMP_SPLIT_RERUN]:
+        if not fl[_lib.KMP_SPLIT_RERUN] and not fl[_lib.KMP_SPLIT_HEAVY]:
             break
         learn = fl
         cap = max(cap, fl[_lib.KMP_SPLIT_MAX_PART] * 17 // 16 + 1024)
     recvs = [torch.cat([sends[r][d * cap:(d + 1) * cap] for r in range(g)]) for d in range(g)]
     per = []
     for r, (lo, hi) in enumerate(row_ranges(b.n, g)):
-        t1 = timed(lambda: pipes[r].split_expand(r, g, cap, sends[r], flags[r], stats[r]))
-        t2 = timed(lambda: pipes[r].split_edges(recvs[r], lo, hi))
+        t1, d1 = timed(lambda: pipes[r].split_expand(r, g, cap, sends[r], flags[r], stats[r]))
+        t2, d2 = timed(lambda: pipes[r].split_edges(recvs[r], lo, hi))
         per.append({"rows": [lo, hi], "expand_ms": t1, "edges_ms": t2, "ms": t1 + t2,
-                    "send_MB": g * cap * 8 / 1e6, "edges": pipes[r].n_edges})
+                    "dev_expand_ms": d1, "dev_edges_ms": d2, "dev_ms": d1 + d2,
+                    "send_MB": g * cap * 8 / 1e6, "sent_keys": int(stats[r][6].item()), "edges": pipes[r].n_edges})
     return per
 
 
@@ -64,8 +76,8 @@ def main():
     b = load_batch(name)
     out = {"config": name, "mode": mode, "n": b.n, "ranks": {}}
     full = DevicePipeline(b, k, "cuda:0")
-    out["single_gpu_ms"] = timed(lambda: full.step(), 20)
-    print("single", round(out["single_gpu_ms"], 3), flush=True)
+    out["single_gpu_ms"], out["single_gpu_dev_ms"] = timed(lambda: full.step(), 20)
+    print("single", round(out["single_gpu_ms"], 3), "device", round(out["single_gpu_dev_ms"], 3), flush=True)
     del full
     for g in [int(x) for x in sys.argv[3:]] or (1, 2, 4, 8):
         if mode == "kmer":
@@ -74,10 +86,13 @@ def main():
             per = []
             for r, (lo, hi) in enumerate(row_ranges(b.n, g)):
                 pipe = DevicePipeline(b, k, "cuda:0")
-                per.append({"rows": [lo, hi], "ms": timed(lambda: pipe.rows(lo, hi)), "edges": pipe.n_edges})
+                w, d = timed(lambda: pipe.rows(lo, hi))
+                per.append({"rows": [lo, hi], "ms": w, "dev_ms": d, "edges": pipe.n_edges})
                 del pipe
-        out["ranks"][g] = {"max_ms": max(x["ms"] for x in per), "per_rank": per}
-        print(g, round(out["ranks"][g]["max_ms"], 3), [round(x["ms"], 3) for x in per], flush=True)
+        out["ranks"][g] = {"max_ms": max(x["ms"] for x in per), "max_dev_ms": max(x["dev_ms"] for x in per),
+                           "per_rank": per}
+        print(g, "wall", round(out["ranks"][g]["max_ms"], 3), [round(x["ms"], 3) for x in per],
+              "device", round(out["ranks"][g]["max_dev_ms"], 3), [round(x["dev_ms"], 3) for x in per], flush=True)
         torch.cuda.empty_cache()
     print(json.dumps(out))
 

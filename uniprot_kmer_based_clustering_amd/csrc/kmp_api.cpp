@@ -711,9 +711,12 @@ struct PassPlan {
         const double A = a, B = b, N = n;
         return (B - A) * (N - 1) - (B * (B - 1) - A * (A - 1)) / 2;
     }
+    // the end of the pass starting at a: always > a while a < end (a zero max_rows is rejected
+    // by the callers before planning: a batch too large for the scored key)
     uint32_t next(uint32_t a) const {
         const uint32_t e = std::min(end, n);
         if (a >= e) return e;
+        if (max_rows == 0) return a;
         const uint32_t lim = (uint32_t)std::min<uint64_t>(e, (uint64_t)a + max_rows);
         if (density < 0) return std::min<uint32_t>(lim, a + std::max<uint32_t>(1, n / 256));
         const double target = 0.75 * budget / std::max(density, 1e-12);
@@ -821,6 +824,7 @@ int pass_pairs(kmp_ctx* c, const kmp_pair_opts& o, uint64_t* count, bool scored)
     int rc = KMP_OK;
     for (uint32_t a = 0; a < c->n && rc == KMP_OK;) {
         const uint32_t b = plan.next(a);
+        if (b <= a) return fail(c, KMP_EINVAL, "pass planner: no row fits one pass at N = %u", c->n);
         kmp_postings_stats st{};
         uint64_t ne = 0;
         rc = rows_into(c, c->postings, c->k_sets, o, a, b, c->ep, c->eq, c->ew, c->edge_cap, off, &ne, &st,
@@ -1047,7 +1051,9 @@ int kmp_pairs(kmp_ctx* c, const kmp_pair_opts* opts, kmp_edges** out) {
         if (!c->postings) KMP_TRY(c, kmp_postings_create(&c->postings));
         const uint64_t slots = kmp_set_capacity(c->n, c->total_res);
         const bool residues = o.engine == KMP_ENGINE_AUTO || o.engine == KMP_ENGINE_RESIDUES;
-        const bool scored = residues && o.score == KMP_SCORE_BLOSUM;  // the score summed in the reduction
+        // the score summed in the reduction; a batch too large for the scored key (N >= 2^24:
+        // kmp_dev_rows_max 0) takes the unscored reduction and the per-edge BLOSUM pass of finish_edges
+        const bool scored = residues && o.score == KMP_SCORE_BLOSUM && kmp_dev_rows_max(c->n, 1) > 0;
         if (residues && (c->pass_keys || slots > kPassSlots || (scored && kmp_dev_rows_max(c->n, 1) < c->n))) {
             uint64_t total = 0;
             KMP_TRY(c, pass_pairs(c, o, &total, scored));
@@ -1250,6 +1256,7 @@ struct StreamLane {
     Lane L;
     int device = 0;
     uint32_t rank = 0, row_lo = 0, row_hi = 0;
+    uint32_t share = 1;  // lanes streaming on this lane's device at once: they split its memory budget
     std::vector<std::unique_ptr<kmp_kset>>* ks = nullptr;
     DevBuf *ep = nullptr, *eq = nullptr, *ew = nullptr, *mscore = nullptr, *mwk = nullptr, *mscratch = nullptr;
     kmp::DigestAcc* acc = nullptr;
@@ -1291,11 +1298,17 @@ static int stream_passes(kmp_ctx* c, const kmp_pair_opts& o, const int* ks, uint
     if (!dev.ready()) return fail(c, KMP_EDEVICE, "events");
     const bool blosum = o.score == KMP_SCORE_BLOSUM;
     const uint64_t slots = kmp_set_capacity(c->n, c->total_res);
-    PassPlan plan{c->n, (double)pass_budget(c, nk == 2)};
+    // the budget comes from the device's free memory unless set (kmp_ctx_set_pass_keys): virtual
+    // ranks on one device (devices = [0, 0, ...]) take an equal part of it each
+    PassPlan plan{c->n, (double)(c->pass_keys ? pass_budget(c, nk == 2) : pass_budget(c, nk == 2) / std::max(1u, ln.share))};
     plan.end = ln.row_hi;
     const bool fused = nk == 2;  // both k reduced together (kmp_dev_pairs_rows_multi): no merge
     if (fused) plan.max_rows = kmp_dev_rows_max(c->n, 2);
     else if (blosum) plan.max_rows = kmp_dev_rows_max(c->n, 1);
+    if (plan.max_rows == 0)
+        return fail(c, KMP_EINVAL, "%s at N = %u: the %s key needs more than 31 bits (N < 2^%u)",
+                    fused ? "combined k" : "BLOSUM stream", c->n, fused ? "fused k-bit + score" : "scored",
+                    fused ? 23u : 24u);
     if (!c->pass_keys && slots <= kPassSlots && plan.max_rows >= ln.row_hi - ln.row_lo)
         plan.density = 0;  // small batch: one pass
     const hipStream_t st = ln.L.stream;
@@ -1312,6 +1325,7 @@ static int stream_passes(kmp_ctx* c, const kmp_pair_opts& o, const int* ks, uint
     int rc = KMP_OK;
     for (uint32_t a = ln.row_lo; a < ln.row_hi && rc == KMP_OK;) {
         const uint32_t b = plan.density == 0 ? ln.row_hi : plan.next(a);
+        if (b <= a) return fail(c, KMP_EINVAL, "pass planner: no row fits one pass at N = %u", c->n);
         MergeIn in{};
         in.nk = nk;
         uint64_t total = 0, inc = 0;
@@ -1621,6 +1635,9 @@ static int multi_stream(kmp_ctx* c, const kmp_pair_opts& o, const int* ks, uint3
         }
         ln.rank = g;
     }
+    for (uint32_t g = 0; g < G; ++g)
+        for (uint32_t h = 0; h < G; ++h)
+            if (h != g && lanes[h].device == lanes[g].device) ++lanes[g].share;
     run_parts((int)G, [&](int gi) {
         const uint32_t g = (uint32_t)gi;
         StreamLane& ln = lanes[g];

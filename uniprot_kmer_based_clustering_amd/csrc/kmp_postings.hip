@@ -58,6 +58,21 @@ unsigned bits_for(uint64_t v) {  // bits needed for values < v
 
 constexpr unsigned long long kNoKey = ~0ull;
 
+// compute units of the current device (persistent grids), looked up once per device and thread
+uint32_t device_cus() {
+    static thread_local int dev = -1;
+    static thread_local uint32_t cus = 256;
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess) return cus;
+    if (d != dev) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && v > 0)
+            cus = (uint32_t)v;
+        dev = d;
+    }
+    return cus;
+}
+
 
 // rocprim 4.2 (ROCm 7.2): with the default config, radix_sort_keys on fewer than 1M keys takes a
 // merge-sort path that returns unsorted, non-permuted data for bit ranges [b, 64) with b > 0
@@ -632,6 +647,12 @@ __device__ __forceinline__ void block_scan_n(uint32_t v, uint32_t& excl, uint32_
     total = tot;
 }
 
+constexpr uint32_t kSplitMax = 64;  // ranks of the k-mer split
+struct SplitRows {
+    uint32_t start[kSplitMax + 1];  // row range of rank d: [start[d], start[d+1])
+    uint32_t parts;
+};
+
 // Arguments of the bucket kernels (one struct, passed by value).
 //   out / shard_cap / cursor: kShards pair-key regions; a workgroup reserves its range on
 //     cursor[b % kShards] and writes the keys min(p,q) * mul + max(p,q) (writes past shard_cap are
@@ -673,6 +694,13 @@ struct BucketArgs {
     int k;
     unsigned sb;
     uint32_t sor;
+    // k-mer split, routed (send != nullptr): each pair key goes straight to the send region of the
+    // rank owning its row (rows), sub-region `shard` of send_sub keys, reserved on
+    // dcur[rank * kShards + shard]; no shard regions, no route kernel (unscored calls only)
+    unsigned long long* send;
+    uint64_t send_cap, send_sub;
+    unsigned long long* dcur;
+    SplitRows rows;
 };
 
 // descriptor: spill index (40 bits) | keys (23 bits) << 40 | whole bucket (several k-mers) << 63
@@ -1133,7 +1161,7 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
     }
     uint32_t excl, total;
     block_scan_n<kThreads>(mine, excl, total, wave_tot);
-    if (tid == kThreads - 64) sbase = total ? atomicAdd(&a.cursor[shard], (unsigned long long)total) : 0ull;
+    if (tid == kThreads - 64 && !a.send) sbase = total ? atomicAdd(&a.cursor[shard], (unsigned long long)total) : 0ull;
     if (tid < kStN) {
         uint32_t v = 0;
 #pragma unroll
@@ -1190,6 +1218,72 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
         }
     };
     constexpr uint32_t kStage = kTab / 2;
+    if (!kScore && a.send) {  // the k-mer split: straight to the row owners' send sub-regions
+        // (SZ and CC are dead after step C: per-destination counts / row starts, and bases)
+        uint32_t* dcnt = SZ;
+        uint32_t* rst = SZ + 64;
+        uint32_t* dbase = CC;
+        static_assert(kHeavySub + 1 >= 64 + kSplitMax + 1 && kCap / kRunMin * 4 >= kSplitMax, "route tables");
+        const uint32_t parts = a.rows.parts;
+        if (tid < (int)parts) dcnt[tid] = 0;
+        if (tid <= (int)parts) rst[tid] = a.rows.start[tid];
+        const unsigned pb = lay.pbits;
+        auto dest = [&](unsigned long long key) {  // the rank owning row min(p, q)
+            const uint32_t p = (uint32_t)(key >> pb);
+            uint32_t lo = 0, hi = parts;  // last d with rst[d] <= p
+            while (lo + 1 < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (rst[mid] <= p) lo = mid;
+                else hi = mid;
+            }
+            return lo;
+        };
+        auto reserve = [&]() {
+            if (tid < (int)parts)
+                dbase[tid] = dcnt[tid] ? (uint32_t)atomicAdd(&a.dcur[tid * kShards + shard], (unsigned long long)dcnt[tid])
+                                       : 0u;
+        };
+        auto put = [&](uint32_t d, uint32_t pos, unsigned long long key) {
+            if (pos < a.send_sub) a.send[d * a.send_cap + (uint64_t)shard * a.send_sub + pos] = key;
+        };
+        if (total <= kStage) {  // staged: ranked per destination in LDS, one reservation each
+            unsigned long long* stage = reinterpret_cast<unsigned long long*>(H);
+            uint32_t lpos = excl;
+            if (mine) partners([&](unsigned long long key) { stage[lpos++] = key; });
+            __syncthreads();
+            constexpr uint32_t kSt = kStage / kThreads;
+            uint32_t dr[kSt];
+#pragma unroll
+            for (uint32_t j = 0; j < kSt; ++j) {
+                const uint32_t t = tid + j * kThreads;
+                dr[j] = ~0u;
+                if (t < total) {
+                    const uint32_t d = dest(stage[t]);
+                    dr[j] = d << 24 | atomicAdd(&dcnt[d], 1u);
+                }
+            }
+            __syncthreads();
+            reserve();
+            __syncthreads();
+#pragma unroll
+            for (uint32_t j = 0; j < kSt; ++j)
+                if (dr[j] != ~0u) put(dr[j] >> 24, dbase[dr[j] >> 24] + (dr[j] & 0xFFFFFFu), stage[tid + j * kThreads]);
+        } else {  // a bucket above the staging: count, reserve, then write with LDS cursors
+            __syncthreads();
+            if (mine) partners([&](unsigned long long key) { atomicAdd(&dcnt[dest(key)], 1u); });
+            __syncthreads();
+            reserve();
+            __syncthreads();
+            if (tid < (int)parts) dcnt[tid] = 0;
+            __syncthreads();
+            if (mine)
+                partners([&](unsigned long long key) {
+                    const uint32_t d = dest(key);
+                    put(d, dbase[d] + atomicAdd(&dcnt[d], 1u), key);
+                });
+        }
+        return;
+    }
     if (total <= kStage) {  // uniform over the workgroup
         unsigned long long* stage = reinterpret_cast<unsigned long long*>(H);
         uint32_t lpos = excl;
@@ -2352,63 +2446,199 @@ constexpr uint32_t kBpGatherTile = 4096;  // keys per round of a level-2 tile
 #ifndef KMP_L1_THREADS
 #define KMP_L1_THREADS 512
 #endif
-// level 1, local: the chunk's own-digit keys grouped by digit1 at out[chunk * kKeyChunk ...]
+
+// Chunk descriptors of the local level 1: desc[c] = {first, last, r0, r1} = the proteins whose
+// regions overlap chunk c ([first, last]; n is the tail past the last region) and the residue span
+// [r0, r1) its windows read.  One thread per protein p <= n writes the chunks that start in its
+// region (first, r0) and those that end in it (last, r1); the grid also clears the cursor level 2's
+// bucket counts (one launch less per step).  Residue offsets fit u32 (bp_level1 checks slots).
+__global__ void chunk_desc_kernel(const uint64_t* __restrict__ res_off, uint32_t n, uint64_t slots,
+                                  uint32_t n_chunks, int k, uint4* __restrict__ desc, uint32_t* __restrict__ cur,
+                                  uint32_t ncur) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint32_t i = t; i < ncur; i += gridDim.x * blockDim.x) cur[i] = 0;
+    const uint32_t p = t;
+    if (p > n) return;
+    const uint64_t off = res_off[p], L = p < n ? res_off[p + 1] - off : 0;
+    const uint64_t b = set_base(off, p), e = p < n ? set_base(res_off[p + 1], p + 1) : slots;
+    for (uint64_t c = (b + kKeyChunk - 1) / kKeyChunk; c * kKeyChunk < e && c < n_chunks; ++c) {
+        desc[c].x = p;
+        desc[c].z = (uint32_t)(off + min<uint64_t>(c * kKeyChunk - b, L));
+    }
+    // chunks whose last slot min((c + 1) * kKeyChunk, slots) - 1 lies in [b, e)
+    for (uint64_t c = b / kKeyChunk; c < n_chunks; ++c) {
+        const uint64_t c1 = min<uint64_t>((c + 1) * kKeyChunk, slots);
+        if (c1 - 1 >= e) break;
+        if (c1 - 1 < b) continue;
+        desc[c].y = p;
+        desc[c].w = (uint32_t)(p < n ? off + min<uint64_t>(L, c1 - b + k - 1) : off);
+    }
+}
+
+// waves per SIMD the persistent level 1 is compiled for (VGPR budget: 6 -> 80 registers, three
+// 512-thread workgroups per CU)
+#ifndef KMP_L1P_WAVES
+#define KMP_L1P_WAVES 6
+#endif
+// Level 1, local, persistent: workgroup w takes chunks w, w + grid, ...; chunk c's keys of the
+// call's digits [dlo, dhi) grouped by digit1 at out[c * kKeyChunk ...] (its own 4,096-key segment),
+// its run table (start << 16 | count per own digit) in H1[c][digit - dlo].  The next chunk's
+// residues and protein table are loaded into registers while this chunk is keyed, ranked and
+// written (its descriptor one chunk earlier still), so the three dependent global round trips of
+// a chunk (descriptor, protein offsets, residues) stay off the critical path: the one-chunk-per-
+// workgroup kernel spent ~13 us per chunk waiting on them.
 template <uint32_t kThr>
-__global__ __launch_bounds__(kThr) void bp_scatter1l_kernel(
+__global__ __launch_bounds__(kThr, KMP_L1P_WAVES) void bp_scatter1p_kernel(
     const uint8_t* __restrict__ res, const uint64_t* __restrict__ res_off, const uint16_t* __restrict__ cls, int k,
-    uint32_t p_hi, uint64_t slots, const uint32_t* __restrict__ chunk_first, Layout lay, BpDigits dg, uint32_t pw21,
+    uint32_t n, uint64_t slots, uint32_t G, const uint4* __restrict__ desc, Layout lay, BpDigits dg, uint32_t pw21,
     uint32_t dlo, uint32_t dhi, uint32_t* __restrict__ H1, unsigned long long* __restrict__ out,
     uint32_t* __restrict__ flags) {
     __shared__ union {
         KeyChunk kc;
         unsigned long long S[kKeyChunk];
     } u;
+    __shared__ uint8_t lut[256];
     __shared__ uint32_t lh[kBpMaxBins];
     __shared__ uint32_t wave_tot[kThr / 64];
     __shared__ uint32_t s_n;
-    constexpr uint32_t kPer = kKeyChunk / kThr, kQ = kBpMaxBins / kThr;
-    const uint64_t c0 = (uint64_t)blockIdx.x * kKeyChunk, c1 = min(c0 + kKeyChunk, slots);
-    for (uint32_t d = threadIdx.x; d < dg.nb1; d += kThr) lh[d] = 0;
-    if (threadIdx.x == 0) s_n = 0;
-    const uint32_t first = chunk_first[blockIdx.x];
-    key_chunk_load<kThr>(u.kc, res, res_off, cls, k, p_hi, c0, c1, first, lay, flags);
-    unsigned long long x[kPer];
-    uint32_t r[kPer], nk = 0;
+    constexpr uint32_t kPer = kKeyChunk / kThr, kPP = (kKeyProtMax + kThr - 1) / kThr;
+    const uint32_t tid = threadIdx.x, nown = dhi - dlo;
+    uint32_t c = blockIdx.x;
+    if (c >= G) return;
+    for (uint32_t i = tid; i < 256; i += kThr) lut[i] = c_lut.v[i];
+    const uint64_t res_end = res_off[n];
+    const bool vec_ok = ((uintptr_t)res & 15u) == 0;
+    // one chunk's loads, held in registers until it is staged
+    uint4 pv = make_uint4(0, 0, 0, 0);
+    uint32_t po[kPP], pe[kPP];  // residue offsets (< 2^32: bp_level1 checks slots)
+    uint16_t pcl[kPP];
+    auto span = [&](const uint4& d, uint64_t& a0, uint32_t& nv, uint32_t& np) {
+        a0 = d.z & ~15u;
+        nv = (uint32_t)((max(d.w, d.z) - a0 + 15) >> 4);
+        np = d.x < n ? min(d.y, n - 1) + 1 - d.x : 0u;
+    };
+    auto issue = [&](const uint4& d) {
+        uint64_t a0;
+        uint32_t nv, np;
+        span(d, a0, nv, np);
+        if (tid < nv) {
+            const uint64_t g = a0 + 16ull * tid;
+            if (vec_ok && g + 16 <= res_end) {
+                pv = *reinterpret_cast<const uint4*>(res + g);
+            } else {
+                uint32_t w[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    w[q] = 0;
+#pragma unroll
+                    for (int bb = 0; bb < 4; ++bb) {
+                        const uint64_t i = g + 4 * q + bb;
+                        w[q] |= (uint32_t)(i < res_end ? res[i] : 0) << (8 * bb);
+                    }
+                }
+                pv = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kPP; ++j) {
+            const uint32_t t = tid + j * kThr;
+            if (t < np) {
+                po[j] = (uint32_t)res_off[d.x + t];
+                pe[j] = (uint32_t)res_off[d.x + t + 1];
+                pcl[j] = cls[d.x + t];
+            }
+        }
+    };
+    uint4 dcur = desc[c];
+    uint4 dnxt = c + gridDim.x < G ? desc[c + gridDim.x] : make_uint4(0, 0, 0, 0);
+    issue(dcur);
     const unsigned hs1 = dg.sh1 - lay.hshift;
-    key_chunk_run<kPer>(u.kc, threadIdx.x * kPer, (uint32_t)(c1 - c0), k, pw21, first, lay,
-                          [&](uint32_t e, bool valid, uint32_t h, unsigned long long lo) {
-                              const uint32_t d = h >> hs1;
-                              const bool mine = valid && d >= dlo && d < dhi;  // the call's coarse bins
-                              x[e] = mine ? ((unsigned long long)h << lay.hshift) | lo : kNoKey;
-                              r[e] = mine ? atomicAdd(&lh[d], 1u) : 0u;
-                              nk += mine;
-                          });
-    if (nk) atomicAdd(&s_n, nk);
-    __syncthreads();  // the chunk's staging (u.kc) is dead from here: u.S reuses it
-    uint32_t cnt[kQ];
+    while (true) {
+        const uint64_t c0 = (uint64_t)c * kKeyChunk, c1 = min(c0 + kKeyChunk, slots);
+        // ---- stage chunk c from the registers ----
+        {
+            uint64_t a0;
+            uint32_t nv, np;
+            span(dcur, a0, nv, np);
+            if (tid < nv) {
+                auto code4 = [&](uint32_t x) {
+                    return (uint32_t)lut[x & 255u] | (uint32_t)lut[(x >> 8) & 255u] << 8 |
+                           (uint32_t)lut[(x >> 16) & 255u] << 16 | (uint32_t)lut[x >> 24] << 24;
+                };
+                *reinterpret_cast<uint4*>(u.kc.rc + 16 * tid) =
+                    make_uint4(code4(pv.x), code4(pv.y), code4(pv.z), code4(pv.w));
+            }
 #pragma unroll
-    for (uint32_t t = 0; t < kQ; ++t) {
-        const uint32_t d = threadIdx.x + t * kThr;
-        cnt[t] = d < dg.nb1 ? lh[d] : 0u;
-    }
-    lds_bins_scan<kThr>(lh, dg.nb1, wave_tot);
-    uint32_t* row = H1 + (uint64_t)blockIdx.x * dg.nb1;
+            for (uint32_t j = 0; j < kPP; ++j) {
+                const uint32_t t = tid + j * kThr;
+                if (t < np) {
+                    const uint32_t p = dcur.x + t;
+                    const uint32_t L = pe[j] - po[j];
+                    u.kc.pb[t] = (uint32_t)(set_base(po[j], p) - c0);  // wraps for the first protein
+                    u.kc.pw[t] = L >= (uint32_t)k ? L - k + 1 : 0u;
+                    u.kc.pc[t] = pcl[j];
+                    u.kc.pr[t] = (int32_t)((int64_t)po[j] - (int64_t)a0);
+                    check_class(pcl[j], lay, flags);
+                }
+            }
+            if (tid == 0) {
+                u.kc.np = np;
+                s_n = 0;
+            }
+            for (uint32_t d = tid; d < nown; d += kThr) lh[dlo + d] = 0;
+        }
+        __syncthreads();
+        // ---- the next chunk's loads go out now; the descriptor after it too ----
+        const uint32_t cn = c + gridDim.x;
+        uint4 dnn = make_uint4(0, 0, 0, 0);
+        if (cn < G) {
+            issue(dnxt);
+            if (cn + gridDim.x < G) dnn = desc[cn + gridDim.x];
+        }
+        // ---- key, rank by digit1, write the segment ----
+        unsigned long long x[kPer];
+        uint32_t r[kPer], nk = 0;
+        key_chunk_run<kPer>(u.kc, tid * kPer, (uint32_t)(c1 - c0), k, pw21, dcur.x, lay,
+                            [&](uint32_t e, bool valid, uint32_t h, unsigned long long lo) {
+                                const uint32_t d = h >> hs1;
+                                const bool mine = valid && d >= dlo && d < dhi;  // the call's coarse bins
+                                x[e] = mine ? ((unsigned long long)h << lay.hshift) | lo : kNoKey;
+                                r[e] = mine ? atomicAdd(&lh[d], 1u) : 0u;
+                                nk += mine;
+                            });
+        if (nk) atomicAdd(&s_n, nk);
+        __syncthreads();  // the chunk's staging (u.kc) is dead from here: u.S reuses it
+        constexpr uint32_t kQ = kBpMaxBins / kThr;
+        uint32_t cnt[kQ];
 #pragma unroll
-    for (uint32_t t = 0; t < kQ; ++t) {
-        const uint32_t d = threadIdx.x + t * kThr;
-        if (d < dg.nb1) row[d] = lh[d] << 16 | cnt[t];
-    }
+        for (uint32_t t = 0; t < kQ; ++t) {
+            const uint32_t d = tid + t * kThr;
+            cnt[t] = d < nown ? lh[dlo + d] : 0u;
+        }
+        lds_bins_scan<kThr>(lh + dlo, nown, wave_tot);
+        uint32_t* row = H1 + (uint64_t)c * nown;
 #pragma unroll
-    for (uint32_t e = 0; e < kPer; ++e)
-        if (x[e] != kNoKey) u.S[lh[(uint32_t)(x[e] >> dg.sh1)] + r[e]] = x[e];
-    __syncthreads();
-    const uint32_t n_in = s_n;
-    unsigned long long* seg = out + c0;  // c0 = chunk * kKeyChunk: 16-byte aligned
-    for (uint32_t i = 2 * threadIdx.x; i < n_in; i += 2 * kThr) {
-        if (i + 1 < n_in)
-            *reinterpret_cast<ulonglong2*>(seg + i) = *reinterpret_cast<const ulonglong2*>(u.S + i);
-        else
-            seg[i] = u.S[i];
+        for (uint32_t t = 0; t < kQ; ++t) {
+            const uint32_t d = tid + t * kThr;
+            if (d < nown) row[d] = lh[dlo + d] << 16 | cnt[t];
+        }
+#pragma unroll
+        for (uint32_t e = 0; e < kPer; ++e)
+            if (x[e] != kNoKey) u.S[lh[(uint32_t)(x[e] >> dg.sh1)] + r[e]] = x[e];
+        __syncthreads();
+        const uint32_t n_in = s_n;
+        unsigned long long* seg = out + c0;  // c0 = chunk * kKeyChunk: 16-byte aligned
+        for (uint32_t i = 2 * tid; i < n_in; i += 2 * kThr) {
+            if (i + 1 < n_in)
+                *reinterpret_cast<ulonglong2*>(seg + i) = *reinterpret_cast<const ulonglong2*>(u.S + i);
+            else
+                seg[i] = u.S[i];
+        }
+        if (cn >= G) break;
+        __syncthreads();  // S read before the next chunk's staging overwrites it
+        c = cn;
+        dcur = dnxt;
+        dnxt = dnn;
     }
 }
 
@@ -2430,6 +2660,8 @@ __global__ __launch_bounds__(256) void bp_h1t_kernel(const uint32_t* __restrict_
 }
 
 // level 2 over the local level 1: tile (j, c) = coarse bin c's runs in chunks [j*T, j*T + T),
+// read from the run table at H1T[(c - dlo) * hsb + chunk * hsc] (the transposed table: hsb = G,
+// hsc = 1; the level-1 table itself for a few own bins: hsb = 1, hsc = own bins),
 // gathered and reserved in the bucket regions as bp_scatter2c.  The run table (off, src) and a
 // key -> run map live in S until the keys are in registers, so the loads go out coalesced
 // (element tid + e*kKeyThreads, as the other scatters).  A tile above kBpTile keys (a skewed
@@ -2440,6 +2672,7 @@ __global__ __launch_bounds__(256) void bp_h1t_kernel(const uint32_t* __restrict_
 template <uint32_t kPer, uint32_t kThr>
 __global__ __launch_bounds__(kThr) void bp_scatter2g_kernel(const unsigned long long* __restrict__ in,
                                                                    const uint32_t* __restrict__ H1T, uint32_t G,
+                                                                   uint32_t hsb, uint32_t hsc,
                                                                    uint32_t T, uint32_t ntiles, uint32_t nbins,
                                                                    BpDigits dg, CurGeom cg,
                                                                    uint32_t* __restrict__ bcur,
@@ -2462,12 +2695,12 @@ __global__ __launch_bounds__(kThr) void bp_scatter2g_kernel(const unsigned long 
     const uint32_t c = c0 + w / ntiles, ch0 = (w % ntiles) * T;
     if (ch0 >= G) return;
     const uint32_t nch = min(T, G - ch0);
-    const uint32_t* row = H1T + (uint64_t)(c - dlo) * G + ch0;
+    const uint32_t* row = H1T + (uint64_t)(c - dlo) * hsb + (uint64_t)ch0 * hsc;
     const uint32_t q = (nch + kThr - 1) / kThr, b0 = threadIdx.x * q;
     uint32_t p[kQ], v = 0;
 #pragma unroll
     for (uint32_t t = 0; t < kQ; ++t) {
-        p[t] = t < q && b0 + t < nch ? row[b0 + t] : 0u;
+        p[t] = t < q && b0 + t < nch ? row[(uint64_t)(b0 + t) * hsc] : 0u;
         v += p[t] & 0xFFFFu;
     }
     uint32_t excl0, tn;
@@ -2523,7 +2756,7 @@ __global__ __launch_bounds__(kThr) void bp_scatter2g_kernel(const unsigned long 
 constexpr uint32_t kBucketCap1024Mean = 800;  // at config 3 (mean 897) the 1,280 variant measured faster
 // buckets [b0, b0 + nb)
 template <bool kRows, bool kScore>
-void launch_buckets(const BucketArgs& a, uint32_t b0, uint32_t nb, hipStream_t st) {
+void launch_buckets(const BucketArgs& a, uint32_t b0, uint32_t nb, uint32_t large_grid, hipStream_t st) {
     if (a.lay.bbits >= kMergeMinBits && a.lay.mean_keys <= kBucketCap1024Mean)  // four keys per thread
         bucket_small_kernel<1024, kBucketSmallThreads, kBucketSmallTab, true, kRows, kScore>
             <<<nb, kBucketSmallThreads, 0, st>>>(a, b0);
@@ -2534,7 +2767,7 @@ void launch_buckets(const BucketArgs& a, uint32_t b0, uint32_t nb, hipStream_t s
         bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallTab, false, kRows, kScore>
             <<<nb, kBucketSmallThreads, 0, st>>>(a, b0);
     bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeTab, kRows, kScore>
-        <<<kBucketLargeGrid, kBucketLargeThreads, 0, st>>>(a);
+        <<<large_grid, kBucketLargeThreads, 0, st>>>(a);
 }
 
 // (pair key, w) runs -> edges with w >= min_shared, canonical order kept
@@ -2607,11 +2840,13 @@ struct kmp_postings {
     bool last_bucketed = false; // layout the last call ran on
     bool last_fused = false;    // ... single-synchronisation step (else the split step)
     bool last_heavy = false;    // ... with spilled frequent k-mers
+    bool last_fast = false;     // ... reduced by the fast row-block tail
     uint32_t last_ovf = 0;      // ... row blocks finished by the overflow sort
     uint64_t shard_cap = 0;     // capacity of each pair-key shard region
     uint64_t shard_floor = 0;   // ... at least (kmp_postings_set_shard_floor: a stream's planned pass size)
     uint64_t stage_floor = 0;   // tail_multi's staging capacity at least (keys; same call)
     Grow<uint32_t> chunk_first;
+    Grow<uint32_t> chunk_desc;  // local level 1: per chunk {first, last, r0, r1}
     Grow<uint32_t> bp;          // bucket partition: H1 | P1 | R | C1 | H2 (see bp_level1)
     Grow<uint32_t> pt;          // row-block tail (pt_bufs)
     Grow<uint32_t> ovf;         // listed row blocks | segment starts | segment ends
@@ -2632,12 +2867,23 @@ struct kmp_postings {
     std::vector<unsigned long long> split_shape;
     bool split_heavy = false;  // k-mer split: this batch spills, its heavy path runs on every call
     unsigned pt_rb_max = 16;    // rows-per-block bound learned from overflowing row blocks
+    unsigned long long* clear_extra = nullptr;  // cleared with the step's flags (the split's send cursors)
+    // the k-mer split's routed bucket output (BucketArgs.send): send buffer, capacity per rank, rows
+    unsigned long long* route_send = nullptr;
+    uint64_t route_cap = 0;
+    SplitRows route_rows{};
+    uint32_t clear_n = 0;
+    uint32_t large_grid = 1024;  // workgroups of the large-bucket kernel (from the last call's list)
+    bool fast_mode = true;      // kmp_postings_set_tail: the fast tail allowed
+    bool fast_tail = true;      // unscored calls take the fast row-block tail (off for a shape whose
+                                // row-block regions overflowed: kRbFast)
     uint32_t bp_J = 0;          // level-2 tiles per coarse bin ...
     uint32_t bp_J_min = 0;      // ... at least (learned from an overflowing bin)
     uint64_t bp_c1 = 0;         // offset of C1 (coarse bin starts) in ws->bp
     bool parted = false;        // ws->keys holds level-1 output (bp_level1 ran for this call)
     bool bp_local = false;      // ... in chunk segments (local level 1: H1T at bp + bp_h1t)
     uint32_t bp_G = 0, bp_T = 0;
+    uint32_t bp_hsb = 0, bp_hsc = 1;  // level 2's run-table strides (bin, chunk)
     uint64_t bp_h1t = 0;
     // coarse bins [bin_lo, bin_hi) of this call (bin_hi 0: all): the bucket-range share of a rank
     // of the multi-GPU k-mer split (kmp_dev_split_expand); level 1 keeps only their keys
@@ -2693,7 +2939,7 @@ struct kmp_postings {
         for (auto* g : {&keys, &sorted, &inc, &inc_sorted, &uniq, &bstats, &btot, &boff, &spill, &hkeys, &hsorted,
                         &hGS, &htc, &htoff, &hoff, &hRH, &hseg, &hcur, &ovk, &ovx, &split_cur})
             g->release();
-        for (auto* g : {&w, &keep, &pos, &small, &cnt, &flags, &chunk_first, &bp, &pt, &ovf, &ovr, &ova, &stg2, &k2, &dsc, &hE, &hgi, &hcnt,
+        for (auto* g : {&w, &keep, &pos, &small, &cnt, &flags, &chunk_first, &chunk_desc, &bp, &pt, &ovf, &ovr, &ova, &stg2, &k2, &dsc, &hE, &hgi, &hcnt,
                         &hrun, &hblk, &cur, &hGH})
             g->release();
         tmp.release();
@@ -2766,24 +3012,43 @@ hipError_t bp_level1(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_r
     const uint32_t nb = 1u << lay.bbits;
     if (ws->bp_local) e = ws->cur.reserve(nb);
     if (e != hipSuccess) return e;
-    if (ws->bp_local)  // the cursor level 2's bucket counts cleared here (bp_level2c does not)
-        chunk_first_clear_kernel<<<(n + 1 + 255) / 256, 256, 0, st>>>(d_res_off, n, slots, G, ws->chunk_first.p,
-                                                                    ws->cur.p, nb);
-    else
-        chunk_first_kernel<<<(n + 1 + 255) / 256, 256, 0, st>>>(d_res_off, 0u, n, 0ull, slots, G, ws->chunk_first.p);
-    if (ws->bp_local) {  // local level 1 for the cursor level 2: H1 | H1T (own digits)
+    if (ws->bp_local) {  // local level 1 for the cursor level 2: H1 (own digits) | H1T
+        e = ws->chunk_desc.reserve(4ull * G);
+        if (e != hipSuccess) return e;
+        // descriptors + the cursor level 2's bucket counts cleared (bp_level2c does not)
+        chunk_desc_kernel<<<(n + 1 + 255) / 256, 256, 0, st>>>(d_res_off, n, slots, G, k,
+                                                               reinterpret_cast<uint4*>(ws->chunk_desc.p), ws->cur.p,
+                                                               nb);
         ws->bp_G = G;
         ws->bp_h1t = h1;
         // T chunks per level-2 tile: ~7/4 of a round at the hash-uniform mean (two rounds; kKeyChunk / nb1 keys
         // per chunk and bin)
         ws->bp_T = std::min<uint32_t>(kBpGatherMax, std::max<uint32_t>(1, kBpGatherTile * 7 / 4 * dg.nb1 / kKeyChunk));
-        bp_scatter1l_kernel<KMP_L1_THREADS><<<G, KMP_L1_THREADS, 0, st>>>(d_res, d_res_off, d_class, k, n, slots, ws->chunk_first.p, lay,
-                                                        dg, pw21, dlo, dhi, H1, ws->keys.p, ws->flags.p);
-        if (dhi > dlo)
-            bp_h1t_kernel<<<dim3((G + 31) / 32, (dhi - dlo + 31) / 32), 256, 0, st>>>(H1, G, dg.nb1, dlo, dhi,
-                                                                                     H1 + h1);
+        const uint32_t nown = dhi - dlo;
+        // a few own bins (a rank's share of the k-mer split): level 2 reads the run table as level 1
+        // wrote it (bp_hsc = own bins); otherwise transposed, so a bin's runs are contiguous
+        const bool direct = nown <= 64 && nown < dg.nb1;
+        ws->bp_hsb = direct ? 1u : G;
+        ws->bp_hsc = direct ? nown : 1u;
+        if (direct) ws->bp_h1t = 0;
+        // persistent: as many workgroups as fit the device at once, each walking its chunks with the
+        // next one's loads in flight
+        static thread_local int per_cu = 0;
+        if (!per_cu && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bp_scatter1p_kernel<KMP_L1_THREADS>,
+                                                                     KMP_L1_THREADS, 0) != hipSuccess ||
+                        per_cu < 1))
+            per_cu = 2;
+        const uint32_t grid = std::min<uint32_t>(G, (uint32_t)per_cu * device_cus());
+        if (nown) {
+            bp_scatter1p_kernel<KMP_L1_THREADS><<<grid, KMP_L1_THREADS, 0, st>>>(
+                d_res, d_res_off, d_class, k, n, slots, G, reinterpret_cast<const uint4*>(ws->chunk_desc.p), lay, dg,
+                pw21, dlo, dhi, H1, ws->keys.p, ws->flags.p);
+            if (!direct)
+                bp_h1t_kernel<<<dim3((G + 31) / 32, (nown + 31) / 32), 256, 0, st>>>(H1, G, nown, 0, nown, H1 + h1);
+        }
         return hipGetLastError();
     }
+    chunk_first_kernel<<<(n + 1 + 255) / 256, 256, 0, st>>>(d_res_off, 0u, n, 0ull, slots, G, ws->chunk_first.p);
     bp_hist1_kernel<<<G, kKeyThreads, 0, st>>>(d_res, d_res_off, d_class, k, n, slots, ws->chunk_first.p, lay, dg,
                                                 pw21, dlo, dhi, H1, ws->flags.p);
     bp_colsum_kernel<<<dim3(groups, (dg.nb1 + 255) / 256), 256, 0, st>>>(H1, G, dg.nb1, R);
@@ -2842,7 +3107,7 @@ int bp_level2c(kmp_postings* ws, const Layout& lay, hipStream_t st) {
         bp_cur_clear_kernel<<<std::min<uint32_t>((nb + 1023) / 1024, 1024), 1024, 0, st>>>(ws->cur.p, nb);
     if (c1 > c0 && ws->bp_local) {
         const uint32_t ntiles = (ws->bp_G + ws->bp_T - 1) / ws->bp_T, per = (ntiles * (c1 - c0) + 7) / 8;
-        bp_scatter2g_kernel<kBpGatherTile / KMP_GATHER_THREADS, KMP_GATHER_THREADS><<<8 * per, KMP_GATHER_THREADS, 0, st>>>(ws->keys.p, ws->bp.p + ws->bp_h1t, ws->bp_G, ws->bp_T,
+        bp_scatter2g_kernel<kBpGatherTile / KMP_GATHER_THREADS, KMP_GATHER_THREADS><<<8 * per, KMP_GATHER_THREADS, 0, st>>>(ws->keys.p, ws->bp.p + ws->bp_h1t, ws->bp_G, ws->bp_hsb, ws->bp_hsc, ws->bp_T,
                                                              ntiles, c1 - c0, dg, ws->cg, ws->cur.p, ws->sorted.p,
                                                              ws->flags.p, c0, c0);
     } else if (c1 > c0)
@@ -3128,6 +3393,88 @@ __global__ __launch_bounds__(kPtThreads) void pt_scatter_kernel(const unsigned l
     __syncthreads();
     const uint32_t placed = s_n;  // m counts the kNoKey padding of a flat array too
     for (uint32_t i = threadIdx.x; i < placed; i += kPtThreads) out[lh[SR[i]] + i] = S[i];
+}
+
+// The fast tail's scatter (pt_reduce_fast): a tile of kThr * 16 keys ranked by row block in LDS;
+// cur[r] counts from zero and block r's keys go to the fixed region [r * kFtCap, (r + 1) * kFtCap)
+// of out, written as u32 (p - r * 2^rbits) << pbits | q (keys past the region are dropped; the
+// reduce sees the count and flags the overflow) — no histogram pass, no scan.  Workgroup (0, 0)
+// also clears the reduce's look-back words lb[0, nrb).  Tiles of 8,192 keys: twice the workgroups
+// of the counting tail's 16,384-key tiles (which ran one per CU), at LDS for two per CU.
+constexpr uint32_t kFtCap = 8192;  // fast tail: keys per row-block region
+constexpr uint32_t kFtScThreads = 512, kFtScTile = kFtScThreads * 16;
+__global__ __launch_bounds__(kFtScThreads) void pt_scatter_capped_kernel(const unsigned long long* __restrict__ in,
+                                                                         const unsigned long long* __restrict__ cursor,
+                                                                         PtGeom g, uint32_t* __restrict__ cur,
+                                                                         uint32_t* __restrict__ out,
+                                                                         unsigned long long* __restrict__ lb) {
+    constexpr uint32_t kThr = kFtScThreads, kPer = 16;
+    __shared__ uint32_t lh[kPtMaxBlocks];
+    __shared__ uint32_t S[kFtScTile];
+    __shared__ uint16_t SR[kFtScTile];
+    __shared__ uint32_t wave_tot[kThr / 64];
+    __shared__ uint32_t s_n;
+    const uint32_t j = blockIdx.x, s = blockIdx.y;
+    if (j == 0 && s == 0)
+        for (uint32_t r = threadIdx.x; r < g.nrb; r += kThr) lb[r] = 0;
+    const uint64_t ns = g.flat_n ? g.flat_n : min<unsigned long long>(cursor[s], g.sc);
+    const uint64_t t0 = (uint64_t)j * kFtScTile;
+    if (t0 >= ns) return;
+    const uint32_t m = (uint32_t)min<uint64_t>(kFtScTile, ns - t0);
+    for (uint32_t r = threadIdx.x; r < g.nrb; r += kThr) lh[r] = 0;
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
+    const unsigned long long* src = in + s * g.sc + t0;
+    const unsigned sh = g.pbits + g.rbits;
+    const unsigned long long lowm = (1ull << sh) - 1;
+    const unsigned long long base = (unsigned long long)g.row0 << g.pbits;
+    unsigned long long x[kPer];
+    uint32_t rk[kPer];
+#pragma unroll
+    for (uint32_t e = 0; e < kPer; ++e) {
+        const uint32_t i = threadIdx.x + e * kThr;
+        x[e] = i < m ? src[i] : kNoKey;
+        if (x[e] != kNoKey) x[e] -= base;  // rows from row0
+    }
+    uint32_t nk = 0;
+#pragma unroll
+    for (uint32_t e = 0; e < kPer; ++e) {
+        rk[e] = x[e] != kNoKey ? atomicAdd(&lh[(uint32_t)(x[e] >> sh)], 1u) : 0u;
+        nk += x[e] != kNoKey;
+    }
+    if (nk) atomicAdd(&s_n, nk);
+    __syncthreads();
+    constexpr uint32_t kQ = kPtMaxBlocks / kThr;
+    uint32_t cnt[kQ];
+#pragma unroll
+    for (uint32_t t = 0; t < kQ; ++t) {
+        const uint32_t r = threadIdx.x + t * kThr;
+        cnt[t] = r < g.nrb ? lh[r] : 0u;
+    }
+    lds_bins_scan<kThr>(lh, g.nrb, wave_tot);
+    uint32_t rbase[kQ];
+#pragma unroll
+    for (uint32_t t = 0; t < kQ; ++t)  // reserved while the tile is placed
+        rbase[t] = cnt[t] ? atomicAdd(&cur[threadIdx.x + t * kThr], cnt[t]) : 0u;
+#pragma unroll
+    for (uint32_t e = 0; e < kPer; ++e)
+        if (x[e] != kNoKey) {
+            const uint32_t r = (uint32_t)(x[e] >> sh), pos = lh[r] + rk[e];
+            S[pos] = (uint32_t)(x[e] & lowm);
+            SR[pos] = (uint16_t)r;
+        }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t t = 0; t < kQ; ++t) {
+        const uint32_t r = threadIdx.x + t * kThr;
+        if (r < g.nrb) lh[r] = rbase[t] - lh[r];  // in-region offset of the tile's run, minus its staging start
+    }
+    __syncthreads();
+    const uint32_t placed = s_n;
+    for (uint32_t i = threadIdx.x; i < placed; i += kThr) {
+        const uint32_t r = SR[i], pos = lh[r] + i;
+        if (pos < kFtCap) out[(uint64_t)r * kFtCap + pos] = S[i];
+    }
 }
 
 template <uint32_t kE>
@@ -3822,7 +4169,8 @@ __global__ __launch_bounds__(kPtScanThreads) void pt_offsets_kernel(const uint32
 }
 
 __device__ void step_pack_body(const unsigned long long* __restrict__ gstats, const uint32_t* __restrict__ flags,
-                               const uint32_t* __restrict__ runs, unsigned long long* __restrict__ rb);
+                               const uint32_t* __restrict__ runs, unsigned long long* __restrict__ rb,
+                               unsigned long long fast_ovf = 0);
 
 // pack: nonzero -> workgroup 0 also writes the step's read-back (step_pack_kernel's work: every
 // input of it is final once pt_offsets has run)
@@ -3902,13 +4250,16 @@ __global__ __launch_bounds__(256) void pt_emit_kernel(const uint32_t* __restrict
 // read-back: gstats (8 per shard) | pair cursors | spill cursors | the words below
 enum : uint32_t {
     kRbCursor = kShards * 8, kRbSpill = kShards * 9, kRbFlagBin = kShards * 10, kRbFlagClass, kRbRuns, kRbOvf,
-    kRbMaxBlock, kRbBinTiles, kRbFlagCur, kRbSegs, kRbSegMax, kRbWords
+    kRbMaxBlock, kRbBinTiles, kRbFlagCur, kRbSegs, kRbSegMax, kRbFast, kRbList, kRbWords
 };
 constexpr uint32_t kGsWords = kShards * 10;  // gstats | cursors | spill cursors (u64)
 
-__global__ void step_clear_kernel(uint32_t* __restrict__ flags, unsigned long long* __restrict__ gstats) {
+// clears a step's flags and statistics (and extra[0, n_extra): the k-mer split's send cursors)
+__global__ void step_clear_kernel(uint32_t* __restrict__ flags, unsigned long long* __restrict__ gstats,
+                                  unsigned long long* __restrict__ extra = nullptr, uint32_t n_extra = 0) {
     for (uint32_t i = threadIdx.x; i < kGsWords; i += blockDim.x) gstats[i] = 0;
     if (threadIdx.x < kFlN) flags[threadIdx.x] = 0;
+    for (uint32_t i = threadIdx.x; i < n_extra; i += blockDim.x) extra[i] = 0;
 }
 
 __global__ void step_pack_kernel(const unsigned long long* __restrict__ gstats, const uint32_t* __restrict__ flags,
@@ -3917,9 +4268,12 @@ __global__ void step_pack_kernel(const unsigned long long* __restrict__ gstats, 
 }
 
 __device__ void step_pack_body(const unsigned long long* __restrict__ gstats, const uint32_t* __restrict__ flags,
-                               const uint32_t* __restrict__ runs, unsigned long long* __restrict__ rb) {
+                               const uint32_t* __restrict__ runs, unsigned long long* __restrict__ rb,
+                               unsigned long long fast_ovf) {
     for (uint32_t i = threadIdx.x; i < kGsWords; i += blockDim.x) rb[i] = gstats[i];
     if (threadIdx.x == 0) {
+        rb[kRbFast] = fast_ovf;
+        rb[kRbList] = flags[kFlList];
         rb[kRbFlagBin] = flags[kFlBin];
         rb[kRbFlagClass] = flags[kFlClass];
         rb[kRbRuns] = runs ? runs[0] : 0;
@@ -3931,6 +4285,279 @@ __device__ void step_pack_body(const unsigned long long* __restrict__ gstats, co
         rb[kRbSegMax] = flags[kFlSegMax];
     }
     __threadfence_system();  // rb is host memory, read after the stream synchronises
+}
+
+// ------------------------------------------------------------- fast row-block tail --------
+// The default tail of an unscored single-k call (combine_edges, mod.rs:322-546; KmerEdgeGroup::new,
+// edge.rs:56-85): no histogram pass, no scan, no staging, no emit kernel.
+//   pt_scatter<true>  row block r's keys (u32 p_local << pbits | q) into the fixed region
+//                     [r * kFtCap, (r + 1) * kFtCap), reserved on fcur[r] (from zero);
+//   pt_reduce_fast    one workgroup per row block: its keys aggregated in an LDS hash table on the
+//                     pair (count = w, i.e. one KmerEdge::Group per pair with len(kmers) = w), the
+//                     distinct pairs grouped by row (a counting sort on the row), each ranked within
+//                     its row by q (its rank = the row's pairs with a smaller q), and written in
+//                     canonical order straight to (d_p, d_q, d_w) at the block's edge offset, which a
+//                     decoupled look-back over the blocks before it supplies (wave 0, while nothing
+//                     else of the block waits on it until the copy-out).  It re-zeroes fcur[r] for the
+//                     next call.  A block above kFtHashMax keys, one with a row of more than
+//                     kFtRankMax pairs, or one whose pair count would pass 16 bits sorts its keys
+//                     instead (block radix sort + run-length encoding).  A block above kFtCap keys
+//                     (its region overflowed) raises the read-back's kRbFast word: the caller reruns
+//                     the call on the counting tail and keeps it for the shape.
+// The last block writes the edge count and the step's read-back.
+constexpr uint32_t kFtThreads = 512, kFtHashMax = 6144, kFtSlots = 8192, kFtRowsMax = 1024, kFtRankMax = 256;
+constexpr uint32_t kFtEmpty = 0xFFFFFFFFu;
+constexpr unsigned long long kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbOvf = 1ull << 61;
+static_assert(kFtCap == 16 * kFtThreads && kFtHashMax <= 12 * kFtThreads && kFtSlots == 16 * kFtThreads,
+              "per-thread register arrays of pt_reduce_fast");
+
+// look-back words: one 8-B word per block, written and polled with agent-scope relaxed atomics
+// (sc1): the word itself is the only datum handed over
+__device__ __forceinline__ unsigned long long lb_load(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_store(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// wave 0 of block r: publishes the block's aggregate (count | overflow bit), sums the aggregates of
+// the blocks before it (64 per round, one per lane) back to the nearest inclusive prefix, publishes
+// its own inclusive prefix; returns the exclusive one (count | overflow bit of any earlier block).
+// Blocks are dispatched in index order, so every predecessor is resident or done: the polls end.
+__device__ unsigned long long ft_lookback(unsigned long long* lb, uint32_t r, unsigned long long agg) {
+    const uint32_t lane = threadIdx.x & 63;
+    if (r == 0) {
+        if (lane == 0) lb_store(lb, kLbInc | agg);
+        return 0;
+    }
+    if (lane == 0) lb_store(lb + r, kLbAgg | agg);
+    uint32_t cnt = 0;
+    bool ovf = false;
+    int64_t top = (int64_t)r - 1;
+    while (true) {
+        const int64_t j = top - (int64_t)lane;
+        const unsigned long long v = j >= 0 ? lb_load(lb + j) : kLbInc;
+        const uint32_t st = (uint32_t)(v >> 62);
+        const unsigned long long inc = __ballot(st == 2), none = __ballot(st == 0);
+        const uint32_t first = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;
+        const unsigned long long upto = first >= 63 ? ~0ull : (2ull << first) - 1;
+        if (none & upto) {  // a predecessor has not published yet
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        const bool in = lane <= first;
+        cnt += wave_sum(in ? (uint32_t)v : 0u);
+        ovf |= __ballot(in && (v & kLbOvf)) != 0;
+        if (first < 64) break;
+        top -= 64;
+    }
+    const unsigned long long excl = (unsigned long long)cnt | (ovf ? kLbOvf : 0ull);
+    if (lane == 0) lb_store(lb + r, kLbInc | ((unsigned long long)(cnt + (uint32_t)agg) | ((agg | excl) & kLbOvf)));
+    return excl;
+}
+
+struct FtLds {
+    union {
+        struct {
+            uint32_t K[kFtSlots];  // hash slots (pair key), then the block's pairs in row / canonical order
+            uint16_t C[kFtSlots];  // counts (w), two per 32-bit word for the LDS atomics
+        } h;
+        typename PtSort<16>::storage_type s16;
+    };
+    uint32_t RC[kFtRowsMax + 1];  // pairs per row -> row starts
+    uint32_t last[kFtThreads];
+    uint32_t wave_tot[kFtThreads / 64];
+    uint32_t s_max, s_flag;
+    unsigned long long s_excl;
+};
+
+__global__ __launch_bounds__(kFtThreads) void pt_reduce_fast_kernel(const uint32_t* __restrict__ keys,
+                                                                    uint32_t* __restrict__ fcur, PtGeom g,
+                                                                    unsigned long long* __restrict__ lb,
+                                                                    uint32_t* __restrict__ d_p,
+                                                                    uint32_t* __restrict__ d_q,
+                                                                    uint32_t* __restrict__ d_w, uint64_t cap,
+                                                                    uint32_t stride, PtPack pack,
+                                                                    uint32_t* __restrict__ runs) {
+    __shared__ FtLds u;
+    const uint32_t r = blockIdx.x, tid = threadIdx.x;
+    const uint32_t nraw = fcur[r];
+    __syncthreads();  // every thread has its count before the cursor is cleared for the next call
+    if (tid == 0) fcur[r] = 0;
+    const bool ovf = nraw > kFtCap;
+    const uint32_t n = ovf ? 0u : nraw;
+    const uint32_t* src = keys + (uint64_t)r * kFtCap;
+    const unsigned pb = g.pbits;
+    const uint32_t R = 1u << g.rbits;
+    uint32_t D = 0;  // the block's kept pairs
+    bool sort = n > kFtHashMax;
+    if (!sort) {
+        // ---- hash aggregation: pair -> slot, count per slot ----
+        for (uint32_t i = tid; i < kFtSlots; i += kFtThreads) u.h.K[i] = kFtEmpty;
+        for (uint32_t i = tid; i < kFtSlots / 2; i += kFtThreads) reinterpret_cast<uint32_t*>(u.h.C)[i] = 0;
+        for (uint32_t i = tid; i <= R; i += kFtThreads) u.RC[i] = 0;
+        if (tid == 0) u.s_max = u.s_flag = 0;
+        uint32_t x[12];
+#pragma unroll
+        for (uint32_t e = 0; e < 12; ++e) {
+            const uint32_t i = tid + e * kFtThreads;
+            x[e] = i < n ? src[i] : kFtEmpty;
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t e = 0; e < 12; ++e) {
+            if (x[e] == kFtEmpty) continue;
+            uint32_t sl = (x[e] * 0x9E3779B1u) >> 19;  // 13 bits: kFtSlots
+            while (true) {
+                const uint32_t old = atomicCAS(&u.h.K[sl], kFtEmpty, x[e]);
+                if (old == kFtEmpty || old == x[e]) break;
+                sl = (sl + 1) & (kFtSlots - 1);
+            }
+            const uint32_t sh = 16 * (sl & 1);
+            const uint32_t old = atomicAdd(reinterpret_cast<uint32_t*>(u.h.C) + (sl >> 1), 1u << sh);
+            if (((old >> sh) & 0xFFFFu) >= 0xFFFEu) u.s_flag = 1;  // w would reach 16 bits: sort instead
+        }
+        __syncthreads();
+        // ---- kept pairs (w >= min_shared) counted per row, ranked in arrival order ----
+        uint32_t ek[16], er[16];  // pair key | rank in its row << 16 | w
+#pragma unroll
+        for (uint32_t j = 0; j < 16; ++j) {
+            const uint32_t sl = tid + j * kFtThreads;
+            const uint32_t k = u.h.K[sl], w = u.h.C[sl];
+            ek[j] = kFtEmpty;
+            if (k != kFtEmpty && w >= g.min_shared) {
+                ek[j] = k;
+                er[j] = atomicAdd(&u.RC[k >> pb], 1u) << 16 | w;
+            }
+        }
+        __syncthreads();
+        // row starts (R <= kFtRowsMax = 2 * kFtThreads rows) and the largest row
+        const uint32_t a0 = 2 * tid < R ? u.RC[2 * tid] : 0u, a1 = 2 * tid + 1 < R ? u.RC[2 * tid + 1] : 0u;
+        const uint32_t mx = wave_max(max(a0, a1));
+        if ((tid & 63) == 0) atomicMax(&u.s_max, mx);
+        uint32_t excl, total;
+        block_scan_n<kFtThreads>(a0 + a1, excl, total, u.wave_tot);
+        if (2 * tid < R) u.RC[2 * tid] = excl;
+        if (2 * tid + 1 < R) u.RC[2 * tid + 1] = excl + a0;
+        if (tid == 0) u.RC[R] = total;
+        __syncthreads();
+        D = total;
+        sort = u.s_flag || u.s_max > kFtRankMax;  // uniform
+        if (!sort) {
+            // grouped by row (the slots were read above the barriers)
+#pragma unroll
+            for (uint32_t j = 0; j < 16; ++j)
+                if (ek[j] != kFtEmpty) {
+                    const uint32_t pos = u.RC[ek[j] >> pb] + (er[j] >> 16);
+                    u.h.K[pos] = ek[j];
+                    u.h.C[pos] = (uint16_t)er[j];
+                }
+            __syncthreads();
+            // rank within the row by q: canonical position
+            uint32_t fk[12], fp[12];  // key | position << 16 | w
+#pragma unroll
+            for (uint32_t e = 0; e < 12; ++e) {
+                const uint32_t i = tid + e * kFtThreads;
+                fk[e] = kFtEmpty;
+                if (i < D) {
+                    const uint32_t key = u.h.K[i], row = key >> pb, a = u.RC[row], b = u.RC[row + 1];
+                    uint32_t rk = 0;
+                    for (uint32_t t = a; t < b; ++t) rk += u.h.K[t] < key;
+                    fk[e] = key;
+                    fp[e] = (a + rk) << 16 | u.h.C[i];
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (uint32_t e = 0; e < 12; ++e)
+                if (fk[e] != kFtEmpty) {
+                    u.h.K[fp[e] >> 16] = fk[e];
+                    u.h.C[fp[e] >> 16] = (uint16_t)fp[e];
+                }
+        }
+        __syncthreads();
+    }
+    if (sort) {
+        // ---- a block too large or too skewed for the hash: block radix sort + run-length encode ----
+        uint32_t k[16];
+#pragma unroll
+        for (uint32_t e = 0; e < 16; ++e) {
+            const uint32_t i = tid + e * kFtThreads;
+            k[e] = i < n ? src[i] : kFtEmpty;
+        }
+        PtSort<16>().sort(k, u.s16, 0, pb + g.rbits + 1);  // blocked: thread t holds ranks t * 16 + e
+        u.last[tid] = k[15];
+        __syncthreads();
+        uint32_t prev = tid ? u.last[tid - 1] : 0u, nh = 0;
+        bool head[16];
+#pragma unroll
+        for (uint32_t e = 0; e < 16; ++e) {
+            const uint32_t rank = tid * 16 + e;
+            head[e] = rank < n && (rank == 0 || k[e] != prev);
+            prev = k[e];
+            nh += head[e];
+        }
+        uint32_t base, nruns;
+        block_scan_n<kFtThreads>(nh, base, nruns, u.wave_tot);  // barriers: the sort storage is dead
+        // run keys in K, head ranks in C (ranks < kFtCap fit 16 bits; C[nruns] = n needs n < 2^16)
+#pragma unroll
+        for (uint32_t e = 0; e < 16; ++e)
+            if (head[e]) {
+                u.h.K[base] = k[e];
+                u.h.C[base] = (uint16_t)(tid * 16 + e);
+                ++base;
+            }
+        if (tid == 0) u.h.C[nruns] = (uint16_t)n;
+        __syncthreads();
+        // runs with w >= min_shared, compacted in order (thread t: runs [t q, t q + q))
+        const uint32_t q = (nruns + kFtThreads - 1) / kFtThreads;
+        uint32_t kv[16], wv[16], kept = 0;
+#pragma unroll
+        for (uint32_t e = 0; e < 16; ++e) {
+            const uint32_t jr = tid * q + e;
+            wv[e] = 0;
+            if (e < q && jr < nruns) {
+                kv[e] = u.h.K[jr];
+                wv[e] = (uint32_t)u.h.C[jr + 1] - u.h.C[jr];
+                kept += wv[e] >= g.min_shared;
+            }
+        }
+        uint32_t o;
+        block_scan_n<kFtThreads>(kept, o, D, u.wave_tot);
+#pragma unroll
+        for (uint32_t e = 0; e < 16; ++e)
+            if (wv[e] && wv[e] >= g.min_shared) {
+                u.h.K[o] = kv[e];
+                u.h.C[o] = (uint16_t)wv[e];
+                ++o;
+            }
+        __syncthreads();
+    }
+    // ---- the block's edge offset, then the pairs straight to the edge arrays ----
+    if (tid < 64) {
+        const unsigned long long ex = ft_lookback(lb, r, (unsigned long long)D | (ovf ? kLbOvf : 0ull));
+        if (tid == 0) u.s_excl = ex;
+    }
+    __syncthreads();
+    const unsigned long long ex = u.s_excl;
+    const uint64_t o = (uint32_t)ex;
+    const uint32_t rowbase = g.row0 + (r << g.rbits), qm = (1u << pb) - 1;
+    for (uint32_t i = tid; i < D; i += kFtThreads) {
+        if (o + i >= cap) break;
+        const uint32_t key = u.h.K[i];
+        d_p[(o + i) * stride] = rowbase + (key >> pb);
+        d_q[(o + i) * stride] = key & qm;
+        d_w[(o + i) * stride] = u.h.C[i];
+    }
+    if (r + 1 == gridDim.x) {  // the last block: the edge count and the read-back
+        const bool any_ovf = ovf || (ex & kLbOvf);
+        if (tid == 0) {
+            runs[0] = (uint32_t)(o + D);
+            runs[1] = 0;
+        }
+        __syncthreads();
+        if (pack.rb) step_pack_body(pack.gstats, pack.flags, runs, pack.rb, any_ovf ? 1ull : 0ull);
+    }
 }
 
 // one call's parameters
@@ -3959,6 +4586,9 @@ struct StepCfg {
 
 // row-block tail geometry: rows per block so that an average block holds about a quarter of
 // kPtCap keys (from the expected incidence count)
+#ifndef KMP_FT_TARGET
+#define KMP_FT_TARGET 2275
+#endif
 bool pt_geometry(const kmp_postings* ws, const StepCfg& c, uint64_t inc, PtGeom* g) {
     g->pbits = bits_for(c.n);
     g->sbits = c.sb;
@@ -3969,7 +4599,10 @@ bool pt_geometry(const kmp_postings* ws, const StepCfg& c, uint64_t inc, PtGeom*
     // of 2.4-4.8K keys; the first rows (p is the smaller index) hold about twice the average.  A
     // small call (a rank's rows of the k-mer split) takes smaller blocks, down to ~1K keys, so
     // that ~1,000 workgroups still fill the GPU
-    const double per_block = std::min((double)kPtCap / 2.4, std::max(1024.0, (double)est / 1024));
+    // the fast tail (unscored) keeps its blocks well inside its fixed regions and hash table: an
+    // average of ~1.1-2.3K keys (KMP_FT_TARGET), twice that in the first rows
+    const double target = (!c.sb && ws->fast_tail) ? (double)KMP_FT_TARGET : (double)kPtCap / 2.4;
+    const double per_block = std::min(target, std::max(1024.0, (double)est / 1024));
     const double want = per_block * std::max<uint32_t>(rows, 1) / est;
     unsigned rb = 0;
     while (rb < 16 && (double)(1u << rb) * 1.41421356 < want) ++rb;
@@ -3994,30 +4627,40 @@ bool pt_geometry(const kmp_postings* ws, const StepCfg& c, uint64_t inc, PtGeom*
     return true;
 }
 
-// ws->pt: H | P | R | block starts (nrb + 1) | run counts (nrb) | edge offsets (nrb + 1)
+// ws->pt: T (totals) | fcur (fast-tail cursors) | cur | lb (fast-tail look-back, u64) | block starts
+// (nrb + 1) | run counts (nrb) | edge offsets (nrb + 1)
 struct PtBufs {
-    uint32_t *T, *cur, *bst, *counts, *eoff;  // row-block totals | scatter cursors | starts | runs | edge offsets
+    uint32_t *T, *fcur, *cur, *bst, *counts, *eoff;  // row-block totals | fast cursors | scatter cursors | starts | runs | edge offsets
+    unsigned long long* lb;
 };
 PtBufs pt_bufs(kmp_postings* ws, const PtGeom& g, bool reserve, hipError_t* e, hipStream_t st = nullptr) {
     PtBufs b{};
     if (reserve) {
-        *e = ws->pt.reserve(2 * (uint64_t)kPtMaxBlocks + 3 * (uint64_t)g.nrb + 2);
-        // T (row-block totals) must be zero: pt_tscan re-zeroes what it used, a new allocation
-        // (a new pointer or capacity: reserve only reallocates to grow) is cleared once, on the
-        // step's stream (a null-stream memset does not order with the non-blocking streams: the
-        // first pt_hist of a grown buffer could run before it)
+        *e = ws->pt.reserve(5 * (uint64_t)kPtMaxBlocks + 3 * (uint64_t)g.nrb + 2);
+        // T (row-block totals) and fcur must be zero: pt_tscan / pt_reduce_fast re-zero what they
+        // used, a new allocation (a new pointer or capacity: reserve only reallocates to grow) is
+        // cleared once, on the step's stream (a null-stream memset does not order with the
+        // non-blocking streams: the first pt_hist of a grown buffer could run before it)
         if (*e == hipSuccess && (ws->pt_zero_p != ws->pt.p || ws->pt_zero_n != ws->pt.n)) {
-            *e = hipMemsetAsync(ws->pt.p, 0, kPtMaxBlocks * sizeof(uint32_t), st);
+            *e = hipMemsetAsync(ws->pt.p, 0, 2 * kPtMaxBlocks * sizeof(uint32_t), st);
             ws->pt_zero_p = ws->pt.p;
             ws->pt_zero_n = ws->pt.n;
         }
     }
     b.T = ws->pt.p;
-    b.cur = b.T + kPtMaxBlocks;
-    b.bst = b.cur + kPtMaxBlocks;
+    b.fcur = b.T + kPtMaxBlocks;
+    b.cur = b.fcur + kPtMaxBlocks;
+    b.lb = reinterpret_cast<unsigned long long*>(b.cur + kPtMaxBlocks);
+    b.bst = b.cur + 3 * kPtMaxBlocks;
     b.counts = b.bst + g.nrb + 1;
     b.eoff = b.counts + g.nrb;
     return b;
+}
+
+// the fast row-block tail applies: unscored keys, at most kFtRowsMax rows per block, not turned off
+// for the shape
+bool pt_fast(const kmp_postings* ws, const PtGeom& g) {
+    return ws->fast_tail && !g.sbits && g.rbits <= 10 && (1u << g.rbits) <= kFtRowsMax;
 }
 
 // spill segments: every one holds more than kHeavySub keys (a heavy group, or a whole bucket)
@@ -4055,6 +4698,13 @@ BucketArgs bucket_args(kmp_postings* ws, const StepCfg& c, bool spill) {
     a.k = c.k;
     a.sb = c.sb;
     a.sor = c.sor;
+    if (ws->route_send && !c.sb) {
+        a.send = ws->route_send;
+        a.send_cap = ws->route_cap;
+        a.send_sub = ws->route_cap / kShards;
+        a.dcur = ws->split_cur.p;
+        a.rows = ws->route_rows;
+    }
     return a;
 }
 
@@ -4070,7 +4720,8 @@ int step_reserve(kmp_postings* ws, const StepCfg& c, const PtGeom& g, hipStream_
     PG(ws->small.reserve(16));  // [1] run count, [2] largest row block
     PG(ws->inc_sorted.reserve(total));
     if (!c.expand_only) {  // an expand-only call leaves the tail (and its staging) to tail_multi
-        PG(ws->inc.reserve(total));  // u32 row-block keys (pt_scatter) ...
+        // u32 row-block keys (pt_scatter; the fast tail's fixed regions) ...
+        PG(ws->inc.reserve(pt_fast(ws, g) ? std::max<uint64_t>(total, (uint64_t)g.nrb * kFtCap / 2) : total));
         PG(ws->uniq.reserve(total));  // ... staged p | q (u32 each)
         PG(ws->w.reserve(total));     // ... staged w
         if (c.sb) PG(ws->stg2.reserve(2 * total));  // ... staged scores | second-k weights
@@ -4089,7 +4740,7 @@ int step_reserve(kmp_postings* ws, const StepCfg& c, const PtGeom& g, hipStream_
 template <class MakeKeys>
 int enqueue_front(kmp_postings* ws, MakeKeys& make_keys, const StepCfg& c, bool spill, hipStream_t st,
                   bool keys = true) {
-    step_clear_kernel<<<1, 256, 0, st>>>(ws->flags.p, ws->bstats.p);
+    step_clear_kernel<<<1, 256, 0, st>>>(ws->flags.p, ws->bstats.p, ws->clear_extra, ws->clear_n);
     ws->mark(0, st);
     if (keys) {  // else: the keys grouped by bucket of the last call (front reuse)
         PG(make_keys(c.lay, st));
@@ -4105,12 +4756,16 @@ int enqueue_front(kmp_postings* ws, MakeKeys& make_keys, const StepCfg& c, bool 
     uint32_t c0, c1;
     own_bins(ws, dg, &c0, &c1);
     const uint32_t b0 = c0 * dg.nb2, nbk = (c1 - c0) * dg.nb2;  // the call's buckets
+    // the large-bucket kernel loops over its list: a grid sized from the last call's list (a
+    // thousand idle 1,024-thread workgroups cost ~5 us); a bucket-range share of the k-mer split
+    // lists about 1/parts of them
+    const uint32_t lg = ws->bin_hi ? std::max<uint32_t>(64, kBucketLargeGrid * (c1 - c0) / dg.nb1) : ws->large_grid;
     if (c.sb) {
-        if (c.ranged) launch_buckets<true, true>(a, b0, nbk, st);
-        else launch_buckets<false, true>(a, b0, nbk, st);
+        if (c.ranged) launch_buckets<true, true>(a, b0, nbk, lg, st);
+        else launch_buckets<false, true>(a, b0, nbk, lg, st);
     } else {
-        if (c.ranged) launch_buckets<true, false>(a, b0, nbk, st);
-        else launch_buckets<false, false>(a, b0, nbk, st);
+        if (c.ranged) launch_buckets<true, false>(a, b0, nbk, lg, st);
+        else launch_buckets<false, false>(a, b0, nbk, lg, st);
     }
     PG(hipGetLastError());
     return KMP_OK;
@@ -4130,6 +4785,19 @@ int enqueue_tail_in(kmp_postings* ws, const StepCfg& c, const PtGeom& g, const u
     hipError_t e = hipSuccess;
     const PtBufs b = pt_bufs(ws, g, false, &e);
     uint32_t* keys32 = reinterpret_cast<uint32_t*>(ws->inc.p);
+    if (pt_fast(ws, g)) {  // capped scatter, then one reduce that writes the edges (marks 4, 5, 6)
+        const uint32_t jt = (uint32_t)(((g.flat_n ? g.flat_n : g.sc) + kFtScTile - 1) / kFtScTile);
+        pt_scatter_capped_kernel<<<dim3(jt, g.nshards), kFtScThreads, 0, st>>>(in, cursor, g, b.fcur, keys32, b.lb);
+        ws->mark(4, st);
+        pt_reduce_fast_kernel<<<g.nrb, kFtThreads, 0, st>>>(keys32, b.fcur, g, b.lb, c.d_p, c.d_q, c.d_w, c.cap,
+                                                             c.stride,
+                                                             PtPack{ws->bstats.p, ws->flags.p, nullptr, ws->hrb},
+                                                             ws->small.p + 1);
+        ws->mark(5, st);
+        ws->mark(6, st);
+        PG(hipGetLastError());
+        return KMP_OK;
+    }
     uint32_t* stage_p = reinterpret_cast<uint32_t*>(ws->uniq.p);
     uint32_t* stage_q = stage_p + total;
     pt_hist_kernel<<<dim3(g.jt, g.nshards), kPtThreads, 0, st>>>(in, cursor, g, b.T);
@@ -4565,6 +5233,8 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
         ws->shape = shape;
         ws->pt_inc = 0;
         ws->pt_rb_max = 16;
+        ws->fast_tail = ws->fast_mode;
+        ws->large_grid = kBucketLargeGrid;
         ws->bp_J_min = 0;
         ws->heavy = false;
         ws->cur_on = ws->cur_mode;
@@ -4593,8 +5263,10 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
             key.push_back(g.rbits + 1);
             key.push_back(g_grow_gen.load());
             key.push_back(ws->cur_on);
+            key.push_back(ws->fast_tail);
+            key.push_back(ws->large_grid);
             int rc = fused_launch(ws, make_keys, key, c, g, st);
-            key.resize(key.size() - 6);
+            key.resize(key.size() - 8);
             if (rc != KMP_OK) return rc;
             PG(hipStreamSynchronize(st));
         } else {
@@ -4679,7 +5351,18 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
             if (rc != KMP_OK) return rc;
             PG(hipStreamSynchronize(st));
         }
+        if (rb[kRbFast]) {  // a fast-tail row-block region overflowed: the counting tail for this shape
+            if (debug) fprintf(stderr, "kmp: fast tail region overflow (rows per block %u): counting tail\n", 1u << g.rbits);
+            ws->fast_tail = false;
+            continue;
+        }
         ws->pt_inc = n_inc;  // sizes the next call's row blocks
+        ws->last_fast = pt_fast(ws, g);
+        {  // the large-bucket grid of the next call: twice the listed buckets, 64 .. kBucketLargeGrid
+            uint32_t lg = 64;
+            while (lg < kBucketLargeGrid && lg < 2 * rb[kRbList]) lg *= 2;
+            ws->large_grid = lg;
+        }
         uint64_t ne = rb[kRbRuns];
         ws->last_ovf = (uint32_t)rb[kRbOvf];
         if (rb[kRbOvf] && !pt_rowhist_ok(g)) {
@@ -5020,11 +5703,6 @@ int run_postings(kmp_postings* ws, MakeKeys make_keys, const std::vector<unsigne
 // keys to the rank owning the row of their smaller protein, and that rank reduces them with the
 // row-block tail.  A pair's incidences from every k-mer meet on its row owner, so w is complete
 // there, and the ranks' row ranges are ordered: the rank-order concatenation is canonical.
-constexpr uint32_t kSplitMax = 64;  // ranks
-struct SplitRows {
-    uint32_t start[kSplitMax + 1];  // row range of rank d: [start[d], start[d+1])
-    uint32_t parts;
-};
 constexpr uint32_t kRtThreads = 256, kRtPer = 16, kRtTile = kRtThreads * kRtPer;
 
 // pair keys (p << pbits | q) of the shard regions -> region d (cap keys) of send, d = the rank
@@ -5073,25 +5751,23 @@ __global__ __launch_bounds__(kRtThreads) void split_route_kernel(const unsigned 
     }
 }
 
-// the unused tail of every send region -> kNoKey (the receiver's tail skips it)
-__global__ void split_pad_kernel(unsigned long long* __restrict__ send, uint64_t cap,
-                                 const unsigned long long* __restrict__ dcursor) {
+// the unused tail of every send region -> kNoKey (the receiver's tail skips it); workgroup (0, 0)
+// also writes the rank's flags (KMP_SPLIT_*) and statistics (kSt* order, summed over the shards)
+// routed (the bucket kernels wrote the send regions themselves, kShards sub-regions of cap / kShards
+// keys per destination, the buffer pre-filled with kNoKey): no padding; the part size reported is
+// kShards x the fullest sub-region, so a grown cap gives every sub-region its need
+__global__ void split_pad_finish_kernel(unsigned long long* __restrict__ send, uint64_t cap,
+                                        const unsigned long long* __restrict__ dcursor,
+                                        const unsigned long long* __restrict__ gstats,
+                                        const uint32_t* __restrict__ wflags, uint64_t sc, uint32_t parts,
+                                        uint32_t* __restrict__ out, unsigned long long* __restrict__ stats,
+                                        int heavy_done, int routed) {
     const uint32_t d = blockIdx.y;
-    for (uint64_t i = dcursor[d] + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap;
-         i += (uint64_t)gridDim.x * blockDim.x)
-        send[d * cap + i] = kNoKey;
-}
-
-__global__ void split_clear_kernel(unsigned long long* __restrict__ dcursor, uint32_t parts) {
-    if (threadIdx.x < parts) dcursor[threadIdx.x] = 0;
-}
-
-// the rank's flags (KMP_SPLIT_*) and statistics (kSt* order, summed over the shards)
-__global__ void split_finish_kernel(const unsigned long long* __restrict__ gstats,
-                                    const uint32_t* __restrict__ wflags, uint64_t sc,
-                                    const unsigned long long* __restrict__ dcursor, uint32_t parts, uint64_t cap,
-                                    uint32_t* __restrict__ out, unsigned long long* __restrict__ stats,
-                                    int heavy_done) {
+    if (!routed)
+        for (uint64_t i = dcursor[d] + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap;
+             i += (uint64_t)gridDim.x * blockDim.x)
+            send[d * cap + i] = kNoKey;
+    if (blockIdx.x || blockIdx.y) return;
     const uint32_t t = threadIdx.x;
     if (t < kStN) {
         unsigned long long v = 0;
@@ -5107,7 +5783,10 @@ __global__ void split_finish_kernel(const unsigned long long* __restrict__ gstat
             shard = max(shard, gstats[kRbCursor + sh]);
             spill += gstats[kRbSpill + sh];
         }
-        for (uint32_t d = 0; d < parts; ++d) part = max(part, dcursor[d]);
+        if (routed)
+            for (uint32_t q = 0; q < parts * kShards; ++q) part = max(part, dcursor[q] * kShards);
+        else
+            for (uint32_t q = 0; q < parts; ++q) part = max(part, dcursor[q]);
         const uint32_t clamp = 0xFFFFFFFFu;
         out[KMP_SPLIT_CLASS] = wflags[kFlClass];
         out[KMP_SPLIT_HEAVY] = spill != 0 && !heavy_done;  // spilled with the heavy path off: rerun with it on
@@ -5152,6 +5831,18 @@ int kmp_postings_last_layout(const kmp_postings* ws) {
 }
 
 uint32_t kmp_postings_last_overflow_blocks(const kmp_postings* ws) { return ws ? ws->last_ovf : 0u; }
+
+int kmp_postings_set_tail(kmp_postings* ws, int mode) {
+    if (!ws || (mode != KMP_TAIL_FAST && mode != KMP_TAIL_COUNT)) return KMP_EINVAL;
+    ws->fast_mode = mode == KMP_TAIL_FAST;
+    ws->fast_tail = ws->fast_mode;
+    return KMP_OK;
+}
+
+int kmp_postings_last_tail(const kmp_postings* ws) {
+    if (!ws || !ws->last_bucketed) return -1;
+    return ws->last_fast ? KMP_TAIL_FAST : KMP_TAIL_COUNT;
+}
 
 int kmp_postings_set_graph(kmp_postings* ws, int enable) {
     if (!ws) return KMP_EINVAL;
@@ -5387,6 +6078,7 @@ int kmp_dev_split_expand(kmp_postings* ws, const uint8_t* d_res, const uint64_t*
         ws->cur_on = ws->cur_mode;
         ws->shape.clear();
         ws->split_heavy = false;
+        ws->fast_tail = ws->fast_mode;
     }
     if (learn) {  // the last call's flags, reduced over the ranks: every rank grows the same way
         if (learn[KMP_SPLIT_HEAVY]) ws->split_heavy = true;  // a rank spilled: the heavy path from now on
@@ -5412,7 +6104,7 @@ int kmp_dev_split_expand(kmp_postings* ws, const uint8_t* d_res, const uint64_t*
         const int rc = step_reserve(ws, c, g, st);
         if (rc != KMP_OK) return rc;
     }
-    PG(ws->split_cur.reserve(kSplitMax));
+    PG(ws->split_cur.reserve((uint64_t)kSplitMax * kShards));
     const BpDigits dg = bp_digits(lay);
     ws->bin_lo = (uint32_t)((uint64_t)part * dg.nb1 / parts);
     ws->bin_hi = (uint32_t)((uint64_t)(part + 1) * dg.nb1 / parts);
@@ -5424,20 +6116,40 @@ int kmp_dev_split_expand(kmp_postings* ws, const uint8_t* d_res, const uint64_t*
     SplitRows rows{};
     rows.parts = parts;
     kmp_row_split(n, parts, rows.start);
+    // the send cursors are cleared with the step's flags (step_clear_kernel in the front); routed
+    // (no heavy path): the bucket kernels write the send regions, pre-filled with kNoKey
+    const bool routed = !ws->split_heavy;
     auto front = [&](hipStream_t s) -> int {
-        if (ws->bin_hi > ws->bin_lo) return enqueue_front(ws, make_keys, c, true, s);
-        step_clear_kernel<<<1, 256, 0, s>>>(ws->flags.p, ws->bstats.p);  // no bins: nothing to expand
-        return KMP_OK;
+        const uint32_t ncur = routed ? parts * kShards : parts;
+        ws->clear_extra = ws->split_cur.p;
+        ws->clear_n = ncur;
+        if (routed) {
+            PG(hipMemsetAsync(d_send, 0xFF, (size_t)parts * cap * sizeof(unsigned long long), s));
+            ws->route_send = d_send;
+            ws->route_cap = cap;
+            ws->route_rows = rows;
+        }
+        int rc = KMP_OK;
+        if (ws->bin_hi > ws->bin_lo) rc = enqueue_front(ws, make_keys, c, true, s);
+        else step_clear_kernel<<<1, 256, 0, s>>>(ws->flags.p, ws->bstats.p, ws->split_cur.p, ncur);  // no bins
+        ws->clear_extra = nullptr;
+        ws->clear_n = 0;
+        ws->route_send = nullptr;
+        return rc;
     };
     auto route = [&](hipStream_t s, int heavy_done) -> int {
-        split_clear_kernel<<<1, kSplitMax, 0, s>>>(ws->split_cur.p, parts);
+        if (routed) {  // the bucket kernels routed the keys: the flags and statistics only
+            split_pad_finish_kernel<<<dim3(1, 1), 256, 0, s>>>(d_send, cap, ws->split_cur.p, ws->bstats.p, ws->flags.p,
+                                                                ws->shard_cap, parts, d_flags, d_stats, heavy_done, 1);
+            PG(hipGetLastError());
+            return KMP_OK;
+        }
         const unsigned long long* cursor = ws->bstats.p + kRbCursor;
         split_route_kernel<<<dim3((uint32_t)((ws->shard_cap + kRtTile - 1) / kRtTile), kShards), kRtThreads, 0, s>>>(
             ws->inc_sorted.p, cursor, ws->shard_cap, bits_for(n), rows, cap, d_send, ws->split_cur.p);
-        split_pad_kernel<<<dim3((uint32_t)std::min<uint64_t>((cap + 1023) / 1024, 256), parts), 256, 0, s>>>(
-            d_send, cap, ws->split_cur.p);
-        split_finish_kernel<<<1, 64, 0, s>>>(ws->bstats.p, ws->flags.p, ws->shard_cap, ws->split_cur.p, parts, cap,
-                                              d_flags, d_stats, heavy_done);
+        split_pad_finish_kernel<<<dim3((uint32_t)std::min<uint64_t>((cap + 1023) / 1024, 256), parts), 256, 0, s>>>(
+            d_send, cap, ws->split_cur.p, ws->bstats.p, ws->flags.p, ws->shard_cap, parts, d_flags, d_stats,
+            heavy_done, 0);
         PG(hipGetLastError());
         return KMP_OK;
     };
@@ -5448,6 +6160,7 @@ int kmp_dev_split_expand(kmp_postings* ws, const uint8_t* d_res, const uint64_t*
         // are the rank's own, so a spill overflow reruns the front here; every other capacity is
         // reported in the flags and grown identically on every rank.  Host-synchronous.
         int rc = KMP_OK;
+        bool routed = false;
         for (int attempt = 0; attempt < 4; ++attempt) {
             if ((rc = step_reserve(ws, c, g, st)) != KMP_OK) break;
             if ((rc = front(st)) != KMP_OK) break;
@@ -5468,9 +6181,12 @@ int kmp_dev_split_expand(kmp_postings* ws, const uint8_t* d_res, const uint64_t*
                 if ((rc = heavy_phase(ws, c, spill_total, true, st)) != KMP_OK) break;
             }
             rc = route(st, 1);
+            routed = true;
             break;
         }
         ws->bin_lo = ws->bin_hi = 0;
+        // every attempt grew the spill regions: the send buffer and flags were never written
+        if (rc == KMP_OK && !routed) return KMP_EOVERFLOW;
         return rc;
     }
     auto enqueue = [&](hipStream_t s) -> int {
@@ -5506,47 +6222,54 @@ int kmp_dev_split_edges(kmp_postings* ws, const unsigned long long* d_keys, uint
     c.d_w = d_w;
     c.cap = cap;
     c.stride = 1;
-    PtGeom g;
-    if (!pt_geometry(ws, c, m, &g)) return KMP_EINVAL;
-    g.flat_n = m;  // the received regions, padded with kNoKey, read as one array
-    g.nshards = 1;
-    g.sc = m;
-    g.jt = (uint32_t)((m + kPtTile - 1) / kPtTile);
-    hipError_t e = hipSuccess;
-    pt_bufs(ws, g, true, &e, st);
-    PG(e);
-    PG(ws->inc.reserve(m));  // u32 row-block keys
-    PG(ws->uniq.reserve(m));  // staged p | q (u32 each)
-    PG(ws->w.reserve(m));
-    PG(ws->ovf.reserve((uint64_t)g.nrb + 1));
-    PG(ws->small.reserve(16));
-    PG(ws->flags.reserve(kFlN));
-    PG(ws->bstats.reserve(kGsWords));
-    if (!ws->hrb) PG(hipHostMalloc((void**)&ws->hrb, kRbWords * sizeof(unsigned long long), hipHostMallocCoherent));
-    auto enqueue = [&](hipStream_t s) -> int {
-        step_clear_kernel<<<1, 256, 0, s>>>(ws->flags.p, ws->bstats.p);  // flags (the expand's stats are out)
-        return enqueue_tail_in(ws, c, g, d_keys, nullptr, m, s);
-    };
-    const std::vector<unsigned long long> key = {m, n, row_lo, row_hi, c.min_shared, cap, (uintptr_t)d_keys,
-                                                 (uintptr_t)d_p, (uintptr_t)d_q, (uintptr_t)d_w, g.rbits,
-                                                 ws->timing};
-    int rc = slot_launch(ws, ws->split_g[1], key, enqueue, st);
-    if (rc != KMP_OK) return rc;
-    PG(hipStreamSynchronize(st));
-    const unsigned long long* rb = ws->hrb;
-    uint64_t ne = rb[kRbRuns];
-    if (rb[kRbOvf] && !pt_rowhist_ok(g)) {  // row blocks above the LDS capacity: the segmented sort, fewer rows per block next time
-        if (g.rbits > 0) {
-            const double over = (double)rb[kRbMaxBlock] / (0.8 * kPtCap);
-            unsigned shrink = 1;
-            while (shrink < 16 && (double)(1u << shrink) < over) ++shrink;
-            ws->pt_rb_max = g.rbits > shrink ? g.rbits - shrink : 0u;
-        }
-        rc = pt_finish_overflow(ws, c, g, (uint32_t)rb[kRbOvf], &ne, st, m);
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        PtGeom g;
+        if (!pt_geometry(ws, c, m, &g)) return KMP_EINVAL;
+        g.flat_n = m;  // the received regions, padded with kNoKey, read as one array
+        g.nshards = 1;
+        g.sc = m;
+        g.jt = (uint32_t)((m + kPtTile - 1) / kPtTile);
+        hipError_t e = hipSuccess;
+        pt_bufs(ws, g, true, &e, st);
+        PG(e);
+        PG(ws->inc.reserve(pt_fast(ws, g) ? std::max<uint64_t>(m, (uint64_t)g.nrb * kFtCap / 2) : m));  // u32 row-block keys
+        PG(ws->uniq.reserve(m));  // staged p | q (u32 each)
+        PG(ws->w.reserve(m));
+        PG(ws->ovf.reserve((uint64_t)g.nrb + 1));
+        PG(ws->small.reserve(16));
+        PG(ws->flags.reserve(kFlN));
+        PG(ws->bstats.reserve(kGsWords));
+        if (!ws->hrb) PG(hipHostMalloc((void**)&ws->hrb, kRbWords * sizeof(unsigned long long), hipHostMallocCoherent));
+        auto enqueue = [&](hipStream_t s) -> int {
+            step_clear_kernel<<<1, 256, 0, s>>>(ws->flags.p, ws->bstats.p);  // flags (the expand's stats are out)
+            return enqueue_tail_in(ws, c, g, d_keys, nullptr, m, s);
+        };
+        const std::vector<unsigned long long> key = {m, n, row_lo, row_hi, c.min_shared, cap, (uintptr_t)d_keys,
+                                                     (uintptr_t)d_p, (uintptr_t)d_q, (uintptr_t)d_w, g.rbits,
+                                                     ws->timing, ws->fast_tail};
+        int rc = slot_launch(ws, ws->split_g[1], key, enqueue, st);
         if (rc != KMP_OK) return rc;
+        PG(hipStreamSynchronize(st));
+        const unsigned long long* rb = ws->hrb;
+        if (rb[kRbFast]) {  // a fast-tail region overflowed: the counting tail (learned until a new shape)
+            ws->fast_tail = false;
+            continue;
+        }
+        uint64_t ne = rb[kRbRuns];
+        if (rb[kRbOvf] && !pt_rowhist_ok(g)) {  // row blocks above the LDS capacity: the segmented sort, fewer rows per block next time
+            if (g.rbits > 0) {
+                const double over = (double)rb[kRbMaxBlock] / (0.8 * kPtCap);
+                unsigned shrink = 1;
+                while (shrink < 16 && (double)(1u << shrink) < over) ++shrink;
+                ws->pt_rb_max = g.rbits > shrink ? g.rbits - shrink : 0u;
+            }
+            rc = pt_finish_overflow(ws, c, g, (uint32_t)rb[kRbOvf], &ne, st, m);
+            if (rc != KMP_OK) return rc;
+        }
+        *n_edges = ne;
+        return ne > cap ? KMP_EOVERFLOW : KMP_OK;
     }
-    *n_edges = ne;
-    return ne > cap ? KMP_EOVERFLOW : KMP_OK;
+    return KMP_EDEVICE;
 }
 
 // Row ranges of a split of the pair space: a pair belongs to its smaller protein, so row p owns

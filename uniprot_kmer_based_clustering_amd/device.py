@@ -250,10 +250,19 @@ class DevicePipeline:
         """Whether the last call spilled frequent k-mers (df > 128) to the heavy path."""
         return lib().kmp_postings_last_layout(self._workspace()) == _lib.KMP_LAYOUT_BUCKETED_HEAVY
 
+    def set_tail(self, mode: str = "fast") -> None:
+        """Row-block tail of unscored calls: 'fast' (default, where it applies) or 'count'."""
+        m = {"fast": _lib.KMP_TAIL_FAST, "count": _lib.KMP_TAIL_COUNT}[mode]
+        check(lib().kmp_postings_set_tail(self._workspace(), m), "kmp_postings_set_tail")
+
     def last_tail(self) -> str:
-        """How the last postings call reduced its pair keys: 'rows' (row-block LDS sort tail,
-        bucketed layout) or 'sort' (global pair-key sort, flat layout)."""
-        return "sort" if self.last_layout() == "flat" else "rows"
+        """How the last postings call reduced its pair keys: 'fast' (fixed row-block regions, LDS
+        hash-aggregate + rank, edges written at look-back offsets), 'rows' (the counting row-block
+        tail: histogram, scan, scatter, block sort, emit) or 'sort' (global pair-key sort, flat
+        layout)."""
+        if self.last_layout() == "flat":
+            return "sort"
+        return "fast" if lib().kmp_postings_last_tail(self._workspace()) == _lib.KMP_TAIL_FAST else "rows"
 
     def overflow_blocks(self) -> int:
         """Row blocks of the last call above the LDS capacity (finished by the segmented sort)."""
