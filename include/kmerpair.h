@@ -539,7 +539,8 @@ int kmp_dev_pairs_rows_multi(kmp_postings* const* ws, const int* ks, uint32_t nk
  *   kmp_dev_split_expand  every window of the batch is keyed, the rank keeps the k-mers of its
  *     share of the bucket hash range (a contiguous range of coarse bins), groups and expands them
  *     (all rows), and routes each pair key (p << bits(N) | q) to the rank owning row p
- *     (kmp_row_split): region d of d_send (cap keys, unused tail kNoKey) is rank d's.  No host
+ *     (kmp_row_split): region d of d_send (cap keys, padded with kNoKey = all ones: the bucket
+ *     kernels write it in 64 sub-regions of cap / 64 keys each) is rank d's.  No host
  *     synchronisation (except with the heavy path on: one read-back of the front's spill, which
  *     the rank compacts, plans and expands into its routed keys); d_flags[KMP_SPLIT_FLAGS] and
  *     d_stats[8] (Σ|K(p)|, distinct, repeat,

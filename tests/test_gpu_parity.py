@@ -398,24 +398,34 @@ def test_frequent_kmers_heavy_path(oracle_mod, copies):
     np.testing.assert_array_equal(pipe.edges()[1], q)
 
 
-def test_uniprot_k5_on_bucketed_heavy_path(oracle_mod, uni):
+@pytest.mark.parametrize("tail", ["fast", "count"])
+def test_uniprot_k5_on_bucketed_heavy_path(oracle_mod, uni, tail):
     """The reference's dataset at k = 5 (max df 3,694): bucketed layout with the heavy path and
-    the row-block tail, edge list sha equal to the golden one (repeat: graph replay is not used
-    on the split step, every call recomputes)."""
+    the row-block tail — the fast tail's dense variant (N < 2^14: per-block LDS bins over (row, q))
+    or the counting tail — edge list sha equal to the golden one (repeat: graph replay is not used
+    on the split step, every call recomputes); min_shared 2 against the oracle."""
     import torch
     from uniprot_kmer_based_clustering_amd.device import DevicePipeline
     res, off, cls = uni
     g = load_json("uniprot_counters.json")["5"]
     pipe = DevicePipeline(K.Proteins(res, off, cls), 5, "cuda:0")
+    pipe.set_tail(tail)
     for _ in range(2):
         m = pipe.step(engine="residues")
         torch.cuda.synchronize()
-        assert pipe.last_layout() == "bucketed" and pipe.last_heavy() and pipe.last_tail() in ("rows", "fast")
+        assert pipe.last_layout() == "bucketed" and pipe.last_heavy()
+        assert pipe.last_tail() == ("fast" if tail == "fast" else "rows")
         assert m == g["n_edges"]
         assert edges_sha256(*pipe.edges()) == g["edges_sha256"]
         st = pipe.postings_stats.as_dict()
         assert st["max_df"] == g["max_df"] and st["sum_cdf2_light"] == g["sum_cdf2"]
         assert st["incidences"] == g["sum_w_diff"] and st["distinct"] == g["distinct"]
+    p, q, w = oracle_mod.Oracle(res, off, cls, k=5, threads=8).pairs(min_shared=2)
+    assert pipe.step(min_shared=2, engine="residues") == len(p)
+    ep, eq, ew = pipe.edges()
+    np.testing.assert_array_equal(ep, p)
+    np.testing.assert_array_equal(eq, q)
+    np.testing.assert_array_equal(ew, w)
 
 
 @pytest.mark.parametrize("k", [5, 7])

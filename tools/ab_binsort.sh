@@ -1,15 +1,11 @@
-# A/B of the row-block reduce's sort (KMP_BINSORT: 0 radix, 2 bins everywhere, 1 default) on
-# config 3 and config 5
+# A/B of the row-block reduce's sort on config 3 and config 5: builds the library with
+# KMP_BINSORT_MODE=0 (radix everywhere) and =2 (bins everywhere) into tools/ab/ (run on the CPU
+# side first: bash tools/ab_binsort.sh build), then the A/B on the GPU box (bash tools/ab_binsort.sh)
 set -e
+if [ "$1" = build ]; then
+  bash "$(dirname "$0")/ab_build.sh" bs0 -DKMP_BINSORT_MODE=0
+  bash "$(dirname "$0")/ab_build.sh" bs2 -DKMP_BINSORT_MODE=2
+  exit 0
+fi
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out
-for m in 0 2; do
-  KMP_BINSORT=$m timeout -k 10 120 python3 bench.py --no-cpu-baseline > gpurun_out/ab_c3_$m.json 2>/dev/null
-  python3 -c "
-import json; d=json.load(open('gpurun_out/ab_c3_$m.json')); print('c3 mode $m', round(d['ms_per_step'],4), {k: round(v['ms'],4) for k,v in d['roofline']['stages'].items()})"
-done
-for m in 0 2; do
-  KMP_BINSORT=$m timeout -k 10 200 python3 bench.py --config config5 --no-cpu-baseline > gpurun_out/ab_c5_$m.json 2>/dev/null
-  python3 -c "
-import json; d=json.load(open('gpurun_out/ab_c5_$m.json')); print('c5 mode $m', round(d['ms_per_step']), {k: round(v['ms']) for k,v in d['roofline']['stages'].items()})"
-done
+CONFIGS="config3 config5" bash tools/ab_multi.sh

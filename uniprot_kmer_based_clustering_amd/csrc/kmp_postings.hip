@@ -3238,6 +3238,8 @@ struct PtGeom {
     uint32_t nprot;         // proteins (q < nprot): the pair range of a row block (pt_bin_sort)
     uint32_t rowend;        // the call's last row + 1
     int binsort;            // the reduce sorts by bins (pt_bin_sort), else the block radix sort
+    uint32_t ftcap;         // fast tail: keys per row-block region
+    int dense;              // fast tail: per-block dense histogram over (row, q) (2^(pbits + rbits) bins)
 };
 
 // The blocks a reduce runs over: row blocks (size == nullptr: block r is keys [start[r], start[r+1])
@@ -3396,12 +3398,13 @@ __global__ __launch_bounds__(kPtThreads) void pt_scatter_kernel(const unsigned l
 }
 
 // The fast tail's scatter (pt_reduce_fast): a tile of kThr * 16 keys ranked by row block in LDS;
-// cur[r] counts from zero and block r's keys go to the fixed region [r * kFtCap, (r + 1) * kFtCap)
+// cur[r] counts from zero and block r's keys go to the fixed region [r * ftcap, (r + 1) * ftcap)
 // of out, written as u32 (p - r * 2^rbits) << pbits | q (keys past the region are dropped; the
 // reduce sees the count and flags the overflow) — no histogram pass, no scan.  Workgroup (0, 0)
 // also clears the reduce's look-back words lb[0, nrb).  Tiles of 8,192 keys: twice the workgroups
 // of the counting tail's 16,384-key tiles (which ran one per CU), at LDS for two per CU.
-constexpr uint32_t kFtCap = 8192;  // fast tail: keys per row-block region
+constexpr uint32_t kFtCap = 8192;  // fast tail, hash reduce: keys per row-block region (dense: kFdCap)
+constexpr uint32_t kFdCap = 32768, kFdBitsMax = 15;  // dense reduce: region keys, bins 2^(pbits + rbits)
 constexpr uint32_t kFtScThreads = 512, kFtScTile = kFtScThreads * 16;
 __global__ __launch_bounds__(kFtScThreads) void pt_scatter_capped_kernel(const unsigned long long* __restrict__ in,
                                                                          const unsigned long long* __restrict__ cursor,
@@ -3473,7 +3476,7 @@ __global__ __launch_bounds__(kFtScThreads) void pt_scatter_capped_kernel(const u
     const uint32_t placed = s_n;
     for (uint32_t i = threadIdx.x; i < placed; i += kThr) {
         const uint32_t r = SR[i], pos = lh[r] + i;
-        if (pos < kFtCap) out[(uint64_t)r * kFtCap + pos] = S[i];
+        if (pos < g.ftcap) out[(uint64_t)r * g.ftcap + pos] = S[i];
     }
 }
 
@@ -4386,7 +4389,7 @@ __global__ __launch_bounds__(kFtThreads) void pt_reduce_fast_kernel(const uint32
     if (tid == 0) fcur[r] = 0;
     const bool ovf = nraw > kFtCap;
     const uint32_t n = ovf ? 0u : nraw;
-    const uint32_t* src = keys + (uint64_t)r * kFtCap;
+    const uint32_t* src = keys + (uint64_t)r * kFtCap;  // g.ftcap == kFtCap in this mode
     const unsigned pb = g.pbits;
     const uint32_t R = 1u << g.rbits;
     uint32_t D = 0;  // the block's kept pairs
@@ -4560,6 +4563,107 @@ __global__ __launch_bounds__(kFtThreads) void pt_reduce_fast_kernel(const uint32
     }
 }
 
+
+// The dense variant (small batches: pbits + rbits <= kFdBitsMax, the reference's uniprot_arg.fasta at
+// k = 5 among them, whose rows pair with thousands of later proteins): block r's keys counted in
+// 2^(pbits + rbits) LDS bins over (row, q) — u16 counts, two per word — so the bins ARE the canonical
+// order: no hash, no rank, no sort.  Thread t owns the contiguous words [t q, t q + q) (q = words /
+// kFtThreads); stored XOR-swizzled (word w at w ^ ((w / q) mod min(q, 32))) so the owners' reads of
+// their words hit distinct banks.  Regions of kFdCap keys; a count that would reach 16 bits raises
+// the overflow like a full region (the caller reruns on the counting tail).
+__device__ __forceinline__ uint32_t fd_phys(uint32_t w, unsigned qs) {
+    return w ^ ((w >> qs) & ((1u << min(qs, 5u)) - 1));
+}
+__global__ __launch_bounds__(kFtThreads) void pt_reduce_dense_kernel(const uint32_t* __restrict__ keys,
+                                                                     uint32_t* __restrict__ fcur, PtGeom g,
+                                                                     unsigned long long* __restrict__ lb,
+                                                                     uint32_t* __restrict__ d_p,
+                                                                     uint32_t* __restrict__ d_q,
+                                                                     uint32_t* __restrict__ d_w, uint64_t cap,
+                                                                     uint32_t stride, PtPack pack,
+                                                                     uint32_t* __restrict__ runs) {
+    __shared__ uint32_t W[1u << (kFdBitsMax - 1)];  // 64 KB
+    __shared__ uint32_t wave_tot[kFtThreads / 64];
+    __shared__ uint32_t s_flag;
+    __shared__ unsigned long long s_excl;
+    const uint32_t r = blockIdx.x, tid = threadIdx.x;
+    const uint32_t nraw = fcur[r];
+    __syncthreads();  // every thread has its count before the cursor is cleared for the next call
+    if (tid == 0) {
+        fcur[r] = 0;
+        s_flag = 0;
+    }
+    bool ovf = nraw > g.ftcap;
+    const uint32_t n = ovf ? 0u : nraw;
+    const uint32_t* src = keys + (uint64_t)r * g.ftcap;
+    const unsigned pb = g.pbits, bits = g.pbits + g.rbits;
+    const uint32_t words = 1u << (bits - 1);
+    unsigned qs = 0;  // q = words / kFtThreads = 2^qs words per thread (at least one)
+    while ((kFtThreads << qs) < words) ++qs;
+    for (uint32_t i = tid; i < words; i += kFtThreads) W[i] = 0;
+    __syncthreads();
+    for (uint32_t i0 = 0; i0 < n; i0 += 8 * kFtThreads) {  // loads in batches ahead of their atomics
+        uint32_t x[8];
+#pragma unroll
+        for (uint32_t e = 0; e < 8; ++e) {
+            const uint32_t i = i0 + e * kFtThreads + tid;
+            x[e] = i < n ? src[i] : kFtEmpty;
+        }
+#pragma unroll
+        for (uint32_t e = 0; e < 8; ++e)
+            if (x[e] != kFtEmpty) {
+                const uint32_t sh = 16 * (x[e] & 1u);
+                const uint32_t old = atomicAdd(&W[fd_phys(x[e] >> 1, qs)], 1u << sh);
+                if (((old >> sh) & 0xFFFFu) >= 0xFFFEu) s_flag = 1;
+            }
+    }
+    __syncthreads();
+    ovf = ovf || s_flag;  // uniform
+    // kept bins (w >= min_shared) of the thread's words, in bin order
+    const uint32_t q = 1u << qs, w0 = tid << qs;
+    uint32_t kept = 0;
+    if (!ovf)
+        for (uint32_t j = 0; j < q && w0 + j < words; ++j) {
+            const uint32_t v = W[fd_phys(w0 + j, qs)];
+            kept += ((v & 0xFFFFu) >= g.min_shared) + ((v >> 16) >= g.min_shared);
+        }
+    uint32_t excl, D;
+    block_scan_n<kFtThreads>(kept, excl, D, wave_tot);
+    if (tid < 64) {
+        const unsigned long long ex = ft_lookback(lb, r, (unsigned long long)D | (ovf ? kLbOvf : 0ull));
+        if (tid == 0) s_excl = ex;
+    }
+    __syncthreads();
+    const unsigned long long ex = s_excl;
+    uint64_t o = (uint32_t)ex + (uint64_t)excl;
+    const uint32_t rowbase = g.row0 + (r << g.rbits), qm = (1u << pb) - 1;
+    if (kept)
+        for (uint32_t j = 0; j < q && w0 + j < words; ++j) {
+            const uint32_t v = W[fd_phys(w0 + j, qs)];
+#pragma unroll
+            for (uint32_t h = 0; h < 2; ++h) {
+                const uint32_t c = h ? v >> 16 : v & 0xFFFFu;
+                if (c < g.min_shared || c == 0) continue;
+                const uint32_t bin = 2 * (w0 + j) + h;
+                if (o < cap) {
+                    d_p[o * stride] = rowbase + (bin >> pb);
+                    d_q[o * stride] = bin & qm;
+                    d_w[o * stride] = c;
+                }
+                ++o;
+            }
+        }
+    if (r + 1 == gridDim.x) {  // the last block: the edge count and the read-back
+        const bool any_ovf = ovf || (ex & kLbOvf);
+        if (tid == 0) {
+            runs[0] = (uint32_t)ex + D;
+            runs[1] = 0;
+        }
+        __syncthreads();
+        if (pack.rb) step_pack_body(pack.gstats, pack.flags, runs, pack.rb, any_ovf ? 1ull : 0ull);
+    }
+}
+
 // one call's parameters
 struct StepCfg {
     uint64_t slots;
@@ -4588,6 +4692,9 @@ struct StepCfg {
 // kPtCap keys (from the expected incidence count)
 #ifndef KMP_FT_TARGET
 #define KMP_FT_TARGET 2275
+#endif
+#ifndef KMP_BINSORT_MODE
+#define KMP_BINSORT_MODE 1
 #endif
 bool pt_geometry(const kmp_postings* ws, const StepCfg& c, uint64_t inc, PtGeom* g) {
     g->pbits = bits_for(c.n);
@@ -4622,8 +4729,25 @@ bool pt_geometry(const kmp_postings* ws, const StepCfg& c, uint64_t inc, PtGeom*
     g->min_shared = std::max(1u, c.min_shared);
     g->nprot = c.n;
     g->rowend = c.ranged ? c.row_hi : c.n;
-    static const int bs_mode = getenv("KMP_BINSORT") ? atoi(getenv("KMP_BINSORT")) : 1;  // A/B switch
-    g->binsort = bs_mode == 2 ? 1 : bs_mode == 0 ? 0 : (g->sbits != 0);
+    g->ftcap = kFtCap;
+    g->dense = 0;
+    if (!c.sb && ws->fast_tail && g->pbits < kFdBitsMax) {
+        // dense fast tail: the fewest rows per block that the block count allows, when the blocks
+        // still average a few hundred keys (a sparse call keeps the hash reduce: clearing 2^15 bins
+        // for a handful of keys would dominate)
+        unsigned rd = 0;
+        while (((rows + (1ull << rd) - 1) >> rd) > kPtMaxBlocks) ++rd;
+        const uint64_t nrd = (rows + (1ull << rd) - 1) >> rd;
+        if (g->pbits + rd <= kFdBitsMax && est / std::max<uint64_t>(1, nrd) >= 256) {
+            g->rbits = rd;
+            g->nrb = (uint32_t)std::max<uint64_t>(1, nrd);
+            g->ftcap = kFdCap;
+            g->dense = 1;
+        }
+    }
+    // the bin sort for scored blocks only (unscored at config 3: 0.130 -> 0.387 ms);
+    // KMP_BINSORT_MODE (A/B builds): 0 the radix sort everywhere, 2 the bin sort everywhere
+    g->binsort = KMP_BINSORT_MODE == 2 ? 1 : KMP_BINSORT_MODE == 0 ? 0 : (g->sbits != 0);
     return true;
 }
 
@@ -4721,7 +4845,7 @@ int step_reserve(kmp_postings* ws, const StepCfg& c, const PtGeom& g, hipStream_
     PG(ws->inc_sorted.reserve(total));
     if (!c.expand_only) {  // an expand-only call leaves the tail (and its staging) to tail_multi
         // u32 row-block keys (pt_scatter; the fast tail's fixed regions) ...
-        PG(ws->inc.reserve(pt_fast(ws, g) ? std::max<uint64_t>(total, (uint64_t)g.nrb * kFtCap / 2) : total));
+        PG(ws->inc.reserve(pt_fast(ws, g) ? std::max<uint64_t>(total, (uint64_t)g.nrb * g.ftcap / 2) : total));
         PG(ws->uniq.reserve(total));  // ... staged p | q (u32 each)
         PG(ws->w.reserve(total));     // ... staged w
         if (c.sb) PG(ws->stg2.reserve(2 * total));  // ... staged scores | second-k weights
@@ -4789,10 +4913,16 @@ int enqueue_tail_in(kmp_postings* ws, const StepCfg& c, const PtGeom& g, const u
         const uint32_t jt = (uint32_t)(((g.flat_n ? g.flat_n : g.sc) + kFtScTile - 1) / kFtScTile);
         pt_scatter_capped_kernel<<<dim3(jt, g.nshards), kFtScThreads, 0, st>>>(in, cursor, g, b.fcur, keys32, b.lb);
         ws->mark(4, st);
-        pt_reduce_fast_kernel<<<g.nrb, kFtThreads, 0, st>>>(keys32, b.fcur, g, b.lb, c.d_p, c.d_q, c.d_w, c.cap,
-                                                             c.stride,
-                                                             PtPack{ws->bstats.p, ws->flags.p, nullptr, ws->hrb},
-                                                             ws->small.p + 1);
+        if (g.dense)
+            pt_reduce_dense_kernel<<<g.nrb, kFtThreads, 0, st>>>(keys32, b.fcur, g, b.lb, c.d_p, c.d_q, c.d_w, c.cap,
+                                                                  c.stride,
+                                                                  PtPack{ws->bstats.p, ws->flags.p, nullptr, ws->hrb},
+                                                                  ws->small.p + 1);
+        else
+            pt_reduce_fast_kernel<<<g.nrb, kFtThreads, 0, st>>>(keys32, b.fcur, g, b.lb, c.d_p, c.d_q, c.d_w, c.cap,
+                                                                 c.stride,
+                                                                 PtPack{ws->bstats.p, ws->flags.p, nullptr, ws->hrb},
+                                                                 ws->small.p + 1);
         ws->mark(5, st);
         ws->mark(6, st);
         PG(hipGetLastError());
@@ -6232,7 +6362,7 @@ int kmp_dev_split_edges(kmp_postings* ws, const unsigned long long* d_keys, uint
         hipError_t e = hipSuccess;
         pt_bufs(ws, g, true, &e, st);
         PG(e);
-        PG(ws->inc.reserve(pt_fast(ws, g) ? std::max<uint64_t>(m, (uint64_t)g.nrb * kFtCap / 2) : m));  // u32 row-block keys
+        PG(ws->inc.reserve(pt_fast(ws, g) ? std::max<uint64_t>(m, (uint64_t)g.nrb * g.ftcap / 2) : m));  // u32 row-block keys
         PG(ws->uniq.reserve(m));  // staged p | q (u32 each)
         PG(ws->w.reserve(m));
         PG(ws->ovf.reserve((uint64_t)g.nrb + 1));
