@@ -2506,6 +2506,7 @@ __global__ __launch_bounds__(kThr, KMP_L1P_WAVES) void bp_scatter1p_kernel(
     uint32_t c = blockIdx.x;
     if (c >= G) return;
     for (uint32_t i = tid; i < 256; i += kThr) lut[i] = c_lut.v[i];
+    __syncthreads();  // the table before the first staging reads it
     const uint64_t res_end = res_off[n];
     const bool vec_ok = ((uintptr_t)res & 15u) == 0;
     // one chunk's loads, held in registers until it is staged
@@ -4363,7 +4364,8 @@ struct FtLds {
     union {
         struct {
             uint32_t K[kFtSlots];  // hash slots (pair key), then the block's pairs in row / canonical order
-            uint16_t C[kFtSlots];  // counts (w), two per 32-bit word for the LDS atomics
+            uint16_t C[kFtSlots + 2];  // counts (w), two per 32-bit word for the LDS atomics; the
+                                       // sort path's run heads use C[0, nruns] (nruns <= kFtCap)
         } h;
         typename PtSort<16>::storage_type s16;
     };
