@@ -647,6 +647,24 @@ __device__ __forceinline__ void block_scan_n(uint32_t v, uint32_t& excl, uint32_
     total = tot;
 }
 
+// exclusive scan of lh[0, nb) in place (kThreads threads); ends with a barrier
+template <int kThreads = kKeyThreads>
+__device__ __forceinline__ void lds_bins_scan(uint32_t* lh, uint32_t nb, uint32_t* wave_tot) {
+    const uint32_t q = (nb + kThreads - 1) / kThreads, b0 = threadIdx.x * q;
+    uint32_t v = 0;
+    for (uint32_t t = 0; t < q; ++t)
+        if (b0 + t < nb) v += lh[b0 + t];
+    uint32_t excl, total;
+    block_scan_n<kThreads>(v, excl, total, wave_tot);  // barriers inside
+    for (uint32_t t = 0; t < q; ++t)
+        if (b0 + t < nb) {
+            const uint32_t c = lh[b0 + t];
+            lh[b0 + t] = excl;
+            excl += c;
+        }
+    __syncthreads();
+}
+
 constexpr uint32_t kSplitMax = 64;  // ranks of the k-mer split
 struct SplitRows {
     uint32_t start[kSplitMax + 1];  // row range of rank d: [start[d], start[d+1])
@@ -1403,6 +1421,7 @@ __global__ __launch_bounds__(kN / kSegItems) void heavy_segsort_kernel(const uns
     const uint32_t cnt = (uint32_t)(sd >> 40) & 0x7FFFFFu;
     if (cnt <= kLo || cnt > kN) return;
     const bool whole = sd >> 63;
+    if (ho.cls && !whole) return;  // heavy_segclass_kernel
     const uint64_t pos = sd & ((1ull << 40) - 1), shard = pos / spill_cap;
     uint64_t dst = pos - shard * spill_cap;
     for (uint64_t t = 0; t < shard; ++t) dst += cursor[t];
@@ -1426,6 +1445,126 @@ __global__ __launch_bounds__(kN / kSegItems) void heavy_segsort_kernel(const uns
     }
 }
 
+// Class order, one k-mer per segment (a heavy group, not a whole bucket): what the compaction and the
+// class-order expansion need is class runs in ascending class, each protein once per run — not its
+// proteins ascending (only plain order, the ranged calls', searches by protein).  So: a counting sort
+// by class in LDS, a protein's later windows dropped through an LDS hash set on p (vertex.rs:59-140
+// counts a protein once per k-mer), and the segment's tail (as many slots as windows dropped) filled
+// with copies of its last key, which the compaction sees as duplicates of their neighbour.  O(n) per
+// segment with four barriers, instead of a bitonic sort (66 compare-exchange rounds at 2,048 keys) or
+// a 4-pass block radix sort.  A segment whose classes reach kScClasses sorts its keys in LDS (bitonic)
+// instead.
+constexpr uint32_t kScThreads = 512, kScItems = kSegLarge / kScThreads, kScClasses = 256, kScSlots = 2 * kSegLarge;
+__global__ __launch_bounds__(kScThreads) void heavy_segclass_kernel(const unsigned long long* __restrict__ spill,
+                                                                    uint64_t spill_cap,
+                                                                    const unsigned long long* __restrict__ cursor,
+                                                                    const unsigned long long* __restrict__ seg,
+                                                                    HeavyOrder ho, unsigned long long* __restrict__ out) {
+    __shared__ union {
+        uint32_t P[kScSlots];            // hash set of the segment's proteins (64 KB)
+        unsigned long long K[kSegLarge]; // the fallback's keys
+    } u;
+    __shared__ uint32_t CH[kScClasses];  // keys per class, then each class run's start
+    __shared__ uint32_t wave_tot[kScThreads / 64];
+    __shared__ uint32_t s_maxc;
+    __shared__ unsigned long long s_last;
+    const unsigned long long sd = seg[blockIdx.x];
+    const uint32_t cnt = (uint32_t)(sd >> 40) & 0x7FFFFFu;
+    if ((sd >> 63) || cnt > kSegLarge) return;  // a whole bucket, or above the LDS: the sorts
+    const uint32_t tid = threadIdx.x;
+    const uint64_t pos = sd & ((1ull << 40) - 1), shard = pos / spill_cap;
+    uint64_t dst = pos - shard * spill_cap;
+    for (uint64_t t = 0; t < shard; ++t) dst += cursor[t];
+    const unsigned long long cm = (1ull << ho.cb) - 1, hm = ~((1ull << ho.hshift) - 1);
+    const uint32_t pm = (uint32_t)((1ull << ho.pbits) - 1);
+    unsigned long long v[kScItems];
+    uint32_t mc = 0;
+#pragma unroll
+    for (uint32_t e = 0; e < kScItems; ++e) {
+        const uint32_t i = tid + e * kScThreads;
+        v[e] = ~0ull;
+        if (i < cnt) {
+            const unsigned long long x = spill[pos + i];
+            v[e] = (x & hm) | (x & cm) << ho.pbits | ((x & ~hm) >> ho.cb);  // [h | class | p]
+            mc = max(mc, (uint32_t)(v[e] >> ho.pbits) & (uint32_t)cm);
+        }
+    }
+    for (uint32_t i = tid; i < kScSlots; i += kScThreads) u.P[i] = 0xFFFFFFFFu;
+    for (uint32_t i = tid; i < kScClasses; i += kScThreads) CH[i] = 0;
+    if (tid == 0) s_maxc = 0;
+    __syncthreads();
+    const uint32_t wm = wave_max(mc);
+    if ((tid & 63) == 0) atomicMax(&s_maxc, wm);
+    __syncthreads();
+    if (s_maxc >= kScClasses) {  // (uniform) many classes: a bitonic sort of the segment
+        uint32_t N = 1;
+        while (N < cnt) N <<= 1;
+        __syncthreads();  // P is dead: K reuses it
+        for (uint32_t i = tid; i < N; i += kScThreads) u.K[i] = ~0ull;
+        __syncthreads();
+#pragma unroll
+        for (uint32_t e = 0; e < kScItems; ++e) {
+            const uint32_t i = tid + e * kScThreads;
+            if (i < cnt) u.K[i] = v[e];
+        }
+        __syncthreads();
+        for (uint32_t k = 2; k <= N; k <<= 1)
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                for (uint32_t i = tid; i < N / 2; i += kScThreads) {
+                    const uint32_t lo = 2 * j * (i / j) + (i % j), hi = lo + j;
+                    const unsigned long long x = u.K[lo], y = u.K[hi];
+                    if ((x > y) == !(lo & k)) {
+                        u.K[lo] = y;
+                        u.K[hi] = x;
+                    }
+                }
+                __syncthreads();
+            }
+        for (uint32_t i = tid; i < cnt; i += kScThreads) out[dst + i] = u.K[i];
+        return;
+    }
+    // a protein's first window in the segment keeps its key, later ones are dropped; each kept key
+    // ranked in its class
+    uint32_t rk[kScItems];
+#pragma unroll
+    for (uint32_t e = 0; e < kScItems; ++e) {
+        rk[e] = ~0u;
+        if (v[e] == ~0ull) continue;
+        const uint32_t p = (uint32_t)v[e] & pm;
+        uint32_t sl = (p * 0x9E3779B1u) >> (32 - 14);  // kScSlots = 2^14
+        bool first = false;
+        while (true) {
+            const uint32_t old = atomicCAS(&u.P[sl], 0xFFFFFFFFu, p);
+            if (old == 0xFFFFFFFFu) {
+                first = true;
+                break;
+            }
+            if (old == p) break;
+            sl = (sl + 1) & (kScSlots - 1);
+        }
+        if (first) rk[e] = atomicAdd(&CH[(uint32_t)(v[e] >> ho.pbits) & (uint32_t)cm], 1u);
+    }
+    __syncthreads();
+    lds_bins_scan<kScThreads>(CH, kScClasses, wave_tot);  // CH: run starts; the kept count below
+    uint32_t kept = 0;
+#pragma unroll
+    for (uint32_t e = 0; e < kScItems; ++e)
+        if (rk[e] != ~0u) {
+            const uint32_t at = CH[(uint32_t)(v[e] >> ho.pbits) & (uint32_t)cm] + rk[e];
+            out[dst + at] = v[e];
+            ++kept;
+        }
+    // the segment's last kept key: the largest (class, position) — the highest class run's last slot
+    uint32_t D, excl;
+    block_scan_n<kScThreads>(kept, excl, D, wave_tot);
+#pragma unroll
+    for (uint32_t e = 0; e < kScItems; ++e)
+        if (rk[e] != ~0u && CH[(uint32_t)(v[e] >> ho.pbits) & (uint32_t)cm] + rk[e] == D - 1) s_last = v[e];
+    __syncthreads();
+    const unsigned long long last = s_last;
+    for (uint32_t i = D + tid; i < cnt; i += kScThreads) out[dst + i] = last;
+}
+
 // the small segments (<= kSegSmall keys): a bitonic sort of the next power of two, 256 threads
 // (the radix sort's four passes measured 0.081 ms there against 0.064 ms)
 template <uint32_t kN, uint32_t kThreads>
@@ -1435,7 +1574,7 @@ __global__ __launch_bounds__(kThreads) void heavy_segsort_bitonic_kernel(
     __shared__ unsigned long long K[kN];
     const unsigned long long sd = seg[blockIdx.x];
     const uint32_t cnt = (uint32_t)(sd >> 40) & 0x7FFFFFu;
-    if (cnt > kN) return;
+    if (cnt > kN || (ho.cls && !(sd >> 63))) return;  // one k-mer in class order: heavy_segclass_kernel
     const uint64_t pos = sd & ((1ull << 40) - 1), shard = pos / spill_cap;
     uint64_t dst = pos - shard * spill_cap;
     for (uint64_t t = 0; t < shard; ++t) dst += cursor[t];
@@ -1955,23 +2094,6 @@ BpDigits bp_digits(const Layout& lay) {
     return d;
 }
 
-// exclusive scan of lh[0, nb) in place (nb <= kBpMaxBins, kThreads threads); ends with a barrier
-template <int kThreads = kKeyThreads>
-__device__ __forceinline__ void lds_bins_scan(uint32_t* lh, uint32_t nb, uint32_t* wave_tot) {
-    const uint32_t q = (nb + kThreads - 1) / kThreads, b0 = threadIdx.x * q;
-    uint32_t v = 0;
-    for (uint32_t t = 0; t < q; ++t)
-        if (b0 + t < nb) v += lh[b0 + t];
-    uint32_t excl, total;
-    block_scan_n<kThreads>(v, excl, total, wave_tot);  // barriers inside
-    for (uint32_t t = 0; t < q; ++t)
-        if (b0 + t < nb) {
-            const uint32_t c = lh[b0 + t];
-            lh[b0 + t] = excl;
-            excl += c;
-        }
-    __syncthreads();
-}
 
 // sum of x[i * stride], i < m, with the loads issued in batches of 8 (an accumulation loop would
 // otherwise wait on every load in turn)
@@ -5158,6 +5280,9 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
         const unsigned long long* spill_cursor = ws->hcur.p;
         if (ws->h_segs && ws->h_segs <= seg_capacity(ws) && ws->h_segmax <= kSegLarge) {
             const uint32_t ns = (uint32_t)ws->h_segs;
+            if (ho.cls)
+                heavy_segclass_kernel<<<ns, kScThreads, 0, st>>>(ws->spill.p, ws->spill_cap, spill_cursor, ws->hseg.p,
+                                                                 ho, ws->hsorted.p);
             heavy_segsort_bitonic_kernel<kSegSmall, 256><<<ns, 256, 0, st>>>(
                 ws->spill.p, ws->spill_cap, spill_cursor, ws->hseg.p, ho, ws->hsorted.p);
             if (ws->h_segmax > kSegSmall)
