@@ -684,11 +684,13 @@ struct SplitRows {
 //   row_lo / row_hi (kRows): emit only the pairs whose smaller protein lies in [row_lo, row_hi)
 //     (a pass or a rank of the row split).
 //   capb: 0 -> bucket b is [bstart[b], bstart[b+1]) of sorted; else (cursor partition) bucket b
-//     is the region [b * capb, b * capb + bstart[b]) (bstart holds the counts)
+//     is the region [b * capb, b * capb + bstart[b]) (bstart holds the counts), or, with a learned
+//     layout (vreg), [vreg[b], vreg[b] + bstart[b])
 struct BucketArgs {
     const unsigned long long* sorted;
     const uint32_t* bstart;
     uint32_t capb;
+    const uint32_t* vreg;
     Layout lay;
     uint32_t mul;
     int require_diff;
@@ -789,7 +791,10 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
     __shared__ uint32_t CC[kCap / kRunMin * 4];
     uint64_t s0;
     uint32_t n;
-    if (a.capb) {
+    if (a.vreg) {
+        s0 = a.vreg[b];
+        n = min(a.bstart[b], a.vreg[b + 1] - a.vreg[b]);  // a larger count raised kFlCur: the call reruns
+    } else if (a.capb) {
         s0 = (uint64_t)b * a.capb;
         n = min(a.bstart[b], a.capb);  // a larger count raised kFlCur: the call reruns
     } else {
@@ -2056,6 +2061,7 @@ constexpr int kBucketLargeCap = 4096, kBucketLargeThreads = 1024, kBucketLargeTa
 // the large kernel grid-strides the list of large buckets (usually empty at config 3; most
 // buckets of a k = 5 batch of real proteins): four workgroups per CU (one per CU measured 8 % slower)
 constexpr int kBucketLargeGrid = 1024;
+constexpr uint32_t kVregTries = 3;  // learned bucket layouts in a row before the counting partition
 
 // ------------------------------------------------------------- bucket partition ------------
 // The residue path groups its keys by bucket (the top bbits of h) with two counting passes
@@ -2440,16 +2446,19 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scatter2_kernel(const unsigned
 // workgroups waits on its 256 returning atomics before it can write, which costs more than
 // the counting pass it replaces.
 struct CurGeom {
-    uint32_t capb;  // keys per bucket region
+    uint32_t capb;         // keys per bucket region
+    const uint32_t* vreg;  // learned layout (nullptr: fixed): bucket b's region [vreg[b], vreg[b + 1])
+    __device__ uint32_t region(uint32_t b) const { return vreg ? vreg[b] : b * capb; }
+    __device__ uint32_t cap(uint32_t b) const { return vreg ? vreg[b + 1] - vreg[b] : capb; }
 };
 
 // lh holds the tile's digit histogram and r[e] every key's rank in its digit: reserve each digit's
 // run on cursor(d) (start of its region: region(d), cap keys), place the tile digit-major into S
 // and write each run at its reservation; keys past their region's end are dropped (kFlCur)
-template <uint32_t kPer, class Digit, class Cursor, class Region, uint32_t kThr = kKeyThreads>
+template <uint32_t kPer, class Digit, class Cursor, class Region, class Cap, uint32_t kThr = kKeyThreads>
 __device__ __forceinline__ void bp_place_cur(const unsigned long long (&x)[kPer], const uint32_t (&r)[kPer],
                                              uint32_t n_in, uint32_t nb, Digit digit, Cursor cursor, Region region,
-                                             uint32_t cap, uint32_t* lh, uint32_t* wave_tot, unsigned long long* S,
+                                             Cap cap, uint32_t* lh, uint32_t* wave_tot, unsigned long long* S,
                                              unsigned long long* __restrict__ out, uint32_t* __restrict__ flags) {
     constexpr uint32_t kQ = kBpMaxBins / kThr;
     const uint32_t q = (nb + kThr - 1) / kThr, b0 = threadIdx.x * q;
@@ -2479,22 +2488,23 @@ __device__ __forceinline__ void bp_place_cur(const unsigned long long (&x)[kPer]
 #pragma unroll
     for (uint32_t t = 0; t < kQ; ++t)
         if (t < q && b0 + t < nb) {
-            const bool fits = base[t] + c[t] <= cap;
+            const uint32_t cp = cap(b0 + t);
+            const bool fits = base[t] + c[t] <= cp;
             over |= !fits;
-            lh[b0 + t] = region(b0 + t) + (fits ? base[t] : cap) - lh[b0 + t];
+            lh[b0 + t] = region(b0 + t) + (fits ? base[t] : cp) - lh[b0 + t];
         }
     if (over) flags[kFlCur] = 1;
     __syncthreads();
     for (uint32_t i = 2 * threadIdx.x; i < n_in; i += 2 * kThr) {
         const ulonglong2 y = *reinterpret_cast<const ulonglong2*>(S + i);
-        const uint32_t d0 = digit(y.x), a0 = lh[d0] + i, e0 = region(d0) + cap;
+        const uint32_t d0 = digit(y.x), a0 = lh[d0] + i, e0 = region(d0) + cap(d0);
         if (i + 1 < n_in) {
             const uint32_t d1 = digit(y.y), a1 = lh[d1] + i + 1;
             if (d0 == d1 && !(a0 & 1) && a1 < e0) {
                 *reinterpret_cast<ulonglong2*>(out + a0) = y;
             } else {
                 if (a0 < e0) out[a0] = y.x;
-                if (a1 < region(d1) + cap) out[a1] = y.y;
+                if (a1 < region(d1) + cap(d1)) out[a1] = y.y;
             }
         } else if (a0 < e0) {
             out[a0] = y.x;
@@ -2546,7 +2556,27 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scatter2c_kernel(const unsigne
     const uint32_t bb = c * dg.nb2;
     bp_place_cur(
         x, r, tn, dg.nb2, digit, [&](uint32_t d) { return &bcur[bb + d]; },
-        [&](uint32_t d) { return (bb + d) * cg.capb; }, cg.capb, lh, wave_tot, S, out, flags);
+        [&](uint32_t d) { return cg.region(bb + d); }, [&](uint32_t d) { return cg.cap(bb + d); }, lh, wave_tot, S,
+        out, flags);
+}
+
+// learned bucket regions: vreg[b] = Σ_{c < b} cap(c), cap(c) = count(c) + count(c) / 8 + 64 rounded
+// to 16 keys (counts from the cursors of a call whose regions overflowed: they count every key,
+// dropped or not); one workgroup, vreg[nb] = the total
+__global__ __launch_bounds__(1024) void vreg_kernel(const uint32_t* __restrict__ counts, uint32_t nb,
+                                                    uint32_t* __restrict__ vreg) {
+    __shared__ uint32_t wave_tot[1024 / 64];
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < nb; base += 1024) {
+        const uint32_t b = base + threadIdx.x;
+        const uint32_t c = b < nb ? counts[b] : 0u;
+        const uint32_t cap = b < nb ? (c + c / 8 + 64 + 15) / 16 * 16 : 0u;
+        uint32_t excl, total;
+        block_scan_n<1024>(cap, excl, total, wave_tot);
+        if (b < nb) vreg[b] = carry + excl;
+        carry += total;
+    }
+    if (threadIdx.x == 0) vreg[nb] = carry;
 }
 
 __global__ void bp_cur_clear_kernel(uint32_t* __restrict__ cur, uint32_t n) {
@@ -2831,7 +2861,8 @@ __global__ __launch_bounds__(kThr) void bp_scatter2g_kernel(const unsigned long 
     auto digit = [&](unsigned long long y) { return (uint32_t)(y >> dg.sh2) & dg.m2; };
     const uint32_t bb = c * dg.nb2;
     auto cursor = [&](uint32_t d) { return &bcur[bb + d]; };
-    auto region = [&](uint32_t d) { return (bb + d) * cg.capb; };
+    auto region = [&](uint32_t d) { return cg.region(bb + d); };
+    auto capof = [&](uint32_t d) { return cg.cap(bb + d); };
     for (uint32_t base = 0; base < tn; base += kTile) {
         if (base) __syncthreads();  // the previous round's writes have read lh and S
         const uint32_t n_in = min(kTile, tn - base);
@@ -2868,8 +2899,8 @@ __global__ __launch_bounds__(kThr) void bp_scatter2g_kernel(const unsigned long 
 #pragma unroll
         for (uint32_t e = 0; e < kPer; ++e) r[e] = x[e] != kNoKey ? atomicAdd(&lh[digit(x[e])], 1u) : 0u;
         __syncthreads();  // every key loaded: S is free for the placement
-        bp_place_cur<kPer, decltype(digit), decltype(cursor), decltype(region), kThr>(
-            x, r, n_in, dg.nb2, digit, cursor, region, cg.capb, lh, wave_tot, S, out, flags);
+        bp_place_cur<kPer, decltype(digit), decltype(cursor), decltype(region), decltype(capof), kThr>(
+            x, r, n_in, dg.nb2, digit, cursor, region, capof, lh, wave_tot, S, out, flags);
     }
 }
 
@@ -3017,6 +3048,14 @@ struct kmp_postings {
     bool cur_mode = true, cur_on = true, cur_used = false;
     Grow<uint32_t> cur;
     CurGeom cg{};
+    // learned bucket layout of the cursor level 2 (a batch whose frequent k-mers overflow the
+    // hash-uniform regions: the reference's uniprot_arg at k = 5): region starts from the last
+    // call's exact bucket counts with an eighth of headroom; relearned on an overflow, the counting
+    // partition after kVregTries in a row
+    Grow<uint32_t> vreg;
+    bool vreg_on = false;
+    uint64_t vreg_total = 0;
+    uint32_t vreg_tries = 0;
     // heavy path (frequent k-mers): spill regions, the gathered + sorted spill, its elements,
     // k-mer starts, per-k-mer row bounds / tile counts / tile offsets
     Grow<unsigned long long> spill, hkeys, hsorted, hGS, htc, htoff, hoff, hRH, hseg, hcur;
@@ -3207,6 +3246,7 @@ bool cur_geometry(const Layout& lay, CurGeom* cg) {
     const uint64_t capb = (std::max<uint64_t>(2ull * lay.mean_keys + 512, 1536) + 63) / 64 * 64;
     if (nb * capb + capb >= (1ull << 32) - 2 * kBpTile) return false;
     cg->capb = (uint32_t)capb;
+    cg->vreg = nullptr;  // the fixed layout (a residue call may switch to its learned one)
     return true;
 }
 
@@ -3222,7 +3262,7 @@ int bp_level2c(kmp_postings* ws, const Layout& lay, hipStream_t st) {
     const uint32_t nb = 1u << lay.bbits;
     uint32_t* C1 = ws->bp.p + ws->bp_c1;
     PG(ws->cur.reserve(nb));
-    PG(ws->sorted.reserve((uint64_t)nb * ws->cg.capb));
+    PG(ws->sorted.reserve(ws->cg.vreg ? ws->vreg_total : (uint64_t)nb * ws->cg.capb));
     PG(ws->cnt.reserve(2 * (uint64_t)nb + 2));  // the large-bucket list
     uint32_t c0, c1;
     own_bins(ws, dg, &c0, &c1);
@@ -4924,6 +4964,7 @@ BucketArgs bucket_args(kmp_postings* ws, const StepCfg& c, bool spill) {
     if (ws->cur_used) {
         a.bstart = ws->cur.p;  // bucket counts
         a.capb = ws->cg.capb;
+        a.vreg = ws->cg.vreg;
     }
     a.lay = c.lay;
     a.mul = 1u << bits_for(c.n);  // pair key p << pbits | q (the row-block tail's key)
@@ -5492,6 +5533,8 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
         ws->pt_rb_max = 16;
         ws->fast_tail = ws->fast_mode;
         ws->large_grid = kBucketLargeGrid;
+        ws->vreg_on = false;
+        ws->vreg_tries = 0;
         ws->bp_J_min = 0;
         ws->heavy = false;
         ws->cur_on = ws->cur_mode;
@@ -5522,8 +5565,9 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
             key.push_back(ws->cur_on);
             key.push_back(ws->fast_tail);
             key.push_back(ws->large_grid);
+            key.push_back(ws->vreg_on ? ws->vreg_total + 1 : 0);
             int rc = fused_launch(ws, make_keys, key, c, g, st);
-            key.resize(key.size() - 8);
+            key.resize(key.size() - 9);
             if (rc != KMP_OK) return rc;
             PG(hipStreamSynchronize(st));
         } else {
@@ -5539,7 +5583,24 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
         sum_stats(rb, acc, &most, &n_inc, &spill_most, &spill_total);
         bool rerun = false;
         if (rb[kRbFlagCur] && ws->cur_used) {  // a region of the cursor partition overflowed
-            ws->cur_on = false;
+            // learn the layout from this call's exact bucket counts (own bins: all of them here);
+            // the counting partition only if the learned layout keeps overflowing
+            const uint32_t nb = 1u << c.lay.bbits;
+            bool learned = false;
+            if (ws->vreg_tries < kVregTries && ws->vreg.reserve(nb + 1) == hipSuccess) {
+                vreg_kernel<<<1, 1024, 0, st>>>(ws->cur.p, nb, ws->vreg.p);
+                uint32_t tot = 0;
+                if (hipMemcpyAsync(&tot, ws->vreg.p + nb, 4, hipMemcpyDeviceToHost, st) == hipSuccess &&
+                    hipStreamSynchronize(st) == hipSuccess && (uint64_t)tot + 2 * kBpTile < (1ull << 32)) {
+                    ws->vreg_total = tot;
+                    ws->vreg_on = learned = true;
+                    ++ws->vreg_tries;
+                }
+            }
+            if (!learned) {
+                ws->vreg_on = false;
+                ws->cur_on = false;
+            }
             rerun = true;
         }
         if (rb[kRbFlagBin]) {  // a coarse bin above its level-2 tile budget
@@ -5615,6 +5676,7 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
         }
         ws->pt_inc = n_inc;  // sizes the next call's row blocks
         ws->last_fast = pt_fast(ws, g);
+        ws->vreg_tries = 0;  // a call without a region overflow
         {  // the large-bucket grid of the next call: twice the listed buckets, 64 .. kBucketLargeGrid
             uint32_t lg = 64;
             while (lg < kBucketLargeGrid && lg < 2 * rb[kRbList]) lg *= 2;
@@ -6181,6 +6243,7 @@ static int residues_impl(kmp_postings* ws, const uint8_t* d_res, const uint64_t*
         if (lay.bucketed) {
             ws->parted = true;
             ws->cur_used = ws->cur_on && cur_geometry(lay, &ws->cg);
+            ws->cg.vreg = ws->cur_used && ws->vreg_on ? ws->vreg.p : nullptr;
             return bp_level1(ws, d_res, d_res_off, d_class, k, n, slots, lay, st);
         }
         ws->cur_used = false;
