@@ -3566,8 +3566,8 @@ __global__ __launch_bounds__(kPtThreads) void pt_scatter_kernel(const unsigned l
 // reduce sees the count and flags the overflow) — no histogram pass, no scan.  Workgroup (0, 0)
 // also clears the reduce's look-back words lb[0, nrb).  Tiles of 8,192 keys: twice the workgroups
 // of the counting tail's 16,384-key tiles (which ran one per CU), at LDS for two per CU.
-constexpr uint32_t kFtCap = 8192;  // fast tail, hash reduce: keys per row-block region (dense: kFdCap)
-constexpr uint32_t kFdCap = 32768, kFdBitsMax = 15;  // dense reduce: region keys, bins 2^(pbits + rbits)
+constexpr uint32_t kFtCap = 8192;  // fast tail, hash reduce: keys per row-block region
+constexpr uint32_t kFdBitsMax = 15;  // dense reduce: bins 2^(pbits + rbits)
 constexpr uint32_t kFtScThreads = 512, kFtScTile = kFtScThreads * 16;
 __global__ __launch_bounds__(kFtScThreads) void pt_scatter_capped_kernel(const unsigned long long* __restrict__ in,
                                                                          const unsigned long long* __restrict__ cursor,
@@ -4729,17 +4729,19 @@ __global__ __launch_bounds__(kFtThreads) void pt_reduce_fast_kernel(const uint32
 
 
 // The dense variant (small batches: pbits + rbits <= kFdBitsMax, the reference's uniprot_arg.fasta at
-// k = 5 among them, whose rows pair with thousands of later proteins): block r's keys counted in
-// 2^(pbits + rbits) LDS bins over (row, q) — u16 counts, two per word — so the bins ARE the canonical
-// order: no hash, no rank, no sort.  Thread t owns the contiguous words [t q, t q + q) (q = words /
-// kFtThreads); stored XOR-swizzled (word w at w ^ ((w / q) mod min(q, 32))) so the owners' reads of
-// their words hit distinct banks.  Regions of kFdCap keys; a count that would reach 16 bits raises
-// the overflow like a full region (the caller reruns on the counting tail).
+// k = 5 among them, whose rows pair with thousands of later proteins — up to ~10^5 keys in one row:
+// near-identical AMR families): block r's keys counted in 2^(pbits + rbits) LDS bins over (row, q) —
+// u16 counts, two per word — so the bins ARE the canonical order: no hash, no rank, no sort.  Its
+// keys come from the counting partition (bst: block r is [bst[r], bst[r + 1]), any size; a fixed
+// region would overflow on such rows).  Thread t owns the contiguous words [t q, t q + q) (q = words
+// / kFtThreads); stored XOR-swizzled (word w at w ^ ((w / q) mod min(q, 32))) so the owners' reads of
+// their words hit distinct banks.  A count that would reach 16 bits raises the fast tail's overflow
+// (the caller reruns on the counting tail).
 __device__ __forceinline__ uint32_t fd_phys(uint32_t w, unsigned qs) {
     return w ^ ((w >> qs) & ((1u << min(qs, 5u)) - 1));
 }
 __global__ __launch_bounds__(kFtThreads) void pt_reduce_dense_kernel(const uint32_t* __restrict__ keys,
-                                                                     uint32_t* __restrict__ fcur, PtGeom g,
+                                                                     const uint32_t* __restrict__ bst, PtGeom g,
                                                                      unsigned long long* __restrict__ lb,
                                                                      uint32_t* __restrict__ d_p,
                                                                      uint32_t* __restrict__ d_q,
@@ -4751,15 +4753,10 @@ __global__ __launch_bounds__(kFtThreads) void pt_reduce_dense_kernel(const uint3
     __shared__ uint32_t s_flag;
     __shared__ unsigned long long s_excl;
     const uint32_t r = blockIdx.x, tid = threadIdx.x;
-    const uint32_t nraw = fcur[r];
-    __syncthreads();  // every thread has its count before the cursor is cleared for the next call
-    if (tid == 0) {
-        fcur[r] = 0;
-        s_flag = 0;
-    }
-    bool ovf = nraw > g.ftcap;
-    const uint32_t n = ovf ? 0u : nraw;
-    const uint32_t* src = keys + (uint64_t)r * g.ftcap;
+    if (tid == 0) s_flag = 0;
+    bool ovf = false;
+    const uint32_t s0 = bst[r], n = bst[r + 1] - s0;
+    const uint32_t* src = keys + s0;
     const unsigned pb = g.pbits, bits = g.pbits + g.rbits;
     const uint32_t words = 1u << (bits - 1);
     unsigned qs = 0;  // q = words / kFtThreads = 2^qs words per thread (at least one)
@@ -4905,8 +4902,7 @@ bool pt_geometry(const kmp_postings* ws, const StepCfg& c, uint64_t inc, PtGeom*
         if (g->pbits + rd <= kFdBitsMax && est / std::max<uint64_t>(1, nrd) >= 256) {
             g->rbits = rd;
             g->nrb = (uint32_t)std::max<uint64_t>(1, nrd);
-            g->ftcap = kFdCap;
-            g->dense = 1;
+            g->dense = 1;  // on the counting partition (blocks of any size)
         }
     }
     // the bin sort for scored blocks only (unscored at config 3: 0.130 -> 0.387 ms);
@@ -5010,7 +5006,8 @@ int step_reserve(kmp_postings* ws, const StepCfg& c, const PtGeom& g, hipStream_
     PG(ws->inc_sorted.reserve(total));
     if (!c.expand_only) {  // an expand-only call leaves the tail (and its staging) to tail_multi
         // u32 row-block keys (pt_scatter; the fast tail's fixed regions) ...
-        PG(ws->inc.reserve(pt_fast(ws, g) ? std::max<uint64_t>(total, (uint64_t)g.nrb * g.ftcap / 2) : total));
+        PG(ws->inc.reserve(pt_fast(ws, g) && !g.dense ? std::max<uint64_t>(total, (uint64_t)g.nrb * g.ftcap / 2)
+                                                         : total));
         PG(ws->uniq.reserve(total));  // ... staged p | q (u32 each)
         PG(ws->w.reserve(total));     // ... staged w
         if (c.sb) PG(ws->stg2.reserve(2 * total));  // ... staged scores | second-k weights
@@ -5074,20 +5071,33 @@ int enqueue_tail_in(kmp_postings* ws, const StepCfg& c, const PtGeom& g, const u
     hipError_t e = hipSuccess;
     const PtBufs b = pt_bufs(ws, g, false, &e);
     uint32_t* keys32 = reinterpret_cast<uint32_t*>(ws->inc.p);
-    if (pt_fast(ws, g)) {  // capped scatter, then one reduce that writes the edges (marks 4, 5, 6)
-        const uint32_t jt = (uint32_t)(((g.flat_n ? g.flat_n : g.sc) + kFtScTile - 1) / kFtScTile);
-        pt_scatter_capped_kernel<<<dim3(jt, g.nshards), kFtScThreads, 0, st>>>(in, cursor, g, b.fcur, keys32, b.lb);
-        ws->mark(4, st);
-        if (g.dense)
-            pt_reduce_dense_kernel<<<g.nrb, kFtThreads, 0, st>>>(keys32, b.fcur, g, b.lb, c.d_p, c.d_q, c.d_w, c.cap,
+    if (pt_fast(ws, g)) {  // one reduce that writes the edges (marks 4, 5, 6)
+        if (g.dense) {  // the counting partition (blocks of any size), the dense reduce
+            pt_hist_kernel<<<dim3(g.jt, g.nshards), kPtThreads, 0, st>>>(in, cursor, g, b.T);
+            pt_tscan_kernel<<<1, kPtScanThreads, 0, st>>>(b.T, g.nrb, b.bst, b.cur, ws->small.p + 2);
+            pt_scatter_kernel<<<dim3(g.jt, g.nshards), kPtThreads, 0, st>>>(in, cursor, g, b.cur, keys32);
+            ws->mark(4, st);
+            if (g.nrb) {  // the look-back words (the capped scatter clears them otherwise)
+                PG(hipMemsetAsync(b.lb, 0, (size_t)g.nrb * sizeof(unsigned long long), st));
+            }
+            pt_reduce_dense_kernel<<<g.nrb, kFtThreads, 0, st>>>(keys32, b.bst, g, b.lb, c.d_p, c.d_q, c.d_w, c.cap,
                                                                   c.stride,
                                                                   PtPack{ws->bstats.p, ws->flags.p, nullptr, ws->hrb},
                                                                   ws->small.p + 1);
-        else
+            ws->mark(5, st);
+            ws->mark(6, st);
+            PG(hipGetLastError());
+            return KMP_OK;
+        }
+        const uint32_t jt = (uint32_t)(((g.flat_n ? g.flat_n : g.sc) + kFtScTile - 1) / kFtScTile);
+        pt_scatter_capped_kernel<<<dim3(jt, g.nshards), kFtScThreads, 0, st>>>(in, cursor, g, b.fcur, keys32, b.lb);
+        ws->mark(4, st);
+        {
             pt_reduce_fast_kernel<<<g.nrb, kFtThreads, 0, st>>>(keys32, b.fcur, g, b.lb, c.d_p, c.d_q, c.d_w, c.cap,
                                                                  c.stride,
                                                                  PtPack{ws->bstats.p, ws->flags.p, nullptr, ws->hrb},
                                                                  ws->small.p + 1);
+        }
         ws->mark(5, st);
         ws->mark(6, st);
         PG(hipGetLastError());
@@ -6552,7 +6562,7 @@ int kmp_dev_split_edges(kmp_postings* ws, const unsigned long long* d_keys, uint
         hipError_t e = hipSuccess;
         pt_bufs(ws, g, true, &e, st);
         PG(e);
-        PG(ws->inc.reserve(pt_fast(ws, g) ? std::max<uint64_t>(m, (uint64_t)g.nrb * g.ftcap / 2) : m));  // u32 row-block keys
+        PG(ws->inc.reserve(pt_fast(ws, g) && !g.dense ? std::max<uint64_t>(m, (uint64_t)g.nrb * g.ftcap / 2) : m));  // u32 row-block keys
         PG(ws->uniq.reserve(m));  // staged p | q (u32 each)
         PG(ws->w.reserve(m));
         PG(ws->ovf.reserve((uint64_t)g.nrb + 1));
