@@ -89,6 +89,8 @@ def order_xcd(items: np.ndarray) -> np.ndarray:
 
 
 class DevicePipeline:
+    split_edges_syncs = True  # kmp_dev_split_edges synchronises the stream (dist.kmer_split_step relies on it)
+
     def __init__(self, proteins: Proteins, k: int, device: torch.device | str = "cuda",
                  edge_cap: int | None = None):
         self.k = k

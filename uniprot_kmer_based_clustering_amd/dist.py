@@ -54,9 +54,9 @@ def gather_rows(parts: list, count: int, rank: int, world: int, group=None, grow
     them).  Returns the total count on rank 0 and `count` elsewhere."""
     dev = parts[0].device
     cnt = torch.tensor([count], dtype=torch.int64, device=dev)
-    counts = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
-    dist.all_gather(counts, cnt, group=group)
-    counts = [int(c.item()) for c in counts]
+    allc = torch.zeros(world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(allc, cnt, group=group)
+    counts = [int(c) for c in allc.tolist()]  # one read-back, not one per rank
     if rank != 0:
         ops = [dist.P2POp(dist.isend, t[:count], 0, group=group) for t in parts] if count else []
         for w in (dist.batch_isend_irecv(ops) if ops else []):
@@ -103,13 +103,15 @@ def distributed_step(pipe, rank: int, world: int, group=None, min_shared: int = 
 class SplitState:
     """Learned state of the k-mer split, identical on every rank (it only changes from flags
     reduced over the ranks): the per-destination send capacity, the flags to learn from on a
-    rerun, the exchange buffers, and whether the batch needs the row split."""
+    rerun, the exchange buffers, the host copy of the reduced flags, and whether the batch needs
+    the row split."""
 
     def __init__(self, key=None):
         self.key = key  # (n, total residues, k, residue buffer) of the batch it was learned on
         self.cap = 0
         self.learn = None
         self.bufs = None
+        self.host_flags = None  # pinned (CUDA) host copy of the reduced flags, copied asynchronously
         self.row_split = False
         self.reruns = 0
 
@@ -162,12 +164,20 @@ def kmer_split_step(pipe, rank: int, world: int, group=None, min_shared: int = 1
             dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=group)
         else:
             recv = send
+        # the reduced flags go to the host behind the collectives on the same stream; split_edges
+        # synchronises that stream for its edge count, so reading them below waits on nothing more
+        # (no read-back of its own per step)
+        if st.host_flags is None or st.host_flags.numel() != flags.numel():
+            st.host_flags = torch.empty(flags.shape, dtype=flags.dtype, pin_memory=dev.type == "cuda")
+        st.host_flags.copy_(flags, non_blocking=dev.type == "cuda")
         if ev:
             ev[2].record()
         m = pipe.split_edges(recv, lo, hi, min_shared)
         if ev:
             ev[3].record()
-        fl = [int(x) for x in flags.cpu().tolist()]  # the step's one flag read-back
+        if dev.type == "cuda" and not hasattr(pipe, "split_edges_syncs"):
+            torch.cuda.current_stream().synchronize()  # a stand-in stage that does not synchronise
+        fl = [int(x) for x in st.host_flags.tolist()]
         if fl[_lib.KMP_SPLIT_CLASS]:
             st.row_split = True
             return distributed_step(pipe, rank, world, group, min_shared, require_class_diff)
