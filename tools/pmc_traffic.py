@@ -50,10 +50,16 @@ def main():
               f"{r['write_bytes']/1e6:>9.1f}")
     # per-step traffic of the residue step's stages (bench.py STAGE_NAMES["rows"]); one
     # level-1 scatter dispatch per step
-    calls = max([r["dispatches"] for r in rows if r["kernel"].split("<")[0] in ("bp_scatter1_kernel", "bp_scatter1l_kernel")] or [1])
+    calls = max([r["dispatches"] for r in rows if r["kernel"].split("<")[0] in
+                 ("bp_scatter1_kernel", "bp_scatter1l_kernel", "bp_scatter1p_kernel")] or [1])
+    # the fast tail (round 4): the capped scatter is the pair partition, the reduce writes the edges
+    # (its emit share is in pair_sort_rle); the counting tail as before
     by_kernel = {
         "chunk_first_kernel": "keys_level1", "bp_hist1_kernel": "keys_level1", "bp_colscan_kernel": "keys_level1",
         "bp_scatter1_kernel": "keys_level1", "bp_scatter1l_kernel": "keys_level1", "bp_h1t_kernel": "keys_level1",
+        "chunk_desc_kernel": "keys_level1", "bp_scatter1p_kernel": "keys_level1",
+        "pt_scatter_capped_kernel": "pair_partition", "pt_reduce_fast_kernel": "pair_sort_rle",
+        "pt_reduce_dense_kernel": "pair_sort_rle",
         "bp_scatter2g_kernel": "buckets_level2", "bp_colsum_kernel": "keys_level1", "bp_colprefix_kernel": "keys_level1",
         "bp_hist2_kernel": "buckets_level2", "bp_scan2_kernel": "buckets_level2",
         "bp_scatter2_kernel": "buckets_level2", "bp_scatter2c_kernel": "buckets_level2",
