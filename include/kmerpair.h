@@ -209,6 +209,13 @@ int kmp_edges_get(const kmp_edges* e, uint32_t* p, uint32_t* q, uint32_t* w, flo
  * rows).  keys = 0 (default): from the free device memory.  kmp_ctx_last_passes: passes of the
  * last call. */
 int kmp_ctx_set_pass_keys(kmp_ctx* ctx, uint64_t keys);
+/* kmp_ctx_set_direct_tail: kmp_pairs_stream's fused multi-k reduction writes each pass's edges in
+ * place (default 1; kmp_postings_set_direct) or (0) stages them and emits after a scan. */
+int kmp_ctx_set_direct_tail(kmp_ctx* ctx, int enable);
+/* Sub-blocks of the last kmp_pairs_stream that the in-place reduce took in windows of pair positions
+ * (above its LDS sort capacity: a row pairing many times with few partners); staged: the ones the
+ * overflow sort finished. */
+uint64_t kmp_ctx_last_tail_windows(const kmp_ctx* ctx);
 uint32_t kmp_ctx_last_passes(const kmp_ctx* ctx);
 #define KMP_MULTI_K_MAX 4
 int kmp_pairs_multi_k(kmp_ctx* ctx, const kmp_pair_opts* opts, const int* ks, uint32_t nk, kmp_edges** out);
@@ -453,6 +460,10 @@ int kmp_postings_last_tail(const kmp_postings* ws);
 /* kmp_postings_set_tail: KMP_TAIL_FAST (default: the fast tail where it applies) or KMP_TAIL_COUNT
  * (the counting tail only).  Same edges either way. */
 int kmp_postings_set_tail(kmp_postings* ws, int mode);
+/* kmp_postings_set_direct: the fused multi-k tail (kmp_dev_pairs_rows_multi, kmp_pairs_stream)
+ * writes its edges in place from the sub-block reduce, at offsets from a decoupled look-back
+ * (default 1), or (0) stages its runs and emits them after a scan.  Same edges either way. */
+int kmp_postings_set_direct(kmp_postings* ws, int enable);
 /* The bucketed step as a HIP graph (default 1): captured on the second call with an unchanged
  * shape (pointers, sizes, options, workspace buffers), replayed after that.
  * kmp_postings_graph_replays: calls served by a replay so far. */

@@ -43,6 +43,11 @@ class HostBounce:
         self.d.all_reduce(h, op=op or self.d.ReduceOp.SUM)
         t.copy_(h)
 
+    def all_gather_into_tensor(self, out, t, group=None):
+        h = torch.empty(out.shape, dtype=out.dtype)
+        self.d.all_gather_into_tensor(h, t.cpu())
+        out.copy_(h)
+
     def all_gather(self, outs, t, group=None):
         hs = [torch.empty(o.shape, dtype=o.dtype) for o in outs]
         self.d.all_gather(hs, t.cpu())
@@ -94,6 +99,9 @@ def worker(rank, world, port, out_q):
             if rank == 0:
                 out_q.put(("heavy", n == g["n_edges"] and edges_sha256(*pipe5.edges()) == g["edges_sha256"],
                            state5.row_split, state5.reruns))
+    except BaseException as e:  # the test fails at once instead of waiting out its queue
+        out_q.put(("error", rank, repr(e)))
+        raise
     finally:
         dist.destroy_process_group()
 
@@ -106,7 +114,10 @@ def test_kmer_split_step_device_stages(world):
     procs = [ctx.Process(target=worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    msgs = [q.get(timeout=200) for _ in range(4)]
+    msgs = []
+    while len(msgs) < 4:
+        msgs.append(q.get(timeout=150))
+        assert msgs[-1][0] != "error", msgs[-1]
     for p in procs:
         p.join(timeout=60)
     assert all(p.exitcode == 0 for p in procs)

@@ -79,17 +79,20 @@ def test_scored_heavy_path_uniprot_k5(oracle_mod):
         np.testing.assert_array_equal(got.score, want.astype(np.float32))
 
 
+@pytest.mark.parametrize("direct", [True, False])
 @pytest.mark.parametrize("ks", [(5,), (5, 7)])
-def test_stream_host_chunks_concatenate(oracle_mod, ks):
+def test_stream_host_chunks_concatenate(oracle_mod, ks, direct):
     """kmp_pairs_stream with a host sink: the chunks (consecutive row ranges, each canonical)
     concatenate to the oracle's union edge list (w, score, every w_k), and the summary equals the
-    oracle's digest and counters."""
+    oracle's digest and counters.  direct: the fused reduction writes each pass's edges in place
+    (pt_reduce_direct_kernel), else it stages them and emits after a scan."""
     b = K.synth(30000, 5, 1)
     orcs = [oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=k, threads=16) for k in ks]
     want, (p, q, w, s, wk) = oracle_mod.stream(orcs, collect=True, threads=16)
     chunks = []
     with K.KmerPairEngine(0, 8) as e:
         e.load(b)
+        e.set_direct_tail(direct)
         e.set_pass_keys(1 << 21)
         sm = e.pairs_stream(ks, score=BLOSUM, sink=chunks.append)
     assert sm["passes"] == len(chunks) > 1
@@ -105,19 +108,60 @@ def test_stream_host_chunks_concatenate(oracle_mod, ks):
     assert_summary(sm, want)
 
 
-def test_stream_count_and_filters(oracle_mod):
+@pytest.mark.parametrize("direct", [True, False])
+def test_stream_count_and_filters(oracle_mod, direct):
     """COUNT score (score = w), min_shared = 3 (kept when either k reaches it) and the class filter
-    off, streamed over passes: summary equal to the oracle's."""
+    off, streamed over passes: summary equal to the oracle's (in-place and staged reduction)."""
     b = K.synth(15000, 5, 1)
     orcs = [oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=k, threads=16) for k in (5, 7)]
     with K.KmerPairEngine(0, 8) as e:
         e.load(b)
+        e.set_direct_tail(direct)
         e.set_pass_keys(1 << 20)
         for kw in ({"min_shared": 3}, {"require_class_diff": False}, {}):
             want = oracle_mod.stream(orcs, blosum=False, threads=16, **kw)
             sm = e.pairs_stream((5, 7), score=_lib.KMP_SCORE_COUNT, **kw)
             assert_summary(sm, want)
             assert sm["sum_score"] == sm["sum_w"]
+
+
+@pytest.mark.parametrize("direct", [True, False])
+def test_stream_dense_pairs_windows(oracle_mod, direct):
+    """Rows that pair many times with few partners: four copies of one 3,000-residue protein (rows
+    0, 1, 9,000 and 19,000, four classes) in 20,000 synthetic ones, k = 5 + 7 — pairs of ~6,000
+    shared k-mers, so the row blocks of rows 0 and 1 hold fine bins far above the reduce's LDS sort
+    capacity: the in-place reduce takes them in windows of pair positions (the staged one, the
+    overflow sort).  Every edge, score and w_k equal to the oracle's."""
+    base = K.synth(20000, 5, 1)
+    rng = np.random.default_rng(77)
+    dup = rng.integers(0, 20, 3000).astype(np.uint8)
+    lens = np.diff(base.offsets.astype(np.int64))
+    seqs = [base.residues[base.offsets[i]:base.offsets[i + 1]] for i in range(base.n)]
+    cls = base.class_id.astype(np.uint16).copy()
+    for j, row in enumerate((0, 1, 9000, 19000)):
+        seqs[row] = dup
+        cls[row] = j + 1
+    lens = np.array([len(x) for x in seqs], np.int64)
+    off = np.zeros(len(seqs) + 1, np.uint64)
+    off[1:] = np.cumsum(lens)
+    b = K.Proteins(np.concatenate(seqs).astype(np.uint8), off, cls)
+    orcs = [oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=k, threads=16) for k in (5, 7)]
+    want, (p, q, w, s, wk) = oracle_mod.stream(orcs, collect=True, threads=16)
+    assert w.max() > 5000
+    chunks = []
+    with K.KmerPairEngine(0, 8) as e:
+        e.load(b)
+        e.set_direct_tail(direct)
+        sm = e.pairs_stream((5, 7), score=BLOSUM, sink=chunks.append)
+        assert e.last_tail_windows >= 2
+    cat = {key: np.concatenate([c[key] for c in chunks]) for key in ("p", "q", "w", "score")}
+    np.testing.assert_array_equal(cat["p"], p)
+    np.testing.assert_array_equal(cat["q"], q)
+    np.testing.assert_array_equal(cat["w"], w)
+    np.testing.assert_array_equal(cat["score"], s)
+    for j in range(2):
+        np.testing.assert_array_equal(np.concatenate([c["wk"][j] for c in chunks]), wk[j])
+    assert_summary(sm, want)
 
 
 def test_stream_device_sink_100k(oracle_mod):

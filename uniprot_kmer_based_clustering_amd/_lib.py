@@ -163,6 +163,9 @@ SIGNATURES = {
     "kmp_ctx_create_multi": (C.c_int, [C.POINTER(P), C.c_int, C.POINTER(C.c_int), C.c_int]),
     "kmp_ctx_gpus": (C.c_int, [P]),
     "kmp_ctx_set_pass_keys": (C.c_int, [P, C.c_uint64]),
+    "kmp_ctx_set_direct_tail": (C.c_int, [P, C.c_int]),
+    "kmp_ctx_last_tail_windows": (C.c_uint64, [P]),
+    "kmp_postings_set_direct": (C.c_int, [P, C.c_int]),
     "kmp_ctx_last_passes": (C.c_uint32, [P]),
     "kmp_ctx_transport": (C.c_char_p, [P]),
     "kmp_ctx_last_split": (C.c_char_p, [P]),

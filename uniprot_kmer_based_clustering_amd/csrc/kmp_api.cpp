@@ -157,6 +157,8 @@ struct kmp_ctx {
     // last kmp_pairs / kmp_pairs_multi_k
     uint64_t pass_keys = 0;
     uint32_t last_passes = 0;
+    int direct_tail = 1;  // kmp_ctx_set_direct_tail: the fused tail writes its edges in place
+    uint64_t last_windows = 0;  // kmp_ctx_last_tail_windows
     // kmp_ctx_set_rows: the rows kmp_pairs_stream covers ([0, 0): all) — a process's share of a
     // multi-process split (one process per GPU)
     uint32_t rows_lo = 0, rows_hi = 0;
@@ -1263,6 +1265,7 @@ struct StreamLane {
     uint64_t incidences = 0;
     uint32_t passes = 0;
     float stage_ms[4] = {0, 0, 0, 0};  // kmp_stream_summary.stage_ms
+    uint64_t windows = 0;              // sub-blocks the in-place reduce took in windows
 };
 
 // two HIP events around the summary kernel of a pass (lane-local, created on first use)
@@ -1293,6 +1296,7 @@ static int stream_passes(kmp_ctx* c, const kmp_pair_opts& o, const int* ks, uint
         if (!kv[j]->ws) KMP_TRY(c, kmp_postings_create(&kv[j]->ws));
         KMP_TRY(c, kmp_postings_set_reuse(kv[j]->ws, 1));
         KMP_TRY(c, kmp_postings_set_timing(kv[j]->ws, 1));  // stage times of the summary
+        KMP_TRY(c, kmp_postings_set_direct(kv[j]->ws, c->direct_tail));
     }
     EventPair dev;
     if (!dev.ready()) return fail(c, KMP_EDEVICE, "events");
@@ -1368,6 +1372,7 @@ static int stream_passes(kmp_ctx* c, const kmp_pair_opts& o, const int* ks, uint
             }
             if (rc == KMP_OK && total > mcap) rc = fail(c, KMP_EDEVICE, "rows [%u, %u): edge count unstable", a, b);
             if (rc != KMP_OK) break;
+            ln.windows += kmp_postings_last_overflow_blocks(kv[0]->ws);
             ch.n = total;
             ch.p = ln.ep->as<uint32_t>();
             ch.q = ln.eq->as<uint32_t>();
@@ -1522,6 +1527,7 @@ static int finish_summary(kmp_ctx* c, const kmp_pair_opts& o, const std::vector<
                           kmp_stream_summary* out) {
     kmp_stream_summary sm{};
     bool bad = false;
+    uint64_t windows = 0;
     for (StreamLane* ln : lanes) {
         kmp::DigestAcc h{};
         KMP_HIP(c, hipSetDevice(ln->device));
@@ -1540,8 +1546,10 @@ static int finish_summary(kmp_ctx* c, const kmp_pair_opts& o, const std::vector<
         sm.incidences += ln->incidences;
         sm.passes += ln->passes;
         for (int i = 0; i < 4; ++i) sm.stage_ms[i] += ln->stage_ms[i];
+        windows += ln->windows;
         bad |= h.bad != 0;
     }
+    c->last_windows = windows;
     KMP_TRY(c, use_device(c));
     // Σ w over class-differing pairs: every edge when the class filter is on
     if (o.require_class_diff) sm.sum_w_diff = sm.sum_w;
@@ -1785,6 +1793,14 @@ int kmp_ctx_set_pass_keys(kmp_ctx* c, uint64_t keys) {
 }
 
 uint32_t kmp_ctx_last_passes(const kmp_ctx* c) { return c ? c->last_passes : 0u; }
+
+uint64_t kmp_ctx_last_tail_windows(const kmp_ctx* c) { return c ? c->last_windows : 0u; }
+
+int kmp_ctx_set_direct_tail(kmp_ctx* c, int enable) {
+    if (!c) return KMP_EINVAL;
+    c->direct_tail = enable ? 1 : 0;
+    return KMP_OK;
+}
 
 int kmp_edges_get_wk(const kmp_edges* e, uint32_t j, uint32_t* wk, uint64_t cap, uint64_t* n) {
     if (!e || !n) return KMP_EINVAL;

@@ -2952,6 +2952,25 @@ __global__ void keep_flags_kernel(const uint32_t* __restrict__ w, const uint32_t
 // thread each at the same time (kmp_api.cpp split_rank_edges / rows_rank_edges)
 std::atomic<unsigned long long> g_grow_gen{0};
 
+// the row-block tail's geometry (pt_geometry)
+struct PtGeom {
+    unsigned pbits, rbits;  // key = p << pbits | q; rows per block = 1 << rbits
+    unsigned sbits;         // scored: the score field below the pair ((pair << sbits) | field), else 0
+    int kbit;               // scored multi-k: bit kScoreBits of the field marks the second k (w1 counted)
+    uint32_t nrb;           // row blocks, from row row0
+    uint32_t jt;            // tiles per shard region
+    uint64_t sc;            // shard region capacity
+    uint32_t nshards;       // shard regions (kShards), or 1 for a flat array
+    uint32_t row0;          // first row (a pass's or rank's row range)
+    uint64_t flat_n;        // nonzero: one region of flat_n keys with kNoKey padding (no cursors)
+    uint32_t min_shared;    // runs with w < min_shared are dropped
+    uint32_t nprot;         // proteins (q < nprot): the pair range of a row block (pt_bin_sort)
+    uint32_t rowend;        // the call's last row + 1
+    int binsort;            // the reduce sorts by bins (pt_bin_sort), else the block radix sort
+    uint32_t ftcap;         // fast tail: keys per row-block region
+    int dense;              // fast tail: per-block dense histogram over (row, q) (2^(pbits + rbits) bins)
+};
+
 template <class T>
 struct Grow {
     T* p = nullptr;
@@ -3017,6 +3036,11 @@ struct kmp_postings {
     uint32_t pend_nd = 0;
     uint64_t pend_total = 0, pend_ne = 0;
     std::vector<unsigned long long> pend_key;
+    // the fused tail writes its edges in place (pt_reduce_direct_kernel); 0: staged runs + emit
+    int direct_tail = 1;
+    bool pend_direct = false;  // the pending re-emit reruns the in-place reduce (its keys still held)
+    PtGeom pend_g{};
+    Grow<unsigned long long> dlb;  // its look-back words (one per sub-block) | the pass's edge count
     Grow<unsigned long long> split_cur;  // k-mer split: per-destination send cursors
     std::vector<unsigned long long> split_shape;
     bool split_heavy = false;  // k-mer split: this batch spills, its heavy path runs on every call
@@ -3387,41 +3411,32 @@ constexpr uint32_t kPtThreads = 1024, kPtPer = KMP_PT_PER, kPtTile = kPtThreads 
 constexpr uint32_t kPtRThreads = 512, kPtCap = 8192;  // pt_reduce: up to 16 keys per thread
 constexpr uint32_t kPtMaxBlocks = 8192;  // row blocks (LDS histogram of pt_hist / pt_scatter)
 
-struct PtGeom {
-    unsigned pbits, rbits;  // key = p << pbits | q; rows per block = 1 << rbits
-    unsigned sbits;         // scored: the score field below the pair ((pair << sbits) | field), else 0
-    int kbit;               // scored multi-k: bit kScoreBits of the field marks the second k (w1 counted)
-    uint32_t nrb;           // row blocks, from row row0
-    uint32_t jt;            // tiles per shard region
-    uint64_t sc;            // shard region capacity
-    uint32_t nshards;       // shard regions (kShards), or 1 for a flat array
-    uint32_t row0;          // first row (a pass's or rank's row range)
-    uint64_t flat_n;        // nonzero: one region of flat_n keys with kNoKey padding (no cursors)
-    uint32_t min_shared;    // runs with w < min_shared are dropped
-    uint32_t nprot;         // proteins (q < nprot): the pair range of a row block (pt_bin_sort)
-    uint32_t rowend;        // the call's last row + 1
-    int binsort;            // the reduce sorts by bins (pt_bin_sort), else the block radix sort
-    uint32_t ftcap;         // fast tail: keys per row-block region
-    int dense;              // fast tail: per-block dense histogram over (row, q) (2^(pbits + rbits) bins)
-};
 
 // The blocks a reduce runs over: row blocks (size == nullptr: block r is keys [start[r], start[r+1])
 // of row block r) or sub-blocks (block d is keys [start[d], start[d] + size[d]) of row block row[d]:
 // a row block above kPtCap cut by pt_split).
+// A sub-block whose size has bit 31 set is a whole row block that fitted: its keys are read in place
+// from whole (the row-block keys), not from the cut keys.
 struct BlkSrc {
     const uint32_t* start;
     const uint32_t* size;
     const uint32_t* row;
+    const uint32_t* whole;
 };
+constexpr uint32_t kBlkWhole = 0x80000000u;
 __device__ __forceinline__ void blk_of(const BlkSrc& b, uint32_t i, uint32_t& s0, uint32_t& n, uint32_t& r) {
     s0 = b.start[i];
     if (b.size) {
-        n = b.size[i];
+        n = b.size[i] & ~kBlkWhole;
         r = b.row[i];
     } else {
         n = b.start[i + 1] - s0;
         r = i;
     }
+}
+// the keys block i reads (keys: the cut keys)
+__device__ __forceinline__ const uint32_t* blk_keys(const BlkSrc& b, uint32_t i, const uint32_t* keys) {
+    return b.size && (b.size[i] & kBlkWhole) ? b.whole : keys;
 }
 
 __device__ __forceinline__ uint32_t pt_tile_keys(const unsigned long long* __restrict__ cursor, const PtGeom& g,
@@ -4020,8 +4035,9 @@ __global__ __launch_bounds__(kPtRThreads) void pt_reduce_scored_kernel(const uin
         }
         return;
     }
+    const uint32_t* kp = blk_keys(bs, d, keys);
 #define PT_SCORED(E, S) \
-    pt_reduce_scored_block<E, kKbit>(u, u.S, last, wave_tot, keys, r, d, s0, n, g, stage_p, stage_q, stage_w, stage_s, \
+    pt_reduce_scored_block<E, kKbit>(u, u.S, last, wave_tot, kp, r, d, s0, n, g, stage_p, stage_q, stage_w, stage_s, \
                                      stage_w1, counts)
     if (n <= 2 * kPtRThreads) PT_SCORED(2, s2);
     else if (n <= 4 * kPtRThreads) PT_SCORED(4, s4);
@@ -4197,11 +4213,10 @@ __global__ __launch_bounds__(kSbThreads) void pt_split_kernel(const uint32_t* __
     const uint32_t r = blockIdx.x, s0 = bst[r], n = bst[r + 1] - s0;
     const unsigned lj = pt_sub_log(n);
     const uint32_t nf = 1u << lj, d0 = dbase[r];
-    if (lj == 0) {  // fits: one sub-block (the keys copied, so every sub-block reads keys2)
-        for (uint32_t i = threadIdx.x; i < n; i += kSbThreads) keys2[s0 + i] = keys[s0 + i];
+    if (lj == 0) {  // fits: one sub-block, read in place (kBlkWhole)
         if (threadIdx.x == 0) {
             dstart[d0] = s0;
-            dsize[d0] = n;
+            dsize[d0] = n | kBlkWhole;
             drow[d0] = r;
         }
         return;
@@ -4823,6 +4838,314 @@ __global__ __launch_bounds__(kFtThreads) void pt_reduce_dense_kernel(const uint3
         __syncthreads();
         if (pack.rb) step_pack_body(pack.gstats, pack.flags, runs, pack.rb, any_ovf ? 1ull : 0ull);
     }
+}
+
+// The fused multi-k tail with its edges written in place (no staging, no offsets scan, no emit
+// kernel): one workgroup per sub-block, in canonical order, reduces its keys like
+// pt_reduce_scored_block and takes its output offset from a decoupled look-back over the
+// sub-blocks before it (ft_lookback), then writes (p, q, w, score, w0, w1) coalesced, one run per
+// thread: the runs' first ranks (| k-bit scan << 16) and pair keys sit in LDS (H, P), then P is
+// overwritten with the score scan at the heads for the score column.  A sub-block above kPtCap
+// (a fine bin of pt_split above kPtCap - kSbChunk keys: a row pairing many times with a few
+// partners) is reduced in place in windows of kDwWin pair positions — per position a count
+// (| w1 << 16) and a score sum in LDS, the windows visiting only occupied positions, twice: the
+// kept count first (the look-back needs it), then the writes — so no block leaves the kernel and no
+// device sort runs.  The last block writes the pass's edge count to *total.
+constexpr uint32_t kDwWin = 8192;
+struct PtDirectOut {
+    uint32_t *d_p, *d_q, *d_w, *d_s, *d_w0, *d_w1;
+    uint64_t cap;
+    uint32_t stride;
+};
+struct PtDirectLds {
+    union {
+        typename PtSort<2>::storage_type s2;
+        typename PtSort<4>::storage_type s4;
+        typename PtSort<8>::storage_type s8;
+        typename PtSort<16>::storage_type s16;
+        PtBinLds b;
+        struct {
+            uint32_t H[kPtCap + 1];  // each run's first rank | k-bit scan at it << 16
+            uint32_t P[kPtCap + 1];  // each run's pair key, then the score scan at its head
+        } r;
+        struct {
+            uint32_t A[kDwWin];  // count | w1 << 16 per pair position of the window
+            uint32_t S[kDwWin];  // score sum
+        } w;
+    };
+    uint32_t last[kPtRThreads];
+    uint32_t wave_tot[kPtRThreads / 64];
+    unsigned long long s_excl, s_next;
+};
+
+__device__ __forceinline__ bool pt_keep(uint32_t w, uint32_t w1, bool kbit, uint32_t ms) {
+    return w != 0 && (kbit ? (w - w1 >= ms || w1 >= ms) : w >= ms);
+}
+
+__device__ __forceinline__ void pt_direct_write(const PtDirectOut& o, uint64_t at, uint32_t p, uint32_t q, uint32_t w,
+                                                uint32_t s, uint32_t w1, bool kbit) {
+    if (at >= o.cap) return;
+    const uint64_t x = at * o.stride;
+    o.d_p[x] = p;
+    o.d_q[x] = q;
+    o.d_w[x] = w;
+    o.d_s[x] = s;
+    if (kbit) {
+        o.d_w1[x] = w1;
+        o.d_w0[x] = w - w1;
+    }
+}
+
+template <uint32_t kE, bool kKbit>
+__device__ __forceinline__ void pt_direct_block(PtDirectLds& L, typename PtSort<kE>::storage_type& st,
+                                                const uint32_t* __restrict__ src, uint32_t s0, uint32_t n, uint32_t r,
+                                                uint32_t d, const PtGeom& g, unsigned long long* __restrict__ lb,
+                                                const PtDirectOut& out, unsigned long long& agg_out) {
+    uint32_t k[kE];
+#pragma unroll
+    for (uint32_t e = 0; e < kE; ++e) {
+        const uint32_t i = threadIdx.x + e * kPtRThreads;
+        k[e] = i < n ? src[s0 + i] : 0xFFFFFFFFu;
+    }
+    const unsigned sb = g.sbits;
+    const uint32_t rowbase = g.row0 + (r << g.rbits);
+    if (!g.binsort || !pt_bin_sort<kE>(k, n, g, rowbase, L.b, L.last, L.last + 2 * kPtRThreads / 64, L.wave_tot))
+        PtSort<kE>().sort(k, st, 0, g.pbits + sb + g.rbits + 1);  // blocked: thread t holds ranks t*kE + e
+    L.last[threadIdx.x] = k[kE - 1] >> sb;
+    __syncthreads();
+    const uint32_t rank0 = threadIdx.x * kE, smask = (1u << kScoreBits) - 1;
+    uint32_t prev = threadIdx.x ? L.last[threadIdx.x - 1] : 0u, nh = 0, ssum = 0, ksum = 0;
+    uint32_t hm = 0;  // head bits
+#pragma unroll
+    for (uint32_t e = 0; e < kE; ++e) {
+        const uint32_t rank = rank0 + e, pk = k[e] >> sb;
+        const bool h = rank < n && (rank == 0 || pk != prev);
+        hm |= (uint32_t)h << e;
+        prev = pk;
+        nh += h;
+        if (rank < n) {
+            ssum += k[e] & smask;
+            if (kKbit) ksum += (k[e] >> kScoreBits) & 1u;
+        }
+    }
+    uint32_t base0, nruns, sx0, stot, kx = 0, ktot = 0;
+    block_scan_n<kPtRThreads>(nh, base0, nruns, L.wave_tot);  // barriers: the sort storage is dead
+    block_scan_n<kPtRThreads>(ssum, sx0, stot, L.wave_tot);
+    if (kKbit) block_scan_n<kPtRThreads>(ksum, kx, ktot, L.wave_tot);
+    {
+        uint32_t base = base0;
+#pragma unroll
+        for (uint32_t e = 0; e < kE; ++e) {
+            if (hm >> e & 1u) {
+                L.r.H[base] = (rank0 + e) | (kKbit ? kx << 16 : 0u);
+                L.r.P[base] = k[e] >> sb;
+                ++base;
+            }
+            if (kKbit && rank0 + e < n) kx += (k[e] >> kScoreBits) & 1u;
+        }
+    }
+    if (threadIdx.x == 0) L.r.H[nruns] = n | (kKbit ? ktot << 16 : 0u);
+    __syncthreads();
+    const bool filter = g.min_shared > 1;
+    auto run_w = [&](uint32_t i, uint32_t& w, uint32_t& w1) {
+        const uint32_t h0 = L.r.H[i], h1 = L.r.H[i + 1];
+        w = (h1 & 0xFFFFu) - (h0 & 0xFFFFu);
+        w1 = kKbit ? (h1 >> 16) - (h0 >> 16) : 0u;
+    };
+    uint32_t total = nruns;
+    if (filter) {
+        uint32_t kept = 0;
+        for (uint32_t i = threadIdx.x; i < nruns; i += kPtRThreads) {
+            uint32_t w, w1;
+            run_w(i, w, w1);
+            kept += pt_keep(w, w1, kKbit, g.min_shared);
+        }
+        uint32_t ex;
+        block_scan_n<kPtRThreads>(kept, ex, total, L.wave_tot);
+    }
+    if (threadIdx.x < 64) {
+        const unsigned long long ex = ft_lookback(lb, d, total);
+        if (threadIdx.x == 0) L.s_excl = ex;
+    }
+    __syncthreads();
+    const uint64_t ex = (uint32_t)L.s_excl;
+    agg_out = L.s_excl + total;
+    const uint32_t qm = (1u << g.pbits) - 1;
+    // rounds of kPtRThreads runs, thread t the round's run t; filter: the kept runs compacted
+    // (a block scan per round — uniform trip count)
+    auto rounds = [&](auto&& body) {
+        uint32_t o = 0;
+        for (uint32_t i0 = 0; i0 < nruns; i0 += kPtRThreads) {
+            const uint32_t i = i0 + threadIdx.x;
+            uint32_t w = 0, w1 = 0;
+            if (i < nruns) run_w(i, w, w1);
+            const bool keep = i < nruns && pt_keep(w, w1, kKbit, g.min_shared);
+            uint32_t at = i, rt = 0;
+            if (filter) {
+                uint32_t e;
+                block_scan_n<kPtRThreads>(keep ? 1u : 0u, e, rt, L.wave_tot);
+                at = o + e;
+                o += rt;
+            }
+            if (keep) body(i, ex + at, w, w1);
+        }
+    };
+    rounds([&](uint32_t i, uint64_t at, uint32_t w, uint32_t w1) {
+        const uint32_t pk = L.r.P[i];
+        if (at >= out.cap) return;
+        const uint64_t x = at * out.stride;
+        out.d_p[x] = rowbase + (pk >> g.pbits);
+        out.d_q[x] = pk & qm;
+        out.d_w[x] = w;
+        if (kKbit) {
+            out.d_w1[x] = w1;
+            out.d_w0[x] = w - w1;
+        }
+    });
+    __syncthreads();  // P read: it takes the score scan
+    {
+        uint32_t base = base0, sx = sx0;
+#pragma unroll
+        for (uint32_t e = 0; e < kE; ++e) {
+            if (hm >> e & 1u) L.r.P[base++] = sx;
+            if (rank0 + e < n) sx += k[e] & smask;
+        }
+    }
+    if (threadIdx.x == 0) L.r.P[nruns] = stot;
+    __syncthreads();
+    rounds([&](uint32_t i, uint64_t at, uint32_t, uint32_t) {
+        if (at < out.cap) out.d_s[at * out.stride] = L.r.P[i + 1] - L.r.P[i];
+    });
+}
+
+// a sub-block above kPtCap: windows of kDwWin pair positions (the monotone position of pt_bin_sort)
+template <bool kKbit>
+__device__ void pt_direct_windows(PtDirectLds& L, const uint32_t* __restrict__ src, uint32_t s0, uint32_t n,
+                                  uint32_t r, uint32_t d, const PtGeom& g, unsigned long long* __restrict__ lb,
+                                  const PtDirectOut& out, unsigned long long& agg_out) {
+    constexpr uint32_t kPer = kDwWin / kPtRThreads;
+    const unsigned sb = g.sbits, rs = g.pbits + g.sbits;
+    const uint32_t rowbase = g.row0 + (r << g.rbits), qm = (1u << g.pbits) - 1, qlo = rowbase + 1;
+    const uint64_t span = g.nprot > qlo ? g.nprot - qlo : 1u;
+    const uint32_t smask = (1u << kScoreBits) - 1;
+    auto pos = [&](uint32_t x) -> uint64_t {
+        const uint32_t q = (x >> sb) & qm;
+        return (uint64_t)(x >> rs) * span + (q > qlo ? q - qlo : 0u);
+    };
+    auto wave_min64 = [](unsigned long long v) {
+        for (int off = 32; off > 0; off >>= 1) v = min(v, (unsigned long long)__shfl_xor(v, off));
+        return v;
+    };
+    // the first occupied position
+    unsigned long long mn = ~0ull;
+    for (uint32_t i = threadIdx.x; i < n; i += kPtRThreads) mn = min(mn, (unsigned long long)pos(src[s0 + i]));
+    if (threadIdx.x == 0) L.s_next = ~0ull;
+    __syncthreads();
+    mn = wave_min64(mn);
+    if ((threadIdx.x & 63) == 0) atomicMin(&L.s_next, mn);
+    __syncthreads();
+    const unsigned long long first = L.s_next;
+    uint64_t ex = 0;
+    uint32_t total = 0;
+    for (int pass = 0; pass < 2; ++pass) {  // 0: the kept count; 1: the writes
+        if (pass == 1) {
+            if (threadIdx.x < 64) {
+                const unsigned long long e = ft_lookback(lb, d, total);
+                if (threadIdx.x == 0) L.s_excl = e;
+            }
+            __syncthreads();
+            ex = (uint32_t)L.s_excl;
+            agg_out = L.s_excl + total;
+        }
+        uint64_t o = 0;
+        unsigned long long wlo = first;
+        while (wlo != ~0ull) {  // uniform
+            __syncthreads();  // the previous window's reads are done
+            for (uint32_t i = threadIdx.x; i < kDwWin; i += kPtRThreads) {
+                L.w.A[i] = 0;
+                L.w.S[i] = 0;
+            }
+            if (threadIdx.x == 0) L.s_next = ~0ull;
+            __syncthreads();
+            unsigned long long nx = ~0ull;
+            for (uint32_t i0 = 0; i0 < n; i0 += 8 * kPtRThreads) {  // loads in batches ahead of the atomics
+                uint32_t v[8];
+#pragma unroll
+                for (uint32_t e = 0; e < 8; ++e) {
+                    const uint32_t i = i0 + e * kPtRThreads + threadIdx.x;
+                    v[e] = i < n ? src[s0 + i] : 0xFFFFFFFFu;
+                }
+#pragma unroll
+                for (uint32_t e = 0; e < 8; ++e) {
+                    if (i0 + e * kPtRThreads + threadIdx.x >= n) continue;
+                    const uint64_t ps = pos(v[e]);
+                    if (ps < wlo) continue;
+                    if (ps >= wlo + kDwWin) {
+                        nx = min(nx, (unsigned long long)ps);
+                        continue;
+                    }
+                    const uint32_t a = (uint32_t)(ps - wlo);
+                    atomicAdd(&L.w.A[a], 1u | (kKbit ? ((v[e] >> kScoreBits) & 1u) << 16 : 0u));
+                    if (pass) atomicAdd(&L.w.S[a], v[e] & smask);
+                }
+            }
+            nx = wave_min64(nx);
+            if ((threadIdx.x & 63) == 0) atomicMin(&L.s_next, nx);
+            __syncthreads();
+            // thread t: positions [t kPer, t kPer + kPer)
+            uint32_t kept = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < kPer; ++j) {
+                const uint32_t a = L.w.A[threadIdx.x * kPer + j];
+                kept += pt_keep(a & 0xFFFFu, a >> 16, kKbit, g.min_shared);
+            }
+            uint32_t e0, wt;
+            block_scan_n<kPtRThreads>(kept, e0, wt, L.wave_tot);
+            if (pass) {
+                uint64_t at = ex + o + e0;
+                for (uint32_t j = 0; j < kPer; ++j) {
+                    const uint32_t x = threadIdx.x * kPer + j, a = L.w.A[x];
+                    const uint32_t w = a & 0xFFFFu, w1 = a >> 16;
+                    if (!pt_keep(w, w1, kKbit, g.min_shared)) continue;
+                    const uint64_t ps = wlo + x, rl = ps / span;
+                    pt_direct_write(out, at, rowbase + (uint32_t)rl, qlo + (uint32_t)(ps - rl * span), w, L.w.S[x], w1,
+                                    kKbit);
+                    ++at;
+                }
+            }
+            o += wt;
+            wlo = L.s_next;
+        }
+        if (pass == 0) total = (uint32_t)o;
+    }
+}
+
+template <bool kKbit>
+__global__ __launch_bounds__(kPtRThreads) void pt_reduce_direct_kernel(const uint32_t* __restrict__ keys, BlkSrc bs,
+                                                                       PtGeom g, unsigned long long* __restrict__ lb,
+                                                                       PtDirectOut out,
+                                                                       unsigned long long* __restrict__ total) {
+    __shared__ PtDirectLds L;
+    const uint32_t d = blockIdx.x;
+    uint32_t s0, n, r;
+    blk_of(bs, d, s0, n, r);
+    const uint32_t* src = blk_keys(bs, d, keys);
+    unsigned long long agg = 0;
+    if (n == 0) {
+        if (threadIdx.x < 64) agg = ft_lookback(lb, d, 0);
+    } else if (n <= 2 * kPtRThreads) {
+        pt_direct_block<2, kKbit>(L, L.s2, src, s0, n, r, d, g, lb, out, agg);
+    } else if (n <= 4 * kPtRThreads) {
+        pt_direct_block<4, kKbit>(L, L.s4, src, s0, n, r, d, g, lb, out, agg);
+    } else if (n <= 8 * kPtRThreads) {
+        pt_direct_block<8, kKbit>(L, L.s8, src, s0, n, r, d, g, lb, out, agg);
+    } else if (n <= kPtCap) {
+        pt_direct_block<16, kKbit>(L, L.s16, src, s0, n, r, d, g, lb, out, agg);
+    } else {
+        pt_direct_windows<kKbit>(L, src, s0, n, r, d, g, lb, out, agg);
+        if (threadIdx.x == 0) atomicAdd(&total[1], 1ull);  // windowed sub-blocks (a statistic)
+    }
+    if (d + 1 == gridDim.x && threadIdx.x == 0) total[0] = agg;  // inclusive: the pass's edges
 }
 
 // one call's parameters
@@ -5733,6 +6056,27 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
 // reduced together by the row-block tail of ws[0]: one run per pair over both k, w = its length,
 // w1 = its k-bit entries, score = Σ s — the union of the per-k lists without building or merging
 // them.  Host-synchronous; *n_edges = the kept pairs.
+// the in-place reduce of tail_multi's nd sub-blocks (keys in k2 / inc, descriptors in dsc) into the
+// call's arrays; *ne = the pass's edges (only the first c.cap written)
+int tail_direct(kmp_postings* w0, const StepCfg& c, const PtGeom& g, uint32_t nd, uint64_t* ne, hipStream_t st) {
+    uint32_t *dstart = w0->dsc.p, *dsize = dstart + nd, *drow = dsize + nd;
+    const BlkSrc bs{dstart, dsize, drow, reinterpret_cast<const uint32_t*>(w0->inc.p)};
+    const PtDirectOut out{c.d_p, c.d_q, c.d_w, c.d_s, c.d_w0, c.d_w1, c.cap, c.stride};
+    unsigned long long* tot = w0->dlb.p + nd;  // | windowed sub-blocks
+    PG(hipMemsetAsync(tot, 0, 2 * sizeof(unsigned long long), st));
+    if (g.kbit)
+        pt_reduce_direct_kernel<true><<<nd, kPtRThreads, 0, st>>>(w0->k2.p, bs, g, w0->dlb.p, out, tot);
+    else
+        pt_reduce_direct_kernel<false><<<nd, kPtRThreads, 0, st>>>(w0->k2.p, bs, g, w0->dlb.p, out, tot);
+    PG(hipGetLastError());
+    unsigned long long h[2] = {0, 0};
+    PG(hipMemcpyAsync(h, tot, sizeof(h), hipMemcpyDeviceToHost, st));
+    PG(hipStreamSynchronize(st));
+    *ne = (uint32_t)h[0];
+    w0->last_ovf = (uint32_t)h[1];
+    return KMP_OK;
+}
+
 int tail_multi(kmp_postings* const* ws, uint32_t nk, const StepCfg& c, const uint64_t* inc, uint64_t* n_edges,
                kmp_postings_stats* stats, hipStream_t st) {
     kmp_postings* w0 = ws[0];
@@ -5745,9 +6089,12 @@ int tail_multi(kmp_postings* const* ws, uint32_t nk, const StepCfg& c, const uin
     uint64_t total = T + 1;
     for (uint32_t j = 0; j < nk; ++j) total = std::max<uint64_t>(total, ws[j]->stage_floor);
     PG(w0->inc.reserve(total / 2 + 1));  // u32 keys in a u64 buffer
-    PG(w0->uniq.reserve(total));
-    PG(w0->w.reserve(total));
-    PG(w0->stg2.reserve(2 * total));
+    const bool direct = w0->direct_tail != 0;
+    if (!direct) {  // staged runs (the direct reduce writes the edges in place)
+        PG(w0->uniq.reserve(total));
+        PG(w0->w.reserve(total));
+        PG(w0->stg2.reserve(2 * total));
+    }
     PG(w0->ovf.reserve((uint64_t)g.nrb + 1));
     PG(w0->small.reserve(16));
     hipError_t e = hipSuccess;
@@ -5791,7 +6138,28 @@ int tail_multi(kmp_postings* const* ws, uint32_t nk, const StepCfg& c, const uin
     PG(hipMemcpyAsync(dbase, hd.data(), (g.nrb + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, st));
     pt_split_kernel<<<g.nrb, kSbThreads, 0, st>>>(keys32, b.bst, dbase, g, c.n, c.ranged ? c.row_hi : c.n,
                                                   w0->k2.p, dstart, dsize, drow);
-    const BlkSrc bs{dstart, dsize, drow};
+    const BlkSrc bs{dstart, dsize, drow, keys32};
+    if (direct) {
+        PG(w0->dlb.reserve((uint64_t)nd + 2));
+        PG(hipMemsetAsync(w0->dlb.p, 0, (size_t)nd * sizeof(unsigned long long), st));
+        w0->pend_g = g;
+        w0->pend_nd = nd;
+        w0->pend_direct = true;
+        w0->last_ovf = 0;
+        uint64_t ne = 0;
+        const int rc = tail_direct(w0, c, g, nd, &ne, st);
+        if (rc != KMP_OK) return rc;
+        for (uint32_t j = 0; j < nk; ++j) ws[j]->shard_cap = ws[j]->last_most + ws[j]->last_most / 4 + 256;
+        w0->pt_inc = T;
+        w0->pend_ne = ne;
+        if (stats) {
+            stats->incidences = T;
+            stats->pairs = ne;
+        }
+        *n_edges = ne;
+        return ne > c.cap ? KMP_EOVERFLOW : KMP_OK;
+    }
+    w0->pend_direct = false;
     if (g.kbit)
         pt_reduce_scored_kernel<true><<<nd, kPtRThreads, 0, st>>>(w0->k2.p, bs, g, w0->flags.p, w0->ovf.p, stage_p,
                                                                   stage_q, w0->w.p, w0->stg2.p, w0->stg2.p + total,
@@ -5844,6 +6212,13 @@ int tail_multi(kmp_postings* const* ws, uint32_t nk, const StepCfg& c, const uin
 // the emit of the last tail_multi of w0 again, into larger arrays (its runs are still staged)
 int tail_multi_emit(kmp_postings* w0, const StepCfg& c, uint64_t* n_edges, hipStream_t st) {
     const uint32_t nd = w0->pend_nd;
+    if (w0->pend_direct) {  // the in-place reduce again, into the larger arrays
+        *n_edges = w0->pend_ne;
+        if (w0->pend_ne > c.cap) return KMP_EOVERFLOW;
+        PG(hipMemsetAsync(w0->dlb.p, 0, (size_t)nd * sizeof(unsigned long long), st));
+        uint64_t ne = 0;
+        return tail_direct(w0, c, w0->pend_g, nd, &ne, st);
+    }
     const uint64_t total = w0->pend_total;
     uint32_t *dstart = w0->dsc.p, *dsize = dstart + nd, *drow = dsize + nd, *dcnt = drow + nd, *deoff = dcnt + nd + 1;
     (void)drow;
@@ -6160,6 +6535,12 @@ int kmp_postings_last_layout(const kmp_postings* ws) {
 }
 
 uint32_t kmp_postings_last_overflow_blocks(const kmp_postings* ws) { return ws ? ws->last_ovf : 0u; }
+
+int kmp_postings_set_direct(kmp_postings* ws, int enable) {
+    if (!ws) return KMP_EINVAL;
+    ws->direct_tail = enable ? 1 : 0;
+    return KMP_OK;
+}
 
 int kmp_postings_set_tail(kmp_postings* ws, int mode) {
     if (!ws || (mode != KMP_TAIL_FAST && mode != KMP_TAIL_COUNT)) return KMP_EINVAL;

@@ -125,6 +125,15 @@ class KmerPairEngine:
         """Bounded-memory passes: pair keys per pass (0: auto, from the free device memory)."""
         self._check(lib().kmp_ctx_set_pass_keys(self._ctx, keys), "kmp_ctx_set_pass_keys")
 
+    def set_direct_tail(self, enable: bool = True) -> None:
+        """kmp_pairs_stream's fused reduction writes its edges in place (default) or stages them."""
+        self._check(lib().kmp_ctx_set_direct_tail(self._ctx, int(enable)), "kmp_ctx_set_direct_tail")
+
+    @property
+    def last_tail_windows(self) -> int:
+        """Sub-blocks of the last pairs_stream reduced in windows (above the LDS sort capacity)."""
+        return int(lib().kmp_ctx_last_tail_windows(self._ctx))
+
     def set_rows(self, row_lo: int = 0, row_hi: int = 0) -> None:
         """Rows kmp_pairs_stream covers ([0, 0): all): a process's share of a multi-process split."""
         self._check(lib().kmp_ctx_set_rows(self._ctx, row_lo, row_hi), "kmp_ctx_set_rows")
