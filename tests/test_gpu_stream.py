@@ -134,8 +134,7 @@ def test_stream_dense_pairs_windows(oracle_mod, direct):
     overflow sort).  Every edge, score and w_k equal to the oracle's."""
     base = K.synth(20000, 5, 1)
     rng = np.random.default_rng(77)
-    dup = rng.integers(0, 20, 3000).astype(np.uint8)
-    lens = np.diff(base.offsets.astype(np.int64))
+    dup = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", np.uint8)[rng.integers(0, 20, 3000)]
     seqs = [base.residues[base.offsets[i]:base.offsets[i + 1]] for i in range(base.n)]
     cls = base.class_id.astype(np.uint16).copy()
     for j, row in enumerate((0, 1, 9000, 19000)):

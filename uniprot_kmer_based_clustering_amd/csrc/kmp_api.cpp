@@ -749,8 +749,10 @@ uint64_t pass_budget(kmp_ctx* c, bool fused = false) {
     // sub-blocks, sizes its buffers once per stream (kmp_postings_set_shard_floor): shard regions
     // of the smaller k with a 2x fullest-region allowance 20, row-block and sub-block keys 8,
     // staged runs 20, the pass's edges 17 (edges / incidences ~0.63), +25 % growth headroom:
-    // ~86 B per key of the 3/4-budget pass, so 3/4 of the free memory over 90 B leaves ~40 % free
-    if (fused) return std::max<uint64_t>(1u << 20, std::min<uint64_t>(fr / 4 * 3 / 90, 3ull << 30));
+    // ~86 B per key of the 3/4-budget pass, so 3/4 of the free memory over 90 B leaves ~40 % free;
+    // the in-place reduce (kmp_ctx_set_direct_tail, default) stages nothing: ~56 B, budget 66 B
+    if (fused)
+        return std::max<uint64_t>(1u << 20, std::min<uint64_t>(fr / 4 * 3 / (c->direct_tail ? 66 : 90), 3ull << 30));
     return std::max<uint64_t>(1u << 20, std::min<uint64_t>(fr / 2 / 96, 3ull << 30));
 }
 
