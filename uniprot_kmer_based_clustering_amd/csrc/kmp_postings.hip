@@ -4206,7 +4206,8 @@ __global__ __launch_bounds__(kSbThreads) void pt_split_kernel(const uint32_t* __
                                                               uint32_t* __restrict__ keys2,
                                                               uint32_t* __restrict__ dstart,
                                                               uint32_t* __restrict__ dsize,
-                                                              uint32_t* __restrict__ drow) {
+                                                              uint32_t* __restrict__ drow,
+                                                              uint32_t* __restrict__ ovl) {
     __shared__ uint32_t cnt[1u << kSbMaxLog];  // per bin: count, then first key (local), then cursor
     __shared__ uint32_t lst[1u << kSbMaxLog];  // per sub-block: first key (local)
     __shared__ uint32_t wave_tot[kSbThreads / 64];
@@ -4251,6 +4252,7 @@ __global__ __launch_bounds__(kSbThreads) void pt_split_kernel(const uint32_t* __
         dstart[d0 + j] = s0 + a;
         dsize[d0 + j] = e - a;
         drow[d0 + j] = r;
+        if (e - a > kPtCap) ovl[1 + atomicAdd(&ovl[0], 1u)] = d0 + j;  // above the LDS sort: listed
     }
     for (uint32_t i = threadIdx.x; i < n; i += kSbThreads) {  // a bin's keys stay inside its sub-block
         const uint32_t k = keys[s0 + i];
@@ -5018,11 +5020,12 @@ __device__ __forceinline__ void pt_direct_block(PtDirectLds& L, typename PtSort<
     });
 }
 
-// a sub-block above kPtCap: windows of kDwWin pair positions (the monotone position of pt_bin_sort)
+// a sub-block above kPtCap: windows of kDwWin pair positions (the monotone position of pt_bin_sort),
+// visiting only occupied positions; one pass: the kept count (write false), or the writes from
+// output offset ex.  Returns the kept count.
 template <bool kKbit>
-__device__ void pt_direct_windows(PtDirectLds& L, const uint32_t* __restrict__ src, uint32_t s0, uint32_t n,
-                                  uint32_t r, uint32_t d, const PtGeom& g, unsigned long long* __restrict__ lb,
-                                  const PtDirectOut& out, unsigned long long& agg_out) {
+__device__ uint32_t pt_windows(PtDirectLds& L, const uint32_t* __restrict__ src, uint32_t s0, uint32_t n, uint32_t r,
+                               const PtGeom& g, bool write, uint64_t ex, const PtDirectOut& out) {
     constexpr uint32_t kPer = kDwWin / kPtRThreads;
     const unsigned sb = g.sbits, rs = g.pbits + g.sbits;
     const uint32_t rowbase = g.row0 + (r << g.rbits), qm = (1u << g.pbits) - 1, qlo = rowbase + 1;
@@ -5039,91 +5042,96 @@ __device__ void pt_direct_windows(PtDirectLds& L, const uint32_t* __restrict__ s
     // the first occupied position
     unsigned long long mn = ~0ull;
     for (uint32_t i = threadIdx.x; i < n; i += kPtRThreads) mn = min(mn, (unsigned long long)pos(src[s0 + i]));
+    __syncthreads();  // the caller's LDS reads are done
     if (threadIdx.x == 0) L.s_next = ~0ull;
     __syncthreads();
     mn = wave_min64(mn);
     if ((threadIdx.x & 63) == 0) atomicMin(&L.s_next, mn);
     __syncthreads();
-    const unsigned long long first = L.s_next;
-    uint64_t ex = 0;
-    uint32_t total = 0;
-    for (int pass = 0; pass < 2; ++pass) {  // 0: the kept count; 1: the writes
-        if (pass == 1) {
-            if (threadIdx.x < 64) {
-                const unsigned long long e = ft_lookback(lb, d, total);
-                if (threadIdx.x == 0) L.s_excl = e;
-            }
-            __syncthreads();
-            ex = (uint32_t)L.s_excl;
-            agg_out = L.s_excl + total;
+    unsigned long long wlo = L.s_next;
+    uint64_t o = 0;
+    while (wlo != ~0ull) {  // uniform
+        __syncthreads();  // the previous window's reads are done
+        for (uint32_t i = threadIdx.x; i < kDwWin; i += kPtRThreads) {
+            L.w.A[i] = 0;
+            L.w.S[i] = 0;
         }
-        uint64_t o = 0;
-        unsigned long long wlo = first;
-        while (wlo != ~0ull) {  // uniform
-            __syncthreads();  // the previous window's reads are done
-            for (uint32_t i = threadIdx.x; i < kDwWin; i += kPtRThreads) {
-                L.w.A[i] = 0;
-                L.w.S[i] = 0;
+        if (threadIdx.x == 0) L.s_next = ~0ull;
+        __syncthreads();
+        unsigned long long nx = ~0ull;
+        for (uint32_t i0 = 0; i0 < n; i0 += 8 * kPtRThreads) {  // loads in batches ahead of the atomics
+            uint32_t v[8];
+#pragma unroll
+            for (uint32_t e = 0; e < 8; ++e) {
+                const uint32_t i = i0 + e * kPtRThreads + threadIdx.x;
+                v[e] = i < n ? src[s0 + i] : 0xFFFFFFFFu;
             }
-            if (threadIdx.x == 0) L.s_next = ~0ull;
-            __syncthreads();
-            unsigned long long nx = ~0ull;
-            for (uint32_t i0 = 0; i0 < n; i0 += 8 * kPtRThreads) {  // loads in batches ahead of the atomics
-                uint32_t v[8];
 #pragma unroll
-                for (uint32_t e = 0; e < 8; ++e) {
-                    const uint32_t i = i0 + e * kPtRThreads + threadIdx.x;
-                    v[e] = i < n ? src[s0 + i] : 0xFFFFFFFFu;
+            for (uint32_t e = 0; e < 8; ++e) {
+                if (i0 + e * kPtRThreads + threadIdx.x >= n) continue;
+                const uint64_t ps = pos(v[e]);
+                if (ps < wlo) continue;
+                if (ps >= wlo + kDwWin) {
+                    nx = min(nx, (unsigned long long)ps);
+                    continue;
                 }
-#pragma unroll
-                for (uint32_t e = 0; e < 8; ++e) {
-                    if (i0 + e * kPtRThreads + threadIdx.x >= n) continue;
-                    const uint64_t ps = pos(v[e]);
-                    if (ps < wlo) continue;
-                    if (ps >= wlo + kDwWin) {
-                        nx = min(nx, (unsigned long long)ps);
-                        continue;
-                    }
-                    const uint32_t a = (uint32_t)(ps - wlo);
-                    atomicAdd(&L.w.A[a], 1u | (kKbit ? ((v[e] >> kScoreBits) & 1u) << 16 : 0u));
-                    if (pass) atomicAdd(&L.w.S[a], v[e] & smask);
-                }
+                const uint32_t a = (uint32_t)(ps - wlo);
+                atomicAdd(&L.w.A[a], 1u | (kKbit ? ((v[e] >> kScoreBits) & 1u) << 16 : 0u));
+                if (write) atomicAdd(&L.w.S[a], v[e] & smask);
             }
-            nx = wave_min64(nx);
-            if ((threadIdx.x & 63) == 0) atomicMin(&L.s_next, nx);
-            __syncthreads();
-            // thread t: positions [t kPer, t kPer + kPer)
-            uint32_t kept = 0;
+        }
+        nx = wave_min64(nx);
+        if ((threadIdx.x & 63) == 0) atomicMin(&L.s_next, nx);
+        __syncthreads();
+        // thread t: positions [t kPer, t kPer + kPer)
+        uint32_t kept = 0;
 #pragma unroll
+        for (uint32_t j = 0; j < kPer; ++j) {
+            const uint32_t a = L.w.A[threadIdx.x * kPer + j];
+            kept += pt_keep(a & 0xFFFFu, a >> 16, kKbit, g.min_shared);
+        }
+        uint32_t e0, wt;
+        block_scan_n<kPtRThreads>(kept, e0, wt, L.wave_tot);
+        if (write) {
+            uint64_t at = ex + o + e0;
             for (uint32_t j = 0; j < kPer; ++j) {
-                const uint32_t a = L.w.A[threadIdx.x * kPer + j];
-                kept += pt_keep(a & 0xFFFFu, a >> 16, kKbit, g.min_shared);
+                const uint32_t x = threadIdx.x * kPer + j, a = L.w.A[x];
+                const uint32_t w = a & 0xFFFFu, w1 = a >> 16;
+                if (!pt_keep(w, w1, kKbit, g.min_shared)) continue;
+                const uint64_t ps = wlo + x, rl = ps / span;
+                pt_direct_write(out, at, rowbase + (uint32_t)rl, qlo + (uint32_t)(ps - rl * span), w, L.w.S[x], w1,
+                                kKbit);
+                ++at;
             }
-            uint32_t e0, wt;
-            block_scan_n<kPtRThreads>(kept, e0, wt, L.wave_tot);
-            if (pass) {
-                uint64_t at = ex + o + e0;
-                for (uint32_t j = 0; j < kPer; ++j) {
-                    const uint32_t x = threadIdx.x * kPer + j, a = L.w.A[x];
-                    const uint32_t w = a & 0xFFFFu, w1 = a >> 16;
-                    if (!pt_keep(w, w1, kKbit, g.min_shared)) continue;
-                    const uint64_t ps = wlo + x, rl = ps / span;
-                    pt_direct_write(out, at, rowbase + (uint32_t)rl, qlo + (uint32_t)(ps - rl * span), w, L.w.S[x], w1,
-                                    kKbit);
-                    ++at;
-                }
-            }
-            o += wt;
-            wlo = L.s_next;
         }
-        if (pass == 0) total = (uint32_t)o;
+        o += wt;
+        wlo = L.s_next;
+    }
+    return (uint32_t)o;
+}
+
+// the kept counts of the sub-blocks above kPtCap (listed by pt_split: ovl[0] of them at ovl + 1),
+// before the in-place reduce: there each publishes its count at once, so the look-back of the
+// blocks after it never waits on its windows
+template <bool kKbit>
+__global__ __launch_bounds__(kPtRThreads) void pt_window_count_kernel(const uint32_t* __restrict__ keys, BlkSrc bs,
+                                                                      PtGeom g, const uint32_t* __restrict__ ovl,
+                                                                      uint32_t* __restrict__ wc) {
+    __shared__ PtDirectLds L;
+    const uint32_t m = ovl[0];
+    for (uint32_t i = blockIdx.x; i < m; i += gridDim.x) {
+        const uint32_t d = ovl[1 + i];
+        uint32_t s0, n, r;
+        blk_of(bs, d, s0, n, r);
+        const uint32_t t = pt_windows<kKbit>(L, blk_keys(bs, d, keys), s0, n, r, g, false, 0, PtDirectOut{});
+        if (threadIdx.x == 0) wc[d] = t;
     }
 }
 
 template <bool kKbit>
 __global__ __launch_bounds__(kPtRThreads) void pt_reduce_direct_kernel(const uint32_t* __restrict__ keys, BlkSrc bs,
                                                                        PtGeom g, unsigned long long* __restrict__ lb,
-                                                                       PtDirectOut out,
+                                                                       PtDirectOut out, const uint32_t* __restrict__ wc,
                                                                        unsigned long long* __restrict__ total) {
     __shared__ PtDirectLds L;
     const uint32_t d = blockIdx.x;
@@ -5141,8 +5149,16 @@ __global__ __launch_bounds__(kPtRThreads) void pt_reduce_direct_kernel(const uin
         pt_direct_block<8, kKbit>(L, L.s8, src, s0, n, r, d, g, lb, out, agg);
     } else if (n <= kPtCap) {
         pt_direct_block<16, kKbit>(L, L.s16, src, s0, n, r, d, g, lb, out, agg);
-    } else {
-        pt_direct_windows<kKbit>(L, src, s0, n, r, d, g, lb, out, agg);
+    } else {  // counted by pt_window_count_kernel: published at once, then the writes
+        const uint32_t kept = wc[d];
+        if (threadIdx.x < 64) {
+            const unsigned long long e = ft_lookback(lb, d, kept);
+            if (threadIdx.x == 0) L.s_excl = e;
+        }
+        __syncthreads();
+        const unsigned long long e = L.s_excl;
+        agg = e + kept;
+        pt_windows<kKbit>(L, src, s0, n, r, g, true, (uint32_t)e, out);
         if (threadIdx.x == 0) atomicAdd(&total[1], 1ull);  // windowed sub-blocks (a statistic)
     }
     if (d + 1 == gridDim.x && threadIdx.x == 0) total[0] = agg;  // inclusive: the pass's edges
@@ -6062,12 +6078,19 @@ int tail_direct(kmp_postings* w0, const StepCfg& c, const PtGeom& g, uint32_t nd
     uint32_t *dstart = w0->dsc.p, *dsize = dstart + nd, *drow = dsize + nd;
     const BlkSrc bs{dstart, dsize, drow, reinterpret_cast<const uint32_t*>(w0->inc.p)};
     const PtDirectOut out{c.d_p, c.d_q, c.d_w, c.d_s, c.d_w0, c.d_w1, c.cap, c.stride};
+    // dsc's run counts | offsets regions (the staged path's) hold the windows' kept counts | the
+    // list of the oversized sub-blocks (pt_split)
+    uint32_t *wc = drow + nd, *ovl = wc + nd + 1;
     unsigned long long* tot = w0->dlb.p + nd;  // | windowed sub-blocks
     PG(hipMemsetAsync(tot, 0, 2 * sizeof(unsigned long long), st));
-    if (g.kbit)
-        pt_reduce_direct_kernel<true><<<nd, kPtRThreads, 0, st>>>(w0->k2.p, bs, g, w0->dlb.p, out, tot);
-    else
-        pt_reduce_direct_kernel<false><<<nd, kPtRThreads, 0, st>>>(w0->k2.p, bs, g, w0->dlb.p, out, tot);
+    constexpr uint32_t kWcGrid = 1024;
+    if (g.kbit) {
+        pt_window_count_kernel<true><<<kWcGrid, kPtRThreads, 0, st>>>(w0->k2.p, bs, g, ovl, wc);
+        pt_reduce_direct_kernel<true><<<nd, kPtRThreads, 0, st>>>(w0->k2.p, bs, g, w0->dlb.p, out, wc, tot);
+    } else {
+        pt_window_count_kernel<false><<<kWcGrid, kPtRThreads, 0, st>>>(w0->k2.p, bs, g, ovl, wc);
+        pt_reduce_direct_kernel<false><<<nd, kPtRThreads, 0, st>>>(w0->k2.p, bs, g, w0->dlb.p, out, wc, tot);
+    }
     PG(hipGetLastError());
     unsigned long long h[2] = {0, 0};
     PG(hipMemcpyAsync(h, tot, sizeof(h), hipMemcpyDeviceToHost, st));
@@ -6136,8 +6159,9 @@ int tail_multi(kmp_postings* const* ws, uint32_t nk, const StepCfg& c, const uin
              *dbase = deoff + nd + 1;
     PG(w0->ovf.reserve((uint64_t)std::max(nd, g.nrb) + 1));  // the sub-blocks the reduce lists
     PG(hipMemcpyAsync(dbase, hd.data(), (g.nrb + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    PG(hipMemsetAsync(deoff, 0, sizeof(uint32_t), st));  // the oversized sub-blocks' list count
     pt_split_kernel<<<g.nrb, kSbThreads, 0, st>>>(keys32, b.bst, dbase, g, c.n, c.ranged ? c.row_hi : c.n,
-                                                  w0->k2.p, dstart, dsize, drow);
+                                                  w0->k2.p, dstart, dsize, drow, deoff);
     const BlkSrc bs{dstart, dsize, drow, keys32};
     if (direct) {
         PG(w0->dlb.reserve((uint64_t)nd + 2));
