@@ -212,6 +212,9 @@ int kmp_ctx_set_pass_keys(kmp_ctx* ctx, uint64_t keys);
 /* kmp_ctx_set_direct_tail: kmp_pairs_stream's fused multi-k reduction writes each pass's edges in
  * place (default 1; kmp_postings_set_direct) or (0) stages them and emits after a scan. */
 int kmp_ctx_set_direct_tail(kmp_ctx* ctx, int enable);
+/* kmp_ctx_set_flat_heavy: kmp_pairs_stream's passes expand frequent k-mers by rows (default 1;
+ * kmp_postings_set_flat_heavy) or by per-k-mer tiles (0). */
+int kmp_ctx_set_flat_heavy(kmp_ctx* ctx, int enable);
 /* Sub-blocks of the last kmp_pairs_stream that the in-place reduce took in windows of pair positions
  * (above its LDS sort capacity: a row pairing many times with few partners); staged: the ones the
  * overflow sort finished. */
@@ -464,6 +467,10 @@ int kmp_postings_set_tail(kmp_postings* ws, int mode);
  * writes its edges in place from the sub-block reduce, at offsets from a decoupled look-back
  * (default 1), or (0) stages its runs and emits them after a scan.  Same edges either way. */
 int kmp_postings_set_direct(kmp_postings* ws, int enable);
+/* kmp_postings_set_flat_heavy: ranged calls with front reuse (the row passes of one batch) expand
+ * the frequent k-mers by rows — a per-protein index of the compacted elements, built once, makes
+ * a pass's work its own rows' pairs (default 1) — or (0) by per-k-mer tiles.  Same edges. */
+int kmp_postings_set_flat_heavy(kmp_postings* ws, int enable);
 /* The bucketed step as a HIP graph (default 1): captured on the second call with an unchanged
  * shape (pointers, sizes, options, workspace buffers), replayed after that.
  * kmp_postings_graph_replays: calls served by a replay so far. */

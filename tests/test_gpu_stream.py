@@ -79,13 +79,14 @@ def test_scored_heavy_path_uniprot_k5(oracle_mod):
         np.testing.assert_array_equal(got.score, want.astype(np.float32))
 
 
-@pytest.mark.parametrize("direct", [True, False])
+@pytest.mark.parametrize("direct,flat", [(True, True), (False, False)])
 @pytest.mark.parametrize("ks", [(5,), (5, 7)])
-def test_stream_host_chunks_concatenate(oracle_mod, ks, direct):
+def test_stream_host_chunks_concatenate(oracle_mod, ks, direct, flat):
     """kmp_pairs_stream with a host sink: the chunks (consecutive row ranges, each canonical)
     concatenate to the oracle's union edge list (w, score, every w_k), and the summary equals the
     oracle's digest and counters.  direct: the fused reduction writes each pass's edges in place
-    (pt_reduce_direct_kernel), else it stages them and emits after a scan."""
+    (pt_reduce_direct_kernel), else it stages them and emits after a scan; flat: the frequent k-mers
+    are expanded by rows (heavy_flat_kernel), else by per-k-mer tiles."""
     b = K.synth(30000, 5, 1)
     orcs = [oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=k, threads=16) for k in ks]
     want, (p, q, w, s, wk) = oracle_mod.stream(orcs, collect=True, threads=16)
@@ -93,6 +94,7 @@ def test_stream_host_chunks_concatenate(oracle_mod, ks, direct):
     with K.KmerPairEngine(0, 8) as e:
         e.load(b)
         e.set_direct_tail(direct)
+        e.set_flat_heavy(flat)
         e.set_pass_keys(1 << 21)
         sm = e.pairs_stream(ks, score=BLOSUM, sink=chunks.append)
     assert sm["passes"] == len(chunks) > 1
@@ -108,8 +110,8 @@ def test_stream_host_chunks_concatenate(oracle_mod, ks, direct):
     assert_summary(sm, want)
 
 
-@pytest.mark.parametrize("direct", [True, False])
-def test_stream_count_and_filters(oracle_mod, direct):
+@pytest.mark.parametrize("direct,flat", [(True, True), (False, False), (True, False)])
+def test_stream_count_and_filters(oracle_mod, direct, flat):
     """COUNT score (score = w), min_shared = 3 (kept when either k reaches it) and the class filter
     off, streamed over passes: summary equal to the oracle's (in-place and staged reduction)."""
     b = K.synth(15000, 5, 1)
@@ -117,6 +119,7 @@ def test_stream_count_and_filters(oracle_mod, direct):
     with K.KmerPairEngine(0, 8) as e:
         e.load(b)
         e.set_direct_tail(direct)
+        e.set_flat_heavy(flat)
         e.set_pass_keys(1 << 20)
         for kw in ({"min_shared": 3}, {"require_class_diff": False}, {}):
             want = oracle_mod.stream(orcs, blosum=False, threads=16, **kw)

@@ -158,6 +158,7 @@ struct kmp_ctx {
     uint64_t pass_keys = 0;
     uint32_t last_passes = 0;
     int direct_tail = 1;  // kmp_ctx_set_direct_tail: the fused tail writes its edges in place
+    int flat_heavy = 1;   // kmp_ctx_set_flat_heavy: passes expand frequent k-mers by rows
     uint64_t last_windows = 0;  // kmp_ctx_last_tail_windows
     // kmp_ctx_set_rows: the rows kmp_pairs_stream covers ([0, 0): all) — a process's share of a
     // multi-process split (one process per GPU)
@@ -1299,6 +1300,7 @@ static int stream_passes(kmp_ctx* c, const kmp_pair_opts& o, const int* ks, uint
         KMP_TRY(c, kmp_postings_set_reuse(kv[j]->ws, 1));
         KMP_TRY(c, kmp_postings_set_timing(kv[j]->ws, 1));  // stage times of the summary
         KMP_TRY(c, kmp_postings_set_direct(kv[j]->ws, c->direct_tail));
+        KMP_TRY(c, kmp_postings_set_flat_heavy(kv[j]->ws, c->flat_heavy));
     }
     EventPair dev;
     if (!dev.ready()) return fail(c, KMP_EDEVICE, "events");
@@ -1797,6 +1799,12 @@ int kmp_ctx_set_pass_keys(kmp_ctx* c, uint64_t keys) {
 uint32_t kmp_ctx_last_passes(const kmp_ctx* c) { return c ? c->last_passes : 0u; }
 
 uint64_t kmp_ctx_last_tail_windows(const kmp_ctx* c) { return c ? c->last_windows : 0u; }
+
+int kmp_ctx_set_flat_heavy(kmp_ctx* c, int enable) {
+    if (!c) return KMP_EINVAL;
+    c->flat_heavy = enable ? 1 : 0;
+    return KMP_OK;
+}
 
 int kmp_ctx_set_direct_tail(kmp_ctx* c, int enable) {
     if (!c) return KMP_EINVAL;

@@ -1651,7 +1651,8 @@ __global__ __launch_bounds__(kHvThreads) void heavy_compact_kernel(const unsigne
                                                                    uint64_t* __restrict__ GS,
                                                                    uint32_t* __restrict__ RUN,
                                                                    uint64_t* __restrict__ RH,
-                                                                   uint32_t* __restrict__ GH) {
+                                                                   uint32_t* __restrict__ GH,
+                                                                   uint32_t* __restrict__ KG) {
     __shared__ uint32_t wave_tot[kHvThreads / 64];
     const uint64_t t0 = (uint64_t)blockIdx.x * kHvTile;
     uint64_t eb = eoff[blockIdx.x], gb = goff[blockIdx.x], rb = ho.cls ? roff[blockIdx.x] : 0;
@@ -1671,6 +1672,7 @@ __global__ __launch_bounds__(kHvThreads) void heavy_compact_kernel(const unsigne
         block_scan_n<kHvThreads>(ke, xe, te, wave_tot);
         block_scan_n<kHvThreads>(kg, xg, tg, wave_tot);
         if (ke) E[eb + xe] = ho.elem(v);
+        if (ke && KG) KG[eb + xe] = (uint32_t)(gb + xg + kg - 1);  // its k-mer (the last head up to it)
         if (kg) {
             GS[gb + xg] = eb + xe;  // a k-mer head is always a new element
             GH[gb + xg] = (uint32_t)(v >> ho.hshift);  // the k-mer's h (scored calls: its self-score)
@@ -1708,7 +1710,7 @@ __global__ __launch_bounds__(256) void heavy_plan_kernel(const uint32_t* __restr
                                                          HeavyOrder ho, const uint32_t* __restrict__ RUN,
                                                          const uint64_t* __restrict__ RH, int flat_ok,
                                                          uint32_t row_lo, uint32_t row_hi, uint32_t heavy_df,
-                                                         int stats,
+                                                         int stats, int tiles_on,
                                                          unsigned long long* __restrict__ gstats,
                                                          uint32_t* __restrict__ gi, uint32_t* __restrict__ BT,
                                                          uint32_t* __restrict__ BP,
@@ -1736,7 +1738,9 @@ __global__ __launch_bounds__(256) void heavy_plan_kernel(const uint32_t* __restr
         uint32_t i0 = 0, i1 = 0;
         unsigned long long tiles = 0;
         const uint32_t nruns = ho.cls && d ? RUN[b + d - 1] - RUN[b] + 1 : 0u;
-        if (d >= 2 && d <= heavy_df && flat_ok && nruns <= kHvFlatRuns) {
+        if (!tiles_on) {
+            // statistics only
+        } else if (d >= 2 && d <= heavy_df && flat_ok && nruns <= kHvFlatRuns) {
             // flat: the k-mer's cross-class pairs as one index space, cut into kHvFlat-pair tiles
             const uint32_t ra = RUN[b];
             unsigned long long pairs = 0;
@@ -2046,6 +2050,125 @@ __global__ __launch_bounds__(kHvI) void heavy_expand_kernel(const uint32_t* __re
                 }
             }
         }
+    }
+}
+
+// Ranged calls in plain order (the passes of a streamed batch): the rows of a pass, not its
+// k-mers, drive the expansion.  A per-protein index of the compacted elements (PE: element
+// indices grouped by protein, PO: each protein's start; built once per compaction) makes a pass's
+// active elements the contiguous range PE[PO[row_lo], PO[row_hi]); each pairs with the later
+// elements of its k-mer (E is sorted by protein within a k-mer, so every partner's protein is
+// larger: the pair's smaller protein is the active row).  One workgroup per 256 active elements:
+// their candidate counts scanned in LDS, the candidates split into one contiguous slice per wave,
+// the class test counted (pass 1), one cursor reservation for the workgroup, and the kept keys
+// written compacted by ballot (pass 2; consecutive lanes read consecutive partners).  No per-k-mer
+// plan, tile table or search: the work is the pass's own pairs.
+constexpr uint32_t kHfThreads = 256, kHfWaves = kHfThreads / 64;
+__global__ __launch_bounds__(kHfThreads) void heavy_flat_kernel(
+        const uint32_t* __restrict__ E, const uint64_t* __restrict__ GS, const uint32_t* __restrict__ KG,
+        const uint32_t* __restrict__ GH, const uint32_t* __restrict__ PE, uint32_t a0, uint32_t a1, unsigned cb,
+        uint32_t mul, int require_diff, uint32_t heavy_df, int k, unsigned sb, uint32_t sor,
+        unsigned long long* __restrict__ out, uint64_t shard_cap, unsigned long long* __restrict__ cursor,
+        unsigned long long* __restrict__ gstats) {
+    __shared__ uint32_t s_ex[kHfThreads + 1], s_e[kHfThreads], s_x[kHfThreads], s_f[kHfThreads];
+    __shared__ uint32_t wave_tot[kHfWaves], s_wk[kHfWaves];
+    __shared__ unsigned long long s_base;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t a = a0 + blockIdx.x * kHfThreads + tid;
+    uint32_t cand = 0, e = 0, x = 0, f = 0;
+    if (a < a1) {
+        e = PE[a];
+        const uint32_t g = KG[e];
+        const uint64_t gs0 = GS[g], gs1 = GS[g + 1];
+        x = E[e];
+        if (gs1 - gs0 <= heavy_df) cand = (uint32_t)(gs1 - e - 1);
+        f = sb ? sor | kmer_self_score(GH[g], k) : 0u;
+    }
+    uint32_t ex, total;
+    block_scan_n<kHfThreads>(cand, ex, total, wave_tot);
+    s_ex[tid] = ex;
+    s_e[tid] = e;
+    s_x[tid] = x;
+    s_f[tid] = f;
+    if (tid == 0) s_ex[kHfThreads] = total;
+    __syncthreads();
+    if (total == 0) return;  // (uniform)
+    const uint32_t S = (total + kHfWaves - 1) / kHfWaves;
+    const uint32_t c0 = min(total, wv * S), c1 = min(total, c0 + S);
+    const uint32_t cmask = (1u << cb) - 1;
+    auto search = [&](uint32_t o) {  // the last row with s_ex[i] <= o (o < total: a row with candidates)
+        uint32_t lo = 0, hi = kHfThreads;
+        while (lo + 1 < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_ex[mid] <= o) lo = mid;
+            else hi = mid;
+        }
+        return lo;
+    };
+    uint32_t kept = 0;
+    if (require_diff) {
+        uint32_t i = c0 + lane < c1 ? search(c0 + lane) : 0u;
+        for (uint32_t o = c0 + lane; o < c1; o += 64) {
+            while (s_ex[i + 1] <= o) ++i;
+            const uint32_t j = s_e[i] + 1 + (o - s_ex[i]);
+            kept += ((E[j] ^ s_x[i]) & cmask) != 0u;
+        }
+        kept = wave_sum(kept);
+    } else {
+        kept = c1 - c0;
+    }
+    if (lane == 0) s_wk[wv] = kept;
+    __syncthreads();
+    uint32_t before = 0, K = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kHfWaves; ++w) {
+        before += w < wv ? s_wk[w] : 0u;
+        K += s_wk[w];
+    }
+    uint32_t hx = (blockIdx.x * 0x9E3779B1u) ^ (a0 * 0x85EBCA6Bu);
+    hx ^= hx >> 16;
+    const uint32_t shard = (hx * 0x7FEB352Du) >> 26;
+    if (tid == 0) {
+        s_base = K ? atomicAdd(&cursor[shard], (unsigned long long)K) : 0ull;
+        if (K) atomicAdd(&gstats[(uint64_t)shard * 8 + kStInc], (unsigned long long)K);
+    }
+    __syncthreads();
+    unsigned long long* dst = out + (uint64_t)shard * shard_cap;
+    uint64_t run = s_base + before;
+    uint32_t i = c0 + lane < c1 ? search(c0 + lane) : 0u;
+    for (uint32_t o0 = c0; o0 < c1; o0 += 64) {  // uniform over the wave (ballot)
+        const uint32_t o = o0 + lane;
+        bool keep = false;
+        unsigned long long key = 0;
+        if (o < c1) {
+            while (s_ex[i + 1] <= o) ++i;
+            const uint32_t j = s_e[i] + 1 + (o - s_ex[i]), xj = E[j], xi = s_x[i];
+            keep = !require_diff || ((xj ^ xi) & cmask) != 0u;
+            key = ((unsigned long long)(xi >> cb) * mul + (xj >> cb)) << sb | s_f[i];
+        }
+        const unsigned long long m = __ballot(keep);
+        if (keep) {
+            const uint64_t pos = run + __popcll(m & ((1ull << lane) - 1));
+            if (pos < shard_cap) dst[pos] = key;
+        }
+        run += __popcll(m);
+    }
+}
+
+// per-protein index of the compacted elements: counts, then (after a scan into PO) the scatter
+__global__ void heavy_pcount_kernel(const uint32_t* __restrict__ E, const unsigned long long* __restrict__ tot,
+                                    unsigned cb, uint32_t* __restrict__ cnt) {
+    const uint64_t ne = tot[0];
+    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < ne; e += (uint64_t)gridDim.x * blockDim.x)
+        atomicAdd(&cnt[E[e] >> cb], 1u);
+}
+__global__ void heavy_pscatter_kernel(const uint32_t* __restrict__ E, const unsigned long long* __restrict__ tot,
+                                      unsigned cb, const uint32_t* __restrict__ PO, uint32_t* __restrict__ cur,
+                                      uint32_t* __restrict__ PE) {
+    const uint64_t ne = tot[0];
+    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < ne; e += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t p = E[e] >> cb;
+        PE[PO[p] + atomicAdd(&cur[p], 1u)] = (uint32_t)e;
     }
 }
 
@@ -3038,6 +3161,7 @@ struct kmp_postings {
     std::vector<unsigned long long> pend_key;
     // the fused tail writes its edges in place (pt_reduce_direct_kernel); 0: staged runs + emit
     int direct_tail = 1;
+    int flat_heavy = 1;  // ranged plain-order heavy expansion by rows (heavy_flat_kernel); 0: tiles
     bool pend_direct = false;  // the pending re-emit reruns the in-place reduce (its keys still held)
     PtGeom pend_g{};
     Grow<unsigned long long> dlb;  // its look-back words (one per sub-block) | the pass's edge count
@@ -3085,6 +3209,12 @@ struct kmp_postings {
     Grow<unsigned long long> spill, hkeys, hsorted, hGS, htc, htoff, hoff, hRH, hseg, hcur;
     bool hcur_valid = false;  // hcur holds the current front's spill cursors
     Grow<uint32_t> hE, hgi, hcnt, hrun, hblk, hGH;  // hGH: each heavy k-mer's h
+    // ranged plain-order calls (heavy_flat_kernel): each element's k-mer, the per-protein index
+    // (elements by protein | protein starts, host copy) and its build scratch
+    Grow<uint32_t> hKG, hPE, hPO, hPC;
+    std::vector<uint32_t> hPOh;
+    bool h_flat_ready = false, h_kg = false;
+    uint64_t h_ng = 0;  // k-mers of the compaction (read back with the index)
     uint64_t spill_cap = 0;     // keys per spill shard region
     bool heavy = false;         // this workspace's batches spill: run the split step
     bool heavy_ready = false;   // hE / hGS hold the current front's compacted spill
@@ -5646,7 +5776,15 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
     // left one CU writing 4 MB), and a filtered tile (the class test per pair) takes its kept
     // partners through a per-row bit mask of the chunk (8 words a row)
     ho.hj = kHvJ;
+    // the passes of one batch (front reuse), plain order: the rows drive the expansion
+    const bool flat = c.ranged && !ho.cls && ws->flat_heavy && ws->reuse;
+    if (flat && ws->heavy_ready && !ws->h_kg) {  // compacted without each element's k-mer: again
+        ws->heavy_ready = false;
+        m = ws->h_m;
+    }
     if (!ws->heavy_ready) {
+        ws->h_flat_ready = false;
+        if (flat) PG(ws->hKG.reserve(m + 1));
         const uint64_t nt = (m + kHvTile - 1) / kHvTile;
         PG(ws->hkeys.reserve(m));
         PG(ws->hsorted.reserve(m));
@@ -5711,7 +5849,8 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
         heavy_compact_kernel<<<(uint32_t)nt, kHvThreads, 0, st>>>(
             ws->hsorted.p, m, ho, reinterpret_cast<const uint64_t*>(off),
             reinterpret_cast<const uint64_t*>(off + nt + 1), reinterpret_cast<const uint64_t*>(off + 2 * (nt + 1)),
-            ws->hE.p, GS, ho.cls ? ws->hrun.p : nullptr, RH, ws->hGH.p);
+            ws->hE.p, GS, ho.cls ? ws->hrun.p : nullptr, RH, ws->hGH.p, flat ? ws->hKG.p : nullptr);
+        ws->h_kg = flat;
         if (!one_wg) heavy_sentinel_kernel<<<1, 64, 0, st>>>(tot, GS, RH);
         PG(hipGetLastError());
         ws->heavy_ready = true;
@@ -5720,7 +5859,35 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
         ws->h_tot = tot;
     }
     if (ws->h_cls != ho.cls) return KMP_EINVAL;  // (compacted above in this call's order)
-    const uint64_t ngb = ws->h_m;  // bound on the k-mer count (device: h_tot[1])
+    if (flat && !ws->h_flat_ready) {
+        // once per compaction: the per-protein index (one read-back: the element and k-mer counts)
+        unsigned long long ht[2] = {0, 0};
+        PG(hipMemcpyAsync(ht, ws->h_tot, sizeof(ht), hipMemcpyDeviceToHost, st));
+        PG(hipStreamSynchronize(st));
+        if (ht[0] >= (1ull << 32)) return KMP_EINVAL;
+        const uint32_t np = c.n;
+        PG(ws->hPE.reserve(ht[0] + 1));
+        PG(ws->hPO.reserve((uint64_t)np + 1));
+        PG(ws->hPC.reserve((uint64_t)np + 1));
+        PG(hipMemsetAsync(ws->hPC.p, 0, ((size_t)np + 1) * sizeof(uint32_t), st));
+        const uint32_t grid = (uint32_t)std::min<uint64_t>((ht[0] + 255) / 256 + 1, 16384);
+        heavy_pcount_kernel<<<grid, 256, 0, st>>>(ws->hE.p, ws->h_tot, ho.cb, ws->hPC.p);
+        size_t tb = 0;
+        PG(rocprim::exclusive_scan(nullptr, tb, ws->hPC.p, ws->hPO.p, 0u, (size_t)np + 1, rocprim::plus<uint32_t>(), st));
+        PG(ws->tmp.reserve(std::max(tb, ws->tmp.n)));
+        PG(rocprim::exclusive_scan(ws->tmp.p, tb, ws->hPC.p, ws->hPO.p, 0u, (size_t)np + 1, rocprim::plus<uint32_t>(),
+                                   st));
+        PG(hipMemsetAsync(ws->hPC.p, 0, ((size_t)np + 1) * sizeof(uint32_t), st));
+        heavy_pscatter_kernel<<<grid, 256, 0, st>>>(ws->hE.p, ws->h_tot, ho.cb, ws->hPO.p, ws->hPC.p, ws->hPE.p);
+        PG(hipGetLastError());
+        ws->hPOh.resize((size_t)np + 1);
+        PG(hipMemcpyAsync(ws->hPOh.data(), ws->hPO.p, ((size_t)np + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        PG(hipStreamSynchronize(st));
+        ws->h_ng = ht[1];
+        ws->h_flat_ready = true;
+    }
+    // bound on the k-mer count (device: h_tot[1]); exact once the flat index read it back
+    const uint64_t ngb = flat ? ws->h_ng : ws->h_m;
     if (ngb == 0) return KMP_OK;
     PG(ws->hgi.reserve(2 * (ngb + 1)));
     PG(ws->htc.reserve(ngb + 1));
@@ -5734,8 +5901,18 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
     const uint32_t* RUN = ho.cls ? ws->hrun.p : nullptr;
     heavy_plan_kernel<<<(uint32_t)((ngb + 1 + 255) / 256), 256, 0, st>>>(
         ws->hE.p, GS, ngb + 1, ws->h_tot + 1, ho, RUN, RH, ho.cls && !c.ranged ? 1 : 0, row_lo, row_hi, c.heavy_df,
-        stats ? 1 : 0, ws->bstats.p,
+        stats ? 1 : 0, flat ? 0 : 1, ws->bstats.p,
         ws->hgi.p, BT, BP, ws->htc.p);
+    if (flat) {
+        const uint32_t a0 = ws->hPOh[row_lo], a1 = ws->hPOh[row_hi];
+        if (a1 > a0)
+            heavy_flat_kernel<<<(a1 - a0 + kHfThreads - 1) / kHfThreads, kHfThreads, 0, st>>>(
+                ws->hE.p, GS, ws->hKG.p, ws->hGH.p, ws->hPE.p, a0, a1, ho.cb, 1u << bits_for(c.n), c.require_diff,
+                c.heavy_df, c.k, c.sb, c.sor, ws->inc_sorted.p, ws->shard_cap, ws->bstats.p + kRbCursor,
+                ws->bstats.p);
+        PG(hipGetLastError());
+        return KMP_OK;
+    }
     size_t t2 = 0;
     PG(rocprim::exclusive_scan(nullptr, t2, ws->htc.p, ws->htoff.p, 0ull, (size_t)ngb + 1,
                                rocprim::plus<unsigned long long>(), st));
@@ -6559,6 +6736,12 @@ int kmp_postings_last_layout(const kmp_postings* ws) {
 }
 
 uint32_t kmp_postings_last_overflow_blocks(const kmp_postings* ws) { return ws ? ws->last_ovf : 0u; }
+
+int kmp_postings_set_flat_heavy(kmp_postings* ws, int enable) {
+    if (!ws) return KMP_EINVAL;
+    ws->flat_heavy = enable ? 1 : 0;
+    return KMP_OK;
+}
 
 int kmp_postings_set_direct(kmp_postings* ws, int enable) {
     if (!ws) return KMP_EINVAL;

@@ -129,6 +129,10 @@ class KmerPairEngine:
         """kmp_pairs_stream's fused reduction writes its edges in place (default) or stages them."""
         self._check(lib().kmp_ctx_set_direct_tail(self._ctx, int(enable)), "kmp_ctx_set_direct_tail")
 
+    def set_flat_heavy(self, enable: bool = True) -> None:
+        """pairs_stream's passes expand frequent k-mers by rows (default) or by per-k-mer tiles."""
+        self._check(lib().kmp_ctx_set_flat_heavy(self._ctx, int(enable)), "kmp_ctx_set_flat_heavy")
+
     @property
     def last_tail_windows(self) -> int:
         """Sub-blocks of the last pairs_stream reduced in windows (above the LDS sort capacity)."""
