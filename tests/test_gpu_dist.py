@@ -98,7 +98,7 @@ def worker(rank, world, port, out_q):
             n = D.kmer_split_step(pipe5, rank, world, gather=True, state=state5)
             if rank == 0:
                 out_q.put(("heavy", n == g["n_edges"] and edges_sha256(*pipe5.edges()) == g["edges_sha256"],
-                           state5.row_split, state5.reruns))
+                           state5.row_split, state5.reruns, list(state5.rerun_flags)))
     except BaseException as e:  # the test fails at once instead of waiting out its queue
         out_q.put(("error", rank, repr(e)))
         raise

@@ -12,7 +12,8 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 # KMP_LIB: an alternative build of the same library (tools/_ab_kernels.sh A/B timing only)
-LIB_PATH = os.environ.get("KMP_LIB") or os.path.join(HERE, "lib", "libkmerpair.so")
+_DEFAULT_LIB = os.path.join(HERE, "lib", "libkmerpair.so")
+LIB_PATH = os.environ.get("KMP_LIB") or _DEFAULT_LIB
 HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "kmerpair.h")
 
 KMP_OK, KMP_EINVAL, KMP_ENOMEM, KMP_EDEVICE, KMP_ERCCL, KMP_EOVERFLOW, KMP_ESTATE, KMP_EIO = range(8)
@@ -242,7 +243,10 @@ def lib():
                 "(hipcc --offload-arch=gfx950); the k-mer pair path has no CPU fallback")
         _bind_hip_runtime()
         L = C.CDLL(LIB_PATH)
+        ab = LIB_PATH != _DEFAULT_LIB  # an A/B variant (KMP_LIB) may predate newer entry points
         for name, (res, args) in SIGNATURES.items():
+            if ab and not hasattr(L, name):
+                continue
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -2184,7 +2184,10 @@ constexpr int kBucketLargeCap = 4096, kBucketLargeThreads = 1024, kBucketLargeTa
 // the large kernel grid-strides the list of large buckets (usually empty at config 3; most
 // buckets of a k = 5 batch of real proteins): four workgroups per CU (one per CU measured 8 % slower)
 constexpr int kBucketLargeGrid = 1024;
-constexpr uint32_t kVregTries = 3;  // learned bucket layouts in a row before the counting partition
+#ifndef KMP_VREG_TRIES
+#define KMP_VREG_TRIES 3
+#endif
+constexpr uint32_t kVregTries = KMP_VREG_TRIES;  // learned bucket layouts in a row before the counting partition
 
 // ------------------------------------------------------------- bucket partition ------------
 // The residue path groups its keys by bucket (the top bbits of h) with two counting passes
@@ -5262,9 +5265,19 @@ template <bool kKbit>
 __global__ __launch_bounds__(kPtRThreads) void pt_reduce_direct_kernel(const uint32_t* __restrict__ keys, BlkSrc bs,
                                                                        PtGeom g, unsigned long long* __restrict__ lb,
                                                                        PtDirectOut out, const uint32_t* __restrict__ wc,
-                                                                       unsigned long long* __restrict__ total) {
+                                                                       uint32_t nd, unsigned long long* __restrict__ total) {
     __shared__ PtDirectLds L;
-    const uint32_t d = blockIdx.x;
+    __shared__ uint32_t s_d;
+    // persistent: the sub-blocks are taken in ticket order (total[2]), so every predecessor of a
+    // sub-block is held by a running workgroup.  By block index, one XCD's dispatch running ahead
+    // of another's filled its CUs with workgroups polling for predecessors not yet dispatched
+    // (the sub-blocks of a pass number ~4e5: 3.3x slower than the staged reduce at config 5).
+    for (;;) {
+    __syncthreads();  // the last sub-block's LDS reads are done
+    if (threadIdx.x == 0) s_d = (uint32_t)atomicAdd(&total[2], 1ull);
+    __syncthreads();
+    const uint32_t d = s_d;
+    if (d >= nd) break;
     uint32_t s0, n, r;
     blk_of(bs, d, s0, n, r);
     const uint32_t* src = blk_keys(bs, d, keys);
@@ -5291,7 +5304,8 @@ __global__ __launch_bounds__(kPtRThreads) void pt_reduce_direct_kernel(const uin
         pt_windows<kKbit>(L, src, s0, n, r, g, true, (uint32_t)e, out);
         if (threadIdx.x == 0) atomicAdd(&total[1], 1ull);  // windowed sub-blocks (a statistic)
     }
-    if (d + 1 == gridDim.x && threadIdx.x == 0) total[0] = agg;  // inclusive: the pass's edges
+    if (d + 1 == nd && threadIdx.x == 0) total[0] = agg;  // inclusive: the pass's edges
+    }
 }
 
 // one call's parameters
@@ -6258,15 +6272,16 @@ int tail_direct(kmp_postings* w0, const StepCfg& c, const PtGeom& g, uint32_t nd
     // dsc's run counts | offsets regions (the staged path's) hold the windows' kept counts | the
     // list of the oversized sub-blocks (pt_split)
     uint32_t *wc = drow + nd, *ovl = wc + nd + 1;
-    unsigned long long* tot = w0->dlb.p + nd;  // | windowed sub-blocks
-    PG(hipMemsetAsync(tot, 0, 2 * sizeof(unsigned long long), st));
+    unsigned long long* tot = w0->dlb.p + nd;  // | windowed sub-blocks | ticket
+    PG(hipMemsetAsync(tot, 0, 3 * sizeof(unsigned long long), st));
+    const uint32_t grid = std::min<uint32_t>(nd, 2048);  // persistent (2 resident per CU)
     constexpr uint32_t kWcGrid = 1024;
     if (g.kbit) {
         pt_window_count_kernel<true><<<kWcGrid, kPtRThreads, 0, st>>>(w0->k2.p, bs, g, ovl, wc);
-        pt_reduce_direct_kernel<true><<<nd, kPtRThreads, 0, st>>>(w0->k2.p, bs, g, w0->dlb.p, out, wc, tot);
+        pt_reduce_direct_kernel<true><<<grid, kPtRThreads, 0, st>>>(w0->k2.p, bs, g, w0->dlb.p, out, wc, nd, tot);
     } else {
         pt_window_count_kernel<false><<<kWcGrid, kPtRThreads, 0, st>>>(w0->k2.p, bs, g, ovl, wc);
-        pt_reduce_direct_kernel<false><<<nd, kPtRThreads, 0, st>>>(w0->k2.p, bs, g, w0->dlb.p, out, wc, tot);
+        pt_reduce_direct_kernel<false><<<grid, kPtRThreads, 0, st>>>(w0->k2.p, bs, g, w0->dlb.p, out, wc, nd, tot);
     }
     PG(hipGetLastError());
     unsigned long long h[2] = {0, 0};
@@ -6341,7 +6356,7 @@ int tail_multi(kmp_postings* const* ws, uint32_t nk, const StepCfg& c, const uin
                                                   w0->k2.p, dstart, dsize, drow, deoff);
     const BlkSrc bs{dstart, dsize, drow, keys32};
     if (direct) {
-        PG(w0->dlb.reserve((uint64_t)nd + 2));
+        PG(w0->dlb.reserve((uint64_t)nd + 3));
         PG(hipMemsetAsync(w0->dlb.p, 0, (size_t)nd * sizeof(unsigned long long), st));
         w0->pend_g = g;
         w0->pend_nd = nd;

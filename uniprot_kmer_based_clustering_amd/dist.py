@@ -114,6 +114,7 @@ class SplitState:
         self.host_flags = None  # pinned (CUDA) host copy of the reduced flags, copied asynchronously
         self.row_split = False
         self.reruns = 0
+        self.rerun_flags = []  # the reduced flags of each rerun (diagnostics)
 
 
 def _pipe_state(pipe) -> SplitState:
@@ -183,6 +184,7 @@ def kmer_split_step(pipe, rank: int, world: int, group=None, min_shared: int = 1
             return distributed_step(pipe, rank, world, group, min_shared, require_class_diff)
         if fl[_lib.KMP_SPLIT_RERUN] or fl[_lib.KMP_SPLIT_HEAVY]:  # HEAVY: the heavy path on every rank
             st.reruns += 1
+            st.rerun_flags.append(fl)
             st.learn = fl
             if fl[_lib.KMP_SPLIT_MAX_PART] > st.cap:
                 st.cap = fl[_lib.KMP_SPLIT_MAX_PART] + fl[_lib.KMP_SPLIT_MAX_PART] // 16 + 1024
