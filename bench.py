@@ -79,6 +79,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="oracle threads of the all-cores run (0: every usable core)")
     ap.add_argument("--score", default="blosum", choices=["blosum", "count"], help="config5: edge score")
     ap.add_argument("--split", default="kmer", choices=["kmer", "rows"], help="multi-GPU flow (N > 1)")
+    ap.add_argument("--direct-tail", type=int, default=1, help="config5: fused reduction writes edges in place (A/B)")
+    ap.add_argument("--flat-heavy", type=int, default=1, help="config5: passes expand frequent k-mers by rows (A/B)")
     return ap.parse_args()
 
 
@@ -237,6 +239,8 @@ def bench_config5(args):
     lo, hi = (int(x) for x in _lib.row_split(n, world)[rank:rank + 2])
     with K.KmerPairEngine(local, 16) as e:
         e.load(proteins)
+        e.set_direct_tail(bool(args.direct_tail))
+        e.set_flat_heavy(bool(args.flat_heavy))
         if world > 1:
             e.set_rows(lo, hi)
         for _ in range(warmup):

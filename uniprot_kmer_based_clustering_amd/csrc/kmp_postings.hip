@@ -4975,6 +4975,12 @@ __global__ __launch_bounds__(kFtThreads) void pt_reduce_dense_kernel(const uint3
     }
 }
 
+#ifndef KMP_DIRECT_NOLB
+#define KMP_DIRECT_NOLB 0
+#endif
+#ifndef KMP_DIRECT_NOWRITE
+#define KMP_DIRECT_NOWRITE 0
+#endif
 // The fused multi-k tail with its edges written in place (no staging, no offsets scan, no emit
 // kernel): one workgroup per sub-block, in canonical order, reduces its keys like
 // pt_reduce_scored_block and takes its output offset from a decoupled look-back over the
@@ -5099,12 +5105,19 @@ __device__ __forceinline__ void pt_direct_block(PtDirectLds& L, typename PtSort<
         block_scan_n<kPtRThreads>(kept, ex, total, L.wave_tot);
     }
     if (threadIdx.x < 64) {
+#if KMP_DIRECT_NOLB  // A/B timing builds only (wrong offsets): no look-back
+        const unsigned long long ex = 0;
+#else
         const unsigned long long ex = ft_lookback(lb, d, total);
+#endif
         if (threadIdx.x == 0) L.s_excl = ex;
     }
     __syncthreads();
     const uint64_t ex = (uint32_t)L.s_excl;
     agg_out = L.s_excl + total;
+#if KMP_DIRECT_NOWRITE  // A/B timing builds only (no output)
+    if (out.cap) return;
+#endif
     const uint32_t qm = (1u << g.pbits) - 1;
     // rounds of kPtRThreads runs, thread t the round's run t; filter: the kept runs compacted
     // (a block scan per round — uniform trip count)
