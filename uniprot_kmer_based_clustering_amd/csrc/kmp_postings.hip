@@ -2574,8 +2574,13 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scatter2_kernel(const unsigned
 struct CurGeom {
     uint32_t capb;         // keys per bucket region
     const uint32_t* vreg;  // learned layout (nullptr: fixed): bucket b's region [vreg[b], vreg[b + 1])
+#if KMP_CURGEOM_FIXED  // A/B timing builds only: the fixed layout compiled in (a learned one is wrong)
+    __device__ uint32_t region(uint32_t b) const { return b * capb; }
+    __device__ uint32_t cap(uint32_t) const { return capb; }
+#else
     __device__ uint32_t region(uint32_t b) const { return vreg ? vreg[b] : b * capb; }
     __device__ uint32_t cap(uint32_t b) const { return vreg ? vreg[b + 1] - vreg[b] : capb; }
+#endif
 };
 
 // lh holds the tile's digit histogram and r[e] every key's rank in its digit: reserve each digit's
@@ -3357,7 +3362,11 @@ hipError_t bp_level1(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_r
                                                                      KMP_L1_THREADS, 0) != hipSuccess ||
                         per_cu < 1))
             per_cu = 2;
+#if KMP_L1P_FULLGRID  // A/B timing: one workgroup per chunk, chunks in dispatch order
+        const uint32_t grid = G;
+#else
         const uint32_t grid = std::min<uint32_t>(G, (uint32_t)per_cu * device_cus());
+#endif
         if (nown) {
             bp_scatter1p_kernel<KMP_L1_THREADS><<<grid, KMP_L1_THREADS, 0, st>>>(
                 d_res, d_res_off, d_class, k, n, slots, G, reinterpret_cast<const uint4*>(ws->chunk_desc.p), lay, dg,
