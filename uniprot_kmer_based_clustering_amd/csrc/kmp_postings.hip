@@ -2574,13 +2574,12 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scatter2_kernel(const unsigned
 struct CurGeom {
     uint32_t capb;         // keys per bucket region
     const uint32_t* vreg;  // learned layout (nullptr: fixed): bucket b's region [vreg[b], vreg[b + 1])
-#if KMP_CURGEOM_FIXED  // A/B timing builds only: the fixed layout compiled in (a learned one is wrong)
-    __device__ uint32_t region(uint32_t b) const { return b * capb; }
-    __device__ uint32_t cap(uint32_t) const { return capb; }
-#else
-    __device__ uint32_t region(uint32_t b) const { return vreg ? vreg[b] : b * capb; }
-    __device__ uint32_t cap(uint32_t b) const { return vreg ? vreg[b + 1] - vreg[b] : capb; }
-#endif
+    // bucket b's region and capacity; the level-2 kernels take kVreg as a template argument: a
+    // run-time choice per key cost bp_scatter2g 138 -> 230 us at config 3
+    template <bool kVreg>
+    __device__ __forceinline__ uint32_t region(uint32_t b) const { return kVreg ? vreg[b] : b * capb; }
+    template <bool kVreg>
+    __device__ __forceinline__ uint32_t cap(uint32_t b) const { return kVreg ? vreg[b + 1] - vreg[b] : capb; }
 };
 
 // lh holds the tile's digit histogram and r[e] every key's rank in its digit: reserve each digit's
@@ -2645,6 +2644,7 @@ __device__ __forceinline__ void bp_place_cur(const unsigned long long (&x)[kPer]
 
 // level 2, cursor variant: tile (j, c) of coarse bin c as bp_scatter2, each digit's run reserved
 // in its bucket's region; bcur[b] counts bucket b
+template <bool kVreg>
 __global__ __launch_bounds__(kKeyThreads) void bp_scatter2c_kernel(const unsigned long long* __restrict__ in,
                                                                    const uint32_t* __restrict__ C1, uint32_t J,
                                                                    BpDigits dg, CurGeom cg,
@@ -2687,7 +2687,8 @@ __global__ __launch_bounds__(kKeyThreads) void bp_scatter2c_kernel(const unsigne
     const uint32_t bb = c * dg.nb2;
     bp_place_cur(
         x, r, tn, dg.nb2, digit, [&](uint32_t d) { return &bcur[bb + d]; },
-        [&](uint32_t d) { return cg.region(bb + d); }, [&](uint32_t d) { return cg.cap(bb + d); }, lh, wave_tot, S,
+        [&](uint32_t d) { return cg.region<kVreg>(bb + d); }, [&](uint32_t d) { return cg.cap<kVreg>(bb + d); }, lh,
+        wave_tot, S,
         out, flags);
 }
 
@@ -2953,7 +2954,7 @@ __global__ __launch_bounds__(256) void bp_h1t_kernel(const uint32_t* __restrict_
 // takes the tiles [x * per, (x + 1) * per) of the bin-major tile list, so neighbouring bins' tiles
 // of a chunk range (whose runs share the 128-B lines at their ends) run on one L2 at about the
 // same time.
-template <uint32_t kPer, uint32_t kThr>
+template <uint32_t kPer, uint32_t kThr, bool kVreg>
 __global__ __launch_bounds__(kThr) void bp_scatter2g_kernel(const unsigned long long* __restrict__ in,
                                                                    const uint32_t* __restrict__ H1T, uint32_t G,
                                                                    uint32_t hsb, uint32_t hsc,
@@ -2992,8 +2993,8 @@ __global__ __launch_bounds__(kThr) void bp_scatter2g_kernel(const unsigned long 
     auto digit = [&](unsigned long long y) { return (uint32_t)(y >> dg.sh2) & dg.m2; };
     const uint32_t bb = c * dg.nb2;
     auto cursor = [&](uint32_t d) { return &bcur[bb + d]; };
-    auto region = [&](uint32_t d) { return cg.region(bb + d); };
-    auto capof = [&](uint32_t d) { return cg.cap(bb + d); };
+    auto region = [&](uint32_t d) { return cg.region<kVreg>(bb + d); };
+    auto capof = [&](uint32_t d) { return cg.cap<kVreg>(bb + d); };
     for (uint32_t base = 0; base < tn; base += kTile) {
         if (base) __syncthreads();  // the previous round's writes have read lh and S
         const uint32_t n_in = min(kTile, tn - base);
@@ -3362,11 +3363,9 @@ hipError_t bp_level1(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_r
                                                                      KMP_L1_THREADS, 0) != hipSuccess ||
                         per_cu < 1))
             per_cu = 2;
-#if KMP_L1P_FULLGRID  // A/B timing: one workgroup per chunk, chunks in dispatch order
-        const uint32_t grid = G;
-#else
-        const uint32_t grid = std::min<uint32_t>(G, (uint32_t)per_cu * device_cus());
-#endif
+        // every bin owned (one GPU): one workgroup per chunk, in order (bp_scatter1p 112 -> 103 us at
+        // config 3); a share of the bins (a rank of the k-mer split, little work per chunk): persistent
+        const uint32_t grid = nown >= dg.nb1 ? G : std::min<uint32_t>(G, (uint32_t)per_cu * device_cus());
         if (nown) {
             bp_scatter1p_kernel<KMP_L1_THREADS><<<grid, KMP_L1_THREADS, 0, st>>>(
                 d_res, d_res_off, d_class, k, n, slots, G, reinterpret_cast<const uint4*>(ws->chunk_desc.p), lay, dg,
@@ -3436,12 +3435,23 @@ int bp_level2c(kmp_postings* ws, const Layout& lay, hipStream_t st) {
         bp_cur_clear_kernel<<<std::min<uint32_t>((nb + 1023) / 1024, 1024), 1024, 0, st>>>(ws->cur.p, nb);
     if (c1 > c0 && ws->bp_local) {
         const uint32_t ntiles = (ws->bp_G + ws->bp_T - 1) / ws->bp_T, per = (ntiles * (c1 - c0) + 7) / 8;
-        bp_scatter2g_kernel<kBpGatherTile / KMP_GATHER_THREADS, KMP_GATHER_THREADS><<<8 * per, KMP_GATHER_THREADS, 0, st>>>(ws->keys.p, ws->bp.p + ws->bp_h1t, ws->bp_G, ws->bp_hsb, ws->bp_hsc, ws->bp_T,
-                                                             ntiles, c1 - c0, dg, ws->cg, ws->cur.p, ws->sorted.p,
-                                                             ws->flags.p, c0, c0);
-    } else if (c1 > c0)
-        bp_scatter2c_kernel<<<dim3(ws->bp_J, c1 - c0), kKeyThreads, 0, st>>>(ws->keys.p, C1, ws->bp_J, dg, ws->cg,
-                                                                            ws->cur.p, ws->sorted.p, ws->flags.p, c0);
+        constexpr uint32_t kGp = kBpGatherTile / KMP_GATHER_THREADS, kGt = KMP_GATHER_THREADS;
+        if (ws->cg.vreg)
+            bp_scatter2g_kernel<kGp, kGt, true><<<8 * per, kGt, 0, st>>>(
+                ws->keys.p, ws->bp.p + ws->bp_h1t, ws->bp_G, ws->bp_hsb, ws->bp_hsc, ws->bp_T, ntiles, c1 - c0, dg, ws->cg,
+                ws->cur.p, ws->sorted.p, ws->flags.p, c0, c0);
+        else
+            bp_scatter2g_kernel<kGp, kGt, false><<<8 * per, kGt, 0, st>>>(
+                ws->keys.p, ws->bp.p + ws->bp_h1t, ws->bp_G, ws->bp_hsb, ws->bp_hsc, ws->bp_T, ntiles, c1 - c0, dg, ws->cg,
+                ws->cur.p, ws->sorted.p, ws->flags.p, c0, c0);
+    } else if (c1 > c0) {
+        if (ws->cg.vreg)
+            bp_scatter2c_kernel<true><<<dim3(ws->bp_J, c1 - c0), kKeyThreads, 0, st>>>(
+                ws->keys.p, C1, ws->bp_J, dg, ws->cg, ws->cur.p, ws->sorted.p, ws->flags.p, c0);
+        else
+            bp_scatter2c_kernel<false><<<dim3(ws->bp_J, c1 - c0), kKeyThreads, 0, st>>>(
+                ws->keys.p, C1, ws->bp_J, dg, ws->cg, ws->cur.p, ws->sorted.p, ws->flags.p, c0);
+    }
     PG(hipGetLastError());
     return KMP_OK;
 }
@@ -5006,7 +5016,11 @@ struct PtDirectOut {
     uint32_t *d_p, *d_q, *d_w, *d_s, *d_w0, *d_w1;
     uint64_t cap;
     uint32_t stride;
+    unsigned long long* prof;  // KMP_DIRECT_PROF builds: 100 MHz ticks in sort | look-back | writes, blocks, radix
 };
+#ifndef KMP_DIRECT_PROF
+#define KMP_DIRECT_PROF 0
+#endif
 struct PtDirectLds {
     union {
         typename PtSort<2>::storage_type s2;
@@ -5051,6 +5065,9 @@ __device__ __forceinline__ void pt_direct_block(PtDirectLds& L, typename PtSort<
                                                 const uint32_t* __restrict__ src, uint32_t s0, uint32_t n, uint32_t r,
                                                 uint32_t d, const PtGeom& g, unsigned long long* __restrict__ lb,
                                                 const PtDirectOut& out, unsigned long long& agg_out) {
+#if KMP_DIRECT_PROF
+    const unsigned long long t0 = wall_clock64();
+#endif
     uint32_t k[kE];
 #pragma unroll
     for (uint32_t e = 0; e < kE; ++e) {
@@ -5059,8 +5076,12 @@ __device__ __forceinline__ void pt_direct_block(PtDirectLds& L, typename PtSort<
     }
     const unsigned sb = g.sbits;
     const uint32_t rowbase = g.row0 + (r << g.rbits);
-    if (!g.binsort || !pt_bin_sort<kE>(k, n, g, rowbase, L.b, L.last, L.last + 2 * kPtRThreads / 64, L.wave_tot))
+    if (!g.binsort || !pt_bin_sort<kE>(k, n, g, rowbase, L.b, L.last, L.last + 2 * kPtRThreads / 64, L.wave_tot)) {
         PtSort<kE>().sort(k, st, 0, g.pbits + sb + g.rbits + 1);  // blocked: thread t holds ranks t*kE + e
+#if KMP_DIRECT_PROF
+        if (threadIdx.x == 0) atomicAdd(&out.prof[4], 1ull);
+#endif
+    }
     L.last[threadIdx.x] = k[kE - 1] >> sb;
     __syncthreads();
     const uint32_t rank0 = threadIdx.x * kE, smask = (1u << kScoreBits) - 1;
@@ -5113,6 +5134,9 @@ __device__ __forceinline__ void pt_direct_block(PtDirectLds& L, typename PtSort<
         uint32_t ex;
         block_scan_n<kPtRThreads>(kept, ex, total, L.wave_tot);
     }
+#if KMP_DIRECT_PROF
+    const unsigned long long t1 = wall_clock64();
+#endif
     if (threadIdx.x < 64) {
 #if KMP_DIRECT_NOLB  // A/B timing builds only (wrong offsets): no look-back
         const unsigned long long ex = 0;
@@ -5122,6 +5146,9 @@ __device__ __forceinline__ void pt_direct_block(PtDirectLds& L, typename PtSort<
         if (threadIdx.x == 0) L.s_excl = ex;
     }
     __syncthreads();
+#if KMP_DIRECT_PROF
+    const unsigned long long t2 = wall_clock64();
+#endif
     const uint64_t ex = (uint32_t)L.s_excl;
     agg_out = L.s_excl + total;
 #if KMP_DIRECT_NOWRITE  // A/B timing builds only (no output)
@@ -5173,6 +5200,15 @@ __device__ __forceinline__ void pt_direct_block(PtDirectLds& L, typename PtSort<
     rounds([&](uint32_t i, uint64_t at, uint32_t, uint32_t) {
         if (at < out.cap) out.d_s[at * out.stride] = L.r.P[i + 1] - L.r.P[i];
     });
+#if KMP_DIRECT_PROF
+    if (threadIdx.x == 0) {
+        const unsigned long long t3 = wall_clock64();
+        atomicAdd(&out.prof[0], t1 - t0);
+        atomicAdd(&out.prof[1], t2 - t1);
+        atomicAdd(&out.prof[2], t3 - t2);
+        atomicAdd(&out.prof[3], 1ull);
+    }
+#endif
 }
 
 // a sub-block above kPtCap: windows of kDwWin pair positions (the monotone position of pt_bin_sort),
@@ -6290,12 +6326,12 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
 int tail_direct(kmp_postings* w0, const StepCfg& c, const PtGeom& g, uint32_t nd, uint64_t* ne, hipStream_t st) {
     uint32_t *dstart = w0->dsc.p, *dsize = dstart + nd, *drow = dsize + nd;
     const BlkSrc bs{dstart, dsize, drow, reinterpret_cast<const uint32_t*>(w0->inc.p)};
-    const PtDirectOut out{c.d_p, c.d_q, c.d_w, c.d_s, c.d_w0, c.d_w1, c.cap, c.stride};
+    const PtDirectOut out{c.d_p, c.d_q, c.d_w, c.d_s, c.d_w0, c.d_w1, c.cap, c.stride, w0->dlb.p + nd + 3};
     // dsc's run counts | offsets regions (the staged path's) hold the windows' kept counts | the
     // list of the oversized sub-blocks (pt_split)
     uint32_t *wc = drow + nd, *ovl = wc + nd + 1;
     unsigned long long* tot = w0->dlb.p + nd;  // | windowed sub-blocks | ticket
-    PG(hipMemsetAsync(tot, 0, 3 * sizeof(unsigned long long), st));
+    PG(hipMemsetAsync(tot, 0, (KMP_DIRECT_PROF ? 8 : 3) * sizeof(unsigned long long), st));
     const uint32_t grid = std::min<uint32_t>(nd, 2048);  // persistent (2 resident per CU)
     constexpr uint32_t kWcGrid = 1024;
     if (g.kbit) {
@@ -6311,6 +6347,15 @@ int tail_direct(kmp_postings* w0, const StepCfg& c, const PtGeom& g, uint32_t nd
     PG(hipStreamSynchronize(st));
     *ne = (uint32_t)h[0];
     w0->last_ovf = (uint32_t)h[1];
+#if KMP_DIRECT_PROF
+    {
+        unsigned long long pf[5];
+        PG(hipMemcpy(pf, tot + 3, sizeof(pf), hipMemcpyDeviceToHost));
+        fprintf(stderr, "kmp direct: nd %u blocks %llu radix %llu | per block us: sort %.2f lookback %.2f write %.2f\n", nd,
+                pf[3], pf[4], pf[0] / 100.0 / std::max(1ull, pf[3]), pf[1] / 100.0 / std::max(1ull, pf[3]),
+                pf[2] / 100.0 / std::max(1ull, pf[3]));
+    }
+#endif
     return KMP_OK;
 }
 
@@ -6378,7 +6423,7 @@ int tail_multi(kmp_postings* const* ws, uint32_t nk, const StepCfg& c, const uin
                                                   w0->k2.p, dstart, dsize, drow, deoff);
     const BlkSrc bs{dstart, dsize, drow, keys32};
     if (direct) {
-        PG(w0->dlb.reserve((uint64_t)nd + 3));
+        PG(w0->dlb.reserve((uint64_t)nd + 8));
         PG(hipMemsetAsync(w0->dlb.p, 0, (size_t)nd * sizeof(unsigned long long), st));
         w0->pend_g = g;
         w0->pend_nd = nd;
