@@ -3168,12 +3168,13 @@ struct kmp_postings {
     uint32_t pend_nd = 0;
     uint64_t pend_total = 0, pend_ne = 0;
     std::vector<unsigned long long> pend_key;
-    // the fused tail writes its edges in place (pt_reduce_direct_kernel); 0: staged runs + emit
+    // the fused tail writes its edges in place (pt_reduce_count + pt_reduce_write); 0: staged runs + emit
     int direct_tail = 1;
     int flat_heavy = 1;  // ranged plain-order heavy expansion by rows (heavy_flat_kernel); 0: tiles
     bool pend_direct = false;  // the pending re-emit reruns the in-place reduce (its keys still held)
     PtGeom pend_g{};
-    Grow<unsigned long long> dlb;  // its look-back words (one per sub-block) | the pass's edge count
+    Grow<unsigned long long> dlb;  // its statistics (windowed sub-blocks)
+    Grow<uint32_t> doff;           // its sub-blocks' edge offsets
     Grow<unsigned long long> split_cur;  // k-mer split: per-destination send cursors
     std::vector<unsigned long long> split_shape;
     bool split_heavy = false;  // k-mer split: this batch spills, its heavy path runs on every call
@@ -5000,33 +5001,20 @@ __global__ __launch_bounds__(kFtThreads) void pt_reduce_dense_kernel(const uint3
     }
 }
 
-#ifndef KMP_DIRECT_NOLB
-#define KMP_DIRECT_NOLB 0
-#endif
-#ifndef KMP_DIRECT_NOWRITE
-#define KMP_DIRECT_NOWRITE 0
-#endif
-// The fused multi-k tail with its edges written in place (no staging, no offsets scan, no emit
-// kernel): one workgroup per sub-block, in canonical order, reduces its keys like
-// pt_reduce_scored_block and takes its output offset from a decoupled look-back over the
-// sub-blocks before it (ft_lookback), then writes (p, q, w, score, w0, w1) coalesced, one run per
-// thread: the runs' first ranks (| k-bit scan << 16) and pair keys sit in LDS (H, P), then P is
-// overwritten with the score scan at the heads for the score column.  A sub-block above kPtCap
-// (a fine bin of pt_split above kPtCap - kSbChunk keys: a row pairing many times with a few
-// partners) is reduced in place in windows of kDwWin pair positions — per position a count
-// (| w1 << 16) and a score sum in LDS, the windows visiting only occupied positions, twice: the
-// kept count first (the look-back needs it), then the writes — so no block leaves the kernel and no
-// device sort runs.  The last block writes the pass's edge count to *total.
+// The fused multi-k tail with its edges written in place (no staging and no emit kernel): the
+// sub-blocks of a pass are sorted in place and their kept runs counted (pt_reduce_count_kernel),
+// the counts scanned on the device, and each sub-block's runs written at its offset
+// (pt_reduce_write_kernel) as (p, q, w, score, w0, w1) columns.  A sub-block above kPtCap (a fine
+// bin of pt_split above kPtCap - kSbChunk keys: a row pairing many times with a few partners) is
+// reduced in windows of kDwWin pair positions — per position a count (| w1 << 16) and a score sum
+// in LDS, the windows visiting only occupied positions — counted by pt_window_count_kernel and
+// written by the write launch: no device sort anywhere.
 constexpr uint32_t kDwWin = 8192;
 struct PtDirectOut {
     uint32_t *d_p, *d_q, *d_w, *d_s, *d_w0, *d_w1;
     uint64_t cap;
     uint32_t stride;
-    unsigned long long* prof;  // KMP_DIRECT_PROF builds: 100 MHz ticks in sort | look-back | writes, blocks, radix
 };
-#ifndef KMP_DIRECT_PROF
-#define KMP_DIRECT_PROF 0
-#endif
 struct PtDirectLds {
     union {
         typename PtSort<2>::storage_type s2;
@@ -5066,31 +5054,40 @@ __device__ __forceinline__ void pt_direct_write(const PtDirectOut& o, uint64_t a
     }
 }
 
-template <uint32_t kE, bool kKbit>
+// One sub-block of at most kPtCap keys, in two launches with a device scan between them (no
+// look-back: waiting on the predecessors' counts cost as much as the sort at config 5, where the
+// ~4e5 sub-blocks of a pass finish in no particular order).  kWrite false: load, sort (bins, or the
+// block radix sort), store the sorted keys back in place, count the kept runs into *wc.  kWrite
+// true: load the sorted keys (thread t: ranks t kE + e), encode, and write the runs from edge
+// offset ex: the runs' first ranks (| k-bit scan << 16) and pair keys sit in LDS (H, P), then P
+// takes the score scan at the heads for the score column; one run per thread per round, coalesced.
+template <uint32_t kE, bool kKbit, bool kWrite>
 __device__ __forceinline__ void pt_direct_block(PtDirectLds& L, typename PtSort<kE>::storage_type& st,
-                                                const uint32_t* __restrict__ src, uint32_t s0, uint32_t n, uint32_t r,
-                                                uint32_t d, const PtGeom& g, unsigned long long* __restrict__ lb,
-                                                const PtDirectOut& out, unsigned long long& agg_out) {
-#if KMP_DIRECT_PROF
-    const unsigned long long t0 = wall_clock64();
-#endif
+                                                uint32_t* __restrict__ src, uint32_t s0, uint32_t n, uint32_t r,
+                                                const PtGeom& g, const PtDirectOut& out, uint32_t* __restrict__ wc,
+                                                uint64_t ex) {
     uint32_t k[kE];
-#pragma unroll
-    for (uint32_t e = 0; e < kE; ++e) {
-        const uint32_t i = threadIdx.x + e * kPtRThreads;
-        k[e] = i < n ? src[s0 + i] : 0xFFFFFFFFu;
-    }
     const unsigned sb = g.sbits;
     const uint32_t rowbase = g.row0 + (r << g.rbits);
-    if (!g.binsort || !pt_bin_sort<kE>(k, n, g, rowbase, L.b, L.last, L.last + 2 * kPtRThreads / 64, L.wave_tot)) {
-        PtSort<kE>().sort(k, st, 0, g.pbits + sb + g.rbits + 1);  // blocked: thread t holds ranks t*kE + e
-#if KMP_DIRECT_PROF
-        if (threadIdx.x == 0) atomicAdd(&out.prof[4], 1ull);
-#endif
+    const uint32_t rank0 = threadIdx.x * kE, smask = (1u << kScoreBits) - 1;
+    if (!kWrite) {
+#pragma unroll
+        for (uint32_t e = 0; e < kE; ++e) {
+            const uint32_t i = threadIdx.x + e * kPtRThreads;
+            k[e] = i < n ? src[s0 + i] : 0xFFFFFFFFu;
+        }
+        if (!g.binsort || !pt_bin_sort<kE>(k, n, g, rowbase, L.b, L.last, L.last + 2 * kPtRThreads / 64, L.wave_tot))
+            PtSort<kE>().sort(k, st, 0, g.pbits + sb + g.rbits + 1);  // blocked: thread t holds ranks t*kE + e
+#pragma unroll
+        for (uint32_t e = 0; e < kE; ++e)
+            if (rank0 + e < n) src[s0 + rank0 + e] = k[e];
+    } else {
+#pragma unroll
+        for (uint32_t e = 0; e < kE; ++e) k[e] = rank0 + e < n ? src[s0 + rank0 + e] : 0xFFFFFFFFu;
     }
+    __syncthreads();  // the sort's LDS is dead before last (aliased) is written
     L.last[threadIdx.x] = k[kE - 1] >> sb;
     __syncthreads();
-    const uint32_t rank0 = threadIdx.x * kE, smask = (1u << kScoreBits) - 1;
     uint32_t prev = threadIdx.x ? L.last[threadIdx.x - 1] : 0u, nh = 0, ssum = 0, ksum = 0;
     uint32_t hm = 0;  // head bits
 #pragma unroll
@@ -5105,9 +5102,14 @@ __device__ __forceinline__ void pt_direct_block(PtDirectLds& L, typename PtSort<
             if (kKbit) ksum += (k[e] >> kScoreBits) & 1u;
         }
     }
-    uint32_t base0, nruns, sx0, stot, kx = 0, ktot = 0;
-    block_scan_n<kPtRThreads>(nh, base0, nruns, L.wave_tot);  // barriers: the sort storage is dead
-    block_scan_n<kPtRThreads>(ssum, sx0, stot, L.wave_tot);
+    const bool filter = g.min_shared > 1;
+    uint32_t base0, nruns, sx0 = 0, stot = 0, kx = 0, ktot = 0;
+    block_scan_n<kPtRThreads>(nh, base0, nruns, L.wave_tot);
+    if (!kWrite && !filter) {  // every run kept: the count is the run count
+        if (threadIdx.x == 0) *wc = nruns;
+        return;
+    }
+    if (kWrite) block_scan_n<kPtRThreads>(ssum, sx0, stot, L.wave_tot);
     if (kKbit) block_scan_n<kPtRThreads>(ksum, kx, ktot, L.wave_tot);
     {
         uint32_t base = base0;
@@ -5123,43 +5125,23 @@ __device__ __forceinline__ void pt_direct_block(PtDirectLds& L, typename PtSort<
     }
     if (threadIdx.x == 0) L.r.H[nruns] = n | (kKbit ? ktot << 16 : 0u);
     __syncthreads();
-    const bool filter = g.min_shared > 1;
     auto run_w = [&](uint32_t i, uint32_t& w, uint32_t& w1) {
         const uint32_t h0 = L.r.H[i], h1 = L.r.H[i + 1];
         w = (h1 & 0xFFFFu) - (h0 & 0xFFFFu);
         w1 = kKbit ? (h1 >> 16) - (h0 >> 16) : 0u;
     };
-    uint32_t total = nruns;
-    if (filter) {
+    if (!kWrite) {  // min_shared > 1: the kept runs
         uint32_t kept = 0;
         for (uint32_t i = threadIdx.x; i < nruns; i += kPtRThreads) {
             uint32_t w, w1;
             run_w(i, w, w1);
             kept += pt_keep(w, w1, kKbit, g.min_shared);
         }
-        uint32_t ex;
-        block_scan_n<kPtRThreads>(kept, ex, total, L.wave_tot);
+        uint32_t e, total;
+        block_scan_n<kPtRThreads>(kept, e, total, L.wave_tot);
+        if (threadIdx.x == 0) *wc = total;
+        return;
     }
-#if KMP_DIRECT_PROF
-    const unsigned long long t1 = wall_clock64();
-#endif
-    if (threadIdx.x < 64) {
-#if KMP_DIRECT_NOLB  // A/B timing builds only (wrong offsets): no look-back
-        const unsigned long long ex = 0;
-#else
-        const unsigned long long ex = ft_lookback(lb, d, total);
-#endif
-        if (threadIdx.x == 0) L.s_excl = ex;
-    }
-    __syncthreads();
-#if KMP_DIRECT_PROF
-    const unsigned long long t2 = wall_clock64();
-#endif
-    const uint64_t ex = (uint32_t)L.s_excl;
-    agg_out = L.s_excl + total;
-#if KMP_DIRECT_NOWRITE  // A/B timing builds only (no output)
-    if (out.cap) return;
-#endif
     const uint32_t qm = (1u << g.pbits) - 1;
     // rounds of kPtRThreads runs, thread t the round's run t; filter: the kept runs compacted
     // (a block scan per round — uniform trip count)
@@ -5206,15 +5188,6 @@ __device__ __forceinline__ void pt_direct_block(PtDirectLds& L, typename PtSort<
     rounds([&](uint32_t i, uint64_t at, uint32_t, uint32_t) {
         if (at < out.cap) out.d_s[at * out.stride] = L.r.P[i + 1] - L.r.P[i];
     });
-#if KMP_DIRECT_PROF
-    if (threadIdx.x == 0) {
-        const unsigned long long t3 = wall_clock64();
-        atomicAdd(&out.prof[0], t1 - t0);
-        atomicAdd(&out.prof[1], t2 - t1);
-        atomicAdd(&out.prof[2], t3 - t2);
-        atomicAdd(&out.prof[3], 1ull);
-    }
-#endif
 }
 
 // a sub-block above kPtCap: windows of kDwWin pair positions (the monotone position of pt_bin_sort),
@@ -5325,55 +5298,55 @@ __global__ __launch_bounds__(kPtRThreads) void pt_window_count_kernel(const uint
     }
 }
 
+// count launch: every sub-block of at most kPtCap keys sorted in place and its kept runs counted
+// into wc (the larger ones: pt_window_count_kernel; stat[0] counts them)
 template <bool kKbit>
-__global__ __launch_bounds__(kPtRThreads) void pt_reduce_direct_kernel(const uint32_t* __restrict__ keys, BlkSrc bs,
-                                                                       PtGeom g, unsigned long long* __restrict__ lb,
-                                                                       PtDirectOut out, const uint32_t* __restrict__ wc,
-                                                                       uint32_t nd, unsigned long long* __restrict__ total) {
+__global__ __launch_bounds__(kPtRThreads) void pt_reduce_count_kernel(uint32_t* __restrict__ keys, BlkSrc bs, PtGeom g,
+                                                                      uint32_t* __restrict__ wc,
+                                                                      unsigned long long* __restrict__ stat) {
     __shared__ PtDirectLds L;
-    __shared__ uint32_t s_d;
-    // persistent: the sub-blocks are taken in ticket order (total[2]), so every predecessor of a
-    // sub-block is held by a running workgroup.  By block index, one XCD's dispatch running ahead
-    // of another's filled its CUs with workgroups polling for predecessors not yet dispatched
-    // (the sub-blocks of a pass number ~4e5: 3.3x slower than the staged reduce at config 5).
-    for (;;) {
-    __syncthreads();  // the last sub-block's LDS reads are done
-    if (threadIdx.x == 0) s_d = (uint32_t)atomicAdd(&total[2], 1ull);
-    __syncthreads();
-    const uint32_t d = s_d;
-    if (d >= nd) break;
+    const uint32_t d = blockIdx.x;
     uint32_t s0, n, r;
     blk_of(bs, d, s0, n, r);
-    const uint32_t* src = blk_keys(bs, d, keys);
-    unsigned long long agg = 0;
-    if (n == 0) {  // an aggregate of zero (the blocks after it sum past it); sub-block 0: the prefix
-        if (d == 0 || d + 1 == nd) {
-            if (threadIdx.x < 64) agg = ft_lookback(lb, d, 0);
-        } else if (threadIdx.x == 0) {
-            lb_store(lb + d, kLbAgg);
-        }
+    uint32_t* src = const_cast<uint32_t*>(blk_keys(bs, d, keys));
+    const PtDirectOut none{};
+    if (n == 0) {
+        if (threadIdx.x == 0) wc[d] = 0;
     } else if (n <= 2 * kPtRThreads) {
-        pt_direct_block<2, kKbit>(L, L.s2, src, s0, n, r, d, g, lb, out, agg);
+        pt_direct_block<2, kKbit, false>(L, L.s2, src, s0, n, r, g, none, wc + d, 0);
     } else if (n <= 4 * kPtRThreads) {
-        pt_direct_block<4, kKbit>(L, L.s4, src, s0, n, r, d, g, lb, out, agg);
+        pt_direct_block<4, kKbit, false>(L, L.s4, src, s0, n, r, g, none, wc + d, 0);
     } else if (n <= 8 * kPtRThreads) {
-        pt_direct_block<8, kKbit>(L, L.s8, src, s0, n, r, d, g, lb, out, agg);
+        pt_direct_block<8, kKbit, false>(L, L.s8, src, s0, n, r, g, none, wc + d, 0);
     } else if (n <= kPtCap) {
-        pt_direct_block<16, kKbit>(L, L.s16, src, s0, n, r, d, g, lb, out, agg);
-    } else {  // counted by pt_window_count_kernel: published at once, then the writes
-        const uint32_t kept = wc[d];
-        if (threadIdx.x < 64) {
-            const unsigned long long e = ft_lookback(lb, d, kept);
-            if (threadIdx.x == 0) L.s_excl = e;
-        }
-        __syncthreads();
-        const unsigned long long e = L.s_excl;
-        agg = e + kept;
-        pt_windows<kKbit>(L, src, s0, n, r, g, true, (uint32_t)e, out);
-        if (threadIdx.x == 0) atomicAdd(&total[1], 1ull);  // windowed sub-blocks (a statistic)
+        pt_direct_block<16, kKbit, false>(L, L.s16, src, s0, n, r, g, none, wc + d, 0);
+    } else if (threadIdx.x == 0) {
+        atomicAdd(&stat[0], 1ull);
     }
-    if (d + 1 == nd && threadIdx.x == 0) total[0] = agg;  // inclusive: the pass's edges
-    }
+}
+
+// write launch: each sub-block's runs at its offset off[d] (the exclusive scan of the counts)
+template <bool kKbit>
+__global__ __launch_bounds__(kPtRThreads) void pt_reduce_write_kernel(uint32_t* __restrict__ keys, BlkSrc bs, PtGeom g,
+                                                                      PtDirectOut out,
+                                                                      const uint32_t* __restrict__ off) {
+    __shared__ PtDirectLds L;
+    const uint32_t d = blockIdx.x;
+    uint32_t s0, n, r;
+    blk_of(bs, d, s0, n, r);
+    uint32_t* src = const_cast<uint32_t*>(blk_keys(bs, d, keys));
+    const uint64_t ex = off[d];
+    if (n == 0) return;
+    if (n <= 2 * kPtRThreads)
+        pt_direct_block<2, kKbit, true>(L, L.s2, src, s0, n, r, g, out, nullptr, ex);
+    else if (n <= 4 * kPtRThreads)
+        pt_direct_block<4, kKbit, true>(L, L.s4, src, s0, n, r, g, out, nullptr, ex);
+    else if (n <= 8 * kPtRThreads)
+        pt_direct_block<8, kKbit, true>(L, L.s8, src, s0, n, r, g, out, nullptr, ex);
+    else if (n <= kPtCap)
+        pt_direct_block<16, kKbit, true>(L, L.s16, src, s0, n, r, g, out, nullptr, ex);
+    else
+        pt_windows<kKbit>(L, src, s0, n, r, g, true, ex, out);
 }
 
 // one call's parameters
@@ -6331,41 +6304,51 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
 // reduced together by the row-block tail of ws[0]: one run per pair over both k, w = its length,
 // w1 = its k-bit entries, score = Σ s — the union of the per-k lists without building or merging
 // them.  Host-synchronous; *n_edges = the kept pairs.
-// the in-place reduce of tail_multi's nd sub-blocks (keys in k2 / inc, descriptors in dsc) into the
-// call's arrays; *ne = the pass's edges (only the first c.cap written)
-int tail_direct(kmp_postings* w0, const StepCfg& c, const PtGeom& g, uint32_t nd, uint64_t* ne, hipStream_t st) {
+// the in-place reduce of tail_multi's nd sub-blocks (keys in k2 / inc, descriptors in dsc): the
+// count launches and the scan (*ne = the pass's edges; one read-back), then (tail_direct_write)
+// the writes into the call's arrays — only the first c.cap edges
+int tail_direct_count(kmp_postings* w0, const PtGeom& g, uint32_t nd, uint64_t* ne, hipStream_t st) {
     uint32_t *dstart = w0->dsc.p, *dsize = dstart + nd, *drow = dsize + nd;
     const BlkSrc bs{dstart, dsize, drow, reinterpret_cast<const uint32_t*>(w0->inc.p)};
-    const PtDirectOut out{c.d_p, c.d_q, c.d_w, c.d_s, c.d_w0, c.d_w1, c.cap, c.stride, w0->dlb.p + nd + 3};
-    // dsc's run counts | offsets regions (the staged path's) hold the windows' kept counts | the
-    // list of the oversized sub-blocks (pt_split)
+    // dsc's run counts | offsets regions (the staged path's): the kept counts | the list of the
+    // oversized sub-blocks (pt_split); the offsets in doff, the statistics in dlb
     uint32_t *wc = drow + nd, *ovl = wc + nd + 1;
-    unsigned long long* tot = w0->dlb.p + nd;  // | windowed sub-blocks | ticket
-    PG(hipMemsetAsync(tot, 0, (KMP_DIRECT_PROF ? 8 : 3) * sizeof(unsigned long long), st));
-    const uint32_t grid = std::min<uint32_t>(nd, 2048);  // persistent (2 resident per CU)
+    PG(w0->doff.reserve((uint64_t)nd + 1));
+    PG(w0->dlb.reserve(2));
+    PG(hipMemsetAsync(wc + nd, 0, sizeof(uint32_t), st));
+    PG(hipMemsetAsync(w0->dlb.p, 0, sizeof(unsigned long long), st));
     constexpr uint32_t kWcGrid = 1024;
     if (g.kbit) {
         pt_window_count_kernel<true><<<kWcGrid, kPtRThreads, 0, st>>>(w0->k2.p, bs, g, ovl, wc);
-        pt_reduce_direct_kernel<true><<<grid, kPtRThreads, 0, st>>>(w0->k2.p, bs, g, w0->dlb.p, out, wc, nd, tot);
+        pt_reduce_count_kernel<true><<<nd, kPtRThreads, 0, st>>>(w0->k2.p, bs, g, wc, w0->dlb.p);
     } else {
         pt_window_count_kernel<false><<<kWcGrid, kPtRThreads, 0, st>>>(w0->k2.p, bs, g, ovl, wc);
-        pt_reduce_direct_kernel<false><<<grid, kPtRThreads, 0, st>>>(w0->k2.p, bs, g, w0->dlb.p, out, wc, nd, tot);
+        pt_reduce_count_kernel<false><<<nd, kPtRThreads, 0, st>>>(w0->k2.p, bs, g, wc, w0->dlb.p);
     }
     PG(hipGetLastError());
-    unsigned long long h[2] = {0, 0};
-    PG(hipMemcpyAsync(h, tot, sizeof(h), hipMemcpyDeviceToHost, st));
+    size_t tb = 0;
+    PG(rocprim::exclusive_scan(nullptr, tb, wc, w0->doff.p, 0u, (size_t)nd + 1, rocprim::plus<uint32_t>(), st));
+    PG(w0->tmp.reserve(std::max(tb, w0->tmp.n)));
+    PG(rocprim::exclusive_scan(w0->tmp.p, tb, wc, w0->doff.p, 0u, (size_t)nd + 1, rocprim::plus<uint32_t>(), st));
+    uint32_t h_ne = 0;
+    unsigned long long h_win = 0;
+    PG(hipMemcpyAsync(&h_ne, w0->doff.p + nd, sizeof(h_ne), hipMemcpyDeviceToHost, st));
+    PG(hipMemcpyAsync(&h_win, w0->dlb.p, sizeof(h_win), hipMemcpyDeviceToHost, st));
     PG(hipStreamSynchronize(st));
-    *ne = (uint32_t)h[0];
-    w0->last_ovf = (uint32_t)h[1];
-#if KMP_DIRECT_PROF
-    {
-        unsigned long long pf[5];
-        PG(hipMemcpy(pf, tot + 3, sizeof(pf), hipMemcpyDeviceToHost));
-        fprintf(stderr, "kmp direct: nd %u blocks %llu radix %llu | per block us: sort %.2f lookback %.2f write %.2f\n", nd,
-                pf[3], pf[4], pf[0] / 100.0 / std::max(1ull, pf[3]), pf[1] / 100.0 / std::max(1ull, pf[3]),
-                pf[2] / 100.0 / std::max(1ull, pf[3]));
-    }
-#endif
+    *ne = h_ne;
+    w0->last_ovf = (uint32_t)h_win;
+    return KMP_OK;
+}
+
+int tail_direct_write(kmp_postings* w0, const StepCfg& c, const PtGeom& g, uint32_t nd, hipStream_t st) {
+    uint32_t *dstart = w0->dsc.p, *dsize = dstart + nd, *drow = dsize + nd;
+    const BlkSrc bs{dstart, dsize, drow, reinterpret_cast<const uint32_t*>(w0->inc.p)};
+    const PtDirectOut out{c.d_p, c.d_q, c.d_w, c.d_s, c.d_w0, c.d_w1, c.cap, c.stride};
+    if (g.kbit)
+        pt_reduce_write_kernel<true><<<nd, kPtRThreads, 0, st>>>(w0->k2.p, bs, g, out, w0->doff.p);
+    else
+        pt_reduce_write_kernel<false><<<nd, kPtRThreads, 0, st>>>(w0->k2.p, bs, g, out, w0->doff.p);
+    PG(hipGetLastError());
     return KMP_OK;
 }
 
@@ -6433,14 +6416,13 @@ int tail_multi(kmp_postings* const* ws, uint32_t nk, const StepCfg& c, const uin
                                                   w0->k2.p, dstart, dsize, drow, deoff);
     const BlkSrc bs{dstart, dsize, drow, keys32};
     if (direct) {
-        PG(w0->dlb.reserve((uint64_t)nd + 8));
-        PG(hipMemsetAsync(w0->dlb.p, 0, (size_t)nd * sizeof(unsigned long long), st));
         w0->pend_g = g;
         w0->pend_nd = nd;
         w0->pend_direct = true;
         w0->last_ovf = 0;
         uint64_t ne = 0;
-        const int rc = tail_direct(w0, c, g, nd, &ne, st);
+        int rc = tail_direct_count(w0, g, nd, &ne, st);
+        if (rc == KMP_OK && ne <= c.cap) rc = tail_direct_write(w0, c, g, nd, st);
         if (rc != KMP_OK) return rc;
         for (uint32_t j = 0; j < nk; ++j) ws[j]->shard_cap = ws[j]->last_most + ws[j]->last_most / 4 + 256;
         w0->pt_inc = T;
@@ -6508,9 +6490,7 @@ int tail_multi_emit(kmp_postings* w0, const StepCfg& c, uint64_t* n_edges, hipSt
     if (w0->pend_direct) {  // the in-place reduce again, into the larger arrays
         *n_edges = w0->pend_ne;
         if (w0->pend_ne > c.cap) return KMP_EOVERFLOW;
-        PG(hipMemsetAsync(w0->dlb.p, 0, (size_t)nd * sizeof(unsigned long long), st));
-        uint64_t ne = 0;
-        return tail_direct(w0, c, w0->pend_g, nd, &ne, st);
+        return tail_direct_write(w0, c, w0->pend_g, nd, st);  // the keys stay sorted in place
     }
     const uint64_t total = w0->pend_total;
     uint32_t *dstart = w0->dsc.p, *dsize = dstart + nd, *drow = dsize + nd, *dcnt = drow + nd, *deoff = dcnt + nd + 1;
