@@ -721,6 +721,9 @@ struct BucketArgs {
     uint64_t send_cap, send_sub;
     unsigned long long* dcur;
     SplitRows rows;
+    // the passes of one batch with the row-driven heavy expansion (heavy_flat_kernel): every bucket
+    // goes to the heavy path whole on the first pass, so later passes launch no bucket kernel
+    int spill_all;
 };
 
 // descriptor: spill index (40 bits) | keys (23 bits) << 40 | whole bucket (several k-mers) << 63
@@ -805,8 +808,8 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
     const Layout& lay = a.lay;
     if (n == 0) return;
     const uint32_t shard = b % kShards;
-    if (n > (uint32_t)kCap) {
-        if (small) {
+    if (n > (uint32_t)kCap || a.spill_all) {
+        if (small && !a.spill_all) {
             if (tid == 0) a.list[atomicAdd(a.list_count, 1u)] = b;  // the large kernel takes it
             return;
         }
@@ -1720,8 +1723,10 @@ __global__ __launch_bounds__(256) void heavy_plan_kernel(const uint32_t* __restr
     const unsigned cb = ho.cb;
     unsigned long long st[kStN] = {0, 0, 0, 0, 0, 0, 0};
     if (g >= ng && g < ngb) {
-        gi[2 * g] = gi[2 * g + 1] = 0;
-        tcount[g] = 0;
+        if (tiles_on) {
+            gi[2 * g] = gi[2 * g + 1] = 0;
+            tcount[g] = 0;
+        }
     }
     if (g < ng) {
         const uint64_t b = GS[g];
@@ -1762,9 +1767,11 @@ __global__ __launch_bounds__(256) void heavy_plan_kernel(const uint32_t* __restr
                 tiles += ps < d ? (d - ps + ho.hj - 1) / ho.hj : 0u;
             }
         }
-        gi[2 * g] = i0;
-        gi[2 * g + 1] = i1;
-        tcount[g] = tiles;
+        if (tiles_on) gi[2 * g] = i0;
+        if (tiles_on) {
+            gi[2 * g + 1] = i1;
+            tcount[g] = tiles;
+        }
         st[kStSumS] = d;
         st[kStDistinct] = 1;
         st[kStRepeat] = d >= 2;
@@ -3171,6 +3178,7 @@ struct kmp_postings {
     // the fused tail writes its edges in place (pt_reduce_count + pt_reduce_write); 0: staged runs + emit
     int direct_tail = 1;
     int flat_heavy = 1;  // ranged plain-order heavy expansion by rows (heavy_flat_kernel); 0: tiles
+    int spill_all_on = 1;  // ... with every bucket spilled on the first pass (no bucket kernel after it)
     bool pend_direct = false;  // the pending re-emit reruns the in-place reduce (its keys still held)
     PtGeom pend_g{};
     Grow<unsigned long long> dlb;  // its statistics (windowed sub-blocks)
@@ -5507,6 +5515,7 @@ BucketArgs bucket_args(kmp_postings* ws, const StepCfg& c, bool spill) {
     a.k = c.k;
     a.sb = c.sb;
     a.sor = c.sor;
+    a.spill_all = c.ranged && ws->reuse && ws->flat_heavy && ws->spill_all_on;
     if (ws->route_send && !c.sb) {
         a.send = ws->route_send;
         a.send_cap = ws->route_cap;
@@ -5570,6 +5579,7 @@ int enqueue_front(kmp_postings* ws, MakeKeys& make_keys, const StepCfg& c, bool 
     // thousand idle 1,024-thread workgroups cost ~5 us); a bucket-range share of the k-mer split
     // lists about 1/parts of them
     const uint32_t lg = ws->bin_hi ? std::max<uint32_t>(64, kBucketLargeGrid * (c1 - c0) / dg.nb1) : ws->large_grid;
+    if (a.spill_all && !a.spill) return KMP_OK;  // every bucket already in the heavy path (a later pass)
     if (c.sb) {
         if (c.ranged) launch_buckets<true, true>(a, b0, nbk, lg, st);
         else launch_buckets<false, true>(a, b0, nbk, lg, st);
@@ -5914,7 +5924,9 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
         ws->h_tot = tot;
     }
     if (ws->h_cls != ho.cls) return KMP_EINVAL;  // (compacted above in this call's order)
+    bool index_built = false;
     if (flat && !ws->h_flat_ready) {
+        index_built = true;
         // once per compaction: the per-protein index (one read-back: the element and k-mer counts)
         unsigned long long ht[2] = {0, 0};
         PG(hipMemcpyAsync(ht, ws->h_tot, sizeof(ht), hipMemcpyDeviceToHost, st));
@@ -5944,21 +5956,17 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
     // bound on the k-mer count (device: h_tot[1]); exact once the flat index read it back
     const uint64_t ngb = flat ? ws->h_ng : ws->h_m;
     if (ngb == 0) return KMP_OK;
-    PG(ws->hgi.reserve(2 * (ngb + 1)));
-    PG(ws->htc.reserve(ngb + 1));
-    PG(ws->htoff.reserve(ngb + 1));
-    PG(ws->hblk.reserve(2 * (ngb + ngb / kHvI + 2)));
-    uint32_t* BT = ws->hblk.p;
-    uint32_t* BP = BT + ngb + ngb / kHvI + 2;
     const uint32_t row_lo = c.ranged ? c.row_lo : 0, row_hi = c.ranged ? c.row_hi : c.n;
     const uint64_t* GS = reinterpret_cast<const uint64_t*>(ws->hGS.p);
     const uint64_t* RH = ho.cls ? reinterpret_cast<const uint64_t*>(ws->hRH.p) : nullptr;
     const uint32_t* RUN = ho.cls ? ws->hrun.p : nullptr;
-    heavy_plan_kernel<<<(uint32_t)((ngb + 1 + 255) / 256), 256, 0, st>>>(
-        ws->hE.p, GS, ngb + 1, ws->h_tot + 1, ho, RUN, RH, ho.cls && !c.ranged ? 1 : 0, row_lo, row_hi, c.heavy_df,
-        stats ? 1 : 0, flat ? 0 : 1, ws->bstats.p,
-        ws->hgi.p, BT, BP, ws->htc.p);
     if (flat) {
+        // the plan only for the k-mers' statistics, on the pass that built the index (they do not
+        // change between the passes; a spill-all batch holds every k-mer, ~10^8 at k = 7)
+        if (stats && index_built)
+            heavy_plan_kernel<<<(uint32_t)((ngb + 1 + 255) / 256), 256, 0, st>>>(
+                ws->hE.p, GS, ngb + 1, ws->h_tot + 1, ho, RUN, RH, 0, row_lo, row_hi, c.heavy_df, 1, 0, ws->bstats.p,
+                nullptr, nullptr, nullptr, nullptr);
         const uint32_t a0 = ws->hPOh[row_lo], a1 = ws->hPOh[row_hi];
         if (a1 > a0)
             heavy_flat_kernel<<<(a1 - a0 + kHfThreads - 1) / kHfThreads, kHfThreads, 0, st>>>(
@@ -5968,6 +5976,15 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
         PG(hipGetLastError());
         return KMP_OK;
     }
+    PG(ws->hgi.reserve(2 * (ngb + 1)));
+    PG(ws->htc.reserve(ngb + 1));
+    PG(ws->htoff.reserve(ngb + 1));
+    PG(ws->hblk.reserve(2 * (ngb + ngb / kHvI + 2)));
+    uint32_t* BT = ws->hblk.p;
+    uint32_t* BP = BT + ngb + ngb / kHvI + 2;
+    heavy_plan_kernel<<<(uint32_t)((ngb + 1 + 255) / 256), 256, 0, st>>>(
+        ws->hE.p, GS, ngb + 1, ws->h_tot + 1, ho, RUN, RH, ho.cls && !c.ranged ? 1 : 0, row_lo, row_hi, c.heavy_df,
+        stats ? 1 : 0, 1, ws->bstats.p, ws->hgi.p, BT, BP, ws->htc.p);
     size_t t2 = 0;
     PG(rocprim::exclusive_scan(nullptr, t2, ws->htc.p, ws->htoff.p, 0ull, (size_t)ngb + 1,
                                rocprim::plus<unsigned long long>(), st));
