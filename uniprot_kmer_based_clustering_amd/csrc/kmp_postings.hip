@@ -3179,6 +3179,7 @@ struct kmp_postings {
     int direct_tail = 1;
     int flat_heavy = 1;  // ranged plain-order heavy expansion by rows (heavy_flat_kernel); 0: tiles
     int spill_all_on = 1;  // ... with every bucket spilled on the first pass (no bucket kernel after it)
+    bool front_all = false;  // the current front's spill holds every bucket
     bool pend_direct = false;  // the pending re-emit reruns the in-place reduce (its keys still held)
     PtGeom pend_g{};
     Grow<unsigned long long> dlb;  // its statistics (windowed sub-blocks)
@@ -5579,6 +5580,7 @@ int enqueue_front(kmp_postings* ws, MakeKeys& make_keys, const StepCfg& c, bool 
     // thousand idle 1,024-thread workgroups cost ~5 us); a bucket-range share of the k-mer split
     // lists about 1/parts of them
     const uint32_t lg = ws->bin_hi ? std::max<uint32_t>(64, kBucketLargeGrid * (c1 - c0) / dg.nb1) : ws->large_grid;
+    if (spill) ws->front_all = a.spill_all != 0;  // what the spill of this front will hold
     if (a.spill_all && !a.spill) return KMP_OK;  // every bucket already in the heavy path (a later pass)
     if (c.sb) {
         if (c.ranged) launch_buckets<true, true>(a, b0, nbk, lg, st);
@@ -6140,7 +6142,11 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
     if (ws->shard_cap == 0) ws->shard_cap = c.slots / 4 / kShards + 4096;
     if (ws->spill_cap == 0) ws->spill_cap = 1024;
     const bool debug = getenv("KMP_DEBUG") != nullptr;
-    const bool reuse = ws->reuse && ws->front_ok && c.front_key && *c.front_key == ws->front_key;
+    // a front whose spill holds every bucket (spill-all passes) and one holding the frequent k-mers
+    // only are not interchangeable: a whole-batch call between passes of the same batch recomputes
+    const bool want_all = c.ranged && ws->reuse && ws->flat_heavy && ws->spill_all_on;
+    const bool reuse = ws->reuse && ws->front_ok && c.front_key && *c.front_key == ws->front_key &&
+                       ws->front_all == want_all;
     if (!reuse) ws->front_ok = false;
     // every rerun grows a capacity to its measured need, so a handful of attempts suffices
     for (int attempt = 0; attempt < 16; ++attempt) {
