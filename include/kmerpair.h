@@ -458,9 +458,12 @@ uint32_t kmp_postings_last_overflow_blocks(const kmp_postings* ws);
  * rank per block writing the edges in canonical order at offsets from a decoupled look-back),
  * KMP_TAIL_COUNT (histogram, scan, scatter, block sort, emit: scored / multi-k calls, and a shape
  * whose row-block regions overflowed), or -1 (the flat layout's global sort). */
-enum { KMP_TAIL_COUNT = 0, KMP_TAIL_FAST = 1 };
+enum { KMP_TAIL_COUNT = 0, KMP_TAIL_FAST = 1, KMP_TAIL_DENSE = 2 };
 int kmp_postings_last_tail(const kmp_postings* ws);
-/* kmp_postings_set_tail: KMP_TAIL_FAST (default: the fast tail where it applies) or KMP_TAIL_COUNT
+/* kmp_postings_set_tail: KMP_TAIL_FAST (default: the fast tail where it applies), KMP_TAIL_DENSE (the
+ * fast tail and, for batches with pbits + rbits <= 15, its dense variant: per-block LDS bins over
+ * (row, q) on the counting partition; measured slower than the counting tail on uniprot k = 5) or
+ * KMP_TAIL_COUNT
  * (the counting tail only).  Same edges either way. */
 int kmp_postings_set_tail(kmp_postings* ws, int mode);
 /* kmp_postings_set_direct: the fused multi-k tail (kmp_dev_pairs_rows_multi, kmp_pairs_stream)

@@ -1883,7 +1883,7 @@ __global__ __launch_bounds__(kHvI) void heavy_expand_kernel(const uint32_t* __re
             __syncthreads();
             const unsigned long long o0 = (unsigned long long)local * kHvFlat, o1 = min(f_c[nr], o0 + kHvFlat);
             const uint32_t total = (uint32_t)(o1 - o0);
-            uint32_t hx = (E[b] * 0x9E3779B1u) ^ (local * 0xC2B2AE35u) ^ 0x27D4EB2Fu;
+            uint32_t hx = (GH[g] * 0x9E3779B1u) ^ (local * 0xC2B2AE35u) ^ 0x27D4EB2Fu;
             hx ^= hx >> 16;
             const uint32_t shard = (hx * 0x7FEB352Du) >> 26;
             if (threadIdx.x == 0) {
@@ -1964,10 +1964,12 @@ __global__ __launch_bounds__(kHvI) void heavy_expand_kernel(const uint32_t* __re
         block_scan_n<kHvI>(c, excl, total, wave_tot);
         // Shards, which size the next call's regions: a large unfiltered tile spreads its output
         // evenly over all of them (output o in shard 64 o / total); another tile takes one shard from
-        // what it is (its k-mer's first element, block, chunk) — not from t: the k-mers' order in E
+        // what it is (its k-mer's h, block, chunk) — not from t: the k-mers' order in E
         // follows the spill's (atomic) order, and the shard loads must not
         const bool spread = !(test_cls || test_row) && total >= kHvSpread;
-        uint32_t hx = (E[b] * 0x9E3779B1u) ^ (klo * 0x85EBCA6Bu) ^ (local * 0xC2B2AE35u);
+        // the k-mer's h, not its first element: class runs come in LDS-atomic order
+        // (heavy_segclass), so E[b] varied between calls and so did the fullest region (8 %)
+        uint32_t hx = (GH[g] * 0x9E3779B1u) ^ (klo * 0x85EBCA6Bu) ^ (local * 0xC2B2AE35u);
         hx ^= hx >> 16;
         const uint32_t shard = (hx * 0x7FEB352Du) >> 26;  // the top bits: kShards = 64
         if (spread) {
@@ -3196,6 +3198,7 @@ struct kmp_postings {
     uint32_t clear_n = 0;
     uint32_t large_grid = 1024;  // workgroups of the large-bucket kernel (from the last call's list)
     bool fast_mode = true;      // kmp_postings_set_tail: the fast tail allowed
+    bool dense_on = false;      // ... its dense variant too (KMP_TAIL_DENSE: measured slower on uniprot k = 5)
     bool fast_tail = true;      // unscored calls take the fast row-block tail (off for a shape whose
                                 // row-block regions overflowed: kRbFast)
     uint32_t bp_J = 0;          // level-2 tiles per coarse bin ...
@@ -4675,13 +4678,20 @@ __device__ __forceinline__ void lb_store(unsigned long long* p, unsigned long lo
 // the blocks before it (64 per round, one per lane) back to the nearest inclusive prefix, publishes
 // its own inclusive prefix; returns the exclusive one (count | overflow bit of any earlier block).
 // Blocks are dispatched in index order, so every predecessor is resident or done: the polls end.
-__device__ unsigned long long ft_lookback(unsigned long long* lb, uint32_t r, unsigned long long agg) {
+// ft_publish: the aggregate alone, as soon as it is known (a block that still has work before its
+// writes publishes early, so the blocks after it find it there); ft_lookback(..., published) then
+// skips the store.
+__device__ __forceinline__ void ft_publish(unsigned long long* lb, uint32_t r, unsigned long long agg) {
+    if ((threadIdx.x & 63) == 0) lb_store(lb + r, (r ? kLbAgg : kLbInc) | agg);
+}
+__device__ unsigned long long ft_lookback(unsigned long long* lb, uint32_t r, unsigned long long agg,
+                                          bool published = false) {
     const uint32_t lane = threadIdx.x & 63;
     if (r == 0) {
-        if (lane == 0) lb_store(lb, kLbInc | agg);
+        if (lane == 0 && !published) lb_store(lb, kLbInc | agg);
         return 0;
     }
-    if (lane == 0) lb_store(lb + r, kLbAgg | agg);
+    if (lane == 0 && !published) lb_store(lb + r, kLbAgg | agg);
     uint32_t cnt = 0;
     bool ovf = false;
     int64_t top = (int64_t)r - 1;
@@ -4742,7 +4752,7 @@ __global__ __launch_bounds__(kFtThreads) void pt_reduce_fast_kernel(const uint32
     const unsigned pb = g.pbits;
     const uint32_t R = 1u << g.rbits;
     uint32_t D = 0;  // the block's kept pairs
-    bool sort = n > kFtHashMax;
+    bool sort = n > kFtHashMax, published = false;
     if (!sort) {
         // ---- hash aggregation: pair -> slot, count per slot ----
         for (uint32_t i = tid; i < kFtSlots; i += kFtThreads) u.h.K[i] = kFtEmpty;
@@ -4796,6 +4806,9 @@ __global__ __launch_bounds__(kFtThreads) void pt_reduce_fast_kernel(const uint32
         D = total;
         sort = u.s_flag || u.s_max > kFtRankMax;  // uniform
         if (!sort) {
+            // the count is final: published before the ranking, the blocks after this one wait less
+            if (tid < 64) ft_publish(lb, r, (unsigned long long)D | (ovf ? kLbOvf : 0ull));
+            published = true;
             // grouped by row (the slots were read above the barriers)
 #pragma unroll
             for (uint32_t j = 0; j < 16; ++j)
@@ -4887,7 +4900,7 @@ __global__ __launch_bounds__(kFtThreads) void pt_reduce_fast_kernel(const uint32
     }
     // ---- the block's edge offset, then the pairs straight to the edge arrays ----
     if (tid < 64) {
-        const unsigned long long ex = ft_lookback(lb, r, (unsigned long long)D | (ovf ? kLbOvf : 0ull));
+        const unsigned long long ex = ft_lookback(lb, r, (unsigned long long)D | (ovf ? kLbOvf : 0ull), published);
         if (tid == 0) u.s_excl = ex;
     }
     __syncthreads();
@@ -5425,7 +5438,7 @@ bool pt_geometry(const kmp_postings* ws, const StepCfg& c, uint64_t inc, PtGeom*
     g->rowend = c.ranged ? c.row_hi : c.n;
     g->ftcap = kFtCap;
     g->dense = 0;
-    if (!c.sb && ws->fast_tail && g->pbits < kFdBitsMax) {
+    if (!c.sb && ws->fast_tail && ws->dense_on && g->pbits < kFdBitsMax) {
         // dense fast tail: the fewest rows per block that the block count allows, when the blocks
         // still average a few hundred keys (a sparse call keeps the hash reduce: clearing 2^15 bins
         // for a handful of keys would dominate)
@@ -6248,7 +6261,9 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
                     fprintf(stderr, "kmp: rerun after the heavy path (shard %llu/%llu, segments %llu, largest %llu)\n",
                             most, (unsigned long long)ws->shard_cap, (unsigned long long)ws->h_segs,
                             (unsigned long long)ws->h_segmax);
-                ws->shard_cap = most + most / 64 + 256;
+                // an eighth of slack: the heavy path's region loads vary by a few percent between
+                // calls, and with 1/64 uniprot k = 5 reran its front on most steps
+                ws->shard_cap = most + most / 8 + 256;
                 continue;
             }
             ws->pt_inc = n_inc;
@@ -6768,7 +6783,10 @@ __global__ void split_pad_finish_kernel(unsigned long long* __restrict__ send, u
              i += (uint64_t)gridDim.x * blockDim.x)
             send[d * cap + i] = kNoKey;
     if (blockIdx.x || blockIdx.y) return;
+    // one workgroup: the statistics and the fullest regions reduced over its threads (one thread
+    // walking the parts x kShards cursors took 45 us at G = 8)
     const uint32_t t = threadIdx.x;
+    __shared__ unsigned long long s_red[3][256 / 64];
     if (t < kStN) {
         unsigned long long v = 0;
         for (int sh = 0; sh < kShards; ++sh) {
@@ -6777,16 +6795,31 @@ __global__ void split_pad_finish_kernel(unsigned long long* __restrict__ send, u
         }
         stats[t] = v;
     }
+    unsigned long long shard = 0, spill = 0, part = 0;
+    for (uint32_t sh = t; sh < kShards; sh += blockDim.x) {
+        shard = max(shard, gstats[kRbCursor + sh]);
+        spill += gstats[kRbSpill + sh];
+    }
+    const uint32_t nq = routed ? parts * kShards : parts;
+    for (uint32_t q = t; q < nq; q += blockDim.x) part = max(part, dcursor[q] * (routed ? kShards : 1u));
+    for (int off = 32; off > 0; off >>= 1) {
+        shard = max(shard, (unsigned long long)__shfl_xor(shard, off));
+        spill += (unsigned long long)__shfl_xor(spill, off);
+        part = max(part, (unsigned long long)__shfl_xor(part, off));
+    }
+    if ((t & 63) == 0) {
+        s_red[0][t >> 6] = shard;
+        s_red[1][t >> 6] = spill;
+        s_red[2][t >> 6] = part;
+    }
+    __syncthreads();
     if (t == 0) {
-        unsigned long long shard = 0, spill = 0, part = 0;
-        for (int sh = 0; sh < kShards; ++sh) {
-            shard = max(shard, gstats[kRbCursor + sh]);
-            spill += gstats[kRbSpill + sh];
+        shard = spill = part = 0;
+        for (uint32_t w = 0; w < (blockDim.x + 63) / 64; ++w) {
+            shard = max(shard, s_red[0][w]);
+            spill += s_red[1][w];
+            part = max(part, s_red[2][w]);
         }
-        if (routed)
-            for (uint32_t q = 0; q < parts * kShards; ++q) part = max(part, dcursor[q] * kShards);
-        else
-            for (uint32_t q = 0; q < parts; ++q) part = max(part, dcursor[q]);
         const uint32_t clamp = 0xFFFFFFFFu;
         out[KMP_SPLIT_CLASS] = wflags[kFlClass];
         out[KMP_SPLIT_HEAVY] = spill != 0 && !heavy_done;  // spilled with the heavy path off: rerun with it on
@@ -6845,8 +6878,9 @@ int kmp_postings_set_direct(kmp_postings* ws, int enable) {
 }
 
 int kmp_postings_set_tail(kmp_postings* ws, int mode) {
-    if (!ws || (mode != KMP_TAIL_FAST && mode != KMP_TAIL_COUNT)) return KMP_EINVAL;
-    ws->fast_mode = mode == KMP_TAIL_FAST;
+    if (!ws || (mode != KMP_TAIL_FAST && mode != KMP_TAIL_COUNT && mode != KMP_TAIL_DENSE)) return KMP_EINVAL;
+    ws->fast_mode = mode != KMP_TAIL_COUNT;
+    ws->dense_on = mode == KMP_TAIL_DENSE;
     ws->fast_tail = ws->fast_mode;
     return KMP_OK;
 }
