@@ -2,6 +2,8 @@
 #   bash tools/profile.sh kernels TAG [bench args]   kernel trace + stats of bench.py -> gpurun_out/prof_TAG
 #   bash tools/profile.sh traffic TAG                FETCH_SIZE and WRITE_SIZE passes of the config-3 bench
 #                                                    -> gpurun_out/pmc_traffic_TAG.json (tools/pmc_traffic.py)
+#   bash tools/profile.sh traffic5 TAG               the same over one config-5 step (reduce + expansion kernels)
+#                                                    -> gpurun_out/pmc_config5_TAG.json (tools/pmc_config5.py)
 #   bash tools/profile.sh sq REGEX TAG               two SQ counter passes (8 counters each) over the kernels
 #                                                    matching REGEX -> gpurun_out/sq_TAG.txt
 set -e
@@ -28,6 +30,18 @@ traffic)
     python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/pmc_write_$tag.log 2>&1
   python3 tools/pmc_traffic.py $(find gpurun_out/pmc_fetch_$tag -name 'run_counter_collection.csv') \
     $(find gpurun_out/pmc_write_$tag -name 'run_counter_collection.csv') gpurun_out/pmc_traffic_$tag.json
+  ;;
+traffic5)
+  # config 5: the fused reduce's and the expansion's kernels only (one step; each pass its own run)
+  tag=$1
+  re="pt_hist|pt_tscan|pt_scatter_kernel|pt_split|pt_window_count|pt_reduce_count|pt_reduce_write|heavy_flat|bucket_small|bucket_large|edge_digest"
+  rm -rf gpurun_out/pmc5_fetch_$tag gpurun_out/pmc5_write_$tag
+  timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$re" --output-format csv -d gpurun_out/pmc5_fetch_$tag -o run -- \
+    python3 bench.py --config config5 --no-cpu-baseline > gpurun_out/pmc5_fetch_$tag.log 2>&1
+  timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$re" --output-format csv -d gpurun_out/pmc5_write_$tag -o run -- \
+    python3 bench.py --config config5 --no-cpu-baseline > gpurun_out/pmc5_write_$tag.log 2>&1
+  python3 tools/pmc_config5.py $(find gpurun_out/pmc5_fetch_$tag -name 'run_counter_collection.csv') \
+    $(find gpurun_out/pmc5_write_$tag -name 'run_counter_collection.csv') gpurun_out/pmc_config5_$tag.json
   ;;
 sq)
   regex=$1; tag=$2
