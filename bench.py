@@ -289,6 +289,17 @@ def bench_config5(args):
                   "GBs": alg[s] / (stg[s] * 1e-3) / 1e9 if s in alg and stg[s] > 0 else None} for s in stg}
     dom = max(alg, key=lambda s: stg[s])
     ach = stages[dom]["GBs"]
+    # the dominant stage's HBM bytes per step from the newest committed config-5 PMC table
+    # (tools/profile.sh traffic5: FETCH_SIZE / WRITE_SIZE passes over one step, corrected)
+    traffic, traffic_src = None, None
+    import glob
+    pmc5 = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_config5.json")))
+    if pmc5 and world == 1:
+        try:
+            traffic = json.load(open(pmc5[-1]))["stages"][dom]["bytes"]
+            traffic_src = os.path.relpath(pmc5[-1], ROOT)
+        except (OSError, KeyError, ValueError):
+            traffic = None
     out = {"metric": "protein pairs/sec (+ edges/sec), config 5: 1M synthetic log-uniform 50-2000, k=5+7 combined, "
                      "BLOSUM-weighted",
            "value": pairs_total / (dt / steps), "unit": "pairs/s", "n_gpus": world, "steps": steps,
@@ -304,7 +315,9 @@ def bench_config5(args):
            "incidences_per_s": tot["incidences"] / (dt / steps),
            "summary": {k: tot[k] for k in ("n_edges", "sum_w", "sum_score", "n_align")},
            "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": ach / HBM_PEAK_GBS if ach else None, "traffic": None, "kernel": dom,
+                        "frac": ach / HBM_PEAK_GBS if ach else None, "traffic": traffic,
+                        "traffic_source": traffic_src,
+                        "traffic_over_alg": traffic / alg[dom] if traffic else None, "kernel": dom,
                         "kernel_ms": stg[dom], "alg_bytes_per_launch": alg[dom], "stages": stages,
                         "note": "stage times summed over the passes (HIP events on the stream); "
                                 "rank 0's when N > 1"}}
