@@ -3061,8 +3061,9 @@ void launch_buckets(const BucketArgs& a, uint32_t b0, uint32_t nb, uint32_t larg
     else
         bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallTab, false, kRows, kScore>
             <<<nb, kBucketSmallThreads, 0, st>>>(a, b0);
-    bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeTab, kRows, kScore>
-        <<<large_grid, kBucketLargeThreads, 0, st>>>(a);
+    if (large_grid)  // 0: the last call listed no bucket (a listed one now makes the call rerun)
+        bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeTab, kRows, kScore>
+            <<<large_grid, kBucketLargeThreads, 0, st>>>(a);
 }
 
 // (pair key, w) runs -> edges with w >= min_shared, canonical order kept
@@ -3196,7 +3197,8 @@ struct kmp_postings {
     uint64_t route_cap = 0;
     SplitRows route_rows{};
     uint32_t clear_n = 0;
-    uint32_t large_grid = 1024;  // workgroups of the large-bucket kernel (from the last call's list)
+    uint32_t large_grid = 1024;  // workgroups of the large-bucket kernel (from the last call's list; 0: none)
+    uint32_t large_used = 1024;  // ... the grid the last front launched
     bool fast_mode = true;      // kmp_postings_set_tail: the fast tail allowed
     bool dense_on = false;      // ... its dense variant too (KMP_TAIL_DENSE: measured slower on uniprot k = 5)
     bool fast_tail = true;      // unscored calls take the fast row-block tail (off for a shape whose
@@ -5597,6 +5599,7 @@ int enqueue_front(kmp_postings* ws, MakeKeys& make_keys, const StepCfg& c, bool 
     // thousand idle 1,024-thread workgroups cost ~5 us); a bucket-range share of the k-mer split
     // lists about 1/parts of them
     const uint32_t lg = ws->bin_hi ? std::max<uint32_t>(64, kBucketLargeGrid * (c1 - c0) / dg.nb1) : ws->large_grid;
+    ws->large_used = lg;
     if (spill) ws->front_all = a.spill_all != 0;  // what the spill of this front will hold
     if (a.spill_all && !a.spill) return KMP_OK;  // every bucket already in the heavy path (a later pass)
     if (c.sb) {
@@ -6203,6 +6206,10 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
         }
         sum_stats(rb, acc, &most, &n_inc, &spill_most, &spill_total);
         bool rerun = false;
+        if (rb[kRbList] && ws->large_used == 0) {  // listed buckets, no large-bucket launch: again with it
+            ws->large_grid = kBucketLargeGrid;
+            rerun = true;
+        }
         if (rb[kRbFlagCur] && ws->cur_used) {  // a region of the cursor partition overflowed
             // learn the layout from this call's exact bucket counts (own bins: all of them here);
             // the counting partition only if the learned layout keeps overflowing
@@ -6300,9 +6307,10 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
         ws->pt_inc = n_inc;  // sizes the next call's row blocks
         ws->last_fast = pt_fast(ws, g);
         ws->vreg_tries = 0;  // a call without a region overflow
-        {  // the large-bucket grid of the next call: twice the listed buckets, 64 .. kBucketLargeGrid
-            uint32_t lg = 64;
-            while (lg < kBucketLargeGrid && lg < 2 * rb[kRbList]) lg *= 2;
+        {  // the large-bucket grid of the next call: twice the listed buckets, 64 .. kBucketLargeGrid;
+           // none listed: not launched (an idle 64-workgroup launch cost ~5 us of the config-3 step)
+            uint32_t lg = rb[kRbList] ? 64u : 0u;
+            while (lg && lg < kBucketLargeGrid && lg < 2 * rb[kRbList]) lg *= 2;
             ws->large_grid = lg;
         }
         uint64_t ne = rb[kRbRuns];
