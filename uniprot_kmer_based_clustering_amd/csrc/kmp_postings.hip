@@ -2768,10 +2768,11 @@ __global__ void chunk_desc_kernel(const uint64_t* __restrict__ res_off, uint32_t
     }
 }
 
-// waves per SIMD the persistent level 1 is compiled for (VGPR budget: 6 -> 80 registers, three
-// 512-thread workgroups per CU)
+// waves per SIMD the persistent level 1 is compiled for (VGPR budget: 8 -> 64 registers and 24 B of
+// scratch per lane, four 512-thread workgroups per CU; 6 -> 79 registers measured 91 -> 86 us slower
+// per rank of the k-mer split at G = 8, the same on one GPU)
 #ifndef KMP_L1P_WAVES
-#define KMP_L1P_WAVES 6
+#define KMP_L1P_WAVES 8
 #endif
 // Level 1, local, persistent: workgroup w takes chunks w, w + grid, ...; chunk c's keys of the
 // call's digits [dlo, dhi) grouped by digit1 at out[c * kKeyChunk ...] (its own 4,096-key segment),
