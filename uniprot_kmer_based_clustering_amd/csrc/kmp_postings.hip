@@ -2769,8 +2769,8 @@ __global__ void chunk_desc_kernel(const uint64_t* __restrict__ res_off, uint32_t
 }
 
 // waves per SIMD the persistent level 1 is compiled for (VGPR budget: 8 -> 64 registers and 24 B of
-// scratch per lane, four 512-thread workgroups per CU; 6 -> 79 registers measured 91 -> 86 us slower
-// per rank of the k-mer split at G = 8, the same on one GPU)
+// scratch per lane, four 512-thread workgroups per CU; at 6 waves, 79 registers, a rank of the k-mer
+// split at G = 8 spent 91 us in it against 86 us at 8; one GPU: the same)
 #ifndef KMP_L1P_WAVES
 #define KMP_L1P_WAVES 8
 #endif
