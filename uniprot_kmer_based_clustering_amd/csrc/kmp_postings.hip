@@ -1533,41 +1533,24 @@ __global__ __launch_bounds__(kScThreads) void heavy_segclass_kernel(const unsign
     }
     // a protein's first window in the segment keeps its key, later ones are dropped; each kept key
     // ranked in its class
-    uint32_t rk[kScItems], fm = 0;
+    uint32_t rk[kScItems];
 #pragma unroll
     for (uint32_t e = 0; e < kScItems; ++e) {
         rk[e] = ~0u;
         if (v[e] == ~0ull) continue;
         const uint32_t p = (uint32_t)v[e] & pm;
         uint32_t sl = (p * 0x9E3779B1u) >> (32 - 14);  // kScSlots = 2^14
+        bool first = false;
         while (true) {
             const uint32_t old = atomicCAS(&u.P[sl], 0xFFFFFFFFu, p);
             if (old == 0xFFFFFFFFu) {
-                fm |= 1u << e;
+                first = true;
                 break;
             }
             if (old == p) break;
             sl = (sl + 1) & (kScSlots - 1);
         }
-    }
-    // ranks in class, aggregated per wave: one LDS atomic per (wave, class) instead of per key (a
-    // frequent k-mer's keys sit in a few classes: the per-key atomics serialised on them)
-    const uint32_t lane = tid & 63;
-#pragma unroll
-    for (uint32_t e = 0; e < kScItems; ++e) {
-        const bool f = (fm >> e) & 1u;
-        const uint32_t cls = (uint32_t)(v[e] >> ho.pbits) & (uint32_t)cm;
-        unsigned long long todo = __ballot(f);
-        while (todo) {  // uniform over the wave
-            const int leader = __builtin_ctzll(todo);
-            const uint32_t lc = __shfl(cls, leader);
-            const unsigned long long grp = __ballot(f && cls == lc);
-            uint32_t base = 0;
-            if ((int)lane == leader) base = atomicAdd(&CH[lc], (uint32_t)__popcll(grp));
-            base = __shfl(base, leader);
-            if (f && cls == lc) rk[e] = base + (uint32_t)__popcll(grp & ((1ull << lane) - 1));
-            todo &= ~grp;
-        }
+        if (first) rk[e] = atomicAdd(&CH[(uint32_t)(v[e] >> ho.pbits) & (uint32_t)cm], 1u);
     }
     __syncthreads();
     lds_bins_scan<kScThreads>(CH, kScClasses, wave_tot);  // CH: run starts; the kept count below
