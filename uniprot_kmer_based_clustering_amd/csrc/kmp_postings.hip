@@ -2745,11 +2745,26 @@ constexpr uint32_t kBpGatherTile = 4096;  // keys per round of a level-2 tile
 // [r0, r1) its windows read.  One thread per protein p <= n writes the chunks that start in its
 // region (first, r0) and those that end in it (last, r1); the grid also clears the cursor level 2's
 // bucket counts (one launch less per step).  Residue offsets fit u32 (bp_level1 checks slots).
+// StepClear: the step's flags and statistics (and extra words: the k-mer split's send cursors),
+// cleared by the first kernel of the residue front instead of a kernel of their own
+struct StepClear {
+    uint32_t* flags;
+    uint32_t n_flags;
+    unsigned long long* gstats;
+    uint32_t n_gstats;
+    unsigned long long* extra;
+    uint32_t n_extra;
+};
 __global__ void chunk_desc_kernel(const uint64_t* __restrict__ res_off, uint32_t n, uint64_t slots,
                                   uint32_t n_chunks, int k, uint4* __restrict__ desc, uint32_t* __restrict__ cur,
-                                  uint32_t ncur) {
+                                  uint32_t ncur, StepClear sc) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     for (uint32_t i = t; i < ncur; i += gridDim.x * blockDim.x) cur[i] = 0;
+    if (blockIdx.x == 0 && sc.flags) {
+        for (uint32_t i = threadIdx.x; i < sc.n_gstats; i += blockDim.x) sc.gstats[i] = 0;
+        for (uint32_t i = threadIdx.x; i < sc.n_flags; i += blockDim.x) sc.flags[i] = 0;
+        for (uint32_t i = threadIdx.x; i < sc.n_extra; i += blockDim.x) sc.extra[i] = 0;
+    }
     const uint32_t p = t;
     if (p > n) return;
     const uint64_t off = res_off[p], L = p < n ? res_off[p + 1] - off : 0;
@@ -3209,6 +3224,8 @@ struct kmp_postings {
     uint64_t bp_c1 = 0;         // offset of C1 (coarse bin starts) in ws->bp
     bool parted = false;        // ws->keys holds level-1 output (bp_level1 ran for this call)
     bool bp_local = false;      // ... in chunk segments (local level 1: H1T at bp + bp_h1t)
+    bool clear_in_keys = false;  // the call's key path clears the step's flags (residue paths)
+    bool defer_clear = false;    // ... and has not yet
     uint32_t bp_G = 0, bp_T = 0;
     uint32_t bp_hsb = 0, bp_hsc = 1;  // level 2's run-table strides (bin, chunk)
     uint64_t bp_h1t = 0;
@@ -3330,6 +3347,9 @@ void own_bins(const kmp_postings* ws, const BpDigits& dg, uint32_t* lo, uint32_t
     *hi = ws->bin_hi ? std::min(ws->bin_hi, dg.nb1) : dg.nb1;
 }
 
+__global__ void step_clear_kernel(uint32_t* __restrict__ flags, unsigned long long* __restrict__ gstats,
+                                  unsigned long long* __restrict__ extra, uint32_t n_extra);
+
 hipError_t bp_level1(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
                      int k, uint32_t n, uint64_t slots, const Layout& lay, hipStream_t st) {
     const BpDigits dg = bp_digits(lay);
@@ -3353,13 +3373,22 @@ hipError_t bp_level1(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_r
     const uint32_t nb = 1u << lay.bbits;
     if (ws->bp_local) e = ws->cur.reserve(nb);
     if (e != hipSuccess) return e;
+    if (ws->defer_clear && !ws->bp_local) {  // no chunk descriptors on this path: the clear first
+        step_clear_kernel<<<1, 256, 0, st>>>(ws->flags.p, ws->bstats.p, ws->clear_extra, ws->clear_n);
+        ws->defer_clear = false;
+    }
     if (ws->bp_local) {  // local level 1 for the cursor level 2: H1 (own digits) | H1T
         e = ws->chunk_desc.reserve(4ull * G);
         if (e != hipSuccess) return e;
         // descriptors + the cursor level 2's bucket counts cleared (bp_level2c does not)
+        StepClear sc{};
+        if (ws->defer_clear) {  // the front's clear, folded into this first kernel
+            sc = StepClear{ws->flags.p, kFlN, ws->bstats.p, kShards * 10, ws->clear_extra, ws->clear_n};
+            ws->defer_clear = false;
+        }
         chunk_desc_kernel<<<(n + 1 + 255) / 256, 256, 0, st>>>(d_res_off, n, slots, G, k,
                                                                reinterpret_cast<uint4*>(ws->chunk_desc.p), ws->cur.p,
-                                                               nb);
+                                                               nb, sc);
         ws->bp_G = G;
         ws->bp_h1t = h1;
         // T chunks per level-2 tile: ~7/4 of a round at the hash-uniform mean (two rounds; kKeyChunk / nb1 keys
@@ -5580,10 +5609,17 @@ int step_reserve(kmp_postings* ws, const StepCfg& c, const PtGeom& g, hipStream_
 template <class MakeKeys>
 int enqueue_front(kmp_postings* ws, MakeKeys& make_keys, const StepCfg& c, bool spill, hipStream_t st,
                   bool keys = true) {
-    step_clear_kernel<<<1, 256, 0, st>>>(ws->flags.p, ws->bstats.p, ws->clear_extra, ws->clear_n);
+    // the residue front folds the clear into its first kernel (chunk_desc); any other: a kernel here
+    ws->defer_clear = keys && ws->clear_in_keys;
+    if (!ws->defer_clear)
+        step_clear_kernel<<<1, 256, 0, st>>>(ws->flags.p, ws->bstats.p, ws->clear_extra, ws->clear_n);
     ws->mark(0, st);
     if (keys) {  // else: the keys grouped by bucket of the last call (front reuse)
         PG(make_keys(c.lay, st));
+        if (ws->defer_clear) {  // (a key path that did not take it)
+            ws->defer_clear = false;
+            return KMP_EINVAL;
+        }
         ws->mark(1, st);
         int rc = bucket_group(ws, ws->keys.p, c.slots, c.lay, st);  // marks 2
         if (rc != KMP_OK) return rc;
@@ -6969,6 +7005,16 @@ int kmp_dev_pairs_postings(kmp_postings* ws, const uint32_t* d_set, const uint32
                         n, d_p, d_q, d_w, cap, n_edges, stats, st);
 }
 
+// the residue key paths take the step's clear into their first kernel, for the call that sets this
+struct ClearInKeys {
+    kmp_postings* ws;
+    explicit ClearInKeys(kmp_postings* w) : ws(w) { ws->clear_in_keys = true; }
+    ~ClearInKeys() {
+        ws->clear_in_keys = false;
+        ws->defer_clear = false;
+    }
+};
+
 static int residues_impl(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
                          uint32_t n, int k, uint64_t slots, uint32_t heavy_df, uint32_t min_shared,
                          int require_class_diff, bool ranged, uint32_t row_lo, uint32_t row_hi, uint32_t* d_p,
@@ -6987,9 +7033,14 @@ static int residues_impl(kmp_postings* ws, const uint8_t* d_res, const uint64_t*
             return bp_level1(ws, d_res, d_res_off, d_class, k, n, slots, lay, st);
         }
         ws->cur_used = false;
+        if (ws->defer_clear) {
+            step_clear_kernel<<<1, 256, 0, st>>>(ws->flags.p, ws->bstats.p, ws->clear_extra, ws->clear_n);
+            ws->defer_clear = false;
+        }
         return launch_residue_keys(ws, d_res, d_res_off, d_class, k, 0u, n, 0ull, slots, lay, st);
     };
     const std::vector<unsigned long long> key_extra = {1, (uintptr_t)d_res, (uintptr_t)d_res_off, (uintptr_t)d_class};
+    const ClearInKeys guard(ws);
     return run_postings(ws, keys, key_extra, n, k, slots, d_class, heavy_df, min_shared, require_class_diff, ranged,
                         row_lo, row_hi, d_p, d_q, d_w, cap, n_edges, stats, st, sb, sor, d_s, d_w1, n_inc_out);
 }
@@ -7175,10 +7226,11 @@ int kmp_dev_split_expand(kmp_postings* ws, const uint8_t* d_res, const uint64_t*
         ws->cur_used = ws->cur_on && cur_geometry(l, &ws->cg);
         return bp_level1(ws, d_res, d_res_off, d_class, k, n, slots, l, s);
     };
+    const ClearInKeys guard(ws);
     SplitRows rows{};
     rows.parts = parts;
     kmp_row_split(n, parts, rows.start);
-    // the send cursors are cleared with the step's flags (step_clear_kernel in the front); routed
+    // the send cursors are cleared with the step's flags (by chunk_desc_kernel in the front); routed
     // (no heavy path): the bucket kernels write the send regions, pre-filled with kNoKey
     const bool routed = !ws->split_heavy;
     auto front = [&](hipStream_t s) -> int {
