@@ -126,3 +126,21 @@ def test_kmer_split_step_device_stages(world):
     heavy = [m for m in msgs if m[0] == "heavy"]
     assert all(m[1] and not m[2] for m in heavy), heavy  # golden edges, never the row split
     assert heavy[0][3] == heavy[1][3] >= 1, heavy  # the heavy path turned on once, then kept
+
+
+def test_kmer_split_step_one_rank():
+    """At world 1 kmer_split_step has nothing to route or exchange: it runs the fused step (no
+    process group needed) and returns the oracle's edges, its timings as (step, 0, 0)."""
+    import uniprot_kmer_based_clustering_amd as K
+    import uniprot_kmer_based_clustering_amd.dist as D
+    from oracle.oracle import Oracle
+    from uniprot_kmer_based_clustering_amd.device import DevicePipeline
+    b = K.synth(5000, 32)
+    p, q, w = Oracle(b.residues, b.offsets, b.class_id, k=7, threads=4).pairs()
+    pipe = DevicePipeline(b, 7, "cuda:0")
+    tims = []
+    for _ in range(2):
+        n = D.kmer_split_step(pipe, 0, 1, gather=True, timings=tims)
+        assert n == len(p) and all(np.array_equal(a, x) for a, x in zip(pipe.edges(), (p, q, w)))
+    assert len(tims) == 2 and all(t[0] > 0 and t[1] == 0 and t[2] == 0 for t in tims)
+    assert pipe.__dict__.get("_split_state") is None or pipe._split_state.reruns == 0

@@ -2,7 +2,8 @@
   rows   the row split: every rank's kmp_dev_pairs_rows over its kmp_row_split rows;
   kmer   the k-mer split: every rank's kmp_dev_split_expand (its share of the bucket hash range,
          pair keys routed by row owner) and kmp_dev_split_edges over the keys it would receive.
-For G = 1, 2, 4, 8 each rank's stages are timed in turn on its own DevicePipeline; the slowest
+For G = 2, 4, 8 each rank's stages are timed in turn on its own DevicePipeline (G = 1: the fused
+step, which kmer_split_step runs at world 1); the slowest
 rank bounds the step.  Exchanges (all-to-all, gather) are not included.  Each phase is reported as
 wall time (host clock over back-to-back calls: launches and the edges phase's read-back included)
 and device time (HIP events around each call on its stream).
@@ -44,6 +45,11 @@ def timed(fn, reps=10):
 
 
 def kmer_ranks(b, k, g):
+    if g == 1:  # dist.kmer_split_step at world 1: nothing to exchange, the fused step
+        pipe = DevicePipeline(b, k, "cuda:0")
+        w, d = timed(lambda: pipe.step())
+        return [{"rows": [0, b.n], "fused_step": True, "ms": w, "dev_ms": d, "send_MB": 0.0, "sent_keys": 0,
+                 "edges": pipe.n_edges}]
     pipes = [DevicePipeline(b, k, "cuda:0") for _ in range(g)]
     cap = max(4096, pipes[0].total // 4 // (g * g))
     learn = None
