@@ -458,12 +458,9 @@ uint32_t kmp_postings_last_overflow_blocks(const kmp_postings* ws);
  * rank per block writing the edges in canonical order at offsets from a decoupled look-back),
  * KMP_TAIL_COUNT (histogram, scan, scatter, block sort, emit: scored / multi-k calls, and a shape
  * whose row-block regions overflowed), or -1 (the flat layout's global sort). */
-enum { KMP_TAIL_COUNT = 0, KMP_TAIL_FAST = 1, KMP_TAIL_DENSE = 2 };
+enum { KMP_TAIL_COUNT = 0, KMP_TAIL_FAST = 1 };
 int kmp_postings_last_tail(const kmp_postings* ws);
-/* kmp_postings_set_tail: KMP_TAIL_FAST (default: the fast tail where it applies), KMP_TAIL_DENSE (the
- * fast tail and, for batches with pbits + rbits <= 15, its dense variant: per-block LDS bins over
- * (row, q) on the counting partition; measured slower than the counting tail on uniprot k = 5) or
- * KMP_TAIL_COUNT
+/* kmp_postings_set_tail: KMP_TAIL_FAST (default: the fast tail where it applies) or KMP_TAIL_COUNT
  * (the counting tail only).  Same edges either way. */
 int kmp_postings_set_tail(kmp_postings* ws, int mode);
 /* kmp_postings_set_direct: the fused multi-k tail (kmp_dev_pairs_rows_multi, kmp_pairs_stream)
@@ -567,13 +564,13 @@ int kmp_dev_pairs_rows_multi(kmp_postings* const* ws, const int* ks, uint32_t nk
  *     d_stats[8] (Σ|K(p)|, distinct, repeat,
  *     Σ C(df,2), max df, heavy entries, incidences, 0 — this rank's k-mers) are written on `stream`.
  *     learn: the previous call's flags reduced (max) over the ranks, or NULL for a first call;
- *     every rank grows its capacities from them identically.  KMP_EOVERFLOW (heavy path only):
- *     the rank's spill regions kept overflowing; d_send and d_flags were not written (call again). 
+ *     every rank grows its capacities from them identically.  A rank whose spill regions kept
+ *     overflowing (heavy path) sends no keys and raises RERUN, so every rank reruns in lockstep. 
  *   exchange (the caller's collective): region d of rank g's d_send -> region g of rank d's receive
  *     buffer (an all-to-all of equal splits, cap keys each).
  *   kmp_dev_split_edges   the m = parts * cap received keys -> the canonical edges of rows
  *     [row_lo, row_hi) (the row-block tail), *n_edges; KMP_EOVERFLOW when cap is smaller (grow and
- *     call again with the same keys).  Synchronises `stream`.
+ *     call again with the same keys).  Synchronises `stream` (also when there is nothing to reduce).
  * The rank-order concatenation of the ranks' edges is the canonical list.  Flags: RERUN (a send
  * region, pair-key shard or bucket region overflowed: call expand again with learn, after growing
  * cap to at least MAX_PART when that is the cause), CLASS (class ids too wide: single GPU) and

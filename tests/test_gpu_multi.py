@@ -104,7 +104,7 @@ def test_rccl_transport_single_device(oracle_mod):
             assert_edges(e.pairs(), p, q, w)
 
 
-def emulate_kmer_split(b, k, G, cap=None, min_shared=1):
+def emulate_kmer_split(b, k, G, cap=None, min_shared=1, require_class_diff=True):
     """The k-mer split's G ranks on one GPU, in one process: every rank's kmp_dev_split_expand on
     its own DevicePipeline, the all-to-all done by slicing the send regions, every rank's
     kmp_dev_split_edges; flags reduced (max) over the ranks and fed back as `learn` on a rerun,
@@ -121,7 +121,8 @@ def emulate_kmer_split(b, k, G, cap=None, min_shared=1):
         flags = [torch.zeros(_lib.KMP_SPLIT_FLAGS, dtype=torch.int32, device="cuda:0") for _ in range(G)]
         stats = [torch.zeros(8, dtype=torch.int64, device="cuda:0") for _ in range(G)]
         for r in range(G):
-            pipes[r].split_expand(r, G, cap, sends[r], flags[r], stats[r], learn=learn)
+            pipes[r].split_expand(r, G, cap, sends[r], flags[r], stats[r], learn=learn,
+                                  require_class_diff=require_class_diff)
         fl = torch.stack(flags).max(dim=0).values.cpu().tolist()
         out = [[], [], []]
         for d in range(G):
@@ -177,3 +178,43 @@ def test_kmer_split_reruns_and_options(oracle_mod):
         (ep, eq, ew), fl, tot, reruns = emulate_kmer_split(K.Proteins(res, off, cls), 5, G)
         assert reruns >= 1 and not fl[_lib.KMP_SPLIT_HEAVY] and not fl[_lib.KMP_SPLIT_RERUN]
         assert len(ep) == g["n_edges"] and edges_sha256(ep, eq, ew) == g["edges_sha256"]
+
+
+def dense_families(n_fam=40, members=60, length=300, mu=0.02, seed=11):
+    """Families of near-identical proteins (per-site substitution rate mu), shuffled, 15 classes
+    at random: most k-mers occur in ~`members` proteins, so bucket groups hold 32+ keys (below the
+    heavy path's 128) and a bucket expands to thousands of pair keys."""
+    rng = np.random.default_rng(seed)
+    aa = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", dtype=np.uint8)
+    seqs = []
+    for _ in range(n_fam):
+        anc = rng.choice(aa, length)
+        for _ in range(members):
+            s = anc.copy()
+            mut = rng.random(length) < mu
+            s[mut] = rng.choice(aa, int(mut.sum()))
+            seqs.append(s)
+    order = rng.permutation(len(seqs))
+    res = np.concatenate([seqs[i] for i in order]).astype(np.uint8)
+    off = np.arange(len(seqs) + 1, dtype=np.uint64) * length
+    cls = rng.integers(0, 15, len(seqs)).astype(np.uint16)
+    return K.Proteins(res, off, cls)
+
+
+@pytest.mark.parametrize("g", [2, 3])
+def test_kmer_split_routed_large_groups(oracle_mod, g):
+    """The routed bucket output of the k-mer split on buckets above the LDS staging (groups of
+    ~60 keys: a bucket expands to more pair keys than its stage holds, so it counts, reserves per
+    destination and writes with LDS cursors), class filter on and off: bit-exact at G ranks."""
+    b = dense_families()
+    o = oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=7, threads=8)
+    for diff in (True, False):
+        (ep, eq, ew), fl, tot, _ = emulate_kmer_split(b, 7, g, require_class_diff=diff)
+        assert not fl[_lib.KMP_SPLIT_HEAVY] and not fl[_lib.KMP_SPLIT_CLASS]
+        c = o.counters()
+        assert c["max_df"] >= 32
+        p, q, w = o.pairs(require_class_diff=diff)
+        assert len(p) > 10_000
+        np.testing.assert_array_equal(ep, p)
+        np.testing.assert_array_equal(eq, q)
+        np.testing.assert_array_equal(ew, w)

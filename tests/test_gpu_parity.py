@@ -398,13 +398,13 @@ def test_frequent_kmers_heavy_path(oracle_mod, copies):
     np.testing.assert_array_equal(pipe.edges()[1], q)
 
 
-@pytest.mark.parametrize("tail", ["fast", "dense", "count"])
+@pytest.mark.parametrize("tail", ["fast", "count"])
 def test_uniprot_k5_on_bucketed_heavy_path(oracle_mod, uni, tail):
     """The reference's dataset at k = 5 (max df 3,694): bucketed layout with the heavy path and
     the row-block tail — the fast tail (its fixed regions overflow on rows of ~10^5 keys: the
-    counting tail, learned), its dense variant (N < 2^14: per-block LDS bins over (row, q)) or the
-    counting tail — edge list sha equal to the golden one (repeat: graph replay is not used on the
-    split step, every call recomputes); min_shared 2 against the oracle."""
+    counting tail, learned) or the counting tail — edge list sha equal to the golden one (repeat:
+    graph replay is not used on the split step, every call recomputes); min_shared 2 against the
+    oracle."""
     import torch
     from uniprot_kmer_based_clustering_amd.device import DevicePipeline
     res, off, cls = uni
@@ -415,7 +415,7 @@ def test_uniprot_k5_on_bucketed_heavy_path(oracle_mod, uni, tail):
         m = pipe.step(engine="residues")
         torch.cuda.synchronize()
         assert pipe.last_layout() == "bucketed" and pipe.last_heavy()
-        assert pipe.last_tail() == ("fast" if tail == "dense" else "rows")
+        assert pipe.last_tail() == "rows"
         assert m == g["n_edges"]
         assert edges_sha256(*pipe.edges()) == g["edges_sha256"]
         st = pipe.postings_stats.as_dict()

@@ -22,7 +22,7 @@ KMP_SCORE_COUNT, KMP_SCORE_JACCARD, KMP_SCORE_BLOSUM = 0, 1, 2
 KMP_ENGINE_AUTO, KMP_ENGINE_POSTINGS, KMP_ENGINE_TILES, KMP_ENGINE_RESIDUES = 0, 1, 2, 3
 KMP_KMERS_CODES, KMP_KMERS_IDS = 0, 1
 KMP_LAYOUT_FLAT, KMP_LAYOUT_BUCKETED, KMP_LAYOUT_BUCKETED_HEAVY = 0, 1, 2
-KMP_TAIL_COUNT, KMP_TAIL_FAST, KMP_TAIL_DENSE = 0, 1, 2
+KMP_TAIL_COUNT, KMP_TAIL_FAST = 0, 1
 KMP_PARTITION_AUTO, KMP_PARTITION_COUNT, KMP_PARTITION_CURSOR = 0, 1, 2
 (KMP_SPLIT_RERUN, KMP_SPLIT_CLASS, KMP_SPLIT_HEAVY, KMP_SPLIT_MAX_PART, KMP_SPLIT_MAX_SHARD, KMP_SPLIT_BIN_TILES,
  KMP_SPLIT_CURSOR) = range(7)

@@ -1,0 +1,528 @@
+// postings/api.hip — the extern "C" entry points of the postings engine (include/kmerpair.h).
+// Part of kmp_postings.hip (included there; not a translation unit of its own).
+
+extern "C" {
+
+int kmp_postings_create(kmp_postings** ws) {
+    if (!ws) return KMP_EINVAL;
+    *ws = new (std::nothrow) kmp_postings;
+    return *ws ? KMP_OK : KMP_ENOMEM;
+}
+
+void kmp_postings_destroy(kmp_postings* ws) { delete ws; }
+
+int kmp_postings_set_timing(kmp_postings* ws, int enable) {
+    if (!ws) return KMP_EINVAL;
+    if (enable && !ws->ev[0])
+        for (auto& e : ws->ev) PG(hipEventCreate(&e));
+    ws->timing = enable != 0;
+    return KMP_OK;
+}
+
+int kmp_postings_set_layout(kmp_postings* ws, int bucketed) {
+    if (!ws) return KMP_EINVAL;
+    ws->bucketed = bucketed != 0;
+    return KMP_OK;
+}
+
+int kmp_postings_last_layout(const kmp_postings* ws) {
+    if (!ws || !ws->last_bucketed) return KMP_LAYOUT_FLAT;
+    return ws->last_heavy ? KMP_LAYOUT_BUCKETED_HEAVY : KMP_LAYOUT_BUCKETED;
+}
+
+uint32_t kmp_postings_last_overflow_blocks(const kmp_postings* ws) { return ws ? ws->last_ovf : 0u; }
+
+int kmp_postings_set_flat_heavy(kmp_postings* ws, int enable) {
+    if (!ws) return KMP_EINVAL;
+    ws->flat_heavy = enable ? 1 : 0;
+    return KMP_OK;
+}
+
+int kmp_postings_set_direct(kmp_postings* ws, int enable) {
+    if (!ws) return KMP_EINVAL;
+    ws->direct_tail = enable ? 1 : 0;
+    return KMP_OK;
+}
+
+int kmp_postings_set_tail(kmp_postings* ws, int mode) {
+    if (!ws || (mode != KMP_TAIL_FAST && mode != KMP_TAIL_COUNT)) return KMP_EINVAL;
+    ws->fast_mode = mode != KMP_TAIL_COUNT;
+    ws->fast_tail = ws->fast_mode;
+    return KMP_OK;
+}
+
+int kmp_postings_last_tail(const kmp_postings* ws) {
+    if (!ws || !ws->last_bucketed) return -1;
+    return ws->last_fast ? KMP_TAIL_FAST : KMP_TAIL_COUNT;
+}
+
+int kmp_postings_set_graph(kmp_postings* ws, int enable) {
+    if (!ws) return KMP_EINVAL;
+    ws->graph_on = enable != 0;
+    if (!ws->graph_on && ws->gexec) {
+        (void)hipGraphExecDestroy(ws->gexec);
+        ws->gexec = nullptr;
+        ws->gkey.clear();
+    }
+    if (!ws->graph_on)
+        for (auto& g : ws->split_g) g.reset();
+    ws->gkey_seen.clear();
+    return KMP_OK;
+}
+
+uint64_t kmp_postings_graph_replays(const kmp_postings* ws) { return ws ? ws->graph_replays : 0; }
+
+int kmp_postings_set_partition(kmp_postings* ws, int mode) {
+    if (!ws || (mode != KMP_PARTITION_AUTO && mode != KMP_PARTITION_COUNT)) return KMP_EINVAL;
+    ws->cur_mode = mode == KMP_PARTITION_AUTO;
+    ws->cur_on = ws->cur_mode;
+    ws->front_ok = false;
+    return KMP_OK;
+}
+
+int kmp_postings_last_partition(const kmp_postings* ws) {
+    if (!ws || !ws->last_bucketed) return -1;
+    return ws->cur_used ? KMP_PARTITION_CURSOR : KMP_PARTITION_COUNT;
+}
+
+int kmp_postings_set_shard_floor(kmp_postings* ws, uint64_t keys) {
+    if (!ws) return KMP_EINVAL;
+    // the fullest region at up to twice the mean (measured 1.6x at config 5: frequent k-mers' tiles
+    // land on few shards), a quarter of slack; the fused tail's staging for the pass + 15 %
+    ws->shard_floor = keys ? 2 * keys / kShards + 2 * keys / kShards / 4 + 256 : 0;
+    ws->stage_floor = keys + keys * 3 / 20;
+    return KMP_OK;
+}
+
+int kmp_postings_set_reuse(kmp_postings* ws, int enable) {
+    if (!ws) return KMP_EINVAL;
+    ws->reuse = enable != 0;
+    if (!ws->reuse) ws->front_ok = false;
+    return KMP_OK;
+}
+
+int kmp_dev_pairs_postings(kmp_postings* ws, const uint32_t* d_set, const uint32_t* d_set_len,
+                           const uint64_t* d_res_off, const uint16_t* d_class, uint32_t n, int k, uint64_t slots,
+                           uint32_t heavy_df, uint32_t min_shared, int require_class_diff, uint32_t* d_p,
+                           uint32_t* d_q, uint32_t* d_w, uint64_t cap, uint64_t* n_edges,
+                           kmp_postings_stats* stats, void* stream) {
+    int rc = postings_args(ws, k, n_edges, stats, d_p, d_q, d_w, cap);
+    if (rc != KMP_OK || n < 2) return rc;
+    if (!d_set || !d_set_len || !d_res_off || !d_class) return KMP_EINVAL;
+    hipStream_t st = as_stream(stream);
+    auto keys = [&](const Layout& lay, hipStream_t st) {
+        ws->cur_used = false;  // keys grouped by the bucket sort
+        set_keys_kernel<<<n + 1, 256, 0, st>>>(d_set, d_set_len, d_res_off, d_class, n, slots, lay, ws->keys.p,
+                                               ws->flags.p);
+        return hipGetLastError();
+    };
+    const std::vector<unsigned long long> key_extra = {0, (uintptr_t)d_set, (uintptr_t)d_set_len, (uintptr_t)d_res_off,
+                                                       (uintptr_t)d_class};
+    return run_postings(ws, keys, key_extra, n, k, slots, d_class, heavy_df, min_shared, require_class_diff, false, 0,
+                        n, d_p, d_q, d_w, cap, n_edges, stats, st);
+}
+
+// the residue key paths take the step's clear into their first kernel, for the call that sets this
+struct ClearInKeys {
+    kmp_postings* ws;
+    explicit ClearInKeys(kmp_postings* w) : ws(w) { ws->clear_in_keys = true; }
+    ~ClearInKeys() {
+        ws->clear_in_keys = false;
+        ws->defer_clear = false;
+    }
+};
+
+static int residues_impl(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
+                         uint32_t n, int k, uint64_t slots, uint32_t heavy_df, uint32_t min_shared,
+                         int require_class_diff, bool ranged, uint32_t row_lo, uint32_t row_hi, uint32_t* d_p,
+                         uint32_t* d_q, uint32_t* d_w, uint64_t cap, uint64_t* n_edges, kmp_postings_stats* stats,
+                         void* stream, unsigned sb = 0, uint32_t sor = 0, uint32_t* d_s = nullptr,
+                         uint32_t* d_w1 = nullptr, uint64_t* n_inc_out = nullptr) {
+    int rc = postings_args(ws, k, n_edges, stats, d_p, d_q, d_w, cap);
+    if (rc != KMP_OK || n < 2) return rc;
+    if (!d_res || !d_res_off || !d_class) return KMP_EINVAL;
+    hipStream_t st = as_stream(stream);
+    auto keys = [&](const Layout& lay, hipStream_t st) {
+        if (lay.bucketed) {
+            ws->parted = true;
+            ws->cur_used = ws->cur_on && cur_geometry(lay, &ws->cg);
+            ws->cg.vreg = ws->cur_used && ws->vreg_on ? ws->vreg.p : nullptr;
+            return bp_level1(ws, d_res, d_res_off, d_class, k, n, slots, lay, st);
+        }
+        ws->cur_used = false;
+        if (ws->defer_clear) {
+            step_clear_kernel<<<1, 256, 0, st>>>(ws->flags.p, ws->bstats.p, ws->clear_extra, ws->clear_n);
+            ws->defer_clear = false;
+        }
+        return launch_residue_keys(ws, d_res, d_res_off, d_class, k, 0u, n, 0ull, slots, lay, st);
+    };
+    const std::vector<unsigned long long> key_extra = {1, (uintptr_t)d_res, (uintptr_t)d_res_off, (uintptr_t)d_class};
+    const ClearInKeys guard(ws);
+    return run_postings(ws, keys, key_extra, n, k, slots, d_class, heavy_df, min_shared, require_class_diff, ranged,
+                        row_lo, row_hi, d_p, d_q, d_w, cap, n_edges, stats, st, sb, sor, d_s, d_w1, n_inc_out);
+}
+
+int kmp_dev_pairs_residues(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off,
+                           const uint16_t* d_class, uint32_t n, int k, uint64_t slots, uint32_t heavy_df,
+                           uint32_t min_shared, int require_class_diff, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w,
+                           uint64_t cap, uint64_t* n_edges, kmp_postings_stats* stats, void* stream) {
+    return residues_impl(ws, d_res, d_res_off, d_class, n, k, slots, heavy_df, min_shared, require_class_diff, false,
+                         0, n, d_p, d_q, d_w, cap, n_edges, stats, stream);
+}
+
+int kmp_dev_pairs_rows(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
+                       uint32_t n, int k, uint64_t slots, uint32_t heavy_df, uint32_t min_shared,
+                       int require_class_diff, uint32_t row_lo, uint32_t row_hi, uint32_t* d_p, uint32_t* d_q,
+                       uint32_t* d_w, uint64_t cap, uint64_t* n_edges, kmp_postings_stats* stats, void* stream) {
+    if (row_lo > row_hi || row_hi > n) return KMP_EINVAL;
+    if (row_lo == row_hi) {
+        int rc = postings_args(ws, k, n_edges, stats, d_p, d_q, d_w, cap);
+        return rc;
+    }
+    return residues_impl(ws, d_res, d_res_off, d_class, n, k, slots, heavy_df, min_shared, require_class_diff, true,
+                         row_lo, row_hi, d_p, d_q, d_w, cap, n_edges, stats, stream);
+}
+
+uint32_t kmp_dev_rows_max(uint32_t n, int scored) {
+    // the row-block tail's u32 key (p_local << pbits | q, scored << kScoreBits more, multi-k one k
+    // bit more, one padding bit) and its kPtMaxBlocks row blocks bound the rows of one call
+    const unsigned used = bits_for(n) + (scored ? kScoreBits : 0u) + (scored > 1 ? 1u : 0u);
+    if (used >= 31) return 0;
+    const uint64_t m = (uint64_t)kPtMaxBlocks << (31 - used);
+    return (uint32_t)std::min<uint64_t>(m, n);
+}
+
+int kmp_dev_pairs_rows_scored(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
+                              uint32_t n, int k, uint64_t slots, uint32_t heavy_df, uint32_t min_shared,
+                              int require_class_diff, uint32_t row_lo, uint32_t row_hi, uint32_t* d_p, uint32_t* d_q,
+                              uint32_t* d_w, uint32_t* d_score, uint64_t cap, uint64_t* n_edges,
+                              kmp_postings_stats* stats, void* stream) {
+    if (row_lo > row_hi || row_hi > n) return KMP_EINVAL;
+    if (cap && !d_score) return KMP_EINVAL;
+    if (row_hi - row_lo > kmp_dev_rows_max(n, 1)) return KMP_EINVAL;
+    if (row_lo == row_hi) return postings_args(ws, k, n_edges, stats, d_p, d_q, d_w, cap);
+    const bool ranged = !(row_lo == 0 && row_hi == n);
+    return residues_impl(ws, d_res, d_res_off, d_class, n, k, slots, heavy_df, min_shared, require_class_diff, ranged,
+                         row_lo, row_hi, d_p, d_q, d_w, cap, n_edges, stats, stream, kScoreBits, 0u, d_score, nullptr);
+}
+
+int kmp_dev_pairs_rows_multi(kmp_postings* const* ws, const int* ks, uint32_t nk, const uint8_t* d_res,
+                             const uint64_t* d_res_off, const uint16_t* d_class, uint32_t n, uint64_t slots,
+                             uint32_t min_shared, int require_class_diff, uint32_t row_lo, uint32_t row_hi,
+                             uint32_t* d_p, uint32_t* d_q, uint32_t* d_w, uint32_t* d_score, uint32_t* d_w0,
+                             uint32_t* d_w1, uint64_t cap, uint64_t* n_edges, kmp_postings_stats* stats,
+                             void* stream) {
+    if (!ws || !ks || nk != 2 || !n_edges || row_lo > row_hi || row_hi > n) return KMP_EINVAL;
+    if (!ws[0] || !ws[1] || ws[0] == ws[1] || ks[0] == ks[1]) return KMP_EINVAL;
+    for (uint32_t j = 0; j < nk; ++j)
+        if (ks[j] < 1 || ks[j] > kMaxK) return KMP_EINVAL;
+    if (cap && (!d_p || !d_q || !d_w || !d_score || !d_w0 || !d_w1)) return KMP_EINVAL;
+    if (row_hi - row_lo > kmp_dev_rows_max(n, 2)) return KMP_EINVAL;
+    *n_edges = 0;
+    if (stats) *stats = kmp_postings_stats{};
+    if (row_lo == row_hi || n < 2) return KMP_OK;
+    if (!d_res || !d_res_off || !d_class) return KMP_EINVAL;
+    hipStream_t st = as_stream(stream);
+    const bool ranged = !(row_lo == 0 && row_hi == n);
+    // the tail's geometry and outputs (the same StepCfg fields the step uses)
+    StepCfg c{};
+    c.n = n;
+    c.min_shared = std::max(1u, min_shared);
+    c.ranged = ranged;
+    c.row_lo = row_lo;
+    c.row_hi = row_hi;
+    c.d_p = d_p;
+    c.d_q = d_q;
+    c.d_w = d_w;
+    c.cap = cap;
+    c.stride = 1;
+    c.sb = kScoreBits + 1;
+    c.d_s = d_score;
+    c.d_w1 = d_w1;
+    c.d_w0 = d_w0;
+    const std::vector<unsigned long long> call = {n, (unsigned long long)ks[0], (unsigned long long)ks[1], row_lo, row_hi,
+                                                  c.min_shared, (unsigned long long)require_class_diff, slots,
+                                                  (uintptr_t)d_res, (uintptr_t)ws[1]};
+    if (ws[0]->pend_key == call) {  // the same call after KMP_EOVERFLOW: emit the staged runs again
+        const int rc = tail_multi_emit(ws[0], c, n_edges, st);
+        if (rc == KMP_OK) ws[0]->pend_key.clear();
+        return rc;
+    }
+    ws[0]->pend_key.clear();
+    uint64_t inc[2] = {0, 0};
+    kmp_postings_stats s0{};
+    const bool timed = stats != nullptr;  // stage_ms: [0] first k expanded, [1] second k, [2] the fused tail
+    if (timed && !ws[0]->mev[0])
+        for (auto& e : ws[0]->mev) PG(hipEventCreate(&e));
+    if (timed) PG(hipEventRecord(ws[0]->mev[0], st));
+    for (uint32_t j = 0; j < nk; ++j) {
+        // expand only: every incidence keyed (pair << 8) | j << 7 | s(x)
+        uint64_t unused = 0;
+        int rc = residues_impl(ws[j], d_res, d_res_off, d_class, n, ks[j], slots, 0xFFFFFFFFu, 1, require_class_diff,
+                               ranged, row_lo, row_hi, d_p, d_q, d_w, cap, &unused, j == 0 ? &s0 : nullptr, stream,
+                               kScoreBits + 1, j << kScoreBits, d_score, d_w1, &inc[j]);
+        if (rc != KMP_OK) return rc;
+        if (timed) PG(hipEventRecord(ws[0]->mev[1 + j], st));
+    }
+    int rc = tail_multi(ws, nk, c, inc, n_edges, stats, st);
+    if (rc == KMP_EOVERFLOW) ws[0]->pend_key = call;
+    if (timed && (rc == KMP_OK || rc == KMP_EOVERFLOW)) {
+        PG(hipEventRecord(ws[0]->mev[3], st));
+        PG(hipEventSynchronize(ws[0]->mev[3]));
+        for (int i = 0; i < 3; ++i) {
+            float ms = 0.f;
+            stats->stage_ms[i] = hipEventElapsedTime(&ms, ws[0]->mev[i], ws[0]->mev[i + 1]) == hipSuccess ? ms : -1.f;
+        }
+        (void)hipGetLastError();
+        for (int i = 3; i < KMP_POSTINGS_STAGES; ++i) stats->stage_ms[i] = 0.f;
+    }
+    if (stats) {  // the first k's front statistics
+        stats->sum_S = s0.sum_S;
+        stats->distinct = s0.distinct;
+        stats->repeat = s0.repeat;
+        stats->sum_cdf2_light = s0.sum_cdf2_light;
+        stats->max_df = s0.max_df;
+        stats->heavy_entries = s0.heavy_entries;
+    }
+    return rc;
+}
+
+int kmp_dev_split_expand(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
+                         uint32_t n, int k, uint64_t slots, uint32_t heavy_df, int require_class_diff, uint32_t part,
+                         uint32_t parts, uint64_t cap, const uint32_t* learn, unsigned long long* d_send,
+                         uint32_t* d_flags, unsigned long long* d_stats, void* stream) {
+    if (!ws || !d_res || !d_res_off || !d_class || !d_send || !d_flags || !d_stats || k < 1 || k > kMaxK ||
+        parts < 1 || parts > kSplitMax || part >= parts || cap < 1)
+        return KMP_EINVAL;
+    hipStream_t st = as_stream(stream);
+    if (heavy_df < 2) heavy_df = 2;
+    const Layout lay = make_layout(n, k, slots, true);
+    if (!lay.bucketed) return KMP_ESTATE;
+    const std::vector<unsigned long long> shape = {n, slots, (unsigned long long)k, parts};
+    if (ws->split_shape != shape) {  // a new batch: learned capacities start over
+        ws->split_shape = shape;
+        ws->shard_cap = slots / 4 / kShards / parts + 4096;
+        ws->bp_J_min = 0;
+        ws->cur_on = ws->cur_mode;
+        ws->shape.clear();
+        ws->split_heavy = false;
+        ws->fast_tail = ws->fast_mode;
+    }
+    if (learn) {  // the last call's flags, reduced over the ranks: every rank grows the same way
+        if (learn[KMP_SPLIT_HEAVY]) ws->split_heavy = true;  // a rank spilled: the heavy path from now on
+        // an eighth of slack: the fullest region varies by a few percent from call to call with the
+        // heavy path on (3.8 % measured on uniprot k = 5 at G = 2), and a rerun costs a whole step
+        if (learn[KMP_SPLIT_MAX_SHARD] > ws->shard_cap)
+            ws->shard_cap = learn[KMP_SPLIT_MAX_SHARD] + learn[KMP_SPLIT_MAX_SHARD] / 8 + 256;
+        if (learn[KMP_SPLIT_BIN_TILES]) ws->bp_J_min = std::max(ws->bp_J_min, learn[KMP_SPLIT_BIN_TILES] + 2);
+        if (learn[KMP_SPLIT_CURSOR]) ws->cur_on = false;
+    }
+    if (ws->spill_cap == 0) ws->spill_cap = 1024;
+    ws->front_ok = false;  // the front below holds one bucket range only
+    StepCfg c{};
+    c.slots = slots;
+    c.lay = lay;
+    c.n = n;
+    c.heavy_df = heavy_df;
+    c.min_shared = 1;
+    c.require_diff = require_class_diff;
+    c.row_hi = n;
+    c.stride = 1;
+    PtGeom g;
+    if (!pt_geometry(ws, c, slots / 4, &g)) return KMP_EINVAL;
+    {
+        const int rc = step_reserve(ws, c, g, st);
+        if (rc != KMP_OK) return rc;
+    }
+    PG(ws->split_cur.reserve((uint64_t)kSplitMax * kShards));
+    const BpDigits dg = bp_digits(lay);
+    ws->bin_lo = (uint32_t)((uint64_t)part * dg.nb1 / parts);
+    ws->bin_hi = (uint32_t)((uint64_t)(part + 1) * dg.nb1 / parts);
+    auto make_keys = [&](const Layout& l, hipStream_t s) {
+        ws->parted = true;
+        ws->cur_used = ws->cur_on && cur_geometry(l, &ws->cg);
+        return bp_level1(ws, d_res, d_res_off, d_class, k, n, slots, l, s);
+    };
+    const ClearInKeys guard(ws);
+    SplitRows rows{};
+    rows.parts = parts;
+    kmp_row_split(n, parts, rows.start);
+    // the send cursors are cleared with the step's flags (by chunk_desc_kernel in the front); routed
+    // (no heavy path): the bucket kernels write the send regions, pre-filled with kNoKey
+    const bool routed = !ws->split_heavy;
+    auto front = [&](hipStream_t s) -> int {
+        const uint32_t ncur = routed ? parts * kShards : parts;
+        ws->clear_extra = ws->split_cur.p;
+        ws->clear_n = ncur;
+        if (routed) {
+            PG(hipMemsetAsync(d_send, 0xFF, (size_t)parts * cap * sizeof(unsigned long long), s));
+            ws->route_send = d_send;
+            ws->route_cap = cap;
+            ws->route_rows = rows;
+        }
+        int rc = KMP_OK;
+        if (ws->bin_hi > ws->bin_lo) rc = enqueue_front(ws, make_keys, c, true, s);
+        else step_clear_kernel<<<1, 256, 0, s>>>(ws->flags.p, ws->bstats.p, ws->split_cur.p, ncur);  // no bins
+        ws->clear_extra = nullptr;
+        ws->clear_n = 0;
+        ws->route_send = nullptr;
+        return rc;
+    };
+    auto route = [&](hipStream_t s, int heavy_done) -> int {
+        if (routed) {  // the bucket kernels routed the keys: the flags and statistics only
+            split_pad_finish_kernel<<<dim3(1, 1), 256, 0, s>>>(d_send, cap, ws->split_cur.p, ws->bstats.p, ws->flags.p,
+                                                                ws->shard_cap, parts, d_flags, d_stats, heavy_done, 1);
+            PG(hipGetLastError());
+            return KMP_OK;
+        }
+        const unsigned long long* cursor = ws->bstats.p + kRbCursor;
+        split_route_kernel<<<dim3((uint32_t)((ws->shard_cap + kRtTile - 1) / kRtTile), kShards), kRtThreads, 0, s>>>(
+            ws->inc_sorted.p, cursor, ws->shard_cap, bits_for(n), rows, cap, d_send, ws->split_cur.p);
+        split_pad_finish_kernel<<<dim3((uint32_t)std::min<uint64_t>((cap + 1023) / 1024, 256), parts), 256, 0, s>>>(
+            d_send, cap, ws->split_cur.p, ws->bstats.p, ws->flags.p, ws->shard_cap, parts, d_flags, d_stats,
+            heavy_done, 0);
+        PG(hipGetLastError());
+        return KMP_OK;
+    };
+    if (ws->split_heavy) {
+        // frequent k-mers (vertex.rs:59-140 at k = 5): the rank's front, one read-back, its spill
+        // compacted, planned and expanded by the heavy path into the same shard regions (the heavy
+        // pairs of the rank's k-mers, all rows), then routed like the light keys.  The spill regions
+        // are the rank's own, so a spill overflow reruns the front here; every other capacity is
+        // reported in the flags and grown identically on every rank.  Host-synchronous.
+        int rc = KMP_OK;
+        bool routed = false;
+        for (int attempt = 0; attempt < 4; ++attempt) {
+            if ((rc = step_reserve(ws, c, g, st)) != KMP_OK) break;
+            if ((rc = front(st)) != KMP_OK) break;
+            step_pack_kernel<<<1, 256, 0, st>>>(ws->bstats.p, ws->flags.p, nullptr, ws->hrb);
+            PG(hipStreamSynchronize(st));
+            const unsigned long long* rb = ws->hrb;
+            unsigned long long acc[kStN], most, n_inc, spill_most, spill_total;
+            sum_stats(rb, acc, &most, &n_inc, &spill_most, &spill_total);
+            if (spill_most > ws->spill_cap) {
+                ws->spill_cap = spill_most + spill_most / 8 + 1024;
+                continue;
+            }
+            // a bin or cursor-region overflow: the flags rerun the step, no heavy work on it
+            if (spill_total && !rb[kRbFlagBin] && !(rb[kRbFlagCur] && ws->cur_used)) {
+                ws->heavy_ready = ws->hcur_valid = false;  // this call's front
+                ws->h_segs = rb[kRbSegs];
+                ws->h_segmax = rb[kRbSegMax];
+                if ((rc = heavy_phase(ws, c, spill_total, true, st)) != KMP_OK) break;
+            }
+            rc = route(st, 1);
+            routed = true;
+            break;
+        }
+        ws->bin_lo = ws->bin_hi = 0;
+        if (rc == KMP_OK && !routed) {
+            // every attempt grew the spill regions: no keys are sent and the flags ask every rank for
+            // a rerun, so the ranks stay in lockstep through the collectives (an error returned here
+            // on one rank alone would leave the others waiting in the all-to-all); the grown regions
+            // are this rank's own and stay for the rerun
+            PG(hipMemsetAsync(d_send, 0xFF, (size_t)parts * cap * sizeof(unsigned long long), st));
+            PG(hipMemsetAsync(d_flags, 0, KMP_SPLIT_FLAGS * sizeof(uint32_t), st));
+            PG(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_flags + KMP_SPLIT_RERUN), 1, 1, st));
+            PG(hipMemsetAsync(d_stats, 0, 8 * sizeof(unsigned long long), st));
+        }
+        return rc;
+    }
+    auto enqueue = [&](hipStream_t s) -> int {
+        const int rc = front(s);
+        return rc != KMP_OK ? rc : route(s, 0);
+    };
+    const std::vector<unsigned long long> key = {
+        n, slots, (unsigned long long)k, heavy_df, (unsigned long long)require_class_diff, part, parts, cap,
+        (uintptr_t)d_res, (uintptr_t)d_res_off, (uintptr_t)d_class, (uintptr_t)d_send, (uintptr_t)d_flags,
+        (uintptr_t)d_stats, ws->shard_cap, ws->spill_cap, ws->bp_J_min, ws->cur_on, ws->timing};
+    const int rc = slot_launch(ws, ws->split_g[0], key, enqueue, st);
+    ws->bin_lo = ws->bin_hi = 0;
+    return rc;
+}
+
+int kmp_dev_split_edges(kmp_postings* ws, const unsigned long long* d_keys, uint64_t m, uint32_t n, uint32_t row_lo,
+                        uint32_t row_hi, uint32_t min_shared, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w,
+                        uint64_t cap, uint64_t* n_edges, void* stream) {
+    if (!ws || !n_edges || row_lo > row_hi || row_hi > n || (m && !d_keys) || (cap && (!d_p || !d_q || !d_w)))
+        return KMP_EINVAL;
+    *n_edges = 0;
+    hipStream_t st = as_stream(stream);
+    if (m == 0 || row_lo == row_hi) {  // nothing to reduce; still synchronous, as the full path is
+        PG(hipStreamSynchronize(st));
+        return KMP_OK;
+    }
+    if (m > 0xFFFFFFFFull) return KMP_EINVAL;
+    StepCfg c{};
+    c.n = n;
+    c.min_shared = std::max(1u, min_shared);
+    c.ranged = true;
+    c.row_lo = row_lo;
+    c.row_hi = row_hi;
+    c.d_p = d_p;
+    c.d_q = d_q;
+    c.d_w = d_w;
+    c.cap = cap;
+    c.stride = 1;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        PtGeom g;
+        if (!pt_geometry(ws, c, m, &g)) return KMP_EINVAL;
+        g.flat_n = m;  // the received regions, padded with kNoKey, read as one array
+        g.nshards = 1;
+        g.sc = m;
+        g.jt = (uint32_t)((m + kPtTile - 1) / kPtTile);
+        hipError_t e = hipSuccess;
+        pt_bufs(ws, g, true, &e, st);
+        PG(e);
+        PG(ws->inc.reserve(pt_fast(ws, g) ? std::max<uint64_t>(m, (uint64_t)g.nrb * g.ftcap / 2) : m));  // u32 row-block keys
+        PG(ws->uniq.reserve(m));  // staged p | q (u32 each)
+        PG(ws->w.reserve(m));
+        PG(ws->ovf.reserve((uint64_t)g.nrb + 1));
+        PG(ws->small.reserve(16));
+        PG(ws->flags.reserve(kFlN));
+        PG(ws->bstats.reserve(kGsWords));
+        if (!ws->hrb) PG(hipHostMalloc((void**)&ws->hrb, kRbWords * sizeof(unsigned long long), hipHostMallocCoherent));
+        auto enqueue = [&](hipStream_t s) -> int {
+            step_clear_kernel<<<1, 256, 0, s>>>(ws->flags.p, ws->bstats.p);  // flags (the expand's stats are out)
+            return enqueue_tail_in(ws, c, g, d_keys, nullptr, m, s);
+        };
+        const std::vector<unsigned long long> key = {m, n, row_lo, row_hi, c.min_shared, cap, (uintptr_t)d_keys,
+                                                     (uintptr_t)d_p, (uintptr_t)d_q, (uintptr_t)d_w, g.rbits,
+                                                     ws->timing, ws->fast_tail};
+        int rc = slot_launch(ws, ws->split_g[1], key, enqueue, st);
+        if (rc != KMP_OK) return rc;
+        PG(hipStreamSynchronize(st));
+        const unsigned long long* rb = ws->hrb;
+        if (rb[kRbFast]) {  // a fast-tail region overflowed: the counting tail (learned until a new shape)
+            ws->fast_tail = false;
+            continue;
+        }
+        uint64_t ne = rb[kRbRuns];
+        if (rb[kRbOvf] && !pt_rowhist_ok(g)) {  // row blocks above the LDS capacity: the segmented sort, fewer rows per block next time
+            if (g.rbits > 0) {
+                const double over = (double)rb[kRbMaxBlock] / (0.8 * kPtCap);
+                unsigned shrink = 1;
+                while (shrink < 16 && (double)(1u << shrink) < over) ++shrink;
+                ws->pt_rb_max = g.rbits > shrink ? g.rbits - shrink : 0u;
+            }
+            rc = pt_finish_overflow(ws, c, g, (uint32_t)rb[kRbOvf], &ne, st, m);
+            if (rc != KMP_OK) return rc;
+        }
+        *n_edges = ne;
+        return ne > cap ? KMP_EOVERFLOW : KMP_OK;
+    }
+    return KMP_EDEVICE;
+}
+
+// Row ranges of a split of the pair space: a pair belongs to its smaller protein, so row p owns
+// about N - p pairs; range d starts at N * (1 - sqrt(1 - d/parts)) (equal expected pair counts).
+void kmp_row_split(uint32_t n, uint32_t parts, uint32_t* start) {
+    for (uint32_t d = 0; d <= parts; ++d) {
+        const double x = 1.0 - std::sqrt(1.0 - (double)d / parts);
+        start[d] = d == parts ? n : (uint32_t)std::min<double>(n, std::floor(x * n));
+    }
+}
+
+}  // extern "C"
+
+#undef PG

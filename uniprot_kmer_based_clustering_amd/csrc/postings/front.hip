@@ -1,0 +1,259 @@
+// postings/front.hip — host side of the front: level 1 / level 2 / bucket launches.
+// Part of kmp_postings.hip (included there; not a translation unit of its own).
+
+void fill_stats(kmp_postings_stats* stats, const unsigned long long* acc) {
+    if (!stats) return;
+    stats->sum_S = acc[kStSumS];
+    stats->distinct = acc[kStDistinct];
+    stats->repeat = acc[kStRepeat];
+    stats->sum_cdf2_light = acc[kStCdf2];
+    stats->max_df = acc[kStMaxDf];
+    stats->heavy_entries = acc[kStHeavy];
+    stats->incidences = acc[kStInc];
+}
+
+// Level 1 of the bucket partition for proteins [0, n): ws->keys = the valid keys grouped by
+// digit1; C1 = coarse bin starts (C1[nb1] = key count) in ws->bp for level 2.
+// the call's coarse bins [*lo, *hi)
+void own_bins(const kmp_postings* ws, const BpDigits& dg, uint32_t* lo, uint32_t* hi) {
+    *lo = ws->bin_hi ? ws->bin_lo : 0u;
+    *hi = ws->bin_hi ? std::min(ws->bin_hi, dg.nb1) : dg.nb1;
+}
+
+__global__ void step_clear_kernel(uint32_t* __restrict__ flags, unsigned long long* __restrict__ gstats,
+                                  unsigned long long* __restrict__ extra, uint32_t n_extra);
+
+hipError_t bp_level1(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
+                     int k, uint32_t n, uint64_t slots, const Layout& lay, hipStream_t st) {
+    const BpDigits dg = bp_digits(lay);
+    uint32_t dlo, dhi;
+    own_bins(ws, dg, &dlo, &dhi);
+    const uint64_t G64 = (slots + kKeyChunk - 1) / kKeyChunk;
+    if (G64 * dg.nb1 > 0xFFFFFFFFull || slots > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    const uint32_t G = (uint32_t)G64, groups = (G + kBpRowGroup - 1) / kBpRowGroup;
+    // coarse bins are hash-uniform: a budget of 1.25x the mean plus two tiles
+    ws->bp_J = std::max(ws->bp_J_min, (uint32_t)((slots / dg.nb1 * 5 / 4 + kBpTile - 1) / kBpTile) + 2);
+    const uint64_t h1 = (uint64_t)G * dg.nb1, r = (uint64_t)groups * dg.nb1;
+    const uint64_t need = 2 * h1 + r + 2 * (dg.nb1 + 1) + (uint64_t)dg.nb1 * ws->bp_J * dg.nb2;
+    hipError_t e = ws->bp.reserve(need);
+    if (e == hipSuccess) e = ws->keys.reserve(slots + (uint64_t)kBpAlign * dg.nb1);  // + alignment gaps
+    if (e == hipSuccess) e = ws->chunk_first.reserve(G + 1);
+    if (e != hipSuccess) return e;
+    uint32_t *H1 = ws->bp.p, *P1 = H1 + h1, *R = P1 + h1, *C1 = R + r;
+    ws->bp_c1 = 2 * h1 + r;
+    const uint32_t pw21 = (uint32_t)pow21(k - 1);
+    ws->bp_local = ws->cur_used;
+    const uint32_t nb = 1u << lay.bbits;
+    if (ws->bp_local) e = ws->cur.reserve(nb);
+    if (e != hipSuccess) return e;
+    if (ws->defer_clear && !ws->bp_local) {  // no chunk descriptors on this path: the clear first
+        step_clear_kernel<<<1, 256, 0, st>>>(ws->flags.p, ws->bstats.p, ws->clear_extra, ws->clear_n);
+        ws->defer_clear = false;
+    }
+    if (ws->bp_local) {  // local level 1 for the cursor level 2: H1 (own digits) | H1T
+        e = ws->chunk_desc.reserve(4ull * G);
+        if (e != hipSuccess) return e;
+        // descriptors + the cursor level 2's bucket counts cleared (bp_level2c does not)
+        StepClear sc{};
+        if (ws->defer_clear) {  // the front's clear, folded into this first kernel
+            sc = StepClear{ws->flags.p, kFlN, ws->bstats.p, kShards * 10, ws->clear_extra, ws->clear_n};
+            ws->defer_clear = false;
+        }
+        chunk_desc_kernel<<<(n + 1 + 255) / 256, 256, 0, st>>>(d_res_off, n, slots, G, k,
+                                                               reinterpret_cast<uint4*>(ws->chunk_desc.p), ws->cur.p,
+                                                               nb, sc);
+        ws->bp_G = G;
+        ws->bp_h1t = h1;
+        // T chunks per level-2 tile: ~7/4 of a round at the hash-uniform mean (two rounds; kKeyChunk / nb1 keys
+        // per chunk and bin)
+        ws->bp_T = std::min<uint32_t>(kBpGatherMax, std::max<uint32_t>(1, kBpGatherTile * 7 / 4 * dg.nb1 / kKeyChunk));
+        const uint32_t nown = dhi - dlo;
+        // a few own bins (a rank's share of the k-mer split): level 2 reads the run table as level 1
+        // wrote it (bp_hsc = own bins); otherwise transposed, so a bin's runs are contiguous
+        const bool direct = nown <= 64 && nown < dg.nb1;
+        ws->bp_hsb = direct ? 1u : G;
+        ws->bp_hsc = direct ? nown : 1u;
+        if (direct) ws->bp_h1t = 0;
+        // persistent: as many workgroups as fit the device at once, each walking its chunks with the
+        // next one's loads in flight
+        static thread_local int per_cu = 0;
+        if (!per_cu && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bp_scatter1p_kernel<KMP_L1_THREADS>,
+                                                                     KMP_L1_THREADS, 0) != hipSuccess ||
+                        per_cu < 1))
+            per_cu = 2;
+        // every bin owned (one GPU): one workgroup per chunk, in order (bp_scatter1p 112 -> 103 us at
+        // config 3); a share of the bins (a rank of the k-mer split, little work per chunk): persistent
+#ifndef KMP_L1P_ALWAYS
+#define KMP_L1P_ALWAYS 0  // A/B: the persistent grid on one GPU too
+#endif
+        const uint32_t grid = nown >= dg.nb1 && !KMP_L1P_ALWAYS ? G
+                                                                 : std::min<uint32_t>(G, (uint32_t)per_cu * device_cus());
+        if (nown) {
+            bp_scatter1p_kernel<KMP_L1_THREADS><<<grid, KMP_L1_THREADS, 0, st>>>(
+                d_res, d_res_off, d_class, k, n, slots, G, reinterpret_cast<const uint4*>(ws->chunk_desc.p), lay, dg,
+                pw21, dlo, dhi, H1, ws->keys.p, ws->flags.p);
+            if (!direct)
+                bp_h1t_kernel<<<dim3((G + 31) / 32, (nown + 31) / 32), 256, 0, st>>>(H1, G, nown, 0, nown, H1 + h1);
+        }
+        return hipGetLastError();
+    }
+    chunk_first_kernel<<<(n + 1 + 255) / 256, 256, 0, st>>>(d_res_off, 0u, n, 0ull, slots, G, ws->chunk_first.p);
+    bp_hist1_kernel<<<G, kKeyThreads, 0, st>>>(d_res, d_res_off, d_class, k, n, slots, ws->chunk_first.p, lay, dg,
+                                                pw21, dlo, dhi, H1, ws->flags.p);
+    bp_colsum_kernel<<<dim3(groups, (dg.nb1 + 255) / 256), 256, 0, st>>>(H1, G, dg.nb1, R);
+    bp_colscan_kernel<<<1, kColThreads, 0, st>>>(R, groups, dg.nb1, C1);
+    bp_colprefix_kernel<<<dim3(groups, (dg.nb1 + 255) / 256), 256, 0, st>>>(H1, G, dg.nb1, R, P1);
+    bp_scatter1_kernel<<<G, kKeyThreads, 0, st>>>(d_res, d_res_off, d_class, k, n, slots, ws->chunk_first.p, lay, dg,
+                                                   pw21, dlo, dhi, P1, ws->keys.p, ws->flags.p);
+    return hipGetLastError();
+}
+
+// Level 2: ws->keys (level 1) -> ws->sorted grouped by bucket, bstart[0..nb] in ws->cnt.
+int bp_level2(kmp_postings* ws, const Layout& lay, hipStream_t st) {
+    const BpDigits dg = bp_digits(lay);
+    uint32_t* C1 = ws->bp.p + ws->bp_c1;
+    uint32_t* H2 = C1 + 2 * (dg.nb1 + 1);
+    const uint32_t nb = 1u << lay.bbits, J = ws->bp_J;
+    uint32_t c0, c1;
+    own_bins(ws, dg, &c0, &c1);
+    PG(ws->cnt.reserve(2 * (uint64_t)nb + 2));
+    if (c1 > c0) {
+        bp_hist2_kernel<<<dim3(J, c1 - c0), kKeyThreads, 0, st>>>(ws->keys.p, C1, J, dg, H2, c0);
+        bp_scan2_kernel<<<c1 - c0, kKeyThreads, 0, st>>>(H2, C1, J, dg, ws->cnt.p, ws->flags.p, c0);
+        bp_scatter2_kernel<<<dim3(J, c1 - c0), kKeyThreads, 0, st>>>(ws->keys.p, C1, J, dg, H2, ws->sorted.p, c0);
+    }
+    PG(hipGetLastError());
+    return KMP_OK;
+}
+
+// Cursor level-2 geometry from the hash-uniform mean bucket; false when the region offsets
+// would not fit the u32 arithmetic of the kernels
+bool cur_geometry(const Layout& lay, CurGeom* cg) {
+    const uint64_t nb = 1ull << lay.bbits;
+    const uint64_t capb = (std::max<uint64_t>(2ull * lay.mean_keys + 512, 1536) + 63) / 64 * 64;
+    if (nb * capb + capb >= (1ull << 32) - 2 * kBpTile) return false;
+    cg->capb = (uint32_t)capb;
+    cg->vreg = nullptr;  // the fixed layout (a residue call may switch to its learned one)
+    return true;
+}
+
+// KMP_GATHER_THREADS: workgroup size of the level-2 gather (a 4,096-key round either way).  512
+// threads x 8 keys (82 VGPRs, 6 waves per SIMD instead of 3) measured no faster at config 3
+// (buckets_level2 0.159-0.164 ms vs 0.149-0.160 ms), so 256 x 16 stays
+#ifndef KMP_GATHER_THREADS
+#define KMP_GATHER_THREADS 256
+#endif
+// Level 2, cursor variant: ws->keys (level 1) -> the bucket regions of ws->sorted, counts in ws->cur.
+int bp_level2c(kmp_postings* ws, const Layout& lay, hipStream_t st) {
+    const BpDigits dg = bp_digits(lay);
+    const uint32_t nb = 1u << lay.bbits;
+    uint32_t* C1 = ws->bp.p + ws->bp_c1;
+    PG(ws->cur.reserve(nb));
+    PG(ws->sorted.reserve(ws->cg.vreg ? ws->vreg_total : (uint64_t)nb * ws->cg.capb));
+    PG(ws->cnt.reserve(2 * (uint64_t)nb + 2));  // the large-bucket list
+    uint32_t c0, c1;
+    own_bins(ws, dg, &c0, &c1);
+    if (!ws->bp_local)  // the local level 1 cleared the counts with its chunk_first
+        bp_cur_clear_kernel<<<std::min<uint32_t>((nb + 1023) / 1024, 1024), 1024, 0, st>>>(ws->cur.p, nb);
+    if (c1 > c0 && ws->bp_local) {
+        const uint32_t ntiles = (ws->bp_G + ws->bp_T - 1) / ws->bp_T, per = (ntiles * (c1 - c0) + 7) / 8;
+        constexpr uint32_t kGp = kBpGatherTile / KMP_GATHER_THREADS, kGt = KMP_GATHER_THREADS;
+        if (ws->cg.vreg)
+            bp_scatter2g_kernel<kGp, kGt, true><<<8 * per, kGt, 0, st>>>(
+                ws->keys.p, ws->bp.p + ws->bp_h1t, ws->bp_G, ws->bp_hsb, ws->bp_hsc, ws->bp_T, ntiles, c1 - c0, dg, ws->cg,
+                ws->cur.p, ws->sorted.p, ws->flags.p, c0, c0);
+        else
+            bp_scatter2g_kernel<kGp, kGt, false><<<8 * per, kGt, 0, st>>>(
+                ws->keys.p, ws->bp.p + ws->bp_h1t, ws->bp_G, ws->bp_hsb, ws->bp_hsc, ws->bp_T, ntiles, c1 - c0, dg, ws->cg,
+                ws->cur.p, ws->sorted.p, ws->flags.p, c0, c0);
+    } else if (c1 > c0) {
+        if (ws->cg.vreg)
+            bp_scatter2c_kernel<true><<<dim3(ws->bp_J, c1 - c0), kKeyThreads, 0, st>>>(
+                ws->keys.p, C1, ws->bp_J, dg, ws->cg, ws->cur.p, ws->sorted.p, ws->flags.p, c0);
+        else
+            bp_scatter2c_kernel<false><<<dim3(ws->bp_J, c1 - c0), kKeyThreads, 0, st>>>(
+                ws->keys.p, C1, ws->bp_J, dg, ws->cg, ws->cur.p, ws->sorted.p, ws->flags.p, c0);
+    }
+    PG(hipGetLastError());
+    return KMP_OK;
+}
+
+// Bucketed front: keys `in` grouped by bucket into ws->sorted, bstart[0..nb] in ws->cnt.  After
+// bp_level1 (ws->parted) that is level 2; otherwise a radix sort on the bucket field and a binary
+// search per bucket.  Marks 2 after the grouping.
+int bucket_group(kmp_postings* ws, const unsigned long long* in, uint64_t slots, const Layout& lay, hipStream_t st) {
+    const uint32_t nb = 1u << lay.bbits;
+    PG(ws->sorted.reserve(slots));
+    if (ws->parted && in == ws->keys.p) {
+        ws->parted = false;
+        int rc = ws->cur_used ? bp_level2c(ws, lay, st) : bp_level2(ws, lay, st);
+        ws->mark(2, st);
+        return rc;
+    }
+    size_t t_sort = 0;
+    PG(rocprim::radix_sort_keys<SortCfg>(nullptr, t_sort, in, ws->sorted.p, (size_t)slots, lay.sort_lo, lay.sort_hi, st));
+    PG(ws->tmp.reserve(std::max(t_sort, ws->tmp.n)));
+    PG(rocprim::radix_sort_keys<SortCfg>(ws->tmp.p, t_sort, in, ws->sorted.p, (size_t)slots, lay.sort_lo, lay.sort_hi, st));
+    ws->mark(2, st);
+    PG(ws->cnt.reserve(2 * (uint64_t)nb + 2));
+    bucket_bounds_kernel<<<(nb + 1 + 255) / 256, 256, 0, st>>>(ws->sorted.p, slots, lay.sort_lo, nb, ws->cnt.p);
+    PG(hipGetLastError());
+    return KMP_OK;
+}
+
+// Flat front end (keys already in ws->keys): stable code sort, count pass, offsets, write pass.
+// Marks 2 (sort), 3 (count + offsets), 4 (write).  On return ws->inc holds *n_inc pair keys.
+int front_flat(kmp_postings* ws, uint64_t slots, const Layout& lay, const uint16_t* d_class, uint32_t n,
+               uint32_t heavy_df, int require_class_diff, unsigned long long* n_inc, kmp_postings_stats* stats,
+               hipStream_t st) {
+    size_t t_sort = 0;
+    PG(rocprim::radix_sort_keys<SortCfg>(nullptr, t_sort, ws->keys.p, ws->sorted.p, (size_t)slots, lay.sort_lo, lay.sort_hi,
+                                st));
+    PG(ws->tmp.reserve(std::max(t_sort, ws->tmp.n)));
+    PG(rocprim::radix_sort_keys<SortCfg>(ws->tmp.p, t_sort, ws->keys.p, ws->sorted.p, (size_t)slots, lay.sort_lo,
+                                lay.sort_hi, st));
+    ws->mark(2, st);
+
+    const uint64_t nb64 = (slots + kExpChunk - 1) / kExpChunk;
+    if (nb64 > 0x7FFFFFFFull) return KMP_EINVAL;
+    const uint32_t nb = (uint32_t)nb64;
+    PG(ws->cnt.reserve(slots));
+    PG(ws->bstats.reserve((uint64_t)nb * kStN + kStN));
+    PG(ws->btot.reserve(nb));
+    PG(ws->boff.reserve(nb));
+    unsigned long long* acc_d = ws->bstats.p + (uint64_t)nb * kStN;
+    if (lay.cls_in_key)
+        expand_kernel<false, true><<<nb, kExpThreads, 0, st>>>(ws->sorted.p, slots, lay, d_class, n, require_class_diff,
+                                                               heavy_df, ws->cnt.p, ws->bstats.p, ws->btot.p, nullptr,
+                                                               nullptr);
+    else
+        expand_kernel<false, false><<<nb, kExpThreads, 0, st>>>(ws->sorted.p, slots, lay, d_class, n,
+                                                                require_class_diff, heavy_df, ws->cnt.p, ws->bstats.p,
+                                                                ws->btot.p, nullptr, nullptr);
+    reduce_stats_kernel<<<1, 1024, 0, st>>>(ws->bstats.p, nb, acc_d);
+    size_t t_scan = 0;
+    PG(rocprim::exclusive_scan(nullptr, t_scan, ws->btot.p, ws->boff.p, 0ull, (size_t)nb,
+                               rocprim::plus<unsigned long long>(), st));
+    PG(ws->tmp.reserve(std::max(t_scan, ws->tmp.n)));
+    PG(rocprim::exclusive_scan(ws->tmp.p, t_scan, ws->btot.p, ws->boff.p, 0ull, (size_t)nb,
+                               rocprim::plus<unsigned long long>(), st));
+    ws->mark(3, st);
+    unsigned long long acc[kStN];
+    PG(hipMemcpyAsync(acc, acc_d, sizeof acc, hipMemcpyDeviceToHost, st));
+    PG(hipStreamSynchronize(st));
+    fill_stats(stats, acc);
+    *n_inc = acc[kStInc];
+    if (*n_inc && *n_inc <= 0xFFFFFFFFull) {
+        PG(ws->inc.reserve(*n_inc));
+        if (lay.cls_in_key)
+            expand_kernel<true, true><<<nb, kExpThreads, 0, st>>>(ws->sorted.p, slots, lay, d_class, n,
+                                                                  require_class_diff, heavy_df, ws->cnt.p, nullptr,
+                                                                  nullptr, ws->boff.p, ws->inc.p);
+        else
+            expand_kernel<true, false><<<nb, kExpThreads, 0, st>>>(ws->sorted.p, slots, lay, d_class, n,
+                                                                   require_class_diff, heavy_df, ws->cnt.p, nullptr,
+                                                                   nullptr, ws->boff.p, ws->inc.p);
+    }
+    ws->mark(4, st);
+    return KMP_OK;
+}

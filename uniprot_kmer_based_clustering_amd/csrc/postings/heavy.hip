@@ -1,0 +1,856 @@
+// postings/heavy.hip — the heavy path: frequent k-mers spilled by the bucket kernels.
+// Part of kmp_postings.hip (included there; not a translation unit of its own).
+
+// ------------------------------------------------------------- heavy path ------------------
+// Frequent k-mers (a group above kHeavySub keys) and buckets above every LDS capacity are
+// spilled by the bucket kernels (their keys, unchanged) and expanded here, with no cap on df:
+//   1. the spilled keys, gathered, are radix sorted on (h, p) (bits [clsbits, 63)): one run per
+//      k-mer, its proteins ascending, duplicate windows of one protein adjacent;
+//   2. heavy_scan / heavy_compact (4,096-key tiles + a scan of the tile counts): the distinct
+//      (k-mer, protein) elements E = p << cb | class, and each k-mer's start GS[g] in E;
+//      df(g) = GS[g+1] - GS[g] (main.rs:77-122 restated on the spill);
+//   3. heavy_plan (one thread per k-mer): statistics, the element range [i0, i1) whose proteins
+//      lie in the call's rows, and the tile count: element blocks of kHvI rows x partner chunks
+//      of kHvJ (the upper triangle of the k-mer's C(df,2) pairs, vertex.rs:103-137);
+//   4. heavy_expand (one workgroup per tile): the partner chunk in LDS, one row per thread, the
+//      class test (mod.rs:580-587) on every pair (p_i, p_j), j > i; a workgroup scan and one
+//      cursor reservation place the pair keys p_i * mul + p_j in the shard regions the bucket
+//      kernels fill.  A k-mer of df 10^4 is ~400 tiles: no workgroup walks a long posting list.
+constexpr uint32_t kHvTile = 4096, kHvThreads = 256, kHvPer = kHvTile / kHvThreads;
+constexpr uint32_t kHvI = 256, kHvJ = 256, kHvMW = kHvJ / 32;
+constexpr uint32_t kHvSpread = 64 * 256;  // a tile with this many pairs spreads them over the shards
+// flat tiles (class order, every pair kept, a k-mer of at most kHvFlatRuns class runs): the
+// k-mer's cross-class pairs (row of run r, any element past r's end) numbered run by run, row by
+// row, cut into kHvFlat-pair tiles: every tile full, nothing per row to plan
+constexpr uint32_t kHvFlat = 1024, kHvFlatRuns = 64, kHvFlatMark = 0xFFFFFFFFu;
+
+// Heavy key order.  Plain: the spilled keys [h | p | class] sorted on (h, p).  Class order (the
+// class test is on): gather_shards rewrites them to [h | class | p] and the sort is on every bit,
+// so each k-mer's elements come in class runs, proteins ascending inside a run.  A pair of
+// different classes is then (row i, partner j) with j past the end of i's run: the expansion
+// walks only those — at k = 5 on uniprot_arg 98% of a frequent k-mer's pairs share a class and
+// were enumerated and tested one by one in the plain order.
+struct HeavyOrder {
+    unsigned cb, hshift, pbits;  // class bits, h shift, protein bits (hshift - cb)
+    int cls;                     // class order
+    uint32_t hj;                 // partners per tile (<= kHvJ)
+    // element-distinct test shift: plain keys drop the class (a function of p), class-ordered keys
+    // compare whole
+    __host__ __device__ unsigned eshift() const { return cls ? 0u : cb; }
+    // E value (p << cb | class) of a sorted key
+    __device__ uint32_t elem(unsigned long long v) const {
+        const unsigned long long lmask = (1ull << hshift) - 1;
+        if (!cls) return (uint32_t)(v & lmask);
+        const uint32_t pm = (uint32_t)((1ull << pbits) - 1), cm = (1u << cb) - 1;
+        return ((uint32_t)v & pm) << cb | ((uint32_t)(v >> pbits) & cm);
+    }
+};
+
+// spill shard regions -> one contiguous array (shard order); class order: keys rewritten to
+// [h | class | p]
+__global__ void gather_shards_kernel(const unsigned long long* __restrict__ src, uint64_t shard_cap,
+                                     const unsigned long long* __restrict__ cursor, HeavyOrder ho,
+                                     unsigned long long* __restrict__ dst) {
+    const int s = blockIdx.y;
+    unsigned long long off = 0;
+    for (int t = 0; t < s; ++t) off += cursor[t];
+    const unsigned long long m = cursor[s];
+    const unsigned long long cm = (1ull << ho.cb) - 1, hm = ~((1ull << ho.hshift) - 1);
+    for (unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; i < m;
+         i += (unsigned long long)gridDim.x * blockDim.x) {
+        const unsigned long long v = src[(uint64_t)s * shard_cap + i];
+        dst[off + i] = ho.cls ? (v & hm) | (v & cm) << ho.pbits | ((v & ~hm) >> ho.cb) : v;
+    }
+}
+
+// The spill is a list of segments (BucketArgs::seg): one heavy group (one k-mer) or one whole
+// bucket, each holding every key of its k-mers.  Each sorted alone, in LDS, and written where the
+// gather would have put it, is the whole sort the heavy path needs (k-mers contiguous, each
+// sorted): no global radix sort (eight onesweep passes over 1M keys at k = 5, 0.3 ms).  One
+// workgroup per segment.  Above kSegSmall keys: a block radix sort (rocprim, 8-bit digits,
+// 1,024 threads) of the key bits that differ — [0, hshift) for one k-mer (protein and class: four
+// passes instead of eight), every bit for a whole bucket (0.057 ms at config 1 against 0.074 ms
+// for a bitonic sort).
+constexpr uint32_t kSegSmall = 2048, kSegLarge = 8192, kSegItems = 8;
+template <uint32_t kLo, uint32_t kN>
+__global__ __launch_bounds__(kN / kSegItems) void heavy_segsort_kernel(const unsigned long long* __restrict__ spill,
+                                                                       uint64_t spill_cap,
+                                                                       const unsigned long long* __restrict__ cursor,
+                                                                       const unsigned long long* __restrict__ seg,
+                                                                       HeavyOrder ho,
+                                                                       unsigned long long* __restrict__ out) {
+    constexpr uint32_t kThreads = kN / kSegItems;
+    using Sort = rocprim::block_radix_sort<unsigned long long, kThreads, kSegItems>;
+    __shared__ typename Sort::storage_type st;
+    const unsigned long long sd = seg[blockIdx.x];
+    const uint32_t cnt = (uint32_t)(sd >> 40) & 0x7FFFFFu;
+    if (cnt <= kLo || cnt > kN) return;
+    const bool whole = sd >> 63;
+    if (ho.cls && !whole) return;  // heavy_segclass_kernel
+    const uint64_t pos = sd & ((1ull << 40) - 1), shard = pos / spill_cap;
+    uint64_t dst = pos - shard * spill_cap;
+    for (uint64_t t = 0; t < shard; ++t) dst += cursor[t];
+    const unsigned long long cm = (1ull << ho.cb) - 1, hm = ~((1ull << ho.hshift) - 1);
+    unsigned long long k[kSegItems];  // blocked: thread t holds keys t * kSegItems + e
+#pragma unroll
+    for (uint32_t e = 0; e < kSegItems; ++e) {
+        const uint32_t i = threadIdx.x * kSegItems + e;
+        unsigned long long v = ~0ull;  // padding: after every key (the sort is stable)
+        if (i < cnt) {
+            v = spill[pos + i];
+            if (ho.cls) v = (v & hm) | (v & cm) << ho.pbits | ((v & ~hm) >> ho.cb);
+        }
+        k[e] = v;
+    }
+    Sort().sort(k, st, 0, whole ? 64u : ho.hshift);
+#pragma unroll
+    for (uint32_t e = 0; e < kSegItems; ++e) {
+        const uint32_t i = threadIdx.x * kSegItems + e;
+        if (i < cnt) out[dst + i] = k[e];
+    }
+}
+
+// Class order, one k-mer per segment (a heavy group, not a whole bucket): what the compaction and the
+// class-order expansion need is class runs in ascending class, each protein once per run — not its
+// proteins ascending (only plain order, the ranged calls', searches by protein).  So: a counting sort
+// by class in LDS, a protein's later windows dropped through an LDS hash set on p (vertex.rs:59-140
+// counts a protein once per k-mer), and the segment's tail (as many slots as windows dropped) filled
+// with copies of its last key, which the compaction sees as duplicates of their neighbour.  O(n) per
+// segment with four barriers, instead of a bitonic sort (66 compare-exchange rounds at 2,048 keys) or
+// a 4-pass block radix sort.  A segment whose classes reach kScClasses sorts its keys in LDS (bitonic)
+// instead.
+constexpr uint32_t kScThreads = 512, kScItems = kSegLarge / kScThreads, kScClasses = 256, kScSlots = 2 * kSegLarge;
+__global__ __launch_bounds__(kScThreads) void heavy_segclass_kernel(const unsigned long long* __restrict__ spill,
+                                                                    uint64_t spill_cap,
+                                                                    const unsigned long long* __restrict__ cursor,
+                                                                    const unsigned long long* __restrict__ seg,
+                                                                    HeavyOrder ho, unsigned long long* __restrict__ out) {
+    __shared__ union {
+        uint32_t P[kScSlots];            // hash set of the segment's proteins (64 KB)
+        unsigned long long K[kSegLarge]; // the fallback's keys
+    } u;
+    __shared__ uint32_t CH[kScClasses];  // keys per class, then each class run's start
+    __shared__ uint32_t wave_tot[kScThreads / 64];
+    __shared__ uint32_t s_maxc;
+    __shared__ unsigned long long s_last;
+    const unsigned long long sd = seg[blockIdx.x];
+    const uint32_t cnt = (uint32_t)(sd >> 40) & 0x7FFFFFu;
+    if ((sd >> 63) || cnt > kSegLarge) return;  // a whole bucket, or above the LDS: the sorts
+    const uint32_t tid = threadIdx.x;
+    const uint64_t pos = sd & ((1ull << 40) - 1), shard = pos / spill_cap;
+    uint64_t dst = pos - shard * spill_cap;
+    for (uint64_t t = 0; t < shard; ++t) dst += cursor[t];
+    const unsigned long long cm = (1ull << ho.cb) - 1, hm = ~((1ull << ho.hshift) - 1);
+    const uint32_t pm = (uint32_t)((1ull << ho.pbits) - 1);
+    unsigned long long v[kScItems];
+    uint32_t mc = 0;
+#pragma unroll
+    for (uint32_t e = 0; e < kScItems; ++e) {
+        const uint32_t i = tid + e * kScThreads;
+        v[e] = ~0ull;
+        if (i < cnt) {
+            const unsigned long long x = spill[pos + i];
+            v[e] = (x & hm) | (x & cm) << ho.pbits | ((x & ~hm) >> ho.cb);  // [h | class | p]
+            mc = max(mc, (uint32_t)(v[e] >> ho.pbits) & (uint32_t)cm);
+        }
+    }
+    for (uint32_t i = tid; i < kScSlots; i += kScThreads) u.P[i] = 0xFFFFFFFFu;
+    for (uint32_t i = tid; i < kScClasses; i += kScThreads) CH[i] = 0;
+    if (tid == 0) s_maxc = 0;
+    __syncthreads();
+    const uint32_t wm = wave_max(mc);
+    if ((tid & 63) == 0) atomicMax(&s_maxc, wm);
+    __syncthreads();
+    if (s_maxc >= kScClasses) {  // (uniform) many classes: a bitonic sort of the segment
+        uint32_t N = 1;
+        while (N < cnt) N <<= 1;
+        __syncthreads();  // P is dead: K reuses it
+        for (uint32_t i = tid; i < N; i += kScThreads) u.K[i] = ~0ull;
+        __syncthreads();
+#pragma unroll
+        for (uint32_t e = 0; e < kScItems; ++e) {
+            const uint32_t i = tid + e * kScThreads;
+            if (i < cnt) u.K[i] = v[e];
+        }
+        __syncthreads();
+        for (uint32_t k = 2; k <= N; k <<= 1)
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                for (uint32_t i = tid; i < N / 2; i += kScThreads) {
+                    const uint32_t lo = 2 * j * (i / j) + (i % j), hi = lo + j;
+                    const unsigned long long x = u.K[lo], y = u.K[hi];
+                    if ((x > y) == !(lo & k)) {
+                        u.K[lo] = y;
+                        u.K[hi] = x;
+                    }
+                }
+                __syncthreads();
+            }
+        for (uint32_t i = tid; i < cnt; i += kScThreads) out[dst + i] = u.K[i];
+        return;
+    }
+    // a protein's first window in the segment keeps its key, later ones are dropped; each kept key
+    // ranked in its class
+    uint32_t rk[kScItems];
+#pragma unroll
+    for (uint32_t e = 0; e < kScItems; ++e) {
+        rk[e] = ~0u;
+        if (v[e] == ~0ull) continue;
+        const uint32_t p = (uint32_t)v[e] & pm;
+        uint32_t sl = (p * 0x9E3779B1u) >> (32 - 14);  // kScSlots = 2^14
+        bool first = false;
+        while (true) {
+            const uint32_t old = atomicCAS(&u.P[sl], 0xFFFFFFFFu, p);
+            if (old == 0xFFFFFFFFu) {
+                first = true;
+                break;
+            }
+            if (old == p) break;
+            sl = (sl + 1) & (kScSlots - 1);
+        }
+        if (first) rk[e] = atomicAdd(&CH[(uint32_t)(v[e] >> ho.pbits) & (uint32_t)cm], 1u);
+    }
+    __syncthreads();
+    lds_bins_scan<kScThreads>(CH, kScClasses, wave_tot);  // CH: run starts; the kept count below
+    uint32_t kept = 0;
+#pragma unroll
+    for (uint32_t e = 0; e < kScItems; ++e)
+        if (rk[e] != ~0u) {
+            const uint32_t at = CH[(uint32_t)(v[e] >> ho.pbits) & (uint32_t)cm] + rk[e];
+            out[dst + at] = v[e];
+            ++kept;
+        }
+    // the segment's last kept key: the largest (class, position) — the highest class run's last slot
+    uint32_t D, excl;
+    block_scan_n<kScThreads>(kept, excl, D, wave_tot);
+#pragma unroll
+    for (uint32_t e = 0; e < kScItems; ++e)
+        if (rk[e] != ~0u && CH[(uint32_t)(v[e] >> ho.pbits) & (uint32_t)cm] + rk[e] == D - 1) s_last = v[e];
+    __syncthreads();
+    const unsigned long long last = s_last;
+    for (uint32_t i = D + tid; i < cnt; i += kScThreads) out[dst + i] = last;
+}
+
+// the small segments (<= kSegSmall keys): a bitonic sort of the next power of two, 256 threads
+// (the radix sort's four passes measured 0.081 ms there against 0.064 ms)
+template <uint32_t kN, uint32_t kThreads>
+__global__ __launch_bounds__(kThreads) void heavy_segsort_bitonic_kernel(
+    const unsigned long long* __restrict__ spill, uint64_t spill_cap, const unsigned long long* __restrict__ cursor,
+    const unsigned long long* __restrict__ seg, HeavyOrder ho, unsigned long long* __restrict__ out) {
+    __shared__ unsigned long long K[kN];
+    const unsigned long long sd = seg[blockIdx.x];
+    const uint32_t cnt = (uint32_t)(sd >> 40) & 0x7FFFFFu;
+    if (cnt > kN || (ho.cls && !(sd >> 63))) return;  // one k-mer in class order: heavy_segclass_kernel
+    const uint64_t pos = sd & ((1ull << 40) - 1), shard = pos / spill_cap;
+    uint64_t dst = pos - shard * spill_cap;
+    for (uint64_t t = 0; t < shard; ++t) dst += cursor[t];
+    uint32_t N = 1;
+    while (N < cnt) N <<= 1;
+    const unsigned long long cm = (1ull << ho.cb) - 1, hm = ~((1ull << ho.hshift) - 1);
+    for (uint32_t i = threadIdx.x; i < N; i += kThreads) {
+        unsigned long long v = ~0ull;  // padding sorts last
+        if (i < cnt) {
+            v = spill[pos + i];
+            if (ho.cls) v = (v & hm) | (v & cm) << ho.pbits | ((v & ~hm) >> ho.cb);
+        }
+        K[i] = v;
+    }
+    __syncthreads();
+    for (uint32_t k = 2; k <= N; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < N / 2; i += kThreads) {
+                const uint32_t lo = 2 * j * (i / j) + (i % j), hi = lo + j;
+                const unsigned long long x = K[lo], y = K[hi];
+                if ((x > y) == !(lo & k)) {
+                    K[lo] = y;
+                    K[hi] = x;
+                }
+            }
+            __syncthreads();
+        }
+    for (uint32_t i = threadIdx.x; i < cnt; i += kThreads) out[dst + i] = K[i];
+}
+
+// per tile: distinct (h, p) elements, k-mer heads and (class order) class-run heads
+__global__ __launch_bounds__(kHvThreads) void heavy_scan_kernel(const unsigned long long* __restrict__ x, uint64_t m,
+                                                                HeavyOrder ho, uint32_t* __restrict__ ecnt,
+                                                                uint32_t* __restrict__ gcnt,
+                                                                uint32_t* __restrict__ rcnt) {
+    __shared__ uint32_t s_e, s_g, s_r;
+    if (threadIdx.x == 0) s_e = s_g = s_r = 0;
+    __syncthreads();
+    const uint64_t t0 = (uint64_t)blockIdx.x * kHvTile;
+    const unsigned es = ho.eshift();
+    uint32_t ne = 0, ng = 0, nr = 0;
+    for (uint32_t r = 0; r < kHvPer; ++r) {
+        const uint64_t i = t0 + r * kHvThreads + threadIdx.x;
+        if (i >= m) break;
+        const unsigned long long v = x[i], u = i ? x[i - 1] : ~0ull;
+        ne += (v >> es) != (u >> es);
+        ng += (v >> ho.hshift) != (u >> ho.hshift);
+        nr += (v >> ho.pbits) != (u >> ho.pbits);
+    }
+    if (ne) atomicAdd(&s_e, ne);
+    if (ng) atomicAdd(&s_g, ng);
+    if (nr && ho.cls) atomicAdd(&s_r, nr);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        ecnt[blockIdx.x] = s_e;
+        gcnt[blockIdx.x] = s_g;
+        if (ho.cls) rcnt[blockIdx.x] = s_r;
+    }
+}
+
+// per tile: the elements at eoff[t] + their rank, the k-mer starts at goff[t] + rank; class order:
+// the class-run starts at roff[t] + rank (RH) and every element's run (RUN)
+__global__ __launch_bounds__(kHvThreads) void heavy_compact_kernel(const unsigned long long* __restrict__ x,
+                                                                   uint64_t m, HeavyOrder ho,
+                                                                   const uint64_t* __restrict__ eoff,
+                                                                   const uint64_t* __restrict__ goff,
+                                                                   const uint64_t* __restrict__ roff,
+                                                                   uint32_t* __restrict__ E,
+                                                                   uint64_t* __restrict__ GS,
+                                                                   uint32_t* __restrict__ RUN,
+                                                                   uint64_t* __restrict__ RH,
+                                                                   uint32_t* __restrict__ GH,
+                                                                   uint32_t* __restrict__ KG) {
+    __shared__ uint32_t wave_tot[kHvThreads / 64];
+    const uint64_t t0 = (uint64_t)blockIdx.x * kHvTile;
+    uint64_t eb = eoff[blockIdx.x], gb = goff[blockIdx.x], rb = ho.cls ? roff[blockIdx.x] : 0;
+    const unsigned es = ho.eshift();
+    for (uint32_t r = 0; r < kHvPer; ++r) {
+        const uint64_t i = t0 + r * kHvThreads + threadIdx.x;
+        bool ke = false, kg = false, kr = false;
+        unsigned long long v = 0;
+        if (i < m) {
+            v = x[i];
+            const unsigned long long u = i ? x[i - 1] : ~0ull;
+            ke = (v >> es) != (u >> es);
+            kg = (v >> ho.hshift) != (u >> ho.hshift);
+            kr = (v >> ho.pbits) != (u >> ho.pbits);
+        }
+        uint32_t xe, te, xg, tg;
+        block_scan_n<kHvThreads>(ke, xe, te, wave_tot);
+        block_scan_n<kHvThreads>(kg, xg, tg, wave_tot);
+        if (ke) E[eb + xe] = ho.elem(v);
+        if (ke && KG) KG[eb + xe] = (uint32_t)(gb + xg + kg - 1);  // its k-mer (the last head up to it)
+        if (kg) {
+            GS[gb + xg] = eb + xe;  // a k-mer head is always a new element
+            GH[gb + xg] = (uint32_t)(v >> ho.hshift);  // the k-mer's h (scored calls: its self-score)
+        }
+        if (ho.cls) {
+            uint32_t xr, tr;
+            block_scan_n<kHvThreads>(kr, xr, tr, wave_tot);
+            if (kr) RH[rb + xr] = eb + xe;  // a run head too
+            if (ke) RUN[eb + xe] = (uint32_t)(rb + xr + kr - 1);
+            rb += tr;
+        }
+        eb += te;
+        gb += tg;
+    }
+}
+
+// Row blocks of kHvI elements: k-mer g's blocks are entries [bbase(g), bbase(g) + nblk) of the
+// block tables (GS[g] / kHvI + g: disjoint for consecutive k-mers), BT = the k-mer's tiles before
+// the block, BP = the block's partner start (its first row's).
+__device__ __forceinline__ uint64_t heavy_bbase(uint64_t gs, uint64_t g) { return gs / kHvI + g; }
+
+// a row's partner start (local index): past its class run (class order) or past itself
+__device__ __forceinline__ uint32_t heavy_pstart(uint32_t i, uint64_t b, const HeavyOrder& ho,
+                                                 const uint32_t* __restrict__ RUN,
+                                                 const uint64_t* __restrict__ RH) {
+    return ho.cls ? (uint32_t)(RH[RUN[b + i] + 1] - b) : i + 1;
+}
+
+// per k-mer: statistics (stats != 0), rows [i0, i1) of the call, the block tables and the tile
+// count.  Plain order: the rows whose protein lies in [row_lo, row_hi) (a contiguous range);
+// class order: every element (a ranged call tests each pair's smaller protein instead).
+__global__ __launch_bounds__(256) void heavy_plan_kernel(const uint32_t* __restrict__ E,
+                                                         const uint64_t* __restrict__ GS, uint64_t ngb,
+                                                         const unsigned long long* __restrict__ ng_dev,
+                                                         HeavyOrder ho, const uint32_t* __restrict__ RUN,
+                                                         const uint64_t* __restrict__ RH, int flat_ok,
+                                                         uint32_t row_lo, uint32_t row_hi, uint32_t heavy_df,
+                                                         int stats, int tiles_on,
+                                                         unsigned long long* __restrict__ gstats,
+                                                         uint32_t* __restrict__ gi, uint32_t* __restrict__ BT,
+                                                         uint32_t* __restrict__ BP,
+                                                         unsigned long long* __restrict__ tcount) {
+    const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const uint64_t ng = *ng_dev;  // k-mers; threads up to the bound ngb write empty plans
+    const unsigned cb = ho.cb;
+    unsigned long long st[kStN] = {0, 0, 0, 0, 0, 0, 0};
+    if (g >= ng && g < ngb) {
+        if (tiles_on) {
+            gi[2 * g] = gi[2 * g + 1] = 0;
+            tcount[g] = 0;
+        }
+    }
+    if (g < ng) {
+        const uint64_t b = GS[g];
+        const uint32_t d = (uint32_t)(GS[g + 1] - b);
+        auto lower = [&](uint32_t row) {  // first element whose protein >= row
+            uint32_t lo = 0, hi = d;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if ((E[b + mid] >> cb) < row) lo = mid + 1;
+                else hi = mid;
+            }
+            return lo;
+        };
+        uint32_t i0 = 0, i1 = 0;
+        unsigned long long tiles = 0;
+        const uint32_t nruns = ho.cls && d ? RUN[b + d - 1] - RUN[b] + 1 : 0u;
+        if (!tiles_on) {
+            // statistics only
+        } else if (d >= 2 && d <= heavy_df && flat_ok && nruns <= kHvFlatRuns) {
+            // flat: the k-mer's cross-class pairs as one index space, cut into kHvFlat-pair tiles
+            const uint32_t ra = RUN[b];
+            unsigned long long pairs = 0;
+            for (uint32_t r = 0; r < nruns; ++r) {
+                const uint64_t rs = RH[ra + r], re = RH[ra + r + 1];
+                pairs += (re - rs) * (b + d - re);
+            }
+            i0 = kHvFlatMark;
+            i1 = nruns;
+            tiles = (pairs + kHvFlat - 1) / kHvFlat;
+        } else if (d >= 2 && d <= heavy_df) {
+            i0 = ho.cls ? 0u : lower(row_lo);
+            i1 = ho.cls ? d : lower(row_hi);
+            const uint64_t bb = heavy_bbase(b, g);
+            for (uint32_t r = i0, k = 0; r < i1; r += kHvI, ++k) {
+                const uint32_t ps = heavy_pstart(r, b, ho, RUN, RH);
+                BT[bb + k] = (uint32_t)tiles;
+                BP[bb + k] = ps;
+                tiles += ps < d ? (d - ps + ho.hj - 1) / ho.hj : 0u;
+            }
+        }
+        if (tiles_on) gi[2 * g] = i0;
+        if (tiles_on) {
+            gi[2 * g + 1] = i1;
+            tcount[g] = tiles;
+        }
+        st[kStSumS] = d;
+        st[kStDistinct] = 1;
+        st[kStRepeat] = d >= 2;
+        if (d <= heavy_df) st[kStCdf2] = (unsigned long long)d * (d - 1) / 2;
+        else st[kStHeavy] = d;
+        st[kStMaxDf] = d;
+    }
+    if (!stats) return;
+    __shared__ unsigned long long red[4][kStN];
+#pragma unroll
+    for (int t = 0; t < kStN; ++t) {
+        unsigned long long v = st[t];
+        for (int s = 32; s > 0; s >>= 1) v = stat_op(t, v, __shfl_down(v, s));
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][t] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < kStN && threadIdx.x != kStInc) {
+        const int t = threadIdx.x;
+        unsigned long long v = red[0][t];
+        for (int w = 1; w < 4; ++w) v = stat_op(t, v, red[w][t]);
+        unsigned long long* gp = gstats + (uint64_t)(blockIdx.x % kShards) * 8 + t;
+        if (t == kStMaxDf) atomicMax(gp, v);
+        else if (v) atomicAdd(gp, v);
+    }
+}
+
+// one workgroup per tile (grid-stride): rows i of block k of k-mer g against partner chunk
+// [j0, j0 + kHvJ).  Plain order: partners j > i, the class test per pair when require_diff.
+// Class order: partners past i's class run (every one of another class); a ranged call keeps the
+// pairs whose smaller protein lies in [row_lo, row_hi).  Keys min(p) * mul + max(p).
+__global__ __launch_bounds__(kHvI) void heavy_expand_kernel(const uint32_t* __restrict__ E,
+                                                            const uint64_t* __restrict__ GS,
+                                                            const uint32_t* __restrict__ gi,
+                                                            const uint32_t* __restrict__ BT,
+                                                            const uint32_t* __restrict__ BP,
+                                                            const uint32_t* __restrict__ RUN,
+                                                            const uint64_t* __restrict__ RH,
+                                                            const unsigned long long* __restrict__ toff,
+                                                            const unsigned long long* __restrict__ ng_dev,
+                                                            HeavyOrder ho, uint32_t mul, int require_diff, int ranged,
+                                                            uint32_t row_lo, uint32_t row_hi,
+                                                            unsigned long long* __restrict__ out, uint64_t shard_cap,
+                                                            unsigned long long* __restrict__ cursor,
+                                                            unsigned long long* __restrict__ gstats,
+                                                            const uint32_t* __restrict__ GH, int k, unsigned sb,
+                                                            uint32_t sor) {
+    __shared__ uint32_t J[kHvJ];
+    __shared__ uint32_t s_ex[kHvI + 1], s_js[kHvI], s_p[kHvI];
+    __shared__ uint32_t s_m[kHvI * kHvMW];  // filtered tile: each row's kept partners (bit j - j0)
+    __shared__ unsigned long long s_sb[kShards];  // spread tile: shard base minus its first output
+    __shared__ uint32_t f_s[kHvFlatRuns], f_e[kHvFlatRuns];  // flat tile: the k-mer's runs (local)
+    __shared__ unsigned long long f_c[kHvFlatRuns + 1];       // ... and their first pair's index
+    __shared__ uint32_t wave_tot[kHvI / 64];
+    __shared__ unsigned long long sbase;
+    const uint64_t ng = *ng_dev;
+    const unsigned long long T = toff[ng];
+    const unsigned cb = ho.cb;
+    const uint32_t cmask = (1u << cb) - 1;
+    const bool test_cls = require_diff && !ho.cls, test_row = ho.cls && ranged;
+    // workgroup w takes the consecutive tiles [w * per, (w + 1) * per): one binary search for its
+    // first tile's k-mer, then the k-mer and row block advance (a search per tile was a chain of
+    // ~15 dependent loads, the bulk of a tile's time)
+    const unsigned long long per = (T + gridDim.x - 1) / gridDim.x, tb = blockIdx.x * per;
+    const unsigned long long te = min(T, tb + per);
+    uint64_t g = 0;
+    if (tb < te) {
+        uint64_t lo = 0, hi = ng;  // the last k-mer with toff[g] <= tb
+        while (lo + 1 < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (toff[mid] <= tb) lo = mid;
+            else hi = mid;
+        }
+        g = lo;
+    }
+    uint32_t klo = 0;
+    for (unsigned long long t = tb; t < te; ++t) {
+        if (toff[g + 1] <= t) {  // the next k-mer with tiles (toff[ng] = T > t)
+            do ++g;
+            while (toff[g + 1] <= t);
+            klo = 0;
+        }
+        const uint64_t b = GS[g];
+        const uint32_t d = (uint32_t)(GS[g + 1] - b), i0 = gi[2 * g], i1 = gi[2 * g + 1];
+        const uint32_t local = (uint32_t)(t - toff[g]);
+        // pair key; scored (sb > 0): (pair << sb) | sor | s(x) of this k-mer
+        const uint32_t sfield = sb ? sor | kmer_self_score(GH[g], k) : 0u;
+        auto mk = [&](uint32_t pa, uint32_t pb) {
+            return ((unsigned long long)min(pa, pb) * mul + max(pa, pb)) << sb | sfield;
+        };
+        if (i0 == kHvFlatMark) {  // flat tile (uniform over the workgroup)
+            const uint32_t nr = i1, ra = RUN[b];
+            __syncthreads();  // the run table's reuse
+            unsigned long long pr = 0;
+            if (threadIdx.x < nr) {
+                const uint32_t rs = (uint32_t)(RH[ra + threadIdx.x] - b), re = (uint32_t)(RH[ra + threadIdx.x + 1] - b);
+                f_s[threadIdx.x] = rs;
+                f_e[threadIdx.x] = re;
+                pr = (unsigned long long)(re - rs) * (d - re);
+            }
+            if (threadIdx.x < 64) {  // exclusive scan of the runs' pair counts (nr <= 64: one wave)
+                unsigned long long incl = pr;
+                for (int sh = 1; sh < 64; sh <<= 1) {
+                    const unsigned long long y = __shfl_up(incl, sh);
+                    if ((int)threadIdx.x >= sh) incl += y;
+                }
+                if (threadIdx.x < nr) f_c[threadIdx.x] = incl - pr;
+                if (threadIdx.x == nr - 1) f_c[nr] = incl;
+            }
+            __syncthreads();
+            const unsigned long long o0 = (unsigned long long)local * kHvFlat, o1 = min(f_c[nr], o0 + kHvFlat);
+            const uint32_t total = (uint32_t)(o1 - o0);
+            uint32_t hx = (GH[g] * 0x9E3779B1u) ^ (local * 0xC2B2AE35u) ^ 0x27D4EB2Fu;
+            hx ^= hx >> 16;
+            const uint32_t shard = (hx * 0x7FEB352Du) >> 26;
+            if (threadIdx.x == 0) {
+                sbase = atomicAdd(&cursor[shard], (unsigned long long)total);
+                atomicAdd(&gstats[(uint64_t)shard * 8 + kStInc], (unsigned long long)total);
+            }
+            __syncthreads();
+            unsigned long long* dst = out + (uint64_t)shard * shard_cap;
+            for (uint32_t u = threadIdx.x; u < total; u += kHvI) {
+                const unsigned long long o = o0 + u;
+                uint32_t r = 0, hi = nr;  // the last run with f_c[r] <= o
+                while (r + 1 < hi) {
+                    const uint32_t mid = (r + hi) >> 1;
+                    if (f_c[mid] <= o) r = mid;
+                    else hi = mid;
+                }
+                const unsigned long long off = o - f_c[r];
+                const uint32_t part = d - f_e[r];
+                const uint32_t row = f_s[r] + (uint32_t)(off / part), j = f_e[r] + (uint32_t)(off % part);
+                const uint32_t pa = E[b + row] >> cb, pj = E[b + j] >> cb;
+                const unsigned long long pos = sbase + u;
+                if (pos < shard_cap) dst[pos] = mk(pa, pj);
+            }
+            continue;
+        }
+        // row block: the last with BT <= local (blocks without tiles share the next one's BT)
+        const uint64_t bb = heavy_bbase(b, g);
+        const uint32_t nblk = (i1 - i0 + kHvI - 1) / kHvI;
+        if (t == tb) {  // entered mid-k-mer: search
+            uint32_t khi = nblk;
+            while (klo + 1 < khi) {
+                const uint32_t mid = (klo + khi) >> 1;
+                if (BT[bb + mid] <= local) klo = mid;
+                else khi = mid;
+            }
+        }
+        while (klo + 1 < nblk && BT[bb + klo + 1] <= local) ++klo;
+        const uint32_t r = i0 + klo * kHvI;
+        const uint32_t j0 = BP[bb + klo] + (local - BT[bb + klo]) * ho.hj, j1 = min(d, j0 + ho.hj);
+        __syncthreads();  // J reuse
+        for (uint32_t j = j0 + threadIdx.x; j < j1; j += kHvI) J[j - j0] = E[b + j];
+        const uint32_t i = r + threadIdx.x;
+        const bool row = i < i1;
+        const uint32_t xi = row ? E[b + i] : 0u;
+        const uint32_t js = row ? max(heavy_pstart(i, b, ho, RUN, RH), j0) : j1;
+        const uint32_t pi = xi >> cb;
+        __syncthreads();
+        auto keep = [&](uint32_t xj) {
+            if (test_cls) return ((xj ^ xi) & cmask) != 0u;
+            if (test_row) {
+                const uint32_t pm = min(pi, xj >> cb);
+                return pm >= row_lo && pm < row_hi;
+            }
+            return true;
+        };
+        uint32_t c = 0;
+        if (test_cls || test_row) {
+            // the row's kept partners as a bit mask over the chunk (hj <= kHvJ): the emit below
+            // writes the tile's output coalesced (a row writing its own run, one lane per row, cost
+            // one memory transaction per key)
+            uint32_t* mrow = s_m + threadIdx.x * kHvMW;
+#pragma unroll
+            for (uint32_t w = 0; w < kHvMW; ++w) {
+                uint32_t bits = 0;
+                const uint32_t jw = j0 + w * 32;
+                if (jw < j1 && jw + 32 > js)
+                    for (uint32_t t = 0; t < 32; ++t) {
+                        const uint32_t j = jw + t;
+                        if (j >= js && j < j1 && keep(J[j - j0])) bits |= 1u << t;
+                    }
+                mrow[w] = bits;
+                c += __popc(bits);
+            }
+        } else {
+            c = js < j1 ? j1 - js : 0u;
+        }
+        uint32_t excl, total;
+        block_scan_n<kHvI>(c, excl, total, wave_tot);
+        // Shards, which size the next call's regions: a large unfiltered tile spreads its output
+        // evenly over all of them (output o in shard 64 o / total); another tile takes one shard from
+        // what it is (its k-mer's h, block, chunk) — not from t: the k-mers' order in E
+        // follows the spill's (atomic) order, and the shard loads must not
+        const bool spread = !(test_cls || test_row) && total >= kHvSpread;
+        // the k-mer's h, not its first element: class runs come in LDS-atomic order
+        // (heavy_segclass), so E[b] varied between calls and so did the fullest region (8 %)
+        uint32_t hx = (GH[g] * 0x9E3779B1u) ^ (klo * 0x85EBCA6Bu) ^ (local * 0xC2B2AE35u);
+        hx ^= hx >> 16;
+        const uint32_t shard = (hx * 0x7FEB352Du) >> 26;  // the top bits: kShards = 64
+        if (spread) {
+            if (threadIdx.x < kShards) {
+                const uint32_t sh = threadIdx.x;
+                const uint64_t a0 = ((uint64_t)sh * total + kShards - 1) / kShards;
+                const uint64_t a1 = ((uint64_t)(sh + 1) * total + kShards - 1) / kShards;
+                s_sb[sh] = atomicAdd(&cursor[sh], (unsigned long long)(a1 - a0)) - a0;  // pos = s_sb + o
+                if (a1 > a0) atomicAdd(&gstats[(uint64_t)sh * 8 + kStInc], (unsigned long long)(a1 - a0));
+            }
+        } else if (threadIdx.x == 0) {
+            sbase = total ? atomicAdd(&cursor[shard], (unsigned long long)total) : 0ull;
+            if (total) atomicAdd(&gstats[(uint64_t)shard * 8 + kStInc], (unsigned long long)total);
+        }
+        __syncthreads();
+        unsigned long long* dst = out + (uint64_t)shard * shard_cap;
+        if (test_cls || test_row) {
+            // filtered tile: output o of row i (the last with s_ex[i] <= o) is the row's
+            // (o - s_ex[i])-th kept partner, selected from its mask; consecutive lanes write
+            // consecutive keys
+            s_ex[threadIdx.x] = excl;
+            s_p[threadIdx.x] = pi;
+            if (threadIdx.x == 0) s_ex[kHvI] = total;
+            __syncthreads();
+            uint32_t i = 0, hi = kHvI;
+            if (threadIdx.x < total) {
+                while (i + 1 < hi) {
+                    const uint32_t mid = (i + hi) >> 1;
+                    if (s_ex[mid] <= threadIdx.x) i = mid;
+                    else hi = mid;
+                }
+            }
+            for (uint32_t o = threadIdx.x; o < total; o += kHvI) {
+                while (s_ex[i + 1] <= o) ++i;
+                uint32_t rk = o - s_ex[i], w = 0, x = s_m[i * kHvMW];
+                while (rk >= (uint32_t)__popc(x)) {  // the word holding it
+                    rk -= __popc(x);
+                    x = s_m[i * kHvMW + ++w];
+                }
+                uint32_t bit = 0;  // the rk-th set bit of x
+                for (uint32_t half = 16; half; half >>= 1) {
+                    const uint32_t low = __popc(x & ((1u << half) - 1));
+                    if (rk >= low) {
+                        rk -= low;
+                        x >>= half;
+                        bit += half;
+                    }
+                }
+                const uint32_t pj = J[w * 32 + bit] >> cb;
+                const unsigned long long pos = sbase + o;
+                if (pos < shard_cap) dst[pos] = mk(s_p[i], pj);
+            }
+        } else {
+            // every partner kept: the tile's output [0, total) in coalesced order, output o of row
+            // i (the last with s_ex[i] <= o) = partner js_i + o - s_ex[i]; a thread's rows only move
+            // forward as o grows
+            s_ex[threadIdx.x] = excl;
+            s_js[threadIdx.x] = js;
+            s_p[threadIdx.x] = pi;
+            if (threadIdx.x == 0) s_ex[kHvI] = total;
+            __syncthreads();
+            uint32_t i = 0, hi = kHvI;
+            if (threadIdx.x < total) {
+                while (i + 1 < hi) {
+                    const uint32_t mid = (i + hi) >> 1;
+                    if (s_ex[mid] <= threadIdx.x) i = mid;
+                    else hi = mid;
+                }
+            }
+            // spread: output o's shard sh = 64 o / total, advanced as o grows (total < 2^26)
+            uint32_t sh = spread ? threadIdx.x * kShards / total : 0u;
+            uint32_t sh_end = spread ? ((sh + 1) * total + kShards - 1) / kShards : 0u;
+            for (uint32_t o = threadIdx.x; o < total; o += kHvI) {
+                while (s_ex[i + 1] <= o) ++i;
+                const uint32_t pa = s_p[i], pj = J[s_js[i] + (o - s_ex[i]) - j0] >> cb;
+                const unsigned long long key = mk(pa, pj);
+                if (spread) {
+                    while (o >= sh_end) {
+                        ++sh;
+                        sh_end = ((sh + 1) * total + kShards - 1) / kShards;
+                    }
+                    const unsigned long long pos = s_sb[sh] + o;
+                    if (pos < shard_cap) out[(uint64_t)sh * shard_cap + pos] = key;
+                } else {
+                    const unsigned long long pos = sbase + o;
+                    if (pos < shard_cap) dst[pos] = key;
+                }
+            }
+        }
+    }
+}
+
+// Ranged calls in plain order (the passes of a streamed batch): the rows of a pass, not its
+// k-mers, drive the expansion.  A per-protein index of the compacted elements (PE: element
+// indices grouped by protein, PO: each protein's start; built once per compaction) makes a pass's
+// active elements the contiguous range PE[PO[row_lo], PO[row_hi]); each pairs with the later
+// elements of its k-mer (E is sorted by protein within a k-mer, so every partner's protein is
+// larger: the pair's smaller protein is the active row).  One workgroup per 256 active elements:
+// their candidate counts scanned in LDS, the candidates split into one contiguous slice per wave,
+// the class test counted (pass 1), one cursor reservation for the workgroup, and the kept keys
+// written compacted by ballot (pass 2; consecutive lanes read consecutive partners).  No per-k-mer
+// plan, tile table or search: the work is the pass's own pairs.
+constexpr uint32_t kHfThreads = 256, kHfWaves = kHfThreads / 64;
+__global__ __launch_bounds__(kHfThreads) void heavy_flat_kernel(
+        const uint32_t* __restrict__ E, const uint64_t* __restrict__ GS, const uint32_t* __restrict__ KG,
+        const uint32_t* __restrict__ GH, const uint32_t* __restrict__ PE, uint32_t a0, uint32_t a1, unsigned cb,
+        uint32_t mul, int require_diff, uint32_t heavy_df, int k, unsigned sb, uint32_t sor,
+        unsigned long long* __restrict__ out, uint64_t shard_cap, unsigned long long* __restrict__ cursor,
+        unsigned long long* __restrict__ gstats) {
+    __shared__ uint32_t s_ex[kHfThreads + 1], s_e[kHfThreads], s_x[kHfThreads], s_f[kHfThreads];
+    __shared__ uint32_t wave_tot[kHfWaves], s_wk[kHfWaves];
+    __shared__ unsigned long long s_base;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t a = a0 + blockIdx.x * kHfThreads + tid;
+    uint32_t cand = 0, e = 0, x = 0, f = 0;
+    if (a < a1) {
+        e = PE[a];
+        const uint32_t g = KG[e];
+        const uint64_t gs0 = GS[g], gs1 = GS[g + 1];
+        x = E[e];
+        if (gs1 - gs0 <= heavy_df) cand = (uint32_t)(gs1 - e - 1);
+        f = sb ? sor | kmer_self_score(GH[g], k) : 0u;
+    }
+    uint32_t ex, total;
+    block_scan_n<kHfThreads>(cand, ex, total, wave_tot);
+    s_ex[tid] = ex;
+    s_e[tid] = e;
+    s_x[tid] = x;
+    s_f[tid] = f;
+    if (tid == 0) s_ex[kHfThreads] = total;
+    __syncthreads();
+    if (total == 0) return;  // (uniform)
+    const uint32_t S = (total + kHfWaves - 1) / kHfWaves;
+    const uint32_t c0 = min(total, wv * S), c1 = min(total, c0 + S);
+    const uint32_t cmask = (1u << cb) - 1;
+    auto search = [&](uint32_t o) {  // the last row with s_ex[i] <= o (o < total: a row with candidates)
+        uint32_t lo = 0, hi = kHfThreads;
+        while (lo + 1 < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_ex[mid] <= o) lo = mid;
+            else hi = mid;
+        }
+        return lo;
+    };
+    uint32_t kept = 0;
+    if (require_diff) {
+        uint32_t i = c0 + lane < c1 ? search(c0 + lane) : 0u;
+        for (uint32_t o = c0 + lane; o < c1; o += 64) {
+            while (s_ex[i + 1] <= o) ++i;
+            const uint32_t j = s_e[i] + 1 + (o - s_ex[i]);
+            kept += ((E[j] ^ s_x[i]) & cmask) != 0u;
+        }
+        kept = wave_sum(kept);
+    } else {
+        kept = c1 - c0;
+    }
+    if (lane == 0) s_wk[wv] = kept;
+    __syncthreads();
+    uint32_t before = 0, K = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kHfWaves; ++w) {
+        before += w < wv ? s_wk[w] : 0u;
+        K += s_wk[w];
+    }
+    uint32_t hx = (blockIdx.x * 0x9E3779B1u) ^ (a0 * 0x85EBCA6Bu);
+    hx ^= hx >> 16;
+    const uint32_t shard = (hx * 0x7FEB352Du) >> 26;
+    if (tid == 0) {
+        s_base = K ? atomicAdd(&cursor[shard], (unsigned long long)K) : 0ull;
+        if (K) atomicAdd(&gstats[(uint64_t)shard * 8 + kStInc], (unsigned long long)K);
+    }
+    __syncthreads();
+    unsigned long long* dst = out + (uint64_t)shard * shard_cap;
+    uint64_t run = s_base + before;
+    uint32_t i = c0 + lane < c1 ? search(c0 + lane) : 0u;
+    for (uint32_t o0 = c0; o0 < c1; o0 += 64) {  // uniform over the wave (ballot)
+        const uint32_t o = o0 + lane;
+        bool keep = false;
+        unsigned long long key = 0;
+        if (o < c1) {
+            while (s_ex[i + 1] <= o) ++i;
+            const uint32_t j = s_e[i] + 1 + (o - s_ex[i]), xj = E[j], xi = s_x[i];
+            keep = !require_diff || ((xj ^ xi) & cmask) != 0u;
+            key = ((unsigned long long)(xi >> cb) * mul + (xj >> cb)) << sb | s_f[i];
+        }
+        const unsigned long long m = __ballot(keep);
+        if (keep) {
+            const uint64_t pos = run + __popcll(m & ((1ull << lane) - 1));
+            if (pos < shard_cap) dst[pos] = key;
+        }
+        run += __popcll(m);
+    }
+}
+
+// per-protein index of the compacted elements: counts, then (after a scan into PO) the scatter
+__global__ void heavy_pcount_kernel(const uint32_t* __restrict__ E, const unsigned long long* __restrict__ tot,
+                                    unsigned cb, uint32_t* __restrict__ cnt) {
+    const uint64_t ne = tot[0];
+    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < ne; e += (uint64_t)gridDim.x * blockDim.x)
+        atomicAdd(&cnt[E[e] >> cb], 1u);
+}
+__global__ void heavy_pscatter_kernel(const uint32_t* __restrict__ E, const unsigned long long* __restrict__ tot,
+                                      unsigned cb, const uint32_t* __restrict__ PO, uint32_t* __restrict__ cur,
+                                      uint32_t* __restrict__ PE) {
+    const uint64_t ne = tot[0];
+    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < ne; e += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t p = E[e] >> cb;
+        PE[PO[p] + atomicAdd(&cur[p], 1u)] = (uint32_t)e;
+    }
+}
+
+// bucket kernels: capacity (keys), threads, log2 of the k-mer table (>= capacity)
+#ifndef KMP_SMALL_GEOM
+#define KMP_SMALL_GEOM 1280, 256, 11
+#endif
+constexpr int kSmallGeom[3] = {KMP_SMALL_GEOM};
+constexpr int kBucketSmallCap = kSmallGeom[0], kBucketSmallThreads = kSmallGeom[1], kBucketSmallTab = kSmallGeom[2];
+// larger buckets (up to 4,096 keys: four per thread, no register spills) take the large kernel;
+// above that the whole bucket goes to the heavy path
+constexpr int kBucketLargeCap = 4096, kBucketLargeThreads = 1024, kBucketLargeTab = 12;
+// the large kernel grid-strides the list of large buckets (usually empty at config 3; most
+// buckets of a k = 5 batch of real proteins): four workgroups per CU (one per CU measured 8 % slower)
+constexpr int kBucketLargeGrid = 1024;
+#ifndef KMP_VREG_TRIES
+#define KMP_VREG_TRIES 3
+#endif
+constexpr uint32_t kVregTries = KMP_VREG_TRIES;  // learned bucket layouts in a row before the counting partition

@@ -89,7 +89,6 @@ def order_xcd(items: np.ndarray) -> np.ndarray:
 
 
 class DevicePipeline:
-    split_edges_syncs = True  # kmp_dev_split_edges synchronises the stream (dist.kmer_split_step relies on it)
 
     def __init__(self, proteins: Proteins, k: int, device: torch.device | str = "cuda",
                  edge_cap: int | None = None):
@@ -253,9 +252,8 @@ class DevicePipeline:
         return lib().kmp_postings_last_layout(self._workspace()) == _lib.KMP_LAYOUT_BUCKETED_HEAVY
 
     def set_tail(self, mode: str = "fast") -> None:
-        """Row-block tail of unscored calls: 'fast' (default, where it applies), 'dense' (the fast tail
-        and its dense variant for small batches) or 'count'."""
-        m = {"fast": _lib.KMP_TAIL_FAST, "count": _lib.KMP_TAIL_COUNT, "dense": _lib.KMP_TAIL_DENSE}[mode]
+        """Row-block tail of unscored calls: 'fast' (default, where it applies) or 'count'."""
+        m = {"fast": _lib.KMP_TAIL_FAST, "count": _lib.KMP_TAIL_COUNT}[mode]
         check(lib().kmp_postings_set_tail(self._workspace(), m), "kmp_postings_set_tail")
 
     def last_tail(self) -> str:

@@ -177,19 +177,22 @@ def kmer_split_step(pipe, rank: int, world: int, group=None, min_shared: int = 1
             dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=group)
         else:
             recv = send
-        # the reduced flags go to the host behind the collectives on the same stream; split_edges
-        # synchronises that stream for its edge count, so reading them below waits on nothing more
-        # (no read-back of its own per step)
+        # the reduced flags go to the host behind the collectives on the same stream, with an event
+        # behind the copy; split_edges usually synchronises the stream already, so waiting on the
+        # event below costs nothing more (no read-back of its own per step)
         if st.host_flags is None or st.host_flags.numel() != flags.numel():
             st.host_flags = torch.empty(flags.shape, dtype=flags.dtype, pin_memory=dev.type == "cuda")
         st.host_flags.copy_(flags, non_blocking=dev.type == "cuda")
+        copied = torch.cuda.Event() if dev.type == "cuda" else None
+        if copied is not None:
+            copied.record()
         if ev:
             ev[2].record()
         m = pipe.split_edges(recv, lo, hi, min_shared)
         if ev:
             ev[3].record()
-        if dev.type == "cuda" and not hasattr(pipe, "split_edges_syncs"):
-            torch.cuda.current_stream().synchronize()  # a stand-in stage that does not synchronise
+        if copied is not None:
+            copied.synchronize()  # the host copy of the flags has landed
         fl = [int(x) for x in st.host_flags.tolist()]
         if fl[_lib.KMP_SPLIT_CLASS]:
             st.row_split = True
