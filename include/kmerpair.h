@@ -578,7 +578,8 @@ int kmp_dev_pairs_rows_multi(kmp_postings* const* ws, const int* ks, uint32_t nk
  * again with learn — every rank turns its heavy path on for the batch, vertex.rs:59-140). */
 enum {
     KMP_SPLIT_RERUN = 0, KMP_SPLIT_CLASS = 1, KMP_SPLIT_HEAVY = 2, KMP_SPLIT_MAX_PART = 3,
-    KMP_SPLIT_MAX_SHARD = 4, KMP_SPLIT_BIN_TILES = 5, KMP_SPLIT_CURSOR = 6, KMP_SPLIT_FLAGS = 8
+    KMP_SPLIT_MAX_SHARD = 4, KMP_SPLIT_BIN_TILES = 5, KMP_SPLIT_CURSOR = 6, KMP_SPLIT_MAX_KEYS = 7,
+    KMP_SPLIT_FLAGS = 8
 };
 int kmp_dev_split_expand(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
                          uint32_t n, int k, uint64_t slots, uint32_t heavy_df, int require_class_diff, uint32_t part,
@@ -587,6 +588,38 @@ int kmp_dev_split_expand(kmp_postings* ws, const uint8_t* d_res, const uint64_t*
 int kmp_dev_split_edges(kmp_postings* ws, const unsigned long long* d_keys, uint64_t m, uint32_t n, uint32_t row_lo,
                         uint32_t row_hi, uint32_t min_shared, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w,
                         uint64_t cap, uint64_t* n_edges, void* stream);
+
+/* The k-mer split with a SHARDED START (the default multi-GPU flow of bench.py --gpus N, dist.py):
+ * rank `part` holds only the residues its chunks read — chunks [c_lo, c_hi) of the batch's
+ * 4,096-slot chunks (kmp_split_plan; slice [res_lo, res_hi) of the packed residues, 16-byte aligned
+ * start) — plus the batch's offsets and class ids.  Instead of keying every window (the replicated
+ * level 1 of kmp_dev_split_expand), each rank keys its own chunks once and the keys travel:
+ *   kmp_dev_split_keys   the rank's windows keyed (radix-21 codes, protein.rs:29-37,107-132) and
+ *     ranked by coarse bin; region d of d_ksend (kcap u64 words) receives the keys of rank d's bins
+ *     with a run table per chunk (no host synchronisation).  d_flags: RERUN when a region was too
+ *     small (MAX_KEYS = the region size that fits, every rank's the same after the max-reduce).
+ *   exchange (the caller's collective): an all-to-all of equal splits of kcap words.
+ *   kmp_dev_split_group  the received keys (parts regions of kcap words) grouped and expanded like
+ *     kmp_dev_split_expand's (its bins, all rows, routed to the row owners in d_send), merging the
+ *     keys phase's flags into d_flags (same buffer, same step).
+ *   then the pair-key exchange and kmp_dev_split_edges as above.
+ * kmp_split_plan: the rank's chunk range, residue slice and the default region size (key_cap). */
+typedef struct {
+    uint64_t slots;            /* kmp_set_capacity(n, ΣL) */
+    uint32_t n_chunks, c_lo, c_hi;
+    uint64_t res_lo, res_hi;   /* the residue slice the rank's chunks read */
+    uint64_t key_table_words;  /* run-table words at the start of every key region */
+    uint64_t key_cap;          /* a default key-region size (u64 words; grown from MAX_KEYS) */
+} kmp_split_span;
+int kmp_split_plan(const uint64_t* offsets, uint32_t n, int k, uint32_t part, uint32_t parts, kmp_split_span* out);
+int kmp_dev_split_keys(kmp_postings* ws, const uint8_t* d_res, uint64_t res_lo, uint64_t res_hi,
+                       const uint64_t* d_res_off, const uint16_t* d_class, uint32_t n, int k, uint64_t slots,
+                       uint32_t part, uint32_t parts, uint64_t kcap, unsigned long long* d_ksend, uint32_t* d_flags,
+                       void* stream);
+int kmp_dev_split_group(kmp_postings* ws, const unsigned long long* d_krecv, uint64_t kcap, uint32_t n, int k,
+                        uint64_t slots, uint32_t heavy_df, int require_class_diff, uint32_t part, uint32_t parts,
+                        uint64_t cap, const uint32_t* learn, unsigned long long* d_send, uint32_t* d_flags,
+                        unsigned long long* d_stats, void* stream);
 
 /* Row ranges of a split of the pair space: range d = [start[d], start[d+1]) with start[d] =
  * floor(N (1 - sqrt(1 - d/parts))): a pair belongs to its smaller protein, so the ranges hold about

@@ -218,3 +218,114 @@ def test_kmer_split_routed_large_groups(oracle_mod, g):
         np.testing.assert_array_equal(ep, p)
         np.testing.assert_array_equal(eq, q)
         np.testing.assert_array_equal(ew, w)
+
+
+def emulate_sharded_split(b, k, G, kcap=None, cap=None, min_shared=1, require_class_diff=True):
+    """The k-mer split with a sharded start, G ranks on one GPU in one process: each rank's
+    ShardPipeline holds only its residue slice; kmp_dev_split_keys per rank, the key all-to-all done
+    by slicing the key regions, kmp_dev_split_group per rank, the pair-key all-to-all likewise,
+    kmp_dev_split_edges per rank; flags max-reduced and fed back as `learn`, as
+    dist.sharded_split_step does over RCCL.  Returns (edges, flags, summed stats, reruns)."""
+    import torch
+    from uniprot_kmer_based_clustering_amd.device import ShardPipeline
+    pipes = [ShardPipeline(b.residues, b.offsets, b.class_id, k, r, G, "cuda:0") for r in range(G)]
+    for r, pp in enumerate(pipes):  # the slice is the rank's share of the residues, not the batch
+        assert pp.res.numel() <= int(b.offsets[-1]) // G + 4096 or G == 1
+    start = _lib.row_split(b.n, G)
+    kcap = kcap or int(pipes[0].span.key_cap)
+    cap = cap or max(4096, pipes[0].total // 4 // (G * G))
+    learn, reruns = None, 0
+    for _ in range(8):
+        ksend = [torch.empty(G * kcap, dtype=torch.int64, device="cuda:0") for _ in range(G)]
+        sends = [torch.empty(G * cap, dtype=torch.int64, device="cuda:0") for _ in range(G)]
+        flags = [torch.zeros(_lib.KMP_SPLIT_FLAGS, dtype=torch.int32, device="cuda:0") for _ in range(G)]
+        stats = [torch.zeros(8, dtype=torch.int64, device="cuda:0") for _ in range(G)]
+        for r in range(G):
+            pipes[r].split_keys(r, G, kcap, ksend[r], flags[r])
+        for d in range(G):
+            krecv = torch.cat([ksend[r][d * kcap:(d + 1) * kcap] for r in range(G)])
+            pipes[d].split_group(krecv, kcap, d, G, cap, sends[d], flags[d], stats[d], learn=learn,
+                                 require_class_diff=require_class_diff)
+        torch.cuda.synchronize()
+        fl = torch.stack(flags).max(dim=0).values.cpu().tolist()
+        out = [[], [], []]
+        for d in range(G):
+            recv = torch.cat([sends[r][d * cap:(d + 1) * cap] for r in range(G)])
+            pipes[d].split_edges(recv, int(start[d]), int(start[d + 1]), min_shared)
+            for a, x in zip(out, pipes[d].edges()):
+                a.append(x)
+        if (fl[_lib.KMP_SPLIT_RERUN] or fl[_lib.KMP_SPLIT_HEAVY]) and not fl[_lib.KMP_SPLIT_CLASS]:
+            reruns += 1
+            learn = fl
+            cap = max(cap, fl[_lib.KMP_SPLIT_MAX_PART] + fl[_lib.KMP_SPLIT_MAX_PART] // 16 + 1024)
+            kcap = max(kcap, fl[_lib.KMP_SPLIT_MAX_KEYS] + fl[_lib.KMP_SPLIT_MAX_KEYS] // 32 + 1024)
+            continue
+        st = torch.stack(stats).cpu().numpy()
+        tot = st.sum(axis=0)
+        tot[4] = st[:, 4].max()
+        return [np.concatenate(a) for a in out], fl, tot, reruns
+    raise AssertionError("capacities unstable")
+
+
+@pytest.mark.parametrize("g", [1, 2, 4, 8])
+def test_sharded_split_config4(config4, oracle_mod, g):
+    """Config 4's workload through the k-mer split with a sharded start (each rank holds 1/G of the
+    residues, keys its own windows once, the keys travel to their bins' owners): the rank-order
+    concatenation equals the oracle's canonical list and the ranks' statistics add up to the batch's;
+    no rerun with the default capacities."""
+    b, (p, q, w) = config4
+    (ep, eq, ew), fl, tot, reruns = emulate_sharded_split(b, 7, g)
+    assert not fl[_lib.KMP_SPLIT_HEAVY] and not fl[_lib.KMP_SPLIT_CLASS] and reruns == 0
+    np.testing.assert_array_equal(ep, p)
+    np.testing.assert_array_equal(eq, q)
+    np.testing.assert_array_equal(ew, w)
+    c = oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=7, threads=16).counters()
+    assert tot[3] == c["sum_cdf2"] and tot[1] == c["distinct"] and tot[4] == c["max_df"]
+    assert tot[0] == c["sum_S"] and tot[6] == int(w.sum())
+
+
+def test_sharded_split_reruns_heavy_and_options(oracle_mod):
+    """Key regions and pair-key regions far too small rerun with the sizes the reduced flags report
+    (same edges, capacities learned from counts: the same reruns every time); min_shared and the
+    class filter off; the reference's dataset at k = 5 (frequent 5-mers: HEAVY, then every rank's
+    heavy path) gives the golden edge list at G = 2 and 3; routed buckets above the LDS stage."""
+    b = K.synth(20000, 9)
+    o = oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=7, threads=8)
+    seen = set()
+    for ms in (1, 2, 1):
+        (ep, eq, ew), fl, _, reruns = emulate_sharded_split(b, 7, 3, kcap=4096, cap=64, min_shared=ms)
+        p, q, w = o.pairs(min_shared=ms)
+        seen.add(reruns)
+        np.testing.assert_array_equal(ep, p)
+        np.testing.assert_array_equal(eq, q)
+        np.testing.assert_array_equal(ew, w)
+    assert len(seen) == 1 and seen.pop() >= 1
+    (ep, eq, ew), _, _, _ = emulate_sharded_split(b, 7, 4, require_class_diff=False)
+    p, q, w = o.pairs(require_class_diff=False)
+    np.testing.assert_array_equal(ep, p)
+    np.testing.assert_array_equal(ew, w)
+    res, off, cls, _ = uniprot()
+    g = load_json("uniprot_counters.json")["5"]
+    for G in (2, 3):
+        (ep, eq, ew), fl, tot, reruns = emulate_sharded_split(K.Proteins(res, off, cls), 5, G)
+        assert reruns >= 1 and not fl[_lib.KMP_SPLIT_HEAVY] and not fl[_lib.KMP_SPLIT_RERUN]
+        assert len(ep) == g["n_edges"] and edges_sha256(ep, eq, ew) == g["edges_sha256"]
+    d = dense_families()
+    (ep, eq, ew), fl, _, _ = emulate_sharded_split(d, 7, 2)
+    p, q, w = oracle_mod.Oracle(d.residues, d.offsets, d.class_id, k=7, threads=8).pairs()
+    np.testing.assert_array_equal(ep, p)
+    np.testing.assert_array_equal(eq, q)
+    np.testing.assert_array_equal(ew, w)
+
+
+def test_sharded_split_small_batches(oracle_mod):
+    """More ranks than chunks or bins (ranks with nothing to key or no bins), a protein shorter than
+    k, and one class: every rank still steps in lockstep and the result is the oracle's."""
+    for n, G in ((5, 8), (300, 8), (3000, 5)):
+        b = K.synth(n, 4)
+        o = oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=5, threads=4)
+        (ep, eq, ew), fl, _, _ = emulate_sharded_split(b, 5, G, require_class_diff=False)
+        p, q, w = o.pairs(require_class_diff=False)
+        np.testing.assert_array_equal(ep, p)
+        np.testing.assert_array_equal(eq, q)
+        np.testing.assert_array_equal(ew, w)

@@ -25,9 +25,16 @@ KMP_LAYOUT_FLAT, KMP_LAYOUT_BUCKETED, KMP_LAYOUT_BUCKETED_HEAVY = 0, 1, 2
 KMP_TAIL_COUNT, KMP_TAIL_FAST = 0, 1
 KMP_PARTITION_AUTO, KMP_PARTITION_COUNT, KMP_PARTITION_CURSOR = 0, 1, 2
 (KMP_SPLIT_RERUN, KMP_SPLIT_CLASS, KMP_SPLIT_HEAVY, KMP_SPLIT_MAX_PART, KMP_SPLIT_MAX_SHARD, KMP_SPLIT_BIN_TILES,
- KMP_SPLIT_CURSOR) = range(7)
+ KMP_SPLIT_CURSOR, KMP_SPLIT_MAX_KEYS) = range(8)
 KMP_SPLIT_FLAGS = 8
 KMP_LDS_SORT_MAX = 4096
+
+
+class SplitSpan(C.Structure):
+    """kmp_split_span: a rank's chunk range and residue slice of the sharded k-mer split."""
+    _fields_ = [("slots", C.c_uint64), ("n_chunks", C.c_uint32), ("c_lo", C.c_uint32), ("c_hi", C.c_uint32),
+                ("res_lo", C.c_uint64), ("res_hi", C.c_uint64), ("key_table_words", C.c_uint64),
+                ("key_cap", C.c_uint64)]
 
 
 class KmpError(RuntimeError):
@@ -195,6 +202,11 @@ SIGNATURES = {
                                         C.c_uint32, C.c_uint32, C.c_uint64, P, P, P, P, P]),
     "kmp_dev_split_edges": (C.c_int, [P, P, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P, P, P,
                                        C.c_uint64, U64P, P]),
+    "kmp_split_plan": (C.c_int, [P, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32, C.POINTER(SplitSpan)]),
+    "kmp_dev_split_keys": (C.c_int, [P, P, C.c_uint64, C.c_uint64, P, P, C.c_uint32, C.c_int, C.c_uint64,
+                                      C.c_uint32, C.c_uint32, C.c_uint64, P, P, P]),
+    "kmp_dev_split_group": (C.c_int, [P, P, C.c_uint64, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32, C.c_int,
+                                       C.c_uint32, C.c_uint32, C.c_uint64, P, P, P, P, P]),
     "kmp_dev_pairs_rows": (C.c_int, [P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32, C.c_uint32,
                                      C.c_int, C.c_uint32, C.c_uint32, P, P, P, C.c_uint64, U64P, P, P]),
     "kmp_row_split": (None, [C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]),
@@ -274,6 +286,16 @@ def geometry() -> PairGeometry:
     g = PairGeometry()
     lib().kmp_pair_geometry_get(C.byref(g))
     return g
+
+
+def split_plan(offsets, k: int, part: int, parts: int) -> SplitSpan:
+    """kmp_split_plan over host offsets (u64[N+1])."""
+    import numpy as np
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    sp = SplitSpan()
+    check(lib().kmp_split_plan(C.c_void_p(off.ctypes.data), len(off) - 1, k, part, parts, C.byref(sp)),
+          "kmp_split_plan")
+    return sp
 
 
 def row_split(n: int, parts: int):

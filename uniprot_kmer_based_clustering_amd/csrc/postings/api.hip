@@ -287,18 +287,26 @@ int kmp_dev_pairs_rows_multi(kmp_postings* const* ws, const int* ks, uint32_t nk
     return rc;
 }
 
-int kmp_dev_split_expand(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
-                         uint32_t n, int k, uint64_t slots, uint32_t heavy_df, int require_class_diff, uint32_t part,
-                         uint32_t parts, uint64_t cap, const uint32_t* learn, unsigned long long* d_send,
-                         uint32_t* d_flags, unsigned long long* d_stats, void* stream) {
-    if (!ws || !d_res || !d_res_off || !d_class || !d_send || !d_flags || !d_stats || k < 1 || k > kMaxK ||
-        parts < 1 || parts > kSplitMax || part >= parts || cap < 1)
-        return KMP_EINVAL;
+// the key source of a split expand: the whole batch's residues (every rank keys every window and
+// keeps its bins: kmp_dev_split_expand) or the pieces every rank sent (kmp_dev_split_group)
+struct SplitSrc {
+    const uint8_t* d_res;
+    const uint64_t* d_res_off;
+    const uint16_t* d_class;
+    const unsigned long long* d_krecv;  // non-null: the received pieces (kcap u64 words per source)
+    uint64_t kcap;
+};
+
+static int split_expand_impl(kmp_postings* ws, const SplitSrc& src, uint32_t n, int k, uint64_t slots,
+                             uint32_t heavy_df, int require_class_diff, uint32_t part, uint32_t parts, uint64_t cap,
+                             const uint32_t* learn, unsigned long long* d_send, uint32_t* d_flags,
+                             unsigned long long* d_stats, void* stream) {
     hipStream_t st = as_stream(stream);
     if (heavy_df < 2) heavy_df = 2;
     const Layout lay = make_layout(n, k, slots, true);
     if (!lay.bucketed) return KMP_ESTATE;
-    const std::vector<unsigned long long> shape = {n, slots, (unsigned long long)k, parts};
+    const bool recv = src.d_krecv != nullptr;
+    const std::vector<unsigned long long> shape = {n, slots, (unsigned long long)k, parts, recv};
     if (ws->split_shape != shape) {  // a new batch: learned capacities start over
         ws->split_shape = shape;
         ws->shard_cap = slots / 4 / kShards / parts + 4096;
@@ -307,7 +315,9 @@ int kmp_dev_split_expand(kmp_postings* ws, const uint8_t* d_res, const uint64_t*
         ws->shape.clear();
         ws->split_heavy = false;
         ws->fast_tail = ws->fast_mode;
+        ws->vreg_on = false;
     }
+    const uint32_t nb = 1u << lay.bbits;
     if (learn) {  // the last call's flags, reduced over the ranks: every rank grows the same way
         if (learn[KMP_SPLIT_HEAVY]) ws->split_heavy = true;  // a rank spilled: the heavy path from now on
         // an eighth of slack: the fullest region varies by a few percent from call to call with the
@@ -315,7 +325,23 @@ int kmp_dev_split_expand(kmp_postings* ws, const uint8_t* d_res, const uint64_t*
         if (learn[KMP_SPLIT_MAX_SHARD] > ws->shard_cap)
             ws->shard_cap = learn[KMP_SPLIT_MAX_SHARD] + learn[KMP_SPLIT_MAX_SHARD] / 8 + 256;
         if (learn[KMP_SPLIT_BIN_TILES]) ws->bp_J_min = std::max(ws->bp_J_min, learn[KMP_SPLIT_BIN_TILES] + 2);
-        if (learn[KMP_SPLIT_CURSOR]) ws->cur_on = false;
+        if (learn[KMP_SPLIT_CURSOR]) {
+            if (recv && ws->cur.p) {
+                // a bucket region overflowed on some rank: this rank's regions from its last call's
+                // exact bucket counts (the cursors count dropped keys too; cleared only by the next
+                // front), its own bins only — the layout is the rank's own business
+                PG(ws->vreg.reserve(nb + 1));
+                vreg_kernel<<<1, 1024, 0, st>>>(ws->cur.p, nb, ws->vreg.p);
+                uint32_t tot = 0;
+                PG(hipMemcpyAsync(&tot, ws->vreg.p + nb, 4, hipMemcpyDeviceToHost, st));
+                PG(hipStreamSynchronize(st));
+                if ((uint64_t)tot + 2 * kBpTile >= (1ull << 32)) return KMP_EINVAL;
+                ws->vreg_total = tot;
+                ws->vreg_on = true;
+            } else {
+                ws->cur_on = false;  // the residue source: the counting partition
+            }
+        }
     }
     if (ws->spill_cap == 0) ws->spill_cap = 1024;
     ws->front_ok = false;  // the front below holds one bucket range only
@@ -336,19 +362,30 @@ int kmp_dev_split_expand(kmp_postings* ws, const uint8_t* d_res, const uint64_t*
     }
     PG(ws->split_cur.reserve((uint64_t)kSplitMax * kShards));
     const BpDigits dg = bp_digits(lay);
-    ws->bin_lo = (uint32_t)((uint64_t)part * dg.nb1 / parts);
-    ws->bin_hi = (uint32_t)((uint64_t)(part + 1) * dg.nb1 / parts);
+    ws->bin_lo = split_bin_lo(part, dg.nb1, parts);
+    ws->bin_hi = split_bin_lo(part + 1, dg.nb1, parts);
     auto make_keys = [&](const Layout& l, hipStream_t s) {
         ws->parted = true;
+        if (recv) {
+            // the cursor level 2 always (the counting partition needs level 1's own output)
+            if (!cur_geometry(l, &ws->cg)) return hipErrorInvalidValue;
+            if (ws->vreg_on) {
+                ws->cg.vreg = ws->vreg.p;
+                const hipError_t e = ws->sorted.reserve(ws->vreg_total);
+                if (e != hipSuccess) return e;
+            }
+            ws->cur_used = true;
+            return bp_level1_recv(ws, src.d_krecv, src.kcap, parts, l, slots, s);
+        }
         ws->cur_used = ws->cur_on && cur_geometry(l, &ws->cg);
-        return bp_level1(ws, d_res, d_res_off, d_class, k, n, slots, l, s);
+        return bp_level1(ws, src.d_res, src.d_res_off, src.d_class, k, n, slots, l, s);
     };
     const ClearInKeys guard(ws);
     SplitRows rows{};
     rows.parts = parts;
     kmp_row_split(n, parts, rows.start);
-    // the send cursors are cleared with the step's flags (by chunk_desc_kernel in the front); routed
-    // (no heavy path): the bucket kernels write the send regions, pre-filled with kNoKey
+    // the send cursors are cleared with the step's flags (by the front's first kernel); routed (no
+    // heavy path): the bucket kernels write the send regions, pre-filled with kNoKey
     const bool routed = !ws->split_heavy;
     auto front = [&](hipStream_t s) -> int {
         const uint32_t ncur = routed ? parts * kShards : parts;
@@ -369,9 +406,12 @@ int kmp_dev_split_expand(kmp_postings* ws, const uint8_t* d_res, const uint64_t*
         return rc;
     };
     auto route = [&](hipStream_t s, int heavy_done) -> int {
+        // merge: the keys phase wrote this step's key-exchange flags into d_flags first
+        const int merge = recv ? 1 : 0;
         if (routed) {  // the bucket kernels routed the keys: the flags and statistics only
             split_pad_finish_kernel<<<dim3(1, 1), 256, 0, s>>>(d_send, cap, ws->split_cur.p, ws->bstats.p, ws->flags.p,
-                                                                ws->shard_cap, parts, d_flags, d_stats, heavy_done, 1);
+                                                                ws->shard_cap, parts, d_flags, d_stats, heavy_done, 1,
+                                                                merge);
             PG(hipGetLastError());
             return KMP_OK;
         }
@@ -380,9 +420,15 @@ int kmp_dev_split_expand(kmp_postings* ws, const uint8_t* d_res, const uint64_t*
             ws->inc_sorted.p, cursor, ws->shard_cap, bits_for(n), rows, cap, d_send, ws->split_cur.p);
         split_pad_finish_kernel<<<dim3((uint32_t)std::min<uint64_t>((cap + 1023) / 1024, 256), parts), 256, 0, s>>>(
             d_send, cap, ws->split_cur.p, ws->bstats.p, ws->flags.p, ws->shard_cap, parts, d_flags, d_stats,
-            heavy_done, 0);
+            heavy_done, 0, merge);
         PG(hipGetLastError());
         return KMP_OK;
+    };
+    auto unbind = [&]() {
+        ws->bin_lo = ws->bin_hi = 0;
+        ws->l1_in = nullptr;
+        ws->l2_tab = nullptr;
+        ws->cg.vreg = nullptr;
     };
     if (ws->split_heavy) {
         // frequent k-mers (vertex.rs:59-140 at k = 5): the rank's front, one read-back, its spill
@@ -391,7 +437,7 @@ int kmp_dev_split_expand(kmp_postings* ws, const uint8_t* d_res, const uint64_t*
         // are the rank's own, so a spill overflow reruns the front here; every other capacity is
         // reported in the flags and grown identically on every rank.  Host-synchronous.
         int rc = KMP_OK;
-        bool routed = false;
+        bool routed_done = false;
         for (int attempt = 0; attempt < 4; ++attempt) {
             if ((rc = step_reserve(ws, c, g, st)) != KMP_OK) break;
             if ((rc = front(st)) != KMP_OK) break;
@@ -412,17 +458,17 @@ int kmp_dev_split_expand(kmp_postings* ws, const uint8_t* d_res, const uint64_t*
                 if ((rc = heavy_phase(ws, c, spill_total, true, st)) != KMP_OK) break;
             }
             rc = route(st, 1);
-            routed = true;
+            routed_done = true;
             break;
         }
-        ws->bin_lo = ws->bin_hi = 0;
-        if (rc == KMP_OK && !routed) {
+        unbind();
+        if (rc == KMP_OK && !routed_done) {
             // every attempt grew the spill regions: no keys are sent and the flags ask every rank for
             // a rerun, so the ranks stay in lockstep through the collectives (an error returned here
             // on one rank alone would leave the others waiting in the all-to-all); the grown regions
             // are this rank's own and stay for the rerun
             PG(hipMemsetAsync(d_send, 0xFF, (size_t)parts * cap * sizeof(unsigned long long), st));
-            PG(hipMemsetAsync(d_flags, 0, KMP_SPLIT_FLAGS * sizeof(uint32_t), st));
+            if (!recv) PG(hipMemsetAsync(d_flags, 0, KMP_SPLIT_FLAGS * sizeof(uint32_t), st));
             PG(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_flags + KMP_SPLIT_RERUN), 1, 1, st));
             PG(hipMemsetAsync(d_stats, 0, 8 * sizeof(unsigned long long), st));
         }
@@ -434,11 +480,122 @@ int kmp_dev_split_expand(kmp_postings* ws, const uint8_t* d_res, const uint64_t*
     };
     const std::vector<unsigned long long> key = {
         n, slots, (unsigned long long)k, heavy_df, (unsigned long long)require_class_diff, part, parts, cap,
-        (uintptr_t)d_res, (uintptr_t)d_res_off, (uintptr_t)d_class, (uintptr_t)d_send, (uintptr_t)d_flags,
-        (uintptr_t)d_stats, ws->shard_cap, ws->spill_cap, ws->bp_J_min, ws->cur_on, ws->timing};
+        (uintptr_t)src.d_res, (uintptr_t)src.d_res_off, (uintptr_t)src.d_class, (uintptr_t)src.d_krecv, src.kcap,
+        (uintptr_t)d_send, (uintptr_t)d_flags, (uintptr_t)d_stats, ws->shard_cap, ws->spill_cap, ws->bp_J_min,
+        ws->cur_on, ws->timing, ws->vreg_on ? ws->vreg_total + 1 : 0};
     const int rc = slot_launch(ws, ws->split_g[0], key, enqueue, st);
-    ws->bin_lo = ws->bin_hi = 0;
+    unbind();
     return rc;
+}
+
+int kmp_dev_split_expand(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
+                         uint32_t n, int k, uint64_t slots, uint32_t heavy_df, int require_class_diff, uint32_t part,
+                         uint32_t parts, uint64_t cap, const uint32_t* learn, unsigned long long* d_send,
+                         uint32_t* d_flags, unsigned long long* d_stats, void* stream) {
+    if (!ws || !d_res || !d_res_off || !d_class || !d_send || !d_flags || !d_stats || k < 1 || k > kMaxK ||
+        parts < 1 || parts > kSplitMax || part >= parts || cap < 1)
+        return KMP_EINVAL;
+    return split_expand_impl(ws, SplitSrc{d_res, d_res_off, d_class, nullptr, 0}, n, k, slots, heavy_df,
+                             require_class_diff, part, parts, cap, learn, d_send, d_flags, d_stats, stream);
+}
+
+int kmp_split_plan(const uint64_t* offsets, uint32_t n, int k, uint32_t part, uint32_t parts, kmp_split_span* out) {
+    if (!offsets || !out || k < 1 || k > kMaxK || parts < 1 || parts > kSplitMax || part >= parts) return KMP_EINVAL;
+    *out = kmp_split_span{};
+    const uint64_t total = offsets[n];
+    const uint64_t slots = kmp_set_capacity(n, total);
+    if (slots > 0xFFFFFFFFull) return KMP_EINVAL;
+    const Layout lay = make_layout(n, k, slots, true);
+    if (!lay.bucketed) return KMP_ESTATE;
+    const SplitGeom sg = split_geom(lay, slots, parts);
+    const uint32_t c_lo = split_chunk_lo(sg, part, parts), c_hi = split_chunk_lo(sg, part + 1, parts);
+    out->slots = slots;
+    out->n_chunks = sg.n_chunks;
+    out->c_lo = c_lo;
+    out->c_hi = c_hi;
+    // the protein whose slot region [set_base(off[p], p), set_base(off[p + 1], p + 1)) holds slot s
+    // (n: the tail past the last region) — chunk_desc_kernel's view of a chunk's ends
+    auto prot = [&](uint64_t s) {
+        uint32_t lo = 0, hi = n;  // largest p in [0, n] with base(p) <= s
+        while (lo < hi) {
+            const uint32_t mid = (uint32_t)(((uint64_t)lo + hi + 1) / 2);
+            if (set_base(offsets[mid], mid) <= s) lo = mid;
+            else hi = mid - 1;
+        }
+        return lo;
+    };
+    if (c_hi > c_lo) {
+        const uint64_t s0 = (uint64_t)c_lo * kKeyChunk, s1 = std::min<uint64_t>((uint64_t)c_hi * kKeyChunk, slots);
+        uint32_t p = prot(s0);
+        uint64_t L = p < n ? offsets[p + 1] - offsets[p] : 0, b = set_base(offsets[p], p);
+        const uint64_t r0 = offsets[p] + std::min<uint64_t>(s0 - b, L);
+        p = prot(s1 - 1);
+        L = p < n ? offsets[p + 1] - offsets[p] : 0;
+        b = set_base(offsets[p], p);
+        const uint64_t r1 = p < n ? offsets[p] + std::min<uint64_t>(L, s1 - b + k - 1) : offsets[p];
+        out->res_lo = r0 & ~15ull;  // the level-1 kernel's 16-byte loads start on 16-byte boundaries
+        out->res_hi = std::max(r1, out->res_lo);
+    }
+    out->key_table_words = sg.tb;
+    // a region: the table plus kSendShards sub-regions of a fair share of the windows with 1/16 slack
+    const uint64_t per = slots / parts / parts / kSendShards;
+    out->key_cap = sg.tb + kSendShards * (per + per / 16 + 256);
+    return KMP_OK;
+}
+
+int kmp_dev_split_keys(kmp_postings* ws, const uint8_t* d_res, uint64_t res_lo, uint64_t res_hi,
+                       const uint64_t* d_res_off, const uint16_t* d_class, uint32_t n, int k, uint64_t slots,
+                       uint32_t part, uint32_t parts, uint64_t kcap, unsigned long long* d_ksend, uint32_t* d_flags,
+                       void* stream) {
+    if (!ws || !d_res_off || !d_class || !d_ksend || !d_flags || k < 1 || k > kMaxK || parts < 1 ||
+        parts > kSplitMax || part >= parts || res_hi < res_lo || (res_lo & 15u) || (res_hi > res_lo && !d_res))
+        return KMP_EINVAL;
+    if (slots > 0xFFFFFFFFull || (uint64_t)parts * kcap >= (1ull << 32)) return KMP_EINVAL;
+    hipStream_t st = as_stream(stream);
+    const Layout lay = make_layout(n, k, slots, true);
+    if (!lay.bucketed) return KMP_ESTATE;
+    const SplitGeom sg = split_geom(lay, slots, parts);
+    // a region too small for its run table: nothing is sent, the flags report the size that fits
+    const uint64_t sub64 = kcap >= sg.tb + kSendShards ? (kcap - sg.tb) / kSendShards : 0;
+    const uint32_t sub = (uint32_t)std::min<uint64_t>(sub64, 0xFFFFFFFFull);
+    const uint32_t c_lo = split_chunk_lo(sg, part, parts), c_hi = split_chunk_lo(sg, part + 1, parts);
+    const uint32_t G = c_hi - c_lo, nkc = parts * kSendShards;
+    PG(ws->chunk_desc.reserve(4ull * std::max(1u, G)));
+    PG(ws->split_kcur.reserve(nkc));
+    PG(ws->flags.reserve(kFlN));
+    const BpDigits dg = bp_digits(lay);
+    const uint32_t pw21 = (uint32_t)pow21(k - 1);
+    auto enqueue = [&](hipStream_t s) -> int {
+        // descriptors of the rank's chunks, the send cursors and the flags cleared
+        chunk_desc_kernel<<<(n + 1 + 255) / 256, 256, 0, s>>>(
+            d_res_off, n, slots, c_lo, c_hi, k, reinterpret_cast<uint4*>(ws->chunk_desc.p), ws->split_kcur.p, nkc,
+            StepClear{ws->flags.p, kFlN, nullptr, 0, nullptr, 0});
+        if (G) {
+            const SendL1 sl{d_ksend, kcap, sg.tb, sub, ws->split_kcur.p, part, parts, c_lo, sg.rowlen, res_lo, res_hi};
+            // one workgroup per chunk (every digit ranked: the single-GPU geometry)
+            bp_scatter1p_kernel<KMP_L1_THREADS, true><<<G, KMP_L1_THREADS, 0, s>>>(
+                d_res, d_res_off, d_class, k, n, slots, G, reinterpret_cast<const uint4*>(ws->chunk_desc.p), lay, dg,
+                pw21, 0u, dg.nb1, nullptr, nullptr, ws->flags.p, sl);
+        }
+        split_keys_finish_kernel<<<1, 256, 0, s>>>(ws->split_kcur.p, nkc, ws->flags.p, sg.tb, d_flags);
+        PG(hipGetLastError());
+        return KMP_OK;
+    };
+    const std::vector<unsigned long long> key = {n, slots, (unsigned long long)k, part, parts, kcap, res_lo, res_hi,
+                                                 (uintptr_t)d_res, (uintptr_t)d_res_off, (uintptr_t)d_class,
+                                                 (uintptr_t)d_ksend, (uintptr_t)d_flags};
+    return slot_launch(ws, ws->split_g[2], key, enqueue, st);
+}
+
+int kmp_dev_split_group(kmp_postings* ws, const unsigned long long* d_krecv, uint64_t kcap, uint32_t n, int k,
+                        uint64_t slots, uint32_t heavy_df, int require_class_diff, uint32_t part, uint32_t parts,
+                        uint64_t cap, const uint32_t* learn, unsigned long long* d_send, uint32_t* d_flags,
+                        unsigned long long* d_stats, void* stream) {
+    if (!ws || !d_krecv || !d_send || !d_flags || !d_stats || k < 1 || k > kMaxK || parts < 1 || parts > kSplitMax ||
+        part >= parts || cap < 1 || (uint64_t)parts * kcap >= (1ull << 32))
+        return KMP_EINVAL;
+    return split_expand_impl(ws, SplitSrc{nullptr, nullptr, nullptr, d_krecv, kcap}, n, k, slots, heavy_df,
+                             require_class_diff, part, parts, cap, learn, d_send, d_flags, d_stats, stream);
 }
 
 int kmp_dev_split_edges(kmp_postings* ws, const unsigned long long* d_keys, uint64_t m, uint32_t n, uint32_t row_lo,

@@ -59,7 +59,7 @@ hipError_t bp_level1(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_r
             sc = StepClear{ws->flags.p, kFlN, ws->bstats.p, kShards * 10, ws->clear_extra, ws->clear_n};
             ws->defer_clear = false;
         }
-        chunk_desc_kernel<<<(n + 1 + 255) / 256, 256, 0, st>>>(d_res_off, n, slots, G, k,
+        chunk_desc_kernel<<<(n + 1 + 255) / 256, 256, 0, st>>>(d_res_off, n, slots, 0u, G, k,
                                                                reinterpret_cast<uint4*>(ws->chunk_desc.p), ws->cur.p,
                                                                nb, sc);
         ws->bp_G = G;
@@ -77,7 +77,7 @@ hipError_t bp_level1(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_r
         // persistent: as many workgroups as fit the device at once, each walking its chunks with the
         // next one's loads in flight
         static thread_local int per_cu = 0;
-        if (!per_cu && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bp_scatter1p_kernel<KMP_L1_THREADS>,
+        if (!per_cu && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bp_scatter1p_kernel<KMP_L1_THREADS, false>,
                                                                      KMP_L1_THREADS, 0) != hipSuccess ||
                         per_cu < 1))
             per_cu = 2;
@@ -89,9 +89,9 @@ hipError_t bp_level1(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_r
         const uint32_t grid = nown >= dg.nb1 && !KMP_L1P_ALWAYS ? G
                                                                  : std::min<uint32_t>(G, (uint32_t)per_cu * device_cus());
         if (nown) {
-            bp_scatter1p_kernel<KMP_L1_THREADS><<<grid, KMP_L1_THREADS, 0, st>>>(
+            bp_scatter1p_kernel<KMP_L1_THREADS, false><<<grid, KMP_L1_THREADS, 0, st>>>(
                 d_res, d_res_off, d_class, k, n, slots, G, reinterpret_cast<const uint4*>(ws->chunk_desc.p), lay, dg,
-                pw21, dlo, dhi, H1, ws->keys.p, ws->flags.p);
+                pw21, dlo, dhi, H1, ws->keys.p, ws->flags.p, SendL1{});
             if (!direct)
                 bp_h1t_kernel<<<dim3((G + 31) / 32, (nown + 31) / 32), 256, 0, st>>>(H1, G, nown, 0, nown, H1 + h1);
         }
@@ -158,14 +158,24 @@ int bp_level2c(kmp_postings* ws, const Layout& lay, hipStream_t st) {
     if (c1 > c0 && ws->bp_local) {
         const uint32_t ntiles = (ws->bp_G + ws->bp_T - 1) / ws->bp_T, per = (ntiles * (c1 - c0) + 7) / 8;
         constexpr uint32_t kGp = kBpGatherTile / KMP_GATHER_THREADS, kGt = KMP_GATHER_THREADS;
-        if (ws->cg.vreg)
-            bp_scatter2g_kernel<kGp, kGt, true><<<8 * per, kGt, 0, st>>>(
-                ws->keys.p, ws->bp.p + ws->bp_h1t, ws->bp_G, ws->bp_hsb, ws->bp_hsc, ws->bp_T, ntiles, c1 - c0, dg, ws->cg,
-                ws->cur.p, ws->sorted.p, ws->flags.p, c0, c0);
-        else
-            bp_scatter2g_kernel<kGp, kGt, false><<<8 * per, kGt, 0, st>>>(
-                ws->keys.p, ws->bp.p + ws->bp_h1t, ws->bp_G, ws->bp_hsb, ws->bp_hsc, ws->bp_T, ntiles, c1 - c0, dg, ws->cg,
-                ws->cur.p, ws->sorted.p, ws->flags.p, c0, c0);
+        // level 1's output: this call's own segments, or (the k-mer split's sharded start) the
+        // pieces every rank sent (ws->l2_tab: their run tables in the receive buffer)
+        const bool recv = ws->l2_tab != nullptr;
+        const unsigned long long* in = recv ? ws->l1_in : ws->keys.p;
+        const uint32_t* tab = recv ? ws->l2_tab : ws->bp.p + ws->bp_h1t;
+        const uint32_t grid = 8 * per;
+#define KMP_L2G(V, R)                                                                                           \
+    bp_scatter2g_kernel<kGp, kGt, V, R><<<grid, kGt, 0, st>>>(in, tab, ws->bp_G, ws->bp_hsb, ws->bp_hsc, ws->bp_T, \
+                                                              ntiles, c1 - c0, dg, ws->cg, ws->cur.p, ws->sorted.p,   \
+                                                              ws->flags.p, c0, c0, ws->l2_rt)
+        if (recv) {
+            if (ws->cg.vreg) KMP_L2G(true, true);
+            else KMP_L2G(false, true);
+        } else {
+            if (ws->cg.vreg) KMP_L2G(true, false);
+            else KMP_L2G(false, false);
+        }
+#undef KMP_L2G
     } else if (c1 > c0) {
         if (ws->cg.vreg)
             bp_scatter2c_kernel<true><<<dim3(ws->bp_J, c1 - c0), kKeyThreads, 0, st>>>(
@@ -256,4 +266,62 @@ int front_flat(kmp_postings* ws, uint64_t slots, const Layout& lay, const uint16
     }
     ws->mark(4, st);
     return KMP_OK;
+}
+
+// ---- the k-mer split with a sharded start (kmp_dev_split_keys / kmp_dev_split_group) ----
+// geometry every rank derives alike from (batch, k, parts): chunks, the most chunks a rank holds,
+// the run-table row length (the most bins a rank owns + 1) and the table's u64 words per region
+struct SplitGeom {
+    uint32_t n_chunks, cm, rowlen, nb1;
+    uint64_t tb;
+};
+SplitGeom split_geom(const Layout& lay, uint64_t slots, uint32_t parts) {
+    SplitGeom g{};
+    g.n_chunks = (uint32_t)((slots + kKeyChunk - 1) / kKeyChunk);
+    g.cm = (g.n_chunks + parts - 1) / parts;
+    g.nb1 = bp_digits(lay).nb1;
+    g.rowlen = (g.nb1 + parts - 1) / parts + 1;
+    g.tb = ((uint64_t)g.cm * g.rowlen + 1) / 2;
+    return g;
+}
+uint32_t split_chunk_lo(const SplitGeom& g, uint32_t part, uint32_t parts) {
+    return (uint32_t)((uint64_t)part * g.n_chunks / parts);
+}
+
+// clears the bucket counts of the cursor level 2 and (sc) the step's flags: the front of a call
+// whose level 1 ran elsewhere (the received pieces)
+__global__ void split_recv_clear_kernel(uint32_t* __restrict__ cur, uint32_t ncur, StepClear sc) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint32_t i = t; i < ncur; i += gridDim.x * blockDim.x) cur[i] = 0;
+    if (blockIdx.x == 0 && sc.flags) {
+        for (uint32_t i = threadIdx.x; i < sc.n_gstats; i += blockDim.x) sc.gstats[i] = 0;
+        for (uint32_t i = threadIdx.x; i < sc.n_flags; i += blockDim.x) sc.flags[i] = 0;
+        for (uint32_t i = threadIdx.x; i < sc.n_extra; i += blockDim.x) sc.extra[i] = 0;
+    }
+}
+
+// level 1 of a call over received pieces: nothing to compute, only the clears and level 2's
+// geometry (bp_level2c reads the pieces where they landed)
+hipError_t bp_level1_recv(kmp_postings* ws, const unsigned long long* krecv, uint64_t kcap, uint32_t parts,
+                          const Layout& lay, uint64_t slots, hipStream_t st) {
+    const BpDigits dg = bp_digits(lay);
+    const SplitGeom sg = split_geom(lay, slots, parts);
+    const uint32_t nb = 1u << lay.bbits;
+    hipError_t e = ws->cur.reserve(nb);
+    if (e != hipSuccess) return e;
+    StepClear sc{};
+    if (ws->defer_clear) {
+        sc = StepClear{ws->flags.p, kFlN, ws->bstats.p, kShards * 10, ws->clear_extra, ws->clear_n};
+        ws->defer_clear = false;
+    }
+    split_recv_clear_kernel<<<std::min<uint32_t>((nb + 255) / 256, 1024), 256, 0, st>>>(ws->cur.p, nb, sc);
+    ws->bp_local = true;
+    ws->bp_G = parts * sg.cm;
+    ws->bp_T = std::min<uint32_t>(kBpGatherMax, std::max<uint32_t>(1, kBpGatherTile * 7 / 4 * dg.nb1 / kKeyChunk));
+    ws->bp_hsb = 0;
+    ws->bp_hsc = sg.rowlen;
+    ws->l1_in = krecv;
+    ws->l2_tab = reinterpret_cast<const uint32_t*>(krecv);
+    ws->l2_rt = RecvTab{sg.cm, sg.n_chunks, parts, 2 * kcap};
+    return hipGetLastError();
 }

@@ -558,8 +558,9 @@ struct StepClear {
     unsigned long long* extra;
     uint32_t n_extra;
 };
+// (chunk range [c_lo, c_hi) only, at desc[c - c_lo]: a rank of the k-mer split keys its own chunks)
 __global__ void chunk_desc_kernel(const uint64_t* __restrict__ res_off, uint32_t n, uint64_t slots,
-                                  uint32_t n_chunks, int k, uint4* __restrict__ desc, uint32_t* __restrict__ cur,
+                                  uint32_t c_lo, uint32_t c_hi, int k, uint4* __restrict__ desc, uint32_t* __restrict__ cur,
                                   uint32_t ncur, StepClear sc) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     for (uint32_t i = t; i < ncur; i += gridDim.x * blockDim.x) cur[i] = 0;
@@ -572,18 +573,49 @@ __global__ void chunk_desc_kernel(const uint64_t* __restrict__ res_off, uint32_t
     if (p > n) return;
     const uint64_t off = res_off[p], L = p < n ? res_off[p + 1] - off : 0;
     const uint64_t b = set_base(off, p), e = p < n ? set_base(res_off[p + 1], p + 1) : slots;
-    for (uint64_t c = (b + kKeyChunk - 1) / kKeyChunk; c * kKeyChunk < e && c < n_chunks; ++c) {
-        desc[c].x = p;
-        desc[c].z = (uint32_t)(off + min<uint64_t>(c * kKeyChunk - b, L));
+    for (uint64_t c = max<uint64_t>((b + kKeyChunk - 1) / kKeyChunk, c_lo); c * kKeyChunk < e && c < c_hi; ++c) {
+        desc[c - c_lo].x = p;
+        desc[c - c_lo].z = (uint32_t)(off + min<uint64_t>(c * kKeyChunk - b, L));
     }
     // chunks whose last slot min((c + 1) * kKeyChunk, slots) - 1 lies in [b, e)
-    for (uint64_t c = b / kKeyChunk; c < n_chunks; ++c) {
+    for (uint64_t c = max<uint64_t>(b / kKeyChunk, c_lo); c < c_hi; ++c) {
         const uint64_t c1 = min<uint64_t>((c + 1) * kKeyChunk, slots);
         if (c1 - 1 >= e) break;
         if (c1 - 1 < b) continue;
-        desc[c].y = p;
-        desc[c].w = (uint32_t)(p < n ? off + min<uint64_t>(L, c1 - b + k - 1) : off);
+        desc[c - c_lo].y = p;
+        desc[c - c_lo].w = (uint32_t)(p < n ? off + min<uint64_t>(L, c1 - b + k - 1) : off);
     }
+}
+
+// The k-mer split with a sharded start (kmp_dev_split_keys): rank `part` holds the residues of its
+// chunk range only, keys those chunks with the level-1 kernel below, and sends each chunk's keys
+// of rank d's coarse bins (one contiguous digit-major piece of the ranked chunk) to region d of
+// the send buffer; the all-to-all of the send buffers hands every rank the keys of its bins from
+// every chunk, and its level 2 reads them where they landed (bp_scatter2g<.., kRecv>).
+// Region d (cap u64 words): a run table of cm rows (the most chunks a rank holds), row i =
+// {chunk i's piece: its u64 index in the RECEIVER's buffer (the sender is source `part`, whose
+// region lands at part * cap) | start << 16 | count of each of d's bins, relative to it}, then the
+// pieces, in kSendShards sub-regions of sub keys (chunk c's piece goes to sub-region c mod
+// kSendShards, reserved on a cursor per (destination, sub-region): the fill of each sub-region
+// depends on the chunks only, never on the order of the atomics).  A piece that does not fit is
+// dropped with its counts (0) and raises kFlSend; the cursors still count it, so the rerun's
+// region size is exact.
+constexpr uint32_t kSendShards = 16;
+struct SendL1 {
+    unsigned long long* send;  // parts regions of cap u64 words
+    uint64_t cap, tb;          // region size; run-table words (u64) at its start
+    uint32_t sub;              // keys per sub-region
+    uint32_t* kcur;            // parts x kSendShards cursors
+    uint32_t part, parts, c_lo, rowlen;  // rowlen: u32 words per table row (most bins a rank owns + 1)
+    uint64_t res_base, res_end;  // the residue slice [res_base, res_end) at res
+};
+// coarse bins [bin_lo(d), bin_lo(d + 1)) belong to rank d (the k-mer split's share), and bin t to
+// owner(t) = the largest d with bin_lo(d) <= t
+__host__ __device__ __forceinline__ uint32_t split_bin_lo(uint32_t d, uint32_t nb1, uint32_t parts) {
+    return (uint32_t)((uint64_t)d * nb1 / parts);
+}
+__device__ __forceinline__ uint32_t split_owner(uint32_t t, uint32_t nb1, uint32_t parts) {
+    return (uint32_t)(((uint64_t)(t + 1) * parts - 1) / nb1);
 }
 
 // waves per SIMD the persistent level 1 is compiled for (VGPR budget: 8 -> 64 registers and 24 B of
@@ -599,12 +631,16 @@ __global__ void chunk_desc_kernel(const uint64_t* __restrict__ res_off, uint32_t
 // written (its descriptor one chunk earlier still), so the three dependent global round trips of
 // a chunk (descriptor, protein offsets, residues) stay off the critical path: the one-chunk-per-
 // workgroup kernel spent ~13 us per chunk waiting on them.
-template <uint32_t kThr>
+// kSend (the k-mer split's sharded start): the chunks are [sl.c_lo, sl.c_lo + G) of the batch (desc
+// and the loop count them from 0), the residues a slice (SendL1.res_base / res_end), every digit is
+// ranked and each rank's piece goes to the send buffer with its run-table row (SendL1 above)
+// instead of the segment + H1.
+template <uint32_t kThr, bool kSend>
 __global__ __launch_bounds__(kThr, KMP_L1P_WAVES) void bp_scatter1p_kernel(
     const uint8_t* __restrict__ res, const uint64_t* __restrict__ res_off, const uint16_t* __restrict__ cls, int k,
     uint32_t n, uint64_t slots, uint32_t G, const uint4* __restrict__ desc, Layout lay, BpDigits dg, uint32_t pw21,
     uint32_t dlo, uint32_t dhi, uint32_t* __restrict__ H1, unsigned long long* __restrict__ out,
-    uint32_t* __restrict__ flags) {
+    uint32_t* __restrict__ flags, SendL1 sl) {
     __shared__ union {
         KeyChunk kc;
         unsigned long long S[kKeyChunk];
@@ -619,8 +655,9 @@ __global__ __launch_bounds__(kThr, KMP_L1P_WAVES) void bp_scatter1p_kernel(
     if (c >= G) return;
     for (uint32_t i = tid; i < 256; i += kThr) lut[i] = c_lut.v[i];
     __syncthreads();  // the table before the first staging reads it
-    const uint64_t res_end = res_off[n];
-    const bool vec_ok = ((uintptr_t)res & 15u) == 0;
+    // residue i (absolute) is res[i - rb]: the whole batch, or (kSend) a slice starting at rb
+    const uint64_t rb = kSend ? sl.res_base : 0ull, res_end = kSend ? sl.res_end : res_off[n];
+    const bool vec_ok = ((uintptr_t)res & 15u) == 0 && (rb & 15u) == 0;
     // one chunk's loads, held in registers until it is staged
     uint4 pv = make_uint4(0, 0, 0, 0);
     uint32_t po[kPP], pe[kPP];  // residue offsets (< 2^32: bp_level1 checks slots)
@@ -637,7 +674,7 @@ __global__ __launch_bounds__(kThr, KMP_L1P_WAVES) void bp_scatter1p_kernel(
         if (tid < nv) {
             const uint64_t g = a0 + 16ull * tid;
             if (vec_ok && g + 16 <= res_end) {
-                pv = *reinterpret_cast<const uint4*>(res + g);
+                pv = *reinterpret_cast<const uint4*>(res + (g - rb));
             } else {
                 uint32_t w[4];
 #pragma unroll
@@ -646,7 +683,7 @@ __global__ __launch_bounds__(kThr, KMP_L1P_WAVES) void bp_scatter1p_kernel(
 #pragma unroll
                     for (int bb = 0; bb < 4; ++bb) {
                         const uint64_t i = g + 4 * q + bb;
-                        w[q] |= (uint32_t)(i < res_end ? res[i] : 0) << (8 * bb);
+                        w[q] |= (uint32_t)(i >= rb && i < res_end ? res[i - rb] : 0) << (8 * bb);
                     }
                 }
                 pv = make_uint4(w[0], w[1], w[2], w[3]);
@@ -666,8 +703,10 @@ __global__ __launch_bounds__(kThr, KMP_L1P_WAVES) void bp_scatter1p_kernel(
     uint4 dnxt = c + gridDim.x < G ? desc[c + gridDim.x] : make_uint4(0, 0, 0, 0);
     issue(dcur);
     const unsigned hs1 = dg.sh1 - lay.hshift;
+    __shared__ uint32_t sd_base[kSend ? kSplitMax : 1], sd_start[kSend ? kSplitMax : 1];
     while (true) {
-        const uint64_t c0 = (uint64_t)c * kKeyChunk, c1 = min(c0 + kKeyChunk, slots);
+        const uint32_t gc = kSend ? c + sl.c_lo : c;  // the chunk's index in the batch
+        const uint64_t c0 = (uint64_t)gc * kKeyChunk, c1 = min(c0 + kKeyChunk, slots);
         // ---- stage chunk c from the registers ----
         {
             uint64_t a0;
@@ -729,23 +768,63 @@ __global__ __launch_bounds__(kThr, KMP_L1P_WAVES) void bp_scatter1p_kernel(
             cnt[t] = d < nown ? lh[dlo + d] : 0u;
         }
         lds_bins_scan<kThr>(lh + dlo, nown, wave_tot);
-        uint32_t* row = H1 + (uint64_t)c * nown;
+        if (!kSend) {
+            uint32_t* row = H1 + (uint64_t)c * nown;
 #pragma unroll
-        for (uint32_t t = 0; t < kQ; ++t) {
-            const uint32_t d = tid + t * kThr;
-            if (d < nown) row[d] = lh[dlo + d] << 16 | cnt[t];
+            for (uint32_t t = 0; t < kQ; ++t) {
+                const uint32_t d = tid + t * kThr;
+                if (d < nown) row[d] = lh[dlo + d] << 16 | cnt[t];
+            }
         }
 #pragma unroll
         for (uint32_t e = 0; e < kPer; ++e)
             if (x[e] != kNoKey) u.S[lh[(uint32_t)(x[e] >> dg.sh1)] + r[e]] = x[e];
         __syncthreads();
         const uint32_t n_in = s_n;
-        unsigned long long* seg = out + c0;  // c0 = chunk * kKeyChunk: 16-byte aligned
-        for (uint32_t i = 2 * tid; i < n_in; i += 2 * kThr) {
-            if (i + 1 < n_in)
-                *reinterpret_cast<ulonglong2*>(seg + i) = *reinterpret_cast<const ulonglong2*>(u.S + i);
-            else
-                seg[i] = u.S[i];
+        if (kSend) {
+            // every digit is the call's (dlo = 0, dhi = nb1): rank d's piece is the chunk's keys of
+            // its bins, contiguous in S; one reservation per destination
+            const uint32_t nb1 = dg.nb1;
+            if (tid < sl.parts) {
+                const uint32_t b0 = split_bin_lo(tid, nb1, sl.parts), b1 = split_bin_lo(tid + 1, nb1, sl.parts);
+                const uint32_t s0 = b0 < nb1 ? lh[b0] : n_in, s1 = b1 < nb1 ? lh[b1] : n_in;
+                const uint32_t size = s1 - s0, shard = gc % kSendShards;
+                const uint32_t pos = size ? atomicAdd(&sl.kcur[tid * kSendShards + shard], size) : 0u;
+                const bool fits = pos + size <= sl.sub;
+                if (!fits) flags[kFlSend] = 1;
+                sd_base[tid] = fits && sl.sub ? shard * sl.sub + pos : 0xFFFFFFFFu;
+                sd_start[tid] = s0;
+                // the row's first word: where the piece lands in the receiver's buffer (sub = 0: the
+                // region cannot even hold the run table — nothing is written, the cursors count)
+                if (sl.sub)
+                    reinterpret_cast<uint32_t*>(sl.send + (uint64_t)tid * sl.cap)[(uint64_t)c * sl.rowlen] =
+                        fits ? (uint32_t)((uint64_t)sl.part * sl.cap + sl.tb + shard * sl.sub + pos) : 0u;
+            }
+            __syncthreads();
+#pragma unroll
+            for (uint32_t t = 0; t < kQ; ++t) {
+                const uint32_t dgt = tid + t * kThr;
+                if (dgt < nb1 && sl.sub) {
+                    const uint32_t d = split_owner(dgt, nb1, sl.parts);
+                    const bool fits = sd_base[d] != 0xFFFFFFFFu;
+                    uint32_t* row = reinterpret_cast<uint32_t*>(sl.send + (uint64_t)d * sl.cap) + (uint64_t)c * sl.rowlen;
+                    row[1 + dgt - split_bin_lo(d, nb1, sl.parts)] = fits ? (lh[dgt] - sd_start[d]) << 16 | cnt[t] : 0u;
+                }
+            }
+            for (uint32_t i = tid; i < n_in; i += kThr) {
+                const unsigned long long y = u.S[i];
+                const uint32_t d = split_owner((uint32_t)(y >> dg.sh1), nb1, sl.parts);
+                const uint32_t b = sd_base[d];
+                if (b != 0xFFFFFFFFu) sl.send[(uint64_t)d * sl.cap + sl.tb + b + (i - sd_start[d])] = y;
+            }
+        } else {
+            unsigned long long* seg = out + c0;  // c0 = chunk * kKeyChunk: 16-byte aligned
+            for (uint32_t i = 2 * tid; i < n_in; i += 2 * kThr) {
+                if (i + 1 < n_in)
+                    *reinterpret_cast<ulonglong2*>(seg + i) = *reinterpret_cast<const ulonglong2*>(u.S + i);
+                else
+                    seg[i] = u.S[i];
+            }
         }
         if (cn >= G) break;
         __syncthreads();  // S read before the next chunk's staging overwrites it
@@ -782,7 +861,17 @@ __global__ __launch_bounds__(256) void bp_h1t_kernel(const uint32_t* __restrict_
 // takes the tiles [x * per, (x + 1) * per) of the bin-major tile list, so neighbouring bins' tiles
 // of a chunk range (whose runs share the 128-B lines at their ends) run on one L2 at about the
 // same time.
-template <uint32_t kPer, uint32_t kThr, bool kVreg>
+// kRecv (the k-mer split's sharded start): the runs are the received pieces — chunk row g of the
+// G = parts * cm rows is row g mod cm of source g / cm's region (stride u32 words apart), rows past
+// that source's chunk count are empty, and each row starts with the u64 index its runs are
+// relative to (SendL1)
+struct RecvTab {
+    uint32_t cm;         // rows per source region (the most chunks a rank holds)
+    uint32_t n_chunks;   // chunks of the batch (source s holds [s C / parts, (s + 1) C / parts))
+    uint32_t parts;
+    uint64_t stride;     // u32 words between source regions (2 x the region's u64 words)
+};
+template <uint32_t kPer, uint32_t kThr, bool kVreg, bool kRecv>
 __global__ __launch_bounds__(kThr) void bp_scatter2g_kernel(const unsigned long long* __restrict__ in,
                                                                    const uint32_t* __restrict__ H1T, uint32_t G,
                                                                    uint32_t hsb, uint32_t hsc,
@@ -791,7 +880,7 @@ __global__ __launch_bounds__(kThr) void bp_scatter2g_kernel(const unsigned long 
                                                                    uint32_t* __restrict__ bcur,
                                                                    unsigned long long* __restrict__ out,
                                                                    uint32_t* __restrict__ flags, uint32_t c0,
-                                                                   uint32_t dlo) {
+                                                                   uint32_t dlo, RecvTab rt) {
     constexpr uint32_t kTile = kPer * kThr;
     __shared__ __attribute__((aligned(16))) unsigned long long S[kTile];
     __shared__ uint32_t lh[kBpMaxBins];
@@ -810,10 +899,21 @@ __global__ __launch_bounds__(kThr) void bp_scatter2g_kernel(const unsigned long 
     const uint32_t nch = min(T, G - ch0);
     const uint32_t* row = H1T + (uint64_t)(c - dlo) * hsb + (uint64_t)ch0 * hsc;
     const uint32_t q = (nch + kThr - 1) / kThr, b0 = threadIdx.x * q;
-    uint32_t p[kQ], v = 0;
+    uint32_t p[kQ], rbase[kRecv ? kQ : 1], v = 0;
 #pragma unroll
     for (uint32_t t = 0; t < kQ; ++t) {
-        p[t] = t < q && b0 + t < nch ? row[(uint64_t)(b0 + t) * hsc] : 0u;
+        if (kRecv) {
+            const uint32_t g = ch0 + b0 + t, s = g / rt.cm, i = g - s * rt.cm;
+            const uint32_t nsrc = s < rt.parts ? (uint32_t)((uint64_t)(s + 1) * rt.n_chunks / rt.parts -
+                                                            (uint64_t)s * rt.n_chunks / rt.parts)
+                                               : 0u;
+            const bool ok = t < q && b0 + t < nch && i < nsrc;
+            const uint32_t* rw = H1T + s * rt.stride + (uint64_t)i * hsc;
+            p[t] = ok ? rw[1 + c - dlo] : 0u;
+            rbase[t] = ok ? rw[0] : 0u;
+        } else {
+            p[t] = t < q && b0 + t < nch ? row[(uint64_t)(b0 + t) * hsc] : 0u;
+        }
         v += p[t] & 0xFFFFu;
     }
     uint32_t excl0, tn;
@@ -831,7 +931,7 @@ __global__ __launch_bounds__(kThr) void bp_scatter2g_kernel(const unsigned long 
 #pragma unroll
         for (uint32_t t = 0; t < kQ; ++t)
             if (t < q && b0 + t < nch) {
-                src[b0 + t] = (ch0 + b0 + t) * kKeyChunk + (p[t] >> 16) - excl;
+                src[b0 + t] = (kRecv ? rbase[t] : (ch0 + b0 + t) * kKeyChunk) + (p[t] >> 16) - excl;
                 excl += p[t] & 0xFFFFu;
             }
         // key -> run map of the round's window [base, base + n_in)

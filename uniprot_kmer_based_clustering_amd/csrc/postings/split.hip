@@ -60,13 +60,15 @@ __global__ __launch_bounds__(kRtThreads) void split_route_kernel(const unsigned 
 // also writes the rank's flags (KMP_SPLIT_*) and statistics (kSt* order, summed over the shards)
 // routed (the bucket kernels wrote the send regions themselves, kShards sub-regions of cap / kShards
 // keys per destination, the buffer pre-filled with kNoKey): no padding; the part size reported is
-// kShards x the fullest sub-region, so a grown cap gives every sub-region its need
+// kShards x the fullest sub-region, so a grown cap gives every sub-region its need.  merge: the keys
+// phase of the same step (kmp_dev_split_keys) wrote its flags first: RERUN and CLASS are or-ed,
+// MAX_KEYS kept
 __global__ void split_pad_finish_kernel(unsigned long long* __restrict__ send, uint64_t cap,
                                         const unsigned long long* __restrict__ dcursor,
                                         const unsigned long long* __restrict__ gstats,
                                         const uint32_t* __restrict__ wflags, uint64_t sc, uint32_t parts,
                                         uint32_t* __restrict__ out, unsigned long long* __restrict__ stats,
-                                        int heavy_done, int routed) {
+                                        int heavy_done, int routed, int merge) {
     const uint32_t d = blockIdx.y;
     if (!routed)
         for (uint64_t i = dcursor[d] + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap;
@@ -111,13 +113,38 @@ __global__ void split_pad_finish_kernel(unsigned long long* __restrict__ send, u
             part = max(part, s_red[2][w]);
         }
         const uint32_t clamp = 0xFFFFFFFFu;
-        out[KMP_SPLIT_CLASS] = wflags[kFlClass];
+        const uint32_t k_rerun = merge ? out[KMP_SPLIT_RERUN] : 0u, k_class = merge ? out[KMP_SPLIT_CLASS] : 0u;
+        const uint32_t k_keys = merge ? out[KMP_SPLIT_MAX_KEYS] : 0u;
+        out[KMP_SPLIT_CLASS] = wflags[kFlClass] | k_class;
         out[KMP_SPLIT_HEAVY] = spill != 0 && !heavy_done;  // spilled with the heavy path off: rerun with it on
         out[KMP_SPLIT_MAX_PART] = (uint32_t)min<unsigned long long>(part, clamp);
         out[KMP_SPLIT_MAX_SHARD] = (uint32_t)min<unsigned long long>(shard, clamp);
         out[KMP_SPLIT_BIN_TILES] = wflags[kFlBin] ? wflags[kFlBinTiles] : 0u;
         out[KMP_SPLIT_CURSOR] = wflags[kFlCur];
-        out[KMP_SPLIT_RERUN] = (part > cap || shard > sc || wflags[kFlBin] || wflags[kFlCur]) ? 1u : 0u;
+        out[KMP_SPLIT_RERUN] = (part > cap || shard > sc || wflags[kFlBin] || wflags[kFlCur] || k_rerun) ? 1u : 0u;
         for (uint32_t i = KMP_SPLIT_CURSOR + 1; i < KMP_SPLIT_FLAGS; ++i) out[i] = 0;
+        out[KMP_SPLIT_MAX_KEYS] = k_keys;
+    }
+}
+
+// the keys phase's flags (kmp_dev_split_keys): RERUN when a piece did not fit its sub-region,
+// CLASS from the keying, MAX_KEYS = the region size that fits every sub-region (the cursors count
+// every piece, dropped or not); the other words zero
+__global__ void split_keys_finish_kernel(const uint32_t* __restrict__ kcur, uint32_t nkc,
+                                         const uint32_t* __restrict__ wflags, uint64_t tb,
+                                         uint32_t* __restrict__ out) {
+    __shared__ uint32_t s_max[256 / 64];
+    const uint32_t t = threadIdx.x;
+    uint32_t m = 0;
+    for (uint32_t i = t; i < nkc; i += blockDim.x) m = max(m, kcur[i]);
+    m = wave_max(m);
+    if ((t & 63) == 0) s_max[t >> 6] = m;
+    __syncthreads();
+    if (t == 0) {
+        for (uint32_t w = 0; w < (blockDim.x + 63) / 64; ++w) m = max(m, s_max[w]);
+        for (uint32_t i = 0; i < KMP_SPLIT_FLAGS; ++i) out[i] = 0;
+        out[KMP_SPLIT_RERUN] = wflags[kFlSend];
+        out[KMP_SPLIT_CLASS] = wflags[kFlClass];
+        out[KMP_SPLIT_MAX_KEYS] = (uint32_t)min<unsigned long long>(tb + (unsigned long long)kSendShards * m, 0xFFFFFFFFull);
     }
 }

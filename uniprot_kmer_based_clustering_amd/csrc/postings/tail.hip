@@ -1198,37 +1198,40 @@ __global__ __launch_bounds__(kFtThreads) void pt_reduce_fast_kernel(const uint32
                                                                     uint32_t stride, PtPack pack,
                                                                     uint32_t* __restrict__ runs) {
     __shared__ FtLds u;
-    __shared__ uint32_t s_r;
+    __shared__ uint32_t s_r, s_n;
     const uint32_t tid = threadIdx.x;
+    const unsigned pb = g.pbits;
+    const uint32_t R = 1u << g.rbits;
     // the row block = the look-back position = the order the workgroups started in (a ticket), so
     // every block a look-back polls is resident or done, whatever the dispatch order across XCDs and
-    // whatever other kernels share the device
-    if (tid == 0) s_r = atomicAdd(ticket, 1u);
+    // whatever other kernels share the device.  One thread takes it, reads and re-zeroes the block's
+    // cursor while the others clear the hash table (used only when the block is small enough: a
+    // sort-path block overwrites it)
+    if (tid == 0) {
+        const uint32_t r0 = atomicAdd(ticket, 1u);
+        s_r = r0;
+        s_n = fcur[r0];
+        fcur[r0] = 0;  // for the next call
+        u.s_max = u.s_flag = 0;
+    }
+    for (uint32_t i = tid; i < kFtSlots; i += kFtThreads) u.h.K[i] = kFtEmpty;
+    for (uint32_t i = tid; i < kFtSlots / 2; i += kFtThreads) reinterpret_cast<uint32_t*>(u.h.C)[i] = 0;
+    for (uint32_t i = tid; i <= R; i += kFtThreads) u.RC[i] = 0;
     __syncthreads();
-    const uint32_t r = s_r;
-    const uint32_t nraw = fcur[r];
-    __syncthreads();  // every thread has its count before the cursor is cleared for the next call
-    if (tid == 0) fcur[r] = 0;
+    const uint32_t r = s_r, nraw = s_n;
     const bool ovf = nraw > kFtCap;
     const uint32_t n = ovf ? 0u : nraw;
     const uint32_t* src = keys + (uint64_t)r * kFtCap;  // g.ftcap == kFtCap in this mode
-    const unsigned pb = g.pbits;
-    const uint32_t R = 1u << g.rbits;
     uint32_t D = 0;  // the block's kept pairs
     bool sort = n > kFtHashMax, published = false;
     if (!sort) {
-        // ---- hash aggregation: pair -> slot, count per slot ----
-        for (uint32_t i = tid; i < kFtSlots; i += kFtThreads) u.h.K[i] = kFtEmpty;
-        for (uint32_t i = tid; i < kFtSlots / 2; i += kFtThreads) reinterpret_cast<uint32_t*>(u.h.C)[i] = 0;
-        for (uint32_t i = tid; i <= R; i += kFtThreads) u.RC[i] = 0;
-        if (tid == 0) u.s_max = u.s_flag = 0;
+        // ---- hash aggregation: pair -> slot, count per slot (the table was cleared above) ----
         uint32_t x[12];
 #pragma unroll
         for (uint32_t e = 0; e < 12; ++e) {
             const uint32_t i = tid + e * kFtThreads;
             x[e] = i < n ? src[i] : kFtEmpty;
         }
-        __syncthreads();
 #pragma unroll
         for (uint32_t e = 0; e < 12; ++e) {
             if (x[e] == kFtEmpty) continue;

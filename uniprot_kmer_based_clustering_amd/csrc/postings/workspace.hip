@@ -70,6 +70,12 @@ struct kmp_postings {
     // coarse bins [bin_lo, bin_hi) of this call (bin_hi 0: all): the bucket-range share of a rank
     // of the multi-GPU k-mer split (kmp_dev_split_expand); level 1 keeps only their keys
     uint32_t bin_lo = 0, bin_hi = 0;
+    // level 2 over received pieces (the k-mer split's sharded start, kmp_dev_split_group): the
+    // receive buffer (keys) and its run tables; nullptr: level 1's own output (ws->keys, ws->bp)
+    const unsigned long long* l1_in = nullptr;
+    const uint32_t* l2_tab = nullptr;
+    RecvTab l2_rt{};
+    Grow<uint32_t> split_kcur;  // the key pieces' send cursors (parts x kSendShards)
     // cursor level 2 (fixed-capacity bucket regions, no counting passes): tried first for a new
     // shape (cur_on), dropped for the shape after a region overflow; cur_used: the buckets in
     // ws->sorted came from it (ws->cur: bucket counts)
@@ -120,7 +126,7 @@ struct kmp_postings {
             key.clear();
             seen.clear();
         }
-    } split_g[2];  // the k-mer split's phases (expand, edges)
+    } split_g[3];  // the k-mer split's phases (expand or group, edges, keys)
     hipGraphExec_t gexec = nullptr;
     hipStream_t cst = nullptr;  // capture stream
     std::vector<unsigned long long> gkey, gkey_seen;
@@ -136,7 +142,7 @@ struct kmp_postings {
                         &hGS, &htc, &htoff, &hoff, &hRH, &hseg, &hcur, &ovk, &ovx, &split_cur})
             g->release();
         for (auto* g : {&w, &keep, &pos, &small, &cnt, &flags, &chunk_first, &chunk_desc, &bp, &pt, &ovf, &ovr, &ova, &stg2, &k2, &dsc, &hE, &hgi, &hcnt,
-                        &hrun, &hblk, &cur, &hGH})
+                        &hrun, &hblk, &cur, &hGH, &split_kcur})
             g->release();
         tmp.release();
         for (auto& e : ev)

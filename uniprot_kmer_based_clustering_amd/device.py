@@ -88,8 +88,116 @@ def order_xcd(items: np.ndarray) -> np.ndarray:
     return out[:n.value]
 
 
-class DevicePipeline:
+class _SplitEdges:
+    """The stages the two multi-GPU pipelines share: the workspace, the edge arrays and the k-mer
+    split's edges phase (kmp_dev_split_edges)."""
 
+    def _workspace(self):
+        if self._postings is None:
+            ws = C.c_void_p()
+            check(lib().kmp_postings_create(C.byref(ws)), "kmp_postings_create")
+            self._postings = ws
+        return self._postings
+
+    def _alloc_edges(self, cap):
+        self.edge_cap = cap
+        self.ep = torch.empty(cap, dtype=torch.int32, device=self.dev)
+        self.eq = torch.empty(cap, dtype=torch.int32, device=self.dev)
+        self.ew = torch.empty(cap, dtype=torch.int32, device=self.dev)
+
+    def split_edges(self, recv: torch.Tensor, row_lo: int, row_hi: int, min_shared: int = 1) -> int:
+        """Multi-GPU k-mer split, last phase (kmp_dev_split_edges): the received pair keys -> the
+        canonical edges of rows [row_lo, row_hi) in ep/eq/ew (syncs)."""
+        for _ in range(2):
+            ne = C.c_uint64()
+            st = lib().kmp_dev_split_edges(self._workspace(), _p(recv), recv.numel(), self.n, row_lo, row_hi,
+                                           min_shared, _p(self.ep), _p(self.eq), _p(self.ew), self.edge_cap,
+                                           C.byref(ne), _stream())
+            if st == _lib.KMP_EOVERFLOW:
+                self._alloc_edges(ne.value + ne.value // 8 + 1024)
+                continue
+            check(st, "kmp_dev_split_edges")
+            self.n_edges = ne.value
+            return self.n_edges
+        raise RuntimeError("edge count unstable across reruns")
+
+    def edges(self):
+        n = self.n_edges
+        return (self.ep[:n].cpu().numpy().view(np.uint32), self.eq[:n].cpu().numpy().view(np.uint32),
+                self.ew[:n].cpu().numpy().view(np.uint32))
+
+    def __del__(self):
+        if getattr(self, "_postings", None) is not None:
+            try:
+                lib().kmp_postings_destroy(self._postings)
+            except Exception:
+                pass
+            self._postings = None
+
+
+class ShardPipeline(_SplitEdges):
+    """One rank of the multi-GPU k-mer split with a SHARDED START: this GPU
+    holds the batch's offsets and class ids (metadata: 10 B per protein) and only the residues its
+    own 4,096-slot chunks read (kmp_split_plan: about 1/parts of the packed residues).  A step:
+      split_keys    the rank's windows keyed once, each key sent toward the rank owning its coarse
+                    bin (no rank keys another rank's windows);
+      (all-to-all of the key regions over RCCL)
+      split_group   the received keys of the rank's bins grouped and expanded, pair keys routed to
+                    their row owners;
+      (all-to-all of the pair keys, max-reduce of the flags)
+      split_edges   the rank's rows reduced to canonical edges.
+    `residues` is a host copy of the packed batch (the bench generates it whole); only the rank's
+    slice is copied to the device."""
+
+    def __init__(self, residues: np.ndarray, offsets: np.ndarray, class_id: np.ndarray, k: int, part: int,
+                 parts: int, device: torch.device | str = "cuda", edge_cap: int | None = None):
+        self.k = k
+        self.part, self.parts = part, parts
+        self.dev = torch.device(device)
+        self.offsets_host = np.ascontiguousarray(offsets, dtype=np.uint64)
+        self.n = len(self.offsets_host) - 1
+        self.total = int(self.offsets_host[-1])
+        self.span = _lib.split_plan(self.offsets_host, k, part, parts)
+        lo, hi = int(self.span.res_lo), int(self.span.res_hi)
+        self.res_lo, self.res_hi = lo, hi
+        sl = np.ascontiguousarray(np.asarray(residues, dtype=np.uint8)[lo:hi])
+        self.res = torch.from_numpy(sl if sl.size else np.zeros(16, dtype=np.uint8)).to(self.dev)
+        self.off = torch.from_numpy(self.offsets_host.view(np.int64)).to(self.dev)
+        cls = np.ascontiguousarray(class_id, dtype=np.uint16)
+        self.cls = torch.from_numpy((cls if cls.size else np.zeros(1, np.uint16)).view(np.int16)).to(self.dev)
+        self._postings = None
+        self._alloc_edges(edge_cap or max(1 << 20, 4 * self.n // max(1, parts)))
+        self.n_edges = 0
+
+    def split_keys(self, part: int, parts: int, kcap: int, ksend: torch.Tensor, flags: torch.Tensor) -> None:
+        """kmp_dev_split_keys: this rank's windows keyed, region d of ksend (kcap int64 words) bound
+        for rank d; flags (int32[KMP_SPLIT_FLAGS]) on the stream.  No host synchronisation."""
+        assert (part, parts) == (self.part, self.parts), "the slice was planned for another split"
+        check(lib().kmp_dev_split_keys(self._workspace(), _p(self.res), self.res_lo, self.res_hi, _p(self.off),
+                                       _p(self.cls), self.n, self.k, int(self.span.slots), part, parts, kcap,
+                                       _p(ksend), _p(flags), _stream()), "kmp_dev_split_keys")
+
+    def split_group(self, krecv: torch.Tensor, kcap: int, part: int, parts: int, cap: int, send: torch.Tensor,
+                    flags: torch.Tensor, stats: torch.Tensor, learn=None, require_class_diff: bool = True,
+                    heavy_df: int = 0xFFFFFFFF) -> None:
+        """kmp_dev_split_group: the received keys (parts regions of kcap words) of this rank's bins
+        grouped and expanded, pair keys routed to their row owners in `send` (parts regions of cap);
+        its flags merged into `flags` (the keys phase's, same step), stats (int64[8])."""
+        lp = None if learn is None else (C.c_uint32 * _lib.KMP_SPLIT_FLAGS)(*[int(x) for x in learn])
+        check(lib().kmp_dev_split_group(self._workspace(), _p(krecv), kcap, self.n, self.k, int(self.span.slots),
+                                        heavy_df, int(require_class_diff), part, parts, cap, lp, _p(send),
+                                        _p(flags), _p(stats), _stream()), "kmp_dev_split_group")
+
+    def own_residues(self):
+        """(lo, hi, tensor): the residues this rank contributes when the batch is rebuilt on every
+        rank (the row-split fallback): [res_lo, the next rank's res_lo) within its slice."""
+        nxt = (_lib.split_plan(self.offsets_host, self.k, self.part + 1, self.parts).res_lo
+               if self.part + 1 < self.parts else self.total)
+        hi = max(self.res_lo, min(int(nxt), self.res_hi))
+        return self.res_lo, hi, self.res[:hi - self.res_lo]
+
+
+class DevicePipeline(_SplitEdges):
     def __init__(self, proteins: Proteins, k: int, device: torch.device | str = "cuda",
                  edge_cap: int | None = None):
         self.k = k
@@ -126,12 +234,6 @@ class DevicePipeline:
         self.long_rank = None
         self._postings = None
         self.postings_stats = _lib.PostingsStats()
-
-    def _alloc_edges(self, cap):
-        self.edge_cap = cap
-        self.ep = torch.empty(cap, dtype=torch.int32, device=self.dev)
-        self.eq = torch.empty(cap, dtype=torch.int32, device=self.dev)
-        self.ew = torch.empty(cap, dtype=torch.int32, device=self.dev)
 
     # -- stages ---------------------------------------------------------------------
     def build_sets(self, lo: int = 0, hi: int | None = None) -> None:
@@ -203,13 +305,6 @@ class DevicePipeline:
             self._sort_tmp = torch.empty(nbytes + 256, dtype=torch.uint8, device=self.dev)
         check(L.kmp_dev_sort_edges(_p(self.ep), _p(self.eq), _p(self.ew), n, self.n, _p(self._sort_tmp),
                                    self._sort_tmp.numel(), _stream()), "kmp_dev_sort_edges")
-
-    def _workspace(self):
-        if self._postings is None:
-            ws = C.c_void_p()
-            check(lib().kmp_postings_create(C.byref(ws)), "kmp_postings_create")
-            self._postings = ws
-        return self._postings
 
     def set_stage_timing(self, enable: bool = True) -> None:
         """Per-stage HIP-event times of the postings engine into postings_stats.stage_ms."""
@@ -302,22 +397,6 @@ class DevicePipeline:
                                          slots, heavy_df, int(require_class_diff), part, parts, cap, lp, _p(send),
                                          _p(flags), _p(stats), _stream()), "kmp_dev_split_expand")
 
-    def split_edges(self, recv: torch.Tensor, row_lo: int, row_hi: int, min_shared: int = 1) -> int:
-        """Multi-GPU k-mer split, phase 2 (kmp_dev_split_edges): the received pair keys -> the
-        canonical edges of rows [row_lo, row_hi) in ep/eq/ew (syncs)."""
-        for _ in range(2):
-            ne = C.c_uint64()
-            st = lib().kmp_dev_split_edges(self._workspace(), _p(recv), recv.numel(), self.n, row_lo, row_hi,
-                                           min_shared, _p(self.ep), _p(self.eq), _p(self.ew), self.edge_cap,
-                                           C.byref(ne), _stream())
-            if st == _lib.KMP_EOVERFLOW:
-                self._alloc_edges(ne.value + ne.value // 8 + 1024)
-                continue
-            check(st, "kmp_dev_split_edges")
-            self.n_edges = ne.value
-            return self.n_edges
-        raise RuntimeError("edge count unstable across reruns")
-
     def postings(self, min_shared: int = 1, require_class_diff: bool = True,
                  heavy_df: int = 0xFFFFFFFF, from_residues: bool = False) -> int:
         """Postings engine: canonical edges into ep/eq/ew (syncs).  Reads the K(p) slots
@@ -369,19 +448,6 @@ class DevicePipeline:
         n = self.pairs(min_shared, require_class_diff)
         self.sort(n)
         return n
-
-    def __del__(self):
-        if getattr(self, "_postings", None) is not None:
-            try:
-                lib().kmp_postings_destroy(self._postings)
-            except Exception:
-                pass
-            self._postings = None
-
-    def edges(self):
-        n = self.n_edges
-        return (self.ep[:n].cpu().numpy().view(np.uint32), self.eq[:n].cpu().numpy().view(np.uint32),
-                self.ew[:n].cpu().numpy().view(np.uint32))
 
     def set_of(self, p: int, repeat_only: bool = False) -> np.ndarray:
         base = int(lib().kmp_set_base(int(self.offsets_host[p]), p))

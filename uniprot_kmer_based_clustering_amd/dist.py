@@ -1,34 +1,37 @@
 """Multi-GPU split of the pair path: one process per GPU, torch.distributed over
-RCCL (``nccl`` backend) — the path used by ``bench.py --gpus N`` under torch.distributed.run.
+RCCL (``nccl`` backend) — the path of ``bench.py --gpus N`` under torch.distributed.run.  The
+reference's own parallelism is a pool of `threads` workers over the same work (main.rs:84-121,
+graph/mod.rs:81-124); here the work is split over GPUs by k-mer and by row.
 
-The pair space is split by ROWS.  A pair (p, q), p < q, belongs to its smaller protein p, and
-rank r owns the rows [start[r], start[r+1]) of ``kmp_row_split`` (equal expected pair counts:
-row p holds about N - p pairs).  Every rank holds the whole packed residue batch (ΣL bytes:
-30 MB at config 3), groups every k-mer itself and expands only its own rows
-(``kmp_dev_pairs_rows``): a k-mer group is never split, so every pair's w is complete on the
-rank that owns it.  There is no exchange in the data path — the ranks' edge lists are disjoint
-and each is already canonical — and rank 0 gathers them in rank order: the concatenation IS the
-canonical list, no final sort (cf. main.rs:84-121 / mod.rs:81-124, the reference's own split of
-the same work over `threads` workers).
+**Default: the k-mer split with a sharded start** (``sharded_split_step`` on a ``ShardPipeline``).
+Rank r holds only the residues of its own 4,096-slot chunks (about 1/G of the packed batch; the
+offsets and class ids are replicated metadata).  One step:
+  1. split_keys: the rank keys its windows once (radix-21 codes, protein.rs:29-37) and ranks them
+     by coarse bin of h(code); the keys of rank d's bins go to region d of the key buffer;
+  2. all-to-all of the key regions (8 B per window: 29 MB per rank at config 4 and G = 8, the same
+     volume an all-gather of the residues would move, but nothing is keyed twice);
+  3. split_group: the received keys of the rank's bins grouped by k-mer and expanded to pair keys
+     (Graph::new + update_graph_edges with the class filter, vertex.rs:59-140, mod.rs:580-587),
+     each routed to the rank owning the pair's row (the smaller protein; ``kmp_row_split`` ranges
+     of equal pair counts);
+  4. all-to-all of the pair keys (8 B per incidence: 42 MB in total at config 4) and a max-reduce
+     of the flags (capacities learned identically on every rank; frequent k-mers turn every rank's
+     heavy path on);
+  5. split_edges: the rank's rows reduced to canonical (p, q, w) (combine_edges, mod.rs:322-546).
+A pair's incidences from every k-mer meet on its row owner, so w is complete there; the rank-order
+concatenation of the ranks' edges is the canonical list, and with ``gather`` rank 0 receives every
+rank's block behind its own (point-to-point) so the timed step ends with the whole list on rank 0.
 
-Why not an all-to-all: sharding the k-mers instead (each rank groups 1/G of them) moves every
-pair key to its row owner — 42 MB per step at config 3, but Σ C(df,2) x 8 B ≈ 10^12 B at
-config 5, far more than recomputing the grouping on each rank (≈ 5·10^8 windows).
+**Fallbacks.**  Class ids wider than the key's class field (every rank sees KMP_SPLIT_CLASS in the
+reduced flags) rebuild the batch on every rank with an all-gather of the residue slices and take
+the row split (``distributed_step``: every rank groups every k-mer and expands only its own rows,
+no exchange in the data path).  ``kmer_split_step`` on a ``DevicePipeline`` is the split with a
+replicated start (every rank holds the whole batch and keys every window, keeping its bins): the
+C ABI's multi-GPU context runs that flow.  Config 5 (bounded-memory row passes) keeps the row split:
+its Σ C(df,2) ≈ 10^10-10^11 pair keys would cross the links, far more than recomputing the grouping.
 
-The gather only moves tensors, so the same code runs on gloo with CPU tensors in the
-multi-process CPU tests (tests/test_dist.py).
-
-The k-mer split (``kmer_split_step``, the default of ``bench.py --gpus N``) divides the work
-instead of repeating the grouping on every rank: rank r keys every window but keeps only the
-k-mers of its share of the bucket hash range, groups and expands them, and routes each pair key
-to the rank owning the pair's row (kmp_dev_split_expand); one all-to-all of equal, padded splits
-moves the pair keys (42 MB in total per step at config 4, about 5 MB per rank at 8 ranks); every
-rank reduces its rows (kmp_dev_split_edges).  Frequent k-mers stay on the k-mer split: a rank
-whose share spills raises KMP_SPLIT_HEAVY, the step reruns with the heavy path on in every rank
-(each compacts, plans and expands the spill of its own k-mers into the keys it routes).  The row
-split stays the fallback for class ids wider than the key's field and the bounded-memory mode: at
-config 5 Σ C(df,2) ≈ 10^10-10^11 pair keys would cross the links, far more than recomputing the
-grouping.
+The collectives only move tensors, so the same code runs on gloo with CPU tensors and stand-in
+stages in the multi-process CPU tests (tests/test_dist.py).
 """
 from __future__ import annotations
 
@@ -113,6 +116,8 @@ class SplitState:
         self.bufs = None
         self.host_flags = None  # pinned (CUDA) host copy of the reduced flags, copied asynchronously
         self.row_split = False
+        self.kcap = 0  # sharded start: key-region size (u64 words per destination)
+        self.kbufs = None  # ... its send and receive buffers
         self.reruns = 0
         self.rerun_flags = []  # the reduced flags of each rerun (diagnostics)
 
@@ -120,7 +125,8 @@ class SplitState:
 def _pipe_state(pipe) -> SplitState:
     """The pipe's cached SplitState, reset when its batch or k changed (a k that spills frequent
     k-mers must not pin the row split, or its capacities, on another k of the same batch)."""
-    key = (pipe.n, pipe.total, pipe.k, pipe.res.data_ptr() if hasattr(pipe, "res") else 0)
+    key = (pipe.n, pipe.total, pipe.k, pipe.res.data_ptr() if hasattr(pipe, "res") else 0,
+           getattr(pipe, "parts", 0))
     st = pipe.__dict__.get("_split_state")
     if st is None or st.key != key:
         st = SplitState(key)
@@ -208,6 +214,150 @@ def kmer_split_step(pipe, rank: int, world: int, group=None, min_shared: int = 1
         if ev:
             torch.cuda.synchronize()
             timings.append(tuple(ev[i].elapsed_time(ev[i + 1]) for i in range(3)))
+        break
+    else:
+        raise RuntimeError("k-mer split: capacities unstable across reruns")
+    if not gather or world == 1:
+        return m
+
+    def grow(total):
+        old = (pipe.ep[:m].clone(), pipe.eq[:m].clone(), pipe.ew[:m].clone())
+        pipe._alloc_edges(total + total // 8)
+        for dst, src in zip((pipe.ep, pipe.eq, pipe.ew), old):
+            dst[:m].copy_(src)
+        return [pipe.ep, pipe.eq, pipe.ew]
+
+    total = gather_rows([pipe.ep, pipe.eq, pipe.ew], m, rank, world, group, grow)
+    if rank == 0:
+        pipe.n_edges = total
+    return total
+
+
+def gather_residues(pipe, group=None):
+    """The whole packed batch on every rank, from the ranks' slices (an all-gather over RCCL): the
+    row-split fallback of the sharded start.  Bytes no rank holds belong to proteins with fewer than
+    k residues, which have no window and so no edge; they stay zero."""
+    world = dist.get_world_size(group)
+    lo, hi, own = pipe.own_residues()
+    dev = own.device
+    spans = torch.zeros(2 * world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(spans, torch.tensor([lo, hi], dtype=torch.int64, device=dev), group=group)
+    sp = spans.view(world, 2).tolist()
+    width = max(1, max(h - l for l, h in sp))
+    buf = torch.zeros(width, dtype=torch.uint8, device=dev)
+    buf[:hi - lo] = own
+    allb = torch.empty(world * width, dtype=torch.uint8, device=dev)
+    dist.all_gather_into_tensor(allb, buf, group=group)
+    res = torch.zeros(max(1, pipe.total), dtype=torch.uint8, device=dev)
+    for r, (l, h) in enumerate(sp):
+        if h > l:
+            res[l:h] = allb[r * width:r * width + (h - l)]
+    return res[:pipe.total]
+
+
+def _row_split_from_shards(pipe, rank, world, group, min_shared, require_class_diff, gather):
+    """The row split over the rebuilt batch (class ids too wide for the k-mer split's key)."""
+    from .device import DevicePipeline
+    from .engine import Proteins
+    full = pipe.__dict__.get("_full")
+    if full is None:
+        res = gather_residues(pipe, group).cpu().numpy()
+        cls = pipe.cls.cpu().numpy().view(np.uint16)
+        full = DevicePipeline(Proteins(res, pipe.offsets_host, cls), pipe.k, pipe.dev)
+        pipe.__dict__["_full"] = full
+    if gather:
+        m = distributed_step(full, rank, world, group, min_shared, require_class_diff)
+    else:
+        lo, hi = row_ranges(full.n, world)[rank]
+        m = full.rows(lo, hi, min_shared=min_shared, require_class_diff=require_class_diff)
+    pipe.ep, pipe.eq, pipe.ew, pipe.n_edges = full.ep, full.eq, full.ew, full.n_edges
+    return m
+
+
+def sharded_split_step(pipe, rank: int, world: int, group=None, min_shared: int = 1,
+                       require_class_diff: bool = True, gather: bool = False, state: SplitState | None = None,
+                       timings: list | None = None) -> int:
+    """One multi-GPU step of the k-mer split with a sharded start (module docstring): keys, key
+    all-to-all, group + expand, pair-key all-to-all, edges.  Every rank ends holding the canonical
+    edges of its row range in pipe.ep/eq/ew and returns their count; with gather, rank 0 also
+    receives every rank's block behind its own and returns the total.  timings: a list to append
+    this rank's (keys, key exchange, group, pair exchange, edges) milliseconds to (CUDA events on
+    the current stream, which the library's stages and the collectives are ordered with)."""
+    st = state if state is not None else _pipe_state(pipe)
+    if st.row_split:
+        return _row_split_from_shards(pipe, rank, world, group, min_shared, require_class_diff, gather)
+    lo, hi = row_ranges(pipe.n, world)[rank]
+    dev = pipe.dev
+    cuda = dev.type == "cuda"
+    if st.kcap == 0:
+        st.kcap = int(pipe.span.key_cap)
+    if st.cap == 0:  # expected pair keys per (source, destination): a quarter of the windows / world^2
+        st.cap = max(4096, int(pipe.total // 4 // (world * world)))
+    m = 0
+    for _ in range(8):
+        if st.kbufs is None or st.kbufs[0].numel() != world * st.kcap:
+            st.kbufs = (torch.empty(world * st.kcap, dtype=torch.int64, device=dev),
+                        torch.empty(world * st.kcap, dtype=torch.int64, device=dev))
+        if st.bufs is None or st.bufs[0].numel() != world * st.cap:
+            st.bufs = (torch.empty(world * st.cap, dtype=torch.int64, device=dev),
+                       torch.empty(world * st.cap, dtype=torch.int64, device=dev),
+                       torch.zeros(_lib.KMP_SPLIT_FLAGS, dtype=torch.int32, device=dev),
+                       torch.zeros(8, dtype=torch.int64, device=dev))
+        ksend, krecv = st.kbufs
+        send, recv, flags, stats = st.bufs
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)] if timings is not None else None
+        if ev:
+            ev[0].record()
+        pipe.split_keys(rank, world, st.kcap, ksend, flags)
+        if ev:
+            ev[1].record()
+        if world > 1:
+            dist.all_to_all_single(krecv, ksend, group=group)
+        else:
+            krecv = ksend
+        if ev:
+            ev[2].record()
+        pipe.split_group(krecv, st.kcap, rank, world, st.cap, send, flags, stats, learn=st.learn,
+                         require_class_diff=require_class_diff)
+        if ev:
+            ev[3].record()
+        if world > 1:
+            dist.all_to_all_single(recv, send, group=group)
+            dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=group)
+        else:
+            recv = send
+        # the reduced flags go to the host behind the collectives on the same stream, with an event
+        # behind the copy (split_edges synchronises the stream anyway: no read-back of its own)
+        if st.host_flags is None or st.host_flags.numel() != flags.numel():
+            st.host_flags = torch.empty(flags.shape, dtype=flags.dtype, pin_memory=cuda)
+        st.host_flags.copy_(flags, non_blocking=cuda)
+        copied = torch.cuda.Event() if cuda else None
+        if copied is not None:
+            copied.record()
+        if ev:
+            ev[4].record()
+        m = pipe.split_edges(recv, lo, hi, min_shared)
+        if ev:
+            ev[5].record()
+        if copied is not None:
+            copied.synchronize()
+        fl = [int(x) for x in st.host_flags.tolist()]
+        if fl[_lib.KMP_SPLIT_CLASS]:
+            st.row_split = True
+            return _row_split_from_shards(pipe, rank, world, group, min_shared, require_class_diff, gather)
+        if fl[_lib.KMP_SPLIT_RERUN] or fl[_lib.KMP_SPLIT_HEAVY]:  # HEAVY: the heavy path on every rank
+            st.reruns += 1
+            st.rerun_flags.append(fl)
+            st.learn = fl
+            if fl[_lib.KMP_SPLIT_MAX_PART] > st.cap:
+                st.cap = fl[_lib.KMP_SPLIT_MAX_PART] + fl[_lib.KMP_SPLIT_MAX_PART] // 16 + 1024
+            if fl[_lib.KMP_SPLIT_MAX_KEYS] > st.kcap:
+                st.kcap = fl[_lib.KMP_SPLIT_MAX_KEYS] + fl[_lib.KMP_SPLIT_MAX_KEYS] // 32 + 1024
+            continue
+        st.learn = None
+        if ev:
+            torch.cuda.synchronize()
+            timings.append(tuple(ev[i].elapsed_time(ev[i + 1]) for i in range(5)))
         break
     else:
         raise RuntimeError("k-mer split: capacities unstable across reruns")
