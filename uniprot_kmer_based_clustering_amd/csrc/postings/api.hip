@@ -364,6 +364,9 @@ static int split_expand_impl(kmp_postings* ws, const SplitSrc& src, uint32_t n, 
     const BpDigits dg = bp_digits(lay);
     ws->bin_lo = split_bin_lo(part, dg.nb1, parts);
     ws->bin_hi = split_bin_lo(part + 1, dg.nb1, parts);
+    // key regions too small for their run tables carry nothing readable (the keys phase sent no
+    // table and raised RERUN with the size that fits): this step groups nothing
+    if (recv && src.kcap < split_geom(lay, slots, parts).tb + kSendShards) ws->bin_hi = ws->bin_lo;
     auto make_keys = [&](const Layout& l, hipStream_t s) {
         ws->parted = true;
         if (recv) {

@@ -322,6 +322,6 @@ hipError_t bp_level1_recv(kmp_postings* ws, const unsigned long long* krecv, uin
     ws->bp_hsc = sg.rowlen;
     ws->l1_in = krecv;
     ws->l2_tab = reinterpret_cast<const uint32_t*>(krecv);
-    ws->l2_rt = RecvTab{sg.cm, sg.n_chunks, parts, 2 * kcap};
+    ws->l2_rt = RecvTab{sg.cm, sg.n_chunks, parts, 2 * kcap, sg.tb};
     return hipGetLastError();
 }

@@ -870,6 +870,7 @@ struct RecvTab {
     uint32_t n_chunks;   // chunks of the batch (source s holds [s C / parts, (s + 1) C / parts))
     uint32_t parts;
     uint64_t stride;     // u32 words between source regions (2 x the region's u64 words)
+    uint64_t tb;         // run-table u64 words at the start of a region
 };
 template <uint32_t kPer, uint32_t kThr, bool kVreg, bool kRecv>
 __global__ __launch_bounds__(kThr) void bp_scatter2g_kernel(const unsigned long long* __restrict__ in,
@@ -907,10 +908,17 @@ __global__ __launch_bounds__(kThr) void bp_scatter2g_kernel(const unsigned long 
             const uint32_t nsrc = s < rt.parts ? (uint32_t)((uint64_t)(s + 1) * rt.n_chunks / rt.parts -
                                                             (uint64_t)s * rt.n_chunks / rt.parts)
                                                : 0u;
-            const bool ok = t < q && b0 + t < nch && i < nsrc;
+            // a row past the region's table, or a run outside the source's key part, reads as empty
+            // (only a sender's error path could produce one; nothing is read out of bounds)
+            const bool ok = t < q && b0 + t < nch && i < nsrc && ((uint64_t)i + 1) * hsc <= 2 * rt.tb;
             const uint32_t* rw = H1T + s * rt.stride + (uint64_t)i * hsc;
             p[t] = ok ? rw[1 + c - dlo] : 0u;
             rbase[t] = ok ? rw[0] : 0u;
+            const uint64_t lo = (uint64_t)s * (rt.stride / 2) + rt.tb, hi = (uint64_t)(s + 1) * (rt.stride / 2);
+            if ((p[t] & 0xFFFFu) && (rbase[t] + (p[t] >> 16) < lo || rbase[t] + (p[t] >> 16) + (p[t] & 0xFFFFu) > hi)) {
+                p[t] = 0;
+                flags[kFlSend] = 1;
+            }
         } else {
             p[t] = t < q && b0 + t < nch ? row[(uint64_t)(b0 + t) * hsc] : 0u;
         }

@@ -121,7 +121,8 @@ __global__ void split_pad_finish_kernel(unsigned long long* __restrict__ send, u
         out[KMP_SPLIT_MAX_SHARD] = (uint32_t)min<unsigned long long>(shard, clamp);
         out[KMP_SPLIT_BIN_TILES] = wflags[kFlBin] ? wflags[kFlBinTiles] : 0u;
         out[KMP_SPLIT_CURSOR] = wflags[kFlCur];
-        out[KMP_SPLIT_RERUN] = (part > cap || shard > sc || wflags[kFlBin] || wflags[kFlCur] || k_rerun) ? 1u : 0u;
+        out[KMP_SPLIT_RERUN] =
+            (part > cap || shard > sc || wflags[kFlBin] || wflags[kFlCur] || wflags[kFlSend] || k_rerun) ? 1u : 0u;
         for (uint32_t i = KMP_SPLIT_CURSOR + 1; i < KMP_SPLIT_FLAGS; ++i) out[i] = 0;
         out[KMP_SPLIT_MAX_KEYS] = k_keys;
     }
