@@ -575,11 +575,13 @@ int kmp_dev_pairs_rows_multi(kmp_postings* const* ws, const int* ks, uint32_t nk
  * region, pair-key shard or bucket region overflowed: call expand again with learn, after growing
  * cap to at least MAX_PART when that is the cause), CLASS (class ids too wide: single GPU) and
  * HEAVY (k-mers above the LDS group limit spilled while the rank's heavy path was off: call expand
- * again with learn — every rank turns its heavy path on for the batch, vertex.rs:59-140). */
+ * again with learn — every rank turns its heavy path on for the batch, vertex.rs:59-140), LARGE
+ * (a bucket above the small kernel's LDS capacity was listed while the rank did not launch the
+ * large-bucket kernel: every rank launches it from then on; RERUN is set too). */
 enum {
     KMP_SPLIT_RERUN = 0, KMP_SPLIT_CLASS = 1, KMP_SPLIT_HEAVY = 2, KMP_SPLIT_MAX_PART = 3,
     KMP_SPLIT_MAX_SHARD = 4, KMP_SPLIT_BIN_TILES = 5, KMP_SPLIT_CURSOR = 6, KMP_SPLIT_MAX_KEYS = 7,
-    KMP_SPLIT_FLAGS = 8
+    KMP_SPLIT_LARGE = 8, KMP_SPLIT_FLAGS = 16
 };
 int kmp_dev_split_expand(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
                          uint32_t n, int k, uint64_t slots, uint32_t heavy_df, int require_class_diff, uint32_t part,

@@ -106,8 +106,28 @@ def sharded_ranks(b, k, g):
     per = []
     for r, (lo, hi) in enumerate(row_ranges(b.n, g)):
         p = pipes[r]
-        t0, d0 = timed(lambda: p.split_keys(r, g, kcap, ksend[r], flags[r]))
-        t1, d1 = timed(lambda: p.split_group(krecv[r], kcap, r, g, cap, sends[r], flags[r], stats[r]))
+        # keys and group back to back, as in a step (the group phase reads and resets the keys
+        # phase's cursors); device time split at an event between them
+        mid = []
+
+        def kg():
+            p.split_keys(r, g, kcap, ksend[r], flags[r])
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            mid.append(e)
+            p.split_group(krecv[r], kcap, r, g, cap, sends[r], flags[r], stats[r])
+        t01, d01 = timed(kg)
+        ev0 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
+        d0 = 0.0
+        for a, b in ev0:
+            a.record()
+            p.split_keys(r, g, kcap, ksend[r], flags[r])
+            b.record()
+            p.split_group(krecv[r], kcap, r, g, cap, sends[r], flags[r], stats[r])
+        torch.cuda.synchronize()
+        d0 = sum(a.elapsed_time(b) for a, b in ev0) / len(ev0)
+        d1 = d01 - d0
+        t0, t1 = d0, t01 - d0
         t2, d2 = timed(lambda: p.split_edges(recvs[r], lo, hi))
         # bytes this rank sends to the others in each exchange (its own region stays local)
         kbytes = (g - 1) * kcap * 8

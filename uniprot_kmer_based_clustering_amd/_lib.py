@@ -25,8 +25,8 @@ KMP_LAYOUT_FLAT, KMP_LAYOUT_BUCKETED, KMP_LAYOUT_BUCKETED_HEAVY = 0, 1, 2
 KMP_TAIL_COUNT, KMP_TAIL_FAST = 0, 1
 KMP_PARTITION_AUTO, KMP_PARTITION_COUNT, KMP_PARTITION_CURSOR = 0, 1, 2
 (KMP_SPLIT_RERUN, KMP_SPLIT_CLASS, KMP_SPLIT_HEAVY, KMP_SPLIT_MAX_PART, KMP_SPLIT_MAX_SHARD, KMP_SPLIT_BIN_TILES,
- KMP_SPLIT_CURSOR, KMP_SPLIT_MAX_KEYS) = range(8)
-KMP_SPLIT_FLAGS = 8
+ KMP_SPLIT_CURSOR, KMP_SPLIT_MAX_KEYS, KMP_SPLIT_LARGE) = range(9)
+KMP_SPLIT_FLAGS = 16
 KMP_LDS_SORT_MAX = 4096
 
 

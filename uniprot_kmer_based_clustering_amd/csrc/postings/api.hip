@@ -325,6 +325,7 @@ static int split_expand_impl(kmp_postings* ws, const SplitSrc& src, uint32_t n, 
         if (learn[KMP_SPLIT_MAX_SHARD] > ws->shard_cap)
             ws->shard_cap = learn[KMP_SPLIT_MAX_SHARD] + learn[KMP_SPLIT_MAX_SHARD] / 8 + 256;
         if (learn[KMP_SPLIT_BIN_TILES]) ws->bp_J_min = std::max(ws->bp_J_min, learn[KMP_SPLIT_BIN_TILES] + 2);
+        if (learn[KMP_SPLIT_LARGE]) ws->split_large = true;
         if (learn[KMP_SPLIT_CURSOR]) {
             if (recv && ws->cur.p) {
                 // a bucket region overflowed on some rank: this rank's regions from its last call's
@@ -394,27 +395,41 @@ static int split_expand_impl(kmp_postings* ws, const SplitSrc& src, uint32_t n, 
         const uint32_t ncur = routed ? parts * kShards : parts;
         ws->clear_extra = ws->split_cur.p;
         ws->clear_n = ncur;
+        const bool bins = ws->bin_hi > ws->bin_lo;
         if (routed) {
-            PG(hipMemsetAsync(d_send, 0xFF, (size_t)parts * cap * sizeof(unsigned long long), s));
+            // the send regions pre-filled with kNoKey: by the received front's clear kernel, else here
+            if (recv && bins) {
+                ws->fill_p = d_send;
+                ws->fill_n = (uint64_t)parts * cap;
+            } else {
+                PG(hipMemsetAsync(d_send, 0xFF, (size_t)parts * cap * sizeof(unsigned long long), s));
+            }
             ws->route_send = d_send;
             ws->route_cap = cap;
             ws->route_rows = rows;
         }
         int rc = KMP_OK;
-        if (ws->bin_hi > ws->bin_lo) rc = enqueue_front(ws, make_keys, c, true, s);
+        if (bins) rc = enqueue_front(ws, make_keys, c, true, s);
         else step_clear_kernel<<<1, 256, 0, s>>>(ws->flags.p, ws->bstats.p, ws->split_cur.p, ncur);  // no bins
         ws->clear_extra = nullptr;
         ws->clear_n = 0;
         ws->route_send = nullptr;
+        ws->fill_p = nullptr;
+        ws->fill_n = 0;
         return rc;
     };
+    // the sharded start's keys phase (this rank's send cursors and flags): read and reset by the finish
+    uint32_t* kcur = recv && ws->kcur_dirty ? ws->split_kcur.p : nullptr;
+    const uint32_t nkc = parts * kSendShards;
+    const uint64_t ktb = recv ? split_geom(lay, slots, parts).tb : 0;
     auto route = [&](hipStream_t s, int heavy_done) -> int {
         // merge: the keys phase wrote this step's key-exchange flags into d_flags first
         const int merge = recv ? 1 : 0;
+        const int large = ws->large_used != 0 || ws->bin_hi <= ws->bin_lo;
         if (routed) {  // the bucket kernels routed the keys: the flags and statistics only
             split_pad_finish_kernel<<<dim3(1, 1), 256, 0, s>>>(d_send, cap, ws->split_cur.p, ws->bstats.p, ws->flags.p,
                                                                 ws->shard_cap, parts, d_flags, d_stats, heavy_done, 1,
-                                                                merge);
+                                                                merge, kcur, nkc, ktb, large);
             PG(hipGetLastError());
             return KMP_OK;
         }
@@ -423,7 +438,7 @@ static int split_expand_impl(kmp_postings* ws, const SplitSrc& src, uint32_t n, 
             ws->inc_sorted.p, cursor, ws->shard_cap, bits_for(n), rows, cap, d_send, ws->split_cur.p);
         split_pad_finish_kernel<<<dim3((uint32_t)std::min<uint64_t>((cap + 1023) / 1024, 256), parts), 256, 0, s>>>(
             d_send, cap, ws->split_cur.p, ws->bstats.p, ws->flags.p, ws->shard_cap, parts, d_flags, d_stats,
-            heavy_done, 0, merge);
+            heavy_done, 0, merge, kcur, nkc, ktb, large);
         PG(hipGetLastError());
         return KMP_OK;
     };
@@ -465,6 +480,7 @@ static int split_expand_impl(kmp_postings* ws, const SplitSrc& src, uint32_t n, 
             break;
         }
         unbind();
+        if (kcur && routed_done) ws->kcur_dirty = false;
         if (rc == KMP_OK && !routed_done) {
             // every attempt grew the spill regions: no keys are sent and the flags ask every rank for
             // a rerun, so the ranks stay in lockstep through the collectives (an error returned here
@@ -485,9 +501,10 @@ static int split_expand_impl(kmp_postings* ws, const SplitSrc& src, uint32_t n, 
         n, slots, (unsigned long long)k, heavy_df, (unsigned long long)require_class_diff, part, parts, cap,
         (uintptr_t)src.d_res, (uintptr_t)src.d_res_off, (uintptr_t)src.d_class, (uintptr_t)src.d_krecv, src.kcap,
         (uintptr_t)d_send, (uintptr_t)d_flags, (uintptr_t)d_stats, ws->shard_cap, ws->spill_cap, ws->bp_J_min,
-        ws->cur_on, ws->timing, ws->vreg_on ? ws->vreg_total + 1 : 0};
+        ws->cur_on, ws->timing, ws->vreg_on ? ws->vreg_total + 1 : 0, (uintptr_t)kcur, ws->split_large};
     const int rc = slot_launch(ws, ws->split_g[0], key, enqueue, st);
     unbind();
+    if (kcur) ws->kcur_dirty = false;
     return rc;
 }
 
@@ -563,30 +580,42 @@ int kmp_dev_split_keys(kmp_postings* ws, const uint8_t* d_res, uint64_t res_lo, 
     const uint32_t sub = (uint32_t)std::min<uint64_t>(sub64, 0xFFFFFFFFull);
     const uint32_t c_lo = split_chunk_lo(sg, part, parts), c_hi = split_chunk_lo(sg, part + 1, parts);
     const uint32_t G = c_hi - c_lo, nkc = parts * kSendShards;
-    PG(ws->chunk_desc.reserve(4ull * std::max(1u, G)));
-    PG(ws->split_kcur.reserve(nkc));
-    PG(ws->flags.reserve(kFlN));
+    PG(ws->split_desc.reserve(std::max(1u, G)));
+    // the send cursors | the keys phase's flags: zero when allocated, and reset by the group phase
+    // that reads them (kmp_dev_split_group's finish), so this call clears nothing
+    PG(ws->split_kcur.reserve(nkc + kFlN));
+    if (ws->kcur_zero_p != ws->split_kcur.p || ws->kcur_dirty) {
+        PG(hipMemsetAsync(ws->split_kcur.p, 0, ws->split_kcur.n * sizeof(uint32_t), st));
+        ws->kcur_zero_p = ws->split_kcur.p;
+    }
+    ws->kcur_dirty = true;
     const BpDigits dg = bp_digits(lay);
     const uint32_t pw21 = (uint32_t)pow21(k - 1);
+    // the rank's chunk descriptors depend on the batch's offsets only: computed once per batch
+    const std::vector<unsigned long long> dkey = {(uintptr_t)d_res_off, n, slots, (unsigned long long)k, c_lo, c_hi,
+                                                  (uintptr_t)ws->split_desc.p};
+    if (ws->split_desc_key != dkey) {
+        chunk_desc_kernel<<<(n + 1 + 255) / 256, 256, 0, st>>>(d_res_off, n, slots, c_lo, c_hi, k, ws->split_desc.p,
+                                                               nullptr, 0, StepClear{});
+        PG(hipGetLastError());
+        ws->split_desc_key = dkey;
+    }
     auto enqueue = [&](hipStream_t s) -> int {
-        // descriptors of the rank's chunks, the send cursors and the flags cleared
-        chunk_desc_kernel<<<(n + 1 + 255) / 256, 256, 0, s>>>(
-            d_res_off, n, slots, c_lo, c_hi, k, reinterpret_cast<uint4*>(ws->chunk_desc.p), ws->split_kcur.p, nkc,
-            StepClear{ws->flags.p, kFlN, nullptr, 0, nullptr, 0});
         if (G) {
             const SendL1 sl{d_ksend, kcap, sg.tb, sub, ws->split_kcur.p, part, parts, c_lo, sg.rowlen, res_lo, res_hi};
-            // one workgroup per chunk (every digit ranked: the single-GPU geometry)
+            // one workgroup per chunk (every digit ranked: the single-GPU geometry); its flags go to
+            // the words after the cursors
             bp_scatter1p_kernel<KMP_L1_THREADS, true><<<G, KMP_L1_THREADS, 0, s>>>(
-                d_res, d_res_off, d_class, k, n, slots, G, reinterpret_cast<const uint4*>(ws->chunk_desc.p), lay, dg,
-                pw21, 0u, dg.nb1, nullptr, nullptr, ws->flags.p, sl);
+                d_res, d_res_off, d_class, k, n, slots, G, ws->split_desc.p, lay, dg, pw21, 0u, dg.nb1, nullptr,
+                nullptr, ws->split_kcur.p + nkc, sl);
         }
-        split_keys_finish_kernel<<<1, 256, 0, s>>>(ws->split_kcur.p, nkc, ws->flags.p, sg.tb, d_flags);
         PG(hipGetLastError());
         return KMP_OK;
     };
     const std::vector<unsigned long long> key = {n, slots, (unsigned long long)k, part, parts, kcap, res_lo, res_hi,
                                                  (uintptr_t)d_res, (uintptr_t)d_res_off, (uintptr_t)d_class,
-                                                 (uintptr_t)d_ksend, (uintptr_t)d_flags};
+                                                 (uintptr_t)d_ksend, (uintptr_t)d_flags, (uintptr_t)ws->split_kcur.p,
+                                                 (uintptr_t)ws->split_desc.p};
     return slot_launch(ws, ws->split_g[2], key, enqueue, st);
 }
 
@@ -643,8 +672,16 @@ int kmp_dev_split_edges(kmp_postings* ws, const unsigned long long* d_keys, uint
         PG(ws->bstats.reserve(kGsWords));
         if (!ws->hrb) PG(hipHostMalloc((void**)&ws->hrb, kRbWords * sizeof(unsigned long long), hipHostMallocCoherent));
         auto enqueue = [&](hipStream_t s) -> int {
-            step_clear_kernel<<<1, 256, 0, s>>>(ws->flags.p, ws->bstats.p);  // flags (the expand's stats are out)
-            return enqueue_tail_in(ws, c, g, d_keys, nullptr, m, s);
+            // the step's flags and statistics cleared (the expand's stats are out): by the fast tail's
+            // scatter kernel, or a kernel of its own before the counting tail
+            if (pt_fast(ws, g)) {
+                ws->tail_clear = true;
+            } else {
+                step_clear_kernel<<<1, 256, 0, s>>>(ws->flags.p, ws->bstats.p);
+            }
+            const int rc = enqueue_tail_in(ws, c, g, d_keys, nullptr, m, s);
+            ws->tail_clear = false;
+            return rc;
         };
         const std::vector<unsigned long long> key = {m, n, row_lo, row_hi, c.min_shared, cap, (uintptr_t)d_keys,
                                                      (uintptr_t)d_p, (uintptr_t)d_q, (uintptr_t)d_w, g.rbits,

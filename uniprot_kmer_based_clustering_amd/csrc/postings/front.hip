@@ -290,9 +290,14 @@ uint32_t split_chunk_lo(const SplitGeom& g, uint32_t part, uint32_t parts) {
 
 // clears the bucket counts of the cursor level 2 and (sc) the step's flags: the front of a call
 // whose level 1 ran elsewhere (the received pieces)
-__global__ void split_recv_clear_kernel(uint32_t* __restrict__ cur, uint32_t ncur, StepClear sc) {
+// and fills [fill, fill + nfill) with kNoKey (the routed send regions)
+__global__ void split_recv_clear_kernel(uint32_t* __restrict__ cur, uint32_t ncur, StepClear sc,
+                                        unsigned long long* __restrict__ fill, uint64_t nfill) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     for (uint32_t i = t; i < ncur; i += gridDim.x * blockDim.x) cur[i] = 0;
+    ulonglong2* f2 = reinterpret_cast<ulonglong2*>(fill);  // 16-B aligned (a device allocation)
+    for (uint64_t i = t; i < nfill / 2; i += (uint64_t)gridDim.x * blockDim.x) f2[i] = make_ulonglong2(kNoKey, kNoKey);
+    if (t == 0 && (nfill & 1)) fill[nfill - 1] = kNoKey;
     if (blockIdx.x == 0 && sc.flags) {
         for (uint32_t i = threadIdx.x; i < sc.n_gstats; i += blockDim.x) sc.gstats[i] = 0;
         for (uint32_t i = threadIdx.x; i < sc.n_flags; i += blockDim.x) sc.flags[i] = 0;
@@ -314,7 +319,8 @@ hipError_t bp_level1_recv(kmp_postings* ws, const unsigned long long* krecv, uin
         sc = StepClear{ws->flags.p, kFlN, ws->bstats.p, kShards * 10, ws->clear_extra, ws->clear_n};
         ws->defer_clear = false;
     }
-    split_recv_clear_kernel<<<std::min<uint32_t>((nb + 255) / 256, 1024), 256, 0, st>>>(ws->cur.p, nb, sc);
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((nb + 255) / 256, ws->fill_n / 2 / 256 / 8 + 1), 2048);
+    split_recv_clear_kernel<<<grid, 256, 0, st>>>(ws->cur.p, nb, sc, ws->fill_p, ws->fill_n);
     ws->bp_local = true;
     ws->bp_G = parts * sg.cm;
     ws->bp_T = std::min<uint32_t>(kBpGatherMax, std::max<uint32_t>(1, kBpGatherTile * 7 / 4 * dg.nb1 / kKeyChunk));

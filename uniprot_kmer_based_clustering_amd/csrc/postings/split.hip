@@ -60,15 +60,18 @@ __global__ __launch_bounds__(kRtThreads) void split_route_kernel(const unsigned 
 // also writes the rank's flags (KMP_SPLIT_*) and statistics (kSt* order, summed over the shards)
 // routed (the bucket kernels wrote the send regions themselves, kShards sub-regions of cap / kShards
 // keys per destination, the buffer pre-filled with kNoKey): no padding; the part size reported is
-// kShards x the fullest sub-region, so a grown cap gives every sub-region its need.  merge: the keys
-// phase of the same step (kmp_dev_split_keys) wrote its flags first: RERUN and CLASS are or-ed,
-// MAX_KEYS kept
+// kShards x the fullest sub-region, so a grown cap gives every sub-region its need.  kcur (the sharded
+// start): the keys phase's send cursors (nkc) and its flags (kFlN words after them) on this rank —
+// MAX_KEYS = the region size that fits every sub-region (the cursors count every piece, dropped or
+// not), RERUN when a piece was dropped — read and reset for the next keys phase.  A listed bucket
+// with no large-bucket launch raises LARGE (and RERUN).
 __global__ void split_pad_finish_kernel(unsigned long long* __restrict__ send, uint64_t cap,
                                         const unsigned long long* __restrict__ dcursor,
                                         const unsigned long long* __restrict__ gstats,
                                         const uint32_t* __restrict__ wflags, uint64_t sc, uint32_t parts,
                                         uint32_t* __restrict__ out, unsigned long long* __restrict__ stats,
-                                        int heavy_done, int routed, int merge) {
+                                        int heavy_done, int routed, int merge, uint32_t* __restrict__ kcur,
+                                        uint32_t nkc, uint64_t tb, int large_launched) {
     const uint32_t d = blockIdx.y;
     if (!routed)
         for (uint64_t i = dcursor[d] + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap;
@@ -78,7 +81,7 @@ __global__ void split_pad_finish_kernel(unsigned long long* __restrict__ send, u
     // one workgroup: the statistics and the fullest regions reduced over its threads (one thread
     // walking the parts x kShards cursors took 45 us at G = 8)
     const uint32_t t = threadIdx.x;
-    __shared__ unsigned long long s_red[3][256 / 64];
+    __shared__ unsigned long long s_red[4][256 / 64];
     if (t < kStN) {
         unsigned long long v = 0;
         for (int sh = 0; sh < kShards; ++sh) {
@@ -94,27 +97,35 @@ __global__ void split_pad_finish_kernel(unsigned long long* __restrict__ send, u
     }
     const uint32_t nq = routed ? parts * kShards : parts;
     for (uint32_t q = t; q < nq; q += blockDim.x) part = max(part, dcursor[q] * (routed ? kShards : 1u));
+    unsigned long long kmax = 0;
+    if (kcur)
+        for (uint32_t q = t; q < nkc; q += blockDim.x) kmax = max(kmax, (unsigned long long)kcur[q]);
     for (int off = 32; off > 0; off >>= 1) {
         shard = max(shard, (unsigned long long)__shfl_xor(shard, off));
         spill += (unsigned long long)__shfl_xor(spill, off);
         part = max(part, (unsigned long long)__shfl_xor(part, off));
+        kmax = max(kmax, (unsigned long long)__shfl_xor(kmax, off));
     }
     if ((t & 63) == 0) {
         s_red[0][t >> 6] = shard;
         s_red[1][t >> 6] = spill;
         s_red[2][t >> 6] = part;
+        s_red[3][t >> 6] = kmax;
     }
     __syncthreads();
     if (t == 0) {
-        shard = spill = part = 0;
+        shard = spill = part = kmax = 0;
         for (uint32_t w = 0; w < (blockDim.x + 63) / 64; ++w) {
             shard = max(shard, s_red[0][w]);
             spill += s_red[1][w];
             part = max(part, s_red[2][w]);
+            kmax = max(kmax, s_red[3][w]);
         }
         const uint32_t clamp = 0xFFFFFFFFu;
-        const uint32_t k_rerun = merge ? out[KMP_SPLIT_RERUN] : 0u, k_class = merge ? out[KMP_SPLIT_CLASS] : 0u;
-        const uint32_t k_keys = merge ? out[KMP_SPLIT_MAX_KEYS] : 0u;
+        const uint32_t* kfl = kcur ? kcur + nkc : nullptr;  // the keys phase's flags
+        const uint32_t k_rerun = kfl ? kfl[kFlSend] : 0u, k_class = kfl ? kfl[kFlClass] : 0u;
+        const uint32_t k_keys = kcur ? (uint32_t)min<unsigned long long>(tb + kSendShards * kmax, clamp) : 0u;
+        const uint32_t large = !large_launched && wflags[kFlList] ? 1u : 0u;
         out[KMP_SPLIT_CLASS] = wflags[kFlClass] | k_class;
         out[KMP_SPLIT_HEAVY] = spill != 0 && !heavy_done;  // spilled with the heavy path off: rerun with it on
         out[KMP_SPLIT_MAX_PART] = (uint32_t)min<unsigned long long>(part, clamp);
@@ -122,30 +133,15 @@ __global__ void split_pad_finish_kernel(unsigned long long* __restrict__ send, u
         out[KMP_SPLIT_BIN_TILES] = wflags[kFlBin] ? wflags[kFlBinTiles] : 0u;
         out[KMP_SPLIT_CURSOR] = wflags[kFlCur];
         out[KMP_SPLIT_RERUN] =
-            (part > cap || shard > sc || wflags[kFlBin] || wflags[kFlCur] || wflags[kFlSend] || k_rerun) ? 1u : 0u;
+            (part > cap || shard > sc || wflags[kFlBin] || wflags[kFlCur] || wflags[kFlSend] || k_rerun || large) ? 1u
+                                                                                                              : 0u;
         for (uint32_t i = KMP_SPLIT_CURSOR + 1; i < KMP_SPLIT_FLAGS; ++i) out[i] = 0;
         out[KMP_SPLIT_MAX_KEYS] = k_keys;
+        out[KMP_SPLIT_LARGE] = large;
+    }
+    if (kcur) {  // read above (the reduction's barrier): cleared for the next keys phase
+        __syncthreads();
+        for (uint32_t q = t; q < nkc + kFlN; q += blockDim.x) kcur[q] = 0;
     }
 }
 
-// the keys phase's flags (kmp_dev_split_keys): RERUN when a piece did not fit its sub-region,
-// CLASS from the keying, MAX_KEYS = the region size that fits every sub-region (the cursors count
-// every piece, dropped or not); the other words zero
-__global__ void split_keys_finish_kernel(const uint32_t* __restrict__ kcur, uint32_t nkc,
-                                         const uint32_t* __restrict__ wflags, uint64_t tb,
-                                         uint32_t* __restrict__ out) {
-    __shared__ uint32_t s_max[256 / 64];
-    const uint32_t t = threadIdx.x;
-    uint32_t m = 0;
-    for (uint32_t i = t; i < nkc; i += blockDim.x) m = max(m, kcur[i]);
-    m = wave_max(m);
-    if ((t & 63) == 0) s_max[t >> 6] = m;
-    __syncthreads();
-    if (t == 0) {
-        for (uint32_t w = 0; w < (blockDim.x + 63) / 64; ++w) m = max(m, s_max[w]);
-        for (uint32_t i = 0; i < KMP_SPLIT_FLAGS; ++i) out[i] = 0;
-        out[KMP_SPLIT_RERUN] = wflags[kFlSend];
-        out[KMP_SPLIT_CLASS] = wflags[kFlClass];
-        out[KMP_SPLIT_MAX_KEYS] = (uint32_t)min<unsigned long long>(tb + (unsigned long long)kSendShards * m, 0xFFFFFFFFull);
-    }
-}

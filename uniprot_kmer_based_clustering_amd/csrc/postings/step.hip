@@ -217,7 +217,9 @@ int enqueue_front(kmp_postings* ws, MakeKeys& make_keys, const StepCfg& c, bool 
     // the large-bucket kernel loops over its list: a grid sized from the last call's list (a
     // thousand idle 1,024-thread workgroups cost ~5 us); a bucket-range share of the k-mer split
     // lists about 1/parts of them
-    const uint32_t lg = ws->bin_hi ? std::max<uint32_t>(64, kBucketLargeGrid * (c1 - c0) / dg.nb1) : ws->large_grid;
+    // (a rank of the k-mer split: about 1/parts of them, and none at all until a call lists one)
+    const uint32_t lg = ws->bin_hi ? (ws->split_large ? std::max<uint32_t>(64, kBucketLargeGrid * (c1 - c0) / dg.nb1) : 0u)
+                                   : ws->large_grid;
     ws->large_used = lg;
     if (spill) ws->front_all = a.spill_all != 0;  // what the spill of this front will hold
     if (a.spill_all && !a.spill) return KMP_OK;  // every bucket already in the heavy path (a later pass)
@@ -248,8 +250,9 @@ int enqueue_tail_in(kmp_postings* ws, const StepCfg& c, const PtGeom& g, const u
     uint32_t* keys32 = reinterpret_cast<uint32_t*>(ws->inc.p);
     if (pt_fast(ws, g)) {  // one reduce that writes the edges (marks 4, 5, 6)
         const uint32_t jt = (uint32_t)(((g.flat_n ? g.flat_n : g.sc) + kFtScTile - 1) / kFtScTile);
+        const StepClear sc = ws->tail_clear ? StepClear{ws->flags.p, kFlN, ws->bstats.p, kGsWords, nullptr, 0} : StepClear{};
         pt_scatter_capped_kernel<<<dim3(jt, g.nshards), kFtScThreads, 0, st>>>(in, cursor, g, b.fcur, keys32, b.lb,
-                                                                                b.ticket);
+                                                                                b.ticket, sc);
         ws->mark(4, st);
         pt_reduce_fast_kernel<<<g.nrb, kFtThreads, 0, st>>>(keys32, b.fcur, g, b.lb, b.ticket, c.d_p, c.d_q, c.d_w,
                                                              c.cap, c.stride,

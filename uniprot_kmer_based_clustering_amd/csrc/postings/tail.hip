@@ -205,7 +205,7 @@ __global__ __launch_bounds__(kFtScThreads) void pt_scatter_capped_kernel(const u
                                                                          PtGeom g, uint32_t* __restrict__ cur,
                                                                          uint32_t* __restrict__ out,
                                                                          unsigned long long* __restrict__ lb,
-                                                                         uint32_t* __restrict__ ticket) {
+                                                                         uint32_t* __restrict__ ticket, StepClear sc) {
     constexpr uint32_t kThr = kFtScThreads, kPer = 16;
     __shared__ uint32_t lh[kPtMaxBlocks];
     __shared__ uint32_t S[kFtScTile];
@@ -216,6 +216,11 @@ __global__ __launch_bounds__(kFtScThreads) void pt_scatter_capped_kernel(const u
     if (j == 0 && s == 0) {
         for (uint32_t r = threadIdx.x; r < g.nrb; r += kThr) lb[r] = 0;
         if (threadIdx.x == 0) *ticket = 0;
+        // (a tail-only call: the step's flags and statistics, which only the reduce reads)
+        if (sc.flags)
+            for (uint32_t i = threadIdx.x; i < sc.n_flags; i += kThr) sc.flags[i] = 0;
+        if (sc.gstats)
+            for (uint32_t i = threadIdx.x; i < sc.n_gstats; i += kThr) sc.gstats[i] = 0;
     }
     const uint64_t ns = g.flat_n ? g.flat_n : min<unsigned long long>(cursor[s], g.sc);
     const uint64_t t0 = (uint64_t)j * kFtScTile;

@@ -75,7 +75,15 @@ struct kmp_postings {
     const unsigned long long* l1_in = nullptr;
     const uint32_t* l2_tab = nullptr;
     RecvTab l2_rt{};
-    Grow<uint32_t> split_kcur;  // the key pieces' send cursors (parts x kSendShards)
+    bool tail_clear = false;  // the fast tail's scatter clears the step's flags and statistics first
+    unsigned long long* fill_p = nullptr;  // filled with kNoKey by the received front's clear kernel
+    uint64_t fill_n = 0;
+    Grow<uint32_t> split_kcur;  // the key pieces' send cursors (parts x kSendShards) | kFlSend | kFlClass
+    const uint32_t* kcur_zero_p = nullptr;  // the split_kcur allocation that was cleared
+    bool kcur_dirty = false;    // a keys phase's cursors not yet read (and reset) by a group phase
+    bool split_large = false;   // the k-mer split launches the large-bucket kernel (a call listed one)
+    Grow<uint4> split_desc;     // the sharded keys phase's chunk descriptors (per batch and rank)
+    std::vector<unsigned long long> split_desc_key;
     // cursor level 2 (fixed-capacity bucket regions, no counting passes): tried first for a new
     // shape (cur_on), dropped for the shape after a region overflow; cur_used: the buckets in
     // ws->sorted came from it (ws->cur: bucket counts)
@@ -143,6 +151,8 @@ struct kmp_postings {
             g->release();
         for (auto* g : {&w, &keep, &pos, &small, &cnt, &flags, &chunk_first, &chunk_desc, &bp, &pt, &ovf, &ovr, &ova, &stg2, &k2, &dsc, &hE, &hgi, &hcnt,
                         &hrun, &hblk, &cur, &hGH, &split_kcur})
+            g->release();
+        for (auto* g : {&split_desc})
             g->release();
         tmp.release();
         for (auto& e : ev)
