@@ -11,11 +11,15 @@ Inputs are synthetic (N = 100,000, seed 3, len ~ N(300
   python bench.py [--gpus N] [--steps K] [--warmup W] [--engine residues|postings|tiles]
   N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N [--split kmer|rows]
 
-N > 1 (config 4): one process per GPU over RCCL, the k-mer split (dist.kmer_split_step): each rank
-groups and expands its share of the k-mers, one all-to-all moves the pair keys to their row
-owners, each rank reduces its rows, and rank 0 gathers every rank's row block behind its own (rank
-order = canonical order): the timed step ends with the canonical list resident on rank 0
-(SURVEY.md §8d); the row-sharded step without that gather is reported as a breakdown.
+N > 1 (config 4): one process per GPU over RCCL, the k-mer split with a sharded start
+(dist.sharded_split_step): rank r holds only the residues of its own chunks (about
+1/N of the batch), keys its windows once and an all-to-all sends every key to the rank owning its
+k-mer's bins; each rank groups and expands its k-mers, a second all-to-all moves the pair keys to
+their row owners, each rank reduces its rows, and rank 0 gathers every rank's row block behind its
+own (rank order = canonical order).  Both exchanges are inside the timed step, which ends with the
+canonical list resident on rank 0; the row-sharded step without that gather is
+reported as a breakdown.  --split replicated: every rank holds the whole batch and keys every window
+(dist.kmer_split_step); --split rows: the row split.
 
 --config config5: config 5 at its stated shape (1M proteins, k = 5 + 7, BLOSUM, streamed row
 passes; bench_config5); N > 1 splits its rows over the ranks with no data-path collective.
@@ -78,7 +82,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="oracle threads of the all-cores run (0: every usable core)")
     ap.add_argument("--score", default="blosum", choices=["blosum", "count"], help="config5: edge score")
-    ap.add_argument("--split", default="kmer", choices=["kmer", "rows"], help="multi-GPU flow (N > 1)")
+    ap.add_argument("--split", default="kmer", choices=["kmer", "replicated", "rows"], help="multi-GPU flow (N > 1)")
     ap.add_argument("--direct-tail", type=int, default=1, help="config5: fused reduction writes edges in place (A/B)")
     ap.add_argument("--flat-heavy", type=int, default=1, help="config5: passes expand frequent k-mers by rows (A/B)")
     return ap.parse_args()
@@ -330,8 +334,8 @@ def bench_config5(args):
             out["cpu_baseline"] = config5_cpu_baseline(args.cpu_threads or usable_cores()["all"])
             # no published number: the ratio is to the reference's algorithm restated on
             # this box's host cores (a bounded sample of the same law, pairs/s)
-            out["vs_baseline"] = out["value"] / out["cpu_baseline"]["value"]
-            out["vs_baseline_of"] = "cpu_baseline.value (the oracle on a config-5-law sample, every usable host core)"
+            # vs_baseline stays null (no published number); the ratio to the CPU sample apart
+            out["vs_cpu_baseline"] = out["value"] / out["cpu_baseline"]["value"]
     print(json.dumps(out))
 
 
@@ -348,8 +352,8 @@ def main():
 
     import uniprot_kmer_based_clustering_amd as K
     from uniprot_kmer_based_clustering_amd import _lib
-    from uniprot_kmer_based_clustering_amd.device import DevicePipeline
-    from uniprot_kmer_based_clustering_amd.dist import distributed_step, kmer_split_step
+    from uniprot_kmer_based_clustering_amd.device import DevicePipeline, ShardPipeline
+    from uniprot_kmer_based_clustering_amd.dist import distributed_step, kmer_split_step, sharded_split_step
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -364,12 +368,20 @@ def main():
     _, seed, law, k = CONFIGS[args.config]
     proteins = load_batch(args.config)
     n = proteins.n
-    pipe = DevicePipeline(proteins, k, f"cuda:{local}")
+    sharded = world > 1 and args.split == "kmer"
+    if sharded:
+        # the start state of SURVEY.md §8e: this GPU holds its chunks' residues only (plus offsets
+        # and class ids); the host batch is generated whole by every rank, and only the slice moves
+        pipe = ShardPipeline(proteins.residues, proteins.offsets, proteins.class_id, k, rank, world, f"cuda:{local}")
+    else:
+        pipe = DevicePipeline(proteins, k, f"cuda:{local}")
     torch.cuda.synchronize()
     postings = args.engine in ("residues", "postings")
 
     def one_step(timings=None, gather=False):
-        if world > 1 and args.split == "kmer":
+        if sharded:
+            return sharded_split_step(pipe, rank, world, gather=gather, timings=timings)
+        if world > 1 and args.split == "replicated":
             return kmer_split_step(pipe, rank, world, gather=gather, timings=timings)
         if world > 1:
             return distributed_step(pipe, rank, world)
@@ -405,25 +417,35 @@ def main():
         # untimed: per-rank phase times and the step without the gather (the breakdown)
         ne = torch.tensor([n_edges], dtype=torch.int64, device=f"cuda:{local}")
         dist.broadcast(ne, 0)  # rank 0 holds the whole list: its count is the total
-        if args.split == "kmer":
-            stt = pipe._split_state.bufs[3].clone()
+        if args.split in ("kmer", "replicated"):
+            step_fn = sharded_split_step if sharded else kmer_split_step
+            st_ = pipe._split_state
+            stt = st_.bufs[3].clone()
             dist.all_reduce(stt)  # every rank's k-mers' statistics: the batch's
             split_stats = [int(x) for x in stt.tolist()]
             tims = []
             for _ in range(5):
-                kmer_split_step(pipe, rank, world, timings=tims)
+                step_fn(pipe, rank, world, timings=tims)
             ph = torch.tensor(np.mean(np.array(tims), axis=0), dtype=torch.float64, device=f"cuda:{local}")
             lo, hi = (int(x) for x in _lib.row_split(n, world)[rank:rank + 2])
-            mine = torch.tensor([rank, lo, hi, n_edges, *ph.tolist()], dtype=torch.float64, device=f"cuda:{local}")
+            # bytes this rank sends to the other ranks per step (equal splits: its own region stays)
+            kx = (world - 1) * st_.kcap * 8 if sharded else 0
+            px = (world - 1) * st_.cap * 8
+            res_mb = pipe.res.numel() / 1e6
+            mine = torch.tensor([rank, lo, hi, n_edges, kx, px, res_mb, *ph.tolist()], dtype=torch.float64,
+                                device=f"cuda:{local}")
             allv = [torch.zeros_like(mine) for _ in range(world)]
             dist.all_gather(allv, mine)
-            rank_info = [dict(zip(("rank", "row_lo", "row_hi", "edges", "expand_ms", "exchange_ms", "edges_ms"),
-                                  [int(v) if i < 4 else v for i, v in enumerate(x.tolist())])) for x in allv]
+            names = (("rank", "row_lo", "row_hi", "edges", "key_exchange_bytes", "pair_exchange_bytes",
+                      "residues_resident_MB") +
+                     (("keys_ms", "key_exchange_ms", "group_ms", "pair_exchange_ms", "edges_ms") if sharded else
+                      ("expand_ms", "exchange_ms", "edges_ms")))
+            rank_info = [dict(zip(names, [int(v) if i < 6 else v for i, v in enumerate(x.tolist())])) for x in allv]
             dist.barrier()
             torch.cuda.synchronize()
             g0 = time.perf_counter()
             for _ in range(5):
-                kmer_split_step(pipe, rank, world, gather=False)
+                step_fn(pipe, rank, world, gather=False)
             torch.cuda.synchronize()
             dist.barrier()
             t = torch.tensor([(time.perf_counter() - g0) / 5 * 1e3], dtype=torch.float64, device=f"cuda:{local}")
@@ -454,8 +476,10 @@ def main():
                        "proteins": n, "k": k, "pairs": int(pairs_total), "edges": int(n_edges),
                        "engine": args.engine,
                        "parallelism": ("single GPU" if world == 1 else
-                                       f"k-mer split x{world} (all-to-all of pair keys)" if args.split == "kmer"
-                                       else f"row split x{world}")},
+                                       f"k-mer split x{world}, sharded start (all-to-all of keys, then of pair keys)"
+                                       if args.split == "kmer" else
+                                       f"k-mer split x{world}, replicated start (all-to-all of pair keys)"
+                                       if args.split == "replicated" else f"row split x{world}")},
             "edges_per_s": n_edges / (dt / args.steps),
         }
         if rank_info is not None:
@@ -469,7 +493,11 @@ def main():
             out["roofline"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
                                "frac": ach / (HBM_PEAK_GBS * world), "traffic": None,
                                "kernel": f"whole step over {world} GPUs", "alg_bytes_per_step": byts,
-                               "incidences": n_inc, "exchange_bytes": 8 * n_inc}
+                               "incidences": n_inc,
+                               # algorithmic exchange bytes: one 8-B key per window (sharded start) and
+                               # one 8-B pair key per incidence, the (N-1)/N of them that leave a rank
+                               "exchange_bytes": int((8 * n_win * (1 if sharded else 0) + 8 * n_inc)
+                                                     * (world - 1) / world)}
             out["ranks"] = rank_info
             out["step_without_gather_ms"] = no_gather_ms
             out["gather_ms"] = ms - no_gather_ms
@@ -512,8 +540,9 @@ def main():
         out["cpu_baseline"] = cpu_baseline(proteins, k, args.cpu_threads)
         # the reference has no published number: the ratio is to its algorithm
         # restated on this box's host cores, measured in this run
-        out["vs_baseline"] = out["value"] / out["cpu_baseline"]["value"]
-        out["vs_baseline_of"] = "cpu_baseline.value (the oracle over the same workload on every usable host core)"
+        # vs_baseline stays null: BASELINE.md holds no published number for this metric; the ratio to
+        # the reference's algorithm restated on this box's host cores is reported apart
+        out["vs_cpu_baseline"] = out["value"] / out["cpu_baseline"]["value"]
     if rank == 0:
         print(json.dumps(out))
     if world > 1:

@@ -226,3 +226,111 @@ def test_row_split_balance():
         total = n * (n - 1) // 2
         assert sum(pairs) == total
         assert max(abs(x - total / parts) for x in pairs) <= n
+
+
+class OracleShardPipe(OracleSplitPipe):
+    """CPU stand-in for the sharded start's stages (ShardPipeline).  split_keys: rank `part` holds
+    proteins [part N / parts, (part + 1) N / parts) and sends every window (code, p) of them to the
+    rank owning the code's bin (code mod parts here), region d = [count, keys...] of kcap words;
+    split_group: the received windows grouped by code, df = distinct proteins, every pair (p < q)
+    of a code with different classes one incidence key p << bits(N) | q routed to its row owner;
+    the keys phase's overflow (RERUN, MAX_KEYS) merged into the flags, as the library does."""
+
+    def __init__(self, b, o, cap, part, parts):
+        P, Q, W = o.pairs()
+        super().__init__(b.n, P, Q, W, cap)
+        self.cls = np.asarray(b.class_id)
+        self.part, self.parts = part, parts
+        codes, woff = o.codes(), o.win_off()
+        lo, hi = part * b.n // parts, (part + 1) * b.n // parts
+        self.win = [(int(c), p) for p in range(lo, hi) for c in codes[woff[p]:woff[p + 1]]]
+        self.kflags = (0, 0)
+
+    def split_keys(self, part, parts, kcap, ksend, flags):
+        need = 0
+        ksend.fill_(0)
+        for d in range(parts):
+            mine = [(c << 32) | p for c, p in self.win if c % parts == d]
+            need = max(need, len(mine) + 1)
+            if len(mine) + 1 <= kcap:
+                ksend[d * kcap] = len(mine)
+                ksend[d * kcap + 1:d * kcap + 1 + len(mine)] = torch.tensor(mine, dtype=torch.int64)
+            else:
+                ksend[d * kcap] = 0  # dropped: the receiver reads nothing, the flags rerun the step
+        self.kflags = (int(need > kcap), need)
+
+    def split_group(self, krecv, kcap, part, parts, cap, send, flags, stats, learn=None, require_class_diff=True):
+        from uniprot_kmer_based_clustering_amd import _lib
+        from uniprot_kmer_based_clustering_amd.dist import row_ranges
+        x = krecv.numpy()
+        groups = {}
+        for s in range(parts):
+            m = int(x[s * kcap])
+            for v in x[s * kcap + 1:s * kcap + 1 + m]:
+                groups.setdefault(int(v) >> 32, set()).add(int(v) & 0xFFFFFFFF)
+        keys = []
+        for ps in groups.values():
+            ps = sorted(ps)
+            for i, p in enumerate(ps):
+                for q in ps[i + 1:]:
+                    if not require_class_diff or self.cls[p] != self.cls[q]:
+                        keys.append((p << self.pbits) | q)
+        keys = np.array(keys, dtype=np.int64)
+        send.fill_(-1)
+        most = 0
+        for d, (lo, hi) in enumerate(row_ranges(self.n, parts)):
+            kd = keys[((keys >> self.pbits) >= lo) & ((keys >> self.pbits) < hi)]
+            most = max(most, len(kd))
+            send[d * cap:d * cap + min(cap, len(kd))] = torch.from_numpy(kd[:cap].copy())
+        flags.zero_()
+        flags[_lib.KMP_SPLIT_MAX_PART] = most
+        flags[_lib.KMP_SPLIT_MAX_KEYS] = self.kflags[1]
+        flags[_lib.KMP_SPLIT_RERUN] = int(most > cap or self.kflags[0])
+        stats.zero_()
+        stats[6] = len(keys)
+
+
+def shard_worker(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, ROOT)
+        from uniprot_kmer_based_clustering_amd.dist import SplitState, sharded_split_step
+        b, o = build_case()
+        P, Q, W = o.pairs()
+        pipe = OracleShardPipe(b, o, cap=16 if rank == 0 else 1 << 20, part=rank, parts=world)
+        state = SplitState()
+        state.cap, state.kcap = 64, 256  # far too small: the first step reruns with both learned
+        for ms in (1, 3):
+            n = sharded_split_step(pipe, rank, world, min_shared=ms, gather=True, state=state)
+            if rank == 0:
+                keep = W >= ms
+                ok = (n == int(keep.sum())
+                      and np.array_equal(pipe.ep[:n].numpy().view(np.uint32), P[keep])
+                      and np.array_equal(pipe.eq[:n].numpy().view(np.uint32), Q[keep])
+                      and np.array_equal(pipe.ew[:n].numpy().view(np.uint32), W[keep]))
+                out_q.put(("sharded", ms, ok, n, state.reruns, state.cap, state.kcap))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_split_exchange(world):
+    """sharded_split_step over gloo: the key all-to-all (each rank's windows to their bins' owners),
+    the grouping, the pair-key all-to-all and the per-rank reduction give the canonical list
+    gathered on rank 0; undersized key and pair-key regions rerun with sizes learned from the
+    reduced flags (the same on every rank), and the learned sizes stay for the next step."""
+    port = free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=shard_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    msgs = [q.get(timeout=300) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert all(m[2] for m in msgs), msgs
+    assert msgs[0][4] >= 1 and msgs[0][5] > 64 and msgs[0][6] > 256
+    assert msgs[1][4] == msgs[0][4]  # the second step reran nothing

@@ -106,33 +106,40 @@ def sharded_ranks(b, k, g):
     per = []
     for r, (lo, hi) in enumerate(row_ranges(b.n, g)):
         p = pipes[r]
-        # keys and group back to back, as in a step (the group phase reads and resets the keys
-        # phase's cursors); device time split at an event between them
-        mid = []
-
-        def kg():
+        # the rank's whole step without its exchanges, back to back as in dist.sharded_split_step
+        # (keys, group, edges; the host's launches of a phase overlap the GPU's work of the one
+        # before, and the step ends with the edges phase's synchronisation); device time from
+        # events around the sequence, the phases split at events between them
+        def seq(ev=None):
+            if ev:
+                ev[0].record()
             p.split_keys(r, g, kcap, ksend[r], flags[r])
-            e = torch.cuda.Event(enable_timing=True)
-            e.record()
-            mid.append(e)
+            if ev:
+                ev[1].record()
             p.split_group(krecv[r], kcap, r, g, cap, sends[r], flags[r], stats[r])
-        t01, d01 = timed(kg)
-        ev0 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
-        d0 = 0.0
-        for a, b in ev0:
-            a.record()
-            p.split_keys(r, g, kcap, ksend[r], flags[r])
-            b.record()
-            p.split_group(krecv[r], kcap, r, g, cap, sends[r], flags[r], stats[r])
+            if ev:
+                ev[2].record()
+            p.split_edges(recvs[r], lo, hi)
+            if ev:
+                ev[3].record()
+        for _ in range(3):
+            seq()
         torch.cuda.synchronize()
-        d0 = sum(a.elapsed_time(b) for a, b in ev0) / len(ev0)
-        d1 = d01 - d0
-        t0, t1 = d0, t01 - d0
-        t2, d2 = timed(lambda: p.split_edges(recvs[r], lo, hi))
+        t0 = time.perf_counter()
+        for _ in range(10):
+            seq()
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t0) / 10 * 1e3
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(10)]
+        for ev in evs:
+            seq(ev)
+        torch.cuda.synchronize()
+        d0, d1, d2 = (sum(ev[i].elapsed_time(ev[i + 1]) for ev in evs) / len(evs) for i in range(3))
+        t0, t1, t2 = d0, d1, wall - d0 - d1
         # bytes this rank sends to the others in each exchange (its own region stays local)
         kbytes = (g - 1) * kcap * 8
         pbytes = (g - 1) * cap * 8
-        per.append({"rows": [lo, hi], "keys_ms": t0, "group_ms": t1, "edges_ms": t2, "ms": t0 + t1 + t2,
+        per.append({"rows": [lo, hi], "keys_ms": t0, "group_ms": t1, "edges_ms": t2, "ms": wall,
                     "dev_keys_ms": d0, "dev_group_ms": d1, "dev_edges_ms": d2, "dev_ms": d0 + d1 + d2,
                     "residue_slice_MB": p.res.numel() / 1e6, "key_exchange_MB": kbytes / 1e6,
                     "pair_exchange_MB": pbytes / 1e6, "key_cap": kcap, "pair_cap": cap,

@@ -600,7 +600,9 @@ __global__ void chunk_desc_kernel(const uint64_t* __restrict__ res_off, uint32_t
 // depends on the chunks only, never on the order of the atomics).  A piece that does not fit is
 // dropped with its counts (0) and raises kFlSend; the cursors still count it, so the rerun's
 // region size is exact.
-constexpr uint32_t kSendShards = 16;
+// 64 sub-regions: the returning reservation atomics of ~1,000 simultaneous chunks spread over 64 x
+// parts cursors (16 sub-regions: 46 us for a rank's keys at G = 8, 64: 36 us; 128: 35 us)
+constexpr uint32_t kSendShards = 64;
 struct SendL1 {
     unsigned long long* send;  // parts regions of cap u64 words
     uint64_t cap, tb;          // region size; run-table words (u64) at its start
@@ -610,12 +612,9 @@ struct SendL1 {
     uint64_t res_base, res_end;  // the residue slice [res_base, res_end) at res
 };
 // coarse bins [bin_lo(d), bin_lo(d + 1)) belong to rank d (the k-mer split's share), and bin t to
-// owner(t) = the largest d with bin_lo(d) <= t
+// owner(t) = the largest d with bin_lo(d) <= t = ((t + 1) parts - 1) / nb1
 __host__ __device__ __forceinline__ uint32_t split_bin_lo(uint32_t d, uint32_t nb1, uint32_t parts) {
     return (uint32_t)((uint64_t)d * nb1 / parts);
-}
-__device__ __forceinline__ uint32_t split_owner(uint32_t t, uint32_t nb1, uint32_t parts) {
-    return (uint32_t)(((uint64_t)(t + 1) * parts - 1) / nb1);
 }
 
 // waves per SIMD the persistent level 1 is compiled for (VGPR budget: 8 -> 64 registers and 24 B of
@@ -704,6 +703,9 @@ __global__ __launch_bounds__(kThr, KMP_L1P_WAVES) void bp_scatter1p_kernel(
     issue(dcur);
     const unsigned hs1 = dg.sh1 - lay.hshift;
     __shared__ uint32_t sd_base[kSend ? kSplitMax : 1], sd_start[kSend ? kSplitMax : 1];
+    __shared__ uint32_t s_blo[kSend ? kSplitMax + 1 : 1];  // first bin of each rank (split_bin_lo)
+    if (kSend)
+        for (uint32_t d = tid; d <= sl.parts; d += kThr) s_blo[d] = split_bin_lo(d, dg.nb1, sl.parts);
     while (true) {
         const uint32_t gc = kSend ? c + sl.c_lo : c;  // the chunk's index in the batch
         const uint64_t c0 = (uint64_t)gc * kKeyChunk, c1 = min(c0 + kKeyChunk, slots);
@@ -784,9 +786,11 @@ __global__ __launch_bounds__(kThr, KMP_L1P_WAVES) void bp_scatter1p_kernel(
         if (kSend) {
             // every digit is the call's (dlo = 0, dhi = nb1): rank d's piece is the chunk's keys of
             // its bins, contiguous in S; one reservation per destination
-            const uint32_t nb1 = dg.nb1;
+            const uint32_t nb1 = dg.nb1, l1 = __builtin_ctz(nb1);  // nb1 is a power of two
+            // owner(t) = ((t + 1) parts - 1) / nb1: a multiply and a shift per key (split_owner)
+            auto owner = [&](uint32_t t) { return ((t + 1) * sl.parts - 1) >> l1; };
             if (tid < sl.parts) {
-                const uint32_t b0 = split_bin_lo(tid, nb1, sl.parts), b1 = split_bin_lo(tid + 1, nb1, sl.parts);
+                const uint32_t b0 = s_blo[tid], b1 = s_blo[tid + 1];
                 const uint32_t s0 = b0 < nb1 ? lh[b0] : n_in, s1 = b1 < nb1 ? lh[b1] : n_in;
                 const uint32_t size = s1 - s0, shard = gc % kSendShards;
                 const uint32_t pos = size ? atomicAdd(&sl.kcur[tid * kSendShards + shard], size) : 0u;
@@ -805,15 +809,15 @@ __global__ __launch_bounds__(kThr, KMP_L1P_WAVES) void bp_scatter1p_kernel(
             for (uint32_t t = 0; t < kQ; ++t) {
                 const uint32_t dgt = tid + t * kThr;
                 if (dgt < nb1 && sl.sub) {
-                    const uint32_t d = split_owner(dgt, nb1, sl.parts);
+                    const uint32_t d = owner(dgt);
                     const bool fits = sd_base[d] != 0xFFFFFFFFu;
                     uint32_t* row = reinterpret_cast<uint32_t*>(sl.send + (uint64_t)d * sl.cap) + (uint64_t)c * sl.rowlen;
-                    row[1 + dgt - split_bin_lo(d, nb1, sl.parts)] = fits ? (lh[dgt] - sd_start[d]) << 16 | cnt[t] : 0u;
+                    row[1 + dgt - s_blo[d]] = fits ? (lh[dgt] - sd_start[d]) << 16 | cnt[t] : 0u;
                 }
             }
             for (uint32_t i = tid; i < n_in; i += kThr) {
                 const unsigned long long y = u.S[i];
-                const uint32_t d = split_owner((uint32_t)(y >> dg.sh1), nb1, sl.parts);
+                const uint32_t d = owner((uint32_t)(y >> dg.sh1));
                 const uint32_t b = sd_base[d];
                 if (b != 0xFFFFFFFFu) sl.send[(uint64_t)d * sl.cap + sl.tb + b + (i - sd_start[d])] = y;
             }
