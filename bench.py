@@ -72,7 +72,7 @@ def load_batch(name):
         return K.read_fasta(t.name)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None, help="timed steps (default 20; config5: 1)")
@@ -85,7 +85,7 @@ def parse():
     ap.add_argument("--split", default="kmer", choices=["kmer", "replicated", "rows"], help="multi-GPU flow (N > 1)")
     ap.add_argument("--direct-tail", type=int, default=1, help="config5: fused reduction writes edges in place (A/B)")
     ap.add_argument("--flat-heavy", type=int, default=1, help="config5: passes expand frequent k-mers by rows (A/B)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def cpu_model() -> str:
@@ -339,8 +339,10 @@ def bench_config5(args):
     print(json.dumps(out))
 
 
-def main():
-    args = parse()
+def main(argv=None, dist_mod=None):
+    """dist_mod (tests): a torch.distributed stand-in whose process group is already up (the GPU
+    test of this N > 1 path runs two ranks on one GPU over gloo through host copies)."""
+    args = parse(argv)
     if args.config == "config5":
         return bench_config5(args)
     if args.steps is None:
@@ -351,6 +353,9 @@ def main():
     import torch.distributed as dist
 
     import uniprot_kmer_based_clustering_amd as K
+    if dist_mod is not None:
+        import uniprot_kmer_based_clustering_amd.dist as D
+        dist = D.dist = dist_mod
     from uniprot_kmer_based_clustering_amd import _lib
     from uniprot_kmer_based_clustering_amd.device import DevicePipeline, ShardPipeline
     from uniprot_kmer_based_clustering_amd.dist import distributed_step, kmer_split_step, sharded_split_step
@@ -362,7 +367,7 @@ def main():
         print("run N>1 under torch.distributed.run (one process per GPU)", file=sys.stderr)
         sys.exit(2)
     torch.cuda.set_device(local)
-    if world > 1:
+    if world > 1 and dist_mod is None:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     _, seed, law, k = CONFIGS[args.config]
@@ -544,9 +549,10 @@ def main():
         # the reference's algorithm restated on this box's host cores is reported apart
         out["vs_cpu_baseline"] = out["value"] / out["cpu_baseline"]["value"]
     if rank == 0:
-        print(json.dumps(out))
-    if world > 1:
+        print(json.dumps(out), flush=True)
+    if world > 1 and dist_mod is None:
         dist.destroy_process_group()
+    return out
 
 
 if __name__ == "__main__":
