@@ -121,6 +121,28 @@ class _SplitEdges:
             return self.n_edges
         raise RuntimeError("edge count unstable across reruns")
 
+    def last_layout(self) -> str:
+        """Layout of the last postings call: 'bucketed' (LDS group + expand per hash bucket,
+        frequent k-mers on the heavy path) or 'flat' (the fallback for very wide class ids)."""
+        return "flat" if lib().kmp_postings_last_layout(self._workspace()) == _lib.KMP_LAYOUT_FLAT else "bucketed"
+
+    def last_heavy(self) -> bool:
+        """Whether the last call spilled frequent k-mers (df > 128) to the heavy path."""
+        return lib().kmp_postings_last_layout(self._workspace()) == _lib.KMP_LAYOUT_BUCKETED_HEAVY
+
+    def last_tail(self) -> str:
+        """How the last postings call reduced its pair keys: 'fast' (fixed row-block regions, LDS
+        hash-aggregate + rank, edges written at look-back offsets), 'rows' (the counting row-block
+        tail: histogram, scan, scatter, block sort, emit) or 'sort' (global pair-key sort, flat
+        layout)."""
+        if self.last_layout() == "flat":
+            return "sort"
+        return "fast" if lib().kmp_postings_last_tail(self._workspace()) == _lib.KMP_TAIL_FAST else "rows"
+
+    def overflow_blocks(self) -> int:
+        """Row blocks of the last call above the LDS capacity (finished by the segmented sort)."""
+        return int(lib().kmp_postings_last_overflow_blocks(self._workspace()))
+
     def edges(self):
         n = self.n_edges
         return (self.ep[:n].cpu().numpy().view(np.uint32), self.eq[:n].cpu().numpy().view(np.uint32),
@@ -337,32 +359,10 @@ class DevicePipeline(_SplitEdges):
     def graph_replays(self) -> int:
         return int(lib().kmp_postings_graph_replays(self._workspace()))
 
-    def last_layout(self) -> str:
-        """Layout of the last postings call: 'bucketed' (LDS group + expand per hash bucket,
-        frequent k-mers on the heavy path) or 'flat' (the fallback for very wide class ids)."""
-        return "flat" if lib().kmp_postings_last_layout(self._workspace()) == _lib.KMP_LAYOUT_FLAT else "bucketed"
-
-    def last_heavy(self) -> bool:
-        """Whether the last call spilled frequent k-mers (df > 128) to the heavy path."""
-        return lib().kmp_postings_last_layout(self._workspace()) == _lib.KMP_LAYOUT_BUCKETED_HEAVY
-
     def set_tail(self, mode: str = "fast") -> None:
         """Row-block tail of unscored calls: 'fast' (default, where it applies) or 'count'."""
         m = {"fast": _lib.KMP_TAIL_FAST, "count": _lib.KMP_TAIL_COUNT}[mode]
         check(lib().kmp_postings_set_tail(self._workspace(), m), "kmp_postings_set_tail")
-
-    def last_tail(self) -> str:
-        """How the last postings call reduced its pair keys: 'fast' (fixed row-block regions, LDS
-        hash-aggregate + rank, edges written at look-back offsets), 'rows' (the counting row-block
-        tail: histogram, scan, scatter, block sort, emit) or 'sort' (global pair-key sort, flat
-        layout)."""
-        if self.last_layout() == "flat":
-            return "sort"
-        return "fast" if lib().kmp_postings_last_tail(self._workspace()) == _lib.KMP_TAIL_FAST else "rows"
-
-    def overflow_blocks(self) -> int:
-        """Row blocks of the last call above the LDS capacity (finished by the segmented sort)."""
-        return int(lib().kmp_postings_last_overflow_blocks(self._workspace()))
 
     def rows(self, row_lo: int, row_hi: int, min_shared: int = 1, require_class_diff: bool = True,
              heavy_df: int = 0xFFFFFFFF) -> int:
