@@ -430,14 +430,14 @@ def main(argv=None, dist_mod=None):
             split_stats = [int(x) for x in stt.tolist()]
             tims = []
             for _ in range(5):
-                step_fn(pipe, rank, world, timings=tims)
+                own_edges = step_fn(pipe, rank, world, timings=tims)  # without the gather: this rank's rows
             ph = torch.tensor(np.mean(np.array(tims), axis=0), dtype=torch.float64, device=f"cuda:{local}")
             lo, hi = (int(x) for x in _lib.row_split(n, world)[rank:rank + 2])
             # bytes this rank sends to the other ranks per step (equal splits: its own region stays)
             kx = (world - 1) * st_.kcap * 8 if sharded else 0
             px = (world - 1) * st_.cap * 8
             res_mb = pipe.res.numel() / 1e6
-            mine = torch.tensor([rank, lo, hi, n_edges, kx, px, res_mb, *ph.tolist()], dtype=torch.float64,
+            mine = torch.tensor([rank, lo, hi, own_edges, kx, px, res_mb, *ph.tolist()], dtype=torch.float64,
                                 device=f"cuda:{local}")
             allv = [torch.zeros_like(mine) for _ in range(world)]
             dist.all_gather(allv, mine)

@@ -481,6 +481,8 @@ static int split_expand_impl(kmp_postings* ws, const SplitSrc& src, uint32_t n, 
         }
         unbind();
         if (kcur && routed_done) ws->kcur_dirty = false;
+        ws->last_bucketed = true;
+        ws->last_heavy = true;
         if (rc == KMP_OK && !routed_done) {
             // every attempt grew the spill regions: no keys are sent and the flags ask every rank for
             // a rerun, so the ranks stay in lockstep through the collectives (an error returned here
@@ -505,6 +507,8 @@ static int split_expand_impl(kmp_postings* ws, const SplitSrc& src, uint32_t n, 
     const int rc = slot_launch(ws, ws->split_g[0], key, enqueue, st);
     unbind();
     if (kcur) ws->kcur_dirty = false;
+    ws->last_bucketed = true;
+    ws->last_heavy = false;
     return rc;
 }
 
@@ -696,6 +700,8 @@ int kmp_dev_split_edges(kmp_postings* ws, const unsigned long long* d_keys, uint
             continue;
         }
         uint64_t ne = rb[kRbRuns];
+        ws->last_fast = pt_fast(ws, g);
+        ws->last_ovf = (uint32_t)rb[kRbOvf];
         if (rb[kRbOvf] && !pt_rowhist_ok(g)) {  // row blocks above the LDS capacity: the segmented sort, fewer rows per block next time
             if (g.rbits > 0) {
                 const double over = (double)rb[kRbMaxBlock] / (0.8 * kPtCap);
