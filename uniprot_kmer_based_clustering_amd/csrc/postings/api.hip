@@ -658,7 +658,7 @@ int kmp_dev_split_edges(kmp_postings* ws, const unsigned long long* d_keys, uint
     c.d_w = d_w;
     c.cap = cap;
     c.stride = 1;
-    for (int attempt = 0; attempt < 2; ++attempt) {
+    for (int attempt = 0; attempt < 8; ++attempt) {
         PtGeom g;
         if (!pt_geometry(ws, c, m, &g)) return KMP_EINVAL;
         g.flat_n = m;  // the received regions, padded with kNoKey, read as one array
@@ -668,11 +668,14 @@ int kmp_dev_split_edges(kmp_postings* ws, const unsigned long long* d_keys, uint
         hipError_t e = hipSuccess;
         pt_bufs(ws, g, true, &e, st);
         PG(e);
-        PG(ws->inc.reserve(pt_fast(ws, g) ? std::max<uint64_t>(m, (uint64_t)g.nrb * g.ftcap / 2) : m));  // u32 row-block keys
+        // u32 row-block keys (the fast tail's fixed or learned regions)
+        PG(ws->inc.reserve(pt_fast(ws, g) ? std::max<uint64_t>(m, g.freg ? (ws->freg_total + 1) / 2
+                                                                        : (uint64_t)g.nrb * g.ftcap / 2)
+                                          : m));
         PG(ws->uniq.reserve(m));  // staged p | q (u32 each)
         PG(ws->w.reserve(m));
         PG(ws->ovf.reserve((uint64_t)g.nrb + 1));
-        PG(ws->small.reserve(16));
+        PG(small_reserve(ws, st));
         PG(ws->flags.reserve(kFlN));
         PG(ws->bstats.reserve(kGsWords));
         if (!ws->hrb) PG(hipHostMalloc((void**)&ws->hrb, kRbWords * sizeof(unsigned long long), hipHostMallocCoherent));
@@ -690,13 +693,14 @@ int kmp_dev_split_edges(kmp_postings* ws, const unsigned long long* d_keys, uint
         };
         const std::vector<unsigned long long> key = {m, n, row_lo, row_hi, c.min_shared, cap, (uintptr_t)d_keys,
                                                      (uintptr_t)d_p, (uintptr_t)d_q, (uintptr_t)d_w, g.rbits,
-                                                     ws->timing, ws->fast_tail};
+                                                     ws->timing, ws->fast_tail, g.freg ? ws->freg_total + 1 : 0};
         int rc = slot_launch(ws, ws->split_g[1], key, enqueue, st);
         if (rc != KMP_OK) return rc;
         PG(hipStreamSynchronize(st));
         const unsigned long long* rb = ws->hrb;
-        if (rb[kRbFast]) {  // a fast-tail region overflowed: the counting tail (learned until a new shape)
-            ws->fast_tail = false;
+        if (rb[kRbFast]) {  // a fast-tail region overflowed: learned regions, then the counting tail
+            const int rc = fast_overflow(ws, g, rb, st);
+            if (rc != KMP_OK) return rc;
             continue;
         }
         uint64_t ne = rb[kRbRuns];

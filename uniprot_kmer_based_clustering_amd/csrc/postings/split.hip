@@ -82,13 +82,22 @@ __global__ void split_pad_finish_kernel(unsigned long long* __restrict__ send, u
     // walking the parts x kShards cursors took 45 us at G = 8)
     const uint32_t t = threadIdx.x;
     __shared__ unsigned long long s_red[4][256 / 64];
-    if (t < kStN) {
-        unsigned long long v = 0;
-        for (int sh = 0; sh < kShards; ++sh) {
-            const unsigned long long x = gstats[sh * 8 + t];
-            v = t == kStMaxDf ? max(v, x) : v + x;
+    static_assert(kShards == 64 && kStN <= 8, "one wave per pair of statistics, a lane per shard");
+    {
+        // wave w (of 4) sums statistics w and w + 4 over the 64 shards (a lane per shard): every load
+        // in flight at once (one thread walking the shards serialised 64 dependent loads)
+        const uint32_t w = t >> 6, sh = t & 63;
+#pragma unroll
+        for (uint32_t j = 0; j < 2; ++j) {
+            const uint32_t st = w + 4 * j;
+            if (st >= kStN) continue;  // (uniform per wave)
+            unsigned long long v = gstats[sh * 8 + st];
+            for (int off = 32; off > 0; off >>= 1) {
+                const unsigned long long o = (unsigned long long)__shfl_xor(v, off);
+                v = st == kStMaxDf ? max(v, o) : v + o;
+            }
+            if (sh == 0) stats[st] = v;
         }
-        stats[t] = v;
     }
     unsigned long long shard = 0, spill = 0, part = 0;
     for (uint32_t sh = t; sh < kShards; sh += blockDim.x) {

@@ -67,6 +67,8 @@ bool pt_geometry(const kmp_postings* ws, const StepCfg& c, uint64_t inc, PtGeom*
     g->nprot = c.n;
     g->rowend = c.ranged ? c.row_hi : c.n;
     g->ftcap = kFtCap;
+    g->freg = ws->freg_on && ws->freg_geom == std::vector<unsigned long long>{rb, g->nrb, g->row0} ? ws->freg.p
+                                                                                                  : nullptr;
     // the bin sort for scored blocks only (unscored at config 3: 0.130 -> 0.387 ms);
     // KMP_BINSORT_MODE (A/B builds): 0 the radix sort everywhere, 2 the bin sort everywhere
     g->binsort = KMP_BINSORT_MODE == 2 ? 1 : KMP_BINSORT_MODE == 0 ? 0 : (g->sbits != 0);
@@ -158,6 +160,51 @@ BucketArgs bucket_args(kmp_postings* ws, const StepCfg& c, bool spill) {
     return a;
 }
 
+// ws->small (16 words), cleared when allocated (the fast tail's largest-block accumulator starts at 0)
+hipError_t small_reserve(kmp_postings* ws, hipStream_t st) {
+    hipError_t e = ws->small.reserve(16);
+    if (e == hipSuccess && ws->small_zero_p != ws->small.p) {
+        e = hipMemsetAsync(ws->small.p, 0, 16 * sizeof(uint32_t), st);
+        ws->small_zero_p = ws->small.p;
+    }
+    return e;
+}
+
+// A fast-tail region overflowed (kRbFast): learn the regions from this call's exact row-block counts
+// (the reduce kept them in counts[]: every key, dropped or not) with an eighth of slack, or first
+// fewer rows per block when a block is beyond what one reduce takes (kFtCap keys, unless its (row, q)
+// bins fit kFdBins); after kFregTries tries the counting tail for the shape
+constexpr uint32_t kFregTries = 3;
+int fast_overflow(kmp_postings* ws, const PtGeom& g, const unsigned long long* rb, hipStream_t st) {
+    if (ws->freg_tries >= kFregTries) {
+        ws->fast_tail = false;
+        ws->freg_on = false;
+        return KMP_OK;
+    }
+    ++ws->freg_tries;
+    const uint64_t most = rb[kRbMaxBlock];
+    const bool dense_ok = ((1ull << g.rbits) << g.pbits) <= kFdBins;
+    if (most > kFtCap && !dense_ok && g.rbits > 0) {
+        const double over = (double)most / (0.8 * kFtCap);
+        unsigned shrink = 1;
+        while (shrink < 16 && (double)(1u << shrink) < over) ++shrink;
+        ws->pt_rb_max = g.rbits > shrink ? g.rbits - shrink : 0u;
+        ws->freg_on = false;  // learned again on the new geometry if its blocks still overflow
+        return KMP_OK;
+    }
+    hipError_t e = hipSuccess;
+    const PtBufs b = pt_bufs(ws, g, false, &e);
+    PG(ws->freg.reserve((uint64_t)g.nrb + 1));
+    vreg_kernel<<<1, 1024, 0, st>>>(b.counts, g.nrb, ws->freg.p);  // the same rule as the bucket regions
+    uint32_t tot = 0;
+    PG(hipMemcpyAsync(&tot, ws->freg.p + g.nrb, 4, hipMemcpyDeviceToHost, st));
+    PG(hipStreamSynchronize(st));
+    ws->freg_total = tot;
+    ws->freg_on = true;
+    ws->freg_geom = {g.rbits, g.nrb, g.row0};
+    return KMP_OK;
+}
+
 // buffers of one step (reserved before any launch, so a capture allocates nothing)
 int step_reserve(kmp_postings* ws, const StepCfg& c, const PtGeom& g, hipStream_t st) {
     if (ws->shard_cap < ws->shard_floor) ws->shard_cap = ws->shard_floor;
@@ -167,12 +214,13 @@ int step_reserve(kmp_postings* ws, const StepCfg& c, const PtGeom& g, hipStream_
     PG(ws->flags.reserve(kFlN));
     PG(ws->cnt.reserve(2 * ((uint64_t)1 << c.lay.bbits) + 2));
     PG(ws->bstats.reserve(kGsWords));
-    PG(ws->small.reserve(16));  // [1] run count, [2] largest row block
+    PG(small_reserve(ws, st));  // [1] run count, [2] largest row block, [3] its accumulator (fast tail)
     PG(ws->inc_sorted.reserve(total));
     if (!c.expand_only) {  // an expand-only call leaves the tail (and its staging) to tail_multi
         // u32 row-block keys (pt_scatter; the fast tail's fixed regions) ...
-        PG(ws->inc.reserve(pt_fast(ws, g) ? std::max<uint64_t>(total, (uint64_t)g.nrb * g.ftcap / 2)
-                                                         : total));
+        PG(ws->inc.reserve(pt_fast(ws, g) ? std::max<uint64_t>(total, g.freg ? (ws->freg_total + 1) / 2
+                                                                                 : (uint64_t)g.nrb * g.ftcap / 2)
+                                          : total));
         PG(ws->uniq.reserve(total));  // ... staged p | q (u32 each)
         PG(ws->w.reserve(total));     // ... staged w
         if (c.sb) PG(ws->stg2.reserve(2 * total));  // ... staged scores | second-k weights
@@ -257,7 +305,7 @@ int enqueue_tail_in(kmp_postings* ws, const StepCfg& c, const PtGeom& g, const u
         pt_reduce_fast_kernel<<<g.nrb, kFtThreads, 0, st>>>(keys32, b.fcur, g, b.lb, b.ticket, c.d_p, c.d_q, c.d_w,
                                                              c.cap, c.stride,
                                                              PtPack{ws->bstats.p, ws->flags.p, nullptr, ws->hrb},
-                                                             ws->small.p + 1);
+                                                             ws->small.p + 1, b.counts);
         ws->mark(5, st);
         ws->mark(6, st);
         PG(hipGetLastError());
@@ -762,6 +810,8 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
         ws->bp_J_min = 0;
         ws->heavy = false;
         ws->cur_on = ws->cur_mode;
+        ws->freg_on = false;
+        ws->freg_tries = 0;
     }
     if (ws->shard_cap == 0) ws->shard_cap = c.slots / 4 / kShards + 4096;
     if (ws->spill_cap == 0) ws->spill_cap = 1024;
@@ -794,8 +844,9 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
             key.push_back(ws->fast_tail);
             key.push_back(ws->large_grid);
             key.push_back(ws->vreg_on ? ws->vreg_total + 1 : 0);
+            key.push_back(g.freg ? ws->freg_total + 1 : 0);
             int rc = fused_launch(ws, make_keys, key, c, g, st);
-            key.resize(key.size() - 9);
+            key.resize(key.size() - 10);
             if (rc != KMP_OK) return rc;
             PG(hipStreamSynchronize(st));
         } else {
@@ -903,11 +954,15 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
             if (rc != KMP_OK) return rc;
             PG(hipStreamSynchronize(st));
         }
-        if (rb[kRbFast]) {  // a fast-tail row-block region overflowed: the counting tail for this shape
-            if (debug) fprintf(stderr, "kmp: fast tail region overflow (rows per block %u): counting tail\n", 1u << g.rbits);
-            ws->fast_tail = false;
+        if (rb[kRbFast]) {  // a fast-tail row-block region overflowed: learned regions (or fewer rows per block)
+            if (debug)
+                fprintf(stderr, "kmp: fast tail region overflow (rows per block %u, largest block %llu, try %u)\n",
+                        1u << g.rbits, rb[kRbMaxBlock], ws->freg_tries);
+            int rc = fast_overflow(ws, g, rb, st);
+            if (rc != KMP_OK) return rc;
             continue;
         }
+        if (pt_fast(ws, g)) ws->freg_tries = 0;  // a call whose regions held
         ws->pt_inc = n_inc;  // sizes the next call's row blocks
         ws->last_fast = pt_fast(ws, g);
         ws->vreg_tries = 0;  // a call without a region overflow
@@ -1025,7 +1080,7 @@ int tail_multi(kmp_postings* const* ws, uint32_t nk, const StepCfg& c, const uin
         PG(w0->stg2.reserve(2 * total));
     }
     PG(w0->ovf.reserve((uint64_t)g.nrb + 1));
-    PG(w0->small.reserve(16));
+    PG(small_reserve(w0, st));
     hipError_t e = hipSuccess;
     const PtBufs b = pt_bufs(w0, g, true, &e, st);
     PG(e);
@@ -1174,7 +1229,7 @@ int tail(kmp_postings* ws, const unsigned long long* in, unsigned long long n_in
     PG(ws->inc_sorted.reserve(n_inc));
     PG(ws->uniq.reserve(n_inc));
     PG(ws->w.reserve(n_inc));
-    PG(ws->small.reserve(16));
+    PG(small_reserve(ws, st));
     const bool filter_w = min_shared > 1;
     if (filter_w) {
         PG(ws->keep.reserve(n_inc));

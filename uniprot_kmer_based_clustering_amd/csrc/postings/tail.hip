@@ -261,6 +261,18 @@ __global__ __launch_bounds__(kFtScThreads) void pt_scatter_capped_kernel(const u
 #pragma unroll
     for (uint32_t t = 0; t < kQ; ++t)  // reserved while the tile is placed
         rbase[t] = cnt[t] ? atomicAdd(&cur[threadIdx.x + t * kThr], cnt[t]) : 0u;
+    // block r's region: [r * ftcap, (r + 1) * ftcap), or the learned [freg[r], freg[r + 1]); a run
+    // that does not fit is dropped whole (the cursor still counts it: the reduce flags the block)
+    uint32_t rabs[kQ];
+#pragma unroll
+    for (uint32_t t = 0; t < kQ; ++t) {
+        const uint32_t r = threadIdx.x + t * kThr;
+        rabs[t] = 0xFFFFFFFFu;
+        if (cnt[t]) {
+            const uint32_t b0 = g.freg ? g.freg[r] : r * g.ftcap, cp = g.freg ? g.freg[r + 1] - b0 : g.ftcap;
+            if (rbase[t] + cnt[t] <= cp) rabs[t] = b0 + rbase[t];
+        }
+    }
 #pragma unroll
     for (uint32_t e = 0; e < kPer; ++e)
         if (x[e] != kNoKey) {
@@ -272,13 +284,14 @@ __global__ __launch_bounds__(kFtScThreads) void pt_scatter_capped_kernel(const u
 #pragma unroll
     for (uint32_t t = 0; t < kQ; ++t) {
         const uint32_t r = threadIdx.x + t * kThr;
-        if (r < g.nrb) lh[r] = rbase[t] - lh[r];  // in-region offset of the tile's run, minus its staging start
+        // the run's position in out minus its staging start (all ones: dropped)
+        if (r < g.nrb) lh[r] = rabs[t] == 0xFFFFFFFFu ? 0xFFFFFFFFu : rabs[t] - lh[r];
     }
     __syncthreads();
     const uint32_t placed = s_n;
     for (uint32_t i = threadIdx.x; i < placed; i += kThr) {
-        const uint32_t r = SR[i], pos = lh[r] + i;
-        if (pos < g.ftcap) out[(uint64_t)r * g.ftcap + pos] = S[i];
+        const uint32_t a = lh[SR[i]];
+        if (a != 0xFFFFFFFFu) out[a + i] = S[i];
     }
 }
 
@@ -1119,6 +1132,15 @@ __device__ void step_pack_body(const unsigned long long* __restrict__ gstats, co
 //                     the call on the counting tail and keeps it for the shape.
 // The last block writes the edge count and the step's read-back.
 constexpr uint32_t kFtThreads = 512, kFtHashMax = 6144, kFtSlots = 8192, kFtRowsMax = 1024, kFtRankMax = 256;
+// a block above kFtCap keys (a learned region: rows pairing with thousands of later proteins, the
+// reference's uniprot_arg at k = 5) is counted in LDS bins over (row, q): up to kFdBins bins (u16
+// counts, two per word, 64 KB aliased on the hash table), so the bins are the canonical order
+constexpr uint32_t kFdBins = 32768, kFdWords = kFdBins / 2;
+// thread t owns the contiguous words [t q, t q + q) (q = 2^qs); stored XOR-swizzled so the owners'
+// reads of their words hit distinct banks
+__device__ __forceinline__ uint32_t fd_phys(uint32_t w, unsigned qs) {
+    return w ^ ((w >> qs) & ((1u << min(qs, 5u)) - 1));
+}
 constexpr uint32_t kFtEmpty = 0xFFFFFFFFu;
 constexpr unsigned long long kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbOvf = 1ull << 61;
 static_assert(kFtCap == 16 * kFtThreads && kFtHashMax <= 12 * kFtThreads && kFtSlots == 16 * kFtThreads,
@@ -1185,6 +1207,7 @@ struct FtLds {
                                        // sort path's run heads use C[0, nruns] (nruns <= kFtCap)
         } h;
         typename PtSort<16>::storage_type s16;
+        uint32_t W[kFdWords];  // dense block: u16 counts per (row, q) bin, two per word
     };
     uint32_t RC[kFtRowsMax + 1];  // pairs per row -> row starts
     uint32_t last[kFtThreads];
@@ -1201,7 +1224,8 @@ __global__ __launch_bounds__(kFtThreads) void pt_reduce_fast_kernel(const uint32
                                                                     uint32_t* __restrict__ d_q,
                                                                     uint32_t* __restrict__ d_w, uint64_t cap,
                                                                     uint32_t stride, PtPack pack,
-                                                                    uint32_t* __restrict__ runs) {
+                                                                    uint32_t* __restrict__ runs,
+                                                                    uint32_t* __restrict__ counts) {
     __shared__ FtLds u;
     __shared__ uint32_t s_r, s_n;
     const uint32_t tid = threadIdx.x;
@@ -1224,11 +1248,90 @@ __global__ __launch_bounds__(kFtThreads) void pt_reduce_fast_kernel(const uint32
     for (uint32_t i = tid; i <= R; i += kFtThreads) u.RC[i] = 0;
     __syncthreads();
     const uint32_t r = s_r, nraw = s_n;
-    const bool ovf = nraw > kFtCap;
+    // the block's region; its exact count is kept (counts[r]) so an overflowing call can learn the
+    // regions, and the largest block goes to the read-back (runs[2] -> kRbMaxBlock)
+    const uint32_t rb0 = g.freg ? g.freg[r] : r * kFtCap, rcap = g.freg ? g.freg[r + 1] - rb0 : kFtCap;
+    if (tid == 0) {
+        counts[r] = nraw;
+        if (nraw) atomicMax(&runs[2], nraw);
+    }
+    // a block above kFtCap keys takes the dense bins when (row, q) fits them
+    const uint32_t fd_words = (R << pb) / 2;
+    const bool dense_ok = (R << pb) <= kFdBins && (R << pb) >= 2;
+    bool ovf = nraw > rcap || (nraw > kFtCap && !dense_ok);
     const uint32_t n = ovf ? 0u : nraw;
-    const uint32_t* src = keys + (uint64_t)r * kFtCap;  // g.ftcap == kFtCap in this mode
+    const uint32_t* src = keys + rb0;
     uint32_t D = 0;  // the block's kept pairs
     bool sort = n > kFtHashMax, published = false;
+    if (n > kFtCap) {
+        // ---- dense block: counts in (row, q) bins, read back in bin order ----
+        unsigned qs = 0;  // q = 2^qs words per thread (at least one)
+        while ((kFtThreads << qs) < fd_words) ++qs;
+        for (uint32_t i = tid; i < fd_words; i += kFtThreads) u.W[i] = 0;
+        __syncthreads();
+        for (uint32_t i0 = 0; i0 < n; i0 += 8 * kFtThreads) {  // loads in batches ahead of their atomics
+            uint32_t x[8];
+#pragma unroll
+            for (uint32_t e = 0; e < 8; ++e) {
+                const uint32_t i = i0 + e * kFtThreads + tid;
+                x[e] = i < n ? src[i] : kFtEmpty;
+            }
+#pragma unroll
+            for (uint32_t e = 0; e < 8; ++e)
+                if (x[e] != kFtEmpty) {
+                    const uint32_t sh = 16 * (x[e] & 1u);
+                    const uint32_t old = atomicAdd(&u.W[fd_phys(x[e] >> 1, qs)], 1u << sh);
+                    if (((old >> sh) & 0xFFFFu) >= 0xFFFEu) u.s_flag = 1;
+                }
+        }
+        __syncthreads();
+        const bool fov = u.s_flag != 0;  // (uniform) a count would pass 16 bits: flagged, nothing written
+        const uint32_t qn = 1u << qs, w0 = tid << qs;
+        uint32_t kept = 0;
+        if (!fov)
+            for (uint32_t j = 0; j < qn && w0 + j < fd_words; ++j) {
+                const uint32_t v = u.W[fd_phys(w0 + j, qs)];
+                kept += ((v & 0xFFFFu) >= g.min_shared) + ((v >> 16) >= g.min_shared);
+            }
+        uint32_t excl;
+        block_scan_n<kFtThreads>(kept, excl, D, u.wave_tot);
+        if (tid < 64) {
+            const unsigned long long ex = ft_lookback(lb, r, (unsigned long long)D | (fov ? kLbOvf : 0ull));
+            if (tid == 0) u.s_excl = ex;
+        }
+        __syncthreads();
+        const unsigned long long ex = u.s_excl;
+        uint64_t o = (uint32_t)ex + (uint64_t)excl;
+        const uint32_t rowbase = g.row0 + (r << g.rbits), qm = (1u << pb) - 1;
+        if (kept)
+            for (uint32_t j = 0; j < qn && w0 + j < fd_words; ++j) {
+                const uint32_t v = u.W[fd_phys(w0 + j, qs)];
+#pragma unroll
+                for (uint32_t h = 0; h < 2; ++h) {
+                    const uint32_t c = h ? v >> 16 : v & 0xFFFFu;
+                    if (c < g.min_shared || c == 0) continue;
+                    const uint32_t bin = 2 * (w0 + j) + h;
+                    if (o < cap) {
+                        d_p[o * stride] = rowbase + (bin >> pb);
+                        d_q[o * stride] = bin & qm;
+                        d_w[o * stride] = c;
+                    }
+                    ++o;
+                }
+            }
+        ovf = fov;
+        sort = false;
+        if (r + 1 == gridDim.x) {  // the last block: the edge count and the read-back
+            const bool any_ovf = ovf || (ex & kLbOvf);
+            if (tid == 0) {
+                runs[0] = (uint32_t)ex + D;
+                runs[1] = atomicExch(&runs[2], 0u);  // the largest block, reset for the next call
+            }
+            __syncthreads();
+            if (pack.rb) step_pack_body(pack.gstats, pack.flags, runs, pack.rb, any_ovf ? 1ull : 0ull);
+        }
+        return;
+    }
     if (!sort) {
         // ---- hash aggregation: pair -> slot, count per slot (the table was cleared above) ----
         uint32_t x[12];
@@ -1389,7 +1492,7 @@ __global__ __launch_bounds__(kFtThreads) void pt_reduce_fast_kernel(const uint32
         const bool any_ovf = ovf || (ex & kLbOvf);
         if (tid == 0) {
             runs[0] = (uint32_t)(o + D);
-            runs[1] = 0;
+            runs[1] = atomicExch(&runs[2], 0u);  // the largest block, reset for the next call
         }
         __syncthreads();
         if (pack.rb) step_pack_body(pack.gstats, pack.flags, runs, pack.rb, any_ovf ? 1ull : 0ull);
