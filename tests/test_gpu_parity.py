@@ -348,17 +348,21 @@ def test_rowtail_overflow_blocks(oracle_mod):
             seqs2 = seqs[1:] + seqs[:1]
             res, off, cls = make_batch(seqs2, ["b"] * 220 + ["a"])
             p, q, w = oracle_mod.Oracle(res, off, cls, k=7, threads=8).pairs()
-        pipe = DevicePipeline(K.Proteins(res, off, cls), 7, "cuda:0")
-        for it in range(3):
-            m = pipe.step(engine="residues")
-            torch.cuda.synchronize()
-            # the long row passes a fast-tail region: the counting tail (learned for the shape)
-            assert pipe.last_tail() == ("rows" if long_first else "fast") and m == len(p)
-            if it == 0:
-                assert (pipe.overflow_blocks() > 0) == long_first
-            np.testing.assert_array_equal(pipe.edges()[0], p)
-            np.testing.assert_array_equal(pipe.edges()[1], q)
-            np.testing.assert_array_equal(pipe.edges()[2], w)
+        for tail in ("count", "fast"):
+            pipe = DevicePipeline(K.Proteins(res, off, cls), 7, "cuda:0")
+            pipe.set_tail(tail)
+            for it in range(3):
+                m = pipe.step(engine="residues")
+                torch.cuda.synchronize()
+                # counting tail: the long row's block is listed and sorted; fast tail: the long row
+                # passes its fixed region, the regions are learned and its block is counted in
+                # (row, q) bins
+                assert pipe.last_tail() == ("rows" if tail == "count" else "fast") and m == len(p)
+                if it == 0:
+                    assert (pipe.overflow_blocks() > 0) == (long_first and tail == "count")
+                np.testing.assert_array_equal(pipe.edges()[0], p)
+                np.testing.assert_array_equal(pipe.edges()[1], q)
+                np.testing.assert_array_equal(pipe.edges()[2], w)
         for ms in (2, 30):  # min_shared inside the overflow encoder too
             keep = w >= ms
             assert pipe.step(min_shared=ms, engine="residues") == int(keep.sum())
@@ -401,8 +405,9 @@ def test_frequent_kmers_heavy_path(oracle_mod, copies):
 @pytest.mark.parametrize("tail", ["fast", "count"])
 def test_uniprot_k5_on_bucketed_heavy_path(oracle_mod, uni, tail):
     """The reference's dataset at k = 5 (max df 3,694): bucketed layout with the heavy path and
-    the row-block tail — the fast tail (its fixed regions overflow on rows of ~10^5 keys: the
-    counting tail, learned) or the counting tail — edge list sha equal to the golden one (repeat:
+    the row-block tail — the fast tail (its fixed regions overflow on rows of ~10^4 keys: learned
+    regions, the densest blocks counted in (row, q) bins) or the counting tail — edge list sha equal
+    to the golden one (repeat:
     graph replay is not used on the split step, every call recomputes); min_shared 2 against the
     oracle."""
     import torch
@@ -415,7 +420,9 @@ def test_uniprot_k5_on_bucketed_heavy_path(oracle_mod, uni, tail):
         m = pipe.step(engine="residues")
         torch.cuda.synchronize()
         assert pipe.last_layout() == "bucketed" and pipe.last_heavy()
-        assert pipe.last_tail() == "rows"
+        # the fast tail's fixed regions overflow on rows of ~10^4 keys: it learns its regions from the
+        # exact counts (the densest blocks in (row, q) bins) and stays fast
+        assert pipe.last_tail() == ("fast" if tail == "fast" else "rows")
         assert m == g["n_edges"]
         assert edges_sha256(*pipe.edges()) == g["edges_sha256"]
         st = pipe.postings_stats.as_dict()
