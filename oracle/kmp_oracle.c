@@ -99,21 +99,6 @@ static void radix_u32(uint32_t* a, uint32_t* tmp, uint64_t n) {
     if (src != a) memcpy(a, src, n * sizeof(uint32_t));
 }
 
-static void radix_u64(uint64_t* a, uint64_t* tmp, uint64_t n) {
-    uint64_t cnt[2048];
-    uint64_t *src = a, *dst = tmp;
-    for (int shift = 0; shift < 64; shift += 11) {
-        memset(cnt, 0, sizeof cnt);
-        for (uint64_t i = 0; i < n; ++i) cnt[(src[i] >> shift) & 2047]++;
-        if (n == 0 || cnt[(src[0] >> shift) & 2047] == n) continue;
-        uint64_t s = 0;
-        for (int d = 0; d < 2048; ++d) { uint64_t c = cnt[d]; cnt[d] = s; s += c; }
-        for (uint64_t i = 0; i < n; ++i) dst[cnt[(src[i] >> shift) & 2047]++] = src[i];
-        uint64_t* t = src; src = dst; dst = t;
-    }
-    if (src != a) memcpy(a, src, n * sizeof(uint64_t));
-}
-
 static void insertion_u32(uint32_t* a, uint64_t n) {
     for (uint64_t i = 1; i < n; ++i) {
         uint32_t v = a[i];
@@ -210,7 +195,199 @@ static void run_pool(int threads, void* (*fn)(void*), void* arg) {
 
 void orc_free_ctx(orc_ctx* x);
 
-/* Builds windows, K(p), df, repeat ids and posting lists. */
+/* ---- the build's phases on the `threads` pool (main.rs:84-121 runs every phase on its pool) ---- */
+typedef struct {
+    orc_ctx* x;
+    const uint8_t* res;
+    const uint64_t* off;
+    const uint8_t* lut;
+    _Atomic uint32_t cursor;
+} extract_job;
+
+static void* extract_worker(void* arg) {  /* Protein::new for blocks of 64 proteins */
+    extract_job* j = (extract_job*)arg;
+    orc_ctx* x = j->x;
+    for (;;) {
+        uint32_t p0 = atomic_fetch_add(&j->cursor, 64);
+        if (p0 >= x->n) break;
+        uint32_t p1 = p0 + 64 < x->n ? p0 + 64 : x->n;
+        for (uint32_t p = p0; p < p1; ++p) {
+            const uint8_t* s = j->res + j->off[p];
+            uint64_t w = x->win_off[p], nw = x->win_off[p + 1] - w;
+            for (uint64_t t = 0; t < nw; ++t) {
+                uint32_t v = 0;
+                for (int i = 0; i < x->k; ++i) v = v * 21u + j->lut[s[t + i]];
+                x->codes[w + t] = v;
+            }
+        }
+    }
+    return NULL;
+}
+
+/* stable LSD radix sort of u64 keys on bits [lo, hi), each pass split over the pool: per-chunk
+ * digit counts, an exclusive scan over (digit, chunk), chunk-ordered scatter */
+enum { RX_BITS = 11, RX_BINS = 1 << RX_BITS };
+typedef struct {
+    uint64_t *src, *dst;
+    uint64_t n;
+    int shift, T;
+    uint64_t* cnt;  /* T x RX_BINS */
+    _Atomic int next;
+} rx_pass;
+
+static void* rx_hist(void* arg) {
+    rx_pass* r = (rx_pass*)arg;
+    int t = atomic_fetch_add(&r->next, 1);
+    uint64_t* c = r->cnt + (uint64_t)t * RX_BINS;
+    memset(c, 0, sizeof(uint64_t) * RX_BINS);
+    for (uint64_t i = r->n * t / r->T, e = r->n * (t + 1) / r->T; i < e; ++i) c[(r->src[i] >> r->shift) & (RX_BINS - 1)]++;
+    return NULL;
+}
+
+static void* rx_scatter(void* arg) {
+    rx_pass* r = (rx_pass*)arg;
+    int t = atomic_fetch_add(&r->next, 1);
+    uint64_t* c = r->cnt + (uint64_t)t * RX_BINS;
+    for (uint64_t i = r->n * t / r->T, e = r->n * (t + 1) / r->T; i < e; ++i)
+        r->dst[c[(r->src[i] >> r->shift) & (RX_BINS - 1)]++] = r->src[i];
+    return NULL;
+}
+
+static void radix_u64_par(uint64_t* a, uint64_t* tmp, uint64_t n, int lo, int hi, int T) {
+    if (T < 1) T = 1;
+    if ((uint64_t)T > n / 4096 + 1) T = (int)(n / 4096 + 1);
+    rx_pass r;
+    r.n = n;
+    r.T = T;
+    r.cnt = (uint64_t*)malloc(sizeof(uint64_t) * RX_BINS * T);
+    uint64_t *src = a, *dst = tmp;
+    for (int shift = lo; shift < hi; shift += RX_BITS) {
+        r.src = src; r.dst = dst; r.shift = shift;
+        atomic_init(&r.next, 0);
+        run_pool(T, rx_hist, &r);
+        uint64_t s = 0, tot0 = 0;
+        for (int t = 0; t < T; ++t) tot0 += r.cnt[(uint64_t)t * RX_BINS + ((n ? src[0] >> shift : 0) & (RX_BINS - 1))];
+        if (n == 0 || tot0 == n) continue;  /* digit constant: skip the pass */
+        for (int d = 0; d < RX_BINS; ++d)
+            for (int t = 0; t < T; ++t) {
+                uint64_t* c = &r.cnt[(uint64_t)t * RX_BINS + d];
+                uint64_t v = *c;
+                *c = s;
+                s += v;
+            }
+        atomic_init(&r.next, 0);
+        run_pool(T, rx_scatter, &r);
+        uint64_t* t = src; src = dst; dst = t;
+    }
+    if (src != a) memcpy(a, src, n * sizeof(uint64_t));
+    free(r.cnt);
+}
+
+/* keys (code << 32 | p) of K(p) in protein order, and the compacted set array */
+typedef struct {
+    orc_ctx* x;
+    uint64_t* key;
+    uint32_t* dst;        /* compacted K(p) values */
+    const uint64_t* nset; /* |K(p)| (set_off before the prefix) */
+    _Atomic uint32_t cursor;
+} key_job;
+
+static void* key_worker(void* arg) {
+    key_job* j = (key_job*)arg;
+    orc_ctx* x = j->x;
+    for (;;) {
+        uint32_t p0 = atomic_fetch_add(&j->cursor, 64);
+        if (p0 >= x->n) break;
+        uint32_t p1 = p0 + 64 < x->n ? p0 + 64 : x->n;
+        for (uint32_t p = p0; p < p1; ++p) {
+            const uint32_t* src = x->set_val + x->win_off[p];
+            for (uint64_t i = x->set_off[p], t = 0; i < x->set_off[p + 1]; ++i, ++t) {
+                j->dst[i] = src[t];
+                j->key[i] = ((uint64_t)src[t] << 32) | p;
+            }
+        }
+    }
+    return NULL;
+}
+
+/* the sorted keys cut into T chunks at k-mer boundaries; pass 0 counts each chunk's distinct and
+ * repeat k-mers and posting entries, pass 1 fills the arrays at the chunks' prefix offsets */
+typedef struct {
+    orc_ctx* x;
+    const uint64_t* key;
+    uint64_t s;
+    int T, pass;
+    uint64_t* cut;   /* [T+1] */
+    uint64_t* cd;    /* per chunk: distinct, repeat, posting entries, Σ C(df,2), max df */
+    _Atomic int next;
+} run_job;
+
+static void* run_worker(void* arg) {
+    run_job* j = (run_job*)arg;
+    orc_ctx* x = j->x;
+    int t = atomic_fetch_add(&j->next, 1);
+    const uint64_t* key = j->key;
+    uint64_t* c = j->cd + 5 * (uint64_t)t;
+    uint64_t d = j->pass ? c[0] : 0, r = j->pass ? c[1] : 0, tot = j->pass ? c[2] : 0, cdf2 = 0, maxdf = 0;
+    for (uint64_t i = j->cut[t], e = j->cut[t + 1]; i < e;) {
+        uint64_t k = i;
+        while (k < e && (key[k] >> 32) == (key[i] >> 32)) ++k;
+        uint32_t f = (uint32_t)(k - i);
+        if (j->pass) {
+            x->distinct[d] = (uint32_t)(key[i] >> 32);
+            x->df[d] = f;
+            if (f >= 2) {   /* repeat split (main.rs:127-149); dense id = rank among repeats */
+                x->rep_codes[r] = (uint32_t)(key[i] >> 32);
+                x->rep_df[r] = f;
+                x->post_off[r] = tot;
+                for (uint64_t q = i; q < k; ++q) x->post_val[tot++] = (uint32_t)key[q];
+                ++r;
+            }
+        } else if (f >= 2) {
+            ++r;
+            tot += f;
+            cdf2 += (uint64_t)f * (f - 1) / 2;
+            if (f > maxdf) maxdf = f;
+        }
+        ++d;
+        i = k;
+    }
+    if (!j->pass) {
+        c[0] = d; c[1] = r; c[2] = tot; c[3] = cdf2; c[4] = maxdf;
+    }
+    return NULL;
+}
+
+/* each protein's repeat ids, ascending, with the position inside the id's posting list: the pool's
+ * workers own consecutive id ranges, count per protein, then fill at per-(protein, worker) offsets */
+typedef struct {
+    orc_ctx* x;
+    int T, pass;
+    uint64_t* hcut;   /* [T+1] id ranges */
+    uint32_t* cnt;    /* T x n: entries per (worker, protein), then the worker's cursor */
+    _Atomic int next;
+} hid_job;
+
+static void* hid_worker(void* arg) {
+    hid_job* j = (hid_job*)arg;
+    orc_ctx* x = j->x;
+    int t = atomic_fetch_add(&j->next, 1);
+    uint32_t* c = j->cnt + (uint64_t)t * x->n;
+    for (uint64_t h = j->hcut[t]; h < j->hcut[t + 1]; ++h)
+        for (uint64_t q = x->post_off[h]; q < x->post_off[h + 1]; ++q) {
+            uint32_t p = x->post_val[q];
+            if (!j->pass) {
+                c[p]++;
+            } else {
+                uint64_t o = x->hid_off[p] + c[p]++;
+                x->hid_val[o] = (uint32_t)h;
+                x->hid_pos[o] = (uint32_t)(q - x->post_off[h]);
+            }
+        }
+    return NULL;
+}
+
+/* Builds windows, K(p), df, repeat ids and posting lists, every phase on the `threads` pool. */
 orc_ctx* orc_build(const uint8_t* res, const uint64_t* off, uint32_t n, const uint16_t* cls, int k,
                    int threads) {
     if (k < 1 || k > 7) return NULL;
@@ -222,7 +399,18 @@ orc_ctx* orc_build(const uint8_t* res, const uint64_t* off, uint32_t n, const ui
     uint64_t nw = 0;
     for (uint32_t p = 0; p < n; ++p) nw += n_windows(off[p + 1] - off[p], k);
     x->codes = (uint32_t*)malloc(sizeof(uint32_t) * (nw ? nw : 1));
-    orc_extract(res, off, n, k, x->codes, x->win_off);
+    {
+        uint8_t lut[256];
+        for (int b = 0; b < 256; ++b) lut[b] = orc_residue_code((uint8_t)b);
+        uint64_t w = 0;
+        for (uint32_t p = 0; p < n; ++p) {
+            x->win_off[p] = w;
+            w += n_windows(off[p + 1] - off[p], k);
+        }
+        x->win_off[n] = w;
+        extract_job ej = {x, res, off, lut, 0};
+        run_pool(x->threads, extract_worker, &ej);
+    }
     x->c.n_windows = nw;
 
     /* per-protein sort + dedup (main.rs:99-101,187-189) */
@@ -231,9 +419,8 @@ orc_ctx* orc_build(const uint8_t* res, const uint64_t* off, uint32_t n, const ui
     set_job sj = {x, 0};
     run_pool(x->threads, set_worker, &sj);
     uint64_t s = 0;
-    for (uint32_t p = 0; p < n; ++p) {  /* compact in place (dst <= src always) */
+    for (uint32_t p = 0; p < n; ++p) {  /* |K(p)| -> offsets of the compacted sets */
         uint64_t m = x->set_off[p];
-        memmove(x->set_val + s, x->set_val + x->win_off[p], m * sizeof(uint32_t));
         x->set_off[p] = s;
         s += m;
     }
@@ -243,21 +430,45 @@ orc_ctx* orc_build(const uint8_t* res, const uint64_t* off, uint32_t n, const ui
     /* global df over distinct per-protein k-mers (main.rs:77-122): one radix sort of
      * (code << 32 | protein) keys; each run of equal codes is one distinct k-mer, its
      * length the df, its low halves the posting list in protein-index order (the
-     * visitor order of vertex.rs:100 with threads == 1). */
+     * visitor order of vertex.rs:100 with threads == 1).  The keys are built in protein
+     * order, so a stable sort on the code bits alone keeps each run's proteins ascending. */
     uint64_t* key = (uint64_t*)malloc(sizeof(uint64_t) * (s ? s : 1));
     uint64_t* ktmp = (uint64_t*)malloc(sizeof(uint64_t) * (s ? s : 1));
-    for (uint32_t p = 0; p < n; ++p)
-        for (uint64_t i = x->set_off[p]; i < x->set_off[p + 1]; ++i)
-            key[i] = ((uint64_t)x->set_val[i] << 32) | p;
-    radix_u64(key, ktmp, s);
+    {
+        uint32_t* sv = (uint32_t*)malloc(sizeof(uint32_t) * (s ? s : 1));
+        key_job kj = {x, key, sv, NULL, 0};
+        run_pool(x->threads, key_worker, &kj);
+        free(x->set_val);
+        x->set_val = sv;
+    }
+    int cbits = 1;
+    { uint64_t top = 1; for (int i = 0; i < k; ++i) top *= 21; while ((1ull << cbits) < top) ++cbits; }
+    radix_u64_par(key, ktmp, s, 32, 32 + cbits, x->threads);
     free(ktmp);
+    /* k-mer runs: chunks cut at run starts, counted, scanned, filled */
+    int T = x->threads;
+    if ((uint64_t)T > s / 4096 + 1) T = (int)(s / 4096 + 1);
+    run_job rj;
+    rj.x = x; rj.key = key; rj.s = s; rj.T = T;
+    rj.cut = (uint64_t*)malloc(sizeof(uint64_t) * (T + 1));
+    rj.cd = (uint64_t*)calloc(5 * (uint64_t)T, sizeof(uint64_t));
+    for (int t = 0; t <= T; ++t) {
+        uint64_t c = s * t / T;
+        while (c > 0 && c < s && (key[c] >> 32) == (key[c - 1] >> 32)) ++c;
+        rj.cut[t] = t == T ? s : c;
+    }
+    for (int t = 1; t <= T; ++t) if (rj.cut[t] < rj.cut[t - 1]) rj.cut[t] = rj.cut[t - 1];
+    rj.pass = 0;
+    atomic_init(&rj.next, 0);
+    run_pool(T, run_worker, &rj);
     uint64_t d = 0, r = 0, cdf2 = 0, maxdf = 0, tot = 0;
-    for (uint64_t i = 0; i < s;) {
-        uint64_t j = i;
-        while (j < s && (key[j] >> 32) == (key[i] >> 32)) ++j;
-        ++d;
-        if (j - i >= 2) { ++r; tot += j - i; }
-        i = j;
+    for (int t = 0; t < T; ++t) {  /* chunk totals -> chunk offsets (kept in cd[0..2]) */
+        uint64_t* c = rj.cd + 5 * (uint64_t)t;
+        uint64_t cd0 = c[0], cr = c[1], ct = c[2];
+        c[0] = d; c[1] = r; c[2] = tot;
+        d += cd0; r += cr; tot += ct;
+        cdf2 += c[3];
+        if (c[4] > maxdf) maxdf = c[4];
     }
     x->distinct = (uint32_t*)malloc(sizeof(uint32_t) * (d ? d : 1));
     x->df = (uint32_t*)malloc(sizeof(uint32_t) * (d ? d : 1));
@@ -265,26 +476,12 @@ orc_ctx* orc_build(const uint8_t* res, const uint64_t* off, uint32_t n, const ui
     x->rep_df = (uint32_t*)malloc(sizeof(uint32_t) * (r ? r : 1));
     x->post_off = (uint64_t*)malloc(sizeof(uint64_t) * (r + 1));
     x->post_val = (uint32_t*)malloc(sizeof(uint32_t) * (tot ? tot : 1));
-    d = 0; r = 0; tot = 0;
-    for (uint64_t i = 0; i < s;) {
-        uint64_t j = i;
-        while (j < s && (key[j] >> 32) == (key[i] >> 32)) ++j;
-        uint32_t f = (uint32_t)(j - i);
-        x->distinct[d] = (uint32_t)(key[i] >> 32);
-        x->df[d] = f;
-        ++d;
-        if (f >= 2) {   /* repeat split (main.rs:127-149); dense id = rank among repeats */
-            x->rep_codes[r] = (uint32_t)(key[i] >> 32);
-            x->rep_df[r] = f;
-            x->post_off[r] = tot;
-            for (uint64_t t = i; t < j; ++t) x->post_val[tot++] = (uint32_t)key[t];
-            cdf2 += (uint64_t)f * (f - 1) / 2;
-            if (f > maxdf) maxdf = f;
-            ++r;
-        }
-        i = j;
-    }
+    rj.pass = 1;
+    atomic_init(&rj.next, 0);
+    run_pool(T, run_worker, &rj);
     x->post_off[r] = tot;
+    free(rj.cut);
+    free(rj.cd);
     free(key);
     x->n_distinct = d;
     x->n_repeat = r;
@@ -296,20 +493,41 @@ orc_ctx* orc_build(const uint8_t* res, const uint64_t* off, uint32_t n, const ui
     /* remove_unique_five_mers + modify_hash_five_mer (protein.rs:151-174): each protein's
      * repeat ids, ascending, with its position inside the id's posting list */
     x->hid_off = (uint64_t*)calloc(n + 1, sizeof(uint64_t));
-    for (uint64_t t = 0; t < tot; ++t) x->hid_off[x->post_val[t] + 1]++;
-    for (uint32_t p = 0; p < n; ++p) x->hid_off[p + 1] += x->hid_off[p];
     x->hid_val = (uint32_t*)malloc(sizeof(uint32_t) * (tot ? tot : 1));
     x->hid_pos = (uint32_t*)malloc(sizeof(uint32_t) * (tot ? tot : 1));
-    uint64_t* fill = (uint64_t*)malloc(sizeof(uint64_t) * (n + 1));
-    memcpy(fill, x->hid_off, sizeof(uint64_t) * (n + 1));
-    for (uint64_t h = 0; h < r; ++h)
-        for (uint64_t t = x->post_off[h]; t < x->post_off[h + 1]; ++t) {
-            uint32_t p = x->post_val[t];
-            x->hid_val[fill[p]] = (uint32_t)h;
-            x->hid_pos[fill[p]] = (uint32_t)(t - x->post_off[h]);
-            fill[p]++;
+    {
+        int H = x->threads;
+        if ((uint64_t)H > tot / 65536 + 1) H = (int)(tot / 65536 + 1);
+        hid_job hj;
+        hj.x = x; hj.T = H;
+        hj.hcut = (uint64_t*)malloc(sizeof(uint64_t) * (H + 1));
+        hj.cnt = (uint32_t*)calloc((uint64_t)H * (n ? n : 1), sizeof(uint32_t));
+        uint64_t h = 0;  /* id ranges of about equal posting entries */
+        for (int t = 0; t <= H; ++t) {
+            uint64_t want = tot * t / H;
+            while (h < r && x->post_off[h] < want) ++h;
+            hj.hcut[t] = t == H ? r : h;
         }
-    free(fill);
+        hj.pass = 0;
+        atomic_init(&hj.next, 0);
+        run_pool(H, hid_worker, &hj);
+        uint64_t o = 0;  /* protein-major offsets; inside a protein the workers in id order */
+        for (uint32_t p = 0; p < n; ++p) {
+            x->hid_off[p] = o;
+            for (int t = 0; t < H; ++t) {
+                uint32_t* c = &hj.cnt[(uint64_t)t * n + p];
+                uint32_t v = *c;
+                *c = (uint32_t)(o - x->hid_off[p]);
+                o += v;
+            }
+        }
+        x->hid_off[n] = o;
+        hj.pass = 1;
+        atomic_init(&hj.next, 0);
+        run_pool(H, hid_worker, &hj);
+        free(hj.hcut);
+        free(hj.cnt);
+    }
     return x;
 }
 
