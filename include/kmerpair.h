@@ -473,9 +473,12 @@ int kmp_postings_set_direct(kmp_postings* ws, int enable);
 int kmp_postings_set_flat_heavy(kmp_postings* ws, int enable);
 /* The bucketed step as a HIP graph (default 1): captured on the second call with an unchanged
  * shape (pointers, sizes, options, workspace buffers), replayed after that.
- * kmp_postings_graph_replays: calls served by a replay so far. */
+ * kmp_postings_graph_replays: calls served by a replay so far.  kmp_postings_reruns: calls (or phases
+ * of a split call) run again after a capacity grew — every learned capacity is sized from counts, so
+ * the same inputs rerun the same number of times whatever the order of the device's atomics. */
 int kmp_postings_set_graph(kmp_postings* ws, int enable);
 uint64_t kmp_postings_graph_replays(const kmp_postings* ws);
+uint64_t kmp_postings_reruns(const kmp_postings* ws);
 /* Bucket partition of the residue path (level 1 is always the counting pass).  AUTO (default):
  * level 2 by cursors — every run of keys reserved with one atomic in its bucket's fixed-capacity
  * region (sized from the hash-uniform mean), no histogram / scan passes — and, for a shape where a

@@ -192,6 +192,7 @@ SIGNATURES = {
     "kmp_edges_get_wk": (C.c_int, [P, C.c_uint32, P, C.c_uint64, C.POINTER(C.c_uint64)]),
     "kmp_postings_set_graph": (C.c_int, [P, C.c_int]),
     "kmp_postings_graph_replays": (C.c_uint64, [P]),
+    "kmp_postings_reruns": (C.c_uint64, [P]),
     "kmp_postings_set_partition": (C.c_int, [P, C.c_int]),
     "kmp_postings_last_partition": (C.c_int, [P]),
     "kmp_postings_set_reuse": (C.c_int, [P, C.c_int]),

@@ -71,6 +71,7 @@ int kmp_postings_set_graph(kmp_postings* ws, int enable) {
 }
 
 uint64_t kmp_postings_graph_replays(const kmp_postings* ws) { return ws ? ws->graph_replays : 0; }
+uint64_t kmp_postings_reruns(const kmp_postings* ws) { return ws ? ws->reruns : 0; }
 
 int kmp_postings_set_partition(kmp_postings* ws, int mode) {
     if (!ws || (mode != KMP_PARTITION_AUTO && mode != KMP_PARTITION_COUNT)) return KMP_EINVAL;
@@ -457,6 +458,7 @@ static int split_expand_impl(kmp_postings* ws, const SplitSrc& src, uint32_t n, 
         int rc = KMP_OK;
         bool routed_done = false;
         for (int attempt = 0; attempt < 4; ++attempt) {
+            if (attempt) ++ws->reruns;
             if ((rc = step_reserve(ws, c, g, st)) != KMP_OK) break;
             if ((rc = front(st)) != KMP_OK) break;
             step_pack_kernel<<<1, 256, 0, st>>>(ws->bstats.p, ws->flags.p, nullptr, ws->hrb);
@@ -659,6 +661,7 @@ int kmp_dev_split_edges(kmp_postings* ws, const unsigned long long* d_keys, uint
     c.cap = cap;
     c.stride = 1;
     for (int attempt = 0; attempt < 8; ++attempt) {
+        if (attempt) ++ws->reruns;
         PtGeom g;
         if (!pt_geometry(ws, c, m, &g)) return KMP_EINVAL;
         g.flat_n = m;  // the received regions, padded with kNoKey, read as one array

@@ -824,6 +824,7 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
     if (!reuse) ws->front_ok = false;
     // every rerun grows a capacity to its measured need, so a handful of attempts suffices
     for (int attempt = 0; attempt < 16; ++attempt) {
+        if (attempt) ++ws->reruns;
         PtGeom g;
         if (!pt_geometry(ws, c, ws->pt_inc ? ws->pt_inc : c.slots / 4, &g)) return KMP_EINVAL;
         {

@@ -147,6 +147,7 @@ struct kmp_postings {
     hipStream_t cst = nullptr;  // capture stream
     std::vector<unsigned long long> gkey, gkey_seen;
     uint64_t graph_replays = 0;
+    uint64_t reruns = 0;  // calls (or a split call's phases) run again with a grown capacity
     // read-back of a step (kRb* layout), written by the pack kernel into coherent pinned memory
     unsigned long long* hrb = nullptr;
     hipEvent_t ev[KMP_POSTINGS_STAGES + 1] = {};

@@ -143,6 +143,10 @@ class _SplitEdges:
         """Row blocks of the last call above the LDS capacity (finished by the segmented sort)."""
         return int(lib().kmp_postings_last_overflow_blocks(self._workspace()))
 
+    def reruns(self) -> int:
+        """Calls of this pipeline's workspace run again after a learned capacity grew."""
+        return int(lib().kmp_postings_reruns(self._workspace()))
+
     def edges(self):
         n = self.n_edges
         return (self.ep[:n].cpu().numpy().view(np.uint32), self.eq[:n].cpu().numpy().view(np.uint32),
@@ -358,6 +362,7 @@ class DevicePipeline(_SplitEdges):
 
     def graph_replays(self) -> int:
         return int(lib().kmp_postings_graph_replays(self._workspace()))
+
 
     def set_tail(self, mode: str = "fast") -> None:
         """Row-block tail of unscored calls: 'fast' (default, where it applies) or 'count'."""
