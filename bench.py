@@ -9,12 +9,15 @@ w = |K(p) ∩ K(q)| in canonical order (Graph::new + remove_uninteresting_edges 
 Inputs are synthetic (N = 100,000, seed 3, len ~ N(300, 30^2), k = 7).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--engine residues|postings|tiles]
-  N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N [--split kmer|rows]
+  N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N [--split kmer|replicated|rows]
+        [--start auto|keys|residues]
 
 N > 1 (config 4): one process per GPU over RCCL, the k-mer split with a sharded start
 (dist.sharded_split_step): rank r holds only the residues of its own chunks (about
-1/N of the batch), keys its windows once and an all-to-all sends every key to the rank owning its
-k-mer's bins; each rank groups and expands its k-mers, a second all-to-all moves the pair keys to
+1/N of the batch).  From 8 GPUs up (--start keys) it keys its windows once and an all-to-all sends
+every key to the rank owning its k-mer's bins; below 8 (--start residues) the ranks all-gather the
+residue slices (1 B per residue instead of 8 B per key) and every rank keys the whole batch, keeping
+its bins.  Each rank groups and expands its k-mers, a second all-to-all moves the pair keys to
 their row owners, each rank reduces its rows, and rank 0 gathers every rank's row block behind its
 own (rank order = canonical order).  Both exchanges are inside the timed step, which ends with the
 canonical list resident on rank 0; the row-sharded step without that gather is
@@ -83,6 +86,9 @@ def parse(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0, help="oracle threads of the all-cores run (0: every usable core)")
     ap.add_argument("--score", default="blosum", choices=["blosum", "count"], help="config5: edge score")
     ap.add_argument("--split", default="kmer", choices=["kmer", "replicated", "rows"], help="multi-GPU flow (N > 1)")
+    ap.add_argument("--start", default="auto", choices=["auto", "keys", "residues"],
+                    help="the sharded start's first exchange (--split kmer, N > 1): the key all-to-all, the "
+                         "residue all-gather, or auto (keys from 8 GPUs up)")
     ap.add_argument("--direct-tail", type=int, default=1, help="config5: fused reduction writes edges in place (A/B)")
     ap.add_argument("--flat-heavy", type=int, default=1, help="config5: passes expand frequent k-mers by rows (A/B)")
     return ap.parse_args(argv)
@@ -358,7 +364,7 @@ def main(argv=None, dist_mod=None):
         dist = D.dist = dist_mod
     from uniprot_kmer_based_clustering_amd import _lib
     from uniprot_kmer_based_clustering_amd.device import DevicePipeline, ShardPipeline
-    from uniprot_kmer_based_clustering_amd.dist import distributed_step, kmer_split_step, sharded_split_step
+    from uniprot_kmer_based_clustering_amd.dist import distributed_step, kmer_split_step, sharded_split_step, start_mode
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -374,6 +380,7 @@ def main(argv=None, dist_mod=None):
     proteins = load_batch(args.config)
     n = proteins.n
     sharded = world > 1 and args.split == "kmer"
+    start = start_mode(args.start, world) if sharded else None
     if sharded:
         # the start state of SURVEY.md §8e: this GPU holds its chunks' residues only (plus offsets
         # and class ids); the host batch is generated whole by every rank, and only the slice moves
@@ -385,7 +392,7 @@ def main(argv=None, dist_mod=None):
 
     def one_step(timings=None, gather=False):
         if sharded:
-            return sharded_split_step(pipe, rank, world, gather=gather, timings=timings)
+            return sharded_split_step(pipe, rank, world, gather=gather, timings=timings, start=start)
         if world > 1 and args.split == "replicated":
             return kmer_split_step(pipe, rank, world, gather=gather, timings=timings)
         if world > 1:
@@ -423,7 +430,7 @@ def main(argv=None, dist_mod=None):
         ne = torch.tensor([n_edges], dtype=torch.int64, device=f"cuda:{local}")
         dist.broadcast(ne, 0)  # rank 0 holds the whole list: its count is the total
         if args.split in ("kmer", "replicated"):
-            step_fn = sharded_split_step if sharded else kmer_split_step
+            step_fn = (lambda *a_, **kw: sharded_split_step(*a_, start=start, **kw)) if sharded else kmer_split_step
             st_ = pipe._split_state
             stt = st_.bufs[3].clone()
             dist.all_reduce(stt)  # every rank's k-mers' statistics: the batch's
@@ -434,16 +441,23 @@ def main(argv=None, dist_mod=None):
             ph = torch.tensor(np.mean(np.array(tims), axis=0), dtype=torch.float64, device=f"cuda:{local}")
             lo, hi = (int(x) for x in _lib.row_split(n, world)[rank:rank + 2])
             # bytes this rank sends to the other ranks per step (equal splits: its own region stays)
-            kx = (world - 1) * st_.kcap * 8 if sharded else 0
-            px = (world - 1) * st_.cap * 8
+            # the start exchange: the padded key regions, or the rank's residue slice to every peer;
+            # the residue start's pair keys travel in its rebuilt batch's split state
+            if start == "residues":
+                lo_, hi_, _ = pipe.own_residues()
+                kx = (world - 1) * (hi_ - lo_)
+                px = (world - 1) * st_.cap * 8
+            else:
+                kx = (world - 1) * st_.kcap * 8 if sharded else 0
+                px = (world - 1) * st_.cap * 8
             res_mb = pipe.res.numel() / 1e6
             mine = torch.tensor([rank, lo, hi, own_edges, kx, px, res_mb, *ph.tolist()], dtype=torch.float64,
                                 device=f"cuda:{local}")
             allv = [torch.zeros_like(mine) for _ in range(world)]
             dist.all_gather(allv, mine)
-            names = (("rank", "row_lo", "row_hi", "edges", "key_exchange_bytes", "pair_exchange_bytes",
+            names = (("rank", "row_lo", "row_hi", "edges", "start_exchange_bytes", "pair_exchange_bytes",
                       "residues_resident_MB") +
-                     (("keys_ms", "key_exchange_ms", "group_ms", "pair_exchange_ms", "edges_ms") if sharded else
+                     (("keys_ms", "start_exchange_ms", "group_ms", "pair_exchange_ms", "edges_ms") if sharded else
                       ("expand_ms", "exchange_ms", "edges_ms")))
             rank_info = [dict(zip(names, [int(v) if i < 6 else v for i, v in enumerate(x.tolist())])) for x in allv]
             dist.barrier()
@@ -481,7 +495,10 @@ def main(argv=None, dist_mod=None):
                        "proteins": n, "k": k, "pairs": int(pairs_total), "edges": int(n_edges),
                        "engine": args.engine,
                        "parallelism": ("single GPU" if world == 1 else
-                                       f"k-mer split x{world}, sharded start (all-to-all of keys, then of pair keys)"
+                                       (f"k-mer split x{world}, sharded start (all-to-all of keys, then of pair keys)"
+                                        if start == "keys" else
+                                        f"k-mer split x{world}, sharded start (all-gather of residue slices, "
+                                        "all-to-all of pair keys)")
                                        if args.split == "kmer" else
                                        f"k-mer split x{world}, replicated start (all-to-all of pair keys)"
                                        if args.split == "replicated" else f"row split x{world}")},
@@ -501,8 +518,8 @@ def main(argv=None, dist_mod=None):
                                "incidences": n_inc,
                                # algorithmic exchange bytes: one 8-B key per window (sharded start) and
                                # one 8-B pair key per incidence, the (N-1)/N of them that leave a rank
-                               "exchange_bytes": int((8 * n_win * (1 if sharded else 0) + 8 * n_inc)
-                                                     * (world - 1) / world)}
+                               "exchange_bytes": int((8 * n_win * (start == "keys") + 8 * n_inc) * (world - 1) / world
+                                                     + (world - 1) * int(proteins.offsets[-1]) * (start == "residues"))}
             out["ranks"] = rank_info
             out["step_without_gather_ms"] = no_gather_ms
             out["gather_ms"] = ms - no_gather_ms

@@ -245,6 +245,26 @@ class OracleShardPipe(OracleSplitPipe):
         lo, hi = part * b.n // parts, (part + 1) * b.n // parts
         self.win = [(int(c), p) for p in range(lo, hi) for c in codes[woff[p]:woff[p + 1]]]
         self.kflags = (0, 0)
+        self.b, self.o = b, o
+        self.offsets_host = np.asarray(b.offsets, dtype=np.uint64)
+        self.total = int(self.offsets_host[-1])
+        self.res_lo, self.res_hi = int(self.offsets_host[lo]), int(self.offsets_host[hi])
+        self.res = torch.from_numpy(np.asarray(b.residues, dtype=np.uint8)[self.res_lo:self.res_hi].copy())
+        self.cap0 = cap
+        self.gathered = []
+
+    def own_residues(self):
+        return self.res_lo, self.res_hi, self.res
+
+    def gathered_pipeline(self, residues):
+        """The residue start's rebuilt batch: an OracleSplitPipe (kmer_split_step's stand-in)
+        carrying the gathered residues, kept for the test to compare with the batch."""
+        P, Q, W = self.o.pairs()
+        full = OracleSplitPipe(self.n, P, Q, W, self.cap0)
+        full.res = residues.clone()
+        full.k = 7
+        self.gathered.append(full)
+        return full
 
     def split_keys(self, part, parts, kcap, ksend, flags):
         need = 0
@@ -303,7 +323,7 @@ def shard_worker(rank, world, port, out_q):
         state = SplitState()
         state.cap, state.kcap = 64, 256  # far too small: the first step reruns with both learned
         for ms in (1, 3):
-            n = sharded_split_step(pipe, rank, world, min_shared=ms, gather=True, state=state)
+            n = sharded_split_step(pipe, rank, world, min_shared=ms, gather=True, state=state, start="keys")
             if rank == 0:
                 keep = W >= ms
                 ok = (n == int(keep.sum())
@@ -313,6 +333,53 @@ def shard_worker(rank, world, port, out_q):
                 out_q.put(("sharded", ms, ok, n, state.reruns, state.cap, state.kcap))
     finally:
         dist.destroy_process_group()
+
+
+def residue_start_worker(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, ROOT)
+        from uniprot_kmer_based_clustering_amd.dist import SplitState, sharded_split_step, start_mode
+        b, o = build_case()
+        P, Q, W = o.pairs()
+        pipe = OracleShardPipe(b, o, cap=16 if rank == 0 else 1 << 20, part=rank, parts=world)
+        state = SplitState()
+        res = np.asarray(b.residues, dtype=np.uint8)
+        for step, ms in enumerate((1, 3)):
+            if step:  # the rebuilt batch is refreshed in place from the slices every step
+                state.full.res.zero_()
+            n = sharded_split_step(pipe, rank, world, min_shared=ms, gather=True, state=state)
+            same = np.array_equal(state.full.res.numpy(), res)
+            if rank == 0:
+                keep = W >= ms
+                ok = (n == int(keep.sum())
+                      and np.array_equal(pipe.ep[:n].numpy().view(np.uint32), P[keep])
+                      and np.array_equal(pipe.eq[:n].numpy().view(np.uint32), Q[keep])
+                      and np.array_equal(pipe.ew[:n].numpy().view(np.uint32), W[keep]))
+                out_q.put(("residues", ms, ok and same, n, len(pipe.gathered), start_mode("auto", world)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_split_residue_start(world):
+    """sharded_split_step's residue start (the default below 8 ranks): the ranks' residue slices
+    all-gathered into the whole batch on every rank (built once, then refreshed in place by
+    point-to-point receives), the k-mer split over it, the canonical list gathered on rank 0."""
+    port = free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=residue_start_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    msgs = [q.get(timeout=300) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert all(m[2] for m in msgs), msgs
+    assert all(m[4] == 1 and m[5] == "residues" for m in msgs)  # built once; auto picks residues
 
 
 @pytest.mark.parametrize("world", [2, 3])

@@ -1,5 +1,5 @@
-"""dist.sharded_split_step (the bench's multi-GPU flow: each rank holds its residue slice, keys
-its own windows, two all-to-alls) and dist.kmer_split_step (the replicated start) with the real
+"""dist.sharded_split_step (the bench's multi-GPU flow: each rank holds its residue slice; the
+key start keys its own windows, two all-to-alls; the residue start all-gathers the slices) and dist.kmer_split_step (the replicated start) with the real
 device stages in 2 and 3 processes sharing the one GPU of the test box: RCCL admits one rank per device, so the
 collectives go over gloo through host copies (a shim with torch.distributed's signatures that
 bounces each tensor through the CPU).  The edges gathered on rank 0 equal the oracle's canonical
@@ -58,23 +58,35 @@ class HostBounce:
     def barrier(self, group=None):
         self.d.barrier()
 
+    def get_world_size(self, group=None):
+        return self.d.get_world_size()
+
+    def get_rank(self, group=None):
+        return self.d.get_rank()
+
     def broadcast(self, t, src, group=None):
         h = t.cpu()
         self.d.broadcast(h, src)
         t.copy_(h)
 
     def batch_isend_irecv(self, ops):
-        for kind, t, peer in ops:  # gather_rows: non-zero ranks only send, rank 0 only receives
+        # non-blocking, then waited (the residue all-gather has every rank sending and receiving)
+        works, sent, recvd = [], [], []
+        for kind, t, peer in ops:
             if kind == "send":
-                self.d.send(t.cpu(), peer)
+                sent.append(t.cpu())
+                works.append(self.d.isend(sent[-1], peer))
             else:
-                h = torch.empty(t.shape, dtype=t.dtype)
-                self.d.recv(h, peer)
-                t.copy_(h)
+                recvd.append((t, torch.empty(t.shape, dtype=t.dtype)))
+                works.append(self.d.irecv(recvd[-1][1], peer))
+        for w in works:
+            w.wait()
+        for t, h in recvd:
+            t.copy_(h)
         return []
 
 
-def worker(rank, world, port, out_q, sharded=False):
+def worker(rank, world, port, out_q, sharded=False, start="keys"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -88,7 +100,7 @@ def worker(rank, world, port, out_q, sharded=False):
         from oracle.oracle import Oracle
         from uniprot_kmer_based_clustering_amd.device import DevicePipeline, ShardPipeline
         D.dist = HostBounce(dist)
-        step = D.sharded_split_step if sharded else D.kmer_split_step
+        step = (lambda *a, **kw: D.sharded_split_step(*a, start=start, **kw)) if sharded else D.kmer_split_step
 
         def make(bb, k):
             if sharded:
@@ -99,7 +111,9 @@ def worker(rank, world, port, out_q, sharded=False):
         pipe = make(b, 7)
         state = D.SplitState()
         state.cap = 128
-        for it in range(2):
+        # four steps: the first reruns (cap too small), the next captures each phase's HIP graph, the
+        # last two replay them (a graph replay once wrote garbage where its launch had been right)
+        for it in range(4):
             n = step(pipe, rank, world, gather=True, state=state)
             torch.cuda.synchronize()
             if rank == 0:
@@ -121,16 +135,17 @@ def worker(rank, world, port, out_q, sharded=False):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,sharded", [(2, True), (3, True), (2, False), (3, False)])
-def test_kmer_split_step_device_stages(world, sharded):
+@pytest.mark.parametrize("world,sharded,start", [(2, True, "keys"), (3, True, "keys"), (2, True, "residues"),
+                                                 (3, True, "residues"), (2, False, None), (3, False, None)])
+def test_kmer_split_step_device_stages(world, sharded, start):
     port = free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=worker, args=(r, world, port, q, sharded)) for r in range(world)]
+    procs = [ctx.Process(target=worker, args=(r, world, port, q, sharded, start)) for r in range(world)]
     for p in procs:
         p.start()
     msgs = []
-    while len(msgs) < 4:
+    while len(msgs) < 6:
         msgs.append(q.get(timeout=150))
         assert msgs[-1][0] != "error", msgs[-1]
     for p in procs:
@@ -208,5 +223,6 @@ def test_bench_multi_gpu_path():
     r = out["ranks"]
     assert len(r) == 2 and sum(x["edges"] for x in r) == out["config"]["edges"]
     assert all(0 < x["residues_resident_MB"] < 2.6 for x in r)  # about half of config 2's 3 MB each
-    assert all(x["key_exchange_bytes"] > 0 and x["pair_exchange_bytes"] > 0 for x in r)
+    assert all(x["start_exchange_bytes"] > 0 and x["pair_exchange_bytes"] > 0 for x in r)
+    assert "residue slices" in out["config"]["parallelism"]  # the start below 8 GPUs
     assert out["roofline"]["exchange_bytes"] > 0

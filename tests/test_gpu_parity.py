@@ -355,11 +355,12 @@ def test_rowtail_overflow_blocks(oracle_mod):
                 m = pipe.step(engine="residues")
                 torch.cuda.synchronize()
                 # counting tail: the long row's block is listed and sorted; fast tail: the long row
-                # passes its fixed region, the regions are learned and its block is counted in
-                # (row, q) bins
-                assert pipe.last_tail() == ("rows" if tail == "count" else "fast") and m == len(p)
+                # (one row above a fast block's 8,192 keys) passes its region, so the shape takes
+                # the counting tail from the first call on; the long row last holds no pair
+                fast = tail == "fast" and not long_first
+                assert pipe.last_tail() == ("fast" if fast else "rows") and m == len(p)
                 if it == 0:
-                    assert (pipe.overflow_blocks() > 0) == (long_first and tail == "count")
+                    assert (pipe.overflow_blocks() > 0) == long_first
                 np.testing.assert_array_equal(pipe.edges()[0], p)
                 np.testing.assert_array_equal(pipe.edges()[1], q)
                 np.testing.assert_array_equal(pipe.edges()[2], w)
@@ -405,8 +406,8 @@ def test_frequent_kmers_heavy_path(oracle_mod, copies):
 @pytest.mark.parametrize("tail", ["fast", "count"])
 def test_uniprot_k5_on_bucketed_heavy_path(oracle_mod, uni, tail):
     """The reference's dataset at k = 5 (max df 3,694): bucketed layout with the heavy path and
-    the row-block tail — the fast tail (its fixed regions overflow on rows of ~10^4 keys: learned
-    regions, the densest blocks counted in (row, q) bins) or the counting tail — edge list sha equal
+    the row-block tail — the fast tail (its 8,192-key regions overflow on the densest rows: fewer
+    rows per block, or the counting tail when one row passes them) or the counting tail — edge list sha equal
     to the golden one (repeat:
     graph replay is not used on the split step, every call recomputes); min_shared 2 against the
     oracle."""
@@ -416,13 +417,16 @@ def test_uniprot_k5_on_bucketed_heavy_path(oracle_mod, uni, tail):
     g = load_json("uniprot_counters.json")["5"]
     pipe = DevicePipeline(K.Proteins(res, off, cls), 5, "cuda:0")
     pipe.set_tail(tail)
+    p5, _, w5 = oracle_mod.Oracle(res, off, cls, k=5, threads=8).pairs()
+    row_max = int(np.bincount(p5, weights=w5).max())  # a row's pair keys = the sum of its w
     for _ in range(2):
         m = pipe.step(engine="residues")
         torch.cuda.synchronize()
         assert pipe.last_layout() == "bucketed" and pipe.last_heavy()
-        # the fast tail's fixed regions overflow on rows of ~10^4 keys: it learns its regions from the
-        # exact counts (the densest blocks in (row, q) bins) and stays fast
-        assert pipe.last_tail() == ("fast" if tail == "fast" else "rows")
+        # the fast tail's regions overflow on the densest rows: it takes fewer rows per block, and
+        # the counting tail when a single row holds more than a fast block's 8,192 keys
+        if tail == "count" or row_max > 8192:
+            assert pipe.last_tail() == "rows"
         assert m == g["n_edges"]
         assert edges_sha256(*pipe.edges()) == g["edges_sha256"]
         st = pipe.postings_stats.as_dict()

@@ -1,5 +1,5 @@
 """Per-kernel resources of a device object (VGPRs, SGPRs, spills, LDS): compiles a .hip with
---cuda-device-only and parses llvm-readelf --notes.  Usage: kernel_resources.py file.hip [-I dir] [filter]"""
+--cuda-device-only and parses llvm-readelf --notes.  Usage: kernel_resources.py file.hip [-I dir] [-D macro] [filter]"""
 import re
 import subprocess
 import sys
@@ -7,7 +7,8 @@ import tempfile
 
 src = sys.argv[1]
 inc = [a for a in sys.argv[2:] if a.startswith("-I")] or ["-I/root/repo/include"]
-flt = [a for a in sys.argv[2:] if not a.startswith("-I")]
+inc += [a for a in sys.argv[2:] if a.startswith("-D")]
+flt = [a for a in sys.argv[2:] if not a.startswith(("-I", "-D"))]
 with tempfile.TemporaryDirectory() as d:
     o = f"{d}/k.o"
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", *inc,

@@ -399,11 +399,17 @@ static int split_expand_impl(kmp_postings* ws, const SplitSrc& src, uint32_t n, 
         const bool bins = ws->bin_hi > ws->bin_lo;
         if (routed) {
             // the send regions pre-filled with kNoKey: by the received front's clear kernel, else here
+            // (a kernel, never a memset node: this sequence is captured as a HIP graph, and a captured
+            // hipMemsetAsync of the send buffer measured correct on the capturing launch but filled the
+            // whole buffer with pointer-sized garbage on the graph's first replay)
+            const uint64_t nfill = (uint64_t)parts * cap;
             if (recv && bins) {
                 ws->fill_p = d_send;
-                ws->fill_n = (uint64_t)parts * cap;
+                ws->fill_n = nfill;
             } else {
-                PG(hipMemsetAsync(d_send, 0xFF, (size_t)parts * cap * sizeof(unsigned long long), s));
+                const uint32_t grid = (uint32_t)std::min<uint64_t>(nfill / 2 / 256 / 8 + 1, 2048);
+                split_recv_clear_kernel<<<grid, 256, 0, s>>>(nullptr, 0, StepClear{}, d_send, nfill);
+                PG(hipGetLastError());
             }
             ws->route_send = d_send;
             ws->route_cap = cap;
@@ -506,7 +512,31 @@ static int split_expand_impl(kmp_postings* ws, const SplitSrc& src, uint32_t n, 
         (uintptr_t)src.d_res, (uintptr_t)src.d_res_off, (uintptr_t)src.d_class, (uintptr_t)src.d_krecv, src.kcap,
         (uintptr_t)d_send, (uintptr_t)d_flags, (uintptr_t)d_stats, ws->shard_cap, ws->spill_cap, ws->bp_J_min,
         ws->cur_on, ws->timing, ws->vreg_on ? ws->vreg_total + 1 : 0, (uintptr_t)kcur, ws->split_large};
+    if (getenv("KMP_TRACE"))
+        fprintf(stderr, "kmp-trace: split_expand n %u part %u/%u cap %llu recv %d kcap %llu routed %d large %d shard_cap %llu\n",
+                n, part, parts, (unsigned long long)cap, (int)recv, (unsigned long long)src.kcap, (int)routed,
+                (int)ws->split_large, (unsigned long long)ws->shard_cap);
     const int rc = slot_launch(ws, ws->split_g[0], key, enqueue, st);
+    if (getenv("KMP_TRACE") && rc == KMP_OK) {  // diagnostics: every routed key inside its region's rows
+        PG(hipStreamSynchronize(st));
+        std::vector<unsigned long long> h((size_t)parts * cap);
+        PG(hipMemcpy(h.data(), d_send, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        const unsigned pb = bits_for(n);
+        uint64_t bad = 0, keys = 0;
+        unsigned long long first = 0;
+        for (uint32_t d = 0; d < parts; ++d)
+            for (uint64_t i = 0; i < cap; ++i) {
+                const unsigned long long x = h[(size_t)d * cap + i];
+                if (x == kNoKey) continue;
+                ++keys;
+                const uint64_t p = x >> pb, q = x & ((1ull << pb) - 1);
+                if (p < rows.start[d] || p >= rows.start[d + 1] || q <= p || q >= n) {
+                    if (!bad++) first = x;
+                }
+            }
+        fprintf(stderr, "kmp-trace: split_expand part %u sent %llu keys, %llu outside their rows (first %llx)\n", part,
+                (unsigned long long)keys, (unsigned long long)bad, first);
+    }
     unbind();
     if (kcur) ws->kcur_dirty = false;
     ws->last_bucketed = true;
@@ -672,9 +702,7 @@ int kmp_dev_split_edges(kmp_postings* ws, const unsigned long long* d_keys, uint
         pt_bufs(ws, g, true, &e, st);
         PG(e);
         // u32 row-block keys (the fast tail's fixed or learned regions)
-        PG(ws->inc.reserve(pt_fast(ws, g) ? std::max<uint64_t>(m, g.freg ? (ws->freg_total + 1) / 2
-                                                                        : (uint64_t)g.nrb * g.ftcap / 2)
-                                          : m));
+        PG(ws->inc.reserve(pt_fast(ws, g) ? std::max<uint64_t>(m, (uint64_t)g.nrb * g.ftcap / 2) : m));
         PG(ws->uniq.reserve(m));  // staged p | q (u32 each)
         PG(ws->w.reserve(m));
         PG(ws->ovf.reserve((uint64_t)g.nrb + 1));
@@ -696,15 +724,40 @@ int kmp_dev_split_edges(kmp_postings* ws, const unsigned long long* d_keys, uint
         };
         const std::vector<unsigned long long> key = {m, n, row_lo, row_hi, c.min_shared, cap, (uintptr_t)d_keys,
                                                      (uintptr_t)d_p, (uintptr_t)d_q, (uintptr_t)d_w, g.rbits,
-                                                     ws->timing, ws->fast_tail, g.freg ? ws->freg_total + 1 : 0};
+                                                     ws->timing, ws->fast_tail};
+        if (getenv("KMP_TRACE")) {
+            fprintf(stderr,
+                    "kmp-trace: split_edges m %llu n %u rows [%u, %u) cap %llu rbits %u nrb %u fast %d inc %llu pt %llu\n",
+                    (unsigned long long)m, n, row_lo, row_hi, (unsigned long long)cap, g.rbits, g.nrb,
+                    (int)pt_fast(ws, g), (unsigned long long)ws->inc.n, (unsigned long long)ws->pt.n);
+            PG(hipStreamSynchronize(st));
+            std::vector<unsigned long long> h(m);
+            PG(hipMemcpy(h.data(), d_keys, m * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+            const unsigned pb = bits_for(n);
+            uint64_t bad = 0, keys = 0;
+            unsigned long long first = 0;
+            for (const unsigned long long x : h) {
+                if (x == kNoKey) continue;
+                ++keys;
+                const uint64_t p = x >> pb, q = x & ((1ull << pb) - 1);
+                if (p < row_lo || p >= row_hi || q <= p || q >= n)
+                    if (!bad++) first = x;
+            }
+            fprintf(stderr, "kmp-trace: split_edges received %llu keys, %llu outside rows (first %llx)\n",
+                    (unsigned long long)keys, (unsigned long long)bad, first);
+        }
         int rc = slot_launch(ws, ws->split_g[1], key, enqueue, st);
         if (rc != KMP_OK) return rc;
         PG(hipStreamSynchronize(st));
         const unsigned long long* rb = ws->hrb;
-        if (rb[kRbFast]) {  // a fast-tail region overflowed: learned regions, then the counting tail
-            const int rc = fast_overflow(ws, g, rb, st);
-            if (rc != KMP_OK) return rc;
+        if (rb[kRbFast]) {  // a fast-tail region overflowed: fewer rows per block, or the counting tail
+            fast_overflow(ws, g, rb);
             continue;
+        }
+        if (rb[kRbRange]) {  // a received key outside [row_lo, row_hi): nothing written out of bounds
+            PG(hipMemsetAsync(ws->flags.p + kFlRange, 0, sizeof(uint32_t), st));
+            PG(hipStreamSynchronize(st));
+            return KMP_EINVAL;
         }
         uint64_t ne = rb[kRbRuns];
         ws->last_fast = pt_fast(ws, g);

@@ -44,7 +44,9 @@ static_assert(kShards == 64, "the heavy tiles hash to a shard with a 6-bit shift
 // device flags of a step (ws->flags): a coarse bin above its level-2 tile budget, a class id too
 // wide for the key, the large-bucket list count, row blocks above the LDS capacity, the tile
 // budget an overflowing bin needs, a cursor-partition region overflow
-enum : uint32_t { kFlBin = 0, kFlClass = 1, kFlList = 2, kFlOvf = 3, kFlBinTiles = 4, kFlCur = 5, kFlSegs = 6, kFlSegMax = 7, kFlSend = 8, kFlN = 9 };
+// kFlRange: a pair key outside the call's row blocks reached the fast tail's scatter (dropped there;
+// the call fails with KMP_EINVAL instead of writing out of bounds)
+enum : uint32_t { kFlBin = 0, kFlClass = 1, kFlList = 2, kFlOvf = 3, kFlBinTiles = 4, kFlCur = 5, kFlSegs = 6, kFlSegMax = 7, kFlSend = 8, kFlRange = 9, kFlN = 10 };
 
 template <int kThreads>
 __device__ __forceinline__ void block_scan_n(uint32_t v, uint32_t& excl, uint32_t& total, uint32_t* wave_tot) {

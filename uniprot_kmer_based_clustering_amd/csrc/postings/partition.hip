@@ -1041,7 +1041,6 @@ struct PtGeom {
     uint32_t rowend;        // the call's last row + 1
     int binsort;            // the reduce sorts by bins (pt_bin_sort), else the block radix sort
     uint32_t ftcap;         // fast tail: keys per row-block region
-    const uint32_t* freg;   // fast tail: learned regions, block r at [freg[r], freg[r + 1]) (nullptr: r * ftcap)
 };
 
 template <class T>

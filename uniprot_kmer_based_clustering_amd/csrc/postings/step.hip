@@ -67,8 +67,6 @@ bool pt_geometry(const kmp_postings* ws, const StepCfg& c, uint64_t inc, PtGeom*
     g->nprot = c.n;
     g->rowend = c.ranged ? c.row_hi : c.n;
     g->ftcap = kFtCap;
-    g->freg = ws->freg_on && ws->freg_geom == std::vector<unsigned long long>{rb, g->nrb, g->row0} ? ws->freg.p
-                                                                                                  : nullptr;
     // the bin sort for scored blocks only (unscored at config 3: 0.130 -> 0.387 ms);
     // KMP_BINSORT_MODE (A/B builds): 0 the radix sort everywhere, 2 the bin sort everywhere
     g->binsort = KMP_BINSORT_MODE == 2 ? 1 : KMP_BINSORT_MODE == 0 ? 0 : (g->sbits != 0);
@@ -110,7 +108,7 @@ PtBufs pt_bufs(kmp_postings* ws, const PtGeom& g, bool reserve, hipError_t* e, h
 // the fast row-block tail applies: unscored keys, at most kFtRowsMax rows per block, not turned off
 // for the shape
 bool pt_fast(const kmp_postings* ws, const PtGeom& g) {
-    return ws->fast_tail && !g.sbits && g.rbits <= 10 && (1u << g.rbits) <= kFtRowsMax;
+    return ws->fast_tail && !g.sbits && g.rbits <= 10 && (1u << g.rbits) <= kFtRowsMax && g.nrb <= kFtScBlocks;
 }
 
 // spill segments: every one holds more than kHeavySub keys (a heavy group, or a whole bucket)
@@ -170,39 +168,26 @@ hipError_t small_reserve(kmp_postings* ws, hipStream_t st) {
     return e;
 }
 
-// A fast-tail region overflowed (kRbFast): learn the regions from this call's exact row-block counts
-// (the reduce kept them in counts[]: every key, dropped or not) with an eighth of slack, or first
-// fewer rows per block when a block is beyond what one reduce takes (kFtCap keys, unless its (row, q)
-// bins fit kFdBins); after kFregTries tries the counting tail for the shape
-constexpr uint32_t kFregTries = 3;
-int fast_overflow(kmp_postings* ws, const PtGeom& g, const unsigned long long* rb, hipStream_t st) {
-    if (ws->freg_tries >= kFregTries) {
-        ws->fast_tail = false;
-        ws->freg_on = false;
-        return KMP_OK;
-    }
-    ++ws->freg_tries;
+// A fast-tail row block passed its kFtCap-key region (kRbFast): fewer rows per block, by the largest
+// block's excess, at most kFastShrinks times; a single row above kFtCap, or blocks still too large
+// after that, turn the counting tail on for the shape.  (Regions learned from the blocks' exact
+// counts, with the blocks above kFtCap counted in LDS bins over (row, q), were measured and removed
+// in round 5: uniprot at k = 5 0.91 ms against 0.744 ms on the counting tail.)
+#ifndef KMP_FAST_SHRINKS
+#define KMP_FAST_SHRINKS 2
+#endif
+constexpr uint32_t kFastShrinks = KMP_FAST_SHRINKS;
+void fast_overflow(kmp_postings* ws, const PtGeom& g, const unsigned long long* rb) {
     const uint64_t most = rb[kRbMaxBlock];
-    const bool dense_ok = ((1ull << g.rbits) << g.pbits) <= kFdBins;
-    if (most > kFtCap && !dense_ok && g.rbits > 0) {
-        const double over = (double)most / (0.8 * kFtCap);
-        unsigned shrink = 1;
-        while (shrink < 16 && (double)(1u << shrink) < over) ++shrink;
-        ws->pt_rb_max = g.rbits > shrink ? g.rbits - shrink : 0u;
-        ws->freg_on = false;  // learned again on the new geometry if its blocks still overflow
-        return KMP_OK;
+    if (ws->fast_tries >= kFastShrinks || g.rbits == 0) {
+        ws->fast_tail = false;
+        return;
     }
-    hipError_t e = hipSuccess;
-    const PtBufs b = pt_bufs(ws, g, false, &e);
-    PG(ws->freg.reserve((uint64_t)g.nrb + 1));
-    vreg_kernel<<<1, 1024, 0, st>>>(b.counts, g.nrb, ws->freg.p);  // the same rule as the bucket regions
-    uint32_t tot = 0;
-    PG(hipMemcpyAsync(&tot, ws->freg.p + g.nrb, 4, hipMemcpyDeviceToHost, st));
-    PG(hipStreamSynchronize(st));
-    ws->freg_total = tot;
-    ws->freg_on = true;
-    ws->freg_geom = {g.rbits, g.nrb, g.row0};
-    return KMP_OK;
+    ++ws->fast_tries;
+    const double over = (double)most / (0.8 * kFtCap);
+    unsigned shrink = 1;
+    while (shrink < 16 && (double)(1u << shrink) < over) ++shrink;
+    ws->pt_rb_max = g.rbits > shrink ? g.rbits - shrink : 0u;
 }
 
 // buffers of one step (reserved before any launch, so a capture allocates nothing)
@@ -218,9 +203,7 @@ int step_reserve(kmp_postings* ws, const StepCfg& c, const PtGeom& g, hipStream_
     PG(ws->inc_sorted.reserve(total));
     if (!c.expand_only) {  // an expand-only call leaves the tail (and its staging) to tail_multi
         // u32 row-block keys (pt_scatter; the fast tail's fixed regions) ...
-        PG(ws->inc.reserve(pt_fast(ws, g) ? std::max<uint64_t>(total, g.freg ? (ws->freg_total + 1) / 2
-                                                                                 : (uint64_t)g.nrb * g.ftcap / 2)
-                                          : total));
+        PG(ws->inc.reserve(pt_fast(ws, g) ? std::max<uint64_t>(total, (uint64_t)g.nrb * g.ftcap / 2) : total));
         PG(ws->uniq.reserve(total));  // ... staged p | q (u32 each)
         PG(ws->w.reserve(total));     // ... staged w
         if (c.sb) PG(ws->stg2.reserve(2 * total));  // ... staged scores | second-k weights
@@ -298,14 +281,16 @@ int enqueue_tail_in(kmp_postings* ws, const StepCfg& c, const PtGeom& g, const u
     uint32_t* keys32 = reinterpret_cast<uint32_t*>(ws->inc.p);
     if (pt_fast(ws, g)) {  // one reduce that writes the edges (marks 4, 5, 6)
         const uint32_t jt = (uint32_t)(((g.flat_n ? g.flat_n : g.sc) + kFtScTile - 1) / kFtScTile);
-        const StepClear sc = ws->tail_clear ? StepClear{ws->flags.p, kFlN, ws->bstats.p, kGsWords, nullptr, 0} : StepClear{};
+        // (the clear leaves kFlRange, which its own workgroups may set meanwhile: reset where it is read)
+        const StepClear sc = ws->tail_clear ? StepClear{ws->flags.p, kFlRange, ws->bstats.p, kGsWords, nullptr, 0} : StepClear{};
+        static_assert(kFlRange + 1 == kFlN, "the range flag is the last one");
         pt_scatter_capped_kernel<<<dim3(jt, g.nshards), kFtScThreads, 0, st>>>(in, cursor, g, b.fcur, keys32, b.lb,
-                                                                                b.ticket, sc);
+                                                                                b.ticket, sc, ws->flags.p);
         ws->mark(4, st);
         pt_reduce_fast_kernel<<<g.nrb, kFtThreads, 0, st>>>(keys32, b.fcur, g, b.lb, b.ticket, c.d_p, c.d_q, c.d_w,
                                                              c.cap, c.stride,
                                                              PtPack{ws->bstats.p, ws->flags.p, nullptr, ws->hrb},
-                                                             ws->small.p + 1, b.counts);
+                                                             ws->small.p + 1);
         ws->mark(5, st);
         ws->mark(6, st);
         PG(hipGetLastError());
@@ -684,6 +669,14 @@ template <class Enqueue>
 int slot_launch(kmp_postings* ws, kmp_postings::GraphSlot& slot, std::vector<unsigned long long> key,
                 Enqueue enqueue, hipStream_t st) {
     key.push_back(g_grow_gen.load());
+    static const bool trace = getenv("KMP_TRACE") != nullptr;
+    if (trace)
+        fprintf(stderr, "kmp-trace: slot %p key[0..2] %llu %llu %llu gen %llu: %s\n", (void*)&slot, key[0],
+                key.size() > 1 ? key[1] : 0ull, key.size() > 2 ? key[2] : 0ull, key.back(),
+                !ws->graph_on ? "plain (graphs off)"
+                : (slot.gexec && slot.key == key) ? "replay"
+                : slot.seen != key                ? "plain (first)"
+                                                  : "capture");
     if (!ws->graph_on) return enqueue(st);
     if (slot.gexec && slot.key == key) {
         PG(hipGraphLaunch(slot.gexec, st));
@@ -810,8 +803,7 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
         ws->bp_J_min = 0;
         ws->heavy = false;
         ws->cur_on = ws->cur_mode;
-        ws->freg_on = false;
-        ws->freg_tries = 0;
+        ws->fast_tries = 0;
     }
     if (ws->shard_cap == 0) ws->shard_cap = c.slots / 4 / kShards + 4096;
     if (ws->spill_cap == 0) ws->spill_cap = 1024;
@@ -845,9 +837,8 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
             key.push_back(ws->fast_tail);
             key.push_back(ws->large_grid);
             key.push_back(ws->vreg_on ? ws->vreg_total + 1 : 0);
-            key.push_back(g.freg ? ws->freg_total + 1 : 0);
             int rc = fused_launch(ws, make_keys, key, c, g, st);
-            key.resize(key.size() - 10);
+            key.resize(key.size() - 9);
             if (rc != KMP_OK) return rc;
             PG(hipStreamSynchronize(st));
         } else {
@@ -955,15 +946,13 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
             if (rc != KMP_OK) return rc;
             PG(hipStreamSynchronize(st));
         }
-        if (rb[kRbFast]) {  // a fast-tail row-block region overflowed: learned regions (or fewer rows per block)
+        if (rb[kRbFast]) {  // a fast-tail row block passed its region: fewer rows per block, or the counting tail
             if (debug)
                 fprintf(stderr, "kmp: fast tail region overflow (rows per block %u, largest block %llu, try %u)\n",
-                        1u << g.rbits, rb[kRbMaxBlock], ws->freg_tries);
-            int rc = fast_overflow(ws, g, rb, st);
-            if (rc != KMP_OK) return rc;
+                        1u << g.rbits, rb[kRbMaxBlock], ws->fast_tries);
+            fast_overflow(ws, g, rb);
             continue;
         }
-        if (pt_fast(ws, g)) ws->freg_tries = 0;  // a call whose regions held
         ws->pt_inc = n_inc;  // sizes the next call's row blocks
         ws->last_fast = pt_fast(ws, g);
         ws->vreg_tries = 0;  // a call without a region overflow
@@ -972,6 +961,11 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
             uint32_t lg = rb[kRbList] ? 64u : 0u;
             while (lg && lg < kBucketLargeGrid && lg < 2 * rb[kRbList]) lg *= 2;
             ws->large_grid = lg;
+        }
+        if (rb[kRbRange]) {  // a pair key outside the call's rows (a device fault upstream)
+            PG(hipMemsetAsync(ws->flags.p + kFlRange, 0, sizeof(uint32_t), st));
+            PG(hipStreamSynchronize(st));
+            return KMP_EDEVICE;
         }
         uint64_t ne = rb[kRbRuns];
         ws->last_ovf = (uint32_t)rb[kRbOvf];

@@ -197,19 +197,25 @@ __global__ __launch_bounds__(kPtThreads) void pt_scatter_kernel(const unsigned l
 // of out, written as u32 (p - r * 2^rbits) << pbits | q (keys past the region are dropped; the
 // reduce sees the count and flags the overflow) — no histogram pass, no scan.  Workgroup (0, 0)
 // also clears the reduce's look-back words lb[0, nrb) and its ticket.  Tiles of 8,192 keys: twice the workgroups
-// of the counting tail's 16,384-key tiles (which ran one per CU), at LDS for two per CU.
+// of the counting tail's 16,384-key tiles (which ran one per CU), at LDS for two per CU: 80 KB at
+// most, so the histogram holds kFtScBlocks = kPtMaxBlocks - 16 row blocks (the fast tail's limit;
+// the full 8,192 plus the scan's words was 36 B over, one workgroup per CU)
 constexpr uint32_t kFtCap = 8192;  // fast tail, hash reduce: keys per row-block region
-constexpr uint32_t kFtScThreads = 512, kFtScTile = kFtScThreads * 16;
+constexpr uint32_t kFtScThreads = 512, kFtScTile = kFtScThreads * 16, kFtScBlocks = kPtMaxBlocks - 16;
 __global__ __launch_bounds__(kFtScThreads) void pt_scatter_capped_kernel(const unsigned long long* __restrict__ in,
                                                                          const unsigned long long* __restrict__ cursor,
                                                                          PtGeom g, uint32_t* __restrict__ cur,
                                                                          uint32_t* __restrict__ out,
                                                                          unsigned long long* __restrict__ lb,
-                                                                         uint32_t* __restrict__ ticket, StepClear sc) {
+                                                                         uint32_t* __restrict__ ticket, StepClear sc,
+                                                                         uint32_t* __restrict__ flags) {
     constexpr uint32_t kThr = kFtScThreads, kPer = 16;
-    __shared__ uint32_t lh[kPtMaxBlocks];
+    __shared__ uint32_t lh[kFtScBlocks];
     __shared__ uint32_t S[kFtScTile];
     __shared__ uint16_t SR[kFtScTile];
+    static_assert(sizeof(uint32_t) * (kFtScBlocks + kFtScTile + kFtScThreads / 64 + 1) + sizeof(uint16_t) * kFtScTile <=
+                      80 * 1024,
+                  "two workgroups per CU");
     __shared__ uint32_t wave_tot[kThr / 64];
     __shared__ uint32_t s_n;
     const uint32_t j = blockIdx.x, s = blockIdx.y;
@@ -233,14 +239,23 @@ __global__ __launch_bounds__(kFtScThreads) void pt_scatter_capped_kernel(const u
     const unsigned sh = g.pbits + g.rbits;
     const unsigned long long lowm = (1ull << sh) - 1;
     const unsigned long long base = (unsigned long long)g.row0 << g.pbits;
+    const unsigned long long span = (unsigned long long)g.nrb << sh;  // the call's row blocks
     unsigned long long x[kPer];
     uint32_t rk[kPer];
+    bool outside = false;
 #pragma unroll
     for (uint32_t e = 0; e < kPer; ++e) {
         const uint32_t i = threadIdx.x + e * kThr;
         x[e] = i < m ? src[i] : kNoKey;
-        if (x[e] != kNoKey) x[e] -= base;  // rows from row0
+        if (x[e] != kNoKey) {
+            x[e] -= base;  // rows from row0 (a row below it wraps past the span)
+            if (x[e] >= span) {
+                outside = true;
+                x[e] = kNoKey;
+            }
+        }
     }
+    if (outside) flags[kFlRange] = 1;
     uint32_t nk = 0;
 #pragma unroll
     for (uint32_t e = 0; e < kPer; ++e) {
@@ -260,17 +275,20 @@ __global__ __launch_bounds__(kFtScThreads) void pt_scatter_capped_kernel(const u
     uint32_t rbase[kQ];
 #pragma unroll
     for (uint32_t t = 0; t < kQ; ++t)  // reserved while the tile is placed
+#ifndef KMP_AB_SC
         rbase[t] = cnt[t] ? atomicAdd(&cur[threadIdx.x + t * kThr], cnt[t]) : 0u;
-    // block r's region: [r * ftcap, (r + 1) * ftcap), or the learned [freg[r], freg[r + 1]); a run
-    // that does not fit is dropped whole (the cursor still counts it: the reduce flags the block)
+#else  // A/B timing only (wrong results): no reservation atomics
+        rbase[t] = (j * 4) % 4096;
+#endif
+    // block r's region: [r * ftcap, (r + 1) * ftcap); a run that does not fit is dropped whole (the
+    // cursor still counts it: the reduce flags the block)
     uint32_t rabs[kQ];
 #pragma unroll
     for (uint32_t t = 0; t < kQ; ++t) {
         const uint32_t r = threadIdx.x + t * kThr;
         rabs[t] = 0xFFFFFFFFu;
         if (cnt[t]) {
-            const uint32_t b0 = g.freg ? g.freg[r] : r * g.ftcap, cp = g.freg ? g.freg[r + 1] - b0 : g.ftcap;
-            if (rbase[t] + cnt[t] <= cp) rabs[t] = b0 + rbase[t];
+            if (rbase[t] + cnt[t] <= g.ftcap) rabs[t] = r * g.ftcap + rbase[t];
         }
     }
 #pragma unroll
@@ -1076,7 +1094,7 @@ __global__ __launch_bounds__(256) void pt_emit_kernel(const uint32_t* __restrict
 // read-back: gstats (8 per shard) | pair cursors | spill cursors | the words below
 enum : uint32_t {
     kRbCursor = kShards * 8, kRbSpill = kShards * 9, kRbFlagBin = kShards * 10, kRbFlagClass, kRbRuns, kRbOvf,
-    kRbMaxBlock, kRbBinTiles, kRbFlagCur, kRbSegs, kRbSegMax, kRbFast, kRbList, kRbWords
+    kRbMaxBlock, kRbBinTiles, kRbFlagCur, kRbSegs, kRbSegMax, kRbFast, kRbList, kRbRange, kRbWords
 };
 constexpr uint32_t kGsWords = kShards * 10;  // gstats | cursors | spill cursors (u64)
 
@@ -1109,6 +1127,7 @@ __device__ void step_pack_body(const unsigned long long* __restrict__ gstats, co
         rb[kRbFlagCur] = flags[kFlCur];
         rb[kRbSegs] = flags[kFlSegs];
         rb[kRbSegMax] = flags[kFlSegMax];
+        rb[kRbRange] = flags[kFlRange];
     }
     __threadfence_system();  // rb is host memory, read after the stream synchronises
 }
@@ -1127,20 +1146,15 @@ __device__ void step_pack_body(const unsigned long long* __restrict__ gstats, co
 //                     else of the block waits on it until the copy-out).  It re-zeroes fcur[r] for the
 //                     next call.  A block above kFtHashMax keys, one with a row of more than
 //                     kFtRankMax pairs, or one whose pair count would pass 16 bits sorts its keys
-//                     instead (block radix sort + run-length encoding).  A block above kFtCap keys
-//                     (its region overflowed) raises the read-back's kRbFast word: the caller reruns
-//                     the call on the counting tail and keeps it for the shape.
+//                     instead (block radix sort + run-length encoding).  A block whose region
+//                     overflowed, or above kFtCap keys, raises the read-back's kRbFast word: the
+//                     caller learns the regions from the blocks' exact counts (fast_overflow), or
+//                     takes fewer rows per block, and after kFregTries the counting tail for the shape.
+//                     (A dense variant counting blocks above kFtCap in LDS bins over (row, q) was
+//                     measured and removed in round 5: uniprot at k = 5 0.91 ms against 0.744 ms on
+//                     the counting tail, and its 64 KB of bins held the reduce to two workgroups per CU.)
 // The last block writes the edge count and the step's read-back.
 constexpr uint32_t kFtThreads = 512, kFtHashMax = 6144, kFtSlots = 8192, kFtRowsMax = 1024, kFtRankMax = 256;
-// a block above kFtCap keys (a learned region: rows pairing with thousands of later proteins, the
-// reference's uniprot_arg at k = 5) is counted in LDS bins over (row, q): up to kFdBins bins (u16
-// counts, two per word, 64 KB aliased on the hash table), so the bins are the canonical order
-constexpr uint32_t kFdBins = 32768, kFdWords = kFdBins / 2;
-// thread t owns the contiguous words [t q, t q + q) (q = 2^qs); stored XOR-swizzled so the owners'
-// reads of their words hit distinct banks
-__device__ __forceinline__ uint32_t fd_phys(uint32_t w, unsigned qs) {
-    return w ^ ((w >> qs) & ((1u << min(qs, 5u)) - 1));
-}
 constexpr uint32_t kFtEmpty = 0xFFFFFFFFu;
 constexpr unsigned long long kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbOvf = 1ull << 61;
 static_assert(kFtCap == 16 * kFtThreads && kFtHashMax <= 12 * kFtThreads && kFtSlots == 16 * kFtThreads,
@@ -1207,16 +1221,21 @@ struct FtLds {
                                        // sort path's run heads use C[0, nruns] (nruns <= kFtCap)
         } h;
         typename PtSort<16>::storage_type s16;
-        uint32_t W[kFdWords];  // dense block: u16 counts per (row, q) bin, two per word
+        uint32_t last[kFtThreads];  // the sort path: each thread's last sorted key
     };
     uint32_t RC[kFtRowsMax + 1];  // pairs per row -> row starts
-    uint32_t last[kFtThreads];
     uint32_t wave_tot[kFtThreads / 64];
     uint32_t s_max, s_flag;
     unsigned long long s_excl;
 };
 
-__global__ __launch_bounds__(kFtThreads) void pt_reduce_fast_kernel(const uint32_t* __restrict__ keys,
+// KMP_FT_WAVES: waves per SIMD the fast reduce is compiled for (0: the compiler's choice).  6: at
+// most 80 VGPRs, so three 512-thread workgroups per CU (53 KB of LDS each): pair_sort_rle 0.083 ->
+// 0.071 ms at config 3
+#ifndef KMP_FT_WAVES
+#define KMP_FT_WAVES 6
+#endif
+__global__ __launch_bounds__(kFtThreads, KMP_FT_WAVES ? KMP_FT_WAVES : 1) void pt_reduce_fast_kernel(const uint32_t* __restrict__ keys,
                                                                     uint32_t* __restrict__ fcur, PtGeom g,
                                                                     unsigned long long* __restrict__ lb,
                                                                     uint32_t* __restrict__ ticket,
@@ -1224,8 +1243,7 @@ __global__ __launch_bounds__(kFtThreads) void pt_reduce_fast_kernel(const uint32
                                                                     uint32_t* __restrict__ d_q,
                                                                     uint32_t* __restrict__ d_w, uint64_t cap,
                                                                     uint32_t stride, PtPack pack,
-                                                                    uint32_t* __restrict__ runs,
-                                                                    uint32_t* __restrict__ counts) {
+                                                                    uint32_t* __restrict__ runs) {
     __shared__ FtLds u;
     __shared__ uint32_t s_r, s_n;
     const uint32_t tid = threadIdx.x;
@@ -1248,90 +1266,14 @@ __global__ __launch_bounds__(kFtThreads) void pt_reduce_fast_kernel(const uint32
     for (uint32_t i = tid; i <= R; i += kFtThreads) u.RC[i] = 0;
     __syncthreads();
     const uint32_t r = s_r, nraw = s_n;
-    // the block's region; its exact count is kept (counts[r]) so an overflowing call can learn the
-    // regions, and the largest block goes to the read-back (runs[2] -> kRbMaxBlock)
-    const uint32_t rb0 = g.freg ? g.freg[r] : r * kFtCap, rcap = g.freg ? g.freg[r + 1] - rb0 : kFtCap;
-    if (tid == 0) {
-        counts[r] = nraw;
-        if (nraw) atomicMax(&runs[2], nraw);
-    }
-    // a block above kFtCap keys takes the dense bins when (row, q) fits them
-    const uint32_t fd_words = (R << pb) / 2;
-    const bool dense_ok = (R << pb) <= kFdBins && (R << pb) >= 2;
-    bool ovf = nraw > rcap || (nraw > kFtCap && !dense_ok);
+    // the block's region [r kFtCap, (r + 1) kFtCap); the largest block goes to the read-back (runs[2]
+    // -> kRbMaxBlock: how many fewer rows per block an overflowing call takes)
+    if (tid == 0 && nraw) atomicMax(&runs[2], nraw);
+    bool ovf = nraw > kFtCap;
     const uint32_t n = ovf ? 0u : nraw;
-    const uint32_t* src = keys + rb0;
+    const uint32_t* src = keys + (uint64_t)r * kFtCap;
     uint32_t D = 0;  // the block's kept pairs
     bool sort = n > kFtHashMax, published = false;
-    if (n > kFtCap) {
-        // ---- dense block: counts in (row, q) bins, read back in bin order ----
-        unsigned qs = 0;  // q = 2^qs words per thread (at least one)
-        while ((kFtThreads << qs) < fd_words) ++qs;
-        for (uint32_t i = tid; i < fd_words; i += kFtThreads) u.W[i] = 0;
-        __syncthreads();
-        for (uint32_t i0 = 0; i0 < n; i0 += 8 * kFtThreads) {  // loads in batches ahead of their atomics
-            uint32_t x[8];
-#pragma unroll
-            for (uint32_t e = 0; e < 8; ++e) {
-                const uint32_t i = i0 + e * kFtThreads + tid;
-                x[e] = i < n ? src[i] : kFtEmpty;
-            }
-#pragma unroll
-            for (uint32_t e = 0; e < 8; ++e)
-                if (x[e] != kFtEmpty) {
-                    const uint32_t sh = 16 * (x[e] & 1u);
-                    const uint32_t old = atomicAdd(&u.W[fd_phys(x[e] >> 1, qs)], 1u << sh);
-                    if (((old >> sh) & 0xFFFFu) >= 0xFFFEu) u.s_flag = 1;
-                }
-        }
-        __syncthreads();
-        const bool fov = u.s_flag != 0;  // (uniform) a count would pass 16 bits: flagged, nothing written
-        const uint32_t qn = 1u << qs, w0 = tid << qs;
-        uint32_t kept = 0;
-        if (!fov)
-            for (uint32_t j = 0; j < qn && w0 + j < fd_words; ++j) {
-                const uint32_t v = u.W[fd_phys(w0 + j, qs)];
-                kept += ((v & 0xFFFFu) >= g.min_shared) + ((v >> 16) >= g.min_shared);
-            }
-        uint32_t excl;
-        block_scan_n<kFtThreads>(kept, excl, D, u.wave_tot);
-        if (tid < 64) {
-            const unsigned long long ex = ft_lookback(lb, r, (unsigned long long)D | (fov ? kLbOvf : 0ull));
-            if (tid == 0) u.s_excl = ex;
-        }
-        __syncthreads();
-        const unsigned long long ex = u.s_excl;
-        uint64_t o = (uint32_t)ex + (uint64_t)excl;
-        const uint32_t rowbase = g.row0 + (r << g.rbits), qm = (1u << pb) - 1;
-        if (kept)
-            for (uint32_t j = 0; j < qn && w0 + j < fd_words; ++j) {
-                const uint32_t v = u.W[fd_phys(w0 + j, qs)];
-#pragma unroll
-                for (uint32_t h = 0; h < 2; ++h) {
-                    const uint32_t c = h ? v >> 16 : v & 0xFFFFu;
-                    if (c < g.min_shared || c == 0) continue;
-                    const uint32_t bin = 2 * (w0 + j) + h;
-                    if (o < cap) {
-                        d_p[o * stride] = rowbase + (bin >> pb);
-                        d_q[o * stride] = bin & qm;
-                        d_w[o * stride] = c;
-                    }
-                    ++o;
-                }
-            }
-        ovf = fov;
-        sort = false;
-        if (r + 1 == gridDim.x) {  // the last block: the edge count and the read-back
-            const bool any_ovf = ovf || (ex & kLbOvf);
-            if (tid == 0) {
-                runs[0] = (uint32_t)ex + D;
-                runs[1] = atomicExch(&runs[2], 0u);  // the largest block, reset for the next call
-            }
-            __syncthreads();
-            if (pack.rb) step_pack_body(pack.gstats, pack.flags, runs, pack.rb, any_ovf ? 1ull : 0ull);
-        }
-        return;
-    }
     if (!sort) {
         // ---- hash aggregation: pair -> slot, count per slot (the table was cleared above) ----
         uint32_t x[12];
@@ -1425,6 +1367,7 @@ __global__ __launch_bounds__(kFtThreads) void pt_reduce_fast_kernel(const uint32
             k[e] = i < n ? src[i] : kFtEmpty;
         }
         PtSort<16>().sort(k, u.s16, 0, pb + g.rbits + 1);  // blocked: thread t holds ranks t * 16 + e
+        __syncthreads();  // last aliases the sort storage
         u.last[tid] = k[15];
         __syncthreads();
         uint32_t prev = tid ? u.last[tid - 1] : 0u, nh = 0;

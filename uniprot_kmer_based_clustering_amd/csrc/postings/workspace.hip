@@ -56,14 +56,8 @@ struct kmp_postings {
     uint32_t large_used = 1024;  // ... the grid the last front launched
     bool fast_mode = true;      // kmp_postings_set_tail: the fast tail allowed
     bool fast_tail = true;      // unscored calls take the fast row-block tail (off for a shape whose
-                                // row-block regions overflowed kFregTries times: kRbFast)
-    // the fast tail's learned regions (a call whose fixed regions overflowed: the exact counts of its
-    // row blocks + 1/8 + 64, prefix-summed), for the geometry they were learned on (rbits, nrb, row0)
-    Grow<uint32_t> freg;
-    bool freg_on = false;
-    uint64_t freg_total = 0;
-    uint32_t freg_tries = 0;
-    std::vector<unsigned long long> freg_geom;
+                                // row blocks still pass kFtCap after kFastShrinks tries: kRbFast)
+    uint32_t fast_tries = 0;    // ... fewer rows per block tried so far
     const uint32_t* small_zero_p = nullptr;  // the ws->small allocation that was cleared
     uint32_t bp_J = 0;          // level-2 tiles per coarse bin ...
     uint32_t bp_J_min = 0;      // ... at least (learned from an overflowing bin)

@@ -214,6 +214,14 @@ class ShardPipeline(_SplitEdges):
                                         heavy_df, int(require_class_diff), part, parts, cap, lp, _p(send),
                                         _p(flags), _p(stats), _stream()), "kmp_dev_split_group")
 
+    def gathered_pipeline(self, residues: torch.Tensor) -> "DevicePipeline":
+        """A DevicePipeline over the whole batch rebuilt from every rank's slice (the residue start
+        and the row-split fallback of dist.sharded_split_step); built once per batch, its residues
+        refreshed in place afterwards."""
+        from .engine import Proteins
+        cls = self.cls.cpu().numpy().view(np.uint16)[:self.n]
+        return DevicePipeline(Proteins(residues.cpu().numpy(), self.offsets_host, cls), self.k, self.dev)
+
     def own_residues(self):
         """(lo, hi, tensor): the residues this rank contributes when the batch is rebuilt on every
         rank (the row-split fallback): [res_lo, the next rank's res_lo) within its slice."""

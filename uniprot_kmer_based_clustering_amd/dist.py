@@ -22,6 +22,11 @@ A pair's incidences from every k-mer meet on its row owner, so w is complete the
 concatenation of the ranks' edges is the canonical list, and with ``gather`` rank 0 receives every
 rank's block behind its own (point-to-point) so the timed step ends with the whole list on rank 0.
 
+**The start exchange** (``start_mode``): from KEYS_START_MIN_WORLD = 8 ranks up the keys
+all-to-all above; below it the ranks all-gather their residue slices instead (1 B per residue:
+15 MB per rank at G = 2 against 67 MB of padded key regions) and every rank keys every window,
+keeping its own bins (``kmer_split_step`` on the rebuilt batch, refreshed in place every step).
+
 **Fallbacks.**  Class ids wider than the key's class field (every rank sees KMP_SPLIT_CLASS in the
 reduced flags) rebuild the batch on every rank with an all-gather of the residue slices and take
 the row split (``distributed_step``: every rank groups every k-mer and expands only its own rows,
@@ -120,6 +125,8 @@ class SplitState:
         self.kbufs = None  # ... its send and receive buffers
         self.reruns = 0
         self.rerun_flags = []  # the reduced flags of each rerun (diagnostics)
+        self.full = None  # residue start: the whole batch rebuilt on this rank (a DevicePipeline)
+        self.spans = None  # ... and every rank's residue range
 
 
 def _pipe_state(pipe) -> SplitState:
@@ -233,6 +240,53 @@ def kmer_split_step(pipe, rank: int, world: int, group=None, min_shared: int = 1
     return total
 
 
+# the sharded start's first exchange: keys (all-to-all of 8-B window keys, each rank keys only its
+# own windows) from this many ranks up, residues (all-gather of the 1-B residue slices, then every
+# rank keys every window and keeps its bins) below.  Bytes per rank at config 4: keys 66.7 / 50.3
+# / 30.1 MB (G = 2 / 4 / 8, padded regions) against residues 15.0 / 22.5 / 26.3 MB; the residue
+# start re-keys the whole batch (~0.09 ms per rank) where the key start keys 1/G of it
+KEYS_START_MIN_WORLD = 8
+
+
+def start_mode(start: str, world: int) -> str:
+    """'keys' or 'residues' for sharded_split_step's `start` ('auto' picks by world size)."""
+    if start == "auto":
+        return "keys" if world >= KEYS_START_MIN_WORLD else "residues"
+    if start not in ("keys", "residues"):
+        raise ValueError(f"unknown sharded start {start!r}")
+    return start
+
+
+def residue_spans(pipe, group=None) -> list:
+    """[(lo, hi)] per rank: the residue ranges the ranks contribute (own_residues), all-gathered."""
+    world = dist.get_world_size(group)
+    lo, hi, own = pipe.own_residues()
+    spans = torch.zeros(2 * world, dtype=torch.int64, device=own.device)
+    dist.all_gather_into_tensor(spans, torch.tensor([lo, hi], dtype=torch.int64, device=own.device), group=group)
+    return [tuple(x) for x in spans.view(world, 2).tolist()]
+
+
+def gather_residues_into(pipe, dst: torch.Tensor, spans: list, group=None) -> None:
+    """The packed batch in dst on every rank: this rank's slice copied in, every other rank's slice
+    received straight into its place (point-to-point over xGMI on RCCL; no staging buffer)."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    lo, hi, own = pipe.own_residues()
+    if hi > lo:
+        dst[lo:hi].copy_(own)
+    ops = []
+    for r in range(world):
+        if r == rank:
+            continue
+        if hi > lo:
+            ops.append(dist.P2POp(dist.isend, dst[lo:hi], r, group=group))
+        l, h = spans[r]
+        if h > l:
+            ops.append(dist.P2POp(dist.irecv, dst[l:h], r, group=group))
+    for w in (dist.batch_isend_irecv(ops) if ops else []):
+        w.wait()
+
+
 def gather_residues(pipe, group=None):
     """The whole packed batch on every rank, from the ranks' slices (an all-gather over RCCL): the
     row-split fallback of the sharded start.  Bytes no rank holds belong to proteins with fewer than
@@ -255,16 +309,11 @@ def gather_residues(pipe, group=None):
     return res[:pipe.total]
 
 
-def _row_split_from_shards(pipe, rank, world, group, min_shared, require_class_diff, gather):
+def _row_split_from_shards(pipe, rank, world, group, min_shared, require_class_diff, gather, st):
     """The row split over the rebuilt batch (class ids too wide for the k-mer split's key)."""
-    from .device import DevicePipeline
-    from .engine import Proteins
-    full = pipe.__dict__.get("_full")
-    if full is None:
-        res = gather_residues(pipe, group).cpu().numpy()
-        cls = pipe.cls.cpu().numpy().view(np.uint16)
-        full = DevicePipeline(Proteins(res, pipe.offsets_host, cls), pipe.k, pipe.dev)
-        pipe.__dict__["_full"] = full
+    if st.full is None:
+        st.full = pipe.gathered_pipeline(gather_residues(pipe, group))
+    full = st.full
     if gather:
         m = distributed_step(full, rank, world, group, min_shared, require_class_diff)
     else:
@@ -274,18 +323,53 @@ def _row_split_from_shards(pipe, rank, world, group, min_shared, require_class_d
     return m
 
 
+def _residue_start(pipe, rank, world, group, min_shared, require_class_diff, st, timings):
+    """The sharded start through the residues: the ranks' slices all-gathered into a whole batch
+    (built once per batch, refreshed in place every step), then the k-mer split with every rank
+    keying every window (kmer_split_step).  The rank's edges end in pipe.ep/eq/ew."""
+    cuda = pipe.dev.type == "cuda"
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)] if timings is not None and cuda else None
+    if ev:
+        ev[0].record()
+    if st.full is None:
+        st.spans = residue_spans(pipe, group)
+        st.full = pipe.gathered_pipeline(gather_residues(pipe, group))
+    else:
+        gather_residues_into(pipe, st.full.res, st.spans, group)
+    if ev:
+        ev[1].record()
+    inner = [] if timings is not None else None
+    # the same SplitState: the pair-key capacity, reruns and fallback are the step's
+    m = kmer_split_step(st.full, rank, world, group, min_shared, require_class_diff, state=st, timings=inner)
+    full = st.full
+    pipe.ep, pipe.eq, pipe.ew, pipe.n_edges = full.ep, full.eq, full.ew, m
+    pipe.edge_cap = full.edge_cap
+    if timings is not None and inner:
+        gx = ev[0].elapsed_time(ev[1]) if ev else 0.0
+        timings.append((0.0, gx) + tuple(inner[-1]))
+    return m
+
+
 def sharded_split_step(pipe, rank: int, world: int, group=None, min_shared: int = 1,
                        require_class_diff: bool = True, gather: bool = False, state: SplitState | None = None,
-                       timings: list | None = None) -> int:
+                       timings: list | None = None, start: str = "auto") -> int:
     """One multi-GPU step of the k-mer split with a sharded start (module docstring): keys, key
     all-to-all, group + expand, pair-key all-to-all, edges.  Every rank ends holding the canonical
     edges of its row range in pipe.ep/eq/ew and returns their count; with gather, rank 0 also
-    receives every rank's block behind its own and returns the total.  timings: a list to append
-    this rank's (keys, key exchange, group, pair exchange, edges) milliseconds to (CUDA events on
-    the current stream, which the library's stages and the collectives are ordered with)."""
+    receives every rank's block behind its own and returns the total.  start: 'keys' (the key
+    all-to-all), 'residues' (all-gather of the residue slices, then every rank keys the batch) or
+    'auto' (keys from KEYS_START_MIN_WORLD ranks up).  timings: a list to append this rank's
+    (keys, start exchange, group, pair exchange, edges) milliseconds to (CUDA events on the current
+    stream, which the library's stages and the collectives are ordered with; the residue start's
+    keys are 0 and its group is the whole expand)."""
     st = state if state is not None else _pipe_state(pipe)
     if st.row_split:
-        return _row_split_from_shards(pipe, rank, world, group, min_shared, require_class_diff, gather)
+        return _row_split_from_shards(pipe, rank, world, group, min_shared, require_class_diff, gather, st)
+    if world > 1 and start_mode(start, world) == "residues":
+        m = _residue_start(pipe, rank, world, group, min_shared, require_class_diff, st, timings)
+        if not gather:
+            return m
+        return _gather_to_rank0(pipe, m, rank, world, group)
     lo, hi = row_ranges(pipe.n, world)[rank]
     dev = pipe.dev
     cuda = dev.type == "cuda"
@@ -344,7 +428,7 @@ def sharded_split_step(pipe, rank: int, world: int, group=None, min_shared: int 
         fl = [int(x) for x in st.host_flags.tolist()]
         if fl[_lib.KMP_SPLIT_CLASS]:
             st.row_split = True
-            return _row_split_from_shards(pipe, rank, world, group, min_shared, require_class_diff, gather)
+            return _row_split_from_shards(pipe, rank, world, group, min_shared, require_class_diff, gather, st)
         if fl[_lib.KMP_SPLIT_RERUN] or fl[_lib.KMP_SPLIT_HEAVY]:  # HEAVY: the heavy path on every rank
             st.reruns += 1
             st.rerun_flags.append(fl)
@@ -363,6 +447,11 @@ def sharded_split_step(pipe, rank: int, world: int, group=None, min_shared: int 
         raise RuntimeError("k-mer split: capacities unstable across reruns")
     if not gather or world == 1:
         return m
+    return _gather_to_rank0(pipe, m, rank, world, group)
+
+
+def _gather_to_rank0(pipe, m, rank, world, group):
+    """gather_rows of the rank's m edges onto rank 0 (which grows its arrays when they are short)."""
 
     def grow(total):
         old = (pipe.ep[:m].clone(), pipe.eq[:m].clone(), pipe.ew[:m].clone())
