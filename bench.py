@@ -257,6 +257,10 @@ def bench_config5(args):
             e.pairs_stream(ks, score=score)
         if world > 1:
             dist.barrier()
+        # a marker kernel between the warm-up and the timed streams (untimed): profiles of this
+        # command keep what follows it (tools/pmc_config5.py, tools/trace_after_marker.py)
+        torch.cuda._sleep(1000)
+        torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):
             sm = e.pairs_stream(ks, score=score)

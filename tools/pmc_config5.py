@@ -21,8 +21,16 @@ STAGE = {  # bench_config5's stage names
 
 
 def load(path):
+    """Per kernel, the counter summed over the dispatches after the last marker kernel (torch's
+    spin_kernel, which bench.py launches between the warm-up and the timed stream), or over every
+    dispatch of a run without one."""
+    rows = list(csv.DictReader(open(path)))
+    marks = [int(r["Dispatch_Id"]) for r in rows if "spin_kernel" in r["Kernel_Name"]]
+    after = max(marks) if marks else -1
     out = collections.defaultdict(float)
-    for r in csv.DictReader(open(path)):
+    for r in rows:
+        if int(r["Dispatch_Id"]) <= after or "spin_kernel" in r["Kernel_Name"]:
+            continue
         out[short(r["Kernel_Name"]).removeprefix("void ").split("<")[0]] += float(r["Counter_Value"]) * 1024.0
     return out
 

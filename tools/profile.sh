@@ -34,12 +34,13 @@ traffic)
 traffic5)
   # config 5: the fused reduce's and the expansion's kernels only (one step; each pass its own run)
   tag=$1
-  re="pt_hist|pt_tscan|pt_scatter_kernel|pt_split|pt_window_count|pt_reduce_count|pt_reduce_write|heavy_flat|bucket_small|bucket_large|edge_digest"
+  # (the warm step: one warm-up stream, then the marker kernel the table starts after)
+  re="pt_hist|pt_tscan|pt_scatter_kernel|pt_split|pt_window_count|pt_reduce_count|pt_reduce_write|heavy_flat|bucket_small|bucket_large|edge_digest|spin_kernel"
   rm -rf gpurun_out/pmc5_fetch_$tag gpurun_out/pmc5_write_$tag
-  timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$re" --output-format csv -d gpurun_out/pmc5_fetch_$tag -o run -- \
-    python3 bench.py --config config5 --no-cpu-baseline > gpurun_out/pmc5_fetch_$tag.log 2>&1
-  timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$re" --output-format csv -d gpurun_out/pmc5_write_$tag -o run -- \
-    python3 bench.py --config config5 --no-cpu-baseline > gpurun_out/pmc5_write_$tag.log 2>&1
+  timeout -s KILL 500 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$re" --output-format csv -d gpurun_out/pmc5_fetch_$tag -o run -- \
+    python3 bench.py --config config5 --no-cpu-baseline --warmup 1 > gpurun_out/pmc5_fetch_$tag.log 2>&1
+  timeout -s KILL 500 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$re" --output-format csv -d gpurun_out/pmc5_write_$tag -o run -- \
+    python3 bench.py --config config5 --no-cpu-baseline --warmup 1 > gpurun_out/pmc5_write_$tag.log 2>&1
   python3 tools/pmc_config5.py $(find gpurun_out/pmc5_fetch_$tag -name 'run_counter_collection.csv') \
     $(find gpurun_out/pmc5_write_$tag -name 'run_counter_collection.csv') gpurun_out/pmc_config5_$tag.json
   ;;

@@ -201,7 +201,10 @@ __global__ __launch_bounds__(kPtThreads) void pt_scatter_kernel(const unsigned l
 // most, so the histogram holds kFtScBlocks = kPtMaxBlocks - 16 row blocks (the fast tail's limit;
 // the full 8,192 plus the scan's words was 36 B over, one workgroup per CU)
 constexpr uint32_t kFtCap = 8192;  // fast tail, hash reduce: keys per row-block region
-constexpr uint32_t kFtScThreads = 512, kFtScTile = kFtScThreads * 16, kFtScBlocks = kPtMaxBlocks - 16;
+#ifndef KMP_FTSC_BLOCKS
+#define KMP_FTSC_BLOCKS (kPtMaxBlocks - 16)
+#endif
+constexpr uint32_t kFtScThreads = 512, kFtScTile = kFtScThreads * 16, kFtScBlocks = KMP_FTSC_BLOCKS;
 __global__ __launch_bounds__(kFtScThreads) void pt_scatter_capped_kernel(const unsigned long long* __restrict__ in,
                                                                          const unsigned long long* __restrict__ cursor,
                                                                          PtGeom g, uint32_t* __restrict__ cur,
@@ -213,8 +216,9 @@ __global__ __launch_bounds__(kFtScThreads) void pt_scatter_capped_kernel(const u
     __shared__ uint32_t lh[kFtScBlocks];
     __shared__ uint32_t S[kFtScTile];
     __shared__ uint16_t SR[kFtScTile];
-    static_assert(sizeof(uint32_t) * (kFtScBlocks + kFtScTile + kFtScThreads / 64 + 1) + sizeof(uint16_t) * kFtScTile <=
-                      80 * 1024,
+    static_assert(KMP_FTSC_BLOCKS != kPtMaxBlocks - 16 ||
+                      sizeof(uint32_t) * (kFtScBlocks + kFtScTile + kFtScThreads / 64 + 1) +
+                              sizeof(uint16_t) * kFtScTile <= 80 * 1024,
                   "two workgroups per CU");
     __shared__ uint32_t wave_tot[kThr / 64];
     __shared__ uint32_t s_n;
@@ -239,23 +243,28 @@ __global__ __launch_bounds__(kFtScThreads) void pt_scatter_capped_kernel(const u
     const unsigned sh = g.pbits + g.rbits;
     const unsigned long long lowm = (1ull << sh) - 1;
     const unsigned long long base = (unsigned long long)g.row0 << g.pbits;
-    const unsigned long long span = (unsigned long long)g.nrb << sh;  // the call's row blocks
     unsigned long long x[kPer];
     uint32_t rk[kPer];
-    bool outside = false;
 #pragma unroll
     for (uint32_t e = 0; e < kPer; ++e) {
         const uint32_t i = threadIdx.x + e * kThr;
         x[e] = i < m ? src[i] : kNoKey;
-        if (x[e] != kNoKey) {
-            x[e] -= base;  // rows from row0 (a row below it wraps past the span)
-            if (x[e] >= span) {
+        if (x[e] != kNoKey) x[e] -= base;  // rows from row0 (a row below it wraps past the span)
+    }
+    if (g.flat_n) {
+        // received keys (the k-mer split's edges phase: another rank's output): a key outside the
+        // call's row blocks is dropped and fails the call, never indexes past the histogram.  The
+        // call's own bucket kernels (one GPU) write nothing else, so its step skips the test
+        const unsigned long long span = (unsigned long long)g.nrb << sh;
+        bool outside = false;
+#pragma unroll
+        for (uint32_t e = 0; e < kPer; ++e)
+            if (x[e] != kNoKey && x[e] >= span) {
                 outside = true;
                 x[e] = kNoKey;
             }
-        }
+        if (outside) flags[kFlRange] = 1;
     }
-    if (outside) flags[kFlRange] = 1;
     uint32_t nk = 0;
 #pragma unroll
     for (uint32_t e = 0; e < kPer; ++e) {
