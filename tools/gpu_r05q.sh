@@ -1,0 +1,11 @@
+# level 1 keyed one chunk per workgroup without next-chunk registers (no spills): the GPU suite, the
+# A/B against the persistent form (l1pers) on configs 3 and 1, the per-rank split timing
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/tests_r05q.log 2>&1; rc=$?
+tail -2 gpurun_out/tests_r05q.log
+grep -E "FAILED|Error" gpurun_out/tests_r05q.log | head -5
+if [ $rc -ne 0 ]; then exit $rc; fi
+CONFIGS="config3 config1" timeout -k 10 600 bash tools/ab_multi.sh > gpurun_out/ab_r05q.txt 2>&1 || { cat gpurun_out/ab_r05q.txt; exit 2; }
+cat gpurun_out/ab_r05q.txt
+timeout -k 10 300 python -u tools/time_dist_rank.py config3 sharded 2 4 8 > gpurun_out/dist_sharded_r05q.txt 2>&1 || exit 3
+head -5 gpurun_out/dist_sharded_r05q.txt

@@ -77,7 +77,7 @@ hipError_t bp_level1(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_r
         // persistent: as many workgroups as fit the device at once, each walking its chunks with the
         // next one's loads in flight
         static thread_local int per_cu = 0;
-        if (!per_cu && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bp_scatter1p_kernel<KMP_L1_THREADS, false>,
+        if (!per_cu && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bp_scatter1p_kernel<KMP_L1_THREADS, false, true>,
                                                                      KMP_L1_THREADS, 0) != hipSuccess ||
                         per_cu < 1))
             per_cu = 2;
@@ -89,9 +89,18 @@ hipError_t bp_level1(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_r
         const uint32_t grid = nown >= dg.nb1 && !KMP_L1P_ALWAYS ? G
                                                                  : std::min<uint32_t>(G, (uint32_t)per_cu * device_cus());
         if (nown) {
-            bp_scatter1p_kernel<KMP_L1_THREADS, false><<<grid, KMP_L1_THREADS, 0, st>>>(
-                d_res, d_res_off, d_class, k, n, slots, G, reinterpret_cast<const uint4*>(ws->chunk_desc.p), lay, dg,
-                pw21, dlo, dhi, H1, ws->keys.p, ws->flags.p, SendL1{});
+            const uint4* desc = reinterpret_cast<const uint4*>(ws->chunk_desc.p);
+#ifndef KMP_L1_ONECHUNK
+#define KMP_L1_ONECHUNK 1  // A/B: 0 runs the persistent form for a grid of one workgroup per chunk too
+#endif
+            if (grid < G || !KMP_L1_ONECHUNK)
+                bp_scatter1p_kernel<KMP_L1_THREADS, false, true><<<grid, KMP_L1_THREADS, 0, st>>>(
+                    d_res, d_res_off, d_class, k, n, slots, G, desc, lay, dg, pw21, dlo, dhi, H1, ws->keys.p,
+                    ws->flags.p, SendL1{});
+            else
+                bp_scatter1p_kernel<KMP_L1_THREADS, false, false><<<grid, KMP_L1_THREADS, 0, st>>>(
+                    d_res, d_res_off, d_class, k, n, slots, G, desc, lay, dg, pw21, dlo, dhi, H1, ws->keys.p,
+                    ws->flags.p, SendL1{});
             if (!direct)
                 bp_h1t_kernel<<<dim3((G + 31) / 32, (nown + 31) / 32), 256, 0, st>>>(H1, G, nown, 0, nown, H1 + h1);
         }
@@ -143,20 +152,23 @@ bool cur_geometry(const Layout& lay, CurGeom* cg) {
 #ifndef KMP_GATHER_THREADS
 #define KMP_GATHER_THREADS 256
 #endif
-// Level 2, cursor variant: ws->keys (level 1) -> the bucket regions of ws->sorted, counts in ws->cur.
-int bp_level2c(kmp_postings* ws, const Layout& lay, hipStream_t st) {
-    const BpDigits dg = bp_digits(lay);
+// the cursor level 2's buffers (before any launch of the call's front)
+int bp_level2c_reserve(kmp_postings* ws, const Layout& lay) {
     const uint32_t nb = 1u << lay.bbits;
-    uint32_t* C1 = ws->bp.p + ws->bp_c1;
     PG(ws->cur.reserve(nb));
     PG(ws->sorted.reserve(ws->cg.vreg ? ws->vreg_total : (uint64_t)nb * ws->cg.capb));
     PG(ws->cnt.reserve(2 * (uint64_t)nb + 2));  // the large-bucket list
+    return KMP_OK;
+}
+
+// the level-2 gather of coarse bins [a, b) (of the call's bins [c0, c1), whose run table level 1
+// wrote from bin c0): a local level 1's output or the received pieces
+int bp_level2c_bins(kmp_postings* ws, const Layout& lay, uint32_t a, uint32_t b, hipStream_t st) {
+    const BpDigits dg = bp_digits(lay);
     uint32_t c0, c1;
     own_bins(ws, dg, &c0, &c1);
-    if (!ws->bp_local)  // the local level 1 cleared the counts with its chunk_first
-        bp_cur_clear_kernel<<<std::min<uint32_t>((nb + 1023) / 1024, 1024), 1024, 0, st>>>(ws->cur.p, nb);
-    if (c1 > c0 && ws->bp_local) {
-        const uint32_t ntiles = (ws->bp_G + ws->bp_T - 1) / ws->bp_T, per = (ntiles * (c1 - c0) + 7) / 8;
+    if (b > a) {
+        const uint32_t ntiles = (ws->bp_G + ws->bp_T - 1) / ws->bp_T, per = (ntiles * (b - a) + 7) / 8;
         constexpr uint32_t kGp = kBpGatherTile / KMP_GATHER_THREADS, kGt = KMP_GATHER_THREADS;
         // level 1's output: this call's own segments, or (the k-mer split's sharded start) the
         // pieces every rank sent (ws->l2_tab: their run tables in the receive buffer)
@@ -166,8 +178,8 @@ int bp_level2c(kmp_postings* ws, const Layout& lay, hipStream_t st) {
         const uint32_t grid = 8 * per;
 #define KMP_L2G(V, R)                                                                                           \
     bp_scatter2g_kernel<kGp, kGt, V, R><<<grid, kGt, 0, st>>>(in, tab, ws->bp_G, ws->bp_hsb, ws->bp_hsc, ws->bp_T, \
-                                                              ntiles, c1 - c0, dg, ws->cg, ws->cur.p, ws->sorted.p,   \
-                                                              ws->flags.p, c0, c0, ws->l2_rt)
+                                                              ntiles, b - a, dg, ws->cg, ws->cur.p, ws->sorted.p,     \
+                                                              ws->flags.p, a, c0, ws->l2_rt)
         if (recv) {
             if (ws->cg.vreg) KMP_L2G(true, true);
             else KMP_L2G(false, true);
@@ -176,6 +188,24 @@ int bp_level2c(kmp_postings* ws, const Layout& lay, hipStream_t st) {
             else KMP_L2G(false, false);
         }
 #undef KMP_L2G
+    }
+    PG(hipGetLastError());
+    return KMP_OK;
+}
+
+// Level 2, cursor variant: ws->keys (level 1) -> the bucket regions of ws->sorted, counts in ws->cur.
+int bp_level2c(kmp_postings* ws, const Layout& lay, hipStream_t st) {
+    const BpDigits dg = bp_digits(lay);
+    const uint32_t nb = 1u << lay.bbits;
+    uint32_t* C1 = ws->bp.p + ws->bp_c1;
+    const int rc = bp_level2c_reserve(ws, lay);
+    if (rc != KMP_OK) return rc;
+    uint32_t c0, c1;
+    own_bins(ws, dg, &c0, &c1);
+    if (!ws->bp_local)  // the local level 1 cleared the counts with its chunk_first
+        bp_cur_clear_kernel<<<std::min<uint32_t>((nb + 1023) / 1024, 1024), 1024, 0, st>>>(ws->cur.p, nb);
+    if (c1 > c0 && ws->bp_local) {
+        return bp_level2c_bins(ws, lay, c0, c1, st);
     } else if (c1 > c0) {
         if (ws->cg.vreg)
             bp_scatter2c_kernel<true><<<dim3(ws->bp_J, c1 - c0), kKeyThreads, 0, st>>>(

@@ -634,7 +634,11 @@ __host__ __device__ __forceinline__ uint32_t split_bin_lo(uint32_t d, uint32_t n
 // and the loop count them from 0), the residues a slice (SendL1.res_base / res_end), every digit is
 // ranked and each rank's piece goes to the send buffer with its run-table row (SendL1 above)
 // instead of the segment + H1.
-template <uint32_t kThr, bool kSend>
+// kPersist: a workgroup walks chunks blockIdx.x, + gridDim.x, ... with the next chunk's loads in
+// flight (a rank's share of the bins, a grid of what fits the device); otherwise it keys chunk
+// blockIdx.x alone (one GPU, and the sharded start: a grid of one workgroup per chunk), with no
+// next-chunk registers held across the chunk's work
+template <uint32_t kThr, bool kSend, bool kPersist>
 __global__ __launch_bounds__(kThr, KMP_L1P_WAVES) void bp_scatter1p_kernel(
     const uint8_t* __restrict__ res, const uint64_t* __restrict__ res_off, const uint16_t* __restrict__ cls, int k,
     uint32_t n, uint64_t slots, uint32_t G, const uint4* __restrict__ desc, Layout lay, BpDigits dg, uint32_t pw21,
@@ -699,7 +703,7 @@ __global__ __launch_bounds__(kThr, KMP_L1P_WAVES) void bp_scatter1p_kernel(
         }
     };
     uint4 dcur = desc[c];
-    uint4 dnxt = c + gridDim.x < G ? desc[c + gridDim.x] : make_uint4(0, 0, 0, 0);
+    uint4 dnxt = kPersist && c + gridDim.x < G ? desc[c + gridDim.x] : make_uint4(0, 0, 0, 0);
     issue(dcur);
     const unsigned hs1 = dg.sh1 - lay.hshift;
     __shared__ uint32_t sd_base[kSend ? kSplitMax : 1], sd_start[kSend ? kSplitMax : 1];
@@ -743,9 +747,9 @@ __global__ __launch_bounds__(kThr, KMP_L1P_WAVES) void bp_scatter1p_kernel(
         }
         __syncthreads();
         // ---- the next chunk's loads go out now; the descriptor after it too ----
-        const uint32_t cn = c + gridDim.x;
+        const uint32_t cn = kPersist ? c + gridDim.x : G;
         uint4 dnn = make_uint4(0, 0, 0, 0);
-        if (cn < G) {
+        if (kPersist && cn < G) {
             issue(dnxt);
             if (cn + gridDim.x < G) dnn = desc[cn + gridDim.x];
         }
@@ -876,8 +880,11 @@ struct RecvTab {
     uint64_t stride;     // u32 words between source regions (2 x the region's u64 words)
     uint64_t tb;         // run-table u64 words at the start of a region
 };
+#ifndef KMP_L2_WAVES
+#define KMP_L2_WAVES 0  // waves per SIMD level 2 is compiled for (0: the compiler's choice, ~140 VGPRs)
+#endif
 template <uint32_t kPer, uint32_t kThr, bool kVreg, bool kRecv>
-__global__ __launch_bounds__(kThr) void bp_scatter2g_kernel(const unsigned long long* __restrict__ in,
+__global__ __launch_bounds__(kThr, KMP_L2_WAVES ? KMP_L2_WAVES : 1) void bp_scatter2g_kernel(const unsigned long long* __restrict__ in,
                                                                    const uint32_t* __restrict__ H1T, uint32_t G,
                                                                    uint32_t hsb, uint32_t hsc,
                                                                    uint32_t T, uint32_t ntiles, uint32_t nbins,
@@ -980,9 +987,10 @@ __global__ __launch_bounds__(kThr) void bp_scatter2g_kernel(const unsigned long 
 // a 1,024-key capacity (four keys per thread) when the mean bucket is small enough that a bucket
 // above it is a > 4-sigma event (the large kernel takes those)
 constexpr uint32_t kBucketCap1024Mean = 800;  // at config 3 (mean 897) the 1,280 variant measured faster
-// buckets [b0, b0 + nb)
+// the small kernel over buckets [b0, b0 + nb)
 template <bool kRows, bool kScore>
-void launch_buckets(const BucketArgs& a, uint32_t b0, uint32_t nb, uint32_t large_grid, hipStream_t st) {
+void launch_small(const BucketArgs& a, uint32_t b0, uint32_t nb, hipStream_t st) {
+    if (!nb) return;
     if (a.lay.bbits >= kMergeMinBits && a.lay.mean_keys <= kBucketCap1024Mean)  // four keys per thread
         bucket_small_kernel<1024, kBucketSmallThreads, kBucketSmallTab, true, kRows, kScore>
             <<<nb, kBucketSmallThreads, 0, st>>>(a, b0);
@@ -992,6 +1000,11 @@ void launch_buckets(const BucketArgs& a, uint32_t b0, uint32_t nb, uint32_t larg
     else
         bucket_small_kernel<kBucketSmallCap, kBucketSmallThreads, kBucketSmallTab, false, kRows, kScore>
             <<<nb, kBucketSmallThreads, 0, st>>>(a, b0);
+}
+// buckets [b0, b0 + nb): the small kernel, then the large one over the buckets it listed
+template <bool kRows, bool kScore>
+void launch_buckets(const BucketArgs& a, uint32_t b0, uint32_t nb, uint32_t large_grid, hipStream_t st) {
+    launch_small<kRows, kScore>(a, b0, nb, st);
     if (large_grid)  // 0: the last call listed no bucket (a listed one now makes the call rerun)
         bucket_large_kernel<kBucketLargeCap, kBucketLargeThreads, kBucketLargeTab, kRows, kScore>
             <<<large_grid, kBucketLargeThreads, 0, st>>>(a);

@@ -227,6 +227,9 @@ int enqueue_front(kmp_postings* ws, MakeKeys& make_keys, const StepCfg& c, bool 
     if (!ws->defer_clear)
         step_clear_kernel<<<1, 256, 0, st>>>(ws->flags.p, ws->bstats.p, ws->clear_extra, ws->clear_n);
     ws->mark(0, st);
+    const BpDigits dg = bp_digits(c.lay);
+    uint32_t c0, c1;
+    own_bins(ws, dg, &c0, &c1);
     if (keys) {  // else: the keys grouped by bucket of the last call (front reuse)
         PG(make_keys(c.lay, st));
         if (ws->defer_clear) {  // (a key path that did not take it)
@@ -234,6 +237,9 @@ int enqueue_front(kmp_postings* ws, MakeKeys& make_keys, const StepCfg& c, bool 
             return KMP_EINVAL;
         }
         ws->mark(1, st);
+        // (level 2 and the bucket kernels of half the bins each on two streams, forked and joined
+        // with events, measured no faster in round 5: config 3 level 2 + group 0.320 ms either way,
+        // config 1 0.76 ms against 0.74 ms, a G = 8 rank 0.196 against 0.175 ms)
         int rc = bucket_group(ws, ws->keys.p, c.slots, c.lay, st);  // marks 2
         if (rc != KMP_OK) return rc;
     } else {
@@ -241,9 +247,6 @@ int enqueue_front(kmp_postings* ws, MakeKeys& make_keys, const StepCfg& c, bool 
         ws->mark(2, st);
     }
     const BucketArgs a = bucket_args(ws, c, spill);
-    const BpDigits dg = bp_digits(c.lay);
-    uint32_t c0, c1;
-    own_bins(ws, dg, &c0, &c1);
     const uint32_t b0 = c0 * dg.nb2, nbk = (c1 - c0) * dg.nb2;  // the call's buckets
     // the large-bucket kernel loops over its list: a grid sized from the last call's list (a
     // thousand idle 1,024-thread workgroups cost ~5 us); a bucket-range share of the k-mer split

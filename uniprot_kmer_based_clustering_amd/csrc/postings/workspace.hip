@@ -139,6 +139,7 @@ struct kmp_postings {
     } split_g[3];  // the k-mer split's phases (expand or group, edges, keys)
     hipGraphExec_t gexec = nullptr;
     hipStream_t cst = nullptr;  // capture stream
+
     std::vector<unsigned long long> gkey, gkey_seen;
     uint64_t graph_replays = 0;
     uint64_t reruns = 0;  // calls (or a split call's phases) run again with a grown capacity
