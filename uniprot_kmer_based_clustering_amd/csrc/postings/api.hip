@@ -481,6 +481,7 @@ static int split_expand_impl(kmp_postings* ws, const SplitSrc& src, uint32_t n, 
                 ws->heavy_ready = ws->hcur_valid = false;  // this call's front
                 ws->h_segs = rb[kRbSegs];
                 ws->h_segmax = rb[kRbSegMax];
+                ws->h_segl = rb[kRbSegL];
                 if ((rc = heavy_phase(ws, c, spill_total, true, st)) != KMP_OK) break;
             }
             rc = route(st, 1);

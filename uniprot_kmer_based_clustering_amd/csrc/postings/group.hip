@@ -46,7 +46,7 @@ static_assert(kShards == 64, "the heavy tiles hash to a shard with a 6-bit shift
 // budget an overflowing bin needs, a cursor-partition region overflow
 // kFlRange: a pair key outside the call's row blocks reached the fast tail's scatter (dropped there;
 // the call fails with KMP_EINVAL instead of writing out of bounds)
-enum : uint32_t { kFlBin = 0, kFlClass = 1, kFlList = 2, kFlOvf = 3, kFlBinTiles = 4, kFlCur = 5, kFlSegs = 6, kFlSegMax = 7, kFlSend = 8, kFlRange = 9, kFlN = 10 };
+enum : uint32_t { kFlBin = 0, kFlClass = 1, kFlList = 2, kFlOvf = 3, kFlBinTiles = 4, kFlCur = 5, kFlSegs = 6, kFlSegMax = 7, kFlSend = 8, kFlSegL = 9, kFlRange = 10, kFlN = 11 };
 
 template <int kThreads>
 __device__ __forceinline__ void block_scan_n(uint32_t v, uint32_t& excl, uint32_t& total, uint32_t* wave_tot) {
@@ -126,7 +126,8 @@ struct BucketArgs {
     uint64_t spill_cap;
     unsigned long long* spill_cursor;
     // spill segments (a heavy group, or a whole bucket): spill index | keys << 40, counted in
-    // flags[kFlSegs], the largest in flags[kFlSegMax]; the heavy path sorts each in LDS
+    // flags[kFlSegs], the largest in flags[kFlSegMax]; the heavy path sorts each in LDS.  2 seg_cap
+    // words: the second half lists the large segments (spill_segment)
     unsigned long long* seg;
     uint32_t seg_cap;
     // scored calls (kScore kernels): pair keys (pair << sb) | sor | s(x), s(x) of the group's k-mer
@@ -145,12 +146,19 @@ struct BucketArgs {
     int spill_all;
 };
 
-// descriptor: spill index (40 bits) | keys (23 bits) << 40 | whole bucket (several k-mers) << 63
+// descriptor: spill index (40 bits) | keys (23 bits) << 40 | whole bucket (several k-mers) << 63.
+// A segment above kSegSmall keys is also listed (its index) in seg[seg_cap + j], j counted in
+// flags[kFlSegL]: the heavy path's large-segment kernel runs one workgroup per listed segment only.
+constexpr uint32_t kSegSmall = 2048;
 __device__ __forceinline__ void spill_segment(const BucketArgs& a, uint64_t pos, uint32_t keys, bool whole) {
     const uint32_t s = atomicAdd(&a.flags[kFlSegs], 1u);
     if (s < a.seg_cap)
         a.seg[s] = pos | (unsigned long long)min(keys, 0x7FFFFFu) << 40 | (unsigned long long)whole << 63;
     atomicMax(&a.flags[kFlSegMax], keys);
+    if (keys > kSegSmall) {
+        const uint32_t j = atomicAdd(&a.flags[kFlSegL], 1u);
+        if (j < a.seg_cap) a.seg[a.seg_cap + j] = s;
+    }
 }
 
 // One workgroup per bucket with size <= kCap (the bucket: keys with the same top bbits of

@@ -64,118 +64,87 @@ __global__ void gather_shards_kernel(const unsigned long long* __restrict__ src,
 }
 
 // The spill is a list of segments (BucketArgs::seg): one heavy group (one k-mer) or one whole
-// bucket, each holding every key of its k-mers.  Each sorted alone, in LDS, and written where the
-// gather would have put it, is the whole sort the heavy path needs (k-mers contiguous, each
-// sorted): no global radix sort (eight onesweep passes over 1M keys at k = 5, 0.3 ms).  One
-// workgroup per segment.  Above kSegSmall keys: a block radix sort (rocprim, 8-bit digits,
-// 1,024 threads) of the key bits that differ — [0, hshift) for one k-mer (protein and class: four
-// passes instead of eight), every bit for a whole bucket (0.057 ms at config 1 against 0.074 ms
-// for a bitonic sort).
-constexpr uint32_t kSegSmall = 2048, kSegLarge = 8192, kSegItems = 8;
-template <uint32_t kLo, uint32_t kN>
-__global__ __launch_bounds__(kN / kSegItems) void heavy_segsort_kernel(const unsigned long long* __restrict__ spill,
-                                                                       uint64_t spill_cap,
-                                                                       const unsigned long long* __restrict__ cursor,
-                                                                       const unsigned long long* __restrict__ seg,
-                                                                       HeavyOrder ho,
-                                                                       unsigned long long* __restrict__ out) {
-    constexpr uint32_t kThreads = kN / kSegItems;
-    using Sort = rocprim::block_radix_sort<unsigned long long, kThreads, kSegItems>;
-    __shared__ typename Sort::storage_type st;
-    const unsigned long long sd = seg[blockIdx.x];
+// bucket, each holding every key of its k-mers.  Each put in order alone, in LDS, and written where
+// the gather would have put it, is the whole sort the heavy path needs (k-mers contiguous, each
+// sorted or in class runs): no global radix sort (eight onesweep passes over 1M keys at k = 5,
+// 0.3 ms).  One workgroup per segment, in two size classes — config 1 has 3,808 one-k-mer segments
+// (93 % of them at most 512 keys) and two whole buckets of ~4,600 keys:
+//   heavy_seg_kernel<256, 0, 2048>      up to 2,048 keys: 256 threads, 17 KB of LDS
+//   heavy_seg_kernel<1024, 2048, 8192>  2,049 - 8,192 keys: 1,024 threads, 64 KB; one workgroup per
+//                                       listed large segment (list: spill_segment)
+// (one 512-thread class kernel with a 64 KB hash set for every segment, a bitonic kernel and a
+// radix kernel, each over every segment, took 55 + 5 + 56 us at config 1).
+//
+// A one-k-mer segment in class order: what the compaction and the class-order expansion need is
+// class runs in ascending class, each protein once per run — not its proteins ascending (only plain
+// order, the ranged calls', searches by protein).  So: a counting sort by class in LDS, a protein's
+// later windows dropped through an LDS hash set on p sized to the segment (vertex.rs:59-140 counts a
+// protein once per k-mer), and the segment's tail (as many slots as windows dropped) filled with
+// copies of its last key, which the compaction sees as duplicates of their neighbour.  O(n) with
+// four barriers.  A segment whose classes reach kScClasses sorts instead.
+//
+// Otherwise (a whole bucket, or plain order) a sort: bitonic in LDS up to 2,048 keys; above, a
+// block radix sort (rocprim, 8-bit digits) of a compacted key (k-mer slot | the varying low bits:
+// 4 passes instead of 8 at config 1).
+constexpr uint32_t kSegLarge = 8192, kScClasses = 256;  // (kSegSmall: group.hip)
+struct NoBlockSort {
+    struct storage_type {
+        char c;
+    };
+};
+template <uint32_t kThr, uint32_t kLo, uint32_t kN>
+__global__ __launch_bounds__(kThr) void heavy_seg_kernel(const unsigned long long* __restrict__ spill,
+                                                         uint64_t spill_cap,
+                                                         const unsigned long long* __restrict__ cursor,
+                                                         const unsigned long long* __restrict__ seg,
+                                                         const unsigned long long* __restrict__ list, HeavyOrder ho,
+                                                         unsigned long long* __restrict__ out) {
+    constexpr uint32_t kItems = kN / kThr;
+    constexpr bool kRadix = kN > kSegSmall;
+    using Sort = std::conditional_t<kRadix, rocprim::block_radix_sort<unsigned long long, kThr, kItems>, NoBlockSort>;
+    __shared__ union {
+        uint32_t P[2 * kN];                // hash set of the segment's proteins
+        unsigned long long K[kN];          // an LDS bitonic sort's keys
+        typename Sort::storage_type st;    // the radix sort's
+    } u;
+    __shared__ uint32_t CH[kScClasses];  // keys per class, then each class run's start
+    __shared__ uint32_t HT[kRadix ? 2 * kN : 1];  // the radix sort's k-mer slots (h per slot)
+    __shared__ uint32_t wave_tot[kThr / 64];
+    __shared__ uint32_t s_maxc;
+    __shared__ unsigned long long s_last, s_or;
+    const unsigned long long sd = seg[kLo ? list[blockIdx.x] : blockIdx.x];
     const uint32_t cnt = (uint32_t)(sd >> 40) & 0x7FFFFFu;
     if (cnt <= kLo || cnt > kN) return;
     const bool whole = sd >> 63;
-    if (ho.cls && !whole) return;  // heavy_segclass_kernel
-    const uint64_t pos = sd & ((1ull << 40) - 1), shard = pos / spill_cap;
-    uint64_t dst = pos - shard * spill_cap;
-    for (uint64_t t = 0; t < shard; ++t) dst += cursor[t];
-    const unsigned long long cm = (1ull << ho.cb) - 1, hm = ~((1ull << ho.hshift) - 1);
-    unsigned long long k[kSegItems];  // blocked: thread t holds keys t * kSegItems + e
-#pragma unroll
-    for (uint32_t e = 0; e < kSegItems; ++e) {
-        const uint32_t i = threadIdx.x * kSegItems + e;
-        unsigned long long v = ~0ull;  // padding: after every key (the sort is stable)
-        if (i < cnt) {
-            v = spill[pos + i];
-            if (ho.cls) v = (v & hm) | (v & cm) << ho.pbits | ((v & ~hm) >> ho.cb);
-        }
-        k[e] = v;
-    }
-    Sort().sort(k, st, 0, whole ? 64u : ho.hshift);
-#pragma unroll
-    for (uint32_t e = 0; e < kSegItems; ++e) {
-        const uint32_t i = threadIdx.x * kSegItems + e;
-        if (i < cnt) out[dst + i] = k[e];
-    }
-}
-
-// Class order, one k-mer per segment (a heavy group, not a whole bucket): what the compaction and the
-// class-order expansion need is class runs in ascending class, each protein once per run — not its
-// proteins ascending (only plain order, the ranged calls', searches by protein).  So: a counting sort
-// by class in LDS, a protein's later windows dropped through an LDS hash set on p (vertex.rs:59-140
-// counts a protein once per k-mer), and the segment's tail (as many slots as windows dropped) filled
-// with copies of its last key, which the compaction sees as duplicates of their neighbour.  O(n) per
-// segment with four barriers, instead of a bitonic sort (66 compare-exchange rounds at 2,048 keys) or
-// a 4-pass block radix sort.  A segment whose classes reach kScClasses sorts its keys in LDS (bitonic)
-// instead.
-constexpr uint32_t kScThreads = 512, kScItems = kSegLarge / kScThreads, kScClasses = 256, kScSlots = 2 * kSegLarge;
-__global__ __launch_bounds__(kScThreads) void heavy_segclass_kernel(const unsigned long long* __restrict__ spill,
-                                                                    uint64_t spill_cap,
-                                                                    const unsigned long long* __restrict__ cursor,
-                                                                    const unsigned long long* __restrict__ seg,
-                                                                    HeavyOrder ho, unsigned long long* __restrict__ out) {
-    __shared__ union {
-        uint32_t P[kScSlots];            // hash set of the segment's proteins (64 KB)
-        unsigned long long K[kSegLarge]; // the fallback's keys
-    } u;
-    __shared__ uint32_t CH[kScClasses];  // keys per class, then each class run's start
-    __shared__ uint32_t wave_tot[kScThreads / 64];
-    __shared__ uint32_t s_maxc;
-    __shared__ unsigned long long s_last;
-    const unsigned long long sd = seg[blockIdx.x];
-    const uint32_t cnt = (uint32_t)(sd >> 40) & 0x7FFFFFu;
-    if ((sd >> 63) || cnt > kSegLarge) return;  // a whole bucket, or above the LDS: the sorts
     const uint32_t tid = threadIdx.x;
     const uint64_t pos = sd & ((1ull << 40) - 1), shard = pos / spill_cap;
     uint64_t dst = pos - shard * spill_cap;
     for (uint64_t t = 0; t < shard; ++t) dst += cursor[t];
     const unsigned long long cm = (1ull << ho.cb) - 1, hm = ~((1ull << ho.hshift) - 1);
-    const uint32_t pm = (uint32_t)((1ull << ho.pbits) - 1);
-    unsigned long long v[kScItems];
-    uint32_t mc = 0;
-#pragma unroll
-    for (uint32_t e = 0; e < kScItems; ++e) {
-        const uint32_t i = tid + e * kScThreads;
-        v[e] = ~0ull;
-        if (i < cnt) {
-            const unsigned long long x = spill[pos + i];
-            v[e] = (x & hm) | (x & cm) << ho.pbits | ((x & ~hm) >> ho.cb);  // [h | class | p]
-            mc = max(mc, (uint32_t)(v[e] >> ho.pbits) & (uint32_t)cm);
-        }
+    // class order: [h | p | class] -> [h | class | p]
+    auto order = [&](unsigned long long x) {
+        return ho.cls ? (x & hm) | (x & cm) << ho.pbits | ((x & ~hm) >> ho.cb) : x;
+    };
+    if (tid == 0) {
+        s_maxc = 0;
+        s_or = 0;
     }
-    for (uint32_t i = tid; i < kScSlots; i += kScThreads) u.P[i] = 0xFFFFFFFFu;
-    for (uint32_t i = tid; i < kScClasses; i += kScThreads) CH[i] = 0;
-    if (tid == 0) s_maxc = 0;
-    __syncthreads();
-    const uint32_t wm = wave_max(mc);
-    if ((tid & 63) == 0) atomicMax(&s_maxc, wm);
-    __syncthreads();
-    if (s_maxc >= kScClasses) {  // (uniform) many classes: a bitonic sort of the segment
+    // an LDS bitonic sort of the segment's keys (v: striped, thread t holds keys t + e * kThr)
+    auto bitonic = [&](const unsigned long long* v) {
         uint32_t N = 1;
         while (N < cnt) N <<= 1;
-        __syncthreads();  // P is dead: K reuses it
-        for (uint32_t i = tid; i < N; i += kScThreads) u.K[i] = ~0ull;
+        __syncthreads();  // u is free
+        for (uint32_t i = tid; i < N; i += kThr) u.K[i] = ~0ull;  // padding sorts last
         __syncthreads();
 #pragma unroll
-        for (uint32_t e = 0; e < kScItems; ++e) {
-            const uint32_t i = tid + e * kScThreads;
+        for (uint32_t e = 0; e < kItems; ++e) {
+            const uint32_t i = tid + e * kThr;
             if (i < cnt) u.K[i] = v[e];
         }
         __syncthreads();
         for (uint32_t k = 2; k <= N; k <<= 1)
             for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                for (uint32_t i = tid; i < N / 2; i += kScThreads) {
+                for (uint32_t i = tid; i < N / 2; i += kThr) {
                     const uint32_t lo = 2 * j * (i / j) + (i % j), hi = lo + j;
                     const unsigned long long x = u.K[lo], y = u.K[hi];
                     if ((x > y) == !(lo & k)) {
@@ -185,18 +154,106 @@ __global__ __launch_bounds__(kScThreads) void heavy_segclass_kernel(const unsign
                 }
                 __syncthreads();
             }
-        for (uint32_t i = tid; i < cnt; i += kScThreads) out[dst + i] = u.K[i];
+        for (uint32_t i = tid; i < cnt; i += kThr) out[dst + i] = u.K[i];
+    };
+    unsigned long long v[kItems];
+    if (whole || !ho.cls) {
+        if constexpr (kRadix) {
+            // The sort key, compacted: the k-mer's slot in an LDS hash table of h (a segment's k-mers
+            // only need to be contiguous, in any order) above the bits of the [class | p] (or
+            // [p | class]) field that vary in the segment.  At config 1 a whole bucket sorts 13 + 18
+            // bits (4 passes of 8 bits) instead of the 51 below its keys' highest differing bit (7).
+            // Padding (all ones) sorts after every compacted key.  Every h of a segment shares h0's
+            // top bit (a bucket is a range of top bits of h), so ~h0 marks an empty slot.
+            const unsigned long long k0 = order(spill[pos]);
+            const unsigned long long lowm = (1ull << ho.hshift) - 1;
+            const uint32_t hempty = ~(uint32_t)(k0 >> ho.hshift);
+            uint32_t lg = 6;  // slots: a power of two >= 2 cnt
+            while ((1u << lg) < 2 * cnt) ++lg;
+            const uint32_t nsl = 1u << lg;
+            for (uint32_t i = tid; i < nsl; i += kThr) HT[i] = hempty;
+            unsigned long long ox = 0;
+#pragma unroll
+            for (uint32_t e = 0; e < kItems; ++e) {  // blocked: thread t holds keys t * kItems + e
+                const uint32_t i = tid * kItems + e;
+                v[e] = ~0ull;
+                if (i < cnt) {
+                    v[e] = order(spill[pos + i]);
+                    ox |= (v[e] ^ k0) & lowm;
+                }
+            }
+#pragma unroll
+            for (int o = 32; o; o >>= 1) ox |= __shfl_xor(ox, o);
+            __syncthreads();  // s_or cleared, HT filled
+            if ((tid & 63) == 0 && ox) atomicOr(&s_or, ox);
+            __syncthreads();
+            const unsigned long long dl = s_or;
+            const uint32_t lb = dl ? 64u - (uint32_t)__clzll((long long)dl) : 0u;  // varying low bits [0, lb)
+            const unsigned long long lbm = (1ull << lb) - 1;
+#pragma unroll
+            for (uint32_t e = 0; e < kItems; ++e) {
+                if (v[e] == ~0ull) continue;
+                const uint32_t h = (uint32_t)(v[e] >> ho.hshift);
+                uint32_t sl = (h * 0x85EBCA6Bu) >> (32 - lg);
+                for (;;) {
+                    const uint32_t old = atomicCAS(&HT[sl], hempty, h);
+                    if (old == hempty || old == h) break;
+                    sl = (sl + 1) & (nsl - 1);
+                }
+                v[e] = (unsigned long long)sl << lb | (v[e] & lbm);
+            }
+            Sort().sort(v, u.st, 0, lg + lb);  // (barriers inside: HT complete before it is read)
+            const unsigned long long fixed = k0 & lowm & ~lbm;
+#pragma unroll
+            for (uint32_t e = 0; e < kItems; ++e) {
+                const uint32_t i = tid * kItems + e;
+                if (i < cnt) out[dst + i] = (unsigned long long)HT[v[e] >> lb] << ho.hshift | fixed | (v[e] & lbm);
+            }
+        } else {
+#pragma unroll
+            for (uint32_t e = 0; e < kItems; ++e) {
+                const uint32_t i = tid + e * kThr;
+                v[e] = i < cnt ? order(spill[pos + i]) : ~0ull;
+            }
+            bitonic(v);
+        }
+        return;
+    }
+    // one k-mer, class order
+    const uint32_t pm = (uint32_t)((1ull << ho.pbits) - 1);
+    uint32_t mc = 0;
+#pragma unroll
+    for (uint32_t e = 0; e < kItems; ++e) {
+        const uint32_t i = tid + e * kThr;
+        v[e] = ~0ull;
+        if (i < cnt) {
+            v[e] = order(spill[pos + i]);
+            mc = max(mc, (uint32_t)(v[e] >> ho.pbits) & (uint32_t)cm);
+        }
+    }
+    uint32_t lg = 6;  // hash slots: a power of two >= 2 cnt
+    while ((1u << lg) < 2 * cnt) ++lg;
+    const uint32_t nsl = 1u << lg;
+    for (uint32_t i = tid; i < nsl; i += kThr) u.P[i] = 0xFFFFFFFFu;
+    for (uint32_t i = tid; i < kScClasses; i += kThr) CH[i] = 0;
+    __syncthreads();
+    const uint32_t wm = wave_max(mc);
+    if ((tid & 63) == 0) atomicMax(&s_maxc, wm);
+    __syncthreads();
+    const uint32_t maxc = s_maxc;
+    if (maxc >= kScClasses) {  // (uniform) many classes: sort the segment
+        bitonic(v);
         return;
     }
     // a protein's first window in the segment keeps its key, later ones are dropped; each kept key
     // ranked in its class
-    uint32_t rk[kScItems];
+    uint32_t rk[kItems];
 #pragma unroll
-    for (uint32_t e = 0; e < kScItems; ++e) {
+    for (uint32_t e = 0; e < kItems; ++e) {
         rk[e] = ~0u;
         if (v[e] == ~0ull) continue;
         const uint32_t p = (uint32_t)v[e] & pm;
-        uint32_t sl = (p * 0x9E3779B1u) >> (32 - 14);  // kScSlots = 2^14
+        uint32_t sl = (p * 0x9E3779B1u) >> (32 - lg);
         bool first = false;
         while (true) {
             const uint32_t old = atomicCAS(&u.P[sl], 0xFFFFFFFFu, p);
@@ -205,15 +262,15 @@ __global__ __launch_bounds__(kScThreads) void heavy_segclass_kernel(const unsign
                 break;
             }
             if (old == p) break;
-            sl = (sl + 1) & (kScSlots - 1);
+            sl = (sl + 1) & (nsl - 1);
         }
         if (first) rk[e] = atomicAdd(&CH[(uint32_t)(v[e] >> ho.pbits) & (uint32_t)cm], 1u);
     }
     __syncthreads();
-    lds_bins_scan<kScThreads>(CH, kScClasses, wave_tot);  // CH: run starts; the kept count below
+    lds_bins_scan<kThr>(CH, maxc + 1, wave_tot);  // CH: run starts; the kept count below
     uint32_t kept = 0;
 #pragma unroll
-    for (uint32_t e = 0; e < kScItems; ++e)
+    for (uint32_t e = 0; e < kItems; ++e)
         if (rk[e] != ~0u) {
             const uint32_t at = CH[(uint32_t)(v[e] >> ho.pbits) & (uint32_t)cm] + rk[e];
             out[dst + at] = v[e];
@@ -221,53 +278,13 @@ __global__ __launch_bounds__(kScThreads) void heavy_segclass_kernel(const unsign
         }
     // the segment's last kept key: the largest (class, position) — the highest class run's last slot
     uint32_t D, excl;
-    block_scan_n<kScThreads>(kept, excl, D, wave_tot);
+    block_scan_n<kThr>(kept, excl, D, wave_tot);
 #pragma unroll
-    for (uint32_t e = 0; e < kScItems; ++e)
+    for (uint32_t e = 0; e < kItems; ++e)
         if (rk[e] != ~0u && CH[(uint32_t)(v[e] >> ho.pbits) & (uint32_t)cm] + rk[e] == D - 1) s_last = v[e];
     __syncthreads();
     const unsigned long long last = s_last;
-    for (uint32_t i = D + tid; i < cnt; i += kScThreads) out[dst + i] = last;
-}
-
-// the small segments (<= kSegSmall keys): a bitonic sort of the next power of two, 256 threads
-// (the radix sort's four passes measured 0.081 ms there against 0.064 ms)
-template <uint32_t kN, uint32_t kThreads>
-__global__ __launch_bounds__(kThreads) void heavy_segsort_bitonic_kernel(
-    const unsigned long long* __restrict__ spill, uint64_t spill_cap, const unsigned long long* __restrict__ cursor,
-    const unsigned long long* __restrict__ seg, HeavyOrder ho, unsigned long long* __restrict__ out) {
-    __shared__ unsigned long long K[kN];
-    const unsigned long long sd = seg[blockIdx.x];
-    const uint32_t cnt = (uint32_t)(sd >> 40) & 0x7FFFFFu;
-    if (cnt > kN || (ho.cls && !(sd >> 63))) return;  // one k-mer in class order: heavy_segclass_kernel
-    const uint64_t pos = sd & ((1ull << 40) - 1), shard = pos / spill_cap;
-    uint64_t dst = pos - shard * spill_cap;
-    for (uint64_t t = 0; t < shard; ++t) dst += cursor[t];
-    uint32_t N = 1;
-    while (N < cnt) N <<= 1;
-    const unsigned long long cm = (1ull << ho.cb) - 1, hm = ~((1ull << ho.hshift) - 1);
-    for (uint32_t i = threadIdx.x; i < N; i += kThreads) {
-        unsigned long long v = ~0ull;  // padding sorts last
-        if (i < cnt) {
-            v = spill[pos + i];
-            if (ho.cls) v = (v & hm) | (v & cm) << ho.pbits | ((v & ~hm) >> ho.cb);
-        }
-        K[i] = v;
-    }
-    __syncthreads();
-    for (uint32_t k = 2; k <= N; k <<= 1)
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t i = threadIdx.x; i < N / 2; i += kThreads) {
-                const uint32_t lo = 2 * j * (i / j) + (i % j), hi = lo + j;
-                const unsigned long long x = K[lo], y = K[hi];
-                if ((x > y) == !(lo & k)) {
-                    K[lo] = y;
-                    K[hi] = x;
-                }
-            }
-            __syncthreads();
-        }
-    for (uint32_t i = threadIdx.x; i < cnt; i += kThreads) out[dst + i] = K[i];
+    for (uint32_t i = D + tid; i < cnt; i += kThr) out[dst + i] = last;
 }
 
 // per tile: distinct (h, p) elements, k-mer heads and (class order) class-run heads

@@ -880,6 +880,9 @@ struct RecvTab {
     uint64_t stride;     // u32 words between source regions (2 x the region's u64 words)
     uint64_t tb;         // run-table u64 words at the start of a region
 };
+#ifndef KMP_L2_MAPSCAN
+#define KMP_L2_MAPSCAN 1  // level 2's key -> run map by a block max-scan of the runs' first positions
+#endif
 #ifndef KMP_L2_WAVES
 #define KMP_L2_WAVES 0  // waves per SIMD level 2 is compiled for (0: the compiler's choice, ~140 VGPRs)
 #endif
@@ -954,6 +957,58 @@ __global__ __launch_bounds__(kThr, KMP_L2_WAVES ? KMP_L2_WAVES : 1) void bp_scat
                 excl += p[t] & 0xFFFFu;
             }
         // key -> run map of the round's window [base, base + n_in)
+#if KMP_L2_MAPSCAN
+        // each run marks its first position in the window (the run covering position base marks
+        // 0), then a block-wide inclusive max-scan carries every mark over its run: run ids grow
+        // with position.  (A thread filling its runs' positions in a loop ran as long as its wave's
+        // longest runs: ~30-50 iterations per round.)
+        static_assert(kTile == 16 * kThr, "16 map positions per thread");
+        uint4* m4 = reinterpret_cast<uint4*>(map) + 2 * threadIdx.x;
+        m4[0] = m4[1] = make_uint4(0, 0, 0, 0);
+        __syncthreads();
+        excl = excl0;
+#pragma unroll
+        for (uint32_t t = 0; t < kQ; ++t)
+            if (t < q && b0 + t < nch) {
+                const uint32_t e1 = excl + (p[t] & 0xFFFFu);
+                const uint32_t lo = max(excl, base), hi = min(e1, base + n_in);
+                if (lo < hi) map[lo - base] = (uint16_t)(b0 + t);
+                excl = e1;
+            }
+        __syncthreads();
+        {
+            uint4 w0 = m4[0], w1 = m4[1];
+            uint32_t wd[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+            uint32_t agg = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) agg = max(agg, max(wd[j] & 0xFFFFu, wd[j] >> 16));
+            // inclusive max over the lanes, then the wave's lanes before this one, then earlier waves
+            uint32_t inc = agg;
+            inc = max(inc, dpp_mov<0x111>(inc));
+            inc = max(inc, dpp_mov<0x112>(inc));
+            inc = max(inc, dpp_mov<0x114>(inc));
+            inc = max(inc, dpp_mov<0x118>(inc));
+            inc = max(inc, dpp_mov<0x142, 0xA>(inc));
+            inc = max(inc, dpp_mov<0x143, 0xC>(inc));
+            const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+            uint32_t before = (uint32_t)__shfl_up((int)inc, 1);
+            if (lane == 0) before = 0;
+            if (lane == 63) wave_tot[wv] = inc;
+            __syncthreads();
+#pragma unroll
+            for (uint32_t i = 0; i < kThr / 64; ++i)
+                if (i < wv) before = max(before, wave_tot[i]);
+            uint32_t run = before;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t lo16 = max(run, wd[j] & 0xFFFFu);
+                run = max(lo16, wd[j] >> 16);
+                wd[j] = lo16 | run << 16;
+            }
+            m4[0] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+            m4[1] = make_uint4(wd[4], wd[5], wd[6], wd[7]);
+        }
+#else
         excl = excl0;
 #pragma unroll
         for (uint32_t t = 0; t < kQ; ++t)
@@ -963,6 +1018,7 @@ __global__ __launch_bounds__(kThr, KMP_L2_WAVES ? KMP_L2_WAVES : 1) void bp_scat
                 for (uint32_t i = lo; i < hi; ++i) map[i - base] = (uint16_t)(b0 + t);
                 excl = e1;
             }
+#endif
         __syncthreads();
         unsigned long long x[kPer];
         uint32_t r[kPer];

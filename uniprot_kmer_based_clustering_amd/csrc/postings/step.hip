@@ -209,7 +209,7 @@ int step_reserve(kmp_postings* ws, const StepCfg& c, const PtGeom& g, hipStream_
         if (c.sb) PG(ws->stg2.reserve(2 * total));  // ... staged scores | second-k weights
     }
     PG(ws->spill.reserve(ws->spill_cap * kShards));
-    PG(ws->hseg.reserve(seg_capacity(ws)));
+    PG(ws->hseg.reserve(2ull * seg_capacity(ws)));  // segments | the large ones' list
     PG(ws->ovf.reserve((uint64_t)g.nrb + 1));
     if (!ws->hrb) PG(hipHostMalloc((void**)&ws->hrb, kRbWords * sizeof(unsigned long long), hipHostMallocCoherent));
     hipError_t e = hipSuccess;
@@ -533,16 +533,38 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
             ws->hcur_valid = true;
         }
         const unsigned long long* spill_cursor = ws->hcur.p;
-        if (ws->h_segs && ws->h_segs <= seg_capacity(ws) && ws->h_segmax <= kSegLarge) {
+        if (ws->h_segs && ws->h_segs <= seg_capacity(ws) && ws->h_segmax <= kSegLarge &&
+            ws->h_segl <= seg_capacity(ws)) {
             const uint32_t ns = (uint32_t)ws->h_segs;
-            if (ho.cls)
-                heavy_segclass_kernel<<<ns, kScThreads, 0, st>>>(ws->spill.p, ws->spill_cap, spill_cursor, ws->hseg.p,
-                                                                 ho, ws->hsorted.p);
-            heavy_segsort_bitonic_kernel<kSegSmall, 256><<<ns, 256, 0, st>>>(
-                ws->spill.p, ws->spill_cap, spill_cursor, ws->hseg.p, ho, ws->hsorted.p);
-            if (ws->h_segmax > kSegSmall)
-                heavy_segsort_kernel<kSegSmall, kSegLarge><<<ns, kSegLarge / kSegItems, 0, st>>>(
-                    ws->spill.p, ws->spill_cap, spill_cursor, ws->hseg.p, ho, ws->hsorted.p);
+            static const bool trace = getenv("KMP_TRACE") != nullptr;
+            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+            if (trace && hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
+                // diagnostics: the segment sizes (one k-mer / whole bucket) by power-of-two class
+                std::vector<unsigned long long> sd(ns);
+                if (hipMemcpyAsync(sd.data(), ws->hseg.p, ns * 8ull, hipMemcpyDeviceToHost, st) == hipSuccess &&
+                    hipStreamSynchronize(st) == hipSuccess) {
+                    uint64_t n[2][15] = {}, k[2][15] = {};
+                    for (unsigned long long d : sd) {
+                        const uint32_t cnt = (uint32_t)(d >> 40) & 0x7FFFFFu, w = (uint32_t)(d >> 63);
+                        uint32_t b = 0;
+                        while (b < 14 && (1u << b) < cnt) ++b;
+                        ++n[w][b];
+                        k[w][b] += cnt;
+                    }
+                    for (int w = 0; w < 2; ++w)
+                        for (int b = 0; b < 15; ++b)
+                            if (n[w][b])
+                                fprintf(stderr, "[kmp] segs %s <=%u: %llu segments, %llu keys\n",
+                                        w ? "whole" : "kmer", 1u << b, (unsigned long long)n[w][b],
+                                        (unsigned long long)k[w][b]);
+                }
+            }
+            if (ws->h_segl)  // the listed large segments (every one when a front listed them all)
+                heavy_seg_kernel<1024, kSegSmall, kSegLarge><<<(uint32_t)ws->h_segl, 1024, 0, st>>>(
+                    ws->spill.p, ws->spill_cap, spill_cursor, ws->hseg.p, ws->hseg.p + seg_capacity(ws), ho,
+                    ws->hsorted.p);
+            heavy_seg_kernel<256, 0, kSegSmall><<<ns, 256, 0, st>>>(ws->spill.p, ws->spill_cap, spill_cursor,
+                                                                    ws->hseg.p, nullptr, ho, ws->hsorted.p);
         } else {  // a segment above the LDS sort: gather and one radix sort
             gather_shards_kernel<<<dim3((uint32_t)std::min<uint64_t>((ws->spill_cap + 255) / 256, 1024), kShards),
                                    256, 0, st>>>(ws->spill.p, ws->spill_cap, spill_cursor, ho, ws->hkeys.p);
@@ -909,6 +931,7 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
                 if (spill_total) {  // a new spill (a reused front spills nothing: keep its segments)
                     ws->h_segs = rb[kRbSegs];
                     ws->h_segmax = rb[kRbSegMax];
+                    ws->h_segl = rb[kRbSegL];
                 }
                 int rc = heavy_phase(ws, c, spill_total ? spill_total : ws->h_m, true, st);
                 if (rc != KMP_OK) return rc;
