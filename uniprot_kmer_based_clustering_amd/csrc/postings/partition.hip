@@ -883,6 +883,9 @@ struct RecvTab {
 #ifndef KMP_L2_MAPSCAN
 #define KMP_L2_MAPSCAN 1  // level 2's key -> run map by a block max-scan of the runs' first positions
 #endif
+#ifndef KMP_L2_TILEMAJOR
+#define KMP_L2_TILEMAJOR 1  // level 2's workgroup order: tile-major (adjacent bins together) or bin-major
+#endif
 #ifndef KMP_L2_WAVES
 #define KMP_L2_WAVES 0  // waves per SIMD level 2 is compiled for (0: the compiler's choice, ~140 VGPRs)
 #endif
@@ -909,7 +912,13 @@ __global__ __launch_bounds__(kThr, KMP_L2_WAVES ? KMP_L2_WAVES : 1) void bp_scat
     const uint32_t total = ntiles * nbins, per = (total + 7) / 8;
     const uint32_t w = (blockIdx.x % 8) * per + blockIdx.x / 8;
     if (w >= total) return;
+#if KMP_L2_TILEMAJOR
+    // consecutive workgroups of an XCD take adjacent bins of one chunk range: a run's first and last
+    // 128-B lines are shared with the neighbouring bins' runs, read by the next workgroup from L2
+    const uint32_t c = c0 + w % nbins, ch0 = (w / nbins) * T;
+#else
     const uint32_t c = c0 + w / ntiles, ch0 = (w % ntiles) * T;
+#endif
     if (ch0 >= G) return;
     const uint32_t nch = min(T, G - ch0);
     const uint32_t* row = H1T + (uint64_t)(c - dlo) * hsb + (uint64_t)ch0 * hsc;
