@@ -866,9 +866,10 @@ __global__ __launch_bounds__(256) void bp_h1t_kernel(const uint32_t* __restrict_
 // key -> run map live in S until the keys are in registers, so the loads go out coalesced
 // (element tid + e*kKeyThreads, as the other scatters).  A tile above kBpTile keys (a skewed
 // batch) goes in several rounds.  XCD-aware order: workgroup L runs on XCD L % 8, and XCD x
-// takes the tiles [x * per, (x + 1) * per) of the bin-major tile list, so neighbouring bins' tiles
-// of a chunk range (whose runs share the 128-B lines at their ends) run on one L2 at about the
-// same time.
+// takes the tiles [x * per, (x + 1) * per) of the tile list, tile-major (KMP_L2_TILEMAJOR): the
+// consecutive workgroups of an XCD take adjacent bins of one chunk range, whose runs share the
+// 128-B lines at their ends, so the second reader finds them in L2 (bp_scatter2g's fetch at config 3:
+// 349 MB bin-major, 242 MB tile-major, for 235 MB of keys).
 // kRecv (the k-mer split's sharded start): the runs are the received pieces — chunk row g of the
 // G = parts * cm rows is row g mod cm of source g / cm's region (stride u32 words apart), rows past
 // that source's chunk count are empty, and each row starts with the u64 index its runs are
