@@ -83,17 +83,10 @@ hipError_t bp_level1(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_r
             per_cu = 2;
         // every bin owned (one GPU): one workgroup per chunk, in order (bp_scatter1p 112 -> 103 us at
         // config 3); a share of the bins (a rank of the k-mer split, little work per chunk): persistent
-#ifndef KMP_L1P_ALWAYS
-#define KMP_L1P_ALWAYS 0  // A/B: the persistent grid on one GPU too
-#endif
-        const uint32_t grid = nown >= dg.nb1 && !KMP_L1P_ALWAYS ? G
-                                                                 : std::min<uint32_t>(G, (uint32_t)per_cu * device_cus());
+        const uint32_t grid = nown >= dg.nb1 ? G : std::min<uint32_t>(G, (uint32_t)per_cu * device_cus());
         if (nown) {
             const uint4* desc = reinterpret_cast<const uint4*>(ws->chunk_desc.p);
-#ifndef KMP_L1_ONECHUNK
-#define KMP_L1_ONECHUNK 1  // A/B: 0 runs the persistent form for a grid of one workgroup per chunk too
-#endif
-            if (grid < G || !KMP_L1_ONECHUNK)
+            if (grid < G)
                 bp_scatter1p_kernel<KMP_L1_THREADS, false, true><<<grid, KMP_L1_THREADS, 0, st>>>(
                     d_res, d_res_off, d_class, k, n, slots, G, desc, lay, dg, pw21, dlo, dhi, H1, ws->keys.p,
                     ws->flags.p, SendL1{});

@@ -866,7 +866,7 @@ __global__ __launch_bounds__(256) void bp_h1t_kernel(const uint32_t* __restrict_
 // key -> run map live in S until the keys are in registers, so the loads go out coalesced
 // (element tid + e*kKeyThreads, as the other scatters).  A tile above kBpTile keys (a skewed
 // batch) goes in several rounds.  XCD-aware order: workgroup L runs on XCD L % 8, and XCD x
-// takes the tiles [x * per, (x + 1) * per) of the tile list, tile-major (KMP_L2_TILEMAJOR): the
+// takes the tiles [x * per, (x + 1) * per) of the tile list, tile-major: the
 // consecutive workgroups of an XCD take adjacent bins of one chunk range, whose runs share the
 // 128-B lines at their ends, so the second reader finds them in L2 (bp_scatter2g's fetch at config 3:
 // 349 MB bin-major, 242 MB tile-major, for 235 MB of keys).
@@ -881,12 +881,6 @@ struct RecvTab {
     uint64_t stride;     // u32 words between source regions (2 x the region's u64 words)
     uint64_t tb;         // run-table u64 words at the start of a region
 };
-#ifndef KMP_L2_MAPSCAN
-#define KMP_L2_MAPSCAN 1  // level 2's key -> run map by a block max-scan of the runs' first positions
-#endif
-#ifndef KMP_L2_TILEMAJOR
-#define KMP_L2_TILEMAJOR 1  // level 2's workgroup order: tile-major (adjacent bins together) or bin-major
-#endif
 #ifndef KMP_L2_WAVES
 #define KMP_L2_WAVES 0  // waves per SIMD level 2 is compiled for (0: the compiler's choice, ~140 VGPRs)
 #endif
@@ -913,13 +907,9 @@ __global__ __launch_bounds__(kThr, KMP_L2_WAVES ? KMP_L2_WAVES : 1) void bp_scat
     const uint32_t total = ntiles * nbins, per = (total + 7) / 8;
     const uint32_t w = (blockIdx.x % 8) * per + blockIdx.x / 8;
     if (w >= total) return;
-#if KMP_L2_TILEMAJOR
-    // consecutive workgroups of an XCD take adjacent bins of one chunk range: a run's first and last
-    // 128-B lines are shared with the neighbouring bins' runs, read by the next workgroup from L2
+    // tile-major: consecutive workgroups of an XCD take adjacent bins of one chunk range, whose runs
+    // share their first and last 128-B lines, read by the next workgroup from L2
     const uint32_t c = c0 + w % nbins, ch0 = (w / nbins) * T;
-#else
-    const uint32_t c = c0 + w / ntiles, ch0 = (w % ntiles) * T;
-#endif
     if (ch0 >= G) return;
     const uint32_t nch = min(T, G - ch0);
     const uint32_t* row = H1T + (uint64_t)(c - dlo) * hsb + (uint64_t)ch0 * hsc;
@@ -967,7 +957,6 @@ __global__ __launch_bounds__(kThr, KMP_L2_WAVES ? KMP_L2_WAVES : 1) void bp_scat
                 excl += p[t] & 0xFFFFu;
             }
         // key -> run map of the round's window [base, base + n_in)
-#if KMP_L2_MAPSCAN
         // each run marks its first position in the window (the run covering position base marks
         // 0), then a block-wide inclusive max-scan carries every mark over its run: run ids grow
         // with position.  (A thread filling its runs' positions in a loop ran as long as its wave's
@@ -1018,17 +1007,6 @@ __global__ __launch_bounds__(kThr, KMP_L2_WAVES ? KMP_L2_WAVES : 1) void bp_scat
             m4[0] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
             m4[1] = make_uint4(wd[4], wd[5], wd[6], wd[7]);
         }
-#else
-        excl = excl0;
-#pragma unroll
-        for (uint32_t t = 0; t < kQ; ++t)
-            if (t < q && b0 + t < nch) {
-                const uint32_t e1 = excl + (p[t] & 0xFFFFu);
-                const uint32_t lo = max(excl, base), hi = min(e1, base + n_in);
-                for (uint32_t i = lo; i < hi; ++i) map[i - base] = (uint16_t)(b0 + t);
-                excl = e1;
-            }
-#endif
         __syncthreads();
         unsigned long long x[kPer];
         uint32_t r[kPer];

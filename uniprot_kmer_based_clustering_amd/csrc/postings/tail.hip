@@ -284,11 +284,7 @@ __global__ __launch_bounds__(kFtScThreads) void pt_scatter_capped_kernel(const u
     uint32_t rbase[kQ];
 #pragma unroll
     for (uint32_t t = 0; t < kQ; ++t)  // reserved while the tile is placed
-#ifndef KMP_AB_SC
         rbase[t] = cnt[t] ? atomicAdd(&cur[threadIdx.x + t * kThr], cnt[t]) : 0u;
-#else  // A/B timing only (wrong results): no reservation atomics
-        rbase[t] = (j * 4) % 4096;
-#endif
     // block r's region: [r * ftcap, (r + 1) * ftcap); a run that does not fit is dropped whole (the
     // cursor still counts it: the reduce flags the block)
     uint32_t rabs[kQ];
