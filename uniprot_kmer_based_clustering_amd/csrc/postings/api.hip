@@ -482,6 +482,7 @@ static int split_expand_impl(kmp_postings* ws, const SplitSrc& src, uint32_t n, 
                 ws->h_segs = rb[kRbSegs];
                 ws->h_segmax = rb[kRbSegMax];
                 ws->h_segl = rb[kRbSegL];
+                ws->h_segw = rb[kRbSegW];
                 if ((rc = heavy_phase(ws, c, spill_total, true, st)) != KMP_OK) break;
             }
             rc = route(st, 1);

@@ -46,7 +46,7 @@ static_assert(kShards == 64, "the heavy tiles hash to a shard with a 6-bit shift
 // budget an overflowing bin needs, a cursor-partition region overflow
 // kFlRange: a pair key outside the call's row blocks reached the fast tail's scatter (dropped there;
 // the call fails with KMP_EINVAL instead of writing out of bounds)
-enum : uint32_t { kFlBin = 0, kFlClass = 1, kFlList = 2, kFlOvf = 3, kFlBinTiles = 4, kFlCur = 5, kFlSegs = 6, kFlSegMax = 7, kFlSend = 8, kFlSegL = 9, kFlRange = 10, kFlN = 11 };
+enum : uint32_t { kFlBin = 0, kFlClass = 1, kFlList = 2, kFlOvf = 3, kFlBinTiles = 4, kFlCur = 5, kFlSegs = 6, kFlSegMax = 7, kFlSend = 8, kFlSegL = 9, kFlSegW = 10, kFlRange = 11, kFlN = 12 };
 
 template <int kThreads>
 __device__ __forceinline__ void block_scan_n(uint32_t v, uint32_t& excl, uint32_t& total, uint32_t* wave_tot) {
@@ -155,6 +155,7 @@ __device__ __forceinline__ void spill_segment(const BucketArgs& a, uint64_t pos,
     if (s < a.seg_cap)
         a.seg[s] = pos | (unsigned long long)min(keys, 0x7FFFFFu) << 40 | (unsigned long long)whole << 63;
     atomicMax(&a.flags[kFlSegMax], keys);
+    if (whole) atomicAdd(&a.flags[kFlSegW], keys);  // (with the segment count: a bound on the spill's k-mers)
     if (keys > kSegSmall) {
         const uint32_t j = atomicAdd(&a.flags[kFlSegL], 1u);
         if (j < a.seg_cap) a.seg[a.seg_cap + j] = s;

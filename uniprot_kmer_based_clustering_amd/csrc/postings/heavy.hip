@@ -391,9 +391,13 @@ __global__ __launch_bounds__(256) void heavy_plan_kernel(const uint32_t* __restr
                                                          unsigned long long* __restrict__ gstats,
                                                          uint32_t* __restrict__ gi, uint32_t* __restrict__ BT,
                                                          uint32_t* __restrict__ BP,
-                                                         unsigned long long* __restrict__ tcount) {
+                                                         unsigned long long* __restrict__ tcount,
+                                                         unsigned long long* __restrict__ ng_plan) {
     const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     const uint64_t ng = *ng_dev;  // k-mers; threads up to the bound ngb write empty plans
+    // the k-mers the expansion walks: every one, within the arrays' bound (ngb - 1 k-mers + the scan's
+    // end; the host's bound holds: the clamp only keeps a broken bound from reading past them)
+    if (g == 0 && ng_plan) *ng_plan = ng < ngb ? ng : ngb - 1;
     const unsigned cb = ho.cb;
     unsigned long long st[kStN] = {0, 0, 0, 0, 0, 0, 0};
     if (g >= ng && g < ngb) {

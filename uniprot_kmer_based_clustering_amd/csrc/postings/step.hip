@@ -637,8 +637,11 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
         ws->h_ng = ht[1];
         ws->h_flat_ready = true;
     }
-    // bound on the k-mer count (device: h_tot[1]); exact once the flat index read it back
-    const uint64_t ngb = flat ? ws->h_ng : ws->h_m;
+    // bound on the k-mer count (device: h_tot[1]); exact once the flat index read it back.  Else the
+    // spill's segments bound it: one k-mer per heavy group, at most one per key of a whole bucket
+    // (config 1: 13,050 against the 1.0 M spilled keys that sized the plan, its scan and the expansion
+    // grid before: 19 + 19 + 29 us)
+    const uint64_t ngb = flat ? ws->h_ng : ws->h_segs ? std::min<uint64_t>(ws->h_m, ws->h_segs + ws->h_segw) : ws->h_m;
     if (ngb == 0) return KMP_OK;
     const uint32_t row_lo = c.ranged ? c.row_lo : 0, row_hi = c.ranged ? c.row_hi : c.n;
     const uint64_t* GS = reinterpret_cast<const uint64_t*>(ws->hGS.p);
@@ -650,7 +653,7 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
         if (stats && index_built)
             heavy_plan_kernel<<<(uint32_t)((ngb + 1 + 255) / 256), 256, 0, st>>>(
                 ws->hE.p, GS, ngb + 1, ws->h_tot + 1, ho, RUN, RH, 0, row_lo, row_hi, c.heavy_df, 1, 0, ws->bstats.p,
-                nullptr, nullptr, nullptr, nullptr);
+                nullptr, nullptr, nullptr, nullptr, nullptr);
         const uint32_t a0 = ws->hPOh[row_lo], a1 = ws->hPOh[row_hi];
         if (a1 > a0)
             heavy_flat_kernel<<<(a1 - a0 + kHfThreads - 1) / kHfThreads, kHfThreads, 0, st>>>(
@@ -663,12 +666,14 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
     PG(ws->hgi.reserve(2 * (ngb + 1)));
     PG(ws->htc.reserve(ngb + 1));
     PG(ws->htoff.reserve(ngb + 1));
-    PG(ws->hblk.reserve(2 * (ngb + ngb / kHvI + 2)));
+    // row-block tables: k-mer g's blocks at GS[g] / kHvI + g (heavy_bbase), GS <= the elements <= h_m
+    const uint64_t nbb = ngb + ws->h_m / kHvI + 2;
+    PG(ws->hblk.reserve(2 * nbb));
     uint32_t* BT = ws->hblk.p;
-    uint32_t* BP = BT + ngb + ngb / kHvI + 2;
+    uint32_t* BP = BT + nbb;
     heavy_plan_kernel<<<(uint32_t)((ngb + 1 + 255) / 256), 256, 0, st>>>(
         ws->hE.p, GS, ngb + 1, ws->h_tot + 1, ho, RUN, RH, ho.cls && !c.ranged ? 1 : 0, row_lo, row_hi, c.heavy_df,
-        stats ? 1 : 0, 1, ws->bstats.p, ws->hgi.p, BT, BP, ws->htc.p);
+        stats ? 1 : 0, 1, ws->bstats.p, ws->hgi.p, BT, BP, ws->htc.p, ws->h_tot + 3);
     size_t t2 = 0;
     PG(rocprim::exclusive_scan(nullptr, t2, ws->htc.p, ws->htoff.p, 0ull, (size_t)ngb + 1,
                                rocprim::plus<unsigned long long>(), st));
@@ -677,7 +682,7 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
                                rocprim::plus<unsigned long long>(), st));
     // tiles = htoff[ng] (device); the grid strides them
     const uint32_t grid = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(ngb / 4, 256), 8192);
-    heavy_expand_kernel<<<grid, kHvI, 0, st>>>(ws->hE.p, GS, ws->hgi.p, BT, BP, RUN, RH, ws->htoff.p, ws->h_tot + 1,
+    heavy_expand_kernel<<<grid, kHvI, 0, st>>>(ws->hE.p, GS, ws->hgi.p, BT, BP, RUN, RH, ws->htoff.p, ws->h_tot + 3,
                                                ho, 1u << bits_for(c.n), c.require_diff, c.ranged ? 1 : 0, row_lo,
                                                row_hi, ws->inc_sorted.p, ws->shard_cap, ws->bstats.p + kRbCursor,
                                                ws->bstats.p, ws->hGH.p, c.k, c.sb, c.sor);
@@ -932,6 +937,7 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
                     ws->h_segs = rb[kRbSegs];
                     ws->h_segmax = rb[kRbSegMax];
                     ws->h_segl = rb[kRbSegL];
+                    ws->h_segw = rb[kRbSegW];
                 }
                 int rc = heavy_phase(ws, c, spill_total ? spill_total : ws->h_m, true, st);
                 if (rc != KMP_OK) return rc;

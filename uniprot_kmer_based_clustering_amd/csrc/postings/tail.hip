@@ -1099,7 +1099,7 @@ __global__ __launch_bounds__(256) void pt_emit_kernel(const uint32_t* __restrict
 // read-back: gstats (8 per shard) | pair cursors | spill cursors | the words below
 enum : uint32_t {
     kRbCursor = kShards * 8, kRbSpill = kShards * 9, kRbFlagBin = kShards * 10, kRbFlagClass, kRbRuns, kRbOvf,
-    kRbMaxBlock, kRbBinTiles, kRbFlagCur, kRbSegs, kRbSegMax, kRbFast, kRbList, kRbRange, kRbSegL, kRbWords
+    kRbMaxBlock, kRbBinTiles, kRbFlagCur, kRbSegs, kRbSegMax, kRbFast, kRbList, kRbRange, kRbSegL, kRbSegW, kRbWords
 };
 constexpr uint32_t kGsWords = kShards * 10;  // gstats | cursors | spill cursors (u64)
 
@@ -1134,6 +1134,7 @@ __device__ void step_pack_body(const unsigned long long* __restrict__ gstats, co
         rb[kRbSegMax] = flags[kFlSegMax];
         rb[kRbRange] = flags[kFlRange];
         rb[kRbSegL] = flags[kFlSegL];
+        rb[kRbSegW] = flags[kFlSegW];
     }
     __threadfence_system();  // rb is host memory, read after the stream synchronises
 }

@@ -115,7 +115,8 @@ struct kmp_postings {
     bool heavy = false;         // this workspace's batches spill: run the split step
     bool heavy_ready = false;   // hE / hGS hold the current front's compacted spill
     uint64_t h_m = 0;                // spill keys behind hE (the bound on elements and k-mers)
-    uint64_t h_segs = 0, h_segmax = 0, h_segl = 0;  // the front's spill segments: count, largest, large ones (read-back)
+    // the front's spill segments (read-back): count, largest, large ones, keys in whole buckets
+    uint64_t h_segs = 0, h_segmax = 0, h_segl = 0, h_segw = 0;
     int h_cls = 0;                   // hE in class order
     unsigned long long* h_tot = nullptr;  // device: elements, k-mers, class runs
     std::vector<unsigned long long> shape;  // (n, slots, code bits, bucket bits) of the last batch
