@@ -1,0 +1,11 @@
+# heavy compaction tiles of 1,024 keys (base) against 4,096 (hv4096): parity, config-1 A/B, config 5 (warm step) for each
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_multi.py -m gpu > gpurun_out/r05ak_tests.log 2>&1 || { tail -20 gpurun_out/r05ak_tests.log; exit 1; }
+tail -1 gpurun_out/r05ak_tests.log
+CONFIGS="config1" timeout -k 10 600 bash tools/ab_multi.sh || exit 2
+for v in base hv4096; do
+  if [ $v = base ]; then unset KMP_LIB; else export KMP_LIB=$GRAFT_REPO_ROOT/tools/ab/$v/libkmerpair.so; fi
+  timeout -k 10 300 python3 bench.py --no-cpu-baseline --config config5 --warmup 1 > gpurun_out/r05ak_c5_$v.json 2> gpurun_out/r05ak_c5_$v.err || exit 3
+  python3 -c "
+import json; d=json.load(open('gpurun_out/r05ak_c5_$v.json')); print('config5 $v', round(d['ms_per_step'],1), {k: round(v['ms'],1) for k,v in d['roofline']['stages'].items()})"
+done

@@ -16,7 +16,10 @@
 //      class test (mod.rs:580-587) on every pair (p_i, p_j), j > i; a workgroup scan and one
 //      cursor reservation place the pair keys p_i * mul + p_j in the shard regions the bucket
 //      kernels fill.  A k-mer of df 10^4 is ~400 tiles: no workgroup walks a long posting list.
-constexpr uint32_t kHvTile = 4096, kHvThreads = 256, kHvPer = kHvTile / kHvThreads;
+#ifndef KMP_HV_TILE
+#define KMP_HV_TILE 1024  // spilled keys per compaction tile (4,096 ran 249 workgroups at config 1: 11 + 15 us)
+#endif
+constexpr uint32_t kHvTile = KMP_HV_TILE, kHvThreads = 256, kHvPer = kHvTile / kHvThreads;
 constexpr uint32_t kHvI = 256, kHvJ = 256, kHvMW = kHvJ / 32;
 constexpr uint32_t kHvSpread = 64 * 256;  // a tile with this many pairs spreads them over the shards
 // flat tiles (class order, every pair kept, a k-mer of at most kHvFlatRuns class runs): the
@@ -298,13 +301,19 @@ __global__ __launch_bounds__(kHvThreads) void heavy_scan_kernel(const unsigned l
     const uint64_t t0 = (uint64_t)blockIdx.x * kHvTile;
     const unsigned es = ho.eshift();
     uint32_t ne = 0, ng = 0, nr = 0;
+    unsigned long long v[kHvPer], u[kHvPer];  // every load issued before any is used
+#pragma unroll
     for (uint32_t r = 0; r < kHvPer; ++r) {
         const uint64_t i = t0 + r * kHvThreads + threadIdx.x;
-        if (i >= m) break;
-        const unsigned long long v = x[i], u = i ? x[i - 1] : ~0ull;
-        ne += (v >> es) != (u >> es);
-        ng += (v >> ho.hshift) != (u >> ho.hshift);
-        nr += (v >> ho.pbits) != (u >> ho.pbits);
+        v[r] = i < m ? x[i] : 0ull;
+        u[r] = i < m && i ? x[i - 1] : ~0ull;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kHvPer; ++r) {
+        if (t0 + r * kHvThreads + threadIdx.x >= m) break;
+        ne += (v[r] >> es) != (u[r] >> es);
+        ng += (v[r] >> ho.hshift) != (u[r] >> ho.hshift);
+        nr += (v[r] >> ho.pbits) != (u[r] >> ho.pbits);
     }
     if (ne) atomicAdd(&s_e, ne);
     if (ng) atomicAdd(&s_g, ng);
