@@ -484,6 +484,26 @@ __global__ __launch_bounds__(kHvScanThreads) void heavy_tscan_kernel(const uint3
     }
 }
 
+// a side stream forked from st (its work after what st has queued) and joined back
+bool side_fork(kmp_postings* ws, hipStream_t st) {
+    static const bool off = getenv("KMP_SIDE") && getenv("KMP_SIDE")[0] == '0';
+    if (off) return false;
+    if (!ws->side && hipStreamCreateWithFlags(&ws->side, hipStreamNonBlocking) != hipSuccess) {
+        ws->side = nullptr;
+        return false;
+    }
+    for (hipEvent_t* e : {&ws->sev[0], &ws->sev[1]})
+        if (!*e && hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) {
+            *e = nullptr;
+            return false;
+        }
+    return hipEventRecord(ws->sev[0], st) == hipSuccess && hipStreamWaitEvent(ws->side, ws->sev[0], 0) == hipSuccess;
+}
+hipError_t side_join(kmp_postings* ws, hipStream_t st) {
+    hipError_t e = hipEventRecord(ws->sev[1], ws->side);
+    return e == hipSuccess ? hipStreamWaitEvent(st, ws->sev[1], 0) : e;
+}
+
 int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipStream_t st) {
     const Layout& lay = c.lay;
     HeavyOrder ho{};
@@ -559,12 +579,17 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
                                         (unsigned long long)k[w][b]);
                 }
             }
-            if (ws->h_segl)  // the listed large segments (every one when a front listed them all)
-                heavy_seg_kernel<1024, kSegSmall, kSegLarge><<<(uint32_t)ws->h_segl, 1024, 0, st>>>(
+            // the listed large segments on a side stream beside the small ones: a few workgroups'
+            // latency (~40 us at config 1) under the small kernel's throughput (~25 us)
+            hipStream_t ls = st;
+            if (ws->h_segl && side_fork(ws, st)) ls = ws->side;
+            if (ws->h_segl)
+                heavy_seg_kernel<1024, kSegSmall, kSegLarge><<<(uint32_t)ws->h_segl, 1024, 0, ls>>>(
                     ws->spill.p, ws->spill_cap, spill_cursor, ws->hseg.p, ws->hseg.p + seg_capacity(ws), ho,
                     ws->hsorted.p);
             heavy_seg_kernel<256, 0, kSegSmall><<<ns, 256, 0, st>>>(ws->spill.p, ws->spill_cap, spill_cursor,
                                                                     ws->hseg.p, nullptr, ho, ws->hsorted.p);
+            if (ls != st) PG(side_join(ws, st));
         } else {  // a segment above the LDS sort: gather and one radix sort
             gather_shards_kernel<<<dim3((uint32_t)std::min<uint64_t>((ws->spill_cap + 255) / 256, 1024), kShards),
                                    256, 0, st>>>(ws->spill.p, ws->spill_cap, spill_cursor, ho, ws->hkeys.p);

@@ -140,6 +140,8 @@ struct kmp_postings {
     } split_g[3];  // the k-mer split's phases (expand or group, edges, keys)
     hipGraphExec_t gexec = nullptr;
     hipStream_t cst = nullptr;  // capture stream
+    hipStream_t side = nullptr;   // side_fork: the heavy path's large segment sorts
+    hipEvent_t sev[2] = {};
 
     std::vector<unsigned long long> gkey, gkey_seen;
     uint64_t graph_replays = 0;
@@ -168,6 +170,9 @@ struct kmp_postings {
         if (gexec) (void)hipGraphExecDestroy(gexec);
         for (auto& g : split_g) g.reset();
         if (cst) (void)hipStreamDestroy(cst);
+        if (side) (void)hipStreamDestroy(side);
+        for (auto& e : sev)
+            if (e) (void)hipEventDestroy(e);
     }
     void mark(int stage, hipStream_t st) {
         if (timing) (void)hipEventRecord(ev[stage], st);
