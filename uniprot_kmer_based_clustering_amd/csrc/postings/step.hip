@@ -504,6 +504,11 @@ hipError_t side_join(kmp_postings* ws, hipStream_t st) {
     return e == hipSuccess ? hipStreamWaitEvent(st, ws->sev[1], 0) : e;
 }
 
+__global__ void copy_u64_kernel(unsigned long long* __restrict__ dst, const unsigned long long* __restrict__ src,
+                                uint32_t n) {
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+}
+
 int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipStream_t st) {
     const Layout& lay = c.lay;
     HeavyOrder ho{};
@@ -548,8 +553,9 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
         // (its cursors cleared by the next call) can be compacted again in the other order
         PG(ws->hcur.reserve(kShards));
         if (!ws->hcur_valid) {
-            PG(hipMemcpyAsync(ws->hcur.p, ws->bstats.p + kRbSpill, kShards * sizeof(unsigned long long),
-                              hipMemcpyDeviceToDevice, st));
+            // a kernel, not a device-to-device copy: the blit and the launch after it left ~15 us of
+            // idle GPU at config 1
+            copy_u64_kernel<<<1, kShards, 0, st>>>(ws->hcur.p, ws->bstats.p + kRbSpill, kShards);
             ws->hcur_valid = true;
         }
         const unsigned long long* spill_cursor = ws->hcur.p;
