@@ -403,6 +403,33 @@ def test_frequent_kmers_heavy_path(oracle_mod, copies):
     np.testing.assert_array_equal(pipe.edges()[1], q)
 
 
+def test_whole_bucket_segment(oracle_mod):
+    """A bucket between the large bucket kernel's 4,096 keys and the LDS segment sort's 8,192 (one
+    7-mer in 4,500 proteins, once each, plus the bucket's other keys): spilled whole and sorted by
+    heavy_seg_kernel<1024, 2048, 8192> on its compacted key (k-mer slot | varying low bits), in
+    class order (class filter on) and plain order (off); the edges equal the oracle's."""
+    import torch
+    from uniprot_kmer_based_clustering_amd.device import DevicePipeline
+    rng = np.random.default_rng(17)
+    alpha = np.frombuffer(b"ACDEFGHIKLMNPQRSTVY", dtype=np.uint8)  # no W before the W block
+    n = 4500
+    seqs = [alpha[rng.integers(0, 19, 110)].tobytes() + b"WWWWWWW" for i in range(n)]
+    res, off, cls = make_batch(seqs, [str(i % 5) for i in range(n)])
+    o = oracle_mod.Oracle(res, off, cls, k=7, threads=8)
+    pipe = DevicePipeline(K.Proteins(res, off, cls), 7, "cuda:0")
+    for eng in ("residues", "postings"):
+        for diff in (True, False):
+            m = pipe.step(require_class_diff=diff, engine=eng)
+            torch.cuda.synchronize()
+            assert pipe.last_layout() == "bucketed" and pipe.last_heavy()
+            p, q, w = o.pairs(require_class_diff=diff)
+            assert m == len(p)
+            np.testing.assert_array_equal(pipe.edges()[0], p)
+            np.testing.assert_array_equal(pipe.edges()[1], q)
+            np.testing.assert_array_equal(pipe.edges()[2], w)
+    assert pipe.postings_stats.as_dict()["max_df"] == o.counters()["max_df"] == n
+
+
 @pytest.mark.parametrize("tail", ["fast", "count"])
 def test_uniprot_k5_on_bucketed_heavy_path(oracle_mod, uni, tail):
     """The reference's dataset at k = 5 (max df 3,694): bucketed layout with the heavy path and
