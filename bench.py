@@ -404,7 +404,10 @@ def main(argv=None, dist_mod=None):
         return pipe.step(engine=args.engine)
 
     stage_sum = None
-    if postings and world == 1:
+    # (BENCH_NO_STAGE_TIMING=1: diagnostic only — the step without its stage events; the line then
+    # carries no measured roofline)
+    stage_timing = postings and world == 1 and os.environ.get("BENCH_NO_STAGE_TIMING") != "1"
+    if stage_timing:
         pipe.set_stage_timing(True)  # before the warm-up: the timed steps replay the same graph
     for _ in range(args.warmup):
         one_step()
@@ -416,14 +419,14 @@ def main(argv=None, dist_mod=None):
         # N > 1: the step ends with the canonical list on rank 0 (SURVEY.md §8d's clock), so it
         # includes the rank-order gather of every rank's rows
         n_edges = one_step(gather=True)
-        if postings and world == 1:
+        if stage_timing:
             st = np.array(pipe.postings_stats.stage_ms[:], dtype=np.float64)
             stage_sum = st if stage_sum is None else stage_sum + st
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    if postings and world == 1:
+    if stage_timing:
         pipe.set_stage_timing(False)
     rank_info = None
     if world > 1:
