@@ -401,3 +401,96 @@ def test_sharded_split_exchange(world):
     assert all(m[2] for m in msgs), msgs
     assert msgs[0][4] >= 1 and msgs[0][5] > 64 and msgs[0][6] > 256
     assert msgs[1][4] == msgs[0][4]  # the second step reran nothing
+
+
+class OracleClassWidePipe(OracleSplitPipe):
+    """The rebuilt batch of a class-wide batch: every split_expand raises KMP_SPLIT_CLASS (class ids
+    too wide for the k-mer split's key), as the library's flags do."""
+
+    def split_expand(self, part, parts, cap, send, flags, stats, learn=None, require_class_diff=True):
+        from uniprot_kmer_based_clustering_amd import _lib
+        super().split_expand(part, parts, cap, send, flags, stats, learn, require_class_diff)
+        flags[_lib.KMP_SPLIT_CLASS] = 1
+
+
+class OracleClassWideShardPipe(OracleShardPipe):
+    def gathered_pipeline(self, residues):
+        P, Q, W = self.o.pairs()
+        full = OracleClassWidePipe(self.n, P, Q, W, self.cap0)
+        full.res = residues.clone()
+        full.k = 7
+        self.gathered.append(full)
+        return full
+
+
+def class_fallback_worker(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, ROOT)
+        from uniprot_kmer_based_clustering_amd.dist import SplitState, row_ranges, sharded_split_step
+        b, o = build_case()
+        P, Q, W = o.pairs()
+        lo, hi = row_ranges(b.n, world)[rank]
+        for gather in (True, False):
+            pipe = OracleClassWideShardPipe(b, o, cap=16 if rank == 0 else 1 << 20, part=rank, parts=world)
+            state = SplitState()
+            for step in range(2):  # the first step falls back inside the split, the second starts there
+                n = sharded_split_step(pipe, rank, world, gather=gather, state=state, start="residues")
+                if gather and rank != 0:
+                    continue
+                keep = np.ones(len(P), bool) if gather else (P >= lo) & (P < hi)
+                ok = (n == int(keep.sum())
+                      and np.array_equal(pipe.ep[:n].numpy().view(np.uint32), P[keep])
+                      and np.array_equal(pipe.eq[:n].numpy().view(np.uint32), Q[keep])
+                      and np.array_equal(pipe.ew[:n].numpy().view(np.uint32), W[keep]))
+                out_q.put(("class", gather, step, rank, ok, n, state.row_split, len(pipe.gathered)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_class_fallback_on_residue_start(world):
+    """Class ids too wide for the key on the residue start: the split's reduced CLASS flag sends the
+    step to the row split over the same rebuilt batch, once — rank 0 holds the canonical list exactly
+    (no rank's block gathered twice) with gather, and every rank its own rows without it, on the
+    step that falls back and on the next one."""
+    port = free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=class_fallback_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    msgs = [q.get(timeout=300) for _ in range(2 + 2 * world)]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert all(m[4] and m[6] for m in msgs), msgs
+    assert all(m[7] == 1 for m in msgs)  # the batch rebuilt once
+
+
+def test_own_residues_with_fewer_chunks_than_ranks():
+    """ShardPipeline.own_residues: with 2 key chunks on 4 ranks, two ranks hold no chunk.  The
+    ranks' contributions still tile the residues every window reads, so the batch the residue start
+    and the row-split fallback rebuild is the batch (host-only: the split plan and the slices)."""
+    import uniprot_kmer_based_clustering_amd as K
+    from uniprot_kmer_based_clustering_amd import _lib
+    from uniprot_kmer_based_clustering_amd.device import ShardPipeline
+    b = K.synth(20, 3)  # ~6,000 residues: two 4,096-slot chunks
+    res = np.asarray(b.residues, dtype=np.uint8)
+    off = np.asarray(b.offsets, dtype=np.uint64)
+    for parts in (2, 3, 4, 8):
+        spans = []
+        for part in range(parts):
+            sp = ShardPipeline(res, off, b.class_id, 7, part, parts, device="cpu")
+            lo, hi, own = sp.own_residues()
+            assert own.numel() == hi - lo and np.array_equal(own.numpy(), res[lo:hi])
+            if hi > lo:
+                spans.append((lo, hi))
+        assert spans[0][0] == 0 and spans[-1][1] == int(off[-1]), (parts, spans)
+        assert all(a[1] == c[0] for a, c in zip(spans, spans[1:])), (parts, spans)
+        if parts == 4:
+            empty = [d for d in range(parts) if int(_lib.split_plan(off, 7, d, parts).res_hi) ==
+                     int(_lib.split_plan(off, 7, d, parts).res_lo)]
+            assert empty, "the case needs a rank without chunks"

@@ -1,10 +1,10 @@
 # A/B of the bench over library variants: base (in-tree) and tools/ab/<name>/libkmerpair.so,
-# alternating, twice; CONFIGS (default "config3") picks the bench configs
+# alternating, ROUNDS times (default 2); CONFIGS (default "config3") picks the bench configs
 set -e
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 for cfg in ${CONFIGS:-config3}; do
-  for i in 1 2; do
+  for i in $(seq ${ROUNDS:-2}); do
     for v in base $(ls tools/ab 2>/dev/null); do
       if [ $v = base ]; then unset KMP_LIB; else export KMP_LIB=$GRAFT_REPO_ROOT/tools/ab/$v/libkmerpair.so; fi
       timeout -k 10 120 python3 bench.py --no-cpu-baseline --config $cfg > gpurun_out/ab_$v.json 2>/dev/null

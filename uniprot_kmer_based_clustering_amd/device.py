@@ -224,10 +224,19 @@ class ShardPipeline(_SplitEdges):
 
     def own_residues(self):
         """(lo, hi, tensor): the residues this rank contributes when the batch is rebuilt on every
-        rank (the row-split fallback): [res_lo, the next rank's res_lo) within its slice."""
-        nxt = (_lib.split_plan(self.offsets_host, self.k, self.part + 1, self.parts).res_lo
-               if self.part + 1 < self.parts else self.total)
-        hi = max(self.res_lo, min(int(nxt), self.res_hi))
+        rank (the residue start and the row-split fallback): [res_lo, the res_lo of the next rank
+        that holds chunks) within its slice.  With fewer chunks than ranks some ranks hold none
+        (kmp_split_plan reports an empty span for them) and contribute nothing; the rank before
+        them contributes up to the next rank that does."""
+        if self.res_hi <= self.res_lo:
+            return self.res_lo, self.res_lo, self.res[:0]
+        nxt = self.total
+        for d in range(self.part + 1, self.parts):
+            sp = _lib.split_plan(self.offsets_host, self.k, d, self.parts)
+            if int(sp.res_hi) > int(sp.res_lo):
+                nxt = int(sp.res_lo)
+                break
+        hi = max(self.res_lo, min(nxt, self.res_hi))
         return self.res_lo, hi, self.res[:hi - self.res_lo]
 
 

@@ -142,7 +142,8 @@ def _pipe_state(pipe) -> SplitState:
 
 
 def kmer_split_step(pipe, rank: int, world: int, group=None, min_shared: int = 1, require_class_diff: bool = True,
-                    gather: bool = False, state: SplitState | None = None, timings: list | None = None) -> int:
+                    gather: bool = False, state: SplitState | None = None, timings: list | None = None,
+                    class_fallback: bool = True) -> int | None:
     """One multi-GPU step of the k-mer split: expand this rank's k-mers, exchange the pair keys by
     row owner (all-to-all), reduce this rank's rows.  Every rank ends holding the canonical edges
     of its row range in pipe.ep/eq/ew (rank order = canonical order) and returns their count; with
@@ -150,11 +151,15 @@ def kmer_split_step(pipe, rank: int, world: int, group=None, min_shared: int = 1
     that spills frequent k-mers reruns with the heavy path on (KMP_SPLIT_HEAVY in the reduced flags);
     one whose class ids overflow the key falls back to the row split (distributed_step).  timings: a
     list to append this rank's (expand, exchange, edges) milliseconds to (CUDA events on the
-    current stream, which the library's stages and the collectives are ordered with)."""
+    current stream, which the library's stages and the collectives are ordered with).
+    class_fallback=False: a batch whose class ids overflow the key sets state.row_split and returns
+    None instead of running the row split here (the caller's start runs it over its own batch)."""
     st = state if state is not None else _pipe_state(pipe)
-    if st.row_split:
-        return distributed_step(pipe, rank, world, group, min_shared, require_class_diff)
     lo, hi = row_ranges(pipe.n, world)[rank]
+    if st.row_split:
+        if gather:
+            return distributed_step(pipe, rank, world, group, min_shared, require_class_diff)
+        return pipe.rows(lo, hi, min_shared=min_shared, require_class_diff=require_class_diff)
     dev = pipe.dev if hasattr(pipe, "dev") else torch.device("cpu")
     if world == 1 and hasattr(pipe, "step"):
         # one rank owns every k-mer and every row: nothing to route or exchange, so the fused
@@ -209,7 +214,10 @@ def kmer_split_step(pipe, rank: int, world: int, group=None, min_shared: int = 1
         fl = [int(x) for x in st.host_flags.tolist()]
         if fl[_lib.KMP_SPLIT_CLASS]:
             st.row_split = True
-            return distributed_step(pipe, rank, world, group, min_shared, require_class_diff)
+            if not class_fallback:
+                return None
+            return distributed_step(pipe, rank, world, group, min_shared, require_class_diff) if gather else \
+                pipe.rows(lo, hi, min_shared=min_shared, require_class_diff=require_class_diff)
         if fl[_lib.KMP_SPLIT_RERUN] or fl[_lib.KMP_SPLIT_HEAVY]:  # HEAVY: the heavy path on every rank
             st.reruns += 1
             st.rerun_flags.append(fl)
@@ -323,10 +331,13 @@ def _row_split_from_shards(pipe, rank, world, group, min_shared, require_class_d
     return m
 
 
-def _residue_start(pipe, rank, world, group, min_shared, require_class_diff, st, timings):
+def _residue_start(pipe, rank, world, group, min_shared, require_class_diff, st, timings, gather):
     """The sharded start through the residues: the ranks' slices all-gathered into a whole batch
     (built once per batch, refreshed in place every step), then the k-mer split with every rank
-    keying every window (kmer_split_step).  The rank's edges end in pipe.ep/eq/ew."""
+    keying every window (kmer_split_step).  The rank's edges end in pipe.ep/eq/ew; with gather,
+    rank 0's hold every rank's block and it returns the total.  Class ids too wide for the key:
+    the row split over the same rebuilt batch (once: the split's own fallback is not taken, so no
+    rank's block is gathered twice)."""
     cuda = pipe.dev.type == "cuda"
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)] if timings is not None and cuda else None
     if ev:
@@ -340,14 +351,19 @@ def _residue_start(pipe, rank, world, group, min_shared, require_class_diff, st,
         ev[1].record()
     inner = [] if timings is not None else None
     # the same SplitState: the pair-key capacity, reruns and fallback are the step's
-    m = kmer_split_step(st.full, rank, world, group, min_shared, require_class_diff, state=st, timings=inner)
+    m = kmer_split_step(st.full, rank, world, group, min_shared, require_class_diff, state=st, timings=inner,
+                        class_fallback=False)
+    if m is None:  # class ids too wide (st.row_split is set)
+        return _row_split_from_shards(pipe, rank, world, group, min_shared, require_class_diff, gather, st)
     full = st.full
     pipe.ep, pipe.eq, pipe.ew, pipe.n_edges = full.ep, full.eq, full.ew, m
     pipe.edge_cap = full.edge_cap
     if timings is not None and inner:
         gx = ev[0].elapsed_time(ev[1]) if ev else 0.0
         timings.append((0.0, gx) + tuple(inner[-1]))
-    return m
+    if not gather:
+        return m
+    return _gather_to_rank0(pipe, m, rank, world, group)
 
 
 def sharded_split_step(pipe, rank: int, world: int, group=None, min_shared: int = 1,
@@ -366,10 +382,7 @@ def sharded_split_step(pipe, rank: int, world: int, group=None, min_shared: int 
     if st.row_split:
         return _row_split_from_shards(pipe, rank, world, group, min_shared, require_class_diff, gather, st)
     if world > 1 and start_mode(start, world) == "residues":
-        m = _residue_start(pipe, rank, world, group, min_shared, require_class_diff, st, timings)
-        if not gather:
-            return m
-        return _gather_to_rank0(pipe, m, rank, world, group)
+        return _residue_start(pipe, rank, world, group, min_shared, require_class_diff, st, timings, gather)
     lo, hi = row_ranges(pipe.n, world)[rank]
     dev = pipe.dev
     cuda = dev.type == "cuda"
