@@ -310,7 +310,7 @@ class OracleShardPipe(OracleSplitPipe):
         stats[6] = len(keys)
 
 
-def shard_worker(rank, world, port, out_q):
+def shard_worker(rank, world, port, out_q, start="keys"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -323,7 +323,7 @@ def shard_worker(rank, world, port, out_q):
         state = SplitState()
         state.cap, state.kcap = 64, 256  # far too small: the first step reruns with both learned
         for ms in (1, 3):
-            n = sharded_split_step(pipe, rank, world, min_shared=ms, gather=True, state=state, start="keys")
+            n = sharded_split_step(pipe, rank, world, min_shared=ms, gather=True, state=state, start=start)
             if rank == 0:
                 keep = W >= ms
                 ok = (n == int(keep.sum())
@@ -494,3 +494,25 @@ def test_own_residues_with_fewer_chunks_than_ranks():
             empty = [d for d in range(parts) if int(_lib.split_plan(off, 7, d, parts).res_hi) ==
                      int(_lib.split_plan(off, 7, d, parts).res_lo)]
             assert empty, "the case needs a rank without chunks"
+
+
+def test_sharded_split_world8_auto_start():
+    """The collective sequence the 8-GPU bench runs (bench.py --gpus 8: sharded_split_step with
+    start='auto', which resolves to the key start from KEYS_START_MIN_WORLD ranks): key all-to-all,
+    pair-key all-to-all, flag all-reduce, reruns with learned capacities and the rank-order gather,
+    in 8 processes over gloo — the canonical list on rank 0."""
+    from uniprot_kmer_based_clustering_amd.dist import KEYS_START_MIN_WORLD, start_mode
+    world = 8
+    assert start_mode("auto", world) == "keys" and KEYS_START_MIN_WORLD <= world
+    port = free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=shard_worker, args=(r, world, port, q, "auto")) for r in range(world)]
+    for p in procs:
+        p.start()
+    msgs = [q.get(timeout=600) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in procs)
+    assert all(m[2] for m in msgs), msgs
+    assert msgs[0][4] >= 1 and msgs[1][4] == msgs[0][4]  # reran once with the learned sizes, then not
