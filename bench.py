@@ -83,12 +83,18 @@ def parse(argv=None):
     ap.add_argument("--config", default="config3", choices=sorted(CONFIGS))
     ap.add_argument("--engine", default="residues", choices=["residues", "postings", "tiles"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sync", action="store_true",
+                    help="one GPU: a synchronous call per step (kmp_dev_pairs_residues) instead of pipelined "
+                         "submissions (kmp_dev_pairs_residues_submit / kmp_postings_wait)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="oracle threads of the all-cores run (0: every usable core)")
     ap.add_argument("--score", default="blosum", choices=["blosum", "count"], help="config5: edge score")
     ap.add_argument("--split", default="kmer", choices=["kmer", "replicated", "rows"], help="multi-GPU flow (N > 1)")
     ap.add_argument("--start", default="auto", choices=["auto", "keys", "residues"],
                     help="the sharded start's first exchange (--split kmer, N > 1): the key all-to-all, the "
                          "residue all-gather, or auto (keys from 8 GPUs up)")
+    ap.add_argument("--rank-of", default=None, metavar="R/G",
+                    help="config5, one GPU: stream only rank R's rows of a G-rank split (kmp_row_split), the "
+                         "per-rank share of the N > 1 run, measured alone")
     ap.add_argument("--direct-tail", type=int, default=1, help="config5: fused reduction writes edges in place (A/B)")
     ap.add_argument("--flat-heavy", type=int, default=1, help="config5: passes expand frequent k-mers by rows (A/B)")
     return ap.parse_args(argv)
@@ -247,11 +253,16 @@ def bench_config5(args):
     score = _lib.KMP_SCORE_BLOSUM if args.score == "blosum" else _lib.KMP_SCORE_COUNT
     proteins = K.synth(n, seed, law)
     lo, hi = (int(x) for x in _lib.row_split(n, world)[rank:rank + 2])
+    emulated = None
+    if args.rank_of and world == 1:  # one rank's share of a G-rank row split, on this one GPU
+        er, eg = (int(x) for x in args.rank_of.split("/"))
+        lo, hi = (int(x) for x in _lib.row_split(n, eg)[er:er + 2])
+        emulated = {"rank": er, "of": eg, "row_lo": lo, "row_hi": hi}
     with K.KmerPairEngine(local, 16) as e:
         e.load(proteins)
         e.set_direct_tail(bool(args.direct_tail))
         e.set_flat_heavy(bool(args.flat_heavy))
-        if world > 1:
+        if world > 1 or emulated:
             e.set_rows(lo, hi)
         for _ in range(warmup):
             e.pairs_stream(ks, score=score)
@@ -337,7 +348,13 @@ def bench_config5(args):
                                 "rank 0's when N > 1"}}
     if ranks:
         out["ranks"] = ranks
-    if world == 1:
+    if emulated:
+        # one rank's rows measured alone: value and edges are that rank's share, not the batch's
+        emulated["stage_ms"] = sm["stage_ms"]
+        out["emulated_rank"] = emulated
+        out["value"] = None
+        out["note"] = "per-rank evidence (--rank-of): ms_per_step is one rank's stream of its kmp_row_split rows"
+    if world == 1 and not emulated:
         if not ranks and "digest" in sm:
             out["digest"] = str(sm["digest"])
         if not args.no_cpu_baseline:
@@ -409,23 +426,62 @@ def main(argv=None, dist_mod=None):
     stage_timing = postings and world == 1 and os.environ.get("BENCH_NO_STAGE_TIMING") != "1"
     if stage_timing:
         pipe.set_stage_timing(True)  # before the warm-up: the timed steps replay the same graph
-    for _ in range(args.warmup):
-        one_step()
+    # one GPU, residues engine: the steps go out as pipelined submissions — step i + 1 is queued
+    # behind step i, then step i is waited for and its read-back checked (a step that asks for a rerun
+    # runs again at its wait) — so the device does not idle between steps while the host checks the
+    # last one and launches the next; --sync: one synchronous call per step
+    pipelined = world == 1 and args.engine == "residues" and not args.sync
+
+    def run_steps(count, record=None):
+        n = 0
+        if not pipelined:
+            for _ in range(count):
+                # N > 1: the step ends with the canonical list on rank 0 (SURVEY.md §8d's clock), so
+                # it includes the rank-order gather of every rank's rows
+                n = one_step(gather=True)
+                if record:
+                    record()
+            return n
+        prev = None
+        for _ in range(count):
+            t = pipe.submit()
+            if prev is not None:
+                n = pipe.wait(prev)
+                if record:
+                    record()
+            prev = t
+        if prev is not None:
+            n = pipe.wait(prev)
+            if record:
+                record()
+        return n
+
+    def record():
+        nonlocal stage_sum
+        if stage_timing:
+            st = np.array(pipe.postings_stats.stage_ms[:], dtype=np.float64)
+            stage_sum = st if stage_sum is None else stage_sum + st
+
+    run_steps(args.warmup)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        # N > 1: the step ends with the canonical list on rank 0 (SURVEY.md §8d's clock), so it
-        # includes the rank-order gather of every rank's rows
-        n_edges = one_step(gather=True)
-        if stage_timing:
-            st = np.array(pipe.postings_stats.stage_ms[:], dtype=np.float64)
-            stage_sum = st if stage_sum is None else stage_sum + st
+    n_edges = run_steps(args.steps, record)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    sync_ms = None
+    if pipelined:  # untimed: the synchronous call's latency per step, for the record
+        for _ in range(3):
+            pipe.step(engine=args.engine)
+        torch.cuda.synchronize()
+        s0 = time.perf_counter()
+        for _ in range(10):
+            pipe.step(engine=args.engine)
+        torch.cuda.synchronize()
+        sync_ms = (time.perf_counter() - s0) / 10 * 1e3
     if stage_timing:
         pipe.set_stage_timing(False)
     rank_info = None
@@ -511,6 +567,11 @@ def main(argv=None, dist_mod=None):
                                        if args.split == "replicated" else f"row split x{world}")},
             "edges_per_s": n_edges / (dt / args.steps),
         }
+        if world == 1:
+            out["config"]["steps_issued"] = ("pipelined submissions (two outstanding; each step waited for and "
+                                             "its read-back checked)" if pipelined else "one synchronous call per step")
+            if sync_ms is not None:
+                out["ms_per_step_sync"] = sync_ms
         if rank_info is not None:
             # roofline of the whole multi-GPU step: its algorithmic bytes (the single-GPU stage
             # model over all ranks' work plus the pair keys crossing the links) against N x peak

@@ -515,6 +515,23 @@ int kmp_dev_pairs_residues(kmp_postings* ws, const uint8_t* d_res, const uint64_
                            uint32_t min_shared, int require_class_diff, uint32_t* d_p, uint32_t* d_q, uint32_t* d_w,
                            uint64_t cap, uint64_t* n_edges, kmp_postings_stats* stats, void* stream);
 
+/* Pipelined form of kmp_dev_pairs_residues (the reference's main.rs:57-234 run over a stream of
+ * batches: one call per batch, back to back).  submit enqueues the step on `stream` and returns a
+ * ticket; once the step's HIP graph is captured (the third submission of an unchanged shape), it
+ * goes out without a host wait, so the next submission is queued behind it before its read-back is
+ * checked and the device does not idle between steps.  kmp_postings_wait(ticket) waits for that
+ * step, checks its read-back and returns its edge count and statistics exactly as the synchronous
+ * call does; a step whose read-back asks for a rerun (a capacity overflow, a fallback) is run again
+ * synchronously at its wait, after the stream has drained.  At most two submissions are
+ * outstanding (KMP_ESTATE otherwise); each has its own read-back and stage events.  Edge arrays of
+ * two outstanding submissions must differ if the caller reads both (the later step overwrites the
+ * earlier's arrays otherwise).  Waits may come in any order; every ticket is waited once. */
+int kmp_dev_pairs_residues_submit(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off,
+                                  const uint16_t* d_class, uint32_t n, int k, uint64_t slots, uint32_t heavy_df,
+                                  uint32_t min_shared, int require_class_diff, uint32_t* d_p, uint32_t* d_q,
+                                  uint32_t* d_w, uint64_t cap, void* stream, uint64_t* ticket);
+int kmp_postings_wait(kmp_postings* ws, uint64_t ticket, uint64_t* n_edges, kmp_postings_stats* stats);
+
 /* The residue path restricted to rows [row_lo, row_hi): only the pairs (p, q), p < q, whose
  * smaller protein p lies in the range (every k-mer group still grouped in full, so each pair's
  * w is complete).  The edges come out in canonical order; concatenating the calls of

@@ -1,0 +1,108 @@
+"""Pipelined submissions (kmp_dev_pairs_residues_submit / kmp_postings_wait, include/kmerpair.h):
+the bench's one-GPU steps.  Every waited step is bit-exact against the oracle — the first
+submissions of a shape (run synchronously at submit), the captures, and the replays that go out
+without a host wait while the previous step is still in flight — and the read-back checks of a
+waited step behave as the synchronous call's (an edge array that is too short: KMP_EOVERFLOW at
+the wait, grown, exact).  All calls go through the C ABI."""
+import numpy as np
+import pytest
+
+import uniprot_kmer_based_clustering_amd as K
+from uniprot_kmer_based_clustering_amd import _lib
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(pipe, p, q, w):
+    ep, eq, ew = pipe.edges()
+    np.testing.assert_array_equal(ep, p)
+    np.testing.assert_array_equal(eq, q)
+    np.testing.assert_array_equal(ew, w)
+
+
+@pytest.mark.parametrize("tail", ["fast", "count"])
+def test_pipelined_steps_bit_exact(oracle_mod, tail):
+    import torch
+    from uniprot_kmer_based_clustering_amd.device import DevicePipeline
+    b = K.synth(20000, 21)
+    p, q, w = oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=7, threads=8).pairs()
+    pipe = DevicePipeline(b, 7, "cuda:0")
+    pipe.set_tail(tail)
+    pipe.set_stage_timing(True)
+    replays0 = pipe.graph_replays()
+    prev = None
+    for i in range(10):  # two outstanding from the second submission on
+        t = pipe.submit()
+        if prev is not None:
+            assert pipe.wait(prev) == len(p)
+            st = pipe.postings_stats.as_dict()
+            assert st["pairs"] == len(p) and st["incidences"] > 0
+            assert all(x >= 0 for x in pipe.postings_stats.stage_ms[:6])
+        prev = t
+    assert pipe.wait(prev) == len(p)
+    torch.cuda.synchronize()
+    _check(pipe, p, q, w)
+    assert pipe.last_tail() == ("fast" if tail == "fast" else "rows")
+    assert pipe.graph_replays() - replays0 >= 5  # the slots' graphs replayed without host waits
+    # the synchronous call between submissions of the same shape, and after them
+    assert pipe.step(engine="residues") == len(p)
+    t1 = pipe.submit()
+    assert pipe.step(engine="residues") == len(p)  # (queued behind the submission on the stream)
+    assert pipe.wait(t1) == len(p)
+    _check(pipe, p, q, w)
+
+
+def test_pipelined_limits_and_overflow(oracle_mod):
+    """Two outstanding submissions at most (KMP_ESTATE on a third); an unknown or already waited
+    ticket is KMP_EINVAL; edge arrays too short for the step: KMP_EOVERFLOW at the wait, the arrays
+    grown and the step run again, bit-exact."""
+    import ctypes as C
+    from uniprot_kmer_based_clustering_amd.device import DevicePipeline
+    b = K.synth(8000, 5)
+    p, q, w = oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=7, threads=8).pairs()
+    pipe = DevicePipeline(b, 7, "cuda:0", edge_cap=1024)  # far too short
+    t0 = pipe.submit()
+    assert pipe.wait(t0) == len(p)  # grown at the wait
+    _check(pipe, p, q, w)
+    for _ in range(4):  # to the replaying graphs
+        pipe.wait(pipe.submit())
+    a, c = pipe.submit(), pipe.submit()
+    lib = _lib.lib()
+    ws = pipe._workspace()
+    args = pipe._sub_call[1]
+    tk = C.c_uint64()
+    third = lib.kmp_dev_pairs_residues_submit(*args[:-1], C.byref(tk))
+    assert third == _lib.KMP_ESTATE
+    assert pipe.wait(c) == len(p) and pipe.wait(a) == len(p)  # any order
+    ne = C.c_uint64()
+    assert lib.kmp_postings_wait(ws, a, C.byref(ne), None) == _lib.KMP_EINVAL  # waited already
+    _check(pipe, p, q, w)
+
+
+def test_split_front_graph_replay_verified(oracle_mod, monkeypatch):
+    """The split step's front (frequent k-mers: a bucket above every LDS capacity and a level-2 bin
+    above its tile budget, so the first calls rerun with learned sizes) is captured and replayed as
+    a HIP graph; with KMP_GRAPH_VERIFY every replay is first re-captured and its launches (function,
+    grid, block, shared memory) compared with the graph's — a launch input missing from the key
+    fails the call.  The postings entry's front holds rocPRIM's memset nodes and is never replayed
+    (graph_replayable).  Every call bit-exact."""
+    import torch
+    from common import make_batch
+    from uniprot_kmer_based_clustering_amd.device import DevicePipeline
+    monkeypatch.setenv("KMP_GRAPH_VERIFY", "1")
+    rng = np.random.default_rng(11)
+    alpha = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", dtype=np.uint8)
+    copies = 12000
+    seqs = [alpha[rng.integers(0, 20, 120)].tobytes() + b"WWWWWWW" * (1 + i % 2) for i in range(copies)]
+    res, off, cls = make_batch(seqs, [str(i % 7) for i in range(copies)])
+    p, q, w = oracle_mod.Oracle(res, off, cls, k=7, threads=8).pairs()
+    pipe = DevicePipeline(K.Proteins(res, off, cls), 7, "cuda:0")
+    for eng in ("residues", "postings"):
+        r0 = pipe.graph_replays()
+        for _ in range(5):
+            assert pipe.step(engine=eng) == len(p)
+            torch.cuda.synchronize()
+            assert pipe.last_heavy()
+            _check(pipe, p, q, w)
+        if eng == "residues":
+            assert pipe.graph_replays() - r0 >= 2  # the front replayed (verified)

@@ -199,6 +199,9 @@ SIGNATURES = {
     "kmp_postings_set_shard_floor": (C.c_int, [P, C.c_uint64]),
     "kmp_dev_pairs_residues": (C.c_int, [P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32,
                                          C.c_uint32, C.c_int, P, P, P, C.c_uint64, U64P, P, P]),
+    "kmp_dev_pairs_residues_submit": (C.c_int, [P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32,
+                                                C.c_uint32, C.c_int, P, P, P, C.c_uint64, P, U64P]),
+    "kmp_postings_wait": (C.c_int, [P, C.c_uint64, U64P, P]),
     "kmp_dev_split_expand": (C.c_int, [P, P, P, P, C.c_uint32, C.c_int, C.c_uint64, C.c_uint32, C.c_int,
                                         C.c_uint32, C.c_uint32, C.c_uint64, P, P, P, P, P]),
     "kmp_dev_split_edges": (C.c_int, [P, P, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P, P, P,

@@ -1824,6 +1824,7 @@ int kmp_ctx_set_flat_heavy(kmp_ctx* c, int enable) {
 int kmp_ctx_set_direct_tail(kmp_ctx* c, int enable) {
     if (!c) return KMP_EINVAL;
     c->direct_tail = enable ? 1 : 0;
+    c->budget[1] = 0;  // the fused pass budget depends on the bytes per key of the tail
     return KMP_OK;
 }
 

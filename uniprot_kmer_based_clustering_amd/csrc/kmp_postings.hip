@@ -37,6 +37,7 @@
 #include <cstdlib>
 #include <cstdint>
 #include <chrono>
+#include <memory>
 #include <vector>
 
 #include "kmerpair.h"

@@ -171,6 +171,122 @@ int kmp_dev_pairs_residues(kmp_postings* ws, const uint8_t* d_res, const uint64_
                          0, n, d_p, d_q, d_w, cap, n_edges, stats, stream);
 }
 
+}  // extern "C"
+
+// pipelined submissions (kmp_dev_pairs_residues_submit / kmp_postings_wait), held in ws->async
+struct AsyncSub {
+    bool used = false, launched = false;  // launched: in flight without a host wait (else finished at submit)
+    uint64_t ticket = 0;
+    int rc = KMP_OK;
+    uint64_t n_edges = 0;
+    kmp_postings_stats stats{};
+    const uint8_t* d_res = nullptr;
+    const uint64_t* d_res_off = nullptr;
+    const uint16_t* d_class = nullptr;
+    uint32_t n = 0;
+    int k = 0;
+    uint64_t slots = 0;
+    uint32_t heavy_df = 0, min_shared = 0;
+    int require_class_diff = 0;
+    uint32_t *d_p = nullptr, *d_q = nullptr, *d_w = nullptr;
+    uint64_t cap = 0;
+    void* stream = nullptr;
+    PtGeom g{};
+};
+struct AsyncState {
+    AsyncSub sub[2];
+    uint64_t next = 1;
+};
+
+extern "C" {
+
+int kmp_dev_pairs_residues_submit(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off,
+                                  const uint16_t* d_class, uint32_t n, int k, uint64_t slots, uint32_t heavy_df,
+                                  uint32_t min_shared, int require_class_diff, uint32_t* d_p, uint32_t* d_q,
+                                  uint32_t* d_w, uint64_t cap, void* stream, uint64_t* ticket) {
+    if (!ws || !ticket) return KMP_EINVAL;
+    if (!ws->async) ws->async = std::make_shared<AsyncState>();
+    auto* as = static_cast<AsyncState*>(ws->async.get());
+    const int s = !as->sub[0].used ? 0 : !as->sub[1].used ? 1 : -1;
+    if (s < 0) return KMP_ESTATE;  // two outstanding: wait for one first
+    if (!ws->hrb_slot[s])
+        PG(hipHostMalloc((void**)&ws->hrb_slot[s], kRbWords * sizeof(unsigned long long), hipHostMallocCoherent));
+    if (!ws->done_ev[s]) PG(hipEventCreateWithFlags(&ws->done_ev[s], hipEventDisableTiming));
+    if (ws->timing)
+        for (auto& e : ws->evs[s])
+            if (!e) PG(hipEventCreate(&e));
+    AsyncSub& a = as->sub[s];
+    a = AsyncSub{};
+    a.d_res = d_res, a.d_res_off = d_res_off, a.d_class = d_class, a.n = n, a.k = k, a.slots = slots;
+    a.heavy_df = heavy_df, a.min_shared = min_shared, a.require_class_diff = require_class_diff;
+    a.d_p = d_p, a.d_q = d_q, a.d_w = d_w, a.cap = cap, a.stream = stream;
+    // the call on the slot's read-back and stage events; its step graph is the slot's own
+    unsigned long long* const rb_sync = ws->hrb;
+    ws->hrb = ws->hrb_slot[s];
+    ws->evp = ws->evs[s];
+    ws->async_slot = s;
+    ws->async_launched = false;
+    a.rc = residues_impl(ws, d_res, d_res_off, d_class, n, k, slots, heavy_df, min_shared, require_class_diff, false, 0,
+                         n, d_p, d_q, d_w, cap, &a.n_edges, &a.stats, stream);
+    a.launched = ws->async_launched;
+    a.g = ws->async_geom;
+    ws->hrb = rb_sync;
+    ws->evp = ws->ev;
+    ws->async_slot = -1;
+    ws->async_launched = false;
+    if (!a.launched && a.rc != KMP_OK && a.rc != KMP_EOVERFLOW) return a.rc;  // (the slot stays free)
+    a.used = true;
+    a.ticket = as->next++;
+    *ticket = a.ticket;
+    return KMP_OK;
+}
+
+int kmp_postings_wait(kmp_postings* ws, uint64_t ticket, uint64_t* n_edges, kmp_postings_stats* stats) {
+    if (!ws || !n_edges || !ws->async) return KMP_EINVAL;
+    auto* as = static_cast<AsyncState*>(ws->async.get());
+    int s = -1;
+    for (int i = 0; i < 2; ++i)
+        if (as->sub[i].used && as->sub[i].ticket == ticket) s = i;
+    if (s < 0) return KMP_EINVAL;
+    AsyncSub& a = as->sub[s];
+    a.used = false;
+    if (!a.launched) {  // finished at submit
+        *n_edges = a.n_edges;
+        if (stats) *stats = a.stats;
+        return a.rc;
+    }
+    PG(hipEventSynchronize(ws->done_ev[s]));
+    const unsigned long long* rb = ws->hrb_slot[s];
+    if (!fused_clean(ws, a.g, rb)) {
+        // the read-back asks for more (a rerun with a grown capacity, a fallback): the stream
+        // drained (the other submission too, so nothing in flight uses a buffer that may grow),
+        // then this step again, synchronously
+        PG(hipStreamSynchronize(as_stream(a.stream)));
+        return residues_impl(ws, a.d_res, a.d_res_off, a.d_class, a.n, a.k, a.slots, a.heavy_df, a.min_shared,
+                             a.require_class_diff, false, 0, a.n, a.d_p, a.d_q, a.d_w, a.cap, n_edges, stats, a.stream);
+    }
+    if (stats) *stats = kmp_postings_stats{};
+    // the call's configuration as run_postings built it (what fused_finish reads: cap, the front key)
+    const uint32_t hd = std::max(2u, a.heavy_df);
+    const std::vector<unsigned long long> front_key = {a.n, (unsigned long long)a.k, a.slots, hd,
+                                                       (unsigned long long)a.require_class_diff, 1,
+                                                       (uintptr_t)a.d_res, (uintptr_t)a.d_res_off, (uintptr_t)a.d_class};
+    StepCfg c{};
+    c.n = a.n;
+    c.slots = a.slots;
+    c.cap = a.cap;
+    c.front_key = &front_key;
+    const int rc = fused_finish(ws, c, a.g, rb, n_edges, stats);
+    ws->last_bucketed = true;
+    if (ws->timing && stats)
+        for (int i = 0; i < KMP_POSTINGS_STAGES; ++i) {
+            float ms = 0.f;
+            stats->stage_ms[i] = hipEventElapsedTime(&ms, ws->evs[s][i], ws->evs[s][i + 1]) == hipSuccess ? ms : -1.f;
+        }
+    (void)hipGetLastError();
+    return rc;
+}
+
 int kmp_dev_pairs_rows(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_res_off, const uint16_t* d_class,
                        uint32_t n, int k, uint64_t slots, uint32_t heavy_df, uint32_t min_shared,
                        int require_class_diff, uint32_t row_lo, uint32_t row_hi, uint32_t* d_p, uint32_t* d_q,
@@ -497,9 +613,11 @@ static int split_expand_impl(kmp_postings* ws, const SplitSrc& src, uint32_t n, 
             // every attempt grew the spill regions: no keys are sent and the flags ask every rank for
             // a rerun, so the ranks stay in lockstep through the collectives (an error returned here
             // on one rank alone would leave the others waiting in the all-to-all); the grown regions
-            // are this rank's own and stay for the rerun
+            // are this rank's own and stay for the rerun.  The flags are this step's alone, RERUN
+            // (with the sharded start too: d_flags still held the last step's reduced flags, and the
+            // keys phase's own flags sit in its cursor words, which the rerun's keys phase clears)
             PG(hipMemsetAsync(d_send, 0xFF, (size_t)parts * cap * sizeof(unsigned long long), st));
-            if (!recv) PG(hipMemsetAsync(d_flags, 0, KMP_SPLIT_FLAGS * sizeof(uint32_t), st));
+            PG(hipMemsetAsync(d_flags, 0, KMP_SPLIT_FLAGS * sizeof(uint32_t), st));
             PG(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_flags + KMP_SPLIT_RERUN), 1, 1, st));
             PG(hipMemsetAsync(d_stats, 0, 8 * sizeof(unsigned long long), st));
         }

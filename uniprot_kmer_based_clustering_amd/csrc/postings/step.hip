@@ -721,6 +721,79 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
     return KMP_OK;
 }
 
+// A captured sequence is replayed only if it holds kernel (and event) nodes alone.  Memset nodes
+// replay wrongly on this stack: round 5's captured hipMemsetAsync of the split's send buffer was
+// right on the capturing launch and filled the buffer with pointer-sized values on the first replay,
+// and r05aq's fault (an aperture violation in rocPRIM's onesweep on the replay of a captured
+// postings front, test_frequent_kmers_heavy_path[12000]) is the same input: rocPRIM's radix sort
+// issues two hipMemsetAsync per call (its digit offsets and look-back states), and the captured
+// front held them.  Every fill of this library's own captured sequences is a kernel; a sequence with
+// a rocPRIM sort in it (the postings entry's front) runs plain instead.
+bool graph_replayable(hipGraph_t gr) {
+    size_t n = 0;
+    if (hipGraphGetNodes(gr, nullptr, &n) != hipSuccess) return false;
+    std::vector<hipGraphNode_t> nodes(n);
+    if (n && hipGraphGetNodes(gr, nodes.data(), &n) != hipSuccess) return false;
+    for (hipGraphNode_t x : nodes) {
+        hipGraphNodeType t;
+        if (hipGraphNodeGetType(x, &t) != hipSuccess) return false;
+        if (t != hipGraphNodeTypeKernel && t != hipGraphNodeTypeEventRecord && t != hipGraphNodeTypeEmpty) {
+            if (getenv("KMP_DEBUG")) fprintf(stderr, "kmp: captured sequence holds a node of type %d: run plain\n", (int)t);
+            return false;
+        }
+    }
+    return true;
+}
+
+// the kernel launches of a graph, in node order: function, grid, block, shared memory
+std::vector<std::vector<unsigned long long>> graph_launches(hipGraph_t gr) {
+    std::vector<std::vector<unsigned long long>> out;
+    size_t n = 0;
+    if (hipGraphGetNodes(gr, nullptr, &n) != hipSuccess) return out;
+    std::vector<hipGraphNode_t> nodes(n);
+    if (n && hipGraphGetNodes(gr, nodes.data(), &n) != hipSuccess) return out;
+    for (hipGraphNode_t x : nodes) {
+        hipGraphNodeType t;
+        if (hipGraphNodeGetType(x, &t) != hipSuccess || t != hipGraphNodeTypeKernel) continue;
+        hipKernelNodeParams kp{};
+        if (hipGraphKernelNodeGetParams(x, &kp) != hipSuccess) continue;
+        out.push_back({(uintptr_t)kp.func, kp.gridDim.x, kp.gridDim.y, kp.gridDim.z, kp.blockDim.x, kp.blockDim.y,
+                       kp.blockDim.z, kp.sharedMemBytes});
+    }
+    return out;
+}
+
+// KMP_GRAPH_VERIFY=1: before a replay, the sequence is captured again (not launched) and its launches —
+// function, grid, block, shared memory — must equal the replayed graph's, in order: a launch input
+// the graph key missed (a grid from a read-back, a capacity) fails the call loudly instead of
+// replaying stale launches.  Returns false on a mismatch.
+template <class Enqueue>
+bool graph_verify(kmp_postings* ws, const std::vector<std::vector<unsigned long long>>& want, Enqueue& enqueue) {
+    if (!ws->cst) return true;
+    hipGraph_t gr = nullptr;
+    if (hipStreamBeginCapture(ws->cst, hipStreamCaptureModeRelaxed) != hipSuccess) {
+        (void)hipGetLastError();
+        return true;
+    }
+    const int rc = enqueue(ws->cst);
+    if (hipStreamEndCapture(ws->cst, &gr) != hipSuccess || !gr) {
+        (void)hipGetLastError();
+        return rc == KMP_OK;
+    }
+    const auto got = graph_launches(gr);
+    (void)hipGraphDestroy(gr);
+    if (rc == KMP_OK && got == want) return true;
+    fprintf(stderr, "kmp: graph replay check failed: %zu launches captured now, %zu in the replayed graph\n",
+            got.size(), want.size());
+    for (size_t i = 0; i < std::max(got.size(), want.size()); ++i)
+        if (i >= got.size() || i >= want.size() || got[i] != want[i])
+            fprintf(stderr, "kmp:   launch %zu: now grid %llu x %llu block %llu, graph grid %llu x %llu block %llu\n", i,
+                    i < got.size() ? got[i][1] : 0ull, i < got.size() ? got[i][2] : 0ull,
+                    i < got.size() ? got[i][4] : 0ull, i < want.size() ? want[i][1] : 0ull,
+                    i < want.size() ? want[i][2] : 0ull, i < want.size() ? want[i][4] : 0ull);
+    return false;
+}
+
 // enqueue the fused step: replay the captured graph when the shape matches the capture, capture
 // it when the shape repeats a plain run (buffers sized), else run plain
 // enqueue(s) on `st` as a HIP graph of `slot`: replayed when key matches its capture, captured when
@@ -740,6 +813,7 @@ int slot_launch(kmp_postings* ws, kmp_postings::GraphSlot& slot, std::vector<uns
                                                   : "capture");
     if (!ws->graph_on) return enqueue(st);
     if (slot.gexec && slot.key == key) {
+        if (getenv("KMP_GRAPH_VERIFY") && !graph_verify(ws, slot.launches, enqueue)) return KMP_EDEVICE;
         PG(hipGraphLaunch(slot.gexec, st));
         ++ws->graph_replays;
         return KMP_OK;
@@ -751,6 +825,7 @@ int slot_launch(kmp_postings* ws, kmp_postings::GraphSlot& slot, std::vector<uns
     if (slot.gexec) (void)hipGraphExecDestroy(slot.gexec);
     slot.gexec = nullptr;
     slot.key.clear();
+    slot.launches.clear();
     if (!ws->cst && hipStreamCreateWithFlags(&ws->cst, hipStreamNonBlocking) != hipSuccess) ws->cst = nullptr;
     hipGraph_t gr = nullptr;
     if (!ws->cst || hipStreamBeginCapture(ws->cst, hipStreamCaptureModeRelaxed) != hipSuccess) {
@@ -761,8 +836,12 @@ int slot_launch(kmp_postings* ws, kmp_postings::GraphSlot& slot, std::vector<uns
     int rc = enqueue(ws->cst);
     hipError_t e = hipStreamEndCapture(ws->cst, &gr);
     hipGraphExec_t ex = nullptr;
-    if (rc == KMP_OK && e == hipSuccess && gr && gen == g_grow_gen.load()) e = hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0);
-    else if (e == hipSuccess) e = hipErrorUnknown;
+    if (rc == KMP_OK && e == hipSuccess && gr && gen == g_grow_gen.load() && graph_replayable(gr)) {
+        slot.launches = graph_launches(gr);
+        e = hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0);
+    } else if (e == hipSuccess) {
+        e = hipErrorUnknown;
+    }
     if (gr) (void)hipGraphDestroy(gr);
     if (e != hipSuccess || !ex) {  // not capturable this time: plain
         (void)hipGetLastError();
@@ -785,8 +864,32 @@ int fused_launch(kmp_postings* ws, MakeKeys& make_keys, const std::vector<unsign
         }
         return rc;
     };
+    if (ws->async_slot >= 0) {
+        // a submission: its slot's graph (the key holds the slot's read-back, so the two slots'
+        // graphs differ); replayed without a host wait when it matches, else plain or captured and
+        // finished synchronously by the caller
+        kmp_postings::GraphSlot& gs = ws->fg[ws->async_slot];
+        std::vector<unsigned long long> kg = key;
+        kg.push_back((uintptr_t)ws->hrb);
+        std::vector<unsigned long long> kr = kg;
+        kr.push_back(g_grow_gen.load());  // (slot_launch's own last word)
+        if (ws->graph_on && gs.gexec && gs.key == kr) {
+            if (getenv("KMP_GRAPH_VERIFY") && !graph_verify(ws, gs.launches, enqueue)) return KMP_EDEVICE;
+            PG(hipGraphLaunch(gs.gexec, st));
+            ++ws->graph_replays;
+            PG(hipEventRecord(ws->done_ev[ws->async_slot], st));
+            ws->async_launched = true;
+            ws->async_geom = g;
+            return KMP_OK;
+        }
+        // a shape that already finished clean (ok_key, either slot or a synchronous call) is captured
+        // on the slot's first use, so both slots replay from the third submission of a shape on
+        if (ws->ok_key == key) gs.seen = kr;
+        return slot_launch(ws, gs, kg, enqueue, st);
+    }
     if (!ws->graph_on) return enqueue(st);
     if (ws->gexec && ws->gkey == key) {
+        if (getenv("KMP_GRAPH_VERIFY") && !graph_verify(ws, ws->glaunches, enqueue)) return KMP_EDEVICE;
         PG(hipGraphLaunch(ws->gexec, st));
         ++ws->graph_replays;
         return KMP_OK;
@@ -813,10 +916,12 @@ int fused_launch(kmp_postings* ws, MakeKeys& make_keys, const std::vector<unsign
     int rc = enqueue(ws->cst);
     hipError_t e = hipStreamEndCapture(ws->cst, &gr);
     hipGraphExec_t ex = nullptr;
-    if (rc == KMP_OK && e == hipSuccess && gr && gen == g_grow_gen.load())
+    if (rc == KMP_OK && e == hipSuccess && gr && gen == g_grow_gen.load() && graph_replayable(gr)) {
+        ws->glaunches = graph_launches(gr);
         e = hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0);
-    else if (e == hipSuccess)
+    } else if (e == hipSuccess) {
         e = hipErrorUnknown;
+    }
     if (gr) (void)hipGraphDestroy(gr);
     if (e != hipSuccess || !ex) {  // capture not usable: plain from now on
         (void)hipGetLastError();
@@ -845,6 +950,70 @@ void sum_stats(const unsigned long long* rb, unsigned long long* acc, unsigned l
         *spill_total += rb[kRbSpill + sh];
     }
 }
+
+// The fused step's read-back asks for nothing more: no fallback, rerun, learned capacity, overflow
+// finish or error (then fused_finish completes the call; a submission checks this at its wait)
+bool fused_clean(const kmp_postings* ws, const PtGeom& g, const unsigned long long* rb) {
+    unsigned long long acc[kStN], most, n_inc, spill_most, spill_total;
+    sum_stats(rb, acc, &most, &n_inc, &spill_most, &spill_total);
+    return !rb[kRbFlagClass] && !(rb[kRbList] && ws->large_used == 0) && !(rb[kRbFlagCur] && ws->cur_used) &&
+           !rb[kRbFlagBin] && spill_most <= ws->spill_cap && !spill_total && most <= ws->shard_cap && !rb[kRbFast] &&
+           !rb[kRbRange] && !(rb[kRbOvf] && !pt_rowhist_ok(g));
+}
+
+// a clean fused step (fused_clean): what it teaches the next call, its statistics and edge count
+int fused_finish(kmp_postings* ws, const StepCfg& c, const PtGeom& g, const unsigned long long* rb, uint64_t* n_edges,
+                 kmp_postings_stats* stats) {
+    unsigned long long acc[kStN], most, n_inc, spill_most, spill_total;
+    sum_stats(rb, acc, &most, &n_inc, &spill_most, &spill_total);
+    ws->pt_inc = n_inc;  // sizes the next call's row blocks
+    ws->last_fast = pt_fast(ws, g);
+    ws->vreg_tries = 0;  // a call without a region overflow
+    {  // the large-bucket grid of the next call: twice the listed buckets, 64 .. kBucketLargeGrid;
+       // none listed: not launched (an idle 64-workgroup launch cost ~5 us of the config-3 step)
+        uint32_t lg = rb[kRbList] ? 64u : 0u;
+        while (lg && lg < kBucketLargeGrid && lg < 2 * rb[kRbList]) lg *= 2;
+        ws->large_grid = lg;
+    }
+    const uint64_t ne = rb[kRbRuns];
+    ws->last_ovf = (uint32_t)rb[kRbOvf];
+    ws->shard_cap = most + most / 64 + 256;  // learned for the next call
+    fill_stats(stats, acc);
+    if (stats) {
+        stats->incidences = n_inc;
+        stats->pairs = ne;
+    }
+    ws->last_heavy = ws->heavy_ready;
+    ws->last_fused = true;
+    if (c.front_key) {
+        ws->front_ok = true;
+        ws->front_key = *c.front_key;
+    }
+    *n_edges = ne;
+    return ne > c.cap ? KMP_EOVERFLOW : KMP_OK;
+}
+
+// KMP_HOSTPROF=1 (diagnostic): host time of the fused step's phases, averaged over 50 calls on stderr
+struct HostProf {
+    bool on = getenv("KMP_HOSTPROF") != nullptr;
+    std::chrono::steady_clock::time_point t[5];
+    double acc[4] = {0, 0, 0, 0};
+    int n = 0;
+    void mark(int i) {
+        if (on) t[i] = std::chrono::steady_clock::now();
+    }
+    void done() {
+        if (!on) return;
+        for (int i = 0; i < 4; ++i) acc[i] += std::chrono::duration<double, std::micro>(t[i + 1] - t[i]).count();
+        if (++n == 50) {
+            fprintf(stderr, "kmp-hostprof: us per call: prep %.1f launch %.1f sync %.1f finish %.1f\n", acc[0] / n,
+                    acc[1] / n, acc[2] / n, acc[3] / n);
+            n = 0;
+            for (double& a : acc) a = 0;
+        }
+    }
+};
+HostProf g_hprof;
 
 // One call: the fused step, or the split step when the batch spills.  *fallback: a class id
 // wider than the key's class field (the caller reruns on the flat layout).
@@ -898,14 +1067,39 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
             key.push_back(ws->fast_tail);
             key.push_back(ws->large_grid);
             key.push_back(ws->vreg_on ? ws->vreg_total + 1 : 0);
+            key.push_back(ws->bp_J_min);  // (the counting level 2's tile budget, learned from a bin overflow)
+            g_hprof.mark(1);
+            ws->cur_key = key;
             int rc = fused_launch(ws, make_keys, key, c, g, st);
-            key.resize(key.size() - 9);
+            g_hprof.mark(2);
+            key.resize(key.size() - 10);
             if (rc != KMP_OK) return rc;
+            if (ws->async_launched) return KMP_OK;  // a submission in flight: kmp_postings_wait checks it
             PG(hipStreamSynchronize(st));
+            g_hprof.mark(3);
         } else {
-            int rc = enqueue_front(ws, make_keys, c, !ws->heavy_ready, st, !reuse);
+            // the split step's front (+ its read-back) as a graph of its own (slot_launch: replayed from
+            // the third call of an unchanged key): config 1's ~7 front launches without host gaps.  The
+            // key holds every host input of the sequence — the fused key's, the spill / keys switches
+            // and the spill-all inputs; a postings entry's front holds rocPRIM's memset nodes and runs
+            // plain (graph_replayable)
+            const bool spill = !ws->heavy_ready, keys = !reuse;
+            auto front = [&](hipStream_t s) -> int {
+                int rc = enqueue_front(ws, make_keys, c, spill, s, keys);
+                if (rc == KMP_OK) {
+                    step_pack_kernel<<<1, 256, 0, s>>>(ws->bstats.p, ws->flags.p, nullptr, ws->hrb);
+                    if (hipGetLastError() != hipSuccess) rc = KMP_EDEVICE;
+                }
+                return rc;
+            };
+            std::vector<unsigned long long> fk = key;
+            fk.insert(fk.end(), {ws->shard_cap, ws->spill_cap, (unsigned long long)ws->timing, (unsigned long long)ws->cur_on,
+                                 ws->large_grid, ws->vreg_on ? ws->vreg_total + 1 : 0, ws->bp_J_min,
+                                 (unsigned long long)spill, (unsigned long long)keys, (unsigned long long)c.expand_only,
+                                 (uintptr_t)ws->hrb, (unsigned long long)ws->flat_heavy,
+                                 (unsigned long long)ws->spill_all_on, (unsigned long long)ws->reuse});
+            int rc = slot_launch(ws, ws->front_g, fk, front, st);
             if (rc != KMP_OK) return rc;
-            step_pack_kernel<<<1, 256, 0, st>>>(ws->bstats.p, ws->flags.p, nullptr, ws->hrb);
             PG(hipStreamSynchronize(st));
         }
         if (rb[kRbFlagClass]) {
@@ -1008,6 +1202,10 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
             rc = enqueue_tail(ws, c, g, st);
             if (rc != KMP_OK) return rc;
             PG(hipStreamSynchronize(st));
+        }
+        if (!split && !rerun && fused_clean(ws, g, rb)) {
+            ws->ok_key = ws->cur_key;
+            return fused_finish(ws, c, g, rb, n_edges, stats);
         }
         if (rb[kRbFast]) {  // a fast-tail row block passed its region: fewer rows per block, or the counting tail
             if (debug)
@@ -1328,11 +1526,11 @@ int tail(kmp_postings* ws, const unsigned long long* in, unsigned long long n_in
 }
 
 void finish_timing(kmp_postings* ws, kmp_postings_stats* stats, hipStream_t st) {
-    if (!ws->timing || !stats) return;
+    if (!ws->timing || !stats || ws->async_launched) return;
     (void)hipStreamSynchronize(st);
     for (int s = 0; s < KMP_POSTINGS_STAGES; ++s) {
         float ms = 0.f;
-        stats->stage_ms[s] = hipEventElapsedTime(&ms, ws->ev[s], ws->ev[s + 1]) == hipSuccess ? ms : -1.f;
+        stats->stage_ms[s] = hipEventElapsedTime(&ms, ws->evp[s], ws->evp[s + 1]) == hipSuccess ? ms : -1.f;
     }
     (void)hipGetLastError();  // a stage the call did not run (never recorded) must not poison the next launch check
 }
@@ -1368,6 +1566,7 @@ int run_postings(kmp_postings* ws, MakeKeys make_keys, const std::vector<unsigne
                  uint32_t* d_w, uint64_t cap, uint64_t* n_edges, kmp_postings_stats* stats, hipStream_t st,
                  unsigned sb = 0, uint32_t sor = 0, uint32_t* d_s = nullptr, uint32_t* d_w1 = nullptr,
                  uint64_t* n_inc_out = nullptr) {
+    g_hprof.mark(0);
     if (heavy_df < 2) heavy_df = 2;
     if (min_shared < 1) min_shared = 1;
     ws->bin_lo = ws->bin_hi = 0;  // every bucket (the k-mer split restricts its own calls)
@@ -1416,6 +1615,8 @@ int run_postings(kmp_postings* ws, MakeKeys make_keys, const std::vector<unsigne
         if (!fallback) {
             ws->last_bucketed = true;
             if (rc == KMP_OK) finish_timing(ws, stats, st);
+            g_hprof.mark(4);
+            if (rc == KMP_OK && ws->last_fused && !ws->async_launched) g_hprof.done();
             return rc;
         }
     }

@@ -131,24 +131,43 @@ struct kmp_postings {
     struct GraphSlot {  // one captured sequence: its executable and the shape it was captured for
         hipGraphExec_t gexec = nullptr;
         std::vector<unsigned long long> key, seen;
+        std::vector<std::vector<unsigned long long>> launches;  // its kernel launches (KMP_DEBUG replay check)
         void reset() {
             if (gexec) (void)hipGraphExecDestroy(gexec);
             gexec = nullptr;
             key.clear();
             seen.clear();
+            launches.clear();
         }
     } split_g[3];  // the k-mer split's phases (expand or group, edges, keys)
+    // pipelined submissions (kmp_dev_pairs_residues_submit / kmp_postings_wait): a submission whose
+    // step graph replays goes out without a host wait; it has a slot of its own (two), with its own
+    // read-back, stage events, completion event and captured graph, so the next submission can be
+    // queued behind it before its read-back is checked
+    GraphSlot fg[2];
+    GraphSlot front_g;  // the split step's front + read-back (run_step)
+    unsigned long long* hrb_slot[2] = {nullptr, nullptr};
+    hipEvent_t evs[2][KMP_POSTINGS_STAGES + 1] = {};
+    hipEvent_t done_ev[2] = {};
+    int async_slot = -1;          // the slot of the submission being enqueued (-1: a synchronous call)
+    bool async_launched = false;  // ... its step went out without a host wait (async_geom: its tail geometry)
+    PtGeom async_geom{};
+    std::shared_ptr<void> async;  // the submissions (AsyncState, api.hip)
+    // the fused step's graph key of this call, and of the last call that finished clean
+    std::vector<unsigned long long> cur_key, ok_key;
     hipGraphExec_t gexec = nullptr;
     hipStream_t cst = nullptr;  // capture stream
     hipStream_t side = nullptr;   // side_fork: the heavy path's large segment sorts
     hipEvent_t sev[2] = {};
 
     std::vector<unsigned long long> gkey, gkey_seen;
+    std::vector<std::vector<unsigned long long>> glaunches;  // the fused graph's kernel launches (KMP_DEBUG check)
     uint64_t graph_replays = 0;
     uint64_t reruns = 0;  // calls (or a split call's phases) run again with a grown capacity
     // read-back of a step (kRb* layout), written by the pack kernel into coherent pinned memory
     unsigned long long* hrb = nullptr;
     hipEvent_t ev[KMP_POSTINGS_STAGES + 1] = {};
+    hipEvent_t* evp = ev;  // the stage events a call's marks record into (a submission: its slot's)
     hipEvent_t mev[4] = {};  // kmp_dev_pairs_rows_multi: start, first k expanded, second k, tail done
     const uint32_t* pt_zero_p = nullptr;  // the pt allocation whose totals T were cleared
     size_t pt_zero_n = 0;
@@ -167,6 +186,14 @@ struct kmp_postings {
         for (auto& e : mev)
             if (e) (void)hipEventDestroy(e);
         if (hrb) (void)hipHostFree(hrb);
+        for (int i = 0; i < 2; ++i) {
+            if (hrb_slot[i]) (void)hipHostFree(hrb_slot[i]);
+            for (auto& e : evs[i])
+                if (e) (void)hipEventDestroy(e);
+            if (done_ev[i]) (void)hipEventDestroy(done_ev[i]);
+            fg[i].reset();
+        }
+        front_g.reset();
         if (gexec) (void)hipGraphExecDestroy(gexec);
         for (auto& g : split_g) g.reset();
         if (cst) (void)hipStreamDestroy(cst);
@@ -175,7 +202,7 @@ struct kmp_postings {
             if (e) (void)hipEventDestroy(e);
     }
     void mark(int stage, hipStream_t st) {
-        if (timing) (void)hipEventRecord(ev[stage], st);
+        if (timing) (void)hipEventRecord(evp[stage], st);
     }
 };
 

@@ -455,6 +455,37 @@ class DevicePipeline(_SplitEdges):
             return self.n_edges
         raise RuntimeError("edge count unstable across reruns")
 
+    def submit(self, min_shared: int = 1, require_class_diff: bool = True, heavy_df: int = 0xFFFFFFFF) -> int:
+        """kmp_dev_pairs_residues_submit: the fused residue step enqueued on the current stream (no host
+        wait once its graph replays, so the next submission queues behind it); returns the ticket
+        for wait().  At most two outstanding; both write ep/eq/ew (the later overwrites the earlier)."""
+        ws = self._workspace()
+        stream = torch.cuda.current_stream().cuda_stream
+        key = (self.ep.data_ptr(), self.edge_cap, stream, heavy_df, min_shared, require_class_diff)
+        cached = getattr(self, "_sub_call", None)
+        if cached is None or cached[0] != key:
+            t = C.c_uint64()
+            slots = int(lib().kmp_set_capacity(self.n, self.total))
+            args = (ws, _p(self.res), _p(self.off), _p(self.cls), self.n, self.k, slots, heavy_df, min_shared,
+                    int(require_class_diff), _p(self.ep), _p(self.eq), _p(self.ew), self.edge_cap,
+                    C.c_void_p(stream), C.byref(t))
+            cached = self._sub_call = (key, args, t, (min_shared, require_class_diff, heavy_df))
+        check(lib().kmp_dev_pairs_residues_submit(*cached[1]), "kmp_dev_pairs_residues_submit")
+        return cached[2].value
+
+    def wait(self, ticket: int) -> int:
+        """kmp_postings_wait: the submitted step's edge count (its read-back checked; a step that asked
+        for a rerun ran again at the wait) and its statistics in postings_stats."""
+        ne = C.c_uint64()
+        st = lib().kmp_postings_wait(self._workspace(), ticket, C.byref(ne), C.byref(self.postings_stats))
+        if st == _lib.KMP_EOVERFLOW:  # the edge arrays were short: grown, and the step run again
+            self._alloc_edges(ne.value + ne.value // 8 + 1024)
+            ms, rcd, hd = self._sub_call[3]
+            return self.postings(ms, rcd, hd, from_residues=True)
+        check(st, "kmp_postings_wait")
+        self.n_edges = ne.value
+        return self.n_edges
+
     def step(self, min_shared: int = 1, require_class_diff: bool = True, engine: str = "residues") -> int:
         """The whole single-GPU path, packed residues in HBM -> canonical edges in HBM.
         residues: windows -> sort/expand/reduce (kmp_dev_pairs_residues, fused);
