@@ -421,11 +421,13 @@ def main(argv=None, dist_mod=None):
         return pipe.step(engine=args.engine)
 
     stage_sum = None
-    # (BENCH_NO_STAGE_TIMING=1: diagnostic only — the step without its stage events; the line then
-    # carries no measured roofline)
+    # stage times (the roofline): HIP events on the library's stream between its stages, measured in
+    # an untimed pass after the timed steps, with graphs off — event-record nodes of a replayed HIP
+    # graph keep the times of the graph's first launch on this stack (tools/pipe_probe.py: identical
+    # stage times on every replay), so the timed steps carry no events.  BENCH_NO_STAGE_TIMING=1:
+    # no stage pass (the line then carries no measured roofline)
     stage_timing = postings and world == 1 and os.environ.get("BENCH_NO_STAGE_TIMING") != "1"
-    if stage_timing:
-        pipe.set_stage_timing(True)  # before the warm-up: the timed steps replay the same graph
+    stage_steps = 10
     # one GPU, residues engine: the steps go out as pipelined submissions — step i + 1 is queued
     # behind step i, then step i is waited for and its read-back checked (a step that asks for a rerun
     # runs again at its wait) — so the device does not idle between steps while the host checks the
@@ -456,22 +458,26 @@ def main(argv=None, dist_mod=None):
                 record()
         return n
 
-    def record():
-        nonlocal stage_sum
-        if stage_timing:
-            st = np.array(pipe.postings_stats.stage_ms[:], dtype=np.float64)
-            stage_sum = st if stage_sum is None else stage_sum + st
-
     run_steps(args.warmup)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    n_edges = run_steps(args.steps, record)
+    n_edges = run_steps(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    if stage_timing:  # untimed: the stage times, plain launches with events between the stages
+        pipe.set_graph(False)
+        pipe.set_stage_timing(True)
+        pipe.step(engine=args.engine)
+        for _ in range(stage_steps):
+            pipe.step(engine=args.engine)
+            st = np.array(pipe.postings_stats.stage_ms[:], dtype=np.float64)
+            stage_sum = st if stage_sum is None else stage_sum + st
+        pipe.set_stage_timing(False)
+        pipe.set_graph(True)
     sync_ms = None
     if pipelined:  # untimed: the synchronous call's latency per step, for the record
         for _ in range(3):
@@ -482,8 +488,6 @@ def main(argv=None, dist_mod=None):
             pipe.step(engine=args.engine)
         torch.cuda.synchronize()
         sync_ms = (time.perf_counter() - s0) / 10 * 1e3
-    if stage_timing:
-        pipe.set_stage_timing(False)
     rank_info = None
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
@@ -604,7 +608,7 @@ def main(argv=None, dist_mod=None):
             n_win = int(np.maximum(lens - k + 1, 0).sum())  # windows = keys of the residue path
             byts = stage_bytes(int(proteins.offsets[-1]), ps["incidences"], n_edges, ps["pairs"], n_win, tail)
             names = STAGE_NAMES
-            stage_ms = dict(zip(names, (stage_sum / args.steps).tolist()))
+            stage_ms = dict(zip(names, (stage_sum / stage_steps).tolist()))
             stages = {s: {"ms": stage_ms[s], "alg_bytes": byts[s],
                           "GBs": byts[s] / (stage_ms[s] * 1e-3) / 1e9 if stage_ms[s] > 1e-4 else None}
                       for s in stage_ms}
@@ -619,7 +623,10 @@ def main(argv=None, dist_mod=None):
                                "kernel_ms": stage_ms[dom], "alg_bytes_per_launch": byts[dom],
                                "layout": pipe.last_layout(), "tail": tail, "stages": stages,
                                "step_alg_bytes": sum(byts.values()),
-                               "step_GBs": sum(byts.values()) / (ms * 1e-3) / 1e9}
+                               "step_GBs": sum(byts.values()) / (ms * 1e-3) / 1e9,
+                               "stage_timing": f"HIP events between the stages, {stage_steps} untimed steps with "
+                                               "plain launches after the timed ones (graph event nodes keep "
+                                               "their first launch's times on this stack)"}
             # SURVEY.md §8d model: 4·(S_p + S_q) bytes per pair, i.e. a merge-intersection of every
             # pair's sets; the postings engine never touches non-sharing pairs, so this is an
             # effective figure far above the HBM peak

@@ -79,13 +79,14 @@ def test_pipelined_limits_and_overflow(oracle_mod):
     _check(pipe, p, q, w)
 
 
-def test_split_front_graph_replay_verified(oracle_mod, monkeypatch):
-    """The split step's front (frequent k-mers: a bucket above every LDS capacity and a level-2 bin
-    above its tile budget, so the first calls rerun with learned sizes) is captured and replayed as
-    a HIP graph; with KMP_GRAPH_VERIFY every replay is first re-captured and its launches (function,
-    grid, block, shared memory) compared with the graph's — a launch input missing from the key
-    fails the call.  The postings entry's front holds rocPRIM's memset nodes and is never replayed
-    (graph_replayable).  Every call bit-exact."""
+def test_graph_replays_verified(oracle_mod, monkeypatch):
+    """With KMP_GRAPH_VERIFY every graph replay is first re-captured and its launches (function,
+    grid, block, shared memory) compared with the graph's — a launch input missing from the key fails
+    the call.  A batch of frequent k-mers (a bucket above every LDS capacity and a level-2 bin above
+    its tile budget, so the first calls rerun with learned sizes: the split step and its heavy path)
+    on both entries, then the fused step of a plain batch (replayed); the postings entry's front
+    holds rocPRIM's memset nodes and is never captured for replay (graph_replayable).  Every call
+    bit-exact."""
     import torch
     from common import make_batch
     from uniprot_kmer_based_clustering_amd.device import DevicePipeline
@@ -98,11 +99,20 @@ def test_split_front_graph_replay_verified(oracle_mod, monkeypatch):
     p, q, w = oracle_mod.Oracle(res, off, cls, k=7, threads=8).pairs()
     pipe = DevicePipeline(K.Proteins(res, off, cls), 7, "cuda:0")
     for eng in ("residues", "postings"):
-        r0 = pipe.graph_replays()
-        for _ in range(5):
+        for _ in range(4):
             assert pipe.step(engine=eng) == len(p)
             torch.cuda.synchronize()
             assert pipe.last_heavy()
             _check(pipe, p, q, w)
+    b = K.synth(20000, 21)
+    p, q, w = oracle_mod.Oracle(b.residues, b.offsets, b.class_id, k=7, threads=8).pairs()
+    pipe = DevicePipeline(b, 7, "cuda:0")
+    for eng in ("residues", "postings"):
+        r0 = pipe.graph_replays()
+        for _ in range(5):
+            assert pipe.step(engine=eng) == len(p)
+            _check(pipe, p, q, w)
         if eng == "residues":
-            assert pipe.graph_replays() - r0 >= 2  # the front replayed (verified)
+            assert pipe.graph_replays() - r0 >= 2  # replayed (each one verified first)
+        else:
+            assert pipe.graph_replays() == r0  # rocPRIM's memsets: plain launches

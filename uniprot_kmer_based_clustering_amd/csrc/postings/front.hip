@@ -86,16 +86,24 @@ hipError_t bp_level1(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_r
         const uint32_t grid = nown >= dg.nb1 ? G : std::min<uint32_t>(G, (uint32_t)per_cu * device_cus());
         if (nown) {
             const uint4* desc = reinterpret_cast<const uint4*>(ws->chunk_desc.p);
-            if (grid < G)
-                bp_scatter1p_kernel<KMP_L1_THREADS, false, true><<<grid, KMP_L1_THREADS, 0, st>>>(
-                    d_res, d_res_off, d_class, k, n, slots, G, desc, lay, dg, pw21, dlo, dhi, H1, ws->keys.p,
+            if (nown >= dg.nb1) {
+                // every bin (one GPU): the run table written transposed by the level-1 workgroups
+                // themselves (XCD-aware chunk order; 8 * ceil(G / 8) workgroups, the few past G return)
+                bp_scatter1p_kernel<KMP_L1_THREADS, false, false, true><<<8 * ((G + 7) / 8), KMP_L1_THREADS, 0, st>>>(
+                    d_res, d_res_off, d_class, k, n, slots, G, desc, lay, dg, pw21, dlo, dhi, H1 + h1, ws->keys.p,
                     ws->flags.p, SendL1{});
-            else
-                bp_scatter1p_kernel<KMP_L1_THREADS, false, false><<<grid, KMP_L1_THREADS, 0, st>>>(
-                    d_res, d_res_off, d_class, k, n, slots, G, desc, lay, dg, pw21, dlo, dhi, H1, ws->keys.p,
-                    ws->flags.p, SendL1{});
-            if (!direct)
-                bp_h1t_kernel<<<dim3((G + 31) / 32, (nown + 31) / 32), 256, 0, st>>>(H1, G, nown, 0, nown, H1 + h1);
+            } else {
+                if (grid < G)
+                    bp_scatter1p_kernel<KMP_L1_THREADS, false, true><<<grid, KMP_L1_THREADS, 0, st>>>(
+                        d_res, d_res_off, d_class, k, n, slots, G, desc, lay, dg, pw21, dlo, dhi, H1, ws->keys.p,
+                        ws->flags.p, SendL1{});
+                else
+                    bp_scatter1p_kernel<KMP_L1_THREADS, false, false><<<grid, KMP_L1_THREADS, 0, st>>>(
+                        d_res, d_res_off, d_class, k, n, slots, G, desc, lay, dg, pw21, dlo, dhi, H1, ws->keys.p,
+                        ws->flags.p, SendL1{});
+                if (!direct)
+                    bp_h1t_kernel<<<dim3((G + 31) / 32, (nown + 31) / 32), 256, 0, st>>>(H1, G, nown, 0, nown, H1 + h1);
+            }
         }
         return hipGetLastError();
     }

@@ -638,7 +638,7 @@ __host__ __device__ __forceinline__ uint32_t split_bin_lo(uint32_t d, uint32_t n
 // flight (a rank's share of the bins, a grid of what fits the device); otherwise it keys chunk
 // blockIdx.x alone (one GPU, and the sharded start: a grid of one workgroup per chunk), with no
 // next-chunk registers held across the chunk's work
-template <uint32_t kThr, bool kSend, bool kPersist>
+template <uint32_t kThr, bool kSend, bool kPersist, bool kTrans = false>
 __global__ __launch_bounds__(kThr, KMP_L1P_WAVES) void bp_scatter1p_kernel(
     const uint8_t* __restrict__ res, const uint64_t* __restrict__ res_off, const uint16_t* __restrict__ cls, int k,
     uint32_t n, uint64_t slots, uint32_t G, const uint4* __restrict__ desc, Layout lay, BpDigits dg, uint32_t pw21,
@@ -654,7 +654,16 @@ __global__ __launch_bounds__(kThr, KMP_L1P_WAVES) void bp_scatter1p_kernel(
     __shared__ uint32_t s_n;
     constexpr uint32_t kPer = kKeyChunk / kThr, kPP = (kKeyProtMax + kThr - 1) / kThr;
     const uint32_t tid = threadIdx.x, nown = dhi - dlo;
+    // kTrans (one GPU: every bin, one chunk per workgroup): XCD-aware chunk order — workgroup L runs
+    // on XCD L % 8, and XCD x keys the consecutive chunks [x per, (x + 1) per) — so the run table is
+    // written transposed (H1T[digit][chunk], level 2's reading order) straight from here: the words
+    // of one table row come from the consecutive chunks of one XCD and meet in its L2 (no bp_h1t)
+    static_assert(!kTrans || (!kSend && !kPersist), "the transposed table: one chunk per workgroup");
     uint32_t c = blockIdx.x;
+    if (kTrans) {
+        const uint32_t per = (G + 7) / 8;
+        c = (blockIdx.x % 8) * per + blockIdx.x / 8;
+    }
     if (c >= G) return;
     for (uint32_t i = tid; i < 256; i += kThr) lut[i] = c_lut.v[i];
     __syncthreads();  // the table before the first staging reads it
@@ -774,7 +783,13 @@ __global__ __launch_bounds__(kThr, KMP_L1P_WAVES) void bp_scatter1p_kernel(
             cnt[t] = d < nown ? lh[dlo + d] : 0u;
         }
         lds_bins_scan<kThr>(lh + dlo, nown, wave_tot);
-        if (!kSend) {
+        if (kTrans) {  // H1 is the transposed table here: row d - dlo holds the G chunks' runs of digit d
+#pragma unroll
+            for (uint32_t t = 0; t < kQ; ++t) {
+                const uint32_t d = tid + t * kThr;
+                if (d < nown) H1[(uint64_t)d * G + c] = lh[dlo + d] << 16 | cnt[t];
+            }
+        } else if (!kSend) {
             uint32_t* row = H1 + (uint64_t)c * nown;
 #pragma unroll
             for (uint32_t t = 0; t < kQ; ++t) {

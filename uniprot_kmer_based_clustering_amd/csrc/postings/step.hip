@@ -818,7 +818,7 @@ int slot_launch(kmp_postings* ws, kmp_postings::GraphSlot& slot, std::vector<uns
         ++ws->graph_replays;
         return KMP_OK;
     }
-    if (slot.seen != key) {
+    if (slot.seen != key || slot.plain == key) {  // (plain: its capture held a node that does not replay)
         slot.seen = key;
         return enqueue(st);
     }
@@ -836,11 +836,13 @@ int slot_launch(kmp_postings* ws, kmp_postings::GraphSlot& slot, std::vector<uns
     int rc = enqueue(ws->cst);
     hipError_t e = hipStreamEndCapture(ws->cst, &gr);
     hipGraphExec_t ex = nullptr;
-    if (rc == KMP_OK && e == hipSuccess && gr && gen == g_grow_gen.load() && graph_replayable(gr)) {
+    const bool ok = rc == KMP_OK && e == hipSuccess && gr && gen == g_grow_gen.load();
+    if (ok && graph_replayable(gr)) {
         slot.launches = graph_launches(gr);
         e = hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0);
-    } else if (e == hipSuccess) {
-        e = hipErrorUnknown;
+    } else {
+        if (ok) slot.plain = key;
+        if (e == hipSuccess) e = hipErrorUnknown;
     }
     if (gr) (void)hipGraphDestroy(gr);
     if (e != hipSuccess || !ex) {  // not capturable this time: plain
@@ -894,7 +896,7 @@ int fused_launch(kmp_postings* ws, MakeKeys& make_keys, const std::vector<unsign
         ++ws->graph_replays;
         return KMP_OK;
     }
-    if (ws->gkey_seen != key) {
+    if (ws->gkey_seen != key || ws->gkey_plain == key) {  // (plain: its capture held a node that does not replay)
         ws->gkey_seen = key;
         return enqueue(st);
     }
@@ -916,7 +918,13 @@ int fused_launch(kmp_postings* ws, MakeKeys& make_keys, const std::vector<unsign
     int rc = enqueue(ws->cst);
     hipError_t e = hipStreamEndCapture(ws->cst, &gr);
     hipGraphExec_t ex = nullptr;
-    if (rc == KMP_OK && e == hipSuccess && gr && gen == g_grow_gen.load() && graph_replayable(gr)) {
+    const bool ok = rc == KMP_OK && e == hipSuccess && gr && gen == g_grow_gen.load();
+    if (ok && !graph_replayable(gr)) {  // this sequence runs plain (the workspace keeps its graphs)
+        (void)hipGraphDestroy(gr);
+        ws->gkey_plain = key;
+        return enqueue(st);
+    }
+    if (ok) {
         ws->glaunches = graph_launches(gr);
         e = hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0);
     } else if (e == hipSuccess) {
@@ -1078,28 +1086,11 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
             PG(hipStreamSynchronize(st));
             g_hprof.mark(3);
         } else {
-            // the split step's front (+ its read-back) as a graph of its own (slot_launch: replayed from
-            // the third call of an unchanged key): config 1's ~7 front launches without host gaps.  The
-            // key holds every host input of the sequence — the fused key's, the spill / keys switches
-            // and the spill-all inputs; a postings entry's front holds rocPRIM's memset nodes and runs
-            // plain (graph_replayable)
-            const bool spill = !ws->heavy_ready, keys = !reuse;
-            auto front = [&](hipStream_t s) -> int {
-                int rc = enqueue_front(ws, make_keys, c, spill, s, keys);
-                if (rc == KMP_OK) {
-                    step_pack_kernel<<<1, 256, 0, s>>>(ws->bstats.p, ws->flags.p, nullptr, ws->hrb);
-                    if (hipGetLastError() != hipSuccess) rc = KMP_EDEVICE;
-                }
-                return rc;
-            };
-            std::vector<unsigned long long> fk = key;
-            fk.insert(fk.end(), {ws->shard_cap, ws->spill_cap, (unsigned long long)ws->timing, (unsigned long long)ws->cur_on,
-                                 ws->large_grid, ws->vreg_on ? ws->vreg_total + 1 : 0, ws->bp_J_min,
-                                 (unsigned long long)spill, (unsigned long long)keys, (unsigned long long)c.expand_only,
-                                 (uintptr_t)ws->hrb, (unsigned long long)ws->flat_heavy,
-                                 (unsigned long long)ws->spill_all_on, (unsigned long long)ws->reuse});
-            int rc = slot_launch(ws, ws->front_g, fk, front, st);
+            // (the split step's front as a graph of its own measured no faster at config 1: 0.624-0.629
+            // ms against 0.618 with plain launches, tools/front_probe.py; it runs plain)
+            int rc = enqueue_front(ws, make_keys, c, !ws->heavy_ready, st, !reuse);
             if (rc != KMP_OK) return rc;
+            step_pack_kernel<<<1, 256, 0, st>>>(ws->bstats.p, ws->flags.p, nullptr, ws->hrb);
             PG(hipStreamSynchronize(st));
         }
         if (rb[kRbFlagClass]) {

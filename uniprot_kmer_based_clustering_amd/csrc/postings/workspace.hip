@@ -130,13 +130,14 @@ struct kmp_postings {
     bool graph_on = true;
     struct GraphSlot {  // one captured sequence: its executable and the shape it was captured for
         hipGraphExec_t gexec = nullptr;
-        std::vector<unsigned long long> key, seen;
-        std::vector<std::vector<unsigned long long>> launches;  // its kernel launches (KMP_DEBUG replay check)
+        std::vector<unsigned long long> key, seen, plain;  // plain: a key whose capture does not replay
+        std::vector<std::vector<unsigned long long>> launches;  // its kernel launches (KMP_GRAPH_VERIFY check)
         void reset() {
             if (gexec) (void)hipGraphExecDestroy(gexec);
             gexec = nullptr;
             key.clear();
             seen.clear();
+            plain.clear();
             launches.clear();
         }
     } split_g[3];  // the k-mer split's phases (expand or group, edges, keys)
@@ -145,7 +146,6 @@ struct kmp_postings {
     // read-back, stage events, completion event and captured graph, so the next submission can be
     // queued behind it before its read-back is checked
     GraphSlot fg[2];
-    GraphSlot front_g;  // the split step's front + read-back (run_step)
     unsigned long long* hrb_slot[2] = {nullptr, nullptr};
     hipEvent_t evs[2][KMP_POSTINGS_STAGES + 1] = {};
     hipEvent_t done_ev[2] = {};
@@ -160,7 +160,7 @@ struct kmp_postings {
     hipStream_t side = nullptr;   // side_fork: the heavy path's large segment sorts
     hipEvent_t sev[2] = {};
 
-    std::vector<unsigned long long> gkey, gkey_seen;
+    std::vector<unsigned long long> gkey, gkey_seen, gkey_plain;  // gkey_plain: a key whose capture does not replay
     std::vector<std::vector<unsigned long long>> glaunches;  // the fused graph's kernel launches (KMP_DEBUG check)
     uint64_t graph_replays = 0;
     uint64_t reruns = 0;  // calls (or a split call's phases) run again with a grown capacity
@@ -193,7 +193,6 @@ struct kmp_postings {
             if (done_ev[i]) (void)hipEventDestroy(done_ev[i]);
             fg[i].reset();
         }
-        front_g.reset();
         if (gexec) (void)hipGraphExecDestroy(gexec);
         for (auto& g : split_g) g.reset();
         if (cst) (void)hipStreamDestroy(cst);
