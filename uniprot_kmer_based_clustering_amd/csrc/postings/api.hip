@@ -372,16 +372,29 @@ int kmp_dev_pairs_rows_multi(kmp_postings* const* ws, const int* ks, uint32_t nk
     if (timed && !ws[0]->mev[0])
         for (auto& e : ws[0]->mev) PG(hipEventCreate(&e));
     if (timed) PG(hipEventRecord(ws[0]->mev[0], st));
-    for (uint32_t j = 0; j < nk; ++j) {
-        // expand only: every incidence keyed (pair << 8) | j << 7 | s(x)
+    // expand only: every incidence keyed (pair << 8) | j << 7 | s(x); rd: the row-count path's
+    // phase (the front's statistics from the call that computes it: phase 1 or the partition path)
+    auto expand = [&](uint32_t j, RowDirect* rd) -> int {
         uint64_t unused = 0;
-        int rc = residues_impl(ws[j], d_res, d_res_off, d_class, n, ks[j], slots, 0xFFFFFFFFu, 1, require_class_diff,
-                               ranged, row_lo, row_hi, d_p, d_q, d_w, cap, &unused, j == 0 ? &s0 : nullptr, stream,
-                               kScoreBits + 1, j << kScoreBits, d_score, d_w1, &inc[j]);
-        if (rc != KMP_OK) return rc;
-        if (timed) PG(hipEventRecord(ws[0]->mev[1 + j], st));
+        ws[j]->rdir = rd;
+        const bool front = !rd || rd->phase == 1;
+        const int rc = residues_impl(ws[j], d_res, d_res_off, d_class, n, ks[j], slots, 0xFFFFFFFFu, 1,
+                                     require_class_diff, ranged, row_lo, row_hi, d_p, d_q, d_w, cap, &unused,
+                                     j == 0 && front ? &s0 : nullptr, stream, kScoreBits + 1, j << kScoreBits, d_score,
+                                     d_w1, &inc[j]);
+        ws[j]->rdir = nullptr;
+        if (rc == KMP_OK && timed && (!rd || rd->phase == 2)) PG(hipEventRecord(ws[0]->mev[1 + j], st));
+        return rc;
+    };
+    // the passes of a batch (a row range, the in-place reduce): the row-count path
+    int rc = KMP_OK;
+    bool taken = false;
+    if (ranged && ws[0]->direct_tail)
+        rc = tail_multi_rows(ws, nk, c, expand, inc, &taken, n_edges, stats, st);
+    if (rc == KMP_OK && !taken) {
+        for (uint32_t j = 0; j < nk && rc == KMP_OK; ++j) rc = expand(j, nullptr);
+        if (rc == KMP_OK) rc = tail_multi(ws, nk, c, inc, n_edges, stats, st);
     }
-    int rc = tail_multi(ws, nk, c, inc, n_edges, stats, st);
     if (rc == KMP_EOVERFLOW) ws[0]->pend_key = call;
     if (timed && (rc == KMP_OK || rc == KMP_EOVERFLOW)) {
         PG(hipEventRecord(ws[0]->mev[3], st));

@@ -851,6 +851,169 @@ __global__ __launch_bounds__(kHfThreads) void heavy_flat_kernel(
     }
 }
 
+// The passes of a fused multi-k batch without the row-block partition (tail_multi_rows, step.hip):
+// every pair key of a pass comes from the row-driven expansion (a spill-all front), so the row
+// blocks' sizes can be counted before any key exists.  Phase 1 counts each row's kept keys; the
+// host scans them into row blocks; phase 2 writes every key straight into its row block as the
+// u32 row-block key — the u64 shard keys, the histogram pass over them (pt_hist) and their
+// partition (pt_scatter) are gone: 20 of the ~50 bytes of tail traffic per key at config 5.
+struct RowDirect {
+    int phase;            // 1: count, 2: write
+    uint32_t row0;        // the call's first row
+    unsigned pbits, rbits;
+    uint32_t* cnt;        // phase 1: kept keys per row of the call
+    uint32_t* cur;        // phase 2: each row block's cursor (its start on entry)
+    uint32_t* keys;       // phase 2: the row-block keys
+    uint64_t cap;         // ... their capacity
+    bool ran;             // set by heavy_phase when its row-driven expansion took the call
+};
+
+// Both phases, heavy_flat's work split (one workgroup per 256 active elements, their candidates in
+// one contiguous slice per wave).  The elements come by protein, so the threads form runs of one
+// row (phase 1) or one row block (phase 2; key (p - row0) >> shift): run r owns the candidates
+// [rs[r], rs[r + 1]).  Kept counts per (wave, run): without the class test the slice's overlap
+// with the run; with it, counted on a first walk (each lane's count held for its current run and
+// added to LDS when the run changes).  Phase 1 adds each run's count to cnt[row].  Phase 2
+// reserves each run's keys on its block cursor once, gives each wave its offset inside, and
+// writes: a lane's position = its wave's offset in its run + the kept lanes before it in the
+// same run (ballot), the offsets advanced by the last lane of each run segment.
+template <bool kWrite>
+__global__ __launch_bounds__(kHfThreads) void heavy_rows_kernel(
+        const uint32_t* __restrict__ E, const uint64_t* __restrict__ GS, const uint32_t* __restrict__ KG,
+        const uint32_t* __restrict__ GH, const uint32_t* __restrict__ PE, uint32_t a0, uint32_t a1, unsigned cb,
+        int require_diff, uint32_t heavy_df, int k, unsigned sb, uint32_t sor, RowDirect rd,
+        unsigned long long* __restrict__ gstats) {
+    __shared__ uint32_t s_ex[kHfThreads + 1], s_e[kHfThreads], s_x[kHfThreads], s_f[kHfThreads];
+    __shared__ uint32_t s_run[kHfThreads], s_rs[kHfThreads + 1], s_rb[kHfThreads], s_rr[kHfThreads];
+    __shared__ uint32_t s_wk[kHfWaves][kHfThreads];  // kept per (wave, run); phase 2: then the write offsets
+    __shared__ uint32_t wave_tot[kHfWaves];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t a = a0 + blockIdx.x * kHfThreads + tid;
+    const unsigned shift = kWrite ? rd.rbits : 0u;
+    uint32_t cand = 0, e = 0, x = 0, f = 0, rb = ~0u;
+    if (a < a1) {
+        e = PE[a];
+        const uint32_t g = KG[e];
+        const uint64_t gs0 = GS[g], gs1 = GS[g + 1];
+        x = E[e];
+        if (gs1 - gs0 <= heavy_df) cand = (uint32_t)(gs1 - e - 1);
+        if (kWrite) f = sb ? sor | kmer_self_score(GH[g], k) : 0u;
+        rb = ((x >> cb) - rd.row0) >> shift;
+    }
+    uint32_t ex, total;
+    block_scan_n<kHfThreads>(cand, ex, total, wave_tot);
+    s_ex[tid] = ex;
+    s_e[tid] = e;
+    s_x[tid] = x;
+    s_f[tid] = f;
+    s_rb[tid] = rb;
+    if (tid == 0) s_ex[kHfThreads] = total;
+    __syncthreads();
+    if (total == 0) return;  // (uniform)
+    // runs of threads (the valid threads are a prefix, their keys ascending)
+    const bool head = a < a1 && (tid == 0 || s_rb[tid - 1] != rb);
+    uint32_t ri, nruns;
+    block_scan_n<kHfThreads>(head ? 1u : 0u, ri, nruns, wave_tot);
+    if (head) {
+        s_rs[ri] = ex;
+        s_rr[ri] = rb;
+    }
+    if (tid == 0) s_rs[nruns] = total;  // (the invalid threads' ex)
+    s_run[tid] = head ? ri : ri - 1u;
+    const uint32_t S = (total + kHfWaves - 1) / kHfWaves;
+    const uint32_t c0 = min(total, wv * S), c1 = min(total, c0 + S);
+#pragma unroll
+    for (uint32_t w = 0; w < kHfWaves; ++w) s_wk[w][tid] = 0;
+    __syncthreads();
+    auto search = [&](uint32_t o) {  // the last row with s_ex[i] <= o (o < total: a row with candidates)
+        uint32_t lo = 0, hi = kHfThreads;
+        while (lo + 1 < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_ex[mid] <= o) lo = mid;
+            else hi = mid;
+        }
+        return lo;
+    };
+    const uint32_t cmask = (1u << cb) - 1;
+    if (require_diff) {  // the first walk: kept per (wave, run)
+        uint32_t i = c0 + lane < c1 ? search(c0 + lane) : 0u, cr = ~0u, acc = 0;
+        for (uint32_t o = c0 + lane; o < c1; o += 64) {
+            while (s_ex[i + 1] <= o) ++i;
+            const uint32_t r = s_run[i];
+            if (r != cr) {
+                if (acc) atomicAdd(&s_wk[wv][cr], acc);
+                cr = r;
+                acc = 0;
+            }
+            acc += ((E[s_e[i] + 1 + (o - s_ex[i])] ^ s_x[i]) & cmask) != 0u;
+        }
+        if (acc) atomicAdd(&s_wk[wv][cr], acc);
+    } else {  // every candidate kept: the slices' overlaps with the runs
+        for (uint32_t r = tid; r < nruns; r += kHfThreads)
+#pragma unroll
+            for (uint32_t w = 0; w < kHfWaves; ++w) {
+                const uint32_t wc0 = min(total, w * S), wc1 = min(total, wc0 + S);
+                const uint32_t lo = max(wc0, s_rs[r]), hi = min(wc1, s_rs[r + 1]);
+                s_wk[w][r] = hi > lo ? hi - lo : 0u;
+            }
+    }
+    __syncthreads();
+    if (!kWrite) {
+        for (uint32_t r = tid; r < nruns; r += kHfThreads) {
+            uint32_t t = 0;
+#pragma unroll
+            for (uint32_t w = 0; w < kHfWaves; ++w) t += s_wk[w][r];
+            if (t) atomicAdd(&rd.cnt[s_rr[r]], t);
+        }
+        return;
+    }
+    uint32_t K = 0;
+    for (uint32_t r = tid; r < nruns; r += kHfThreads) {
+        uint32_t t = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < kHfWaves; ++w) t += s_wk[w][r];
+        K += t;
+        uint32_t at = t ? atomicAdd(&rd.cur[s_rr[r]], t) : 0u;
+#pragma unroll
+        for (uint32_t w = 0; w < kHfWaves; ++w) {
+            const uint32_t v = s_wk[w][r];
+            s_wk[w][r] = at;
+            at += v;
+        }
+    }
+    K = wave_sum(K);
+    if (lane == 0 && K) {  // the incidences written (statistics: any shard's slot)
+        uint32_t hx = (blockIdx.x * 0x9E3779B1u) ^ (a0 * 0x85EBCA6Bu) ^ wv;
+        hx ^= hx >> 16;
+        atomicAdd(&gstats[(uint64_t)((hx * 0x7FEB352Du) >> 26) * 8 + kStInc], (unsigned long long)K);
+    }
+    __syncthreads();
+    const uint32_t rmask = (1u << rd.rbits) - 1;
+    const unsigned long long below = (1ull << lane) - 1, upto = (2ull << lane) - 1;
+    uint32_t i = c0 + lane < c1 ? search(c0 + lane) : 0u;
+    for (uint32_t o0 = c0; o0 < c1; o0 += 64) {  // uniform over the wave (ballots)
+        const uint32_t o = o0 + lane;
+        bool keep = false;
+        uint32_t key = 0, r = ~0u;
+        if (o < c1) {
+            while (s_ex[i + 1] <= o) ++i;
+            const uint32_t xj = E[s_e[i] + 1 + (o - s_ex[i])], xi = s_x[i];
+            keep = !require_diff || ((xj ^ xi) & cmask) != 0u;
+            key = ((((xi >> cb) - rd.row0) & rmask) << rd.pbits | (xj >> cb)) << sb | s_f[i];
+            r = s_run[i];
+        }
+        const unsigned long long m = __ballot(keep);
+        const uint32_t pr = __shfl_up(r, 1), nr = __shfl_down(r, 1);
+        const unsigned long long heads = __ballot(lane == 0 || pr != r);
+        const unsigned long long seg = ~((1ull << (63 - __clzll(heads & upto))) - 1);  // lanes from the run's first
+        if (keep) {
+            const uint64_t pos = (uint64_t)s_wk[wv][r] + __popcll(m & below & seg);
+            if (pos < rd.cap) rd.keys[pos] = key;
+        }
+        if ((lane == 63 || nr != r) && r != ~0u) s_wk[wv][r] += __popcll(m & upto & seg);
+    }
+}
+
 // per-protein index of the compacted elements: counts, then (after a scan into PO) the scatter
 __global__ void heavy_pcount_kernel(const uint32_t* __restrict__ E, const unsigned long long* __restrict__ tot,
                                     unsigned cb, uint32_t* __restrict__ cnt) {

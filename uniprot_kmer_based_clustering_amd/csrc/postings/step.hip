@@ -486,8 +486,6 @@ __global__ __launch_bounds__(kHvScanThreads) void heavy_tscan_kernel(const uint3
 
 // a side stream forked from st (its work after what st has queued) and joined back
 bool side_fork(kmp_postings* ws, hipStream_t st) {
-    static const bool off = getenv("KMP_SIDE") && getenv("KMP_SIDE")[0] == '0';
-    if (off) return false;
     if (!ws->side && hipStreamCreateWithFlags(&ws->side, hipStreamNonBlocking) != hipSuccess) {
         ws->side = nullptr;
         return false;
@@ -686,7 +684,19 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
                 ws->hE.p, GS, ngb + 1, ws->h_tot + 1, ho, RUN, RH, 0, row_lo, row_hi, c.heavy_df, 1, 0, ws->bstats.p,
                 nullptr, nullptr, nullptr, nullptr, nullptr);
         const uint32_t a0 = ws->hPOh[row_lo], a1 = ws->hPOh[row_hi];
-        if (a1 > a0)
+        RowDirect* rd = ws->rdir;
+        if (rd) {  // tail_multi_rows: its row counts, or its keys by row block
+            rd->ran = true;
+            const uint32_t grid = (a1 - a0 + kHfThreads - 1) / kHfThreads;
+            if (a1 > a0 && rd->phase == 1)
+                heavy_rows_kernel<false><<<grid, kHfThreads, 0, st>>>(
+                        ws->hE.p, GS, ws->hKG.p, ws->hGH.p, ws->hPE.p, a0, a1, ho.cb, c.require_diff, c.heavy_df, c.k,
+                        c.sb, c.sor, *rd, ws->bstats.p);
+            else if (a1 > a0)
+                heavy_rows_kernel<true><<<grid, kHfThreads, 0, st>>>(
+                        ws->hE.p, GS, ws->hKG.p, ws->hGH.p, ws->hPE.p, a0, a1, ho.cb, c.require_diff, c.heavy_df, c.k,
+                        c.sb, c.sor, *rd, ws->bstats.p);
+        } else if (a1 > a0)
             heavy_flat_kernel<<<(a1 - a0 + kHfThreads - 1) / kHfThreads, kHfThreads, 0, st>>>(
                 ws->hE.p, GS, ws->hKG.p, ws->hGH.p, ws->hPE.p, a0, a1, ho.cb, 1u << bits_for(c.n), c.require_diff,
                 c.heavy_df, c.k, c.sb, c.sor, ws->inc_sorted.p, ws->shard_cap, ws->bstats.p + kRbCursor,
@@ -1183,7 +1193,8 @@ int run_step(kmp_postings* ws, MakeKeys& make_keys, std::vector<unsigned long lo
                     ws->front_ok = true;
                     ws->front_key = *c.front_key;
                 }
-                *c.n_inc_out = n_inc;
+                // (the row-count path: no shard keys, its expansion counts what it wrote)
+                *c.n_inc_out = ws->rdir ? acc[kStInc] : n_inc;
                 *n_edges = 0;
                 return KMP_OK;
             }
@@ -1308,33 +1319,44 @@ int tail_direct_write(kmp_postings* w0, const StepCfg& c, const PtGeom& g, uint3
     return KMP_OK;
 }
 
+int tail_multi_cut(kmp_postings* const* ws, uint32_t nk, const StepCfg& c, const PtGeom& g, uint64_t T,
+                   uint64_t total, const PtBufs& b, const std::vector<uint32_t>& hb, bool learn_shards,
+                   uint64_t* n_edges, kmp_postings_stats* stats, hipStream_t st);
+
+// the fused tail's geometry and buffers for T keys: *g, *total (the staging capacity), *b
+int tail_multi_prep(kmp_postings* const* ws, uint32_t nk, const StepCfg& c, uint64_t T, PtGeom* g, uint64_t* total,
+                    PtBufs* b, hipStream_t st) {
+    kmp_postings* w0 = ws[0];
+    if (!pt_geometry(w0, c, std::max<uint64_t>(T, 1), g)) return KMP_EINVAL;
+    // staging capacity: every key of the pass (the row-block positions); a stream's planned pass
+    // size at least, so the staging arrays are allocated once, not regrown as the passes vary
+    *total = T + 1;
+    for (uint32_t j = 0; j < nk; ++j) *total = std::max<uint64_t>(*total, ws[j]->stage_floor);
+    PG(w0->inc.reserve(*total / 2 + 1));  // u32 keys in a u64 buffer
+    if (!w0->direct_tail) {  // staged runs (the direct reduce writes the edges in place)
+        PG(w0->uniq.reserve(*total));
+        PG(w0->w.reserve(*total));
+        PG(w0->stg2.reserve(2 * *total));
+    }
+    PG(w0->ovf.reserve((uint64_t)g->nrb + 1));
+    PG(small_reserve(w0, st));
+    hipError_t e = hipSuccess;
+    *b = pt_bufs(w0, *g, true, &e, st);
+    PG(e);
+    PG(hipMemsetAsync(w0->flags.p + kFlOvf, 0, sizeof(uint32_t), st));
+    return KMP_OK;
+}
+
 int tail_multi(kmp_postings* const* ws, uint32_t nk, const StepCfg& c, const uint64_t* inc, uint64_t* n_edges,
                kmp_postings_stats* stats, hipStream_t st) {
     kmp_postings* w0 = ws[0];
     uint64_t T = 0;
     for (uint32_t j = 0; j < nk; ++j) T += inc[j];
     PtGeom g;
-    if (!pt_geometry(w0, c, std::max<uint64_t>(T, 1), &g)) return KMP_EINVAL;
-    // staging capacity: every key of the pass (the row-block positions); a stream's planned pass
-    // size at least, so the staging arrays are allocated once, not regrown as the passes vary
-    uint64_t total = T + 1;
-    for (uint32_t j = 0; j < nk; ++j) total = std::max<uint64_t>(total, ws[j]->stage_floor);
-    PG(w0->inc.reserve(total / 2 + 1));  // u32 keys in a u64 buffer
-    const bool direct = w0->direct_tail != 0;
-    if (!direct) {  // staged runs (the direct reduce writes the edges in place)
-        PG(w0->uniq.reserve(total));
-        PG(w0->w.reserve(total));
-        PG(w0->stg2.reserve(2 * total));
-    }
-    PG(w0->ovf.reserve((uint64_t)g.nrb + 1));
-    PG(small_reserve(w0, st));
-    hipError_t e = hipSuccess;
-    const PtBufs b = pt_bufs(w0, g, true, &e, st);
-    PG(e);
-    PG(hipMemsetAsync(w0->flags.p + kFlOvf, 0, sizeof(uint32_t), st));
+    uint64_t total = 0;
+    PtBufs b{};
+    if (int rc = tail_multi_prep(ws, nk, c, T, &g, &total, &b, st)) return rc;
     uint32_t* keys32 = reinterpret_cast<uint32_t*>(w0->inc.p);
-    uint32_t* stage_p = reinterpret_cast<uint32_t*>(w0->uniq.p);
-    uint32_t* stage_q = stage_p + total;
     auto geo = [&](uint32_t j) {  // input j: its shard regions
         PtGeom gj = g;
         gj.sc = ws[j]->shard_cap;
@@ -1349,10 +1371,24 @@ int tail_multi(kmp_postings* const* ws, uint32_t nk, const StepCfg& c, const uin
         pt_scatter_kernel<<<dim3(geo(j).jt, kShards), kPtThreads, 0, st>>>(ws[j]->inc_sorted.p,
                                                                           ws[j]->bstats.p + kRbCursor, geo(j), b.cur,
                                                                           keys32);
-    // the row blocks' sizes -> sub-blocks (a block above kPtCap cut into pieces the LDS reduce takes)
-    std::vector<uint32_t> hb(g.nrb + 1), hd(g.nrb + 1);
+    std::vector<uint32_t> hb(g.nrb + 1);
     PG(hipMemcpyAsync(hb.data(), b.bst, (g.nrb + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     PG(hipStreamSynchronize(st));
+    return tail_multi_cut(ws, nk, c, g, T, total, b, hb, true, n_edges, stats, st);
+}
+
+// tail_multi after the partition: the row blocks' keys in w0->inc at their starts hb (host copy;
+// b.bst on the device) -> sub-blocks (a block above kPtCap cut into pieces the LDS reduce takes),
+// the reduce and the edges.  learn_shards: size the inputs' next shard regions from this call's.
+int tail_multi_cut(kmp_postings* const* ws, uint32_t nk, const StepCfg& c, const PtGeom& g, uint64_t T,
+                   uint64_t total, const PtBufs& b, const std::vector<uint32_t>& hb, bool learn_shards,
+                   uint64_t* n_edges, kmp_postings_stats* stats, hipStream_t st) {
+    kmp_postings* w0 = ws[0];
+    uint32_t* keys32 = reinterpret_cast<uint32_t*>(w0->inc.p);
+    uint32_t* stage_p = reinterpret_cast<uint32_t*>(w0->uniq.p);
+    uint32_t* stage_q = stage_p + total;
+    const bool direct = w0->direct_tail != 0;
+    std::vector<uint32_t> hd(g.nrb + 1);
     uint32_t nd = 0;
     for (uint32_t r = 0; r < g.nrb; ++r) {
         hd[r] = nd;
@@ -1380,7 +1416,8 @@ int tail_multi(kmp_postings* const* ws, uint32_t nk, const StepCfg& c, const uin
         int rc = tail_direct_count(w0, g, nd, &ne, st);
         if (rc == KMP_OK && ne <= c.cap) rc = tail_direct_write(w0, c, g, nd, st);
         if (rc != KMP_OK) return rc;
-        for (uint32_t j = 0; j < nk; ++j) ws[j]->shard_cap = ws[j]->last_most + ws[j]->last_most / 4 + 256;
+        if (learn_shards)
+            for (uint32_t j = 0; j < nk; ++j) ws[j]->shard_cap = ws[j]->last_most + ws[j]->last_most / 4 + 256;
         w0->pt_inc = T;
         w0->pend_ne = ne;
         if (stats) {
@@ -1430,7 +1467,8 @@ int tail_multi(kmp_postings* const* ws, uint32_t nk, const StepCfg& c, const uin
     }
     // the next call's regions, learned now that the tail has read them; a quarter of slack (the
     // passes' sizes and shard loads vary, and an overflow reruns the whole expansion)
-    for (uint32_t j = 0; j < nk; ++j) ws[j]->shard_cap = ws[j]->last_most + ws[j]->last_most / 4 + 256;
+    if (learn_shards)
+        for (uint32_t j = 0; j < nk; ++j) ws[j]->shard_cap = ws[j]->last_most + ws[j]->last_most / 4 + 256;
     w0->pt_inc = T;
     if (stats) {
         stats->incidences = T;
@@ -1438,6 +1476,80 @@ int tail_multi(kmp_postings* const* ws, uint32_t nk, const StepCfg& c, const uin
     }
     *n_edges = ne;
     return ne > c.cap ? KMP_EOVERFLOW : KMP_OK;
+}
+
+// The fused passes' row-count path (heavy_rowcount / heavy_flat_rows, heavy.hip): expand(j, rd)
+// runs input j's expand-only call with ws[j]->rdir = rd.  Phase 1 counts each row's keys, the
+// host scans them into row blocks (the geometry from their exact total), phase 2 writes the keys
+// into their blocks and tail_multi_cut reduces them: no shard keys, no pt_hist / pt_tscan /
+// pt_scatter.  *taken false: a call the path does not cover (a front that left pair keys in its
+// shard regions, an expansion that is not row-driven): nothing of the tail ran, and the caller
+// takes the partition path (expand, tail_multi).
+template <class Expand>
+int tail_multi_rows(kmp_postings* const* ws, uint32_t nk, const StepCfg& c, Expand&& expand, uint64_t* inc,
+                    bool* taken, uint64_t* n_edges, kmp_postings_stats* stats, hipStream_t st) {
+    kmp_postings* w0 = ws[0];
+    *taken = false;
+    const uint32_t rows = c.row_hi - c.row_lo;
+    PG(w0->rcnt.reserve((uint64_t)rows + 1));
+    PG(hipMemsetAsync(w0->rcnt.p, 0, (size_t)rows * sizeof(uint32_t), st));
+    RowDirect rd{};
+    rd.phase = 1;
+    rd.row0 = c.row_lo;
+    rd.cnt = w0->rcnt.p;
+    for (uint32_t j = 0; j < nk; ++j) {
+        rd.ran = false;
+        if (int rc = expand(j, &rd)) return rc;
+        if (!rd.ran || ws[j]->last_most) return KMP_OK;  // keys outside the row-driven expansion
+    }
+    std::vector<uint32_t> hc(rows);
+    PG(hipMemcpyAsync(hc.data(), w0->rcnt.p, (size_t)rows * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    PG(hipStreamSynchronize(st));
+    uint64_t T = 0;
+    for (uint32_t v : hc) T += v;
+    if (T >= 0xFFFFFFFFull) return KMP_OK;  // (u32 key positions: the partition path reports it)
+    PtGeom g;
+    uint64_t total = 0;
+    PtBufs b{};
+    if (int rc = tail_multi_prep(ws, nk, c, T, &g, &total, &b, st)) return rc;
+    std::vector<uint32_t> hb(g.nrb + 1, 0);
+    {
+        uint64_t at = 0;
+        for (uint32_t r = 0; r < g.nrb; ++r) {
+            hb[r] = (uint32_t)at;
+            const uint64_t r0 = (uint64_t)r << g.rbits, r1 = std::min<uint64_t>(rows, (uint64_t)(r + 1) << g.rbits);
+            for (uint64_t i = r0; i < r1; ++i) at += hc[i];
+        }
+        hb[g.nrb] = (uint32_t)at;
+    }
+    PG(hipMemcpyAsync(b.bst, hb.data(), (g.nrb + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    PG(hipMemcpyAsync(b.cur, hb.data(), g.nrb * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    rd.phase = 2;
+    rd.pbits = g.pbits;
+    rd.rbits = g.rbits;
+    rd.cur = b.cur;
+    rd.keys = reinterpret_cast<uint32_t*>(w0->inc.p);
+    rd.cap = total;
+    uint64_t got = 0;
+    for (uint32_t j = 0; j < nk; ++j) {
+        rd.ran = false;
+        if (int rc = expand(j, &rd)) return rc;
+        if (!rd.ran || ws[j]->last_most) {  // (phase 1 took this front)
+            if (getenv("KMP_DEBUG"))
+                fprintf(stderr, "kmp: row-count path, input %u: expansion %d, shard keys %llu\n", j, (int)rd.ran,
+                        (unsigned long long)ws[j]->last_most);
+            return KMP_EDEVICE;
+        }
+        got += inc[j];
+    }
+    if (got != T) {  // the writes disagree with the counts
+        if (getenv("KMP_DEBUG"))
+            fprintf(stderr, "kmp: row-count path wrote %llu keys, counted %llu\n", (unsigned long long)got,
+                    (unsigned long long)T);
+        return KMP_EDEVICE;
+    }
+    *taken = true;
+    return tail_multi_cut(ws, nk, c, g, T, total, b, hb, false, n_edges, stats, st);
 }
 
 // the emit of the last tail_multi of w0 again, into larger arrays (its runs are still staged)

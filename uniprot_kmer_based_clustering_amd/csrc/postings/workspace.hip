@@ -110,6 +110,10 @@ struct kmp_postings {
     Grow<uint32_t> hKG, hPE, hPO, hPC;
     std::vector<uint32_t> hPOh;
     bool h_flat_ready = false, h_kg = false;
+    // tail_multi_rows: the phase its calls run (set around them; nullptr otherwise), and the pass's
+    // per-row key counts (ws[0]'s)
+    RowDirect* rdir = nullptr;
+    Grow<uint32_t> rcnt;
     uint64_t h_ng = 0;  // k-mers of the compaction (read back with the index)
     uint64_t spill_cap = 0;     // keys per spill shard region
     bool heavy = false;         // this workspace's batches spill: run the split step
@@ -173,10 +177,10 @@ struct kmp_postings {
     size_t pt_zero_n = 0;
     ~kmp_postings() {
         for (auto* g : {&keys, &sorted, &inc, &inc_sorted, &uniq, &bstats, &btot, &boff, &spill, &hkeys, &hsorted,
-                        &hGS, &htc, &htoff, &hoff, &hRH, &hseg, &hcur, &ovk, &ovx, &split_cur})
+                        &hGS, &htc, &htoff, &hoff, &hRH, &hseg, &hcur, &ovk, &ovx, &split_cur, &dlb})
             g->release();
         for (auto* g : {&w, &keep, &pos, &small, &cnt, &flags, &chunk_first, &chunk_desc, &bp, &pt, &ovf, &ovr, &ova, &stg2, &k2, &dsc, &hE, &hgi, &hcnt,
-                        &hrun, &hblk, &cur, &hGH, &split_kcur})
+                        &hrun, &hblk, &cur, &hGH, &split_kcur, &hKG, &hPE, &hPO, &hPC, &rcnt, &doff, &vreg})
             g->release();
         for (auto* g : {&split_desc})
             g->release();
