@@ -304,12 +304,12 @@ def bench_config5(args):
     win = {k: int(np.maximum(lens - k + 1, 0).sum()) for k in ks}
     stg = (ranks[0]["stage_ms"] if ranks else sm["stage_ms"])
     # algorithmic bytes per stage (one read of every input, one write of every output), per rank 0
-    # or the single GPU: expand of k0 re-reads the grouped keys each pass and writes the pair keys;
-    # the reduce reads each pair key (partition, scatter), writes and re-reads the u32 row key, and
-    # writes the edges (p q w score w5 w7)
+    # or the single GPU: the expansion re-reads the grouped elements each pass, reads each key's
+    # partner element and writes the u32 row-block key; the reduce reads each row-block key once and
+    # writes the edges (p q w score w5 w7: 24 B)
     r0 = ranks[0] if ranks else {"incidences": sm["incidences"], "n_edges": sm["n_edges"], "passes": sm["passes"]}
     alg = {"expand_k0": 8 * win[5] * r0["passes"] + 8 * r0["incidences"],
-           "reduce": 24 * r0["incidences"] + 24 * r0["n_edges"]}
+           "reduce": 4 * r0["incidences"] + 24 * r0["n_edges"]}
     stages = {s: {"ms": stg[s], "alg_bytes": alg.get(s),
                   "GBs": alg[s] / (stg[s] * 1e-3) / 1e9 if s in alg and stg[s] > 0 else None} for s in stg}
     dom = max(alg, key=lambda s: stg[s])

@@ -15,7 +15,7 @@ STAGE = {  # bench_config5's stage names
     "pt_hist_kernel": "reduce", "pt_tscan_kernel": "reduce", "pt_scatter_kernel": "reduce",
     "pt_split_kernel": "reduce", "pt_window_count_kernel": "reduce", "pt_reduce_count_kernel": "reduce",
     "pt_reduce_write_kernel": "reduce", "pt_reduce_scored_kernel": "reduce", "pt_emit_kernel": "reduce",
-    "heavy_flat_kernel": "expand", "bucket_small_kernel": "expand", "bucket_large_kernel": "expand",
+    "heavy_flat_kernel": "expand", "heavy_rows_kernel": "expand", "bucket_small_kernel": "expand", "bucket_large_kernel": "expand",
     "edge_digest_kernel": "summary",
 }
 

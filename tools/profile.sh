@@ -6,6 +6,7 @@
 #                                                    -> gpurun_out/pmc_config5_TAG.json (tools/pmc_config5.py)
 #   bash tools/profile.sh sq REGEX TAG               two SQ counter passes (8 counters each) over the kernels
 #                                                    matching REGEX -> gpurun_out/sq_TAG.txt
+#   bash tools/profile.sh sq5 REGEX TAG              the same over one cold config-5 step
 set -e
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
@@ -35,7 +36,7 @@ traffic5)
   # config 5: the fused reduce's and the expansion's kernels only (one step; each pass its own run)
   tag=$1
   # (the warm step: one warm-up stream, then the marker kernel the table starts after)
-  re="pt_hist|pt_tscan|pt_scatter_kernel|pt_split|pt_window_count|pt_reduce_count|pt_reduce_write|heavy_flat|bucket_small|bucket_large|edge_digest|spin_kernel"
+  re="pt_hist|pt_tscan|pt_scatter_kernel|pt_split|pt_window_count|pt_reduce_count|pt_reduce_write|heavy_flat|heavy_rows|bucket_small|bucket_large|edge_digest|spin_kernel"
   rm -rf gpurun_out/pmc5_fetch_$tag gpurun_out/pmc5_write_$tag
   timeout -s KILL 500 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$re" --output-format csv -d gpurun_out/pmc5_fetch_$tag -o run -- \
     python3 bench.py --config config5 --no-cpu-baseline --warmup 1 > gpurun_out/pmc5_fetch_$tag.log 2>&1
@@ -44,15 +45,17 @@ traffic5)
   python3 tools/pmc_config5.py $(find gpurun_out/pmc5_fetch_$tag -name 'run_counter_collection.csv') \
     $(find gpurun_out/pmc5_write_$tag -name 'run_counter_collection.csv') gpurun_out/pmc_config5_$tag.json
   ;;
-sq)
+sq|sq5)
   regex=$1; tag=$2
+  cmd="python3 bench.py --no-cpu-baseline --steps 3 --warmup 1"
+  [ $mode = sq5 ] && cmd="python3 bench.py --config config5 --no-cpu-baseline --warmup 0" 
   rm -rf gpurun_out/sq1_$tag gpurun_out/sq2_$tag
-  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_LDS \
+  timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_LDS \
     SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVE_CYCLES --kernel-include-regex "$regex" --output-format csv \
-    -d gpurun_out/sq1_$tag -o run -- python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/sq1_$tag.log 2>&1
-  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VMEM SQ_INSTS_SMEM SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+    -d gpurun_out/sq1_$tag -o run -- $cmd > gpurun_out/sq1_$tag.log 2>&1
+  timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VMEM SQ_INSTS_SMEM SQ_WAIT_ANY SQ_WAIT_INST_ANY \
     SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_ANY --kernel-include-regex "$regex" --output-format csv \
-    -d gpurun_out/sq2_$tag -o run -- python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/sq2_$tag.log 2>&1
+    -d gpurun_out/sq2_$tag -o run -- $cmd > gpurun_out/sq2_$tag.log 2>&1
   python3 tools/sq_summary.py gpurun_out/sq1_$tag gpurun_out/sq2_$tag > gpurun_out/sq_$tag.txt
   cat gpurun_out/sq_$tag.txt
   ;;

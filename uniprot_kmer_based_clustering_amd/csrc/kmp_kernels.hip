@@ -229,11 +229,16 @@ __global__ __launch_bounds__(kFilterThreads) void mark_kernel(const uint32_t* __
     const uint32_t p = blockIdx.x;
     const uint32_t len = set_len[p];
     const uint32_t* s = set + set_base(res_off[p], p);
+    // plain loads first: a k-mer already marked twice needs nothing, one already seen by another
+    // protein (a set holds each k-mer once) only the second mark — at k = 5 nearly every k-mer of a
+    // large batch, so the atomics (two per entry, on a 512 KB bitmap) mostly become cached loads.
+    // A stale 0 falls through to the atomics: the bits only ever gain ones.
     for (uint32_t e = threadIdx.x; e < len; e += kFilterThreads) {
         const uint32_t x = s[e];
         const uint32_t bit = 1u << (x & 31u);
-        const uint32_t old = atomicOr(&bits1[x >> 5], bit);
-        if (old & bit) atomicOr(&bits2[x >> 5], bit);
+        if (bits2[x >> 5] & bit) continue;
+        if ((bits1[x >> 5] & bit) || (atomicOr(&bits1[x >> 5], bit) & bit))
+            atomicOr(&bits2[x >> 5], bit);
     }
 }
 

@@ -253,17 +253,23 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
         const uint32_t i = tid + e * kThreads;
         xk[e] = i < n ? a.sorted[s0 + i] : 0ull;
     }
-    __syncthreads();  // LDS reuse across the buckets of one workgroup
+    if (!small) __syncthreads();  // LDS reuse across the buckets of one workgroup (the large kernel's loop)
     const unsigned hshift = lay.hshift, cb = lay.clsbits;
     const uint32_t lmask = (1u << hshift) - 1, cmask = (1u << cb) - 1;
     const uint32_t empty = ~b << (32 - lay.bbits);  // top bits differ from every h of bucket b
     const unsigned hb = 32 - lay.bbits;             // merged: low h bits kept in a slot
     const uint32_t hm = (1u << hb) - 1;
     constexpr uint32_t kFree = 0xFFFFFFFFu;          // merged empty slot (count field never all ones)
+    if (kMerge && kPer % 4 == 0) {  // 16-byte stores
+        uint4* h4 = reinterpret_cast<uint4*>(H + tid * kPer);
 #pragma unroll
-    for (int q = 0; q < kPer; ++q) {
-        if (!kMerge) T[tid * kPer + q] = empty;
-        H[tid * kPer + q] = kMerge ? kFree : 0u;
+        for (int q = 0; q < kPer / 4; ++q) h4[q] = make_uint4(kFree, kFree, kFree, kFree);
+    } else {
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) {
+            if (!kMerge) T[tid * kPer + q] = empty;
+            H[tid * kPer + q] = kMerge ? kFree : 0u;
+        }
     }
     for (uint32_t i = tid; i < kCap / 32; i += kThreads) dupw[i] = gdupw[i] = 0;
     for (uint32_t i = tid; i <= kHeavySub; i += kThreads) SZ[i] = 0;

@@ -865,15 +865,21 @@ struct RowDirect {
     uint32_t* cur;        // phase 2: each row block's cursor (its start on entry)
     uint32_t* keys;       // phase 2: the row-block keys
     uint64_t cap;         // ... their capacity
+    uint32_t* rec;        // per (workgroup, wave): phase 1's kept counts by row (the class test)
     bool ran;             // set by heavy_phase when its row-driven expansion took the call
 };
+// records per wave (row, kept); a wave over more rows marks its first record kRecFull and the
+// write phase counts that workgroup itself
+constexpr uint32_t kRecPer = 8, kRecFull = 0xFFFFFFFEu;
 
 // Both phases, heavy_flat's work split (one workgroup per 256 active elements, their candidates in
 // one contiguous slice per wave).  The elements come by protein, so the threads form runs of one
 // row (phase 1) or one row block (phase 2; key (p - row0) >> shift): run r owns the candidates
 // [rs[r], rs[r + 1]).  Kept counts per (wave, run): without the class test the slice's overlap
 // with the run; with it, counted on a first walk (each lane's count held for its current run and
-// added to LDS when the run changes).  Phase 1 adds each run's count to cnt[row].  Phase 2
+// added to LDS when the run changes) in phase 1, which records them per wave by row (rec: the
+// slices are the same in both phases), so phase 2 sums its row blocks' counts from the records
+// instead of walking the partners a third time.  Phase 1 adds each run's count to cnt[row].  Phase 2
 // reserves each run's keys on its block cursor once, gives each wave its offset inside, and
 // writes: a lane's position = its wave's offset in its run + the kept lanes before it in the
 // same run (ballot), the offsets advanced by the last lane of each run segment.
@@ -887,6 +893,7 @@ __global__ __launch_bounds__(kHfThreads) void heavy_rows_kernel(
     __shared__ uint32_t s_run[kHfThreads], s_rs[kHfThreads + 1], s_rb[kHfThreads], s_rr[kHfThreads];
     __shared__ uint32_t s_wk[kHfWaves][kHfThreads];  // kept per (wave, run); phase 2: then the write offsets
     __shared__ uint32_t wave_tot[kHfWaves];
+    __shared__ uint32_t s_full;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t a = a0 + blockIdx.x * kHfThreads + tid;
     const unsigned shift = kWrite ? rd.rbits : 0u;
@@ -924,6 +931,7 @@ __global__ __launch_bounds__(kHfThreads) void heavy_rows_kernel(
     const uint32_t c0 = min(total, wv * S), c1 = min(total, c0 + S);
 #pragma unroll
     for (uint32_t w = 0; w < kHfWaves; ++w) s_wk[w][tid] = 0;
+    if (tid == 0) s_full = 0;
     __syncthreads();
     auto search = [&](uint32_t o) {  // the last row with s_ex[i] <= o (o < total: a row with candidates)
         uint32_t lo = 0, hi = kHfThreads;
@@ -935,7 +943,33 @@ __global__ __launch_bounds__(kHfThreads) void heavy_rows_kernel(
         return lo;
     };
     const uint32_t cmask = (1u << cb) - 1;
-    if (require_diff) {  // the first walk: kept per (wave, run)
+    uint32_t* const rec = rd.rec + (uint64_t)blockIdx.x * kHfWaves * kRecPer * 2;
+    bool walk = require_diff;
+    if (kWrite && require_diff) {  // phase 1's records, summed by row block
+        if (tid < kHfWaves * kRecPer) {
+            const uint32_t row = rec[2 * tid], n = rec[2 * tid + 1];
+            if (row == kRecFull) {
+                s_full = 1;
+            } else if (n) {
+                const uint32_t b = row >> rd.rbits;
+                uint32_t lo = 0, hi = nruns;  // the run of block b (present: b is one of this workgroup's)
+                while (lo + 1 < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (s_rr[mid] <= b) lo = mid;
+                    else hi = mid;
+                }
+                atomicAdd(&s_wk[tid / kRecPer][lo], n);
+            }
+        }
+        __syncthreads();
+        walk = s_full != 0;  // (uniform)
+        if (walk) {
+#pragma unroll
+            for (uint32_t w = 0; w < kHfWaves; ++w) s_wk[w][tid] = 0;
+            __syncthreads();
+        }
+    }
+    if (walk) {  // the first walk: kept per (wave, run)
         uint32_t i = c0 + lane < c1 ? search(c0 + lane) : 0u, cr = ~0u, acc = 0;
         for (uint32_t o = c0 + lane; o < c1; o += 64) {
             while (s_ex[i + 1] <= o) ++i;
@@ -948,7 +982,7 @@ __global__ __launch_bounds__(kHfThreads) void heavy_rows_kernel(
             acc += ((E[s_e[i] + 1 + (o - s_ex[i])] ^ s_x[i]) & cmask) != 0u;
         }
         if (acc) atomicAdd(&s_wk[wv][cr], acc);
-    } else {  // every candidate kept: the slices' overlaps with the runs
+    } else if (!require_diff) {  // every candidate kept: the slices' overlaps with the runs
         for (uint32_t r = tid; r < nruns; r += kHfThreads)
 #pragma unroll
             for (uint32_t w = 0; w < kHfWaves; ++w) {
@@ -959,6 +993,22 @@ __global__ __launch_bounds__(kHfThreads) void heavy_rows_kernel(
     }
     __syncthreads();
     if (!kWrite) {
+        if (require_diff && tid < kHfWaves * kRecPer) {  // this workgroup's records
+            const uint32_t w = tid / kRecPer, i = tid % kRecPer;
+            const uint32_t wc0 = min(total, w * S), wc1 = min(total, wc0 + S);
+            uint32_t row = ~0u, n = 0;
+            if (wc1 > wc0) {
+                const uint32_t rf = s_run[search(wc0)], rl = s_run[search(wc1 - 1)];
+                if (rl - rf >= kRecPer) {
+                    row = kRecFull;
+                } else if (rf + i <= rl) {
+                    row = s_rr[rf + i];
+                    n = s_wk[w][rf + i];
+                }
+            }
+            rec[2 * tid] = row;
+            rec[2 * tid + 1] = n;
+        }
         for (uint32_t r = tid; r < nruns; r += kHfThreads) {
             uint32_t t = 0;
 #pragma unroll

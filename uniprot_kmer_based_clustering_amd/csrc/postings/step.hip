@@ -688,14 +688,17 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
         if (rd) {  // tail_multi_rows: its row counts, or its keys by row block
             rd->ran = true;
             const uint32_t grid = (a1 - a0 + kHfThreads - 1) / kHfThreads;
+            PG(ws->hrec.reserve((uint64_t)grid * kHfWaves * kRecPer * 2 + 1));
+            RowDirect rj = *rd;  // (the records are this workspace's: phase 2 reads what phase 1 wrote)
+            rj.rec = ws->hrec.p;
             if (a1 > a0 && rd->phase == 1)
                 heavy_rows_kernel<false><<<grid, kHfThreads, 0, st>>>(
                         ws->hE.p, GS, ws->hKG.p, ws->hGH.p, ws->hPE.p, a0, a1, ho.cb, c.require_diff, c.heavy_df, c.k,
-                        c.sb, c.sor, *rd, ws->bstats.p);
+                        c.sb, c.sor, rj, ws->bstats.p);
             else if (a1 > a0)
                 heavy_rows_kernel<true><<<grid, kHfThreads, 0, st>>>(
                         ws->hE.p, GS, ws->hKG.p, ws->hGH.p, ws->hPE.p, a0, a1, ho.cb, c.require_diff, c.heavy_df, c.k,
-                        c.sb, c.sor, *rd, ws->bstats.p);
+                        c.sb, c.sor, rj, ws->bstats.p);
         } else if (a1 > a0)
             heavy_flat_kernel<<<(a1 - a0 + kHfThreads - 1) / kHfThreads, kHfThreads, 0, st>>>(
                 ws->hE.p, GS, ws->hKG.p, ws->hGH.p, ws->hPE.p, a0, a1, ho.cb, 1u << bits_for(c.n), c.require_diff,

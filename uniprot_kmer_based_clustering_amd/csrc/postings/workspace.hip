@@ -113,7 +113,7 @@ struct kmp_postings {
     // tail_multi_rows: the phase its calls run (set around them; nullptr otherwise), and the pass's
     // per-row key counts (ws[0]'s)
     RowDirect* rdir = nullptr;
-    Grow<uint32_t> rcnt;
+    Grow<uint32_t> rcnt, hrec;  // hrec: this workspace's heavy_rows records (phase 1 -> phase 2)
     uint64_t h_ng = 0;  // k-mers of the compaction (read back with the index)
     uint64_t spill_cap = 0;     // keys per spill shard region
     bool heavy = false;         // this workspace's batches spill: run the split step
@@ -180,7 +180,7 @@ struct kmp_postings {
                         &hGS, &htc, &htoff, &hoff, &hRH, &hseg, &hcur, &ovk, &ovx, &split_cur, &dlb})
             g->release();
         for (auto* g : {&w, &keep, &pos, &small, &cnt, &flags, &chunk_first, &chunk_desc, &bp, &pt, &ovf, &ovr, &ova, &stg2, &k2, &dsc, &hE, &hgi, &hcnt,
-                        &hrun, &hblk, &cur, &hGH, &split_kcur, &hKG, &hPE, &hPO, &hPC, &rcnt, &doff, &vreg})
+                        &hrun, &hblk, &cur, &hGH, &split_kcur, &hKG, &hPE, &hPO, &hPC, &rcnt, &hrec, &doff, &vreg})
             g->release();
         for (auto* g : {&split_desc})
             g->release();
