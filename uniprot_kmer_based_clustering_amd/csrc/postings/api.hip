@@ -775,7 +775,7 @@ int kmp_dev_split_keys(kmp_postings* ws, const uint8_t* d_res, uint64_t res_lo, 
             // one workgroup per chunk (every digit ranked: the single-GPU geometry; two or four chunks
             // per persistent workgroup measured 5 and 30 % slower at G = 8); its flags go to the words
             // after the cursors
-            bp_scatter1p_kernel<KMP_L1_THREADS, true, false><<<G, KMP_L1_THREADS, 0, s>>>(
+            bp_scatter1p_kernel<kL1Threads, true, false><<<G, kL1Threads, 0, s>>>(
                 d_res, d_res_off, d_class, k, n, slots, G, ws->split_desc.p, lay, dg, pw21, 0u, dg.nb1, nullptr,
                 nullptr, ws->split_kcur.p + nkc, sl);
         }

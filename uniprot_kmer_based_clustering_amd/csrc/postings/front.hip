@@ -77,8 +77,8 @@ hipError_t bp_level1(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_r
         // persistent: as many workgroups as fit the device at once, each walking its chunks with the
         // next one's loads in flight
         static thread_local int per_cu = 0;
-        if (!per_cu && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bp_scatter1p_kernel<KMP_L1_THREADS, false, true>,
-                                                                     KMP_L1_THREADS, 0) != hipSuccess ||
+        if (!per_cu && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bp_scatter1p_kernel<kL1Threads, false, true>,
+                                                                     kL1Threads, 0) != hipSuccess ||
                         per_cu < 1))
             per_cu = 2;
         // every bin owned (one GPU): one workgroup per chunk, in order (bp_scatter1p 112 -> 103 us at
@@ -89,16 +89,16 @@ hipError_t bp_level1(kmp_postings* ws, const uint8_t* d_res, const uint64_t* d_r
             if (nown >= dg.nb1) {
                 // every bin (one GPU): the run table written transposed by the level-1 workgroups
                 // themselves (XCD-aware chunk order; 8 * ceil(G / 8) workgroups, the few past G return)
-                bp_scatter1p_kernel<KMP_L1_THREADS, false, false, true><<<8 * ((G + 7) / 8), KMP_L1_THREADS, 0, st>>>(
+                bp_scatter1p_kernel<kL1Threads, false, false, true><<<8 * ((G + 7) / 8), kL1Threads, 0, st>>>(
                     d_res, d_res_off, d_class, k, n, slots, G, desc, lay, dg, pw21, dlo, dhi, H1 + h1, ws->keys.p,
                     ws->flags.p, SendL1{});
             } else {
                 if (grid < G)
-                    bp_scatter1p_kernel<KMP_L1_THREADS, false, true><<<grid, KMP_L1_THREADS, 0, st>>>(
+                    bp_scatter1p_kernel<kL1Threads, false, true><<<grid, kL1Threads, 0, st>>>(
                         d_res, d_res_off, d_class, k, n, slots, G, desc, lay, dg, pw21, dlo, dhi, H1, ws->keys.p,
                         ws->flags.p, SendL1{});
                 else
-                    bp_scatter1p_kernel<KMP_L1_THREADS, false, false><<<grid, KMP_L1_THREADS, 0, st>>>(
+                    bp_scatter1p_kernel<kL1Threads, false, false><<<grid, kL1Threads, 0, st>>>(
                         d_res, d_res_off, d_class, k, n, slots, G, desc, lay, dg, pw21, dlo, dhi, H1, ws->keys.p,
                         ws->flags.p, SendL1{});
                 if (!direct)
@@ -147,12 +147,10 @@ bool cur_geometry(const Layout& lay, CurGeom* cg) {
     return true;
 }
 
-// KMP_GATHER_THREADS: workgroup size of the level-2 gather (a 4,096-key round either way).  512
-// threads x 8 keys (82 VGPRs, 6 waves per SIMD instead of 3) measured no faster at config 3
-// (buckets_level2 0.159-0.164 ms vs 0.149-0.160 ms), so 256 x 16 stays
-#ifndef KMP_GATHER_THREADS
-#define KMP_GATHER_THREADS 256
-#endif
+// workgroup size of the level-2 gather (a 4,096-key round either way).  512 threads x 8 keys (82
+// VGPRs, 6 waves per SIMD instead of 3) measured no faster at config 3 (buckets_level2 0.159-0.164 ms
+// vs 0.149-0.160 ms), so 256 x 16 stays
+constexpr uint32_t kGatherThreads = 256;
 // the cursor level 2's buffers (before any launch of the call's front)
 int bp_level2c_reserve(kmp_postings* ws, const Layout& lay) {
     const uint32_t nb = 1u << lay.bbits;
@@ -170,7 +168,7 @@ int bp_level2c_bins(kmp_postings* ws, const Layout& lay, uint32_t a, uint32_t b,
     own_bins(ws, dg, &c0, &c1);
     if (b > a) {
         const uint32_t ntiles = (ws->bp_G + ws->bp_T - 1) / ws->bp_T, per = (ntiles * (b - a) + 7) / 8;
-        constexpr uint32_t kGp = kBpGatherTile / KMP_GATHER_THREADS, kGt = KMP_GATHER_THREADS;
+        constexpr uint32_t kGp = kBpGatherTile / kGatherThreads, kGt = kGatherThreads;
         // level 1's output: this call's own segments, or (the k-mer split's sharded start) the
         // pieces every rank sent (ws->l2_tab: their run tables in the receive buffer)
         const bool recv = ws->l2_tab != nullptr;

@@ -688,12 +688,11 @@ __device__ __forceinline__ void process_bucket(const uint32_t b, const BucketArg
     }
 }
 
-// KMP_BS_WAVES: an occupancy floor for the small kernel (waves per SIMD; 0: the compiler's choice)
-#ifndef KMP_BS_WAVES
-#define KMP_BS_WAVES 8  // 64 VGPRs: 8 workgroups per CU (LDS allows 8); group_expand 0.238 -> 0.222 ms at config 3
-#endif
+// the small kernel's occupancy floor: 8 waves per SIMD, 64 VGPRs, 8 workgroups per CU (LDS allows 8):
+// group_expand 0.238 -> 0.222 ms at config 3
+constexpr int kBsWaves = 8;
 template <int kCap, int kThreads, int kTabBits, bool kMerge, bool kRows, bool kScore>
-__global__ __launch_bounds__(kThreads, KMP_BS_WAVES ? KMP_BS_WAVES * 256 / kThreads : 1) void bucket_small_kernel(BucketArgs a, uint32_t b0) {
+__global__ __launch_bounds__(kThreads, kBsWaves * 256 / kThreads) void bucket_small_kernel(BucketArgs a, uint32_t b0) {
     process_bucket<kCap, kThreads, kTabBits, kMerge, kRows, kScore>(b0 + blockIdx.x, a, true);
 }
 

@@ -16,10 +16,8 @@
 //      class test (mod.rs:580-587) on every pair (p_i, p_j), j > i; a workgroup scan and one
 //      cursor reservation place the pair keys p_i * mul + p_j in the shard regions the bucket
 //      kernels fill.  A k-mer of df 10^4 is ~400 tiles: no workgroup walks a long posting list.
-#ifndef KMP_HV_TILE
-#define KMP_HV_TILE 1024  // spilled keys per compaction tile (4,096 ran 249 workgroups at config 1: 11 + 15 us)
-#endif
-constexpr uint32_t kHvTile = KMP_HV_TILE, kHvThreads = 256, kHvPer = kHvTile / kHvThreads;
+// spilled keys per compaction tile (4,096 ran 249 workgroups at config 1: 11 + 15 us)
+constexpr uint32_t kHvTile = 1024, kHvThreads = 256, kHvPer = kHvTile / kHvThreads;
 constexpr uint32_t kHvI = 256, kHvJ = 256, kHvMW = kHvJ / 32;
 constexpr uint32_t kHvSpread = 64 * 256;  // a tile with this many pairs spreads them over the shards
 // flat tiles (class order, every pair kept, a k-mer of at most kHvFlatRuns class runs): the
@@ -1082,18 +1080,11 @@ __global__ void heavy_pscatter_kernel(const uint32_t* __restrict__ E, const unsi
 }
 
 // bucket kernels: capacity (keys), threads, log2 of the k-mer table (>= capacity)
-#ifndef KMP_SMALL_GEOM
-#define KMP_SMALL_GEOM 1280, 256, 11
-#endif
-constexpr int kSmallGeom[3] = {KMP_SMALL_GEOM};
-constexpr int kBucketSmallCap = kSmallGeom[0], kBucketSmallThreads = kSmallGeom[1], kBucketSmallTab = kSmallGeom[2];
+constexpr int kBucketSmallCap = 1280, kBucketSmallThreads = 256, kBucketSmallTab = 11;
 // larger buckets (up to 4,096 keys: four per thread, no register spills) take the large kernel;
 // above that the whole bucket goes to the heavy path
 constexpr int kBucketLargeCap = 4096, kBucketLargeThreads = 1024, kBucketLargeTab = 12;
 // the large kernel grid-strides the list of large buckets (usually empty at config 3; most
 // buckets of a k = 5 batch of real proteins): four workgroups per CU (one per CU measured 8 % slower)
 constexpr int kBucketLargeGrid = 1024;
-#ifndef KMP_VREG_TRIES
-#define KMP_VREG_TRIES 3
-#endif
-constexpr uint32_t kVregTries = KMP_VREG_TRIES;  // learned bucket layouts in a row before the counting partition
+constexpr uint32_t kVregTries = 3;  // learned bucket layouts in a row before the counting partition

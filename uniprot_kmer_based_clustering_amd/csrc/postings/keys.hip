@@ -65,10 +65,7 @@ struct Layout {
     uint32_t mean_keys;         // bucketed: expected keys per bucket (windows / buckets)
 };
 
-#ifndef KMP_BUCKET_TARGET
-#define KMP_BUCKET_TARGET 1024
-#endif
-constexpr uint32_t kBucketTarget = KMP_BUCKET_TARGET;  // mean keys per bucket
+constexpr uint32_t kBucketTarget = 1024;  // mean keys per bucket
 constexpr uint32_t kHashA = 0x9E3779B1u;  // odd: code -> h(code) is a bijection of u32
 
 Layout make_layout(uint32_t n, int k, uint64_t slots, bool bucketed) {

@@ -537,11 +537,9 @@ __global__ void bp_cur_clear_kernel(uint32_t* __restrict__ cur, uint32_t n) {
 constexpr uint32_t kBpGatherMax = 1024;  // chunks per level-2 tile (T)
 constexpr uint32_t kBpGatherTile = 4096;  // keys per round of a level-2 tile
 
-// KMP_L1_THREADS: workgroup size of the local level 1 (a 4,096-slot chunk either way; 512 threads
-// own 8 slots each: twice the waves per CU at the same LDS; keys_level1 0.139 -> 0.127 ms at config 3)
-#ifndef KMP_L1_THREADS
-#define KMP_L1_THREADS 512
-#endif
+// workgroup size of the local level 1 (a 4,096-slot chunk either way; 512 threads own 8 slots each:
+// twice the waves per CU at the same LDS; keys_level1 0.139 -> 0.127 ms at config 3)
+constexpr uint32_t kL1Threads = 512;
 
 // Chunk descriptors of the local level 1: desc[c] = {first, last, r0, r1} = the proteins whose
 // regions overlap chunk c ([first, last]; n is the tail past the last region) and the residue span
@@ -620,9 +618,7 @@ __host__ __device__ __forceinline__ uint32_t split_bin_lo(uint32_t d, uint32_t n
 // waves per SIMD the persistent level 1 is compiled for (VGPR budget: 8 -> 64 registers and 24 B of
 // scratch per lane, four 512-thread workgroups per CU; at 6 waves, 79 registers, a rank of the k-mer
 // split at G = 8 spent 91 us in it against 86 us at 8; one GPU: the same)
-#ifndef KMP_L1P_WAVES
-#define KMP_L1P_WAVES 8
-#endif
+constexpr uint32_t kL1pWaves = 8;
 // Level 1, local, persistent: workgroup w takes chunks w, w + grid, ...; chunk c's keys of the
 // call's digits [dlo, dhi) grouped by digit1 at out[c * kKeyChunk ...] (its own 4,096-key segment),
 // its run table (start << 16 | count per own digit) in H1[c][digit - dlo].  The next chunk's
@@ -639,7 +635,7 @@ __host__ __device__ __forceinline__ uint32_t split_bin_lo(uint32_t d, uint32_t n
 // blockIdx.x alone (one GPU, and the sharded start: a grid of one workgroup per chunk), with no
 // next-chunk registers held across the chunk's work
 template <uint32_t kThr, bool kSend, bool kPersist, bool kTrans = false>
-__global__ __launch_bounds__(kThr, KMP_L1P_WAVES) void bp_scatter1p_kernel(
+__global__ __launch_bounds__(kThr, kL1pWaves) void bp_scatter1p_kernel(
     const uint8_t* __restrict__ res, const uint64_t* __restrict__ res_off, const uint16_t* __restrict__ cls, int k,
     uint32_t n, uint64_t slots, uint32_t G, const uint4* __restrict__ desc, Layout lay, BpDigits dg, uint32_t pw21,
     uint32_t dlo, uint32_t dhi, uint32_t* __restrict__ H1, unsigned long long* __restrict__ out,
@@ -896,11 +892,8 @@ struct RecvTab {
     uint64_t stride;     // u32 words between source regions (2 x the region's u64 words)
     uint64_t tb;         // run-table u64 words at the start of a region
 };
-#ifndef KMP_L2_WAVES
-#define KMP_L2_WAVES 0  // waves per SIMD level 2 is compiled for (0: the compiler's choice, ~140 VGPRs)
-#endif
 template <uint32_t kPer, uint32_t kThr, bool kVreg, bool kRecv>
-__global__ __launch_bounds__(kThr, KMP_L2_WAVES ? KMP_L2_WAVES : 1) void bp_scatter2g_kernel(const unsigned long long* __restrict__ in,
+__global__ __launch_bounds__(kThr) void bp_scatter2g_kernel(const unsigned long long* __restrict__ in,
                                                                    const uint32_t* __restrict__ H1T, uint32_t G,
                                                                    uint32_t hsb, uint32_t hsc,
                                                                    uint32_t T, uint32_t ntiles, uint32_t nbins,

@@ -27,12 +27,7 @@ struct StepCfg {
 
 // row-block tail geometry: rows per block so that an average block holds about a quarter of
 // kPtCap keys (from the expected incidence count)
-#ifndef KMP_FT_TARGET
-#define KMP_FT_TARGET 2275
-#endif
-#ifndef KMP_BINSORT_MODE
-#define KMP_BINSORT_MODE 1
-#endif
+constexpr double kFtTarget = 2275;  // the fast tail's average keys per row block (see pt_geometry)
 bool pt_geometry(const kmp_postings* ws, const StepCfg& c, uint64_t inc, PtGeom* g) {
     g->pbits = bits_for(c.n);
     g->sbits = c.sb;
@@ -44,8 +39,8 @@ bool pt_geometry(const kmp_postings* ws, const StepCfg& c, uint64_t inc, PtGeom*
     // small call (a rank's rows of the k-mer split) takes smaller blocks, down to ~1K keys, so
     // that ~1,000 workgroups still fill the GPU
     // the fast tail (unscored) keeps its blocks well inside its fixed regions and hash table: an
-    // average of ~1.1-2.3K keys (KMP_FT_TARGET), twice that in the first rows
-    const double target = (!c.sb && ws->fast_tail) ? (double)KMP_FT_TARGET : (double)kPtCap / 2.4;
+    // average of ~1.1-2.3K keys (kFtTarget), twice that in the first rows
+    const double target = (!c.sb && ws->fast_tail) ? kFtTarget : (double)kPtCap / 2.4;
     const double per_block = std::min(target, std::max(1024.0, (double)est / 1024));
     const double want = per_block * std::max<uint32_t>(rows, 1) / est;
     unsigned rb = 0;
@@ -67,9 +62,8 @@ bool pt_geometry(const kmp_postings* ws, const StepCfg& c, uint64_t inc, PtGeom*
     g->nprot = c.n;
     g->rowend = c.ranged ? c.row_hi : c.n;
     g->ftcap = kFtCap;
-    // the bin sort for scored blocks only (unscored at config 3: 0.130 -> 0.387 ms);
-    // KMP_BINSORT_MODE (A/B builds): 0 the radix sort everywhere, 2 the bin sort everywhere
-    g->binsort = KMP_BINSORT_MODE == 2 ? 1 : KMP_BINSORT_MODE == 0 ? 0 : (g->sbits != 0);
+    // the bin sort for scored blocks only (unscored at config 3: 0.130 -> 0.387 ms)
+    g->binsort = g->sbits != 0;
     return true;
 }
 
@@ -173,10 +167,7 @@ hipError_t small_reserve(kmp_postings* ws, hipStream_t st) {
 // after that, turn the counting tail on for the shape.  (Regions learned from the blocks' exact
 // counts, with the blocks above kFtCap counted in LDS bins over (row, q), were measured and removed
 // in round 5: uniprot at k = 5 0.91 ms against 0.744 ms on the counting tail.)
-#ifndef KMP_FAST_SHRINKS
-#define KMP_FAST_SHRINKS 2
-#endif
-constexpr uint32_t kFastShrinks = KMP_FAST_SHRINKS;
+constexpr uint32_t kFastShrinks = 2;
 void fast_overflow(kmp_postings* ws, const PtGeom& g, const unsigned long long* rb) {
     const uint64_t most = rb[kRbMaxBlock];
     if (ws->fast_tries >= kFastShrinks || g.rbits == 0) {

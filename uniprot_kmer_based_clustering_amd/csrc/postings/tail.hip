@@ -18,13 +18,7 @@
 // A row block above kPtCap keys (a protein pairing with thousands of later proteins: real data
 // at k = 5) is listed instead; the host sorts the listed blocks with one segmented radix sort
 // and pt_ovf_rle encodes them (pt_finish_overflow), then offsets and emit run again.
-#ifndef KMP_PT_PER
-#define KMP_PT_PER 16
-#endif
-#ifndef KMP_PT_RADIX_BITS
-#define KMP_PT_RADIX_BITS 0  // rocprim's choice (8 bits, match ranking, at 512 threads)
-#endif
-constexpr uint32_t kPtThreads = 1024, kPtPer = KMP_PT_PER, kPtTile = kPtThreads * kPtPer;  // partition tiles: 16,384 keys
+constexpr uint32_t kPtThreads = 1024, kPtPer = 16, kPtTile = kPtThreads * kPtPer;  // partition tiles: 16,384 keys
 constexpr uint32_t kPtRThreads = 512, kPtCap = 8192;  // pt_reduce: up to 16 keys per thread
 constexpr uint32_t kPtMaxBlocks = 8192;  // row blocks (LDS histogram of pt_hist / pt_scatter)
 
@@ -201,10 +195,7 @@ __global__ __launch_bounds__(kPtThreads) void pt_scatter_kernel(const unsigned l
 // most, so the histogram holds kFtScBlocks = kPtMaxBlocks - 16 row blocks (the fast tail's limit;
 // the full 8,192 plus the scan's words was 36 B over, one workgroup per CU)
 constexpr uint32_t kFtCap = 8192;  // fast tail, hash reduce: keys per row-block region
-#ifndef KMP_FTSC_BLOCKS
-#define KMP_FTSC_BLOCKS (kPtMaxBlocks - 16)
-#endif
-constexpr uint32_t kFtScThreads = 512, kFtScTile = kFtScThreads * 16, kFtScBlocks = KMP_FTSC_BLOCKS;
+constexpr uint32_t kFtScThreads = 512, kFtScTile = kFtScThreads * 16, kFtScBlocks = kPtMaxBlocks - 16;
 __global__ __launch_bounds__(kFtScThreads) void pt_scatter_capped_kernel(const unsigned long long* __restrict__ in,
                                                                          const unsigned long long* __restrict__ cursor,
                                                                          PtGeom g, uint32_t* __restrict__ cur,
@@ -216,8 +207,7 @@ __global__ __launch_bounds__(kFtScThreads) void pt_scatter_capped_kernel(const u
     __shared__ uint32_t lh[kFtScBlocks];
     __shared__ uint32_t S[kFtScTile];
     __shared__ uint16_t SR[kFtScTile];
-    static_assert(KMP_FTSC_BLOCKS != kPtMaxBlocks - 16 ||
-                      sizeof(uint32_t) * (kFtScBlocks + kFtScTile + kFtScThreads / 64 + 1) +
+    static_assert(sizeof(uint32_t) * (kFtScBlocks + kFtScTile + kFtScThreads / 64 + 1) +
                               sizeof(uint16_t) * kFtScTile <= 80 * 1024,
                   "two workgroups per CU");
     __shared__ uint32_t wave_tot[kThr / 64];
@@ -319,10 +309,7 @@ __global__ __launch_bounds__(kFtScThreads) void pt_scatter_capped_kernel(const u
 }
 
 template <uint32_t kE>
-using PtSort = rocprim::block_radix_sort<uint32_t, kPtRThreads, kE, rocprim::empty_type, 1, 1, KMP_PT_RADIX_BITS,
-                                         KMP_PT_RADIX_BITS == 4
-                                             ? rocprim::block_radix_rank_algorithm::basic_memoize
-                                             : rocprim::block_radix_rank_algorithm::default_for_radix_sort>;
+using PtSort = rocprim::block_radix_sort<uint32_t, kPtRThreads, kE>;  // rocprim's digits (8 bits, match ranking)
 
 // Binned sort of a block's n keys (the row-block reduce; replaces a block radix sort over all
 // pbits + rbits (+ sbits) key bits, 6-8 passes of rank + scatter).  A run only needs its pair's
@@ -1236,13 +1223,11 @@ struct FtLds {
     unsigned long long s_excl;
 };
 
-// KMP_FT_WAVES: waves per SIMD the fast reduce is compiled for (0: the compiler's choice).  6: at
-// most 80 VGPRs, so three 512-thread workgroups per CU (53 KB of LDS each): pair_sort_rle 0.083 ->
-// 0.071 ms at config 3
-#ifndef KMP_FT_WAVES
-#define KMP_FT_WAVES 6
-#endif
-__global__ __launch_bounds__(kFtThreads, KMP_FT_WAVES ? KMP_FT_WAVES : 1) void pt_reduce_fast_kernel(const uint32_t* __restrict__ keys,
+// waves per SIMD the fast reduce is compiled for: 6, at most 80 VGPRs, so three 512-thread
+// workgroups per CU (53 KB of LDS each): pair_sort_rle 0.083 -> 0.071 ms at config 3 (8 waves with a
+// 4,096-slot table: 0.104 ms, round 6)
+constexpr uint32_t kFtWaves = 6;
+__global__ __launch_bounds__(kFtThreads, kFtWaves) void pt_reduce_fast_kernel(const uint32_t* __restrict__ keys,
                                                                     uint32_t* __restrict__ fcur, PtGeom g,
                                                                     unsigned long long* __restrict__ lb,
                                                                     uint32_t* __restrict__ ticket,
