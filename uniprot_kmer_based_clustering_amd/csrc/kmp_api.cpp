@@ -1720,7 +1720,9 @@ int kmp_pairs_stream(kmp_ctx* c, const kmp_pair_opts* opts, const int* ks, uint3
         lo = c->rows_lo;
         hi = c->rows_hi;
     }
+    if (getenv("KMP_DEBUG")) fprintf(stderr, "kmp: stream rows [%u, %u)\n", lo, hi);
     KMP_TRY(c, prepare_ksets(c, ks, nk));  // the reference's counters per k (kmp_build_sets)
+    if (getenv("KMP_DEBUG")) fprintf(stderr, "kmp: stream sets built\n");
     restore_ksets(c, nk);
     if (c->ranks.size() > 1) return multi_stream(c, o, ks, nk, sink_on_device, sink, user, summary, lo, hi);
     DevBuf dacc;
@@ -1736,7 +1738,9 @@ int kmp_pairs_stream(kmp_ctx* c, const kmp_pair_opts* opts, const int* ks, uint3
         return sink(user, &hc);
     });
     if (rc != KMP_OK) return rc;
-    return finish_summary(c, o, {&ln}, summary);
+    rc = finish_summary(c, o, {&ln}, summary);
+    if (getenv("KMP_DEBUG")) fprintf(stderr, "kmp: stream done (%u passes)\n", ln.passes);
+    return rc;
 }
 
 // kmp_pairs_multi_k: the stream, collected into one device list (D2D appends), then copied out

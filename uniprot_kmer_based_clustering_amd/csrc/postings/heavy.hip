@@ -869,6 +869,8 @@ struct RowDirect {
 // records per wave (row, kept); a wave over more rows marks its first record kRecFull and the
 // write phase counts that workgroup itself
 constexpr uint32_t kRecPer = 8, kRecFull = 0xFFFFFFFEu;
+constexpr uint32_t kHrBatch = 4;  // partner loads a lane of the counting walk issues before using them
+// (the same batching of the write walk measured slower: 406 -> 478 ms at config 5, as did pt_split's)
 
 // Both phases, heavy_flat's work split (one workgroup per 256 active elements, their candidates in
 // one contiguous slice per wave).  The elements come by protein, so the threads form runs of one
@@ -969,15 +971,29 @@ __global__ __launch_bounds__(kHfThreads) void heavy_rows_kernel(
     }
     if (walk) {  // the first walk: kept per (wave, run)
         uint32_t i = c0 + lane < c1 ? search(c0 + lane) : 0u, cr = ~0u, acc = 0;
-        for (uint32_t o = c0 + lane; o < c1; o += 64) {
-            while (s_ex[i + 1] <= o) ++i;
-            const uint32_t r = s_run[i];
-            if (r != cr) {
-                if (acc) atomicAdd(&s_wk[wv][cr], acc);
-                cr = r;
-                acc = 0;
+        for (uint32_t o0 = c0 + lane; o0 < c1; o0 += 64 * kHrBatch) {  // kHrBatch partner loads in flight
+            uint32_t ib[kHrBatch], xb[kHrBatch];
+#pragma unroll
+            for (uint32_t b = 0; b < kHrBatch; ++b) {
+                const uint32_t o = o0 + 64 * b;
+                ib[b] = ~0u;
+                if (o < c1) {
+                    while (s_ex[i + 1] <= o) ++i;
+                    ib[b] = i;
+                    xb[b] = E[s_e[i] + 1 + (o - s_ex[i])];
+                }
             }
-            acc += ((E[s_e[i] + 1 + (o - s_ex[i])] ^ s_x[i]) & cmask) != 0u;
+#pragma unroll
+            for (uint32_t b = 0; b < kHrBatch; ++b) {
+                if (ib[b] == ~0u) continue;
+                const uint32_t r = s_run[ib[b]];
+                if (r != cr) {
+                    if (acc) atomicAdd(&s_wk[wv][cr], acc);
+                    cr = r;
+                    acc = 0;
+                }
+                acc += ((xb[b] ^ s_x[ib[b]]) & cmask) != 0u;
+            }
         }
         if (acc) atomicAdd(&s_wk[wv][cr], acc);
     } else if (!require_diff) {  // every candidate kept: the slices' overlaps with the runs

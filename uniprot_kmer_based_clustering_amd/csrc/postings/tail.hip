@@ -321,14 +321,17 @@ using PtSort = rocprim::block_radix_sort<uint32_t, kPtRThreads, kE>;  // rocprim
 // bin one pair: no sort at all.  A bin above kBinMax keys (a skewed block) makes the caller fall
 // back to the radix sort (k is untouched then).  On success k holds the sorted keys blocked
 // (thread t: ranks t * kE + e), the padding (all ones) last.
-constexpr uint32_t kBinMax = 64, kBinCap = 8192;
-struct PtBinLds {
-    uint32_t H[kBinCap];  // per bin: count, then first rank
-    uint32_t S[kPtCap];   // the keys by bin
+constexpr uint32_t kBinMax = 64;
+template <uint32_t kCap>  // bins at most
+struct PtBinLdsT {
+    uint32_t H[kCap];    // per bin: count, then first rank
+    uint32_t S[kPtCap];  // the keys by bin
 };
-template <uint32_t kE>
+using PtBinLds = PtBinLdsT<8192>;
+template <uint32_t kE, uint32_t kBinCap>
 __device__ __forceinline__ bool pt_bin_sort(uint32_t (&k)[kE], uint32_t n, const PtGeom& g, uint32_t rowbase,
-                                            PtBinLds& b, uint32_t* red, uint32_t* s_flag, uint32_t* wave_tot) {
+                                            PtBinLdsT<kBinCap>& b, uint32_t* red, uint32_t* s_flag,
+                                            uint32_t* wave_tot) {
     constexpr uint32_t kT = kPtRThreads, kW = kT / 64;
     const unsigned sb = g.sbits, rs = g.pbits + g.sbits;
     const uint32_t qm = (1u << g.pbits) - 1, qlo = rowbase + 1;
@@ -365,13 +368,17 @@ __device__ __forceinline__ bool pt_bin_sort(uint32_t (&k)[kE], uint32_t n, const
     }
     const uint64_t range = (uint64_t)hi - lo + 1;
     const bool exact = range <= nb;  // one pair per bin
+    // else bin = v nb / range as a multiply-high by nb 2^32 / range (< 2^32: nb < range), one
+    // division per thread instead of a 64-bit division per key (~1,600 of the count launch's 2,060
+    // VALU instructions per wave at config 5)
+    const uint32_t mul = exact ? 0u : (uint32_t)(((uint64_t)nb << 32) / range);
     uint32_t br[kE];                 // bin | rank in it << 16 (bins, ranks < 2^14)
 #pragma unroll
     for (uint32_t e = 0; e < kE; ++e) {
         br[e] = 0;
         if (threadIdx.x + e * kT < n) {
             const uint32_t v = pos(k[e]) - lo;
-            const uint32_t bin = exact ? v : (uint32_t)((uint64_t)v * nb / range);
+            const uint32_t bin = exact ? v : __umulhi(v, mul);
             br[e] = bin | atomicAdd(&b.H[bin], 1u) << 16;
         }
     }
@@ -881,9 +888,14 @@ __global__ __launch_bounds__(kSbThreads) void pt_split_kernel(const uint32_t* __
     const uint64_t span = n_prot > qlo ? n_prot - qlo : 1u, range = (uint64_t)rows * span;
     const unsigned rs = g.pbits + g.sbits;
     const uint32_t qm = (1u << g.pbits) - 1;
+    // bin = pos nf / range: a multiply-high by nf 2^32 / range when the range fits 32 bits (pos < range;
+    // a range within nf bins is its own binning), the 64-bit division only beyond
+    const bool narrow = range <= 0xFFFFFFFFull;
+    const uint32_t mul = narrow && range > nf ? (uint32_t)(((uint64_t)nf << 32) / range) : 0u;
     auto bin = [&](uint32_t k) -> uint32_t {
         const uint32_t q = (k >> g.sbits) & qm;
         const uint64_t pos = (uint64_t)(k >> rs) * span + (q > qlo ? q - qlo : 0u);
+        if (narrow) return min(range > nf ? __umulhi((uint32_t)pos, mul) : (uint32_t)pos, nf - 1);
         return (uint32_t)min<uint64_t>(pos * nf / range, nf - 1);
     };
     for (uint32_t i = threadIdx.x; i < nf; i += kSbThreads) cnt[i] = 0;

@@ -35,6 +35,24 @@ struct PtDirectLds {
     uint32_t wave_tot[kPtRThreads / 64];
     unsigned long long s_excl, s_next;
 };
+// the count launch's: the sort (4,096 bins at most) and the run heads only, 50 KB — three
+// workgroups per CU where PtDirectLds's 66 KB allowed two (the launch waits on its loads: ~60 % of
+// a wave's cycles at config 5); compiled for 6 waves per SIMD (80 VGPRs) to match
+struct PtCountLds {
+    union {
+        typename PtSort<2>::storage_type s2;
+        typename PtSort<4>::storage_type s4;
+        typename PtSort<8>::storage_type s8;
+        typename PtSort<16>::storage_type s16;
+        PtBinLdsT<4096> b;
+        struct {
+            uint32_t H[kPtCap + 1];  // each run's first rank | k-bit scan at it << 16
+        } r;
+    };
+    uint32_t last[kPtRThreads];
+    uint32_t wave_tot[kPtRThreads / 64];
+};
+static_assert(sizeof(PtCountLds) <= 160 * 1024 / 3, "three count workgroups per CU");
 
 __device__ __forceinline__ bool pt_keep(uint32_t w, uint32_t w1, bool kbit, uint32_t ms) {
     return w != 0 && (kbit ? (w - w1 >= ms || w1 >= ms) : w >= ms);
@@ -61,8 +79,8 @@ __device__ __forceinline__ void pt_direct_write(const PtDirectOut& o, uint64_t a
 // true: load the sorted keys (thread t: ranks t kE + e), encode, and write the runs from edge
 // offset ex: the runs' first ranks (| k-bit scan << 16) and pair keys sit in LDS (H, P), then P
 // takes the score scan at the heads for the score column; one run per thread per round, coalesced.
-template <uint32_t kE, bool kKbit, bool kWrite>
-__device__ __forceinline__ void pt_direct_block(PtDirectLds& L, typename PtSort<kE>::storage_type& st,
+template <uint32_t kE, bool kKbit, bool kWrite, class Lds>
+__device__ __forceinline__ void pt_direct_block(Lds& L, typename PtSort<kE>::storage_type& st,
                                                 uint32_t* __restrict__ src, uint32_t s0, uint32_t n, uint32_t r,
                                                 const PtGeom& g, const PtDirectOut& out, uint32_t* __restrict__ wc,
                                                 uint64_t ex) {
@@ -117,7 +135,7 @@ __device__ __forceinline__ void pt_direct_block(PtDirectLds& L, typename PtSort<
         for (uint32_t e = 0; e < kE; ++e) {
             if (hm >> e & 1u) {
                 L.r.H[base] = (rank0 + e) | (kKbit ? kx << 16 : 0u);
-                L.r.P[base] = k[e] >> sb;
+                if constexpr (kWrite) L.r.P[base] = k[e] >> sb;
                 ++base;
             }
             if (kKbit && rank0 + e < n) kx += (k[e] >> kScoreBits) & 1u;
@@ -130,7 +148,7 @@ __device__ __forceinline__ void pt_direct_block(PtDirectLds& L, typename PtSort<
         w = (h1 & 0xFFFFu) - (h0 & 0xFFFFu);
         w1 = kKbit ? (h1 >> 16) - (h0 >> 16) : 0u;
     };
-    if (!kWrite) {  // min_shared > 1: the kept runs
+    if constexpr (!kWrite) {  // min_shared > 1: the kept runs
         uint32_t kept = 0;
         for (uint32_t i = threadIdx.x; i < nruns; i += kPtRThreads) {
             uint32_t w, w1;
@@ -141,7 +159,7 @@ __device__ __forceinline__ void pt_direct_block(PtDirectLds& L, typename PtSort<
         block_scan_n<kPtRThreads>(kept, e, total, L.wave_tot);
         if (threadIdx.x == 0) *wc = total;
         return;
-    }
+    } else {
     const uint32_t qm = (1u << g.pbits) - 1;
     // rounds of kPtRThreads runs, thread t the round's run t; filter: the kept runs compacted
     // (a block scan per round — uniform trip count)
@@ -188,6 +206,7 @@ __device__ __forceinline__ void pt_direct_block(PtDirectLds& L, typename PtSort<
     rounds([&](uint32_t i, uint64_t at, uint32_t, uint32_t) {
         if (at < out.cap) out.d_s[at * out.stride] = L.r.P[i + 1] - L.r.P[i];
     });
+    }
 }
 
 // a sub-block above kPtCap: windows of kDwWin pair positions (the monotone position of pt_bin_sort),
@@ -301,10 +320,10 @@ __global__ __launch_bounds__(kPtRThreads) void pt_window_count_kernel(const uint
 // count launch: every sub-block of at most kPtCap keys sorted in place and its kept runs counted
 // into wc (the larger ones: pt_window_count_kernel; stat[0] counts them)
 template <bool kKbit>
-__global__ __launch_bounds__(kPtRThreads) void pt_reduce_count_kernel(uint32_t* __restrict__ keys, BlkSrc bs, PtGeom g,
+__global__ __launch_bounds__(kPtRThreads, 6) void pt_reduce_count_kernel(uint32_t* __restrict__ keys, BlkSrc bs, PtGeom g,
                                                                       uint32_t* __restrict__ wc,
                                                                       unsigned long long* __restrict__ stat) {
-    __shared__ PtDirectLds L;
+    __shared__ PtCountLds L;
     const uint32_t d = blockIdx.x;
     uint32_t s0, n, r;
     blk_of(bs, d, s0, n, r);
