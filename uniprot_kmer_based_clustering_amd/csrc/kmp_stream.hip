@@ -47,9 +47,10 @@ __global__ __launch_bounds__(kDgThreads) void edge_digest_kernel(kmp::DigestIn i
     uint32_t seg = ~0u;
     unsigned long long ne = 0, dg = 0, sw = 0, ss = 0, na = 0, wd = 0;
     bool bad = false;
-    for (uint32_t j = 0; j < kDgPer; ++j) {
+#pragma unroll 4
+    for (uint32_t j = 0; j < kDgPer; ++j) {  // (unrolled: the next edges' loads issue ahead of this one's mixing)
         const uint64_t i = t0 + j * kDgThreads + threadIdx.x;
-        if (i >= in.n) break;
+        if (i >= in.n) continue;
         const uint32_t p = in.p[i], q = in.q[i], w = in.w[i];
         const uint32_t s = in.s ? in.s[i] : w, w0 = in.w0 ? in.w0[i] : w;
         if (i > 0) {
