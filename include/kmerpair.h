@@ -464,13 +464,18 @@ int kmp_postings_last_tail(const kmp_postings* ws);
  * (the counting tail only).  Same edges either way. */
 int kmp_postings_set_tail(kmp_postings* ws, int mode);
 /* kmp_postings_set_direct: the fused multi-k tail (kmp_dev_pairs_rows_multi, kmp_pairs_stream)
- * writes its edges in place from the sub-block reduce, at offsets from a decoupled look-back
+ * writes its edges in place from the sub-block reduce, at offsets from a count launch and a scan
  * (default 1), or (0) stages its runs and emits them after a scan.  Same edges either way. */
 int kmp_postings_set_direct(kmp_postings* ws, int enable);
 /* kmp_postings_set_flat_heavy: ranged calls with front reuse (the row passes of one batch) expand
  * the frequent k-mers by rows — a per-protein index of the compacted elements, built once, makes
  * a pass's work its own rows' pairs (default 1) — or (0) by per-k-mer tiles.  Same edges. */
 int kmp_postings_set_flat_heavy(kmp_postings* ws, int enable);
+/* kmp_postings_set_row_span: the rows [lo, hi) every ranged call of the current batch lies in
+ * (one rank's share of a row split; default 0, 0: any row).  The per-protein index of the
+ * row-driven expansion then covers only them: its count and scatter skip the other proteins'
+ * elements.  A call outside the index's rows rebuilds it for every row.  Same edges. */
+int kmp_postings_set_row_span(kmp_postings* ws, uint32_t lo, uint32_t hi);
 /* The bucketed step as a HIP graph (default 1): captured on the second call with an unchanged
  * shape (pointers, sizes, options, workspace buffers), replayed after that.
  * kmp_postings_graph_replays: calls served by a replay so far.  kmp_postings_reruns: calls (or phases

@@ -175,6 +175,7 @@ SIGNATURES = {
     "kmp_ctx_last_tail_windows": (C.c_uint64, [P]),
     "kmp_postings_set_direct": (C.c_int, [P, C.c_int]),
     "kmp_postings_set_flat_heavy": (C.c_int, [P, C.c_int]),
+    "kmp_postings_set_row_span": (C.c_int, [P, C.c_uint32, C.c_uint32]),
     "kmp_ctx_set_flat_heavy": (C.c_int, [P, C.c_int]),
     "kmp_ctx_last_passes": (C.c_uint32, [P]),
     "kmp_ctx_transport": (C.c_char_p, [P]),

@@ -1315,6 +1315,8 @@ static int stream_passes(kmp_ctx* c, const kmp_pair_opts& o, const int* ks, uint
         KMP_TRY(c, kmp_postings_set_timing(kv[j]->ws, 1));  // stage times of the summary
         KMP_TRY(c, kmp_postings_set_direct(kv[j]->ws, c->direct_tail));
         KMP_TRY(c, kmp_postings_set_flat_heavy(kv[j]->ws, c->flat_heavy));
+        // every pass lies in the lane's rows: the flat index covers only them (a rank's share)
+        KMP_TRY(c, kmp_postings_set_row_span(kv[j]->ws, ln.row_lo, ln.row_hi));
     }
     EventPair dev;
     if (!dev.ready()) return fail(c, KMP_EDEVICE, "events");
@@ -1518,6 +1520,7 @@ static int stream_passes(kmp_ctx* c, const kmp_pair_opts& o, const int* ks, uint
         (void)kmp_postings_set_reuse(kv[j]->ws, 0);
         (void)kmp_postings_set_timing(kv[j]->ws, 0);
         (void)kmp_postings_set_shard_floor(kv[j]->ws, 0);
+        (void)kmp_postings_set_row_span(kv[j]->ws, 0, 0);
     }
     return rc;
 }

@@ -38,6 +38,13 @@ int kmp_postings_set_flat_heavy(kmp_postings* ws, int enable) {
     return KMP_OK;
 }
 
+int kmp_postings_set_row_span(kmp_postings* ws, uint32_t lo, uint32_t hi) {
+    if (!ws || lo > hi) return KMP_EINVAL;
+    ws->span_lo = lo;
+    ws->span_hi = hi;
+    return KMP_OK;
+}
+
 int kmp_postings_set_direct(kmp_postings* ws, int enable) {
     if (!ws) return KMP_EINVAL;
     ws->direct_tail = enable ? 1 : 0;

@@ -1078,20 +1078,23 @@ __global__ __launch_bounds__(kHfThreads) void heavy_rows_kernel(
     }
 }
 
-// per-protein index of the compacted elements: counts, then (after a scan into PO) the scatter
+// per-protein index of the compacted elements of proteins [lo, hi) (the batch's row span): counts,
+// then (after a scan into PO) the scatter
 __global__ void heavy_pcount_kernel(const uint32_t* __restrict__ E, const unsigned long long* __restrict__ tot,
-                                    unsigned cb, uint32_t* __restrict__ cnt) {
-    const uint64_t ne = tot[0];
-    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < ne; e += (uint64_t)gridDim.x * blockDim.x)
-        atomicAdd(&cnt[E[e] >> cb], 1u);
-}
-__global__ void heavy_pscatter_kernel(const uint32_t* __restrict__ E, const unsigned long long* __restrict__ tot,
-                                      unsigned cb, const uint32_t* __restrict__ PO, uint32_t* __restrict__ cur,
-                                      uint32_t* __restrict__ PE) {
+                                    unsigned cb, uint32_t lo, uint32_t hi, uint32_t* __restrict__ cnt) {
     const uint64_t ne = tot[0];
     for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < ne; e += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t p = E[e] >> cb;
-        PE[PO[p] + atomicAdd(&cur[p], 1u)] = (uint32_t)e;
+        if (p - lo < hi - lo) atomicAdd(&cnt[p], 1u);
+    }
+}
+__global__ void heavy_pscatter_kernel(const uint32_t* __restrict__ E, const unsigned long long* __restrict__ tot,
+                                      unsigned cb, uint32_t lo, uint32_t hi, const uint32_t* __restrict__ PO,
+                                      uint32_t* __restrict__ cur, uint32_t* __restrict__ PE) {
+    const uint64_t ne = tot[0];
+    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < ne; e += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t p = E[e] >> cb;
+        if (p - lo < hi - lo) PE[PO[p] + atomicAdd(&cur[p], 1u)] = (uint32_t)e;
     }
 }
 

@@ -629,6 +629,10 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
     }
     if (ws->h_cls != ho.cls) return KMP_EINVAL;  // (compacted above in this call's order)
     bool index_built = false;
+    {  // an index built for a row span that does not hold this call's rows: again, for every row
+        const uint32_t lo = c.ranged ? c.row_lo : 0, hi = c.ranged ? c.row_hi : c.n;
+        if (ws->h_flat_ready && (lo < ws->h_span_lo || hi > ws->h_span_hi)) ws->h_flat_ready = false;
+    }
     if (flat && !ws->h_flat_ready) {
         index_built = true;
         // once per compaction: the per-protein index (one read-back: the element and k-mer counts)
@@ -642,14 +646,21 @@ int heavy_phase(kmp_postings* ws, const StepCfg& c, uint64_t m, bool stats, hipS
         PG(ws->hPC.reserve((uint64_t)np + 1));
         PG(hipMemsetAsync(ws->hPC.p, 0, ((size_t)np + 1) * sizeof(uint32_t), st));
         const uint32_t grid = (uint32_t)std::min<uint64_t>((ht[0] + 255) / 256 + 1, 16384);
-        heavy_pcount_kernel<<<grid, 256, 0, st>>>(ws->hE.p, ws->h_tot, ho.cb, ws->hPC.p);
+        // the proteins it covers: the batch's row span when it holds this call's rows (a rank's
+        // share skips the other ranks' elements), else every one
+        const bool spanned = ws->span_hi > ws->span_lo && c.ranged && c.row_lo >= ws->span_lo &&
+                             c.row_hi <= ws->span_hi;
+        ws->h_span_lo = spanned ? ws->span_lo : 0;
+        ws->h_span_hi = spanned ? ws->span_hi : np;
+        heavy_pcount_kernel<<<grid, 256, 0, st>>>(ws->hE.p, ws->h_tot, ho.cb, ws->h_span_lo, ws->h_span_hi, ws->hPC.p);
         size_t tb = 0;
         PG(rocprim::exclusive_scan(nullptr, tb, ws->hPC.p, ws->hPO.p, 0u, (size_t)np + 1, rocprim::plus<uint32_t>(), st));
         PG(ws->tmp.reserve(std::max(tb, ws->tmp.n)));
         PG(rocprim::exclusive_scan(ws->tmp.p, tb, ws->hPC.p, ws->hPO.p, 0u, (size_t)np + 1, rocprim::plus<uint32_t>(),
                                    st));
         PG(hipMemsetAsync(ws->hPC.p, 0, ((size_t)np + 1) * sizeof(uint32_t), st));
-        heavy_pscatter_kernel<<<grid, 256, 0, st>>>(ws->hE.p, ws->h_tot, ho.cb, ws->hPO.p, ws->hPC.p, ws->hPE.p);
+        heavy_pscatter_kernel<<<grid, 256, 0, st>>>(ws->hE.p, ws->h_tot, ho.cb, ws->h_span_lo, ws->h_span_hi, ws->hPO.p,
+                                                    ws->hPC.p, ws->hPE.p);
         PG(hipGetLastError());
         ws->hPOh.resize((size_t)np + 1);
         PG(hipMemcpyAsync(ws->hPOh.data(), ws->hPO.p, ((size_t)np + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));

@@ -110,6 +110,8 @@ struct kmp_postings {
     Grow<uint32_t> hKG, hPE, hPO, hPC;
     std::vector<uint32_t> hPOh;
     bool h_flat_ready = false, h_kg = false;
+    // kmp_postings_set_row_span: the batch's ranged calls' rows (span_hi 0: any); the index's rows
+    uint32_t span_lo = 0, span_hi = 0, h_span_lo = 0, h_span_hi = 0;
     // tail_multi_rows: the phase its calls run (set around them; nullptr otherwise), and the pass's
     // per-row key counts (ws[0]'s)
     RowDirect* rdir = nullptr;
