@@ -1162,6 +1162,7 @@ __device__ void step_pack_body(const unsigned long long* __restrict__ gstats, co
 // The last block writes the edge count and the step's read-back.
 constexpr uint32_t kFtThreads = 512, kFtHashMax = 6144, kFtSlots = 8192, kFtRowsMax = 1024, kFtRankMax = 256;
 constexpr uint32_t kFtEmpty = 0xFFFFFFFFu;
+constexpr uint32_t kFtSmallN = 2048;  // a block of at most this many keys hashes into kFtSlots / 2 slots
 constexpr unsigned long long kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbOvf = 1ull << 61;
 static_assert(kFtCap == 16 * kFtThreads && kFtHashMax <= 12 * kFtThreads && kFtSlots == 16 * kFtThreads,
               "per-thread register arrays of pt_reduce_fast");
@@ -1248,7 +1249,7 @@ __global__ __launch_bounds__(kFtThreads, kFtWaves) void pt_reduce_fast_kernel(co
                                                                     uint32_t* __restrict__ d_w, uint64_t cap,
                                                                     uint32_t stride, PtPack pack,
                                                                     uint32_t* __restrict__ runs) {
-    __shared__ FtLds u;
+    __shared__ __attribute__((aligned(16))) FtLds u;
     __shared__ uint32_t s_r, s_n;
     const uint32_t tid = threadIdx.x;
     const unsigned pb = g.pbits;
@@ -1256,8 +1257,9 @@ __global__ __launch_bounds__(kFtThreads, kFtWaves) void pt_reduce_fast_kernel(co
     // the row block = the look-back position = the order the workgroups started in (a ticket), so
     // every block a look-back polls is resident or done, whatever the dispatch order across XCDs and
     // whatever other kernels share the device.  One thread takes it, reads and re-zeroes the block's
-    // cursor while the others clear the hash table (used only when the block is small enough: a
-    // sort-path block overwrites it)
+    // cursor while the others clear the row counts; the hash table is cleared once the block's key
+    // count is known: at most kFtSmallN keys (most blocks at config 3, mean ~1,700) take a table of
+    // half the slots (half the clear and the slot reads), a sort-path block none
     if (tid == 0) {
         const uint32_t r0 = atomicAdd(ticket, 1u);
         s_r = r0;
@@ -1265,8 +1267,6 @@ __global__ __launch_bounds__(kFtThreads, kFtWaves) void pt_reduce_fast_kernel(co
         fcur[r0] = 0;  // for the next call
         u.s_max = u.s_flag = 0;
     }
-    for (uint32_t i = tid; i < kFtSlots; i += kFtThreads) u.h.K[i] = kFtEmpty;
-    for (uint32_t i = tid; i < kFtSlots / 2; i += kFtThreads) reinterpret_cast<uint32_t*>(u.h.C)[i] = 0;
     for (uint32_t i = tid; i <= R; i += kFtThreads) u.RC[i] = 0;
     __syncthreads();
     const uint32_t r = s_r, nraw = s_n;
@@ -1275,6 +1275,13 @@ __global__ __launch_bounds__(kFtThreads, kFtWaves) void pt_reduce_fast_kernel(co
     if (tid == 0 && nraw) atomicMax(&runs[2], nraw);
     bool ovf = nraw > kFtCap;
     const uint32_t n = ovf ? 0u : nraw;
+    const unsigned tsh = n <= kFtSmallN ? 20u : 19u;  // hash shift: 12 or 13 slot bits
+    const uint32_t nsl = 1u << (32 - tsh);
+    if (n <= kFtHashMax) {
+        for (uint32_t i = tid; i < nsl; i += kFtThreads) u.h.K[i] = kFtEmpty;
+        for (uint32_t i = tid; i < nsl / 2; i += kFtThreads) reinterpret_cast<uint32_t*>(u.h.C)[i] = 0;
+        __syncthreads();
+    }
     const uint32_t* src = keys + (uint64_t)r * kFtCap;
     uint32_t D = 0;  // the block's kept pairs
     bool sort = n > kFtHashMax, published = false;
@@ -1286,18 +1293,20 @@ __global__ __launch_bounds__(kFtThreads, kFtWaves) void pt_reduce_fast_kernel(co
             const uint32_t i = tid + e * kFtThreads;
             x[e] = i < n ? src[i] : kFtEmpty;
         }
+        // the counts as non-returning adds: a 16-bit count cannot wrap, n <= kFtHashMax < 0xFFFF.
+        // (Issuing every key's first probe before any collision loop measured slower: pair_sort_rle
+        // 0.073 -> 0.117 ms at config 3, the probe arrays past the 80-VGPR budget of 6 waves)
+        static_assert(kFtHashMax < 0xFFFFu, "hash-path counts fit 16 bits");
 #pragma unroll
         for (uint32_t e = 0; e < 12; ++e) {
             if (x[e] == kFtEmpty) continue;
-            uint32_t sl = (x[e] * 0x9E3779B1u) >> 19;  // 13 bits: kFtSlots
+            uint32_t sl = (x[e] * 0x9E3779B1u) >> tsh;
             while (true) {
                 const uint32_t old = atomicCAS(&u.h.K[sl], kFtEmpty, x[e]);
                 if (old == kFtEmpty || old == x[e]) break;
-                sl = (sl + 1) & (kFtSlots - 1);
+                sl = (sl + 1) & (nsl - 1);
             }
-            const uint32_t sh = 16 * (sl & 1);
-            const uint32_t old = atomicAdd(reinterpret_cast<uint32_t*>(u.h.C) + (sl >> 1), 1u << sh);
-            if (((old >> sh) & 0xFFFFu) >= 0xFFFEu) u.s_flag = 1;  // w would reach 16 bits: sort instead
+            atomicAdd(reinterpret_cast<uint32_t*>(u.h.C) + (sl >> 1), 1u << (16 * (sl & 1)));
         }
         __syncthreads();
         // ---- kept pairs (w >= min_shared) counted per row, ranked in arrival order ----
@@ -1305,8 +1314,9 @@ __global__ __launch_bounds__(kFtThreads, kFtWaves) void pt_reduce_fast_kernel(co
 #pragma unroll
         for (uint32_t j = 0; j < 16; ++j) {
             const uint32_t sl = tid + j * kFtThreads;
-            const uint32_t k = u.h.K[sl], w = u.h.C[sl];
             ek[j] = kFtEmpty;
+            if (sl >= nsl) continue;  // (uniform per j)
+            const uint32_t k = u.h.K[sl], w = u.h.C[sl];
             if (k != kFtEmpty && w >= g.min_shared) {
                 ek[j] = k;
                 er[j] = atomicAdd(&u.RC[k >> pb], 1u) << 16 | w;
@@ -1346,6 +1356,8 @@ __global__ __launch_bounds__(kFtThreads, kFtWaves) void pt_reduce_fast_kernel(co
                 fk[e] = kFtEmpty;
                 if (i < D) {
                     const uint32_t key = u.h.K[i], row = key >> pb, a = u.RC[row], b = u.RC[row + 1];
+                    // (four row words per 16-byte read measured no faster at config 3, and cost
+                    // four more spilled VGPRs)
                     uint32_t rk = 0;
                     for (uint32_t t = a; t < b; ++t) rk += u.h.K[t] < key;
                     fk[e] = key;
